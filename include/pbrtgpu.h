@@ -1,0 +1,210 @@
+/* pbrtgpu.h -- C ABI of the MI355X spectral path-tracing core (libpbrtgpu.so).
+ *
+ * Drop-in boundary: this library replaces the body of the reference's
+ *   Renderer::Render(const Scene*)              core/renderer.h:35-46
+ * as implemented by SamplerRenderer::Render + SamplerRendererTask::Run
+ *   (renderers/samplerrenderer.cpp:60-222) driving PathIntegrator::Li
+ *   (integrators/path.cpp:44-115), BVHAccel::Intersect/IntersectP
+ *   (accelerators/bvh.cpp:380-481), BSDF::Sample_f/f/Pdf (core/reflection.cpp:514-618)
+ *   and SpectralImageFilm::AddSample (film/spectralImage.cpp:77-152).
+ * The host C++ side (pbrt-v2-spectral_amd/host, GpuPathRenderer) parses the unchanged
+ * pbrt scene format, builds the BVH and hands the flattened scene below to
+ * pbrtgpu_scene_upload.  All pointers are host pointers; sizes are element counts.
+ * No torch / HIP types appear in this interface.
+ *
+ * Return codes: 0 = success; negative = error (PBRTGPU_E_*, or -(1000 + hipError_t)).
+ * pbrtgpu_last_error() returns a thread-local message for the last failure.
+ * Threading: one context per GPU, each driven by one host thread; calls on distinct
+ * contexts may run concurrently.
+ */
+#ifndef PBRTGPU_H
+#define PBRTGPU_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PBRTGPU_ABI_VERSION 1
+#define PBRTGPU_MAX_BANDS 64
+
+#define PBRTGPU_E_INVALID   (-1)
+#define PBRTGPU_E_NODEVICE  (-2)
+#define PBRTGPU_E_NOMEM     (-3)
+#define PBRTGPU_E_UNSUPPORTED (-4)
+#define PBRTGPU_E_STATE     (-5)
+
+/* ---- flattened scene ------------------------------------------------------------ */
+
+/* LinearBVHNode (bvh.cpp:105-115): 32 bytes. leaf iff (meta & 0xff) != 0.
+ * meta = nPrimitives | (axis << 8).  offset = primitivesOffset (leaf) or
+ * secondChildOffset (interior); the first child of an interior node is node+1. */
+typedef struct pbrtgpu_bvh_node {
+    float bmin[3];
+    float bmax[3];
+    uint32_t offset;
+    uint32_t meta;
+} pbrtgpu_bvh_node;
+
+enum { PBRTGPU_SHAPE_TRIANGLE = 0, PBRTGPU_SHAPE_SPHERE = 1, PBRTGPU_SHAPE_DISK = 2 };
+
+/* one GeometricPrimitive, in BVH (orderedPrims) order */
+typedef struct pbrtgpu_prim {
+    int32_t shape_type;   /* PBRTGPU_SHAPE_* */
+    int32_t shape_index;  /* triangle index or quadric index */
+    int32_t material;     /* index into materials */
+    int32_t area_light;   /* index into lights, or -1 */
+} pbrtgpu_prim;
+
+typedef struct pbrtgpu_triangle {
+    int32_t mesh;         /* index into meshes */
+    int32_t v[3];         /* global vertex indices (mesh->vertexIndex + mesh vert_offset) */
+} pbrtgpu_triangle;
+
+/* TriangleMesh (trianglemesh.cpp:33-63): positions are world space (P transformed at
+ * construction), normals object space, uvs optional. */
+typedef struct pbrtgpu_mesh {
+    float o2w_m[16];      /* ObjectToWorld.m (row major) */
+    float o2w_minv[16];   /* ObjectToWorld.mInv  (normals are transformed with this) */
+    int32_t has_normals, has_uvs, reverse_orientation, swaps_handedness;
+    int32_t vert_offset, nverts, pad0, pad1;
+} pbrtgpu_mesh;
+
+/* Sphere (sphere.cpp) / Disk (disk.cpp); WorldToObject = (o2w_minv, o2w_m) */
+typedef struct pbrtgpu_quadric {
+    int32_t type;         /* PBRTGPU_SHAPE_SPHERE or _DISK */
+    int32_t reverse_orientation, swaps_handedness, pad0;
+    float o2w_m[16];
+    float o2w_minv[16];
+    float radius, zmin, zmax, theta_min, theta_max, phi_max, height, inner_radius;
+} pbrtgpu_quadric;
+
+enum {
+    PBRTGPU_MAT_MATTE = 0,      /* spec[0]=Kd; f[0]=sigma (degrees) */
+    PBRTGPU_MAT_PLASTIC = 1,    /* spec[0]=Kd, spec[1]=Ks; f[0]=roughness */
+    PBRTGPU_MAT_METAL = 2,      /* spec[0]=eta, spec[1]=k; f[0]=roughness */
+    PBRTGPU_MAT_SUBSTRATE = 3,  /* spec[0]=Kd, spec[1]=Ks; f[0]=uroughness, f[1]=vroughness */
+    PBRTGPU_MAT_MIRROR = 4,     /* spec[0]=Kr */
+    PBRTGPU_MAT_GLASS = 5,      /* spec[0]=Kr, spec[1]=Kt; f[0]=index */
+    PBRTGPU_MAT_MEASURED = 6    /* aux = measured table index */
+};
+
+/* material with constant textures; f[7] = constant bump displacement (Material::Bump,
+ * material.cpp:39-81, always applied because bumpmap defaults to constant 0) */
+typedef struct pbrtgpu_material {
+    int32_t type;
+    int32_t spec[4];      /* offsets (in floats) into spectra[] */
+    int32_t aux;
+    int32_t pad0, pad1;
+    float f[8];
+} pbrtgpu_material;
+
+enum { PBRTGPU_LIGHT_AREA = 0, PBRTGPU_LIGHT_POINT = 1, PBRTGPU_LIGHT_INFINITE = 2 };
+
+typedef struct pbrtgpu_light {
+    int32_t type;
+    int32_t spec;          /* Lemit (area) / intensity (point) / L (infinite), offset into spectra[] */
+    int32_t shape_offset;  /* area: first entry in light_shapes[] (ShapeSet, light.cpp:114-135) */
+    int32_t n_shapes;
+    float sum_area;        /* ShapeSet::sumArea */
+    float pos[3];          /* point light position LightToWorld(0,0,0) */
+    int32_t is_black;      /* emitted spectrum IsBlack() */
+    int32_t pad[3];
+    float l2w_m[16];
+    float l2w_minv[16];
+} pbrtgpu_light;
+
+typedef struct pbrtgpu_light_shape {
+    int32_t shape_type, shape_index;
+    float area;            /* Shape::Area() */
+    float cdf;             /* Distribution1D cdf[i+1] of the area distribution */
+} pbrtgpu_light_shape;
+
+/* PerspectiveCamera (perspective.cpp, camera.cpp:84-103) + film/sample extent
+ * (spectralImage.cpp:40-50, 176-185) */
+typedef struct pbrtgpu_camera {
+    float raster_to_camera[16];
+    float cam2world_m[16];
+    float lens_radius, focal_distance, shutter_open, shutter_close;
+    int32_t xres, yres;
+    int32_t px_start, px_count, py_start, py_count;   /* film pixel window */
+    int32_t sx_start, sx_end, sy_start, sy_end;       /* sample extent (incl. border) */
+} pbrtgpu_camera;
+
+typedef struct pbrtgpu_flat_scene {
+    int32_t abi_version;
+    int32_t n_bands;              /* nSpectralSamples */
+    int32_t max_depth;            /* PathIntegrator maxdepth */
+    int32_t spp;                  /* pixel samples (power of two) */
+    uint32_t seed;                /* fixed-seed sampler seed */
+    float y_int;                  /* SampledSpectrum::yint */
+    const float *band_Y;          /* [n_bands] SampledSpectrum::Y */
+    pbrtgpu_camera camera;
+    int32_t n_nodes;   const pbrtgpu_bvh_node *nodes;
+    int32_t n_prims;   const pbrtgpu_prim *prims;
+    int32_t n_tris;    const pbrtgpu_triangle *tris;
+    int32_t n_meshes;  const pbrtgpu_mesh *meshes;
+    int32_t n_verts;   const float *vert_p;   /* [n_verts][3] world positions */
+    const float *vert_n;                      /* [n_verts][3] object normals (0 if absent) */
+    const float *vert_uv;                     /* [n_verts][2] (0 if absent) */
+    int32_t n_quadrics; const pbrtgpu_quadric *quadrics;
+    int32_t n_materials; const pbrtgpu_material *materials;
+    int32_t n_lights;  const pbrtgpu_light *lights;
+    int32_t n_light_shapes; const pbrtgpu_light_shape *light_shapes;
+    int32_t n_spectra_floats; const float *spectra;   /* spectrum pool */
+} pbrtgpu_flat_scene;
+
+/* ---- render description ----------------------------------------------------------- */
+typedef struct pbrtgpu_render_desc {
+    int32_t spp_begin, spp_end;   /* sample index range [begin,end) of this call */
+    int32_t tile_w, tile_h;       /* tile size in sample pixels (tile ids index this grid) */
+    int32_t flags;                /* PBRTGPU_F_* */
+    int32_t reserved[3];
+} pbrtgpu_render_desc;
+
+#define PBRTGPU_F_ACCUMULATE 1    /* add into the context film instead of clearing it */
+
+/* stats_out layout (doubles) */
+enum {
+    PBRTGPU_STAT_PATHS = 0,       /* camera paths traced */
+    PBRTGPU_STAT_KERNEL_MS = 1,   /* device time of the path kernel(s) */
+    PBRTGPU_STAT_ACCUM_MS = 2,    /* device time of the film accumulation */
+    PBRTGPU_STAT_ZEROED = 3,      /* samples zeroed by the NaN/negative/inf guard */
+    PBRTGPU_STAT_SPILLS = 4,      /* exact-boundary samples added to neighbour pixels */
+    PBRTGPU_STAT_COUNT = 8
+};
+
+typedef struct pbrtgpu_ctx pbrtgpu_ctx;
+
+int pbrtgpu_abi_version(void);
+int pbrtgpu_device_count(void);
+int pbrtgpu_context_create(int device, pbrtgpu_ctx **out);
+int pbrtgpu_context_destroy(pbrtgpu_ctx *ctx);
+const char *pbrtgpu_last_error(void);
+/* copies the flattened scene into device memory owned by ctx */
+int pbrtgpu_scene_upload(pbrtgpu_ctx *ctx, const pbrtgpu_flat_scene *scene);
+/* Renders the listed tiles of the sample extent for samples [spp_begin, spp_end) and
+ * accumulates into the context's film (film pixels touched by those tiles).
+ * tile_ids == NULL means every tile. stats_out may be NULL. */
+int pbrtgpu_render_tiles(pbrtgpu_ctx *ctx, const pbrtgpu_render_desc *desc,
+                         const int32_t *tile_ids, int32_t ntiles, double *stats_out);
+/* Copies the film (float32 [py_count][px_count][n_bands], Σ L per pixel -- the
+ * reference film does not normalise) to host memory. */
+int pbrtgpu_film_read(pbrtgpu_ctx *ctx, float *film_out, int64_t n_floats);
+int pbrtgpu_film_clear(pbrtgpu_ctx *ctx);
+/* Per-path radiance for a list of path keys (x, y, s): debugging / parity hook.
+ * keys: [n][3] int32; out: [n][n_bands] float32 (after the NaN/inf guard). */
+int pbrtgpu_trace_paths(pbrtgpu_ctx *ctx, const int32_t *keys, int32_t n, float *out);
+/* Closest-hit / any-hit queries for n rays (parity hook for BVHAccel::Intersect/IntersectP):
+ * rays [n][8] = o.xyz, d.xyz, mint, maxt ; hits_out [n][4] = t, b1, b2, prim (as float bits),
+ * prim = -1 on miss; occluded_out [n] (may be NULL). */
+int pbrtgpu_intersect(pbrtgpu_ctx *ctx, const float *rays, int32_t n, float *hits_out,
+                      int32_t *occluded_out);
+/* Timing of the dominant kernel for roofline reporting: average device milliseconds
+ * per launch of the path kernel over the last render call, and launches. */
+int pbrtgpu_last_kernel_timing(pbrtgpu_ctx *ctx, double *avg_ms, int32_t *launches);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PBRTGPU_H */

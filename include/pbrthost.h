@@ -1,0 +1,44 @@
+/* pbrthost.h -- C ABI of the host front end (libpbrthost.so).
+ *
+ * Replaces, for the hot path's inputs, the reference's parse + scene construction
+ * (core/parser.cpp ParseFile -> core/api.cpp pbrt* -> RenderOptions::MakeScene /
+ * MakeCamera, api.cpp:1215-1330) and the film output SpectralImageFilm::WriteImage
+ * (film/spectralImage.cpp:267-378).  The flattened scene it produces is the input of
+ * pbrtgpu_scene_upload (include/pbrtgpu.h).
+ */
+#ifndef PBRTHOST_H
+#define PBRTHOST_H
+#include <stdint.h>
+#include "pbrtgpu.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct pbrthost_scene pbrthost_scene;
+
+/* Overrides of scene-file values: -1 keeps the file's value. */
+typedef struct pbrthost_overrides {
+    int32_t xres, yres;   /* Film "xresolution"/"yresolution" */
+    int32_t spp;          /* Sampler "pixelsamples" (rounded up to a power of two) */
+    int32_t maxdepth;     /* SurfaceIntegrator "path" "maxdepth" */
+    int32_t bands;        /* nSpectralSamples: 32 (reference build) or 60 */
+    uint32_t seed;        /* fixed-seed sampler seed */
+} pbrthost_overrides;
+
+/* path: a .pbrt scene file or a .pack scene pack.  Returns 0 or -1 (message in err). */
+int pbrthost_load(const char *path, const pbrthost_overrides *ov, pbrthost_scene **out, char *err, int errlen);
+int pbrthost_free(pbrthost_scene *s);
+int pbrthost_flat(pbrthost_scene *s, pbrtgpu_flat_scene *out);   /* pointers stay owned by s */
+int pbrthost_save_pack(pbrthost_scene *s, const char *path, char *err, int errlen);
+int pbrthost_set_render(pbrthost_scene *s, int spp, int maxdepth, uint32_t seed);
+/* info[0..15]: bands, spp, maxdepth, nodes, prims, tris, meshes, verts, quadrics,
+ * materials, lights, bvh depth, film W, film H, warnings, 0 */
+int pbrthost_info(pbrthost_scene *s, int64_t *info, int n);
+/* reference .dat writer; film [H][W][N] float32 (raw sums), weight [H][W] or NULL */
+int pbrthost_write_dat(const char *path, const float *film, const float *weight, int W, int H, int N);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,1535 @@
+/* oracle/pathtrace.c -- TEST INFRASTRUCTURE: CPU restatement of the reference hot path.
+ *
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load this
+ * library, and only as the checker / CPU baseline.  The product (libpbrtgpu.so) never
+ * links or calls it.
+ *
+ * Parity pinning: compiled with -DORACLE_LIBM_FLOAT (glibc float transcendentals, as the
+ * reference build) it reproduces the reference harness (oracle/_ref, which runs the
+ * reference's own PathIntegrator/BVH/BSDF/light/camera code) bit for bit; compiled
+ * without it, sinf/cosf/powf/expf/acosf/atan2f/tanf/atanf are evaluated in double and
+ * rounded once (the definition the HIP kernels implement), see DESIGN.md §3.2.
+ *
+ * It consumes the flattened scene of include/pbrtgpu.h and follows, function by function:
+ *   samplerrenderer.cpp:60-164,225-247  render loop, NaN/inf guard, SamplerRenderer::Li
+ *   path.cpp:44-115                     PathIntegrator::Li
+ *   integrator.cpp:74-166               UniformSampleOneLight / EstimateDirect
+ *   bvh.cpp:118-140,380-481             slab test, Intersect, IntersectP
+ *   trianglemesh.cpp:119-360            Triangle::Intersect/IntersectP/GetShadingGeometry
+ *   sphere.cpp, disk.cpp, shape.cpp     quadric intersection / sampling / pdf
+ *   material.cpp:39-81                  Material::Bump (constant displacement)
+ *   matte.cpp, plastic.cpp, mirror.cpp, substrate.cpp   per-hit BSDF assembly
+ *   reflection.cpp:52-618               BSDF and BxDFs
+ *   light.cpp, diffuse.cpp, point.cpp   lights
+ *   perspective.cpp:73-106              camera rays
+ *   spectralImage.cpp:77-152            film accumulation (box filter)
+ *   rng.cpp                             MT19937
+ *   montecarlo.{h,cpp}                  sampling helpers
+ * Compile with -ffp-contract=off (the reference x86-64 build has no FMA contraction).
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include <stdio.h>
+#include <pthread.h>
+#include "pbrtgpu.h"
+
+#define MAXB PBRTGPU_MAX_BANDS
+#define PI_F 3.14159265358979323846f
+#define INV_PI_F 0.31830988618379067154f
+#define INV_TWOPI_F 0.15915494309189533577f
+#define ONE_MINUS_EPS 0x1.fffffep-1f
+
+#ifdef ORACLE_LIBM_FLOAT
+#define SINF sinf
+#define COSF cosf
+#define POWF powf
+#define EXPF expf
+#define ACOSF acosf
+#define ATAN2F atan2f
+#define TANF tanf
+#define ATANF atanf
+#else
+static inline float SINF(float x) { return (float)sin((double)x); }
+static inline float COSF(float x) { return (float)cos((double)x); }
+static inline float POWF(float x, float y) { return (float)pow((double)x, (double)y); }
+static inline float EXPF(float x) { return (float)exp((double)x); }
+static inline float ACOSF(float x) { return (float)acos((double)x); }
+static inline float ATAN2F(float y, float x) { return (float)atan2((double)y, (double)x); }
+static inline float TANF(float x) { return (float)tan((double)x); }
+static inline float ATANF(float x) { return (float)atan((double)x); }
+#endif
+
+/* ------------------------------------------------------------------ vector math */
+typedef struct { float x, y, z; } V;
+static inline V v3(float x, float y, float z) { V r; r.x = x; r.y = y; r.z = z; return r; }
+static inline V vadd(V a, V b) { return v3(a.x + b.x, a.y + b.y, a.z + b.z); }
+static inline V vsub(V a, V b) { return v3(a.x - b.x, a.y - b.y, a.z - b.z); }
+static inline V vneg(V a) { return v3(-a.x, -a.y, -a.z); }
+static inline V vmul(V a, float f) { return v3(f * a.x, f * a.y, f * a.z); }
+static inline V vdiv(V a, float f) { float inv = 1.f / f; return v3(a.x * inv, a.y * inv, a.z * inv); }
+static inline float vdot(V a, V b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+static inline float vlen2(V a) { return a.x * a.x + a.y * a.y + a.z * a.z; }
+static inline float vlen(V a) { return sqrtf(vlen2(a)); }
+static inline V vnorm(V a) { return vdiv(a, vlen(a)); }
+static inline V vcross(V a, V b) {
+    double ax = a.x, ay = a.y, az = a.z, bx = b.x, by = b.y, bz = b.z;
+    return v3((float)((ay * bz) - (az * by)), (float)((az * bx) - (ax * bz)), (float)((ax * by) - (ay * bx)));
+}
+static inline float vcomp(V a, int i) { return i == 0 ? a.x : (i == 1 ? a.y : a.z); }
+static inline float fminf_(float a, float b) { return (b < a) ? b : a; }   /* std::min */
+static inline float fmaxf_(float a, float b) { return (a < b) ? b : a; }   /* std::max */
+static inline float clampf(float v, float lo, float hi) { return v < lo ? lo : (v > hi ? hi : v); }
+static inline float lerpf(float t, float a, float b) { return (1.f - t) * a + t * b; }
+static inline V faceforward(V n, V v) { return (vdot(n, v) < 0.f) ? vneg(n) : n; }
+static inline void coordsys(V v1, V *v2, V *v3_) {
+    if (fabsf(v1.x) > fabsf(v1.y)) {
+        float invLen = 1.f / sqrtf(v1.x * v1.x + v1.z * v1.z);
+        *v2 = v3(-v1.z * invLen, 0.f, v1.x * invLen);
+    } else {
+        float invLen = 1.f / sqrtf(v1.y * v1.y + v1.z * v1.z);
+        *v2 = v3(0.f, v1.z * invLen, -v1.y * invLen);
+    }
+    *v3_ = vcross(v1, *v2);
+}
+/* Transform::operator()(Point) (transform.h:184-194) */
+static inline V xpoint(const float *m, V p) {
+    float xp = m[0] * p.x + m[1] * p.y + m[2] * p.z + m[3];
+    float yp = m[4] * p.x + m[5] * p.y + m[6] * p.z + m[7];
+    float zp = m[8] * p.x + m[9] * p.y + m[10] * p.z + m[11];
+    float wp = m[12] * p.x + m[13] * p.y + m[14] * p.z + m[15];
+    if (wp == 1.) return v3(xp, yp, zp);
+    return vdiv(v3(xp, yp, zp), wp);
+}
+static inline V xvec(const float *m, V v) {
+    return v3(m[0] * v.x + m[1] * v.y + m[2] * v.z, m[4] * v.x + m[5] * v.y + m[6] * v.z,
+              m[8] * v.x + m[9] * v.y + m[10] * v.z);
+}
+static inline V xnormal(const float *minv, V n) {
+    return v3(minv[0] * n.x + minv[4] * n.y + minv[8] * n.z, minv[1] * n.x + minv[5] * n.y + minv[9] * n.z,
+              minv[2] * n.x + minv[6] * n.y + minv[10] * n.z);
+}
+
+typedef struct { V o, d; float mint, maxt, time; } Ray;
+static inline V rayat(const Ray *r, float t) { return vadd(r->o, vmul(r->d, t)); }
+
+/* ------------------------------------------------------------------ sampling */
+static inline uint32_t mix32(uint32_t x) {
+    x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16;
+    return x;
+}
+static inline uint32_t pixel_hash(uint32_t seed, int px, int py) {
+    uint32_t h = mix32(seed + 0x9E3779B9U);
+    h = mix32(h ^ (uint32_t)px);
+    h = mix32(h ^ ((uint32_t)py * 0x85EBCA6BU));
+    return h;
+}
+static inline uint32_t dim_scramble(uint32_t hp, uint32_t d) { return mix32(hp ^ (0x9E3779B9U * (d + 1U))); }
+static inline uint32_t perm_index(uint32_t hp, uint32_t d, uint32_t s, uint32_t spp) {
+    return s ^ (mix32(dim_scramble(hp, d) ^ 0x5BD1E995U) & (spp - 1U));
+}
+static inline uint32_t path_seed(uint32_t hp, uint32_t s) { return mix32(hp ^ mix32(s + 0x7F4A7C15U)); }
+static inline float vdc(uint32_t n, uint32_t scramble) {   /* montecarlo.h:269-278 */
+    n = (n << 16) | (n >> 16);
+    n = ((n & 0x00ff00ff) << 8) | ((n & 0xff00ff00) >> 8);
+    n = ((n & 0x0f0f0f0f) << 4) | ((n & 0xf0f0f0f0) >> 4);
+    n = ((n & 0x33333333) << 2) | ((n & 0xcccccccc) >> 2);
+    n = ((n & 0x55555555) << 1) | ((n & 0xaaaaaaaa) >> 1);
+    n ^= scramble;
+    return fminf_(((n >> 8) & 0xffffff) / (float)(1 << 24), ONE_MINUS_EPS);
+}
+static inline float sobol2(uint32_t n, uint32_t scramble) {   /* montecarlo.h:281-285 */
+    for (uint32_t v = 1u << 31; n != 0; n >>= 1, v ^= v >> 1)
+        if (n & 0x1) scramble ^= v;
+    return fminf_(((scramble >> 8) & 0xffffff) / (float)(1 << 24), ONE_MINUS_EPS);
+}
+static inline float s1d(uint32_t hp, uint32_t d, uint32_t s, uint32_t spp) {
+    return vdc(perm_index(hp, d, s, spp), dim_scramble(hp, d));
+}
+static inline void s2d(uint32_t hp, uint32_t d, uint32_t s, uint32_t spp, float *u) {
+    uint32_t sp = perm_index(hp, d, s, spp), sc = dim_scramble(hp, d);
+    u[0] = vdc(sp, sc);
+    u[1] = sobol2(sp, mix32(sc ^ 0x68BC21EBU));
+}
+/* sample slots of PathIntegrator::RequestSamples (path.cpp:33-41) + emission (2x1D):
+ * 1D slot j -> dim 3+j (bounce b: lightComp 4b, lightNum 4b+1, bsdfComp 4b+2, pathComp 4b+3)
+ * 2D slot k -> dim 17+k (bounce b: lightPos 3b, bsdfDir 3b+1, pathDir 3b+2) */
+#define N1D 14
+#define DIM_1D(j) (3u + (uint32_t)(j))
+#define DIM_2D(k) (3u + N1D + (uint32_t)(k))
+
+/* MT19937 (rng.cpp:35-100) */
+typedef struct { uint32_t mt[624]; int mti; } RNG;
+static void rng_seed(RNG *r, uint32_t seed) {
+    r->mt[0] = seed;
+    for (r->mti = 1; r->mti < 624; r->mti++) r->mt[r->mti] = (1812433253U * (r->mt[r->mti - 1] ^ (r->mt[r->mti - 1] >> 30)) + r->mti);
+}
+static uint32_t rng_uint(RNG *r) {
+    static const uint32_t mag01[2] = {0x0U, 0x9908b0dfU};
+    uint32_t y;
+    if (r->mti >= 624) {
+        int kk;
+        for (kk = 0; kk < 624 - 397; kk++) {
+            y = (r->mt[kk] & 0x80000000U) | (r->mt[kk + 1] & 0x7fffffffU);
+            r->mt[kk] = r->mt[kk + 397] ^ (y >> 1) ^ mag01[y & 0x1U];
+        }
+        for (; kk < 623; kk++) {
+            y = (r->mt[kk] & 0x80000000U) | (r->mt[kk + 1] & 0x7fffffffU);
+            r->mt[kk] = r->mt[kk + (397 - 624)] ^ (y >> 1) ^ mag01[y & 0x1U];
+        }
+        y = (r->mt[623] & 0x80000000U) | (r->mt[0] & 0x7fffffffU);
+        r->mt[623] = r->mt[396] ^ (y >> 1) ^ mag01[y & 0x1U];
+        r->mti = 0;
+    }
+    y = r->mt[r->mti++];
+    y ^= (y >> 11);
+    y ^= (y << 7) & 0x9d2c5680U;
+    y ^= (y << 15) & 0xefc60000U;
+    y ^= (y >> 18);
+    return y;
+}
+static inline float rng_float(RNG *r) { return (rng_uint(r) & 0xffffff) / (float)(1 << 24); }
+
+/* montecarlo.cpp:298-340 */
+static void concentric_disk(float u1, float u2, float *dx, float *dy) {
+    float r, theta;
+    float sx = 2 * u1 - 1;
+    float sy = 2 * u2 - 1;
+    if (sx == 0.0 && sy == 0.0) { *dx = 0.0; *dy = 0.0; return; }
+    if (sx >= -sy) {
+        if (sx > sy) { r = sx; if (sy > 0.0) theta = sy / r; else theta = 8.0f + sy / r; }
+        else { r = sy; theta = 2.0f - sx / r; }
+    } else {
+        if (sx <= sy) { r = -sx; theta = 4.0f - sy / r; }
+        else { r = -sy; theta = 6.0f + sx / r; }
+    }
+    theta *= PI_F / 4.f;
+    *dx = r * COSF(theta);
+    *dy = r * SINF(theta);
+}
+static inline V cosine_hemisphere(float u1, float u2) {
+    V r;
+    concentric_disk(u1, u2, &r.x, &r.y);
+    r.z = sqrtf(fmaxf_(0.f, 1.f - r.x * r.x - r.y * r.y));
+    return r;
+}
+static inline V uniform_sphere(float u1, float u2) {
+    float z = 1.f - 2.f * u1;
+    float r = sqrtf(fmaxf_(0.f, 1.f - z * z));
+    float phi = 2.f * PI_F * u2;
+    return v3(r * COSF(phi), r * SINF(phi), z);
+}
+static inline float power_heuristic(int nf, float fPdf, int ng, float gPdf) {
+    float f = nf * fPdf, g = ng * gPdf;
+    return (f * f) / (f * f + g * g);
+}
+
+/* ------------------------------------------------------------------ scene access */
+typedef struct {
+    const pbrtgpu_flat_scene *s;
+    int nb;
+} Ctx;
+static inline const float *SPEC(const Ctx *c, int off) { return c->s->spectra + off; }
+static inline float spec_y(const Ctx *c, const float *v) {
+    float yy = 0.f;
+    for (int i = 0; i < c->nb; ++i) yy += c->s->band_Y[i] * v[i];
+    return yy / c->s->y_int;
+}
+static inline int spec_black(const Ctx *c, const float *v) {
+    for (int i = 0; i < c->nb; ++i) if (v[i] != 0.) return 0;
+    return 1;
+}
+
+/* ------------------------------------------------------------------ shapes */
+typedef struct {   /* DifferentialGeometry (diffgeom.h) subset */
+    V p, nn, dpdu, dpdv, dndu, dndv;
+    float u, v;
+} DG;
+static void dg_init(DG *dg, V p, V dpdu, V dpdv, V dndu, V dndv, float u, float v, int flip) {
+    dg->p = p; dg->dpdu = dpdu; dg->dpdv = dpdv; dg->dndu = dndu; dg->dndv = dndv;
+    dg->nn = vnorm(vcross(dpdu, dpdv));
+    dg->u = u; dg->v = v;
+    if (flip) dg->nn = vmul(dg->nn, -1.f);
+}
+static void tri_uvs(const Ctx *c, const pbrtgpu_triangle *t, float uv[3][2]) {
+    const pbrtgpu_mesh *m = &c->s->meshes[t->mesh];
+    if (m->has_uvs) {
+        for (int k = 0; k < 3; ++k) { uv[k][0] = c->s->vert_uv[2 * t->v[k]]; uv[k][1] = c->s->vert_uv[2 * t->v[k] + 1]; }
+    } else {
+        uv[0][0] = 0.; uv[0][1] = 0.; uv[1][0] = 1.; uv[1][1] = 0.; uv[2][0] = 1.; uv[2][1] = 1.;
+    }
+}
+static inline V vert(const Ctx *c, int i) { const float *p = c->s->vert_p + 3 * i; return v3(p[0], p[1], p[2]); }
+static inline V vnormal(const Ctx *c, int i) { const float *p = c->s->vert_n + 3 * i; return v3(p[0], p[1], p[2]); }
+
+/* Triangle::Intersect / IntersectP (trianglemesh.cpp:119-273) */
+static int tri_intersect(const Ctx *c, int ti, const Ray *ray, float *tHit, float *rayEps, DG *dg) {
+    const pbrtgpu_triangle *t = &c->s->tris[ti];
+    V p1 = vert(c, t->v[0]), p2 = vert(c, t->v[1]), p3 = vert(c, t->v[2]);
+    V e1 = vsub(p2, p1), e2 = vsub(p3, p1);
+    V s1 = vcross(ray->d, e2);
+    float divisor = vdot(s1, e1);
+    if (divisor == 0.) return 0;
+    float invDivisor = 1.f / divisor;
+    V d = vsub(ray->o, p1);
+    float b1 = vdot(d, s1) * invDivisor;
+    if (b1 < 0. || b1 > 1.) return 0;
+    V s2 = vcross(d, e1);
+    float b2 = vdot(ray->d, s2) * invDivisor;
+    if (b2 < 0. || b1 + b2 > 1.) return 0;
+    float tt = vdot(e2, s2) * invDivisor;
+    if (tt < ray->mint || tt > ray->maxt) return 0;
+    if (!dg) { *tHit = tt; return 1; }
+    float uvs[3][2];
+    tri_uvs(c, t, uvs);
+    float du1 = uvs[0][0] - uvs[2][0], du2 = uvs[1][0] - uvs[2][0];
+    float dv1 = uvs[0][1] - uvs[2][1], dv2 = uvs[1][1] - uvs[2][1];
+    V dp1 = vsub(p1, p3), dp2 = vsub(p2, p3);
+    float determinant = du1 * dv2 - dv1 * du2;
+    V dpdu, dpdv;
+    if (determinant == 0.f) coordsys(vnorm(vcross(e2, e1)), &dpdu, &dpdv);
+    else {
+        float invdet = 1.f / determinant;
+        dpdu = vmul(vsub(vmul(dp1, dv2), vmul(dp2, dv1)), invdet);
+        dpdv = vmul(vadd(vmul(dp1, -du2), vmul(dp2, du1)), invdet);
+    }
+    float b0 = 1 - b1 - b2;
+    float tu = b0 * uvs[0][0] + b1 * uvs[1][0] + b2 * uvs[2][0];
+    float tv = b0 * uvs[0][1] + b1 * uvs[1][1] + b2 * uvs[2][1];
+    const pbrtgpu_mesh *m = &c->s->meshes[t->mesh];
+    dg_init(dg, rayat(ray, tt), dpdu, dpdv, v3(0, 0, 0), v3(0, 0, 0), tu, tv, m->reverse_orientation ^ m->swaps_handedness);
+    *tHit = tt;
+    *rayEps = 1e-3f * *tHit;
+    return 1;
+}
+/* transform.cpp:30-40 */
+static int solve2x2(const float A[2][2], const float B[2], float *x0, float *x1) {
+    float det = A[0][0] * A[1][1] - A[0][1] * A[1][0];
+    if (fabsf(det) < 1e-10f) return 0;
+    *x0 = (A[1][1] * B[0] - A[0][1] * B[1]) / det;
+    *x1 = (A[0][0] * B[1] - A[1][0] * B[0]) / det;
+    if (isnan(*x0) || isnan(*x1)) return 0;
+    return 1;
+}
+/* Triangle::GetShadingGeometry (trianglemesh.cpp:285-360) */
+static void tri_shading(const Ctx *c, int ti, const DG *dg, DG *dgs) {
+    const pbrtgpu_triangle *t = &c->s->tris[ti];
+    const pbrtgpu_mesh *m = &c->s->meshes[t->mesh];
+    if (!m->has_normals) { *dgs = *dg; return; }
+    float b[3];
+    float uv[3][2];
+    tri_uvs(c, t, uv);
+    float A[2][2] = {{uv[1][0] - uv[0][0], uv[2][0] - uv[0][0]}, {uv[1][1] - uv[0][1], uv[2][1] - uv[0][1]}};
+    float C[2] = {dg->u - uv[0][0], dg->v - uv[0][1]};
+    if (!solve2x2(A, C, &b[1], &b[2])) b[0] = b[1] = b[2] = 1.f / 3.f;
+    else b[0] = 1.f - b[1] - b[2];
+    V n0 = vnormal(c, t->v[0]), n1 = vnormal(c, t->v[1]), n2 = vnormal(c, t->v[2]);
+    /* b[0] * n[v0] + b[1] * n[v1] + b[2] * n[v2]  (Normal operator*(float, Normal) = (f*x,...)) */
+    V ni = vadd(vadd(vmul(n0, b[0]), vmul(n1, b[1])), vmul(n2, b[2]));
+    V ns = vnorm(xnormal(m->o2w_minv, ni));
+    V ss = vnorm(dg->dpdu);
+    V ts = vcross(ss, ns);
+    if (vlen2(ts) > 0.f) { ts = vnorm(ts); ss = vcross(ts, ns); }
+    else coordsys(ns, &ss, &ts);
+    V dndu, dndv;
+    {
+        float du1 = uv[0][0] - uv[2][0], du2 = uv[1][0] - uv[2][0];
+        float dv1 = uv[0][1] - uv[2][1], dv2 = uv[1][1] - uv[2][1];
+        V dn1 = vsub(n0, n2), dn2 = vsub(n1, n2);
+        float determinant = du1 * dv2 - dv1 * du2;
+        if (determinant == 0.f) dndu = dndv = v3(0, 0, 0);
+        else {
+            float invdet = 1.f / determinant;
+            /* Normal ops: (dv2 * dn1 - dv1 * dn2) * invdet */
+            dndu = vmul(vsub(vmul(dn1, dv2), vmul(dn2, dv1)), invdet);
+            dndv = vmul(vadd(vmul(dn1, -du2), vmul(dn2, du1)), invdet);
+        }
+    }
+    dg_init(dgs, dg->p, ss, ts, xnormal(m->o2w_minv, dndu), xnormal(m->o2w_minv, dndv), dg->u, dg->v,
+            m->reverse_orientation ^ m->swaps_handedness);
+}
+
+/* pbrt.h:297-311 */
+static int quadratic(float A, float B, float C, float *t0, float *t1) {
+    float discrim = B * B - 4.f * A * C;
+    if (discrim <= 0.) return 0;
+    float rootDiscrim = sqrtf(discrim);
+    float q;
+    if (B < 0) q = -.5f * (B - rootDiscrim);
+    else q = -.5f * (B + rootDiscrim);
+    *t0 = q / A;
+    *t1 = C / q;
+    if (*t0 > *t1) { float tmp = *t0; *t0 = *t1; *t1 = tmp; }
+    return 1;
+}
+/* WorldToObject(r) with WorldToObject = (o2w.mInv, o2w.m): Ray transform (transform.h:253-262) */
+static Ray to_object(const pbrtgpu_quadric *q, const Ray *r) {
+    Ray o = *r;
+    /* 2-arg point form: *ptrans /= w if w != 1 */
+    const float *m = q->o2w_minv;
+    V p = r->o;
+    float x = m[0] * p.x + m[1] * p.y + m[2] * p.z + m[3];
+    float y = m[4] * p.x + m[5] * p.y + m[6] * p.z + m[7];
+    float z = m[8] * p.x + m[9] * p.y + m[10] * p.z + m[11];
+    float w = m[12] * p.x + m[13] * p.y + m[14] * p.z + m[15];
+    o.o = v3(x, y, z);
+    if (w != 1.) o.o = vdiv(o.o, w);
+    o.d = xvec(m, r->d);
+    return o;
+}
+/* Sphere::Intersect (sphere.cpp:50-150); dg may be NULL (IntersectP) */
+static int sphere_intersect(const pbrtgpu_quadric *q, const Ray *r, float *tHit, float *rayEps, DG *dg) {
+    float phi;
+    V phit;
+    Ray ray = to_object(q, r);
+    float A = ray.d.x * ray.d.x + ray.d.y * ray.d.y + ray.d.z * ray.d.z;
+    float B = 2 * (ray.d.x * ray.o.x + ray.d.y * ray.o.y + ray.d.z * ray.o.z);
+    float C = ray.o.x * ray.o.x + ray.o.y * ray.o.y + ray.o.z * ray.o.z - q->radius * q->radius;
+    float t0, t1;
+    if (!quadratic(A, B, C, &t0, &t1)) return 0;
+    if (t0 > ray.maxt || t1 < ray.mint) return 0;
+    float thit = t0;
+    if (t0 < ray.mint) { thit = t1; if (thit > ray.maxt) return 0; }
+    phit = rayat(&ray, thit);
+    if (phit.x == 0.f && phit.y == 0.f) phit.x = 1e-5f * q->radius;
+    phi = ATAN2F(phit.y, phit.x);
+    if (phi < 0.) phi += 2.f * PI_F;
+    if ((q->zmin > -q->radius && phit.z < q->zmin) || (q->zmax < q->radius && phit.z > q->zmax) || phi > q->phi_max) {
+        if (thit == t1) return 0;
+        if (t1 > ray.maxt) return 0;
+        thit = t1;
+        phit = rayat(&ray, thit);
+        if (phit.x == 0.f && phit.y == 0.f) phit.x = 1e-5f * q->radius;
+        phi = ATAN2F(phit.y, phit.x);
+        if (phi < 0.) phi += 2.f * PI_F;
+        if ((q->zmin > -q->radius && phit.z < q->zmin) || (q->zmax < q->radius && phit.z > q->zmax) || phi > q->phi_max)
+            return 0;
+    }
+    if (!dg) { if (tHit) *tHit = thit; return 1; }
+    float u = phi / q->phi_max;
+    float theta = ACOSF(clampf(phit.z / q->radius, -1.f, 1.f));
+    float v = (theta - q->theta_min) / (q->theta_max - q->theta_min);
+    float zradius = sqrtf(phit.x * phit.x + phit.y * phit.y);
+    float invzradius = 1.f / zradius;
+    float cosphi = phit.x * invzradius, sinphi = phit.y * invzradius;
+    V dpdu = v3(-q->phi_max * phit.y, q->phi_max * phit.x, 0);
+    V dpdv = vmul(v3(phit.z * cosphi, phit.z * sinphi, -q->radius * SINF(theta)), q->theta_max - q->theta_min);
+    V d2Pduu = vmul(v3(phit.x, phit.y, 0), -q->phi_max * q->phi_max);
+    V d2Pduv = vmul(v3(-sinphi, cosphi, 0.), (q->theta_max - q->theta_min) * phit.z * q->phi_max);
+    V d2Pdvv = vmul(v3(phit.x, phit.y, phit.z), -(q->theta_max - q->theta_min) * (q->theta_max - q->theta_min));
+    float E = vdot(dpdu, dpdu), F = vdot(dpdu, dpdv), G = vdot(dpdv, dpdv);
+    V N = vnorm(vcross(dpdu, dpdv));
+    float e = vdot(N, d2Pduu), f = vdot(N, d2Pduv), g = vdot(N, d2Pdvv);
+    float invEGF2 = 1.f / (E * G - F * F);
+    V dndu = vadd(vmul(dpdu, (f * F - e * G) * invEGF2), vmul(dpdv, (e * F - f * E) * invEGF2));
+    V dndv = vadd(vmul(dpdu, (g * F - f * G) * invEGF2), vmul(dpdv, (f * F - g * E) * invEGF2));
+    dg_init(dg, xpoint(q->o2w_m, phit), xvec(q->o2w_m, dpdu), xvec(q->o2w_m, dpdv), xnormal(q->o2w_minv, dndu),
+            xnormal(q->o2w_minv, dndv), u, v, q->reverse_orientation ^ q->swaps_handedness);
+    *tHit = thit;
+    *rayEps = 5e-4f * *tHit;
+    return 1;
+}
+/* Disk::Intersect (disk.cpp:48-96) */
+static int disk_intersect(const pbrtgpu_quadric *q, const Ray *r, float *tHit, float *rayEps, DG *dg) {
+    Ray ray = to_object(q, r);
+    if (fabsf(ray.d.z) < 1e-7) return 0;
+    float thit = (q->height - ray.o.z) / ray.d.z;
+    if (thit < ray.mint || thit > ray.maxt) return 0;
+    V phit = rayat(&ray, thit);
+    float dist2 = phit.x * phit.x + phit.y * phit.y;
+    if (dist2 > q->radius * q->radius || dist2 < q->inner_radius * q->inner_radius) return 0;
+    float phi = ATAN2F(phit.y, phit.x);
+    if (phi < 0) phi = (float)((double)phi + 2. * (double)PI_F);
+    if (phi > q->phi_max) return 0;
+    if (!dg) { if (tHit) *tHit = thit; return 1; }
+    float u = phi / q->phi_max;
+    float oneMinusV = ((sqrtf(dist2) - q->inner_radius) / (q->radius - q->inner_radius));
+    float invOneMinusV = (oneMinusV > 0.f) ? (1.f / oneMinusV) : 0.f;
+    float v = 1.f - oneMinusV;
+    V dpdu = v3(-q->phi_max * phit.y, q->phi_max * phit.x, 0.);
+    V dpdv = v3(-phit.x * invOneMinusV, -phit.y * invOneMinusV, 0.);
+    dpdu = v3(dpdu.x * (q->phi_max * INV_TWOPI_F), dpdu.y * (q->phi_max * INV_TWOPI_F), dpdu.z * (q->phi_max * INV_TWOPI_F));
+    float sc = (q->radius - q->inner_radius) / q->radius;
+    dpdv = v3(dpdv.x * sc, dpdv.y * sc, dpdv.z * sc);
+    V zero = v3(0, 0, 0);
+    dg_init(dg, xpoint(q->o2w_m, phit), xvec(q->o2w_m, dpdu), xvec(q->o2w_m, dpdv), xnormal(q->o2w_minv, zero),
+            xnormal(q->o2w_minv, zero), u, v, q->reverse_orientation ^ q->swaps_handedness);
+    *tHit = thit;
+    *rayEps = 5e-4f * *tHit;
+    return 1;
+}
+static float shape_area(const Ctx *c, int type, int idx) {
+    if (type == PBRTGPU_SHAPE_TRIANGLE) {
+        const pbrtgpu_triangle *t = &c->s->tris[idx];
+        V p1 = vert(c, t->v[0]), p2 = vert(c, t->v[1]), p3 = vert(c, t->v[2]);
+        return 0.5f * vlen(vcross(vsub(p2, p1), vsub(p3, p1)));
+    }
+    const pbrtgpu_quadric *q = &c->s->quadrics[idx];
+    if (type == PBRTGPU_SHAPE_SPHERE) return q->phi_max * q->radius * (q->zmax - q->zmin);
+    return q->phi_max * 0.5f * (q->radius * q->radius - q->inner_radius * q->inner_radius);
+}
+static int shape_intersect(const Ctx *c, int type, int idx, const Ray *r, float *tHit, float *eps, DG *dg) {
+    if (type == PBRTGPU_SHAPE_TRIANGLE) return tri_intersect(c, idx, r, tHit, eps, dg);
+    if (type == PBRTGPU_SHAPE_SPHERE) return sphere_intersect(&c->s->quadrics[idx], r, tHit, eps, dg);
+    return disk_intersect(&c->s->quadrics[idx], r, tHit, eps, dg);
+}
+
+/* ------------------------------------------------------------------ BVH */
+static inline int bbox_hit(const pbrtgpu_bvh_node *n, const Ray *ray, V invDir, const int dirIsNeg[3]) {
+    const float *b0 = n->bmin, *b1 = n->bmax;
+    float tmin = ((dirIsNeg[0] ? b1 : b0)[0] - ray->o.x) * invDir.x;
+    float tmax = ((dirIsNeg[0] ? b0 : b1)[0] - ray->o.x) * invDir.x;
+    float tymin = ((dirIsNeg[1] ? b1 : b0)[1] - ray->o.y) * invDir.y;
+    float tymax = ((dirIsNeg[1] ? b0 : b1)[1] - ray->o.y) * invDir.y;
+    if ((tmin > tymax) || (tymin > tmax)) return 0;
+    if (tymin > tmin) tmin = tymin;
+    if (tymax < tmax) tmax = tymax;
+    float tzmin = ((dirIsNeg[2] ? b1 : b0)[2] - ray->o.z) * invDir.z;
+    float tzmax = ((dirIsNeg[2] ? b0 : b1)[2] - ray->o.z) * invDir.z;
+    if ((tmin > tzmax) || (tzmin > tmax)) return 0;
+    if (tzmin > tmin) tmin = tzmin;
+    if (tzmax < tmax) tmax = tzmax;
+    return (tmin < ray->maxt) && (tmax > ray->mint);
+}
+typedef struct { int prim; float t; } Hit;
+/* BVHAccel::Intersect (bvh.cpp:380-432); updates ray->maxt like GeometricPrimitive */
+static int bvh_intersect(const Ctx *c, Ray *ray, Hit *hit) {
+    const pbrtgpu_bvh_node *nodes = c->s->nodes;
+    V invDir = v3(1.f / ray->d.x, 1.f / ray->d.y, 1.f / ray->d.z);
+    int dirIsNeg[3] = {invDir.x < 0, invDir.y < 0, invDir.z < 0};
+    uint32_t todo[64];
+    int todoOffset = 0;
+    uint32_t nodeNum = 0;
+    int found = 0;
+    for (;;) {
+        const pbrtgpu_bvh_node *node = &nodes[nodeNum];
+        if (bbox_hit(node, ray, invDir, dirIsNeg)) {
+            uint32_t np = node->meta & 0xff;
+            if (np > 0) {
+                for (uint32_t i = 0; i < np; ++i) {
+                    const pbrtgpu_prim *pr = &c->s->prims[node->offset + i];
+                    float t, eps;
+                    if (shape_intersect(c, pr->shape_type, pr->shape_index, ray, &t, &eps, NULL)) {
+                        ray->maxt = t;
+                        hit->prim = (int)(node->offset + i);
+                        hit->t = t;
+                        found = 1;
+                    }
+                }
+                if (todoOffset == 0) break;
+                nodeNum = todo[--todoOffset];
+            } else {
+                uint32_t axis = (node->meta >> 8) & 0xff;
+                if (dirIsNeg[axis]) { todo[todoOffset++] = nodeNum + 1; nodeNum = node->offset; }
+                else { todo[todoOffset++] = node->offset; nodeNum = nodeNum + 1; }
+            }
+        } else {
+            if (todoOffset == 0) break;
+            nodeNum = todo[--todoOffset];
+        }
+    }
+    return found;
+}
+static int bvh_intersectP(const Ctx *c, const Ray *ray) {
+    const pbrtgpu_bvh_node *nodes = c->s->nodes;
+    V invDir = v3(1.f / ray->d.x, 1.f / ray->d.y, 1.f / ray->d.z);
+    int dirIsNeg[3] = {invDir.x < 0, invDir.y < 0, invDir.z < 0};
+    uint32_t todo[64];
+    int todoOffset = 0;
+    uint32_t nodeNum = 0;
+    for (;;) {
+        const pbrtgpu_bvh_node *node = &nodes[nodeNum];
+        if (bbox_hit(node, ray, invDir, dirIsNeg)) {
+            uint32_t np = node->meta & 0xff;
+            if (np > 0) {
+                for (uint32_t i = 0; i < np; ++i) {
+                    const pbrtgpu_prim *pr = &c->s->prims[node->offset + i];
+                    float t, eps;
+                    if (shape_intersect(c, pr->shape_type, pr->shape_index, ray, &t, &eps, NULL)) return 1;
+                }
+                if (todoOffset == 0) break;
+                nodeNum = todo[--todoOffset];
+            } else {
+                uint32_t axis = (node->meta >> 8) & 0xff;
+                if (dirIsNeg[axis]) { todo[todoOffset++] = nodeNum + 1; nodeNum = node->offset; }
+                else { todo[todoOffset++] = node->offset; nodeNum = nodeNum + 1; }
+            }
+        } else {
+            if (todoOffset == 0) break;
+            nodeNum = todo[--todoOffset];
+        }
+    }
+    return 0;
+}
+/* full intersection record for a recorded closest hit */
+typedef struct { DG dg; float rayEps; int prim; } Isect;
+static void isect_fill(const Ctx *c, const Ray *ray, const Hit *h, Isect *is) {
+    const pbrtgpu_prim *pr = &c->s->prims[h->prim];
+    Ray r = *ray;
+    r.maxt = h->t;
+    float t;
+    shape_intersect(c, pr->shape_type, pr->shape_index, &r, &t, &is->rayEps, &is->dg);
+    is->prim = h->prim;
+}
+
+/* ------------------------------------------------------------------ BSDF */
+enum { BSDF_REFLECTION = 1, BSDF_TRANSMISSION = 2, BSDF_DIFFUSE = 4, BSDF_GLOSSY = 8, BSDF_SPECULAR = 16,
+       BSDF_ALL = 31 };
+enum { BX_LAMBERT, BX_OREN, BX_MICRO_BLINN_DIEL, BX_SPEC_REFL_NOOP, BX_FRESNEL_BLEND_ANISO };
+typedef struct {
+    int kind, type;
+    const float *R;      /* reflectance spectrum */
+    const float *R2;     /* second spectrum (FresnelBlend Rs) */
+    float a, b;          /* OrenNayar A,B ; Blinn exponent ; Aniso ex,ey */
+    float eta_i, eta_t;  /* FresnelDielectric */
+} BxDF;
+typedef struct {
+    V nn, ng, sn, tn;
+    int n;
+    BxDF bx[4];
+} BSDF;
+static inline int matches(const BxDF *b, int flags) { return (b->type & flags) == b->type; }
+static inline V to_local(const BSDF *b, V v) { return v3(vdot(v, b->sn), vdot(v, b->tn), vdot(v, b->nn)); }
+static inline V to_world(const BSDF *b, V v) {
+    return v3(b->sn.x * v.x + b->tn.x * v.y + b->nn.x * v.z, b->sn.y * v.x + b->tn.y * v.y + b->nn.y * v.z,
+              b->sn.z * v.x + b->tn.z * v.y + b->nn.z * v.z);
+}
+static inline float costh(V w) { return w.z; }
+static inline float abscos(V w) { return fabsf(w.z); }
+static inline float sin2(V w) { return fmaxf_(0.f, 1.f - costh(w) * costh(w)); }
+static inline float sinth(V w) { return sqrtf(sin2(w)); }
+static inline float cosphi(V w) { float s = sinth(w); if (s == 0.f) return 1.f; return clampf(w.x / s, -1.f, 1.f); }
+static inline float sinphi(V w) { float s = sinth(w); if (s == 0.f) return 0.f; return clampf(w.y / s, -1.f, 1.f); }
+static inline int samehemi(V w, V wp) { return w.z * wp.z > 0.f; }
+
+/* FresnelDielectric::Evaluate + FrDiel (reflection.cpp:52-58,112-127); all bands equal */
+static float fr_dielectric(float cosi, float eta_i, float eta_t) {
+    cosi = clampf(cosi, -1.f, 1.f);
+    int entering = cosi > 0.;
+    float ei = eta_i, et = eta_t;
+    if (!entering) { float t = ei; ei = et; et = t; }
+    float sint = ei / et * sqrtf(fmaxf_(0.f, 1.f - cosi * cosi));
+    if (sint >= 1.) return 1.f;
+    float cost = sqrtf(fmaxf_(0.f, 1.f - sint * sint));
+    float ci = fabsf(cosi);
+    float Rparl = ((et * ci) - (ei * cost)) / ((et * ci) + (ei * cost));
+    float Rperp = ((ei * ci) - (et * cost)) / ((ei * ci) + (et * cost));
+    return (Rparl * Rparl + Rperp * Rperp) / 2.f;
+}
+static inline float blinn_D(float e, V wh) { return (e + 2) * INV_TWOPI_F * POWF(abscos(wh), e); }
+static inline float micro_G(V wo, V wi, V wh) {
+    float NdotWh = abscos(wh), NdotWo = abscos(wo), NdotWi = abscos(wi), WOdotWh = fabsf(vdot(wo, wh));
+    return fminf_(1.f, fminf_((2.f * NdotWh * NdotWo / WOdotWh), (2.f * NdotWh * NdotWi / WOdotWh)));
+}
+static float blinn_pdf(float e, V wo, V wi) {
+    V wh = vnorm(vadd(wo, wi));
+    float costheta = abscos(wh);
+    float p = ((e + 1.f) * POWF(costheta, e)) / (2.f * PI_F * 4.f * vdot(wo, wh));
+    if (vdot(wo, wh) <= 0.f) p = 0.f;
+    return p;
+}
+static void blinn_sample(float e, V wo, V *wi, float u1, float u2, float *pdf) {
+    float costheta = POWF(u1, 1.f / (e + 1));
+    float sintheta = sqrtf(fmaxf_(0.f, 1.f - costheta * costheta));
+    float phi = u2 * 2.f * PI_F;
+    V wh = v3(sintheta * COSF(phi), sintheta * SINF(phi), costheta);
+    if (!samehemi(wo, wh)) wh = vneg(wh);
+    *wi = vadd(vneg(wo), vmul(wh, 2.f * vdot(wo, wh)));
+    float p = ((e + 1.f) * POWF(costheta, e)) / (2.f * PI_F * 4.f * vdot(wo, wh));
+    if (vdot(wo, wh) <= 0.f) p = 0.f;
+    *pdf = p;
+}
+/* Anisotropic (reflection.cpp:369-435) */
+static inline float aniso_D(float ex, float ey, V wh) {
+    float costhetah = abscos(wh);
+    float d = 1.f - costhetah * costhetah;
+    if (d == 0.f) return 0.f;
+    float e = (ex * wh.x * wh.x + ey * wh.y * wh.y) / d;
+    return sqrtf((ex + 2.f) * (ey + 2.f)) * INV_TWOPI_F * POWF(costhetah, e);
+}
+static float aniso_pdf(float ex, float ey, V wo, V wi) {
+    V wh = vnorm(vadd(wo, wi));
+    float costhetah = abscos(wh);
+    float ds = 1.f - costhetah * costhetah;
+    float p = 0.f;
+    if (ds > 0.f && vdot(wo, wh) > 0.f) {
+        float e = (ex * wh.x * wh.x + ey * wh.y * wh.y) / ds;
+        float d = sqrtf((ex + 1.f) * (ey + 1.f)) * INV_TWOPI_F * POWF(costhetah, e);
+        p = d / (4.f * vdot(wo, wh));
+    }
+    return p;
+}
+static void aniso_first_quadrant(float ex, float ey, float u1, float u2, float *phi, float *costheta) {
+    if (ex == ey) *phi = PI_F * u1 * 0.5f;
+    else *phi = ATANF(sqrtf((ex + 1.f) / (ey + 1.f)) * TANF(PI_F * u1 * 0.5f));
+    float cp = COSF(*phi), sp = SINF(*phi);
+    *costheta = POWF(u2, 1.f / (ex * cp * cp + ey * sp * sp + 1));
+}
+static void aniso_sample(float ex, float ey, V wo, V *wi, float u1, float u2, float *pdf) {
+    float phi, costheta;
+    if (u1 < .25f) aniso_first_quadrant(ex, ey, 4.f * u1, u2, &phi, &costheta);
+    else if (u1 < .5f) { u1 = 4.f * (.5f - u1); aniso_first_quadrant(ex, ey, u1, u2, &phi, &costheta); phi = PI_F - phi; }
+    else if (u1 < .75f) { u1 = 4.f * (u1 - .5f); aniso_first_quadrant(ex, ey, u1, u2, &phi, &costheta); phi += PI_F; }
+    else { u1 = 4.f * (1.f - u1); aniso_first_quadrant(ex, ey, u1, u2, &phi, &costheta); phi = 2.f * PI_F - phi; }
+    float sintheta = sqrtf(fmaxf_(0.f, 1.f - costheta * costheta));
+    V wh = v3(sintheta * COSF(phi), sintheta * SINF(phi), costheta);
+    if (!samehemi(wo, wh)) wh = vneg(wh);
+    *wi = vadd(vneg(wo), vmul(wh, 2.f * vdot(wo, wh)));
+    float costhetah = abscos(wh);
+    float ds = 1.f - costhetah * costhetah;
+    float p = 0.f;
+    if (ds > 0.f && vdot(wo, wh) > 0.f) {
+        float e = (ex * wh.x * wh.x + ey * wh.y * wh.y) / ds;
+        float d = sqrtf((ex + 1.f) * (ey + 1.f)) * INV_TWOPI_F * POWF(costhetah, e);
+        p = d / (4.f * vdot(wo, wh));
+    }
+    *pdf = p;
+}
+
+/* BxDF::f for one bxdf, accumulated band-wise into out (out += f) */
+static void bx_f_add(const Ctx *c, const BxDF *b, V wo, V wi, float *out) {
+    int nb = c->nb;
+    switch (b->kind) {
+        case BX_LAMBERT:
+            for (int i = 0; i < nb; ++i) out[i] += b->R[i] * INV_PI_F;
+            break;
+        case BX_OREN: {   /* reflection.cpp:170-193 */
+            float sinthetai = sinth(wi), sinthetao = sinth(wo);
+            float maxcos = 0.f;
+            if (sinthetai > 1e-4 && sinthetao > 1e-4) {
+                float sinphii = sinphi(wi), cosphii = cosphi(wi), sinphio = sinphi(wo), cosphio = cosphi(wo);
+                float dcos = cosphii * cosphio + sinphii * sinphio;
+                maxcos = fmaxf_(0.f, dcos);
+            }
+            float sinalpha, tanbeta;
+            if (abscos(wi) > abscos(wo)) { sinalpha = sinthetao; tanbeta = sinthetai / abscos(wi); }
+            else { sinalpha = sinthetai; tanbeta = sinthetao / abscos(wo); }
+            float s = (b->a + b->b * maxcos * sinalpha * tanbeta);
+            for (int i = 0; i < nb; ++i) out[i] += (b->R[i] * INV_PI_F) * s;
+            break;
+        }
+        case BX_MICRO_BLINN_DIEL: {   /* Microfacet::f (reflection.cpp:203-214) */
+            float cosThetaO = abscos(wo), cosThetaI = abscos(wi);
+            if (cosThetaI == 0.f || cosThetaO == 0.f) { for (int i = 0; i < nb; ++i) out[i] += 0.f; break; }
+            V wh = vadd(wi, wo);
+            if (wh.x == 0. && wh.y == 0. && wh.z == 0.) { for (int i = 0; i < nb; ++i) out[i] += 0.f; break; }
+            wh = vnorm(wh);
+            float cosThetaH = vdot(wi, wh);
+            float F = fr_dielectric(cosThetaH, b->eta_i, b->eta_t);
+            float D = blinn_D(b->a, wh), G = micro_G(wo, wi, wh);
+            float den = 4.f * cosThetaI * cosThetaO;
+            for (int i = 0; i < nb; ++i) out[i] += (((b->R[i] * D) * G) * F) / den;
+            break;
+        }
+        case BX_SPEC_REFL_NOOP:
+            for (int i = 0; i < nb; ++i) out[i] += 0.f;
+            break;
+        case BX_FRESNEL_BLEND_ANISO: {   /* FresnelBlend::f (reflection.cpp:224-236) */
+            float cd = (28.f / (23.f * PI_F));
+            float ta = (1.f - POWF(1.f - .5f * abscos(wi), 5)), tb = (1.f - POWF(1.f - .5f * abscos(wo), 5));
+            V wh = vadd(wi, wo);
+            if (wh.x == 0. && wh.y == 0. && wh.z == 0.) { for (int i = 0; i < nb; ++i) out[i] += 0.f; break; }
+            wh = vnorm(wh);
+            float D = aniso_D(b->a, b->b, wh);
+            float den = (4.f * fabsf(vdot(wi, wh)) * fmaxf_(abscos(wi), abscos(wo)));
+            float schl = POWF(1 - vdot(wi, wh), 5.f);
+            for (int i = 0; i < nb; ++i) {
+                float diffuse = ((((cd * b->R[i]) * (1.f - b->R2[i])) * ta) * tb);
+                float schlick = b->R2[i] + schl * (1.f - b->R2[i]);
+                float specular = (D / den) * schlick;
+                out[i] += diffuse + specular;
+            }
+            break;
+        }
+    }
+}
+static float bx_pdf(const BxDF *b, V wo, V wi) {
+    switch (b->kind) {
+        case BX_MICRO_BLINN_DIEL:
+            if (!samehemi(wo, wi)) return 0.f;
+            return blinn_pdf(b->a, wo, wi);
+        case BX_SPEC_REFL_NOOP: return 0.;
+        case BX_FRESNEL_BLEND_ANISO:
+            if (!samehemi(wo, wi)) return 0.f;
+            return .5f * (abscos(wi) * INV_PI_F + aniso_pdf(b->a, b->b, wo, wi));
+        default: return samehemi(wo, wi) ? abscos(wi) * INV_PI_F : 0.f;
+    }
+}
+/* BxDF::Sample_f; returns f into fout (overwritten) */
+static void bx_sample_f(const Ctx *c, const BxDF *b, V wo, V *wi, float u1, float u2, float *pdf, float *fout) {
+    int nb = c->nb;
+    for (int i = 0; i < nb; ++i) fout[i] = 0.f;
+    switch (b->kind) {
+        case BX_MICRO_BLINN_DIEL:
+            blinn_sample(b->a, wo, wi, u1, u2, pdf);
+            if (!samehemi(wo, *wi)) return;
+            bx_f_add(c, b, wo, *wi, fout);
+            return;
+        case BX_SPEC_REFL_NOOP: {   /* SpecularReflection::Sample_f with FresnelNoOp */
+            *wi = v3(-wo.x, -wo.y, wo.z);
+            *pdf = 1.f;
+            float d = abscos(*wi);
+            for (int i = 0; i < nb; ++i) fout[i] = (1.f * b->R[i]) / d;
+            return;
+        }
+        case BX_FRESNEL_BLEND_ANISO:
+            if (u1 < .5) {
+                u1 = 2.f * u1;
+                *wi = cosine_hemisphere(u1, u2);
+                if (wo.z < 0.) wi->z *= -1.f;
+            } else {
+                u1 = 2.f * (u1 - .5f);
+                aniso_sample(b->a, b->b, wo, wi, u1, u2, pdf);
+                if (!samehemi(wo, *wi)) return;
+            }
+            *pdf = bx_pdf(b, wo, *wi);
+            bx_f_add(c, b, wo, *wi, fout);
+            return;
+        default:
+            *wi = cosine_hemisphere(u1, u2);
+            if (wo.z < 0.) wi->z *= -1.f;
+            *pdf = bx_pdf(b, wo, *wi);
+            bx_f_add(c, b, wo, *wi, fout);
+            return;
+    }
+}
+/* BSDF::f (reflection.cpp:604-618) */
+static void bsdf_f(const Ctx *c, const BSDF *bs, V woW, V wiW, int flags, float *f) {
+    V wi = to_local(bs, wiW), wo = to_local(bs, woW);
+    if (vdot(wiW, bs->ng) * vdot(woW, bs->ng) > 0) flags &= ~BSDF_TRANSMISSION;
+    else flags &= ~BSDF_REFLECTION;
+    for (int i = 0; i < c->nb; ++i) f[i] = 0.f;
+    for (int k = 0; k < bs->n; ++k)
+        if (matches(&bs->bx[k], flags)) bx_f_add(c, &bs->bx[k], wo, wi, f);
+}
+/* BSDF::Pdf (reflection.cpp:575-590) */
+static float bsdf_pdf(const BSDF *bs, V woW, V wiW, int flags) {
+    if (bs->n == 0.) return 0.;
+    V wo = to_local(bs, woW), wi = to_local(bs, wiW);
+    float pdf = 0.f;
+    int m = 0;
+    for (int k = 0; k < bs->n; ++k)
+        if (matches(&bs->bx[k], flags)) { ++m; pdf += bx_pdf(&bs->bx[k], wo, wi); }
+    return m > 0 ? pdf / m : 0.f;
+}
+/* BSDF::Sample_f (reflection.cpp:514-572) */
+static void bsdf_sample_f(const Ctx *c, const BSDF *bs, V woW, V *wiW, float u0, float u1, float uc, float *pdf,
+                          int flags, int *sampledType, float *f) {
+    int nb = c->nb;
+    int matching = 0;
+    for (int k = 0; k < bs->n; ++k) if (matches(&bs->bx[k], flags)) ++matching;
+    if (matching == 0) { *pdf = 0.f; *sampledType = 0; for (int i = 0; i < nb; ++i) f[i] = 0.f; return; }
+    int which = (int)floorf(uc * matching);
+    if (which > matching - 1) which = matching - 1;
+    const BxDF *bx = NULL;
+    int count = which;
+    for (int k = 0; k < bs->n; ++k)
+        if (matches(&bs->bx[k], flags) && count-- == 0) { bx = &bs->bx[k]; break; }
+    V wo = to_local(bs, woW), wi;
+    *pdf = 0.f;
+    bx_sample_f(c, bx, wo, &wi, u0, u1, pdf, f);
+    if (*pdf == 0.f) { *sampledType = 0; for (int i = 0; i < nb; ++i) f[i] = 0.f; return; }
+    *sampledType = bx->type;
+    *wiW = to_world(bs, wi);
+    if (!(bx->type & BSDF_SPECULAR) && matching > 1)
+        for (int k = 0; k < bs->n; ++k)
+            if (&bs->bx[k] != bx && matches(&bs->bx[k], flags)) *pdf += bx_pdf(&bs->bx[k], wo, wi);
+    if (matching > 1) *pdf /= matching;
+    if (!(bx->type & BSDF_SPECULAR)) {
+        for (int i = 0; i < nb; ++i) f[i] = 0.f;
+        if (vdot(*wiW, bs->ng) * vdot(woW, bs->ng) > 0) flags &= ~BSDF_TRANSMISSION;
+        else flags &= ~BSDF_REFLECTION;
+        for (int k = 0; k < bs->n; ++k)
+            if (matches(&bs->bx[k], flags)) bx_f_add(c, &bs->bx[k], wo, wi, f);
+    }
+}
+
+/* Intersection::GetBSDF -> GetShadingGeometry -> Material::GetBSDF (with Bump) */
+static void get_bsdf(const Ctx *c, const Isect *is, BSDF *bs, DG *dgsOut) {
+    const pbrtgpu_prim *pr = &c->s->prims[is->prim];
+    const pbrtgpu_material *mt = &c->s->materials[pr->material];
+    DG dgs;
+    int ro, swaps;
+    if (pr->shape_type == PBRTGPU_SHAPE_TRIANGLE) {
+        tri_shading(c, pr->shape_index, &is->dg, &dgs);
+        const pbrtgpu_mesh *m = &c->s->meshes[c->s->tris[pr->shape_index].mesh];
+        ro = m->reverse_orientation; swaps = m->swaps_handedness;
+    } else {
+        dgs = is->dg;
+        const pbrtgpu_quadric *q = &c->s->quadrics[pr->shape_index];
+        ro = q->reverse_orientation; swaps = q->swaps_handedness;
+    }
+    /* Material::Bump with constant displacement d (material.cpp:39-81); du = dv = .01f
+     * gives the identical result for any positive du because (d - d) == 0 */
+    float d = mt->f[7];
+    float du = .01f, dv = .01f;
+    DG b = dgs;
+    b.dpdu = vadd(vadd(dgs.dpdu, vmul(dgs.nn, (d - d) / du)), vmul(dgs.dndu, d));
+    b.dpdv = vadd(vadd(dgs.dpdv, vmul(dgs.nn, (d - d) / dv)), vmul(dgs.dndv, d));
+    b.nn = vnorm(vcross(b.dpdu, b.dpdv));
+    if (ro ^ swaps) b.nn = vmul(b.nn, -1.f);
+    b.nn = faceforward(b.nn, is->dg.nn);
+    /* BSDF ctor (reflection.cpp:593-601) */
+    bs->ng = is->dg.nn;
+    bs->nn = b.nn;
+    bs->sn = vnorm(b.dpdu);
+    bs->tn = vcross(bs->nn, bs->sn);
+    bs->n = 0;
+    *dgsOut = b;
+    switch (mt->type) {
+        case PBRTGPU_MAT_MATTE: {
+            BxDF *x = &bs->bx[bs->n++];
+            x->R = SPEC(c, mt->spec[0]);
+            x->type = BSDF_REFLECTION | BSDF_DIFFUSE;
+            float sig = mt->f[0];
+            if (sig == 0.) x->kind = BX_LAMBERT;
+            else {
+                x->kind = BX_OREN;
+                float sigma = (PI_F / 180.f) * sig;
+                float sigma2 = sigma * sigma;
+                x->a = 1.f - (sigma2 / (2.f * (sigma2 + 0.33f)));
+                x->b = 0.45f * sigma2 / (sigma2 + 0.09f);
+            }
+            break;
+        }
+        case PBRTGPU_MAT_PLASTIC: {
+            BxDF *x = &bs->bx[bs->n++];
+            x->kind = BX_LAMBERT; x->type = BSDF_REFLECTION | BSDF_DIFFUSE; x->R = SPEC(c, mt->spec[0]);
+            x = &bs->bx[bs->n++];
+            x->kind = BX_MICRO_BLINN_DIEL; x->type = BSDF_REFLECTION | BSDF_GLOSSY; x->R = SPEC(c, mt->spec[1]);
+            float e = 1.f / mt->f[0];
+            if (e > 10000.f || isnan(e)) e = 10000.f;   /* Blinn ctor */
+            x->a = e; x->eta_i = 1.5f; x->eta_t = 1.f;
+            break;
+        }
+        case PBRTGPU_MAT_MIRROR: {
+            if (!spec_black(c, SPEC(c, mt->spec[0]))) {
+                BxDF *x = &bs->bx[bs->n++];
+                x->kind = BX_SPEC_REFL_NOOP; x->type = BSDF_REFLECTION | BSDF_SPECULAR; x->R = SPEC(c, mt->spec[0]);
+            }
+            break;
+        }
+        case PBRTGPU_MAT_SUBSTRATE: {
+            BxDF *x = &bs->bx[bs->n++];
+            x->kind = BX_FRESNEL_BLEND_ANISO; x->type = BSDF_REFLECTION | BSDF_GLOSSY;
+            x->R = SPEC(c, mt->spec[0]); x->R2 = SPEC(c, mt->spec[1]);
+            float ex = 1.f / mt->f[0], ey = 1.f / mt->f[1];
+            if (ex > 10000.f || isnan(ex)) ex = 10000.f;
+            if (ey > 10000.f || isnan(ey)) ey = 10000.f;
+            x->a = ex; x->b = ey;
+            break;
+        }
+        default: break;
+    }
+}
+
+/* ------------------------------------------------------------------ lights */
+/* Sphere::Sample(p,u1,u2) (sphere.cpp:228-254) */
+static V sphere_sample_p(const pbrtgpu_quadric *q, V p, float u1, float u2, V *ns) {
+    V Pcenter = xpoint(q->o2w_m, v3(0, 0, 0));
+    V wc = vnorm(vsub(Pcenter, p));
+    V wcX, wcY;
+    coordsys(wc, &wcX, &wcY);
+    if (vlen2(vsub(p, Pcenter)) - q->radius * q->radius < 1e-4f) {
+        V pp = vadd(v3(0, 0, 0), vmul(uniform_sphere(u1, u2), q->radius));
+        *ns = vnorm(xnormal(q->o2w_minv, v3(pp.x, pp.y, pp.z)));
+        if (q->reverse_orientation) *ns = vmul(*ns, -1.f);
+        return xpoint(q->o2w_m, pp);
+    }
+    float sinThetaMax2 = q->radius * q->radius / vlen2(vsub(p, Pcenter));
+    float cosThetaMax = sqrtf(fmaxf_(0.f, 1.f - sinThetaMax2));
+    /* UniformSampleCone(u1,u2,cosThetaMax,wcX,wcY,wc) (montecarlo.cpp:381-388) */
+    float costheta = lerpf(u1, cosThetaMax, 1.f);
+    float sintheta = sqrtf(1.f - costheta * costheta);
+    float phi = u2 * 2.f * PI_F;
+    V dir = vadd(vadd(vmul(wcX, COSF(phi) * sintheta), vmul(wcY, SINF(phi) * sintheta)), vmul(wc, costheta));
+    Ray r; r.o = p; r.d = dir; r.mint = 1e-3f; r.maxt = INFINITY; r.time = 0.f;
+    float thit, eps;
+    DG dgs;
+    if (!sphere_intersect(q, &r, &thit, &eps, &dgs)) thit = vdot(vsub(Pcenter, p), vnorm(r.d));
+    V ps = rayat(&r, thit);
+    *ns = vnorm(vsub(ps, Pcenter));
+    if (q->reverse_orientation) *ns = vmul(*ns, -1.f);
+    return ps;
+}
+/* Shape::Pdf(p, wi) (shape.cpp:78-91) */
+static float shape_pdf_generic(const Ctx *c, int type, int idx, V p, V wi) {
+    Ray ray; ray.o = p; ray.d = wi; ray.mint = 1e-3f; ray.maxt = INFINITY; ray.time = 0.f;
+    float thit, eps;
+    DG dg;
+    if (!shape_intersect(c, type, idx, &ray, &thit, &eps, &dg)) return 0.;
+    float pdf = vlen2(vsub(p, rayat(&ray, thit))) / (fabsf(vdot(dg.nn, vneg(wi))) * shape_area(c, type, idx));
+    if (isinf(pdf)) pdf = 0.f;
+    return pdf;
+}
+static float shape_pdf(const Ctx *c, int type, int idx, V p, V wi) {
+    if (type == PBRTGPU_SHAPE_SPHERE) {   /* sphere.cpp:256-266 */
+        const pbrtgpu_quadric *q = &c->s->quadrics[idx];
+        V Pcenter = xpoint(q->o2w_m, v3(0, 0, 0));
+        if (vlen2(vsub(p, Pcenter)) - q->radius * q->radius < 1e-4f) return shape_pdf_generic(c, type, idx, p, wi);
+        float sinThetaMax2 = q->radius * q->radius / vlen2(vsub(p, Pcenter));
+        float cosThetaMax = sqrtf(fmaxf_(0.f, 1.f - sinThetaMax2));
+        return 1.f / (2.f * PI_F * (1.f - cosThetaMax));
+    }
+    return shape_pdf_generic(c, type, idx, p, wi);
+}
+/* Shape::Sample(p, u1, u2) for triangle / disk = Sample(u1, u2) */
+static V shape_sample_p(const Ctx *c, int type, int idx, V p, float u1, float u2, V *ns) {
+    if (type == PBRTGPU_SHAPE_SPHERE) return sphere_sample_p(&c->s->quadrics[idx], p, u1, u2, ns);
+    if (type == PBRTGPU_SHAPE_DISK) {   /* disk.cpp:140-150 */
+        const pbrtgpu_quadric *q = &c->s->quadrics[idx];
+        V pp;
+        concentric_disk(u1, u2, &pp.x, &pp.y);
+        pp.x *= q->radius; pp.y *= q->radius; pp.z = q->height;
+        *ns = vnorm(xnormal(q->o2w_minv, v3(0, 0, 1)));
+        if (q->reverse_orientation) *ns = vmul(*ns, -1.f);
+        return xpoint(q->o2w_m, pp);
+    }
+    /* Triangle::Sample (trianglemesh.cpp:436-448) */
+    const pbrtgpu_triangle *t = &c->s->tris[idx];
+    const pbrtgpu_mesh *m = &c->s->meshes[t->mesh];
+    float su1 = sqrtf(u1);
+    float b1 = 1.f - su1, b2 = u2 * su1;
+    V p1 = vert(c, t->v[0]), p2 = vert(c, t->v[1]), p3 = vert(c, t->v[2]);
+    V pp = vadd(vadd(vmul(p1, b1), vmul(p2, b2)), vmul(p3, (1.f - b1 - b2)));
+    V n = vcross(vsub(p2, p1), vsub(p3, p1));
+    *ns = vnorm(n);
+    if (m->reverse_orientation) *ns = vmul(*ns, -1.f);
+    return pp;
+}
+/* Distribution1D::SampleDiscrete (montecarlo.h:83-91) over cdf[1..n] (cdf[0] = 0) */
+static int sample_discrete(const pbrtgpu_light_shape *ls, int n, float u) {
+    /* upper_bound(cdf, cdf+n+1, u) with cdf[0]=0 */
+    int lo = 0, count = n + 1;
+    while (count > 0) {
+        int step = count / 2, it = lo + step;
+        float cv = it == 0 ? 0.f : ls[it - 1].cdf;
+        if (!(u < cv)) { lo = it + 1; count -= step + 1; }
+        else count = step;
+    }
+    int off = lo - 1;
+    return off < 0 ? 0 : off;
+}
+typedef struct { V o, d; float mint, maxt; } Seg;
+/* Light::Sample_L (diffuse.cpp:61-74, point.cpp:42-49); returns Li into Li[] */
+static void light_sample_L(const Ctx *c, const pbrtgpu_light *L, V p, float pEps, const float u[3], float time,
+                           V *wi, float *pdf, Seg *vis, float *Li) {
+    int nb = c->nb;
+    const float *Ls = SPEC(c, L->spec);
+    (void)time;
+    if (L->type == PBRTGPU_LIGHT_POINT) {
+        V lp = v3(L->pos[0], L->pos[1], L->pos[2]);
+        *wi = vnorm(vsub(lp, p));
+        *pdf = 1.f;
+        float dist = vlen(vsub(p, lp));
+        vis->o = p; vis->d = vdiv(vsub(lp, p), dist); vis->mint = pEps; vis->maxt = dist * (1.f - 0.f);
+        float d2 = vlen2(vsub(lp, p));
+        for (int i = 0; i < nb; ++i) Li[i] = Ls[i] / d2;
+        return;
+    }
+    /* area: ShapeSet::Sample(p, ls, &ns) (light.cpp:137-151) */
+    const pbrtgpu_light_shape *shs = c->s->light_shapes + L->shape_offset;
+    int sn = sample_discrete(shs, L->n_shapes, u[2]);
+    V ns;
+    V pt = shape_sample_p(c, shs[sn].shape_type, shs[sn].shape_index, p, u[0], u[1], &ns);
+    Ray r; r.o = p; r.d = vsub(pt, p); r.mint = 1e-3f; r.maxt = INFINITY; r.time = 0.f;
+    float rayEps, thit = 1.f;
+    int anyHit = 0;
+    DG dg;
+    for (int i = 0; i < L->n_shapes; ++i) {
+        float th, e;
+        DG d2;
+        if (shape_intersect(c, shs[i].shape_type, shs[i].shape_index, &r, &th, &e, &d2)) { anyHit = 1; thit = th; rayEps = e; dg = d2; }
+    }
+    (void)rayEps;
+    if (anyHit) ns = dg.nn;
+    V ps = rayat(&r, thit);
+    *wi = vnorm(vsub(ps, p));
+    /* ShapeSet::Pdf(p, wi) (light.cpp:159-165) */
+    float pp = 0.f;
+    for (int i = 0; i < L->n_shapes; ++i) pp += shs[i].area * shape_pdf(c, shs[i].shape_type, shs[i].shape_index, p, *wi);
+    *pdf = pp / L->sum_area;
+    /* VisibilityTester::SetSegment(p, pEps, ps, 1e-3f) */
+    float dist = vlen(vsub(p, ps));
+    vis->o = p; vis->d = vdiv(vsub(ps, p), dist); vis->mint = pEps; vis->maxt = dist * (1.f - 1e-3f);
+    /* DiffuseAreaLight::L(ps, ns, -wi) */
+    if (vdot(ns, vneg(*wi)) > 0.f) for (int i = 0; i < nb; ++i) Li[i] = Ls[i];
+    else for (int i = 0; i < nb; ++i) Li[i] = 0.f;
+}
+static float light_pdf(const Ctx *c, const pbrtgpu_light *L, V p, V wi) {
+    if (L->type == PBRTGPU_LIGHT_POINT) return 0.;
+    const pbrtgpu_light_shape *shs = c->s->light_shapes + L->shape_offset;
+    float pp = 0.f;
+    for (int i = 0; i < L->n_shapes; ++i) pp += shs[i].area * shape_pdf(c, shs[i].shape_type, shs[i].shape_index, p, wi);
+    return pp / L->sum_area;
+}
+static inline int light_is_delta(const pbrtgpu_light *L) { return L->type == PBRTGPU_LIGHT_POINT; }
+/* AreaLight::L via Intersection::Le (intersection.cpp:53-57, diffuse.h:43-45) */
+static void isect_Le(const Ctx *c, const Isect *is, V w, float *out) {
+    int al = c->s->prims[is->prim].area_light;
+    if (al < 0) { for (int i = 0; i < c->nb; ++i) out[i] = 0.f; return; }
+    const pbrtgpu_light *L = &c->s->lights[al];
+    const float *Ls = SPEC(c, L->spec);
+    if (vdot(is->dg.nn, w) > 0.f) for (int i = 0; i < c->nb; ++i) out[i] = Ls[i];
+    else for (int i = 0; i < c->nb; ++i) out[i] = 0.f;
+}
+
+/* ------------------------------------------------------------------ integrator */
+typedef struct {
+    uint32_t hp, s, spp;
+    RNG rng;
+} PathSampler;
+/* EstimateDirect (integrator.cpp:109-166) */
+static void estimate_direct(const Ctx *c, int lightNum, V p, V n, V wo, float rayEps, float time, const BSDF *bs,
+                            const float ul[3], const float ub[3], float *Ld) {
+    int nb = c->nb;
+    const pbrtgpu_light *L = &c->s->lights[lightNum];
+    int flags = BSDF_ALL & ~BSDF_SPECULAR;
+    float Li[MAXB], f[MAXB];
+    for (int i = 0; i < nb; ++i) Ld[i] = 0.f;
+    V wi;
+    float lightPdf, bsdfPdf;
+    Seg vis;
+    light_sample_L(c, L, p, rayEps, ul, time, &wi, &lightPdf, &vis, Li);
+    if (lightPdf > 0. && !spec_black(c, Li)) {
+        bsdf_f(c, bs, wo, wi, flags, f);
+        Ray sr; sr.o = vis.o; sr.d = vis.d; sr.mint = vis.mint; sr.maxt = vis.maxt; sr.time = time;
+        if (!spec_black(c, f) && !bvh_intersectP(c, &sr)) {
+            if (light_is_delta(L)) {
+                float s = fabsf(vdot(wi, n)) / lightPdf;
+                for (int i = 0; i < nb; ++i) Ld[i] += (f[i] * Li[i]) * s;
+            } else {
+                bsdfPdf = bsdf_pdf(bs, wo, wi, flags);
+                float weight = power_heuristic(1, lightPdf, 1, bsdfPdf);
+                float s = fabsf(vdot(wi, n)) * weight / lightPdf;
+                for (int i = 0; i < nb; ++i) Ld[i] += (f[i] * Li[i]) * s;
+            }
+        }
+    }
+    if (!light_is_delta(L)) {
+        int sampledType;
+        bsdf_sample_f(c, bs, wo, &wi, ub[0], ub[1], ub[2], &bsdfPdf, flags, &sampledType, f);
+        if (!spec_black(c, f) && bsdfPdf > 0.) {
+            float weight = 1.f;
+            if (!(sampledType & BSDF_SPECULAR)) {
+                lightPdf = light_pdf(c, L, p, wi);
+                if (lightPdf == 0.) return;
+                weight = power_heuristic(1, bsdfPdf, 1, lightPdf);
+            }
+            Ray ray; ray.o = p; ray.d = wi; ray.mint = rayEps; ray.maxt = INFINITY; ray.time = time;
+            Hit h;
+            for (int i = 0; i < nb; ++i) Li[i] = 0.f;
+            if (bvh_intersect(c, &ray, &h)) {
+                if (c->s->prims[h.prim].area_light == lightNum) {
+                    Isect is;
+                    isect_fill(c, &ray, &h, &is);
+                    isect_Le(c, &is, vneg(wi), Li);
+                }
+            }   /* else Li = light->Le(ray) == 0 for area lights */
+            if (!spec_black(c, Li)) {
+                float ad = fabsf(vdot(wi, n));
+                for (int i = 0; i < nb; ++i) Ld[i] += (((f[i] * Li[i]) * ad) * weight) / bsdfPdf;
+            }
+        }
+    }
+}
+/* PathIntegrator::Li (path.cpp:44-115) + SamplerRenderer::Li (samplerrenderer.cpp:225-247) */
+static void radiance(const Ctx *c, Ray ray, PathSampler *ps, float *Lout) {
+    int nb = c->nb;
+    float L[MAXB], beta[MAXB], tmp[MAXB], Ld[MAXB], f[MAXB];
+    for (int i = 0; i < nb; ++i) { L[i] = 0.f; beta[i] = 1.f; }
+    Hit h;
+    Isect is;
+    if (!bvh_intersect(c, &ray, &h)) {
+        /* miss: sum of lights' Le (area/point: 0) */
+        for (int i = 0; i < nb; ++i) Lout[i] = (1.f * 0.f) + 0.f;
+        return;
+    }
+    isect_fill(c, &ray, &h, &is);
+    int specularBounce = 0;
+    int nLights = c->s->n_lights;
+    for (int bounces = 0;; ++bounces) {
+        if (bounces == 0 || specularBounce) {
+            isect_Le(c, &is, vneg(ray.d), tmp);
+            for (int i = 0; i < nb; ++i) L[i] += beta[i] * tmp[i];
+        }
+        BSDF bs;
+        DG dgs;
+        get_bsdf(c, &is, &bs, &dgs);
+        V p = dgs.p, n = dgs.nn;
+        V wo = vneg(ray.d);
+        /* UniformSampleOneLight (integrator.cpp:74-106) */
+        if (nLights > 0) {
+            float ul[3], ub[3], ulnum;
+            if (bounces < 3) {
+                float u2[2];
+                ulnum = s1d(ps->hp, DIM_1D(4 * bounces + 1), ps->s, ps->spp);
+                s2d(ps->hp, DIM_2D(3 * bounces + 0), ps->s, ps->spp, u2); ul[0] = u2[0]; ul[1] = u2[1];
+                ul[2] = s1d(ps->hp, DIM_1D(4 * bounces + 0), ps->s, ps->spp);
+                s2d(ps->hp, DIM_2D(3 * bounces + 1), ps->s, ps->spp, u2); ub[0] = u2[0]; ub[1] = u2[1];
+                ub[2] = s1d(ps->hp, DIM_1D(4 * bounces + 2), ps->s, ps->spp);
+            } else {
+                ulnum = rng_float(&ps->rng);
+                ul[0] = rng_float(&ps->rng); ul[1] = rng_float(&ps->rng); ul[2] = rng_float(&ps->rng);
+                ub[0] = rng_float(&ps->rng); ub[1] = rng_float(&ps->rng); ub[2] = rng_float(&ps->rng);
+            }
+            int lightNum = (int)floorf(ulnum * nLights);
+            if (lightNum > nLights - 1) lightNum = nLights - 1;
+            estimate_direct(c, lightNum, p, n, wo, is.rayEps, ray.time, &bs, ul, ub, Ld);
+            for (int i = 0; i < nb; ++i) L[i] += beta[i] * ((float)nLights * Ld[i]);
+        } else {
+            for (int i = 0; i < nb; ++i) L[i] += beta[i] * 0.f;
+        }
+        /* BSDF sample for the path direction */
+        float up[3];
+        if (bounces < 3) {
+            float u2[2];
+            s2d(ps->hp, DIM_2D(3 * bounces + 2), ps->s, ps->spp, u2); up[0] = u2[0]; up[1] = u2[1];
+            up[2] = s1d(ps->hp, DIM_1D(4 * bounces + 3), ps->s, ps->spp);
+        } else {
+            up[0] = rng_float(&ps->rng); up[1] = rng_float(&ps->rng); up[2] = rng_float(&ps->rng);
+        }
+        V wi;
+        float pdf;
+        int flags;
+        bsdf_sample_f(c, &bs, wo, &wi, up[0], up[1], up[2], &pdf, BSDF_ALL, &flags, f);
+        if (spec_black(c, f) || pdf == 0.) break;
+        specularBounce = (flags & BSDF_SPECULAR) != 0;
+        float ad = fabsf(vdot(wi, n));
+        for (int i = 0; i < nb; ++i) beta[i] *= (f[i] * ad) / pdf;
+        Ray nray; nray.o = p; nray.d = wi; nray.mint = is.rayEps; nray.maxt = INFINITY; nray.time = ray.time;
+        ray = nray;
+        if (bounces > 3) {
+            float cp = fminf_(.5f, spec_y(c, beta));
+            if (rng_float(&ps->rng) > cp) break;
+            for (int i = 0; i < nb; ++i) beta[i] /= cp;
+        }
+        if (bounces == c->s->max_depth) break;
+        if (!bvh_intersect(c, &ray, &h)) {
+            if (specularBounce) for (int i = 0; i < nb; ++i) L[i] += beta[i] * 0.f;   /* area/point Le == 0 */
+            break;
+        }
+        isect_fill(c, &ray, &h, &is);
+        /* pathThroughput *= Transmittance (== 1) */
+        for (int i = 0; i < nb; ++i) beta[i] *= 1.f;
+    }
+    for (int i = 0; i < nb; ++i) Lout[i] = (1.f * L[i]) + 0.f;   /* T * Li + Lvi */
+}
+
+/* camera sample -> world ray (perspective.cpp:73-106, transform.h:253-262) */
+static Ray camera_ray(const Ctx *c, float imageX, float imageY, float lensU, float lensV, float timeU) {
+    const pbrtgpu_camera *cam = &c->s->camera;
+    const float *m = cam->raster_to_camera;
+    float x = imageX, y = imageY, z = 0;
+    V Pc;
+    Pc.x = m[0] * x + m[1] * y + m[2] * z + m[3];
+    Pc.y = m[4] * x + m[5] * y + m[6] * z + m[7];
+    Pc.z = m[8] * x + m[9] * y + m[10] * z + m[11];
+    float w = m[12] * x + m[13] * y + m[14] * z + m[15];
+    if (w != 1.) Pc = vdiv(Pc, w);
+    Ray r;
+    r.o = v3(0, 0, 0);
+    r.d = vnorm(v3(Pc.x, Pc.y, Pc.z));
+    r.mint = 0.f; r.maxt = INFINITY;
+    if (cam->lens_radius > 0.) {
+        float lu, lv;
+        concentric_disk(lensU, lensV, &lu, &lv);
+        lu *= cam->lens_radius; lv *= cam->lens_radius;
+        float ft = cam->focal_distance / r.d.z;
+        V Pfocus = rayat(&r, ft);
+        r.o = v3(lu, lv, 0.f);
+        r.d = vnorm(vsub(Pfocus, r.o));
+    }
+    r.time = lerpf(timeU, cam->shutter_open, cam->shutter_close);
+    const float *cw = cam->cam2world_m;
+    Ray o = r;
+    {
+        V p = r.o;
+        float xp = cw[0] * p.x + cw[1] * p.y + cw[2] * p.z + cw[3];
+        float yp = cw[4] * p.x + cw[5] * p.y + cw[6] * p.z + cw[7];
+        float zp = cw[8] * p.x + cw[9] * p.y + cw[10] * p.z + cw[11];
+        float wp = cw[12] * p.x + cw[13] * p.y + cw[14] * p.z + cw[15];
+        o.o = v3(xp, yp, zp);
+        if (wp != 1.) o.o = vdiv(o.o, wp);
+    }
+    o.d = xvec(cw, r.d);
+    return o;
+}
+
+/* One camera path: sample -> ray -> radiance -> guard (samplerrenderer.cpp:86-133) */
+static int trace_path(const Ctx *c, int px, int py, uint32_t s, float *L, float *imgX, float *imgY) {
+    uint32_t spp = (uint32_t)c->s->spp;
+    PathSampler ps;
+    ps.hp = pixel_hash(c->s->seed, px, py);
+    ps.s = s;
+    ps.spp = spp;
+    float u[2], lens[2];
+    s2d(ps.hp, 0, s, spp, u);
+    float imageX = px + u[0], imageY = py + u[1];
+    s2d(ps.hp, 1, s, spp, lens);
+    float timeU = s1d(ps.hp, 2, s, spp);
+    rng_seed(&ps.rng, path_seed(ps.hp, s));
+    ps.rng.mti = 624;   /* RNG ctor: Seed() leaves mti == N, first draw regenerates */
+    Ray r = camera_ray(c, imageX, imageY, lens[0], lens[1], timeU);
+    float Lr[MAXB];
+    radiance(c, r, &ps, Lr);
+    int nb = c->nb, bad = 0;
+    for (int i = 0; i < nb; ++i) L[i] = 1.f * Lr[i];   /* rayWeight * Li */
+    int nan = 0;
+    for (int i = 0; i < nb; ++i) if (isnan(L[i])) nan = 1;
+    if (nan) bad = 1;
+    else {
+        float yv = spec_y(c, L);
+        if (yv < -1e-5) bad = 1;
+        else if (isinf(yv)) bad = 1;
+    }
+    if (bad) for (int i = 0; i < nb; ++i) L[i] = 0.f;
+    if (imgX) *imgX = imageX;
+    if (imgY) *imgY = imageY;
+    return bad;
+}
+
+/* ------------------------------------------------------------------ exported API */
+int oracle_abi_version(void) { return PBRTGPU_ABI_VERSION; }
+int oracle_libm_float(void) {
+#ifdef ORACLE_LIBM_FLOAT
+    return 1;
+#else
+    return 0;
+#endif
+}
+
+/* per-path radiance for keys [n][3] = (x, y, s) */
+int oracle_trace_paths(const pbrtgpu_flat_scene *s, const int32_t *keys, int32_t n, float *out) {
+    Ctx c = {s, s->n_bands};
+    for (int k = 0; k < n; ++k) trace_path(&c, keys[3 * k], keys[3 * k + 1], (uint32_t)keys[3 * k + 2], out + (size_t)k * s->n_bands, NULL, NULL);
+    return 0;
+}
+
+/* closest / any hit queries: rays [n][8] (o, d, mint, maxt); hits [n][4] (t, b1, b2, prim) */
+int oracle_intersect(const pbrtgpu_flat_scene *s, const float *rays, int32_t n, float *hits, int32_t *occluded) {
+    Ctx c = {s, s->n_bands};
+    for (int k = 0; k < n; ++k) {
+        const float *q = rays + 8 * k;
+        Ray r; r.o = v3(q[0], q[1], q[2]); r.d = v3(q[3], q[4], q[5]); r.mint = q[6]; r.maxt = q[7]; r.time = 0.f;
+        Ray r2 = r;
+        Hit h;
+        if (bvh_intersect(&c, &r, &h)) { hits[4 * k] = h.t; hits[4 * k + 1] = 0.f; hits[4 * k + 2] = 0.f; int32_t p = h.prim; memcpy(&hits[4 * k + 3], &p, 4); }
+        else { hits[4 * k] = INFINITY; hits[4 * k + 1] = 0.f; hits[4 * k + 2] = 0.f; int32_t p = -1; memcpy(&hits[4 * k + 3], &p, 4); }
+        if (occluded) occluded[k] = bvh_intersectP(&c, &r2);
+    }
+    return 0;
+}
+
+/* Film render over a window of sample pixels [x0,x1)x[y0,y1) (clamped to the sample
+ * extent), all samples [0,spp).  film: [py_count][px_count][nb] float32.
+ * The reference harness adds samples in sample-pixel row-major order, samples ascending
+ * (SamplerRendererTask::Run + SpectralImageFilm::AddSample).  A sample whose imageX or
+ * imageY rounds to an integer also lands on a neighbouring pixel ("spill"); for a film
+ * pixel T the contribution order is therefore: spills from earlier sample pixels, T's own
+ * samples, spills from later sample pixels.  Spill samples are found from
+ * the sampler alone (no tracing) and traced first. */
+typedef struct {
+    const Ctx *c;
+    int x0, x1, y0, y1, spp;
+    float *film;
+    int nextRow;
+    pthread_mutex_t mu;
+    long zeroed;
+    int phase;                 /* 0: spill scan, 1: trace spills, 2: own accumulation */
+    int32_t *spillKeys;        /* [n][3] x, y, s */
+    long nSpill, capSpill, nextSpill;
+    float *spillL;             /* [n][nb] */
+} Job;
+
+static inline void footprint(const pbrtgpu_camera *cam, float ix, float iy, int *fx0, int *fx1, int *fy0, int *fy1) {
+    float dx = ix - 0.5f, dy = iy - 0.5f;   /* spectralImage.cpp:80-91, box filter width .5 */
+    *fx0 = (int)ceilf(dx - 0.5f); *fx1 = (int)floorf(dx + 0.5f);
+    *fy0 = (int)ceilf(dy - 0.5f); *fy1 = (int)floorf(dy + 0.5f);
+    if (*fx0 < cam->px_start) *fx0 = cam->px_start;
+    if (*fx1 > cam->px_start + cam->px_count - 1) *fx1 = cam->px_start + cam->px_count - 1;
+    if (*fy0 < cam->py_start) *fy0 = cam->py_start;
+    if (*fy1 > cam->py_start + cam->py_count - 1) *fy1 = cam->py_start + cam->py_count - 1;
+}
+static inline void image_xy(const Ctx *c, int x, int y, uint32_t s, float *ix, float *iy) {
+    uint32_t hp = pixel_hash(c->s->seed, x, y);
+    float u[2];
+    s2d(hp, 0, s, (uint32_t)c->s->spp, u);
+    *ix = x + u[0];
+    *iy = y + u[1];
+}
+static void *worker(void *arg) {
+    Job *j = (Job *)arg;
+    const Ctx *c = j->c;
+    const pbrtgpu_camera *cam = &c->s->camera;
+    int nb = c->nb;
+    float L[MAXB];
+    if (j->phase == 1) {
+        for (;;) {
+            pthread_mutex_lock(&j->mu);
+            long k = j->nextSpill++;
+            pthread_mutex_unlock(&j->mu);
+            if (k >= j->nSpill) break;
+            const int32_t *key = j->spillKeys + 3 * k;
+            trace_path(c, key[0], key[1], (uint32_t)key[2], j->spillL + (size_t)k * nb, NULL, NULL);
+        }
+        return NULL;
+    }
+    for (;;) {
+        pthread_mutex_lock(&j->mu);
+        int y = j->nextRow++;
+        pthread_mutex_unlock(&j->mu);
+        if (y >= j->y1) break;
+        for (int x = j->x0; x < j->x1; ++x) {
+            int own = x >= cam->px_start && x < cam->px_start + cam->px_count && y >= cam->py_start &&
+                      y < cam->py_start + cam->py_count;
+            for (int s = 0; s < j->spp; ++s) {
+                float ix, iy;
+                int fx0, fx1, fy0, fy1;
+                if (j->phase == 0) {
+                    image_xy(c, x, y, (uint32_t)s, &ix, &iy);
+                    footprint(cam, ix, iy, &fx0, &fx1, &fy0, &fy1);
+                    if (fx1 - fx0 < 0 || fy1 - fy0 < 0) continue;
+                    if (fx0 == x && fx1 == x && fy0 == y && fy1 == y) continue;
+                    pthread_mutex_lock(&j->mu);
+                    if (j->nSpill == j->capSpill) {
+                        j->capSpill = j->capSpill ? 2 * j->capSpill : 256;
+                        j->spillKeys = (int32_t *)realloc(j->spillKeys, sizeof(int32_t) * 3 * j->capSpill);
+                    }
+                    int32_t *k = j->spillKeys + 3 * j->nSpill++;
+                    k[0] = x; k[1] = y; k[2] = s;
+                    pthread_mutex_unlock(&j->mu);
+                    continue;
+                }
+                if (!own) continue;
+                memset(L, 0, sizeof(L));
+                int bad = trace_path(c, x, y, (uint32_t)s, L, &ix, &iy);
+                if (bad) { pthread_mutex_lock(&j->mu); j->zeroed++; pthread_mutex_unlock(&j->mu); }
+                float *pix = j->film + ((size_t)(y - cam->py_start) * cam->px_count + (x - cam->px_start)) * nb;
+                for (int i = 0; i < nb; ++i) pix[i] += 1.f * L[i];
+            }
+        }
+    }
+    return NULL;
+}
+typedef struct { int32_t target, src, s, idx; } Contrib;
+static int cmp_contrib(const void *a, const void *b) {
+    const Contrib *x = (const Contrib *)a, *y = (const Contrib *)b;
+    if (x->target != y->target) return x->target < y->target ? -1 : 1;
+    if (x->src != y->src) return x->src < y->src ? -1 : 1;
+    return x->s < y->s ? -1 : (x->s > y->s);
+}
+static void run_phase(Job *j, int phase, int nthreads) {
+    j->phase = phase;
+    j->nextRow = j->y0;
+    j->nextSpill = 0;
+    pthread_t *th = (pthread_t *)malloc(sizeof(pthread_t) * nthreads);
+    for (int t = 0; t < nthreads; ++t) pthread_create(&th[t], NULL, worker, j);
+    for (int t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
+    free(th);
+}
+int oracle_render(const pbrtgpu_flat_scene *s, int x0, int x1, int y0, int y1, float *film, int nthreads,
+                  double *stats) {
+    Ctx c = {s, s->n_bands};
+    const pbrtgpu_camera *cam = &s->camera;
+    int nb = s->n_bands;
+    Job j;
+    memset(&j, 0, sizeof(j));
+    j.c = &c;
+    j.x0 = x0 < cam->sx_start ? cam->sx_start : x0; j.x1 = x1 > cam->sx_end ? cam->sx_end : x1;
+    j.y0 = y0 < cam->sy_start ? cam->sy_start : y0; j.y1 = y1 > cam->sy_end ? cam->sy_end : y1;
+    j.spp = s->spp;
+    j.film = film;
+    pthread_mutex_init(&j.mu, NULL);
+    if (nthreads < 1) nthreads = 1;
+    run_phase(&j, 0, nthreads);            /* find spill samples */
+    j.spillL = (float *)malloc(sizeof(float) * nb * (j.nSpill + 1));
+    run_phase(&j, 1, nthreads);            /* trace them */
+    /* contributions of spill samples to pixels other than their own */
+    long nc = 0, cap = 4 * j.nSpill + 1;
+    Contrib *cs = (Contrib *)malloc(sizeof(Contrib) * cap);
+    int ew = cam->sx_end - cam->sx_start;
+    for (long k = 0; k < j.nSpill; ++k) {
+        const int32_t *key = j.spillKeys + 3 * k;
+        float ix, iy;
+        int fx0, fx1, fy0, fy1;
+        image_xy(&c, key[0], key[1], (uint32_t)key[2], &ix, &iy);
+        footprint(cam, ix, iy, &fx0, &fx1, &fy0, &fy1);
+        for (int fy = fy0; fy <= fy1; ++fy)
+            for (int fx = fx0; fx <= fx1; ++fx) {
+                if (fx == key[0] && fy == key[1]) continue;
+                Contrib *q = &cs[nc++];
+                q->target = (fy - cam->py_start) * cam->px_count + (fx - cam->px_start);
+                q->src = (key[1] - cam->sy_start) * ew + (key[0] - cam->sx_start);
+                q->s = key[2];
+                q->idx = (int32_t)k;
+            }
+    }
+    qsort(cs, nc, sizeof(Contrib), cmp_contrib);
+    /* pre-spills: sources earlier (row-major) than the target's own sample pixel */
+    for (long k = 0; k < nc; ++k) {
+        int tx = cs[k].target % cam->px_count + cam->px_start, ty = cs[k].target / cam->px_count + cam->py_start;
+        int ownIdx = (ty - cam->sy_start) * ew + (tx - cam->sx_start);
+        if (cs[k].src < ownIdx) {
+            float *pix = film + (size_t)cs[k].target * nb;
+            const float *L = j.spillL + (size_t)cs[k].idx * nb;
+            for (int i = 0; i < nb; ++i) pix[i] += 1.f * L[i];
+        }
+    }
+    run_phase(&j, 2, nthreads);            /* own samples, in order */
+    for (long k = 0; k < nc; ++k) {         /* post-spills */
+        int tx = cs[k].target % cam->px_count + cam->px_start, ty = cs[k].target / cam->px_count + cam->py_start;
+        int ownIdx = (ty - cam->sy_start) * ew + (tx - cam->sx_start);
+        if (cs[k].src > ownIdx) {
+            float *pix = film + (size_t)cs[k].target * nb;
+            const float *L = j.spillL + (size_t)cs[k].idx * nb;
+            for (int i = 0; i < nb; ++i) pix[i] += 1.f * L[i];
+        }
+    }
+    if (stats) {
+        stats[0] = (double)(j.x1 - j.x0) * (j.y1 - j.y0) * j.spp;
+        stats[1] = (double)j.zeroed;
+        stats[2] = (double)j.nSpill;
+    }
+    free(cs);
+    free(j.spillKeys);
+    free(j.spillL);
+    pthread_mutex_destroy(&j.mu);
+    return 0;
+}
+
+/* Throughput helper for the CPU baseline: trace a bounded list of paths over the
+ * sample extent (every path traced fully, no film), returns paths traced. */
+typedef struct { const Ctx *c; long n0, n1; long next; pthread_mutex_t mu; int W, H; } TJob;
+static void *tworker(void *arg) {
+    TJob *t = (TJob *)arg;
+    float L[MAXB];
+    for (;;) {
+        pthread_mutex_lock(&t->mu);
+        long k = t->next; t->next += 64;
+        pthread_mutex_unlock(&t->mu);
+        if (k >= t->n1) break;
+        long e = k + 64 < t->n1 ? k + 64 : t->n1;
+        for (long q = k; q < e; ++q) {
+            long pix = q / t->c->s->spp;
+            int s = (int)(q % t->c->s->spp);
+            int x = t->c->s->camera.px_start + (int)(pix % t->W), y = t->c->s->camera.py_start + (int)((pix / t->W) % t->H);
+            trace_path(t->c, x, y, (uint32_t)s, L, NULL, NULL);
+        }
+    }
+    return NULL;
+}
+long oracle_trace_range(const pbrtgpu_flat_scene *s, long first, long count, int nthreads) {
+    Ctx c = {s, s->n_bands};
+    TJob t;
+    t.c = &c; t.n0 = first; t.n1 = first + count; t.next = first; t.W = s->camera.px_count; t.H = s->camera.py_count;
+    pthread_mutex_init(&t.mu, NULL);
+    if (nthreads < 1) nthreads = 1;
+    pthread_t *th = (pthread_t *)malloc(sizeof(pthread_t) * nthreads);
+    for (int i = 0; i < nthreads; ++i) pthread_create(&th[i], NULL, tworker, &t);
+    for (int i = 0; i < nthreads; ++i) pthread_join(th[i], NULL);
+    free(th);
+    pthread_mutex_destroy(&t.mu);
+    return count;
+}

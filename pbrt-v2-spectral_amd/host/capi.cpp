@@ -1,0 +1,109 @@
+// capi.cpp -- C ABI of the host library (libpbrthost.so): scene loading (pbrt files or
+// scene packs), flattening, and the reference's multispectral .dat writer.
+// Declarations: include/pbrthost.h.
+#include "pbrthost.h"
+#include "scene.h"
+#include <cstring>
+#include <cstdio>
+#include <vector>
+#include <algorithm>
+
+using namespace pbrtamd;
+
+static void SetErr(char *err, int errlen, const std::string &msg) {
+    if (err && errlen > 0) { strncpy(err, msg.c_str(), errlen - 1); err[errlen - 1] = 0; }
+}
+
+extern "C" {
+
+int pbrthost_load(const char *path, const pbrthost_overrides *ov, pbrthost_scene **out, char *err, int errlen) {
+    if (!path || !out) { SetErr(err, errlen, "null argument"); return -1; }
+    HostScene *s = new HostScene();
+    std::string e, p(path);
+    bool ok;
+    if (p.size() > 5 && p.substr(p.size() - 5) == ".pack") ok = LoadPack(p, s, &e);
+    else {
+        RenderOverrides o;
+        if (ov) {
+            o.xres = ov->xres; o.yres = ov->yres; o.spp = ov->spp; o.maxdepth = ov->maxdepth;
+            o.bands = ov->bands > 0 ? ov->bands : 32; o.seed = ov->seed;
+        }
+        ok = LoadPbrtScene(p, o, s, &e);
+    }
+    if (!ok) { delete s; SetErr(err, errlen, e); return -1; }
+    // pack overrides that do not change geometry
+    if (ov && p.size() > 5 && p.substr(p.size() - 5) == ".pack") {
+        if (ov->spp > 0) { uint32_t v = ov->spp; v--; v |= v >> 1; v |= v >> 2; v |= v >> 4; v |= v >> 8; v |= v >> 16; s->spp = v + 1; }
+        if (ov->maxdepth >= 0) s->maxDepth = ov->maxdepth;
+        s->seed = ov->seed;
+    }
+    *out = reinterpret_cast<pbrthost_scene *>(s);
+    return 0;
+}
+
+int pbrthost_free(pbrthost_scene *h) { delete reinterpret_cast<HostScene *>(h); return 0; }
+
+int pbrthost_flat(pbrthost_scene *h, pbrtgpu_flat_scene *out) {
+    if (!h || !out) return -1;
+    reinterpret_cast<HostScene *>(h)->Flat(out);
+    return 0;
+}
+
+int pbrthost_save_pack(pbrthost_scene *h, const char *path, char *err, int errlen) {
+    std::string e;
+    if (!SavePack(*reinterpret_cast<HostScene *>(h), path, &e)) { SetErr(err, errlen, e); return -1; }
+    return 0;
+}
+
+int pbrthost_set_render(pbrthost_scene *h, int spp, int maxdepth, uint32_t seed) {
+    HostScene *s = reinterpret_cast<HostScene *>(h);
+    if (spp > 0) { uint32_t v = spp; v--; v |= v >> 1; v |= v >> 2; v |= v >> 4; v |= v >> 8; v |= v >> 16; s->spp = v + 1; }
+    if (maxdepth >= 0) s->maxDepth = maxdepth;
+    s->seed = seed;
+    return 0;
+}
+
+int pbrthost_info(pbrthost_scene *h, int64_t *info, int n) {
+    HostScene *s = reinterpret_cast<HostScene *>(h);
+    int64_t v[16] = {s->nBands, s->spp, s->maxDepth, (int64_t)s->nodes.size(), (int64_t)s->prims.size(),
+                     (int64_t)s->tris.size(), (int64_t)s->meshes.size(), (int64_t)(s->vertP.size() / 3),
+                     (int64_t)s->quadrics.size(), (int64_t)s->materials.size(), (int64_t)s->lights.size(),
+                     s->bvhMaxDepth, s->camera.px_count, s->camera.py_count, (int64_t)s->warnings.size(), 0};
+    for (int i = 0; i < n && i < 16; ++i) info[i] = v[i];
+    return 0;
+}
+
+// SpectralImageFilm::WriteImage (spectralImage.cpp:267-378), identity conversion matrix.
+// film: [H][W][N] float32 raw sums; weight: [H][W] (filter weight sums, may be NULL = all 1).
+int pbrthost_write_dat(const char *path, const float *film, const float *weight, int W, int H, int N) {
+    int nPix = W * H;
+    std::vector<float> finalC((size_t)N * nPix);
+    int offset = 0;
+    for (int x = 0; x < W; ++x)
+        for (int y = 0; y < H; ++y) {
+            for (int i = 0; i < N; ++i) finalC[(size_t)(y * W + x) * N + i] = film[((size_t)y * W + x) * N + i];
+            float ws = weight ? weight[(size_t)y * W + x] : 1.f;
+            if (ws != 0.f)
+                for (int i = 0; i < N; ++i) finalC[(size_t)N * offset + i] = std::max(0.f, finalC[(size_t)N * offset + i]);
+            for (int i = 0; i < N; ++i) finalC[(size_t)N * offset + i] += 1.f * 0.f;   // splatC[N] (pad) == 0
+            ++offset;
+        }
+    std::vector<float> outv((size_t)N * nPix);
+    for (int y = 0; y < H; ++y)
+        for (int x = 0; x < W; ++x)
+            for (int row = 0; row < N; ++row) {
+                float t = 0;
+                for (int it = 0; it < N; ++it) t += (row == it ? 1.f : 0.f) * finalC[(size_t)N * (y * W + x) + it];
+                outv[(size_t)N * (x * H + y) + row] = t;
+            }
+    FILE *f = fopen(path, "w");
+    if (!f) return -1;
+    fprintf(f, "%d %d %d\n", W, H, N);
+    fprintf(f, "0 0 0\n");   // focalLength fStop fov (0 for a perspective camera)
+    for (int i = 0; i < N; ++i)
+        for (int j = 0; j < nPix; ++j) { double r = outv[(size_t)N * j + i]; fwrite(&r, 8, 1, f); }
+    fclose(f);
+    return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,1263 @@
+// frontend.cpp -- pbrt-v2 scene-file front end for the MI355X path tracer.
+//
+// Reads the unchanged pbrt scene format and builds the flattened device scene with the
+// reference's semantics:
+//   * tokenizer / directive grammar        core/pbrtlex.ll, core/pbrtparse.yy (numbers via
+//                                          (float)atof, integers via int(float))
+//   * parameter lists / typed lookups      core/paramset.cpp (color -> FromRGB reflectance)
+//   * graphics state, transform stack,     core/api.cpp:146-330, 733-1330
+//     transform cache, shapes, area lights
+//   * shapes                               shapes/trianglemesh.cpp, shapes/loopsubdiv.cpp,
+//                                          shapes/sphere.cpp, shapes/disk.cpp
+//   * primitive refinement order           core/primitive.cpp:40-53 (LIFO todo list)
+//   * BVH build (SAH, 12 buckets, 4 prims) accelerators/bvh.cpp:145-372
+//   * camera / film extent                 cameras/perspective.cpp, core/camera.cpp:84-103,
+//                                          film/spectralImage.cpp:40-50,176-185
+// Float expressions keep the reference's operand order (compile with -ffp-contract=off).
+#include "scene.h"
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <cctype>
+#include <fstream>
+#include <sstream>
+#include <set>
+#include <memory>
+#include <stdexcept>
+#include <algorithm>
+#include <functional>
+
+namespace pbrtamd {
+
+// ------------------------------------------------------------------------------------
+// Parameter sets
+// ------------------------------------------------------------------------------------
+enum PCat { P_INT, P_BOOL, P_FLOAT, P_POINT, P_VECTOR, P_NORMAL, P_SPECTRUM, P_STRING, P_TEXTURE, P_NCAT };
+struct Param {
+    PCat cat;
+    std::string name;
+    std::vector<float> f;             // float/point/vector/normal
+    std::vector<int> i;               // int
+    std::vector<bool> b;
+    std::vector<std::string> s;       // string / texture
+    std::vector<Spec> spec;
+};
+struct ParamSet {
+    std::vector<Param> items;
+    void Add(const Param &p) {
+        for (size_t k = 0; k < items.size(); ++k)
+            if (items[k].cat == p.cat && items[k].name == p.name) { items.erase(items.begin() + k); break; }
+        items.push_back(p);
+    }
+    const Param *Find(PCat c, const std::string &n) const {
+        for (const Param &p : items) if (p.cat == c && p.name == n) return &p;
+        return nullptr;
+    }
+    float FindOneFloat(const std::string &n, float d) const { const Param *p = Find(P_FLOAT, n); return (p && p->f.size()) ? p->f[0] : d; }
+    int FindOneInt(const std::string &n, int d) const { const Param *p = Find(P_INT, n); return (p && p->i.size()) ? p->i[0] : d; }
+    bool FindOneBool(const std::string &n, bool d) const { const Param *p = Find(P_BOOL, n); return (p && p->b.size()) ? p->b[0] : d; }
+    std::string FindOneString(const std::string &n, const std::string &d) const { const Param *p = Find(P_STRING, n); return (p && p->s.size()) ? p->s[0] : d; }
+    std::string FindTexture(const std::string &n) const { const Param *p = Find(P_TEXTURE, n); return (p && p->s.size()) ? p->s[0] : ""; }
+    Spec FindOneSpectrum(const std::string &n, const Spec &d) const { const Param *p = Find(P_SPECTRUM, n); return (p && p->spec.size()) ? p->spec[0] : d; }
+    V3 FindOnePoint(const std::string &n, const V3 &d) const { const Param *p = Find(P_POINT, n); return (p && p->f.size() >= 3) ? V3(p->f[0], p->f[1], p->f[2]) : d; }
+};
+
+// texture values known at scene-build time (constant textures; 1x1 fallback images)
+struct FloatTex { bool constant = true; float value = 0.f; };
+struct SpecTex { bool constant = true; Spec value; };
+
+// ------------------------------------------------------------------------------------
+// Tokenizer (pbrtlex.ll)
+// ------------------------------------------------------------------------------------
+struct Token {
+    enum Kind { END, IDENT, STRING, NUMBER, LBRACK, RBRACK } kind = END;
+    std::string text;
+    float num = 0.f;
+};
+class Lexer {
+public:
+    bool Open(const std::string &path) {
+        std::ifstream in(path);
+        if (!in) return false;
+        std::stringstream ss; ss << in.rdbuf();
+        stack.push_back({ss.str(), 0, path});
+        return true;
+    }
+    bool Next(Token *t) {
+        while (!stack.empty()) {
+            Src &s = stack.back();
+            const std::string &b = s.buf;
+            size_t &p = s.pos;
+            while (p < b.size()) {
+                char c = b[p];
+                if (isspace((unsigned char)c)) { ++p; continue; }
+                if (c == '#') { while (p < b.size() && b[p] != '\n') ++p; continue; }
+                if (c == '[') { ++p; t->kind = Token::LBRACK; return true; }
+                if (c == ']') { ++p; t->kind = Token::RBRACK; return true; }
+                if (c == '"') {
+                    ++p;
+                    std::string str;
+                    while (p < b.size() && b[p] != '"') {
+                        if (b[p] == '\\' && p + 1 < b.size()) {
+                            ++p;
+                            char e = b[p];
+                            switch (e) {
+                                case 'n': str += '\n'; break; case 't': str += '\t'; break;
+                                case 'b': str += '\b'; break; case 'f': str += '\f'; break;
+                                case 'r': str += '\r'; break; case '\n': break;
+                                default: str += e;
+                            }
+                            ++p;
+                            continue;
+                        }
+                        str += b[p++];
+                    }
+                    ++p;
+                    t->kind = Token::STRING; t->text = str; return true;
+                }
+                if (isdigit((unsigned char)c) || c == '-' || c == '+' || c == '.') {
+                    size_t q = p;
+                    if (b[q] == '-' || b[q] == '+') ++q;
+                    while (q < b.size() && (isdigit((unsigned char)b[q]) || b[q] == '.')) ++q;
+                    if (q < b.size() && (b[q] == 'e' || b[q] == 'E')) {
+                        size_t r = q + 1;
+                        if (r < b.size() && (b[r] == '-' || b[r] == '+')) ++r;
+                        if (r < b.size() && isdigit((unsigned char)b[r])) { q = r; while (q < b.size() && isdigit((unsigned char)b[q])) ++q; }
+                    }
+                    t->kind = Token::NUMBER; t->text = b.substr(p, q - p);
+                    t->num = (float)atof(t->text.c_str());   // pbrtlex.ll:150
+                    p = q;
+                    return true;
+                }
+                if (isalpha((unsigned char)c) || c == '_') {
+                    size_t q = p;
+                    while (q < b.size() && (isalnum((unsigned char)b[q]) || b[q] == '_')) ++q;
+                    t->kind = Token::IDENT; t->text = b.substr(p, q - p);
+                    p = q;
+                    return true;
+                }
+                throw std::runtime_error(std::string("illegal character in ") + s.path);
+            }
+            stack.pop_back();   // end of an included file
+        }
+        t->kind = Token::END;
+        return false;
+    }
+    bool Include(const std::string &path) { return Open(path); }
+private:
+    struct Src { std::string buf; size_t pos; std::string path; };
+    std::vector<Src> stack;
+};
+
+// ------------------------------------------------------------------------------------
+// Scene builder state (api.cpp)
+// ------------------------------------------------------------------------------------
+struct ShapeObj;   // a (possibly refinable) shape
+struct TriMesh {
+    Xform o2w;            // ObjectToWorld (cached transform value)
+    bool ro = false, swaps = false;
+    int ntris = 0, nverts = 0;
+    std::vector<int> vi;
+    std::vector<V3> p;    // world space (trianglemesh.cpp:61-62)
+    std::vector<V3> n;    // object space normals
+    std::vector<float> uv;
+    int flatIndex = -1;   // index into HostScene::meshes once emitted
+};
+struct Quadric {
+    pbrtgpu_quadric q{};
+    Xform o2w;
+    BBox ObjectBound() const {
+        if (q.type == PBRTGPU_SHAPE_SPHERE)
+            return BBox(V3(-q.radius, -q.radius, q.zmin), V3(q.radius, q.radius, q.zmax));
+        return BBox(V3(-q.radius, -q.radius, q.height), V3(q.radius, q.radius, q.height));
+    }
+    float Area() const {
+        if (q.type == PBRTGPU_SHAPE_SPHERE) return q.phi_max * q.radius * (q.zmax - q.zmin);
+        return q.phi_max * 0.5f * (q.radius * q.radius - q.inner_radius * q.inner_radius);
+    }
+    int flatIndex = -1;
+};
+struct LoopSubdivShape;
+// an intersectable shape after refinement
+struct Isect {
+    int kind;             // PBRTGPU_SHAPE_*
+    TriMesh *mesh = nullptr;
+    int tri = -1;
+    Quadric *quad = nullptr;
+    BBox WorldBound() const {
+        if (kind == PBRTGPU_SHAPE_TRIANGLE) {
+            const V3 &p1 = mesh->p[mesh->vi[3 * tri]], &p2 = mesh->p[mesh->vi[3 * tri + 1]], &p3 = mesh->p[mesh->vi[3 * tri + 2]];
+            return Union(BBox(p1, p2), p3);
+        }
+        return quad->o2w(quad->ObjectBound());
+    }
+    float Area() const {
+        if (kind == PBRTGPU_SHAPE_TRIANGLE) {
+            const V3 &p1 = mesh->p[mesh->vi[3 * tri]], &p2 = mesh->p[mesh->vi[3 * tri + 1]], &p3 = mesh->p[mesh->vi[3 * tri + 2]];
+            return 0.5f * Length(Cross(p2 - p1, p3 - p1));
+        }
+        return quad->Area();
+    }
+};
+
+struct MaterialObj { pbrtgpu_material m{}; std::vector<Spec> spectra; int flatIndex = -1; };
+struct LightObj {
+    pbrtgpu_light l{};
+    Spec L;
+    std::vector<Isect> shapeSet;      // area light ShapeSet (light.cpp:114-135)
+};
+struct PrimObj {
+    std::shared_ptr<ShapeObj> shape;
+    std::shared_ptr<MaterialObj> mtl;
+    int areaLight = -1;
+};
+
+struct SDVertex { V3 P; int startFace = -1; int child = -1; bool regular = false, boundary = false; };
+struct SDFace { int v[3] = {-1, -1, -1}; int f[3] = {-1, -1, -1}; int children[4] = {-1, -1, -1, -1}; };
+
+struct ShapeObj {
+    enum { MESH, QUADRIC, LOOP } kind;
+    std::shared_ptr<TriMesh> mesh;
+    std::shared_ptr<Quadric> quad;
+    // loop subdivision control mesh
+    Xform o2w;
+    bool ro = false;
+    int nLevels = 0;
+    std::vector<SDVertex> verts;
+    std::vector<SDFace> faces;
+    std::shared_ptr<TriMesh> refined;   // cached LoopSubdiv::Refine result
+};
+
+#define NEXT(i) (((i) + 1) % 3)
+#define PREV(i) (((i) + 2) % 3)
+
+// ---------------------- Loop subdivision (loopsubdiv.cpp) ---------------------------
+struct LoopMesh {
+    std::vector<SDVertex> &V;
+    std::vector<SDFace> &F;
+    int vnum(int f, int v) const {
+        for (int i = 0; i < 3; ++i) if (F[f].v[i] == v) return i;
+        throw std::runtime_error("loopsubdiv: vnum logic error");
+    }
+    int nextFace(int f, int v) const { return F[f].f[vnum(f, v)]; }
+    int prevFace(int f, int v) const { return F[f].f[PREV(vnum(f, v))]; }
+    int nextVert(int f, int v) const { return F[f].v[NEXT(vnum(f, v))]; }
+    int prevVert(int f, int v) const { return F[f].v[PREV(vnum(f, v))]; }
+    int otherVert(int f, int v0, int v1) const {
+        for (int i = 0; i < 3; ++i) if (F[f].v[i] != v0 && F[f].v[i] != v1) return F[f].v[i];
+        throw std::runtime_error("loopsubdiv: otherVert logic error");
+    }
+    int valence(int v) const {   // loopsubdiv.cpp:121-143
+        int f = V[v].startFace;
+        if (!V[v].boundary) {
+            int nf = 1;
+            while ((f = nextFace(f, v)) != V[v].startFace) ++nf;
+            return nf;
+        }
+        int nf = 1;
+        while ((f = nextFace(f, v)) != -1) ++nf;
+        f = V[v].startFace;
+        while ((f = prevFace(f, v)) != -1) ++nf;
+        return nf + 1;
+    }
+    void oneRing(int v, std::vector<V3> &P) const {   // loopsubdiv.cpp:451-470
+        P.clear();
+        if (!V[v].boundary) {
+            int face = V[v].startFace;
+            do { P.push_back(V[nextVert(face, v)].P); face = nextFace(face, v); } while (face != V[v].startFace);
+        } else {
+            int face = V[v].startFace, f2;
+            while ((f2 = nextFace(face, v)) != -1) face = f2;
+            P.push_back(V[nextVert(face, v)].P);
+            do { P.push_back(V[prevVert(face, v)].P); face = prevFace(face, v); } while (face != -1);
+        }
+    }
+    V3 weightOneRing(int v, float beta) const {   // loopsubdiv.cpp:440-449
+        int valence_ = valence(v);
+        std::vector<V3> Pring;
+        oneRing(v, Pring);
+        V3 P = (1 - valence_ * beta) * V[v].P;
+        for (int i = 0; i < valence_; ++i) P += beta * Pring[i];
+        return P;
+    }
+    V3 weightBoundary(int v, float beta) const {   // loopsubdiv.cpp:473-482
+        int valence_ = valence(v);
+        std::vector<V3> Pring;
+        oneRing(v, Pring);
+        V3 P = (1 - 2 * beta) * V[v].P;
+        P += beta * Pring[0];
+        P += beta * Pring[valence_ - 1];
+        return P;
+    }
+};
+static float LoopBeta(int valence) { return valence == 3 ? 3.f / 16.f : 3.f / (8.f * valence); }
+static float LoopGamma(int valence) { return 1.f / (valence + 3.f / (8.f * LoopBeta(valence))); }
+
+// LoopSubdiv constructor (loopsubdiv.cpp:147-198)
+static void LoopInit(ShapeObj &s, int nfaces, int nvertices, const int *vi, const V3 *P) {
+    s.verts.resize(nvertices);
+    for (int i = 0; i < nvertices; ++i) s.verts[i] = SDVertex(), s.verts[i].P = P[i];
+    s.faces.resize(nfaces);
+    const int *vp = vi;
+    for (int i = 0; i < nfaces; ++i) {
+        for (int j = 0; j < 3; ++j) {
+            int v = vp[j];
+            s.faces[i].v[j] = v;
+            s.verts[v].startFace = i;
+        }
+        vp += 3;
+    }
+    struct Edge { int f0; int f0edgeNum; };
+    std::map<std::pair<int, int>, Edge> edges;
+    for (int i = 0; i < nfaces; ++i) {
+        for (int edgeNum = 0; edgeNum < 3; ++edgeNum) {
+            int a = s.faces[i].v[edgeNum], b = s.faces[i].v[NEXT(edgeNum)];
+            std::pair<int, int> key(std::min(a, b), std::max(a, b));
+            auto it = edges.find(key);
+            if (it == edges.end()) edges[key] = Edge{i, edgeNum};
+            else {
+                Edge e = it->second;
+                s.faces[e.f0].f[e.f0edgeNum] = i;
+                s.faces[i].f[edgeNum] = e.f0;
+                edges.erase(it);
+            }
+        }
+    }
+    LoopMesh lm{s.verts, s.faces};
+    for (int i = 0; i < nvertices; ++i) {
+        int f = s.verts[i].startFace;
+        do { f = lm.nextFace(f, i); } while (f != -1 && f != s.verts[i].startFace);
+        s.verts[i].boundary = (f == -1);
+        if (!s.verts[i].boundary && lm.valence(i) == 6) s.verts[i].regular = true;
+        else if (s.verts[i].boundary && lm.valence(i) == 4) s.verts[i].regular = true;
+        else s.verts[i].regular = false;
+    }
+}
+
+// LoopSubdiv::Refine (loopsubdiv.cpp:222-437) -> TriangleMesh with limit normals
+static std::shared_ptr<TriMesh> LoopRefine(ShapeObj &s) {
+    std::vector<SDVertex> V = s.verts;
+    std::vector<SDFace> F = s.faces;
+    std::vector<int> f(F.size()), v(V.size());
+    for (size_t i = 0; i < F.size(); ++i) f[i] = (int)i;
+    for (size_t i = 0; i < V.size(); ++i) v[i] = (int)i;
+    LoopMesh lm{V, F};
+    for (int level = 0; level < s.nLevels; ++level) {
+        std::vector<int> newFaces, newVertices;
+        for (size_t j = 0; j < v.size(); ++j) {
+            SDVertex c; c.regular = V[v[j]].regular; c.boundary = V[v[j]].boundary;
+            V.push_back(c);
+            V[v[j]].child = (int)V.size() - 1;
+            newVertices.push_back((int)V.size() - 1);
+        }
+        for (size_t j = 0; j < f.size(); ++j)
+            for (int k = 0; k < 4; ++k) {
+                F.push_back(SDFace());
+                F[f[j]].children[k] = (int)F.size() - 1;
+                newFaces.push_back((int)F.size() - 1);
+            }
+        // even vertices
+        for (size_t j = 0; j < v.size(); ++j) {
+            int vv = v[j];
+            V3 P;
+            if (!V[vv].boundary) {
+                if (V[vv].regular) P = lm.weightOneRing(vv, 1.f / 16.f);
+                else P = lm.weightOneRing(vv, LoopBeta(lm.valence(vv)));
+            } else P = lm.weightBoundary(vv, 1.f / 8.f);
+            V[V[vv].child].P = P;
+        }
+        // odd (edge) vertices
+        std::map<std::pair<int, int>, int> edgeVerts;
+        for (size_t j = 0; j < f.size(); ++j) {
+            int face = f[j];
+            for (int k = 0; k < 3; ++k) {
+                int e0 = F[face].v[k], e1 = F[face].v[NEXT(k)];
+                std::pair<int, int> key(std::min(e0, e1), std::max(e0, e1));
+                auto it = edgeVerts.find(key);
+                if (it == edgeVerts.end()) {
+                    SDVertex nv;
+                    nv.regular = true;
+                    nv.boundary = (F[face].f[k] == -1);
+                    nv.startFace = F[face].children[3];
+                    int a = key.first, b = key.second;
+                    if (nv.boundary) {
+                        nv.P = 0.5f * V[a].P;
+                        nv.P += 0.5f * V[b].P;
+                    } else {
+                        nv.P = 3.f / 8.f * V[a].P;
+                        nv.P += 3.f / 8.f * V[b].P;
+                        nv.P += 1.f / 8.f * V[lm.otherVert(face, a, b)].P;
+                        nv.P += 1.f / 8.f * V[lm.otherVert(F[face].f[k], a, b)].P;
+                    }
+                    V.push_back(nv);
+                    newVertices.push_back((int)V.size() - 1);
+                    edgeVerts[key] = (int)V.size() - 1;
+                }
+            }
+        }
+        // topology: even vertex start faces
+        for (size_t j = 0; j < v.size(); ++j) {
+            int vert = v[j];
+            int vertNum = lm.vnum(V[vert].startFace, vert);
+            V[V[vert].child].startFace = F[V[vert].startFace].children[vertNum];
+        }
+        // face neighbour pointers
+        for (size_t j = 0; j < f.size(); ++j) {
+            int face = f[j];
+            for (int k = 0; k < 3; ++k) {
+                F[F[face].children[3]].f[k] = F[face].children[NEXT(k)];
+                F[F[face].children[k]].f[NEXT(k)] = F[face].children[3];
+                int f2 = F[face].f[k];
+                F[F[face].children[k]].f[k] = f2 != -1 ? F[f2].children[lm.vnum(f2, F[face].v[k])] : -1;
+                f2 = F[face].f[PREV(k)];
+                F[F[face].children[k]].f[PREV(k)] = f2 != -1 ? F[f2].children[lm.vnum(f2, F[face].v[k])] : -1;
+            }
+        }
+        // face vertex pointers
+        for (size_t j = 0; j < f.size(); ++j) {
+            int face = f[j];
+            for (int k = 0; k < 3; ++k) {
+                F[F[face].children[k]].v[k] = V[F[face].v[k]].child;
+                int e0 = F[face].v[k], e1 = F[face].v[NEXT(k)];
+                int vert = edgeVerts[std::make_pair(std::min(e0, e1), std::max(e0, e1))];
+                F[F[face].children[k]].v[NEXT(k)] = vert;
+                F[F[face].children[NEXT(k)]].v[k] = vert;
+                F[F[face].children[3]].v[k] = vert;
+            }
+        }
+        f = newFaces;
+        v = newVertices;
+    }
+    // limit surface
+    std::vector<V3> Plimit(v.size());
+    for (size_t i = 0; i < v.size(); ++i) {
+        if (V[v[i]].boundary) Plimit[i] = lm.weightBoundary(v[i], 1.f / 5.f);
+        else Plimit[i] = lm.weightOneRing(v[i], LoopGamma(lm.valence(v[i])));
+    }
+    for (size_t i = 0; i < v.size(); ++i) V[v[i]].P = Plimit[i];
+    // tangents -> normals
+    std::vector<V3> Ns;
+    Ns.reserve(v.size());
+    std::vector<V3> Pring;
+    for (size_t i = 0; i < v.size(); ++i) {
+        int vert = v[i];
+        V3 S(0, 0, 0), T(0, 0, 0);
+        int valence = lm.valence(vert);
+        lm.oneRing(vert, Pring);
+        if (!V[vert].boundary) {
+            for (int k = 0; k < valence; ++k) {
+                S += cosf(2.f * kPi * k / valence) * Pring[k];
+                T += sinf(2.f * kPi * k / valence) * Pring[k];
+            }
+        } else {
+            S = Pring[valence - 1] - Pring[0];
+            if (valence == 2) T = (Pring[0] + Pring[1]) - 2 * V[vert].P;
+            else if (valence == 3) T = Pring[1] - V[vert].P;
+            else if (valence == 4)
+                T = -1 * Pring[0] + 2 * Pring[1] + 2 * Pring[2] + -1 * Pring[3] + -2 * V[vert].P;
+            else {
+                float theta = kPi / float(valence - 1);
+                T = sinf(theta) * (Pring[0] + Pring[valence - 1]);
+                for (int k = 1; k < valence - 1; ++k) {
+                    float wt = (2 * cosf(theta) - 2) * sinf((k) * theta);
+                    T += wt * Pring[k];
+                }
+                T = -T;
+            }
+        }
+        Ns.push_back(Cross(S, T));
+    }
+    auto mesh = std::make_shared<TriMesh>();
+    mesh->o2w = s.o2w;
+    mesh->ro = s.ro;
+    mesh->swaps = s.o2w.SwapsHandedness();
+    mesh->ntris = (int)f.size();
+    mesh->nverts = (int)v.size();
+    std::map<int, int> used;
+    for (size_t i = 0; i < v.size(); ++i) used[v[i]] = (int)i;
+    for (size_t i = 0; i < f.size(); ++i)
+        for (int j = 0; j < 3; ++j) mesh->vi.push_back(used[F[f[i]].v[j]]);
+    mesh->p.resize(v.size());
+    for (size_t i = 0; i < v.size(); ++i) mesh->p[i] = s.o2w.Point(Plimit[i]);
+    mesh->n = Ns;
+    return mesh;
+}
+
+// ------------------------------------------------------------------------------------
+class Builder {
+public:
+    Builder(const std::string &path, const RenderOverrides &ov, HostScene *out)
+        : ov(ov), out(out), spec(ov.bands, ov.bands == 30 ? 400 : 395, ov.bands == 30 ? 700 : 715) {
+        size_t sl = path.find_last_of('/');
+        searchDir = sl == std::string::npos ? std::string(".") : path.substr(0, sl);
+    }
+    void Run(const std::string &path) {
+        if (!lex.Open(path)) throw std::runtime_error("cannot open scene file " + path);
+        Parse();
+        if (!worldEnded) throw std::runtime_error("scene has no WorldEnd");
+    }
+
+private:
+    static const int MAXT = 2;
+    struct TransformSet {
+        Xform t[MAXT];
+        bool IsAnimated() const { return t[0] != t[1]; }
+    };
+    struct GState {
+        std::map<std::string, FloatTex> floatTextures;
+        std::map<std::string, SpecTex> spectrumTextures;
+        ParamSet materialParams;
+        std::string material = "matte";
+        std::map<std::string, std::shared_ptr<MaterialObj> > namedMaterials;
+        std::string currentNamedMaterial;
+        ParamSet areaLightParams;
+        std::string areaLight;
+        bool reverseOrientation = false;
+    };
+
+    RenderOverrides ov;
+    HostScene *out;
+    SpectrumCtx spec;
+    Lexer lex;
+    std::string searchDir;
+    bool worldEnded = false;
+    Token tok;
+    bool havePeek = false;
+
+    TransformSet curT;
+    int activeBits = 3;
+    std::map<std::string, TransformSet> namedCS;
+    GState gs;
+    std::vector<GState> pushedGS;
+    std::vector<TransformSet> pushedT;
+    std::vector<int> pushedBits;
+    std::map<Xform, std::pair<Xform, Xform> > tcache;   // key compares m only (first wins)
+    float tStart = 0.f, tEnd = 1.f;
+    ParamSet filmParams, cameraParams, samplerParams, surfParams, accelParams;
+    std::string cameraName = "perspective";
+    TransformSet cameraToWorld;
+    std::vector<std::shared_ptr<LightObj> > lights;
+    std::vector<PrimObj> primitives;
+    std::vector<std::shared_ptr<TriMesh> > allMeshes;
+    std::vector<std::shared_ptr<Quadric> > allQuads;
+
+    // ----------------------------- tokens -----------------------------------------
+    bool Peek(Token *t) {
+        if (!havePeek) { lex.Next(&tok); havePeek = true; }
+        *t = tok;
+        return tok.kind != Token::END;
+    }
+    Token Take() { Token t; Peek(&t); havePeek = false; return t; }
+    float Num() {
+        Token t = Take();
+        if (t.kind != Token::NUMBER) throw std::runtime_error("expected number, got '" + t.text + "'");
+        return t.num;
+    }
+    std::string Str() {
+        Token t = Take();
+        if (t.kind != Token::STRING) throw std::runtime_error("expected string, got '" + t.text + "'");
+        return t.text;
+    }
+    void NumArray(float *v, int n) {
+        Token t; Peek(&t);
+        bool br = t.kind == Token::LBRACK;
+        if (br) Take();
+        for (int i = 0; i < n; ++i) v[i] = Num();
+        if (br) { Token e = Take(); if (e.kind != Token::RBRACK) throw std::runtime_error("expected ]"); }
+    }
+    std::string Resolve(const std::string &fn) const {
+        if (fn.empty() || fn[0] == '/') return fn;
+        return searchDir + "/" + fn;
+    }
+    ParamSet Params() {   // pbrtparse.yy paramlist + InitParamSet (pbrtparse.yy:620-760)
+        ParamSet ps;
+        for (;;) {
+            Token t;
+            if (!Peek(&t) || t.kind != Token::STRING) break;
+            std::string decl = Take().text;
+            // value: single or bracketed list of numbers or strings
+            std::vector<float> nums;
+            std::vector<std::string> strs;
+            Token v = Take();
+            if (v.kind == Token::LBRACK) {
+                for (;;) {
+                    Token e = Take();
+                    if (e.kind == Token::RBRACK) break;
+                    if (e.kind == Token::NUMBER) nums.push_back(e.num);
+                    else if (e.kind == Token::STRING) strs.push_back(e.text);
+                    else throw std::runtime_error("bad parameter list for " + decl);
+                }
+            } else if (v.kind == Token::NUMBER) nums.push_back(v.num);
+            else if (v.kind == Token::STRING) strs.push_back(v.text);
+            else throw std::runtime_error("bad parameter value for " + decl);
+            AddParam(ps, decl, nums, strs);
+        }
+        return ps;
+    }
+    void AddParam(ParamSet &ps, const std::string &decl, const std::vector<float> &nums,
+                  const std::vector<std::string> &strs) {
+        size_t a = 0;
+        while (a < decl.size() && isspace((unsigned char)decl[a])) ++a;
+        static const char *types[] = {"float", "integer", "bool", "point", "vector", "normal", "string",
+                                      "texture", "color", "rgb", "xyz", "blackbody", "spectrum"};
+        int type = -1;
+        for (int k = 0; k < 13; ++k)
+            if (decl.compare(a, strlen(types[k]), types[k]) == 0) { type = k; a += strlen(types[k]); break; }
+        if (type < 0) { out->warnings.push_back("unknown parameter type: " + decl); return; }
+        while (a < decl.size() && isspace((unsigned char)decl[a])) ++a;
+        size_t e = a;
+        while (e < decl.size() && !isspace((unsigned char)decl[e])) ++e;
+        Param p;
+        p.name = decl.substr(a, e - a);
+        switch (type) {
+            case 0: p.cat = P_FLOAT; p.f = nums; break;
+            case 1: p.cat = P_INT; for (float x : nums) p.i.push_back(int(x)); break;
+            case 2: p.cat = P_BOOL; for (auto &s : strs) p.b.push_back(s == "true"); break;
+            case 3: p.cat = P_POINT; p.f.assign(nums.begin(), nums.begin() + (nums.size() / 3) * 3); break;
+            case 4: p.cat = P_VECTOR; p.f.assign(nums.begin(), nums.begin() + (nums.size() / 3) * 3); break;
+            case 5: p.cat = P_NORMAL; p.f.assign(nums.begin(), nums.begin() + (nums.size() / 3) * 3); break;
+            case 6: p.cat = P_STRING; p.s = strs; break;
+            case 7: p.cat = P_TEXTURE; p.s = strs; break;
+            case 8: case 9:   // AddRGBSpectrum: FromRGB (reflectance) for every colour parameter
+                p.cat = P_SPECTRUM;
+                for (size_t k = 0; k + 2 < nums.size(); k += 3) p.spec.push_back(spec.FromRGB(&nums[k]));
+                break;
+            case 10:
+                p.cat = P_SPECTRUM;
+                for (size_t k = 0; k + 2 < nums.size(); k += 3) p.spec.push_back(spec.FromXYZ(&nums[k]));
+                break;
+            case 11:
+                p.cat = P_SPECTRUM;
+                for (size_t k = 0; k + 1 < nums.size(); k += 2) p.spec.push_back(spec.Blackbody(nums[k], nums[k + 1]));
+                break;
+            case 12:
+                p.cat = P_SPECTRUM;
+                if (!strs.empty()) {
+                    for (auto &fn : strs) p.spec.push_back(ReadSPD(Resolve(fn)));
+                } else {
+                    std::vector<float> wl, vv;
+                    for (size_t k = 0; k + 1 < nums.size(); k += 2) { wl.push_back(nums[k]); vv.push_back(nums[k + 1]); }
+                    p.spec.push_back(spec.FromSampled(wl.data(), vv.data(), (int)wl.size()));
+                }
+                break;
+        }
+        ps.Add(p);
+    }
+    Spec ReadSPD(const std::string &fn) {   // floatfile.cpp ReadFloatFile + paramset.cpp:145-178
+        FILE *f = fopen(fn.c_str(), "r");
+        if (!f) { out->warnings.push_back("unable to read SPD file " + fn + "; using black"); return spec.Const(0.f); }
+        std::vector<float> vals;
+        int c; bool inNumber = false; char buf[64]; int pos = 0;
+        while ((c = getc(f)) != EOF) {
+            if (c == '#') { while ((c = getc(f)) != EOF && c != '\n' && c != '\r') {} continue; }
+            if (inNumber) {
+                if (isdigit(c) || c == '.' || c == 'e' || c == '-' || c == '+') buf[pos++] = (char)c;
+                else { buf[pos] = 0; vals.push_back((float)atof(buf)); inNumber = false; pos = 0; }
+            } else if (isdigit(c) || c == '.' || c == '-' || c == '+') { inNumber = true; buf[pos++] = (char)c; }
+            if (pos >= 63) pos = 62;
+        }
+        if (inNumber) { buf[pos] = 0; vals.push_back((float)atof(buf)); }
+        fclose(f);
+        std::vector<float> wl, v;
+        for (size_t j = 0; j < vals.size() / 2; ++j) { wl.push_back(vals[2 * j]); v.push_back(vals[2 * j + 1]); }
+        return spec.FromSampled(wl.data(), v.data(), (int)wl.size());
+    }
+
+    // ------------------------------ directives ------------------------------------
+    void ForActive(const std::function<void(Xform &)> &fn) {
+        for (int i = 0; i < MAXT; ++i) if (activeBits & (1 << i)) fn(curT.t[i]);
+    }
+    void Parse() {
+        for (;;) {
+            Token t = Take();
+            if (t.kind == Token::END) return;
+            if (t.kind != Token::IDENT) throw std::runtime_error("expected directive, got '" + t.text + "'");
+            const std::string &d = t.text;
+            if (d == "Identity") ForActive([](Xform &x) { x = Xform(); });
+            else if (d == "Translate") { float v[3]; NumArray(v, 3); ForActive([&](Xform &x) { x = x * Translate(V3(v[0], v[1], v[2])); }); }
+            else if (d == "Scale") { float v[3]; NumArray(v, 3); ForActive([&](Xform &x) { x = x * Scale(v[0], v[1], v[2]); }); }
+            else if (d == "Rotate") { float v[4]; NumArray(v, 4); ForActive([&](Xform &x) { x = x * Rotate(v[0], V3(v[1], v[2], v[3])); }); }
+            else if (d == "LookAt") {
+                float v[9]; NumArray(v, 9);
+                ForActive([&](Xform &x) { x = x * LookAt(V3(v[0], v[1], v[2]), V3(v[3], v[4], v[5]), V3(v[6], v[7], v[8])); });
+            } else if (d == "ConcatTransform" || d == "Transform") {
+                float tr[16]; NumArray(tr, 16);
+                M4 m(tr[0], tr[4], tr[8], tr[12], tr[1], tr[5], tr[9], tr[13], tr[2], tr[6], tr[10], tr[14], tr[3], tr[7], tr[11], tr[15]);
+                bool concat = d == "ConcatTransform";
+                ForActive([&](Xform &x) { x = concat ? x * Xform(m) : Xform(m); });
+            } else if (d == "CoordinateSystem") namedCS[Str()] = curT;
+            else if (d == "CoordSysTransform") { std::string n = Str(); if (namedCS.count(n)) curT = namedCS[n]; }
+            else if (d == "ActiveTransform") {
+                Token a = Take();
+                if (a.text == "All") activeBits = 3; else if (a.text == "EndTime") activeBits = 2; else if (a.text == "StartTime") activeBits = 1;
+                else throw std::runtime_error("bad ActiveTransform " + a.text);
+            } else if (d == "TransformTimes") { tStart = Num(); tEnd = Num(); }
+            else if (d == "PixelFilter") { Str(); Params(); }   // api.cpp:857-860 keeps the name only
+            else if (d == "Film") { Str(); filmParams = Params(); }
+            else if (d == "Sampler") { Str(); samplerParams = Params(); }
+            else if (d == "Accelerator") { Str(); accelParams = Params(); }
+            else if (d == "SurfaceIntegrator") { Str(); surfParams = Params(); }
+            else if (d == "VolumeIntegrator") { Str(); Params(); }
+            else if (d == "Renderer") { Str(); Params(); }
+            else if (d == "Camera") {
+                cameraName = Str(); cameraParams = Params();
+                for (int i = 0; i < MAXT; ++i) cameraToWorld.t[i] = Inverse(curT.t[i]);
+                namedCS["camera"] = cameraToWorld;
+            } else if (d == "WorldBegin") {
+                for (int i = 0; i < MAXT; ++i) curT.t[i] = Xform();
+                activeBits = 3;
+                namedCS["world"] = curT;
+            } else if (d == "AttributeBegin") { pushedGS.push_back(gs); pushedT.push_back(curT); pushedBits.push_back(activeBits); }
+            else if (d == "AttributeEnd") {
+                if (pushedGS.empty()) { out->warnings.push_back("unmatched AttributeEnd"); continue; }
+                gs = pushedGS.back(); pushedGS.pop_back();
+                curT = pushedT.back(); pushedT.pop_back();
+                activeBits = pushedBits.back(); pushedBits.pop_back();
+            } else if (d == "TransformBegin") { pushedT.push_back(curT); pushedBits.push_back(activeBits); }
+            else if (d == "TransformEnd") {
+                if (pushedT.empty()) continue;
+                curT = pushedT.back(); pushedT.pop_back();
+                activeBits = pushedBits.back(); pushedBits.pop_back();
+            } else if (d == "ReverseOrientation") gs.reverseOrientation = !gs.reverseOrientation;
+            else if (d == "Material") { gs.material = Str(); gs.materialParams = Params(); gs.currentNamedMaterial = ""; }
+            else if (d == "MakeNamedMaterial") {
+                std::string n = Str(); ParamSet p = Params();
+                std::string type = p.FindOneString("type", "");
+                if (type == "") type = gs.materialParams.FindOneString("type", "");
+                if (type != "") gs.namedMaterials[n] = MakeMaterial(type, p, gs.materialParams);
+            } else if (d == "NamedMaterial") gs.currentNamedMaterial = Str();
+            else if (d == "Texture") { std::string n = Str(), type = Str(), cls = Str(); ParamSet p = Params(); MakeTexture(n, type, cls, p); }
+            else if (d == "LightSource") { std::string n = Str(); ParamSet p = Params(); MakeLight(n, p); }
+            else if (d == "AreaLightSource") { gs.areaLight = Str(); gs.areaLightParams = Params(); }
+            else if (d == "Shape") { std::string n = Str(); ParamSet p = Params(); MakeShapeDirective(n, p); }
+            else if (d == "Include") {
+                std::string fn = Resolve(Str());
+                if (havePeek) throw std::runtime_error("internal: include with pending token");
+                if (!lex.Include(fn)) throw std::runtime_error("cannot open include " + fn);
+            } else if (d == "WorldEnd") { WorldEnd(); worldEnded = true; }
+            else if (d == "ObjectBegin" || d == "ObjectInstance" || d == "Volume")
+                throw std::runtime_error("unsupported directive in this build: " + d);
+            else if (d == "ObjectEnd") {}
+            else throw std::runtime_error("unknown directive " + d);
+        }
+    }
+
+    void LookupCache(const Xform &t, Xform *o2w, Xform *w2o) {   // api.cpp:272-296
+        auto it = tcache.find(t);
+        if (it == tcache.end()) it = tcache.insert(std::make_pair(t, std::make_pair(t, Xform(Inverse(t))))).first;
+        if (o2w) *o2w = it->second.first;
+        if (w2o) *w2o = it->second.second;
+    }
+
+    // ------------------------------ textures / materials ---------------------------
+    void MakeTexture(const std::string &name, const std::string &type, const std::string &cls, const ParamSet &p) {
+        // TextureParams(params, params, ...) -- api.cpp:933-956
+        if (type == "float") {
+            FloatTex t;
+            if (cls == "constant") t.value = GetFloat(p, p, "value", 1.f);
+            else if (cls == "scale") {
+                FloatTex a = GetFloatTex(p, p, "tex1", 1.f), b = GetFloatTex(p, p, "tex2", 1.f);
+                t.constant = a.constant && b.constant; t.value = a.value * b.value;   // ScaleTexture::Evaluate
+            } else { t.constant = false; out->warnings.push_back("float texture '" + cls + "' is not constant"); }
+            gs.floatTextures[name] = t;
+        } else if (type == "color" || type == "spectrum") {
+            SpecTex t;
+            if (cls == "constant") t.value = GetSpec(p, p, "value", spec.Const(1.f));
+            else if (cls == "scale") {
+                SpecTex a = GetSpecTex(p, p, "tex1", spec.Const(1.f)), b = GetSpecTex(p, p, "tex2", spec.Const(1.f));
+                t.constant = a.constant && b.constant; t.value = SpecMul(a.value, b.value);
+            } else { t.constant = false; t.value = spec.Const(0.f); out->warnings.push_back("spectrum texture '" + cls + "' is not constant"); }
+            gs.spectrumTextures[name] = t;
+        }
+    }
+    float GetFloat(const ParamSet &g, const ParamSet &m, const std::string &n, float d) {
+        return g.FindOneFloat(n, m.FindOneFloat(n, d));
+    }
+    Spec GetSpec(const ParamSet &g, const ParamSet &m, const std::string &n, const Spec &d) {
+        return g.FindOneSpectrum(n, m.FindOneSpectrum(n, d));
+    }
+    FloatTex GetFloatTex(const ParamSet &g, const ParamSet &m, const std::string &n, float d) {   // paramset.cpp:608-622
+        std::string name = g.FindTexture(n);
+        if (name == "") name = m.FindTexture(n);
+        if (name != "") {
+            auto it = gs.floatTextures.find(name);
+            if (it != gs.floatTextures.end()) return it->second;
+            out->warnings.push_back("couldn't find float texture " + name);
+        }
+        FloatTex t; t.value = GetFloat(g, m, n, d); return t;
+    }
+    SpecTex GetSpecTex(const ParamSet &g, const ParamSet &m, const std::string &n, const Spec &d) {   // paramset.cpp:591-605
+        std::string name = g.FindTexture(n);
+        if (name == "") name = m.FindTexture(n);
+        if (name != "") {
+            auto it = gs.spectrumTextures.find(name);
+            if (it != gs.spectrumTextures.end()) return it->second;
+            out->warnings.push_back("couldn't find spectrum texture " + name);
+        }
+        SpecTex t; t.value = GetSpec(g, m, n, d); return t;
+    }
+    Spec ConstSpecTex(const ParamSet &g, const ParamSet &m, const std::string &n, const Spec &d) {
+        SpecTex t = GetSpecTex(g, m, n, d);
+        if (!t.constant) throw std::runtime_error("non-constant spectrum texture for '" + n + "' is not supported yet");
+        return t.value;
+    }
+    float ConstFloatTex(const ParamSet &g, const ParamSet &m, const std::string &n, float d) {
+        FloatTex t = GetFloatTex(g, m, n, d);
+        if (!t.constant) throw std::runtime_error("non-constant float texture for '" + n + "' is not supported yet");
+        return t.value;
+    }
+    std::shared_ptr<MaterialObj> MakeMaterial(const std::string &name, const ParamSet &g, const ParamSet &m) {
+        auto mo = std::make_shared<MaterialObj>();
+        pbrtgpu_material &mt = mo->m;
+        // every material: normalmap (constant 0 -> black, skipped) and bumpmap (constant)
+        Spec nmap = ConstSpecTex(g, m, "normalmap", spec.Const(0.f));
+        if (!SpecIsBlack(nmap)) throw std::runtime_error("normal maps are not supported yet");
+        mt.f[7] = ConstFloatTex(g, m, "bumpmap", 0.f);
+        if (name == "matte") {   // matte.cpp:34-72
+            mt.type = PBRTGPU_MAT_MATTE;
+            mo->spectra.push_back(SpecClamp(ConstSpecTex(g, m, "Kd", spec.Const(0.5f))));
+            mt.f[0] = Clamp(ConstFloatTex(g, m, "sigma", 0.f), 0.f, 90.f);
+        } else if (name == "plastic") {   // plastic.cpp:34-74
+            mt.type = PBRTGPU_MAT_PLASTIC;
+            mo->spectra.push_back(SpecClamp(ConstSpecTex(g, m, "Kd", spec.Const(0.25f))));
+            mo->spectra.push_back(SpecClamp(ConstSpecTex(g, m, "Ks", spec.Const(0.25f))));
+            mt.f[0] = ConstFloatTex(g, m, "roughness", .1f);
+        } else if (name == "mirror") {   // mirror.cpp
+            mt.type = PBRTGPU_MAT_MIRROR;
+            mo->spectra.push_back(SpecClamp(ConstSpecTex(g, m, "Kr", spec.Const(0.9f))));
+        } else if (name == "substrate") {   // substrate.cpp
+            mt.type = PBRTGPU_MAT_SUBSTRATE;
+            mo->spectra.push_back(SpecClamp(ConstSpecTex(g, m, "Kd", spec.Const(.5f))));
+            mo->spectra.push_back(SpecClamp(ConstSpecTex(g, m, "Ks", spec.Const(.5f))));
+            mt.f[0] = ConstFloatTex(g, m, "uroughness", .1f);
+            mt.f[1] = ConstFloatTex(g, m, "vroughness", .1f);
+        } else
+            throw std::runtime_error("material '" + name + "' is not supported by this build yet");
+        return mo;
+    }
+    std::shared_ptr<MaterialObj> CreateMaterialFromState(const ParamSet &params) {   // api.cpp:1127-1143
+        if (gs.currentNamedMaterial != "") {
+            auto it = gs.namedMaterials.find(gs.currentNamedMaterial);
+            if (it != gs.namedMaterials.end() && it->second) return it->second;
+        }
+        return MakeMaterial(gs.material, params, gs.materialParams);
+    }
+
+    // ------------------------------ lights ------------------------------------------
+    void MakeLight(const std::string &name, const ParamSet &p) {
+        auto lo = std::make_shared<LightObj>();
+        if (name == "point") {   // point.cpp:34-40, 69-76
+            Spec I = p.FindOneSpectrum("I", spec.Const(1.0f));
+            Spec sc = p.FindOneSpectrum("scale", spec.Const(1.0f));
+            V3 P = p.FindOnePoint("from", V3(0, 0, 0));
+            Xform l2w = Translate(V3(P.x, P.y, P.z)) * curT.t[0];
+            lo->l.type = PBRTGPU_LIGHT_POINT;
+            lo->L = SpecMul(I, sc);
+            V3 lp = l2w.Point(V3(0, 0, 0));
+            lo->l.pos[0] = lp.x; lo->l.pos[1] = lp.y; lo->l.pos[2] = lp.z;
+            memcpy(lo->l.l2w_m, l2w.m.m, 64); memcpy(lo->l.l2w_minv, l2w.mInv.m, 64);
+        } else
+            throw std::runtime_error("light '" + name + "' is not supported by this build yet");
+        lo->l.is_black = SpecIsBlack(lo->L);
+        lights.push_back(lo);
+    }
+    // ShapeSet (light.cpp:114-135): refine with a LIFO todo list
+    void ShapeSetOf(const std::shared_ptr<ShapeObj> &s, std::vector<Isect> *set) {
+        std::vector<Isect> r;
+        RefineShape(s, &r);
+        for (auto it = r.rbegin(); it != r.rend(); ++it) set->push_back(*it);
+    }
+
+    // ------------------------------ shapes ------------------------------------------
+    std::shared_ptr<ShapeObj> MakeShape(const std::string &name, const Xform &o2w, const Xform &w2o, bool ro,
+                                        const ParamSet &p) {
+        (void)w2o;
+        auto s = std::make_shared<ShapeObj>();
+        if (name == "trianglemesh") {   // trianglemesh.cpp:363-433
+            const Param *vi = p.Find(P_INT, "indices"), *P = p.Find(P_POINT, "P");
+            const Param *uvs = p.Find(P_FLOAT, "uv");
+            if (!uvs) uvs = p.Find(P_FLOAT, "st");
+            if (!vi || !P) return nullptr;
+            int npi = (int)P->f.size() / 3;
+            std::vector<float> uv;
+            if (uvs) {
+                if ((int)uvs->f.size() < 2 * npi) out->warnings.push_back("not enough uvs; discarding");
+                else uv.assign(uvs->f.begin(), uvs->f.begin() + 2 * npi);
+            }
+            const Param *N = p.Find(P_NORMAL, "N");
+            if (N && (int)N->f.size() / 3 != npi) N = nullptr;
+            if (p.Find(P_VECTOR, "S")) throw std::runtime_error("trianglemesh 'S' tangents are not supported yet");
+            if (p.FindTexture("alpha") != "" || p.FindOneFloat("alpha", 1.f) == 0.f)
+                throw std::runtime_error("alpha textures are not supported yet");
+            for (int v : vi->i) if (v >= npi) throw std::runtime_error("trianglemesh index out of bounds");
+            auto m = std::make_shared<TriMesh>();
+            m->o2w = o2w; m->ro = ro; m->swaps = o2w.SwapsHandedness();
+            m->ntris = (int)vi->i.size() / 3; m->nverts = npi;
+            m->vi.assign(vi->i.begin(), vi->i.begin() + 3 * m->ntris);
+            m->p.resize(npi);
+            for (int i = 0; i < npi; ++i) m->p[i] = o2w.Point(V3(P->f[3 * i], P->f[3 * i + 1], P->f[3 * i + 2]));
+            if (N) { m->n.resize(npi); for (int i = 0; i < npi; ++i) m->n[i] = V3(N->f[3 * i], N->f[3 * i + 1], N->f[3 * i + 2]); }
+            m->uv = uv;
+            s->kind = ShapeObj::MESH; s->mesh = m;
+            allMeshes.push_back(m);
+        } else if (name == "loopsubdiv") {   // loopsubdiv.cpp:489-502
+            int nlevels = p.FindOneInt("nlevels", 3);
+            const Param *vi = p.Find(P_INT, "indices"), *P = p.Find(P_POINT, "P");
+            if (!vi || !P) return nullptr;
+            std::vector<V3> pts(P->f.size() / 3);
+            for (size_t i = 0; i < pts.size(); ++i) pts[i] = V3(P->f[3 * i], P->f[3 * i + 1], P->f[3 * i + 2]);
+            s->kind = ShapeObj::LOOP; s->o2w = o2w; s->ro = ro; s->nLevels = nlevels;
+            LoopInit(*s, (int)vi->i.size() / 3, (int)pts.size(), vi->i.data(), pts.data());
+        } else if (name == "sphere" || name == "disk") {
+            auto q = std::make_shared<Quadric>();
+            q->o2w = o2w;
+            pbrtgpu_quadric &Q = q->q;
+            Q.reverse_orientation = ro; Q.swaps_handedness = o2w.SwapsHandedness();
+            memcpy(Q.o2w_m, o2w.m.m, 64); memcpy(Q.o2w_minv, o2w.mInv.m, 64);
+            if (name == "sphere") {   // sphere.cpp:33-43, 205-214
+                float radius = p.FindOneFloat("radius", 1.f);
+                float z0 = p.FindOneFloat("zmin", -radius), z1 = p.FindOneFloat("zmax", radius);
+                float pm = p.FindOneFloat("phimax", 360.f);
+                Q.type = PBRTGPU_SHAPE_SPHERE;
+                Q.radius = radius;
+                Q.zmin = Clamp(pmin(z0, z1), -radius, radius);
+                Q.zmax = Clamp(pmax(z0, z1), -radius, radius);
+                Q.theta_min = acosf(Clamp(Q.zmin / radius, -1.f, 1.f));
+                Q.theta_max = acosf(Clamp(Q.zmax / radius, -1.f, 1.f));
+                Q.phi_max = Radians(Clamp(pm, 0.0f, 360.0f));
+            } else {   // disk.cpp:32-38, 125-131
+                Q.type = PBRTGPU_SHAPE_DISK;
+                Q.height = p.FindOneFloat("height", 0.);
+                Q.radius = p.FindOneFloat("radius", 1);
+                Q.inner_radius = p.FindOneFloat("innerradius", 0);
+                Q.phi_max = Radians(Clamp(p.FindOneFloat("phimax", 360), 0.0f, 360.0f));
+            }
+            s->kind = ShapeObj::QUADRIC; s->quad = q;
+            allQuads.push_back(q);
+        } else
+            throw std::runtime_error("shape '" + name + "' is not supported by this build yet");
+        return s;
+    }
+    // Shape::Refine result in order (triangles 0..n-1 of the mesh)
+    void RefineShape(const std::shared_ptr<ShapeObj> &s, std::vector<Isect> *outv) {
+        if (s->kind == ShapeObj::QUADRIC) { Isect is; is.kind = s->quad->q.type; is.quad = s->quad.get(); outv->push_back(is); return; }
+        TriMesh *m;
+        if (s->kind == ShapeObj::LOOP) {
+            if (!s->refined) { s->refined = LoopRefine(*s); allMeshes.push_back(s->refined); }
+            m = s->refined.get();
+        } else m = s->mesh.get();
+        for (int i = 0; i < m->ntris; ++i) { Isect is; is.kind = PBRTGPU_SHAPE_TRIANGLE; is.mesh = m; is.tri = i; outv->push_back(is); }
+    }
+    void MakeShapeDirective(const std::string &name, const ParamSet &params) {   // api.cpp:1051-1123
+        if (curT.IsAnimated())
+            throw std::runtime_error("animated shapes (TransformedPrimitive) are not supported by this build yet");
+        Xform o2w, w2o;
+        LookupCache(curT.t[0], &o2w, &w2o);
+        auto shape = MakeShape(name, o2w, w2o, gs.reverseOrientation, params);
+        if (!shape) return;
+        auto mtl = CreateMaterialFromState(params);
+        int area = -1;
+        std::shared_ptr<LightObj> alo;
+        if (gs.areaLight != "") {
+            if (gs.areaLight != "area" && gs.areaLight != "diffuse")
+                throw std::runtime_error("area light '" + gs.areaLight + "' unknown");
+            // diffuse.cpp:50-58 : Lemit = L * scale, ShapeSet(shape)
+            alo = std::make_shared<LightObj>();
+            alo->l.type = PBRTGPU_LIGHT_AREA;
+            Spec L = gs.areaLightParams.FindOneSpectrum("L", spec.Const(1.0f));
+            Spec sc = gs.areaLightParams.FindOneSpectrum("scale", spec.Const(1.0f));
+            alo->L = SpecMul(L, sc);
+            alo->l.is_black = SpecIsBlack(alo->L);
+            ShapeSetOf(shape, &alo->shapeSet);
+            Xform l2w = curT.t[0];
+            memcpy(alo->l.l2w_m, l2w.m.m, 64); memcpy(alo->l.l2w_minv, l2w.mInv.m, 64);
+        }
+        PrimObj po; po.shape = shape; po.mtl = mtl;
+        if (alo) { lights.push_back(alo); po.areaLight = (int)lights.size() - 1; }
+        primitives.push_back(po);
+    }
+
+    // ------------------------------ WorldEnd ---------------------------------------
+    struct BuildPrim { Isect is; int material; int areaLight; };
+    struct PrimInfo { int primitiveNumber; V3 centroid; BBox bounds; };
+    struct BuildNode { BBox bounds; int children[2] = {-1, -1}; uint32_t splitAxis = 0, firstPrimOffset = 0, nPrimitives = 0; };
+    std::vector<BuildNode> bnodes;
+    std::vector<BuildPrim> refinedPrims, orderedPrims;
+    int maxDepth = 0;
+
+    int RecursiveBuild(std::vector<PrimInfo> &bd, uint32_t start, uint32_t end, int depth) {   // bvh.cpp:202-351
+        maxDepth = std::max(maxDepth, depth);
+        int nodeIdx = (int)bnodes.size();
+        bnodes.push_back(BuildNode());
+        BBox bbox;
+        for (uint32_t i = start; i < end; ++i) bbox = Union(bbox, bd[i].bounds);
+        uint32_t nPrimitives = end - start;
+        auto makeLeaf = [&]() {
+            uint32_t first = (uint32_t)orderedPrims.size();
+            for (uint32_t i = start; i < end; ++i) orderedPrims.push_back(refinedPrims[bd[i].primitiveNumber]);
+            bnodes[nodeIdx].firstPrimOffset = first; bnodes[nodeIdx].nPrimitives = nPrimitives; bnodes[nodeIdx].bounds = bbox;
+            return nodeIdx;
+        };
+        if (nPrimitives == 1) return makeLeaf();
+        BBox cb;
+        for (uint32_t i = start; i < end; ++i) cb = Union(cb, bd[i].centroid);
+        int dim = cb.MaximumExtent();
+        uint32_t mid = (start + end) / 2;
+        if (cb.pMax[dim] == cb.pMin[dim]) return makeLeaf();
+        auto cmpPts = [dim](const PrimInfo &a, const PrimInfo &b) { return a.centroid[dim] < b.centroid[dim]; };
+        if (nPrimitives <= 4) {
+            mid = (start + end) / 2;
+            std::nth_element(&bd[start], &bd[mid], &bd[end - 1] + 1, cmpPts);
+        } else {
+            const int nBuckets = 12;
+            struct Bucket { int count = 0; BBox bounds; } buckets[nBuckets];
+            for (uint32_t i = start; i < end; ++i) {
+                int b = nBuckets * ((bd[i].centroid[dim] - cb.pMin[dim]) / (cb.pMax[dim] - cb.pMin[dim]));
+                if (b == nBuckets) b = nBuckets - 1;
+                buckets[b].count++;
+                buckets[b].bounds = Union(buckets[b].bounds, bd[i].bounds);
+            }
+            float cost[nBuckets - 1];
+            for (int i = 0; i < nBuckets - 1; ++i) {
+                BBox b0, b1;
+                int count0 = 0, count1 = 0;
+                for (int j = 0; j <= i; ++j) { b0 = Union(b0, buckets[j].bounds); count0 += buckets[j].count; }
+                for (int j = i + 1; j < nBuckets; ++j) { b1 = Union(b1, buckets[j].bounds); count1 += buckets[j].count; }
+                cost[i] = .125f + (count0 * b0.SurfaceArea() + count1 * b1.SurfaceArea()) / bbox.SurfaceArea();
+            }
+            float minCost = cost[0];
+            uint32_t minCostSplit = 0;
+            for (int i = 1; i < nBuckets - 1; ++i)
+                if (cost[i] < minCost) { minCost = cost[i]; minCostSplit = i; }
+            const uint32_t maxPrimsInNode = 4;
+            if (nPrimitives > maxPrimsInNode || minCost < nPrimitives) {
+                float pmin_ = cb.pMin[dim], pmax_ = cb.pMax[dim];
+                int splitBucket = (int)minCostSplit;   // CompareToBucket (bvh.cpp:84-101)
+                PrimInfo *pm = std::partition(&bd[start], &bd[end - 1] + 1, [&](const PrimInfo &p) {
+                    int b = nBuckets * ((p.centroid[dim] - pmin_) / (pmax_ - pmin_));
+                    if (b == nBuckets) b = nBuckets - 1;
+                    return b <= splitBucket;
+                });
+                mid = (uint32_t)(pm - &bd[0]);
+            } else
+                return makeLeaf();
+        }
+        int c0 = RecursiveBuild(bd, start, mid, depth + 1);
+        int c1 = RecursiveBuild(bd, mid, end, depth + 1);
+        BuildNode &n = bnodes[nodeIdx];
+        n.children[0] = c0; n.children[1] = c1;
+        n.bounds = Union(bnodes[c0].bounds, bnodes[c1].bounds);
+        n.splitAxis = dim; n.nPrimitives = 0;
+        return nodeIdx;
+    }
+    uint32_t Flatten(int node, uint32_t *offset) {   // bvh.cpp:354-372
+        pbrtgpu_bvh_node &ln = out->nodes[*offset];
+        const BuildNode &bn = bnodes[node];
+        for (int k = 0; k < 3; ++k) { ln.bmin[k] = bn.bounds.pMin[k]; ln.bmax[k] = bn.bounds.pMax[k]; }
+        uint32_t my = (*offset)++;
+        if (bn.nPrimitives > 0) {
+            ln.offset = bn.firstPrimOffset;
+            ln.meta = bn.nPrimitives & 0xff;
+        } else {
+            out->nodes[my].meta = (bn.splitAxis & 0xff) << 8;
+            Flatten(bn.children[0], offset);
+            uint32_t second = Flatten(bn.children[1], offset);
+            out->nodes[my].offset = second;
+        }
+        return my;
+    }
+
+    int EmitMesh(TriMesh *m) {
+        if (m->flatIndex >= 0) return m->flatIndex;
+        pbrtgpu_mesh fm{};
+        memcpy(fm.o2w_m, m->o2w.m.m, 64); memcpy(fm.o2w_minv, m->o2w.mInv.m, 64);
+        fm.has_normals = !m->n.empty(); fm.has_uvs = !m->uv.empty();
+        fm.reverse_orientation = m->ro; fm.swaps_handedness = m->swaps;
+        fm.vert_offset = (int)(out->vertP.size() / 3); fm.nverts = m->nverts;
+        for (int i = 0; i < m->nverts; ++i) {
+            out->vertP.push_back(m->p[i].x); out->vertP.push_back(m->p[i].y); out->vertP.push_back(m->p[i].z);
+            V3 n = m->n.empty() ? V3() : m->n[i];
+            out->vertN.push_back(n.x); out->vertN.push_back(n.y); out->vertN.push_back(n.z);
+            out->vertUV.push_back(m->uv.empty() ? 0.f : m->uv[2 * i]);
+            out->vertUV.push_back(m->uv.empty() ? 0.f : m->uv[2 * i + 1]);
+        }
+        out->meshes.push_back(fm);
+        m->flatIndex = (int)out->meshes.size() - 1;
+        return m->flatIndex;
+    }
+    int EmitShape(const Isect &is, int *type) {
+        *type = is.kind;
+        if (is.kind == PBRTGPU_SHAPE_TRIANGLE) {
+            int mi = EmitMesh(is.mesh);
+            pbrtgpu_triangle t;
+            t.mesh = mi;
+            int off = out->meshes[mi].vert_offset;
+            for (int k = 0; k < 3; ++k) t.v[k] = is.mesh->vi[3 * is.tri + k] + off;
+            out->tris.push_back(t);
+            return (int)out->tris.size() - 1;
+        }
+        if (is.quad->flatIndex < 0) { out->quadrics.push_back(is.quad->q); is.quad->flatIndex = (int)out->quadrics.size() - 1; }
+        return is.quad->flatIndex;
+    }
+    int EmitSpectrum(const Spec &s) {
+        int off = (int)out->spectra.size();
+        out->spectra.insert(out->spectra.end(), s.begin(), s.end());
+        return off;
+    }
+    int EmitMaterial(MaterialObj *m) {
+        if (m->flatIndex >= 0) return m->flatIndex;
+        pbrtgpu_material fm = m->m;
+        for (int k = 0; k < 4; ++k) fm.spec[k] = k < (int)m->spectra.size() ? EmitSpectrum(m->spectra[k]) : -1;
+        out->materials.push_back(fm);
+        m->flatIndex = (int)out->materials.size() - 1;
+        return m->flatIndex;
+    }
+
+    void WorldEnd() {
+        while (!pushedGS.empty()) { gs = pushedGS.back(); pushedGS.pop_back(); }
+        // ---- film (spectralImage.cpp:452-475) and sample extent (176-185)
+        int xres = ov.xres > 0 ? ov.xres : filmParams.FindOneInt("xresolution", 640);
+        int yres = ov.yres > 0 ? ov.yres : filmParams.FindOneInt("yresolution", 480);
+        float crop[4] = {0, 1, 0, 1};
+        const Param *cr = filmParams.Find(P_FLOAT, "cropwindow");
+        if (cr && cr->f.size() == 4) {
+            crop[0] = Clamp(pmin(cr->f[0], cr->f[1]), 0., 1.); crop[1] = Clamp(pmax(cr->f[0], cr->f[1]), 0., 1.);
+            crop[2] = Clamp(pmin(cr->f[2], cr->f[3]), 0., 1.); crop[3] = Clamp(pmax(cr->f[2], cr->f[3]), 0., 1.);
+        }
+        pbrtgpu_camera &C = out->camera;
+        C.xres = xres; C.yres = yres;
+        C.px_start = Ceil2Int(xres * crop[0]);
+        C.px_count = std::max(1, Ceil2Int(xres * crop[1]) - C.px_start);
+        C.py_start = Ceil2Int(yres * crop[2]);
+        C.py_count = std::max(1, Ceil2Int(yres * crop[3]) - C.py_start);
+        const float fw = 0.5f;   // BoxFilter default width (box.cpp:36-41); PixelFilter params ignored
+        C.sx_start = Floor2Int(C.px_start + 0.5f - fw);
+        C.sx_end = Floor2Int(C.px_start + 0.5f + C.px_count + fw);
+        C.sy_start = Floor2Int(C.py_start + 0.5f - fw);
+        C.sy_end = Floor2Int(C.py_start + 0.5f + C.py_count + fw);
+        // ---- camera (perspective.cpp:33-40, 110-147; camera.cpp:84-103)
+        if (cameraName != "perspective") throw std::runtime_error("camera '" + cameraName + "' is not supported by this build");
+        Xform c2w[2];
+        for (int i = 0; i < 2; ++i) LookupCache(cameraToWorld.t[i], &c2w[i], nullptr);
+        if (c2w[0] != c2w[1]) throw std::runtime_error("animated cameras are not supported yet");
+        float sopen = cameraParams.FindOneFloat("shutteropen", 0.f), sclose = cameraParams.FindOneFloat("shutterclose", 1.f);
+        if (sclose < sopen) std::swap(sopen, sclose);
+        float lensr = cameraParams.FindOneFloat("lensradius", 0.f);
+        float focald = cameraParams.FindOneFloat("focaldistance", 1e30f);
+        float frame = cameraParams.FindOneFloat("frameaspectratio", float(xres) / float(yres));
+        float screen[4];
+        if (frame > 1.f) { screen[0] = -frame; screen[1] = frame; screen[2] = -1.f; screen[3] = 1.f; }
+        else { screen[0] = -1.f; screen[1] = 1.f; screen[2] = -1.f / frame; screen[3] = 1.f / frame; }
+        const Param *sw = cameraParams.Find(P_FLOAT, "screenwindow");
+        if (sw && sw->f.size() == 4) for (int k = 0; k < 4; ++k) screen[k] = sw->f[k];
+        float fov = cameraParams.FindOneFloat("fov", 90.);
+        float halffov = cameraParams.FindOneFloat("halffov", -1.f);
+        if (halffov > 0.f) fov = 2.f * halffov;
+        Xform camToScreen = Perspective(fov, 1e-2f, 1000.f);
+        Xform screenToRaster = Scale(float(xres), float(yres), 1.f) *
+                               Scale(1.f / (screen[1] - screen[0]), 1.f / (screen[2] - screen[3]), 1.f) *
+                               Translate(V3(-screen[0], -screen[3], 0.f));
+        Xform rasterToScreen = Inverse(screenToRaster);
+        Xform rasterToCamera = Inverse(camToScreen) * rasterToScreen;
+        memcpy(C.raster_to_camera, rasterToCamera.m.m, 64);
+        memcpy(C.cam2world_m, c2w[0].m.m, 64);
+        C.lens_radius = lensr; C.focal_distance = focald; C.shutter_open = sopen; C.shutter_close = sclose;
+        // ---- integrator / sampler
+        out->maxDepth = ov.maxdepth >= 0 ? ov.maxdepth : surfParams.FindOneInt("maxdepth", 5);
+        int nsamp = ov.spp > 0 ? ov.spp : samplerParams.FindOneInt("pixelsamples", 4);
+        out->spp = (int)RoundUpPow2((uint32_t)nsamp);
+        out->seed = ov.seed;
+        out->nBands = spec.n();
+        out->bandY.assign(spec.Y(), spec.Y() + spec.n());
+        out->yint = spec.yint();
+        // ---- refine primitives (primitive.cpp:40-53, LIFO) and build the BVH
+        for (auto &po : primitives) {
+            std::vector<Isect> r;
+            RefineShape(po.shape, &r);
+            // single intersectable shape -> itself; refinable -> children popped in reverse
+            for (auto it = r.rbegin(); it != r.rend(); ++it) {
+                BuildPrim bp; bp.is = *it; bp.material = EmitMaterial(po.mtl.get()); bp.areaLight = po.areaLight;
+                refinedPrims.push_back(bp);
+            }
+        }
+        if (refinedPrims.empty()) throw std::runtime_error("scene has no primitives");
+        std::vector<PrimInfo> bd(refinedPrims.size());
+        for (size_t i = 0; i < refinedPrims.size(); ++i) {
+            bd[i].primitiveNumber = (int)i;
+            bd[i].bounds = refinedPrims[i].is.WorldBound();
+            bd[i].centroid = .5f * bd[i].bounds.pMin + .5f * bd[i].bounds.pMax;
+        }
+        RecursiveBuild(bd, 0, (uint32_t)bd.size(), 0);
+        out->bvhMaxDepth = maxDepth;
+        out->nodes.assign(bnodes.size(), pbrtgpu_bvh_node());
+        uint32_t off = 0;
+        Flatten(0, &off);
+        for (auto &bp : orderedPrims) {
+            pbrtgpu_prim fp;
+            fp.shape_index = EmitShape(bp.is, &fp.shape_type);
+            fp.material = bp.material;
+            fp.area_light = bp.areaLight;
+            out->prims.push_back(fp);
+        }
+        // ---- lights
+        for (auto &lo : lights) {
+            pbrtgpu_light fl = lo->l;
+            fl.spec = EmitSpectrum(lo->L);
+            if (fl.type == PBRTGPU_LIGHT_AREA) {
+                fl.shape_offset = (int)out->lightShapes.size();
+                fl.n_shapes = (int)lo->shapeSet.size();
+                // ShapeSet areas + Distribution1D (montecarlo.h:46-66)
+                std::vector<float> areas;
+                float sumArea = 0.f;
+                for (auto &is : lo->shapeSet) { float a = is.Area(); areas.push_back(a); sumArea += a; }
+                int n = (int)areas.size();
+                std::vector<float> cdf(n + 1);
+                cdf[0] = 0.;
+                for (int i = 1; i < n + 1; ++i) cdf[i] = cdf[i - 1] + areas[i - 1] / n;
+                float funcInt = cdf[n];
+                if (funcInt == 0.f) for (int i = 1; i < n + 1; ++i) cdf[i] = float(i) / float(n);
+                else for (int i = 1; i < n + 1; ++i) cdf[i] /= funcInt;
+                for (int i = 0; i < n; ++i) {
+                    pbrtgpu_light_shape ls;
+                    ls.shape_index = EmitShape(lo->shapeSet[i], &ls.shape_type);
+                    ls.area = areas[i];
+                    ls.cdf = cdf[i + 1];
+                    out->lightShapes.push_back(ls);
+                }
+                fl.sum_area = sumArea;
+            }
+            out->lights.push_back(fl);
+        }
+    }
+};
+
+bool LoadPbrtScene(const std::string &path, const RenderOverrides &ov, HostScene *out, std::string *err) {
+    try {
+        Builder b(path, ov, out);
+        b.Run(path);
+        return true;
+    } catch (const std::exception &e) {
+        if (err) *err = e.what();
+        return false;
+    }
+}
+
+void HostScene::Flat(pbrtgpu_flat_scene *f) const {
+    memset(f, 0, sizeof(*f));
+    f->abi_version = PBRTGPU_ABI_VERSION;
+    f->n_bands = nBands; f->max_depth = maxDepth; f->spp = spp; f->seed = seed;
+    f->y_int = yint; f->band_Y = bandY.data();
+    f->camera = camera;
+    f->n_nodes = (int)nodes.size(); f->nodes = nodes.data();
+    f->n_prims = (int)prims.size(); f->prims = prims.data();
+    f->n_tris = (int)tris.size(); f->tris = tris.data();
+    f->n_meshes = (int)meshes.size(); f->meshes = meshes.data();
+    f->n_verts = (int)(vertP.size() / 3); f->vert_p = vertP.data(); f->vert_n = vertN.data(); f->vert_uv = vertUV.data();
+    f->n_quadrics = (int)quadrics.size(); f->quadrics = quadrics.data();
+    f->n_materials = (int)materials.size(); f->materials = materials.data();
+    f->n_lights = (int)lights.size(); f->lights = lights.data();
+    f->n_light_shapes = (int)lightShapes.size(); f->light_shapes = lightShapes.data();
+    f->n_spectra_floats = (int)spectra.size(); f->spectra = spectra.data();
+}
+
+}  // namespace pbrtamd

@@ -1,0 +1,54 @@
+// scene.h -- host scene built by the pbrt front end and flattened for the device.
+#pragma once
+#include <string>
+#include <vector>
+#include <map>
+#include "pbrtgpu.h"
+#include "pmath.h"
+#include "spectrum.h"
+
+namespace pbrtamd {
+
+struct RenderOverrides {
+    int xres = -1, yres = -1;     // Film xresolution / yresolution
+    int spp = -1;                 // Sampler pixelsamples (rounded up to a power of two)
+    int maxdepth = -1;            // SurfaceIntegrator "path" maxdepth
+    int bands = 32;               // nSpectralSamples (32 = reference build, 60 = C4 variant)
+    uint32_t seed = 0;
+};
+
+// Host-owned storage behind a pbrtgpu_flat_scene.
+struct HostScene {
+    int nBands = 32;
+    int maxDepth = 5;
+    int spp = 4;
+    uint32_t seed = 0;
+    std::vector<float> bandY;
+    float yint = 0.f;
+    pbrtgpu_camera camera{};
+    std::vector<pbrtgpu_bvh_node> nodes;
+    std::vector<pbrtgpu_prim> prims;          // BVH order
+    std::vector<pbrtgpu_triangle> tris;
+    std::vector<pbrtgpu_mesh> meshes;
+    std::vector<float> vertP, vertN, vertUV;
+    std::vector<pbrtgpu_quadric> quadrics;
+    std::vector<pbrtgpu_material> materials;
+    std::vector<pbrtgpu_light> lights;
+    std::vector<pbrtgpu_light_shape> lightShapes;
+    std::vector<float> spectra;
+    // diagnostics
+    std::vector<std::string> warnings;
+    int bvhMaxDepth = 0;
+
+    void Flat(pbrtgpu_flat_scene *out) const;     // pointers into this object
+};
+
+// Parse a pbrt-v2 scene file (Include resolved relative to its directory) and build the
+// flattened scene with the reference's semantics (api.cpp subset, see frontend.cpp).
+bool LoadPbrtScene(const std::string &path, const RenderOverrides &ov, HostScene *out, std::string *err);
+
+// scene pack: a binary snapshot of a HostScene (so the GPU box needs no scene files)
+bool SavePack(const HostScene &s, const std::string &path, std::string *err);
+bool LoadPack(const std::string &path, HostScene *s, std::string *err);
+
+}  // namespace pbrtamd

@@ -1,0 +1,306 @@
+"""pbrtgpu.py -- Python plumbing over the C ABIs of libpbrthost.so / libpbrtgpu.so.
+
+Mirrors the reference's render entry point (Renderer::Render, core/renderer.h:35-46 as
+driven by pbrtWorldEnd, core/api.cpp:1287-1292) for tests and bench.py:
+
+    scene = Scene.load("killeroo-simple.pbrt", xres=700, yres=700, spp=256)
+    with Device(0) as dev:
+        dev.upload(scene)
+        film = dev.render()            # float32 [H][W][bands], raw sums (no normalisation)
+    scene.write_dat("out.dat", film)   # SpectralImageFilm::WriteImage layout
+
+The product path is libpbrtgpu.so: if it cannot be loaded, Device() raises -- there is no
+CPU fallback.  The CPU oracle (oracle/liboracle.so) is test infrastructure and is only
+loaded by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg via oracle().
+"""
+import ctypes
+import os
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+LIBDIR = os.path.join(HERE, "lib")
+
+MAX_BANDS = 64
+SHAPE_TRIANGLE, SHAPE_SPHERE, SHAPE_DISK = 0, 1, 2
+
+
+class BVHNode(ctypes.Structure):
+    _fields_ = [("bmin", ctypes.c_float * 3), ("bmax", ctypes.c_float * 3),
+                ("offset", ctypes.c_uint32), ("meta", ctypes.c_uint32)]
+
+
+class Camera(ctypes.Structure):
+    _fields_ = [("raster_to_camera", ctypes.c_float * 16), ("cam2world_m", ctypes.c_float * 16),
+                ("lens_radius", ctypes.c_float), ("focal_distance", ctypes.c_float),
+                ("shutter_open", ctypes.c_float), ("shutter_close", ctypes.c_float),
+                ("xres", ctypes.c_int32), ("yres", ctypes.c_int32),
+                ("px_start", ctypes.c_int32), ("px_count", ctypes.c_int32),
+                ("py_start", ctypes.c_int32), ("py_count", ctypes.c_int32),
+                ("sx_start", ctypes.c_int32), ("sx_end", ctypes.c_int32),
+                ("sy_start", ctypes.c_int32), ("sy_end", ctypes.c_int32)]
+
+
+P = ctypes.c_void_p
+I32 = ctypes.c_int32
+
+
+class FlatScene(ctypes.Structure):
+    _fields_ = [("abi_version", I32), ("n_bands", I32), ("max_depth", I32), ("spp", I32),
+                ("seed", ctypes.c_uint32), ("y_int", ctypes.c_float), ("band_Y", P),
+                ("camera", Camera),
+                ("n_nodes", I32), ("nodes", P), ("n_prims", I32), ("prims", P),
+                ("n_tris", I32), ("tris", P), ("n_meshes", I32), ("meshes", P),
+                ("n_verts", I32), ("vert_p", P), ("vert_n", P), ("vert_uv", P),
+                ("n_quadrics", I32), ("quadrics", P), ("n_materials", I32), ("materials", P),
+                ("n_lights", I32), ("lights", P), ("n_light_shapes", I32), ("light_shapes", P),
+                ("n_spectra_floats", I32), ("spectra", P)]
+
+
+class Overrides(ctypes.Structure):
+    _fields_ = [("xres", I32), ("yres", I32), ("spp", I32), ("maxdepth", I32), ("bands", I32),
+                ("seed", ctypes.c_uint32)]
+
+
+class RenderDesc(ctypes.Structure):
+    _fields_ = [("spp_begin", I32), ("spp_end", I32), ("tile_w", I32), ("tile_h", I32),
+                ("flags", I32), ("reserved", I32 * 3)]
+
+
+STAT_PATHS, STAT_KERNEL_MS, STAT_ACCUM_MS, STAT_ZEROED, STAT_SPILLS = 0, 1, 2, 3, 4
+
+_host = None
+_gpu = None
+
+
+def _load(name):
+    path = os.path.join(LIBDIR, name)
+    if not os.path.exists(path):
+        raise RuntimeError("%s not built (run __graft_entry__.build() or make -C pbrt-v2-spectral_amd)" % path)
+    return ctypes.CDLL(path)
+
+
+def host_lib():
+    global _host
+    if _host is None:
+        _host = _load("libpbrthost.so")
+        _host.pbrthost_load.argtypes = [ctypes.c_char_p, ctypes.POINTER(Overrides), ctypes.POINTER(P),
+                                        ctypes.c_char_p, ctypes.c_int]
+        _host.pbrthost_flat.argtypes = [P, ctypes.POINTER(FlatScene)]
+        _host.pbrthost_free.argtypes = [P]
+        _host.pbrthost_save_pack.argtypes = [P, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int]
+        _host.pbrthost_set_render.argtypes = [P, ctypes.c_int, ctypes.c_int, ctypes.c_uint32]
+        _host.pbrthost_info.argtypes = [P, ctypes.POINTER(ctypes.c_int64), ctypes.c_int]
+        _host.pbrthost_write_dat.argtypes = [ctypes.c_char_p, P, P, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+    return _host
+
+
+def gpu_lib():
+    """The product library. Raises if it is missing -- no silent fallback."""
+    global _gpu
+    if _gpu is None:
+        _gpu = _load("libpbrtgpu.so")
+        g = _gpu
+        g.pbrtgpu_last_error.restype = ctypes.c_char_p
+        g.pbrtgpu_context_create.argtypes = [ctypes.c_int, ctypes.POINTER(P)]
+        g.pbrtgpu_context_destroy.argtypes = [P]
+        g.pbrtgpu_scene_upload.argtypes = [P, ctypes.POINTER(FlatScene)]
+        g.pbrtgpu_render_tiles.argtypes = [P, ctypes.POINTER(RenderDesc), P, I32, P]
+        g.pbrtgpu_film_read.argtypes = [P, P, ctypes.c_int64]
+        g.pbrtgpu_film_clear.argtypes = [P]
+        g.pbrtgpu_trace_paths.argtypes = [P, P, I32, P]
+        g.pbrtgpu_intersect.argtypes = [P, P, I32, P, P]
+        g.pbrtgpu_last_kernel_timing.argtypes = [P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(I32)]
+    return _gpu
+
+
+def gpu_symbols():
+    """Symbols declared in include/pbrtgpu.h (checked by the CPU test suite)."""
+    return ["pbrtgpu_abi_version", "pbrtgpu_device_count", "pbrtgpu_context_create",
+            "pbrtgpu_context_destroy", "pbrtgpu_last_error", "pbrtgpu_scene_upload",
+            "pbrtgpu_render_tiles", "pbrtgpu_film_read", "pbrtgpu_film_clear",
+            "pbrtgpu_trace_paths", "pbrtgpu_intersect", "pbrtgpu_last_kernel_timing"]
+
+
+class Scene:
+    """A flattened scene (host-owned arrays), from a .pbrt file or a .pack scene pack."""
+
+    def __init__(self, handle):
+        self._h = handle
+        self.flat = FlatScene()
+        host_lib().pbrthost_flat(self._h, ctypes.byref(self.flat))
+
+    @staticmethod
+    def load(path, xres=-1, yres=-1, spp=-1, maxdepth=-1, bands=32, seed=0):
+        h = P()
+        err = ctypes.create_string_buffer(1024)
+        ov = Overrides(xres, yres, spp, maxdepth, bands, seed)
+        if host_lib().pbrthost_load(path.encode(), ctypes.byref(ov), ctypes.byref(h), err, 1024) != 0:
+            raise RuntimeError("scene load failed: %s" % err.value.decode())
+        return Scene(h)
+
+    def set_render(self, spp=-1, maxdepth=-1, seed=0):
+        host_lib().pbrthost_set_render(self._h, spp, maxdepth, seed)
+        host_lib().pbrthost_flat(self._h, ctypes.byref(self.flat))
+
+    def save_pack(self, path):
+        err = ctypes.create_string_buffer(1024)
+        if host_lib().pbrthost_save_pack(self._h, path.encode(), err, 1024) != 0:
+            raise RuntimeError(err.value.decode())
+
+    def info(self):
+        a = (ctypes.c_int64 * 16)()
+        host_lib().pbrthost_info(self._h, a, 16)
+        keys = ["bands", "spp", "maxdepth", "nodes", "prims", "tris", "meshes", "verts", "quadrics",
+                "materials", "lights", "bvh_depth", "width", "height", "warnings"]
+        return dict(zip(keys, list(a)))
+
+    @property
+    def bands(self):
+        return self.flat.n_bands
+
+    @property
+    def width(self):
+        return self.flat.camera.px_count
+
+    @property
+    def height(self):
+        return self.flat.camera.py_count
+
+    @property
+    def spp(self):
+        return self.flat.spp
+
+    def write_dat(self, path, film):
+        film = np.ascontiguousarray(film, dtype=np.float32)
+        host_lib().pbrthost_write_dat(path.encode(), film.ctypes.data, None, self.width, self.height, self.bands)
+
+    def __del__(self):
+        try:
+            if self._h:
+                host_lib().pbrthost_free(self._h)
+        except Exception:
+            pass
+
+
+def _check(rc):
+    if rc != 0:
+        msg = gpu_lib().pbrtgpu_last_error()
+        raise RuntimeError("pbrtgpu error %d: %s" % (rc, msg.decode() if msg else "?"))
+
+
+class Device:
+    """One pbrtgpu context on one GPU (one host thread drives it)."""
+
+    def __init__(self, device=0):
+        self.lib = gpu_lib()
+        self.ctx = P()
+        _check(self.lib.pbrtgpu_context_create(device, ctypes.byref(self.ctx)))
+        self.scene = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def close(self):
+        if self.ctx:
+            self.lib.pbrtgpu_context_destroy(self.ctx)
+            self.ctx = P()
+
+    def upload(self, scene):
+        _check(self.lib.pbrtgpu_scene_upload(self.ctx, ctypes.byref(scene.flat)))
+        self.scene = scene
+
+    def render(self, spp_begin=0, spp_end=None, tiles=None, tile=(16, 16), accumulate=False, stats=None):
+        s = self.scene
+        desc = RenderDesc(spp_begin, s.spp if spp_end is None else spp_end, tile[0], tile[1],
+                          1 if accumulate else 0, (I32 * 3)())
+        st = np.zeros(8, dtype=np.float64)
+        if tiles is None:
+            _check(self.lib.pbrtgpu_render_tiles(self.ctx, ctypes.byref(desc), None, 0, st.ctypes.data))
+        else:
+            t = np.ascontiguousarray(tiles, dtype=np.int32)
+            _check(self.lib.pbrtgpu_render_tiles(self.ctx, ctypes.byref(desc), t.ctypes.data, len(t),
+                                                 st.ctypes.data))
+        if stats is not None:
+            stats[:] = st
+        return st
+
+    def film(self):
+        s = self.scene
+        out = np.zeros((s.height, s.width, s.bands), dtype=np.float32)
+        _check(self.lib.pbrtgpu_film_read(self.ctx, out.ctypes.data, out.size))
+        return out
+
+    def clear(self):
+        _check(self.lib.pbrtgpu_film_clear(self.ctx))
+
+    def trace_paths(self, keys):
+        keys = np.ascontiguousarray(keys, dtype=np.int32).reshape(-1, 3)
+        out = np.zeros((len(keys), self.scene.bands), dtype=np.float32)
+        _check(self.lib.pbrtgpu_trace_paths(self.ctx, keys.ctypes.data, len(keys), out.ctypes.data))
+        return out
+
+    def intersect(self, rays):
+        rays = np.ascontiguousarray(rays, dtype=np.float32).reshape(-1, 8)
+        hits = np.zeros((len(rays), 4), dtype=np.float32)
+        occ = np.zeros(len(rays), dtype=np.int32)
+        _check(self.lib.pbrtgpu_intersect(self.ctx, rays.ctypes.data, len(rays), hits.ctypes.data,
+                                          occ.ctypes.data))
+        return hits, occ
+
+    def kernel_timing(self):
+        ms = ctypes.c_double()
+        n = I32()
+        _check(self.lib.pbrtgpu_last_kernel_timing(self.ctx, ctypes.byref(ms), ctypes.byref(n)))
+        return ms.value, n.value
+
+
+# ---------------------------------------------------------------- test infrastructure
+class Oracle:
+    """CPU restatement (oracle/liboracle*.so). TEST INFRASTRUCTURE ONLY."""
+
+    def __init__(self, libm_float=False):
+        name = "liboracle_libm.so" if libm_float else "liboracle.so"
+        path = os.path.join(ROOT, "oracle", name)
+        if not os.path.exists(path):
+            raise RuntimeError("%s not built (make -C oracle)" % path)
+        self.lib = ctypes.CDLL(path)
+        self.lib.oracle_trace_paths.argtypes = [ctypes.POINTER(FlatScene), P, I32, P]
+        self.lib.oracle_intersect.argtypes = [ctypes.POINTER(FlatScene), P, I32, P, P]
+        self.lib.oracle_render.argtypes = [ctypes.POINTER(FlatScene), ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                           ctypes.c_int, P, ctypes.c_int, P]
+        self.lib.oracle_trace_range.argtypes = [ctypes.POINTER(FlatScene), ctypes.c_long, ctypes.c_long,
+                                                ctypes.c_int]
+        self.lib.oracle_trace_range.restype = ctypes.c_long
+
+    def trace_paths(self, scene, keys):
+        keys = np.ascontiguousarray(keys, dtype=np.int32).reshape(-1, 3)
+        out = np.zeros((len(keys), scene.bands), dtype=np.float32)
+        self.lib.oracle_trace_paths(ctypes.byref(scene.flat), keys.ctypes.data, len(keys), out.ctypes.data)
+        return out
+
+    def intersect(self, scene, rays):
+        rays = np.ascontiguousarray(rays, dtype=np.float32).reshape(-1, 8)
+        hits = np.zeros((len(rays), 4), dtype=np.float32)
+        occ = np.zeros(len(rays), dtype=np.int32)
+        self.lib.oracle_intersect(ctypes.byref(scene.flat), rays.ctypes.data, len(rays), hits.ctypes.data,
+                                  occ.ctypes.data)
+        return hits, occ
+
+    def render(self, scene, window=None, threads=8):
+        c = scene.flat.camera
+        x0, x1, y0, y1 = window if window is not None else (c.sx_start, c.sx_end, c.sy_start, c.sy_end)
+        film = np.zeros((scene.height, scene.width, scene.bands), dtype=np.float32)
+        st = np.zeros(4, dtype=np.float64)
+        self.lib.oracle_render(ctypes.byref(scene.flat), x0, x1, y0, y1, film.ctypes.data, threads, st.ctypes.data)
+        return film, st
+
+    def trace_range(self, scene, first, count, threads):
+        return self.lib.oracle_trace_range(ctypes.byref(scene.flat), first, count, threads)
+
+
+def oracle(libm_float=False):
+    return Oracle(libm_float)
