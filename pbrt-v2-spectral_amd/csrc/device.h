@@ -1,0 +1,1301 @@
+// device.h -- CDNA4 (gfx950) device code of the spectral path tracer.
+//
+// Every function restates the reference arithmetic exactly (same operand order, float vs
+// double promotion, correctly-rounded div/sqrt, no FMA contraction: build with
+// -ffp-contract=off).  Transcendentals are evaluated in double and rounded once, which is
+// the definition shared with the CPU oracle.
+//
+// GPU-specific structure (not in the reference):
+//   * BVH nodes are read as two 16-byte loads; the traversal stack lives in LDS, one
+//     column per lane (bank = lane), depth sized from the BVH depth at launch.
+//   * triangle vertices are pre-gathered per primitive in BVH leaf order (48 B, 3 loads).
+//   * spectra are NB-wide register arrays (NB = 32 or 60 template parameter); material,
+//     light and band-Y spectra are read from the scene spectrum pool.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "pbrtgpu.h"
+
+namespace pgd {
+
+#define PGD_INLINE __device__ __forceinline__
+#define PGD_HD __host__ __device__ __forceinline__
+static constexpr float kPi = 3.14159265358979323846f;
+static constexpr float kInvPi = 0.31830988618379067154f;
+static constexpr float kInvTwoPi = 0.15915494309189533577f;
+static constexpr float kOneMinusEps = 0x1.fffffep-1f;
+
+PGD_INLINE float SINF(float x) { return (float)sin((double)x); }
+PGD_INLINE float COSF(float x) { return (float)cos((double)x); }
+PGD_INLINE float POWF(float x, float y) { return (float)pow((double)x, (double)y); }
+PGD_INLINE float ACOSF(float x) { return (float)acos((double)x); }
+PGD_INLINE float ATAN2F(float y, float x) { return (float)atan2((double)y, (double)x); }
+PGD_INLINE float TANF(float x) { return (float)tan((double)x); }
+PGD_INLINE float ATANF(float x) { return (float)atan((double)x); }
+
+// ------------------------------------------------------------------ vectors
+struct V { float x, y, z; };
+PGD_INLINE V v3(float x, float y, float z) { V r; r.x = x; r.y = y; r.z = z; return r; }
+PGD_INLINE V vadd(V a, V b) { return v3(a.x + b.x, a.y + b.y, a.z + b.z); }
+PGD_INLINE V vsub(V a, V b) { return v3(a.x - b.x, a.y - b.y, a.z - b.z); }
+PGD_INLINE V vneg(V a) { return v3(-a.x, -a.y, -a.z); }
+PGD_INLINE V vmul(V a, float f) { return v3(f * a.x, f * a.y, f * a.z); }
+PGD_INLINE V vdiv(V a, float f) { float inv = 1.f / f; return v3(a.x * inv, a.y * inv, a.z * inv); }
+PGD_INLINE float vdot(V a, V b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+PGD_INLINE float vlen2(V a) { return a.x * a.x + a.y * a.y + a.z * a.z; }
+PGD_INLINE float vlen(V a) { return sqrtf(vlen2(a)); }
+PGD_INLINE V vnorm(V a) { return vdiv(a, vlen(a)); }
+// geometry.h:461-468: products exact in double, one rounding per component
+PGD_INLINE V vcross(V a, V b) {
+    double ax = a.x, ay = a.y, az = a.z, bx = b.x, by = b.y, bz = b.z;
+    return v3((float)((ay * bz) - (az * by)), (float)((az * bx) - (ax * bz)), (float)((ax * by) - (ay * bx)));
+}
+PGD_HD float pmin(float a, float b) { return (b < a) ? b : a; }
+PGD_HD float pmax(float a, float b) { return (a < b) ? b : a; }
+PGD_INLINE float clampf(float v, float lo, float hi) { return v < lo ? lo : (v > hi ? hi : v); }
+PGD_INLINE float lerpf(float t, float a, float b) { return (1.f - t) * a + t * b; }
+PGD_INLINE V faceforward(V n, V v) { return (vdot(n, v) < 0.f) ? vneg(n) : n; }
+PGD_INLINE void coordsys(V v1, V *v2, V *v3_) {
+    if (fabsf(v1.x) > fabsf(v1.y)) {
+        float invLen = 1.f / sqrtf(v1.x * v1.x + v1.z * v1.z);
+        *v2 = v3(-v1.z * invLen, 0.f, v1.x * invLen);
+    } else {
+        float invLen = 1.f / sqrtf(v1.y * v1.y + v1.z * v1.z);
+        *v2 = v3(0.f, v1.z * invLen, -v1.y * invLen);
+    }
+    *v3_ = vcross(v1, *v2);
+}
+PGD_INLINE V xpoint(const float *m, V p) {
+    float xp = m[0] * p.x + m[1] * p.y + m[2] * p.z + m[3];
+    float yp = m[4] * p.x + m[5] * p.y + m[6] * p.z + m[7];
+    float zp = m[8] * p.x + m[9] * p.y + m[10] * p.z + m[11];
+    float wp = m[12] * p.x + m[13] * p.y + m[14] * p.z + m[15];
+    if (wp == 1.) return v3(xp, yp, zp);
+    return vdiv(v3(xp, yp, zp), wp);
+}
+PGD_INLINE V xvec(const float *m, V v) {
+    return v3(m[0] * v.x + m[1] * v.y + m[2] * v.z, m[4] * v.x + m[5] * v.y + m[6] * v.z,
+              m[8] * v.x + m[9] * v.y + m[10] * v.z);
+}
+PGD_INLINE V xnormal(const float *mi, V n) {
+    return v3(mi[0] * n.x + mi[4] * n.y + mi[8] * n.z, mi[1] * n.x + mi[5] * n.y + mi[9] * n.z,
+              mi[2] * n.x + mi[6] * n.y + mi[10] * n.z);
+}
+struct Ray { V o, d; float mint, maxt, time; };
+PGD_INLINE V rayat(const Ray &r, float t) { return vadd(r.o, vmul(r.d, t)); }
+
+// ------------------------------------------------------------------ sampler
+PGD_HD uint32_t mix32(uint32_t x) {
+    x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16;
+    return x;
+}
+PGD_HD uint32_t pixel_hash(uint32_t seed, int px, int py) {
+    uint32_t h = mix32(seed + 0x9E3779B9U);
+    h = mix32(h ^ (uint32_t)px);
+    h = mix32(h ^ ((uint32_t)py * 0x85EBCA6BU));
+    return h;
+}
+PGD_HD uint32_t dim_scramble(uint32_t hp, uint32_t d) { return mix32(hp ^ (0x9E3779B9U * (d + 1U))); }
+PGD_HD uint32_t perm_index(uint32_t hp, uint32_t d, uint32_t s, uint32_t spp) {
+    return s ^ (mix32(dim_scramble(hp, d) ^ 0x5BD1E995U) & (spp - 1U));
+}
+PGD_HD uint32_t path_seed(uint32_t hp, uint32_t s) { return mix32(hp ^ mix32(s + 0x7F4A7C15U)); }
+PGD_HD float vdc(uint32_t n, uint32_t scramble) {   // montecarlo.h:269-278
+    n = __builtin_bitreverse32(n);
+    n ^= scramble;
+    return pmin(((n >> 8) & 0xffffff) / (float)(1 << 24), kOneMinusEps);
+}
+PGD_HD float sobol2(uint32_t n, uint32_t scramble) {   // montecarlo.h:281-285
+    for (uint32_t v = 1u << 31; n != 0; n >>= 1, v ^= v >> 1)
+        if (n & 0x1) scramble ^= v;
+    return pmin(((scramble >> 8) & 0xffffff) / (float)(1 << 24), kOneMinusEps);
+}
+PGD_HD float s1d(uint32_t hp, uint32_t d, uint32_t s, uint32_t spp) { return vdc(perm_index(hp, d, s, spp), dim_scramble(hp, d)); }
+PGD_HD void s2d(uint32_t hp, uint32_t d, uint32_t s, uint32_t spp, float *u) {
+    uint32_t sp = perm_index(hp, d, s, spp), sc = dim_scramble(hp, d);
+    u[0] = vdc(sp, sc);
+    u[1] = sobol2(sp, mix32(sc ^ 0x68BC21EBU));
+}
+#define PGD_N1D 14
+#define DIM_1D(j) (3u + (uint32_t)(j))
+#define DIM_2D(k) (3u + PGD_N1D + (uint32_t)(k))
+
+// MT19937 first-generation stream (rng.cpp:35-100).  A path draws at most 32 values
+// (3 bounces x 10 + 2 roulette draws at maxdepth 5), all from the first 227-word block,
+// whose outputs depend only on the seed recurrence: out_k = temper(mt[k+397] ^
+// twist(mt[k], mt[k+1])).  State: the recurrence at positions k, k+1 and k+397.
+struct MT {
+    uint32_t k;        // next output index
+    uint32_t a, b;     // mt[k], mt[k+1]
+    uint32_t m;        // mt[k+397]
+    bool init;
+    uint32_t seed;
+};
+PGD_INLINE uint32_t mt_next_word(uint32_t prev, uint32_t idx) { return 1812433253U * (prev ^ (prev >> 30)) + idx; }
+PGD_INLINE void mt_begin(MT &r, uint32_t seed) { r.seed = seed; r.init = false; r.k = 0; }
+PGD_INLINE uint32_t mt_uint(MT &r) {
+    if (!r.init) {
+        r.a = r.seed;
+        r.b = mt_next_word(r.a, 1);
+        uint32_t w = r.b;
+        for (uint32_t i = 2; i <= 397; ++i) w = mt_next_word(w, i);
+        r.m = w;
+        r.init = true;
+    }
+    uint32_t y = (r.a & 0x80000000U) | (r.b & 0x7fffffffU);
+    y = r.m ^ (y >> 1) ^ ((y & 1U) ? 0x9908b0dfU : 0U);
+    // advance the recurrence windows
+    r.a = r.b;
+    r.b = mt_next_word(r.b, r.k + 2);
+    r.m = mt_next_word(r.m, r.k + 398);
+    r.k++;
+    y ^= (y >> 11);
+    y ^= (y << 7) & 0x9d2c5680U;
+    y ^= (y << 15) & 0xefc60000U;
+    y ^= (y >> 18);
+    return y;
+}
+PGD_INLINE float mt_float(MT &r) { return (mt_uint(r) & 0xffffff) / (float)(1 << 24); }
+
+// montecarlo.cpp:298-340
+PGD_INLINE void concentric_disk(float u1, float u2, float *dx, float *dy) {
+    float r, theta;
+    float sx = 2 * u1 - 1;
+    float sy = 2 * u2 - 1;
+    if (sx == 0.0 && sy == 0.0) { *dx = 0.0; *dy = 0.0; return; }
+    if (sx >= -sy) {
+        if (sx > sy) { r = sx; if (sy > 0.0) theta = sy / r; else theta = 8.0f + sy / r; }
+        else { r = sy; theta = 2.0f - sx / r; }
+    } else {
+        if (sx <= sy) { r = -sx; theta = 4.0f - sy / r; }
+        else { r = -sy; theta = 6.0f + sx / r; }
+    }
+    theta *= kPi / 4.f;
+    *dx = r * COSF(theta);
+    *dy = r * SINF(theta);
+}
+PGD_INLINE V cosine_hemisphere(float u1, float u2) {
+    V r;
+    concentric_disk(u1, u2, &r.x, &r.y);
+    r.z = sqrtf(pmax(0.f, 1.f - r.x * r.x - r.y * r.y));
+    return r;
+}
+PGD_INLINE V uniform_sphere(float u1, float u2) {
+    float z = 1.f - 2.f * u1;
+    float r = sqrtf(pmax(0.f, 1.f - z * z));
+    float phi = 2.f * kPi * u2;
+    return v3(r * COSF(phi), r * SINF(phi), z);
+}
+PGD_INLINE float power_heuristic(float fPdf, float gPdf) {
+    float f = 1 * fPdf, g = 1 * gPdf;
+    return (f * f) / (f * f + g * g);
+}
+
+// ------------------------------------------------------------------ device scene
+struct DevTri { float4 a, b, c; };   // p1.xyz,pad | p2.xyz,pad | p3.xyz,pad
+struct DevScene {
+    int nb, maxDepth, spp, stackDepth;
+    uint32_t seed;
+    float yint;
+    const float *bandY;
+    pbrtgpu_camera cam;
+    const float4 *nodes;              // 2 x float4 per node
+    const pbrtgpu_prim *prims;
+    const DevTri *primTri;            // per prim (triangles only meaningful)
+    const pbrtgpu_triangle *tris;
+    const pbrtgpu_mesh *meshes;
+    const float *vertP, *vertN, *vertUV;
+    const pbrtgpu_quadric *quads;
+    const pbrtgpu_material *mats;
+    const pbrtgpu_light *lights;
+    int nLights;
+    const pbrtgpu_light_shape *lightShapes;
+    const float *spectra;
+};
+
+struct DG { V p, nn, dpdu, dpdv, dndu, dndv; float u, v; };
+PGD_INLINE void dg_init(DG &dg, V p, V dpdu, V dpdv, V dndu, V dndv, float u, float v, int flip) {
+    dg.p = p; dg.dpdu = dpdu; dg.dpdv = dpdv; dg.dndu = dndu; dg.dndv = dndv;
+    dg.nn = vnorm(vcross(dpdu, dpdv));
+    dg.u = u; dg.v = v;
+    if (flip) dg.nn = vmul(dg.nn, -1.f);
+}
+PGD_INLINE V ldv(const float *p) { return v3(p[0], p[1], p[2]); }
+
+// Triangle::Intersect hit test (trianglemesh.cpp:119-157), vertices from primTri
+PGD_INLINE bool tri_hit(const DevTri &t, const Ray &ray, float *tHit) {
+    V p1 = v3(t.a.x, t.a.y, t.a.z), p2 = v3(t.b.x, t.b.y, t.b.z), p3 = v3(t.c.x, t.c.y, t.c.z);
+    V e1 = vsub(p2, p1), e2 = vsub(p3, p1);
+    V s1 = vcross(ray.d, e2);
+    float divisor = vdot(s1, e1);
+    if (divisor == 0.) return false;
+    float invDivisor = 1.f / divisor;
+    V d = vsub(ray.o, p1);
+    float b1 = vdot(d, s1) * invDivisor;
+    if (b1 < 0. || b1 > 1.) return false;
+    V s2 = vcross(d, e1);
+    float b2 = vdot(ray.d, s2) * invDivisor;
+    if (b2 < 0. || b1 + b2 > 1.) return false;
+    float tt = vdot(e2, s2) * invDivisor;
+    if (tt < ray.mint || tt > ray.maxt) return false;
+    *tHit = tt;
+    return true;
+}
+PGD_INLINE void tri_uvs(const DevScene &S, const pbrtgpu_triangle &t, float uv[3][2]) {
+    const pbrtgpu_mesh &m = S.meshes[t.mesh];
+    if (m.has_uvs) {
+        for (int k = 0; k < 3; ++k) { uv[k][0] = S.vertUV[2 * t.v[k]]; uv[k][1] = S.vertUV[2 * t.v[k] + 1]; }
+    } else {
+        uv[0][0] = 0.; uv[0][1] = 0.; uv[1][0] = 1.; uv[1][1] = 0.; uv[2][0] = 1.; uv[2][1] = 1.;
+    }
+}
+// full Triangle::Intersect (dg + rayEpsilon) for a known-hit triangle
+PGD_INLINE bool tri_intersect(const DevScene &S, int ti, const Ray &ray, float *tHit, float *rayEps, DG *dg) {
+    const pbrtgpu_triangle t = S.tris[ti];
+    V p1 = ldv(S.vertP + 3 * t.v[0]), p2 = ldv(S.vertP + 3 * t.v[1]), p3 = ldv(S.vertP + 3 * t.v[2]);
+    V e1 = vsub(p2, p1), e2 = vsub(p3, p1);
+    V s1 = vcross(ray.d, e2);
+    float divisor = vdot(s1, e1);
+    if (divisor == 0.) return false;
+    float invDivisor = 1.f / divisor;
+    V d = vsub(ray.o, p1);
+    float b1 = vdot(d, s1) * invDivisor;
+    if (b1 < 0. || b1 > 1.) return false;
+    V s2 = vcross(d, e1);
+    float b2 = vdot(ray.d, s2) * invDivisor;
+    if (b2 < 0. || b1 + b2 > 1.) return false;
+    float tt = vdot(e2, s2) * invDivisor;
+    if (tt < ray.mint || tt > ray.maxt) return false;
+    if (!dg) { *tHit = tt; return true; }
+    float uvs[3][2];
+    tri_uvs(S, t, uvs);
+    float du1 = uvs[0][0] - uvs[2][0], du2 = uvs[1][0] - uvs[2][0];
+    float dv1 = uvs[0][1] - uvs[2][1], dv2 = uvs[1][1] - uvs[2][1];
+    V dp1 = vsub(p1, p3), dp2 = vsub(p2, p3);
+    float determinant = du1 * dv2 - dv1 * du2;
+    V dpdu, dpdv;
+    if (determinant == 0.f) coordsys(vnorm(vcross(e2, e1)), &dpdu, &dpdv);
+    else {
+        float invdet = 1.f / determinant;
+        dpdu = vmul(vsub(vmul(dp1, dv2), vmul(dp2, dv1)), invdet);
+        dpdv = vmul(vadd(vmul(dp1, -du2), vmul(dp2, du1)), invdet);
+    }
+    float b0 = 1 - b1 - b2;
+    float tu = b0 * uvs[0][0] + b1 * uvs[1][0] + b2 * uvs[2][0];
+    float tv = b0 * uvs[0][1] + b1 * uvs[1][1] + b2 * uvs[2][1];
+    const pbrtgpu_mesh &m = S.meshes[t.mesh];
+    dg_init(*dg, rayat(ray, tt), dpdu, dpdv, v3(0, 0, 0), v3(0, 0, 0), tu, tv, m.reverse_orientation ^ m.swaps_handedness);
+    *tHit = tt;
+    *rayEps = 1e-3f * *tHit;
+    return true;
+}
+PGD_INLINE bool solve2x2(const float A[2][2], const float B[2], float *x0, float *x1) {
+    float det = A[0][0] * A[1][1] - A[0][1] * A[1][0];
+    if (fabsf(det) < 1e-10f) return false;
+    *x0 = (A[1][1] * B[0] - A[0][1] * B[1]) / det;
+    *x1 = (A[0][0] * B[1] - A[1][0] * B[0]) / det;
+    if (isnan(*x0) || isnan(*x1)) return false;
+    return true;
+}
+// Triangle::GetShadingGeometry (trianglemesh.cpp:285-360)
+PGD_INLINE void tri_shading(const DevScene &S, int ti, const DG &dg, DG &dgs) {
+    const pbrtgpu_triangle t = S.tris[ti];
+    const pbrtgpu_mesh &m = S.meshes[t.mesh];
+    if (!m.has_normals) { dgs = dg; return; }
+    float b[3];
+    float uv[3][2];
+    tri_uvs(S, t, uv);
+    float A[2][2] = {{uv[1][0] - uv[0][0], uv[2][0] - uv[0][0]}, {uv[1][1] - uv[0][1], uv[2][1] - uv[0][1]}};
+    float C[2] = {dg.u - uv[0][0], dg.v - uv[0][1]};
+    if (!solve2x2(A, C, &b[1], &b[2])) b[0] = b[1] = b[2] = 1.f / 3.f;
+    else b[0] = 1.f - b[1] - b[2];
+    V n0 = ldv(S.vertN + 3 * t.v[0]), n1 = ldv(S.vertN + 3 * t.v[1]), n2 = ldv(S.vertN + 3 * t.v[2]);
+    V ni = vadd(vadd(vmul(n0, b[0]), vmul(n1, b[1])), vmul(n2, b[2]));
+    V ns = vnorm(xnormal(m.o2w_minv, ni));
+    V ss = vnorm(dg.dpdu);
+    V ts = vcross(ss, ns);
+    if (vlen2(ts) > 0.f) { ts = vnorm(ts); ss = vcross(ts, ns); }
+    else coordsys(ns, &ss, &ts);
+    V dndu, dndv;
+    float du1 = uv[0][0] - uv[2][0], du2 = uv[1][0] - uv[2][0];
+    float dv1 = uv[0][1] - uv[2][1], dv2 = uv[1][1] - uv[2][1];
+    V dn1 = vsub(n0, n2), dn2 = vsub(n1, n2);
+    float determinant = du1 * dv2 - dv1 * du2;
+    if (determinant == 0.f) dndu = dndv = v3(0, 0, 0);
+    else {
+        float invdet = 1.f / determinant;
+        dndu = vmul(vsub(vmul(dn1, dv2), vmul(dn2, dv1)), invdet);
+        dndv = vmul(vadd(vmul(dn1, -du2), vmul(dn2, du1)), invdet);
+    }
+    dg_init(dgs, dg.p, ss, ts, xnormal(m.o2w_minv, dndu), xnormal(m.o2w_minv, dndv), dg.u, dg.v,
+            m.reverse_orientation ^ m.swaps_handedness);
+}
+
+PGD_INLINE bool quadratic(float A, float B, float C, float *t0, float *t1) {
+    float discrim = B * B - 4.f * A * C;
+    if (discrim <= 0.) return false;
+    float rootDiscrim = sqrtf(discrim);
+    float q;
+    if (B < 0) q = -.5f * (B - rootDiscrim);
+    else q = -.5f * (B + rootDiscrim);
+    *t0 = q / A;
+    *t1 = C / q;
+    if (*t0 > *t1) { float tmp = *t0; *t0 = *t1; *t1 = tmp; }
+    return true;
+}
+PGD_INLINE Ray to_object(const pbrtgpu_quadric &q, const Ray &r) {
+    Ray o = r;
+    const float *m = q.o2w_minv;
+    V p = r.o;
+    float x = m[0] * p.x + m[1] * p.y + m[2] * p.z + m[3];
+    float y = m[4] * p.x + m[5] * p.y + m[6] * p.z + m[7];
+    float z = m[8] * p.x + m[9] * p.y + m[10] * p.z + m[11];
+    float w = m[12] * p.x + m[13] * p.y + m[14] * p.z + m[15];
+    o.o = v3(x, y, z);
+    if (w != 1.) o.o = vdiv(o.o, w);
+    o.d = xvec(m, r.d);
+    return o;
+}
+// Sphere::Intersect (sphere.cpp:50-150)
+PGD_INLINE bool sphere_intersect(const pbrtgpu_quadric &q, const Ray &r, float *tHit, float *rayEps, DG *dg) {
+    float phi;
+    V phit;
+    Ray ray = to_object(q, r);
+    float A = ray.d.x * ray.d.x + ray.d.y * ray.d.y + ray.d.z * ray.d.z;
+    float B = 2 * (ray.d.x * ray.o.x + ray.d.y * ray.o.y + ray.d.z * ray.o.z);
+    float C = ray.o.x * ray.o.x + ray.o.y * ray.o.y + ray.o.z * ray.o.z - q.radius * q.radius;
+    float t0, t1;
+    if (!quadratic(A, B, C, &t0, &t1)) return false;
+    if (t0 > ray.maxt || t1 < ray.mint) return false;
+    float thit = t0;
+    if (t0 < ray.mint) { thit = t1; if (thit > ray.maxt) return false; }
+    phit = rayat(ray, thit);
+    if (phit.x == 0.f && phit.y == 0.f) phit.x = 1e-5f * q.radius;
+    phi = ATAN2F(phit.y, phit.x);
+    if (phi < 0.) phi += 2.f * kPi;
+    if ((q.zmin > -q.radius && phit.z < q.zmin) || (q.zmax < q.radius && phit.z > q.zmax) || phi > q.phi_max) {
+        if (thit == t1) return false;
+        if (t1 > ray.maxt) return false;
+        thit = t1;
+        phit = rayat(ray, thit);
+        if (phit.x == 0.f && phit.y == 0.f) phit.x = 1e-5f * q.radius;
+        phi = ATAN2F(phit.y, phit.x);
+        if (phi < 0.) phi += 2.f * kPi;
+        if ((q.zmin > -q.radius && phit.z < q.zmin) || (q.zmax < q.radius && phit.z > q.zmax) || phi > q.phi_max)
+            return false;
+    }
+    if (!dg) { *tHit = thit; return true; }
+    float u = phi / q.phi_max;
+    float theta = ACOSF(clampf(phit.z / q.radius, -1.f, 1.f));
+    float v = (theta - q.theta_min) / (q.theta_max - q.theta_min);
+    float zradius = sqrtf(phit.x * phit.x + phit.y * phit.y);
+    float invzradius = 1.f / zradius;
+    float cosphi = phit.x * invzradius, sinphi = phit.y * invzradius;
+    V dpdu = v3(-q.phi_max * phit.y, q.phi_max * phit.x, 0);
+    V dpdv = vmul(v3(phit.z * cosphi, phit.z * sinphi, -q.radius * SINF(theta)), q.theta_max - q.theta_min);
+    V d2Pduu = vmul(v3(phit.x, phit.y, 0), -q.phi_max * q.phi_max);
+    V d2Pduv = vmul(v3(-sinphi, cosphi, 0.), (q.theta_max - q.theta_min) * phit.z * q.phi_max);
+    V d2Pdvv = vmul(v3(phit.x, phit.y, phit.z), -(q.theta_max - q.theta_min) * (q.theta_max - q.theta_min));
+    float E = vdot(dpdu, dpdu), F = vdot(dpdu, dpdv), G = vdot(dpdv, dpdv);
+    V N = vnorm(vcross(dpdu, dpdv));
+    float e = vdot(N, d2Pduu), f = vdot(N, d2Pduv), g = vdot(N, d2Pdvv);
+    float invEGF2 = 1.f / (E * G - F * F);
+    V dndu = vadd(vmul(dpdu, (f * F - e * G) * invEGF2), vmul(dpdv, (e * F - f * E) * invEGF2));
+    V dndv = vadd(vmul(dpdu, (g * F - f * G) * invEGF2), vmul(dpdv, (f * F - g * E) * invEGF2));
+    dg_init(*dg, xpoint(q.o2w_m, phit), xvec(q.o2w_m, dpdu), xvec(q.o2w_m, dpdv), xnormal(q.o2w_minv, dndu),
+            xnormal(q.o2w_minv, dndv), u, v, q.reverse_orientation ^ q.swaps_handedness);
+    *tHit = thit;
+    *rayEps = 5e-4f * *tHit;
+    return true;
+}
+// Disk::Intersect (disk.cpp:48-96)
+PGD_INLINE bool disk_intersect(const pbrtgpu_quadric &q, const Ray &r, float *tHit, float *rayEps, DG *dg) {
+    Ray ray = to_object(q, r);
+    if (fabsf(ray.d.z) < 1e-7) return false;
+    float thit = (q.height - ray.o.z) / ray.d.z;
+    if (thit < ray.mint || thit > ray.maxt) return false;
+    V phit = rayat(ray, thit);
+    float dist2 = phit.x * phit.x + phit.y * phit.y;
+    if (dist2 > q.radius * q.radius || dist2 < q.inner_radius * q.inner_radius) return false;
+    float phi = ATAN2F(phit.y, phit.x);
+    if (phi < 0) phi = (float)((double)phi + 2. * (double)kPi);
+    if (phi > q.phi_max) return false;
+    if (!dg) { *tHit = thit; return true; }
+    float u = phi / q.phi_max;
+    float oneMinusV = ((sqrtf(dist2) - q.inner_radius) / (q.radius - q.inner_radius));
+    float invOneMinusV = (oneMinusV > 0.f) ? (1.f / oneMinusV) : 0.f;
+    float v = 1.f - oneMinusV;
+    V dpdu = v3(-q.phi_max * phit.y, q.phi_max * phit.x, 0.);
+    V dpdv = v3(-phit.x * invOneMinusV, -phit.y * invOneMinusV, 0.);
+    float su = q.phi_max * kInvTwoPi;
+    dpdu = v3(dpdu.x * su, dpdu.y * su, dpdu.z * su);
+    float sc = (q.radius - q.inner_radius) / q.radius;
+    dpdv = v3(dpdv.x * sc, dpdv.y * sc, dpdv.z * sc);
+    V zero = v3(0, 0, 0);
+    dg_init(*dg, xpoint(q.o2w_m, phit), xvec(q.o2w_m, dpdu), xvec(q.o2w_m, dpdv), xnormal(q.o2w_minv, zero),
+            xnormal(q.o2w_minv, zero), u, v, q.reverse_orientation ^ q.swaps_handedness);
+    *tHit = thit;
+    *rayEps = 5e-4f * *tHit;
+    return true;
+}
+PGD_INLINE float shape_area(const DevScene &S, int type, int idx) {
+    if (type == PBRTGPU_SHAPE_TRIANGLE) {
+        const pbrtgpu_triangle t = S.tris[idx];
+        V p1 = ldv(S.vertP + 3 * t.v[0]), p2 = ldv(S.vertP + 3 * t.v[1]), p3 = ldv(S.vertP + 3 * t.v[2]);
+        return 0.5f * vlen(vcross(vsub(p2, p1), vsub(p3, p1)));
+    }
+    const pbrtgpu_quadric &q = S.quads[idx];
+    if (type == PBRTGPU_SHAPE_SPHERE) return q.phi_max * q.radius * (q.zmax - q.zmin);
+    return q.phi_max * 0.5f * (q.radius * q.radius - q.inner_radius * q.inner_radius);
+}
+PGD_INLINE bool shape_intersect(const DevScene &S, int type, int idx, const Ray &r, float *tHit, float *eps, DG *dg) {
+    if (type == PBRTGPU_SHAPE_TRIANGLE) return tri_intersect(S, idx, r, tHit, eps, dg);
+    if (type == PBRTGPU_SHAPE_SPHERE) return sphere_intersect(S.quads[idx], r, tHit, eps, dg);
+    return disk_intersect(S.quads[idx], r, tHit, eps, dg);
+}
+
+// ------------------------------------------------------------------ BVH traversal
+// slab test (bvh.cpp:118-140); node = {bmin.xyz, bmax.x} {bmax.yz, offset, meta}
+PGD_INLINE bool bbox_hit(float4 n0, float4 n1, const Ray &ray, V invDir, const int neg[3]) {
+    float bminx = n0.x, bminy = n0.y, bminz = n0.z, bmaxx = n0.w, bmaxy = n1.x, bmaxz = n1.y;
+    float tmin = ((neg[0] ? bmaxx : bminx) - ray.o.x) * invDir.x;
+    float tmax = ((neg[0] ? bminx : bmaxx) - ray.o.x) * invDir.x;
+    float tymin = ((neg[1] ? bmaxy : bminy) - ray.o.y) * invDir.y;
+    float tymax = ((neg[1] ? bminy : bmaxy) - ray.o.y) * invDir.y;
+    if ((tmin > tymax) || (tymin > tmax)) return false;
+    if (tymin > tmin) tmin = tymin;
+    if (tymax < tmax) tmax = tymax;
+    float tzmin = ((neg[2] ? bmaxz : bminz) - ray.o.z) * invDir.z;
+    float tzmax = ((neg[2] ? bminz : bmaxz) - ray.o.z) * invDir.z;
+    if ((tmin > tzmax) || (tzmin > tmax)) return false;
+    if (tzmin > tmin) tmin = tzmin;
+    if (tzmax < tmax) tmax = tzmax;
+    return (tmin < ray.maxt) && (tmax > ray.mint);
+}
+// LDS stack: column per lane
+struct Stack {
+    uint32_t *base;   // &lds[lane]
+    int stride;       // threads per block
+    PGD_INLINE void set(int i, uint32_t v) { base[i * stride] = v; }
+    PGD_INLINE uint32_t get(int i) const { return base[i * stride]; }
+};
+PGD_INLINE bool prim_hit(const DevScene &S, int pi, const Ray &ray, float *t) {
+    const pbrtgpu_prim pr = S.prims[pi];
+    if (pr.shape_type == PBRTGPU_SHAPE_TRIANGLE) return tri_hit(S.primTri[pi], ray, t);
+    float e;
+    if (pr.shape_type == PBRTGPU_SHAPE_SPHERE) return sphere_intersect(S.quads[pr.shape_index], ray, t, &e, nullptr);
+    return disk_intersect(S.quads[pr.shape_index], ray, t, &e, nullptr);
+}
+// BVHAccel::Intersect (bvh.cpp:380-432): ray.maxt shrinks on every accepted hit
+PGD_INLINE bool bvh_intersect(const DevScene &S, Stack &st, Ray &ray, int *hitPrim, float *hitT) {
+    V invDir = v3(1.f / ray.d.x, 1.f / ray.d.y, 1.f / ray.d.z);
+    int neg[3] = {invDir.x < 0, invDir.y < 0, invDir.z < 0};
+    int todo = 0;
+    uint32_t nodeNum = 0;
+    bool found = false;
+    for (;;) {
+        float4 n0 = S.nodes[2 * nodeNum], n1 = S.nodes[2 * nodeNum + 1];
+        if (bbox_hit(n0, n1, ray, invDir, neg)) {
+            uint32_t off = __float_as_uint(n1.z), meta = __float_as_uint(n1.w);
+            uint32_t np = meta & 0xff;
+            if (np > 0) {
+                for (uint32_t i = 0; i < np; ++i) {
+                    float t;
+                    if (prim_hit(S, (int)(off + i), ray, &t)) {
+                        ray.maxt = t;
+                        *hitPrim = (int)(off + i);
+                        *hitT = t;
+                        found = true;
+                    }
+                }
+                if (todo == 0) break;
+                nodeNum = st.get(--todo);
+            } else {
+                uint32_t axis = (meta >> 8) & 0xff;
+                if (neg[axis]) { st.set(todo++, nodeNum + 1); nodeNum = off; }
+                else { st.set(todo++, off); nodeNum = nodeNum + 1; }
+            }
+        } else {
+            if (todo == 0) break;
+            nodeNum = st.get(--todo);
+        }
+    }
+    return found;
+}
+PGD_INLINE bool bvh_intersectP(const DevScene &S, Stack &st, const Ray &ray) {
+    V invDir = v3(1.f / ray.d.x, 1.f / ray.d.y, 1.f / ray.d.z);
+    int neg[3] = {invDir.x < 0, invDir.y < 0, invDir.z < 0};
+    int todo = 0;
+    uint32_t nodeNum = 0;
+    for (;;) {
+        float4 n0 = S.nodes[2 * nodeNum], n1 = S.nodes[2 * nodeNum + 1];
+        if (bbox_hit(n0, n1, ray, invDir, neg)) {
+            uint32_t off = __float_as_uint(n1.z), meta = __float_as_uint(n1.w);
+            uint32_t np = meta & 0xff;
+            if (np > 0) {
+                for (uint32_t i = 0; i < np; ++i) {
+                    float t;
+                    if (prim_hit(S, (int)(off + i), ray, &t)) return true;
+                }
+                if (todo == 0) break;
+                nodeNum = st.get(--todo);
+            } else {
+                uint32_t axis = (meta >> 8) & 0xff;
+                if (neg[axis]) { st.set(todo++, nodeNum + 1); nodeNum = off; }
+                else { st.set(todo++, off); nodeNum = nodeNum + 1; }
+            }
+        } else {
+            if (todo == 0) break;
+            nodeNum = st.get(--todo);
+        }
+    }
+    return false;
+}
+struct Isect { DG dg; float rayEps; int prim; };
+PGD_INLINE void isect_fill(const DevScene &S, const Ray &ray, int prim, float t, Isect &is) {
+    const pbrtgpu_prim pr = S.prims[prim];
+    Ray r = ray;
+    r.maxt = t;
+    float th;
+    shape_intersect(S, pr.shape_type, pr.shape_index, r, &th, &is.rayEps, &is.dg);
+    is.prim = prim;
+}
+
+// ------------------------------------------------------------------ BSDF
+enum { BSDF_REFLECTION = 1, BSDF_TRANSMISSION = 2, BSDF_DIFFUSE = 4, BSDF_GLOSSY = 8, BSDF_SPECULAR = 16, BSDF_ALL = 31 };
+enum { BX_LAMBERT, BX_OREN, BX_MICRO_BLINN_DIEL, BX_SPEC_REFL_NOOP, BX_FRESNEL_BLEND_ANISO };
+struct BxDF { int kind, type; const float *R, *R2; float a, b; };
+struct BSDF { V nn, ng, sn, tn; int n; BxDF bx[2]; };
+PGD_INLINE bool matches(const BxDF &b, int flags) { return (b.type & flags) == b.type; }
+PGD_INLINE V to_local(const BSDF &b, V v) { return v3(vdot(v, b.sn), vdot(v, b.tn), vdot(v, b.nn)); }
+PGD_INLINE V to_world(const BSDF &b, V v) {
+    return v3(b.sn.x * v.x + b.tn.x * v.y + b.nn.x * v.z, b.sn.y * v.x + b.tn.y * v.y + b.nn.y * v.z,
+              b.sn.z * v.x + b.tn.z * v.y + b.nn.z * v.z);
+}
+PGD_INLINE float abscos(V w) { return fabsf(w.z); }
+PGD_INLINE float sin2(V w) { return pmax(0.f, 1.f - w.z * w.z); }
+PGD_INLINE float sinth(V w) { return sqrtf(sin2(w)); }
+PGD_INLINE float cosphi(V w) { float s = sinth(w); if (s == 0.f) return 1.f; return clampf(w.x / s, -1.f, 1.f); }
+PGD_INLINE float sinphi(V w) { float s = sinth(w); if (s == 0.f) return 0.f; return clampf(w.y / s, -1.f, 1.f); }
+PGD_INLINE bool samehemi(V w, V wp) { return w.z * wp.z > 0.f; }
+// FresnelDielectric(1.5, 1) + FrDiel (reflection.cpp:52-58, 112-127); equal in every band
+PGD_INLINE float fr_dielectric(float cosi, float eta_i, float eta_t) {
+    cosi = clampf(cosi, -1.f, 1.f);
+    bool entering = cosi > 0.;
+    float ei = eta_i, et = eta_t;
+    if (!entering) { float t = ei; ei = et; et = t; }
+    float sint = ei / et * sqrtf(pmax(0.f, 1.f - cosi * cosi));
+    if (sint >= 1.) return 1.f;
+    float cost = sqrtf(pmax(0.f, 1.f - sint * sint));
+    float ci = fabsf(cosi);
+    float Rparl = ((et * ci) - (ei * cost)) / ((et * ci) + (ei * cost));
+    float Rperp = ((ei * ci) - (et * cost)) / ((ei * ci) + (et * cost));
+    return (Rparl * Rparl + Rperp * Rperp) / 2.f;
+}
+PGD_INLINE float blinn_D(float e, V wh) { return (e + 2) * kInvTwoPi * POWF(abscos(wh), e); }
+PGD_INLINE float micro_G(V wo, V wi, V wh) {
+    float NdotWh = abscos(wh), NdotWo = abscos(wo), NdotWi = abscos(wi), WOdotWh = fabsf(vdot(wo, wh));
+    return pmin(1.f, pmin((2.f * NdotWh * NdotWo / WOdotWh), (2.f * NdotWh * NdotWi / WOdotWh)));
+}
+PGD_INLINE float blinn_pdf(float e, V wo, V wi) {
+    V wh = vnorm(vadd(wo, wi));
+    float costheta = abscos(wh);
+    float p = ((e + 1.f) * POWF(costheta, e)) / (2.f * kPi * 4.f * vdot(wo, wh));
+    if (vdot(wo, wh) <= 0.f) p = 0.f;
+    return p;
+}
+PGD_INLINE void blinn_sample(float e, V wo, V *wi, float u1, float u2, float *pdf) {
+    float costheta = POWF(u1, 1.f / (e + 1));
+    float sintheta = sqrtf(pmax(0.f, 1.f - costheta * costheta));
+    float phi = u2 * 2.f * kPi;
+    V wh = v3(sintheta * COSF(phi), sintheta * SINF(phi), costheta);
+    if (!samehemi(wo, wh)) wh = vneg(wh);
+    *wi = vadd(vneg(wo), vmul(wh, 2.f * vdot(wo, wh)));
+    float p = ((e + 1.f) * POWF(costheta, e)) / (2.f * kPi * 4.f * vdot(wo, wh));
+    if (vdot(wo, wh) <= 0.f) p = 0.f;
+    *pdf = p;
+}
+PGD_INLINE float aniso_D(float ex, float ey, V wh) {
+    float costhetah = abscos(wh);
+    float d = 1.f - costhetah * costhetah;
+    if (d == 0.f) return 0.f;
+    float e = (ex * wh.x * wh.x + ey * wh.y * wh.y) / d;
+    return sqrtf((ex + 2.f) * (ey + 2.f)) * kInvTwoPi * POWF(costhetah, e);
+}
+PGD_INLINE float aniso_pdf(float ex, float ey, V wo, V wi) {
+    V wh = vnorm(vadd(wo, wi));
+    float costhetah = abscos(wh);
+    float ds = 1.f - costhetah * costhetah;
+    float p = 0.f;
+    if (ds > 0.f && vdot(wo, wh) > 0.f) {
+        float e = (ex * wh.x * wh.x + ey * wh.y * wh.y) / ds;
+        float d = sqrtf((ex + 1.f) * (ey + 1.f)) * kInvTwoPi * POWF(costhetah, e);
+        p = d / (4.f * vdot(wo, wh));
+    }
+    return p;
+}
+PGD_INLINE void aniso_first_quadrant(float ex, float ey, float u1, float u2, float *phi, float *costheta) {
+    if (ex == ey) *phi = kPi * u1 * 0.5f;
+    else *phi = ATANF(sqrtf((ex + 1.f) / (ey + 1.f)) * TANF(kPi * u1 * 0.5f));
+    float cp = COSF(*phi), sp = SINF(*phi);
+    *costheta = POWF(u2, 1.f / (ex * cp * cp + ey * sp * sp + 1));
+}
+PGD_INLINE void aniso_sample(float ex, float ey, V wo, V *wi, float u1, float u2, float *pdf) {
+    float phi, costheta;
+    if (u1 < .25f) aniso_first_quadrant(ex, ey, 4.f * u1, u2, &phi, &costheta);
+    else if (u1 < .5f) { u1 = 4.f * (.5f - u1); aniso_first_quadrant(ex, ey, u1, u2, &phi, &costheta); phi = kPi - phi; }
+    else if (u1 < .75f) { u1 = 4.f * (u1 - .5f); aniso_first_quadrant(ex, ey, u1, u2, &phi, &costheta); phi += kPi; }
+    else { u1 = 4.f * (1.f - u1); aniso_first_quadrant(ex, ey, u1, u2, &phi, &costheta); phi = 2.f * kPi - phi; }
+    float sintheta = sqrtf(pmax(0.f, 1.f - costheta * costheta));
+    V wh = v3(sintheta * COSF(phi), sintheta * SINF(phi), costheta);
+    if (!samehemi(wo, wh)) wh = vneg(wh);
+    *wi = vadd(vneg(wo), vmul(wh, 2.f * vdot(wo, wh)));
+    float costhetah = abscos(wh);
+    float ds = 1.f - costhetah * costhetah;
+    float p = 0.f;
+    if (ds > 0.f && vdot(wo, wh) > 0.f) {
+        float e = (ex * wh.x * wh.x + ey * wh.y * wh.y) / ds;
+        float d = sqrtf((ex + 1.f) * (ey + 1.f)) * kInvTwoPi * POWF(costhetah, e);
+        p = d / (4.f * vdot(wo, wh));
+    }
+    *pdf = p;
+}
+
+// BxDF::f accumulated band-wise: out[i] += f_i(wo, wi)
+template <int NB>
+PGD_INLINE void bx_f_add(const BxDF &b, V wo, V wi, float (&out)[NB]) {
+    switch (b.kind) {
+        case BX_LAMBERT:
+#pragma unroll
+            for (int i = 0; i < NB; ++i) out[i] += b.R[i] * kInvPi;
+            break;
+        case BX_OREN: {
+            float sinthetai = sinth(wi), sinthetao = sinth(wo);
+            float maxcos = 0.f;
+            if (sinthetai > 1e-4 && sinthetao > 1e-4) {
+                float sinphii = sinphi(wi), cosphii = cosphi(wi), sinphio = sinphi(wo), cosphio = cosphi(wo);
+                float dcos = cosphii * cosphio + sinphii * sinphio;
+                maxcos = pmax(0.f, dcos);
+            }
+            float sinalpha, tanbeta;
+            if (abscos(wi) > abscos(wo)) { sinalpha = sinthetao; tanbeta = sinthetai / abscos(wi); }
+            else { sinalpha = sinthetai; tanbeta = sinthetao / abscos(wo); }
+            float s = (b.a + b.b * maxcos * sinalpha * tanbeta);
+#pragma unroll
+            for (int i = 0; i < NB; ++i) out[i] += (b.R[i] * kInvPi) * s;
+            break;
+        }
+        case BX_MICRO_BLINN_DIEL: {
+            float cosThetaO = abscos(wo), cosThetaI = abscos(wi);
+            bool zero = (cosThetaI == 0.f || cosThetaO == 0.f);
+            V wh = vadd(wi, wo);
+            zero = zero || (wh.x == 0. && wh.y == 0. && wh.z == 0.);
+            if (zero) {
+#pragma unroll
+                for (int i = 0; i < NB; ++i) out[i] += 0.f;
+                break;
+            }
+            wh = vnorm(wh);
+            float cosThetaH = vdot(wi, wh);
+            float F = fr_dielectric(cosThetaH, 1.5f, 1.f);
+            float D = blinn_D(b.a, wh), G = micro_G(wo, wi, wh);
+            float den = 4.f * cosThetaI * cosThetaO;
+#pragma unroll
+            for (int i = 0; i < NB; ++i) out[i] += (((b.R[i] * D) * G) * F) / den;
+            break;
+        }
+        case BX_SPEC_REFL_NOOP:
+#pragma unroll
+            for (int i = 0; i < NB; ++i) out[i] += 0.f;
+            break;
+        case BX_FRESNEL_BLEND_ANISO: {
+            float cd = (28.f / (23.f * kPi));
+            float ta = (1.f - POWF(1.f - .5f * abscos(wi), 5)), tb = (1.f - POWF(1.f - .5f * abscos(wo), 5));
+            V wh = vadd(wi, wo);
+            if (wh.x == 0. && wh.y == 0. && wh.z == 0.) {
+#pragma unroll
+                for (int i = 0; i < NB; ++i) out[i] += 0.f;
+                break;
+            }
+            wh = vnorm(wh);
+            float D = aniso_D(b.a, b.b, wh);
+            float den = (4.f * fabsf(vdot(wi, wh)) * pmax(abscos(wi), abscos(wo)));
+            float schl = POWF(1 - vdot(wi, wh), 5.f);
+#pragma unroll
+            for (int i = 0; i < NB; ++i) {
+                float diffuse = ((((cd * b.R[i]) * (1.f - b.R2[i])) * ta) * tb);
+                float schlick = b.R2[i] + schl * (1.f - b.R2[i]);
+                out[i] += diffuse + (D / den) * schlick;
+            }
+            break;
+        }
+    }
+}
+PGD_INLINE float bx_pdf(const BxDF &b, V wo, V wi) {
+    switch (b.kind) {
+        case BX_MICRO_BLINN_DIEL: if (!samehemi(wo, wi)) return 0.f; return blinn_pdf(b.a, wo, wi);
+        case BX_SPEC_REFL_NOOP: return 0.;
+        case BX_FRESNEL_BLEND_ANISO:
+            if (!samehemi(wo, wi)) return 0.f;
+            return .5f * (abscos(wi) * kInvPi + aniso_pdf(b.a, b.b, wo, wi));
+        default: return samehemi(wo, wi) ? abscos(wi) * kInvPi : 0.f;
+    }
+}
+template <int NB>
+PGD_INLINE void bx_sample_f(const BxDF &b, V wo, V *wi, float u1, float u2, float *pdf, float (&f)[NB]) {
+#pragma unroll
+    for (int i = 0; i < NB; ++i) f[i] = 0.f;
+    switch (b.kind) {
+        case BX_MICRO_BLINN_DIEL:
+            blinn_sample(b.a, wo, wi, u1, u2, pdf);
+            if (!samehemi(wo, *wi)) return;
+            bx_f_add<NB>(b, wo, *wi, f);
+            return;
+        case BX_SPEC_REFL_NOOP: {
+            *wi = v3(-wo.x, -wo.y, wo.z);
+            *pdf = 1.f;
+            float d = abscos(*wi);
+#pragma unroll
+            for (int i = 0; i < NB; ++i) f[i] = (1.f * b.R[i]) / d;
+            return;
+        }
+        case BX_FRESNEL_BLEND_ANISO:
+            if (u1 < .5) {
+                u1 = 2.f * u1;
+                *wi = cosine_hemisphere(u1, u2);
+                if (wo.z < 0.) wi->z *= -1.f;
+            } else {
+                u1 = 2.f * (u1 - .5f);
+                aniso_sample(b.a, b.b, wo, wi, u1, u2, pdf);
+                if (!samehemi(wo, *wi)) return;
+            }
+            *pdf = bx_pdf(b, wo, *wi);
+            bx_f_add<NB>(b, wo, *wi, f);
+            return;
+        default:
+            *wi = cosine_hemisphere(u1, u2);
+            if (wo.z < 0.) wi->z *= -1.f;
+            *pdf = bx_pdf(b, wo, *wi);
+            bx_f_add<NB>(b, wo, *wi, f);
+            return;
+    }
+}
+template <int NB>
+PGD_INLINE void bsdf_f(const BSDF &bs, V woW, V wiW, int flags, float (&f)[NB]) {
+    V wi = to_local(bs, wiW), wo = to_local(bs, woW);
+    if (vdot(wiW, bs.ng) * vdot(woW, bs.ng) > 0) flags &= ~BSDF_TRANSMISSION;
+    else flags &= ~BSDF_REFLECTION;
+#pragma unroll
+    for (int i = 0; i < NB; ++i) f[i] = 0.f;
+    for (int k = 0; k < bs.n; ++k)
+        if (matches(bs.bx[k], flags)) bx_f_add<NB>(bs.bx[k], wo, wi, f);
+}
+PGD_INLINE float bsdf_pdf(const BSDF &bs, V woW, V wiW, int flags) {
+    if (bs.n == 0.) return 0.;
+    V wo = to_local(bs, woW), wi = to_local(bs, wiW);
+    float pdf = 0.f;
+    int m = 0;
+    for (int k = 0; k < bs.n; ++k)
+        if (matches(bs.bx[k], flags)) { ++m; pdf += bx_pdf(bs.bx[k], wo, wi); }
+    return m > 0 ? pdf / m : 0.f;
+}
+template <int NB>
+PGD_INLINE void bsdf_sample_f(const BSDF &bs, V woW, V *wiW, float u0, float u1, float uc, float *pdf, int flags,
+                              int *sampledType, float (&f)[NB]) {
+    int matching = 0;
+    for (int k = 0; k < bs.n; ++k) if (matches(bs.bx[k], flags)) ++matching;
+    if (matching == 0) {
+        *pdf = 0.f; *sampledType = 0;
+#pragma unroll
+        for (int i = 0; i < NB; ++i) f[i] = 0.f;
+        return;
+    }
+    int which = (int)floorf(uc * matching);
+    if (which > matching - 1) which = matching - 1;
+    int sel = -1, count = which;
+    for (int k = 0; k < bs.n; ++k)
+        if (matches(bs.bx[k], flags) && count-- == 0) { sel = k; break; }
+    const BxDF &bx = bs.bx[sel];
+    V wo = to_local(bs, woW), wi;
+    *pdf = 0.f;
+    bx_sample_f<NB>(bx, wo, &wi, u0, u1, pdf, f);
+    if (*pdf == 0.f) {
+        *sampledType = 0;
+#pragma unroll
+        for (int i = 0; i < NB; ++i) f[i] = 0.f;
+        return;
+    }
+    *sampledType = bx.type;
+    *wiW = to_world(bs, wi);
+    if (!(bx.type & BSDF_SPECULAR) && matching > 1)
+        for (int k = 0; k < bs.n; ++k)
+            if (k != sel && matches(bs.bx[k], flags)) *pdf += bx_pdf(bs.bx[k], wo, wi);
+    if (matching > 1) *pdf /= matching;
+    if (!(bx.type & BSDF_SPECULAR)) {
+#pragma unroll
+        for (int i = 0; i < NB; ++i) f[i] = 0.f;
+        if (vdot(*wiW, bs.ng) * vdot(woW, bs.ng) > 0) flags &= ~BSDF_TRANSMISSION;
+        else flags &= ~BSDF_REFLECTION;
+        for (int k = 0; k < bs.n; ++k)
+            if (matches(bs.bx[k], flags)) bx_f_add<NB>(bs.bx[k], wo, wi, f);
+    }
+}
+template <int NB>
+PGD_INLINE bool spec_black(const float (&v)[NB]) {
+    bool black = true;
+#pragma unroll
+    for (int i = 0; i < NB; ++i) black = black && (v[i] == 0.);
+    return black;
+}
+
+// Intersection::GetBSDF -> GetShadingGeometry -> Material::GetBSDF (+ Bump, material.cpp:39-81)
+PGD_INLINE void get_bsdf(const DevScene &S, const Isect &is, BSDF &bs, V *pOut, V *nOut) {
+    const pbrtgpu_prim pr = S.prims[is.prim];
+    const pbrtgpu_material &mt = S.mats[pr.material];
+    DG dgs;
+    int ro, swaps;
+    if (pr.shape_type == PBRTGPU_SHAPE_TRIANGLE) {
+        tri_shading(S, pr.shape_index, is.dg, dgs);
+        const pbrtgpu_mesh &m = S.meshes[S.tris[pr.shape_index].mesh];
+        ro = m.reverse_orientation; swaps = m.swaps_handedness;
+    } else {
+        dgs = is.dg;
+        const pbrtgpu_quadric &q = S.quads[pr.shape_index];
+        ro = q.reverse_orientation; swaps = q.swaps_handedness;
+    }
+    float d = mt.f[7];
+    const float du = .01f, dv = .01f;   // (d - d) / du == +0 for every positive du
+    V bdpdu = vadd(vadd(dgs.dpdu, vmul(dgs.nn, (d - d) / du)), vmul(dgs.dndu, d));
+    V bdpdv = vadd(vadd(dgs.dpdv, vmul(dgs.nn, (d - d) / dv)), vmul(dgs.dndv, d));
+    V nn = vnorm(vcross(bdpdu, bdpdv));
+    if (ro ^ swaps) nn = vmul(nn, -1.f);
+    nn = faceforward(nn, is.dg.nn);
+    bs.ng = is.dg.nn;
+    bs.nn = nn;
+    bs.sn = vnorm(bdpdu);
+    bs.tn = vcross(bs.nn, bs.sn);
+    bs.n = 0;
+    *pOut = dgs.p;
+    *nOut = nn;
+    const float *sp = S.spectra;
+    switch (mt.type) {
+        case PBRTGPU_MAT_MATTE: {
+            BxDF &x = bs.bx[bs.n++];
+            x.R = sp + mt.spec[0]; x.R2 = x.R;
+            x.type = BSDF_REFLECTION | BSDF_DIFFUSE;
+            float sig = mt.f[0];
+            if (sig == 0.) { x.kind = BX_LAMBERT; x.a = x.b = 0.f; }
+            else {
+                x.kind = BX_OREN;
+                float sigma = (kPi / 180.f) * sig;
+                float sigma2 = sigma * sigma;
+                x.a = 1.f - (sigma2 / (2.f * (sigma2 + 0.33f)));
+                x.b = 0.45f * sigma2 / (sigma2 + 0.09f);
+            }
+            break;
+        }
+        case PBRTGPU_MAT_PLASTIC: {
+            BxDF &x0 = bs.bx[bs.n++];
+            x0.kind = BX_LAMBERT; x0.type = BSDF_REFLECTION | BSDF_DIFFUSE; x0.R = sp + mt.spec[0]; x0.R2 = x0.R;
+            x0.a = x0.b = 0.f;
+            BxDF &x1 = bs.bx[bs.n++];
+            x1.kind = BX_MICRO_BLINN_DIEL; x1.type = BSDF_REFLECTION | BSDF_GLOSSY; x1.R = sp + mt.spec[1]; x1.R2 = x1.R;
+            float e = 1.f / mt.f[0];
+            if (e > 10000.f || isnan(e)) e = 10000.f;
+            x1.a = e; x1.b = 0.f;
+            break;
+        }
+        case PBRTGPU_MAT_MIRROR: {
+            bool black = true;
+            for (int i = 0; i < S.nb; ++i) black = black && (sp[mt.spec[0] + i] == 0.);
+            if (!black) {
+                BxDF &x = bs.bx[bs.n++];
+                x.kind = BX_SPEC_REFL_NOOP; x.type = BSDF_REFLECTION | BSDF_SPECULAR; x.R = sp + mt.spec[0]; x.R2 = x.R;
+                x.a = x.b = 0.f;
+            }
+            break;
+        }
+        case PBRTGPU_MAT_SUBSTRATE: {
+            BxDF &x = bs.bx[bs.n++];
+            x.kind = BX_FRESNEL_BLEND_ANISO; x.type = BSDF_REFLECTION | BSDF_GLOSSY;
+            x.R = sp + mt.spec[0]; x.R2 = sp + mt.spec[1];
+            float ex = 1.f / mt.f[0], ey = 1.f / mt.f[1];
+            if (ex > 10000.f || isnan(ex)) ex = 10000.f;
+            if (ey > 10000.f || isnan(ey)) ey = 10000.f;
+            x.a = ex; x.b = ey;
+            break;
+        }
+        default: break;
+    }
+}
+
+// ------------------------------------------------------------------ lights
+PGD_INLINE V sphere_sample_p(const pbrtgpu_quadric &q, V p, float u1, float u2, V *ns) {
+    V Pcenter = xpoint(q.o2w_m, v3(0, 0, 0));
+    V wc = vnorm(vsub(Pcenter, p));
+    V wcX, wcY;
+    coordsys(wc, &wcX, &wcY);
+    if (vlen2(vsub(p, Pcenter)) - q.radius * q.radius < 1e-4f) {
+        V pp = vadd(v3(0, 0, 0), vmul(uniform_sphere(u1, u2), q.radius));
+        *ns = vnorm(xnormal(q.o2w_minv, v3(pp.x, pp.y, pp.z)));
+        if (q.reverse_orientation) *ns = vmul(*ns, -1.f);
+        return xpoint(q.o2w_m, pp);
+    }
+    float sinThetaMax2 = q.radius * q.radius / vlen2(vsub(p, Pcenter));
+    float cosThetaMax = sqrtf(pmax(0.f, 1.f - sinThetaMax2));
+    float costheta = lerpf(u1, cosThetaMax, 1.f);
+    float sintheta = sqrtf(1.f - costheta * costheta);
+    float phi = u2 * 2.f * kPi;
+    V dir = vadd(vadd(vmul(wcX, COSF(phi) * sintheta), vmul(wcY, SINF(phi) * sintheta)), vmul(wc, costheta));
+    Ray r; r.o = p; r.d = dir; r.mint = 1e-3f; r.maxt = INFINITY; r.time = 0.f;
+    float thit, eps;
+    DG dgs;
+    if (!sphere_intersect(q, r, &thit, &eps, &dgs)) thit = vdot(vsub(Pcenter, p), vnorm(r.d));
+    V ps = rayat(r, thit);
+    *ns = vnorm(vsub(ps, Pcenter));
+    if (q.reverse_orientation) *ns = vmul(*ns, -1.f);
+    return ps;
+}
+PGD_INLINE float shape_pdf_generic(const DevScene &S, int type, int idx, V p, V wi) {
+    Ray ray; ray.o = p; ray.d = wi; ray.mint = 1e-3f; ray.maxt = INFINITY; ray.time = 0.f;
+    float thit, eps;
+    DG dg;
+    if (!shape_intersect(S, type, idx, ray, &thit, &eps, &dg)) return 0.;
+    float pdf = vlen2(vsub(p, rayat(ray, thit))) / (fabsf(vdot(dg.nn, vneg(wi))) * shape_area(S, type, idx));
+    if (isinf(pdf)) pdf = 0.f;
+    return pdf;
+}
+PGD_INLINE float shape_pdf(const DevScene &S, int type, int idx, V p, V wi) {
+    if (type == PBRTGPU_SHAPE_SPHERE) {
+        const pbrtgpu_quadric &q = S.quads[idx];
+        V Pcenter = xpoint(q.o2w_m, v3(0, 0, 0));
+        if (vlen2(vsub(p, Pcenter)) - q.radius * q.radius < 1e-4f) return shape_pdf_generic(S, type, idx, p, wi);
+        float sinThetaMax2 = q.radius * q.radius / vlen2(vsub(p, Pcenter));
+        float cosThetaMax = sqrtf(pmax(0.f, 1.f - sinThetaMax2));
+        return 1.f / (2.f * kPi * (1.f - cosThetaMax));
+    }
+    return shape_pdf_generic(S, type, idx, p, wi);
+}
+PGD_INLINE V shape_sample_p(const DevScene &S, int type, int idx, V p, float u1, float u2, V *ns) {
+    if (type == PBRTGPU_SHAPE_SPHERE) return sphere_sample_p(S.quads[idx], p, u1, u2, ns);
+    if (type == PBRTGPU_SHAPE_DISK) {
+        const pbrtgpu_quadric &q = S.quads[idx];
+        V pp;
+        concentric_disk(u1, u2, &pp.x, &pp.y);
+        pp.x *= q.radius; pp.y *= q.radius; pp.z = q.height;
+        *ns = vnorm(xnormal(q.o2w_minv, v3(0, 0, 1)));
+        if (q.reverse_orientation) *ns = vmul(*ns, -1.f);
+        return xpoint(q.o2w_m, pp);
+    }
+    const pbrtgpu_triangle t = S.tris[idx];
+    const pbrtgpu_mesh &m = S.meshes[t.mesh];
+    float su1 = sqrtf(u1);
+    float b1 = 1.f - su1, b2 = u2 * su1;
+    V p1 = ldv(S.vertP + 3 * t.v[0]), p2 = ldv(S.vertP + 3 * t.v[1]), p3 = ldv(S.vertP + 3 * t.v[2]);
+    V pp = vadd(vadd(vmul(p1, b1), vmul(p2, b2)), vmul(p3, (1.f - b1 - b2)));
+    *ns = vnorm(vcross(vsub(p2, p1), vsub(p3, p1)));
+    if (m.reverse_orientation) *ns = vmul(*ns, -1.f);
+    return pp;
+}
+PGD_INLINE int sample_discrete(const pbrtgpu_light_shape *ls, int n, float u) {
+    int lo = 0, count = n + 1;
+    while (count > 0) {
+        int step = count / 2, it = lo + step;
+        float cv = it == 0 ? 0.f : ls[it - 1].cdf;
+        if (!(u < cv)) { lo = it + 1; count -= step + 1; }
+        else count = step;
+    }
+    int off = lo - 1;
+    return off < 0 ? 0 : off;
+}
+struct Seg { V o, d; float mint, maxt; };
+// Light::Sample_L; Li = scale * Ls  (scale = 1 area, 1/d^2 point); returns scale, Ls via pointer
+PGD_INLINE float light_sample_L(const DevScene &S, const pbrtgpu_light &L, V p, float pEps, const float u[3],
+                                V *wi, float *pdf, Seg *vis, bool *litByArea, bool *isPoint) {
+    if (L.type == PBRTGPU_LIGHT_POINT) {
+        V lp = v3(L.pos[0], L.pos[1], L.pos[2]);
+        *wi = vnorm(vsub(lp, p));
+        *pdf = 1.f;
+        float dist = vlen(vsub(p, lp));
+        vis->o = p; vis->d = vdiv(vsub(lp, p), dist); vis->mint = pEps; vis->maxt = dist * (1.f - 0.f);
+        *isPoint = true;
+        *litByArea = false;
+        return vlen2(vsub(lp, p));   // divisor (Intensity / d2)
+    }
+    *isPoint = false;
+    const pbrtgpu_light_shape *shs = S.lightShapes + L.shape_offset;
+    int sn = sample_discrete(shs, L.n_shapes, u[2]);
+    V ns;
+    V pt = shape_sample_p(S, shs[sn].shape_type, shs[sn].shape_index, p, u[0], u[1], &ns);
+    Ray r; r.o = p; r.d = vsub(pt, p); r.mint = 1e-3f; r.maxt = INFINITY; r.time = 0.f;
+    float thit = 1.f;
+    bool anyHit = false;
+    V hitNN = v3(0, 0, 0);
+    for (int i = 0; i < L.n_shapes; ++i) {
+        float th, e;
+        DG d2;
+        if (shape_intersect(S, shs[i].shape_type, shs[i].shape_index, r, &th, &e, &d2)) { anyHit = true; thit = th; hitNN = d2.nn; }
+    }
+    if (anyHit) ns = hitNN;
+    V ps = rayat(r, thit);
+    *wi = vnorm(vsub(ps, p));
+    float pp = 0.f;
+    for (int i = 0; i < L.n_shapes; ++i) pp += shs[i].area * shape_pdf(S, shs[i].shape_type, shs[i].shape_index, p, *wi);
+    *pdf = pp / L.sum_area;
+    float dist = vlen(vsub(p, ps));
+    vis->o = p; vis->d = vdiv(vsub(ps, p), dist); vis->mint = pEps; vis->maxt = dist * (1.f - 1e-3f);
+    *litByArea = vdot(ns, vneg(*wi)) > 0.f;
+    return 1.f;
+}
+PGD_INLINE float light_pdf(const DevScene &S, const pbrtgpu_light &L, V p, V wi) {
+    if (L.type == PBRTGPU_LIGHT_POINT) return 0.;
+    const pbrtgpu_light_shape *shs = S.lightShapes + L.shape_offset;
+    float pp = 0.f;
+    for (int i = 0; i < L.n_shapes; ++i) pp += shs[i].area * shape_pdf(S, shs[i].shape_type, shs[i].shape_index, p, wi);
+    return pp / L.sum_area;
+}
+
+// ------------------------------------------------------------------ integrator
+struct PathKey { uint32_t hp, s, spp; };
+
+// EstimateDirect (integrator.cpp:109-166) and PathIntegrator::Li (path.cpp:44-115)
+template <int NB>
+PGD_INLINE void radiance(const DevScene &S, Stack &st, Ray ray, const PathKey &pk, MT &rng, float (&Lout)[NB]) {
+    float L[NB], beta[NB], f[NB], Ld[NB], fB[NB];
+#pragma unroll
+    for (int i = 0; i < NB; ++i) { L[i] = 0.f; beta[i] = 1.f; }
+    int hp_;
+    float ht_;
+    if (!bvh_intersect(S, st, ray, &hp_, &ht_)) {
+#pragma unroll
+        for (int i = 0; i < NB; ++i) Lout[i] = (1.f * 0.f) + 0.f;
+        return;
+    }
+    Isect is;
+    isect_fill(S, ray, hp_, ht_, is);
+    bool specularBounce = false;
+    const int nLights = S.nLights;
+    for (int bounces = 0;; ++bounces) {
+        if (bounces == 0 || specularBounce) {
+            int al = S.prims[is.prim].area_light;
+            if (al >= 0 && vdot(is.dg.nn, vneg(ray.d)) > 0.f) {
+                const float *Ls = S.spectra + S.lights[al].spec;
+#pragma unroll
+                for (int i = 0; i < NB; ++i) L[i] += beta[i] * Ls[i];
+            } else {
+#pragma unroll
+                for (int i = 0; i < NB; ++i) L[i] += beta[i] * 0.f;
+            }
+        }
+        BSDF bs;
+        V p, n;
+        get_bsdf(S, is, bs, &p, &n);
+        V wo = vneg(ray.d);
+        if (nLights > 0) {
+            float ul[3], ub[3], ulnum;
+            if (bounces < 3) {
+                float u2[2];
+                ulnum = s1d(pk.hp, DIM_1D(4 * bounces + 1), pk.s, pk.spp);
+                s2d(pk.hp, DIM_2D(3 * bounces + 0), pk.s, pk.spp, u2); ul[0] = u2[0]; ul[1] = u2[1];
+                ul[2] = s1d(pk.hp, DIM_1D(4 * bounces + 0), pk.s, pk.spp);
+                s2d(pk.hp, DIM_2D(3 * bounces + 1), pk.s, pk.spp, u2); ub[0] = u2[0]; ub[1] = u2[1];
+                ub[2] = s1d(pk.hp, DIM_1D(4 * bounces + 2), pk.s, pk.spp);
+            } else {
+                ulnum = mt_float(rng);
+                ul[0] = mt_float(rng); ul[1] = mt_float(rng); ul[2] = mt_float(rng);
+                ub[0] = mt_float(rng); ub[1] = mt_float(rng); ub[2] = mt_float(rng);
+            }
+            int lightNum = (int)floorf(ulnum * nLights);
+            if (lightNum > nLights - 1) lightNum = nLights - 1;
+            const pbrtgpu_light &Lt = S.lights[lightNum];
+            const float *Ls = S.spectra + Lt.spec;
+            const int flags = BSDF_ALL & ~BSDF_SPECULAR;
+#pragma unroll
+            for (int i = 0; i < NB; ++i) Ld[i] = 0.f;
+            // ---- light sample
+            V wi;
+            float lightPdf, bsdfPdf;
+            Seg vis;
+            bool lit, isPoint;
+            float lscale = light_sample_L(S, Lt, p, is.rayEps, ul, &wi, &lightPdf, &vis, &lit, &isPoint);
+            // Li = Ls (area, lit) | 0 (area, unlit) | Ls / d2 (point)
+            bool liBlack = isPoint ? false : !lit;
+            if (isPoint) {
+                bool allz = true;
+                for (int i = 0; i < NB; ++i) allz = allz && ((Ls[i] / lscale) == 0.);
+                liBlack = allz;
+            } else if (lit) liBlack = Lt.is_black != 0;
+            if (lightPdf > 0. && !liBlack) {
+                bsdf_f<NB>(bs, wo, wi, flags, f);
+                if (!spec_black<NB>(f)) {
+                    Ray sr; sr.o = vis.o; sr.d = vis.d; sr.mint = vis.mint; sr.maxt = vis.maxt; sr.time = ray.time;
+                    if (!bvh_intersectP(S, st, sr)) {
+                        if (isPoint) {
+                            float s = fabsf(vdot(wi, n)) / lightPdf;
+#pragma unroll
+                            for (int i = 0; i < NB; ++i) Ld[i] += (f[i] * (Ls[i] / lscale)) * s;
+                        } else {
+                            bsdfPdf = bsdf_pdf(bs, wo, wi, flags);
+                            float weight = power_heuristic(lightPdf, bsdfPdf);
+                            float s = fabsf(vdot(wi, n)) * weight / lightPdf;
+#pragma unroll
+                            for (int i = 0; i < NB; ++i) Ld[i] += (f[i] * Ls[i]) * s;
+                        }
+                    }
+                }
+            }
+            // ---- BSDF sample with MIS (area lights)
+            if (!isPoint) {
+                int sampledType;
+                bsdf_sample_f<NB>(bs, wo, &wi, ub[0], ub[1], ub[2], &bsdfPdf, flags, &sampledType, fB);
+                if (!spec_black<NB>(fB) && bsdfPdf > 0.) {
+                    float weight = 1.f;
+                    bool go = true;
+                    if (!(sampledType & BSDF_SPECULAR)) {
+                        lightPdf = light_pdf(S, Lt, p, wi);
+                        if (lightPdf == 0.) go = false;
+                        else weight = power_heuristic(bsdfPdf, lightPdf);
+                    }
+                    if (go) {
+                        Ray mr; mr.o = p; mr.d = wi; mr.mint = is.rayEps; mr.maxt = INFINITY; mr.time = ray.time;
+                        int mp;
+                        float mt;
+                        bool liHit = false;
+                        if (bvh_intersect(S, st, mr, &mp, &mt)) {
+                            if (S.prims[mp].area_light == lightNum) {
+                                Isect lis;
+                                isect_fill(S, mr, mp, mt, lis);
+                                liHit = vdot(lis.dg.nn, vneg(wi)) > 0.f;
+                            }
+                        }
+                        if (liHit && !Lt.is_black) {
+                            float ad = fabsf(vdot(wi, n));
+#pragma unroll
+                            for (int i = 0; i < NB; ++i) Ld[i] += (((fB[i] * Ls[i]) * ad) * weight) / bsdfPdf;
+                        }
+                    }
+                }
+            }
+            const float nl = (float)nLights;
+#pragma unroll
+            for (int i = 0; i < NB; ++i) L[i] += beta[i] * (nl * Ld[i]);
+        } else {
+#pragma unroll
+            for (int i = 0; i < NB; ++i) L[i] += beta[i] * 0.f;
+        }
+        // ---- path continuation
+        float up[3];
+        if (bounces < 3) {
+            float u2[2];
+            s2d(pk.hp, DIM_2D(3 * bounces + 2), pk.s, pk.spp, u2); up[0] = u2[0]; up[1] = u2[1];
+            up[2] = s1d(pk.hp, DIM_1D(4 * bounces + 3), pk.s, pk.spp);
+        } else {
+            up[0] = mt_float(rng); up[1] = mt_float(rng); up[2] = mt_float(rng);
+        }
+        V wi;
+        float pdf;
+        int flags;
+        bsdf_sample_f<NB>(bs, wo, &wi, up[0], up[1], up[2], &pdf, BSDF_ALL, &flags, f);
+        if (spec_black<NB>(f) || pdf == 0.) break;
+        specularBounce = (flags & BSDF_SPECULAR) != 0;
+        float ad = fabsf(vdot(wi, n));
+#pragma unroll
+        for (int i = 0; i < NB; ++i) beta[i] *= (f[i] * ad) / pdf;
+        Ray nray; nray.o = p; nray.d = wi; nray.mint = is.rayEps; nray.maxt = INFINITY; nray.time = ray.time;
+        ray = nray;
+        if (bounces > 3) {
+            float yy = 0.f;
+            for (int i = 0; i < NB; ++i) yy += S.bandY[i] * beta[i];
+            float cp = pmin(.5f, yy / S.yint);
+            if (mt_float(rng) > cp) break;
+#pragma unroll
+            for (int i = 0; i < NB; ++i) beta[i] /= cp;
+        }
+        if (bounces == S.maxDepth) break;
+        if (!bvh_intersect(S, st, ray, &hp_, &ht_)) {
+            if (specularBounce) {
+#pragma unroll
+                for (int i = 0; i < NB; ++i) L[i] += beta[i] * 0.f;
+            }
+            break;
+        }
+        isect_fill(S, ray, hp_, ht_, is);
+#pragma unroll
+        for (int i = 0; i < NB; ++i) beta[i] *= 1.f;
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) Lout[i] = (1.f * L[i]) + 0.f;
+}
+
+// camera sample -> world ray (perspective.cpp:73-106)
+PGD_INLINE Ray camera_ray(const pbrtgpu_camera &cam, float imageX, float imageY, float lensU, float lensV, float timeU) {
+    const float *m = cam.raster_to_camera;
+    float x = imageX, y = imageY, z = 0;
+    V Pc;
+    Pc.x = m[0] * x + m[1] * y + m[2] * z + m[3];
+    Pc.y = m[4] * x + m[5] * y + m[6] * z + m[7];
+    Pc.z = m[8] * x + m[9] * y + m[10] * z + m[11];
+    float w = m[12] * x + m[13] * y + m[14] * z + m[15];
+    if (w != 1.) Pc = vdiv(Pc, w);
+    Ray r;
+    r.o = v3(0, 0, 0);
+    r.d = vnorm(v3(Pc.x, Pc.y, Pc.z));
+    r.mint = 0.f; r.maxt = INFINITY;
+    if (cam.lens_radius > 0.) {
+        float lu, lv;
+        concentric_disk(lensU, lensV, &lu, &lv);
+        lu *= cam.lens_radius; lv *= cam.lens_radius;
+        float ft = cam.focal_distance / r.d.z;
+        V Pfocus = rayat(r, ft);
+        r.o = v3(lu, lv, 0.f);
+        r.d = vnorm(vsub(Pfocus, r.o));
+    }
+    r.time = lerpf(timeU, cam.shutter_open, cam.shutter_close);
+    const float *cw = cam.cam2world_m;
+    Ray o = r;
+    V p = r.o;
+    float xp = cw[0] * p.x + cw[1] * p.y + cw[2] * p.z + cw[3];
+    float yp = cw[4] * p.x + cw[5] * p.y + cw[6] * p.z + cw[7];
+    float zp = cw[8] * p.x + cw[9] * p.y + cw[10] * p.z + cw[11];
+    float wp = cw[12] * p.x + cw[13] * p.y + cw[14] * p.z + cw[15];
+    o.o = v3(xp, yp, zp);
+    if (wp != 1.) o.o = vdiv(o.o, wp);
+    o.d = xvec(cw, r.d);
+    return o;
+}
+
+// one camera path with the NaN / negative / inf guard (samplerrenderer.cpp:86-133)
+template <int NB>
+PGD_INLINE bool trace_path(const DevScene &S, Stack &st, int px, int py, uint32_t s, float (&L)[NB]) {
+    PathKey pk;
+    pk.hp = pixel_hash(S.seed, px, py);
+    pk.s = s;
+    pk.spp = (uint32_t)S.spp;
+    float u[2], lens[2];
+    s2d(pk.hp, 0, s, pk.spp, u);
+    float imageX = px + u[0], imageY = py + u[1];
+    s2d(pk.hp, 1, s, pk.spp, lens);
+    float timeU = s1d(pk.hp, 2, s, pk.spp);
+    MT rng;
+    mt_begin(rng, path_seed(pk.hp, s));
+    Ray r = camera_ray(S.cam, imageX, imageY, lens[0], lens[1], timeU);
+    float Lr[NB];
+    radiance<NB>(S, st, r, pk, rng, Lr);
+    bool nan = false;
+#pragma unroll
+    for (int i = 0; i < NB; ++i) { L[i] = 1.f * Lr[i]; nan = nan || isnan(L[i]); }
+    bool bad = nan;
+    if (!bad) {
+        float yy = 0.f;
+        for (int i = 0; i < NB; ++i) yy += S.bandY[i] * L[i];
+        float yv = yy / S.yint;
+        bad = (yv < -1e-5) || isinf(yv);
+    }
+    if (bad) {
+#pragma unroll
+        for (int i = 0; i < NB; ++i) L[i] = 0.f;
+    }
+    return bad;
+}
+
+}  // namespace pgd

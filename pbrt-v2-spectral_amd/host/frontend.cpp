@@ -1124,44 +1124,30 @@ private:
             crop[0] = Clamp(pmin(cr->f[0], cr->f[1]), 0., 1.); crop[1] = Clamp(pmax(cr->f[0], cr->f[1]), 0., 1.);
             crop[2] = Clamp(pmin(cr->f[2], cr->f[3]), 0., 1.); crop[3] = Clamp(pmax(cr->f[2], cr->f[3]), 0., 1.);
         }
-        pbrtgpu_camera &C = out->camera;
-        C.xres = xres; C.yres = yres;
-        C.px_start = Ceil2Int(xres * crop[0]);
-        C.px_count = std::max(1, Ceil2Int(xres * crop[1]) - C.px_start);
-        C.py_start = Ceil2Int(yres * crop[2]);
-        C.py_count = std::max(1, Ceil2Int(yres * crop[3]) - C.py_start);
-        const float fw = 0.5f;   // BoxFilter default width (box.cpp:36-41); PixelFilter params ignored
-        C.sx_start = Floor2Int(C.px_start + 0.5f - fw);
-        C.sx_end = Floor2Int(C.px_start + 0.5f + C.px_count + fw);
-        C.sy_start = Floor2Int(C.py_start + 0.5f - fw);
-        C.sy_end = Floor2Int(C.py_start + 0.5f + C.py_count + fw);
-        // ---- camera (perspective.cpp:33-40, 110-147; camera.cpp:84-103)
+        // ---- camera (perspective.cpp:110-147) -- parameters kept resolution independent
         if (cameraName != "perspective") throw std::runtime_error("camera '" + cameraName + "' is not supported by this build");
         Xform c2w[2];
         for (int i = 0; i < 2; ++i) LookupCache(cameraToWorld.t[i], &c2w[i], nullptr);
         if (c2w[0] != c2w[1]) throw std::runtime_error("animated cameras are not supported yet");
-        float sopen = cameraParams.FindOneFloat("shutteropen", 0.f), sclose = cameraParams.FindOneFloat("shutterclose", 1.f);
-        if (sclose < sopen) std::swap(sopen, sclose);
-        float lensr = cameraParams.FindOneFloat("lensradius", 0.f);
-        float focald = cameraParams.FindOneFloat("focaldistance", 1e30f);
-        float frame = cameraParams.FindOneFloat("frameaspectratio", float(xres) / float(yres));
-        float screen[4];
-        if (frame > 1.f) { screen[0] = -frame; screen[1] = frame; screen[2] = -1.f; screen[3] = 1.f; }
-        else { screen[0] = -1.f; screen[1] = 1.f; screen[2] = -1.f / frame; screen[3] = 1.f / frame; }
+        CameraParams &cp = out->camParams;
+        cp.shutterOpen = cameraParams.FindOneFloat("shutteropen", 0.f);
+        cp.shutterClose = cameraParams.FindOneFloat("shutterclose", 1.f);
+        if (cp.shutterClose < cp.shutterOpen) std::swap(cp.shutterOpen, cp.shutterClose);
+        cp.lensRadius = cameraParams.FindOneFloat("lensradius", 0.f);
+        cp.focalDistance = cameraParams.FindOneFloat("focaldistance", 1e30f);
+        const Param *fa = cameraParams.Find(P_FLOAT, "frameaspectratio");
+        cp.hasFrameAspect = fa && fa->f.size();
+        cp.frameAspect = cp.hasFrameAspect ? fa->f[0] : 0.f;
         const Param *sw = cameraParams.Find(P_FLOAT, "screenwindow");
-        if (sw && sw->f.size() == 4) for (int k = 0; k < 4; ++k) screen[k] = sw->f[k];
-        float fov = cameraParams.FindOneFloat("fov", 90.);
+        cp.hasScreenWindow = sw && sw->f.size() == 4;
+        if (cp.hasScreenWindow) for (int k = 0; k < 4; ++k) cp.screenWindow[k] = sw->f[k];
+        cp.fov = cameraParams.FindOneFloat("fov", 90.);
         float halffov = cameraParams.FindOneFloat("halffov", -1.f);
-        if (halffov > 0.f) fov = 2.f * halffov;
-        Xform camToScreen = Perspective(fov, 1e-2f, 1000.f);
-        Xform screenToRaster = Scale(float(xres), float(yres), 1.f) *
-                               Scale(1.f / (screen[1] - screen[0]), 1.f / (screen[2] - screen[3]), 1.f) *
-                               Translate(V3(-screen[0], -screen[3], 0.f));
-        Xform rasterToScreen = Inverse(screenToRaster);
-        Xform rasterToCamera = Inverse(camToScreen) * rasterToScreen;
-        memcpy(C.raster_to_camera, rasterToCamera.m.m, 64);
-        memcpy(C.cam2world_m, c2w[0].m.m, 64);
-        C.lens_radius = lensr; C.focal_distance = focald; C.shutter_open = sopen; C.shutter_close = sclose;
+        if (halffov > 0.f) cp.fov = 2.f * halffov;
+        for (int k = 0; k < 4; ++k) cp.crop[k] = crop[k];
+        memcpy(cp.cam2world, c2w[0].m.m, 64);
+        cp.xres = xres; cp.yres = yres;
+        ComputeCamera(cp, xres, yres, &out->camera);
         // ---- integrator / sampler
         out->maxDepth = ov.maxdepth >= 0 ? ov.maxdepth : surfParams.FindOneInt("maxdepth", 5);
         int nsamp = ov.spp > 0 ? ov.spp : samplerParams.FindOneInt("pixelsamples", 4);
@@ -1230,6 +1216,38 @@ private:
         }
     }
 };
+
+// film extent (spectralImage.cpp:40-50, 176-185) and projective camera matrices
+// (camera.cpp:84-103, perspective.cpp:33-40) for a film resolution
+void ComputeCamera(const CameraParams &cp, int xres, int yres, pbrtgpu_camera *outc) {
+    pbrtgpu_camera &C = *outc;
+    memset(&C, 0, sizeof(C));
+    C.xres = xres; C.yres = yres;
+    C.px_start = Ceil2Int(xres * cp.crop[0]);
+    C.px_count = std::max(1, Ceil2Int(xres * cp.crop[1]) - C.px_start);
+    C.py_start = Ceil2Int(yres * cp.crop[2]);
+    C.py_count = std::max(1, Ceil2Int(yres * cp.crop[3]) - C.py_start);
+    const float fw = 0.5f;   // BoxFilter default width (box.cpp:36-41); PixelFilter params are ignored (api.cpp:857-860)
+    C.sx_start = Floor2Int(C.px_start + 0.5f - fw);
+    C.sx_end = Floor2Int(C.px_start + 0.5f + C.px_count + fw);
+    C.sy_start = Floor2Int(C.py_start + 0.5f - fw);
+    C.sy_end = Floor2Int(C.py_start + 0.5f + C.py_count + fw);
+    float frame = cp.hasFrameAspect ? cp.frameAspect : float(xres) / float(yres);
+    float screen[4];
+    if (frame > 1.f) { screen[0] = -frame; screen[1] = frame; screen[2] = -1.f; screen[3] = 1.f; }
+    else { screen[0] = -1.f; screen[1] = 1.f; screen[2] = -1.f / frame; screen[3] = 1.f / frame; }
+    if (cp.hasScreenWindow) for (int k = 0; k < 4; ++k) screen[k] = cp.screenWindow[k];
+    Xform camToScreen = Perspective(cp.fov, 1e-2f, 1000.f);
+    Xform screenToRaster = Scale(float(xres), float(yres), 1.f) *
+                           Scale(1.f / (screen[1] - screen[0]), 1.f / (screen[2] - screen[3]), 1.f) *
+                           Translate(V3(-screen[0], -screen[3], 0.f));
+    Xform rasterToScreen = Inverse(screenToRaster);
+    Xform rasterToCamera = Inverse(camToScreen) * rasterToScreen;
+    memcpy(C.raster_to_camera, rasterToCamera.m.m, 64);
+    memcpy(C.cam2world_m, cp.cam2world, 64);
+    C.lens_radius = cp.lensRadius; C.focal_distance = cp.focalDistance;
+    C.shutter_open = cp.shutterOpen; C.shutter_close = cp.shutterClose;
+}
 
 bool LoadPbrtScene(const std::string &path, const RenderOverrides &ov, HostScene *out, std::string *err) {
     try {

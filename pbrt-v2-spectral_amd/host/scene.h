@@ -17,8 +17,23 @@ struct RenderOverrides {
     uint32_t seed = 0;
 };
 
+// Resolution-independent camera description (perspective.cpp:110-147 parameters); the
+// pbrtgpu_camera block is derived from it for a given film resolution.
+struct CameraParams {
+    float fov = 90.f, lensRadius = 0.f, focalDistance = 1e30f, shutterOpen = 0.f, shutterClose = 1.f;
+    float frameAspect = 0.f;        // "frameaspectratio" if given (hasFrameAspect)
+    int hasFrameAspect = 0;
+    int hasScreenWindow = 0;
+    float screenWindow[4] = {0, 0, 0, 0};
+    float crop[4] = {0, 1, 0, 1};
+    float cam2world[16];
+    int xres = 640, yres = 480;     // film resolution the scene was built with
+};
+void ComputeCamera(const CameraParams &cp, int xres, int yres, pbrtgpu_camera *out);
+
 // Host-owned storage behind a pbrtgpu_flat_scene.
 struct HostScene {
+    CameraParams camParams;
     int nBands = 32;
     int maxDepth = 5;
     int spp = 4;

@@ -1,0 +1,33 @@
+"""tools/make_packs.py -- build scene packs (scenes/*.pack) from the reference scene files.
+
+Run in the build container (needs /root/reference).  The packs are the flattened scenes
+produced by this repository's own front end (pbrt-v2-spectral_amd/host) from the unchanged
+pbrt scene files, so the GPU box -- which has no /root/reference -- can render the config
+scenes.  Resolution / spp / maxdepth stay overridable at load time.
+"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "pbrt-v2-spectral_amd"))
+import pbrtgpu as pg  # noqa: E402
+
+REF = "/root/reference/scenes"
+# (pack name, scene file, bands, xres, yres, spp) -- SURVEY App. B overrides
+PACKS = [
+    ("killeroo-simple", "killeroo-simple.pbrt", 32, 700, 700, 256),
+]
+
+
+def main():
+    out = os.path.join(ROOT, "scenes")
+    os.makedirs(out, exist_ok=True)
+    for name, fn, bands, xr, yr, spp in PACKS:
+        s = pg.Scene.load(os.path.join(REF, fn), xres=xr, yres=yr, spp=spp, maxdepth=5, bands=bands)
+        path = os.path.join(out, name + ".pack")
+        s.save_pack(path)
+        print(name, s.info(), os.path.getsize(path))
+
+
+if __name__ == "__main__":
+    main()
