@@ -200,6 +200,10 @@ int pbrtgpu_trace_paths(pbrtgpu_ctx *ctx, const int32_t *keys, int32_t n, float 
  * prim = -1 on miss; occluded_out [n] (may be NULL). */
 int pbrtgpu_intersect(pbrtgpu_ctx *ctx, const float *rays, int32_t n, float *hits_out,
                       int32_t *occluded_out);
+/* Instrumented traversal statistics for a list of path keys (roofline model): counters_out
+ * [6] = closest-hit rays, shadow rays, BVH nodes visited, triangle tests, quadric tests,
+ * closest hits. */
+int pbrtgpu_path_stats(pbrtgpu_ctx *ctx, const int32_t *keys, int32_t n, uint64_t *counters_out);
 /* Timing of the dominant kernel for roofline reporting: average device milliseconds
  * per launch of the path kernel over the last render call, and launches. */
 int pbrtgpu_last_kernel_timing(pbrtgpu_ctx *ctx, double *avg_ms, int32_t *launches);

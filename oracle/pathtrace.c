@@ -1512,9 +1512,11 @@ static void *tworker(void *arg) {
         if (k >= t->n1) break;
         long e = k + 64 < t->n1 ? k + 64 : t->n1;
         for (long q = k; q < e; ++q) {
-            long pix = q / t->c->s->spp;
+            /* all samples of pseudo-randomly spread pixels: a representative sample of the frame */
+            long npix = (long)t->W * t->H;
+            long pix = (long)(((unsigned long long)(q / t->c->s->spp) * 2654435761ull) % (unsigned long long)npix);
             int s = (int)(q % t->c->s->spp);
-            int x = t->c->s->camera.px_start + (int)(pix % t->W), y = t->c->s->camera.py_start + (int)((pix / t->W) % t->H);
+            int x = t->c->s->camera.px_start + (int)(pix % t->W), y = t->c->s->camera.py_start + (int)(pix / t->W);
             trace_path(t->c, x, y, (uint32_t)s, L, NULL, NULL);
         }
     }

@@ -476,12 +476,15 @@ PGD_INLINE bool bbox_hit(float4 n0, float4 n1, const Ray &ray, V invDir, const i
 struct Stack {
     uint32_t *base;   // &lds[lane]
     int stride;       // threads per block
+    // work counters; only the stats kernel reads them, elsewhere they are dead and removed
+    uint32_t cRays = 0, cNodes = 0, cTris = 0, cQuads = 0, cHits = 0, cShadow = 0;
     PGD_INLINE void set(int i, uint32_t v) { base[i * stride] = v; }
     PGD_INLINE uint32_t get(int i) const { return base[i * stride]; }
 };
-PGD_INLINE bool prim_hit(const DevScene &S, int pi, const Ray &ray, float *t) {
+PGD_INLINE bool prim_hit(const DevScene &S, Stack &st, int pi, const Ray &ray, float *t) {
     const pbrtgpu_prim pr = S.prims[pi];
-    if (pr.shape_type == PBRTGPU_SHAPE_TRIANGLE) return tri_hit(S.primTri[pi], ray, t);
+    if (pr.shape_type == PBRTGPU_SHAPE_TRIANGLE) { st.cTris++; return tri_hit(S.primTri[pi], ray, t); }
+    st.cQuads++;
     float e;
     if (pr.shape_type == PBRTGPU_SHAPE_SPHERE) return sphere_intersect(S.quads[pr.shape_index], ray, t, &e, nullptr);
     return disk_intersect(S.quads[pr.shape_index], ray, t, &e, nullptr);
@@ -493,15 +496,17 @@ PGD_INLINE bool bvh_intersect(const DevScene &S, Stack &st, Ray &ray, int *hitPr
     int todo = 0;
     uint32_t nodeNum = 0;
     bool found = false;
+    st.cRays++;
     for (;;) {
         float4 n0 = S.nodes[2 * nodeNum], n1 = S.nodes[2 * nodeNum + 1];
+        st.cNodes++;
         if (bbox_hit(n0, n1, ray, invDir, neg)) {
             uint32_t off = __float_as_uint(n1.z), meta = __float_as_uint(n1.w);
             uint32_t np = meta & 0xff;
             if (np > 0) {
                 for (uint32_t i = 0; i < np; ++i) {
                     float t;
-                    if (prim_hit(S, (int)(off + i), ray, &t)) {
+                    if (prim_hit(S, st, (int)(off + i), ray, &t)) {
                         ray.maxt = t;
                         *hitPrim = (int)(off + i);
                         *hitT = t;
@@ -520,6 +525,7 @@ PGD_INLINE bool bvh_intersect(const DevScene &S, Stack &st, Ray &ray, int *hitPr
             nodeNum = st.get(--todo);
         }
     }
+    st.cHits += found ? 1u : 0u;
     return found;
 }
 PGD_INLINE bool bvh_intersectP(const DevScene &S, Stack &st, const Ray &ray) {
@@ -527,15 +533,17 @@ PGD_INLINE bool bvh_intersectP(const DevScene &S, Stack &st, const Ray &ray) {
     int neg[3] = {invDir.x < 0, invDir.y < 0, invDir.z < 0};
     int todo = 0;
     uint32_t nodeNum = 0;
+    st.cShadow++;
     for (;;) {
         float4 n0 = S.nodes[2 * nodeNum], n1 = S.nodes[2 * nodeNum + 1];
+        st.cNodes++;
         if (bbox_hit(n0, n1, ray, invDir, neg)) {
             uint32_t off = __float_as_uint(n1.z), meta = __float_as_uint(n1.w);
             uint32_t np = meta & 0xff;
             if (np > 0) {
                 for (uint32_t i = 0; i < np; ++i) {
                     float t;
-                    if (prim_hit(S, (int)(off + i), ray, &t)) return true;
+                    if (prim_hit(S, st, (int)(off + i), ray, &t)) return true;
                 }
                 if (todo == 0) break;
                 nodeNum = st.get(--todo);

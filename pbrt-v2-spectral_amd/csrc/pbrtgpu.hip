@@ -125,6 +125,27 @@ __global__ __launch_bounds__(kBlock) void k_trace_keys(DevScene S, const int3 *_
     for (int i = 0; i < NB; ++i) out[(long)k * NB + i] = L[i];
 }
 
+// instrumented variant: per-path work counters for the algorithmic-bytes model
+template <int NB>
+__global__ __launch_bounds__(kBlock) void k_stats(DevScene S, const int3 *__restrict__ keys, int n,
+                                                   unsigned long long *__restrict__ counters) {
+    extern __shared__ uint32_t lds[];
+    Stack st;
+    st.base = lds + threadIdx.x;
+    st.stride = blockDim.x;
+    int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    int3 key = keys[k];
+    float L[NB];
+    trace_path<NB>(S, st, key.x, key.y, (uint32_t)key.z, L);
+    atomicAdd(&counters[0], (unsigned long long)st.cRays);
+    atomicAdd(&counters[1], (unsigned long long)st.cShadow);
+    atomicAdd(&counters[2], (unsigned long long)st.cNodes);
+    atomicAdd(&counters[3], (unsigned long long)st.cTris);
+    atomicAdd(&counters[4], (unsigned long long)st.cQuads);
+    atomicAdd(&counters[5], (unsigned long long)st.cHits);
+}
+
 // ordered contribution lists: for target t, entries [start[t], start[t+1]) of src in order
 __global__ void k_apply(int nTargets, const int *__restrict__ tgt, const int *__restrict__ start,
                         const int *__restrict__ src, const float *__restrict__ Lsp, int nb, float *__restrict__ film) {
@@ -573,6 +594,36 @@ int pbrtgpu_trace_paths(pbrtgpu_ctx *c, const int32_t *keys, int32_t n, float *o
         case 32: return trace_impl<32>(c, keys, n, out);
         case 60: return trace_impl<60>(c, keys, n, out);
         case 30: return trace_impl<30>(c, keys, n, out);
+    }
+    return fail(PBRTGPU_E_UNSUPPORTED, "band count");
+}
+
+}  // extern "C"
+
+template <int NB>
+static int stats_impl(pbrtgpu_ctx *c, const int32_t *keys, int32_t n, uint64_t *out) {
+    HIPCHK(c->scratch[0].ensure((size_t)n * sizeof(int3)));
+    HIPCHK(c->scratch[1].ensure(64));
+    HIPCHK(hipMemcpyAsync(c->scratch[0].p, keys, (size_t)n * 12, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemsetAsync(c->scratch[1].p, 0, 64, c->stream));
+    size_t lds = (size_t)c->stackDepth * kBlock * 4;
+    hipLaunchKernelGGL(k_stats<NB>, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), lds, c->stream, c->S,
+                       (const int3 *)c->scratch[0].p, n, (unsigned long long *)c->scratch[1].p);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(out, c->scratch[1].p, 6 * 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+extern "C" {
+
+int pbrtgpu_path_stats(pbrtgpu_ctx *c, const int32_t *keys, int32_t n, uint64_t *counters_out) {
+    if (!c || !c->hasScene || !keys || !counters_out || n <= 0) return fail(PBRTGPU_E_INVALID, "bad arguments");
+    HIPCHK(hipSetDevice(c->device));
+    switch (c->nb) {
+        case 32: return stats_impl<32>(c, keys, n, counters_out);
+        case 60: return stats_impl<60>(c, keys, n, counters_out);
+        case 30: return stats_impl<30>(c, keys, n, counters_out);
     }
     return fail(PBRTGPU_E_UNSUPPORTED, "band count");
 }

@@ -110,6 +110,7 @@ def gpu_lib():
         g.pbrtgpu_film_clear.argtypes = [P]
         g.pbrtgpu_trace_paths.argtypes = [P, P, I32, P]
         g.pbrtgpu_intersect.argtypes = [P, P, I32, P, P]
+        g.pbrtgpu_path_stats.argtypes = [P, P, I32, P]
         g.pbrtgpu_last_kernel_timing.argtypes = [P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(I32)]
     return _gpu
 
@@ -119,7 +120,7 @@ def gpu_symbols():
     return ["pbrtgpu_abi_version", "pbrtgpu_device_count", "pbrtgpu_context_create",
             "pbrtgpu_context_destroy", "pbrtgpu_last_error", "pbrtgpu_scene_upload",
             "pbrtgpu_render_tiles", "pbrtgpu_film_read", "pbrtgpu_film_clear",
-            "pbrtgpu_trace_paths", "pbrtgpu_intersect", "pbrtgpu_last_kernel_timing"]
+            "pbrtgpu_trace_paths", "pbrtgpu_intersect", "pbrtgpu_path_stats", "pbrtgpu_last_kernel_timing"]
 
 
 class Scene:
@@ -250,6 +251,13 @@ class Device:
         _check(self.lib.pbrtgpu_intersect(self.ctx, rays.ctypes.data, len(rays), hits.ctypes.data,
                                           occ.ctypes.data))
         return hits, occ
+
+    def path_stats(self, keys):
+        """Traversal work counters: rays, shadow rays, nodes, triangle tests, quadric tests, hits."""
+        keys = np.ascontiguousarray(keys, dtype=np.int32).reshape(-1, 3)
+        out = np.zeros(6, dtype=np.uint64)
+        _check(self.lib.pbrtgpu_path_stats(self.ctx, keys.ctypes.data, len(keys), out.ctypes.data))
+        return dict(zip(["rays", "shadow_rays", "nodes", "tri_tests", "quad_tests", "hits"], [int(v) for v in out]))
 
     def kernel_timing(self):
         ms = ctypes.c_double()
