@@ -38,6 +38,10 @@ int pbrthost_info(pbrthost_scene *s, int64_t *info, int n);
 /* reference .dat writer; film [H][W][N] float32 (raw sums), weight [H][W] or NULL */
 int pbrthost_write_dat(const char *path, const float *film, const float *weight, int W, int H, int N);
 
+/* SampledSpectrum::FromRGB (spectrum.cpp:93-178) at the given band count (32, 60 or 30);
+ * illuminant != 0 selects SPECTRUM_ILLUMINANT.  out[bands]. */
+int pbrthost_spectrum_from_rgb(int bands, const float rgb[3], int illuminant, float *out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1301,6 +1301,13 @@ int oracle_libm_float(void) {
 }
 
 /* per-path radiance for keys [n][3] = (x, y, s) */
+/* first n outputs of MT19937 seeded with seed (RNG::Seed + RandomUInt, rng.cpp:35-100) */
+int oracle_mt_first(uint32_t seed, int n, uint32_t *out) {
+    RNG r;
+    rng_seed(&r, seed);
+    for (int i = 0; i < n; ++i) out[i] = rng_uint(&r);
+    return 0;
+}
 int oracle_trace_paths(const pbrtgpu_flat_scene *s, const int32_t *keys, int32_t n, float *out) {
     Ctx c = {s, s->n_bands};
     for (int k = 0; k < n; ++k) trace_path(&c, keys[3 * k], keys[3 * k + 1], (uint32_t)keys[3 * k + 2], out + (size_t)k * s->n_bands, NULL, NULL);

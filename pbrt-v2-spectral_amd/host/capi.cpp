@@ -111,4 +111,12 @@ int pbrthost_write_dat(const char *path, const float *film, const float *weight,
     return 0;
 }
 
+int pbrthost_spectrum_from_rgb(int bands, const float rgb[3], int illuminant, float *out) {
+    if (!rgb || !out || (bands != 32 && bands != 60 && bands != 30)) return -1;
+    SpectrumCtx ctx(bands, bands == 30 ? 400 : 395, bands == 30 ? 700 : 715);
+    Spec s = ctx.FromRGB(rgb, illuminant != 0);
+    for (int i = 0; i < bands; ++i) out[i] = s[i];
+    return 0;
+}
+
 }  // extern "C"
