@@ -31,27 +31,18 @@ import pbrtgpu as pg  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md "HBM [CDNA4]": 8 TB/s peak
 NODE_BYTES, TRI_BYTES, QUAD_BYTES = 32, 48, 176
-HIT_BYTES = 16 + 3 * (12 + 12 + 8)   # triangle record + 3 vertices (P, N, uv) fetched for shading
+RAY_BYTES, HIT_BYTES, QENTRY_BYTES = 36, 8, 4     # SoA ray record read, hit / occlusion written, queue entry
 
 
-def algorithmic_bytes_per_path(st, paths, bands):
-    """bytes the path kernel must move per camera path, from the measured
-    traversal work (nodes visited, primitive tests, shading fetches) plus the per-sample
-    radiance it writes (bands x f32)."""
-    b = (NODE_BYTES * st["nodes"] + TRI_BYTES * st["tri_tests"] + QUAD_BYTES * st["quad_tests"]
-         + HIT_BYTES * st["hits"]) / float(paths)
-    return b + 4.0 * bands
-
-
-def sample_keys(scene, n, seed=12345):
-    """Uniform random (x, y, sample) keys over the frame, for the traversal statistics."""
-    c = scene.flat.camera
-    rng = np.random.default_rng(seed)
-    k = np.empty((n, 3), dtype=np.int32)
-    k[:, 0] = rng.integers(c.px_start, c.px_start + c.px_count, n)
-    k[:, 1] = rng.integers(c.py_start, c.py_start + c.py_count, n)
-    k[:, 2] = rng.integers(0, scene.spp, n)
-    return k
+def trace_bytes(work, kernel):
+    """algorithmic bytes of a traversal kernel = every BVH node it visits
+    (32 B), every primitive it tests (48 B pre-gathered triangle, 176 B quadric record),
+    plus the ray it reads, the answer it writes and its queue entry."""
+    if kernel == "k_trace_closest":
+        return (NODE_BYTES * work["nodes_closest"] + TRI_BYTES * work["tris_closest"]
+                + QUAD_BYTES * work["quads_closest"] + (RAY_BYTES + HIT_BYTES + QENTRY_BYTES) * work["rays"])
+    return (NODE_BYTES * work["nodes_shadow"] + TRI_BYTES * work["tris_shadow"] + QUAD_BYTES * work["quads_shadow"]
+            + (RAY_BYTES + 4 + QENTRY_BYTES) * work["shadow_rays"])
 
 
 def cpu_baseline(scene, target_s):
@@ -127,13 +118,15 @@ def main():
     sync_all()
     t0 = time.perf_counter()
     paths = 0.0
-    kms, launches = 0.0, 0
+    kern = {}
     for _ in range(args.steps):
         st = step()                      # returns after the film is complete (device synced)
         paths += st[pg.STAT_PATHS]
-        ms, n = dev.kernel_timing()
-        kms += ms * n
-        launches += n
+        tm = dev.timing()
+        for k in pg.Timing.KERNELS:
+            a = kern.setdefault(k, [0.0, 0])
+            a[0] += tm[k]["ms"]
+            a[1] += tm[k]["launches"]
     elapsed = time.perf_counter() - t0
     sync_all()
     if dist is not None:
@@ -146,20 +139,36 @@ def main():
     else:
         total_paths = paths
 
-    # roofline of the dominant kernel (k_render): algorithmic bytes per launch / avg launch time
-    nstat = 1 << 18
-    stt = dev.path_stats(sample_keys(scene, nstat))
-    bpp = algorithmic_bytes_per_path(stt, nstat, scene.bands)
-    avg_ms = kms / max(launches, 1)
-    paths_per_launch = paths / max(launches, 1)
-    achieved = bpp * paths_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
-    traffic = None
-    tf = os.path.join(ROOT, "profiles", "hbm_traffic_k_render.json")
-    if os.path.exists(tf):
-        with open(tf) as f:
-            tr = json.load(f)
-        if tr.get("res") == args.res and tr.get("spp_per_launch") == round(paths_per_launch / (args.res * args.res)):
-            traffic = tr.get("hbm_bytes_per_launch")
+    # roofline of the dominant kernel: algorithmic bytes (from one instrumented, untimed
+    # render of the same frame) / its device time (HIP events around every launch)
+    dom = max(("k_trace_closest", "k_trace_shadow", "k_shade"), key=lambda k: kern[k][0])
+    dev.render(tiles=tiles, tile=(args.tile, args.tile), count_work=True)
+    work = dev.timing()["work"]
+    frame_paths = paths / args.steps
+    roof = None
+    if dom in ("k_trace_closest", "k_trace_shadow"):
+        byts = trace_bytes(work, dom)                     # per frame
+        sec = kern[dom][0] / args.steps * 1e-3            # per frame
+        achieved = byts / sec / 1e9
+        launches = kern[dom][1] / args.steps
+        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "kernel": dom,
+                "avg_launch_ms": round(kern[dom][0] / max(kern[dom][1], 1), 4),
+                "launches_per_step": launches, "alg_bytes_per_launch": round(byts / max(launches, 1)),
+                "per_path": {k: round(v / frame_paths, 3) for k, v in work.items()},
+                "kernel_ms_per_step": {k: round(v[0] / args.steps, 2) for k, v in kern.items()}}
+        tf = os.path.join(ROOT, "profiles", "hbm_traffic.json")
+        if os.path.exists(tf):
+            with open(tf) as f:
+                tr = json.load(f)
+            ent = tr.get(dom)
+            if ent and ent.get("res") == args.res and ent.get("spp") == args.spp:
+                roof["traffic"] = ent.get("hbm_bytes_per_launch")
+                roof["traffic_source"] = tr.get("source")
+    else:
+        roof = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
+                "traffic": None, "kernel": dom,
+                "kernel_ms_per_step": {k: round(v[0] / args.steps, 2) for k, v in kern.items()}}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -178,11 +187,7 @@ def main():
                        % (scene.bands, info["maxdepth"], scene.spp, scene.width, scene.height),
                        "paths_per_step_per_gpu": int(paths / args.steps), "shard": args.shard,
                        "parallelism": "%s x%d" % ("frames" if args.shard == "frames" else "tiles", world)},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "kernel": "k_render<%d>" % scene.bands, "avg_launch_ms": round(avg_ms, 3),
-                         "launches": launches, "bytes_per_path": round(bpp, 1),
-                         "per_path": {k: round(v / nstat, 3) for k, v in stt.items()}},
+            "roofline": roof,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define PBRTGPU_ABI_VERSION 1
+#define PBRTGPU_ABI_VERSION 2
 #define PBRTGPU_MAX_BANDS 64
 
 #define PBRTGPU_E_INVALID   (-1)
@@ -163,14 +163,16 @@ typedef struct pbrtgpu_render_desc {
 } pbrtgpu_render_desc;
 
 #define PBRTGPU_F_ACCUMULATE 1    /* add into the context film instead of clearing it */
+#define PBRTGPU_F_COUNT_WORK 2    /* instrumented traversal kernels: fill pbrtgpu_timing.work */
 
 /* stats_out layout (doubles) */
 enum {
     PBRTGPU_STAT_PATHS = 0,       /* camera paths traced */
-    PBRTGPU_STAT_KERNEL_MS = 1,   /* device time of the path kernel(s) */
+    PBRTGPU_STAT_KERNEL_MS = 1,   /* device time of the path kernels (trace + shade) */
     PBRTGPU_STAT_ACCUM_MS = 2,    /* device time of the film accumulation */
     PBRTGPU_STAT_ZEROED = 3,      /* samples zeroed by the NaN/negative/inf guard */
     PBRTGPU_STAT_SPILLS = 4,      /* exact-boundary samples added to neighbour pixels */
+    PBRTGPU_STAT_PASSES = 5,      /* wavefront passes */
     PBRTGPU_STAT_COUNT = 8
 };
 
@@ -204,9 +206,19 @@ int pbrtgpu_intersect(pbrtgpu_ctx *ctx, const float *rays, int32_t n, float *hit
  * [6] = closest-hit rays, shadow rays, BVH nodes visited, triangle tests, quadric tests,
  * closest hits. */
 int pbrtgpu_path_stats(pbrtgpu_ctx *ctx, const int32_t *keys, int32_t n, uint64_t *counters_out);
-/* Timing of the dominant kernel for roofline reporting: average device milliseconds
- * per launch of the path kernel over the last render call, and launches. */
-int pbrtgpu_last_kernel_timing(pbrtgpu_ctx *ctx, double *avg_ms, int32_t *launches);
+/* Per-kernel device time of the last render / trace call (HIP events on the context's
+ * stream), for roofline reporting.  Index: 0 closest-hit trace, 1 shadow trace, 2 shade
+ * (+ path regeneration), 3 film accumulation.  work[] (with PBRTGPU_F_COUNT_WORK, or after
+ * pbrtgpu_path_stats): closest rays, shadow rays, BVH nodes visited by closest rays, by
+ * shadow rays, triangle tests by closest rays, by shadow rays, quadric tests by closest
+ * rays, by shadow rays, closest hits, 0, 0, 0. */
+typedef struct pbrtgpu_timing {
+    double ms[4];
+    int32_t launches[4];
+    int32_t passes, pad;
+    uint64_t work[12];
+} pbrtgpu_timing;
+int pbrtgpu_last_timing(pbrtgpu_ctx *ctx, pbrtgpu_timing *out);
 
 #ifdef __cplusplus
 }

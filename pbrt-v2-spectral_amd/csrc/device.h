@@ -25,13 +25,14 @@ static constexpr float kInvPi = 0.31830988618379067154f;
 static constexpr float kInvTwoPi = 0.15915494309189533577f;
 static constexpr float kOneMinusEps = 0x1.fffffep-1f;
 
-PGD_INLINE float SINF(float x) { return (float)sin((double)x); }
-PGD_INLINE float COSF(float x) { return (float)cos((double)x); }
-PGD_INLINE float POWF(float x, float y) { return (float)pow((double)x, (double)y); }
-PGD_INLINE float ACOSF(float x) { return (float)acos((double)x); }
-PGD_INLINE float ATAN2F(float y, float x) { return (float)atan2((double)y, (double)x); }
-PGD_INLINE float TANF(float x) { return (float)tan((double)x); }
-PGD_INLINE float ATANF(float x) { return (float)atan((double)x); }
+#define PGD_MATHFN __device__ __attribute__((noinline))
+PGD_MATHFN float SINF(float x) { return (float)sin((double)x); }
+PGD_MATHFN float COSF(float x) { return (float)cos((double)x); }
+PGD_MATHFN float POWF(float x, float y) { return (float)pow((double)x, (double)y); }
+PGD_MATHFN float ACOSF(float x) { return (float)acos((double)x); }
+PGD_MATHFN float ATAN2F(float y, float x) { return (float)atan2((double)y, (double)x); }
+PGD_MATHFN float TANF(float x) { return (float)tan((double)x); }
+PGD_MATHFN float ATANF(float x) { return (float)atan((double)x); }
 
 // ------------------------------------------------------------------ vectors
 struct V { float x, y, z; };
@@ -481,13 +482,18 @@ struct Stack {
     PGD_INLINE void set(int i, uint32_t v) { base[i * stride] = v; }
     PGD_INLINE uint32_t get(int i) const { return base[i * stride]; }
 };
+// quadric hit test kept out of line: its double-precision transcendentals would otherwise
+// set the register budget of every traversal loop
+__device__ __attribute__((noinline)) bool quadric_hit(const DevScene &S, int type, int idx, const Ray &ray, float *t) {
+    float e;
+    if (type == PBRTGPU_SHAPE_SPHERE) return sphere_intersect(S.quads[idx], ray, t, &e, nullptr);
+    return disk_intersect(S.quads[idx], ray, t, &e, nullptr);
+}
 PGD_INLINE bool prim_hit(const DevScene &S, Stack &st, int pi, const Ray &ray, float *t) {
     const pbrtgpu_prim pr = S.prims[pi];
     if (pr.shape_type == PBRTGPU_SHAPE_TRIANGLE) { st.cTris++; return tri_hit(S.primTri[pi], ray, t); }
     st.cQuads++;
-    float e;
-    if (pr.shape_type == PBRTGPU_SHAPE_SPHERE) return sphere_intersect(S.quads[pr.shape_index], ray, t, &e, nullptr);
-    return disk_intersect(S.quads[pr.shape_index], ray, t, &e, nullptr);
+    return quadric_hit(S, pr.shape_type, pr.shape_index, ray, t);
 }
 // BVHAccel::Intersect (bvh.cpp:380-432): ray.maxt shrinks on every accepted hit
 PGD_INLINE bool bvh_intersect(const DevScene &S, Stack &st, Ray &ray, int *hitPrim, float *hitT) {
@@ -572,7 +578,7 @@ PGD_INLINE void isect_fill(const DevScene &S, const Ray &ray, int prim, float t,
 // ------------------------------------------------------------------ BSDF
 enum { BSDF_REFLECTION = 1, BSDF_TRANSMISSION = 2, BSDF_DIFFUSE = 4, BSDF_GLOSSY = 8, BSDF_SPECULAR = 16, BSDF_ALL = 31 };
 enum { BX_LAMBERT, BX_OREN, BX_MICRO_BLINN_DIEL, BX_SPEC_REFL_NOOP, BX_FRESNEL_BLEND_ANISO };
-struct BxDF { int kind, type; const float *R, *R2; float a, b; };
+struct BxDF { int kind, type; int R, R2; float a, b; };   // R, R2: offsets into DevScene::spectra
 struct BSDF { V nn, ng, sn, tn; int n; BxDF bx[2]; };
 PGD_INLINE bool matches(const BxDF &b, int flags) { return (b.type & flags) == b.type; }
 PGD_INLINE V to_local(const BSDF &b, V v) { return v3(vdot(v, b.sn), vdot(v, b.tn), vdot(v, b.nn)); }
@@ -669,14 +675,57 @@ PGD_INLINE void aniso_sample(float ex, float ey, V wo, V *wi, float u1, float u2
     *pdf = p;
 }
 
-// BxDF::f accumulated band-wise: out[i] += f_i(wo, wi)
-template <int NB>
-PGD_INLINE void bx_f_add(const BxDF &b, V wo, V wi, float (&out)[NB]) {
-    switch (b.kind) {
-        case BX_LAMBERT:
+// A BSDF value is a spectrum f_i(wo, wi).  Instead of materialising it as a float[NB]
+// array, evaluation produces the per-direction scalars once (FTerm) and the spectrum is
+// evaluated band by band where it is consumed (fval).  fval reproduces the reference's
+// accumulation exactly: f = 0; for each matching BxDF: f += term_i  (reflection.cpp:
+// 478-512), with every term's operand order as in BxDF::f (reflection.cpp, microfacet.h).
+enum { T_ZERO = 0, T_LAMB, T_OREN, T_BLINN, T_FB };
+struct FTerm { int kind; int R, R2; float s0, s1, s2, s3; };
+enum { FV_SUM = 0, FV_SPEC = 1 };
+struct FVal { int mode, n; FTerm t[2]; float d; int R; };   // FV_SUM with n == 0: zero spectrum
+
+PGD_INLINE float term_eval(const float *sp, const FTerm &t, int i) {
+    switch (t.kind) {
+        case T_LAMB: return sp[t.R + i] * kInvPi;                                    // Lambertian::f
+        case T_OREN: return (sp[t.R + i] * kInvPi) * t.s0;                           // OrenNayar::f
+        case T_BLINN: return (((sp[t.R + i] * t.s0) * t.s1) * t.s2) / t.s3;          // Microfacet::f (D, G, F, den)
+        case T_FB: {                                                                 // FresnelBlend::f
+            const float cd = (28.f / (23.f * kPi));
+            float r = sp[t.R + i], r2 = sp[t.R2 + i];
+            float diffuse = ((((cd * r) * (1.f - r2)) * t.s0) * t.s1);
+            float schlick = r2 + t.s2 * (1.f - r2);
+            return diffuse + t.s3 * schlick;
+        }
+        default: return 0.f;
+    }
+}
+PGD_INLINE float fval(const float *sp, const FVal &F, int i) {
+    if (F.mode == FV_SPEC) return (1.f * sp[F.R + i]) / F.d;                          // SpecularReflection
+    float v = 0.f;
 #pragma unroll
-            for (int i = 0; i < NB; ++i) out[i] += b.R[i] * kInvPi;
-            break;
+    for (int k = 0; k < 2; ++k)
+        if (k < F.n) v += term_eval(sp, F.t[k], i);
+    return v;
+}
+PGD_INLINE bool fval_black(const float *sp, const FVal &F, int nb) {
+    if (F.mode == FV_SUM && F.n == 0) return true;
+    bool black = true;
+    for (int i = 0; i < nb; ++i) black = black && (fval(sp, F, i) == 0.);
+    return black;
+}
+PGD_INLINE void fval_zero(FVal &F) { F.mode = FV_SUM; F.n = 0; }
+PGD_INLINE void fval_push(FVal &F, const FTerm &t) {   // static indices only (no scratch)
+    if (F.n == 0) F.t[0] = t; else F.t[1] = t;
+    F.n++;
+}
+
+// BxDF::f(wo, wi) as a term (scalars per direction pair)
+PGD_INLINE FTerm bx_term(const BxDF &b, V wo, V wi) {
+    FTerm t;
+    t.kind = T_ZERO; t.R = b.R; t.R2 = b.R2; t.s0 = t.s1 = t.s2 = t.s3 = 0.f;
+    switch (b.kind) {
+        case BX_LAMBERT: t.kind = T_LAMB; break;
         case BX_OREN: {
             float sinthetai = sinth(wi), sinthetao = sinth(wo);
             float maxcos = 0.f;
@@ -688,56 +737,40 @@ PGD_INLINE void bx_f_add(const BxDF &b, V wo, V wi, float (&out)[NB]) {
             float sinalpha, tanbeta;
             if (abscos(wi) > abscos(wo)) { sinalpha = sinthetao; tanbeta = sinthetai / abscos(wi); }
             else { sinalpha = sinthetai; tanbeta = sinthetao / abscos(wo); }
-            float s = (b.a + b.b * maxcos * sinalpha * tanbeta);
-#pragma unroll
-            for (int i = 0; i < NB; ++i) out[i] += (b.R[i] * kInvPi) * s;
+            t.kind = T_OREN;
+            t.s0 = (b.a + b.b * maxcos * sinalpha * tanbeta);
             break;
         }
         case BX_MICRO_BLINN_DIEL: {
             float cosThetaO = abscos(wo), cosThetaI = abscos(wi);
-            bool zero = (cosThetaI == 0.f || cosThetaO == 0.f);
+            if (cosThetaI == 0.f || cosThetaO == 0.f) break;
             V wh = vadd(wi, wo);
-            zero = zero || (wh.x == 0. && wh.y == 0. && wh.z == 0.);
-            if (zero) {
-#pragma unroll
-                for (int i = 0; i < NB; ++i) out[i] += 0.f;
-                break;
-            }
+            if (wh.x == 0. && wh.y == 0. && wh.z == 0.) break;
             wh = vnorm(wh);
             float cosThetaH = vdot(wi, wh);
-            float F = fr_dielectric(cosThetaH, 1.5f, 1.f);
-            float D = blinn_D(b.a, wh), G = micro_G(wo, wi, wh);
-            float den = 4.f * cosThetaI * cosThetaO;
-#pragma unroll
-            for (int i = 0; i < NB; ++i) out[i] += (((b.R[i] * D) * G) * F) / den;
+            t.kind = T_BLINN;
+            t.s2 = fr_dielectric(cosThetaH, 1.5f, 1.f);
+            t.s0 = blinn_D(b.a, wh);
+            t.s1 = micro_G(wo, wi, wh);
+            t.s3 = 4.f * cosThetaI * cosThetaO;
             break;
         }
-        case BX_SPEC_REFL_NOOP:
-#pragma unroll
-            for (int i = 0; i < NB; ++i) out[i] += 0.f;
-            break;
         case BX_FRESNEL_BLEND_ANISO: {
-            float cd = (28.f / (23.f * kPi));
             float ta = (1.f - POWF(1.f - .5f * abscos(wi), 5)), tb = (1.f - POWF(1.f - .5f * abscos(wo), 5));
             V wh = vadd(wi, wo);
-            if (wh.x == 0. && wh.y == 0. && wh.z == 0.) {
-#pragma unroll
-                for (int i = 0; i < NB; ++i) out[i] += 0.f;
-                break;
-            }
+            if (wh.x == 0. && wh.y == 0. && wh.z == 0.) break;
             wh = vnorm(wh);
             float D = aniso_D(b.a, b.b, wh);
             float den = (4.f * fabsf(vdot(wi, wh)) * pmax(abscos(wi), abscos(wo)));
-            float schl = POWF(1 - vdot(wi, wh), 5.f);
-#pragma unroll
-            for (int i = 0; i < NB; ++i) {
-                float diffuse = ((((cd * b.R[i]) * (1.f - b.R2[i])) * ta) * tb);
-                float schlick = b.R2[i] + schl * (1.f - b.R2[i]);
-                out[i] += diffuse + (D / den) * schlick;
-            }
+            t.kind = T_FB;
+            t.s0 = ta; t.s1 = tb;
+            t.s2 = POWF(1 - vdot(wi, wh), 5.f);
+            t.s3 = D / den;
             break;
         }
+        default: break;   // SpecularReflection::f == 0
     }
+    return t;
 }
 PGD_INLINE float bx_pdf(const BxDF &b, V wo, V wi) {
     switch (b.kind) {
@@ -749,24 +782,20 @@ PGD_INLINE float bx_pdf(const BxDF &b, V wo, V wi) {
         default: return samehemi(wo, wi) ? abscos(wi) * kInvPi : 0.f;
     }
 }
-template <int NB>
-PGD_INLINE void bx_sample_f(const BxDF &b, V wo, V *wi, float u1, float u2, float *pdf, float (&f)[NB]) {
-#pragma unroll
-    for (int i = 0; i < NB; ++i) f[i] = 0.f;
+// BxDF::Sample_f: direction + pdf; f as a one-term sum (or the specular spectrum)
+PGD_INLINE void bx_sample_f(const BxDF &b, V wo, V *wi, float u1, float u2, float *pdf, FVal &F) {
+    fval_zero(F);
     switch (b.kind) {
         case BX_MICRO_BLINN_DIEL:
             blinn_sample(b.a, wo, wi, u1, u2, pdf);
             if (!samehemi(wo, *wi)) return;
-            bx_f_add<NB>(b, wo, *wi, f);
+            F.n = 1; F.t[0] = bx_term(b, wo, *wi);
             return;
-        case BX_SPEC_REFL_NOOP: {
+        case BX_SPEC_REFL_NOOP:
             *wi = v3(-wo.x, -wo.y, wo.z);
             *pdf = 1.f;
-            float d = abscos(*wi);
-#pragma unroll
-            for (int i = 0; i < NB; ++i) f[i] = (1.f * b.R[i]) / d;
+            F.mode = FV_SPEC; F.R = b.R; F.d = abscos(*wi);
             return;
-        }
         case BX_FRESNEL_BLEND_ANISO:
             if (u1 < .5) {
                 u1 = 2.f * u1;
@@ -778,82 +807,77 @@ PGD_INLINE void bx_sample_f(const BxDF &b, V wo, V *wi, float u1, float u2, floa
                 if (!samehemi(wo, *wi)) return;
             }
             *pdf = bx_pdf(b, wo, *wi);
-            bx_f_add<NB>(b, wo, *wi, f);
+            F.n = 1; F.t[0] = bx_term(b, wo, *wi);
             return;
         default:
             *wi = cosine_hemisphere(u1, u2);
             if (wo.z < 0.) wi->z *= -1.f;
             *pdf = bx_pdf(b, wo, *wi);
-            bx_f_add<NB>(b, wo, *wi, f);
+            F.n = 1; F.t[0] = bx_term(b, wo, *wi);
             return;
     }
 }
-template <int NB>
-PGD_INLINE void bsdf_f(const BSDF &bs, V woW, V wiW, int flags, float (&f)[NB]) {
+// BSDF::f (reflection.cpp:478-494)
+PGD_INLINE void bsdf_f(const BSDF &bs, V woW, V wiW, int flags, FVal &F) {
     V wi = to_local(bs, wiW), wo = to_local(bs, woW);
     if (vdot(wiW, bs.ng) * vdot(woW, bs.ng) > 0) flags &= ~BSDF_TRANSMISSION;
     else flags &= ~BSDF_REFLECTION;
+    fval_zero(F);
 #pragma unroll
-    for (int i = 0; i < NB; ++i) f[i] = 0.f;
-    for (int k = 0; k < bs.n; ++k)
-        if (matches(bs.bx[k], flags)) bx_f_add<NB>(bs.bx[k], wo, wi, f);
+    for (int k = 0; k < 2; ++k)
+        if (k < bs.n && matches(bs.bx[k], flags)) fval_push(F, bx_term(bs.bx[k], wo, wi));
 }
 PGD_INLINE float bsdf_pdf(const BSDF &bs, V woW, V wiW, int flags) {
     if (bs.n == 0.) return 0.;
     V wo = to_local(bs, woW), wi = to_local(bs, wiW);
     float pdf = 0.f;
     int m = 0;
-    for (int k = 0; k < bs.n; ++k)
-        if (matches(bs.bx[k], flags)) { ++m; pdf += bx_pdf(bs.bx[k], wo, wi); }
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+        if (k < bs.n && matches(bs.bx[k], flags)) { ++m; pdf += bx_pdf(bs.bx[k], wo, wi); }
     return m > 0 ? pdf / m : 0.f;
 }
-template <int NB>
+// BSDF::Sample_f (reflection.cpp:514-568)
 PGD_INLINE void bsdf_sample_f(const BSDF &bs, V woW, V *wiW, float u0, float u1, float uc, float *pdf, int flags,
-                              int *sampledType, float (&f)[NB]) {
+                              int *sampledType, FVal &F) {
     int matching = 0;
-    for (int k = 0; k < bs.n; ++k) if (matches(bs.bx[k], flags)) ++matching;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) if (k < bs.n && matches(bs.bx[k], flags)) ++matching;
     if (matching == 0) {
         *pdf = 0.f; *sampledType = 0;
-#pragma unroll
-        for (int i = 0; i < NB; ++i) f[i] = 0.f;
+        fval_zero(F);
         return;
     }
     int which = (int)floorf(uc * matching);
     if (which > matching - 1) which = matching - 1;
     int sel = -1, count = which;
-    for (int k = 0; k < bs.n; ++k)
-        if (matches(bs.bx[k], flags) && count-- == 0) { sel = k; break; }
-    const BxDF &bx = bs.bx[sel];
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+        if (sel < 0 && k < bs.n && matches(bs.bx[k], flags) && count-- == 0) sel = k;
+    const BxDF bx = sel == 0 ? bs.bx[0] : bs.bx[1];
     V wo = to_local(bs, woW), wi;
     *pdf = 0.f;
-    bx_sample_f<NB>(bx, wo, &wi, u0, u1, pdf, f);
+    bx_sample_f(bx, wo, &wi, u0, u1, pdf, F);
     if (*pdf == 0.f) {
         *sampledType = 0;
-#pragma unroll
-        for (int i = 0; i < NB; ++i) f[i] = 0.f;
+        fval_zero(F);
         return;
     }
     *sampledType = bx.type;
     *wiW = to_world(bs, wi);
     if (!(bx.type & BSDF_SPECULAR) && matching > 1)
-        for (int k = 0; k < bs.n; ++k)
-            if (k != sel && matches(bs.bx[k], flags)) *pdf += bx_pdf(bs.bx[k], wo, wi);
+#pragma unroll
+        for (int k = 0; k < 2; ++k)
+            if (k < bs.n && k != sel && matches(bs.bx[k], flags)) *pdf += bx_pdf(bs.bx[k], wo, wi);
     if (matching > 1) *pdf /= matching;
     if (!(bx.type & BSDF_SPECULAR)) {
-#pragma unroll
-        for (int i = 0; i < NB; ++i) f[i] = 0.f;
+        fval_zero(F);
         if (vdot(*wiW, bs.ng) * vdot(woW, bs.ng) > 0) flags &= ~BSDF_TRANSMISSION;
         else flags &= ~BSDF_REFLECTION;
-        for (int k = 0; k < bs.n; ++k)
-            if (matches(bs.bx[k], flags)) bx_f_add<NB>(bs.bx[k], wo, wi, f);
-    }
-}
-template <int NB>
-PGD_INLINE bool spec_black(const float (&v)[NB]) {
-    bool black = true;
 #pragma unroll
-    for (int i = 0; i < NB; ++i) black = black && (v[i] == 0.);
-    return black;
+        for (int k = 0; k < 2; ++k)
+            if (k < bs.n && matches(bs.bx[k], flags)) fval_push(F, bx_term(bs.bx[k], wo, wi));
+    }
 }
 
 // Intersection::GetBSDF -> GetShadingGeometry -> Material::GetBSDF (+ Bump, material.cpp:39-81)
@@ -889,7 +913,7 @@ PGD_INLINE void get_bsdf(const DevScene &S, const Isect &is, BSDF &bs, V *pOut, 
     switch (mt.type) {
         case PBRTGPU_MAT_MATTE: {
             BxDF &x = bs.bx[bs.n++];
-            x.R = sp + mt.spec[0]; x.R2 = x.R;
+            x.R = mt.spec[0]; x.R2 = x.R;
             x.type = BSDF_REFLECTION | BSDF_DIFFUSE;
             float sig = mt.f[0];
             if (sig == 0.) { x.kind = BX_LAMBERT; x.a = x.b = 0.f; }
@@ -904,10 +928,10 @@ PGD_INLINE void get_bsdf(const DevScene &S, const Isect &is, BSDF &bs, V *pOut, 
         }
         case PBRTGPU_MAT_PLASTIC: {
             BxDF &x0 = bs.bx[bs.n++];
-            x0.kind = BX_LAMBERT; x0.type = BSDF_REFLECTION | BSDF_DIFFUSE; x0.R = sp + mt.spec[0]; x0.R2 = x0.R;
+            x0.kind = BX_LAMBERT; x0.type = BSDF_REFLECTION | BSDF_DIFFUSE; x0.R = mt.spec[0]; x0.R2 = x0.R;
             x0.a = x0.b = 0.f;
             BxDF &x1 = bs.bx[bs.n++];
-            x1.kind = BX_MICRO_BLINN_DIEL; x1.type = BSDF_REFLECTION | BSDF_GLOSSY; x1.R = sp + mt.spec[1]; x1.R2 = x1.R;
+            x1.kind = BX_MICRO_BLINN_DIEL; x1.type = BSDF_REFLECTION | BSDF_GLOSSY; x1.R = mt.spec[1]; x1.R2 = x1.R;
             float e = 1.f / mt.f[0];
             if (e > 10000.f || isnan(e)) e = 10000.f;
             x1.a = e; x1.b = 0.f;
@@ -918,7 +942,7 @@ PGD_INLINE void get_bsdf(const DevScene &S, const Isect &is, BSDF &bs, V *pOut, 
             for (int i = 0; i < S.nb; ++i) black = black && (sp[mt.spec[0] + i] == 0.);
             if (!black) {
                 BxDF &x = bs.bx[bs.n++];
-                x.kind = BX_SPEC_REFL_NOOP; x.type = BSDF_REFLECTION | BSDF_SPECULAR; x.R = sp + mt.spec[0]; x.R2 = x.R;
+                x.kind = BX_SPEC_REFL_NOOP; x.type = BSDF_REFLECTION | BSDF_SPECULAR; x.R = mt.spec[0]; x.R2 = x.R;
                 x.a = x.b = 0.f;
             }
             break;
@@ -926,7 +950,7 @@ PGD_INLINE void get_bsdf(const DevScene &S, const Isect &is, BSDF &bs, V *pOut, 
         case PBRTGPU_MAT_SUBSTRATE: {
             BxDF &x = bs.bx[bs.n++];
             x.kind = BX_FRESNEL_BLEND_ANISO; x.type = BSDF_REFLECTION | BSDF_GLOSSY;
-            x.R = sp + mt.spec[0]; x.R2 = sp + mt.spec[1];
+            x.R = mt.spec[0]; x.R2 = mt.spec[1];
             float ex = 1.f / mt.f[0], ey = 1.f / mt.f[1];
             if (ex > 10000.f || isnan(ex)) ex = 10000.f;
             if (ey > 10000.f || isnan(ey)) ey = 10000.f;
@@ -1063,178 +1087,6 @@ PGD_INLINE float light_pdf(const DevScene &S, const pbrtgpu_light &L, V p, V wi)
     return pp / L.sum_area;
 }
 
-// ------------------------------------------------------------------ integrator
-struct PathKey { uint32_t hp, s, spp; };
-
-// EstimateDirect (integrator.cpp:109-166) and PathIntegrator::Li (path.cpp:44-115)
-template <int NB>
-PGD_INLINE void radiance(const DevScene &S, Stack &st, Ray ray, const PathKey &pk, MT &rng, float (&Lout)[NB]) {
-    float L[NB], beta[NB], f[NB], Ld[NB], fB[NB];
-#pragma unroll
-    for (int i = 0; i < NB; ++i) { L[i] = 0.f; beta[i] = 1.f; }
-    int hp_;
-    float ht_;
-    if (!bvh_intersect(S, st, ray, &hp_, &ht_)) {
-#pragma unroll
-        for (int i = 0; i < NB; ++i) Lout[i] = (1.f * 0.f) + 0.f;
-        return;
-    }
-    Isect is;
-    isect_fill(S, ray, hp_, ht_, is);
-    bool specularBounce = false;
-    const int nLights = S.nLights;
-    for (int bounces = 0;; ++bounces) {
-        if (bounces == 0 || specularBounce) {
-            int al = S.prims[is.prim].area_light;
-            if (al >= 0 && vdot(is.dg.nn, vneg(ray.d)) > 0.f) {
-                const float *Ls = S.spectra + S.lights[al].spec;
-#pragma unroll
-                for (int i = 0; i < NB; ++i) L[i] += beta[i] * Ls[i];
-            } else {
-#pragma unroll
-                for (int i = 0; i < NB; ++i) L[i] += beta[i] * 0.f;
-            }
-        }
-        BSDF bs;
-        V p, n;
-        get_bsdf(S, is, bs, &p, &n);
-        V wo = vneg(ray.d);
-        if (nLights > 0) {
-            float ul[3], ub[3], ulnum;
-            if (bounces < 3) {
-                float u2[2];
-                ulnum = s1d(pk.hp, DIM_1D(4 * bounces + 1), pk.s, pk.spp);
-                s2d(pk.hp, DIM_2D(3 * bounces + 0), pk.s, pk.spp, u2); ul[0] = u2[0]; ul[1] = u2[1];
-                ul[2] = s1d(pk.hp, DIM_1D(4 * bounces + 0), pk.s, pk.spp);
-                s2d(pk.hp, DIM_2D(3 * bounces + 1), pk.s, pk.spp, u2); ub[0] = u2[0]; ub[1] = u2[1];
-                ub[2] = s1d(pk.hp, DIM_1D(4 * bounces + 2), pk.s, pk.spp);
-            } else {
-                ulnum = mt_float(rng);
-                ul[0] = mt_float(rng); ul[1] = mt_float(rng); ul[2] = mt_float(rng);
-                ub[0] = mt_float(rng); ub[1] = mt_float(rng); ub[2] = mt_float(rng);
-            }
-            int lightNum = (int)floorf(ulnum * nLights);
-            if (lightNum > nLights - 1) lightNum = nLights - 1;
-            const pbrtgpu_light &Lt = S.lights[lightNum];
-            const float *Ls = S.spectra + Lt.spec;
-            const int flags = BSDF_ALL & ~BSDF_SPECULAR;
-#pragma unroll
-            for (int i = 0; i < NB; ++i) Ld[i] = 0.f;
-            // ---- light sample
-            V wi;
-            float lightPdf, bsdfPdf;
-            Seg vis;
-            bool lit, isPoint;
-            float lscale = light_sample_L(S, Lt, p, is.rayEps, ul, &wi, &lightPdf, &vis, &lit, &isPoint);
-            // Li = Ls (area, lit) | 0 (area, unlit) | Ls / d2 (point)
-            bool liBlack = isPoint ? false : !lit;
-            if (isPoint) {
-                bool allz = true;
-                for (int i = 0; i < NB; ++i) allz = allz && ((Ls[i] / lscale) == 0.);
-                liBlack = allz;
-            } else if (lit) liBlack = Lt.is_black != 0;
-            if (lightPdf > 0. && !liBlack) {
-                bsdf_f<NB>(bs, wo, wi, flags, f);
-                if (!spec_black<NB>(f)) {
-                    Ray sr; sr.o = vis.o; sr.d = vis.d; sr.mint = vis.mint; sr.maxt = vis.maxt; sr.time = ray.time;
-                    if (!bvh_intersectP(S, st, sr)) {
-                        if (isPoint) {
-                            float s = fabsf(vdot(wi, n)) / lightPdf;
-#pragma unroll
-                            for (int i = 0; i < NB; ++i) Ld[i] += (f[i] * (Ls[i] / lscale)) * s;
-                        } else {
-                            bsdfPdf = bsdf_pdf(bs, wo, wi, flags);
-                            float weight = power_heuristic(lightPdf, bsdfPdf);
-                            float s = fabsf(vdot(wi, n)) * weight / lightPdf;
-#pragma unroll
-                            for (int i = 0; i < NB; ++i) Ld[i] += (f[i] * Ls[i]) * s;
-                        }
-                    }
-                }
-            }
-            // ---- BSDF sample with MIS (area lights)
-            if (!isPoint) {
-                int sampledType;
-                bsdf_sample_f<NB>(bs, wo, &wi, ub[0], ub[1], ub[2], &bsdfPdf, flags, &sampledType, fB);
-                if (!spec_black<NB>(fB) && bsdfPdf > 0.) {
-                    float weight = 1.f;
-                    bool go = true;
-                    if (!(sampledType & BSDF_SPECULAR)) {
-                        lightPdf = light_pdf(S, Lt, p, wi);
-                        if (lightPdf == 0.) go = false;
-                        else weight = power_heuristic(bsdfPdf, lightPdf);
-                    }
-                    if (go) {
-                        Ray mr; mr.o = p; mr.d = wi; mr.mint = is.rayEps; mr.maxt = INFINITY; mr.time = ray.time;
-                        int mp;
-                        float mt;
-                        bool liHit = false;
-                        if (bvh_intersect(S, st, mr, &mp, &mt)) {
-                            if (S.prims[mp].area_light == lightNum) {
-                                Isect lis;
-                                isect_fill(S, mr, mp, mt, lis);
-                                liHit = vdot(lis.dg.nn, vneg(wi)) > 0.f;
-                            }
-                        }
-                        if (liHit && !Lt.is_black) {
-                            float ad = fabsf(vdot(wi, n));
-#pragma unroll
-                            for (int i = 0; i < NB; ++i) Ld[i] += (((fB[i] * Ls[i]) * ad) * weight) / bsdfPdf;
-                        }
-                    }
-                }
-            }
-            const float nl = (float)nLights;
-#pragma unroll
-            for (int i = 0; i < NB; ++i) L[i] += beta[i] * (nl * Ld[i]);
-        } else {
-#pragma unroll
-            for (int i = 0; i < NB; ++i) L[i] += beta[i] * 0.f;
-        }
-        // ---- path continuation
-        float up[3];
-        if (bounces < 3) {
-            float u2[2];
-            s2d(pk.hp, DIM_2D(3 * bounces + 2), pk.s, pk.spp, u2); up[0] = u2[0]; up[1] = u2[1];
-            up[2] = s1d(pk.hp, DIM_1D(4 * bounces + 3), pk.s, pk.spp);
-        } else {
-            up[0] = mt_float(rng); up[1] = mt_float(rng); up[2] = mt_float(rng);
-        }
-        V wi;
-        float pdf;
-        int flags;
-        bsdf_sample_f<NB>(bs, wo, &wi, up[0], up[1], up[2], &pdf, BSDF_ALL, &flags, f);
-        if (spec_black<NB>(f) || pdf == 0.) break;
-        specularBounce = (flags & BSDF_SPECULAR) != 0;
-        float ad = fabsf(vdot(wi, n));
-#pragma unroll
-        for (int i = 0; i < NB; ++i) beta[i] *= (f[i] * ad) / pdf;
-        Ray nray; nray.o = p; nray.d = wi; nray.mint = is.rayEps; nray.maxt = INFINITY; nray.time = ray.time;
-        ray = nray;
-        if (bounces > 3) {
-            float yy = 0.f;
-            for (int i = 0; i < NB; ++i) yy += S.bandY[i] * beta[i];
-            float cp = pmin(.5f, yy / S.yint);
-            if (mt_float(rng) > cp) break;
-#pragma unroll
-            for (int i = 0; i < NB; ++i) beta[i] /= cp;
-        }
-        if (bounces == S.maxDepth) break;
-        if (!bvh_intersect(S, st, ray, &hp_, &ht_)) {
-            if (specularBounce) {
-#pragma unroll
-                for (int i = 0; i < NB; ++i) L[i] += beta[i] * 0.f;
-            }
-            break;
-        }
-        isect_fill(S, ray, hp_, ht_, is);
-#pragma unroll
-        for (int i = 0; i < NB; ++i) beta[i] *= 1.f;
-    }
-#pragma unroll
-    for (int i = 0; i < NB; ++i) Lout[i] = (1.f * L[i]) + 0.f;
-}
-
 // camera sample -> world ray (perspective.cpp:73-106)
 PGD_INLINE Ray camera_ray(const pbrtgpu_camera &cam, float imageX, float imageY, float lensU, float lensV, float timeU) {
     const float *m = cam.raster_to_camera;
@@ -1270,40 +1122,6 @@ PGD_INLINE Ray camera_ray(const pbrtgpu_camera &cam, float imageX, float imageY,
     if (wp != 1.) o.o = vdiv(o.o, wp);
     o.d = xvec(cw, r.d);
     return o;
-}
-
-// one camera path with the NaN / negative / inf guard (samplerrenderer.cpp:86-133)
-template <int NB>
-PGD_INLINE bool trace_path(const DevScene &S, Stack &st, int px, int py, uint32_t s, float (&L)[NB]) {
-    PathKey pk;
-    pk.hp = pixel_hash(S.seed, px, py);
-    pk.s = s;
-    pk.spp = (uint32_t)S.spp;
-    float u[2], lens[2];
-    s2d(pk.hp, 0, s, pk.spp, u);
-    float imageX = px + u[0], imageY = py + u[1];
-    s2d(pk.hp, 1, s, pk.spp, lens);
-    float timeU = s1d(pk.hp, 2, s, pk.spp);
-    MT rng;
-    mt_begin(rng, path_seed(pk.hp, s));
-    Ray r = camera_ray(S.cam, imageX, imageY, lens[0], lens[1], timeU);
-    float Lr[NB];
-    radiance<NB>(S, st, r, pk, rng, Lr);
-    bool nan = false;
-#pragma unroll
-    for (int i = 0; i < NB; ++i) { L[i] = 1.f * Lr[i]; nan = nan || isnan(L[i]); }
-    bool bad = nan;
-    if (!bad) {
-        float yy = 0.f;
-        for (int i = 0; i < NB; ++i) yy += S.bandY[i] * L[i];
-        float yv = yy / S.yint;
-        bad = (yv < -1e-5) || isinf(yv);
-    }
-    if (bad) {
-#pragma unroll
-        for (int i = 0; i < NB; ++i) L[i] = 0.f;
-    }
-    return bad;
 }
 
 }  // namespace pgd

@@ -6,15 +6,14 @@
 //   k_spill_scan   : every sample of the sample extent -> imageX/Y footprint; samples that
 //                    land on a film pixel of this context other than their own are queued
 //                    (integer + float sampler work only, no tracing)
-//   k_trace_keys   : traces the queued spill samples (radiance kept for the film pass)
+//   wavefront(spill keys) -> radiance of the spill samples
 //   k_apply        : adds "pre" spill contributions (sources earlier in row-major order)
-//   for each spp batch:
-//     k_render<NB> : persistent grid; one camera path per lane per item, items
-//                    (pixel, sample) interleaved with grid stride; the whole
-//                    PathIntegrator::Li bounce loop runs in registers with the BVH
-//                    traversal stack in LDS; writes L[NB] per item
+//   for each spp batch: wavefront(pixels x batch samples) -> Lbuf, then
 //     k_accum<NB>  : film[p][band] += L in sample order (one lane per (pixel, band))
 //   k_apply        : adds "post" spill contributions
+// wavefront(items): persistent SoA path slots (wavefront.h); per pass
+//   k_trace_closest (camera/continuation + MIS rays), k_trace_shadow, k_shade (+ regeneration)
+// until every item has produced its radiance.
 // The film is the reference's raw sum (spectralImage.cpp:267-296 does not normalise).
 #include <hip/hip_runtime.h>
 #include <vector>
@@ -25,6 +24,7 @@
 #include <mutex>
 #include "pbrtgpu.h"
 #include "device.h"
+#include "wavefront.h"
 
 using namespace pgd;
 
@@ -36,33 +36,116 @@ static int fail(int code, const std::string &msg) { g_err = msg; return code; }
         if (e_ != hipSuccess) return fail(-(1000 + (int)e_), std::string(#x) + ": " + hipGetErrorString(e_)); \
     } while (0)
 
-static const int kBlock = 128;
 
 // ------------------------------------------------------------------ kernels
-template <int NB>
-__global__ __launch_bounds__(kBlock) void k_render(DevScene S, const int2 *__restrict__ pix, int nPix, int s0,
-                                                    int sb, float *__restrict__ Lbuf, unsigned int *__restrict__ zeroed) {
+static const int kTraceBlock = 128;
+static const int kShadeBlock = 256;
+
+// closest-hit queries of one pass (BVHAccel::Intersect, bvh.cpp:380-432): persistent grid,
+// one ray per lane per iteration, LDS traversal stack (column per lane)
+template <bool STATS>
+__global__ __launch_bounds__(kTraceBlock) void k_trace_closest(DevScene S, PathSoA P, int q) {
     extern __shared__ uint32_t lds[];
     Stack st;
     st.base = lds + threadIdx.x;
     st.stride = blockDim.x;
-    const long nItems = (long)nPix * sb;
-    unsigned int bad = 0;
-    for (long it = (long)blockIdx.x * blockDim.x + threadIdx.x; it < nItems; it += (long)gridDim.x * blockDim.x) {
-        int p = (int)(it / sb);
-        int sl = (int)(it - (long)p * sb);
-        int2 xy = pix[p];
-        float L[NB];
-        bad += trace_path<NB>(S, st, xy.x, xy.y, (uint32_t)(s0 + sl), L) ? 1u : 0u;
-        float4 *o = reinterpret_cast<float4 *>(Lbuf + it * NB);
-#pragma unroll
-        for (int i = 0; i < NB / 4; ++i) o[i] = make_float4(L[4 * i], L[4 * i + 1], L[4 * i + 2], L[4 * i + 3]);
-        if (NB % 4) {
-#pragma unroll
-            for (int i = (NB / 4) * 4; i < NB; ++i) Lbuf[it * NB + i] = L[i];
-        }
+    const uint32_t n = P.cnt[CNT_QC(q)];
+    const uint32_t *Q = P.qC + (size_t)q * 2 * P.cap;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const uint32_t e = Q[i];
+        const int slot = (int)(e >> 1), kind = (int)(e & 1);
+        Ray r = ray_load(P, kind, slot);
+        int prim = -1;
+        float t = INFINITY;
+        if (!bvh_intersect(S, st, r, &prim, &t)) prim = -1;
+        P.hitPrim[(size_t)kind * P.cap + slot] = prim;
+        P.hitT[(size_t)kind * P.cap + slot] = t;
     }
-    if (bad) atomicAdd(zeroed, bad);
+    if (STATS) {
+        unsigned long long *w = reinterpret_cast<unsigned long long *>(P.cnt + CNT_WORK);
+        atomicAdd(&w[W_RAYS], (unsigned long long)st.cRays);
+        atomicAdd(&w[W_NODES_C], (unsigned long long)st.cNodes);
+        atomicAdd(&w[W_TRIS_C], (unsigned long long)st.cTris);
+        atomicAdd(&w[W_QUADS_C], (unsigned long long)st.cQuads);
+        atomicAdd(&w[W_HITS], (unsigned long long)st.cHits);
+    }
+}
+
+// any-hit queries of one pass (BVHAccel::IntersectP, bvh.cpp:435-481)
+template <bool STATS>
+__global__ __launch_bounds__(kTraceBlock) void k_trace_shadow(DevScene S, PathSoA P, int q) {
+    extern __shared__ uint32_t lds[];
+    Stack st;
+    st.base = lds + threadIdx.x;
+    st.stride = blockDim.x;
+    const uint32_t n = P.cnt[CNT_QS(q)];
+    const uint32_t *Q = P.qS + (size_t)q * P.cap;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const int slot = (int)Q[i];
+        Ray r = ray_load(P, RAY_S, slot);
+        P.occ[slot] = bvh_intersectP(S, st, r) ? 1u : 0u;
+    }
+    if (STATS) {
+        unsigned long long *w = reinterpret_cast<unsigned long long *>(P.cnt + CNT_WORK);
+        atomicAdd(&w[W_SHADOW], (unsigned long long)st.cShadow);
+        atomicAdd(&w[W_NODES_S], (unsigned long long)st.cNodes);
+        atomicAdd(&w[W_TRIS_S], (unsigned long long)st.cTris);
+        atomicAdd(&w[W_QUADS_S], (unsigned long long)st.cQuads);
+    }
+}
+
+// Block-wide exclusive prefix of a per-thread flag with ONE atomicAdd per block on
+// *counter; returns this thread's index (valid where flag is set).  All threads of the
+// block must call it (it contains barriers).
+__device__ __forceinline__ uint32_t block_push(bool flag, uint32_t *counter, uint32_t *lds4) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const unsigned long long m = __ballot(flag);
+    const uint32_t before = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+    if (lane == 0) lds4[wave] = (uint32_t)__popcll(m);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t tot = 0;
+        for (int w = 0; w < (int)(blockDim.x >> 6); ++w) { uint32_t v = lds4[w]; lds4[w] = tot; tot += v; }
+        lds4[15] = tot ? atomicAdd(counter, tot) : 0u;
+    }
+    __syncthreads();
+    const uint32_t idx = lds4[15] + lds4[wave] + before;
+    __syncthreads();   // lds4 is reused by the next call
+    return idx;
+}
+
+// shading pass over every slot: finish / advance live paths, regenerate free slots, and
+// queue the next pass's rays into queue set qout (block-aggregated queue pushes)
+template <int NB>
+__global__ __launch_bounds__(kShadeBlock) void k_shade(DevScene S, PathSoA P, ItemSrc src, int qout,
+                                                       float *__restrict__ Lout) {
+    __shared__ uint32_t lds4[16];
+    const int slot = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool inRange = slot < P.cap;
+    Pushes pu = {false, false, false};
+    bool freeSlot = inRange && P.item[slot] < 0;
+    bool zeroed = false;
+    if (inRange && !freeSlot) {
+        bool done;
+        pu = shade_slot<NB>(S, P, slot, Lout, &done, &zeroed);
+        if (done) { P.item[slot] = -1; freeSlot = true; }
+    }
+    if (__ballot(zeroed)) {
+        const unsigned long long m = __ballot(zeroed);
+        if ((threadIdx.x & 63) == 0) atomicAdd(&P.cnt[CNT_ZEROED], (uint32_t)__popcll(m));
+    }
+    // regeneration: free slots take the next camera samples
+    const bool want = freeSlot && *(volatile uint32_t *)&P.cnt[CNT_NEXT] < src.nItems;
+    if (__syncthreads_or(want)) {
+        const uint32_t it = block_push(want, &P.cnt[CNT_NEXT], lds4);
+        if (want && it < src.nItems) { path_start<NB>(S, P, src, slot, it); pu.c = true; }
+    }
+    const uint32_t kc = block_push(pu.c, &P.cnt[CNT_QC(qout)], lds4);
+    if (pu.c) P.qC[(size_t)qout * 2 * P.cap + kc] = (uint32_t)slot << 1;
+    const uint32_t km = block_push(pu.m, &P.cnt[CNT_QC(qout)], lds4);
+    if (pu.m) P.qC[(size_t)qout * 2 * P.cap + km] = ((uint32_t)slot << 1) | 1u;
+    const uint32_t ks = block_push(pu.s, &P.cnt[CNT_QS(qout)], lds4);
+    if (pu.s) P.qS[(size_t)qout * P.cap + ks] = (uint32_t)slot;
 }
 
 // film[filmIdx[p]][b] += L(p, s) for s in batch order (spectralImage.cpp:125-131)
@@ -109,43 +192,6 @@ __global__ void k_spill_scan(pbrtgpu_camera cam, uint32_t seed, int spp, const u
     }
 }
 
-template <int NB>
-__global__ __launch_bounds__(kBlock) void k_trace_keys(DevScene S, const int3 *__restrict__ keys, int n,
-                                                        float *__restrict__ out) {
-    extern __shared__ uint32_t lds[];
-    Stack st;
-    st.base = lds + threadIdx.x;
-    st.stride = blockDim.x;
-    int k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= n) return;
-    int3 key = keys[k];
-    float L[NB];
-    trace_path<NB>(S, st, key.x, key.y, (uint32_t)key.z, L);
-#pragma unroll
-    for (int i = 0; i < NB; ++i) out[(long)k * NB + i] = L[i];
-}
-
-// instrumented variant: per-path work counters for the algorithmic-bytes model
-template <int NB>
-__global__ __launch_bounds__(kBlock) void k_stats(DevScene S, const int3 *__restrict__ keys, int n,
-                                                   unsigned long long *__restrict__ counters) {
-    extern __shared__ uint32_t lds[];
-    Stack st;
-    st.base = lds + threadIdx.x;
-    st.stride = blockDim.x;
-    int k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= n) return;
-    int3 key = keys[k];
-    float L[NB];
-    trace_path<NB>(S, st, key.x, key.y, (uint32_t)key.z, L);
-    atomicAdd(&counters[0], (unsigned long long)st.cRays);
-    atomicAdd(&counters[1], (unsigned long long)st.cShadow);
-    atomicAdd(&counters[2], (unsigned long long)st.cNodes);
-    atomicAdd(&counters[3], (unsigned long long)st.cTris);
-    atomicAdd(&counters[4], (unsigned long long)st.cQuads);
-    atomicAdd(&counters[5], (unsigned long long)st.cHits);
-}
-
 // ordered contribution lists: for target t, entries [start[t], start[t+1]) of src in order
 __global__ void k_apply(int nTargets, const int *__restrict__ tgt, const int *__restrict__ start,
                         const int *__restrict__ src, const float *__restrict__ Lsp, int nb, float *__restrict__ film) {
@@ -157,7 +203,7 @@ __global__ void k_apply(int nTargets, const int *__restrict__ tgt, const int *__
     film[(long)tgt[q] * nb + b] = acc;
 }
 
-__global__ __launch_bounds__(kBlock) void k_intersect(DevScene S, const float *__restrict__ rays, int n,
+__global__ __launch_bounds__(kTraceBlock) void k_intersect(DevScene S, const float *__restrict__ rays, int n,
                                                        float *__restrict__ hits, int *__restrict__ occ) {
     extern __shared__ uint32_t lds[];
     Stack st;
@@ -191,19 +237,31 @@ struct DevBuf {
     void release() { if (p) (void)hipFree(p); p = nullptr; n = 0; }
 };
 
+enum { K_CLOSEST = 0, K_SHADOW = 1, K_SHADE = 2, K_ACCUM = 3, K_KINDS = 4 };
+
+struct Timing {
+    double ms[K_KINDS] = {0, 0, 0, 0};
+    int launches[K_KINDS] = {0, 0, 0, 0};
+    int passes = 0;
+    uint64_t work[W_COUNT] = {0};
+};
+
 struct pbrtgpu_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    hipEvent_t ev[8] = {};
     bool hasScene = false;
     DevScene S{};
     int nb = 0, spp = 0, stackDepth = 0;
     pbrtgpu_camera cam{};
     std::vector<DevBuf> sceneBufs;
-    DevBuf film, Lbuf, pix, filmIdx, mask, keys, counter, spillL, zeroed, lists[4], scratch[3];
+    DevBuf film, Lbuf, pix, filmIdx, mask, keys, counter, spillL, lists[4], scratch[3];
+    DevBuf slots;            // PathSoA storage
+    int slotCap = 0, slotNb = 0;
+    PathSoA P{};
+    uint32_t *hostCnt = nullptr;   // pinned mirror of the queue counters
     int numCUs = 256;
-    double lastKernelMs = 0.0;
-    int lastLaunches = 0;
+    Timing last;
 };
 
 template <class T> static hipError_t upload(pbrtgpu_ctx *c, const T *src, size_t count, const T **dst) {
@@ -215,6 +273,110 @@ template <class T> static hipError_t upload(pbrtgpu_ctx *c, const T *src, size_t
     if (count) e = hipMemcpy(b.p, src, count * sizeof(T), hipMemcpyHostToDevice);
     *dst = reinterpret_cast<const T *>(b.p);
     return e;
+}
+
+// path slots: PATH_SLOTS env override (tests use small capacities to exercise regeneration)
+static int slot_target() {
+    const char *e = getenv("PBRTGPU_SLOTS");
+    int v = e ? atoi(e) : 0;
+    return v > 0 ? v : (1 << 21);
+}
+
+static int ensure_slots(pbrtgpu_ctx *c, int cap, int NB) {
+    if (c->slotCap == cap && c->slotNb == NB) return 0;
+    const size_t C = (size_t)cap;
+    const int NBP = (NB + 3) / 4 * 4;   // bands padded to whole float4 quads
+    size_t off = 0;
+    auto take = [&](size_t bytes) { size_t o = off; off += (bytes + 255) & ~(size_t)255; return o; };
+    size_t oItem = take(C * 4), oHp = take(C * 4), oSmp = take(C * 4), oBounce = take(C * 4), oFlags = take(C * 4),
+           oMt = take(C * 20), oBeta = take(C * 2 * NBP * 4), oL = take(C * NBP * 4), oA = take(C * NBP * 4),
+           oB = take(C * NBP * 4), oRay = take(C * 27 * 4), oHitP = take(C * 8), oHitT = take(C * 8), oOcc = take(C * 4),
+           oQC = take(C * 16), oQS = take(C * 8), oCnt = take(CNT_WORDS * 4);
+    HIPCHK(c->slots.ensure(off));
+    char *base = (char *)c->slots.p;
+    PathSoA &P = c->P;
+    P.cap = cap;
+    P.item = (int *)(base + oItem); P.hp = (uint32_t *)(base + oHp); P.smp = (uint32_t *)(base + oSmp);
+    P.bounce = (int *)(base + oBounce); P.flags = (uint32_t *)(base + oFlags); P.mt = (uint32_t *)(base + oMt);
+    P.beta = (float4 *)(base + oBeta); P.L = (float4 *)(base + oL); P.A = (float4 *)(base + oA); P.B = (float4 *)(base + oB);
+    P.ray = (float *)(base + oRay); P.hitPrim = (int *)(base + oHitP); P.hitT = (float *)(base + oHitT);
+    P.occ = (uint32_t *)(base + oOcc); P.qC = (uint32_t *)(base + oQC); P.qS = (uint32_t *)(base + oQS);
+    P.cnt = (uint32_t *)(base + oCnt);
+    c->slotCap = cap;
+    c->slotNb = NB;
+    return 0;
+}
+
+// Runs every item of src through the wavefront pipeline; radiance of item i -> Lout[i][NB].
+template <int NB>
+static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool countWork, Timing &T,
+                         unsigned int *zeroedOut) {
+    if (src.nItems == 0) return 0;
+    const int cap = (int)std::min<uint32_t>(src.nItems, (uint32_t)slot_target());
+    if (int e = ensure_slots(c, cap, NB)) return e;
+    PathSoA &P = c->P;
+    HIPCHK(hipMemsetAsync(P.item, 0xff, (size_t)cap * 4, c->stream));
+    HIPCHK(hipMemsetAsync(P.cnt, 0, CNT_WORDS * 4, c->stream));
+    const size_t lds = (size_t)c->stackDepth * kTraceBlock * sizeof(uint32_t);
+    const int perCU = std::max(1, std::min(16, (int)(160 * 1024 / std::max<size_t>(lds, 1))));
+    const int traceGrid = c->numCUs * perCU;
+    const int shadeGrid = (cap + kShadeBlock - 1) / kShadeBlock;
+    int q = 0;
+    // pass 0: every slot is free -> regeneration fills them with camera rays (queue 0)
+    HIPCHK(hipEventRecord(c->ev[4], c->stream));
+    hipLaunchKernelGGL(k_shade<NB>, dim3(shadeGrid), dim3(kShadeBlock), 0, c->stream, c->S, P, src, q, Lout);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(c->ev[5], c->stream));
+    bool pending = false;   // events ev[0..3] of the previous pass still to be read
+    float m;
+    for (;;) {
+        HIPCHK(hipMemcpyAsync(c->hostCnt, P.cnt, CNT_WORK * 4, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        if (pending) {
+            HIPCHK(hipEventElapsedTime(&m, c->ev[0], c->ev[1])); T.ms[K_CLOSEST] += m;
+            HIPCHK(hipEventElapsedTime(&m, c->ev[1], c->ev[2])); T.ms[K_SHADOW] += m;
+            HIPCHK(hipEventElapsedTime(&m, c->ev[2], c->ev[3])); T.ms[K_SHADE] += m;
+        } else {
+            HIPCHK(hipEventElapsedTime(&m, c->ev[4], c->ev[5])); T.ms[K_SHADE] += m;
+            T.launches[K_SHADE]++;
+        }
+        const uint32_t nC = c->hostCnt[CNT_QC(q)], nS = c->hostCnt[CNT_QS(q)];
+        if (nC == 0 && nS == 0) break;
+        if (T.passes > 4096) return fail(PBRTGPU_E_STATE, "wavefront did not drain");
+        const int nq = q ^ 1;
+        HIPCHK(hipMemsetAsync(P.cnt + CNT_QC(nq), 0, 4, c->stream));
+        HIPCHK(hipMemsetAsync(P.cnt + CNT_QS(nq), 0, 4, c->stream));
+        HIPCHK(hipEventRecord(c->ev[0], c->stream));
+        int gC = (int)std::min<uint32_t>((nC + kTraceBlock - 1) / kTraceBlock, (uint32_t)traceGrid);
+        if (gC > 0) {
+            if (countWork) hipLaunchKernelGGL(k_trace_closest<true>, dim3(gC), dim3(kTraceBlock), lds, c->stream, c->S, P, q);
+            else hipLaunchKernelGGL(k_trace_closest<false>, dim3(gC), dim3(kTraceBlock), lds, c->stream, c->S, P, q);
+            HIPCHK(hipGetLastError());
+            T.launches[K_CLOSEST]++;
+        }
+        HIPCHK(hipEventRecord(c->ev[1], c->stream));
+        int gS = (int)std::min<uint32_t>((nS + kTraceBlock - 1) / kTraceBlock, (uint32_t)traceGrid);
+        if (gS > 0) {
+            if (countWork) hipLaunchKernelGGL(k_trace_shadow<true>, dim3(gS), dim3(kTraceBlock), lds, c->stream, c->S, P, q);
+            else hipLaunchKernelGGL(k_trace_shadow<false>, dim3(gS), dim3(kTraceBlock), lds, c->stream, c->S, P, q);
+            HIPCHK(hipGetLastError());
+            T.launches[K_SHADOW]++;
+        }
+        HIPCHK(hipEventRecord(c->ev[2], c->stream));
+        hipLaunchKernelGGL(k_shade<NB>, dim3(shadeGrid), dim3(kShadeBlock), 0, c->stream, c->S, P, src, nq, Lout);
+        HIPCHK(hipGetLastError());
+        T.launches[K_SHADE]++;
+        HIPCHK(hipEventRecord(c->ev[3], c->stream));
+        pending = true;
+        T.passes++;
+        q = nq;
+    }
+    uint64_t w[W_COUNT];
+    HIPCHK(hipMemcpy(w, P.cnt + CNT_WORK, sizeof(w), hipMemcpyDeviceToHost));
+    if (countWork)
+        for (int i = 0; i < W_COUNT; ++i) T.work[i] += w[i];
+    if (zeroedOut) *zeroedOut += c->hostCnt[CNT_ZEROED];
+    return 0;
 }
 
 extern "C" {
@@ -238,8 +400,10 @@ int pbrtgpu_context_create(int device, pbrtgpu_ctx **out) {
     c->device = device;
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->numCUs = prop.multiProcessorCount;
-    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
+    bool ok = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess;
+    for (int i = 0; i < 8 && ok; ++i) ok = hipEventCreate(&c->ev[i]) == hipSuccess;
+    ok = ok && hipHostMalloc((void **)&c->hostCnt, CNT_WORDS * 4, hipHostMallocDefault) == hipSuccess;
+    if (!ok) {
         delete c;
         return fail(PBRTGPU_E_NODEVICE, "stream/event creation failed");
     }
@@ -253,16 +417,15 @@ int pbrtgpu_context_destroy(pbrtgpu_ctx *c) {
     (void)hipStreamSynchronize(c->stream);
     for (auto &b : c->sceneBufs) b.release();
     DevBuf *bufs[] = {&c->film, &c->Lbuf, &c->pix, &c->filmIdx, &c->mask, &c->keys, &c->counter, &c->spillL,
-                      &c->zeroed, &c->lists[0], &c->lists[1], &c->lists[2], &c->lists[3], &c->scratch[0],
-                      &c->scratch[1], &c->scratch[2]};
+                      &c->lists[0], &c->lists[1], &c->lists[2], &c->lists[3], &c->scratch[0],
+                      &c->scratch[1], &c->scratch[2], &c->slots};
     for (DevBuf *b : bufs) b->release();
-    (void)hipEventDestroy(c->ev0);
-    (void)hipEventDestroy(c->ev1);
+    for (int i = 0; i < 8; ++i) if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
+    if (c->hostCnt) (void)hipHostFree(c->hostCnt);
     (void)hipStreamDestroy(c->stream);
     delete c;
     return 0;
 }
-
 int pbrtgpu_scene_upload(pbrtgpu_ctx *c, const pbrtgpu_flat_scene *s) {
     if (!c || !s) return fail(PBRTGPU_E_INVALID, "null argument");
     if (s->abi_version != PBRTGPU_ABI_VERSION) return fail(PBRTGPU_E_INVALID, "ABI version mismatch");
@@ -278,6 +441,7 @@ int pbrtgpu_scene_upload(pbrtgpu_ctx *c, const pbrtgpu_flat_scene *s) {
         if (s->materials[i].type > PBRTGPU_MAT_SUBSTRATE) return fail(PBRTGPU_E_UNSUPPORTED, "material type not yet supported on the GPU");
     HIPCHK(hipSetDevice(c->device));
     HIPCHK(hipStreamSynchronize(c->stream));
+    c->hasScene = false;
     for (auto &b : c->sceneBufs) b.release();
     c->sceneBufs.clear();
     c->sceneBufs.reserve(32);
@@ -328,6 +492,27 @@ int pbrtgpu_scene_upload(pbrtgpu_ctx *c, const pbrtgpu_flat_scene *s) {
             return fail(PBRTGPU_E_INVALID, "bad quadric index");
         pt[i] = t;
     }
+    // spectrum pool re-laid out with a stride of whole float4 quads (16-byte aligned band
+    // quads for the shading loads); every offset in the flattened scene is a multiple of
+    // n_bands (front end emits whole spectra)
+    const int nbp = (s->n_bands + 3) / 4 * 4;
+    if (s->n_spectra_floats % s->n_bands) return fail(PBRTGPU_E_INVALID, "spectrum pool is not whole spectra");
+    auto remap = [&](int32_t off, int32_t *out) -> bool {
+        if (off < 0) { *out = off; return true; }
+        if (off % s->n_bands || off >= s->n_spectra_floats) return false;
+        *out = off / s->n_bands * nbp;
+        return true;
+    };
+    std::vector<float> pool((size_t)s->n_spectra_floats / s->n_bands * nbp, 0.f);
+    for (int k = 0; k < s->n_spectra_floats / s->n_bands; ++k)
+        for (int i = 0; i < s->n_bands; ++i) pool[(size_t)k * nbp + i] = s->spectra[(size_t)k * s->n_bands + i];
+    std::vector<pbrtgpu_material> mats(s->materials, s->materials + s->n_materials);
+    for (auto &m : mats)
+        for (int k = 0; k < 4; ++k)
+            if (!remap(m.spec[k], &m.spec[k])) return fail(PBRTGPU_E_INVALID, "material spectrum offset");
+    std::vector<pbrtgpu_light> lts(s->lights, s->lights + s->n_lights);
+    for (auto &l : lts)
+        if (!remap(l.spec, &l.spec)) return fail(PBRTGPU_E_INVALID, "light spectrum offset");
     HIPCHK(upload(c, pt.data(), pt.size(), &S.primTri));
     HIPCHK(upload(c, s->tris, (size_t)s->n_tris, &S.tris));
     HIPCHK(upload(c, s->meshes, (size_t)s->n_meshes, &S.meshes));
@@ -335,17 +520,16 @@ int pbrtgpu_scene_upload(pbrtgpu_ctx *c, const pbrtgpu_flat_scene *s) {
     HIPCHK(upload(c, s->vert_n, (size_t)s->n_verts * 3, &S.vertN));
     HIPCHK(upload(c, s->vert_uv, (size_t)s->n_verts * 2, &S.vertUV));
     HIPCHK(upload(c, s->quadrics, (size_t)s->n_quadrics, &S.quads));
-    HIPCHK(upload(c, s->materials, (size_t)s->n_materials, &S.mats));
-    HIPCHK(upload(c, s->lights, (size_t)s->n_lights, &S.lights));
+    HIPCHK(upload(c, mats.data(), mats.size(), &S.mats));
+    HIPCHK(upload(c, lts.data(), lts.size(), &S.lights));
     HIPCHK(upload(c, s->light_shapes, (size_t)s->n_light_shapes, &S.lightShapes));
-    HIPCHK(upload(c, s->spectra, (size_t)s->n_spectra_floats, &S.spectra));
+    HIPCHK(upload(c, pool.data(), pool.size(), &S.spectra));
     c->nb = s->n_bands;
     c->spp = s->spp;
     c->cam = s->camera;
     size_t filmFloats = (size_t)s->camera.px_count * s->camera.py_count * s->n_bands;
     HIPCHK(c->film.ensure(filmFloats * 4));
     HIPCHK(hipMemsetAsync(c->film.p, 0, filmFloats * 4, c->stream));
-    HIPCHK(c->zeroed.ensure(16));
     HIPCHK(c->counter.ensure(16));
     HIPCHK(hipStreamSynchronize(c->stream));
     c->hasScene = true;
@@ -380,6 +564,8 @@ static int render_impl(pbrtgpu_ctx *c, const pbrtgpu_render_desc *d, const int32
     if (s0 < 0 || s1 > spp || s0 >= s1) return fail(PBRTGPU_E_INVALID, "bad sample range");
     int tw = d->tile_w > 0 ? d->tile_w : 16, th = d->tile_h > 0 ? d->tile_h : 16;
     int ntx = (cam.px_count + tw - 1) / tw, nty = (cam.py_count + th - 1) / th;
+    const bool countWork = (d->flags & PBRTGPU_F_COUNT_WORK) != 0;
+    Timing T;
     // pixel list of the requested tiles (film pixels; own sample pixel == film pixel)
     std::vector<int2> pix;
     std::vector<int> fidx;
@@ -405,12 +591,12 @@ static int render_impl(pbrtgpu_ctx *c, const pbrtgpu_render_desc *d, const int32
     double st[PBRTGPU_STAT_COUNT] = {0};
     if (!(d->flags & PBRTGPU_F_ACCUMULATE) && s0 == 0)
         HIPCHK(hipMemsetAsync(c->film.p, 0, (size_t)cam.px_count * cam.py_count * NB * 4, c->stream));
-    if (nPix == 0) { if (stats) memcpy(stats, st, sizeof(st)); return 0; }
+    if (nPix == 0) { if (stats) memcpy(stats, st, sizeof(st)); c->last = T; return 0; }
     HIPCHK(c->pix.ensure(pix.size() * sizeof(int2)));
     HIPCHK(c->filmIdx.ensure(fidx.size() * sizeof(int)));
     HIPCHK(hipMemcpyAsync(c->pix.p, pix.data(), pix.size() * sizeof(int2), hipMemcpyHostToDevice, c->stream));
     HIPCHK(hipMemcpyAsync(c->filmIdx.p, fidx.data(), fidx.size() * sizeof(int), hipMemcpyHostToDevice, c->stream));
-    const size_t ldsBytes = (size_t)c->stackDepth * kBlock * sizeof(uint32_t);
+    unsigned int zeroed = 0;
 
     // ---- spill samples (only meaningful when the whole sample range is rendered)
     std::vector<int> preT, preStart, preSrc, postT, postStart, postSrc;
@@ -421,6 +607,7 @@ static int render_impl(pbrtgpu_ctx *c, const pbrtgpu_render_desc *d, const int32
         HIPCHK(hipMemcpyAsync(c->mask.p, mask.data(), mask.size(), hipMemcpyHostToDevice, c->stream));
         unsigned int cap = 1u << 20;
         HIPCHK(c->keys.ensure((size_t)cap * sizeof(int3)));
+        HIPCHK(c->counter.ensure(16));
         HIPCHK(hipMemsetAsync(c->counter.p, 0, 16, c->stream));
         long nsamp = (long)(cam.sx_end - cam.sx_start) * (cam.sy_end - cam.sy_start) * spp;
         int grid = (int)std::min<long>((nsamp + 255) / 256, (long)c->numCUs * 16);
@@ -443,9 +630,10 @@ static int render_impl(pbrtgpu_ctx *c, const pbrtgpu_render_desc *d, const int32
             });
             HIPCHK(hipMemcpy(c->keys.p, keys.data(), nSpill * sizeof(int3), hipMemcpyHostToDevice));
             HIPCHK(c->spillL.ensure((size_t)nSpill * NB * 4));
-            hipLaunchKernelGGL(k_trace_keys<NB>, dim3((nSpill + kBlock - 1) / kBlock), dim3(kBlock), ldsBytes, c->stream,
-                               c->S, (const int3 *)c->keys.p, nSpill, (float *)c->spillL.p);
-            HIPCHK(hipGetLastError());
+            ItemSrc ks{};
+            ks.keys = (const int3 *)c->keys.p;
+            ks.nItems = (uint32_t)nSpill;
+            if (int e = run_wavefront<NB>(c, ks, (float *)c->spillL.p, countWork, T, nullptr)) return e;
             // contributions per target pixel, split into pre (source before the target's own
             // sample pixel in row-major order) and post
             const int ew = cam.sx_end - cam.sx_start;
@@ -456,8 +644,7 @@ static int render_impl(pbrtgpu_ctx *c, const pbrtgpu_render_desc *d, const int32
                 uint32_t hp = pixel_hash(c->S.seed, x, y);
                 float u[2];
                 s2d(hp, 0, (uint32_t)s, (uint32_t)spp, u);   // same sampler as k_spill_scan
-                float u0 = u[0], u1 = u[1];
-                float ix = x + u0, iy = y + u1;
+                float ix = x + u[0], iy = y + u[1];
                 float dx = ix - 0.5f, dy = iy - 0.5f;
                 int fx0 = (int)ceilf(dx - 0.5f), fx1 = (int)floorf(dx + 0.5f);
                 int fy0 = (int)ceilf(dy - 0.5f), fy1 = (int)floorf(dy + 0.5f);
@@ -481,8 +668,8 @@ static int render_impl(pbrtgpu_ctx *c, const pbrtgpu_render_desc *d, const int32
                 int tx = q.target % cam.px_count + cam.px_start, ty = q.target / cam.px_count + cam.py_start;
                 long own = (long)(ty - cam.sy_start) * ew + (tx - cam.sx_start);
                 bool pre = q.src < own;
-                std::vector<int> &T = pre ? preT : postT, &ST = pre ? preStart : postStart, &SR = pre ? preSrc : postSrc;
-                if (T.empty() || T.back() != q.target) { T.push_back(q.target); ST.push_back((int)SR.size()); }
+                std::vector<int> &Tg = pre ? preT : postT, &ST = pre ? preStart : postStart, &SR = pre ? preSrc : postSrc;
+                if (Tg.empty() || Tg.back() != q.target) { Tg.push_back(q.target); ST.push_back((int)SR.size()); }
                 SR.push_back(q.idx);
             }
             preStart.push_back((int)preSrc.size());
@@ -490,16 +677,16 @@ static int render_impl(pbrtgpu_ctx *c, const pbrtgpu_render_desc *d, const int32
             st[PBRTGPU_STAT_SPILLS] = (double)cbs.size();
         }
     }
-    auto applyLists = [&](std::vector<int> &T, std::vector<int> &ST, std::vector<int> &SR) -> int {
-        if (T.empty()) return 0;
-        HIPCHK(c->lists[0].ensure(T.size() * 4));
+    auto applyLists = [&](std::vector<int> &Tg, std::vector<int> &ST, std::vector<int> &SR) -> int {
+        if (Tg.empty()) return 0;
+        HIPCHK(c->lists[0].ensure(Tg.size() * 4));
         HIPCHK(c->lists[1].ensure(ST.size() * 4));
         HIPCHK(c->lists[2].ensure(SR.size() * 4));
-        HIPCHK(hipMemcpyAsync(c->lists[0].p, T.data(), T.size() * 4, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(hipMemcpyAsync(c->lists[0].p, Tg.data(), Tg.size() * 4, hipMemcpyHostToDevice, c->stream));
         HIPCHK(hipMemcpyAsync(c->lists[1].p, ST.data(), ST.size() * 4, hipMemcpyHostToDevice, c->stream));
         HIPCHK(hipMemcpyAsync(c->lists[2].p, SR.data(), SR.size() * 4, hipMemcpyHostToDevice, c->stream));
-        long n = (long)T.size() * NB;
-        hipLaunchKernelGGL(k_apply, dim3((n + 255) / 256), dim3(256), 0, c->stream, (int)T.size(), (const int *)c->lists[0].p,
+        long n = (long)Tg.size() * NB;
+        hipLaunchKernelGGL(k_apply, dim3((n + 255) / 256), dim3(256), 0, c->stream, (int)Tg.size(), (const int *)c->lists[0].p,
                            (const int *)c->lists[1].p, (const int *)c->lists[2].p, (const float *)c->spillL.p, NB,
                            (float *)c->film.p);
         HIPCHK(hipGetLastError());
@@ -508,48 +695,39 @@ static int render_impl(pbrtgpu_ctx *c, const pbrtgpu_render_desc *d, const int32
     };
     if (int e = applyLists(preT, preStart, preSrc)) return e;
 
-    // ---- main batches
-    const size_t lbudget = (size_t)1 << 30;   // 1 GiB of per-sample radiance per batch
+    // ---- main batches: per-sample radiance for (pixels x batch samples), then the ordered film sum
+    const size_t lbudget = (size_t)4 << 30;   // 4 GiB of per-sample radiance per batch
     int sb = (int)std::max<long>(1, std::min<long>(s1 - s0, (long)(lbudget / ((size_t)nPix * NB * 4))));
+    if ((uint64_t)nPix * sb > 0x7fffffffull) sb = std::max(1, (int)(0x7fffffffll / nPix));
     HIPCHK(c->Lbuf.ensure((size_t)nPix * sb * NB * 4));
-    HIPCHK(hipMemsetAsync(c->zeroed.p, 0, 16, c->stream));
-    float kms = 0.f, ams = 0.f;
-    int launches = 0;
-    hipEvent_t ea, eb, ec;
-    HIPCHK(hipEventCreate(&ea)); HIPCHK(hipEventCreate(&eb)); HIPCHK(hipEventCreate(&ec));
-    // persistent grid: resident blocks per CU from the LDS stack footprint (<= 8 per CU)
-    int perCU = std::max(1, std::min(8, (int)(160 * 1024 / std::max<size_t>(ldsBytes, 1))));
     for (int b0 = s0; b0 < s1; b0 += sb) {
         int n = std::min(sb, s1 - b0);
-        long items = (long)nPix * n;
-        int grid = (int)std::min<long>((items + kBlock - 1) / kBlock, (long)c->numCUs * perCU);
-        HIPCHK(hipEventRecord(ea, c->stream));
-        hipLaunchKernelGGL(k_render<NB>, dim3(grid), dim3(kBlock), ldsBytes, c->stream, c->S, (const int2 *)c->pix.p, nPix,
-                           b0, n, (float *)c->Lbuf.p, (unsigned int *)c->zeroed.p);
-        HIPCHK(hipGetLastError());
-        HIPCHK(hipEventRecord(eb, c->stream));
+        ItemSrc src{};
+        src.pix = (const int2 *)c->pix.p;
+        src.sb = n;
+        src.s0 = b0;
+        src.nItems = (uint32_t)((long)nPix * n);
+        if (int e = run_wavefront<NB>(c, src, (float *)c->Lbuf.p, countWork, T, &zeroed)) return e;
         long na = (long)nPix * NB;
+        HIPCHK(hipEventRecord(c->ev[6], c->stream));
         hipLaunchKernelGGL(k_accum<NB>, dim3((na + 255) / 256), dim3(256), 0, c->stream, (const float *)c->Lbuf.p,
                            (const int *)c->filmIdx.p, nPix, n, (float *)c->film.p);
         HIPCHK(hipGetLastError());
-        HIPCHK(hipEventRecord(ec, c->stream));
-        HIPCHK(hipEventSynchronize(ec));
-        float m1 = 0.f, m2 = 0.f;
-        HIPCHK(hipEventElapsedTime(&m1, ea, eb));
-        HIPCHK(hipEventElapsedTime(&m2, eb, ec));
-        kms += m1; ams += m2; ++launches;
-        st[PBRTGPU_STAT_PATHS] += (double)items;
+        HIPCHK(hipEventRecord(c->ev[7], c->stream));
+        HIPCHK(hipEventSynchronize(c->ev[7]));
+        float m2 = 0.f;
+        HIPCHK(hipEventElapsedTime(&m2, c->ev[6], c->ev[7]));
+        T.ms[K_ACCUM] += m2;
+        T.launches[K_ACCUM]++;
+        st[PBRTGPU_STAT_PATHS] += (double)src.nItems;
     }
-    (void)hipEventDestroy(ea); (void)hipEventDestroy(eb); (void)hipEventDestroy(ec);
     if (int e = applyLists(postT, postStart, postSrc)) return e;
-    unsigned int z = 0;
-    HIPCHK(hipMemcpyAsync(&z, c->zeroed.p, 4, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
-    st[PBRTGPU_STAT_KERNEL_MS] = kms;
-    st[PBRTGPU_STAT_ACCUM_MS] = ams;
-    st[PBRTGPU_STAT_ZEROED] = z;
-    c->lastKernelMs = launches ? kms / launches : 0.0;
-    c->lastLaunches = launches;
+    st[PBRTGPU_STAT_KERNEL_MS] = T.ms[K_CLOSEST] + T.ms[K_SHADOW] + T.ms[K_SHADE];
+    st[PBRTGPU_STAT_ACCUM_MS] = T.ms[K_ACCUM];
+    st[PBRTGPU_STAT_ZEROED] = zeroed;
+    st[PBRTGPU_STAT_PASSES] = T.passes;
+    c->last = T;
     if (stats) memcpy(stats, st, sizeof(st));
     return 0;
 }
@@ -571,15 +749,24 @@ int pbrtgpu_render_tiles(pbrtgpu_ctx *c, const pbrtgpu_render_desc *d, const int
 }  // extern "C"
 
 template <int NB>
-static int trace_impl(pbrtgpu_ctx *c, const int32_t *keys, int32_t n, float *out) {
+static int trace_impl(pbrtgpu_ctx *c, const int32_t *keys, int32_t n, float *out, bool countWork) {
+    const pbrtgpu_camera &cam = c->cam;
+    for (int32_t i = 0; i < n; ++i) {
+        const int32_t *k = keys + 3 * i;
+        if (k[0] < cam.sx_start || k[0] >= cam.sx_end || k[1] < cam.sy_start || k[1] >= cam.sy_end || k[2] < 0 ||
+            k[2] >= c->spp)
+            return fail(PBRTGPU_E_INVALID, "path key outside the sample extent / sample range");
+    }
     HIPCHK(c->scratch[0].ensure((size_t)n * sizeof(int3)));
     HIPCHK(c->scratch[1].ensure((size_t)n * NB * 4));
     HIPCHK(hipMemcpyAsync(c->scratch[0].p, keys, (size_t)n * 12, hipMemcpyHostToDevice, c->stream));
-    size_t lds = (size_t)c->stackDepth * kBlock * 4;
-    hipLaunchKernelGGL(k_trace_keys<NB>, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), lds, c->stream, c->S,
-                       (const int3 *)c->scratch[0].p, n, (float *)c->scratch[1].p);
-    HIPCHK(hipGetLastError());
-    HIPCHK(hipMemcpyAsync(out, c->scratch[1].p, (size_t)n * NB * 4, hipMemcpyDeviceToHost, c->stream));
+    ItemSrc ks{};
+    ks.keys = (const int3 *)c->scratch[0].p;
+    ks.nItems = (uint32_t)n;
+    Timing T;
+    if (int e = run_wavefront<NB>(c, ks, (float *)c->scratch[1].p, countWork, T, nullptr)) return e;
+    c->last = T;
+    if (out) HIPCHK(hipMemcpyAsync(out, c->scratch[1].p, (size_t)n * NB * 4, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     return 0;
 }
@@ -591,41 +778,27 @@ int pbrtgpu_trace_paths(pbrtgpu_ctx *c, const int32_t *keys, int32_t n, float *o
     if (n == 0) return 0;
     HIPCHK(hipSetDevice(c->device));
     switch (c->nb) {
-        case 32: return trace_impl<32>(c, keys, n, out);
-        case 60: return trace_impl<60>(c, keys, n, out);
-        case 30: return trace_impl<30>(c, keys, n, out);
+        case 32: return trace_impl<32>(c, keys, n, out, false);
+        case 60: return trace_impl<60>(c, keys, n, out, false);
+        case 30: return trace_impl<30>(c, keys, n, out, false);
     }
     return fail(PBRTGPU_E_UNSUPPORTED, "band count");
 }
-
-}  // extern "C"
-
-template <int NB>
-static int stats_impl(pbrtgpu_ctx *c, const int32_t *keys, int32_t n, uint64_t *out) {
-    HIPCHK(c->scratch[0].ensure((size_t)n * sizeof(int3)));
-    HIPCHK(c->scratch[1].ensure(64));
-    HIPCHK(hipMemcpyAsync(c->scratch[0].p, keys, (size_t)n * 12, hipMemcpyHostToDevice, c->stream));
-    HIPCHK(hipMemsetAsync(c->scratch[1].p, 0, 64, c->stream));
-    size_t lds = (size_t)c->stackDepth * kBlock * 4;
-    hipLaunchKernelGGL(k_stats<NB>, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), lds, c->stream, c->S,
-                       (const int3 *)c->scratch[0].p, n, (unsigned long long *)c->scratch[1].p);
-    HIPCHK(hipGetLastError());
-    HIPCHK(hipMemcpyAsync(out, c->scratch[1].p, 6 * 8, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
-    return 0;
-}
-
-extern "C" {
 
 int pbrtgpu_path_stats(pbrtgpu_ctx *c, const int32_t *keys, int32_t n, uint64_t *counters_out) {
     if (!c || !c->hasScene || !keys || !counters_out || n <= 0) return fail(PBRTGPU_E_INVALID, "bad arguments");
     HIPCHK(hipSetDevice(c->device));
+    int e = PBRTGPU_E_UNSUPPORTED;
     switch (c->nb) {
-        case 32: return stats_impl<32>(c, keys, n, counters_out);
-        case 60: return stats_impl<60>(c, keys, n, counters_out);
-        case 30: return stats_impl<30>(c, keys, n, counters_out);
+        case 32: e = trace_impl<32>(c, keys, n, nullptr, true); break;
+        case 60: e = trace_impl<60>(c, keys, n, nullptr, true); break;
+        case 30: e = trace_impl<30>(c, keys, n, nullptr, true); break;
     }
-    return fail(PBRTGPU_E_UNSUPPORTED, "band count");
+    if (e) return e;
+    const uint64_t *w = c->last.work;
+    counters_out[0] = w[W_RAYS]; counters_out[1] = w[W_SHADOW]; counters_out[2] = w[W_NODES_C] + w[W_NODES_S];
+    counters_out[3] = w[W_TRIS_C] + w[W_TRIS_S]; counters_out[4] = w[W_QUADS_C] + w[W_QUADS_S]; counters_out[5] = w[W_HITS];
+    return 0;
 }
 
 int pbrtgpu_intersect(pbrtgpu_ctx *c, const float *rays, int32_t n, float *hits, int32_t *occ) {
@@ -636,8 +809,8 @@ int pbrtgpu_intersect(pbrtgpu_ctx *c, const float *rays, int32_t n, float *hits,
     HIPCHK(c->scratch[1].ensure((size_t)n * 16));
     HIPCHK(c->scratch[2].ensure((size_t)n * 4));
     HIPCHK(hipMemcpyAsync(c->scratch[0].p, rays, (size_t)n * 32, hipMemcpyHostToDevice, c->stream));
-    size_t lds = (size_t)c->stackDepth * kBlock * 4;
-    hipLaunchKernelGGL(k_intersect, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), lds, c->stream, c->S,
+    size_t lds = (size_t)c->stackDepth * kTraceBlock * 4;
+    hipLaunchKernelGGL(k_intersect, dim3((n + kTraceBlock - 1) / kTraceBlock), dim3(kTraceBlock), lds, c->stream, c->S,
                        (const float *)c->scratch[0].p, n, (float *)c->scratch[1].p, (int *)c->scratch[2].p);
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(hits, c->scratch[1].p, (size_t)n * 16, hipMemcpyDeviceToHost, c->stream));
@@ -648,10 +821,12 @@ int pbrtgpu_intersect(pbrtgpu_ctx *c, const float *rays, int32_t n, float *hits,
     return 0;
 }
 
-int pbrtgpu_last_kernel_timing(pbrtgpu_ctx *c, double *avg_ms, int32_t *launches) {
-    if (!c) return fail(PBRTGPU_E_INVALID, "null ctx");
-    if (avg_ms) *avg_ms = c->lastKernelMs;
-    if (launches) *launches = c->lastLaunches;
+int pbrtgpu_last_timing(pbrtgpu_ctx *c, pbrtgpu_timing *out) {
+    if (!c || !out) return fail(PBRTGPU_E_INVALID, "null argument");
+    memset(out, 0, sizeof(*out));
+    for (int k = 0; k < K_KINDS; ++k) { out->ms[k] = c->last.ms[k]; out->launches[k] = c->last.launches[k]; }
+    out->passes = c->last.passes;
+    for (int i = 0; i < W_COUNT; ++i) out->work[i] = c->last.work[i];
     return 0;
 }
 

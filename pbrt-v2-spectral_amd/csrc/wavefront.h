@@ -1,0 +1,513 @@
+// wavefront.h -- SoA path state and the per-vertex shading step of the wavefront path
+// tracer.  PathIntegrator::Li (integrators/path.cpp:44-115) and
+// EstimateDirect (core/integrator.cpp:109-166) are split at their three ray queries:
+//
+//   pass k:   k_trace_closest   continuation/camera rays + MIS rays  (BVHAccel::Intersect)
+//             k_trace_shadow    light-sample visibility rays          (BVHAccel::IntersectP)
+//             k_shade           per live path slot:
+//                 1. finish the vertex whose direct light was pending:
+//                      Ld = (0 [+ A if unoccluded]) [+ B if the MIS ray hit the light]
+//                      L += beta_b * (nLights * Ld)
+//                 2. if the continuation ray hit: the next vertex -- emission, BSDF, light
+//                    sample (A + shadow ray), BSDF sample with MIS (B + MIS ray), path
+//                    continuation (beta update, roulette, next ray)
+//                 3. finished paths go through the NaN/negative/inf guard into Lout, and the
+//                    slot takes the next camera sample (path regeneration)
+//
+// Every sampler / MT19937 draw, every float operation and its order are those of the
+// single-path loop, so a path's radiance is identical to the oracle's; the split only
+// defers the additions that need a ray answer.  Band data are stored as band quads,
+// [band/4][slot] float4, so one 16-byte load per lane covers four bands and a wave's 64
+// loads of one quad are a contiguous 1 KiB.
+#pragma once
+#include "device.h"
+
+namespace pgd {
+
+enum {
+    PF_CONT = 1,      // continuation / camera ray queued (answer in hit[0])
+    PF_PEND = 2,      // direct lighting of vertex `bounce` not yet added to L
+    PF_PA = 4,        // light-sample term A waits on the shadow ray
+    PF_PB = 8,        // BSDF-sample term B waits on the MIS ray
+    PF_SPEC = 16,     // specularBounce
+    PF_MTINIT = 32,   // MT19937 recurrence window initialised
+};
+#define PF_LIGHT_SHIFT 8
+
+enum { RAY_C = 0, RAY_M = 1, RAY_S = 2 };
+// counters (u32 words), each on its own 128-byte line so that the per-block atomics of
+// different queues do not serialise on one memory-side atomic unit; work = u64 at CNT_WORK
+#define CNT_QC(q) (32 * (q))          // closest-hit queue size, queue set q = 0, 1
+#define CNT_QS(q) (64 + 32 * (q))     // shadow queue size
+enum { CNT_NEXT = 128, CNT_ZEROED = 160, CNT_WORK = 192, CNT_WORDS = 288 };
+enum { W_RAYS = 0, W_SHADOW = 1, W_NODES_C = 2, W_NODES_S = 3, W_TRIS_C = 4, W_TRIS_S = 5, W_QUADS_C = 6, W_QUADS_S = 7,
+       W_HITS = 8, W_COUNT = 12 };
+
+struct PathSoA {
+    int cap;
+    int *item;          // output index, -1 = free slot
+    uint32_t *hp;       // pixel hash (sampler scramble key)
+    uint32_t *smp;      // sample index
+    int *bounce;        // vertex index of the last processed vertex (-1: camera ray in flight)
+    uint32_t *flags;
+    uint32_t *mt;       // [5][cap]: k, a, b, m, seed
+    float4 *beta;       // [2][NQ][cap]: beta at even / odd vertices
+    float4 *L;          // [NQ][cap]
+    float4 *A, *B;      // [NQ][cap]
+    float *ray;         // [3][9][cap]: o.xyz, d.xyz, mint, maxt, time  for RAY_C, RAY_M, RAY_S
+    int *hitPrim;       // [2][cap]  (RAY_C, RAY_M)
+    float *hitT;        // [2][cap]
+    uint32_t *occ;      // [cap]
+    uint32_t *qC;       // [2][2*cap]: (slot << 1) | kind
+    uint32_t *qS;       // [2][cap]
+    uint32_t *cnt;      // counters (CNT_*), work counters as u64 from word CNT_WORK
+};
+
+// where the camera samples of a pass come from
+struct ItemSrc {
+    const int2 *pix;    // film pixels (sample x, y) of the render call
+    int sb;             // samples per pixel in this batch
+    int s0;             // first sample index
+    const int3 *keys;   // explicit (x, y, s) keys instead (trace_paths / spill samples), or null
+    uint32_t nItems;
+};
+
+PGD_INLINE void ray_store(const PathSoA &P, int kind, int slot, const Ray &r) {
+    float *b = P.ray + (size_t)kind * 9 * P.cap + slot;
+    const size_t c = P.cap;
+    b[0] = r.o.x; b[c] = r.o.y; b[2 * c] = r.o.z;
+    b[3 * c] = r.d.x; b[4 * c] = r.d.y; b[5 * c] = r.d.z;
+    b[6 * c] = r.mint; b[7 * c] = r.maxt; b[8 * c] = r.time;
+}
+PGD_INLINE Ray ray_load(const PathSoA &P, int kind, int slot) {
+    const float *b = P.ray + (size_t)kind * 9 * P.cap + slot;
+    const size_t c = P.cap;
+    Ray r;
+    r.o = v3(b[0], b[c], b[2 * c]);
+    r.d = v3(b[3 * c], b[4 * c], b[5 * c]);
+    r.mint = b[6 * c]; r.maxt = b[7 * c]; r.time = b[8 * c];
+    return r;
+}
+
+PGD_INLINE void mt_load(const PathSoA &P, int slot, uint32_t fl, MT &r) {
+    const size_t c = P.cap;
+    r.k = P.mt[slot]; r.a = P.mt[c + slot]; r.b = P.mt[2 * c + slot]; r.m = P.mt[3 * c + slot];
+    r.seed = P.mt[4 * c + slot];
+    r.init = (fl & PF_MTINIT) != 0;
+}
+PGD_INLINE void mt_store(const PathSoA &P, int slot, const MT &r) {
+    const size_t c = P.cap;
+    P.mt[slot] = r.k; P.mt[c + slot] = r.a; P.mt[2 * c + slot] = r.b; P.mt[3 * c + slot] = r.m;
+}
+
+template <int NB> struct Bands { static constexpr int NQ = (NB + 3) / 4; };
+
+PGD_INLINE float4 ld4(const float *p) { return *reinterpret_cast<const float4 *>(p); }
+PGD_INLINE float &cmp(float4 &v, int k) { return k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w; }
+PGD_INLINE float cmp(const float4 &v, int k) { return k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w; }
+
+// BSDF value of four bands (quad q) -- fval() per component, identical operations
+PGD_INLINE float term_val(const FTerm &t, float r, float r2) {
+    switch (t.kind) {
+        case T_LAMB: return r * kInvPi;
+        case T_OREN: return (r * kInvPi) * t.s0;
+        case T_BLINN: return (((r * t.s0) * t.s1) * t.s2) / t.s3;
+        case T_FB: {
+            const float cd = (28.f / (23.f * kPi));
+            float diffuse = ((((cd * r) * (1.f - r2)) * t.s0) * t.s1);
+            float schlick = r2 + t.s2 * (1.f - r2);
+            return diffuse + t.s3 * schlick;
+        }
+        default: return 0.f;
+    }
+}
+PGD_INLINE float4 fval4(const float *sp, const FVal &F, int q) {
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (F.mode == FV_SPEC) {
+        float4 r = ld4(sp + F.R + 4 * q);
+        return make_float4((1.f * r.x) / F.d, (1.f * r.y) / F.d, (1.f * r.z) / F.d, (1.f * r.w) / F.d);
+    }
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        if (k < F.n) {
+            const FTerm &t = F.t[k];
+            float4 r = ld4(sp + t.R + 4 * q);
+            float4 r2 = t.kind == T_FB ? ld4(sp + t.R2 + 4 * q) : r;
+            v.x += term_val(t, r.x, r2.x);
+            v.y += term_val(t, r.y, r2.y);
+            v.z += term_val(t, r.z, r2.z);
+            v.w += term_val(t, r.w, r2.w);
+        }
+    }
+    return v;
+}
+
+// camera sample of an item -> fresh path in `slot` (SamplerRendererTask::Run,
+// samplerrenderer.cpp:86-108 + the fixed-seed sampler of DESIGN.md §3.1)
+template <int NB>
+PGD_INLINE void path_start(const DevScene &S, const PathSoA &P, const ItemSrc &src, int slot, uint32_t item) {
+    constexpr int NQ = Bands<NB>::NQ;
+    int px, py;
+    uint32_t s;
+    if (src.keys) { int3 k = src.keys[item]; px = k.x; py = k.y; s = (uint32_t)k.z; }
+    else {
+        uint32_t p = item / (uint32_t)src.sb;
+        int2 xy = src.pix[p];
+        px = xy.x; py = xy.y;
+        s = (uint32_t)src.s0 + (item - p * (uint32_t)src.sb);
+    }
+    const uint32_t spp = (uint32_t)S.spp;
+    uint32_t hp = pixel_hash(S.seed, px, py);
+    float u[2], lens[2];
+    s2d(hp, 0, s, spp, u);
+    float imageX = px + u[0], imageY = py + u[1];
+    s2d(hp, 1, s, spp, lens);
+    float timeU = s1d(hp, 2, s, spp);
+    Ray r = camera_ray(S.cam, imageX, imageY, lens[0], lens[1], timeU);
+    ray_store(P, RAY_C, slot, r);
+    P.item[slot] = (int)item;
+    P.hp[slot] = hp;
+    P.smp[slot] = s;
+    P.bounce[slot] = -1;
+    P.flags[slot] = PF_CONT;
+    P.mt[slot] = 0;
+    P.mt[4 * (size_t)P.cap + slot] = path_seed(hp, s);
+    const size_t c = P.cap;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+        P.L[q * c + slot] = make_float4(0.f, 0.f, 0.f, 0.f);
+        P.beta[q * c + slot] = make_float4(1.f, 1.f, 1.f, 1.f);
+    }
+}
+
+// finished path -> guard (samplerrenderer.cpp:111-128) -> Lout[item]; returns "zeroed"
+template <int NB>
+PGD_INLINE bool path_output(const DevScene &S, const float4 (&L)[Bands<NB>::NQ], float *__restrict__ Lout, int item) {
+    constexpr int NQ = Bands<NB>::NQ;
+    bool nan = false;
+    float yy = 0.f;
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+        float v = 1.f * ((1.f * cmp(L[i / 4], i % 4)) + 0.f);
+        nan = nan || isnan(v);
+        yy += S.bandY[i] * v;
+    }
+    bool bad = nan;
+    if (!bad) {
+        float yv = yy / S.yint;
+        bad = (yv < -1e-5) || isinf(yv);
+    }
+    float *o = Lout + (size_t)item * NB;
+    if (NB % 4 == 0) {
+        float4 *o4 = reinterpret_cast<float4 *>(o);
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            float4 v = L[q];
+            o4[q] = bad ? make_float4(0.f, 0.f, 0.f, 0.f)
+                        : make_float4(1.f * ((1.f * v.x) + 0.f), 1.f * ((1.f * v.y) + 0.f), 1.f * ((1.f * v.z) + 0.f),
+                                      1.f * ((1.f * v.w) + 0.f));
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < NB; ++i) o[i] = bad ? 0.f : 1.f * ((1.f * cmp(L[i / 4], i % 4)) + 0.f);
+    }
+    return bad;
+}
+
+// ray requests produced by one shade step
+struct Pushes { bool c, m, s; };
+
+// One vertex of PathIntegrator::Li at bounce `vb` for the path in `slot`, whose
+// continuation ray `ray` hit primitive `prim` at `thit`.  L is the path's radiance (in
+// registers); beta_b is P.beta[vb & 1] in HBM.  BSDF values are evaluated lazily per band
+// quad (fval4).  Updates fl.
+template <int NB>
+PGD_INLINE Pushes shade_vertex(const DevScene &S, const PathSoA &P, int slot, int vb, const Ray &ray, int prim,
+                               float thit, uint32_t &fl, float4 (&L)[Bands<NB>::NQ]) {
+    constexpr int NQ = Bands<NB>::NQ;
+    const size_t c = P.cap;
+    const float *sp = S.spectra;
+    Pushes out = {false, false, false};
+    const float4 *beta = P.beta + (size_t)(vb & 1) * NQ * c + slot;
+    Isect is;
+    isect_fill(S, ray, prim, thit, is);
+    if (vb == 0 || (fl & PF_SPEC)) {
+        int al = S.prims[is.prim].area_light;
+        if (al >= 0 && vdot(is.dg.nn, vneg(ray.d)) > 0.f) {
+            const float *Ls = sp + S.lights[al].spec;
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                float4 b = beta[q * c], e = ld4(Ls + 4 * q);
+                L[q].x += b.x * e.x; L[q].y += b.y * e.y; L[q].z += b.z * e.z; L[q].w += b.w * e.w;
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                float4 b = beta[q * c];
+                L[q].x += b.x * 0.f; L[q].y += b.y * 0.f; L[q].z += b.z * 0.f; L[q].w += b.w * 0.f;
+            }
+        }
+    }
+    BSDF bs;
+    V p, n;
+    get_bsdf(S, is, bs, &p, &n);
+    const V wo = vneg(ray.d);
+    const uint32_t hp = P.hp[slot], s = P.smp[slot], spp = (uint32_t)S.spp;
+    MT rng;
+    const bool useMT = vb >= 3;
+    if (useMT) mt_load(P, slot, fl, rng);
+    const int nLights = S.nLights;
+    fl &= ~(PF_PEND | PF_PA | PF_PB | PF_CONT | (0xffffffu << PF_LIGHT_SHIFT));
+    FVal F;
+    if (nLights > 0) {
+        float ul[3], ub[3], ulnum;
+        if (!useMT) {
+            float u2[2];
+            ulnum = s1d(hp, DIM_1D(4 * vb + 1), s, spp);
+            s2d(hp, DIM_2D(3 * vb + 0), s, spp, u2); ul[0] = u2[0]; ul[1] = u2[1];
+            ul[2] = s1d(hp, DIM_1D(4 * vb + 0), s, spp);
+            s2d(hp, DIM_2D(3 * vb + 1), s, spp, u2); ub[0] = u2[0]; ub[1] = u2[1];
+            ub[2] = s1d(hp, DIM_1D(4 * vb + 2), s, spp);
+        } else {
+            ulnum = mt_float(rng);
+            ul[0] = mt_float(rng); ul[1] = mt_float(rng); ul[2] = mt_float(rng);
+            ub[0] = mt_float(rng); ub[1] = mt_float(rng); ub[2] = mt_float(rng);
+        }
+        int lightNum = (int)floorf(ulnum * nLights);
+        if (lightNum > nLights - 1) lightNum = nLights - 1;
+        const pbrtgpu_light &Lt = S.lights[lightNum];
+        const float *Ls = sp + Lt.spec;
+        const int flags = BSDF_ALL & ~BSDF_SPECULAR;
+        fl |= PF_PEND | ((uint32_t)lightNum << PF_LIGHT_SHIFT);
+        // ---- light sample -> A (added if the shadow ray is unoccluded)
+        V wi;
+        float lightPdf, bsdfPdf;
+        Seg vis;
+        bool lit, isPoint;
+        float lscale = light_sample_L(S, Lt, p, is.rayEps, ul, &wi, &lightPdf, &vis, &lit, &isPoint);
+        bool liBlack = isPoint ? false : !lit;
+        if (isPoint) {
+            bool allz = true;
+            for (int i = 0; i < NB; ++i) allz = allz && ((Ls[i] / lscale) == 0.);
+            liBlack = allz;
+        } else if (lit) liBlack = Lt.is_black != 0;
+        if (lightPdf > 0. && !liBlack) {
+            bsdf_f(bs, wo, wi, flags, F);
+            float sc;
+            if (isPoint) sc = fabsf(vdot(wi, n)) / lightPdf;
+            else {
+                bsdfPdf = bsdf_pdf(bs, wo, wi, flags);
+                float weight = power_heuristic(lightPdf, bsdfPdf);
+                sc = fabsf(vdot(wi, n)) * weight / lightPdf;
+            }
+            // A_i = (f_i * Li_i) * sc ; written while testing f for black (A unused if black)
+            float4 *A = P.A + slot;
+            bool black = true;
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                float4 f = fval4(sp, F, q), e = ld4(Ls + 4 * q), a;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    float li = isPoint ? (cmp(e, k) / lscale) : cmp(e, k);
+                    cmp(a, k) = (cmp(f, k) * li) * sc;
+                    if (4 * q + k < NB) black = black && (cmp(f, k) == 0.);
+                }
+                A[q * c] = a;
+            }
+            if (!black) {
+                Ray sr;
+                sr.o = vis.o; sr.d = vis.d; sr.mint = vis.mint; sr.maxt = vis.maxt; sr.time = ray.time;
+                ray_store(P, RAY_S, slot, sr);
+                fl |= PF_PA;
+                out.s = true;
+            }
+        }
+        // ---- BSDF sample with MIS -> B (added if the MIS ray reaches this light)
+        if (!isPoint) {
+            int sampledType;
+            bsdf_sample_f(bs, wo, &wi, ub[0], ub[1], ub[2], &bsdfPdf, flags, &sampledType, F);
+            if (bsdfPdf > 0. && !(F.mode == FV_SUM && F.n == 0)) {
+                float weight = 1.f;
+                bool go = true;
+                if (!(sampledType & BSDF_SPECULAR)) {
+                    lightPdf = light_pdf(S, Lt, p, wi);
+                    if (lightPdf == 0.) go = false;
+                    else weight = power_heuristic(bsdfPdf, lightPdf);
+                }
+                if (go && !Lt.is_black) {
+                    const float ad = fabsf(vdot(wi, n));
+                    float4 *B = P.B + slot;
+                    bool black = true;
+#pragma unroll
+                    for (int q = 0; q < NQ; ++q) {
+                        float4 f = fval4(sp, F, q), e = ld4(Ls + 4 * q), b;
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) {
+                            cmp(b, k) = (((cmp(f, k) * cmp(e, k)) * ad) * weight) / bsdfPdf;
+                            if (4 * q + k < NB) black = black && (cmp(f, k) == 0.);
+                        }
+                        B[q * c] = b;
+                    }
+                    if (!black) {
+                        Ray mr;
+                        mr.o = p; mr.d = wi; mr.mint = is.rayEps; mr.maxt = INFINITY; mr.time = ray.time;
+                        ray_store(P, RAY_M, slot, mr);
+                        fl |= PF_PB;
+                        out.m = true;
+                    }
+                }
+            }
+        }
+        if (!(fl & (PF_PA | PF_PB))) {
+            // nothing can add to Ld: finish now (L += beta * (nLights * 0))
+            const float z = (float)nLights * 0.f;
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                float4 b = beta[q * c];
+                L[q].x += b.x * z; L[q].y += b.y * z; L[q].z += b.z * z; L[q].w += b.w * z;
+            }
+            fl &= ~PF_PEND;
+        }
+    } else {
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            float4 b = beta[q * c];
+            L[q].x += b.x * 0.f; L[q].y += b.y * 0.f; L[q].z += b.z * 0.f; L[q].w += b.w * 0.f;
+        }
+    }
+    // ---- path continuation
+    float up[3];
+    if (!useMT) {
+        float u2[2];
+        s2d(hp, DIM_2D(3 * vb + 2), s, spp, u2); up[0] = u2[0]; up[1] = u2[1];
+        up[2] = s1d(hp, DIM_1D(4 * vb + 3), s, spp);
+    } else {
+        up[0] = mt_float(rng); up[1] = mt_float(rng); up[2] = mt_float(rng);
+    }
+    V wi;
+    float pdf;
+    int sflags;
+    bsdf_sample_f(bs, wo, &wi, up[0], up[1], up[2], &pdf, BSDF_ALL, &sflags, F);
+    bool cont = pdf != 0. && !(F.mode == FV_SUM && F.n == 0);
+    if (cont) {
+        const float ad = fabsf(vdot(wi, n));
+        float4 *bn = P.beta + (size_t)((vb + 1) & 1) * NQ * c + slot;
+        float4 nb4[NQ];
+        bool black = true;
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            float4 f = fval4(sp, F, q), b = beta[q * c];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                cmp(nb4[q], k) = cmp(b, k) * ((cmp(f, k) * ad) / pdf);
+                if (4 * q + k < NB) black = black && (cmp(f, k) == 0.);
+            }
+        }
+        cont = !black;
+        if (cont) {
+            if (sflags & BSDF_SPECULAR) fl |= PF_SPEC; else fl &= ~PF_SPEC;
+            if (vb > 3) {
+                float yy = 0.f;
+#pragma unroll
+                for (int i = 0; i < NB; ++i) yy += S.bandY[i] * cmp(nb4[i / 4], i % 4);
+                float cp = pmin(.5f, yy / S.yint);
+                if (mt_float(rng) > cp) cont = false;
+                else {
+#pragma unroll
+                    for (int q = 0; q < NQ; ++q) {
+                        nb4[q].x /= cp; nb4[q].y /= cp; nb4[q].z /= cp; nb4[q].w /= cp;
+                    }
+                }
+            }
+            if (vb == S.maxDepth) cont = false;
+        }
+        if (cont) {
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) bn[q * c] = nb4[q];
+            Ray nray;
+            nray.o = p; nray.d = wi; nray.mint = is.rayEps; nray.maxt = INFINITY; nray.time = ray.time;
+            ray_store(P, RAY_C, slot, nray);
+            fl |= PF_CONT;
+            out.c = true;
+        }
+    }
+    if (useMT) {
+        mt_store(P, slot, rng);
+        if (rng.init) fl |= PF_MTINIT;
+    }
+    return out;
+}
+
+// k_shade body for one slot: finish pending direct light, process the next vertex.
+// Returns the ray requests; *done when the path has produced its radiance.
+template <int NB>
+PGD_INLINE Pushes shade_slot(const DevScene &S, const PathSoA &P, int slot, float *__restrict__ Lout, bool *done,
+                             bool *zeroed) {
+    constexpr int NQ = Bands<NB>::NQ;
+    const size_t c = P.cap;
+    uint32_t fl = P.flags[slot];
+    int b = P.bounce[slot];
+    float4 L[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) L[q] = P.L[q * c + slot];
+    Pushes out = {false, false, false};
+    if (fl & PF_PEND) {
+        const bool useA = (fl & PF_PA) && !P.occ[slot];
+        bool useB = false;
+        if (fl & PF_PB) {
+            int mp = P.hitPrim[c + slot];
+            if (mp >= 0 && S.prims[mp].area_light == (int)(fl >> PF_LIGHT_SHIFT)) {
+                Ray mr = ray_load(P, RAY_M, slot);
+                Isect lis;
+                isect_fill(S, mr, mp, P.hitT[c + slot], lis);
+                useB = vdot(lis.dg.nn, vneg(mr.d)) > 0.f;
+            }
+        }
+        const float nl = (float)S.nLights;
+        const float4 *beta = P.beta + (size_t)(b & 1) * NQ * c + slot;
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            float4 bt = beta[q * c];
+            float4 a = useA ? P.A[q * c + slot] : make_float4(0.f, 0.f, 0.f, 0.f);
+            float4 bb = useB ? P.B[q * c + slot] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                float Ld = 0.f;
+                if (useA) Ld += cmp(a, k);
+                if (useB) Ld += cmp(bb, k);
+                cmp(L[q], k) += cmp(bt, k) * (nl * Ld);
+            }
+        }
+        fl &= ~(PF_PEND | PF_PA | PF_PB);
+    }
+    if (fl & PF_CONT) {
+        const int vb = b + 1;
+        const int prim = P.hitPrim[slot];
+        fl &= ~PF_CONT;
+        if (prim < 0) {
+            if (vb > 0 && (fl & PF_SPEC)) {
+                const float4 *beta = P.beta + (size_t)(vb & 1) * NQ * c + slot;
+#pragma unroll
+                for (int q = 0; q < NQ; ++q) {
+                    float4 bt = beta[q * c];
+                    L[q].x += bt.x * 0.f; L[q].y += bt.y * 0.f; L[q].z += bt.z * 0.f; L[q].w += bt.w * 0.f;
+                }
+            }
+        } else {
+            Ray ray = ray_load(P, RAY_C, slot);
+            out = shade_vertex<NB>(S, P, slot, vb, ray, prim, P.hitT[slot], fl, L);
+            P.bounce[slot] = vb;
+        }
+    }
+    *done = !(fl & (PF_CONT | PF_PEND));
+    *zeroed = false;
+    if (*done) *zeroed = path_output<NB>(S, L, Lout, P.item[slot]);
+    else {
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) P.L[q * c + slot] = L[q];
+    }
+    P.flags[slot] = fl;
+    return out;
+}
+
+}  // namespace pgd

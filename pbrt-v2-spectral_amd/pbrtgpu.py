@@ -67,7 +67,17 @@ class RenderDesc(ctypes.Structure):
                 ("flags", I32), ("reserved", I32 * 3)]
 
 
-STAT_PATHS, STAT_KERNEL_MS, STAT_ACCUM_MS, STAT_ZEROED, STAT_SPILLS = 0, 1, 2, 3, 4
+STAT_PATHS, STAT_KERNEL_MS, STAT_ACCUM_MS, STAT_ZEROED, STAT_SPILLS, STAT_PASSES = 0, 1, 2, 3, 4, 5
+F_ACCUMULATE, F_COUNT_WORK = 1, 2
+ABI_VERSION = 2
+
+
+class Timing(ctypes.Structure):
+    _fields_ = [("ms", ctypes.c_double * 4), ("launches", I32 * 4), ("passes", I32), ("pad", I32),
+                ("work", ctypes.c_uint64 * 12)]
+    KERNELS = ("k_trace_closest", "k_trace_shadow", "k_shade", "k_accum")
+    WORK = ("rays", "shadow_rays", "nodes_closest", "nodes_shadow", "tris_closest", "tris_shadow", "quads_closest",
+            "quads_shadow", "hits")
 
 _host = None
 _gpu = None
@@ -111,7 +121,7 @@ def gpu_lib():
         g.pbrtgpu_trace_paths.argtypes = [P, P, I32, P]
         g.pbrtgpu_intersect.argtypes = [P, P, I32, P, P]
         g.pbrtgpu_path_stats.argtypes = [P, P, I32, P]
-        g.pbrtgpu_last_kernel_timing.argtypes = [P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(I32)]
+        g.pbrtgpu_last_timing.argtypes = [P, ctypes.POINTER(Timing)]
     return _gpu
 
 
@@ -120,7 +130,7 @@ def gpu_symbols():
     return ["pbrtgpu_abi_version", "pbrtgpu_device_count", "pbrtgpu_context_create",
             "pbrtgpu_context_destroy", "pbrtgpu_last_error", "pbrtgpu_scene_upload",
             "pbrtgpu_render_tiles", "pbrtgpu_film_read", "pbrtgpu_film_clear",
-            "pbrtgpu_trace_paths", "pbrtgpu_intersect", "pbrtgpu_path_stats", "pbrtgpu_last_kernel_timing"]
+            "pbrtgpu_trace_paths", "pbrtgpu_intersect", "pbrtgpu_path_stats", "pbrtgpu_last_timing"]
 
 
 class Scene:
@@ -214,10 +224,11 @@ class Device:
         _check(self.lib.pbrtgpu_scene_upload(self.ctx, ctypes.byref(scene.flat)))
         self.scene = scene
 
-    def render(self, spp_begin=0, spp_end=None, tiles=None, tile=(16, 16), accumulate=False, stats=None):
+    def render(self, spp_begin=0, spp_end=None, tiles=None, tile=(16, 16), accumulate=False, stats=None,
+               count_work=False):
         s = self.scene
         desc = RenderDesc(spp_begin, s.spp if spp_end is None else spp_end, tile[0], tile[1],
-                          1 if accumulate else 0, (I32 * 3)())
+                          (F_ACCUMULATE if accumulate else 0) | (F_COUNT_WORK if count_work else 0), (I32 * 3)())
         st = np.zeros(8, dtype=np.float64)
         if tiles is None:
             _check(self.lib.pbrtgpu_render_tiles(self.ctx, ctypes.byref(desc), None, 0, st.ctypes.data))
@@ -259,11 +270,15 @@ class Device:
         _check(self.lib.pbrtgpu_path_stats(self.ctx, keys.ctypes.data, len(keys), out.ctypes.data))
         return dict(zip(["rays", "shadow_rays", "nodes", "tri_tests", "quad_tests", "hits"], [int(v) for v in out]))
 
-    def kernel_timing(self):
-        ms = ctypes.c_double()
-        n = I32()
-        _check(self.lib.pbrtgpu_last_kernel_timing(self.ctx, ctypes.byref(ms), ctypes.byref(n)))
-        return ms.value, n.value
+    def timing(self):
+        """Per-kernel device ms / launches of the last call, passes, and work counters."""
+        t = Timing()
+        _check(self.lib.pbrtgpu_last_timing(self.ctx, ctypes.byref(t)))
+        out = {"passes": t.passes}
+        for i, k in enumerate(Timing.KERNELS):
+            out[k] = {"ms": t.ms[i], "launches": t.launches[i]}
+        out["work"] = {k: int(t.work[i]) for i, k in enumerate(Timing.WORK)}
+        return out
 
 
 # ---------------------------------------------------------------- test infrastructure

@@ -33,7 +33,7 @@ def _keys(scene, stride=1):
 def test_native_library_loaded(pg):
     lib = pg.gpu_lib()
     assert lib.pbrtgpu_device_count() >= 1
-    assert lib.pbrtgpu_abi_version() == 1
+    assert lib.pbrtgpu_abi_version() == pg.ABI_VERSION
 
 
 def test_paths_match_oracle(pg, killeroo64, dev):
@@ -71,3 +71,27 @@ def test_intersect_matches_oracle(pg, killeroo64, dev):
     assert np.array_equal(hg[:, 3].view(np.int32), ho[:, 3].view(np.int32))
     assert np.array_equal(hg[:, 0].view(np.int32), ho[:, 0].view(np.int32))
     assert np.array_equal(og, oo)
+
+
+def test_regeneration_small_slot_pool(pg, killeroo64, dev, monkeypatch):
+    """Few path slots -> many regenerations per slot; results must not depend on it."""
+    keys = _keys(killeroo64, stride=3)
+    ref = dev.trace_paths(keys)
+    monkeypatch.setenv("PBRTGPU_SLOTS", "257")
+    small = dev.trace_paths(keys)
+    assert np.array_equal(ref.view(np.int32), small.view(np.int32))
+    st = dev.render()
+    film = dev.film()
+    monkeypatch.delenv("PBRTGPU_SLOTS")
+    dev.render()
+    assert np.array_equal(film.view(np.int32), dev.film().view(np.int32))
+    assert st[pg.STAT_PASSES] > 20
+
+
+def test_work_counters(pg, killeroo64, dev):
+    dev.render(count_work=True)
+    w = dev.timing()["work"]
+    n = killeroo64.width * killeroo64.height * killeroo64.spp
+    assert w["rays"] >= n                      # at least one camera ray per path
+    assert w["nodes_closest"] > w["rays"]
+    assert 0 < w["hits"] <= w["rays"]

@@ -1,0 +1,86 @@
+"""Generate tests/golden/* from the reference harness (oracle/_ref, built from the unmodified
+reference sources by oracle/ref/Makefile).  Runs only in the build container, where
+/root/reference exists; the fixtures it writes are committed and are all the GPU box and the
+CPU test suite need.
+
+Fixtures (numpy .npz, inputs + expected outputs only):
+  killeroo_paths_64x64s4.npz      per-path radiance of every 5th path (x, y, s keys) of
+                                  killeroo-simple at 64x64, 4 spp, seed 0, maxdepth 5
+  killeroo_paths_48x48s8_seed7_md7.npz   every 3rd path, 8 spp, seed 7, maxdepth 7 (MT19937 draws)
+  killeroo_film_80x60s16.npz      raw film sums [60][80][32] at 80x60, 16 spp (includes samples
+                                  that land on neighbouring pixels)
+  mt19937_kat.npz                 first 64 outputs of RNG(seed) for 6 seeds
+  fromrgb_32.npz                  SampledSpectrum::FromRGB (reflectance and illuminant) for 14
+                                  RGB triples, 32 bands 395-715 nm
+Usage: python tools/make_golden.py   (after `make -C oracle ref`)
+"""
+import os
+import subprocess
+import sys
+import tempfile
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HARNESS = os.path.join(ROOT, "oracle", "_ref", "b32", "pbrt_ref_harness")
+SCENE = "/root/reference/scenes/killeroo-simple.pbrt"
+OUT = os.path.join(ROOT, "tests", "golden")
+
+
+def run(args):
+    subprocess.run([HARNESS] + args, check=True, cwd=os.path.dirname(SCENE))
+
+
+def read_paths(fn):
+    raw = np.fromfile(fn, dtype=np.int32)
+    nb, spp, seed = raw[0], raw[1], raw[2]
+    rec = raw[4:].reshape(-1, 3 + nb)
+    return rec[:, :3].copy(), rec[:, 3:].copy().view(np.float32), int(spp), int(seed)
+
+
+def paths_fixture(name, res, spp, seed, maxdepth, every, tmp):
+    fn = os.path.join(tmp, name + ".bin")
+    run([SCENE, "--res", str(res[0]), str(res[1]), "--spp", str(spp), "--seed", str(seed), "--maxdepth",
+         str(maxdepth), "--paths", fn, "--path-every", str(every)])
+    keys, L, _, _ = read_paths(fn)
+    np.savez_compressed(os.path.join(OUT, name + ".npz"), keys=keys, L=L,
+                        config=np.array([res[0], res[1], spp, seed, maxdepth], np.int32))
+    print(name, keys.shape)
+
+
+def film_fixture(name, res, spp, seed, maxdepth, tmp):
+    fn = os.path.join(tmp, name + ".f32")
+    run([SCENE, "--res", str(res[0]), str(res[1]), "--spp", str(spp), "--seed", str(seed), "--maxdepth",
+         str(maxdepth), "--raw", fn])
+    raw = np.fromfile(fn, dtype=np.int32)
+    W, H, N = raw[:3]
+    film = raw[3:].view(np.float32).reshape(H, W, N)
+    np.savez_compressed(os.path.join(OUT, name + ".npz"), film=film,
+                        config=np.array([res[0], res[1], spp, seed, maxdepth], np.int32))
+    print(name, film.shape)
+
+
+def main():
+    if not os.path.exists(HARNESS):
+        sys.exit("build the reference harness first: make -C oracle ref")
+    os.makedirs(OUT, exist_ok=True)
+    with tempfile.TemporaryDirectory() as tmp:
+        paths_fixture("killeroo_paths_64x64s4", (64, 64), 4, 0, 5, 5, tmp)
+        paths_fixture("killeroo_paths_48x48s8_seed7_md7", (48, 48), 8, 7, 7, 3, tmp)
+        film_fixture("killeroo_film_80x60s16", (80, 60), 16, 0, 5, tmp)
+        fn = os.path.join(tmp, "mt.bin")
+        run(["-", "--kat-mt", fn])
+        raw = np.fromfile(fn, dtype=np.uint32).reshape(6, 65)
+        np.savez_compressed(os.path.join(OUT, "mt19937_kat.npz"), seeds=raw[:, 0].copy(), out=raw[:, 1:].copy())
+        fn = os.path.join(tmp, "spec.bin")
+        run(["-", "--spectra", fn])
+        raw = np.fromfile(fn, dtype=np.int32)
+        n = raw[0]
+        rec = raw[1:].reshape(n, 3 + 32 + 32).view(np.float32)
+        np.savez_compressed(os.path.join(OUT, "fromrgb_32.npz"), rgb=rec[:, :3].copy(), refl=rec[:, 3:35].copy(),
+                            illum=rec[:, 35:].copy())
+    print("wrote", sorted(os.listdir(OUT)))
+
+
+if __name__ == "__main__":
+    main()

@@ -2,7 +2,7 @@
 profiles/.  Usage:
   python tools/rocpd_summary.py TAG gpurun_out/TAG   -> profiles/TAG_kernel_stats.txt,
                                                          profiles/TAG_pmc.txt,
-                                                         profiles/hbm_traffic_k_render.json
+                                                         profiles/hbm_traffic.json
 Kernel durations are from the 'kernels' view (ns).  HBM traffic per launch follows
 MI355X_MICROARCH.md "HBM [CDNA4]": FETCH_SIZE and WRITE_SIZE come from separate passes
 (TCC slot limits); FETCH_SIZE is doubled (gfx950 tallies 128-B read requests at 64 B),
@@ -62,18 +62,21 @@ def main():
             pl.append("%-28s %-11s %7d %16.1f" % (k, c, len(v), sum(v) / len(v)))
         open(os.path.join(prof, "%s_pmc.txt" % tag), "w").write("\n".join(pl) + "\n")
         print("\n".join(pl))
-        kr = [k for (k, c) in pm if k.startswith("k_render")]
-        if kr:
-            k = kr[0]
-            fetch = pm.get((k, "FETCH_SIZE"), [0])
-            write = pm.get((k, "WRITE_SIZE"), [0])
-            fb = sum(fetch) / len(fetch) * 1024.0
-            wb = sum(write) / len(write) * 1024.0
-            json.dump({"tag": tag, "kernel": k, "res": 700, "spp_per_launch": 16,
-                       "fetch_size_bytes_raw": fb, "write_size_bytes": wb,
-                       "hbm_bytes_per_launch": 2.0 * fb + wb,
-                       "note": "FETCH_SIZE x2 per MI355X_MICROARCH.md gfx950 correction, plus WRITE_SIZE"},
-                      open(os.path.join(prof, "hbm_traffic_k_render.json"), "w"), indent=1)
+        out = {"source": "%s: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of bench.py --steps 1 --warmup 0; "
+                          "FETCH_SIZE x2 (gfx950 correction, MI355X_MICROARCH.md) + WRITE_SIZE" % tag}
+        for k in ("k_trace_closest<false>", "k_trace_shadow<false>", "k_shade<32>"):
+            fetch = pm.get((k, "FETCH_SIZE"))
+            write = pm.get((k, "WRITE_SIZE"))
+            if not fetch or not write:
+                continue
+            # one frame was rendered per pass: total over its launches / launches
+            fb = sum(fetch) * 1024.0
+            wb = sum(write) * 1024.0
+            n = len(fetch)
+            out[k.split("<")[0]] = {"res": 700, "spp": 256, "launches": n, "fetch_bytes_raw_per_launch": fb / n,
+                                    "write_bytes_per_launch": wb / len(write),
+                                    "hbm_bytes_per_launch": (2.0 * fb + wb) / n}
+        json.dump(out, open(os.path.join(prof, "hbm_traffic.json"), "w"), indent=1)
 
 
 if __name__ == "__main__":
