@@ -66,6 +66,24 @@ def cpu_baseline(scene, target_s):
                       "%.1f s on %d threads" % (n, spp, n // spp, dt, threads)}
 
 
+def shard_tiles(ntiles, rank, world):
+    """Tile ids of one rank when ONE frame's tiles are split over ranks (--shard tiles):
+    round-robin, so every rank gets a spread of cheap and expensive image regions."""
+    return np.arange(rank, ntiles, world, dtype=np.int32)
+
+
+def reduce_over_ranks(dist, elapsed, paths, device):
+    """(max elapsed over ranks, total paths over ranks) -- the only collectives of the run."""
+    if dist is None:
+        return elapsed, paths
+    import torch
+    t = torch.tensor([elapsed, paths], dtype=torch.float64, device=device)
+    mx = t.clone()
+    dist.all_reduce(mx[:1], op=dist.ReduceOp.MAX)
+    dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
+    return float(mx[0]), float(t[1])
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -101,7 +119,7 @@ def main():
         c = scene.flat.camera
         tw = (c.sx_end - c.sx_start + args.tile - 1) // args.tile
         th = (c.sy_end - c.sy_start + args.tile - 1) // args.tile
-        tiles = np.arange(rank, tw * th, world, dtype=np.int32)
+        tiles = shard_tiles(tw * th, rank, world)
 
     def step():
         return dev.render(tiles=tiles, tile=(args.tile, args.tile))
@@ -129,15 +147,7 @@ def main():
             a[1] += tm[k]["launches"]
     elapsed = time.perf_counter() - t0
     sync_all()
-    if dist is not None:
-        import torch
-        t = torch.tensor([elapsed, paths], dtype=torch.float64, device="cuda")
-        mx = t.clone()
-        dist.all_reduce(mx[:1], op=dist.ReduceOp.MAX)
-        dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
-        elapsed, total_paths = float(mx[0]), float(t[1])
-    else:
-        total_paths = paths
+    elapsed, total_paths = reduce_over_ranks(dist, elapsed, paths, "cuda")
 
     # roofline of the dominant kernel: algorithmic bytes (from one instrumented, untimed
     # render of the same frame) / its device time (HIP events around every launch)

@@ -17,13 +17,15 @@ extern "C" {
 
 typedef struct pbrthost_scene pbrthost_scene;
 
+#define PBRTHOST_KEEP_SEED 0xffffffffu
+
 /* Overrides of scene-file values: -1 keeps the file's value. */
 typedef struct pbrthost_overrides {
     int32_t xres, yres;   /* Film "xresolution"/"yresolution" */
     int32_t spp;          /* Sampler "pixelsamples" (rounded up to a power of two) */
     int32_t maxdepth;     /* SurfaceIntegrator "path" "maxdepth" */
     int32_t bands;        /* nSpectralSamples: 32 (reference build) or 60 */
-    uint32_t seed;        /* fixed-seed sampler seed */
+    uint32_t seed;        /* fixed-seed sampler seed; PBRTHOST_KEEP_SEED keeps the pack's (0 for .pbrt) */
 } pbrthost_overrides;
 
 /* path: a .pbrt scene file or a .pack scene pack.  Returns 0 or -1 (message in err). */

@@ -40,7 +40,7 @@ int pbrthost_load(const char *path, const pbrthost_overrides *ov, pbrthost_scene
         if (ov->bands > 0 && ov->bands != s->nBands) { delete s; SetErr(err, errlen, "scene pack was built for a different band count"); return -1; }
         if (ov->spp > 0) { uint32_t v = ov->spp; v--; v |= v >> 1; v |= v >> 2; v |= v >> 4; v |= v >> 8; v |= v >> 16; s->spp = v + 1; }
         if (ov->maxdepth >= 0) s->maxDepth = ov->maxdepth;
-        s->seed = ov->seed;
+        if (ov->seed != PBRTHOST_KEEP_SEED) s->seed = ov->seed;
     }
     *out = reinterpret_cast<pbrthost_scene *>(s);
     return 0;

@@ -1152,7 +1152,7 @@ private:
         out->maxDepth = ov.maxdepth >= 0 ? ov.maxdepth : surfParams.FindOneInt("maxdepth", 5);
         int nsamp = ov.spp > 0 ? ov.spp : samplerParams.FindOneInt("pixelsamples", 4);
         out->spp = (int)RoundUpPow2((uint32_t)nsamp);
-        out->seed = ov.seed;
+        out->seed = ov.seed == 0xffffffffu ? 0u : ov.seed;   // PBRTHOST_KEEP_SEED
         out->nBands = spec.n();
         out->bandY.assign(spec.Y(), spec.Y() + spec.n());
         out->yint = spec.yint();

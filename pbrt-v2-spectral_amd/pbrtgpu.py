@@ -69,6 +69,7 @@ class RenderDesc(ctypes.Structure):
 
 STAT_PATHS, STAT_KERNEL_MS, STAT_ACCUM_MS, STAT_ZEROED, STAT_SPILLS, STAT_PASSES = 0, 1, 2, 3, 4, 5
 F_ACCUMULATE, F_COUNT_WORK = 1, 2
+KEEP_SEED = 0xFFFFFFFF
 ABI_VERSION = 2
 
 
@@ -102,7 +103,23 @@ def host_lib():
         _host.pbrthost_set_render.argtypes = [P, ctypes.c_int, ctypes.c_int, ctypes.c_uint32]
         _host.pbrthost_info.argtypes = [P, ctypes.POINTER(ctypes.c_int64), ctypes.c_int]
         _host.pbrthost_write_dat.argtypes = [ctypes.c_char_p, P, P, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+        _host.pbrthost_spectrum_from_rgb.argtypes = [ctypes.c_int, P, ctypes.c_int, P]
     return _host
+
+
+def host_symbols():
+    """Symbols declared in include/pbrthost.h."""
+    return ["pbrthost_load", "pbrthost_free", "pbrthost_flat", "pbrthost_save_pack", "pbrthost_set_render",
+            "pbrthost_info", "pbrthost_write_dat", "pbrthost_spectrum_from_rgb"]
+
+
+def spectrum_from_rgb(rgb, bands=32, illuminant=False):
+    """SampledSpectrum::FromRGB (spectrum.cpp:93-178) as restated by the host front end."""
+    rgb = np.ascontiguousarray(rgb, dtype=np.float32)
+    out = np.zeros(bands, dtype=np.float32)
+    if host_lib().pbrthost_spectrum_from_rgb(bands, rgb.ctypes.data, 1 if illuminant else 0, out.ctypes.data) != 0:
+        raise ValueError("unsupported band count %d" % bands)
+    return out
 
 
 def gpu_lib():
@@ -142,10 +159,10 @@ class Scene:
         host_lib().pbrthost_flat(self._h, ctypes.byref(self.flat))
 
     @staticmethod
-    def load(path, xres=-1, yres=-1, spp=-1, maxdepth=-1, bands=32, seed=0):
+    def load(path, xres=-1, yres=-1, spp=-1, maxdepth=-1, bands=32, seed=None):
         h = P()
         err = ctypes.create_string_buffer(1024)
-        ov = Overrides(xres, yres, spp, maxdepth, bands, seed)
+        ov = Overrides(xres, yres, spp, maxdepth, bands, KEEP_SEED if seed is None else seed)
         if host_lib().pbrthost_load(path.encode(), ctypes.byref(ov), ctypes.byref(h), err, 1024) != 0:
             raise RuntimeError("scene load failed: %s" % err.value.decode())
         return Scene(h)
@@ -298,6 +315,12 @@ class Oracle:
         self.lib.oracle_trace_range.argtypes = [ctypes.POINTER(FlatScene), ctypes.c_long, ctypes.c_long,
                                                 ctypes.c_int]
         self.lib.oracle_trace_range.restype = ctypes.c_long
+        self.lib.oracle_mt_first.argtypes = [ctypes.c_uint32, ctypes.c_int, P]
+
+    def mt_first(self, seed, n):
+        out = np.zeros(n, dtype=np.uint32)
+        self.lib.oracle_mt_first(seed, n, out.ctypes.data)
+        return out
 
     def trace_paths(self, scene, keys):
         keys = np.ascontiguousarray(keys, dtype=np.int32).reshape(-1, 3)

@@ -95,3 +95,64 @@ def test_work_counters(pg, killeroo64, dev):
     assert w["rays"] >= n                      # at least one camera ray per path
     assert w["nodes_closest"] > w["rays"]
     assert 0 < w["hits"] <= w["rays"]
+
+
+def _golden_scene(pg, cfg):
+    from conftest import PACKS
+    w, h, spp, seed, md = [int(v) for v in cfg]
+    return pg.Scene.load(os.path.join(PACKS, "killeroo-simple.pack"), xres=w, yres=h, spp=spp, maxdepth=md,
+                         seed=seed)
+
+
+@pytest.mark.parametrize("name", ["killeroo_paths_64x64s4", "killeroo_paths_48x48s8_seed7_md7"])
+def test_paths_vs_reference_golden(pg, name):
+    """GPU against the reference harness's own per-path radiance (fixed seeds)."""
+    from conftest import GOLDEN
+    g = np.load(os.path.join(GOLDEN, name + ".npz"))
+    scene = _golden_scene(pg, g["config"])
+    with pg.Device(0) as d:
+        d.upload(scene)
+        L = d.trace_paths(g["keys"])
+    ref = g["L"]
+    same = np.all(L.view(np.int32) == ref.view(np.int32), axis=1)
+    rel = np.abs(L - ref).max(axis=1) / np.maximum(np.abs(ref).max(axis=1), 1e-30)
+    assert same.mean() >= 0.99
+    assert (rel > 1e-4).mean() <= 5e-4
+    assert np.abs(L.sum(0) - ref.sum(0)).max() / np.abs(ref.sum(0)).max() < 1e-5
+
+
+def test_film_vs_reference_golden(pg):
+    """Whole-film render against the reference's film (raw sums, incl. neighbour-pixel
+    samples): image L-inf relative error < 1e-4 (BASELINE.json north star)."""
+    from conftest import GOLDEN
+    g = np.load(os.path.join(GOLDEN, "killeroo_film_96x72s16.npz"))
+    scene = _golden_scene(pg, g["config"])
+    with pg.Device(0) as d:
+        d.upload(scene)
+        st = d.render()
+        film = d.film()
+    ref = g["film"]
+    assert st[pg.STAT_SPILLS] > 0
+    assert np.abs(film - ref).max() / np.abs(ref).max() < 1e-4
+    assert np.all(film.view(np.int32) == ref.view(np.int32), axis=2).mean() >= 0.99
+
+
+def test_tile_shards_compose_to_full_frame(pg, killeroo64, dev):
+    """Rendering tile subsets (as ranks do under --shard tiles) and accumulating them gives
+    the full-frame film bit for bit."""
+    dev.render()
+    full = dev.film()
+    c = killeroo64.flat.camera
+    ntiles = ((c.px_count + 15) // 16) * ((c.py_count + 15) // 16)
+    dev.render(tiles=np.arange(0, ntiles, 2))
+    dev.render(tiles=np.arange(1, ntiles, 2), accumulate=True)
+    assert np.array_equal(full.view(np.int32), dev.film().view(np.int32))
+
+
+def test_sample_range_split_and_bad_arguments(pg, killeroo64, dev):
+    with pytest.raises(RuntimeError):
+        dev.render(spp_begin=3, spp_end=2)
+    with pytest.raises(RuntimeError):
+        dev.render(tiles=[10 ** 6])
+    with pytest.raises(RuntimeError):
+        dev.trace_paths(np.array([[10 ** 5, 0, 0]], np.int32))

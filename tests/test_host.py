@@ -1,0 +1,112 @@
+"""Host front end (libpbrthost.so): scene packs, overrides, the .dat writer, and -- where
+the reference's scene files exist -- parsing the unchanged pbrt scene into the same
+flattened scene the committed pack holds."""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+
+from conftest import PACKS, REF_SCENES
+
+PACK = os.path.join(PACKS, "killeroo-simple.pack")
+
+
+def _arr(ptr, n, dtype):
+    if n == 0:
+        return np.zeros(0, dtype)
+    buf = (ctypes.c_char * (n * np.dtype(dtype).itemsize)).from_address(ptr)
+    return np.frombuffer(buf, dtype=dtype).copy()
+
+
+def flat_arrays(scene):
+    f = scene.flat
+    return {
+        "nodes": _arr(f.nodes, f.n_nodes * 8, np.uint32),
+        "prims": _arr(f.prims, f.n_prims * 4, np.int32),
+        "tris": _arr(f.tris, f.n_tris * 4, np.int32),
+        "vert_p": _arr(f.vert_p, f.n_verts * 3, np.uint32),
+        "vert_n": _arr(f.vert_n, f.n_verts * 3, np.uint32),
+        "materials": _arr(f.materials, f.n_materials * 16, np.uint32),
+        "lights": _arr(f.lights, f.n_lights * 44, np.uint32),
+        "spectra": _arr(f.spectra, f.n_spectra_floats, np.uint32),
+        "camera": np.frombuffer(bytes(f.camera), np.uint32).copy(),
+    }
+
+
+def test_pack_info(pg):
+    s = pg.Scene.load(PACK)
+    info = s.info()
+    assert (info["bands"], info["spp"], info["maxdepth"]) == (32, 256, 5)
+    assert (info["width"], info["height"]) == (700, 700)
+    assert info["nodes"] == 131363 and info["prims"] == 66533 and info["tris"] == 66532
+    assert info["quadrics"] == 1 and info["lights"] == 1 and info["bvh_depth"] == 23
+
+
+def test_pack_roundtrip(pg, tmp_path):
+    s = pg.Scene.load(PACK, xres=64, yres=48, spp=8, seed=3)
+    out = str(tmp_path / "rt.pack")
+    s.save_pack(out)
+    t = pg.Scene.load(out)
+    a, b = flat_arrays(s), flat_arrays(t)
+    for k in a:
+        assert np.array_equal(a[k], b[k]), k
+    assert (t.width, t.height, t.spp, t.flat.seed) == (64, 48, 8, 3)
+
+
+def test_overrides(pg):
+    s = pg.Scene.load(PACK, xres=100, yres=50, spp=5, maxdepth=3, seed=9)
+    assert (s.width, s.height) == (100, 50)
+    assert s.spp == 8                       # LDSampler rounds up to a power of two
+    assert s.flat.max_depth == 3 and s.flat.seed == 9
+    c = s.flat.camera
+    assert (c.sx_start, c.sx_end, c.sy_start, c.sy_end) == (0, 101, 0, 51)   # box filter 0.5 border
+    with pytest.raises(RuntimeError):
+        pg.Scene.load(PACK, bands=60)        # a pack holds one band count
+
+
+def test_bad_inputs(pg, tmp_path):
+    with pytest.raises(RuntimeError):
+        pg.Scene.load(str(tmp_path / "missing.pbrt"))
+    bad = tmp_path / "bad.pack"
+    bad.write_bytes(b"not a pack")
+    with pytest.raises(RuntimeError):
+        pg.Scene.load(str(bad))
+
+
+def test_write_dat_layout(pg, tmp_path):
+    s = pg.Scene.load(PACK, xres=6, yres=4, spp=1)
+    film = np.arange(4 * 6 * 32, dtype=np.float32).reshape(4, 6, 32) - 100.0
+    fn = str(tmp_path / "o.dat")
+    s.write_dat(fn, film)
+    raw = open(fn, "rb").read()
+    l1 = raw.index(b"\n")
+    l2 = raw.index(b"\n", l1 + 1)
+    assert raw[:l1] == b"6 4 32"
+    data = np.frombuffer(raw[l2 + 1:], dtype=np.float64)
+    assert data.size == 6 * 4 * 32
+    # SpectralImageFilm::WriteImage (spectralImage.cpp:267-378): the clamp to >= 0 walks a
+    # running offset (x-major) while the copy is indexed y * W + x, so an entry is clamped
+    # only if it was copied before the walk reached it; planes are band-major, x * H + y.
+    W, H, N = 6, 4, 32
+    finalC = np.zeros((W * H, N), np.float32)
+    off = 0
+    for x in range(W):
+        for y in range(H):
+            finalC[y * W + x] = film[y, x]
+            finalC[off] = np.maximum(finalC[off], 0)
+            off += 1
+    expect = np.zeros((N, W * H))
+    for x in range(W):
+        for y in range(H):
+            expect[:, x * H + y] = finalC[y * W + x]
+    assert np.array_equal(data.reshape(N, W * H), expect)
+
+
+@pytest.mark.reference
+def test_frontend_parses_reference_scene_to_pack(pg):
+    s = pg.Scene.load(os.path.join(REF_SCENES, "killeroo-simple.pbrt"), xres=700, yres=700, spp=256)
+    p = pg.Scene.load(PACK)
+    a, b = flat_arrays(s), flat_arrays(p)
+    for k in a:
+        assert np.array_equal(a[k], b[k]), k

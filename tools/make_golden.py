@@ -7,7 +7,7 @@ Fixtures (numpy .npz, inputs + expected outputs only):
   killeroo_paths_64x64s4.npz      per-path radiance of every 5th path (x, y, s keys) of
                                   killeroo-simple at 64x64, 4 spp, seed 0, maxdepth 5
   killeroo_paths_48x48s8_seed7_md7.npz   every 3rd path, 8 spp, seed 7, maxdepth 7 (MT19937 draws)
-  killeroo_film_80x60s16.npz      raw film sums [60][80][32] at 80x60, 16 spp (includes samples
+  killeroo_film_96x72s16.npz      raw film sums [72][96][32] at 96x72, 16 spp (includes 3 samples
                                   that land on neighbouring pixels)
   mt19937_kat.npz                 first 64 outputs of RNG(seed) for 6 seeds
   fromrgb_32.npz                  SampledSpectrum::FromRGB (reflectance and illuminant) for 14
@@ -67,7 +67,7 @@ def main():
     with tempfile.TemporaryDirectory() as tmp:
         paths_fixture("killeroo_paths_64x64s4", (64, 64), 4, 0, 5, 5, tmp)
         paths_fixture("killeroo_paths_48x48s8_seed7_md7", (48, 48), 8, 7, 7, 3, tmp)
-        film_fixture("killeroo_film_80x60s16", (80, 60), 16, 0, 5, tmp)
+        film_fixture("killeroo_film_96x72s16", (96, 72), 16, 0, 5, tmp)
         fn = os.path.join(tmp, "mt.bin")
         run(["-", "--kat-mt", fn])
         raw = np.fromfile(fn, dtype=np.uint32).reshape(6, 65)
