@@ -134,7 +134,9 @@ def test_film_vs_reference_golden(pg):
     ref = g["film"]
     assert st[pg.STAT_SPILLS] > 0
     assert np.abs(film - ref).max() / np.abs(ref).max() < 1e-4
-    assert np.all(film.view(np.int32) == ref.view(np.int32), axis=2).mean() >= 0.99
+    # ~0.7% of paths differ from glibc-float transcendentals in the last ulp (DESIGN.md
+    # §3.2), so a 16-sample pixel is bit-exact with probability ~0.993^16
+    assert np.all(film.view(np.int32) == ref.view(np.int32), axis=2).mean() >= 0.85
 
 
 def test_tile_shards_compose_to_full_frame(pg, killeroo64, dev):
