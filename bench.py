@@ -45,6 +45,26 @@ def trace_bytes(work, kernel):
             + (RAY_BYTES + 4 + QENTRY_BYTES) * work["shadow_rays"])
 
 
+def shade_bytes(work, paths, bands):
+    """algorithmic bytes of k_shade over a frame, from the event counts of
+    the instrumented render.  S = 4*bands (one spectrum); scene gathers per vertex:
+    prim 16 + triangle 16 + 3 vertices x (P 12, N 12, uv 8) + material 64 = 192 B, plus three
+    BSDF-spectrum reads and one emitted-spectrum read."""
+    S = 4.0 * bands
+    cams = paths
+    cont = work["rays"] - work["mis_rays"] - cams          # continuation rays
+    verts = work["hits"] - work["mis_hits"]                # vertices shaded
+    slot_state = 20.0                                      # item, hash, sample, bounce, flags
+    per_vertex = slot_state * 2 + 2 * S + S + 36 + 8 + 192 + 4 * S   # L r/w, beta_b, ray, hit, scene
+    per_cont = S + 36 + 4                                  # beta_{b+1}, ray, queue entry
+    per_shadow = S + 36 + 4 + S                            # A write, ray, queue, A read at finish
+    per_mis = S + 36 + 4 + S + 8                           # B write, ray, queue, B read, hit
+    per_cam = 2 * S + 36 + 4 + slot_state                  # L, beta init, camera ray
+    per_out = S
+    return (verts * per_vertex + cont * per_cont + work["shadow_rays"] * per_shadow
+            + work["mis_rays"] * per_mis + cams * (per_cam + per_out))
+
+
 def cpu_baseline(scene, target_s):
     """CPU restatement (oracle/liboracle.so, TEST INFRASTRUCTURE) on the host cores: all
     samples of pseudo-randomly spread pixels, sized to ~target_s seconds of work."""
@@ -155,30 +175,31 @@ def main():
     dev.render(tiles=tiles, tile=(args.tile, args.tile), count_work=True)
     work = dev.timing()["work"]
     frame_paths = paths / args.steps
-    roof = None
-    if dom in ("k_trace_closest", "k_trace_shadow"):
-        byts = trace_bytes(work, dom)                     # per frame
-        sec = kern[dom][0] / args.steps * 1e-3            # per frame
-        achieved = byts / sec / 1e9
-        launches = kern[dom][1] / args.steps
-        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "kernel": dom,
-                "avg_launch_ms": round(kern[dom][0] / max(kern[dom][1], 1), 4),
-                "launches_per_step": launches, "alg_bytes_per_launch": round(byts / max(launches, 1)),
-                "per_path": {k: round(v / frame_paths, 3) for k, v in work.items()},
-                "kernel_ms_per_step": {k: round(v[0] / args.steps, 2) for k, v in kern.items()}}
-        tf = os.path.join(ROOT, "profiles", "hbm_traffic.json")
-        if os.path.exists(tf):
-            with open(tf) as f:
-                tr = json.load(f)
-            ent = tr.get(dom)
-            if ent and ent.get("res") == args.res and ent.get("spp") == args.spp:
-                roof["traffic"] = ent.get("hbm_bytes_per_launch")
-                roof["traffic_source"] = tr.get("source")
+    if dom == "k_shade":
+        byts = shade_bytes(work, frame_paths, scene.bands)
     else:
-        roof = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
-                "traffic": None, "kernel": dom,
-                "kernel_ms_per_step": {k: round(v[0] / args.steps, 2) for k, v in kern.items()}}
+        byts = trace_bytes(work, dom)                     # per frame
+    sec = kern[dom][0] / args.steps * 1e-3                # per frame
+    achieved = byts / sec / 1e9
+    launches = kern[dom][1] / args.steps
+    roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "kernel": dom,
+            "avg_launch_ms": round(kern[dom][0] / max(kern[dom][1], 1), 4),
+            "launches_per_step": launches, "alg_bytes_per_launch": round(byts / max(launches, 1)),
+            "per_path": {k: round(v / frame_paths, 3) for k, v in work.items()},
+            "kernel_ms_per_step": {k: round(v[0] / args.steps, 2) for k, v in kern.items()},
+            "kernel_alg_GBps": {
+                "k_trace_closest": round(trace_bytes(work, "k_trace_closest") / (kern["k_trace_closest"][0] / args.steps * 1e-3) / 1e9, 1),
+                "k_trace_shadow": round(trace_bytes(work, "k_trace_shadow") / (kern["k_trace_shadow"][0] / args.steps * 1e-3) / 1e9, 1),
+                "k_shade": round(shade_bytes(work, frame_paths, scene.bands) / (kern["k_shade"][0] / args.steps * 1e-3) / 1e9, 1)}}
+    tf = os.path.join(ROOT, "profiles", "hbm_traffic.json")
+    if os.path.exists(tf):
+        with open(tf) as f:
+            tr = json.load(f)
+        ent = tr.get(dom)
+        if ent and ent.get("res") == args.res and ent.get("spp") == args.spp:
+            roof["traffic"] = ent.get("hbm_bytes_per_launch")
+            roof["traffic_source"] = tr.get("source")
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:

@@ -211,7 +211,7 @@ int pbrtgpu_path_stats(pbrtgpu_ctx *ctx, const int32_t *keys, int32_t n, uint64_
  * (+ path regeneration), 3 film accumulation.  work[] (with PBRTGPU_F_COUNT_WORK, or after
  * pbrtgpu_path_stats): closest rays, shadow rays, BVH nodes visited by closest rays, by
  * shadow rays, triangle tests by closest rays, by shadow rays, quadric tests by closest
- * rays, by shadow rays, closest hits, 0, 0, 0. */
+ * rays, by shadow rays, closest hits, MIS rays (among the closest rays), MIS hits, 0. */
 typedef struct pbrtgpu_timing {
     double ms[4];
     int32_t launches[4];

@@ -7,8 +7,9 @@
  * Parity pinning: compiled with -DORACLE_LIBM_FLOAT (glibc float transcendentals, as the
  * reference build) it reproduces the reference harness (oracle/_ref, which runs the
  * reference's own PathIntegrator/BVH/BSDF/light/camera code) bit for bit; compiled
- * without it, sinf/cosf/powf/expf/acosf/atan2f/tanf/atanf are evaluated in double and
- * rounded once (the definition the HIP kernels implement), see DESIGN.md §3.2.
+ * without it, sinf/cosf/powf/expf/acosf/atan2f/tanf/atanf are the double-precision
+ * algorithms of include/pbrt_fmath.h rounded once to float (the definition the HIP
+ * kernels implement, from the same header), see DESIGN.md §3.2.
  *
  * It consumes the flattened scene of include/pbrtgpu.h and follows, function by function:
  *   samplerrenderer.cpp:60-164,225-247  render loop, NaN/inf guard, SamplerRenderer::Li
@@ -41,6 +42,7 @@
 #define INV_TWOPI_F 0.15915494309189533577f
 #define ONE_MINUS_EPS 0x1.fffffep-1f
 
+#include "pbrt_fmath.h"
 #ifdef ORACLE_LIBM_FLOAT
 #define SINF sinf
 #define COSF cosf
@@ -51,14 +53,15 @@
 #define TANF tanf
 #define ATANF atanf
 #else
-static inline float SINF(float x) { return (float)sin((double)x); }
-static inline float COSF(float x) { return (float)cos((double)x); }
-static inline float POWF(float x, float y) { return (float)pow((double)x, (double)y); }
-static inline float EXPF(float x) { return (float)exp((double)x); }
-static inline float ACOSF(float x) { return (float)acos((double)x); }
-static inline float ATAN2F(float y, float x) { return (float)atan2((double)y, (double)x); }
-static inline float TANF(float x) { return (float)tan((double)x); }
-static inline float ATANF(float x) { return (float)atan((double)x); }
+/* the parity definition shared with the GPU: include/pbrt_fmath.h */
+static inline float SINF(float x) { return (float)pbrt_fm_sin((double)x); }
+static inline float COSF(float x) { return (float)pbrt_fm_cos((double)x); }
+static inline float POWF(float x, float y) { return (float)pbrt_fm_pow((double)x, (double)y); }
+static inline float EXPF(float x) { return (float)pbrt_fm_exp((double)x); }
+static inline float ACOSF(float x) { return (float)pbrt_fm_acos((double)x); }
+static inline float ATAN2F(float y, float x) { return (float)pbrt_fm_atan2((double)y, (double)x); }
+static inline float TANF(float x) { return (float)pbrt_fm_tan((double)x); }
+static inline float ATANF(float x) { return (float)pbrt_fm_atan((double)x); }
 #endif
 
 /* ------------------------------------------------------------------ vector math */

@@ -15,24 +15,43 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include "pbrtgpu.h"
+#include "pbrt_fmath.h"
 
 namespace pgd {
 
 #define PGD_INLINE __device__ __forceinline__
+// large shading routines with several call sites: one out-of-line copy each keeps the shade
+// kernel's code (instruction-cache footprint) small
+#ifdef PGD_OUTLINE
+#define PGD_HEAVY __device__ __attribute__((noinline))
+#else
+#define PGD_HEAVY __device__ __forceinline__
+#endif
 #define PGD_HD __host__ __device__ __forceinline__
 static constexpr float kPi = 3.14159265358979323846f;
 static constexpr float kInvPi = 0.31830988618379067154f;
 static constexpr float kInvTwoPi = 0.15915494309189533577f;
 static constexpr float kOneMinusEps = 0x1.fffffep-1f;
 
-#define PGD_MATHFN __device__ __attribute__((noinline))
-PGD_MATHFN float SINF(float x) { return (float)sin((double)x); }
-PGD_MATHFN float COSF(float x) { return (float)cos((double)x); }
-PGD_MATHFN float POWF(float x, float y) { return (float)pow((double)x, (double)y); }
-PGD_MATHFN float ACOSF(float x) { return (float)acos((double)x); }
-PGD_MATHFN float ATAN2F(float y, float x) { return (float)atan2((double)y, (double)x); }
-PGD_MATHFN float TANF(float x) { return (float)tan((double)x); }
-PGD_MATHFN float ATANF(float x) { return (float)atan((double)x); }
+// transcendentals: the parity definition of DESIGN.md §3.2, (float) f((double) x) with the
+// double algorithms of include/pbrt_fmath.h (shared with the CPU oracle; inline, no calls)
+#ifndef PGD_EXPERIMENT_FASTMATH
+PGD_INLINE float SINF(float x) { return (float)pbrt_fm_sin((double)x); }
+PGD_INLINE float COSF(float x) { return (float)pbrt_fm_cos((double)x); }
+PGD_INLINE float POWF(float x, float y) { return (float)pbrt_fm_pow((double)x, (double)y); }
+PGD_INLINE float ACOSF(float x) { return (float)pbrt_fm_acos((double)x); }
+PGD_INLINE float ATAN2F(float y, float x) { return (float)pbrt_fm_atan2((double)y, (double)x); }
+PGD_INLINE float TANF(float x) { return (float)pbrt_fm_tan((double)x); }
+PGD_INLINE float ATANF(float x) { return (float)pbrt_fm_atan((double)x); }
+#else   // timing experiment only (not the parity definition): float library functions
+PGD_INLINE float SINF(float x) { return __sinf(x); }
+PGD_INLINE float COSF(float x) { return __cosf(x); }
+PGD_INLINE float POWF(float x, float y) { return __powf(x, y); }
+PGD_INLINE float ACOSF(float x) { return acosf(x); }
+PGD_INLINE float ATAN2F(float y, float x) { return atan2f(y, x); }
+PGD_INLINE float TANF(float x) { return __tanf(x); }
+PGD_INLINE float ATANF(float x) { return atanf(x); }
+#endif
 
 // ------------------------------------------------------------------ vectors
 struct V { float x, y, z; };
@@ -449,7 +468,7 @@ PGD_INLINE float shape_area(const DevScene &S, int type, int idx) {
     if (type == PBRTGPU_SHAPE_SPHERE) return q.phi_max * q.radius * (q.zmax - q.zmin);
     return q.phi_max * 0.5f * (q.radius * q.radius - q.inner_radius * q.inner_radius);
 }
-PGD_INLINE bool shape_intersect(const DevScene &S, int type, int idx, const Ray &r, float *tHit, float *eps, DG *dg) {
+PGD_HEAVY bool shape_intersect(const DevScene &S, int type, int idx, const Ray &r, float *tHit, float *eps, DG *dg) {
     if (type == PBRTGPU_SHAPE_TRIANGLE) return tri_intersect(S, idx, r, tHit, eps, dg);
     if (type == PBRTGPU_SHAPE_SPHERE) return sphere_intersect(S.quads[idx], r, tHit, eps, dg);
     return disk_intersect(S.quads[idx], r, tHit, eps, dg);
@@ -566,7 +585,7 @@ PGD_INLINE bool bvh_intersectP(const DevScene &S, Stack &st, const Ray &ray) {
     return false;
 }
 struct Isect { DG dg; float rayEps; int prim; };
-PGD_INLINE void isect_fill(const DevScene &S, const Ray &ray, int prim, float t, Isect &is) {
+PGD_HEAVY void isect_fill(const DevScene &S, const Ray &ray, int prim, float t, Isect &is) {
     const pbrtgpu_prim pr = S.prims[prim];
     Ray r = ray;
     r.maxt = t;
@@ -838,7 +857,7 @@ PGD_INLINE float bsdf_pdf(const BSDF &bs, V woW, V wiW, int flags) {
     return m > 0 ? pdf / m : 0.f;
 }
 // BSDF::Sample_f (reflection.cpp:514-568)
-PGD_INLINE void bsdf_sample_f(const BSDF &bs, V woW, V *wiW, float u0, float u1, float uc, float *pdf, int flags,
+PGD_HEAVY void bsdf_sample_f(const BSDF &bs, V woW, V *wiW, float u0, float u1, float uc, float *pdf, int flags,
                               int *sampledType, FVal &F) {
     int matching = 0;
 #pragma unroll
@@ -881,7 +900,7 @@ PGD_INLINE void bsdf_sample_f(const BSDF &bs, V woW, V *wiW, float u0, float u1,
 }
 
 // Intersection::GetBSDF -> GetShadingGeometry -> Material::GetBSDF (+ Bump, material.cpp:39-81)
-PGD_INLINE void get_bsdf(const DevScene &S, const Isect &is, BSDF &bs, V *pOut, V *nOut) {
+PGD_HEAVY void get_bsdf(const DevScene &S, const Isect &is, BSDF &bs, V *pOut, V *nOut) {
     const pbrtgpu_prim pr = S.prims[is.prim];
     const pbrtgpu_material &mt = S.mats[pr.material];
     DG dgs;
@@ -1042,7 +1061,7 @@ PGD_INLINE int sample_discrete(const pbrtgpu_light_shape *ls, int n, float u) {
 }
 struct Seg { V o, d; float mint, maxt; };
 // Light::Sample_L; Li = scale * Ls  (scale = 1 area, 1/d^2 point); returns scale, Ls via pointer
-PGD_INLINE float light_sample_L(const DevScene &S, const pbrtgpu_light &L, V p, float pEps, const float u[3],
+PGD_HEAVY float light_sample_L(const DevScene &S, const pbrtgpu_light &L, V p, float pEps, const float u[3],
                                 V *wi, float *pdf, Seg *vis, bool *litByArea, bool *isPoint) {
     if (L.type == PBRTGPU_LIGHT_POINT) {
         V lp = v3(L.pos[0], L.pos[1], L.pos[2]);
@@ -1079,7 +1098,7 @@ PGD_INLINE float light_sample_L(const DevScene &S, const pbrtgpu_light &L, V p, 
     *litByArea = vdot(ns, vneg(*wi)) > 0.f;
     return 1.f;
 }
-PGD_INLINE float light_pdf(const DevScene &S, const pbrtgpu_light &L, V p, V wi) {
+PGD_HEAVY float light_pdf(const DevScene &S, const pbrtgpu_light &L, V p, V wi) {
     if (L.type == PBRTGPU_LIGHT_POINT) return 0.;
     const pbrtgpu_light_shape *shs = S.lightShapes + L.shape_offset;
     float pp = 0.f;

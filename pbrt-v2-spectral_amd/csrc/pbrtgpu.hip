@@ -51,6 +51,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_closest(DevScene S, PathS
     st.stride = blockDim.x;
     const uint32_t n = P.cnt[CNT_QC(q)];
     const uint32_t *Q = P.qC + (size_t)q * 2 * P.cap;
+    uint32_t nM = 0, hM = 0;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const uint32_t e = Q[i];
         const int slot = (int)(e >> 1), kind = (int)(e & 1);
@@ -60,6 +61,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_closest(DevScene S, PathS
         if (!bvh_intersect(S, st, r, &prim, &t)) prim = -1;
         P.hitPrim[(size_t)kind * P.cap + slot] = prim;
         P.hitT[(size_t)kind * P.cap + slot] = t;
+        if (STATS && kind == RAY_M) { nM++; hM += prim >= 0 ? 1u : 0u; }
     }
     if (STATS) {
         unsigned long long *w = reinterpret_cast<unsigned long long *>(P.cnt + CNT_WORK);
@@ -68,6 +70,8 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_closest(DevScene S, PathS
         atomicAdd(&w[W_TRIS_C], (unsigned long long)st.cTris);
         atomicAdd(&w[W_QUADS_C], (unsigned long long)st.cQuads);
         atomicAdd(&w[W_HITS], (unsigned long long)st.cHits);
+        atomicAdd(&w[W_RAYS_M], (unsigned long long)nM);
+        atomicAdd(&w[W_HITS_M], (unsigned long long)hM);
     }
 }
 

@@ -41,7 +41,7 @@ enum { RAY_C = 0, RAY_M = 1, RAY_S = 2 };
 #define CNT_QS(q) (64 + 32 * (q))     // shadow queue size
 enum { CNT_NEXT = 128, CNT_ZEROED = 160, CNT_WORK = 192, CNT_WORDS = 288 };
 enum { W_RAYS = 0, W_SHADOW = 1, W_NODES_C = 2, W_NODES_S = 3, W_TRIS_C = 4, W_TRIS_S = 5, W_QUADS_C = 6, W_QUADS_S = 7,
-       W_HITS = 8, W_COUNT = 12 };
+       W_HITS = 8, W_RAYS_M = 9, W_HITS_M = 10, W_COUNT = 12 };
 
 struct PathSoA {
     int cap;
@@ -259,7 +259,11 @@ PGD_INLINE Pushes shade_vertex(const DevScene &S, const PathSoA &P, int slot, in
     const int nLights = S.nLights;
     fl &= ~(PF_PEND | PF_PA | PF_PB | PF_CONT | (0xffffffu << PF_LIGHT_SHIFT));
     FVal F;
+#ifdef PGD_EXPERIMENT_NO_NEE
+    if (false) {
+#else
     if (nLights > 0) {
+#endif
         float ul[3], ub[3], ulnum;
         if (!useMT) {
             float u2[2];

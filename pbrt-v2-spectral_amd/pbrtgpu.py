@@ -78,7 +78,7 @@ class Timing(ctypes.Structure):
                 ("work", ctypes.c_uint64 * 12)]
     KERNELS = ("k_trace_closest", "k_trace_shadow", "k_shade", "k_accum")
     WORK = ("rays", "shadow_rays", "nodes_closest", "nodes_shadow", "tris_closest", "tris_shadow", "quads_closest",
-            "quads_shadow", "hits")
+            "quads_shadow", "hits", "mis_rays", "mis_hits")
 
 _host = None
 _gpu = None
@@ -86,6 +86,8 @@ _gpu = None
 
 def _load(name):
     path = os.path.join(LIBDIR, name)
+    if name == "libpbrtgpu.so" and os.environ.get("PBRTGPU_LIB"):   # timing experiments only
+        path = os.environ["PBRTGPU_LIB"]
     if not os.path.exists(path):
         raise RuntimeError("%s not built (run __graft_entry__.build() or make -C pbrt-v2-spectral_amd)" % path)
     return ctypes.CDLL(path)
