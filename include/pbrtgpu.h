@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define PBRTGPU_ABI_VERSION 2
+#define PBRTGPU_ABI_VERSION 3
 #define PBRTGPU_MAX_BANDS 64
 
 #define PBRTGPU_E_INVALID   (-1)
@@ -46,7 +46,7 @@ typedef struct pbrtgpu_bvh_node {
     uint32_t meta;
 } pbrtgpu_bvh_node;
 
-enum { PBRTGPU_SHAPE_TRIANGLE = 0, PBRTGPU_SHAPE_SPHERE = 1, PBRTGPU_SHAPE_DISK = 2 };
+enum { PBRTGPU_SHAPE_TRIANGLE = 0, PBRTGPU_SHAPE_SPHERE = 1, PBRTGPU_SHAPE_DISK = 2, PBRTGPU_SHAPE_INSTANCE = 3 };
 
 /* one GeometricPrimitive, in BVH (orderedPrims) order */
 typedef struct pbrtgpu_prim {
@@ -120,6 +120,24 @@ typedef struct pbrtgpu_light_shape {
     float cdf;             /* Distribution1D cdf[i+1] of the area distribution */
 } pbrtgpu_light_shape;
 
+/* TransformedPrimitive with an AnimatedTransform world->primitive (primitive.cpp:87-116,
+ * transform.cpp:356-381): the top-level prim of shape_type PBRTGPU_SHAPE_INSTANCE points
+ * here.  Its primitives (refined in object space) are prims[] entries whose prim_instance is
+ * this index; they sit under the nested BVH rooted at node `root` (bvh.cpp, maxPrims 1),
+ * or are the single primitive `single_prim` when refinement gave one primitive. */
+typedef struct pbrtgpu_instance {
+    int32_t root;             /* root node of the nested BVH, -1 if single_prim is used */
+    int32_t single_prim;      /* the one primitive, -1 if root is used */
+    int32_t animated;         /* AnimatedTransform::actuallyAnimated */
+    int32_t pad0;
+    float start_time, end_time, pad1, pad2;
+    float start_m[16], start_minv[16];   /* world->primitive at start_time (m, mInv) */
+    float end_m[16], end_minv[16];       /* ... at end_time */
+    float T[2][4];            /* Decompose(): translation (xyz, 0) */
+    float R[2][4];            /* Decompose(): rotation quaternion (x, y, z, w) */
+    float S[2][16];           /* Decompose(): scale matrix */
+} pbrtgpu_instance;
+
 /* PerspectiveCamera (perspective.cpp, camera.cpp:84-103) + film/sample extent
  * (spectralImage.cpp:40-50, 176-185) */
 typedef struct pbrtgpu_camera {
@@ -152,6 +170,8 @@ typedef struct pbrtgpu_flat_scene {
     int32_t n_lights;  const pbrtgpu_light *lights;
     int32_t n_light_shapes; const pbrtgpu_light_shape *light_shapes;
     int32_t n_spectra_floats; const float *spectra;   /* spectrum pool */
+    int32_t n_instances; const pbrtgpu_instance *instances;
+    const int32_t *prim_instance;                  /* [n_prims]: owning instance or -1 */
 } pbrtgpu_flat_scene;
 
 /* ---- render description ----------------------------------------------------------- */

@@ -316,7 +316,9 @@ static int solve2x2(const float A[2][2], const float B[2], float *x0, float *x1)
     return 1;
 }
 /* Triangle::GetShadingGeometry (trianglemesh.cpp:285-360) */
-static void tri_shading(const Ctx *c, int ti, const DG *dg, DG *dgs) {
+/* obj2wMinv: mInv of the ObjectToWorld passed to GetShadingGeometry (the mesh's, or the
+ * instance-composed one set by TransformedPrimitive::Intersect) */
+static void tri_shading(const Ctx *c, int ti, const float *obj2wMinv, const DG *dg, DG *dgs) {
     const pbrtgpu_triangle *t = &c->s->tris[ti];
     const pbrtgpu_mesh *m = &c->s->meshes[t->mesh];
     if (!m->has_normals) { *dgs = *dg; return; }
@@ -330,7 +332,7 @@ static void tri_shading(const Ctx *c, int ti, const DG *dg, DG *dgs) {
     V n0 = vnormal(c, t->v[0]), n1 = vnormal(c, t->v[1]), n2 = vnormal(c, t->v[2]);
     /* b[0] * n[v0] + b[1] * n[v1] + b[2] * n[v2]  (Normal operator*(float, Normal) = (f*x,...)) */
     V ni = vadd(vadd(vmul(n0, b[0]), vmul(n1, b[1])), vmul(n2, b[2]));
-    V ns = vnorm(xnormal(m->o2w_minv, ni));
+    V ns = vnorm(xnormal(obj2wMinv, ni));
     V ss = vnorm(dg->dpdu);
     V ts = vcross(ss, ns);
     if (vlen2(ts) > 0.f) { ts = vnorm(ts); ss = vcross(ts, ns); }
@@ -349,7 +351,7 @@ static void tri_shading(const Ctx *c, int ti, const DG *dg, DG *dgs) {
             dndv = vmul(vadd(vmul(dn1, -du2), vmul(dn2, du1)), invdet);
         }
     }
-    dg_init(dgs, dg->p, ss, ts, xnormal(m->o2w_minv, dndu), xnormal(m->o2w_minv, dndv), dg->u, dg->v,
+    dg_init(dgs, dg->p, ss, ts, xnormal(obj2wMinv, dndu), xnormal(obj2wMinv, dndv), dg->u, dg->v,
             m->reverse_orientation ^ m->swaps_handedness);
 }
 
@@ -496,30 +498,161 @@ static inline int bbox_hit(const pbrtgpu_bvh_node *n, const Ray *ray, V invDir, 
     return (tmin < ray->maxt) && (tmax > ray->mint);
 }
 typedef struct { int prim; float t; } Hit;
-/* BVHAccel::Intersect (bvh.cpp:380-432); updates ray->maxt like GeometricPrimitive */
-static int bvh_intersect(const Ctx *c, Ray *ray, Hit *hit) {
+
+/* ---- Matrix4x4 / Transform / Quaternion / AnimatedTransform (transform.cpp, quaternion.cpp) */
+static void m4_mul(const float *a, const float *b, float *r) {   /* Matrix4x4::Mul */
+    float t[16];
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j)
+            t[4 * i + j] = a[4 * i + 0] * b[0 * 4 + j] + a[4 * i + 1] * b[1 * 4 + j] + a[4 * i + 2] * b[2 * 4 + j] +
+                           a[4 * i + 3] * b[3 * 4 + j];
+    memcpy(r, t, sizeof(t));
+}
+static void m4_identity(float *m) { memset(m, 0, 64); m[0] = m[5] = m[10] = m[15] = 1.f; }
+static void m4_inverse(const float *m, float *out) {   /* transform.cpp:68-130, Gauss-Jordan, full pivoting */
+    int indxc[4], indxr[4], ipiv[4] = {0, 0, 0, 0};
+    float minv[4][4];
+    memcpy(minv, m, 64);
+    for (int i = 0; i < 4; i++) {
+        int irow = -1, icol = -1;
+        float big = 0.;
+        for (int j = 0; j < 4; j++)
+            if (ipiv[j] != 1)
+                for (int k = 0; k < 4; k++)
+                    if (ipiv[k] == 0 && fabsf(minv[j][k]) >= big) { big = (float)fabsf(minv[j][k]); irow = j; icol = k; }
+        ++ipiv[icol];
+        if (irow != icol)
+            for (int k = 0; k < 4; ++k) { float t = minv[irow][k]; minv[irow][k] = minv[icol][k]; minv[icol][k] = t; }
+        indxr[i] = irow;
+        indxc[i] = icol;
+        float pivinv = 1.f / minv[icol][icol];
+        minv[icol][icol] = 1.f;
+        for (int j = 0; j < 4; j++) minv[icol][j] *= pivinv;
+        for (int j = 0; j < 4; j++)
+            if (j != icol) {
+                float save = minv[j][icol];
+                minv[j][icol] = 0;
+                for (int k = 0; k < 4; k++) minv[j][k] -= minv[icol][k] * save;
+            }
+    }
+    for (int j = 3; j >= 0; j--)
+        if (indxr[j] != indxc[j])
+            for (int k = 0; k < 4; k++) { float t = minv[k][indxr[j]]; minv[k][indxr[j]] = minv[k][indxc[j]]; minv[k][indxc[j]] = t; }
+    memcpy(out, minv, 64);
+}
+typedef struct { float x, y, z, w; } Quat;
+static float qdot(Quat a, Quat b) { return (a.x * b.x + a.y * b.y + a.z * b.z) + a.w * b.w; }
+static Quat qnormalize(Quat q) {   /* q / sqrtf(Dot(q, q)): Vector operator/ (reciprocal), w / d */
+    float d = sqrtf(qdot(q, q));
+    float inv = 1.f / d;
+    Quat r = {q.x * inv, q.y * inv, q.z * inv, q.w / d};
+    return r;
+}
+static Quat qscale(Quat q, float f) { Quat r = {q.x * f, q.y * f, q.z * f, q.w * f}; return r; }
+static Quat qadd(Quat a, Quat b) { Quat r = {a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w}; return r; }
+static Quat qsub(Quat a, Quat b) { Quat r = {a.x - b.x, a.y - b.y, a.z - b.z, a.w - b.w}; return r; }
+static Quat slerp(float t, Quat q1, Quat q2) {   /* quaternion.cpp:39-49 */
+    float cosTheta = qdot(q1, q2);
+    if (cosTheta > .9995f) return qnormalize(qadd(qscale(q1, 1.f - t), qscale(q2, t)));
+    float theta = ACOSF(clampf(cosTheta, -1.f, 1.f));
+    float thetap = theta * t;
+    Quat qperp = qnormalize(qsub(q2, qscale(q1, cosTheta)));
+    return qadd(qscale(q1, COSF(thetap)), qscale(qperp, SINF(thetap)));
+}
+/* Quaternion::ToTransform (quaternion.cpp:52-70): m = Transpose(M), mInv = M */
+static void quat_to_m(Quat q, float *m, float *minv) {
+    float xx = q.x * q.x, yy = q.y * q.y, zz = q.z * q.z;
+    float xy = q.x * q.y, xz = q.x * q.z, yz = q.y * q.z;
+    float wx = q.x * q.w, wy = q.y * q.w, wz = q.z * q.w;
+    float M[16];
+    m4_identity(M);
+    M[0] = 1.f - 2.f * (yy + zz); M[1] = 2.f * (xy + wz); M[2] = 2.f * (xz - wy);
+    M[4] = 2.f * (xy - wz); M[5] = 1.f - 2.f * (xx + zz); M[6] = 2.f * (yz + wx);
+    M[8] = 2.f * (xz + wy); M[9] = 2.f * (yz - wx); M[10] = 1.f - 2.f * (xx + yy);
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j) m[4 * i + j] = M[4 * j + i];
+    if (minv) memcpy(minv, M, 64);
+}
+/* AnimatedTransform::Interpolate (transform.cpp:356-381): world->primitive (m, mInv) */
+static void inst_interp(const pbrtgpu_instance *I, float time, float *m, float *minv) {
+    if (!I->animated || time <= I->start_time) { memcpy(m, I->start_m, 64); if (minv) memcpy(minv, I->start_minv, 64); return; }
+    if (time >= I->end_time) { memcpy(m, I->end_m, 64); if (minv) memcpy(minv, I->end_minv, 64); return; }
+    float dt = (time - I->start_time) / (I->end_time - I->start_time);
+    /* Vector trans = (1-dt) * T[0] + dt * T[1] */
+    float tr[3];
+    for (int k = 0; k < 3; ++k) tr[k] = (1.f - dt) * I->T[0][k] + dt * I->T[1][k];
+    Quat r0 = {I->R[0][0], I->R[0][1], I->R[0][2], I->R[0][3]}, r1 = {I->R[1][0], I->R[1][1], I->R[1][2], I->R[1][3]};
+    Quat rot = slerp(dt, r0, r1);
+    float S[16];
+    m4_identity(S);
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) S[4 * i + j] = lerpf(dt, I->S[0][4 * i + j], I->S[1][4 * i + j]);
+    /* Translate(trans) * rotate.ToTransform() * Transform(scale) */
+    float T[16], Tinv[16], R[16], Rinv[16], TR[16];
+    m4_identity(T); T[3] = tr[0]; T[7] = tr[1]; T[11] = tr[2];
+    quat_to_m(rot, R, Rinv);
+    m4_mul(T, R, TR);
+    m4_mul(TR, S, m);
+    if (minv) {
+        float Sinv[16], RiTi[16];
+        m4_identity(Tinv); Tinv[3] = -tr[0]; Tinv[7] = -tr[1]; Tinv[11] = -tr[2];
+        m4_inverse(S, Sinv);
+        m4_mul(Rinv, Tinv, RiTi);
+        m4_mul(Sinv, RiTi, minv);
+    }
+}
+static int m4_is_identity(const float *m) {
+    for (int i = 0; i < 16; ++i)
+        if (m[i] != ((i % 5 == 0) ? 1.f : 0.f)) return 0;
+    return 1;
+}
+static Ray xray(const float *m, const Ray *r) {   /* Transform::operator()(Ray) */
+    Ray o = *r;
+    o.o = xpoint(m, r->o);
+    o.d = xvec(m, r->d);
+    return o;
+}
+
+/* BVHAccel::Intersect (bvh.cpp:380-432) from node `root`; prims of shape_type INSTANCE run
+ * TransformedPrimitive::Intersect (primitive.cpp:87-116) on their nested BVH.  Updates
+ * ray->maxt like GeometricPrimitive; anyhit = IntersectP (bvh.cpp:435-481). */
+static int bvh_walk(const Ctx *c, uint32_t root, Ray *ray, Hit *hit, int anyhit);
+static int prim_test(const Ctx *c, int pi, Ray *ray, Hit *hit, int anyhit) {
+    const pbrtgpu_prim *pr = &c->s->prims[pi];
+    if (pr->shape_type == PBRTGPU_SHAPE_INSTANCE) {
+        const pbrtgpu_instance *I = &c->s->instances[pr->shape_index];
+        float m[16];
+        inst_interp(I, ray->time, m, NULL);
+        Ray r = xray(m, ray);
+        int found;
+        if (I->single_prim >= 0) found = prim_test(c, I->single_prim, &r, hit, anyhit);
+        else found = bvh_walk(c, (uint32_t)I->root, &r, hit, anyhit);
+        if (found && !anyhit) ray->maxt = r.maxt;
+        return found;
+    }
+    float t, eps;
+    if (!shape_intersect(c, pr->shape_type, pr->shape_index, ray, &t, &eps, NULL)) return 0;
+    if (!anyhit) { ray->maxt = t; hit->prim = pi; hit->t = t; }
+    return 1;
+}
+static int bvh_walk(const Ctx *c, uint32_t root, Ray *ray, Hit *hit, int anyhit) {
     const pbrtgpu_bvh_node *nodes = c->s->nodes;
     V invDir = v3(1.f / ray->d.x, 1.f / ray->d.y, 1.f / ray->d.z);
     int dirIsNeg[3] = {invDir.x < 0, invDir.y < 0, invDir.z < 0};
     uint32_t todo[64];
     int todoOffset = 0;
-    uint32_t nodeNum = 0;
+    uint32_t nodeNum = root;
     int found = 0;
     for (;;) {
         const pbrtgpu_bvh_node *node = &nodes[nodeNum];
         if (bbox_hit(node, ray, invDir, dirIsNeg)) {
             uint32_t np = node->meta & 0xff;
             if (np > 0) {
-                for (uint32_t i = 0; i < np; ++i) {
-                    const pbrtgpu_prim *pr = &c->s->prims[node->offset + i];
-                    float t, eps;
-                    if (shape_intersect(c, pr->shape_type, pr->shape_index, ray, &t, &eps, NULL)) {
-                        ray->maxt = t;
-                        hit->prim = (int)(node->offset + i);
-                        hit->t = t;
+                for (uint32_t i = 0; i < np; ++i)
+                    if (prim_test(c, (int)(node->offset + i), ray, hit, anyhit)) {
+                        if (anyhit) return 1;
                         found = 1;
                     }
-                }
                 if (todoOffset == 0) break;
                 nodeNum = todo[--todoOffset];
             } else {
@@ -534,46 +667,46 @@ static int bvh_intersect(const Ctx *c, Ray *ray, Hit *hit) {
     }
     return found;
 }
+static int bvh_intersect(const Ctx *c, Ray *ray, Hit *hit) { return bvh_walk(c, 0, ray, hit, 0); }
 static int bvh_intersectP(const Ctx *c, const Ray *ray) {
-    const pbrtgpu_bvh_node *nodes = c->s->nodes;
-    V invDir = v3(1.f / ray->d.x, 1.f / ray->d.y, 1.f / ray->d.z);
-    int dirIsNeg[3] = {invDir.x < 0, invDir.y < 0, invDir.z < 0};
-    uint32_t todo[64];
-    int todoOffset = 0;
-    uint32_t nodeNum = 0;
-    for (;;) {
-        const pbrtgpu_bvh_node *node = &nodes[nodeNum];
-        if (bbox_hit(node, ray, invDir, dirIsNeg)) {
-            uint32_t np = node->meta & 0xff;
-            if (np > 0) {
-                for (uint32_t i = 0; i < np; ++i) {
-                    const pbrtgpu_prim *pr = &c->s->prims[node->offset + i];
-                    float t, eps;
-                    if (shape_intersect(c, pr->shape_type, pr->shape_index, ray, &t, &eps, NULL)) return 1;
-                }
-                if (todoOffset == 0) break;
-                nodeNum = todo[--todoOffset];
-            } else {
-                uint32_t axis = (node->meta >> 8) & 0xff;
-                if (dirIsNeg[axis]) { todo[todoOffset++] = nodeNum + 1; nodeNum = node->offset; }
-                else { todo[todoOffset++] = node->offset; nodeNum = nodeNum + 1; }
-            }
-        } else {
-            if (todoOffset == 0) break;
-            nodeNum = todo[--todoOffset];
-        }
-    }
-    return 0;
+    Ray r = *ray;
+    Hit h;
+    return bvh_walk(c, 0, &r, &h, 1);
 }
-/* full intersection record for a recorded closest hit */
-typedef struct { DG dg; float rayEps; int prim; } Isect;
+/* full intersection record for a recorded closest hit; for primitives of a transformed
+ * instance the object-space record is moved to world space as TransformedPrimitive does */
+typedef struct { DG dg; float rayEps; int prim; int inst; float nmat[16]; } Isect;
 static void isect_fill(const Ctx *c, const Ray *ray, const Hit *h, Isect *is) {
     const pbrtgpu_prim *pr = &c->s->prims[h->prim];
+    int inst = c->s->prim_instance ? c->s->prim_instance[h->prim] : -1;
     Ray r = *ray;
     r.maxt = h->t;
     float t;
-    shape_intersect(c, pr->shape_type, pr->shape_index, &r, &t, &is->rayEps, &is->dg);
     is->prim = h->prim;
+    is->inst = -1;
+    if (inst < 0) {
+        shape_intersect(c, pr->shape_type, pr->shape_index, &r, &t, &is->rayEps, &is->dg);
+        return;
+    }
+    const pbrtgpu_instance *I = &c->s->instances[inst];
+    float m[16], minv[16];
+    inst_interp(I, ray->time, m, minv);
+    Ray ro = xray(m, &r);
+    shape_intersect(c, pr->shape_type, pr->shape_index, &ro, &t, &is->rayEps, &is->dg);
+    if (m4_is_identity(m)) return;
+    /* WorldToObject = Identity * w2p ; ObjectToWorld = Inverse(that): normals use Mul(I, w2p.m) */
+    float id[16];
+    m4_identity(id);
+    m4_mul(id, m, is->nmat);
+    is->inst = inst;
+    /* PrimitiveToWorld = Inverse(w2p): points/vectors with w2p.mInv, normals with w2p.m */
+    DG *g = &is->dg;
+    g->p = xpoint(minv, g->p);
+    g->nn = vnorm(xnormal(m, g->nn));
+    g->dpdu = xvec(minv, g->dpdu);
+    g->dpdv = xvec(minv, g->dpdv);
+    g->dndu = xnormal(m, g->dndu);
+    g->dndv = xnormal(m, g->dndv);
 }
 
 /* ------------------------------------------------------------------ BSDF */
@@ -855,8 +988,8 @@ static void get_bsdf(const Ctx *c, const Isect *is, BSDF *bs, DG *dgsOut) {
     DG dgs;
     int ro, swaps;
     if (pr->shape_type == PBRTGPU_SHAPE_TRIANGLE) {
-        tri_shading(c, pr->shape_index, &is->dg, &dgs);
         const pbrtgpu_mesh *m = &c->s->meshes[c->s->tris[pr->shape_index].mesh];
+        tri_shading(c, pr->shape_index, is->inst >= 0 ? is->nmat : m->o2w_minv, &is->dg, &dgs);
         ro = m->reverse_orientation; swaps = m->swaps_handedness;
     } else {
         dgs = is->dg;

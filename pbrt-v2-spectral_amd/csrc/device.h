@@ -231,6 +231,9 @@ struct DevScene {
     int nLights;
     const pbrtgpu_light_shape *lightShapes;
     const float *spectra;
+    const pbrtgpu_instance *insts;    // TransformedPrimitive records (may be empty)
+    const int *primInst;              // per prim: owning instance or -1
+    int nInsts;
 };
 
 struct DG { V p, nn, dpdu, dpdv, dndu, dndv; float u, v; };
@@ -318,7 +321,9 @@ PGD_INLINE bool solve2x2(const float A[2][2], const float B[2], float *x0, float
     return true;
 }
 // Triangle::GetShadingGeometry (trianglemesh.cpp:285-360)
-PGD_INLINE void tri_shading(const DevScene &S, int ti, const DG &dg, DG &dgs) {
+// nmat: mInv of the ObjectToWorld handed to GetShadingGeometry (the mesh's, or the instance-
+// composed one of TransformedPrimitive::Intersect)
+PGD_INLINE void tri_shading(const DevScene &S, int ti, const float *nmat, const DG &dg, DG &dgs) {
     const pbrtgpu_triangle t = S.tris[ti];
     const pbrtgpu_mesh &m = S.meshes[t.mesh];
     if (!m.has_normals) { dgs = dg; return; }
@@ -331,7 +336,7 @@ PGD_INLINE void tri_shading(const DevScene &S, int ti, const DG &dg, DG &dgs) {
     else b[0] = 1.f - b[1] - b[2];
     V n0 = ldv(S.vertN + 3 * t.v[0]), n1 = ldv(S.vertN + 3 * t.v[1]), n2 = ldv(S.vertN + 3 * t.v[2]);
     V ni = vadd(vadd(vmul(n0, b[0]), vmul(n1, b[1])), vmul(n2, b[2]));
-    V ns = vnorm(xnormal(m.o2w_minv, ni));
+    V ns = vnorm(xnormal(nmat, ni));
     V ss = vnorm(dg.dpdu);
     V ts = vcross(ss, ns);
     if (vlen2(ts) > 0.f) { ts = vnorm(ts); ss = vcross(ts, ns); }
@@ -347,7 +352,7 @@ PGD_INLINE void tri_shading(const DevScene &S, int ti, const DG &dg, DG &dgs) {
         dndu = vmul(vsub(vmul(dn1, dv2), vmul(dn2, dv1)), invdet);
         dndv = vmul(vadd(vmul(dn1, -du2), vmul(dn2, du1)), invdet);
     }
-    dg_init(dgs, dg.p, ss, ts, xnormal(m.o2w_minv, dndu), xnormal(m.o2w_minv, dndv), dg.u, dg.v,
+    dg_init(dgs, dg.p, ss, ts, xnormal(nmat, dndu), xnormal(nmat, dndv), dg.u, dg.v,
             m.reverse_orientation ^ m.swaps_handedness);
 }
 
@@ -514,14 +519,174 @@ PGD_INLINE bool prim_hit(const DevScene &S, Stack &st, int pi, const Ray &ray, f
     st.cQuads++;
     return quadric_hit(S, pr.shape_type, pr.shape_index, ray, t);
 }
-// BVHAccel::Intersect (bvh.cpp:380-432): ray.maxt shrinks on every accepted hit
-PGD_INLINE bool bvh_intersect(const DevScene &S, Stack &st, Ray &ray, int *hitPrim, float *hitT) {
+// ---- Matrix4x4 / Quaternion / AnimatedTransform (transform.cpp, quaternion.cpp) for
+// TransformedPrimitive instances
+PGD_INLINE void m4_mul(const float *a, const float *b, float *r) {   // Matrix4x4::Mul
+    float t[16];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            t[4 * i + j] = a[4 * i + 0] * b[j] + a[4 * i + 1] * b[4 + j] + a[4 * i + 2] * b[8 + j] + a[4 * i + 3] * b[12 + j];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) r[i] = t[i];
+}
+PGD_INLINE void m4_identity(float *m) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) m[i] = (i % 5 == 0) ? 1.f : 0.f;
+}
+// transform.cpp:68-130, Gauss-Jordan with full pivoting
+PGD_INLINE void m4_inverse(const float *m, float *out) {
+    int indxc[4], indxr[4], ipiv[4] = {0, 0, 0, 0};
+    float minv[16];
+    for (int i = 0; i < 16; ++i) minv[i] = m[i];
+    for (int i = 0; i < 4; i++) {
+        int irow = -1, icol = -1;
+        float big = 0.;
+        for (int j = 0; j < 4; j++)
+            if (ipiv[j] != 1)
+                for (int k = 0; k < 4; k++)
+                    if (ipiv[k] == 0 && fabsf(minv[4 * j + k]) >= big) { big = fabsf(minv[4 * j + k]); irow = j; icol = k; }
+        ++ipiv[icol];
+        if (irow != icol)
+            for (int k = 0; k < 4; ++k) { float t = minv[4 * irow + k]; minv[4 * irow + k] = minv[4 * icol + k]; minv[4 * icol + k] = t; }
+        indxr[i] = irow;
+        indxc[i] = icol;
+        float pivinv = 1.f / minv[4 * icol + icol];
+        minv[4 * icol + icol] = 1.f;
+        for (int j = 0; j < 4; j++) minv[4 * icol + j] *= pivinv;
+        for (int j = 0; j < 4; j++)
+            if (j != icol) {
+                float save = minv[4 * j + icol];
+                minv[4 * j + icol] = 0;
+                for (int k = 0; k < 4; k++) minv[4 * j + k] -= minv[4 * icol + k] * save;
+            }
+    }
+    for (int j = 3; j >= 0; j--)
+        if (indxr[j] != indxc[j])
+            for (int k = 0; k < 4; k++) {
+                float t = minv[4 * k + indxr[j]]; minv[4 * k + indxr[j]] = minv[4 * k + indxc[j]]; minv[4 * k + indxc[j]] = t;
+            }
+    for (int i = 0; i < 16; ++i) out[i] = minv[i];
+}
+struct Quat { float x, y, z, w; };
+PGD_INLINE float qdot(Quat a, Quat b) { return (a.x * b.x + a.y * b.y + a.z * b.z) + a.w * b.w; }
+PGD_INLINE Quat qmk(float x, float y, float z, float w) { Quat q; q.x = x; q.y = y; q.z = z; q.w = w; return q; }
+PGD_INLINE Quat qnormalize(Quat q) {
+    float d = sqrtf(qdot(q, q));
+    float inv = 1.f / d;
+    return qmk(q.x * inv, q.y * inv, q.z * inv, q.w / d);
+}
+PGD_INLINE Quat qscale(Quat q, float f) { return qmk(q.x * f, q.y * f, q.z * f, q.w * f); }
+PGD_INLINE Quat qadd(Quat a, Quat b) { return qmk(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w); }
+PGD_INLINE Quat qsub(Quat a, Quat b) { return qmk(a.x - b.x, a.y - b.y, a.z - b.z, a.w - b.w); }
+PGD_INLINE Quat slerp(float t, Quat q1, Quat q2) {   // quaternion.cpp:39-49
+    float cosTheta = qdot(q1, q2);
+    if (cosTheta > .9995f) return qnormalize(qadd(qscale(q1, 1.f - t), qscale(q2, t)));
+    float theta = ACOSF(clampf(cosTheta, -1.f, 1.f));
+    float thetap = theta * t;
+    Quat qperp = qnormalize(qsub(q2, qscale(q1, cosTheta)));
+    return qadd(qscale(q1, COSF(thetap)), qscale(qperp, SINF(thetap)));
+}
+// AnimatedTransform::Interpolate (transform.cpp:356-381): world->primitive m (and mInv)
+PGD_INLINE void inst_interp(const pbrtgpu_instance &I, float time, float *m, float *minv) {
+    if (!I.animated || time <= I.start_time) {
+        for (int i = 0; i < 16; ++i) m[i] = I.start_m[i];
+        if (minv) for (int i = 0; i < 16; ++i) minv[i] = I.start_minv[i];
+        return;
+    }
+    if (time >= I.end_time) {
+        for (int i = 0; i < 16; ++i) m[i] = I.end_m[i];
+        if (minv) for (int i = 0; i < 16; ++i) minv[i] = I.end_minv[i];
+        return;
+    }
+    float dt = (time - I.start_time) / (I.end_time - I.start_time);
+    float tr[3];
+    for (int k = 0; k < 3; ++k) tr[k] = (1.f - dt) * I.T[0][k] + dt * I.T[1][k];
+    Quat rot = slerp(dt, qmk(I.R[0][0], I.R[0][1], I.R[0][2], I.R[0][3]), qmk(I.R[1][0], I.R[1][1], I.R[1][2], I.R[1][3]));
+    float Sm[16];
+    m4_identity(Sm);
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) Sm[4 * i + j] = lerpf(dt, I.S[0][4 * i + j], I.S[1][4 * i + j]);
+    // Quaternion::ToTransform: m = Transpose(M), mInv = M
+    float xx = rot.x * rot.x, yy = rot.y * rot.y, zz = rot.z * rot.z;
+    float xy = rot.x * rot.y, xz = rot.x * rot.z, yz = rot.y * rot.z;
+    float wx = rot.x * rot.w, wy = rot.y * rot.w, wz = rot.z * rot.w;
+    float M[16];
+    m4_identity(M);
+    M[0] = 1.f - 2.f * (yy + zz); M[1] = 2.f * (xy + wz); M[2] = 2.f * (xz - wy);
+    M[4] = 2.f * (xy - wz); M[5] = 1.f - 2.f * (xx + zz); M[6] = 2.f * (yz + wx);
+    M[8] = 2.f * (xz + wy); M[9] = 2.f * (yz - wx); M[10] = 1.f - 2.f * (xx + yy);
+    float R[16], T[16], TR[16];
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j) R[4 * i + j] = M[4 * j + i];
+    m4_identity(T); T[3] = tr[0]; T[7] = tr[1]; T[11] = tr[2];
+    m4_mul(T, R, TR);   // Translate(trans) * rotate.ToTransform() * Transform(scale)
+    m4_mul(TR, Sm, m);
+    if (minv) {
+        float Ti[16], Si[16], RiTi[16];
+        m4_identity(Ti); Ti[3] = -tr[0]; Ti[7] = -tr[1]; Ti[11] = -tr[2];
+        m4_inverse(Sm, Si);
+        m4_mul(M, Ti, RiTi);
+        m4_mul(Si, RiTi, minv);
+    }
+}
+PGD_INLINE Ray xray(const float *m, const Ray &r) {   // Transform::operator()(Ray)
+    Ray o = r;
+    o.o = xpoint(m, r.o);
+    o.d = xvec(m, r.d);
+    return o;
+}
+PGD_INLINE bool m4_is_identity(const float *m) {
+    bool id = true;
+    for (int i = 0; i < 16; ++i) id = id && (m[i] == ((i % 5 == 0) ? 1.f : 0.f));
+    return id;
+}
+
+// BVHAccel::Intersect / IntersectP (bvh.cpp:380-481) from node `root`, LDS stack entries
+// from `base`.  Closest hit: ray.maxt shrinks on every accepted hit.  With INST, prims of
+// shape_type INSTANCE run TransformedPrimitive::Intersect/IntersectP (primitive.cpp:87-116):
+// the ray is moved to primitive space at ray.time and the nested BVH is walked with the
+// stack entries above this level's.
+template <bool ANY, bool INST>
+PGD_INLINE bool bvh_walk(const DevScene &S, Stack &st, int base, uint32_t root, Ray &ray, int *hitPrim, float *hitT);
+
+template <bool ANY, bool INST>
+PGD_INLINE bool prim_test(const DevScene &S, Stack &st, int base, int pi, Ray &ray, int *hitPrim, float *hitT) {
+    const pbrtgpu_prim pr = S.prims[pi];
+    float t;
+    if (pr.shape_type == PBRTGPU_SHAPE_TRIANGLE) {
+        st.cTris++;
+        if (!tri_hit(S.primTri[pi], ray, &t)) return false;
+    } else if (!INST || pr.shape_type != PBRTGPU_SHAPE_INSTANCE) {
+        st.cQuads++;
+        if (!quadric_hit(S, pr.shape_type, pr.shape_index, ray, &t)) return false;
+    } else {
+        if constexpr (INST) {
+            const pbrtgpu_instance &I = S.insts[pr.shape_index];
+            float m[16];
+            inst_interp(I, ray.time, m, nullptr);
+            Ray r = xray(m, ray);
+            bool f;
+            if (I.single_prim >= 0) f = prim_test<ANY, false>(S, st, base, I.single_prim, r, hitPrim, hitT);
+            else f = bvh_walk<ANY, false>(S, st, base, (uint32_t)I.root, r, hitPrim, hitT);
+            if (f && !ANY) ray.maxt = r.maxt;
+            return f;
+        }
+        return false;
+    }
+    if (!ANY) { ray.maxt = t; *hitPrim = pi; *hitT = t; }
+    return true;
+}
+
+template <bool ANY, bool INST>
+PGD_INLINE bool bvh_walk(const DevScene &S, Stack &st, int base, uint32_t root, Ray &ray, int *hitPrim, float *hitT) {
     V invDir = v3(1.f / ray.d.x, 1.f / ray.d.y, 1.f / ray.d.z);
     int neg[3] = {invDir.x < 0, invDir.y < 0, invDir.z < 0};
-    int todo = 0;
-    uint32_t nodeNum = 0;
+    int todo = base;
+    uint32_t nodeNum = root;
     bool found = false;
-    st.cRays++;
+    if (ANY) st.cShadow += INST ? 1u : 0u; else st.cRays += INST ? 1u : 0u;
     for (;;) {
         float4 n0 = S.nodes[2 * nodeNum], n1 = S.nodes[2 * nodeNum + 1];
         st.cNodes++;
@@ -529,16 +694,12 @@ PGD_INLINE bool bvh_intersect(const DevScene &S, Stack &st, Ray &ray, int *hitPr
             uint32_t off = __float_as_uint(n1.z), meta = __float_as_uint(n1.w);
             uint32_t np = meta & 0xff;
             if (np > 0) {
-                for (uint32_t i = 0; i < np; ++i) {
-                    float t;
-                    if (prim_hit(S, st, (int)(off + i), ray, &t)) {
-                        ray.maxt = t;
-                        *hitPrim = (int)(off + i);
-                        *hitT = t;
+                for (uint32_t i = 0; i < np; ++i)
+                    if (prim_test<ANY, INST>(S, st, todo, (int)(off + i), ray, hitPrim, hitT)) {
+                        if (ANY) return true;
                         found = true;
                     }
-                }
-                if (todo == 0) break;
+                if (todo == base) break;
                 nodeNum = st.get(--todo);
             } else {
                 uint32_t axis = (meta >> 8) & 0xff;
@@ -546,52 +707,56 @@ PGD_INLINE bool bvh_intersect(const DevScene &S, Stack &st, Ray &ray, int *hitPr
                 else { st.set(todo++, off); nodeNum = nodeNum + 1; }
             }
         } else {
-            if (todo == 0) break;
+            if (todo == base) break;
             nodeNum = st.get(--todo);
         }
     }
-    st.cHits += found ? 1u : 0u;
     return found;
 }
-PGD_INLINE bool bvh_intersectP(const DevScene &S, Stack &st, const Ray &ray) {
-    V invDir = v3(1.f / ray.d.x, 1.f / ray.d.y, 1.f / ray.d.z);
-    int neg[3] = {invDir.x < 0, invDir.y < 0, invDir.z < 0};
-    int todo = 0;
-    uint32_t nodeNum = 0;
-    st.cShadow++;
-    for (;;) {
-        float4 n0 = S.nodes[2 * nodeNum], n1 = S.nodes[2 * nodeNum + 1];
-        st.cNodes++;
-        if (bbox_hit(n0, n1, ray, invDir, neg)) {
-            uint32_t off = __float_as_uint(n1.z), meta = __float_as_uint(n1.w);
-            uint32_t np = meta & 0xff;
-            if (np > 0) {
-                for (uint32_t i = 0; i < np; ++i) {
-                    float t;
-                    if (prim_hit(S, st, (int)(off + i), ray, &t)) return true;
-                }
-                if (todo == 0) break;
-                nodeNum = st.get(--todo);
-            } else {
-                uint32_t axis = (meta >> 8) & 0xff;
-                if (neg[axis]) { st.set(todo++, nodeNum + 1); nodeNum = off; }
-                else { st.set(todo++, off); nodeNum = nodeNum + 1; }
-            }
-        } else {
-            if (todo == 0) break;
-            nodeNum = st.get(--todo);
-        }
-    }
-    return false;
+template <bool INST = true>
+PGD_INLINE bool bvh_intersect(const DevScene &S, Stack &st, Ray &ray, int *hitPrim, float *hitT) {
+    if (!INST) st.cRays++;
+    bool f = bvh_walk<false, INST>(S, st, 0, 0u, ray, hitPrim, hitT);
+    st.cHits += f ? 1u : 0u;
+    return f;
 }
-struct Isect { DG dg; float rayEps; int prim; };
+template <bool INST = true>
+PGD_INLINE bool bvh_intersectP(const DevScene &S, Stack &st, const Ray &ray) {
+    if (!INST) st.cShadow++;
+    Ray r = ray;
+    int hp;
+    float ht;
+    return bvh_walk<true, INST>(S, st, 0, 0u, r, &hp, &ht);
+}
+struct Isect { DG dg; float rayEps; int prim; int inst; float time; };
+// full intersection record for a recorded closest hit; primitives of a transformed instance
+// are intersected in primitive space and moved to world space (primitive.cpp:94-110)
 PGD_HEAVY void isect_fill(const DevScene &S, const Ray &ray, int prim, float t, Isect &is) {
     const pbrtgpu_prim pr = S.prims[prim];
     Ray r = ray;
     r.maxt = t;
     float th;
-    shape_intersect(S, pr.shape_type, pr.shape_index, r, &th, &is.rayEps, &is.dg);
     is.prim = prim;
+    is.inst = -1;
+    is.time = ray.time;
+    const int inst = S.nInsts ? S.primInst[prim] : -1;
+    if (inst < 0) {
+        shape_intersect(S, pr.shape_type, pr.shape_index, r, &th, &is.rayEps, &is.dg);
+        return;
+    }
+    float m[16], minv[16];
+    inst_interp(S.insts[inst], ray.time, m, minv);
+    Ray ro = xray(m, r);
+    shape_intersect(S, pr.shape_type, pr.shape_index, ro, &th, &is.rayEps, &is.dg);
+    if (m4_is_identity(m)) return;
+    is.inst = inst;
+    DG &g = is.dg;   // PrimitiveToWorld = Inverse(w2p): points/vectors with mInv, normals with m
+    g.p = xpoint(minv, g.p);
+    g.nn = vnorm(xnormal(m, g.nn));
+    g.dpdu = xvec(minv, g.dpdu);
+    g.dpdv = xvec(minv, g.dpdv);
+    g.dndu = xnormal(m, g.dndu);
+    g.dndv = xnormal(m, g.dndv);
 }
 
 // ------------------------------------------------------------------ BSDF
@@ -906,8 +1071,16 @@ PGD_HEAVY void get_bsdf(const DevScene &S, const Isect &is, BSDF &bs, V *pOut, V
     DG dgs;
     int ro, swaps;
     if (pr.shape_type == PBRTGPU_SHAPE_TRIANGLE) {
-        tri_shading(S, pr.shape_index, is.dg, dgs);
         const pbrtgpu_mesh &m = S.meshes[S.tris[pr.shape_index].mesh];
+        if (is.inst < 0) tri_shading(S, pr.shape_index, m.o2w_minv, is.dg, dgs);
+        else {
+            // ObjectToWorld = Inverse(Identity * w2p): its mInv is Mul(Identity, w2p.m)
+            float w[16], id[16], nm[16];
+            inst_interp(S.insts[is.inst], is.time, w, nullptr);
+            m4_identity(id);
+            m4_mul(id, w, nm);
+            tri_shading(S, pr.shape_index, nm, is.dg, dgs);
+        }
         ro = m.reverse_orientation; swaps = m.swaps_handedness;
     } else {
         dgs = is.dg;

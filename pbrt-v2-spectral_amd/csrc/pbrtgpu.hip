@@ -43,7 +43,7 @@ static const int kShadeBlock = 256;
 
 // closest-hit queries of one pass (BVHAccel::Intersect, bvh.cpp:380-432): persistent grid,
 // one ray per lane per iteration, LDS traversal stack (column per lane)
-template <bool STATS>
+template <bool STATS, bool INST>
 __global__ __launch_bounds__(kTraceBlock) void k_trace_closest(DevScene S, PathSoA P, int q) {
     extern __shared__ uint32_t lds[];
     Stack st;
@@ -58,7 +58,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_closest(DevScene S, PathS
         Ray r = ray_load(P, kind, slot);
         int prim = -1;
         float t = INFINITY;
-        if (!bvh_intersect(S, st, r, &prim, &t)) prim = -1;
+        if (!bvh_intersect<INST>(S, st, r, &prim, &t)) prim = -1;
         P.hitPrim[(size_t)kind * P.cap + slot] = prim;
         P.hitT[(size_t)kind * P.cap + slot] = t;
         if (STATS && kind == RAY_M) { nM++; hM += prim >= 0 ? 1u : 0u; }
@@ -76,7 +76,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_closest(DevScene S, PathS
 }
 
 // any-hit queries of one pass (BVHAccel::IntersectP, bvh.cpp:435-481)
-template <bool STATS>
+template <bool STATS, bool INST>
 __global__ __launch_bounds__(kTraceBlock) void k_trace_shadow(DevScene S, PathSoA P, int q) {
     extern __shared__ uint32_t lds[];
     Stack st;
@@ -87,7 +87,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_shadow(DevScene S, PathSo
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const int slot = (int)Q[i];
         Ray r = ray_load(P, RAY_S, slot);
-        P.occ[slot] = bvh_intersectP(S, st, r) ? 1u : 0u;
+        P.occ[slot] = bvh_intersectP<INST>(S, st, r) ? 1u : 0u;
     }
     if (STATS) {
         unsigned long long *w = reinterpret_cast<unsigned long long *>(P.cnt + CNT_WORK);
@@ -352,17 +352,28 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
         HIPCHK(hipMemsetAsync(P.cnt + CNT_QS(nq), 0, 4, c->stream));
         HIPCHK(hipEventRecord(c->ev[0], c->stream));
         int gC = (int)std::min<uint32_t>((nC + kTraceBlock - 1) / kTraceBlock, (uint32_t)traceGrid);
+        const bool inst = c->S.nInsts > 0;
         if (gC > 0) {
-            if (countWork) hipLaunchKernelGGL(k_trace_closest<true>, dim3(gC), dim3(kTraceBlock), lds, c->stream, c->S, P, q);
-            else hipLaunchKernelGGL(k_trace_closest<false>, dim3(gC), dim3(kTraceBlock), lds, c->stream, c->S, P, q);
+            if (countWork) {
+                if (inst) hipLaunchKernelGGL((k_trace_closest<true, true>), dim3(gC), dim3(kTraceBlock), lds, c->stream, c->S, P, q);
+                else hipLaunchKernelGGL((k_trace_closest<true, false>), dim3(gC), dim3(kTraceBlock), lds, c->stream, c->S, P, q);
+            } else {
+                if (inst) hipLaunchKernelGGL((k_trace_closest<false, true>), dim3(gC), dim3(kTraceBlock), lds, c->stream, c->S, P, q);
+                else hipLaunchKernelGGL((k_trace_closest<false, false>), dim3(gC), dim3(kTraceBlock), lds, c->stream, c->S, P, q);
+            }
             HIPCHK(hipGetLastError());
             T.launches[K_CLOSEST]++;
         }
         HIPCHK(hipEventRecord(c->ev[1], c->stream));
         int gS = (int)std::min<uint32_t>((nS + kTraceBlock - 1) / kTraceBlock, (uint32_t)traceGrid);
         if (gS > 0) {
-            if (countWork) hipLaunchKernelGGL(k_trace_shadow<true>, dim3(gS), dim3(kTraceBlock), lds, c->stream, c->S, P, q);
-            else hipLaunchKernelGGL(k_trace_shadow<false>, dim3(gS), dim3(kTraceBlock), lds, c->stream, c->S, P, q);
+            if (countWork) {
+                if (inst) hipLaunchKernelGGL((k_trace_shadow<true, true>), dim3(gS), dim3(kTraceBlock), lds, c->stream, c->S, P, q);
+                else hipLaunchKernelGGL((k_trace_shadow<true, false>), dim3(gS), dim3(kTraceBlock), lds, c->stream, c->S, P, q);
+            } else {
+                if (inst) hipLaunchKernelGGL((k_trace_shadow<false, true>), dim3(gS), dim3(kTraceBlock), lds, c->stream, c->S, P, q);
+                else hipLaunchKernelGGL((k_trace_shadow<false, false>), dim3(gS), dim3(kTraceBlock), lds, c->stream, c->S, P, q);
+            }
             HIPCHK(hipGetLastError());
             T.launches[K_SHADOW]++;
         }
@@ -457,17 +468,20 @@ int pbrtgpu_scene_upload(pbrtgpu_ctx *c, const pbrtgpu_flat_scene *s) {
     S.yint = s->y_int;
     S.cam = s->camera;
     S.nLights = s->n_lights;
-    // BVH: verify topology and measure the stack depth traversal needs
-    int maxDepth = 0;
-    {
+    // BVH: verify topology and measure the stack depth traversal needs (top level, plus the
+    // deepest nested instance BVH whose walk stacks above it)
+    if (s->n_instances < 0 || (s->n_instances > 0 && (!s->instances || !s->prim_instance)))
+        return fail(PBRTGPU_E_INVALID, "instance arrays missing");
+    auto walkDepth = [&](uint32_t root, int *depthOut) -> int {
+        int maxD = 0;
         std::vector<std::pair<uint32_t, int> > todo;
-        todo.push_back(std::make_pair(0u, 0));
+        todo.push_back(std::make_pair(root, 0));
         while (!todo.empty()) {
             auto q = todo.back();
             todo.pop_back();
             if (q.first >= (uint32_t)s->n_nodes) return fail(PBRTGPU_E_INVALID, "BVH node index out of range");
             const pbrtgpu_bvh_node &n = s->nodes[q.first];
-            maxDepth = std::max(maxDepth, q.second);
+            maxD = std::max(maxD, q.second);
             if ((n.meta & 0xff) == 0) {
                 if (q.second > 62) return fail(PBRTGPU_E_UNSUPPORTED, "BVH deeper than 63 levels");
                 todo.push_back(std::make_pair(q.first + 1, q.second + 1));
@@ -475,7 +489,25 @@ int pbrtgpu_scene_upload(pbrtgpu_ctx *c, const pbrtgpu_flat_scene *s) {
             } else if (n.offset + (n.meta & 0xff) > (uint32_t)s->n_prims)
                 return fail(PBRTGPU_E_INVALID, "BVH leaf out of range");
         }
+        *depthOut = maxD;
+        return 0;
+    };
+    int maxDepth = 0, instDepth = 0;
+    if (int e = walkDepth(0, &maxDepth)) return e;
+    for (int i = 0; i < s->n_instances; ++i) {
+        const pbrtgpu_instance &I = s->instances[i];
+        if (I.root >= 0) {
+            int dd = 0;
+            if (int e = walkDepth((uint32_t)I.root, &dd)) return e;
+            instDepth = std::max(instDepth, dd + 1);
+        } else if (I.single_prim < 0 || I.single_prim >= s->n_prims)
+            return fail(PBRTGPU_E_INVALID, "instance without primitives");
     }
+    for (int i = 0; i < s->n_prims; ++i)
+        if (s->prims[i].shape_type == PBRTGPU_SHAPE_INSTANCE &&
+            (s->prims[i].shape_index < 0 || s->prims[i].shape_index >= s->n_instances))
+            return fail(PBRTGPU_E_INVALID, "bad instance index");
+    maxDepth += instDepth;
     c->stackDepth = maxDepth + 1;
     S.stackDepth = c->stackDepth;
     HIPCHK(upload(c, s->band_Y, (size_t)s->n_bands, &S.bandY));
@@ -485,6 +517,10 @@ int pbrtgpu_scene_upload(pbrtgpu_ctx *c, const pbrtgpu_flat_scene *s) {
     for (int i = 0; i < s->n_prims; ++i) {
         const pbrtgpu_prim &p = s->prims[i];
         DevTri t{};
+        if (p.shape_type == PBRTGPU_SHAPE_INSTANCE) {
+            pt[i] = t;
+            continue;
+        }
         if (p.shape_type == PBRTGPU_SHAPE_TRIANGLE) {
             if (p.shape_index < 0 || p.shape_index >= s->n_tris) return fail(PBRTGPU_E_INVALID, "bad triangle index");
             const pbrtgpu_triangle &tr = s->tris[p.shape_index];
@@ -527,6 +563,13 @@ int pbrtgpu_scene_upload(pbrtgpu_ctx *c, const pbrtgpu_flat_scene *s) {
     HIPCHK(upload(c, mats.data(), mats.size(), &S.mats));
     HIPCHK(upload(c, lts.data(), lts.size(), &S.lights));
     HIPCHK(upload(c, s->light_shapes, (size_t)s->n_light_shapes, &S.lightShapes));
+    S.nInsts = s->n_instances;
+    HIPCHK(upload(c, s->instances, (size_t)s->n_instances, &S.insts));
+    {
+        std::vector<int> pi(s->n_prims, -1);
+        if (s->n_instances > 0) for (int i = 0; i < s->n_prims; ++i) pi[i] = s->prim_instance[i];
+        HIPCHK(upload(c, pi.data(), pi.size(), &S.primInst));
+    }
     HIPCHK(upload(c, pool.data(), pool.size(), &S.spectra));
     c->nb = s->n_bands;
     c->spp = s->spp;

@@ -184,7 +184,10 @@ struct Isect {
     TriMesh *mesh = nullptr;
     int tri = -1;
     Quadric *quad = nullptr;
+    int inst = -1;        // PBRTGPU_SHAPE_INSTANCE: instance index
+    BBox instBound;       // TransformedPrimitive::WorldBound (motion bounds)
     BBox WorldBound() const {
+        if (kind == PBRTGPU_SHAPE_INSTANCE) return instBound;
         if (kind == PBRTGPU_SHAPE_TRIANGLE) {
             const V3 &p1 = mesh->p[mesh->vi[3 * tri]], &p2 = mesh->p[mesh->vi[3 * tri + 1]], &p3 = mesh->p[mesh->vi[3 * tri + 2]];
             return Union(BBox(p1, p2), p3);
@@ -210,6 +213,7 @@ struct PrimObj {
     std::shared_ptr<ShapeObj> shape;
     std::shared_ptr<MaterialObj> mtl;
     int areaLight = -1;
+    int instance = -1;    // animated shape -> TransformedPrimitive (index into instanceObjs)
 };
 
 struct SDVertex { V3 P; int startFace = -1; int child = -1; bool regular = false, boundary = false; };
@@ -949,8 +953,27 @@ private:
         for (int i = 0; i < m->ntris; ++i) { Isect is; is.kind = PBRTGPU_SHAPE_TRIANGLE; is.mesh = m; is.tri = i; outv->push_back(is); }
     }
     void MakeShapeDirective(const std::string &name, const ParamSet &params) {   // api.cpp:1051-1123
-        if (curT.IsAnimated())
-            throw std::runtime_error("animated shapes (TransformedPrimitive) are not supported by this build yet");
+        if (curT.IsAnimated()) {
+            // api.cpp:1088-1118: shape built with the identity transform, refined, nested
+            // BVH (default maxPrims 1) if more than one primitive, TransformedPrimitive with
+            // the animated world->object transform
+            if (gs.areaLight != "") out->warnings.push_back("Ignoring currently set area light when creating animated shape");
+            Xform id, idInv;
+            LookupCache(Xform(), &id, &idInv);
+            auto shape = MakeShape(name, id, idInv, gs.reverseOrientation, params);
+            if (!shape) return;
+            auto mtl = CreateMaterialFromState(params);
+            Xform w2o0, w2o1;
+            LookupCache(curT.t[0], nullptr, &w2o0);
+            LookupCache(curT.t[1], nullptr, &w2o1);
+            InstanceObj io;
+            io.shape = shape; io.mtl = mtl;
+            io.anim = AnimXform(w2o0, tStart, w2o1, tEnd);
+            instanceObjs.push_back(io);
+            PrimObj po; po.instance = (int)instanceObjs.size() - 1;
+            primitives.push_back(po);
+            return;
+        }
         Xform o2w, w2o;
         LookupCache(curT.t[0], &o2w, &w2o);
         auto shape = MakeShape(name, o2w, w2o, gs.reverseOrientation, params);
@@ -981,90 +1004,123 @@ private:
     struct BuildPrim { Isect is; int material; int areaLight; };
     struct PrimInfo { int primitiveNumber; V3 centroid; BBox bounds; };
     struct BuildNode { BBox bounds; int children[2] = {-1, -1}; uint32_t splitAxis = 0, firstPrimOffset = 0, nPrimitives = 0; };
-    std::vector<BuildNode> bnodes;
-    std::vector<BuildPrim> refinedPrims, orderedPrims;
-    int maxDepth = 0;
-
-    int RecursiveBuild(std::vector<PrimInfo> &bd, uint32_t start, uint32_t end, int depth) {   // bvh.cpp:202-351
-        maxDepth = std::max(maxDepth, depth);
-        int nodeIdx = (int)bnodes.size();
-        bnodes.push_back(BuildNode());
-        BBox bbox;
-        for (uint32_t i = start; i < end; ++i) bbox = Union(bbox, bd[i].bounds);
-        uint32_t nPrimitives = end - start;
-        auto makeLeaf = [&]() {
-            uint32_t first = (uint32_t)orderedPrims.size();
-            for (uint32_t i = start; i < end; ++i) orderedPrims.push_back(refinedPrims[bd[i].primitiveNumber]);
-            bnodes[nodeIdx].firstPrimOffset = first; bnodes[nodeIdx].nPrimitives = nPrimitives; bnodes[nodeIdx].bounds = bbox;
-            return nodeIdx;
-        };
-        if (nPrimitives == 1) return makeLeaf();
-        BBox cb;
-        for (uint32_t i = start; i < end; ++i) cb = Union(cb, bd[i].centroid);
-        int dim = cb.MaximumExtent();
-        uint32_t mid = (start + end) / 2;
-        if (cb.pMax[dim] == cb.pMin[dim]) return makeLeaf();
-        auto cmpPts = [dim](const PrimInfo &a, const PrimInfo &b) { return a.centroid[dim] < b.centroid[dim]; };
-        if (nPrimitives <= 4) {
-            mid = (start + end) / 2;
-            std::nth_element(&bd[start], &bd[mid], &bd[end - 1] + 1, cmpPts);
-        } else {
-            const int nBuckets = 12;
-            struct Bucket { int count = 0; BBox bounds; } buckets[nBuckets];
-            for (uint32_t i = start; i < end; ++i) {
-                int b = nBuckets * ((bd[i].centroid[dim] - cb.pMin[dim]) / (cb.pMax[dim] - cb.pMin[dim]));
-                if (b == nBuckets) b = nBuckets - 1;
-                buckets[b].count++;
-                buckets[b].bounds = Union(buckets[b].bounds, bd[i].bounds);
+    struct InstanceObj {
+        std::shared_ptr<ShapeObj> shape;
+        std::shared_ptr<MaterialObj> mtl;
+        AnimXform anim;
+    };
+    std::vector<InstanceObj> instanceObjs;
+    // one BVHAccel build (bvh.cpp:145-351): input prims in FullyRefine order -> nodes, ordered prims
+    struct BvhBuild {
+        uint32_t maxPrimsInNode = 4;
+        std::vector<BuildNode> bnodes;
+        std::vector<BuildPrim> prims, ordered;
+        int maxDepth = 0;
+        void Build() {
+            std::vector<PrimInfo> bd(prims.size());
+            for (size_t i = 0; i < prims.size(); ++i) {
+                bd[i].primitiveNumber = (int)i;
+                bd[i].bounds = prims[i].is.WorldBound();
+                bd[i].centroid = .5f * bd[i].bounds.pMin + .5f * bd[i].bounds.pMax;
             }
-            float cost[nBuckets - 1];
-            for (int i = 0; i < nBuckets - 1; ++i) {
-                BBox b0, b1;
-                int count0 = 0, count1 = 0;
-                for (int j = 0; j <= i; ++j) { b0 = Union(b0, buckets[j].bounds); count0 += buckets[j].count; }
-                for (int j = i + 1; j < nBuckets; ++j) { b1 = Union(b1, buckets[j].bounds); count1 += buckets[j].count; }
-                cost[i] = .125f + (count0 * b0.SurfaceArea() + count1 * b1.SurfaceArea()) / bbox.SurfaceArea();
-            }
-            float minCost = cost[0];
-            uint32_t minCostSplit = 0;
-            for (int i = 1; i < nBuckets - 1; ++i)
-                if (cost[i] < minCost) { minCost = cost[i]; minCostSplit = i; }
-            const uint32_t maxPrimsInNode = 4;
-            if (nPrimitives > maxPrimsInNode || minCost < nPrimitives) {
-                float pmin_ = cb.pMin[dim], pmax_ = cb.pMax[dim];
-                int splitBucket = (int)minCostSplit;   // CompareToBucket (bvh.cpp:84-101)
-                PrimInfo *pm = std::partition(&bd[start], &bd[end - 1] + 1, [&](const PrimInfo &p) {
-                    int b = nBuckets * ((p.centroid[dim] - pmin_) / (pmax_ - pmin_));
-                    if (b == nBuckets) b = nBuckets - 1;
-                    return b <= splitBucket;
-                });
-                mid = (uint32_t)(pm - &bd[0]);
-            } else
-                return makeLeaf();
+            Recursive(bd, 0, (uint32_t)bd.size(), 0);
         }
-        int c0 = RecursiveBuild(bd, start, mid, depth + 1);
-        int c1 = RecursiveBuild(bd, mid, end, depth + 1);
-        BuildNode &n = bnodes[nodeIdx];
-        n.children[0] = c0; n.children[1] = c1;
-        n.bounds = Union(bnodes[c0].bounds, bnodes[c1].bounds);
-        n.splitAxis = dim; n.nPrimitives = 0;
-        return nodeIdx;
-    }
-    uint32_t Flatten(int node, uint32_t *offset) {   // bvh.cpp:354-372
+            int Recursive(std::vector<PrimInfo> &bd, uint32_t start, uint32_t end, int depth) {   // bvh.cpp:202-351
+            maxDepth = std::max(maxDepth, depth);
+            int nodeIdx = (int)bnodes.size();
+            bnodes.push_back(BuildNode());
+            BBox bbox;
+            for (uint32_t i = start; i < end; ++i) bbox = Union(bbox, bd[i].bounds);
+            uint32_t nPrimitives = end - start;
+            auto makeLeaf = [&]() {
+                uint32_t first = (uint32_t)ordered.size();
+                for (uint32_t i = start; i < end; ++i) ordered.push_back(prims[bd[i].primitiveNumber]);
+                bnodes[nodeIdx].firstPrimOffset = first; bnodes[nodeIdx].nPrimitives = nPrimitives; bnodes[nodeIdx].bounds = bbox;
+                return nodeIdx;
+            };
+            if (nPrimitives == 1) return makeLeaf();
+            BBox cb;
+            for (uint32_t i = start; i < end; ++i) cb = Union(cb, bd[i].centroid);
+            int dim = cb.MaximumExtent();
+            uint32_t mid = (start + end) / 2;
+            if (cb.pMax[dim] == cb.pMin[dim]) return makeLeaf();
+            auto cmpPts = [dim](const PrimInfo &a, const PrimInfo &b) { return a.centroid[dim] < b.centroid[dim]; };
+            if (nPrimitives <= 4) {
+                mid = (start + end) / 2;
+                std::nth_element(&bd[start], &bd[mid], &bd[end - 1] + 1, cmpPts);
+            } else {
+                const int nBuckets = 12;
+                struct Bucket { int count = 0; BBox bounds; } buckets[nBuckets];
+                for (uint32_t i = start; i < end; ++i) {
+                    int b = nBuckets * ((bd[i].centroid[dim] - cb.pMin[dim]) / (cb.pMax[dim] - cb.pMin[dim]));
+                    if (b == nBuckets) b = nBuckets - 1;
+                    buckets[b].count++;
+                    buckets[b].bounds = Union(buckets[b].bounds, bd[i].bounds);
+                }
+                float cost[nBuckets - 1];
+                for (int i = 0; i < nBuckets - 1; ++i) {
+                    BBox b0, b1;
+                    int count0 = 0, count1 = 0;
+                    for (int j = 0; j <= i; ++j) { b0 = Union(b0, buckets[j].bounds); count0 += buckets[j].count; }
+                    for (int j = i + 1; j < nBuckets; ++j) { b1 = Union(b1, buckets[j].bounds); count1 += buckets[j].count; }
+                    cost[i] = .125f + (count0 * b0.SurfaceArea() + count1 * b1.SurfaceArea()) / bbox.SurfaceArea();
+                }
+                float minCost = cost[0];
+                uint32_t minCostSplit = 0;
+                for (int i = 1; i < nBuckets - 1; ++i)
+                    if (cost[i] < minCost) { minCost = cost[i]; minCostSplit = i; }
+                if (nPrimitives > maxPrimsInNode || minCost < nPrimitives) {
+                    float pmin_ = cb.pMin[dim], pmax_ = cb.pMax[dim];
+                    int splitBucket = (int)minCostSplit;   // CompareToBucket (bvh.cpp:84-101)
+                    PrimInfo *pm = std::partition(&bd[start], &bd[end - 1] + 1, [&](const PrimInfo &p) {
+                        int b = nBuckets * ((p.centroid[dim] - pmin_) / (pmax_ - pmin_));
+                        if (b == nBuckets) b = nBuckets - 1;
+                        return b <= splitBucket;
+                    });
+                    mid = (uint32_t)(pm - &bd[0]);
+                } else
+                    return makeLeaf();
+            }
+            int c0 = Recursive(bd, start, mid, depth + 1);
+            int c1 = Recursive(bd, mid, end, depth + 1);
+            BuildNode &n = bnodes[nodeIdx];
+            n.children[0] = c0; n.children[1] = c1;
+            n.bounds = Union(bnodes[c0].bounds, bnodes[c1].bounds);
+            n.splitAxis = dim; n.nPrimitives = 0;
+            return nodeIdx;
+        }
+    };
+    BvhBuild top;
+    std::vector<BvhBuild> blas;   // per instance (no nodes if the instance is a single primitive)
+
+    // bvh.cpp:354-372; nodes go to out->nodes from *offset, leaf prim offsets are shifted by
+    // primBase (prims of all BVHs share one array)
+    uint32_t Flatten(const BvhBuild &B, int node, uint32_t *offset, uint32_t primBase) {
         pbrtgpu_bvh_node &ln = out->nodes[*offset];
-        const BuildNode &bn = bnodes[node];
+        const BuildNode &bn = B.bnodes[node];
         for (int k = 0; k < 3; ++k) { ln.bmin[k] = bn.bounds.pMin[k]; ln.bmax[k] = bn.bounds.pMax[k]; }
         uint32_t my = (*offset)++;
         if (bn.nPrimitives > 0) {
-            ln.offset = bn.firstPrimOffset;
+            ln.offset = primBase + bn.firstPrimOffset;
             ln.meta = bn.nPrimitives & 0xff;
         } else {
             out->nodes[my].meta = (bn.splitAxis & 0xff) << 8;
-            Flatten(bn.children[0], offset);
-            uint32_t second = Flatten(bn.children[1], offset);
+            Flatten(B, bn.children[0], offset, primBase);
+            uint32_t second = Flatten(B, bn.children[1], offset, primBase);
             out->nodes[my].offset = second;
         }
         return my;
+    }
+    void EmitPrims(const std::vector<BuildPrim> &v, int inst) {
+        for (auto &bp : v) {
+            pbrtgpu_prim fp;
+            if (bp.is.kind == PBRTGPU_SHAPE_INSTANCE) { fp.shape_type = PBRTGPU_SHAPE_INSTANCE; fp.shape_index = bp.is.inst; }
+            else fp.shape_index = EmitShape(bp.is, &fp.shape_type);
+            fp.material = bp.material;
+            fp.area_light = bp.areaLight;
+            out->prims.push_back(fp);
+            out->primInstance.push_back(inst);
+        }
     }
 
     int EmitMesh(TriMesh *m) {
@@ -1156,34 +1212,72 @@ private:
         out->nBands = spec.n();
         out->bandY.assign(spec.Y(), spec.Y() + spec.n());
         out->yint = spec.yint();
-        // ---- refine primitives (primitive.cpp:40-53, LIFO) and build the BVH
-        for (auto &po : primitives) {
+        // ---- refine primitives (primitive.cpp:40-53, LIFO) and build the BVHs
+        auto refineInto = [&](const std::shared_ptr<ShapeObj> &shape, MaterialObj *mtl, int areaLight,
+                              std::vector<BuildPrim> *dst) {
             std::vector<Isect> r;
-            RefineShape(po.shape, &r);
+            RefineShape(shape, &r);
             // single intersectable shape -> itself; refinable -> children popped in reverse
             for (auto it = r.rbegin(); it != r.rend(); ++it) {
-                BuildPrim bp; bp.is = *it; bp.material = EmitMaterial(po.mtl.get()); bp.areaLight = po.areaLight;
-                refinedPrims.push_back(bp);
+                BuildPrim bp; bp.is = *it; bp.material = EmitMaterial(mtl); bp.areaLight = areaLight;
+                dst->push_back(bp);
             }
+        };
+        blas.assign(instanceObjs.size(), BvhBuild());
+        for (auto &po : primitives) {
+            if (po.instance < 0) { refineInto(po.shape, po.mtl.get(), po.areaLight, &top.prims); continue; }
+            // TransformedPrimitive (api.cpp:1101-1118): nested BVHAccel(refined) with the
+            // default maxPrims 1, or the single refined primitive itself
+            InstanceObj &io = instanceObjs[po.instance];
+            BvhBuild &B = blas[po.instance];
+            B.maxPrimsInNode = 1;
+            refineInto(io.shape, io.mtl.get(), -1, &B.prims);
+            if (B.prims.empty()) continue;
+            BBox objBound;
+            if (B.prims.size() > 1) { B.Build(); objBound = B.bnodes[0].bounds; }
+            else objBound = B.prims[0].is.WorldBound();
+            BuildPrim tp;
+            tp.is.kind = PBRTGPU_SHAPE_INSTANCE;
+            tp.is.inst = po.instance;
+            tp.is.instBound = io.anim.MotionBounds(objBound, true);   // TransformedPrimitive::WorldBound
+            tp.material = -1; tp.areaLight = -1;
+            top.prims.push_back(tp);
         }
-        if (refinedPrims.empty()) throw std::runtime_error("scene has no primitives");
-        std::vector<PrimInfo> bd(refinedPrims.size());
-        for (size_t i = 0; i < refinedPrims.size(); ++i) {
-            bd[i].primitiveNumber = (int)i;
-            bd[i].bounds = refinedPrims[i].is.WorldBound();
-            bd[i].centroid = .5f * bd[i].bounds.pMin + .5f * bd[i].bounds.pMax;
-        }
-        RecursiveBuild(bd, 0, (uint32_t)bd.size(), 0);
-        out->bvhMaxDepth = maxDepth;
-        out->nodes.assign(bnodes.size(), pbrtgpu_bvh_node());
+        if (top.prims.empty()) throw std::runtime_error("scene has no primitives");
+        top.Build();
+        out->bvhMaxDepth = top.maxDepth;
+        size_t nNodes = top.bnodes.size();
+        for (auto &B : blas) nNodes += B.bnodes.size();
+        out->nodes.assign(nNodes, pbrtgpu_bvh_node());
         uint32_t off = 0;
-        Flatten(0, &off);
-        for (auto &bp : orderedPrims) {
-            pbrtgpu_prim fp;
-            fp.shape_index = EmitShape(bp.is, &fp.shape_type);
-            fp.material = bp.material;
-            fp.area_light = bp.areaLight;
-            out->prims.push_back(fp);
+        Flatten(top, 0, &off, 0);
+        EmitPrims(top.ordered, -1);
+        for (size_t i = 0; i < instanceObjs.size(); ++i) {
+            BvhBuild &B = blas[i];
+            const InstanceObj &io = instanceObjs[i];
+            pbrtgpu_instance fi{};
+            fi.root = -1; fi.single_prim = -1;
+            uint32_t primBase = (uint32_t)out->prims.size();
+            if (B.prims.size() > 1) {
+                fi.root = (int)off;
+                Flatten(B, 0, &off, primBase);
+                EmitPrims(B.ordered, (int)i);
+                out->bvhMaxDepth = std::max(out->bvhMaxDepth, top.maxDepth + 1 + B.maxDepth);
+            } else if (B.prims.size() == 1) {
+                fi.single_prim = (int)primBase;
+                EmitPrims(B.prims, (int)i);
+            }
+            const AnimXform &A = io.anim;
+            fi.animated = A.animated ? 1 : 0;
+            fi.start_time = A.startTime; fi.end_time = A.endTime;
+            memcpy(fi.start_m, A.start.m.m, 64); memcpy(fi.start_minv, A.start.mInv.m, 64);
+            memcpy(fi.end_m, A.end.m.m, 64); memcpy(fi.end_minv, A.end.mInv.m, 64);
+            for (int k = 0; k < 2; ++k) {
+                fi.T[k][0] = A.T[k].x; fi.T[k][1] = A.T[k].y; fi.T[k][2] = A.T[k].z; fi.T[k][3] = 0.f;
+                fi.R[k][0] = A.R[k].v.x; fi.R[k][1] = A.R[k].v.y; fi.R[k][2] = A.R[k].v.z; fi.R[k][3] = A.R[k].w;
+                memcpy(fi.S[k], A.S[k].m, 64);
+            }
+            out->instances.push_back(fi);
         }
         // ---- lights
         for (auto &lo : lights) {
@@ -1276,6 +1370,8 @@ void HostScene::Flat(pbrtgpu_flat_scene *f) const {
     f->n_lights = (int)lights.size(); f->lights = lights.data();
     f->n_light_shapes = (int)lightShapes.size(); f->light_shapes = lightShapes.data();
     f->n_spectra_floats = (int)spectra.size(); f->spectra = spectra.data();
+    f->n_instances = (int)instances.size(); f->instances = instances.empty() ? nullptr : instances.data();
+    f->prim_instance = primInstance.data();
 }
 
 }  // namespace pbrtamd

@@ -51,6 +51,8 @@ struct HostScene {
     std::vector<pbrtgpu_light> lights;
     std::vector<pbrtgpu_light_shape> lightShapes;
     std::vector<float> spectra;
+    std::vector<pbrtgpu_instance> instances;
+    std::vector<int32_t> primInstance;        // per prim: owning instance or -1
     // diagnostics
     std::vector<std::string> warnings;
     int bvhMaxDepth = 0;

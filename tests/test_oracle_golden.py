@@ -15,10 +15,13 @@ import pytest
 from conftest import GOLDEN, PACKS
 
 
-def _scene(pg, cfg):
+def _scene(pg, cfg, name="killeroo"):
     w, h, spp, seed, md = [int(v) for v in cfg]
-    return pg.Scene.load(os.path.join(PACKS, "killeroo-simple.pack"), xres=w, yres=h, spp=spp, maxdepth=md,
-                         seed=seed)
+    pack = "anim-killeroos-moving.pack" if name.startswith("anim") else "killeroo-simple.pack"
+    return pg.Scene.load(os.path.join(PACKS, pack), xres=w, yres=h, spp=spp, maxdepth=md, seed=seed)
+
+
+PATHS = ["killeroo_paths_64x64s4", "killeroo_paths_48x48s8_seed7_md7", "anim_paths_48x48s4"]
 
 
 @pytest.fixture(scope="module")
@@ -26,19 +29,19 @@ def ora_libm(pg):
     return pg.oracle(libm_float=True)
 
 
-@pytest.mark.parametrize("name", ["killeroo_paths_64x64s4", "killeroo_paths_48x48s8_seed7_md7"])
+@pytest.mark.parametrize("name", PATHS)
 def test_paths_bit_exact_vs_reference(pg, ora_libm, name):
     g = np.load(os.path.join(GOLDEN, name + ".npz"))
-    scene = _scene(pg, g["config"])
+    scene = _scene(pg, g["config"], name)
     L = ora_libm.trace_paths(scene, g["keys"])
     same = np.all(L.view(np.int32) == g["L"].view(np.int32), axis=1)
     assert same.all(), "paths differing: %d / %d" % ((~same).sum(), len(same))
 
 
-@pytest.mark.parametrize("name", ["killeroo_paths_64x64s4", "killeroo_paths_48x48s8_seed7_md7"])
+@pytest.mark.parametrize("name", PATHS)
 def test_paths_double_rounded_definition(pg, name):
     g = np.load(os.path.join(GOLDEN, name + ".npz"))
-    scene = _scene(pg, g["config"])
+    scene = _scene(pg, g["config"], name)
     L = pg.oracle().trace_paths(scene, g["keys"])
     ref = g["L"]
     same = np.all(L.view(np.int32) == ref.view(np.int32), axis=1)
@@ -52,11 +55,13 @@ def test_paths_double_rounded_definition(pg, name):
     assert tot < 1e-5
 
 
-def test_film_bit_exact_vs_reference(pg, ora_libm):
-    g = np.load(os.path.join(GOLDEN, "killeroo_film_96x72s16.npz"))
-    scene = _scene(pg, g["config"])
+@pytest.mark.parametrize("name", ["killeroo_film_96x72s16", "anim_film_40x40s8"])
+def test_film_bit_exact_vs_reference(pg, ora_libm, name):
+    g = np.load(os.path.join(GOLDEN, name + ".npz"))
+    scene = _scene(pg, g["config"], name)
     film, st = ora_libm.render(scene, threads=8)
-    assert st[2] > 0, "fixture should contain samples landing on neighbour pixels"
+    if name.startswith("killeroo"):
+        assert st[2] > 0, "fixture should contain samples landing on neighbour pixels"
     assert np.array_equal(film.view(np.int32), g["film"].view(np.int32))
 
 

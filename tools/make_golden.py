@@ -9,6 +9,8 @@ Fixtures (numpy .npz, inputs + expected outputs only):
   killeroo_paths_48x48s8_seed7_md7.npz   every 3rd path, 8 spp, seed 7, maxdepth 7 (MT19937 draws)
   killeroo_film_96x72s16.npz      raw film sums [72][96][32] at 96x72, 16 spp (includes 3 samples
                                   that land on neighbouring pixels)
+  anim_paths_48x48s4.npz, anim_film_40x40s8.npz   the motion-blur scene (C5): animated
+                                  TransformedPrimitives over nested BVHs
   mt19937_kat.npz                 first 64 outputs of RNG(seed) for 6 seeds
   fromrgb_32.npz                  SampledSpectrum::FromRGB (reflectance and illuminant) for 14
                                   RGB triples, 32 bands 395-715 nm
@@ -23,12 +25,12 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HARNESS = os.path.join(ROOT, "oracle", "_ref", "b32", "pbrt_ref_harness")
-SCENE = "/root/reference/scenes/killeroo-simple.pbrt"
+SCENES = "/root/reference/scenes"
 OUT = os.path.join(ROOT, "tests", "golden")
 
 
 def run(args):
-    subprocess.run([HARNESS] + args, check=True, cwd=os.path.dirname(SCENE))
+    subprocess.run([HARNESS] + args, check=True, cwd=SCENES)
 
 
 def read_paths(fn):
@@ -38,9 +40,9 @@ def read_paths(fn):
     return rec[:, :3].copy(), rec[:, 3:].copy().view(np.float32), int(spp), int(seed)
 
 
-def paths_fixture(name, res, spp, seed, maxdepth, every, tmp):
+def paths_fixture(name, res, spp, seed, maxdepth, every, tmp, scene="killeroo-simple.pbrt"):
     fn = os.path.join(tmp, name + ".bin")
-    run([SCENE, "--res", str(res[0]), str(res[1]), "--spp", str(spp), "--seed", str(seed), "--maxdepth",
+    run([os.path.join(SCENES, scene), "--res", str(res[0]), str(res[1]), "--spp", str(spp), "--seed", str(seed), "--maxdepth",
          str(maxdepth), "--paths", fn, "--path-every", str(every)])
     keys, L, _, _ = read_paths(fn)
     np.savez_compressed(os.path.join(OUT, name + ".npz"), keys=keys, L=L,
@@ -48,9 +50,9 @@ def paths_fixture(name, res, spp, seed, maxdepth, every, tmp):
     print(name, keys.shape)
 
 
-def film_fixture(name, res, spp, seed, maxdepth, tmp):
+def film_fixture(name, res, spp, seed, maxdepth, tmp, scene="killeroo-simple.pbrt"):
     fn = os.path.join(tmp, name + ".f32")
-    run([SCENE, "--res", str(res[0]), str(res[1]), "--spp", str(spp), "--seed", str(seed), "--maxdepth",
+    run([os.path.join(SCENES, scene), "--res", str(res[0]), str(res[1]), "--spp", str(spp), "--seed", str(seed), "--maxdepth",
          str(maxdepth), "--raw", fn])
     raw = np.fromfile(fn, dtype=np.int32)
     W, H, N = raw[:3]
@@ -68,6 +70,8 @@ def main():
         paths_fixture("killeroo_paths_64x64s4", (64, 64), 4, 0, 5, 5, tmp)
         paths_fixture("killeroo_paths_48x48s8_seed7_md7", (48, 48), 8, 7, 7, 3, tmp)
         film_fixture("killeroo_film_96x72s16", (96, 72), 16, 0, 5, tmp)
+        paths_fixture("anim_paths_48x48s4", (48, 48), 4, 0, 5, 3, tmp, scene="anim-killeroos-moving.pbrt")
+        film_fixture("anim_film_40x40s8", (40, 40), 8, 0, 5, tmp, scene="anim-killeroos-moving.pbrt")
         fn = os.path.join(tmp, "mt.bin")
         run(["-", "--kat-mt", fn])
         raw = np.fromfile(fn, dtype=np.uint32).reshape(6, 65)

@@ -16,6 +16,7 @@ REF = "/root/reference/scenes"
 # (pack name, scene file, bands, xres, yres, spp) -- SURVEY App. B overrides
 PACKS = [
     ("killeroo-simple", "killeroo-simple.pbrt", 32, 700, 700, 256),
+    ("anim-killeroos-moving", "anim-killeroos-moving.pbrt", 32, 600, 600, 512),
 ]
 
 
