@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define PBRTGPU_ABI_VERSION 3
+#define PBRTGPU_ABI_VERSION 4
 #define PBRTGPU_MAX_BANDS 64
 
 #define PBRTGPU_E_INVALID   (-1)
@@ -86,7 +86,7 @@ enum {
     PBRTGPU_MAT_SUBSTRATE = 3,  /* spec[0]=Kd, spec[1]=Ks; f[0]=uroughness, f[1]=vroughness */
     PBRTGPU_MAT_MIRROR = 4,     /* spec[0]=Kr */
     PBRTGPU_MAT_GLASS = 5,      /* spec[0]=Kr, spec[1]=Kt; f[0]=index */
-    PBRTGPU_MAT_MEASURED = 6    /* aux = measured table index */
+    PBRTGPU_MAT_MEASURED = 6    /* IrregIsotropicBRDF: aux = first kd-tree node, aux2 = node count */
 };
 
 /* material with constant textures; f[7] = constant bump displacement (Material::Bump,
@@ -94,8 +94,8 @@ enum {
 typedef struct pbrtgpu_material {
     int32_t type;
     int32_t spec[4];      /* offsets (in floats) into spectra[] */
-    int32_t aux;
-    int32_t pad0, pad1;
+    int32_t aux, aux2;
+    int32_t pad0;
     float f[8];
 } pbrtgpu_material;
 
@@ -119,6 +119,18 @@ typedef struct pbrtgpu_light_shape {
     float area;            /* Shape::Area() */
     float cdf;             /* Distribution1D cdf[i+1] of the area distribution */
 } pbrtgpu_light_shape;
+
+/* KdTree<IrregIsotropicBRDFSample> node (kdtree.h:37-55) with the sample stored at it:
+ * p = BRDFRemap(wo, wi) of the measurement, spec = its spectrum (offset into spectra[]).
+ * Nodes of one tree are contiguous; child indices are relative to the tree's first node. */
+typedef struct pbrtgpu_kdnode {
+    float p[3];
+    float split_pos;
+    int32_t split_axis;     /* 0..2, 3 = leaf */
+    int32_t has_left;       /* left child = this node + 1 */
+    int32_t right_child;    /* (1 << 29) - 1 if none */
+    int32_t spec;
+} pbrtgpu_kdnode;
 
 /* TransformedPrimitive with an AnimatedTransform world->primitive (primitive.cpp:87-116,
  * transform.cpp:356-381): the top-level prim of shape_type PBRTGPU_SHAPE_INSTANCE points
@@ -172,6 +184,7 @@ typedef struct pbrtgpu_flat_scene {
     int32_t n_spectra_floats; const float *spectra;   /* spectrum pool */
     int32_t n_instances; const pbrtgpu_instance *instances;
     const int32_t *prim_instance;                  /* [n_prims]: owning instance or -1 */
+    int32_t n_kdnodes; const pbrtgpu_kdnode *kdnodes;   /* measured BRDF kd-trees */
 } pbrtgpu_flat_scene;
 
 /* ---- render description ----------------------------------------------------------- */

@@ -712,13 +712,15 @@ static void isect_fill(const Ctx *c, const Ray *ray, const Hit *h, Isect *is) {
 /* ------------------------------------------------------------------ BSDF */
 enum { BSDF_REFLECTION = 1, BSDF_TRANSMISSION = 2, BSDF_DIFFUSE = 4, BSDF_GLOSSY = 8, BSDF_SPECULAR = 16,
        BSDF_ALL = 31 };
-enum { BX_LAMBERT, BX_OREN, BX_MICRO_BLINN_DIEL, BX_SPEC_REFL_NOOP, BX_FRESNEL_BLEND_ANISO };
+enum { BX_LAMBERT, BX_OREN, BX_MICRO_BLINN_DIEL, BX_SPEC_REFL_NOOP, BX_FRESNEL_BLEND_ANISO, BX_MEASURED_IRREG };
 typedef struct {
     int kind, type;
     const float *R;      /* reflectance spectrum */
     const float *R2;     /* second spectrum (FresnelBlend Rs) */
     float a, b;          /* OrenNayar A,B ; Blinn exponent ; Aniso ex,ey */
     float eta_i, eta_t;  /* FresnelDielectric */
+    const pbrtgpu_kdnode *kd;   /* IrregIsotropicBRDF: kd-tree nodes */
+    int nkd;
 } BxDF;
 typedef struct {
     V nn, ng, sn, tn;
@@ -824,9 +826,74 @@ static void aniso_sample(float ex, float ey, V wo, V *wi, float u1, float u2, fl
 }
 
 /* BxDF::f for one bxdf, accumulated band-wise into out (out += f) */
+/* BRDFRemap (reflection.cpp:239-248); pbrt.h defines M_PI as a float literal, so every
+ * operation here is single precision */
+static V brdf_remap(V wo, V wi) {
+    float cosi = wi.z, coso = wo.z;
+    float sini = sinth(wi), sino = sinth(wo);
+    float pi_ = ATAN2F(wi.y, wi.x), po_ = ATAN2F(wo.y, wo.x);
+    float phii = (pi_ < 0.f) ? pi_ + 2.f * PI_F : pi_;   /* SphericalPhi (geometry.h:647-650) */
+    float phio = (po_ < 0.f) ? po_ + 2.f * PI_F : po_;
+    float dphi = phii - phio;
+    if (dphi < 0.) dphi += 2.f * PI_F;
+    if (dphi > 2.f * PI_F) dphi -= 2.f * PI_F;
+    if (dphi > PI_F) dphi = 2.f * PI_F - dphi;
+    return v3(sini * sino, dphi / PI_F, cosi * coso);
+}
+typedef struct { float *v; float sumWeights; int nFound; } IrregProc;
+/* KdTree::privateLookup (kdtree.h:160-185) with IrregIsoProc (reflection.cpp:34-47) */
+static void kd_lookup(const Ctx *c, const pbrtgpu_kdnode *nodes, int nNodes, uint32_t nodeNum, V p, IrregProc *pr,
+                      float maxD2) {
+    const pbrtgpu_kdnode *node = &nodes[nodeNum];
+    int axis = node->split_axis;
+    if (axis != 3) {
+        float pa = vcomp(p, axis);
+        float dist2 = (pa - node->split_pos) * (pa - node->split_pos);
+        if (pa <= node->split_pos) {
+            if (node->has_left) kd_lookup(c, nodes, nNodes, nodeNum + 1, p, pr, maxD2);
+            if (dist2 < maxD2 && node->right_child < nNodes) kd_lookup(c, nodes, nNodes, (uint32_t)node->right_child, p, pr, maxD2);
+        } else {
+            if (node->right_child < nNodes) kd_lookup(c, nodes, nNodes, (uint32_t)node->right_child, p, pr, maxD2);
+            if (dist2 < maxD2 && node->has_left) kd_lookup(c, nodes, nNodes, nodeNum + 1, p, pr, maxD2);
+        }
+    }
+    V d = vsub(v3(node->p[0], node->p[1], node->p[2]), p);   /* DistanceSquared = LengthSquared(p1 - p2) */
+    float dist2 = vlen2(d);
+    if (dist2 < maxD2) {
+        float weight = EXPF(-100.f * dist2);
+        const float *sv = SPEC(c, node->spec);
+        for (int i = 0; i < c->nb; ++i) pr->v[i] += weight * sv[i];
+        pr->sumWeights += weight;
+        ++pr->nFound;
+    }
+}
+/* IrregIsotropicBRDF::f (reflection.cpp:251-264) */
+static void irreg_f(const Ctx *c, const BxDF *b, V wo, V wi, float *f) {
+    V m = brdf_remap(wo, wi);
+    float lastMaxDist2 = .001f;
+    float v[PBRTGPU_MAX_BANDS];
+    for (;;) {
+        IrregProc pr;
+        for (int i = 0; i < c->nb; ++i) v[i] = 0.f;
+        pr.v = v; pr.sumWeights = 0.f; pr.nFound = 0;
+        float maxDist2 = lastMaxDist2;
+        if (b->nkd > 0) kd_lookup(c, b->kd, b->nkd, 0, m, &pr, maxDist2);
+        if (pr.nFound > 2 || lastMaxDist2 > 1.5f) {
+            for (int i = 0; i < c->nb; ++i) f[i] = clampf(v[i], 0.f, INFINITY) / pr.sumWeights;
+            return;
+        }
+        lastMaxDist2 *= 2.f;
+    }
+}
 static void bx_f_add(const Ctx *c, const BxDF *b, V wo, V wi, float *out) {
     int nb = c->nb;
     switch (b->kind) {
+        case BX_MEASURED_IRREG: {
+            float f[PBRTGPU_MAX_BANDS];
+            irreg_f(c, b, wo, wi, f);
+            for (int i = 0; i < nb; ++i) out[i] += f[i];
+            break;
+        }
         case BX_LAMBERT:
             for (int i = 0; i < nb; ++i) out[i] += b->R[i] * INV_PI_F;
             break;
@@ -1044,6 +1111,12 @@ static void get_bsdf(const Ctx *c, const Isect *is, BSDF *bs, DG *dgsOut) {
                 BxDF *x = &bs->bx[bs->n++];
                 x->kind = BX_SPEC_REFL_NOOP; x->type = BSDF_REFLECTION | BSDF_SPECULAR; x->R = SPEC(c, mt->spec[0]);
             }
+            break;
+        }
+        case PBRTGPU_MAT_MEASURED: {   /* measured.cpp:182-206: one IrregIsotropicBRDF */
+            BxDF *x = &bs->bx[bs->n++];
+            x->kind = BX_MEASURED_IRREG; x->type = BSDF_REFLECTION | BSDF_GLOSSY;
+            x->kd = c->s->kdnodes + mt->aux; x->nkd = mt->aux2;
             break;
         }
         case PBRTGPU_MAT_SUBSTRATE: {
@@ -1677,4 +1750,21 @@ long oracle_trace_range(const pbrtgpu_flat_scene *s, long first, long count, int
     free(th);
     pthread_mutex_destroy(&t.mu);
     return count;
+}
+
+/* test hook: IrregIsotropicBRDF::f of material `mat` for local directions wo, wi */
+int oracle_measured_f(const pbrtgpu_flat_scene *s, int mat, const float *wo, const float *wi, float *out) {
+    Ctx c;
+    memset(&c, 0, sizeof(c));
+    c.s = s;
+    c.nb = s->n_bands;
+    const pbrtgpu_material *mt = &s->materials[mat];
+    if (mt->type != PBRTGPU_MAT_MEASURED) return -1;
+    BxDF b;
+    memset(&b, 0, sizeof(b));
+    b.kind = BX_MEASURED_IRREG;
+    b.kd = s->kdnodes + mt->aux;
+    b.nkd = mt->aux2;
+    irreg_f(&c, &b, v3(wo[0], wo[1], wo[2]), v3(wi[0], wi[1], wi[2]), out);
+    return 0;
 }

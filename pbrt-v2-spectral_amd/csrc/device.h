@@ -234,6 +234,7 @@ struct DevScene {
     const pbrtgpu_instance *insts;    // TransformedPrimitive records (may be empty)
     const int *primInst;              // per prim: owning instance or -1
     int nInsts;
+    const pbrtgpu_kdnode *kd;         // measured BRDF kd-trees
 };
 
 struct DG { V p, nn, dpdu, dpdv, dndu, dndv; float u, v; };
@@ -761,7 +762,7 @@ PGD_HEAVY void isect_fill(const DevScene &S, const Ray &ray, int prim, float t, 
 
 // ------------------------------------------------------------------ BSDF
 enum { BSDF_REFLECTION = 1, BSDF_TRANSMISSION = 2, BSDF_DIFFUSE = 4, BSDF_GLOSSY = 8, BSDF_SPECULAR = 16, BSDF_ALL = 31 };
-enum { BX_LAMBERT, BX_OREN, BX_MICRO_BLINN_DIEL, BX_SPEC_REFL_NOOP, BX_FRESNEL_BLEND_ANISO };
+enum { BX_LAMBERT, BX_OREN, BX_MICRO_BLINN_DIEL, BX_SPEC_REFL_NOOP, BX_FRESNEL_BLEND_ANISO, BX_MEASURED_IRREG };
 struct BxDF { int kind, type; int R, R2; float a, b; };   // R, R2: offsets into DevScene::spectra
 struct BSDF { V nn, ng, sn, tn; int n; BxDF bx[2]; };
 PGD_INLINE bool matches(const BxDF &b, int flags) { return (b.type & flags) == b.type; }
@@ -864,7 +865,9 @@ PGD_INLINE void aniso_sample(float ex, float ey, V wo, V *wi, float u1, float u2
 // evaluated band by band where it is consumed (fval).  fval reproduces the reference's
 // accumulation exactly: f = 0; for each matching BxDF: f += term_i  (reflection.cpp:
 // 478-512), with every term's operand order as in BxDF::f (reflection.cpp, microfacet.h).
-enum { T_ZERO = 0, T_LAMB, T_OREN, T_BLINN, T_FB };
+// T_MEAS: IrregIsotropicBRDF at BRDFRemap point (s0, s1, s2), kd-tree nodes [R, R + R2);
+// once looked up (measured_prepare) it becomes T_BUF: the spectrum in the slot's scratch bands
+enum { T_ZERO = 0, T_LAMB, T_OREN, T_BLINN, T_FB, T_MEAS, T_BUF };
 struct FTerm { int kind; int R, R2; float s0, s1, s2, s3; };
 enum { FV_SUM = 0, FV_SPEC = 1 };
 struct FVal { int mode, n; FTerm t[2]; float d; int R; };   // FV_SUM with n == 0: zero spectrum
@@ -905,6 +908,19 @@ PGD_INLINE void fval_push(FVal &F, const FTerm &t) {   // static indices only (n
 }
 
 // BxDF::f(wo, wi) as a term (scalars per direction pair)
+// BRDFRemap (reflection.cpp:239-248); pbrt.h:179 defines M_PI as a float literal
+PGD_INLINE V brdf_remap(V wo, V wi) {
+    float cosi = wi.z, coso = wo.z;
+    float sini = sinth(wi), sino = sinth(wo);
+    float pi_ = ATAN2F(wi.y, wi.x), po_ = ATAN2F(wo.y, wo.x);
+    float phii = (pi_ < 0.f) ? pi_ + 2.f * kPi : pi_;   // SphericalPhi (geometry.h:647-650)
+    float phio = (po_ < 0.f) ? po_ + 2.f * kPi : po_;
+    float dphi = phii - phio;
+    if (dphi < 0.) dphi += 2.f * kPi;
+    if (dphi > 2.f * kPi) dphi -= 2.f * kPi;
+    if (dphi > kPi) dphi = 2.f * kPi - dphi;
+    return v3(sini * sino, dphi / kPi, cosi * coso);
+}
 PGD_INLINE FTerm bx_term(const BxDF &b, V wo, V wi) {
     FTerm t;
     t.kind = T_ZERO; t.R = b.R; t.R2 = b.R2; t.s0 = t.s1 = t.s2 = t.s3 = 0.f;
@@ -950,6 +966,12 @@ PGD_INLINE FTerm bx_term(const BxDF &b, V wo, V wi) {
             t.s0 = ta; t.s1 = tb;
             t.s2 = POWF(1 - vdot(wi, wh), 5.f);
             t.s3 = D / den;
+            break;
+        }
+        case BX_MEASURED_IRREG: {
+            V m = brdf_remap(wo, wi);
+            t.kind = T_MEAS;
+            t.s0 = m.x; t.s1 = m.y; t.s2 = m.z;
             break;
         }
         default: break;   // SpecularReflection::f == 0
@@ -1137,6 +1159,13 @@ PGD_HEAVY void get_bsdf(const DevScene &S, const Isect &is, BSDF &bs, V *pOut, V
                 x.kind = BX_SPEC_REFL_NOOP; x.type = BSDF_REFLECTION | BSDF_SPECULAR; x.R = mt.spec[0]; x.R2 = x.R;
                 x.a = x.b = 0.f;
             }
+            break;
+        }
+        case PBRTGPU_MAT_MEASURED: {   // measured.cpp:182-206: one IrregIsotropicBRDF
+            BxDF &x = bs.bx[bs.n++];
+            x.kind = BX_MEASURED_IRREG; x.type = BSDF_REFLECTION | BSDF_GLOSSY;
+            x.R = mt.aux; x.R2 = mt.aux2;
+            x.a = x.b = 0.f;
             break;
         }
         case PBRTGPU_MAT_SUBSTRATE: {

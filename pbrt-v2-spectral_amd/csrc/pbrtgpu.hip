@@ -294,7 +294,7 @@ static int ensure_slots(pbrtgpu_ctx *c, int cap, int NB) {
     auto take = [&](size_t bytes) { size_t o = off; off += (bytes + 255) & ~(size_t)255; return o; };
     size_t oItem = take(C * 4), oHp = take(C * 4), oSmp = take(C * 4), oBounce = take(C * 4), oFlags = take(C * 4),
            oMt = take(C * 20), oBeta = take(C * 2 * NBP * 4), oL = take(C * NBP * 4), oA = take(C * NBP * 4),
-           oB = take(C * NBP * 4), oRay = take(C * 27 * 4), oHitP = take(C * 8), oHitT = take(C * 8), oOcc = take(C * 4),
+           oB = take(C * NBP * 4), oM = take(C * NBP * 4), oRay = take(C * 27 * 4), oHitP = take(C * 8), oHitT = take(C * 8), oOcc = take(C * 4),
            oQC = take(C * 16), oQS = take(C * 8), oCnt = take(CNT_WORDS * 4);
     HIPCHK(c->slots.ensure(off));
     char *base = (char *)c->slots.p;
@@ -303,6 +303,7 @@ static int ensure_slots(pbrtgpu_ctx *c, int cap, int NB) {
     P.item = (int *)(base + oItem); P.hp = (uint32_t *)(base + oHp); P.smp = (uint32_t *)(base + oSmp);
     P.bounce = (int *)(base + oBounce); P.flags = (uint32_t *)(base + oFlags); P.mt = (uint32_t *)(base + oMt);
     P.beta = (float4 *)(base + oBeta); P.L = (float4 *)(base + oL); P.A = (float4 *)(base + oA); P.B = (float4 *)(base + oB);
+    P.M = (float4 *)(base + oM);
     P.ray = (float *)(base + oRay); P.hitPrim = (int *)(base + oHitP); P.hitT = (float *)(base + oHitT);
     P.occ = (uint32_t *)(base + oOcc); P.qC = (uint32_t *)(base + oQC); P.qS = (uint32_t *)(base + oQS);
     P.cnt = (uint32_t *)(base + oCnt);
@@ -453,7 +454,8 @@ int pbrtgpu_scene_upload(pbrtgpu_ctx *c, const pbrtgpu_flat_scene *s) {
     for (int i = 0; i < s->n_lights; ++i)
         if (s->lights[i].type == PBRTGPU_LIGHT_INFINITE) return fail(PBRTGPU_E_UNSUPPORTED, "infinite lights not yet supported");
     for (int i = 0; i < s->n_materials; ++i)
-        if (s->materials[i].type > PBRTGPU_MAT_SUBSTRATE) return fail(PBRTGPU_E_UNSUPPORTED, "material type not yet supported on the GPU");
+        if (s->materials[i].type > PBRTGPU_MAT_SUBSTRATE && s->materials[i].type != PBRTGPU_MAT_MEASURED)
+            return fail(PBRTGPU_E_UNSUPPORTED, "material type not yet supported on the GPU");
     HIPCHK(hipSetDevice(c->device));
     HIPCHK(hipStreamSynchronize(c->stream));
     c->hasScene = false;
@@ -571,6 +573,15 @@ int pbrtgpu_scene_upload(pbrtgpu_ctx *c, const pbrtgpu_flat_scene *s) {
         HIPCHK(upload(c, pi.data(), pi.size(), &S.primInst));
     }
     HIPCHK(upload(c, pool.data(), pool.size(), &S.spectra));
+    {
+        std::vector<pbrtgpu_kdnode> kd(s->kdnodes, s->kdnodes + std::max(0, s->n_kdnodes));
+        for (auto &k : kd)
+            if (!remap(k.spec, &k.spec)) return fail(PBRTGPU_E_INVALID, "kd-tree spectrum offset");
+        for (auto &m : mats)
+            if (m.type == PBRTGPU_MAT_MEASURED && (m.aux < 0 || m.aux2 < 0 || m.aux + m.aux2 > (int)kd.size()))
+                return fail(PBRTGPU_E_INVALID, "measured material kd-tree range");
+        HIPCHK(upload(c, kd.data(), kd.size(), &S.kd));
+    }
     c->nb = s->n_bands;
     c->spp = s->spp;
     c->cam = s->camera;

@@ -54,6 +54,7 @@ struct PathSoA {
     float4 *beta;       // [2][NQ][cap]: beta at even / odd vertices
     float4 *L;          // [NQ][cap]
     float4 *A, *B;      // [NQ][cap]
+    float4 *M;          // [NQ][cap]: measured-BRDF spectrum of the BSDF value being consumed
     float *ray;         // [3][9][cap]: o.xyz, d.xyz, mint, maxt, time  for RAY_C, RAY_M, RAY_S
     int *hitPrim;       // [2][cap]  (RAY_C, RAY_M)
     float *hitT;        // [2][cap]
@@ -121,7 +122,7 @@ PGD_INLINE float term_val(const FTerm &t, float r, float r2) {
         default: return 0.f;
     }
 }
-PGD_INLINE float4 fval4(const float *sp, const FVal &F, int q) {
+PGD_INLINE float4 fval4(const float *sp, const FVal &F, int q, const float4 *mb, size_t c) {
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
     if (F.mode == FV_SPEC) {
         float4 r = ld4(sp + F.R + 4 * q);
@@ -131,6 +132,11 @@ PGD_INLINE float4 fval4(const float *sp, const FVal &F, int q) {
     for (int k = 0; k < 2; ++k) {
         if (k < F.n) {
             const FTerm &t = F.t[k];
+            if (t.kind == T_BUF) {
+                float4 m = mb[q * c];
+                v.x += m.x; v.y += m.y; v.z += m.z; v.w += m.w;
+                continue;
+            }
             float4 r = ld4(sp + t.R + 4 * q);
             float4 r2 = t.kind == T_FB ? ld4(sp + t.R2 + 4 * q) : r;
             v.x += term_val(t, r.x, r2.x);
@@ -140,6 +146,85 @@ PGD_INLINE float4 fval4(const float *sp, const FVal &F, int q) {
         }
     }
     return v;
+}
+
+// IrregIsotropicBRDF::f (reflection.cpp:251-264): KdTree::Lookup (kdtree.h:160-185) with
+// IrregIsoProc (reflection.cpp:34-47), accumulating the spectrum in the slot's M bands in
+// the reference's visiting order; an iterative walk of the recursive post-order lookup
+template <int NB>
+PGD_INLINE void measured_lookup(const DevScene &S, const FTerm &t, float4 *mb, size_t c) {
+    constexpr int NQ = Bands<NB>::NQ;
+    const pbrtgpu_kdnode *nodes = S.kd + t.R;
+    const int nNodes = t.R2;
+    const float p[3] = {t.s0, t.s1, t.s2};
+    float lastMaxDist2 = .001f;
+    for (;;) {
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) mb[q * c] = make_float4(0.f, 0.f, 0.f, 0.f);
+        float sumWeights = 0.f;
+        int nFound = 0;
+        const float maxD2 = lastMaxDist2;
+        uint32_t stk[64];   // node << 2 | state
+        int top = 0;
+        if (nNodes > 0) stk[top++] = 0u;
+        while (top > 0) {
+            const uint32_t e = stk[--top];
+            const uint32_t n = e >> 2, state = e & 3u;
+            const pbrtgpu_kdnode nd = nodes[n];
+            const int axis = nd.split_axis;
+            const float pa = axis == 0 ? p[0] : (axis == 1 ? p[1] : p[2]);
+            const bool leftFirst = pa <= nd.split_pos;
+            const float dist2s = (pa - nd.split_pos) * (pa - nd.split_pos);
+            const bool hasRight = nd.right_child < nNodes, hasLeft = nd.has_left != 0;
+            if (state == 0u && axis != 3) {
+                stk[top++] = (n << 2) | 1u;
+                if (leftFirst ? hasLeft : hasRight) stk[top++] = (leftFirst ? n + 1 : (uint32_t)nd.right_child) << 2;
+                continue;
+            }
+            if (state == 1u) {
+                stk[top++] = (n << 2) | 2u;
+                if (dist2s < maxD2 && (leftFirst ? hasRight : hasLeft))
+                    stk[top++] = (leftFirst ? (uint32_t)nd.right_child : n + 1) << 2;
+                continue;
+            }
+            // process the node (after its children)
+            V d = vsub(v3(nd.p[0], nd.p[1], nd.p[2]), v3(p[0], p[1], p[2]));
+            float dist2 = vlen2(d);
+            if (dist2 < maxD2) {
+                float weight = (float)pbrt_fm_exp((double)(-100.f * dist2));   // expf
+                const float *sv = S.spectra + nd.spec;
+#pragma unroll
+                for (int q = 0; q < NQ; ++q) {
+                    float4 a = mb[q * c], s = ld4(sv + 4 * q);
+                    a.x += weight * s.x; a.y += weight * s.y; a.z += weight * s.z; a.w += weight * s.w;
+                    mb[q * c] = a;
+                }
+                sumWeights += weight;
+                ++nFound;
+            }
+        }
+        if (nFound > 2 || lastMaxDist2 > 1.5f) {
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                float4 a = mb[q * c];
+                mb[q * c] = make_float4(clampf(a.x, 0.f, INFINITY) / sumWeights, clampf(a.y, 0.f, INFINITY) / sumWeights,
+                                        clampf(a.z, 0.f, INFINITY) / sumWeights, clampf(a.w, 0.f, INFINITY) / sumWeights);
+            }
+            return;
+        }
+        lastMaxDist2 *= 2.f;
+    }
+}
+// materialise a measured term of F into the slot's M bands (T_MEAS -> T_BUF)
+template <int NB>
+PGD_INLINE void fval_prepare(const DevScene &S, FVal &F, float4 *mb, size_t c) {
+    if (F.mode != FV_SUM) return;
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+        if (k < F.n && F.t[k].kind == T_MEAS) {
+            measured_lookup<NB>(S, F.t[k], mb, c);
+            F.t[k].kind = T_BUF;
+        }
 }
 
 // camera sample of an item -> fresh path in `slot` (SamplerRendererTask::Run,
@@ -229,6 +314,7 @@ PGD_INLINE Pushes shade_vertex(const DevScene &S, const PathSoA &P, int slot, in
     const float *sp = S.spectra;
     Pushes out = {false, false, false};
     const float4 *beta = P.beta + (size_t)(vb & 1) * NQ * c + slot;
+    float4 *mb = P.M + slot;
     Isect is;
     isect_fill(S, ray, prim, thit, is);
     if (vb == 0 || (fl & PF_SPEC)) {
@@ -297,6 +383,7 @@ PGD_INLINE Pushes shade_vertex(const DevScene &S, const PathSoA &P, int slot, in
         } else if (lit) liBlack = Lt.is_black != 0;
         if (lightPdf > 0. && !liBlack) {
             bsdf_f(bs, wo, wi, flags, F);
+            fval_prepare<NB>(S, F, mb, c);
             float sc;
             if (isPoint) sc = fabsf(vdot(wi, n)) / lightPdf;
             else {
@@ -309,7 +396,7 @@ PGD_INLINE Pushes shade_vertex(const DevScene &S, const PathSoA &P, int slot, in
             bool black = true;
 #pragma unroll
             for (int q = 0; q < NQ; ++q) {
-                float4 f = fval4(sp, F, q), e = ld4(Ls + 4 * q), a;
+                float4 f = fval4(sp, F, q, mb, c), e = ld4(Ls + 4 * q), a;
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
                     float li = isPoint ? (cmp(e, k) / lscale) : cmp(e, k);
@@ -331,6 +418,7 @@ PGD_INLINE Pushes shade_vertex(const DevScene &S, const PathSoA &P, int slot, in
             int sampledType;
             bsdf_sample_f(bs, wo, &wi, ub[0], ub[1], ub[2], &bsdfPdf, flags, &sampledType, F);
             if (bsdfPdf > 0. && !(F.mode == FV_SUM && F.n == 0)) {
+                fval_prepare<NB>(S, F, mb, c);
                 float weight = 1.f;
                 bool go = true;
                 if (!(sampledType & BSDF_SPECULAR)) {
@@ -344,7 +432,7 @@ PGD_INLINE Pushes shade_vertex(const DevScene &S, const PathSoA &P, int slot, in
                     bool black = true;
 #pragma unroll
                     for (int q = 0; q < NQ; ++q) {
-                        float4 f = fval4(sp, F, q), e = ld4(Ls + 4 * q), b;
+                        float4 f = fval4(sp, F, q, mb, c), e = ld4(Ls + 4 * q), b;
 #pragma unroll
                         for (int k = 0; k < 4; ++k) {
                             cmp(b, k) = (((cmp(f, k) * cmp(e, k)) * ad) * weight) / bsdfPdf;
@@ -394,13 +482,14 @@ PGD_INLINE Pushes shade_vertex(const DevScene &S, const PathSoA &P, int slot, in
     bsdf_sample_f(bs, wo, &wi, up[0], up[1], up[2], &pdf, BSDF_ALL, &sflags, F);
     bool cont = pdf != 0. && !(F.mode == FV_SUM && F.n == 0);
     if (cont) {
+        fval_prepare<NB>(S, F, mb, c);
         const float ad = fabsf(vdot(wi, n));
         float4 *bn = P.beta + (size_t)((vb + 1) & 1) * NQ * c + slot;
         float4 nb4[NQ];
         bool black = true;
 #pragma unroll
         for (int q = 0; q < NQ; ++q) {
-            float4 f = fval4(sp, F, q), b = beta[q * c];
+            float4 f = fval4(sp, F, q, mb, c), b = beta[q * c];
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 cmp(nb4[q], k) = cmp(b, k) * ((cmp(f, k) * ad) / pdf);

@@ -203,7 +203,15 @@ struct Isect {
     }
 };
 
-struct MaterialObj { pbrtgpu_material m{}; std::vector<Spec> spectra; int flatIndex = -1; };
+// measured BRDF (measured.cpp:90-128): samples in BRDFRemap coordinates with spectra
+struct BrdfSample { V3 p; Spec v; };
+struct MeasuredData { std::vector<BrdfSample> samples; int flatFirst = -1; };
+struct MaterialObj {
+    pbrtgpu_material m{};
+    std::vector<Spec> spectra;
+    std::shared_ptr<MeasuredData> measured;
+    int flatIndex = -1;
+};
 struct LightObj {
     pbrtgpu_light l{};
     Spec L;
@@ -777,6 +785,9 @@ private:
     float GetFloat(const ParamSet &g, const ParamSet &m, const std::string &n, float d) {
         return g.FindOneFloat(n, m.FindOneFloat(n, d));
     }
+    std::string GetString(const ParamSet &g, const ParamSet &m, const std::string &n, const std::string &d) {
+        return g.FindOneString(n, m.FindOneString(n, d));   // TextureParams::FindFilename / FindString
+    }
     Spec GetSpec(const ParamSet &g, const ParamSet &m, const std::string &n, const Spec &d) {
         return g.FindOneSpectrum(n, m.FindOneSpectrum(n, d));
     }
@@ -835,9 +846,126 @@ private:
             mo->spectra.push_back(SpecClamp(ConstSpecTex(g, m, "Ks", spec.Const(.5f))));
             mt.f[0] = ConstFloatTex(g, m, "uroughness", .1f);
             mt.f[1] = ConstFloatTex(g, m, "vroughness", .1f);
+        } else if (name == "measured") {   // measured.cpp:66-130, 182-206 (.brdf: IrregIsotropicBRDF)
+            mt.type = PBRTGPU_MAT_MEASURED;
+            std::string fn = Resolve(GetString(g, m, "filename", ""));
+            size_t dot = fn.rfind('.');
+            std::string suf = dot == std::string::npos ? "" : fn.substr(dot);
+            if (suf != ".brdf" && suf != ".BRDF")
+                throw std::runtime_error("measured BRDF '" + fn + "': only the irregular .brdf format is supported");
+            auto it = measuredCache.find(fn);
+            if (it == measuredCache.end()) it = measuredCache.insert(std::make_pair(fn, LoadIrregBrdf(fn))).first;
+            mo->measured = it->second;
         } else
             throw std::runtime_error("material '" + name + "' is not supported by this build yet");
         return mo;
+    }
+    std::map<std::string, std::shared_ptr<MeasuredData> > measuredCache;
+    // ReadFloatFile (floatfile.cpp:30-74)
+    static std::vector<float> ReadFloatFile(const std::string &fn) {
+        FILE *fp = fopen(fn.c_str(), "r");
+        if (!fp) throw std::runtime_error("Unable to open file " + fn);
+        std::vector<float> values;
+        int c;
+        bool inNumber = false;
+        char cur[32];
+        int pos = 0;
+        while ((c = getc(fp)) != EOF) {
+            if (inNumber) {
+                if (isdigit(c) || c == '.' || c == 'e' || c == '-' || c == '+') { if (pos < 31) cur[pos++] = (char)c; }
+                else { cur[pos] = 0; values.push_back((float)atof(cur)); inNumber = false; pos = 0; }
+            } else {
+                if (isdigit(c) || c == '.' || c == '-' || c == '+') { inNumber = true; cur[pos++] = (char)c; }
+                else if (c == '#') { while ((c = getc(fp)) != '\n' && c != EOF) {} }
+            }
+        }
+        fclose(fp);
+        return values;
+    }
+    // BRDFRemap (reflection.cpp:239-248); pbrt.h:179 defines M_PI as a float literal, so
+    // everything is single precision
+    static V3 BRDFRemap(const V3 &wo, const V3 &wi) {
+        const float kPiF = 3.14159265358979323846f;
+        float cosi = wi.z, coso = wo.z;
+        float sini = sqrtf(pmax(0.f, 1.f - cosi * cosi)), sino = sqrtf(pmax(0.f, 1.f - coso * coso));
+        float pi_ = atan2f(wi.y, wi.x); float phii = (pi_ < 0.f) ? pi_ + 2.f * kPiF : pi_;
+        float po_ = atan2f(wo.y, wo.x); float phio = (po_ < 0.f) ? po_ + 2.f * kPiF : po_;
+        float dphi = phii - phio;
+        if (dphi < 0.) dphi += 2.f * kPiF;
+        if (dphi > 2.f * kPiF) dphi -= 2.f * kPiF;
+        if (dphi > kPiF) dphi = 2.f * kPiF - dphi;
+        return V3(sini * sino, dphi / kPiF, cosi * coso);
+    }
+    std::shared_ptr<MeasuredData> LoadIrregBrdf(const std::string &fn) {
+        std::vector<float> values = ReadFloatFile(fn);
+        if (values.empty()) throw std::runtime_error("Unable to read BRDF data from file " + fn);
+        size_t pos = 0;
+        int numWls = (int)values[pos++];
+        if ((values.size() - 1 - numWls) % (4 + numWls) != 0)
+            throw std::runtime_error("Excess or insufficient data in theta, phi BRDF file " + fn);
+        std::vector<float> wls(values.begin() + 1, values.begin() + 1 + numWls);
+        pos += numWls;
+        auto md = std::make_shared<MeasuredData>();
+        while (pos < values.size()) {
+            float thetai = values[pos++], phii = values[pos++], thetao = values[pos++], phio = values[pos++];
+            V3 wo(sinf(thetao) * cosf(phio), sinf(thetao) * sinf(phio), cosf(thetao));   // SphericalDirection
+            V3 wi(sinf(thetai) * cosf(phii), sinf(thetai) * sinf(phii), cosf(thetai));
+            BrdfSample s;
+            s.v = spec.FromSampled(wls.data(), &values[pos], numWls);
+            pos += numWls;
+            s.p = BRDFRemap(wo, wi);
+            md->samples.push_back(s);
+        }
+        return md;
+    }
+    // KdTree construction (kdtree.h:100-148) into out->kdnodes
+    void KdBuild(std::vector<pbrtgpu_kdnode> &nodes, std::vector<int> &nodeSample, uint32_t nodeNum, int start, int end,
+                 const BrdfSample **bn, uint32_t *nextFree, const BrdfSample *base) {
+        if (start + 1 == end) {
+            nodes[nodeNum].split_axis = 3; nodes[nodeNum].right_child = (1 << 29) - 1; nodes[nodeNum].has_left = 0;
+            nodeSample[nodeNum] = (int)(bn[start] - base);
+            return;
+        }
+        BBox bound;
+        for (int i = start; i < end; ++i) bound = Union(bound, bn[i]->p);
+        int axis = bound.MaximumExtent();
+        int splitPos = (start + end) / 2;
+        std::nth_element(&bn[start], &bn[splitPos], &bn[end], [axis](const BrdfSample *a, const BrdfSample *b) {
+            return a->p[axis] == b->p[axis] ? (a < b) : a->p[axis] < b->p[axis];
+        });
+        nodes[nodeNum].split_pos = bn[splitPos]->p[axis];
+        nodes[nodeNum].split_axis = axis;
+        nodes[nodeNum].right_child = (1 << 29) - 1;
+        nodes[nodeNum].has_left = 0;
+        nodeSample[nodeNum] = (int)(bn[splitPos] - base);
+        if (start < splitPos) {
+            nodes[nodeNum].has_left = 1;
+            uint32_t child = (*nextFree)++;
+            KdBuild(nodes, nodeSample, child, start, splitPos, bn, nextFree, base);
+        }
+        if (splitPos + 1 < end) {
+            nodes[nodeNum].right_child = (int)(*nextFree)++;
+            KdBuild(nodes, nodeSample, nodes[nodeNum].right_child, splitPos + 1, end, bn, nextFree, base);
+        }
+    }
+    int EmitMeasured(MeasuredData *md, int *count) {
+        int n = (int)md->samples.size();
+        *count = n;
+        if (md->flatFirst >= 0) return md->flatFirst;
+        std::vector<pbrtgpu_kdnode> nodes(n);
+        std::vector<int> nodeSample(n, -1);
+        std::vector<const BrdfSample *> bn(n);
+        for (int i = 0; i < n; ++i) bn[i] = &md->samples[i];
+        uint32_t nextFree = 1;
+        if (n > 0) KdBuild(nodes, nodeSample, 0, 0, n, bn.data(), &nextFree, md->samples.data());
+        for (int i = 0; i < n; ++i) {
+            const BrdfSample &s = md->samples[nodeSample[i]];
+            for (int k = 0; k < 3; ++k) nodes[i].p[k] = s.p[k];
+            nodes[i].spec = EmitSpectrum(s.v);
+        }
+        md->flatFirst = (int)out->kdnodes.size();
+        out->kdnodes.insert(out->kdnodes.end(), nodes.begin(), nodes.end());
+        return md->flatFirst;
     }
     std::shared_ptr<MaterialObj> CreateMaterialFromState(const ParamSet &params) {   // api.cpp:1127-1143
         if (gs.currentNamedMaterial != "") {
@@ -1164,6 +1292,7 @@ private:
         if (m->flatIndex >= 0) return m->flatIndex;
         pbrtgpu_material fm = m->m;
         for (int k = 0; k < 4; ++k) fm.spec[k] = k < (int)m->spectra.size() ? EmitSpectrum(m->spectra[k]) : -1;
+        if (m->measured) fm.aux = EmitMeasured(m->measured.get(), &fm.aux2);
         out->materials.push_back(fm);
         m->flatIndex = (int)out->materials.size() - 1;
         return m->flatIndex;
@@ -1372,6 +1501,7 @@ void HostScene::Flat(pbrtgpu_flat_scene *f) const {
     f->n_spectra_floats = (int)spectra.size(); f->spectra = spectra.data();
     f->n_instances = (int)instances.size(); f->instances = instances.empty() ? nullptr : instances.data();
     f->prim_instance = primInstance.data();
+    f->n_kdnodes = (int)kdnodes.size(); f->kdnodes = kdnodes.empty() ? nullptr : kdnodes.data();
 }
 
 }  // namespace pbrtamd

@@ -53,6 +53,7 @@ struct HostScene {
     std::vector<float> spectra;
     std::vector<pbrtgpu_instance> instances;
     std::vector<int32_t> primInstance;        // per prim: owning instance or -1
+    std::vector<pbrtgpu_kdnode> kdnodes;      // measured BRDF kd-trees
     // diagnostics
     std::vector<std::string> warnings;
     int bvhMaxDepth = 0;

@@ -55,7 +55,8 @@ class FlatScene(ctypes.Structure):
                 ("n_quadrics", I32), ("quadrics", P), ("n_materials", I32), ("materials", P),
                 ("n_lights", I32), ("lights", P), ("n_light_shapes", I32), ("light_shapes", P),
                 ("n_spectra_floats", I32), ("spectra", P),
-                ("n_instances", I32), ("instances", P), ("prim_instance", P)]
+                ("n_instances", I32), ("instances", P), ("prim_instance", P),
+                ("n_kdnodes", I32), ("kdnodes", P)]
 
 
 class Overrides(ctypes.Structure):
@@ -71,7 +72,7 @@ class RenderDesc(ctypes.Structure):
 STAT_PATHS, STAT_KERNEL_MS, STAT_ACCUM_MS, STAT_ZEROED, STAT_SPILLS, STAT_PASSES = 0, 1, 2, 3, 4, 5
 F_ACCUMULATE, F_COUNT_WORK = 1, 2
 KEEP_SEED = 0xFFFFFFFF
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 
 class Timing(ctypes.Structure):

@@ -11,6 +11,8 @@ Fixtures (numpy .npz, inputs + expected outputs only):
                                   that land on neighbouring pixels)
   anim_paths_48x48s4.npz, anim_film_40x40s8.npz   the motion-blur scene (C5): animated
                                   TransformedPrimitives over nested BVHs
+  bunny_paths_64x36s4.npz, bunny_film_48x27s8.npz   C3: measured BRDF (mystique, kd-tree
+                                  lookups), point light, disk area light
   mt19937_kat.npz                 first 64 outputs of RNG(seed) for 6 seeds
   fromrgb_32.npz                  SampledSpectrum::FromRGB (reflectance and illuminant) for 14
                                   RGB triples, 32 bands 395-715 nm
@@ -72,6 +74,8 @@ def main():
         film_fixture("killeroo_film_96x72s16", (96, 72), 16, 0, 5, tmp)
         paths_fixture("anim_paths_48x48s4", (48, 48), 4, 0, 5, 3, tmp, scene="anim-killeroos-moving.pbrt")
         film_fixture("anim_film_40x40s8", (40, 40), 8, 0, 5, tmp, scene="anim-killeroos-moving.pbrt")
+        paths_fixture("bunny_paths_64x36s4", (64, 36), 4, 0, 5, 3, tmp, scene="bunny.pbrt")
+        film_fixture("bunny_film_48x27s8", (48, 27), 8, 0, 5, tmp, scene="bunny.pbrt")
         fn = os.path.join(tmp, "mt.bin")
         run(["-", "--kat-mt", fn])
         raw = np.fromfile(fn, dtype=np.uint32).reshape(6, 65)

@@ -17,6 +17,7 @@ REF = "/root/reference/scenes"
 PACKS = [
     ("killeroo-simple", "killeroo-simple.pbrt", 32, 700, 700, 256),
     ("anim-killeroos-moving", "anim-killeroos-moving.pbrt", 32, 600, 600, 512),
+    ("bunny", "bunny.pbrt", 32, 1920, 1080, 1024),
 ]
 
 
