@@ -200,6 +200,13 @@ PBRT_FM_FN double pbrt_fm_log(double x) {
     double de = (double)e;
     return (de * PBRT_FM_LN2_HI + lm) + de * PBRT_FM_LN2_LO;
 }
+/* ln(x) for every x (NaN / negative -> NaN, 0 -> -inf, +inf -> +inf) */
+PBRT_FM_FN double pbrt_fm_log_any(double x) {
+    if (pbrt_fm_isnan(x) || x < 0.0) return pbrt_fm_from_bits(0x7ff8000000000000ull);
+    if (x == 0.0) return pbrt_fm_from_bits(0xfff0000000000000ull);
+    if (pbrt_fm_isinf(x)) return x;
+    return pbrt_fm_log(x);
+}
 PBRT_FM_FN double pbrt_fm_exp(double z) {
     if (pbrt_fm_isnan(z)) return z;
     if (z > 709.8) return pbrt_fm_from_bits(0x7ff0000000000000ull);

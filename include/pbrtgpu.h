@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define PBRTGPU_ABI_VERSION 4
+#define PBRTGPU_ABI_VERSION 5
 #define PBRTGPU_MAX_BANDS 64
 
 #define PBRTGPU_E_INVALID   (-1)
@@ -89,14 +89,41 @@ enum {
     PBRTGPU_MAT_MEASURED = 6    /* IrregIsotropicBRDF: aux = first kd-tree node, aux2 = node count */
 };
 
-/* material with constant textures; f[7] = constant bump displacement (Material::Bump,
- * material.cpp:39-81, always applied because bumpmap defaults to constant 0) */
+/* Texture<float> / Texture<Spectrum> (texture.h, textures/{constant,scale,imagemap}.cpp).
+ * IMAGE textures are the reference's one-texel MIPMap: ReadImage's 1x1 RGB 0.5 fallback for
+ * files it cannot decode (imageio.cpp:45-66) or powf(scale, gamma) when a .tga/.pfm is
+ * missing (imagemap.cpp:64-70); texels are stored after convertIn.  Lookups follow
+ * MIPMap::Lookup (EWA, mipmap.h:278-375, or width-based, :232-259) with the ImageWrap mode,
+ * texture coordinates from UVMapping2D (texture.cpp:80-90). */
+enum { PBRTGPU_TEX_CONST = 0, PBRTGPU_TEX_IMAGE = 1, PBRTGPU_TEX_SCALE = 2 };
+enum { PBRTGPU_WRAP_REPEAT = 0, PBRTGPU_WRAP_BLACK = 1, PBRTGPU_WRAP_CLAMP = 2 };
+typedef struct pbrtgpu_texture {
+    int32_t type;          /* PBRTGPU_TEX_* */
+    int32_t spectral;      /* 1: Texture<Spectrum> (value = FromRGB(reflectance) of the texel) */
+    int32_t tex1, tex2;    /* SCALE operands (texture indices; CONST or IMAGE leaves) */
+    int32_t spec;          /* CONST spectral: offset into spectra[] */
+    int32_t wrap;          /* IMAGE: PBRTGPU_WRAP_* */
+    int32_t trilinear;     /* IMAGE: doTrilinear || noFiltering (width-based lookup, no EWA) */
+    float value;           /* CONST float */
+    float texel[3];        /* IMAGE: the single MIPMap texel (RGB; float textures use [0]) */
+    float su, sv, du, dv;  /* UVMapping2D */
+    float max_aniso;
+} pbrtgpu_texture;
+
+/* Material parameters.  A spectrum slot is either the constant spec[i] or, when
+ * tex[i] >= 0, a spectrum texture evaluated per hit (at most one textured slot).  The bump
+ * displacement is the constant f[7] or, when bump_tex >= 0, a float texture (Material::Bump,
+ * material.cpp:39-81, is applied either way: bumpmap defaults to constant 0).
+ * black_mask bit i: constant spec[i] IsBlack() (plastic/substrate/mirror skip such BxDFs). */
 typedef struct pbrtgpu_material {
     int32_t type;
     int32_t spec[4];      /* offsets (in floats) into spectra[] */
     int32_t aux, aux2;
-    int32_t pad0;
+    int32_t bump_tex;
     float f[8];
+    int32_t tex[4];
+    int32_t black_mask;
+    int32_t pad[3];
 } pbrtgpu_material;
 
 enum { PBRTGPU_LIGHT_AREA = 0, PBRTGPU_LIGHT_POINT = 1, PBRTGPU_LIGHT_INFINITE = 2 };
@@ -112,6 +139,12 @@ typedef struct pbrtgpu_light {
     int32_t pad[3];
     float l2w_m[16];
     float l2w_minv[16];
+    /* infinite (InfiniteAreaLight, lights/infinite.cpp): the radiance MIPMap's single texel
+     * (RGB, after L.ToRGBSpectrum()) with its wrap mode; Distribution2D of the one-texel
+     * image: map_pdf = SampleContinuous's pdf, dist_pdf = Distribution2D::Pdf */
+    float texel[3];
+    float map_pdf, dist_pdf;
+    int32_t wrap, pad2[2];
 } pbrtgpu_light;
 
 typedef struct pbrtgpu_light_shape {
@@ -159,6 +192,8 @@ typedef struct pbrtgpu_camera {
     int32_t xres, yres;
     int32_t px_start, px_count, py_start, py_count;   /* film pixel window */
     int32_t sx_start, sx_end, sy_start, sy_end;       /* sample extent (incl. border) */
+    float dx_camera[3], dy_camera[3];                 /* PerspectiveCamera dxCamera / dyCamera */
+    int32_t pad[2];
 } pbrtgpu_camera;
 
 typedef struct pbrtgpu_flat_scene {
@@ -185,6 +220,10 @@ typedef struct pbrtgpu_flat_scene {
     int32_t n_instances; const pbrtgpu_instance *instances;
     const int32_t *prim_instance;                  /* [n_prims]: owning instance or -1 */
     int32_t n_kdnodes; const pbrtgpu_kdnode *kdnodes;   /* measured BRDF kd-trees */
+    int32_t n_textures; const pbrtgpu_texture *textures;
+    const float *ewa_lut;         /* [128] MIPMap::weightLut (mipmap.h:185-193) */
+    const float *rgb_basis;       /* [14][n_bands] rgbRefl2Spect{White,Cyan,Magenta,Yellow,Red,
+                                   * Green,Blue}, rgbIllum2Spect{...} (FromRGB, spectrum.cpp:93-178) */
 } pbrtgpu_flat_scene;
 
 /* ---- render description ----------------------------------------------------------- */

@@ -24,7 +24,7 @@ typedef struct pbrthost_overrides {
     int32_t xres, yres;   /* Film "xresolution"/"yresolution" */
     int32_t spp;          /* Sampler "pixelsamples" (rounded up to a power of two) */
     int32_t maxdepth;     /* SurfaceIntegrator "path" "maxdepth" */
-    int32_t bands;        /* nSpectralSamples: 32 (reference build) or 60 */
+    int32_t bands;        /* nSpectralSamples: 32 (reference build), 60 or 30; <= 0: the pack's own, or 32 */
     uint32_t seed;        /* fixed-seed sampler seed; PBRTHOST_KEEP_SEED keeps the pack's (0 for .pbrt) */
 } pbrthost_overrides;
 

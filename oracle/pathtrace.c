@@ -712,13 +712,15 @@ static void isect_fill(const Ctx *c, const Ray *ray, const Hit *h, Isect *is) {
 /* ------------------------------------------------------------------ BSDF */
 enum { BSDF_REFLECTION = 1, BSDF_TRANSMISSION = 2, BSDF_DIFFUSE = 4, BSDF_GLOSSY = 8, BSDF_SPECULAR = 16,
        BSDF_ALL = 31 };
-enum { BX_LAMBERT, BX_OREN, BX_MICRO_BLINN_DIEL, BX_SPEC_REFL_NOOP, BX_FRESNEL_BLEND_ANISO, BX_MEASURED_IRREG };
+enum { BX_LAMBERT, BX_OREN, BX_MICRO_BLINN_DIEL, BX_SPEC_REFL_NOOP, BX_FRESNEL_BLEND_ANISO, BX_MEASURED_IRREG,
+       BX_MICRO_BLINN_COND };
 typedef struct {
     int kind, type;
     const float *R;      /* reflectance spectrum */
     const float *R2;     /* second spectrum (FresnelBlend Rs) */
     float a, b;          /* OrenNayar A,B ; Blinn exponent ; Aniso ex,ey */
     float eta_i, eta_t;  /* FresnelDielectric */
+    const float *eta, *k;   /* FresnelConductor */
     const pbrtgpu_kdnode *kd;   /* IrregIsotropicBRDF: kd-tree nodes */
     int nkd;
 } BxDF;
@@ -726,6 +728,7 @@ typedef struct {
     V nn, ng, sn, tn;
     int n;
     BxDF bx[4];
+    float texbuf[MAXB];   /* a textured reflectance evaluated at this hit */
 } BSDF;
 static inline int matches(const BxDF *b, int flags) { return (b->type & flags) == b->type; }
 static inline V to_local(const BSDF *b, V v) { return v3(vdot(v, b->sn), vdot(v, b->tn), vdot(v, b->nn)); }
@@ -754,6 +757,14 @@ static float fr_dielectric(float cosi, float eta_i, float eta_t) {
     float Rparl = ((et * ci) - (ei * cost)) / ((et * ci) + (ei * cost));
     float Rperp = ((ei * ci) - (et * cost)) / ((ei * ci) + (et * cost));
     return (Rparl * Rparl + Rperp * Rperp) / 2.f;
+}
+/* FrCond (reflection.cpp:62-71) for one band */
+static inline float fr_cond(float cosi, float eta, float k) {
+    float tmp = ((eta * eta + k * k) * cosi) * cosi;
+    float Rparl2 = ((tmp - ((2.f * eta) * cosi)) + 1.f) / ((tmp + ((2.f * eta) * cosi)) + 1.f);
+    float tmp_f = eta * eta + k * k;
+    float Rperp2 = ((tmp_f - ((2.f * eta) * cosi)) + cosi * cosi) / ((tmp_f + ((2.f * eta) * cosi)) + cosi * cosi);
+    return (Rparl2 + Rperp2) / 2.f;
 }
 static inline float blinn_D(float e, V wh) { return (e + 2) * INV_TWOPI_F * POWF(abscos(wh), e); }
 static inline float micro_G(V wo, V wi, V wh) {
@@ -925,6 +936,18 @@ static void bx_f_add(const Ctx *c, const BxDF *b, V wo, V wi, float *out) {
             for (int i = 0; i < nb; ++i) out[i] += (((b->R[i] * D) * G) * F) / den;
             break;
         }
+        case BX_MICRO_BLINN_COND: {   /* Microfacet::f with FresnelConductor (reflection.cpp:62-71, 102-104) */
+            float cosThetaO = abscos(wo), cosThetaI = abscos(wi);
+            if (cosThetaI == 0.f || cosThetaO == 0.f) { for (int i = 0; i < nb; ++i) out[i] += 0.f; break; }
+            V wh = vadd(wi, wo);
+            if (wh.x == 0. && wh.y == 0. && wh.z == 0.) { for (int i = 0; i < nb; ++i) out[i] += 0.f; break; }
+            wh = vnorm(wh);
+            float cosi = fabsf(vdot(wi, wh));
+            float D = blinn_D(b->a, wh), G = micro_G(wo, wi, wh);
+            float den = 4.f * cosThetaI * cosThetaO;
+            for (int i = 0; i < nb; ++i) out[i] += (((1.f * D) * G) * fr_cond(cosi, b->eta[i], b->k[i])) / den;
+            break;
+        }
         case BX_SPEC_REFL_NOOP:
             for (int i = 0; i < nb; ++i) out[i] += 0.f;
             break;
@@ -950,6 +973,7 @@ static void bx_f_add(const Ctx *c, const BxDF *b, V wo, V wi, float *out) {
 static float bx_pdf(const BxDF *b, V wo, V wi) {
     switch (b->kind) {
         case BX_MICRO_BLINN_DIEL:
+        case BX_MICRO_BLINN_COND:
             if (!samehemi(wo, wi)) return 0.f;
             return blinn_pdf(b->a, wo, wi);
         case BX_SPEC_REFL_NOOP: return 0.;
@@ -965,6 +989,7 @@ static void bx_sample_f(const Ctx *c, const BxDF *b, V wo, V *wi, float u1, floa
     for (int i = 0; i < nb; ++i) fout[i] = 0.f;
     switch (b->kind) {
         case BX_MICRO_BLINN_DIEL:
+        case BX_MICRO_BLINN_COND:
             blinn_sample(b->a, wo, wi, u1, u2, pdf);
             if (!samehemi(wo, *wi)) return;
             bx_f_add(c, b, wo, *wi, fout);
@@ -1048,8 +1073,173 @@ static void bsdf_sample_f(const Ctx *c, const BSDF *bs, V woW, V *wiW, float u0,
     }
 }
 
+/* ------------------------------------------------------------------ RGB spectra, textures */
+#ifdef ORACLE_LIBM_FLOAT
+#define LOGF logf
+#else
+static inline float LOGF(float x) { return (float)pbrt_fm_log_any((double)x); }
+#endif
+/* Log2 (pbrt.h:243-246) */
+static inline float log2_(float x) { float invLog2 = 1.f / LOGF(2.f); return LOGF(x) * invLog2; }
+
+/* SampledSpectrum::FromRGB (spectrum.cpp:93-178), basis tables from the flattened scene */
+static void add_scaled(float *r, int nb, float a, const float *B) { for (int i = 0; i < nb; ++i) r[i] += B[i] * a; }
+static void from_rgb(const Ctx *c, const float rgb[3], int illum, float *r) {
+    int nb = c->nb;
+    const float *base = c->s->rgb_basis + (size_t)(illum ? 7 : 0) * nb;
+    const float *W = base, *Cy = base + nb, *Mg = base + 2 * nb, *Ye = base + 3 * nb, *Rd = base + 4 * nb,
+                *Gr = base + 5 * nb, *Bl = base + 6 * nb;
+    for (int i = 0; i < nb; ++i) r[i] = 0.f;
+    if (rgb[0] <= rgb[1] && rgb[0] <= rgb[2]) {
+        add_scaled(r, nb, rgb[0], W);
+        if (rgb[1] <= rgb[2]) { add_scaled(r, nb, rgb[1] - rgb[0], Cy); add_scaled(r, nb, rgb[2] - rgb[1], Bl); }
+        else { add_scaled(r, nb, rgb[2] - rgb[0], Cy); add_scaled(r, nb, rgb[1] - rgb[2], Gr); }
+    } else if (rgb[1] <= rgb[0] && rgb[1] <= rgb[2]) {
+        add_scaled(r, nb, rgb[1], W);
+        if (rgb[0] <= rgb[2]) { add_scaled(r, nb, rgb[0] - rgb[1], Mg); add_scaled(r, nb, rgb[2] - rgb[0], Bl); }
+        else { add_scaled(r, nb, rgb[2] - rgb[1], Mg); add_scaled(r, nb, rgb[0] - rgb[2], Rd); }
+    } else {
+        add_scaled(r, nb, rgb[2], W);
+        if (rgb[0] <= rgb[1]) { add_scaled(r, nb, rgb[0] - rgb[2], Ye); add_scaled(r, nb, rgb[1] - rgb[0], Gr); }
+        else { add_scaled(r, nb, rgb[1] - rgb[2], Ye); add_scaled(r, nb, rgb[0] - rgb[1], Rd); }
+    }
+    float sc = illum ? .86445f : (float).94;
+    for (int i = 0; i < nb; ++i) r[i] = clampf(r[i] * sc, 0.f, INFINITY);
+}
+
+/* One-texel MIPMap (mipmap.h): Texel with the wrap mode (:197-222), triangle (:263-274),
+ * EWA (:278-375) and the width-based Lookup (:232-259); nc = 3 (RGB) or 1 (float) */
+static inline float texel_c(const float *T, int wrap, int s, int t, int k) {
+    if (wrap == PBRTGPU_WRAP_BLACK && (s != 0 || t != 0)) return 0.f;
+    return T[k];
+}
+static void mip_triangle(const float *T, int nc, int wrap, float s, float t, float *out) {
+    s = s * 1.f - 0.5f;
+    t = t * 1.f - 0.5f;
+    int s0 = (int)floorf(s), t0 = (int)floorf(t);
+    float ds = s - s0, dt = t - t0;
+    float w00 = (1.f - ds) * (1.f - dt), w01 = (1.f - ds) * dt, w10 = ds * (1.f - dt), w11 = ds * dt;
+    for (int k = 0; k < nc; ++k)
+        out[k] = ((w00 * texel_c(T, wrap, s0, t0, k) + w01 * texel_c(T, wrap, s0, t0 + 1, k)) +
+                  w10 * texel_c(T, wrap, s0 + 1, t0, k)) + w11 * texel_c(T, wrap, s0 + 1, t0 + 1, k);
+}
+static void mip_ewa0(const Ctx *c, const float *T, int nc, int wrap, float s, float t, float ds0, float dt0, float ds1,
+                     float dt1, float *out) {
+    s = s * 1.f - 0.5f;
+    t = t * 1.f - 0.5f;
+    ds0 *= 1.f; dt0 *= 1.f; ds1 *= 1.f; dt1 *= 1.f;
+    float A = dt0 * dt0 + dt1 * dt1 + 1;
+    float B = -2.f * (ds0 * dt0 + ds1 * dt1);
+    float C = ds0 * ds0 + ds1 * ds1 + 1;
+    float invF = 1.f / (A * C - B * B * 0.25f);
+    A *= invF; B *= invF; C *= invF;
+    float det = -B * B + 4.f * A * C;
+    float invDet = 1.f / det;
+    float uSqrt = sqrtf(det * C), vSqrt = sqrtf(A * det);
+    int s0 = (int)ceilf(s - 2.f * invDet * uSqrt), s1 = (int)floorf(s + 2.f * invDet * uSqrt);
+    int t0 = (int)ceilf(t - 2.f * invDet * vSqrt), t1 = (int)floorf(t + 2.f * invDet * vSqrt);
+    float sum[3] = {0.f, 0.f, 0.f}, sumWts = 0.f;
+    for (int it = t0; it <= t1; ++it) {
+        float tt = it - t;
+        for (int is = s0; is <= s1; ++is) {
+            float ss = is - s;
+            float r2 = A * ss * ss + B * ss * tt + C * tt * tt;
+            if (r2 < 1.) {
+                int li = (int)(r2 * 128);
+                float weight = c->s->ewa_lut[li < 127 ? li : 127];
+                for (int k = 0; k < nc; ++k) sum[k] += texel_c(T, wrap, is, it, k) * weight;
+                sumWts += weight;
+            }
+        }
+    }
+    for (int k = 0; k < nc; ++k) out[k] = sum[k] / sumWts;
+}
+static void mip_lookup(const Ctx *c, const pbrtgpu_texture *tx, int nc, float s, float t, float ds0, float dt0, float ds1,
+                       float dt1, float *out) {
+    const float *T = tx->texel;
+    if (tx->trilinear) {   /* Lookup(s, t, width): level = 0 + Log2(max(width, 1e-8f)) */
+        float width = 2.f * fmaxf_(fmaxf_(fabsf(ds0), fabsf(dt0)), fmaxf_(fabsf(ds1), fabsf(dt1)));
+        float level = 0.f + log2_(fmaxf_(width, 1e-8f));
+        if (level < 0) mip_triangle(T, nc, tx->wrap, s, t, out);
+        else for (int k = 0; k < nc; ++k) out[k] = texel_c(T, tx->wrap, 0, 0, k);
+        return;
+    }
+    if (ds0 * ds0 + dt0 * dt0 < ds1 * ds1 + dt1 * dt1) {
+        float a = ds0; ds0 = ds1; ds1 = a;
+        a = dt0; dt0 = dt1; dt1 = a;
+    }
+    float majorLength = sqrtf(ds0 * ds0 + dt0 * dt0);
+    float minorLength = sqrtf(ds1 * ds1 + dt1 * dt1);
+    if (minorLength * tx->max_aniso < majorLength && minorLength > 0.f) {
+        float scale = majorLength / (minorLength * tx->max_aniso);
+        ds1 *= scale; dt1 *= scale; minorLength *= scale;
+    }
+    if (minorLength == 0.f) { mip_triangle(T, nc, tx->wrap, s, t, out); return; }
+    float lod = fmaxf_(0.f, 1 - 1.f + log2_(minorLength));
+    int ilod = (int)floorf(lod);
+    float d = lod - ilod;
+    float e0[3], e1[3];
+    if (ilod >= 1) for (int k = 0; k < nc; ++k) e0[k] = texel_c(T, tx->wrap, 0, 0, k);
+    else mip_ewa0(c, T, nc, tx->wrap, s, t, ds0, dt0, ds1, dt1, e0);
+    for (int k = 0; k < nc; ++k) e1[k] = texel_c(T, tx->wrap, 0, 0, k);   /* level ilod + 1 >= nLevels */
+    for (int k = 0; k < nc; ++k) out[k] = (1.f - d) * e0[k] + d * e1[k];
+}
+/* texture-space position and screen-space derivatives of the hit (dgs.u, v, dudx, ...) */
+typedef struct { float u, v, dudx, dvdx, dudy, dvdy; } TexPt;
+/* ImageTexture::Evaluate with UVMapping2D::Map (texture.cpp:80-90) */
+static void tex_image(const Ctx *c, const pbrtgpu_texture *tx, int nc, const TexPt *q, float *out) {
+    float s = tx->su * q->u + tx->du, t = tx->sv * q->v + tx->dv;
+    float dsdx = tx->su * q->dudx, dtdx = tx->sv * q->dvdx, dsdy = tx->su * q->dudy, dtdy = tx->sv * q->dvdy;
+    mip_lookup(c, tx, nc, s, t, dsdx, dtdx, dsdy, dtdy, out);
+}
+static float tex_float(const Ctx *c, int id, const TexPt *q) {
+    const pbrtgpu_texture *tx = &c->s->textures[id];
+    switch (tx->type) {
+        case PBRTGPU_TEX_CONST: return tx->value;
+        case PBRTGPU_TEX_IMAGE: { float v; tex_image(c, tx, 1, q, &v); return v; }
+        default: return tex_float(c, tx->tex1, q) * tex_float(c, tx->tex2, q);   /* ScaleTexture */
+    }
+}
+static void tex_spec(const Ctx *c, int id, const TexPt *q, float *out) {
+    const pbrtgpu_texture *tx = &c->s->textures[id];
+    int nb = c->nb;
+    switch (tx->type) {
+        case PBRTGPU_TEX_CONST: memcpy(out, SPEC(c, tx->spec), sizeof(float) * nb); return;
+        case PBRTGPU_TEX_IMAGE: { float rgb[3]; tex_image(c, tx, 3, q, rgb); from_rgb(c, rgb, 0, out); return; }
+        default: {
+            float a[MAXB], b[MAXB];
+            tex_spec(c, tx->tex1, q, a);
+            tex_spec(c, tx->tex2, q, b);
+            for (int i = 0; i < nb; ++i) out[i] = a[i] * b[i];
+        }
+    }
+}
+/* camera ray differentials (perspective.cpp:98-104 + RayDifferential::ScaleDifferentials) */
+typedef struct { V rxo, rxd, ryo, ryd; int has; } RayDiff;
+/* DifferentialGeometry::ComputeDifferentials (diffgeom.cpp:50-105): out = dudx, dvdx, dudy, dvdy */
+static void compute_differentials(const DG *dg, const RayDiff *rd, float out[4]) {
+    out[0] = out[1] = out[2] = out[3] = 0.f;
+    if (!rd || !rd->has) return;
+    float d = -vdot(dg->nn, dg->p);
+    float tx = -(vdot(dg->nn, rd->rxo) + d) / vdot(dg->nn, rd->rxd);
+    if (isnan(tx)) return;
+    V px = vadd(rd->rxo, vmul(rd->rxd, tx));
+    float ty = -(vdot(dg->nn, rd->ryo) + d) / vdot(dg->nn, rd->ryd);
+    if (isnan(ty)) return;
+    V py = vadd(rd->ryo, vmul(rd->ryd, ty));
+    int a0, a1;
+    if (fabsf(dg->nn.x) > fabsf(dg->nn.y) && fabsf(dg->nn.x) > fabsf(dg->nn.z)) { a0 = 1; a1 = 2; }
+    else if (fabsf(dg->nn.y) > fabsf(dg->nn.z)) { a0 = 0; a1 = 2; }
+    else { a0 = 0; a1 = 1; }
+    float A[2][2] = {{vcomp(dg->dpdu, a0), vcomp(dg->dpdv, a0)}, {vcomp(dg->dpdu, a1), vcomp(dg->dpdv, a1)}};
+    float Bx[2] = {vcomp(px, a0) - vcomp(dg->p, a0), vcomp(px, a1) - vcomp(dg->p, a1)};
+    float By[2] = {vcomp(py, a0) - vcomp(dg->p, a0), vcomp(py, a1) - vcomp(dg->p, a1)};
+    if (!solve2x2(A, Bx, &out[0], &out[1])) out[0] = out[1] = 0.f;
+    if (!solve2x2(A, By, &out[2], &out[3])) out[2] = out[3] = 0.f;
+}
+
 /* Intersection::GetBSDF -> GetShadingGeometry -> Material::GetBSDF (with Bump) */
-static void get_bsdf(const Ctx *c, const Isect *is, BSDF *bs, DG *dgsOut) {
+static void get_bsdf(const Ctx *c, const Isect *is, const float diff[4], BSDF *bs, DG *dgsOut) {
     const pbrtgpu_prim *pr = &c->s->prims[is->prim];
     const pbrtgpu_material *mt = &c->s->materials[pr->material];
     DG dgs;
@@ -1063,13 +1253,29 @@ static void get_bsdf(const Ctx *c, const Isect *is, BSDF *bs, DG *dgsOut) {
         const pbrtgpu_quadric *q = &c->s->quadrics[pr->shape_index];
         ro = q->reverse_orientation; swaps = q->swaps_handedness;
     }
-    /* Material::Bump with constant displacement d (material.cpp:39-81); du = dv = .01f
-     * gives the identical result for any positive du because (d - d) == 0 */
-    float d = mt->f[7];
-    float du = .01f, dv = .01f;
+    const TexPt q = {dgs.u, dgs.v, diff[0], diff[1], diff[2], diff[3]};
     DG b = dgs;
-    b.dpdu = vadd(vadd(dgs.dpdu, vmul(dgs.nn, (d - d) / du)), vmul(dgs.dndu, d));
-    b.dpdv = vadd(vadd(dgs.dpdv, vmul(dgs.nn, (d - d) / dv)), vmul(dgs.dndv, d));
+    if (mt->bump_tex < 0) {
+        /* Material::Bump with constant displacement d (material.cpp:39-81); du = dv = .01f
+         * gives the identical result for any positive du because (d - d) == 0 */
+        float d = mt->f[7];
+        float du = .01f, dv = .01f;
+        b.dpdu = vadd(vadd(dgs.dpdu, vmul(dgs.nn, (d - d) / du)), vmul(dgs.dndu, d));
+        b.dpdv = vadd(vadd(dgs.dpdv, vmul(dgs.nn, (d - d) / dv)), vmul(dgs.dndv, d));
+    } else {
+        /* Material::Bump with a displacement texture: u- and v-shifted evaluations */
+        float du = .5f * (fabsf(q.dudx) + fabsf(q.dudy));
+        if (du == 0.f) du = .01f;
+        TexPt qu = q; qu.u = dgs.u + du;
+        float uDisplace = tex_float(c, mt->bump_tex, &qu);
+        float dv = .5f * (fabsf(q.dvdx) + fabsf(q.dvdy));
+        if (dv == 0.f) dv = .01f;
+        TexPt qv = q; qv.v = dgs.v + dv;
+        float vDisplace = tex_float(c, mt->bump_tex, &qv);
+        float displace = tex_float(c, mt->bump_tex, &q);
+        b.dpdu = vadd(vadd(dgs.dpdu, vmul(dgs.nn, (uDisplace - displace) / du)), vmul(dgs.dndu, displace));
+        b.dpdv = vadd(vadd(dgs.dpdv, vmul(dgs.nn, (vDisplace - displace) / dv)), vmul(dgs.dndv, displace));
+    }
     b.nn = vnorm(vcross(b.dpdu, b.dpdv));
     if (ro ^ swaps) b.nn = vmul(b.nn, -1.f);
     b.nn = faceforward(b.nn, is->dg.nn);
@@ -1080,10 +1286,24 @@ static void get_bsdf(const Ctx *c, const Isect *is, BSDF *bs, DG *dgsOut) {
     bs->tn = vcross(bs->nn, bs->sn);
     bs->n = 0;
     *dgsOut = b;
+    /* material spectra: constants, or the one textured slot evaluated here (.Clamp()) */
+    const float *K[4];
+    int black[4];
+    for (int k = 0; k < 4; ++k) {
+        if (mt->tex[k] >= 0) {
+            tex_spec(c, mt->tex[k], &q, bs->texbuf);
+            for (int i = 0; i < c->nb; ++i) bs->texbuf[i] = clampf(bs->texbuf[i], 0.f, INFINITY);
+            K[k] = bs->texbuf;
+            black[k] = spec_black(c, bs->texbuf);
+        } else {
+            K[k] = mt->spec[k] >= 0 ? SPEC(c, mt->spec[k]) : NULL;
+            black[k] = (mt->black_mask >> k) & 1;
+        }
+    }
     switch (mt->type) {
         case PBRTGPU_MAT_MATTE: {
             BxDF *x = &bs->bx[bs->n++];
-            x->R = SPEC(c, mt->spec[0]);
+            x->R = K[0];
             x->type = BSDF_REFLECTION | BSDF_DIFFUSE;
             float sig = mt->f[0];
             if (sig == 0.) x->kind = BX_LAMBERT;
@@ -1096,20 +1316,29 @@ static void get_bsdf(const Ctx *c, const Isect *is, BSDF *bs, DG *dgsOut) {
             }
             break;
         }
-        case PBRTGPU_MAT_PLASTIC: {
+        case PBRTGPU_MAT_PLASTIC: {   /* plastic.cpp:34-61 */
             BxDF *x = &bs->bx[bs->n++];
-            x->kind = BX_LAMBERT; x->type = BSDF_REFLECTION | BSDF_DIFFUSE; x->R = SPEC(c, mt->spec[0]);
+            x->kind = BX_LAMBERT; x->type = BSDF_REFLECTION | BSDF_DIFFUSE; x->R = K[0];
             x = &bs->bx[bs->n++];
-            x->kind = BX_MICRO_BLINN_DIEL; x->type = BSDF_REFLECTION | BSDF_GLOSSY; x->R = SPEC(c, mt->spec[1]);
+            x->kind = BX_MICRO_BLINN_DIEL; x->type = BSDF_REFLECTION | BSDF_GLOSSY; x->R = K[1];
             float e = 1.f / mt->f[0];
             if (e > 10000.f || isnan(e)) e = 10000.f;   /* Blinn ctor */
             x->a = e; x->eta_i = 1.5f; x->eta_t = 1.f;
             break;
         }
+        case PBRTGPU_MAT_METAL: {   /* metal.cpp:44-62: Microfacet(1, FresnelConductor(eta, k), Blinn(1/rough)) */
+            BxDF *x = &bs->bx[bs->n++];
+            x->kind = BX_MICRO_BLINN_COND; x->type = BSDF_REFLECTION | BSDF_GLOSSY;
+            x->eta = K[0]; x->k = K[1];
+            float e = 1.f / mt->f[0];
+            if (e > 10000.f || isnan(e)) e = 10000.f;
+            x->a = e;
+            break;
+        }
         case PBRTGPU_MAT_MIRROR: {
-            if (!spec_black(c, SPEC(c, mt->spec[0]))) {
+            if (!black[0]) {
                 BxDF *x = &bs->bx[bs->n++];
-                x->kind = BX_SPEC_REFL_NOOP; x->type = BSDF_REFLECTION | BSDF_SPECULAR; x->R = SPEC(c, mt->spec[0]);
+                x->kind = BX_SPEC_REFL_NOOP; x->type = BSDF_REFLECTION | BSDF_SPECULAR; x->R = K[0];
             }
             break;
         }
@@ -1119,10 +1348,10 @@ static void get_bsdf(const Ctx *c, const Isect *is, BSDF *bs, DG *dgsOut) {
             x->kd = c->s->kdnodes + mt->aux; x->nkd = mt->aux2;
             break;
         }
-        case PBRTGPU_MAT_SUBSTRATE: {
+        case PBRTGPU_MAT_SUBSTRATE: {   /* substrate.cpp:34-56 */
             BxDF *x = &bs->bx[bs->n++];
             x->kind = BX_FRESNEL_BLEND_ANISO; x->type = BSDF_REFLECTION | BSDF_GLOSSY;
-            x->R = SPEC(c, mt->spec[0]); x->R2 = SPEC(c, mt->spec[1]);
+            x->R = K[0]; x->R2 = K[1];
             float ex = 1.f / mt->f[0], ey = 1.f / mt->f[1];
             if (ex > 10000.f || isnan(ex)) ex = 10000.f;
             if (ey > 10000.f || isnan(ey)) ey = 10000.f;
@@ -1221,12 +1450,47 @@ static int sample_discrete(const pbrtgpu_light_shape *ls, int n, float u) {
     return off < 0 ? 0 : off;
 }
 typedef struct { V o, d; float mint, maxt; } Seg;
-/* Light::Sample_L (diffuse.cpp:61-74, point.cpp:42-49); returns Li into Li[] */
+/* InfiniteAreaLight (lights/infinite.cpp) with its one-texel radiance map */
+static inline float spherical_theta(V v) { return ACOSF(clampf(v.z, -1.f, 1.f)); }   /* geometry.h:642-650 */
+static inline float spherical_phi(V v) { float p = ATAN2F(v.y, v.x); return (p < 0.f) ? p + 2.f * PI_F : p; }
+static void inf_radiance(const Ctx *c, const pbrtgpu_light *L, float s, float t, float *out) {
+    float rgb[3];
+    mip_triangle(L->texel, 3, L->wrap, s, t, rgb);   /* MIPMap::Lookup(s, t), width 0 */
+    from_rgb(c, rgb, 1, out);                          /* Spectrum(rgb, SPECTRUM_ILLUMINANT) */
+}
+/* InfiniteAreaLight::Le (infinite.cpp:84-89) */
+static void inf_Le(const Ctx *c, const pbrtgpu_light *L, V d, float *out) {
+    V wh = vnorm(xvec(L->l2w_minv, d));
+    inf_radiance(c, L, spherical_phi(wh) * INV_TWOPI_F, spherical_theta(wh) * INV_PI_F, out);
+}
+/* InfiniteAreaLight::Pdf (infinite.cpp:188-197); Distribution2D::Pdf of one texel is dist_pdf */
+static float inf_pdf(const pbrtgpu_light *L, V w) {
+    V wi = xvec(L->l2w_minv, w);
+    float theta = spherical_theta(wi);
+    float sintheta = SINF(theta);
+    if (sintheta == 0.f) return 0.f;
+    return L->dist_pdf / (2.f * PI_F * PI_F * sintheta);
+}
+/* Light::Sample_L (diffuse.cpp:61-74, point.cpp:42-49, infinite.cpp:155-185); returns Li into Li[] */
 static void light_sample_L(const Ctx *c, const pbrtgpu_light *L, V p, float pEps, const float u[3], float time,
                            V *wi, float *pdf, Seg *vis, float *Li) {
     int nb = c->nb;
     const float *Ls = SPEC(c, L->spec);
     (void)time;
+    if (L->type == PBRTGPU_LIGHT_INFINITE) {
+        /* Distribution2D::SampleContinuous of one texel returns (u0, u1) with pdf map_pdf */
+        float uv0 = u[0], uv1 = u[1], mapPdf = L->map_pdf;
+        if (mapPdf == 0.f) { *pdf = 0.f; for (int i = 0; i < nb; ++i) Li[i] = 0.f; return; }
+        float theta = uv1 * PI_F, phi = uv0 * 2.f * PI_F;
+        float costheta = COSF(theta), sintheta = SINF(theta);
+        float sinphi = SINF(phi), cosphi = COSF(phi);
+        *wi = xvec(L->l2w_m, v3(sintheta * cosphi, sintheta * sinphi, costheta));
+        *pdf = mapPdf / (2.f * PI_F * PI_F * sintheta);
+        if (sintheta == 0.f) *pdf = 0.f;
+        vis->o = p; vis->d = *wi; vis->mint = pEps; vis->maxt = INFINITY;   /* VisibilityTester::SetRay */
+        inf_radiance(c, L, uv0, uv1, Li);
+        return;
+    }
     if (L->type == PBRTGPU_LIGHT_POINT) {
         V lp = v3(L->pos[0], L->pos[1], L->pos[2]);
         *wi = vnorm(vsub(lp, p));
@@ -1268,6 +1532,7 @@ static void light_sample_L(const Ctx *c, const pbrtgpu_light *L, V p, float pEps
 }
 static float light_pdf(const Ctx *c, const pbrtgpu_light *L, V p, V wi) {
     if (L->type == PBRTGPU_LIGHT_POINT) return 0.;
+    if (L->type == PBRTGPU_LIGHT_INFINITE) return inf_pdf(L, wi);
     const pbrtgpu_light_shape *shs = c->s->light_shapes + L->shape_offset;
     float pp = 0.f;
     for (int i = 0; i < L->n_shapes; ++i) pp += shs[i].area * shape_pdf(c, shs[i].shape_type, shs[i].shape_index, p, wi);
@@ -1330,12 +1595,13 @@ static void estimate_direct(const Ctx *c, int lightNum, V p, V n, V wo, float ra
             Hit h;
             for (int i = 0; i < nb; ++i) Li[i] = 0.f;
             if (bvh_intersect(c, &ray, &h)) {
-                if (c->s->prims[h.prim].area_light == lightNum) {
+                if (L->type == PBRTGPU_LIGHT_AREA && c->s->prims[h.prim].area_light == lightNum) {
                     Isect is;
                     isect_fill(c, &ray, &h, &is);
                     isect_Le(c, &is, vneg(wi), Li);
                 }
-            }   /* else Li = light->Le(ray) == 0 for area lights */
+            } else if (L->type == PBRTGPU_LIGHT_INFINITE)
+                inf_Le(c, L, ray.d, Li);   /* Li = light->Le(ray) (0 for area lights) */
             if (!spec_black(c, Li)) {
                 float ad = fabsf(vdot(wi, n));
                 for (int i = 0; i < nb; ++i) Ld[i] += (((f[i] * Li[i]) * ad) * weight) / bsdfPdf;
@@ -1344,15 +1610,20 @@ static void estimate_direct(const Ctx *c, int lightNum, V p, V n, V wo, float ra
     }
 }
 /* PathIntegrator::Li (path.cpp:44-115) + SamplerRenderer::Li (samplerrenderer.cpp:225-247) */
-static void radiance(const Ctx *c, Ray ray, PathSampler *ps, float *Lout) {
+static void radiance(const Ctx *c, Ray ray, const RayDiff *rd, PathSampler *ps, float *Lout) {
     int nb = c->nb;
     float L[MAXB], beta[MAXB], tmp[MAXB], Ld[MAXB], f[MAXB];
     for (int i = 0; i < nb; ++i) { L[i] = 0.f; beta[i] = 1.f; }
     Hit h;
     Isect is;
     if (!bvh_intersect(c, &ray, &h)) {
-        /* miss: sum of lights' Le (area/point: 0) */
-        for (int i = 0; i < nb; ++i) Lout[i] = (1.f * 0.f) + 0.f;
+        /* miss: Li = sum of the lights' Le (area/point: 0) */
+        for (int k = 0; k < c->s->n_lights; ++k)
+            if (c->s->lights[k].type == PBRTGPU_LIGHT_INFINITE) {
+                inf_Le(c, &c->s->lights[k], ray.d, tmp);
+                for (int i = 0; i < nb; ++i) L[i] += tmp[i];
+            }
+        for (int i = 0; i < nb; ++i) Lout[i] = (1.f * L[i]) + 0.f;
         return;
     }
     isect_fill(c, &ray, &h, &is);
@@ -1365,7 +1636,9 @@ static void radiance(const Ctx *c, Ray ray, PathSampler *ps, float *Lout) {
         }
         BSDF bs;
         DG dgs;
-        get_bsdf(c, &is, &bs, &dgs);
+        float diff[4];   /* only the camera ray carries differentials (path.cpp:107) */
+        compute_differentials(&is.dg, bounces == 0 ? rd : NULL, diff);
+        get_bsdf(c, &is, diff, &bs, &dgs);
         V p = dgs.p, n = dgs.nn;
         V wo = vneg(ray.d);
         /* UniformSampleOneLight (integrator.cpp:74-106) */
@@ -1416,7 +1689,12 @@ static void radiance(const Ctx *c, Ray ray, PathSampler *ps, float *Lout) {
         }
         if (bounces == c->s->max_depth) break;
         if (!bvh_intersect(c, &ray, &h)) {
-            if (specularBounce) for (int i = 0; i < nb; ++i) L[i] += beta[i] * 0.f;   /* area/point Le == 0 */
+            if (specularBounce)
+                for (int k = 0; k < nLights; ++k) {
+                    if (c->s->lights[k].type == PBRTGPU_LIGHT_INFINITE) inf_Le(c, &c->s->lights[k], ray.d, tmp);
+                    else for (int i = 0; i < nb; ++i) tmp[i] = 0.f;   /* area/point Le == 0 */
+                    for (int i = 0; i < nb; ++i) L[i] += beta[i] * tmp[i];
+                }
             break;
         }
         isect_fill(c, &ray, &h, &is);
@@ -1427,7 +1705,7 @@ static void radiance(const Ctx *c, Ray ray, PathSampler *ps, float *Lout) {
 }
 
 /* camera sample -> world ray (perspective.cpp:73-106, transform.h:253-262) */
-static Ray camera_ray(const Ctx *c, float imageX, float imageY, float lensU, float lensV, float timeU) {
+static Ray camera_ray(const Ctx *c, float imageX, float imageY, float lensU, float lensV, float timeU, RayDiff *rd) {
     const pbrtgpu_camera *cam = &c->s->camera;
     const float *m = cam->raster_to_camera;
     float x = imageX, y = imageY, z = 0;
@@ -1463,6 +1741,18 @@ static Ray camera_ray(const Ctx *c, float imageX, float imageY, float lensU, flo
         if (wp != 1.) o.o = vdiv(o.o, wp);
     }
     o.d = xvec(cw, r.d);
+    if (rd) {   /* rx/ry rays in camera space, CameraToWorld, ScaleDifferentials(1/sqrt(spp)) */
+        const float *dx = cam->dx_camera, *dy = cam->dy_camera;
+        V rxd = vnorm(vadd(Pc, v3(dx[0], dx[1], dx[2]))), ryd = vnorm(vadd(Pc, v3(dy[0], dy[1], dy[2])));
+        V ow = o.o;   /* rxOrigin = ryOrigin = ray->o, transformed like o */
+        rxd = xvec(cw, rxd); ryd = xvec(cw, ryd);
+        float sc = 1.f / sqrtf((float)c->s->spp);
+        rd->rxo = vadd(o.o, vmul(vsub(ow, o.o), sc));
+        rd->ryo = vadd(o.o, vmul(vsub(ow, o.o), sc));
+        rd->rxd = vadd(o.d, vmul(vsub(rxd, o.d), sc));
+        rd->ryd = vadd(o.d, vmul(vsub(ryd, o.d), sc));
+        rd->has = 1;
+    }
     return o;
 }
 
@@ -1480,9 +1770,10 @@ static int trace_path(const Ctx *c, int px, int py, uint32_t s, float *L, float 
     float timeU = s1d(ps.hp, 2, s, spp);
     rng_seed(&ps.rng, path_seed(ps.hp, s));
     ps.rng.mti = 624;   /* RNG ctor: Seed() leaves mti == N, first draw regenerates */
-    Ray r = camera_ray(c, imageX, imageY, lens[0], lens[1], timeU);
+    RayDiff rd;
+    Ray r = camera_ray(c, imageX, imageY, lens[0], lens[1], timeU, &rd);
     float Lr[MAXB];
-    radiance(c, r, &ps, Lr);
+    radiance(c, r, &rd, &ps, Lr);
     int nb = c->nb, bad = 0;
     for (int i = 0; i < nb; ++i) L[i] = 1.f * Lr[i];   /* rayWeight * Li */
     int nan = 0;

@@ -43,7 +43,9 @@ PGD_INLINE float ACOSF(float x) { return (float)pbrt_fm_acos((double)x); }
 PGD_INLINE float ATAN2F(float y, float x) { return (float)pbrt_fm_atan2((double)y, (double)x); }
 PGD_INLINE float TANF(float x) { return (float)pbrt_fm_tan((double)x); }
 PGD_INLINE float ATANF(float x) { return (float)pbrt_fm_atan((double)x); }
-#else   // timing experiment only (not the parity definition): float library functions
+PGD_INLINE float LOGF(float x) { return (float)pbrt_fm_log_any((double)x); }
+#else
+PGD_INLINE float LOGF(float x) { return __logf(x); }   // timing experiment only (not the parity definition): float library functions
 PGD_INLINE float SINF(float x) { return __sinf(x); }
 PGD_INLINE float COSF(float x) { return __cosf(x); }
 PGD_INLINE float POWF(float x, float y) { return __powf(x, y); }
@@ -235,6 +237,11 @@ struct DevScene {
     const int *primInst;              // per prim: owning instance or -1
     int nInsts;
     const pbrtgpu_kdnode *kd;         // measured BRDF kd-trees
+    const pbrtgpu_texture *tex;       // texture nodes (one-texel image maps, scale, constants)
+    const float *ewa;                 // [128] MIPMap::weightLut
+    const float *basis;               // [14][nbp] FromRGB basis spectra, band-quad padded
+    int nbp;                          // padded band count (multiple of 4)
+    int nInf;                         // infinite lights among lights[]
 };
 
 struct DG { V p, nn, dpdu, dpdv, dndu, dndv; float u, v; };
@@ -762,8 +769,10 @@ PGD_HEAVY void isect_fill(const DevScene &S, const Ray &ray, int prim, float t, 
 
 // ------------------------------------------------------------------ BSDF
 enum { BSDF_REFLECTION = 1, BSDF_TRANSMISSION = 2, BSDF_DIFFUSE = 4, BSDF_GLOSSY = 8, BSDF_SPECULAR = 16, BSDF_ALL = 31 };
-enum { BX_LAMBERT, BX_OREN, BX_MICRO_BLINN_DIEL, BX_SPEC_REFL_NOOP, BX_FRESNEL_BLEND_ANISO, BX_MEASURED_IRREG };
-struct BxDF { int kind, type; int R, R2; float a, b; };   // R, R2: offsets into DevScene::spectra
+enum { BX_LAMBERT, BX_OREN, BX_MICRO_BLINN_DIEL, BX_SPEC_REFL_NOOP, BX_FRESNEL_BLEND_ANISO, BX_MEASURED_IRREG,
+       BX_MICRO_BLINN_COND };
+// R, R2: offsets into DevScene::spectra, or -1 for the per-slot textured spectrum (K bands)
+struct BxDF { int kind, type; int R, R2; float a, b; };
 struct BSDF { V nn, ng, sn, tn; int n; BxDF bx[2]; };
 PGD_INLINE bool matches(const BxDF &b, int flags) { return (b.type & flags) == b.type; }
 PGD_INLINE V to_local(const BSDF &b, V v) { return v3(vdot(v, b.sn), vdot(v, b.tn), vdot(v, b.nn)); }
@@ -867,40 +876,12 @@ PGD_INLINE void aniso_sample(float ex, float ey, V wo, V *wi, float u1, float u2
 // 478-512), with every term's operand order as in BxDF::f (reflection.cpp, microfacet.h).
 // T_MEAS: IrregIsotropicBRDF at BRDFRemap point (s0, s1, s2), kd-tree nodes [R, R + R2);
 // once looked up (measured_prepare) it becomes T_BUF: the spectrum in the slot's scratch bands
-enum { T_ZERO = 0, T_LAMB, T_OREN, T_BLINN, T_FB, T_MEAS, T_BUF };
+// T_BLINNC: Microfacet with FresnelConductor, eta = R, k = R2, s2 = |cos theta_h|
+enum { T_ZERO = 0, T_LAMB, T_OREN, T_BLINN, T_FB, T_MEAS, T_BUF, T_BLINNC };
 struct FTerm { int kind; int R, R2; float s0, s1, s2, s3; };
 enum { FV_SUM = 0, FV_SPEC = 1 };
 struct FVal { int mode, n; FTerm t[2]; float d; int R; };   // FV_SUM with n == 0: zero spectrum
 
-PGD_INLINE float term_eval(const float *sp, const FTerm &t, int i) {
-    switch (t.kind) {
-        case T_LAMB: return sp[t.R + i] * kInvPi;                                    // Lambertian::f
-        case T_OREN: return (sp[t.R + i] * kInvPi) * t.s0;                           // OrenNayar::f
-        case T_BLINN: return (((sp[t.R + i] * t.s0) * t.s1) * t.s2) / t.s3;          // Microfacet::f (D, G, F, den)
-        case T_FB: {                                                                 // FresnelBlend::f
-            const float cd = (28.f / (23.f * kPi));
-            float r = sp[t.R + i], r2 = sp[t.R2 + i];
-            float diffuse = ((((cd * r) * (1.f - r2)) * t.s0) * t.s1);
-            float schlick = r2 + t.s2 * (1.f - r2);
-            return diffuse + t.s3 * schlick;
-        }
-        default: return 0.f;
-    }
-}
-PGD_INLINE float fval(const float *sp, const FVal &F, int i) {
-    if (F.mode == FV_SPEC) return (1.f * sp[F.R + i]) / F.d;                          // SpecularReflection
-    float v = 0.f;
-#pragma unroll
-    for (int k = 0; k < 2; ++k)
-        if (k < F.n) v += term_eval(sp, F.t[k], i);
-    return v;
-}
-PGD_INLINE bool fval_black(const float *sp, const FVal &F, int nb) {
-    if (F.mode == FV_SUM && F.n == 0) return true;
-    bool black = true;
-    for (int i = 0; i < nb; ++i) black = black && (fval(sp, F, i) == 0.);
-    return black;
-}
 PGD_INLINE void fval_zero(FVal &F) { F.mode = FV_SUM; F.n = 0; }
 PGD_INLINE void fval_push(FVal &F, const FTerm &t) {   // static indices only (no scratch)
     if (F.n == 0) F.t[0] = t; else F.t[1] = t;
@@ -941,15 +922,16 @@ PGD_INLINE FTerm bx_term(const BxDF &b, V wo, V wi) {
             t.s0 = (b.a + b.b * maxcos * sinalpha * tanbeta);
             break;
         }
-        case BX_MICRO_BLINN_DIEL: {
+        case BX_MICRO_BLINN_DIEL:
+        case BX_MICRO_BLINN_COND: {
             float cosThetaO = abscos(wo), cosThetaI = abscos(wi);
             if (cosThetaI == 0.f || cosThetaO == 0.f) break;
             V wh = vadd(wi, wo);
             if (wh.x == 0. && wh.y == 0. && wh.z == 0.) break;
             wh = vnorm(wh);
             float cosThetaH = vdot(wi, wh);
-            t.kind = T_BLINN;
-            t.s2 = fr_dielectric(cosThetaH, 1.5f, 1.f);
+            if (b.kind == BX_MICRO_BLINN_DIEL) { t.kind = T_BLINN; t.s2 = fr_dielectric(cosThetaH, 1.5f, 1.f); }
+            else { t.kind = T_BLINNC; t.s2 = fabsf(cosThetaH); }   // FresnelConductor::Evaluate
             t.s0 = blinn_D(b.a, wh);
             t.s1 = micro_G(wo, wi, wh);
             t.s3 = 4.f * cosThetaI * cosThetaO;
@@ -980,7 +962,8 @@ PGD_INLINE FTerm bx_term(const BxDF &b, V wo, V wi) {
 }
 PGD_INLINE float bx_pdf(const BxDF &b, V wo, V wi) {
     switch (b.kind) {
-        case BX_MICRO_BLINN_DIEL: if (!samehemi(wo, wi)) return 0.f; return blinn_pdf(b.a, wo, wi);
+        case BX_MICRO_BLINN_DIEL:
+        case BX_MICRO_BLINN_COND: if (!samehemi(wo, wi)) return 0.f; return blinn_pdf(b.a, wo, wi);
         case BX_SPEC_REFL_NOOP: return 0.;
         case BX_FRESNEL_BLEND_ANISO:
             if (!samehemi(wo, wi)) return 0.f;
@@ -993,6 +976,7 @@ PGD_INLINE void bx_sample_f(const BxDF &b, V wo, V *wi, float u1, float u2, floa
     fval_zero(F);
     switch (b.kind) {
         case BX_MICRO_BLINN_DIEL:
+        case BX_MICRO_BLINN_COND:
             blinn_sample(b.a, wo, wi, u1, u2, pdf);
             if (!samehemi(wo, *wi)) return;
             F.n = 1; F.t[0] = bx_term(b, wo, *wi);
@@ -1086,8 +1070,213 @@ PGD_HEAVY void bsdf_sample_f(const BSDF &bs, V woW, V *wiW, float u0, float u1, 
     }
 }
 
+
+// ------------------------------------------------------------------ RGB spectra and textures
+// SampledSpectrum::FromRGB (spectrum.cpp:93-178) for band quad q: the branch picks three basis
+// spectra and weights; every band is r = ((0 + B0*a0) + B1*a1) + B2*a2, then *0.94 / *0.86445
+// and Clamp(0, inf), exactly the reference's per-band operation sequence
+struct RGBPick { int k0, k1, k2; float a0, a1, a2; };
+PGD_INLINE RGBPick rgb_pick(const float rgb[3]) {
+    enum { W = 0, Cy, Mg, Ye, Rd, Gr, Bl };
+    RGBPick p;
+    if (rgb[0] <= rgb[1] && rgb[0] <= rgb[2]) {
+        p.k0 = W; p.a0 = rgb[0];
+        if (rgb[1] <= rgb[2]) { p.k1 = Cy; p.a1 = rgb[1] - rgb[0]; p.k2 = Bl; p.a2 = rgb[2] - rgb[1]; }
+        else { p.k1 = Cy; p.a1 = rgb[2] - rgb[0]; p.k2 = Gr; p.a2 = rgb[1] - rgb[2]; }
+    } else if (rgb[1] <= rgb[0] && rgb[1] <= rgb[2]) {
+        p.k0 = W; p.a0 = rgb[1];
+        if (rgb[0] <= rgb[2]) { p.k1 = Mg; p.a1 = rgb[0] - rgb[1]; p.k2 = Bl; p.a2 = rgb[2] - rgb[0]; }
+        else { p.k1 = Mg; p.a1 = rgb[2] - rgb[1]; p.k2 = Rd; p.a2 = rgb[0] - rgb[2]; }
+    } else {
+        p.k0 = W; p.a0 = rgb[2];
+        if (rgb[0] <= rgb[1]) { p.k1 = Ye; p.a1 = rgb[0] - rgb[2]; p.k2 = Gr; p.a2 = rgb[1] - rgb[0]; }
+        else { p.k1 = Ye; p.a1 = rgb[1] - rgb[2]; p.k2 = Rd; p.a2 = rgb[0] - rgb[1]; }
+    }
+    return p;
+}
+PGD_INLINE float4 from_rgb4(const DevScene &S, const RGBPick &p, bool illum, int q) {
+    const float *b = S.basis + (illum ? 7 : 0) * S.nbp + 4 * q;
+    const float4 x = *reinterpret_cast<const float4 *>(b + p.k0 * S.nbp);
+    const float4 y = *reinterpret_cast<const float4 *>(b + p.k1 * S.nbp);
+    const float4 z = *reinterpret_cast<const float4 *>(b + p.k2 * S.nbp);
+    const float sc = illum ? .86445f : (float).94;
+    float4 r;
+    r.x = clampf((((0.f + x.x * p.a0) + y.x * p.a1) + z.x * p.a2) * sc, 0.f, INFINITY);
+    r.y = clampf((((0.f + x.y * p.a0) + y.y * p.a1) + z.y * p.a2) * sc, 0.f, INFINITY);
+    r.z = clampf((((0.f + x.z * p.a0) + y.z * p.a1) + z.z * p.a2) * sc, 0.f, INFINITY);
+    r.w = clampf((((0.f + x.w * p.a0) + y.w * p.a1) + z.w * p.a2) * sc, 0.f, INFINITY);
+    return r;
+}
+
+// One-texel MIPMap (mipmap.h): Texel with wrap (:197-222), triangle (:263-274), EWA
+// (:278-375), width-based Lookup (:232-259).  NC = 3 (RGB) or 1 (float).
+PGD_INLINE float log2_(float x) { float invLog2 = 1.f / LOGF(2.f); return LOGF(x) * invLog2; }   // pbrt.h:243-246
+PGD_INLINE float texel_c(const float *T, int wrap, int s, int t, int k) {
+    if (wrap == PBRTGPU_WRAP_BLACK && (s != 0 || t != 0)) return 0.f;
+    return T[k];
+}
+template <int NC>
+PGD_INLINE void mip_triangle(const float *T, int wrap, float s, float t, float *out) {
+    s = s * 1.f - 0.5f;
+    t = t * 1.f - 0.5f;
+    int s0 = (int)floorf(s), t0 = (int)floorf(t);
+    float ds = s - s0, dt = t - t0;
+    float w00 = (1.f - ds) * (1.f - dt), w01 = (1.f - ds) * dt, w10 = ds * (1.f - dt), w11 = ds * dt;
+#pragma unroll
+    for (int k = 0; k < NC; ++k)
+        out[k] = ((w00 * texel_c(T, wrap, s0, t0, k) + w01 * texel_c(T, wrap, s0, t0 + 1, k)) +
+                  w10 * texel_c(T, wrap, s0 + 1, t0, k)) + w11 * texel_c(T, wrap, s0 + 1, t0 + 1, k);
+}
+template <int NC>
+PGD_INLINE void mip_ewa0(const DevScene &S, const float *T, int wrap, float s, float t, float ds0, float dt0, float ds1,
+                         float dt1, float *out) {
+    s = s * 1.f - 0.5f;
+    t = t * 1.f - 0.5f;
+    ds0 *= 1.f; dt0 *= 1.f; ds1 *= 1.f; dt1 *= 1.f;
+    float A = dt0 * dt0 + dt1 * dt1 + 1;
+    float B = -2.f * (ds0 * dt0 + ds1 * dt1);
+    float C = ds0 * ds0 + ds1 * ds1 + 1;
+    float invF = 1.f / (A * C - B * B * 0.25f);
+    A *= invF; B *= invF; C *= invF;
+    float det = -B * B + 4.f * A * C;
+    float invDet = 1.f / det;
+    float uSqrt = sqrtf(det * C), vSqrt = sqrtf(A * det);
+    int s0 = (int)ceilf(s - 2.f * invDet * uSqrt), s1 = (int)floorf(s + 2.f * invDet * uSqrt);
+    int t0 = (int)ceilf(t - 2.f * invDet * vSqrt), t1 = (int)floorf(t + 2.f * invDet * vSqrt);
+    float sum[NC], sumWts = 0.f;
+#pragma unroll
+    for (int k = 0; k < NC; ++k) sum[k] = 0.f;
+    for (int it = t0; it <= t1; ++it) {
+        float tt = it - t;
+        for (int is = s0; is <= s1; ++is) {
+            float ss = is - s;
+            float r2 = A * ss * ss + B * ss * tt + C * tt * tt;
+            if (r2 < 1.) {
+                int li = (int)(r2 * 128);
+                float weight = S.ewa[li < 127 ? li : 127];
+#pragma unroll
+                for (int k = 0; k < NC; ++k) sum[k] += texel_c(T, wrap, is, it, k) * weight;
+                sumWts += weight;
+            }
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < NC; ++k) out[k] = sum[k] / sumWts;
+}
+template <int NC>
+PGD_INLINE void mip_lookup(const DevScene &S, const pbrtgpu_texture &tx, float s, float t, float ds0, float dt0,
+                           float ds1, float dt1, float *out) {
+    const float *T = tx.texel;
+    if (tx.trilinear) {
+        float width = 2.f * pmax(pmax(fabsf(ds0), fabsf(dt0)), pmax(fabsf(ds1), fabsf(dt1)));
+        float level = 0.f + log2_(pmax(width, 1e-8f));
+        if (level < 0) mip_triangle<NC>(T, tx.wrap, s, t, out);
+        else {
+#pragma unroll
+            for (int k = 0; k < NC; ++k) out[k] = texel_c(T, tx.wrap, 0, 0, k);
+        }
+        return;
+    }
+    if (ds0 * ds0 + dt0 * dt0 < ds1 * ds1 + dt1 * dt1) {
+        float a = ds0; ds0 = ds1; ds1 = a;
+        a = dt0; dt0 = dt1; dt1 = a;
+    }
+    float majorLength = sqrtf(ds0 * ds0 + dt0 * dt0);
+    float minorLength = sqrtf(ds1 * ds1 + dt1 * dt1);
+    if (minorLength * tx.max_aniso < majorLength && minorLength > 0.f) {
+        float scale = majorLength / (minorLength * tx.max_aniso);
+        ds1 *= scale; dt1 *= scale; minorLength *= scale;
+    }
+    if (minorLength == 0.f) { mip_triangle<NC>(T, tx.wrap, s, t, out); return; }
+    float lod = pmax(0.f, 1 - 1.f + log2_(minorLength));
+    int ilod = (int)floorf(lod);
+    float d = lod - ilod;
+    float e0[NC];
+    if (ilod >= 1) {
+#pragma unroll
+        for (int k = 0; k < NC; ++k) e0[k] = texel_c(T, tx.wrap, 0, 0, k);
+    } else mip_ewa0<NC>(S, T, tx.wrap, s, t, ds0, dt0, ds1, dt1, e0);
+#pragma unroll
+    for (int k = 0; k < NC; ++k) out[k] = (1.f - d) * e0[k] + d * texel_c(T, tx.wrap, 0, 0, k);
+}
+// hit position in texture space with its screen-space derivatives
+struct TexPt { float u, v, dudx, dvdx, dudy, dvdy; };
+// ImageTexture::Evaluate + UVMapping2D::Map (texture.cpp:80-90)
+template <int NC>
+PGD_INLINE void tex_image(const DevScene &S, const pbrtgpu_texture &tx, const TexPt &q, float *out) {
+    float s = tx.su * q.u + tx.du, t = tx.sv * q.v + tx.dv;
+    float dsdx = tx.su * q.dudx, dtdx = tx.sv * q.dvdx, dsdy = tx.su * q.dudy, dtdy = tx.sv * q.dvdy;
+    mip_lookup<NC>(S, tx, s, t, dsdx, dtdx, dsdy, dtdy, out);
+}
+PGD_INLINE float tex_leaf_float(const DevScene &S, int id, const TexPt &q) {
+    const pbrtgpu_texture &tx = S.tex[id];
+    if (tx.type == PBRTGPU_TEX_CONST) return tx.value;
+    float v;
+    tex_image<1>(S, tx, q, &v);
+    return v;
+}
+// Texture<float>: CONST, IMAGE, or ScaleTexture of two leaves (front end guarantees the depth)
+PGD_HEAVY float tex_float(const DevScene &S, int id, const TexPt &q) {
+    const pbrtgpu_texture &tx = S.tex[id];
+    if (tx.type != PBRTGPU_TEX_SCALE) return tex_leaf_float(S, id, q);
+    return tex_leaf_float(S, tx.tex1, q) * tex_leaf_float(S, tx.tex2, q);
+}
+// Texture<Spectrum> in device form: FromRGB(image lookup) [times a constant spectrum, in the
+// ScaleTexture operand order]; SpecTex carries the per-hit part, spec4 evaluates a band quad
+struct SpecTex { RGBPick pick; int constOff; bool constFirst; };
+PGD_HEAVY SpecTex tex_spec_prepare(const DevScene &S, int id, const TexPt &q) {
+    SpecTex r;
+    r.constOff = -1; r.constFirst = false;
+    int img = id;
+    const pbrtgpu_texture &tx = S.tex[id];
+    if (tx.type == PBRTGPU_TEX_SCALE) {
+        const bool firstConst = S.tex[tx.tex1].type == PBRTGPU_TEX_CONST;
+        img = firstConst ? tx.tex2 : tx.tex1;
+        r.constOff = S.tex[firstConst ? tx.tex1 : tx.tex2].spec;
+        r.constFirst = firstConst;
+    }
+    float rgb[3];
+    tex_image<3>(S, S.tex[img], q, rgb);
+    r.pick = rgb_pick(rgb);
+    return r;
+}
+PGD_INLINE float4 tex_spec4(const DevScene &S, const SpecTex &t, int q) {
+    float4 a = from_rgb4(S, t.pick, false, q);
+    if (t.constOff < 0) return a;
+    float4 b = *reinterpret_cast<const float4 *>(S.spectra + t.constOff + 4 * q);
+    return t.constFirst ? make_float4(b.x * a.x, b.y * a.y, b.z * a.z, b.w * a.w)
+                        : make_float4(a.x * b.x, a.y * b.y, a.z * b.z, a.w * b.w);
+}
+// DifferentialGeometry::ComputeDifferentials (diffgeom.cpp:50-105) for the camera ray's
+// offset rays; out = dudx, dvdx, dudy, dvdy
+struct RayDiff { V rxo, rxd, ryo, ryd; };
+PGD_INLINE float vcomp(V a, int i) { return i == 0 ? a.x : (i == 1 ? a.y : a.z); }
+PGD_HEAVY void compute_differentials(const DG &dg, const RayDiff &rd, float out[4]) {
+    out[0] = out[1] = out[2] = out[3] = 0.f;
+    float d = -vdot(dg.nn, dg.p);
+    float tx = -(vdot(dg.nn, rd.rxo) + d) / vdot(dg.nn, rd.rxd);
+    if (isnan(tx)) return;
+    V px = vadd(rd.rxo, vmul(rd.rxd, tx));
+    float ty = -(vdot(dg.nn, rd.ryo) + d) / vdot(dg.nn, rd.ryd);
+    if (isnan(ty)) return;
+    V py = vadd(rd.ryo, vmul(rd.ryd, ty));
+    int a0, a1;
+    if (fabsf(dg.nn.x) > fabsf(dg.nn.y) && fabsf(dg.nn.x) > fabsf(dg.nn.z)) { a0 = 1; a1 = 2; }
+    else if (fabsf(dg.nn.y) > fabsf(dg.nn.z)) { a0 = 0; a1 = 2; }
+    else { a0 = 0; a1 = 1; }
+    float A[2][2] = {{vcomp(dg.dpdu, a0), vcomp(dg.dpdv, a0)}, {vcomp(dg.dpdu, a1), vcomp(dg.dpdv, a1)}};
+    float Bx[2] = {vcomp(px, a0) - vcomp(dg.p, a0), vcomp(px, a1) - vcomp(dg.p, a1)};
+    float By[2] = {vcomp(py, a0) - vcomp(dg.p, a0), vcomp(py, a1) - vcomp(dg.p, a1)};
+    if (!solve2x2(A, Bx, &out[0], &out[1])) out[0] = out[1] = 0.f;
+    if (!solve2x2(A, By, &out[2], &out[3])) out[2] = out[3] = 0.f;
+}
+
 // Intersection::GetBSDF -> GetShadingGeometry -> Material::GetBSDF (+ Bump, material.cpp:39-81)
-PGD_HEAVY void get_bsdf(const DevScene &S, const Isect &is, BSDF &bs, V *pOut, V *nOut) {
+// diff: dudx, dvdx, dudy, dvdy of the hit (zero without ray differentials); the material's
+// textured spectrum, if any, is written clamped into the slot's K bands (kb[q * c]) and its
+// BxDF refers to it with offset -1
+PGD_HEAVY void get_bsdf(const DevScene &S, const Isect &is, const float diff[4], float4 *kb, size_t c, BSDF &bs,
+                        V *pOut, V *nOut) {
     const pbrtgpu_prim pr = S.prims[is.prim];
     const pbrtgpu_material &mt = S.mats[pr.material];
     DG dgs;
@@ -1109,10 +1298,27 @@ PGD_HEAVY void get_bsdf(const DevScene &S, const Isect &is, BSDF &bs, V *pOut, V
         const pbrtgpu_quadric &q = S.quads[pr.shape_index];
         ro = q.reverse_orientation; swaps = q.swaps_handedness;
     }
-    float d = mt.f[7];
-    const float du = .01f, dv = .01f;   // (d - d) / du == +0 for every positive du
-    V bdpdu = vadd(vadd(dgs.dpdu, vmul(dgs.nn, (d - d) / du)), vmul(dgs.dndu, d));
-    V bdpdv = vadd(vadd(dgs.dpdv, vmul(dgs.nn, (d - d) / dv)), vmul(dgs.dndv, d));
+    TexPt tq;
+    tq.u = dgs.u; tq.v = dgs.v; tq.dudx = diff[0]; tq.dvdx = diff[1]; tq.dudy = diff[2]; tq.dvdy = diff[3];
+    V bdpdu, bdpdv;
+    if (mt.bump_tex < 0) {
+        float d = mt.f[7];
+        const float du = .01f, dv = .01f;   // (d - d) / du == +0 for every positive du
+        bdpdu = vadd(vadd(dgs.dpdu, vmul(dgs.nn, (d - d) / du)), vmul(dgs.dndu, d));
+        bdpdv = vadd(vadd(dgs.dpdv, vmul(dgs.nn, (d - d) / dv)), vmul(dgs.dndv, d));
+    } else {
+        float du = .5f * (fabsf(tq.dudx) + fabsf(tq.dudy));
+        if (du == 0.f) du = .01f;
+        TexPt qu = tq; qu.u = dgs.u + du;
+        float uDisplace = tex_float(S, mt.bump_tex, qu);
+        float dv = .5f * (fabsf(tq.dvdx) + fabsf(tq.dvdy));
+        if (dv == 0.f) dv = .01f;
+        TexPt qv = tq; qv.v = dgs.v + dv;
+        float vDisplace = tex_float(S, mt.bump_tex, qv);
+        float displace = tex_float(S, mt.bump_tex, tq);
+        bdpdu = vadd(vadd(dgs.dpdu, vmul(dgs.nn, (uDisplace - displace) / du)), vmul(dgs.dndu, displace));
+        bdpdv = vadd(vadd(dgs.dpdv, vmul(dgs.nn, (vDisplace - displace) / dv)), vmul(dgs.dndv, displace));
+    }
     V nn = vnorm(vcross(bdpdu, bdpdv));
     if (ro ^ swaps) nn = vmul(nn, -1.f);
     nn = faceforward(nn, is.dg.nn);
@@ -1123,11 +1329,36 @@ PGD_HEAVY void get_bsdf(const DevScene &S, const Isect &is, BSDF &bs, V *pOut, V
     bs.n = 0;
     *pOut = dgs.p;
     *nOut = nn;
-    const float *sp = S.spectra;
+    // material spectra: constant offsets, or the textured slot materialised in K
+    int off[4];
+    bool black0 = (mt.black_mask & 1) != 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) off[k] = mt.spec[k];
+    int ts = -1;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        if (mt.tex[k] >= 0) ts = k;
+    if (ts >= 0) {
+        SpecTex st = tex_spec_prepare(S, mt.tex[ts], tq);
+        bool black = true;
+        const int nq = S.nbp / 4;
+        for (int q = 0; q < nq; ++q) {
+            float4 v = tex_spec4(S, st, q);   // FromRGB clamps; .Clamp() again is the identity
+            v = make_float4(clampf(v.x, 0.f, INFINITY), clampf(v.y, 0.f, INFINITY), clampf(v.z, 0.f, INFINITY),
+                            clampf(v.w, 0.f, INFINITY));
+            kb[q * c] = v;
+            black = black && v.x == 0.f && (4 * q + 1 >= S.nb || v.y == 0.f) && (4 * q + 2 >= S.nb || v.z == 0.f) &&
+                    (4 * q + 3 >= S.nb || v.w == 0.f);
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (k == ts) off[k] = -1;   // static indices only (no scratch)
+        if (ts == 0) black0 = black;
+    }
     switch (mt.type) {
         case PBRTGPU_MAT_MATTE: {
             BxDF &x = bs.bx[bs.n++];
-            x.R = mt.spec[0]; x.R2 = x.R;
+            x.R = off[0]; x.R2 = x.R;
             x.type = BSDF_REFLECTION | BSDF_DIFFUSE;
             float sig = mt.f[0];
             if (sig == 0.) { x.kind = BX_LAMBERT; x.a = x.b = 0.f; }
@@ -1142,21 +1373,28 @@ PGD_HEAVY void get_bsdf(const DevScene &S, const Isect &is, BSDF &bs, V *pOut, V
         }
         case PBRTGPU_MAT_PLASTIC: {
             BxDF &x0 = bs.bx[bs.n++];
-            x0.kind = BX_LAMBERT; x0.type = BSDF_REFLECTION | BSDF_DIFFUSE; x0.R = mt.spec[0]; x0.R2 = x0.R;
+            x0.kind = BX_LAMBERT; x0.type = BSDF_REFLECTION | BSDF_DIFFUSE; x0.R = off[0]; x0.R2 = x0.R;
             x0.a = x0.b = 0.f;
             BxDF &x1 = bs.bx[bs.n++];
-            x1.kind = BX_MICRO_BLINN_DIEL; x1.type = BSDF_REFLECTION | BSDF_GLOSSY; x1.R = mt.spec[1]; x1.R2 = x1.R;
+            x1.kind = BX_MICRO_BLINN_DIEL; x1.type = BSDF_REFLECTION | BSDF_GLOSSY; x1.R = off[1]; x1.R2 = x1.R;
             float e = 1.f / mt.f[0];
             if (e > 10000.f || isnan(e)) e = 10000.f;
             x1.a = e; x1.b = 0.f;
             break;
         }
+        case PBRTGPU_MAT_METAL: {   // metal.cpp:44-62: Microfacet(1, FresnelConductor(eta, k), Blinn(1/rough))
+            BxDF &x = bs.bx[bs.n++];
+            x.kind = BX_MICRO_BLINN_COND; x.type = BSDF_REFLECTION | BSDF_GLOSSY;
+            x.R = off[0]; x.R2 = off[1];
+            float e = 1.f / mt.f[0];
+            if (e > 10000.f || isnan(e)) e = 10000.f;
+            x.a = e; x.b = 0.f;
+            break;
+        }
         case PBRTGPU_MAT_MIRROR: {
-            bool black = true;
-            for (int i = 0; i < S.nb; ++i) black = black && (sp[mt.spec[0] + i] == 0.);
-            if (!black) {
+            if (!black0) {
                 BxDF &x = bs.bx[bs.n++];
-                x.kind = BX_SPEC_REFL_NOOP; x.type = BSDF_REFLECTION | BSDF_SPECULAR; x.R = mt.spec[0]; x.R2 = x.R;
+                x.kind = BX_SPEC_REFL_NOOP; x.type = BSDF_REFLECTION | BSDF_SPECULAR; x.R = off[0]; x.R2 = x.R;
                 x.a = x.b = 0.f;
             }
             break;
@@ -1171,7 +1409,7 @@ PGD_HEAVY void get_bsdf(const DevScene &S, const Isect &is, BSDF &bs, V *pOut, V
         case PBRTGPU_MAT_SUBSTRATE: {
             BxDF &x = bs.bx[bs.n++];
             x.kind = BX_FRESNEL_BLEND_ANISO; x.type = BSDF_REFLECTION | BSDF_GLOSSY;
-            x.R = mt.spec[0]; x.R2 = mt.spec[1];
+            x.R = off[0]; x.R2 = off[1];
             float ex = 1.f / mt.f[0], ey = 1.f / mt.f[1];
             if (ex > 10000.f || isnan(ex)) ex = 10000.f;
             if (ey > 10000.f || isnan(ey)) ey = 10000.f;
@@ -1262,20 +1500,54 @@ PGD_INLINE int sample_discrete(const pbrtgpu_light_shape *ls, int n, float u) {
     return off < 0 ? 0 : off;
 }
 struct Seg { V o, d; float mint, maxt; };
-// Light::Sample_L; Li = scale * Ls  (scale = 1 area, 1/d^2 point); returns scale, Ls via pointer
-PGD_HEAVY float light_sample_L(const DevScene &S, const pbrtgpu_light &L, V p, float pEps, const float u[3],
-                                V *wi, float *pdf, Seg *vis, bool *litByArea, bool *isPoint) {
+// The radiance a light sample or a missed ray brings: a pool spectrum (divided by `div` for a
+// point light's 1/d^2), FromRGB(illuminant) of an environment-map lookup, or black
+enum { EM_BLACK = 0, EM_POOL = 1, EM_RGB = 2 };
+struct Emit { int mode; int off; float div; bool point; RGBPick pick; };
+// InfiniteAreaLight (lights/infinite.cpp) with its one-texel radiance map
+PGD_INLINE float spherical_theta(V v) { return ACOSF(clampf(v.z, -1.f, 1.f)); }   // geometry.h:642-650
+PGD_INLINE float spherical_phi(V v) { float p = ATAN2F(v.y, v.x); return (p < 0.f) ? p + 2.f * kPi : p; }
+PGD_INLINE Emit inf_radiance(const pbrtgpu_light &L, float s, float t) {
+    float rgb[3];
+    mip_triangle<3>(L.texel, L.wrap, s, t, rgb);   // MIPMap::Lookup(s, t), width 0
+    Emit e;
+    e.mode = EM_RGB; e.off = -1; e.div = 1.f; e.point = false;
+    e.pick = rgb_pick(rgb);
+    return e;
+}
+// InfiniteAreaLight::Le (infinite.cpp:84-89)
+PGD_HEAVY Emit inf_Le(const pbrtgpu_light &L, V d) {
+    V wh = vnorm(xvec(L.l2w_minv, d));
+    return inf_radiance(L, spherical_phi(wh) * kInvTwoPi, spherical_theta(wh) * kInvPi);
+}
+// Light::Sample_L (diffuse.cpp:61-74, point.cpp:42-49, infinite.cpp:155-185)
+PGD_HEAVY void light_sample_L(const DevScene &S, const pbrtgpu_light &L, V p, float pEps, const float u[3], V *wi,
+                              float *pdf, Seg *vis, Emit *em) {
+    em->mode = EM_BLACK; em->off = L.spec; em->div = 1.f; em->point = false;
+    if (L.type == PBRTGPU_LIGHT_INFINITE) {
+        // Distribution2D::SampleContinuous of one texel returns (u0, u1) with pdf map_pdf
+        float uv0 = u[0], uv1 = u[1], mapPdf = L.map_pdf;
+        if (mapPdf == 0.f) { *pdf = 0.f; return; }
+        float theta = uv1 * kPi, phi = uv0 * 2.f * kPi;
+        float costheta = COSF(theta), sintheta = SINF(theta);
+        float sinphi = SINF(phi), cosphi = COSF(phi);
+        *wi = xvec(L.l2w_m, v3(sintheta * cosphi, sintheta * sinphi, costheta));
+        *pdf = mapPdf / (2.f * kPi * kPi * sintheta);
+        if (sintheta == 0.f) *pdf = 0.f;
+        vis->o = p; vis->d = *wi; vis->mint = pEps; vis->maxt = INFINITY;   // VisibilityTester::SetRay
+        *em = inf_radiance(L, uv0, uv1);
+        return;
+    }
     if (L.type == PBRTGPU_LIGHT_POINT) {
         V lp = v3(L.pos[0], L.pos[1], L.pos[2]);
         *wi = vnorm(vsub(lp, p));
         *pdf = 1.f;
         float dist = vlen(vsub(p, lp));
         vis->o = p; vis->d = vdiv(vsub(lp, p), dist); vis->mint = pEps; vis->maxt = dist * (1.f - 0.f);
-        *isPoint = true;
-        *litByArea = false;
-        return vlen2(vsub(lp, p));   // divisor (Intensity / d2)
+        em->mode = EM_POOL; em->point = true;
+        em->div = vlen2(vsub(lp, p));   // Intensity / DistanceSquared
+        return;
     }
-    *isPoint = false;
     const pbrtgpu_light_shape *shs = S.lightShapes + L.shape_offset;
     int sn = sample_discrete(shs, L.n_shapes, u[2]);
     V ns;
@@ -1297,19 +1569,25 @@ PGD_HEAVY float light_sample_L(const DevScene &S, const pbrtgpu_light &L, V p, f
     *pdf = pp / L.sum_area;
     float dist = vlen(vsub(p, ps));
     vis->o = p; vis->d = vdiv(vsub(ps, p), dist); vis->mint = pEps; vis->maxt = dist * (1.f - 1e-3f);
-    *litByArea = vdot(ns, vneg(*wi)) > 0.f;
-    return 1.f;
+    if (vdot(ns, vneg(*wi)) > 0.f && !L.is_black) em->mode = EM_POOL;   // DiffuseAreaLight::L
 }
 PGD_HEAVY float light_pdf(const DevScene &S, const pbrtgpu_light &L, V p, V wi) {
     if (L.type == PBRTGPU_LIGHT_POINT) return 0.;
+    if (L.type == PBRTGPU_LIGHT_INFINITE) {   // infinite.cpp:188-197; Distribution2D::Pdf of one texel
+        V w = xvec(L.l2w_minv, wi);
+        float sintheta = SINF(spherical_theta(w));
+        if (sintheta == 0.f) return 0.f;
+        return L.dist_pdf / (2.f * kPi * kPi * sintheta);
+    }
     const pbrtgpu_light_shape *shs = S.lightShapes + L.shape_offset;
     float pp = 0.f;
     for (int i = 0; i < L.n_shapes; ++i) pp += shs[i].area * shape_pdf(S, shs[i].shape_type, shs[i].shape_index, p, wi);
     return pp / L.sum_area;
 }
 
-// camera sample -> world ray (perspective.cpp:73-106)
-PGD_INLINE Ray camera_ray(const pbrtgpu_camera &cam, float imageX, float imageY, float lensU, float lensV, float timeU) {
+// camera sample -> camera-space ray before CameraToWorld, and Pcamera (perspective.cpp:73-97)
+PGD_INLINE Ray camera_local(const pbrtgpu_camera &cam, float imageX, float imageY, float lensU, float lensV,
+                            float timeU, V *PcOut) {
     const float *m = cam.raster_to_camera;
     float x = imageX, y = imageY, z = 0;
     V Pc;
@@ -1332,15 +1610,43 @@ PGD_INLINE Ray camera_ray(const pbrtgpu_camera &cam, float imageX, float imageY,
         r.d = vnorm(vsub(Pfocus, r.o));
     }
     r.time = lerpf(timeU, cam.shutter_open, cam.shutter_close);
-    const float *cw = cam.cam2world_m;
-    Ray o = r;
-    V p = r.o;
+    *PcOut = Pc;
+    return r;
+}
+PGD_INLINE V cam_point(const float *cw, V p) {   // Transform::operator()(Point), divide if w != 1
     float xp = cw[0] * p.x + cw[1] * p.y + cw[2] * p.z + cw[3];
     float yp = cw[4] * p.x + cw[5] * p.y + cw[6] * p.z + cw[7];
     float zp = cw[8] * p.x + cw[9] * p.y + cw[10] * p.z + cw[11];
     float wp = cw[12] * p.x + cw[13] * p.y + cw[14] * p.z + cw[15];
-    o.o = v3(xp, yp, zp);
-    if (wp != 1.) o.o = vdiv(o.o, wp);
+    V o = v3(xp, yp, zp);
+    if (wp != 1.) o = vdiv(o, wp);
+    return o;
+}
+// the camera ray's offset rays (perspective.cpp:98-104) in world space, after
+// RayDifferential::ScaleDifferentials(1 / sqrtf(spp)) (samplerrenderer.cpp:91)
+PGD_INLINE RayDiff camera_diff(const pbrtgpu_camera &cam, int spp, float imageX, float imageY, float lensU, float lensV,
+                               float timeU) {
+    V Pc;
+    Ray r = camera_local(cam, imageX, imageY, lensU, lensV, timeU, &Pc);
+    const float *cw = cam.cam2world_m;
+    V o = cam_point(cw, r.o), d = xvec(cw, r.d);
+    V rxd = xvec(cw, vnorm(vadd(Pc, v3(cam.dx_camera[0], cam.dx_camera[1], cam.dx_camera[2]))));
+    V ryd = xvec(cw, vnorm(vadd(Pc, v3(cam.dy_camera[0], cam.dy_camera[1], cam.dy_camera[2]))));
+    float sc = 1.f / sqrtf((float)spp);
+    RayDiff rd;
+    rd.rxo = vadd(o, vmul(vsub(o, o), sc));
+    rd.ryo = rd.rxo;
+    rd.rxd = vadd(d, vmul(vsub(rxd, d), sc));
+    rd.ryd = vadd(d, vmul(vsub(ryd, d), sc));
+    return rd;
+}
+// camera sample -> world ray (perspective.cpp:73-106)
+PGD_INLINE Ray camera_ray(const pbrtgpu_camera &cam, float imageX, float imageY, float lensU, float lensV, float timeU) {
+    V Pc;
+    Ray r = camera_local(cam, imageX, imageY, lensU, lensV, timeU, &Pc);
+    const float *cw = cam.cam2world_m;
+    Ray o = r;
+    o.o = cam_point(cw, r.o);
     o.d = xvec(cw, r.d);
     return o;
 }

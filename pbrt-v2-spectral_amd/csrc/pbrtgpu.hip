@@ -294,7 +294,7 @@ static int ensure_slots(pbrtgpu_ctx *c, int cap, int NB) {
     auto take = [&](size_t bytes) { size_t o = off; off += (bytes + 255) & ~(size_t)255; return o; };
     size_t oItem = take(C * 4), oHp = take(C * 4), oSmp = take(C * 4), oBounce = take(C * 4), oFlags = take(C * 4),
            oMt = take(C * 20), oBeta = take(C * 2 * NBP * 4), oL = take(C * NBP * 4), oA = take(C * NBP * 4),
-           oB = take(C * NBP * 4), oM = take(C * NBP * 4), oRay = take(C * 27 * 4), oHitP = take(C * 8), oHitT = take(C * 8), oOcc = take(C * 4),
+           oB = take(C * NBP * 4), oM = take(C * NBP * 4), oK = take(C * NBP * 4), oPix = take(C * 4), oRay = take(C * 27 * 4), oHitP = take(C * 8), oHitT = take(C * 8), oOcc = take(C * 4),
            oQC = take(C * 16), oQS = take(C * 8), oCnt = take(CNT_WORDS * 4);
     HIPCHK(c->slots.ensure(off));
     char *base = (char *)c->slots.p;
@@ -303,7 +303,7 @@ static int ensure_slots(pbrtgpu_ctx *c, int cap, int NB) {
     P.item = (int *)(base + oItem); P.hp = (uint32_t *)(base + oHp); P.smp = (uint32_t *)(base + oSmp);
     P.bounce = (int *)(base + oBounce); P.flags = (uint32_t *)(base + oFlags); P.mt = (uint32_t *)(base + oMt);
     P.beta = (float4 *)(base + oBeta); P.L = (float4 *)(base + oL); P.A = (float4 *)(base + oA); P.B = (float4 *)(base + oB);
-    P.M = (float4 *)(base + oM);
+    P.M = (float4 *)(base + oM); P.K = (float4 *)(base + oK); P.pix = (uint32_t *)(base + oPix);
     P.ray = (float *)(base + oRay); P.hitPrim = (int *)(base + oHitP); P.hitT = (float *)(base + oHitT);
     P.occ = (uint32_t *)(base + oOcc); P.qC = (uint32_t *)(base + oQC); P.qS = (uint32_t *)(base + oQS);
     P.cnt = (uint32_t *)(base + oCnt);
@@ -452,16 +452,45 @@ int pbrtgpu_scene_upload(pbrtgpu_ctx *c, const pbrtgpu_flat_scene *s) {
         return fail(PBRTGPU_E_UNSUPPORTED, "maxdepth > 20 exceeds the first MT19937 block (DESIGN.md §3.1)");
     if (s->n_nodes <= 0 || s->n_prims <= 0) return fail(PBRTGPU_E_INVALID, "empty scene");
     for (int i = 0; i < s->n_lights; ++i)
-        if (s->lights[i].type == PBRTGPU_LIGHT_INFINITE) return fail(PBRTGPU_E_UNSUPPORTED, "infinite lights not yet supported");
-    for (int i = 0; i < s->n_materials; ++i)
-        if (s->materials[i].type > PBRTGPU_MAT_SUBSTRATE && s->materials[i].type != PBRTGPU_MAT_MEASURED)
+        if (s->lights[i].type < PBRTGPU_LIGHT_AREA || s->lights[i].type > PBRTGPU_LIGHT_INFINITE)
+            return fail(PBRTGPU_E_INVALID, "bad light type");
+    if (!s->rgb_basis || !s->ewa_lut) return fail(PBRTGPU_E_INVALID, "rgb_basis / ewa_lut missing");
+    // texture graph: SCALE nodes combine CONST / IMAGE leaves; a material's spectrum slot is an
+    // IMAGE or SCALE(IMAGE, CONST) spectrum texture, its bump a float texture
+    auto texOk = [&](int id, int spectral, bool slot) -> bool {
+        if (id < 0 || id >= s->n_textures || !s->textures) return false;
+        const pbrtgpu_texture &t = s->textures[id];
+        if (t.spectral != spectral || t.type < PBRTGPU_TEX_CONST || t.type > PBRTGPU_TEX_SCALE) return false;
+        if (t.type == PBRTGPU_TEX_SCALE) {
+            for (int o : {t.tex1, t.tex2}) {
+                if (o < 0 || o >= s->n_textures || s->textures[o].spectral != spectral) return false;
+                if (s->textures[o].type == PBRTGPU_TEX_SCALE) return false;
+            }
+            if (spectral && (s->textures[t.tex1].type == PBRTGPU_TEX_CONST) == (s->textures[t.tex2].type == PBRTGPU_TEX_CONST))
+                return false;
+        }
+        return !(slot && spectral && t.type == PBRTGPU_TEX_CONST);
+    };
+    for (int i = 0; i < s->n_materials; ++i) {
+        const pbrtgpu_material &m = s->materials[i];
+        if (m.type < PBRTGPU_MAT_MATTE || m.type > PBRTGPU_MAT_MEASURED || m.type == PBRTGPU_MAT_GLASS)
             return fail(PBRTGPU_E_UNSUPPORTED, "material type not yet supported on the GPU");
+        int nt = 0;
+        for (int k = 0; k < 4; ++k)
+            if (m.tex[k] >= 0) {
+                ++nt;
+                if (!texOk(m.tex[k], 1, true) || m.type == PBRTGPU_MAT_METAL || m.type == PBRTGPU_MAT_MEASURED)
+                    return fail(PBRTGPU_E_UNSUPPORTED, "material spectrum texture");
+            }
+        if (nt > 1) return fail(PBRTGPU_E_UNSUPPORTED, "more than one textured spectrum per material");
+        if (m.bump_tex >= 0 && !texOk(m.bump_tex, 0, false)) return fail(PBRTGPU_E_INVALID, "bump texture");
+    }
     HIPCHK(hipSetDevice(c->device));
     HIPCHK(hipStreamSynchronize(c->stream));
     c->hasScene = false;
     for (auto &b : c->sceneBufs) b.release();
     c->sceneBufs.clear();
-    c->sceneBufs.reserve(32);
+    c->sceneBufs.reserve(64);
     DevScene &S = c->S;
     S.nb = s->n_bands;
     S.maxDepth = s->max_depth;
@@ -553,8 +582,23 @@ int pbrtgpu_scene_upload(pbrtgpu_ctx *c, const pbrtgpu_flat_scene *s) {
         for (int k = 0; k < 4; ++k)
             if (!remap(m.spec[k], &m.spec[k])) return fail(PBRTGPU_E_INVALID, "material spectrum offset");
     std::vector<pbrtgpu_light> lts(s->lights, s->lights + s->n_lights);
-    for (auto &l : lts)
+    S.nInf = 0;
+    for (auto &l : lts) {
         if (!remap(l.spec, &l.spec)) return fail(PBRTGPU_E_INVALID, "light spectrum offset");
+        if (l.type == PBRTGPU_LIGHT_INFINITE) ++S.nInf;
+    }
+    std::vector<pbrtgpu_texture> texs(s->textures, s->textures + std::max(0, s->n_textures));
+    for (auto &t : texs)
+        if (t.type == PBRTGPU_TEX_CONST && t.spectral && !remap(t.spec, &t.spec))
+            return fail(PBRTGPU_E_INVALID, "texture spectrum offset");
+    // FromRGB basis, each of the 14 spectra padded to whole quads
+    std::vector<float> basis((size_t)14 * nbp, 0.f);
+    for (int k = 0; k < 14; ++k)
+        for (int i = 0; i < s->n_bands; ++i) basis[(size_t)k * nbp + i] = s->rgb_basis[(size_t)k * s->n_bands + i];
+    S.nbp = nbp;
+    HIPCHK(upload(c, texs.data(), texs.size(), &S.tex));
+    HIPCHK(upload(c, basis.data(), basis.size(), &S.basis));
+    HIPCHK(upload(c, s->ewa_lut, (size_t)128, &S.ewa));
     HIPCHK(upload(c, pt.data(), pt.size(), &S.primTri));
     HIPCHK(upload(c, s->tris, (size_t)s->n_tris, &S.tris));
     HIPCHK(upload(c, s->meshes, (size_t)s->n_meshes, &S.meshes));

@@ -47,6 +47,7 @@ struct PathSoA {
     int cap;
     int *item;          // output index, -1 = free slot
     uint32_t *hp;       // pixel hash (sampler scramble key)
+    uint32_t *pix;      // sample pixel (y << 16) | x  (camera ray differentials are re-derived)
     uint32_t *smp;      // sample index
     int *bounce;        // vertex index of the last processed vertex (-1: camera ray in flight)
     uint32_t *flags;
@@ -55,6 +56,7 @@ struct PathSoA {
     float4 *L;          // [NQ][cap]
     float4 *A, *B;      // [NQ][cap]
     float4 *M;          // [NQ][cap]: measured-BRDF spectrum of the BSDF value being consumed
+    float4 *K;          // [NQ][cap]: the material's textured spectrum at the current vertex
     float *ray;         // [3][9][cap]: o.xyz, d.xyz, mint, maxt, time  for RAY_C, RAY_M, RAY_S
     int *hitPrim;       // [2][cap]  (RAY_C, RAY_M)
     float *hitT;        // [2][cap]
@@ -107,12 +109,21 @@ PGD_INLINE float4 ld4(const float *p) { return *reinterpret_cast<const float4 *>
 PGD_INLINE float &cmp(float4 &v, int k) { return k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w; }
 PGD_INLINE float cmp(const float4 &v, int k) { return k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w; }
 
-// BSDF value of four bands (quad q) -- fval() per component, identical operations
+// FrCond (reflection.cpp:62-71) for one band
+PGD_INLINE float fr_cond(float cosi, float eta, float k) {
+    float tmp = ((eta * eta + k * k) * cosi) * cosi;
+    float Rparl2 = ((tmp - ((2.f * eta) * cosi)) + 1.f) / ((tmp + ((2.f * eta) * cosi)) + 1.f);
+    float tmp_f = eta * eta + k * k;
+    float Rperp2 = ((tmp_f - ((2.f * eta) * cosi)) + cosi * cosi) / ((tmp_f + ((2.f * eta) * cosi)) + cosi * cosi);
+    return (Rparl2 + Rperp2) / 2.f;
+}
+// BSDF value of one band of a term, with the reference's operand order per BxDF::f
 PGD_INLINE float term_val(const FTerm &t, float r, float r2) {
     switch (t.kind) {
         case T_LAMB: return r * kInvPi;
         case T_OREN: return (r * kInvPi) * t.s0;
         case T_BLINN: return (((r * t.s0) * t.s1) * t.s2) / t.s3;
+        case T_BLINNC: return (((1.f * t.s0) * t.s1) * fr_cond(t.s2, r, r2)) / t.s3;   // R = Spectrum(1.)
         case T_FB: {
             const float cd = (28.f / (23.f * kPi));
             float diffuse = ((((cd * r) * (1.f - r2)) * t.s0) * t.s1);
@@ -122,10 +133,15 @@ PGD_INLINE float term_val(const FTerm &t, float r, float r2) {
         default: return 0.f;
     }
 }
-PGD_INLINE float4 fval4(const float *sp, const FVal &F, int q, const float4 *mb, size_t c) {
+// band quad q of a spectrum reference: pool offset, or -1 = the slot's K bands
+PGD_INLINE float4 spec4(const float *sp, int off, int q, const float4 *kb, size_t c) {
+    return off >= 0 ? ld4(sp + off + 4 * q) : kb[q * c];
+}
+// BSDF value of four bands (quad q): mb = measured scratch, kb = texture scratch of the slot
+PGD_INLINE float4 fval4(const float *sp, const FVal &F, int q, const float4 *mb, const float4 *kb, size_t c) {
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
     if (F.mode == FV_SPEC) {
-        float4 r = ld4(sp + F.R + 4 * q);
+        float4 r = spec4(sp, F.R, q, kb, c);
         return make_float4((1.f * r.x) / F.d, (1.f * r.y) / F.d, (1.f * r.z) / F.d, (1.f * r.w) / F.d);
     }
 #pragma unroll
@@ -137,8 +153,8 @@ PGD_INLINE float4 fval4(const float *sp, const FVal &F, int q, const float4 *mb,
                 v.x += m.x; v.y += m.y; v.z += m.z; v.w += m.w;
                 continue;
             }
-            float4 r = ld4(sp + t.R + 4 * q);
-            float4 r2 = t.kind == T_FB ? ld4(sp + t.R2 + 4 * q) : r;
+            float4 r = spec4(sp, t.R, q, kb, c);
+            float4 r2 = (t.kind == T_FB || t.kind == T_BLINNC) ? spec4(sp, t.R2, q, kb, c) : r;
             v.x += term_val(t, r.x, r2.x);
             v.y += term_val(t, r.y, r2.y);
             v.z += term_val(t, r.z, r2.z);
@@ -146,6 +162,28 @@ PGD_INLINE float4 fval4(const float *sp, const FVal &F, int q, const float4 *mb,
         }
     }
     return v;
+}
+// band quad q of an emitted radiance (Emit, device.h)
+PGD_INLINE float4 emit4(const DevScene &S, const Emit &e, int q) {
+    if (e.mode == EM_RGB) return from_rgb4(S, e.pick, true, q);
+    if (e.mode == EM_BLACK) return make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 v = ld4(S.spectra + e.off + 4 * q);
+    if (e.point) v = make_float4(v.x / e.div, v.y / e.div, v.z / e.div, v.w / e.div);
+    return v;
+}
+template <int NB>
+PGD_INLINE bool emit_black(const DevScene &S, const Emit &e) {
+    if (e.mode == EM_BLACK) return true;
+    if (e.mode == EM_POOL && !e.point) return false;   // area lights: is_black folded into the mode
+    bool black = true;
+#pragma unroll
+    for (int q = 0; q < Bands<NB>::NQ; ++q) {
+        float4 v = emit4(S, e, q);
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (4 * q + k < NB) black = black && (cmp(v, k) == 0.);
+    }
+    return black;
 }
 
 // IrregIsotropicBRDF::f (reflection.cpp:251-264): KdTree::Lookup (kdtree.h:160-185) with
@@ -252,6 +290,7 @@ PGD_INLINE void path_start(const DevScene &S, const PathSoA &P, const ItemSrc &s
     ray_store(P, RAY_C, slot, r);
     P.item[slot] = (int)item;
     P.hp[slot] = hp;
+    P.pix[slot] = ((uint32_t)py << 16) | (uint32_t)px;
     P.smp[slot] = s;
     P.bounce[slot] = -1;
     P.flags[slot] = PF_CONT;
@@ -334,11 +373,28 @@ PGD_INLINE Pushes shade_vertex(const DevScene &S, const PathSoA &P, int slot, in
             }
         }
     }
+    const uint32_t hp = P.hp[slot], s = P.smp[slot], spp = (uint32_t)S.spp;
+    // only the camera ray carries differentials (path.cpp:107 drops them); they matter only
+    // to textured materials
+    float diff[4] = {0.f, 0.f, 0.f, 0.f};
+    if (vb == 0) {
+        const pbrtgpu_material &mt = S.mats[S.prims[is.prim].material];
+        if (mt.bump_tex >= 0 || mt.tex[0] >= 0 || mt.tex[1] >= 0 || mt.tex[2] >= 0 || mt.tex[3] >= 0) {
+            const uint32_t pxy = P.pix[slot];
+            float u[2], lens[2];
+            s2d(hp, 0, s, spp, u);
+            s2d(hp, 1, s, spp, lens);
+            const float timeU = s1d(hp, 2, s, spp);
+            RayDiff rd = camera_diff(S.cam, S.spp, (int)(pxy & 0xffffu) + u[0], (int)(pxy >> 16) + u[1], lens[0], lens[1],
+                                     timeU);
+            compute_differentials(is.dg, rd, diff);
+        }
+    }
+    float4 *kb = P.K + slot;
     BSDF bs;
     V p, n;
-    get_bsdf(S, is, bs, &p, &n);
+    get_bsdf(S, is, diff, kb, c, bs, &p, &n);
     const V wo = vneg(ray.d);
-    const uint32_t hp = P.hp[slot], s = P.smp[slot], spp = (uint32_t)S.spp;
     MT rng;
     const bool useMT = vb >= 3;
     if (useMT) mt_load(P, slot, fl, rng);
@@ -366,26 +422,19 @@ PGD_INLINE Pushes shade_vertex(const DevScene &S, const PathSoA &P, int slot, in
         int lightNum = (int)floorf(ulnum * nLights);
         if (lightNum > nLights - 1) lightNum = nLights - 1;
         const pbrtgpu_light &Lt = S.lights[lightNum];
-        const float *Ls = sp + Lt.spec;
         const int flags = BSDF_ALL & ~BSDF_SPECULAR;
         fl |= PF_PEND | ((uint32_t)lightNum << PF_LIGHT_SHIFT);
         // ---- light sample -> A (added if the shadow ray is unoccluded)
         V wi;
         float lightPdf, bsdfPdf;
         Seg vis;
-        bool lit, isPoint;
-        float lscale = light_sample_L(S, Lt, p, is.rayEps, ul, &wi, &lightPdf, &vis, &lit, &isPoint);
-        bool liBlack = isPoint ? false : !lit;
-        if (isPoint) {
-            bool allz = true;
-            for (int i = 0; i < NB; ++i) allz = allz && ((Ls[i] / lscale) == 0.);
-            liBlack = allz;
-        } else if (lit) liBlack = Lt.is_black != 0;
-        if (lightPdf > 0. && !liBlack) {
+        Emit em;
+        light_sample_L(S, Lt, p, is.rayEps, ul, &wi, &lightPdf, &vis, &em);
+        if (lightPdf > 0. && !emit_black<NB>(S, em)) {
             bsdf_f(bs, wo, wi, flags, F);
             fval_prepare<NB>(S, F, mb, c);
             float sc;
-            if (isPoint) sc = fabsf(vdot(wi, n)) / lightPdf;
+            if (em.point) sc = fabsf(vdot(wi, n)) / lightPdf;
             else {
                 bsdfPdf = bsdf_pdf(bs, wo, wi, flags);
                 float weight = power_heuristic(lightPdf, bsdfPdf);
@@ -396,11 +445,10 @@ PGD_INLINE Pushes shade_vertex(const DevScene &S, const PathSoA &P, int slot, in
             bool black = true;
 #pragma unroll
             for (int q = 0; q < NQ; ++q) {
-                float4 f = fval4(sp, F, q, mb, c), e = ld4(Ls + 4 * q), a;
+                float4 f = fval4(sp, F, q, mb, kb, c), e = emit4(S, em, q), a;
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
-                    float li = isPoint ? (cmp(e, k) / lscale) : cmp(e, k);
-                    cmp(a, k) = (cmp(f, k) * li) * sc;
+                    cmp(a, k) = (cmp(f, k) * cmp(e, k)) * sc;
                     if (4 * q + k < NB) black = black && (cmp(f, k) == 0.);
                 }
                 A[q * c] = a;
@@ -413,8 +461,9 @@ PGD_INLINE Pushes shade_vertex(const DevScene &S, const PathSoA &P, int slot, in
                 out.s = true;
             }
         }
-        // ---- BSDF sample with MIS -> B (added if the MIS ray reaches this light)
-        if (!isPoint) {
+        // ---- BSDF sample with MIS -> B (added if the MIS ray reaches this light: hits it
+        // facing, for an area light; escapes the scene, for the environment)
+        if (!em.point) {
             int sampledType;
             bsdf_sample_f(bs, wo, &wi, ub[0], ub[1], ub[2], &bsdfPdf, flags, &sampledType, F);
             if (bsdfPdf > 0. && !(F.mode == FV_SUM && F.n == 0)) {
@@ -426,13 +475,19 @@ PGD_INLINE Pushes shade_vertex(const DevScene &S, const PathSoA &P, int slot, in
                     if (lightPdf == 0.) go = false;
                     else weight = power_heuristic(bsdfPdf, lightPdf);
                 }
-                if (go && !Lt.is_black) {
+                Emit eb;
+                if (Lt.type == PBRTGPU_LIGHT_INFINITE) {
+                    if (go) eb = inf_Le(Lt, wi);
+                } else {
+                    eb.mode = Lt.is_black ? EM_BLACK : EM_POOL; eb.off = Lt.spec; eb.div = 1.f; eb.point = false;
+                }
+                if (go && !emit_black<NB>(S, eb)) {
                     const float ad = fabsf(vdot(wi, n));
                     float4 *B = P.B + slot;
                     bool black = true;
 #pragma unroll
                     for (int q = 0; q < NQ; ++q) {
-                        float4 f = fval4(sp, F, q, mb, c), e = ld4(Ls + 4 * q), b;
+                        float4 f = fval4(sp, F, q, mb, kb, c), e = emit4(S, eb, q), b;
 #pragma unroll
                         for (int k = 0; k < 4; ++k) {
                             cmp(b, k) = (((cmp(f, k) * cmp(e, k)) * ad) * weight) / bsdfPdf;
@@ -489,7 +544,7 @@ PGD_INLINE Pushes shade_vertex(const DevScene &S, const PathSoA &P, int slot, in
         bool black = true;
 #pragma unroll
         for (int q = 0; q < NQ; ++q) {
-            float4 f = fval4(sp, F, q, mb, c), b = beta[q * c];
+            float4 f = fval4(sp, F, q, mb, kb, c), b = beta[q * c];
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 cmp(nb4[q], k) = cmp(b, k) * ((cmp(f, k) * ad) / pdf);
@@ -548,8 +603,10 @@ PGD_INLINE Pushes shade_slot(const DevScene &S, const PathSoA &P, int slot, floa
         const bool useA = (fl & PF_PA) && !P.occ[slot];
         bool useB = false;
         if (fl & PF_PB) {
+            const int ln = (int)(fl >> PF_LIGHT_SHIFT);
             int mp = P.hitPrim[c + slot];
-            if (mp >= 0 && S.prims[mp].area_light == (int)(fl >> PF_LIGHT_SHIFT)) {
+            if (S.lights[ln].type == PBRTGPU_LIGHT_INFINITE) useB = mp < 0;   // Li = light->Le(ray)
+            else if (mp >= 0 && S.prims[mp].area_light == ln) {
                 Ray mr = ray_load(P, RAY_M, slot);
                 Isect lis;
                 isect_fill(S, mr, mp, P.hitT[c + slot], lis);
@@ -578,12 +635,35 @@ PGD_INLINE Pushes shade_slot(const DevScene &S, const PathSoA &P, int slot, floa
         const int prim = P.hitPrim[slot];
         fl &= ~PF_CONT;
         if (prim < 0) {
-            if (vb > 0 && (fl & PF_SPEC)) {
-                const float4 *beta = P.beta + (size_t)(vb & 1) * NQ * c + slot;
+            if (vb == 0) {
+                // SamplerRenderer::Li (samplerrenderer.cpp:237-240): Li = sum of the lights' Le,
+                // zero for area and point lights
+                if (S.nInf > 0) {
+                    const Ray ray = ray_load(P, RAY_C, slot);
+                    for (int l = 0; l < S.nLights; ++l)
+                        if (S.lights[l].type == PBRTGPU_LIGHT_INFINITE) {
+                            const Emit e = inf_Le(S.lights[l], ray.d);
 #pragma unroll
-                for (int q = 0; q < NQ; ++q) {
-                    float4 bt = beta[q * c];
-                    L[q].x += bt.x * 0.f; L[q].y += bt.y * 0.f; L[q].z += bt.z * 0.f; L[q].w += bt.w * 0.f;
+                            for (int q = 0; q < NQ; ++q) {
+                                float4 v = emit4(S, e, q);
+                                L[q].x += v.x; L[q].y += v.y; L[q].z += v.z; L[q].w += v.w;
+                            }
+                        }
+                }
+            } else if (fl & PF_SPEC) {
+                // path.cpp:92-96: L += beta * Le(ray) for every light
+                const float4 *beta = P.beta + (size_t)(vb & 1) * NQ * c + slot;
+                V d = v3(0.f, 0.f, 0.f);
+                if (S.nInf > 0) d = ray_load(P, RAY_C, slot).d;
+                for (int l = 0; l < S.nLights; ++l) {
+                    Emit e;
+                    e.mode = EM_BLACK;
+                    if (S.lights[l].type == PBRTGPU_LIGHT_INFINITE) e = inf_Le(S.lights[l], d);
+#pragma unroll
+                    for (int q = 0; q < NQ; ++q) {
+                        float4 bt = beta[q * c], v = emit4(S, e, q);
+                        L[q].x += bt.x * v.x; L[q].y += bt.y * v.y; L[q].z += bt.z * v.z; L[q].w += bt.w * v.w;
+                    }
                 }
             }
         } else {

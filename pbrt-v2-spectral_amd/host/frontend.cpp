@@ -63,8 +63,9 @@ struct ParamSet {
 };
 
 // texture values known at scene-build time (constant textures; 1x1 fallback images)
-struct FloatTex { bool constant = true; float value = 0.f; };
-struct SpecTex { bool constant = true; Spec value; };
+// non-constant ones refer to a pbrtgpu_texture (index `tex` into HostScene::textures)
+struct FloatTex { bool constant = true; float value = 0.f; int tex = -1; };
+struct SpecTex { bool constant = true; Spec value; int tex = -1; };
 
 // ------------------------------------------------------------------------------------
 // Tokenizer (pbrtlex.ll)
@@ -762,23 +763,107 @@ private:
     }
 
     // ------------------------------ textures / materials ---------------------------
+    int AddTexture(const pbrtgpu_texture &t) {
+        out->textures.push_back(t);
+        return (int)out->textures.size() - 1;
+    }
+    static pbrtgpu_texture TexNode(int type, bool spectral) {
+        pbrtgpu_texture t{};
+        t.type = type; t.spectral = spectral ? 1 : 0;
+        t.tex1 = t.tex2 = t.spec = -1;
+        t.su = t.sv = 1.f; t.max_aniso = 8.f;
+        return t;
+    }
+    // What ReadImage (imageio.cpp:45-66) does with a file in this build (no OpenEXR):
+    // 0 = returns the 1x1 RGB 0.5 image (unknown suffix), 1 = returns NULL (.tga/.pfm that
+    // cannot be opened); a readable .tga/.pfm would be decoded -- not supported yet.
+    int ImageFileKind(const std::string &fn) {
+        if (fn.size() >= 5) {
+            std::string suf = fn.substr(fn.size() - 4);
+            if (suf == ".tga" || suf == ".TGA" || suf == ".pfm" || suf == ".PFM") {
+                FILE *f = fopen(fn.c_str(), "rb");
+                if (f) { fclose(f); throw std::runtime_error("image file " + fn + ": decoded image maps are not supported yet"); }
+                return 1;
+            }
+        }
+        return 0;
+    }
+    // ImageTexture (imagemap.cpp:47-73 GetTexture, :97-160 Create*): a one-texel MIPMap
+    int MakeImageTexture(const ParamSet &p, bool spectral) {
+        pbrtgpu_texture t = TexNode(PBRTGPU_TEX_IMAGE, spectral);
+        std::string mapping = GetString(p, p, "mapping", "uv");
+        if (mapping != "uv") throw std::runtime_error("texture mapping '" + mapping + "' is not supported yet");
+        t.su = GetFloat(p, p, "uscale", 1.f); t.sv = GetFloat(p, p, "vscale", 1.f);
+        t.du = GetFloat(p, p, "udelta", 0.f); t.dv = GetFloat(p, p, "vdelta", 0.f);
+        float maxAniso = GetFloat(p, p, "maxanisotropy", 8.f);
+        bool trilerp = p.FindOneBool("trilinear", false), noFilt = p.FindOneBool("noFiltering", false);
+        std::string wrap = GetString(p, p, "wrap", "repeat");
+        int wm = wrap == "black" ? PBRTGPU_WRAP_BLACK : (wrap == "clamp" ? PBRTGPU_WRAP_CLAMP : PBRTGPU_WRAP_REPEAT);
+        float scale = GetFloat(p, p, "scale", 1.f), gamma = GetFloat(p, p, "gamma", 1.f);
+        std::string fn = GetString(p, p, "filename", "");
+        if (!fn.empty()) fn = Resolve(fn);
+        if (ImageFileKind(fn) == 0) {
+            // RGB 0.5 texel through convertIn: Pow(scale * rgb, gamma) / powf(scale * rgb.y(), gamma)
+            if (spectral) for (int k = 0; k < 3; ++k) t.texel[k] = powf(scale * 0.5f, gamma);
+            else t.texel[0] = powf(scale * (0.212671f * 0.5f + 0.715160f * 0.5f + 0.072169f * 0.5f), gamma);
+            t.trilinear = (trilerp || noFilt) ? 1 : 0;
+            t.max_aniso = maxAniso;
+            t.wrap = wm;
+        } else {
+            // one-valued MIPMap(1, 1, &powf(scale, gamma)) with the MIPMap defaults
+            float v = powf(scale, gamma);
+            for (int k = 0; k < 3; ++k) t.texel[k] = spectral ? v : 0.f;
+            if (!spectral) t.texel[0] = v;
+            t.trilinear = 0; t.max_aniso = 8.f; t.wrap = PBRTGPU_WRAP_REPEAT;
+        }
+        return AddTexture(t);
+    }
+    // operand of a ScaleTexture: a CONST or IMAGE node
+    int FloatLeaf(const FloatTex &f) {
+        if (!f.constant) {
+            if (out->textures[f.tex].type == PBRTGPU_TEX_SCALE) throw std::runtime_error("nested scale textures are not supported yet");
+            return f.tex;
+        }
+        pbrtgpu_texture t = TexNode(PBRTGPU_TEX_CONST, false);
+        t.value = f.value;
+        return AddTexture(t);
+    }
     void MakeTexture(const std::string &name, const std::string &type, const std::string &cls, const ParamSet &p) {
         // TextureParams(params, params, ...) -- api.cpp:933-956
         if (type == "float") {
             FloatTex t;
             if (cls == "constant") t.value = GetFloat(p, p, "value", 1.f);
-            else if (cls == "scale") {
+            else if (cls == "scale") {   // ScaleTexture::Evaluate = tex1 * tex2 (scale.h)
                 FloatTex a = GetFloatTex(p, p, "tex1", 1.f), b = GetFloatTex(p, p, "tex2", 1.f);
-                t.constant = a.constant && b.constant; t.value = a.value * b.value;   // ScaleTexture::Evaluate
-            } else { t.constant = false; out->warnings.push_back("float texture '" + cls + "' is not constant"); }
+                if (a.constant && b.constant) t.value = a.value * b.value;
+                else {
+                    pbrtgpu_texture n = TexNode(PBRTGPU_TEX_SCALE, false);
+                    n.tex1 = FloatLeaf(a); n.tex2 = FloatLeaf(b);
+                    t.constant = false; t.tex = AddTexture(n);
+                }
+            } else if (cls == "imagemap") { t.constant = false; t.tex = MakeImageTexture(p, false); }
+            else throw std::runtime_error("float texture '" + cls + "' is not supported yet");
             gs.floatTextures[name] = t;
         } else if (type == "color" || type == "spectrum") {
             SpecTex t;
             if (cls == "constant") t.value = GetSpec(p, p, "value", spec.Const(1.f));
             else if (cls == "scale") {
                 SpecTex a = GetSpecTex(p, p, "tex1", spec.Const(1.f)), b = GetSpecTex(p, p, "tex2", spec.Const(1.f));
-                t.constant = a.constant && b.constant; t.value = SpecMul(a.value, b.value);
-            } else { t.constant = false; t.value = spec.Const(0.f); out->warnings.push_back("spectrum texture '" + cls + "' is not constant"); }
+                if (a.constant && b.constant) t.value = SpecMul(a.value, b.value);
+                else {
+                    // device form: one image leaf times one constant spectrum
+                    if (!a.constant && !b.constant) throw std::runtime_error("scale of two non-constant spectrum textures is not supported yet");
+                    const SpecTex &img = a.constant ? b : a, &cst = a.constant ? a : b;
+                    if (out->textures[img.tex].type != PBRTGPU_TEX_IMAGE) throw std::runtime_error("nested scale textures are not supported yet");
+                    pbrtgpu_texture c = TexNode(PBRTGPU_TEX_CONST, true);
+                    c.spec = EmitSpectrum(cst.value);
+                    int ci = AddTexture(c);
+                    pbrtgpu_texture n = TexNode(PBRTGPU_TEX_SCALE, true);
+                    n.tex1 = a.constant ? ci : img.tex; n.tex2 = a.constant ? img.tex : ci;
+                    t.constant = false; t.tex = AddTexture(n);
+                }
+            } else if (cls == "imagemap") { t.constant = false; t.tex = MakeImageTexture(p, true); }
+            else throw std::runtime_error("spectrum texture '" + cls + "' is not supported yet");
             gs.spectrumTextures[name] = t;
         }
     }
@@ -821,31 +906,53 @@ private:
         if (!t.constant) throw std::runtime_error("non-constant float texture for '" + n + "' is not supported yet");
         return t.value;
     }
+    // spectrum parameter k of a material: a constant (clamped where the material clamps) or
+    // one textured slot evaluated per hit on the device
+    void SpecSlot(MaterialObj &mo, int k, const ParamSet &g, const ParamSet &m, const std::string &n, const Spec &d,
+                  bool clamp) {
+        SpecTex t = GetSpecTex(g, m, n, d);
+        if ((int)mo.spectra.size() != k) throw std::runtime_error("internal: material slot order");
+        if (t.constant) { mo.spectra.push_back(clamp ? SpecClamp(t.value) : t.value); return; }
+        for (int j = 0; j < 4; ++j)
+            if (mo.m.tex[j] >= 0) throw std::runtime_error("more than one textured spectrum parameter per material is not supported yet");
+        if (!clamp) throw std::runtime_error("textured '" + n + "' is not supported yet");
+        mo.m.tex[k] = t.tex;
+        mo.spectra.push_back(spec.Const(0.f));   // placeholder; the device evaluates tex[k]
+    }
     std::shared_ptr<MaterialObj> MakeMaterial(const std::string &name, const ParamSet &g, const ParamSet &m) {
         auto mo = std::make_shared<MaterialObj>();
         pbrtgpu_material &mt = mo->m;
-        // every material: normalmap (constant 0 -> black, skipped) and bumpmap (constant)
+        for (int k = 0; k < 4; ++k) mt.tex[k] = -1;
+        mt.bump_tex = -1;
+        // every material: normalmap (constant 0 -> black, skipped) and bumpmap (float texture)
         Spec nmap = ConstSpecTex(g, m, "normalmap", spec.Const(0.f));
         if (!SpecIsBlack(nmap)) throw std::runtime_error("normal maps are not supported yet");
-        mt.f[7] = ConstFloatTex(g, m, "bumpmap", 0.f);
+        FloatTex bump = GetFloatTex(g, m, "bumpmap", 0.f);
+        if (bump.constant) mt.f[7] = bump.value;
+        else mt.bump_tex = bump.tex;
         if (name == "matte") {   // matte.cpp:34-72
             mt.type = PBRTGPU_MAT_MATTE;
-            mo->spectra.push_back(SpecClamp(ConstSpecTex(g, m, "Kd", spec.Const(0.5f))));
+            SpecSlot(*mo, 0, g, m, "Kd", spec.Const(0.5f), true);
             mt.f[0] = Clamp(ConstFloatTex(g, m, "sigma", 0.f), 0.f, 90.f);
         } else if (name == "plastic") {   // plastic.cpp:34-74
             mt.type = PBRTGPU_MAT_PLASTIC;
-            mo->spectra.push_back(SpecClamp(ConstSpecTex(g, m, "Kd", spec.Const(0.25f))));
-            mo->spectra.push_back(SpecClamp(ConstSpecTex(g, m, "Ks", spec.Const(0.25f))));
+            SpecSlot(*mo, 0, g, m, "Kd", spec.Const(0.25f), true);
+            SpecSlot(*mo, 1, g, m, "Ks", spec.Const(0.25f), true);
             mt.f[0] = ConstFloatTex(g, m, "roughness", .1f);
         } else if (name == "mirror") {   // mirror.cpp
             mt.type = PBRTGPU_MAT_MIRROR;
-            mo->spectra.push_back(SpecClamp(ConstSpecTex(g, m, "Kr", spec.Const(0.9f))));
+            SpecSlot(*mo, 0, g, m, "Kr", spec.Const(0.9f), true);
         } else if (name == "substrate") {   // substrate.cpp
             mt.type = PBRTGPU_MAT_SUBSTRATE;
-            mo->spectra.push_back(SpecClamp(ConstSpecTex(g, m, "Kd", spec.Const(.5f))));
-            mo->spectra.push_back(SpecClamp(ConstSpecTex(g, m, "Ks", spec.Const(.5f))));
+            SpecSlot(*mo, 0, g, m, "Kd", spec.Const(.5f), true);
+            SpecSlot(*mo, 1, g, m, "Ks", spec.Const(.5f), true);
             mt.f[0] = ConstFloatTex(g, m, "uroughness", .1f);
             mt.f[1] = ConstFloatTex(g, m, "vroughness", .1f);
+        } else if (name == "metal") {   // metal.cpp:44-62, 99-110 (eta, k unclamped)
+            mt.type = PBRTGPU_MAT_METAL;
+            SpecSlot(*mo, 0, g, m, "eta", CopperSpectrum(false), false);
+            SpecSlot(*mo, 1, g, m, "k", CopperSpectrum(true), false);
+            mt.f[0] = ConstFloatTex(g, m, "roughness", .01f);
         } else if (name == "measured") {   // measured.cpp:66-130, 182-206 (.brdf: IrregIsotropicBRDF)
             mt.type = PBRTGPU_MAT_MEASURED;
             std::string fn = Resolve(GetString(g, m, "filename", ""));
@@ -859,6 +966,32 @@ private:
         } else
             throw std::runtime_error("material '" + name + "' is not supported by this build yet");
         return mo;
+    }
+    // default metal eta / k: copper, sampled at 56 wavelengths (metal.cpp:71-97), FromSampled
+    Spec CopperSpectrum(bool kAbsorption) const {
+        static const float wl[56] = {
+        298.7570554f, 302.4004341f, 306.1337728f, 309.960445f, 313.8839949f, 317.9081487f, 322.036826f,
+        326.2741526f, 330.6244747f, 335.092373f, 339.6826795f, 344.4004944f, 349.2512056f, 354.2405086f,
+        359.374429f, 364.6593471f, 370.1020239f, 375.7096303f, 381.4897785f, 387.4505563f, 393.6005651f,
+        399.9489613f, 406.5055016f, 413.2805933f, 420.2853492f, 427.5316483f, 435.0322035f, 442.8006357f,
+        450.8515564f, 459.2006593f, 467.8648226f, 476.8622231f, 486.2124627f, 495.936712f, 506.0578694f,
+        516.6007417f, 527.5922468f, 539.0616435f, 551.0407911f, 563.5644455f, 576.6705953f, 590.4008476f,
+        604.8008683f, 619.92089f, 635.8162974f, 652.5483053f, 670.1847459f, 688.8009889f, 708.4810171f,
+        729.3186941f, 751.4192606f, 774.9011125f, 799.8979226f, 826.5611867f, 855.0632966f, 885.6012714f};
+        static const float eta[56] = {
+        1.400313f, 1.38f, 1.358438f, 1.34f, 1.329063f, 1.325f, 1.3325f, 1.34f, 1.334375f, 1.325f, 1.317812f,
+        1.31f, 1.300313f, 1.29f, 1.281563f, 1.27f, 1.249062f, 1.225f, 1.2f, 1.18f, 1.174375f, 1.175f,
+        1.1775f, 1.18f, 1.178125f, 1.175f, 1.172812f, 1.17f, 1.165312f, 1.16f, 1.155312f, 1.15f, 1.142812f,
+        1.135f, 1.131562f, 1.12f, 1.092437f, 1.04f, 0.950375f, 0.826f, 0.645875f, 0.468f, 0.35125f, 0.272f,
+        0.230813f, 0.214f, 0.20925f, 0.213f, 0.21625f, 0.223f, 0.2365f, 0.25f, 0.254188f, 0.26f, 0.28f, 0.3f};
+        static const float kk[56] = {
+        1.662125f, 1.687f, 1.703313f, 1.72f, 1.744563f, 1.77f, 1.791625f, 1.81f, 1.822125f, 1.834f, 1.85175f,
+        1.872f, 1.89425f, 1.916f, 1.931688f, 1.95f, 1.972438f, 2.015f, 2.121562f, 2.21f, 2.177188f, 2.13f,
+        2.160063f, 2.21f, 2.249938f, 2.289f, 2.326f, 2.362f, 2.397625f, 2.433f, 2.469187f, 2.504f, 2.535875f,
+        2.564f, 2.589625f, 2.605f, 2.595562f, 2.583f, 2.5765f, 2.599f, 2.678062f, 2.809f, 3.01075f, 3.24f,
+        3.458187f, 3.67f, 3.863125f, 4.05f, 4.239563f, 4.43f, 4.619563f, 4.817f, 5.034125f, 5.26f, 5.485625f,
+        5.717f};
+        return spec.FromSampled(wl, kAbsorption ? kk : eta, 56);
     }
     std::map<std::string, std::shared_ptr<MeasuredData> > measuredCache;
     // ReadFloatFile (floatfile.cpp:30-74)
@@ -987,6 +1120,29 @@ private:
             lo->L = SpecMul(I, sc);
             V3 lp = l2w.Point(V3(0, 0, 0));
             lo->l.pos[0] = lp.x; lo->l.pos[1] = lp.y; lo->l.pos[2] = lp.z;
+            memcpy(lo->l.l2w_m, l2w.m.m, 64); memcpy(lo->l.l2w_minv, l2w.mInv.m, 64);
+        } else if (name == "infinite" || name == "exinfinite") {   // infinite.cpp:41-80, 232-245
+            Spec L = p.FindOneSpectrum("L", spec.Const(1.0f));
+            Spec sc = p.FindOneSpectrum("scale", spec.Const(1.0f));
+            std::string texmap = p.FindOneString("mapname", "");
+            lo->l.type = PBRTGPU_LIGHT_INFINITE;
+            lo->L = SpecMul(L, sc);
+            float rgb[3];
+            spec.ToRGB(lo->L, rgb);   // L.ToRGBSpectrum()
+            float texel[3] = {rgb[0], rgb[1], rgb[2]};
+            if (texmap != "" && ImageFileKind(Resolve(texmap)) == 0)
+                for (int k = 0; k < 3; ++k) texel[k] = 0.5f * rgb[k];   // RGB 0.5 texel *= L.ToRGBSpectrum()
+            for (int k = 0; k < 3; ++k) lo->l.texel[k] = texel[k];
+            lo->l.wrap = PBRTGPU_WRAP_REPEAT;
+            // Distribution2D of img[0] = Lookup(0, 0, 1).y() * sinTheta (one texel: Texel(0, 0, 0))
+            const float kPiF = 3.14159265358979323846f;
+            float img = 0.212671f * texel[0] + 0.715160f * texel[1] + 0.072169f * texel[2];
+            img *= sinf(kPiF * float(0 + .5f) / float(1));
+            float funcInt = 0.f + img / 1;             // Distribution1D: cdf[1]
+            float margFunc = funcInt, margInt = 0.f + margFunc / 1;
+            lo->l.map_pdf = (img / funcInt) * (margFunc / margInt);   // SampleContinuous pdfs[0] * pdfs[1]
+            lo->l.dist_pdf = (funcInt * margInt == 0.f) ? 0.f : (img * margFunc) / (funcInt * margInt);
+            const Xform &l2w = curT.t[0];
             memcpy(lo->l.l2w_m, l2w.m.m, 64); memcpy(lo->l.l2w_minv, l2w.mInv.m, 64);
         } else
             throw std::runtime_error("light '" + name + "' is not supported by this build yet");
@@ -1292,6 +1448,9 @@ private:
         if (m->flatIndex >= 0) return m->flatIndex;
         pbrtgpu_material fm = m->m;
         for (int k = 0; k < 4; ++k) fm.spec[k] = k < (int)m->spectra.size() ? EmitSpectrum(m->spectra[k]) : -1;
+        fm.black_mask = 0;
+        for (int k = 0; k < (int)m->spectra.size() && k < 4; ++k)
+            if (fm.tex[k] < 0 && SpecIsBlack(m->spectra[k])) fm.black_mask |= 1 << k;
         if (m->measured) fm.aux = EmitMeasured(m->measured.get(), &fm.aux2);
         out->materials.push_back(fm);
         m->flatIndex = (int)out->materials.size() - 1;
@@ -1437,6 +1596,15 @@ private:
             }
             out->lights.push_back(fl);
         }
+        // ---- MIPMap::weightLut (mipmap.h:185-193) and the FromRGB basis tables
+        out->ewaLut.resize(128);
+        for (int i = 0; i < 128; ++i) {
+            float alpha = 2;
+            float r2 = float(i) / float(128 - 1);
+            out->ewaLut[i] = expf(-alpha * r2) - expf(-alpha);
+        }
+        out->rgbBasis.clear();
+        for (int k = 0; k < 14; ++k) out->rgbBasis.insert(out->rgbBasis.end(), spec.Basis(k), spec.Basis(k) + spec.n());
     }
 };
 
@@ -1467,6 +1635,10 @@ void ComputeCamera(const CameraParams &cp, int xres, int yres, pbrtgpu_camera *o
     Xform rasterToScreen = Inverse(screenToRaster);
     Xform rasterToCamera = Inverse(camToScreen) * rasterToScreen;
     memcpy(C.raster_to_camera, rasterToCamera.m.m, 64);
+    // dxCamera / dyCamera (perspective.cpp:45-48)
+    V3 r0 = rasterToCamera.Point(V3(0, 0, 0)), rx = rasterToCamera.Point(V3(1, 0, 0)), ry = rasterToCamera.Point(V3(0, 1, 0));
+    C.dx_camera[0] = rx.x - r0.x; C.dx_camera[1] = rx.y - r0.y; C.dx_camera[2] = rx.z - r0.z;
+    C.dy_camera[0] = ry.x - r0.x; C.dy_camera[1] = ry.y - r0.y; C.dy_camera[2] = ry.z - r0.z;
     memcpy(C.cam2world_m, cp.cam2world, 64);
     C.lens_radius = cp.lensRadius; C.focal_distance = cp.focalDistance;
     C.shutter_open = cp.shutterOpen; C.shutter_close = cp.shutterClose;
@@ -1502,6 +1674,9 @@ void HostScene::Flat(pbrtgpu_flat_scene *f) const {
     f->n_instances = (int)instances.size(); f->instances = instances.empty() ? nullptr : instances.data();
     f->prim_instance = primInstance.data();
     f->n_kdnodes = (int)kdnodes.size(); f->kdnodes = kdnodes.empty() ? nullptr : kdnodes.data();
+    f->n_textures = (int)textures.size(); f->textures = textures.empty() ? nullptr : textures.data();
+    f->ewa_lut = ewaLut.empty() ? nullptr : ewaLut.data();
+    f->rgb_basis = rgbBasis.empty() ? nullptr : rgbBasis.data();
 }
 
 }  // namespace pbrtamd

@@ -11,7 +11,7 @@
 namespace pbrtamd {
 
 static const char kMagic[8] = {'P', 'B', 'R', 'T', 'P', 'A', 'C', 'K'};
-static const uint32_t kVersion = 4;
+static const uint32_t kVersion = 5;
 
 static bool W(gzFile f, const void *p, size_t n) {
     const char *c = (const char *)p;
@@ -45,7 +45,8 @@ bool SavePack(const HostScene &s, const std::string &path, std::string *err) {
     ok = ok && WArr(f, s.bandY) && WArr(f, s.nodes) && WArr(f, s.prims) && WArr(f, s.tris) && WArr(f, s.meshes) &&
          WArr(f, s.vertP) && WArr(f, s.vertN) && WArr(f, s.vertUV) && WArr(f, s.quadrics) && WArr(f, s.materials) &&
          WArr(f, s.lights) && WArr(f, s.lightShapes) && WArr(f, s.spectra) && WArr(f, s.instances) &&
-         WArr(f, s.primInstance) && WArr(f, s.kdnodes);
+         WArr(f, s.primInstance) && WArr(f, s.kdnodes) && WArr(f, s.textures) && WArr(f, s.ewaLut) &&
+         WArr(f, s.rgbBasis);
     ok = (gzclose(f) == Z_OK) && ok;
     if (!ok && err) *err = "write error on " + path;
     return ok;
@@ -64,7 +65,8 @@ bool LoadPack(const std::string &path, HostScene *s, std::string *err) {
     ok = ok && RArr(f, s->bandY) && RArr(f, s->nodes) && RArr(f, s->prims) && RArr(f, s->tris) && RArr(f, s->meshes) &&
          RArr(f, s->vertP) && RArr(f, s->vertN) && RArr(f, s->vertUV) && RArr(f, s->quadrics) && RArr(f, s->materials) &&
          RArr(f, s->lights) && RArr(f, s->lightShapes) && RArr(f, s->spectra) && RArr(f, s->instances) &&
-         RArr(f, s->primInstance) && RArr(f, s->kdnodes);
+         RArr(f, s->primInstance) && RArr(f, s->kdnodes) && RArr(f, s->textures) && RArr(f, s->ewaLut) &&
+         RArr(f, s->rgbBasis);
     gzclose(f);
     if (!ok && err) *err = "bad or truncated scene pack " + path;
     return ok;

@@ -54,6 +54,9 @@ struct HostScene {
     std::vector<pbrtgpu_instance> instances;
     std::vector<int32_t> primInstance;        // per prim: owning instance or -1
     std::vector<pbrtgpu_kdnode> kdnodes;      // measured BRDF kd-trees
+    std::vector<pbrtgpu_texture> textures;
+    std::vector<float> ewaLut;                // [128] MIPMap::weightLut
+    std::vector<float> rgbBasis;              // [14][nBands] FromRGB basis spectra
     // diagnostics
     std::vector<std::string> warnings;
     int bvhMaxDepth = 0;

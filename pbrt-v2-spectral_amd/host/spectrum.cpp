@@ -97,6 +97,19 @@ float SpectrumCtx::y(const Spec &s) const {
     return yy / tyint;
 }
 
+void SpectrumCtx::ToRGB(const Spec &s, float rgb[3]) const {
+    float xyz[3] = {0.f, 0.f, 0.f};
+    for (int i = 0; i < nb; ++i) {
+        xyz[0] += tX[i] * s[i];
+        xyz[1] += tY[i] * s[i];
+        xyz[2] += tZ[i] * s[i];
+    }
+    for (int k = 0; k < 3; ++k) xyz[k] /= tyint;
+    rgb[0] = 3.240479f * xyz[0] - 1.537150f * xyz[1] - 0.498535f * xyz[2];
+    rgb[1] = -0.969256f * xyz[0] + 1.875991f * xyz[1] + 0.041556f * xyz[2];
+    rgb[2] = 0.055648f * xyz[0] - 0.204043f * xyz[1] + 1.057311f * xyz[2];
+}
+
 Spec SpecMul(const Spec &a, const Spec &b) {
     Spec r = a;
     for (size_t i = 0; i < r.size(); ++i) r[i] *= b[i];

@@ -25,6 +25,9 @@ public:
     Spec FromSampled(const float *lambda, const float *v, int n) const;
     Spec Blackbody(float tempK, float scale) const;
     float y(const Spec &s) const;
+    // SampledSpectrum::ToRGB (spectrum.h:352-362, 423-427): ToXYZ then XYZToRGB
+    void ToRGB(const Spec &s, float rgb[3]) const;
+    const float *Basis(int k) const { return basis[k]; }   // FromRGB basis, order as in FromRGB
     const float *Y() const { return tY; }
     float yint() const { return tyint; }
 private:

@@ -38,7 +38,8 @@ class Camera(ctypes.Structure):
                 ("px_start", ctypes.c_int32), ("px_count", ctypes.c_int32),
                 ("py_start", ctypes.c_int32), ("py_count", ctypes.c_int32),
                 ("sx_start", ctypes.c_int32), ("sx_end", ctypes.c_int32),
-                ("sy_start", ctypes.c_int32), ("sy_end", ctypes.c_int32)]
+                ("sy_start", ctypes.c_int32), ("sy_end", ctypes.c_int32),
+                ("dx_camera", ctypes.c_float * 3), ("dy_camera", ctypes.c_float * 3), ("pad", ctypes.c_int32 * 2)]
 
 
 P = ctypes.c_void_p
@@ -56,7 +57,8 @@ class FlatScene(ctypes.Structure):
                 ("n_lights", I32), ("lights", P), ("n_light_shapes", I32), ("light_shapes", P),
                 ("n_spectra_floats", I32), ("spectra", P),
                 ("n_instances", I32), ("instances", P), ("prim_instance", P),
-                ("n_kdnodes", I32), ("kdnodes", P)]
+                ("n_kdnodes", I32), ("kdnodes", P),
+                ("n_textures", I32), ("textures", P), ("ewa_lut", P), ("rgb_basis", P)]
 
 
 class Overrides(ctypes.Structure):
@@ -72,7 +74,7 @@ class RenderDesc(ctypes.Structure):
 STAT_PATHS, STAT_KERNEL_MS, STAT_ACCUM_MS, STAT_ZEROED, STAT_SPILLS, STAT_PASSES = 0, 1, 2, 3, 4, 5
 F_ACCUMULATE, F_COUNT_WORK = 1, 2
 KEEP_SEED = 0xFFFFFFFF
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 
 class Timing(ctypes.Structure):
@@ -163,7 +165,8 @@ class Scene:
         host_lib().pbrthost_flat(self._h, ctypes.byref(self.flat))
 
     @staticmethod
-    def load(path, xres=-1, yres=-1, spp=-1, maxdepth=-1, bands=32, seed=None):
+    def load(path, xres=-1, yres=-1, spp=-1, maxdepth=-1, bands=0, seed=None):
+        """bands <= 0: the pack's own band count, or 32 (the reference build) for a .pbrt file."""
         h = P()
         err = ctypes.create_string_buffer(1024)
         ov = Overrides(xres, yres, spp, maxdepth, bands, KEEP_SEED if seed is None else seed)

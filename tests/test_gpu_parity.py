@@ -10,6 +10,8 @@ double-rounded transcendental lands within one double ulp of a float rounding bo
 import os
 
 import numpy as np
+
+from test_oracle_golden import exact_rate
 import pytest
 
 pytestmark = pytest.mark.gpu
@@ -100,12 +102,13 @@ def test_work_counters(pg, killeroo64, dev):
 def _golden_scene(pg, cfg, name="killeroo"):
     from conftest import PACKS
     w, h, spp, seed, md = [int(v) for v in cfg]
-    pack = {"anim": "anim-killeroos-moving.pack", "bunny": "bunny.pack"}.get(name.split("_")[0], "killeroo-simple.pack")
+    pack = {"anim": "anim-killeroos-moving.pack", "bunny": "bunny.pack", "metal": "metal.pack"}.get(name.split("_")[0],
+                                                                                              "killeroo-simple.pack")
     return pg.Scene.load(os.path.join(PACKS, pack), xres=w, yres=h, spp=spp, maxdepth=md, seed=seed)
 
 
 @pytest.mark.parametrize("name", ["killeroo_paths_64x64s4", "killeroo_paths_48x48s8_seed7_md7", "anim_paths_48x48s4",
-                                  "bunny_paths_64x36s4"])
+                                  "bunny_paths_64x36s4", "metal_paths_48x48s4"])
 def test_paths_vs_reference_golden(pg, name):
     """GPU against the reference harness's own per-path radiance (fixed seeds)."""
     from conftest import GOLDEN
@@ -119,12 +122,13 @@ def test_paths_vs_reference_golden(pg, name):
     rel = np.abs(L - ref).max(axis=1) / np.maximum(np.abs(ref).max(axis=1), 1e-30)
     # a path with many transcendental calls (measured BRDF: 2 atan2 + ~10 exp per lookup)
     # meets a last-ulp difference more often; the bounds that matter are the two below
-    assert same.mean() >= 0.97
+    assert same.mean() >= exact_rate(name)
     assert (rel > 1e-4).mean() <= 5e-4
     assert np.abs(L.sum(0) - ref.sum(0)).max() / np.abs(ref.sum(0)).max() < 1e-5
 
 
-@pytest.mark.parametrize("name", ["killeroo_film_96x72s16", "anim_film_40x40s8", "bunny_film_48x27s8"])
+@pytest.mark.parametrize("name", ["killeroo_film_96x72s16", "anim_film_40x40s8", "bunny_film_48x27s8",
+                                  "metal_film_40x40s8"])
 def test_film_vs_reference_golden(pg, name):
     """Whole-film render against the reference's film (raw sums, incl. neighbour-pixel
     samples): image L-inf relative error < 1e-4 (BASELINE.json north star)."""
@@ -139,9 +143,12 @@ def test_film_vs_reference_golden(pg, name):
     if name.startswith("killeroo"):
         assert st[pg.STAT_SPILLS] > 0
     assert np.abs(film - ref).max() / np.abs(ref).max() < 1e-4
-    # ~0.7% of paths differ from glibc-float transcendentals in the last ulp (DESIGN.md
-    # §3.2), so a 16-sample pixel is bit-exact with probability ~0.993^16
-    assert np.all(film.view(np.int32) == ref.view(np.int32), axis=2).mean() >= 0.85
+    # a fraction 1 - r of paths differs from glibc-float transcendentals in the last ulp
+    # (DESIGN.md §3.2), so an spp-sample pixel is bit-exact with probability ~r^spp
+    # (killeroo: r ~0.993, spp 16 -> 0.89; metal: r ~0.925, spp 8 -> 0.54)
+    spp = int(g["config"][2])
+    r = {"metal": 0.925}.get(name.split("_")[0], 0.993)
+    assert np.all(film.view(np.int32) == ref.view(np.int32), axis=2).mean() >= r ** spp - 0.05
 
 
 def test_tile_shards_compose_to_full_frame(pg, killeroo64, dev):
@@ -200,6 +207,25 @@ def test_measured_brdf_matches_oracle(pg):
     from conftest import PACKS
     scene = pg.Scene.load(os.path.join(PACKS, "bunny.pack"), xres=48, yres=27, spp=4)
     assert scene.flat.n_kdnodes > 0
+    keys = _keys(scene)
+    with pg.Device(0) as d:
+        d.upload(scene)
+        Lg = d.trace_paths(keys)
+        d.render()
+        film = d.film()
+    o = pg.oracle()
+    Lo = o.trace_paths(scene, keys)
+    assert np.all(Lg.view(np.int32) == Lo.view(np.int32), axis=1).mean() >= 1 - 1e-4
+    ref, _ = o.render(scene)
+    assert np.all(film.view(np.int32) == ref.view(np.int32), axis=2).mean() >= 0.999
+
+
+def test_metal_textures_environment_match_oracle(pg):
+    """C4 (60 bands): FresnelConductor metal, imagemap-textured substrate with a textured bump
+    (EWA lookups with camera ray differentials), infinite light -- GPU against the oracle."""
+    from conftest import PACKS
+    scene = pg.Scene.load(os.path.join(PACKS, "metal.pack"), xres=40, yres=40, spp=4)
+    assert scene.bands == 60
     keys = _keys(scene)
     with pg.Device(0) as d:
         d.upload(scene)

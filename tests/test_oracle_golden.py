@@ -17,11 +17,25 @@ from conftest import GOLDEN, PACKS
 
 def _scene(pg, cfg, name="killeroo"):
     w, h, spp, seed, md = [int(v) for v in cfg]
-    pack = {"anim": "anim-killeroos-moving.pack", "bunny": "bunny.pack"}.get(name.split("_")[0], "killeroo-simple.pack")
+    pack = {"anim": "anim-killeroos-moving.pack", "bunny": "bunny.pack", "metal": "metal.pack"}.get(name.split("_")[0],
+                                                                                              "killeroo-simple.pack")
     return pg.Scene.load(os.path.join(PACKS, pack), xres=w, yres=h, spp=spp, maxdepth=md, seed=seed)
 
 
-PATHS = ["killeroo_paths_64x64s4", "killeroo_paths_48x48s8_seed7_md7", "anim_paths_48x48s4", "bunny_paths_64x36s4"]
+# Fraction of paths expected bit-exact between the double-rounded transcendental definition
+# and glibc's float functions: glibc acosf/atan2f/sinf/cosf are not correctly rounded, so
+# a scene that calls them on every path (C4: the environment light's Le / Pdf / Sample_L)
+# meets last-ulp differences on ~8% of its paths (measured per function: acosf 3.2%,
+# atan2f 1.9%, sinf 1.4%, cosf 0.8%, powf 0.2%); the other scenes on < 1%
+EXACT_RATE = {"metal": 0.90}
+
+
+def exact_rate(name):
+    return EXACT_RATE.get(name.split("_")[0], 0.97)
+
+
+PATHS = ["killeroo_paths_64x64s4", "killeroo_paths_48x48s8_seed7_md7", "anim_paths_48x48s4", "bunny_paths_64x36s4",
+         "metal_paths_48x48s4"]
 
 
 @pytest.fixture(scope="module")
@@ -47,7 +61,7 @@ def test_paths_double_rounded_definition(pg, name):
     same = np.all(L.view(np.int32) == ref.view(np.int32), axis=1)
     # a path with many transcendental calls (measured BRDF: 2 atan2 + ~10 exp per lookup)
     # meets a last-ulp difference more often; the bounds that matter are the two below
-    assert same.mean() >= 0.97
+    assert same.mean() >= exact_rate(name)
     rel = np.abs(L - ref).max(axis=1) / np.maximum(np.abs(ref).max(axis=1), 1e-30)
     # a path whose sampled direction or roulette decision flips on a last-ulp difference
     # diverges entirely; such paths must stay rare (<= 1 in 2000) ...
@@ -57,7 +71,8 @@ def test_paths_double_rounded_definition(pg, name):
     assert tot < 1e-5
 
 
-@pytest.mark.parametrize("name", ["killeroo_film_96x72s16", "anim_film_40x40s8", "bunny_film_48x27s8"])
+@pytest.mark.parametrize("name", ["killeroo_film_96x72s16", "anim_film_40x40s8", "bunny_film_48x27s8",
+                                  "metal_film_40x40s8"])
 def test_film_bit_exact_vs_reference(pg, ora_libm, name):
     g = np.load(os.path.join(GOLDEN, name + ".npz"))
     scene = _scene(pg, g["config"], name)
@@ -76,8 +91,18 @@ def test_mt19937_known_answers(pg):
     assert int(o.mt_first(5489, 10000)[-1]) == 4123659995
 
 
-def test_host_fromrgb_bit_exact(pg):
-    g = np.load(os.path.join(GOLDEN, "fromrgb_32.npz"))
+@pytest.mark.parametrize("bands", [32, 60])
+def test_host_fromrgb_bit_exact(pg, bands):
+    g = np.load(os.path.join(GOLDEN, "fromrgb_%d.npz" % bands))
     for rgb, refl, illum in zip(g["rgb"], g["refl"], g["illum"]):
-        assert np.array_equal(pg.spectrum_from_rgb(rgb, 32).view(np.int32), refl.view(np.int32))
-        assert np.array_equal(pg.spectrum_from_rgb(rgb, 32, illuminant=True).view(np.int32), illum.view(np.int32))
+        assert np.array_equal(pg.spectrum_from_rgb(rgb, bands).view(np.int32), refl.view(np.int32))
+        assert np.array_equal(pg.spectrum_from_rgb(rgb, bands, illuminant=True).view(np.int32), illum.view(np.int32))
+
+
+def test_metal_scene_contents(pg):
+    """C4 pack: 60 bands, the Au metal, the textured substrate floor, the environment light."""
+    from conftest import PACKS
+    s = pg.Scene.load(os.path.join(PACKS, "metal.pack"), xres=16, yres=16, spp=1)
+    assert s.bands == 60 and s.flat.n_textures >= 3 and s.flat.n_lights == 1
+    import ctypes
+    assert ctypes.cast(s.flat.lights, ctypes.POINTER(ctypes.c_int32))[0] == 2   # PBRTGPU_LIGHT_INFINITE

@@ -16,7 +16,12 @@ Fixtures (numpy .npz, inputs + expected outputs only):
   mt19937_kat.npz                 first 64 outputs of RNG(seed) for 6 seeds
   fromrgb_32.npz                  SampledSpectrum::FromRGB (reflectance and illuminant) for 14
                                   RGB triples, 32 bands 395-715 nm
-Usage: python tools/make_golden.py   (after `make -C oracle ref`)
+  metal_paths_48x48s4.npz, metal_film_40x40s8.npz, fromrgb_60.npz   C4, 60-band build (b60
+                                  harness): Au metal (FresnelConductor from SPD files), substrate
+                                  floor with imagemap Kd + scaled imagemap bump (1x1 fallback
+                                  texels, EWA filtering with camera ray differentials), infinite
+                                  light (one-texel environment map)
+Usage: python tools/make_golden.py   (after `make -C oracle ref` and `make -C oracle ref60`)
 """
 import os
 import subprocess
@@ -27,12 +32,13 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HARNESS = os.path.join(ROOT, "oracle", "_ref", "b32", "pbrt_ref_harness")
+HARNESS60 = os.path.join(ROOT, "oracle", "_ref", "b60", "pbrt_ref_harness")   # make -C oracle ref60
 SCENES = "/root/reference/scenes"
 OUT = os.path.join(ROOT, "tests", "golden")
 
 
-def run(args):
-    subprocess.run([HARNESS] + args, check=True, cwd=SCENES)
+def run(args, bands=32):
+    subprocess.run([HARNESS60 if bands == 60 else HARNESS] + args, check=True, cwd=SCENES)
 
 
 def read_paths(fn):
@@ -42,20 +48,20 @@ def read_paths(fn):
     return rec[:, :3].copy(), rec[:, 3:].copy().view(np.float32), int(spp), int(seed)
 
 
-def paths_fixture(name, res, spp, seed, maxdepth, every, tmp, scene="killeroo-simple.pbrt"):
+def paths_fixture(name, res, spp, seed, maxdepth, every, tmp, scene="killeroo-simple.pbrt", bands=32):
     fn = os.path.join(tmp, name + ".bin")
     run([os.path.join(SCENES, scene), "--res", str(res[0]), str(res[1]), "--spp", str(spp), "--seed", str(seed), "--maxdepth",
-         str(maxdepth), "--paths", fn, "--path-every", str(every)])
+         str(maxdepth), "--paths", fn, "--path-every", str(every)], bands)
     keys, L, _, _ = read_paths(fn)
     np.savez_compressed(os.path.join(OUT, name + ".npz"), keys=keys, L=L,
                         config=np.array([res[0], res[1], spp, seed, maxdepth], np.int32))
     print(name, keys.shape)
 
 
-def film_fixture(name, res, spp, seed, maxdepth, tmp, scene="killeroo-simple.pbrt"):
+def film_fixture(name, res, spp, seed, maxdepth, tmp, scene="killeroo-simple.pbrt", bands=32):
     fn = os.path.join(tmp, name + ".f32")
     run([os.path.join(SCENES, scene), "--res", str(res[0]), str(res[1]), "--spp", str(spp), "--seed", str(seed), "--maxdepth",
-         str(maxdepth), "--raw", fn])
+         str(maxdepth), "--raw", fn], bands)
     raw = np.fromfile(fn, dtype=np.int32)
     W, H, N = raw[:3]
     film = raw[3:].view(np.float32).reshape(H, W, N)
@@ -76,6 +82,16 @@ def main():
         film_fixture("anim_film_40x40s8", (40, 40), 8, 0, 5, tmp, scene="anim-killeroos-moving.pbrt")
         paths_fixture("bunny_paths_64x36s4", (64, 36), 4, 0, 5, 3, tmp, scene="bunny.pbrt")
         film_fixture("bunny_film_48x27s8", (48, 27), 8, 0, 5, tmp, scene="bunny.pbrt")
+        if os.path.exists(HARNESS60):
+            paths_fixture("metal_paths_48x48s4", (48, 48), 4, 0, 5, 2, tmp, scene="metal.pbrt", bands=60)
+            film_fixture("metal_film_40x40s8", (40, 40), 8, 0, 5, tmp, scene="metal.pbrt", bands=60)
+            fn = os.path.join(tmp, "spec60.bin")
+            run(["-", "--spectra", fn], 60)
+            raw = np.fromfile(fn, dtype=np.int32)
+            n = raw[0]
+            rec = raw[1:].reshape(n, 3 + 60 + 60).view(np.float32)
+            np.savez_compressed(os.path.join(OUT, "fromrgb_60.npz"), rgb=rec[:, :3].copy(), refl=rec[:, 3:63].copy(),
+                                illum=rec[:, 63:].copy())
         fn = os.path.join(tmp, "mt.bin")
         run(["-", "--kat-mt", fn])
         raw = np.fromfile(fn, dtype=np.uint32).reshape(6, 65)

@@ -18,6 +18,7 @@ PACKS = [
     ("killeroo-simple", "killeroo-simple.pbrt", 32, 700, 700, 256),
     ("anim-killeroos-moving", "anim-killeroos-moving.pbrt", 32, 600, 600, 512),
     ("bunny", "bunny.pbrt", 32, 1920, 1080, 1024),
+    ("metal", "metal.pbrt", 60, 400, 400, 4096),
 ]
 
 
