@@ -244,6 +244,10 @@ struct DevScene {
     int nInf;                         // infinite lights among lights[]
 };
 
+// scene features a shade kernel is specialised for (k_shade<NB, FEAT>): a scene without
+// them runs a variant with that code compiled out
+enum { FEAT_MEAS = 1, FEAT_TEX = 2, FEAT_INF = 4, FEAT_ALL = 7 };
+
 struct DG { V p, nn, dpdu, dpdv, dndu, dndv; float u, v; };
 PGD_INLINE void dg_init(DG &dg, V p, V dpdu, V dpdv, V dndu, V dndv, float u, float v, int flip) {
     dg.p = p; dg.dpdu = dpdu; dg.dpdv = dpdv; dg.dndu = dndu; dg.dndv = dndv;
@@ -1275,6 +1279,7 @@ PGD_HEAVY void compute_differentials(const DG &dg, const RayDiff &rd, float out[
 // diff: dudx, dvdx, dudy, dvdy of the hit (zero without ray differentials); the material's
 // textured spectrum, if any, is written clamped into the slot's K bands (kb[q * c]) and its
 // BxDF refers to it with offset -1
+template <int FEAT>
 PGD_HEAVY void get_bsdf(const DevScene &S, const Isect &is, const float diff[4], float4 *kb, size_t c, BSDF &bs,
                         V *pOut, V *nOut) {
     const pbrtgpu_prim pr = S.prims[is.prim];
@@ -1301,7 +1306,7 @@ PGD_HEAVY void get_bsdf(const DevScene &S, const Isect &is, const float diff[4],
     TexPt tq;
     tq.u = dgs.u; tq.v = dgs.v; tq.dudx = diff[0]; tq.dvdx = diff[1]; tq.dudy = diff[2]; tq.dvdy = diff[3];
     V bdpdu, bdpdv;
-    if (mt.bump_tex < 0) {
+    if (!(FEAT & FEAT_TEX) || mt.bump_tex < 0) {
         float d = mt.f[7];
         const float du = .01f, dv = .01f;   // (d - d) / du == +0 for every positive du
         bdpdu = vadd(vadd(dgs.dpdu, vmul(dgs.nn, (d - d) / du)), vmul(dgs.dndu, d));
@@ -1335,10 +1340,12 @@ PGD_HEAVY void get_bsdf(const DevScene &S, const Isect &is, const float diff[4],
 #pragma unroll
     for (int k = 0; k < 4; ++k) off[k] = mt.spec[k];
     int ts = -1;
+    if (FEAT & FEAT_TEX) {
 #pragma unroll
-    for (int k = 0; k < 4; ++k)
-        if (mt.tex[k] >= 0) ts = k;
-    if (ts >= 0) {
+        for (int k = 0; k < 4; ++k)
+            if (mt.tex[k] >= 0) ts = k;
+    }
+    if ((FEAT & FEAT_TEX) && ts >= 0) {
         SpecTex st = tex_spec_prepare(S, mt.tex[ts], tq);
         bool black = true;
         const int nq = S.nbp / 4;
@@ -1521,10 +1528,11 @@ PGD_HEAVY Emit inf_Le(const pbrtgpu_light &L, V d) {
     return inf_radiance(L, spherical_phi(wh) * kInvTwoPi, spherical_theta(wh) * kInvPi);
 }
 // Light::Sample_L (diffuse.cpp:61-74, point.cpp:42-49, infinite.cpp:155-185)
+template <int FEAT>
 PGD_HEAVY void light_sample_L(const DevScene &S, const pbrtgpu_light &L, V p, float pEps, const float u[3], V *wi,
                               float *pdf, Seg *vis, Emit *em) {
     em->mode = EM_BLACK; em->off = L.spec; em->div = 1.f; em->point = false;
-    if (L.type == PBRTGPU_LIGHT_INFINITE) {
+    if ((FEAT & FEAT_INF) && L.type == PBRTGPU_LIGHT_INFINITE) {
         // Distribution2D::SampleContinuous of one texel returns (u0, u1) with pdf map_pdf
         float uv0 = u[0], uv1 = u[1], mapPdf = L.map_pdf;
         if (mapPdf == 0.f) { *pdf = 0.f; return; }
@@ -1571,9 +1579,10 @@ PGD_HEAVY void light_sample_L(const DevScene &S, const pbrtgpu_light &L, V p, fl
     vis->o = p; vis->d = vdiv(vsub(ps, p), dist); vis->mint = pEps; vis->maxt = dist * (1.f - 1e-3f);
     if (vdot(ns, vneg(*wi)) > 0.f && !L.is_black) em->mode = EM_POOL;   // DiffuseAreaLight::L
 }
+template <int FEAT>
 PGD_HEAVY float light_pdf(const DevScene &S, const pbrtgpu_light &L, V p, V wi) {
     if (L.type == PBRTGPU_LIGHT_POINT) return 0.;
-    if (L.type == PBRTGPU_LIGHT_INFINITE) {   // infinite.cpp:188-197; Distribution2D::Pdf of one texel
+    if ((FEAT & FEAT_INF) && L.type == PBRTGPU_LIGHT_INFINITE) {   // infinite.cpp:188-197; Distribution2D::Pdf of one texel
         V w = xvec(L.l2w_minv, wi);
         float sintheta = SINF(spherical_theta(w));
         if (sintheta == 0.f) return 0.f;

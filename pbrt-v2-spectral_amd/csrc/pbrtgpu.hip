@@ -120,7 +120,7 @@ __device__ __forceinline__ uint32_t block_push(bool flag, uint32_t *counter, uin
 
 // shading pass over every slot: finish / advance live paths, regenerate free slots, and
 // queue the next pass's rays into queue set qout (block-aggregated queue pushes)
-template <int NB>
+template <int NB, int FEAT>
 __global__ __launch_bounds__(kShadeBlock) void k_shade(DevScene S, PathSoA P, ItemSrc src, int qout,
                                                        float *__restrict__ Lout) {
     __shared__ uint32_t lds4[16];
@@ -131,7 +131,7 @@ __global__ __launch_bounds__(kShadeBlock) void k_shade(DevScene S, PathSoA P, It
     bool zeroed = false;
     if (inRange && !freeSlot) {
         bool done;
-        pu = shade_slot<NB>(S, P, slot, Lout, &done, &zeroed);
+        pu = shade_slot<NB, FEAT>(S, P, slot, Lout, &done, &zeroed);
         if (done) { P.item[slot] = -1; freeSlot = true; }
     }
     if (__ballot(zeroed)) {
@@ -257,6 +257,7 @@ struct pbrtgpu_ctx {
     bool hasScene = false;
     DevScene S{};
     int nb = 0, spp = 0, stackDepth = 0;
+    int feat = 0;   // FEAT_* of the uploaded scene: selects the k_shade variant
     pbrtgpu_camera cam{};
     std::vector<DevBuf> sceneBufs;
     DevBuf film, Lbuf, pix, filmIdx, mask, keys, counter, spillL, lists[4], scratch[3];
@@ -329,7 +330,10 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
     int q = 0;
     // pass 0: every slot is free -> regeneration fills them with camera rays (queue 0)
     HIPCHK(hipEventRecord(c->ev[4], c->stream));
-    hipLaunchKernelGGL(k_shade<NB>, dim3(shadeGrid), dim3(kShadeBlock), 0, c->stream, c->S, P, src, q, Lout);
+    // scenes without measured BRDFs, textures and environment lights run the variant with
+    // that code compiled out (fewer registers, no kd-tree stack)
+    auto kShade = c->feat ? k_shade<NB, FEAT_ALL> : k_shade<NB, 0>;
+    hipLaunchKernelGGL(kShade, dim3(shadeGrid), dim3(kShadeBlock), 0, c->stream, c->S, P, src, q, Lout);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(c->ev[5], c->stream));
     bool pending = false;   // events ev[0..3] of the previous pass still to be read
@@ -379,7 +383,7 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
             T.launches[K_SHADOW]++;
         }
         HIPCHK(hipEventRecord(c->ev[2], c->stream));
-        hipLaunchKernelGGL(k_shade<NB>, dim3(shadeGrid), dim3(kShadeBlock), 0, c->stream, c->S, P, src, nq, Lout);
+        hipLaunchKernelGGL(kShade, dim3(shadeGrid), dim3(kShadeBlock), 0, c->stream, c->S, P, src, nq, Lout);
         HIPCHK(hipGetLastError());
         T.launches[K_SHADE]++;
         HIPCHK(hipEventRecord(c->ev[3], c->stream));
@@ -626,6 +630,14 @@ int pbrtgpu_scene_upload(pbrtgpu_ctx *c, const pbrtgpu_flat_scene *s) {
                 return fail(PBRTGPU_E_INVALID, "measured material kd-tree range");
         HIPCHK(upload(c, kd.data(), kd.size(), &S.kd));
     }
+    c->feat = S.nInf > 0 ? FEAT_INF : 0;
+    for (int i = 0; i < s->n_materials; ++i) {
+        const pbrtgpu_material &m = s->materials[i];
+        if (m.type == PBRTGPU_MAT_MEASURED) c->feat |= FEAT_MEAS;
+        if (m.bump_tex >= 0 || m.tex[0] >= 0 || m.tex[1] >= 0 || m.tex[2] >= 0 || m.tex[3] >= 0) c->feat |= FEAT_TEX;
+    }
+    if (const char *e = getenv("PBRTGPU_SHADE_FULL"))   // tests: run the full variant on any scene
+        if (atoi(e) != 0) c->feat = FEAT_ALL;
     c->nb = s->n_bands;
     c->spp = s->spp;
     c->cam = s->camera;

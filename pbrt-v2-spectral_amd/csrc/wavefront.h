@@ -138,23 +138,30 @@ PGD_INLINE float4 spec4(const float *sp, int off, int q, const float4 *kb, size_
     return off >= 0 ? ld4(sp + off + 4 * q) : kb[q * c];
 }
 // BSDF value of four bands (quad q): mb = measured scratch, kb = texture scratch of the slot
+template <int FEAT>
 PGD_INLINE float4 fval4(const float *sp, const FVal &F, int q, const float4 *mb, const float4 *kb, size_t c) {
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
     if (F.mode == FV_SPEC) {
-        float4 r = spec4(sp, F.R, q, kb, c);
+        float4 r = (FEAT & FEAT_TEX) ? spec4(sp, F.R, q, kb, c) : ld4(sp + F.R + 4 * q);
         return make_float4((1.f * r.x) / F.d, (1.f * r.y) / F.d, (1.f * r.z) / F.d, (1.f * r.w) / F.d);
     }
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
         if (k < F.n) {
             const FTerm &t = F.t[k];
-            if (t.kind == T_BUF) {
+            if ((FEAT & FEAT_MEAS) && t.kind == T_BUF) {
                 float4 m = mb[q * c];
                 v.x += m.x; v.y += m.y; v.z += m.z; v.w += m.w;
                 continue;
             }
-            float4 r = spec4(sp, t.R, q, kb, c);
-            float4 r2 = (t.kind == T_FB || t.kind == T_BLINNC) ? spec4(sp, t.R2, q, kb, c) : r;
+            float4 r, r2;
+            if (FEAT & FEAT_TEX) {
+                r = spec4(sp, t.R, q, kb, c);
+                r2 = (t.kind == T_FB || t.kind == T_BLINNC) ? spec4(sp, t.R2, q, kb, c) : r;
+            } else {
+                r = ld4(sp + t.R + 4 * q);
+                r2 = (t.kind == T_FB || t.kind == T_BLINNC) ? ld4(sp + t.R2 + 4 * q) : r;
+            }
             v.x += term_val(t, r.x, r2.x);
             v.y += term_val(t, r.y, r2.y);
             v.z += term_val(t, r.z, r2.z);
@@ -164,21 +171,22 @@ PGD_INLINE float4 fval4(const float *sp, const FVal &F, int q, const float4 *mb,
     return v;
 }
 // band quad q of an emitted radiance (Emit, device.h)
+template <int FEAT>
 PGD_INLINE float4 emit4(const DevScene &S, const Emit &e, int q) {
-    if (e.mode == EM_RGB) return from_rgb4(S, e.pick, true, q);
+    if ((FEAT & FEAT_INF) && e.mode == EM_RGB) return from_rgb4(S, e.pick, true, q);
     if (e.mode == EM_BLACK) return make_float4(0.f, 0.f, 0.f, 0.f);
     float4 v = ld4(S.spectra + e.off + 4 * q);
     if (e.point) v = make_float4(v.x / e.div, v.y / e.div, v.z / e.div, v.w / e.div);
     return v;
 }
-template <int NB>
+template <int NB, int FEAT>
 PGD_INLINE bool emit_black(const DevScene &S, const Emit &e) {
     if (e.mode == EM_BLACK) return true;
     if (e.mode == EM_POOL && !e.point) return false;   // area lights: is_black folded into the mode
     bool black = true;
 #pragma unroll
     for (int q = 0; q < Bands<NB>::NQ; ++q) {
-        float4 v = emit4(S, e, q);
+        float4 v = emit4<FEAT>(S, e, q);
 #pragma unroll
         for (int k = 0; k < 4; ++k)
             if (4 * q + k < NB) black = black && (cmp(v, k) == 0.);
@@ -254,9 +262,9 @@ PGD_INLINE void measured_lookup(const DevScene &S, const FTerm &t, float4 *mb, s
     }
 }
 // materialise a measured term of F into the slot's M bands (T_MEAS -> T_BUF)
-template <int NB>
+template <int NB, int FEAT>
 PGD_INLINE void fval_prepare(const DevScene &S, FVal &F, float4 *mb, size_t c) {
-    if (F.mode != FV_SUM) return;
+    if (!(FEAT & FEAT_MEAS) || F.mode != FV_SUM) return;
 #pragma unroll
     for (int k = 0; k < 2; ++k)
         if (k < F.n && F.t[k].kind == T_MEAS) {
@@ -345,7 +353,7 @@ struct Pushes { bool c, m, s; };
 // continuation ray `ray` hit primitive `prim` at `thit`.  L is the path's radiance (in
 // registers); beta_b is P.beta[vb & 1] in HBM.  BSDF values are evaluated lazily per band
 // quad (fval4).  Updates fl.
-template <int NB>
+template <int NB, int FEAT>
 PGD_INLINE Pushes shade_vertex(const DevScene &S, const PathSoA &P, int slot, int vb, const Ray &ray, int prim,
                                float thit, uint32_t &fl, float4 (&L)[Bands<NB>::NQ]) {
     constexpr int NQ = Bands<NB>::NQ;
@@ -377,7 +385,7 @@ PGD_INLINE Pushes shade_vertex(const DevScene &S, const PathSoA &P, int slot, in
     // only the camera ray carries differentials (path.cpp:107 drops them); they matter only
     // to textured materials
     float diff[4] = {0.f, 0.f, 0.f, 0.f};
-    if (vb == 0) {
+    if ((FEAT & FEAT_TEX) && vb == 0) {
         const pbrtgpu_material &mt = S.mats[S.prims[is.prim].material];
         if (mt.bump_tex >= 0 || mt.tex[0] >= 0 || mt.tex[1] >= 0 || mt.tex[2] >= 0 || mt.tex[3] >= 0) {
             const uint32_t pxy = P.pix[slot];
@@ -393,7 +401,7 @@ PGD_INLINE Pushes shade_vertex(const DevScene &S, const PathSoA &P, int slot, in
     float4 *kb = P.K + slot;
     BSDF bs;
     V p, n;
-    get_bsdf(S, is, diff, kb, c, bs, &p, &n);
+    get_bsdf<FEAT>(S, is, diff, kb, c, bs, &p, &n);
     const V wo = vneg(ray.d);
     MT rng;
     const bool useMT = vb >= 3;
@@ -429,10 +437,10 @@ PGD_INLINE Pushes shade_vertex(const DevScene &S, const PathSoA &P, int slot, in
         float lightPdf, bsdfPdf;
         Seg vis;
         Emit em;
-        light_sample_L(S, Lt, p, is.rayEps, ul, &wi, &lightPdf, &vis, &em);
-        if (lightPdf > 0. && !emit_black<NB>(S, em)) {
+        light_sample_L<FEAT>(S, Lt, p, is.rayEps, ul, &wi, &lightPdf, &vis, &em);
+        if (lightPdf > 0. && !emit_black<NB, FEAT>(S, em)) {
             bsdf_f(bs, wo, wi, flags, F);
-            fval_prepare<NB>(S, F, mb, c);
+            fval_prepare<NB, FEAT>(S, F, mb, c);
             float sc;
             if (em.point) sc = fabsf(vdot(wi, n)) / lightPdf;
             else {
@@ -445,7 +453,7 @@ PGD_INLINE Pushes shade_vertex(const DevScene &S, const PathSoA &P, int slot, in
             bool black = true;
 #pragma unroll
             for (int q = 0; q < NQ; ++q) {
-                float4 f = fval4(sp, F, q, mb, kb, c), e = emit4(S, em, q), a;
+                float4 f = fval4<FEAT>(sp, F, q, mb, kb, c), e = emit4<FEAT>(S, em, q), a;
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
                     cmp(a, k) = (cmp(f, k) * cmp(e, k)) * sc;
@@ -467,27 +475,27 @@ PGD_INLINE Pushes shade_vertex(const DevScene &S, const PathSoA &P, int slot, in
             int sampledType;
             bsdf_sample_f(bs, wo, &wi, ub[0], ub[1], ub[2], &bsdfPdf, flags, &sampledType, F);
             if (bsdfPdf > 0. && !(F.mode == FV_SUM && F.n == 0)) {
-                fval_prepare<NB>(S, F, mb, c);
+                fval_prepare<NB, FEAT>(S, F, mb, c);
                 float weight = 1.f;
                 bool go = true;
                 if (!(sampledType & BSDF_SPECULAR)) {
-                    lightPdf = light_pdf(S, Lt, p, wi);
+                    lightPdf = light_pdf<FEAT>(S, Lt, p, wi);
                     if (lightPdf == 0.) go = false;
                     else weight = power_heuristic(bsdfPdf, lightPdf);
                 }
                 Emit eb;
-                if (Lt.type == PBRTGPU_LIGHT_INFINITE) {
+                if ((FEAT & FEAT_INF) && Lt.type == PBRTGPU_LIGHT_INFINITE) {
                     if (go) eb = inf_Le(Lt, wi);
                 } else {
                     eb.mode = Lt.is_black ? EM_BLACK : EM_POOL; eb.off = Lt.spec; eb.div = 1.f; eb.point = false;
                 }
-                if (go && !emit_black<NB>(S, eb)) {
+                if (go && !emit_black<NB, FEAT>(S, eb)) {
                     const float ad = fabsf(vdot(wi, n));
                     float4 *B = P.B + slot;
                     bool black = true;
 #pragma unroll
                     for (int q = 0; q < NQ; ++q) {
-                        float4 f = fval4(sp, F, q, mb, kb, c), e = emit4(S, eb, q), b;
+                        float4 f = fval4<FEAT>(sp, F, q, mb, kb, c), e = emit4<FEAT>(S, eb, q), b;
 #pragma unroll
                         for (int k = 0; k < 4; ++k) {
                             cmp(b, k) = (((cmp(f, k) * cmp(e, k)) * ad) * weight) / bsdfPdf;
@@ -537,14 +545,14 @@ PGD_INLINE Pushes shade_vertex(const DevScene &S, const PathSoA &P, int slot, in
     bsdf_sample_f(bs, wo, &wi, up[0], up[1], up[2], &pdf, BSDF_ALL, &sflags, F);
     bool cont = pdf != 0. && !(F.mode == FV_SUM && F.n == 0);
     if (cont) {
-        fval_prepare<NB>(S, F, mb, c);
+        fval_prepare<NB, FEAT>(S, F, mb, c);
         const float ad = fabsf(vdot(wi, n));
         float4 *bn = P.beta + (size_t)((vb + 1) & 1) * NQ * c + slot;
         float4 nb4[NQ];
         bool black = true;
 #pragma unroll
         for (int q = 0; q < NQ; ++q) {
-            float4 f = fval4(sp, F, q, mb, kb, c), b = beta[q * c];
+            float4 f = fval4<FEAT>(sp, F, q, mb, kb, c), b = beta[q * c];
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 cmp(nb4[q], k) = cmp(b, k) * ((cmp(f, k) * ad) / pdf);
@@ -588,7 +596,7 @@ PGD_INLINE Pushes shade_vertex(const DevScene &S, const PathSoA &P, int slot, in
 
 // k_shade body for one slot: finish pending direct light, process the next vertex.
 // Returns the ray requests; *done when the path has produced its radiance.
-template <int NB>
+template <int NB, int FEAT>
 PGD_INLINE Pushes shade_slot(const DevScene &S, const PathSoA &P, int slot, float *__restrict__ Lout, bool *done,
                              bool *zeroed) {
     constexpr int NQ = Bands<NB>::NQ;
@@ -605,7 +613,7 @@ PGD_INLINE Pushes shade_slot(const DevScene &S, const PathSoA &P, int slot, floa
         if (fl & PF_PB) {
             const int ln = (int)(fl >> PF_LIGHT_SHIFT);
             int mp = P.hitPrim[c + slot];
-            if (S.lights[ln].type == PBRTGPU_LIGHT_INFINITE) useB = mp < 0;   // Li = light->Le(ray)
+            if ((FEAT & FEAT_INF) && S.lights[ln].type == PBRTGPU_LIGHT_INFINITE) useB = mp < 0;   // Li = light->Le(ray)
             else if (mp >= 0 && S.prims[mp].area_light == ln) {
                 Ray mr = ray_load(P, RAY_M, slot);
                 Isect lis;
@@ -638,14 +646,14 @@ PGD_INLINE Pushes shade_slot(const DevScene &S, const PathSoA &P, int slot, floa
             if (vb == 0) {
                 // SamplerRenderer::Li (samplerrenderer.cpp:237-240): Li = sum of the lights' Le,
                 // zero for area and point lights
-                if (S.nInf > 0) {
+                if ((FEAT & FEAT_INF) && S.nInf > 0) {
                     const Ray ray = ray_load(P, RAY_C, slot);
                     for (int l = 0; l < S.nLights; ++l)
                         if (S.lights[l].type == PBRTGPU_LIGHT_INFINITE) {
                             const Emit e = inf_Le(S.lights[l], ray.d);
 #pragma unroll
                             for (int q = 0; q < NQ; ++q) {
-                                float4 v = emit4(S, e, q);
+                                float4 v = emit4<FEAT>(S, e, q);
                                 L[q].x += v.x; L[q].y += v.y; L[q].z += v.z; L[q].w += v.w;
                             }
                         }
@@ -654,21 +662,21 @@ PGD_INLINE Pushes shade_slot(const DevScene &S, const PathSoA &P, int slot, floa
                 // path.cpp:92-96: L += beta * Le(ray) for every light
                 const float4 *beta = P.beta + (size_t)(vb & 1) * NQ * c + slot;
                 V d = v3(0.f, 0.f, 0.f);
-                if (S.nInf > 0) d = ray_load(P, RAY_C, slot).d;
+                if ((FEAT & FEAT_INF) && S.nInf > 0) d = ray_load(P, RAY_C, slot).d;
                 for (int l = 0; l < S.nLights; ++l) {
                     Emit e;
                     e.mode = EM_BLACK;
-                    if (S.lights[l].type == PBRTGPU_LIGHT_INFINITE) e = inf_Le(S.lights[l], d);
+                    if ((FEAT & FEAT_INF) && S.lights[l].type == PBRTGPU_LIGHT_INFINITE) e = inf_Le(S.lights[l], d);
 #pragma unroll
                     for (int q = 0; q < NQ; ++q) {
-                        float4 bt = beta[q * c], v = emit4(S, e, q);
+                        float4 bt = beta[q * c], v = emit4<FEAT>(S, e, q);
                         L[q].x += bt.x * v.x; L[q].y += bt.y * v.y; L[q].z += bt.z * v.z; L[q].w += bt.w * v.w;
                     }
                 }
             }
         } else {
             Ray ray = ray_load(P, RAY_C, slot);
-            out = shade_vertex<NB>(S, P, slot, vb, ray, prim, P.hitT[slot], fl, L);
+            out = shade_vertex<NB, FEAT>(S, P, slot, vb, ray, prim, P.hitT[slot], fl, L);
             P.bounce[slot] = vb;
         }
     }

@@ -237,3 +237,18 @@ def test_metal_textures_environment_match_oracle(pg):
     assert np.all(Lg.view(np.int32) == Lo.view(np.int32), axis=1).mean() >= 1 - 1e-4
     ref, _ = o.render(scene)
     assert np.all(film.view(np.int32) == ref.view(np.int32), axis=2).mean() >= 0.999
+
+
+def test_shade_variants_agree(pg, killeroo64, monkeypatch):
+    """The feature-specialised shade kernel (no measured BRDF / textures / environment light)
+    and the full kernel give the same film bit for bit on a scene both can render."""
+    with pg.Device(0) as d:
+        d.upload(killeroo64)
+        d.render()
+        lean = d.film()
+    monkeypatch.setenv("PBRTGPU_SHADE_FULL", "1")
+    with pg.Device(0) as d:
+        d.upload(killeroo64)
+        d.render()
+        full = d.film()
+    assert np.array_equal(lean.view(np.int32), full.view(np.int32))
