@@ -713,7 +713,7 @@ static void isect_fill(const Ctx *c, const Ray *ray, const Hit *h, Isect *is) {
 enum { BSDF_REFLECTION = 1, BSDF_TRANSMISSION = 2, BSDF_DIFFUSE = 4, BSDF_GLOSSY = 8, BSDF_SPECULAR = 16,
        BSDF_ALL = 31 };
 enum { BX_LAMBERT, BX_OREN, BX_MICRO_BLINN_DIEL, BX_SPEC_REFL_NOOP, BX_FRESNEL_BLEND_ANISO, BX_MEASURED_IRREG,
-       BX_MICRO_BLINN_COND };
+       BX_MICRO_BLINN_COND, BX_SPEC_REFL_DIEL, BX_SPEC_TRANS };   /* eta_t = index of refraction for the last two */
 typedef struct {
     int kind, type;
     const float *R;      /* reflectance spectrum */
@@ -949,6 +949,8 @@ static void bx_f_add(const Ctx *c, const BxDF *b, V wo, V wi, float *out) {
             break;
         }
         case BX_SPEC_REFL_NOOP:
+        case BX_SPEC_REFL_DIEL:
+        case BX_SPEC_TRANS:
             for (int i = 0; i < nb; ++i) out[i] += 0.f;
             break;
         case BX_FRESNEL_BLEND_ANISO: {   /* FresnelBlend::f (reflection.cpp:224-236) */
@@ -976,7 +978,9 @@ static float bx_pdf(const BxDF *b, V wo, V wi) {
         case BX_MICRO_BLINN_COND:
             if (!samehemi(wo, wi)) return 0.f;
             return blinn_pdf(b->a, wo, wi);
-        case BX_SPEC_REFL_NOOP: return 0.;
+        case BX_SPEC_REFL_NOOP:
+        case BX_SPEC_REFL_DIEL:
+        case BX_SPEC_TRANS: return 0.;
         case BX_FRESNEL_BLEND_ANISO:
             if (!samehemi(wo, wi)) return 0.f;
             return .5f * (abscos(wi) * INV_PI_F + aniso_pdf(b->a, b->b, wo, wi));
@@ -999,6 +1003,30 @@ static void bx_sample_f(const Ctx *c, const BxDF *b, V wo, V *wi, float u1, floa
             *pdf = 1.f;
             float d = abscos(*wi);
             for (int i = 0; i < nb; ++i) fout[i] = (1.f * b->R[i]) / d;
+            return;
+        }
+        case BX_SPEC_REFL_DIEL: {   /* SpecularReflection::Sample_f (reflection.cpp:130-136), FresnelDielectric(1, ior) */
+            *wi = v3(-wo.x, -wo.y, wo.z);
+            *pdf = 1.f;
+            float F = fr_dielectric(costh(wo), 1.f, b->eta_t), d = abscos(*wi);
+            for (int i = 0; i < nb; ++i) fout[i] = (F * b->R[i]) / d;
+            return;
+        }
+        case BX_SPEC_TRANS: {   /* SpecularTransmission::Sample_f (reflection.cpp:139-162) */
+            int entering = costh(wo) > 0.;
+            float ei = 1.f, et = b->eta_t;
+            if (!entering) { float t = ei; ei = et; et = t; }
+            float sini2 = sin2(wo);
+            float eta = ei / et;
+            float sint2 = eta * eta * sini2;
+            if (sint2 >= 1.) return;
+            float cost = sqrtf(fmaxf_(0.f, 1.f - sint2));
+            if (entering) cost = -cost;
+            float sintOverSini = eta;
+            *wi = v3(sintOverSini * -wo.x, sintOverSini * -wo.y, cost);
+            *pdf = 1.f;
+            float F = fr_dielectric(costh(wo), 1.f, b->eta_t), d = abscos(*wi);
+            for (int i = 0; i < nb; ++i) fout[i] = ((1.f - F) * b->R[i]) / d;
             return;
         }
         case BX_FRESNEL_BLEND_ANISO:
@@ -1339,6 +1367,17 @@ static void get_bsdf(const Ctx *c, const Isect *is, const float diff[4], BSDF *b
             if (!black[0]) {
                 BxDF *x = &bs->bx[bs->n++];
                 x->kind = BX_SPEC_REFL_NOOP; x->type = BSDF_REFLECTION | BSDF_SPECULAR; x->R = K[0];
+            }
+            break;
+        }
+        case PBRTGPU_MAT_GLASS: {   /* glass.cpp:34-57 */
+            if (!black[0]) {
+                BxDF *x = &bs->bx[bs->n++];
+                x->kind = BX_SPEC_REFL_DIEL; x->type = BSDF_REFLECTION | BSDF_SPECULAR; x->R = K[0]; x->eta_t = mt->f[0];
+            }
+            if (!black[1]) {
+                BxDF *x = &bs->bx[bs->n++];
+                x->kind = BX_SPEC_TRANS; x->type = BSDF_TRANSMISSION | BSDF_SPECULAR; x->R = K[1]; x->eta_t = mt->f[0];
             }
             break;
         }

@@ -774,7 +774,7 @@ PGD_HEAVY void isect_fill(const DevScene &S, const Ray &ray, int prim, float t, 
 // ------------------------------------------------------------------ BSDF
 enum { BSDF_REFLECTION = 1, BSDF_TRANSMISSION = 2, BSDF_DIFFUSE = 4, BSDF_GLOSSY = 8, BSDF_SPECULAR = 16, BSDF_ALL = 31 };
 enum { BX_LAMBERT, BX_OREN, BX_MICRO_BLINN_DIEL, BX_SPEC_REFL_NOOP, BX_FRESNEL_BLEND_ANISO, BX_MEASURED_IRREG,
-       BX_MICRO_BLINN_COND };
+       BX_MICRO_BLINN_COND, BX_SPEC_REFL_DIEL, BX_SPEC_TRANS };   // a = index of refraction for the last two
 // R, R2: offsets into DevScene::spectra, or -1 for the per-slot textured spectrum (K bands)
 struct BxDF { int kind, type; int R, R2; float a, b; };
 struct BSDF { V nn, ng, sn, tn; int n; BxDF bx[2]; };
@@ -884,7 +884,8 @@ PGD_INLINE void aniso_sample(float ex, float ey, V wo, V *wi, float u1, float u2
 enum { T_ZERO = 0, T_LAMB, T_OREN, T_BLINN, T_FB, T_MEAS, T_BUF, T_BLINNC };
 struct FTerm { int kind; int R, R2; float s0, s1, s2, s3; };
 enum { FV_SUM = 0, FV_SPEC = 1 };
-struct FVal { int mode, n; FTerm t[2]; float d; int R; };   // FV_SUM with n == 0: zero spectrum
+// FV_SPEC: a specular BxDF's sampled value (fs * R_i) / d (reflection.cpp:130-162)
+struct FVal { int mode, n; FTerm t[2]; float d, fs; int R; };   // FV_SUM with n == 0: zero spectrum
 
 PGD_INLINE void fval_zero(FVal &F) { F.mode = FV_SUM; F.n = 0; }
 PGD_INLINE void fval_push(FVal &F, const FTerm &t) {   // static indices only (no scratch)
@@ -968,7 +969,9 @@ PGD_INLINE float bx_pdf(const BxDF &b, V wo, V wi) {
     switch (b.kind) {
         case BX_MICRO_BLINN_DIEL:
         case BX_MICRO_BLINN_COND: if (!samehemi(wo, wi)) return 0.f; return blinn_pdf(b.a, wo, wi);
-        case BX_SPEC_REFL_NOOP: return 0.;
+        case BX_SPEC_REFL_NOOP:
+        case BX_SPEC_REFL_DIEL:
+        case BX_SPEC_TRANS: return 0.;
         case BX_FRESNEL_BLEND_ANISO:
             if (!samehemi(wo, wi)) return 0.f;
             return .5f * (abscos(wi) * kInvPi + aniso_pdf(b.a, b.b, wo, wi));
@@ -985,11 +988,30 @@ PGD_INLINE void bx_sample_f(const BxDF &b, V wo, V *wi, float u1, float u2, floa
             if (!samehemi(wo, *wi)) return;
             F.n = 1; F.t[0] = bx_term(b, wo, *wi);
             return;
-        case BX_SPEC_REFL_NOOP:
+        case BX_SPEC_REFL_NOOP:    // SpecularReflection with FresnelNoOp: Spectrum(1) * R / |cos|
+        case BX_SPEC_REFL_DIEL:    // ... with FresnelDielectric(1, ior)
             *wi = v3(-wo.x, -wo.y, wo.z);
             *pdf = 1.f;
             F.mode = FV_SPEC; F.R = b.R; F.d = abscos(*wi);
+            F.fs = b.kind == BX_SPEC_REFL_NOOP ? 1.f : fr_dielectric(wo.z, 1.f, b.a);
             return;
+        case BX_SPEC_TRANS: {      // SpecularTransmission(T, 1, ior): (Spectrum(1) - F) * T / |cos|
+            const bool entering = wo.z > 0.;
+            float ei = 1.f, et = b.a;
+            if (!entering) { float t = ei; ei = et; et = t; }
+            const float sini2 = sin2(wo);
+            const float eta = ei / et;
+            const float sint2 = eta * eta * sini2;
+            if (sint2 >= 1.) return;   // total internal reflection: pdf stays 0
+            float cost = sqrtf(pmax(0.f, 1.f - sint2));
+            if (entering) cost = -cost;
+            const float sintOverSini = eta;
+            *wi = v3(sintOverSini * -wo.x, sintOverSini * -wo.y, cost);
+            *pdf = 1.f;
+            F.mode = FV_SPEC; F.R = b.R; F.d = abscos(*wi);
+            F.fs = 1.f - fr_dielectric(wo.z, 1.f, b.a);
+            return;
+        }
         case BX_FRESNEL_BLEND_ANISO:
             if (u1 < .5) {
                 u1 = 2.f * u1;
@@ -1336,7 +1358,7 @@ PGD_HEAVY void get_bsdf(const DevScene &S, const Isect &is, const float diff[4],
     *nOut = nn;
     // material spectra: constant offsets, or the textured slot materialised in K
     int off[4];
-    bool black0 = (mt.black_mask & 1) != 0;
+    bool black0 = (mt.black_mask & 1) != 0, black1 = (mt.black_mask & 2) != 0;
 #pragma unroll
     for (int k = 0; k < 4; ++k) off[k] = mt.spec[k];
     int ts = -1;
@@ -1361,6 +1383,7 @@ PGD_HEAVY void get_bsdf(const DevScene &S, const Isect &is, const float diff[4],
         for (int k = 0; k < 4; ++k)
             if (k == ts) off[k] = -1;   // static indices only (no scratch)
         if (ts == 0) black0 = black;
+        if (ts == 1) black1 = black;
     }
     switch (mt.type) {
         case PBRTGPU_MAT_MATTE: {
@@ -1403,6 +1426,19 @@ PGD_HEAVY void get_bsdf(const DevScene &S, const Isect &is, const float diff[4],
                 BxDF &x = bs.bx[bs.n++];
                 x.kind = BX_SPEC_REFL_NOOP; x.type = BSDF_REFLECTION | BSDF_SPECULAR; x.R = off[0]; x.R2 = x.R;
                 x.a = x.b = 0.f;
+            }
+            break;
+        }
+        case PBRTGPU_MAT_GLASS: {   // glass.cpp:34-57: each specular lobe if its spectrum is not black
+            if (!black0) {
+                BxDF &x = bs.bx[bs.n++];
+                x.kind = BX_SPEC_REFL_DIEL; x.type = BSDF_REFLECTION | BSDF_SPECULAR; x.R = off[0]; x.R2 = x.R;
+                x.a = mt.f[0]; x.b = 0.f;
+            }
+            if (!black1) {
+                BxDF &x = bs.bx[bs.n++];
+                x.kind = BX_SPEC_TRANS; x.type = BSDF_TRANSMISSION | BSDF_SPECULAR; x.R = off[1]; x.R2 = x.R;
+                x.a = mt.f[0]; x.b = 0.f;
             }
             break;
         }

@@ -477,7 +477,7 @@ int pbrtgpu_scene_upload(pbrtgpu_ctx *c, const pbrtgpu_flat_scene *s) {
     };
     for (int i = 0; i < s->n_materials; ++i) {
         const pbrtgpu_material &m = s->materials[i];
-        if (m.type < PBRTGPU_MAT_MATTE || m.type > PBRTGPU_MAT_MEASURED || m.type == PBRTGPU_MAT_GLASS)
+        if (m.type < PBRTGPU_MAT_MATTE || m.type > PBRTGPU_MAT_MEASURED)
             return fail(PBRTGPU_E_UNSUPPORTED, "material type not yet supported on the GPU");
         int nt = 0;
         for (int k = 0; k < 4; ++k)

@@ -143,7 +143,7 @@ PGD_INLINE float4 fval4(const float *sp, const FVal &F, int q, const float4 *mb,
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
     if (F.mode == FV_SPEC) {
         float4 r = (FEAT & FEAT_TEX) ? spec4(sp, F.R, q, kb, c) : ld4(sp + F.R + 4 * q);
-        return make_float4((1.f * r.x) / F.d, (1.f * r.y) / F.d, (1.f * r.z) / F.d, (1.f * r.w) / F.d);
+        return make_float4((F.fs * r.x) / F.d, (F.fs * r.y) / F.d, (F.fs * r.z) / F.d, (F.fs * r.w) / F.d);
     }
 #pragma unroll
     for (int k = 0; k < 2; ++k) {

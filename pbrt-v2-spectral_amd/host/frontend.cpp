@@ -948,6 +948,11 @@ private:
             SpecSlot(*mo, 1, g, m, "Ks", spec.Const(.5f), true);
             mt.f[0] = ConstFloatTex(g, m, "uroughness", .1f);
             mt.f[1] = ConstFloatTex(g, m, "vroughness", .1f);
+        } else if (name == "glass") {   // glass.cpp:34-68
+            mt.type = PBRTGPU_MAT_GLASS;
+            SpecSlot(*mo, 0, g, m, "Kr", spec.Const(1.f), true);
+            SpecSlot(*mo, 1, g, m, "Kt", spec.Const(1.f), true);
+            mt.f[0] = ConstFloatTex(g, m, "index", 1.5f);
         } else if (name == "metal") {   // metal.cpp:44-62, 99-110 (eta, k unclamped)
             mt.type = PBRTGPU_MAT_METAL;
             SpecSlot(*mo, 0, g, m, "eta", CopperSpectrum(false), false);

@@ -102,13 +102,15 @@ def test_work_counters(pg, killeroo64, dev):
 def _golden_scene(pg, cfg, name="killeroo"):
     from conftest import PACKS
     w, h, spp, seed, md = [int(v) for v in cfg]
-    pack = {"anim": "anim-killeroos-moving.pack", "bunny": "bunny.pack", "metal": "metal.pack"}.get(name.split("_")[0],
+    pack = {"anim": "anim-killeroos-moving.pack", "bunny": "bunny.pack", "metal": "metal.pack",
+            "coverage": "coverage.pack"}.get(name.split("_")[0],
                                                                                               "killeroo-simple.pack")
     return pg.Scene.load(os.path.join(PACKS, pack), xres=w, yres=h, spp=spp, maxdepth=md, seed=seed)
 
 
 @pytest.mark.parametrize("name", ["killeroo_paths_64x64s4", "killeroo_paths_48x48s8_seed7_md7", "anim_paths_48x48s4",
-                                  "bunny_paths_64x36s4", "metal_paths_48x48s4"])
+                                  "bunny_paths_64x36s4", "metal_paths_48x48s4",
+                                  "coverage_paths_64x48s8"])
 def test_paths_vs_reference_golden(pg, name):
     """GPU against the reference harness's own per-path radiance (fixed seeds)."""
     from conftest import GOLDEN
@@ -128,7 +130,7 @@ def test_paths_vs_reference_golden(pg, name):
 
 
 @pytest.mark.parametrize("name", ["killeroo_film_96x72s16", "anim_film_40x40s8", "bunny_film_48x27s8",
-                                  "metal_film_40x40s8"])
+                                  "metal_film_40x40s8", "coverage_film_64x48s8"])
 def test_film_vs_reference_golden(pg, name):
     """Whole-film render against the reference's film (raw sums, incl. neighbour-pixel
     samples): image L-inf relative error < 1e-4 (BASELINE.json north star)."""
@@ -147,7 +149,7 @@ def test_film_vs_reference_golden(pg, name):
     # (DESIGN.md §3.2), so an spp-sample pixel is bit-exact with probability ~r^spp
     # (killeroo: r ~0.993, spp 16 -> 0.89; metal: r ~0.925, spp 8 -> 0.54)
     spp = int(g["config"][2])
-    r = {"metal": 0.925}.get(name.split("_")[0], 0.993)
+    r = {"metal": 0.925, "coverage": 0.955}.get(name.split("_")[0], 0.993)
     assert np.all(film.view(np.int32) == ref.view(np.int32), axis=2).mean() >= r ** spp - 0.05
 
 
@@ -252,3 +254,21 @@ def test_shade_variants_agree(pg, killeroo64, monkeypatch):
         d.render()
         full = d.film()
     assert np.array_equal(lean.view(np.int32), full.view(np.int32))
+
+
+def test_coverage_scene_matches_oracle(pg):
+    """tests/scenes/coverage.pbrt: glass, mirror, Oren-Nayar, copper with textured bump,
+    textures, three light types -- GPU against the oracle path by path and film."""
+    from conftest import PACKS
+    scene = pg.Scene.load(os.path.join(PACKS, "coverage.pack"))
+    keys = _keys(scene)
+    with pg.Device(0) as d:
+        d.upload(scene)
+        Lg = d.trace_paths(keys)
+        d.render()
+        film = d.film()
+    o = pg.oracle()
+    Lo = o.trace_paths(scene, keys)
+    assert np.all(Lg.view(np.int32) == Lo.view(np.int32), axis=1).mean() >= 1 - 1e-4
+    ref, _ = o.render(scene)
+    assert np.all(film.view(np.int32) == ref.view(np.int32), axis=2).mean() >= 0.999

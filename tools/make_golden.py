@@ -16,6 +16,10 @@ Fixtures (numpy .npz, inputs + expected outputs only):
   mt19937_kat.npz                 first 64 outputs of RNG(seed) for 6 seeds
   fromrgb_32.npz                  SampledSpectrum::FromRGB (reflectance and illuminant) for 14
                                   RGB triples, 32 bands 395-715 nm
+  coverage_paths_64x48s8.npz, coverage_film_64x48s8.npz   tests/scenes/coverage.pbrt (this
+                                  repository's feature-coverage scene): glass, mirror, Oren-Nayar,
+                                  copper metal with textured bump, scaled/trilinear/black-wrap
+                                  textures, disk + point + environment lights, maxdepth 6
   metal_paths_48x48s4.npz, metal_film_40x40s8.npz, fromrgb_60.npz   C4, 60-band build (b60
                                   harness): Au metal (FresnelConductor from SPD files), substrate
                                   floor with imagemap Kd + scaled imagemap bump (1x1 fallback
@@ -82,6 +86,9 @@ def main():
         film_fixture("anim_film_40x40s8", (40, 40), 8, 0, 5, tmp, scene="anim-killeroos-moving.pbrt")
         paths_fixture("bunny_paths_64x36s4", (64, 36), 4, 0, 5, 3, tmp, scene="bunny.pbrt")
         film_fixture("bunny_film_48x27s8", (48, 27), 8, 0, 5, tmp, scene="bunny.pbrt")
+        cov = os.path.join(ROOT, "tests", "scenes", "coverage.pbrt")
+        paths_fixture("coverage_paths_64x48s8", (64, 48), 8, 0, 6, 2, tmp, scene=cov)
+        film_fixture("coverage_film_64x48s8", (64, 48), 8, 0, 6, tmp, scene=cov)
         if os.path.exists(HARNESS60):
             paths_fixture("metal_paths_48x48s4", (48, 48), 4, 0, 5, 2, tmp, scene="metal.pbrt", bands=60)
             film_fixture("metal_film_40x40s8", (40, 40), 8, 0, 5, tmp, scene="metal.pbrt", bands=60)

@@ -19,6 +19,7 @@ PACKS = [
     ("anim-killeroos-moving", "anim-killeroos-moving.pbrt", 32, 600, 600, 512),
     ("bunny", "bunny.pbrt", 32, 1920, 1080, 1024),
     ("metal", "metal.pbrt", 60, 400, 400, 4096),
+    ("coverage", os.path.join(ROOT, "tests", "scenes", "coverage.pbrt"), 32, 64, 48, 8),
 ]
 
 
@@ -26,7 +27,8 @@ def main():
     out = os.path.join(ROOT, "scenes")
     os.makedirs(out, exist_ok=True)
     for name, fn, bands, xr, yr, spp in PACKS:
-        s = pg.Scene.load(os.path.join(REF, fn), xres=xr, yres=yr, spp=spp, maxdepth=5, bands=bands)
+        s = pg.Scene.load(os.path.join(REF, fn), xres=xr, yres=yr, spp=spp, maxdepth=-1 if name == "coverage" else 5,
+                          bands=bands)
         path = os.path.join(out, name + ".pack")
         s.save_pack(path)
         print(name, s.info(), os.path.getsize(path))
