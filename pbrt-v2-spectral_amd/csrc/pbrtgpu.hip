@@ -120,8 +120,11 @@ __device__ __forceinline__ uint32_t block_push(bool flag, uint32_t *counter, uin
 
 // shading pass over every slot: finish / advance live paths, regenerate free slots, and
 // queue the next pass's rays into queue set qout (block-aggregated queue pushes)
+#ifndef PGD_SHADE_ATTR
+#define PGD_SHADE_ATTR
+#endif
 template <int NB, int FEAT>
-__global__ __launch_bounds__(kShadeBlock) void k_shade(DevScene S, PathSoA P, ItemSrc src, int qout,
+__global__ __launch_bounds__(kShadeBlock) PGD_SHADE_ATTR void k_shade(DevScene S, PathSoA P, ItemSrc src, int qout,
                                                        float *__restrict__ Lout) {
     __shared__ uint32_t lds4[16];
     const int slot = blockIdx.x * blockDim.x + threadIdx.x;
