@@ -34,16 +34,23 @@ static constexpr float kInvTwoPi = 0.15915494309189533577f;
 static constexpr float kOneMinusEps = 0x1.fffffep-1f;
 
 // transcendentals: the parity definition of DESIGN.md §3.2, (float) f((double) x) with the
-// double algorithms of include/pbrt_fmath.h (shared with the CPU oracle; inline, no calls)
+// double algorithms of include/pbrt_fmath.h (shared with the CPU oracle).  On the GPU each
+// one is a single out-of-line copy: inlined at every call site they grew the shade kernel's
+// code and register budget (shade 379 -> 361 ms/frame on C2 when outlined, r01f ablation)
+#ifdef PGD_TRANS_INLINE
+#define PGD_TFN PGD_INLINE
+#else
+#define PGD_TFN __device__ __attribute__((noinline))
+#endif
 #ifndef PGD_EXPERIMENT_FASTMATH
-PGD_INLINE float SINF(float x) { return (float)pbrt_fm_sin((double)x); }
-PGD_INLINE float COSF(float x) { return (float)pbrt_fm_cos((double)x); }
-PGD_INLINE float POWF(float x, float y) { return (float)pbrt_fm_pow((double)x, (double)y); }
-PGD_INLINE float ACOSF(float x) { return (float)pbrt_fm_acos((double)x); }
-PGD_INLINE float ATAN2F(float y, float x) { return (float)pbrt_fm_atan2((double)y, (double)x); }
-PGD_INLINE float TANF(float x) { return (float)pbrt_fm_tan((double)x); }
-PGD_INLINE float ATANF(float x) { return (float)pbrt_fm_atan((double)x); }
-PGD_INLINE float LOGF(float x) { return (float)pbrt_fm_log_any((double)x); }
+PGD_TFN float SINF(float x) { return (float)pbrt_fm_sin((double)x); }
+PGD_TFN float COSF(float x) { return (float)pbrt_fm_cos((double)x); }
+PGD_TFN float POWF(float x, float y) { return (float)pbrt_fm_pow((double)x, (double)y); }
+PGD_TFN float ACOSF(float x) { return (float)pbrt_fm_acos((double)x); }
+PGD_TFN float ATAN2F(float y, float x) { return (float)pbrt_fm_atan2((double)y, (double)x); }
+PGD_TFN float TANF(float x) { return (float)pbrt_fm_tan((double)x); }
+PGD_TFN float ATANF(float x) { return (float)pbrt_fm_atan((double)x); }
+PGD_TFN float LOGF(float x) { return (float)pbrt_fm_log_any((double)x); }
 #else
 PGD_INLINE float LOGF(float x) { return __logf(x); }   // timing experiment only (not the parity definition): float library functions
 PGD_INLINE float SINF(float x) { return __sinf(x); }
@@ -519,17 +526,28 @@ struct Stack {
     PGD_INLINE uint32_t get(int i) const { return base[i * stride]; }
 };
 // quadric hit test kept out of line: its double-precision transcendentals would otherwise
-// set the register budget of every traversal loop
-__device__ __attribute__((noinline)) bool quadric_hit(const DevScene &S, int type, int idx, const Ray &ray, float *t) {
-    float e;
-    if (type == PBRTGPU_SHAPE_SPHERE) return sphere_intersect(S.quads[idx], ray, t, &e, nullptr);
-    return disk_intersect(S.quads[idx], ray, t, &e, nullptr);
+// set the register budget of every traversal loop.  Scalars in, t out (-inf: miss), so
+// the call passes everything in VGPRs and the traversal kernels need no private memory.
+__device__ __attribute__((noinline)) float quadric_hit(const pbrtgpu_quadric *quads, int type, int idx, float ox,
+                                                       float oy, float oz, float dx, float dy, float dz, float mint,
+                                                       float maxt, float time) {
+    Ray ray;
+    ray.o = v3(ox, oy, oz); ray.d = v3(dx, dy, dz); ray.mint = mint; ray.maxt = maxt; ray.time = time;
+    float t, e;
+    const bool hit = type == PBRTGPU_SHAPE_SPHERE ? sphere_intersect(quads[idx], ray, &t, &e, nullptr)
+                                                  : disk_intersect(quads[idx], ray, &t, &e, nullptr);
+    return hit ? t : -INFINITY;   // a hit has t >= mint >= 0 (or NaN)
+}
+PGD_INLINE bool quadric_test(const DevScene &S, int type, int idx, const Ray &r, float *t) {
+    const float th = quadric_hit(S.quads, type, idx, r.o.x, r.o.y, r.o.z, r.d.x, r.d.y, r.d.z, r.mint, r.maxt, r.time);
+    *t = th;
+    return th != -INFINITY;
 }
 PGD_INLINE bool prim_hit(const DevScene &S, Stack &st, int pi, const Ray &ray, float *t) {
     const pbrtgpu_prim pr = S.prims[pi];
     if (pr.shape_type == PBRTGPU_SHAPE_TRIANGLE) { st.cTris++; return tri_hit(S.primTri[pi], ray, t); }
     st.cQuads++;
-    return quadric_hit(S, pr.shape_type, pr.shape_index, ray, t);
+    return quadric_test(S, pr.shape_type, pr.shape_index, ray, t);
 }
 // ---- Matrix4x4 / Quaternion / AnimatedTransform (transform.cpp, quaternion.cpp) for
 // TransformedPrimitive instances
@@ -672,7 +690,7 @@ PGD_INLINE bool prim_test(const DevScene &S, Stack &st, int base, int pi, Ray &r
         if (!tri_hit(S.primTri[pi], ray, &t)) return false;
     } else if (!INST || pr.shape_type != PBRTGPU_SHAPE_INSTANCE) {
         st.cQuads++;
-        if (!quadric_hit(S, pr.shape_type, pr.shape_index, ray, &t)) return false;
+        if (!quadric_test(S, pr.shape_type, pr.shape_index, ray, &t)) return false;
     } else {
         if constexpr (INST) {
             const pbrtgpu_instance &I = S.insts[pr.shape_index];
