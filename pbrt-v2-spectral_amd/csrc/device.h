@@ -162,15 +162,18 @@ struct MT {
 };
 PGD_INLINE uint32_t mt_next_word(uint32_t prev, uint32_t idx) { return 1812433253U * (prev ^ (prev >> 30)) + idx; }
 PGD_INLINE void mt_begin(MT &r, uint32_t seed) { r.seed = seed; r.init = false; r.k = 0; }
-PGD_INLINE uint32_t mt_uint(MT &r) {
-    if (!r.init) {
-        r.a = r.seed;
-        r.b = mt_next_word(r.a, 1);
-        uint32_t w = r.b;
-        for (uint32_t i = 2; i <= 397; ++i) w = mt_next_word(w, i);
-        r.m = w;
-        r.init = true;
-    }
+// the seed recurrence up to mt[397]: once per path, before its first draw (one copy; a
+// fully unrolled 396-step loop at every draw site would dominate the shade kernel's code)
+__device__ __attribute__((noinline)) void mt_init(MT &r) {
+    r.a = r.seed;
+    r.b = mt_next_word(r.a, 1);
+    uint32_t w = r.b;
+#pragma unroll 4
+    for (uint32_t i = 2; i <= 397; ++i) w = mt_next_word(w, i);
+    r.m = w;
+    r.init = true;
+}
+PGD_INLINE uint32_t mt_uint(MT &r) {   // requires r.init (mt_init)
     uint32_t y = (r.a & 0x80000000U) | (r.b & 0x7fffffffU);
     y = r.m ^ (y >> 1) ^ ((y & 1U) ? 0x9908b0dfU : 0U);
     // advance the recurrence windows
@@ -228,7 +231,9 @@ struct DevScene {
     float yint;
     const float *bandY;
     pbrtgpu_camera cam;
-    const float4 *nodes;              // 2 x float4 per node
+    const float4 *nodes;              // 2 x float4 per node (the flattened scene's BVH; roots are tested here)
+    const float4 *wnodes;             // child-in-parent BVH: 4 x float4 per interior node (wide_bvh)
+    const uint32_t *nodeRef;          // per node: its wide-node index, or a leaf reference (WREF_*)
     const pbrtgpu_prim *prims;
     const DevTri *primTri;            // per prim (triangles only meaningful)
     const pbrtgpu_triangle *tris;
@@ -413,18 +418,26 @@ PGD_INLINE bool sphere_intersect(const pbrtgpu_quadric &q, const Ray &r, float *
     if (t0 > ray.maxt || t1 < ray.mint) return false;
     float thit = t0;
     if (t0 < ray.mint) { thit = t1; if (thit > ray.maxt) return false; }
+    // phi <= 2.f * kPi always (atan2 in [-pi, pi], + 2pi in float), so with phi_max >= that
+    // bound the phi test cannot fail and a hit-only query (no dg) skips the atan2
+    const bool needPhi = dg || !(q.phi_max >= 2.f * kPi);
     phit = rayat(ray, thit);
     if (phit.x == 0.f && phit.y == 0.f) phit.x = 1e-5f * q.radius;
-    phi = ATAN2F(phit.y, phit.x);
-    if (phi < 0.) phi += 2.f * kPi;
+    phi = 0.f;
+    if (needPhi) {
+        phi = ATAN2F(phit.y, phit.x);
+        if (phi < 0.) phi += 2.f * kPi;
+    }
     if ((q.zmin > -q.radius && phit.z < q.zmin) || (q.zmax < q.radius && phit.z > q.zmax) || phi > q.phi_max) {
         if (thit == t1) return false;
         if (t1 > ray.maxt) return false;
         thit = t1;
         phit = rayat(ray, thit);
         if (phit.x == 0.f && phit.y == 0.f) phit.x = 1e-5f * q.radius;
-        phi = ATAN2F(phit.y, phit.x);
-        if (phi < 0.) phi += 2.f * kPi;
+        if (needPhi) {
+            phi = ATAN2F(phit.y, phit.x);
+            if (phi < 0.) phi += 2.f * kPi;
+        }
         if ((q.zmin > -q.radius && phit.z < q.zmin) || (q.zmax < q.radius && phit.z > q.zmax) || phi > q.phi_max)
             return false;
     }
@@ -461,6 +474,8 @@ PGD_INLINE bool disk_intersect(const pbrtgpu_quadric &q, const Ray &r, float *tH
     V phit = rayat(ray, thit);
     float dist2 = phit.x * phit.x + phit.y * phit.y;
     if (dist2 > q.radius * q.radius || dist2 < q.inner_radius * q.inner_radius) return false;
+    // phi <= (float)(2pi) always: with phi_max >= that bound a hit-only query skips the atan2
+    if (!dg && q.phi_max >= 2.f * kPi) { *tHit = thit; return true; }
     float phi = ATAN2F(phit.y, phit.x);
     if (phi < 0) phi = (float)((double)phi + 2. * (double)kPi);
     if (phi > q.phi_max) return false;
@@ -499,6 +514,9 @@ PGD_HEAVY bool shape_intersect(const DevScene &S, int type, int idx, const Ray &
 }
 
 // ------------------------------------------------------------------ BVH traversal
+// child references in the child-in-parent BVH: an interior child is its wide-node index,
+// a leaf is WREF_LEAF | nPrims << 24 | first primitive
+enum : uint32_t { WREF_LEAF = 0x80000000u, WREF_NP_SHIFT = 24, WREF_NP_MASK = 0x7fu, WREF_OFF_MASK = 0xffffffu };
 // slab test (bvh.cpp:118-140); node = {bmin.xyz, bmax.x} {bmax.yz, offset, meta}
 PGD_INLINE bool bbox_hit(float4 n0, float4 n1, const Ray &ray, V invDir, const int neg[3]) {
     float bminx = n0.x, bminy = n0.y, bminz = n0.z, bmaxx = n0.w, bmaxy = n1.x, bmaxz = n1.y;
@@ -516,14 +534,37 @@ PGD_INLINE bool bbox_hit(float4 n0, float4 n1, const Ray &ray, V invDir, const i
     if (tzmax < tmax) tmax = tzmax;
     return (tmin < ray.maxt) && (tmax > ray.mint);
 }
+// the same slab test with its parts split for a child box tested at its parent: returns
+// whether the maxt-independent part passes (the slab intervals overlap and tmax > mint) and
+// the entry distance tmin; the box is hit for a ray extent [mint, maxt] iff that holds and
+// tmin < maxt, exactly as bbox_hit decides it
+PGD_INLINE bool slab_enter(float4 lo, float4 hi, const Ray &ray, V invDir, const int neg[3], float *tEnter) {
+    float tmin = ((neg[0] ? hi.x : lo.x) - ray.o.x) * invDir.x;
+    float tmax = ((neg[0] ? lo.x : hi.x) - ray.o.x) * invDir.x;
+    float tymin = ((neg[1] ? hi.y : lo.y) - ray.o.y) * invDir.y;
+    float tymax = ((neg[1] ? lo.y : hi.y) - ray.o.y) * invDir.y;
+    if ((tmin > tymax) || (tymin > tmax)) return false;
+    if (tymin > tmin) tmin = tymin;
+    if (tymax < tmax) tmax = tymax;
+    float tzmin = ((neg[2] ? hi.z : lo.z) - ray.o.z) * invDir.z;
+    float tzmax = ((neg[2] ? lo.z : hi.z) - ray.o.z) * invDir.z;
+    if ((tmin > tzmax) || (tzmin > tmax)) return false;
+    if (tzmin > tmin) tmin = tzmin;
+    if (tzmax < tmax) tmax = tzmax;
+    *tEnter = tmin;
+    return tmax > ray.mint;
+}
 // LDS stack: column per lane
 struct Stack {
-    uint32_t *base;   // &lds[lane]
+    uint32_t *base;   // &lds[lane]: child refs
+    float *tbase;     // &lds[depth * stride + lane]: entry distance of each pushed child (closest-hit only)
     int stride;       // threads per block
     // work counters; only the stats kernel reads them, elsewhere they are dead and removed
     uint32_t cRays = 0, cNodes = 0, cTris = 0, cQuads = 0, cHits = 0, cShadow = 0;
     PGD_INLINE void set(int i, uint32_t v) { base[i * stride] = v; }
     PGD_INLINE uint32_t get(int i) const { return base[i * stride]; }
+    PGD_INLINE void setT(int i, float v) { tbase[i * stride] = v; }
+    PGD_INLINE float getT(int i) const { return tbase[i * stride]; }
 };
 // quadric hit test kept out of line: its double-precision transcendentals would otherwise
 // set the register budget of every traversal loop.  Scalars in, t out (-inf: miss), so
@@ -709,39 +750,66 @@ PGD_INLINE bool prim_test(const DevScene &S, Stack &st, int base, int pi, Ray &r
     return true;
 }
 
+// The walk runs on the child-in-parent copy of the BVH (DevScene::wnodes): one 64-byte
+// record per interior node holds both children's boxes, so a visit tests both children
+// at once.  Visiting order and culling are the reference's: the children are taken in its
+// dirIsNeg[axis] order, a near child whose box passes is entered at once (bvh.cpp:417-425
+// visits it next with the same maxt), and a pushed far child carries its entry distance,
+// re-checked against the then-current maxt when popped -- the slab test's only
+// maxt-dependent part (bbox_hit == slab_enter && tmin < maxt).  So the primitives tested,
+// and their order, are identical to BVHAccel::Intersect / IntersectP.
 template <bool ANY, bool INST>
 PGD_INLINE bool bvh_walk(const DevScene &S, Stack &st, int base, uint32_t root, Ray &ray, int *hitPrim, float *hitT) {
     V invDir = v3(1.f / ray.d.x, 1.f / ray.d.y, 1.f / ray.d.z);
     int neg[3] = {invDir.x < 0, invDir.y < 0, invDir.z < 0};
-    int todo = base;
-    uint32_t nodeNum = root;
-    bool found = false;
     if (ANY) st.cShadow += INST ? 1u : 0u; else st.cRays += INST ? 1u : 0u;
-    for (;;) {
-        float4 n0 = S.nodes[2 * nodeNum], n1 = S.nodes[2 * nodeNum + 1];
+    {
+        const float4 n0 = S.nodes[2 * root], n1 = S.nodes[2 * root + 1];
         st.cNodes++;
-        if (bbox_hit(n0, n1, ray, invDir, neg)) {
-            uint32_t off = __float_as_uint(n1.z), meta = __float_as_uint(n1.w);
-            uint32_t np = meta & 0xff;
-            if (np > 0) {
-                for (uint32_t i = 0; i < np; ++i)
-                    if (prim_test<ANY, INST>(S, st, todo, (int)(off + i), ray, hitPrim, hitT)) {
-                        if (ANY) return true;
-                        found = true;
-                    }
-                if (todo == base) break;
-                nodeNum = st.get(--todo);
-            } else {
-                uint32_t axis = (meta >> 8) & 0xff;
-                if (neg[axis]) { st.set(todo++, nodeNum + 1); nodeNum = off; }
-                else { st.set(todo++, off); nodeNum = nodeNum + 1; }
-            }
+        if (!bbox_hit(n0, n1, ray, invDir, neg)) return false;
+    }
+    int todo = base;
+    uint32_t ref = S.nodeRef[root];
+    bool found = false;
+    for (;;) {
+        if (ref & WREF_LEAF) {
+            const uint32_t np = (ref >> WREF_NP_SHIFT) & WREF_NP_MASK, off = ref & WREF_OFF_MASK;
+            for (uint32_t i = 0; i < np; ++i)
+                if (prim_test<ANY, INST>(S, st, todo, (int)(off + i), ray, hitPrim, hitT)) {
+                    if (ANY) return true;
+                    found = true;
+                }
         } else {
-            if (todo == base) break;
-            nodeNum = st.get(--todo);
+            const float4 *w = S.wnodes + 4 * (size_t)ref;
+            const float4 l0 = w[0], l1 = w[1], r0 = w[2], r1 = w[3];
+            st.cNodes++;
+            float tl = 0.f, tr = 0.f;
+            const bool hl = slab_enter(l0, l1, ray, invDir, neg, &tl) && tl < ray.maxt;
+            const bool hr = slab_enter(r0, r1, ray, invDir, neg, &tr) && tr < ray.maxt;
+            const uint32_t refL = __float_as_uint(l0.w), refR = __float_as_uint(l1.w);
+            // bvh.cpp:420-425: dirIsNeg[axis] -> second child first
+            const bool swap = neg[__float_as_uint(r0.w)] != 0;
+            const bool hn = swap ? hr : hl, hf = swap ? hl : hr;
+            const uint32_t rn = swap ? refR : refL, rf = swap ? refL : refR;
+            if (hn) {
+                if (hf) {
+                    st.set(todo, rf);
+                    if (!ANY) st.setT(todo, swap ? tl : tr);
+                    ++todo;
+                }
+                ref = rn;
+                continue;
+            }
+            if (hf) { ref = rf; continue; }
+        }
+        // pop the next far child whose box is still entered before maxt
+        for (;;) {
+            if (todo == base) return found;
+            --todo;
+            ref = st.get(todo);
+            if (ANY || st.getT(todo) < ray.maxt) break;
         }
     }
-    return found;
 }
 template <bool INST = true>
 PGD_INLINE bool bvh_intersect(const DevScene &S, Stack &st, Ray &ray, int *hitPrim, float *hitT) {

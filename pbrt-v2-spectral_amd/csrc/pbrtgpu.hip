@@ -39,7 +39,7 @@ static int fail(int code, const std::string &msg) { g_err = msg; return code; }
 
 // ------------------------------------------------------------------ kernels
 static const int kTraceBlock = 128;
-static const int kShadeBlock = 256;
+static const int kStackLDS = 16;   // k_trace_pt: traversal-stack entries per lane kept in LDS (power of two)
 
 // closest-hit queries of one pass (BVHAccel::Intersect, bvh.cpp:380-432): persistent grid,
 // one ray per lane per iteration, LDS traversal stack (column per lane)
@@ -48,6 +48,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_closest(DevScene S, PathS
     extern __shared__ uint32_t lds[];
     Stack st;
     st.base = lds + threadIdx.x;
+    st.tbase = reinterpret_cast<float *>(lds + (size_t)S.stackDepth * blockDim.x) + threadIdx.x;
     st.stride = blockDim.x;
     const uint32_t n = P.cnt[CNT_QC(q)];
     const uint32_t *Q = P.qC + (size_t)q * 2 * P.cap;
@@ -81,6 +82,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_shadow(DevScene S, PathSo
     extern __shared__ uint32_t lds[];
     Stack st;
     st.base = lds + threadIdx.x;
+    st.tbase = reinterpret_cast<float *>(lds + (size_t)S.stackDepth * blockDim.x) + threadIdx.x;
     st.stride = blockDim.x;
     const uint32_t n = P.cnt[CNT_QS(q)];
     const uint32_t *Q = P.qS + (size_t)q * P.cap;
@@ -98,61 +100,158 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_shadow(DevScene S, PathSo
     }
 }
 
-// Block-wide exclusive prefix of a per-thread flag with ONE atomicAdd per block on
-// *counter; returns this thread's index (valid where flag is set).  All threads of the
-// block must call it (it contains barriers).
-__device__ __forceinline__ uint32_t block_push(bool flag, uint32_t *counter, uint32_t *lds4) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const unsigned long long m = __ballot(flag);
-    const uint32_t before = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-    if (lane == 0) lds4[wave] = (uint32_t)__popcll(m);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t tot = 0;
-        for (int w = 0; w < (int)(blockDim.x >> 6); ++w) { uint32_t v = lds4[w]; lds4[w] = tot; tot += v; }
-        lds4[15] = tot ? atomicAdd(counter, tot) : 0u;
+// Ray queries of one pass without instanced primitives (BVHAccel::Intersect / IntersectP,
+// bvh.cpp:380-481, on the child-in-parent BVH of bvh_walk): persistent waves, each owning a
+// contiguous range of the queue, with per-lane ray replacement -- a lane whose ray has
+// finished takes the next ray of the wave's range once `refill` lanes are idle, so lanes
+// do not sit out the longest ray of a batch (SIMD efficiency of the incoherent secondary
+// rays).  One loop trip is one traversal step: an interior node (both children tested) and
+// then, if the lane stands on a leaf, that leaf's primitives.  Per ray the nodes visited,
+// primitives tested and their order are bvh_walk's.
+template <bool ANY, bool STATS>
+__global__ __launch_bounds__(kTraceBlock) void k_trace_pt(DevScene S, PathSoA P, int q, int refill, int ring, uint2 *__restrict__ spill) {
+    // traversal stack: the top kStackLDS entries of each lane in LDS (a ring, column per
+    // lane: refs, then entry distances), deeper entries in the lane's spill area in HBM
+    __shared__ uint32_t sref[kStackLDS * kTraceBlock];
+    __shared__ float stm[ANY ? 1 : kStackLDS * kTraceBlock];
+    uint2 *gsp = spill + (size_t)(blockIdx.x * blockDim.x + threadIdx.x) * S.stackDepth;
+    int bottom = 0;   // entries [0, bottom) live in gsp
+    Stack st;         // work counters only
+    const uint32_t n = ANY ? P.cnt[CNT_QS(q)] : P.cnt[CNT_QC(q)];
+    const uint32_t *Q = ANY ? P.qS + (size_t)q * P.cap : P.qC + (size_t)q * 2 * P.cap;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = (gridDim.x * blockDim.x) >> 6;
+    uint32_t next = (uint32_t)((uint64_t)n * wave / nw);
+    const uint32_t end = (uint32_t)((uint64_t)n * (wave + 1) / nw);
+    bool active = false;
+    int slot = 0, kind = 0, todo = 0, prim = -1;
+    uint32_t ref = 0;
+    float thit = INFINITY;
+    Ray ray;
+    V invDir = v3(0.f, 0.f, 0.f);
+    int neg[3] = {0, 0, 0};
+    uint32_t nM = 0, hM = 0;
+    for (;;) {
+        const unsigned long long idle = __ballot(!active);
+        const uint32_t nIdle = (uint32_t)__popcll(idle);
+        if (next < end && (nIdle >= (uint32_t)refill || nIdle == 64u)) {
+            if (!active) {
+                const uint32_t i = next + (uint32_t)__popcll(idle & ((1ull << lane) - 1ull));
+                if (i < end) {
+                    const uint32_t e = Q[i];
+                    slot = ANY ? (int)e : (int)(e >> 1);
+                    kind = ANY ? RAY_S : (int)(e & 1);
+                    ray = ray_load(P, kind, slot);
+                    invDir = v3(1.f / ray.d.x, 1.f / ray.d.y, 1.f / ray.d.z);
+                    neg[0] = invDir.x < 0; neg[1] = invDir.y < 0; neg[2] = invDir.z < 0;
+                    prim = -1;
+                    thit = INFINITY;
+                    todo = 0;
+                    bottom = 0;
+                    if (ANY) st.cShadow++; else st.cRays++;
+                    st.cNodes++;
+                    if (bbox_hit(S.nodes[0], S.nodes[1], ray, invDir, neg)) {
+                        ref = S.nodeRef[0];
+                        active = true;
+                    } else if (ANY) P.occ[slot] = 0u;
+                    else {
+                        P.hitPrim[(size_t)kind * P.cap + slot] = -1;
+                        P.hitT[(size_t)kind * P.cap + slot] = INFINITY;
+                        if (STATS && kind == RAY_M) nM++;
+                    }
+                }
+            }
+            next = min(end, next + nIdle);
+        }
+        if (!__ballot(active)) {
+            if (next >= end) break;
+            continue;
+        }
+        if (active) {
+            bool done = false, occluded = false;
+            if (!(ref & WREF_LEAF)) {
+                const float4 *w = S.wnodes + 4 * (size_t)ref;
+                const float4 l0 = w[0], l1 = w[1], r0 = w[2], r1 = w[3];
+                st.cNodes++;
+                float tl = 0.f, tr = 0.f;
+                const bool hl = slab_enter(l0, l1, ray, invDir, neg, &tl) && tl < ray.maxt;
+                const bool hr = slab_enter(r0, r1, ray, invDir, neg, &tr) && tr < ray.maxt;
+                const uint32_t refL = __float_as_uint(l0.w), refR = __float_as_uint(l1.w);
+                const bool swap = neg[__float_as_uint(r0.w)] != 0;
+                const bool hn = swap ? hr : hl, hf = swap ? hl : hr;
+                const uint32_t rn = swap ? refR : refL, rf = swap ? refL : refR;
+                if (hn) {
+                    if (hf) {
+                        if (todo - bottom == ring) {   // ring full: oldest entry to HBM
+                            const int j = (bottom & (ring - 1)) * kTraceBlock + threadIdx.x;
+                            gsp[bottom] = make_uint2(sref[j], ANY ? 0u : __float_as_uint(stm[j]));
+                            ++bottom;
+                        }
+                        const int j = (todo & (ring - 1)) * kTraceBlock + threadIdx.x;
+                        sref[j] = rf;
+                        if (!ANY) stm[j] = swap ? tl : tr;
+                        ++todo;
+                    }
+                    ref = rn;
+                } else if (hf) ref = rf;
+                else ref = 0xffffffffu;   // pop below
+            }
+            if (ref != 0xffffffffu && (ref & WREF_LEAF)) {
+                const uint32_t np = (ref >> WREF_NP_SHIFT) & WREF_NP_MASK, off = ref & WREF_OFF_MASK;
+                for (uint32_t i = 0; i < np; ++i)
+                    if (prim_test<ANY, false>(S, st, todo, (int)(off + i), ray, &prim, &thit) && ANY) {
+                        occluded = true;
+                        break;
+                    }
+                ref = 0xffffffffu;
+            }
+            if (occluded) done = true;
+            else if (ref == 0xffffffffu) {
+                done = true;
+                while (todo > 0) {
+                    --todo;
+                    uint32_t r;
+                    float tm;
+                    if (todo < bottom) {
+                        const uint2 g = gsp[todo];
+                        r = g.x; tm = __uint_as_float(g.y);
+                        bottom = todo;
+                    } else {
+                        const int j = (todo & (ring - 1)) * kTraceBlock + threadIdx.x;
+                        r = sref[j]; tm = ANY ? 0.f : stm[j];
+                    }
+                    if (ANY || tm < ray.maxt) { ref = r; done = false; break; }
+                }
+            }
+            if (done) {
+                active = false;
+                if (ANY) P.occ[slot] = occluded ? 1u : 0u;
+                else {
+                    P.hitPrim[(size_t)kind * P.cap + slot] = prim;
+                    P.hitT[(size_t)kind * P.cap + slot] = prim >= 0 ? thit : INFINITY;
+                    st.cHits += prim >= 0 ? 1u : 0u;
+                    if (STATS && kind == RAY_M) { nM++; hM += prim >= 0 ? 1u : 0u; }
+                }
+            }
+        }
     }
-    __syncthreads();
-    const uint32_t idx = lds4[15] + lds4[wave] + before;
-    __syncthreads();   // lds4 is reused by the next call
-    return idx;
-}
-
-// shading pass over every slot: finish / advance live paths, regenerate free slots, and
-// queue the next pass's rays into queue set qout (block-aggregated queue pushes)
-#ifndef PGD_SHADE_ATTR
-#define PGD_SHADE_ATTR
-#endif
-template <int NB, int FEAT>
-__global__ __launch_bounds__(kShadeBlock) PGD_SHADE_ATTR void k_shade(DevScene S, PathSoA P, ItemSrc src, int qout,
-                                                       float *__restrict__ Lout) {
-    __shared__ uint32_t lds4[16];
-    const int slot = blockIdx.x * blockDim.x + threadIdx.x;
-    const bool inRange = slot < P.cap;
-    Pushes pu = {false, false, false};
-    bool freeSlot = inRange && P.item[slot] < 0;
-    bool zeroed = false;
-    if (inRange && !freeSlot) {
-        bool done;
-        pu = shade_slot<NB, FEAT>(S, P, slot, Lout, &done, &zeroed);
-        if (done) { P.item[slot] = -1; freeSlot = true; }
+    if (STATS) {
+        unsigned long long *w = reinterpret_cast<unsigned long long *>(P.cnt + CNT_WORK);
+        if (ANY) {
+            atomicAdd(&w[W_SHADOW], (unsigned long long)st.cShadow);
+            atomicAdd(&w[W_NODES_S], (unsigned long long)st.cNodes);
+            atomicAdd(&w[W_TRIS_S], (unsigned long long)st.cTris);
+            atomicAdd(&w[W_QUADS_S], (unsigned long long)st.cQuads);
+        } else {
+            atomicAdd(&w[W_RAYS], (unsigned long long)st.cRays);
+            atomicAdd(&w[W_NODES_C], (unsigned long long)st.cNodes);
+            atomicAdd(&w[W_TRIS_C], (unsigned long long)st.cTris);
+            atomicAdd(&w[W_QUADS_C], (unsigned long long)st.cQuads);
+            atomicAdd(&w[W_HITS], (unsigned long long)st.cHits);
+            atomicAdd(&w[W_RAYS_M], (unsigned long long)nM);
+            atomicAdd(&w[W_HITS_M], (unsigned long long)hM);
+        }
     }
-    if (__ballot(zeroed)) {
-        const unsigned long long m = __ballot(zeroed);
-        if ((threadIdx.x & 63) == 0) atomicAdd(&P.cnt[CNT_ZEROED], (uint32_t)__popcll(m));
-    }
-    // regeneration: free slots take the next camera samples
-    const bool want = freeSlot && *(volatile uint32_t *)&P.cnt[CNT_NEXT] < src.nItems;
-    if (__syncthreads_or(want)) {
-        const uint32_t it = block_push(want, &P.cnt[CNT_NEXT], lds4);
-        if (want && it < src.nItems) { path_start<NB>(S, P, src, slot, it); pu.c = true; }
-    }
-    const uint32_t kc = block_push(pu.c, &P.cnt[CNT_QC(qout)], lds4);
-    if (pu.c) P.qC[(size_t)qout * 2 * P.cap + kc] = (uint32_t)slot << 1;
-    const uint32_t km = block_push(pu.m, &P.cnt[CNT_QC(qout)], lds4);
-    if (pu.m) P.qC[(size_t)qout * 2 * P.cap + km] = ((uint32_t)slot << 1) | 1u;
-    const uint32_t ks = block_push(pu.s, &P.cnt[CNT_QS(qout)], lds4);
-    if (pu.s) P.qS[(size_t)qout * P.cap + ks] = (uint32_t)slot;
 }
 
 // film[filmIdx[p]][b] += L(p, s) for s in batch order (spectralImage.cpp:125-131)
@@ -215,6 +314,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_intersect(DevScene S, const flo
     extern __shared__ uint32_t lds[];
     Stack st;
     st.base = lds + threadIdx.x;
+    st.tbase = reinterpret_cast<float *>(lds + (size_t)S.stackDepth * blockDim.x) + threadIdx.x;
     st.stride = blockDim.x;
     int k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= n) return;
@@ -265,10 +365,14 @@ struct pbrtgpu_ctx {
     std::vector<DevBuf> sceneBufs;
     DevBuf film, Lbuf, pix, filmIdx, mask, keys, counter, spillL, lists[4], scratch[3];
     DevBuf slots;            // PathSoA storage
+    DevBuf spill;            // k_trace_pt stack spill areas (persistent lanes x stack depth)
     int slotCap = 0, slotNb = 0;
     PathSoA P{};
     uint32_t *hostCnt = nullptr;   // pinned mirror of the queue counters
     int numCUs = 256;
+    int ptBlocksPerCU = 0;    // occupancy of k_trace_pt (computed on first use)
+    int ring = kStackLDS;     // LDS ring entries in use (PBRTGPU_STACK_LDS: tests force HBM spills)
+    int refill = 16;          // idle lanes that trigger ray replacement in k_trace_pt (PBRTGPU_REFILL)
     Timing last;
 };
 
@@ -326,7 +430,8 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
     PathSoA &P = c->P;
     HIPCHK(hipMemsetAsync(P.item, 0xff, (size_t)cap * 4, c->stream));
     HIPCHK(hipMemsetAsync(P.cnt, 0, CNT_WORDS * 4, c->stream));
-    const size_t lds = (size_t)c->stackDepth * kTraceBlock * sizeof(uint32_t);
+    // LDS stack: child refs and (closest-hit) entry distances, one column per lane
+    const size_t ldsS = (size_t)c->stackDepth * kTraceBlock * sizeof(uint32_t), lds = 2 * ldsS;
     const int perCU = std::max(1, std::min(16, (int)(160 * 1024 / std::max<size_t>(lds, 1))));
     const int traceGrid = c->numCUs * perCU;
     const int shadeGrid = (cap + kShadeBlock - 1) / kShadeBlock;
@@ -335,9 +440,8 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
     HIPCHK(hipEventRecord(c->ev[4], c->stream));
     // scenes without measured BRDFs, textures and environment lights run the variant with
     // that code compiled out (fewer registers, no kd-tree stack)
-    auto kShade = c->feat ? k_shade<NB, FEAT_ALL> : k_shade<NB, 0>;
-    hipLaunchKernelGGL(kShade, dim3(shadeGrid), dim3(kShadeBlock), 0, c->stream, c->S, P, src, q, Lout);
-    HIPCHK(hipGetLastError());
+    auto kShade = c->feat ? launch_shade<NB, FEAT_ALL> : launch_shade<NB, 0>;
+    HIPCHK(kShade(shadeGrid, c->stream, c->S, P, src, q, Lout));
     HIPCHK(hipEventRecord(c->ev[5], c->stream));
     bool pending = false;   // events ev[0..3] of the previous pass still to be read
     float m;
@@ -359,15 +463,26 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
         HIPCHK(hipMemsetAsync(P.cnt + CNT_QC(nq), 0, 4, c->stream));
         HIPCHK(hipMemsetAsync(P.cnt + CNT_QS(nq), 0, 4, c->stream));
         HIPCHK(hipEventRecord(c->ev[0], c->stream));
-        int gC = (int)std::min<uint32_t>((nC + kTraceBlock - 1) / kTraceBlock, (uint32_t)traceGrid);
         const bool inst = c->S.nInsts > 0;
+        // instanced scenes walk nested BVHs (bvh_walk); the others run the persistent
+        // ray-replacement kernels over the whole (wave-partitioned) queue
+        if (!c->ptBlocksPerCU) {   // resident blocks of the persistent kernels (registers, LDS)
+            int b0 = 0, b1 = 0;
+            HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&b0, k_trace_pt<false, false>, kTraceBlock, 0));
+            HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&b1, k_trace_pt<true, false>, kTraceBlock, 0));
+            c->ptBlocksPerCU = std::max(1, std::min(b0, b1));
+        }
+        const uint32_t ptGrid = (uint32_t)(c->numCUs * c->ptBlocksPerCU);
+        HIPCHK(c->spill.ensure((size_t)ptGrid * kTraceBlock * c->stackDepth * sizeof(uint2)));
+        int gC = (int)std::min<uint32_t>((nC + kTraceBlock - 1) / kTraceBlock, (uint32_t)traceGrid);
         if (gC > 0) {
-            if (countWork) {
-                if (inst) hipLaunchKernelGGL((k_trace_closest<true, true>), dim3(gC), dim3(kTraceBlock), lds, c->stream, c->S, P, q);
-                else hipLaunchKernelGGL((k_trace_closest<true, false>), dim3(gC), dim3(kTraceBlock), lds, c->stream, c->S, P, q);
+            if (inst) {
+                if (countWork) hipLaunchKernelGGL((k_trace_closest<true, true>), dim3(gC), dim3(kTraceBlock), lds, c->stream, c->S, P, q);
+                else hipLaunchKernelGGL((k_trace_closest<false, true>), dim3(gC), dim3(kTraceBlock), lds, c->stream, c->S, P, q);
             } else {
-                if (inst) hipLaunchKernelGGL((k_trace_closest<false, true>), dim3(gC), dim3(kTraceBlock), lds, c->stream, c->S, P, q);
-                else hipLaunchKernelGGL((k_trace_closest<false, false>), dim3(gC), dim3(kTraceBlock), lds, c->stream, c->S, P, q);
+                const uint32_t g = std::min<uint32_t>(ptGrid, (nC + 63) / 64 * 64 / kTraceBlock + 1);
+                if (countWork) hipLaunchKernelGGL((k_trace_pt<false, true>), dim3(g), dim3(kTraceBlock), 0, c->stream, c->S, P, q, c->refill, c->ring, (uint2 *)c->spill.p);
+                else hipLaunchKernelGGL((k_trace_pt<false, false>), dim3(g), dim3(kTraceBlock), 0, c->stream, c->S, P, q, c->refill, c->ring, (uint2 *)c->spill.p);
             }
             HIPCHK(hipGetLastError());
             T.launches[K_CLOSEST]++;
@@ -375,19 +490,19 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
         HIPCHK(hipEventRecord(c->ev[1], c->stream));
         int gS = (int)std::min<uint32_t>((nS + kTraceBlock - 1) / kTraceBlock, (uint32_t)traceGrid);
         if (gS > 0) {
-            if (countWork) {
-                if (inst) hipLaunchKernelGGL((k_trace_shadow<true, true>), dim3(gS), dim3(kTraceBlock), lds, c->stream, c->S, P, q);
-                else hipLaunchKernelGGL((k_trace_shadow<true, false>), dim3(gS), dim3(kTraceBlock), lds, c->stream, c->S, P, q);
+            if (inst) {
+                if (countWork) hipLaunchKernelGGL((k_trace_shadow<true, true>), dim3(gS), dim3(kTraceBlock), ldsS, c->stream, c->S, P, q);
+                else hipLaunchKernelGGL((k_trace_shadow<false, true>), dim3(gS), dim3(kTraceBlock), ldsS, c->stream, c->S, P, q);
             } else {
-                if (inst) hipLaunchKernelGGL((k_trace_shadow<false, true>), dim3(gS), dim3(kTraceBlock), lds, c->stream, c->S, P, q);
-                else hipLaunchKernelGGL((k_trace_shadow<false, false>), dim3(gS), dim3(kTraceBlock), lds, c->stream, c->S, P, q);
+                const uint32_t g = std::min<uint32_t>(ptGrid, (nS + 63) / 64 * 64 / kTraceBlock + 1);
+                if (countWork) hipLaunchKernelGGL((k_trace_pt<true, true>), dim3(g), dim3(kTraceBlock), 0, c->stream, c->S, P, q, c->refill, c->ring, (uint2 *)c->spill.p);
+                else hipLaunchKernelGGL((k_trace_pt<true, false>), dim3(g), dim3(kTraceBlock), 0, c->stream, c->S, P, q, c->refill, c->ring, (uint2 *)c->spill.p);
             }
             HIPCHK(hipGetLastError());
             T.launches[K_SHADOW]++;
         }
         HIPCHK(hipEventRecord(c->ev[2], c->stream));
-        hipLaunchKernelGGL(kShade, dim3(shadeGrid), dim3(kShadeBlock), 0, c->stream, c->S, P, src, nq, Lout);
-        HIPCHK(hipGetLastError());
+        HIPCHK(kShade(shadeGrid, c->stream, c->S, P, src, nq, Lout));
         T.launches[K_SHADE]++;
         HIPCHK(hipEventRecord(c->ev[3], c->stream));
         pending = true;
@@ -399,6 +514,45 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
     if (countWork)
         for (int i = 0; i < W_COUNT; ++i) T.work[i] += w[i];
     if (zeroedOut) *zeroedOut += c->hostCnt[CNT_ZEROED];
+    return 0;
+}
+
+// Child-in-parent copy of the flattened BVH (LinearBVHNode, bvh.cpp:105-115) for
+// bvh_walk: wide node k of interior node i = {left box lo, ref(left)} {left box hi,
+// ref(right)} {right box lo, axis} {right box hi, 0}, with left = i + 1 and right =
+// secondChildOffset as in the reference's depth-first layout.  ref[] maps every node to its
+// reference (wide index or WREF_LEAF record); the roots of the top-level and instance BVHs
+// are looked up there.
+static float bits_f(uint32_t u) { float f; memcpy(&f, &u, 4); return f; }
+static int wide_bvh(const pbrtgpu_flat_scene *s, std::vector<float4> *wn, std::vector<uint32_t> *ref) {
+    const int n = s->n_nodes;
+    ref->assign(n, 0u);
+    uint32_t nw = 0;
+    for (int i = 0; i < n; ++i) {
+        const pbrtgpu_bvh_node &b = s->nodes[i];
+        const uint32_t np = b.meta & 0xff;
+        if (np == 0) (*ref)[i] = nw++;
+        else {
+            if (np > WREF_NP_MASK || b.offset > WREF_OFF_MASK)
+                return fail(PBRTGPU_E_UNSUPPORTED, "BVH leaf beyond the 2^24-primitive reference range");
+            (*ref)[i] = WREF_LEAF | (np << WREF_NP_SHIFT) | b.offset;
+        }
+    }
+    if (nw >= WREF_LEAF) return fail(PBRTGPU_E_UNSUPPORTED, "BVH too large");
+    wn->assign((size_t)nw * 4, make_float4(0.f, 0.f, 0.f, 0.f));
+    for (int i = 0; i < n; ++i) {
+        const pbrtgpu_bvh_node &b = s->nodes[i];
+        if (b.meta & 0xff) continue;
+        const uint32_t L = (uint32_t)i + 1, R = b.offset;
+        if (L >= (uint32_t)n || R >= (uint32_t)n) return fail(PBRTGPU_E_INVALID, "BVH child out of range");
+        const pbrtgpu_bvh_node &l = s->nodes[L], &r = s->nodes[R];
+        float4 *w = wn->data() + (size_t)(*ref)[i] * 4;
+        w[0] = make_float4(l.bmin[0], l.bmin[1], l.bmin[2], bits_f((*ref)[L]));
+        w[1] = make_float4(l.bmax[0], l.bmax[1], l.bmax[2], bits_f((*ref)[R]));
+        w[2] = make_float4(r.bmin[0], r.bmin[1], r.bmin[2], bits_f((b.meta >> 8) & 0xff));
+        w[3] = make_float4(r.bmax[0], r.bmax[1], r.bmax[2], 0.f);
+        if (((b.meta >> 8) & 0xff) > 2) return fail(PBRTGPU_E_INVALID, "BVH split axis");
+    }
     return 0;
 }
 
@@ -421,6 +575,11 @@ int pbrtgpu_context_create(int device, pbrtgpu_ctx **out) {
     HIPCHK(hipSetDevice(device));
     pbrtgpu_ctx *c = new pbrtgpu_ctx();
     c->device = device;
+    if (const char *e = getenv("PBRTGPU_REFILL")) c->refill = std::max(1, std::min(64, atoi(e)));
+    if (const char *e = getenv("PBRTGPU_STACK_LDS")) {
+        const int r = atoi(e);
+        if (r >= 1 && r <= kStackLDS && (r & (r - 1)) == 0) c->ring = r;
+    }
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->numCUs = prop.multiProcessorCount;
     bool ok = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess;
@@ -441,7 +600,7 @@ int pbrtgpu_context_destroy(pbrtgpu_ctx *c) {
     for (auto &b : c->sceneBufs) b.release();
     DevBuf *bufs[] = {&c->film, &c->Lbuf, &c->pix, &c->filmIdx, &c->mask, &c->keys, &c->counter, &c->spillL,
                       &c->lists[0], &c->lists[1], &c->lists[2], &c->lists[3], &c->scratch[0],
-                      &c->scratch[1], &c->scratch[2], &c->slots};
+                      &c->scratch[1], &c->scratch[2], &c->slots, &c->spill};
     for (DevBuf *b : bufs) b->release();
     for (int i = 0; i < 8; ++i) if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
     if (c->hostCnt) (void)hipHostFree(c->hostCnt);
@@ -550,6 +709,13 @@ int pbrtgpu_scene_upload(pbrtgpu_ctx *c, const pbrtgpu_flat_scene *s) {
     S.stackDepth = c->stackDepth;
     HIPCHK(upload(c, s->band_Y, (size_t)s->n_bands, &S.bandY));
     HIPCHK(upload(c, reinterpret_cast<const float4 *>(s->nodes), (size_t)s->n_nodes * 2, &S.nodes));
+    {
+        std::vector<float4> wn;
+        std::vector<uint32_t> ref;
+        if (int e = wide_bvh(s, &wn, &ref)) return e;
+        HIPCHK(upload(c, wn.data(), wn.size(), &S.wnodes));
+        HIPCHK(upload(c, ref.data(), ref.size(), &S.nodeRef));
+    }
     HIPCHK(upload(c, s->prims, (size_t)s->n_prims, &S.prims));
     std::vector<DevTri> pt(s->n_prims);
     for (int i = 0; i < s->n_prims; ++i) {
@@ -926,7 +1092,7 @@ int pbrtgpu_intersect(pbrtgpu_ctx *c, const float *rays, int32_t n, float *hits,
     HIPCHK(c->scratch[1].ensure((size_t)n * 16));
     HIPCHK(c->scratch[2].ensure((size_t)n * 4));
     HIPCHK(hipMemcpyAsync(c->scratch[0].p, rays, (size_t)n * 32, hipMemcpyHostToDevice, c->stream));
-    size_t lds = (size_t)c->stackDepth * kTraceBlock * 4;
+    size_t lds = 2 * (size_t)c->stackDepth * kTraceBlock * 4;
     hipLaunchKernelGGL(k_intersect, dim3((n + kTraceBlock - 1) / kTraceBlock), dim3(kTraceBlock), lds, c->stream, c->S,
                        (const float *)c->scratch[0].p, n, (float *)c->scratch[1].p, (int *)c->scratch[2].p);
     HIPCHK(hipGetLastError());

@@ -405,7 +405,10 @@ PGD_INLINE Pushes shade_vertex(const DevScene &S, const PathSoA &P, int slot, in
     const V wo = vneg(ray.d);
     MT rng;
     const bool useMT = vb >= 3;
-    if (useMT) mt_load(P, slot, fl, rng);
+    if (useMT) {
+        mt_load(P, slot, fl, rng);
+        if (!rng.init) mt_init(rng);
+    }
     const int nLights = S.nLights;
     fl &= ~(PF_PEND | PF_PA | PF_PB | PF_CONT | (0xffffffu << PF_LIGHT_SHIFT));
     FVal F;
@@ -690,5 +693,11 @@ PGD_INLINE Pushes shade_slot(const DevScene &S, const PathSoA &P, int slot, floa
     P.flags[slot] = fl;
     return out;
 }
+
+static const int kShadeBlock = 256;
+// k_shade<NB, FEAT> launch (defined in shade.hip, one translation unit per variant)
+template <int NB, int FEAT>
+hipError_t launch_shade(int grid, hipStream_t stream, const DevScene &S, const PathSoA &P, const ItemSrc &src, int qout,
+                        float *Lout);
 
 }  // namespace pgd

@@ -272,3 +272,24 @@ def test_coverage_scene_matches_oracle(pg):
     assert np.all(Lg.view(np.int32) == Lo.view(np.int32), axis=1).mean() >= 1 - 1e-4
     ref, _ = o.render(scene)
     assert np.all(film.view(np.int32) == ref.view(np.int32), axis=2).mean() >= 0.999
+
+
+@pytest.mark.parametrize("ring,refill", [("1", "1"), ("2", "64"), ("4", "7")])
+def test_traversal_stack_spill_and_ray_replacement(pg, killeroo64, dev, monkeypatch, ring, refill):
+    """k_trace_pt keeps the top of each lane's traversal stack in an LDS ring and spills the
+    rest to HBM, and replaces finished rays once `refill` lanes idle.  Tiny rings (every
+    deep push spills) and extreme thresholds must give the default's radiance bit for bit."""
+    keys = _keys(killeroo64, stride=2)
+    ref = dev.trace_paths(keys)
+    monkeypatch.setenv("PBRTGPU_STACK_LDS", ring)
+    monkeypatch.setenv("PBRTGPU_REFILL", refill)
+    with pg.Device(0) as d:
+        d.upload(killeroo64)
+        got = d.trace_paths(keys)
+        d.render(count_work=True)
+        w = d.timing()["work"]
+    dev.render(count_work=True)
+    w0 = dev.timing()["work"]
+    assert np.array_equal(ref.view(np.int32), got.view(np.int32))
+    for k in ("rays", "shadow_rays", "nodes_closest", "nodes_shadow", "tris_closest", "tris_shadow", "hits"):
+        assert w[k] == w0[k], k
