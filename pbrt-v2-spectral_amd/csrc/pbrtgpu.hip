@@ -27,6 +27,18 @@
 #include "wavefront.h"
 
 using namespace pgd;
+#ifdef PGD_SECTIONS
+extern "C" {
+int pgd_sections_read_32_0(unsigned long long *, int); int pgd_sections_read_32_7(unsigned long long *, int);
+int pgd_sections_read_60_0(unsigned long long *, int); int pgd_sections_read_60_7(unsigned long long *, int);
+int pgd_sections_read_30_0(unsigned long long *, int); int pgd_sections_read_30_7(unsigned long long *, int);
+}
+static int pgd_sections_read(unsigned long long *out, int reset) {
+    for (int k = 0; k < SEC_N; ++k) out[k] = 0;
+    int e = pgd_sections_read_32_0(out, reset) | pgd_sections_read_32_7(out, reset) | pgd_sections_read_60_0(out, reset);
+    return e | pgd_sections_read_60_7(out, reset) | pgd_sections_read_30_0(out, reset) | pgd_sections_read_30_7(out, reset);
+}
+#endif
 
 static thread_local std::string g_err;
 static int fail(int code, const std::string &msg) { g_err = msg; return code; }
@@ -401,8 +413,8 @@ static int ensure_slots(pbrtgpu_ctx *c, int cap, int NB) {
     size_t off = 0;
     auto take = [&](size_t bytes) { size_t o = off; off += (bytes + 255) & ~(size_t)255; return o; };
     size_t oItem = take(C * 4), oHp = take(C * 4), oSmp = take(C * 4), oBounce = take(C * 4), oFlags = take(C * 4),
-           oMt = take(C * 20), oBeta = take(C * 2 * NBP * 4), oL = take(C * NBP * 4), oA = take(C * NBP * 4),
-           oB = take(C * NBP * 4), oM = take(C * NBP * 4), oK = take(C * NBP * 4), oPix = take(C * 4), oRay = take(C * 27 * 4), oHitP = take(C * 8), oHitT = take(C * 8), oOcc = take(C * 4),
+           oMt = take(C * 20), oBeta = take(C * 3 * NBP * 4), oL = take(C * NBP * 4), oA = take(C * 2 * NBP * 4),
+           oB = take(C * 2 * NBP * 4), oM = take(C * NBP * 4), oK = take(C * NBP * 4), oPix = take(C * 4), oRay = take(C * 27 * 4), oHitP = take(C * 8), oHitT = take(C * 8), oOcc = take(C * 4),
            oQC = take(C * 16), oQS = take(C * 8), oCnt = take(CNT_WORDS * 4);
     HIPCHK(c->slots.ensure(off));
     char *base = (char *)c->slots.p;
@@ -1006,6 +1018,19 @@ static int render_impl(pbrtgpu_ctx *c, const pbrtgpu_render_desc *d, const int32
     }
     if (int e = applyLists(postT, postStart, postSrc)) return e;
     HIPCHK(hipStreamSynchronize(c->stream));
+#ifdef PGD_SECTIONS
+    {   // timing experiment: wave-cycles per k_shade section of this render
+        unsigned long long sec[SEC_N];
+        if (pgd_sections_read(sec, 1) == 0) {
+            static const char *nm[] = {"load", "finish", "isect", "bsdf", "light", "mis", "cont", "out", "regen", "push"};
+            unsigned long long tot = 0;
+            for (int k = 0; k < SEC_PUSH + 1; ++k) tot += sec[k];
+            fprintf(stderr, "sections:");
+            for (int k = 0; k < SEC_PUSH + 1; ++k) fprintf(stderr, " %s %.1f%%", nm[k], 100.0 * sec[k] / std::max(1ull, tot));
+            fprintf(stderr, "  (total %.3e wave-cycles)\n", (double)tot);
+        }
+    }
+#endif
     st[PBRTGPU_STAT_KERNEL_MS] = T.ms[K_CLOSEST] + T.ms[K_SHADOW] + T.ms[K_SHADE];
     st[PBRTGPU_STAT_ACCUM_MS] = T.ms[K_ACCUM];
     st[PBRTGPU_STAT_ZEROED] = zeroed;

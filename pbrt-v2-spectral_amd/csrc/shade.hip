@@ -13,6 +13,24 @@
 
 namespace pgd {
 
+#ifdef PGD_SECTIONS
+// per-section totals of this variant, each on its own 128-byte line, 8 copies striped by block
+#define PGD_CAT2(a, b, c) a##b##_##c
+#define PGD_CAT(a, b, c) PGD_CAT2(a, b, c)
+static __device__ unsigned long long pgd_sec_total[8 * SEC_N * 16];
+extern "C" int PGD_CAT(pgd_sections_read_, SHADE_NB, SHADE_FEAT)(unsigned long long *out, int reset) {
+    unsigned long long h[8 * SEC_N * 16];
+    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(pgd_sec_total), sizeof(h)) != hipSuccess) return -1;
+    for (int k = 0; k < SEC_N; ++k)
+        for (int c = 0; c < 8; ++c) out[k] += h[c * SEC_N * 16 + k * 16];
+    if (reset) {
+        for (auto &v : h) v = 0;
+        if (hipMemcpyToSymbol(HIP_SYMBOL(pgd_sec_total), h, sizeof(h)) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#endif
+
 // Block-wide exclusive prefix of a per-thread flag with ONE atomicAdd per block on
 // *counter; returns this thread's index (valid where flag is set).  All threads of the
 // block must call it (it contains barriers).
@@ -35,13 +53,20 @@ __device__ __forceinline__ uint32_t block_push(bool flag, uint32_t *counter, uin
 
 // shading pass over every slot: finish / advance live paths, regenerate free slots, and
 // queue the next pass's rays into queue set qout (block-aggregated queue pushes)
+// occupancy target: 3 waves/SIMD (<= 168 VGPRs) for <= 32 bands costs a few spilled
+// registers and beats the unconstrained 200-VGPR / 2-wave build (C2 shade 372 -> 335
+// ms/frame, r01l ablation; 4 waves spills ~90 registers and loses); 60 bands: 2 waves
 #ifndef PGD_SHADE_ATTR
-#define PGD_SHADE_ATTR
+#define PGD_SHADE_ATTR __attribute__((amdgpu_waves_per_eu(SHADE_NB > 32 ? 2 : 3, SHADE_NB > 32 ? 2 : 3)))
 #endif
 template <int NB, int FEAT>
 __global__ __launch_bounds__(kShadeBlock) PGD_SHADE_ATTR void k_shade(DevScene S, PathSoA P, ItemSrc src, int qout,
                                                        float *__restrict__ Lout) {
     __shared__ uint32_t lds4[16];
+#ifdef PGD_SECTIONS
+    if (threadIdx.x < SEC_N) pgd_secs[threadIdx.x] = 0;
+    __syncthreads();
+#endif
     const int slot = blockIdx.x * blockDim.x + threadIdx.x;
     const bool inRange = slot < P.cap;
     Pushes pu = {false, false, false};
@@ -57,17 +82,25 @@ __global__ __launch_bounds__(kShadeBlock) PGD_SHADE_ATTR void k_shade(DevScene S
         if ((threadIdx.x & 63) == 0) atomicAdd(&P.cnt[CNT_ZEROED], (uint32_t)__popcll(m));
     }
     // regeneration: free slots take the next camera samples
+    PGD_T0(REGEN);
     const bool want = freeSlot && *(volatile uint32_t *)&P.cnt[CNT_NEXT] < src.nItems;
     if (__syncthreads_or(want)) {
         const uint32_t it = block_push(want, &P.cnt[CNT_NEXT], lds4);
         if (want && it < src.nItems) { path_start<NB>(S, P, src, slot, it); pu.c = true; }
     }
+    PGD_T1(REGEN);
+    PGD_T0(PUSH);
     const uint32_t kc = block_push(pu.c, &P.cnt[CNT_QC(qout)], lds4);
     if (pu.c) P.qC[(size_t)qout * 2 * P.cap + kc] = (uint32_t)slot << 1;
     const uint32_t km = block_push(pu.m, &P.cnt[CNT_QC(qout)], lds4);
     if (pu.m) P.qC[(size_t)qout * 2 * P.cap + km] = ((uint32_t)slot << 1) | 1u;
     const uint32_t ks = block_push(pu.s, &P.cnt[CNT_QS(qout)], lds4);
     if (pu.s) P.qS[(size_t)qout * P.cap + ks] = (uint32_t)slot;
+    PGD_T1(PUSH);
+#ifdef PGD_SECTIONS
+    __syncthreads();
+    if (threadIdx.x < SEC_N) atomicAdd(&pgd_sec_total[(blockIdx.x & 7) * SEC_N * 16 + threadIdx.x * 16], pgd_secs[threadIdx.x]);
+#endif
 }
 
 template <int NB, int FEAT>

@@ -24,6 +24,22 @@
 
 namespace pgd {
 
+// Timing experiment only (-DPGD_SECTIONS, never in the product build): wave-cycles per
+// section of k_shade, summed per block in LDS and written to a per-block array.
+#ifdef PGD_SECTIONS
+enum { SEC_LOAD, SEC_FINISH, SEC_ISECT, SEC_BSDF, SEC_LIGHT, SEC_MIS, SEC_CONT, SEC_OUT, SEC_REGEN, SEC_PUSH, SEC_N = 16 };
+__shared__ unsigned long long pgd_secs[SEC_N];
+#define PGD_T0(k) const unsigned long long pgd_t_##k = clock64()
+#define PGD_T1(k)                                                                                 \
+    do {                                                                                          \
+        const unsigned long long d_ = clock64() - pgd_t_##k;                                      \
+        if (__builtin_amdgcn_readfirstlane(threadIdx.x) == threadIdx.x) atomicAdd(&pgd_secs[SEC_##k], d_); \
+    } while (0)
+#else
+#define PGD_T0(k) do {} while (0)
+#define PGD_T1(k) do {} while (0)
+#endif
+
 enum {
     PF_CONT = 1,      // continuation / camera ray queued (answer in hit[0])
     PF_PEND = 2,      // direct lighting of vertex `bounce` not yet added to L
@@ -52,9 +68,9 @@ struct PathSoA {
     int *bounce;        // vertex index of the last processed vertex (-1: camera ray in flight)
     uint32_t *flags;
     uint32_t *mt;       // [5][cap]: k, a, b, m, seed
-    float4 *beta;       // [2][NQ][cap]: beta at even / odd vertices
+    float4 *beta;       // [3][NQ][cap]: beta at vertex v in buffer v % 3
     float4 *L;          // [NQ][cap]
-    float4 *A, *B;      // [NQ][cap]
+    float4 *A, *B;      // [2][NQ][cap]: pending direct-light terms of vertex v in buffer v & 1
     float4 *M;          // [NQ][cap]: measured-BRDF spectrum of the BSDF value being consumed
     float4 *K;          // [NQ][cap]: the material's textured spectrum at the current vertex
     float *ray;         // [3][9][cap]: o.xyz, d.xyz, mint, maxt, time  for RAY_C, RAY_M, RAY_S
@@ -104,6 +120,17 @@ PGD_INLINE void mt_store(const PathSoA &P, int slot, const MT &r) {
 }
 
 template <int NB> struct Bands { static constexpr int NQ = (NB + 3) / 4; };
+// path-state spectra of vertex v (v >= 0): beta in three buffers, so that a pass can read
+// beta_b (finishing vertex b), beta_{b+1} (shading it) and write beta_{b+2}; A, B in two
+template <int NB> PGD_INLINE float4 *beta_of(const PathSoA &P, int v, int slot) {
+    return P.beta + (size_t)(v % 3) * Bands<NB>::NQ * P.cap + slot;
+}
+template <int NB> PGD_INLINE float4 *A_of(const PathSoA &P, int v, int slot) {
+    return P.A + (size_t)(v & 1) * Bands<NB>::NQ * P.cap + slot;
+}
+template <int NB> PGD_INLINE float4 *B_of(const PathSoA &P, int v, int slot) {
+    return P.B + (size_t)(v & 1) * Bands<NB>::NQ * P.cap + slot;
+}
 
 PGD_INLINE float4 ld4(const float *p) { return *reinterpret_cast<const float4 *>(p); }
 PGD_INLINE float &cmp(float4 &v, int k) { return k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w; }
@@ -349,38 +376,41 @@ PGD_INLINE bool path_output(const DevScene &S, const float4 (&L)[Bands<NB>::NQ],
 // ray requests produced by one shade step
 struct Pushes { bool c, m, s; };
 
+// Additions to L a vertex makes before its direct light is known, in order: emitted
+// radiance (path.cpp:67-68; bounce 0 or after a specular bounce) and the zero direct light
+// of a vertex with nothing pending (L += beta * (nLights * 0)).  Both scale beta of the
+// vertex; they are applied with the rest of the pass's L updates (shade_slot).
+struct LAdds {
+    bool emit;      // L += beta * Le
+    int emitOff;    // spectrum pool offset of Le, or -1: Le = 0 (L += beta * 0)
+    bool zero;      // L += beta * (nLights * 0)
+};
+
 // One vertex of PathIntegrator::Li at bounce `vb` for the path in `slot`, whose
-// continuation ray `ray` hit primitive `prim` at `thit`.  L is the path's radiance (in
-// registers); beta_b is P.beta[vb & 1] in HBM.  BSDF values are evaluated lazily per band
-// quad (fval4).  Updates fl.
+// continuation ray `ray` hit primitive `prim` at `thit`.  L stays in HBM: the vertex's own
+// additions to L are returned in *la.  beta_vb is beta_of(vb) in HBM.  BSDF values are
+// evaluated lazily per band quad (fval4).  Updates fl.
 template <int NB, int FEAT>
 PGD_INLINE Pushes shade_vertex(const DevScene &S, const PathSoA &P, int slot, int vb, const Ray &ray, int prim,
-                               float thit, uint32_t &fl, float4 (&L)[Bands<NB>::NQ]) {
+                               float thit, uint32_t &fl, LAdds *la) {
     constexpr int NQ = Bands<NB>::NQ;
     const size_t c = P.cap;
     const float *sp = S.spectra;
     Pushes out = {false, false, false};
-    const float4 *beta = P.beta + (size_t)(vb & 1) * NQ * c + slot;
+    const float4 *beta = beta_of<NB>(P, vb, slot);
     float4 *mb = P.M + slot;
     Isect is;
+    PGD_T0(ISECT);
     isect_fill(S, ray, prim, thit, is);
+    PGD_T1(ISECT);
+    la->emit = false;
+    la->zero = false;
     if (vb == 0 || (fl & PF_SPEC)) {
         int al = S.prims[is.prim].area_light;
-        if (al >= 0 && vdot(is.dg.nn, vneg(ray.d)) > 0.f) {
-            const float *Ls = sp + S.lights[al].spec;
-#pragma unroll
-            for (int q = 0; q < NQ; ++q) {
-                float4 b = beta[q * c], e = ld4(Ls + 4 * q);
-                L[q].x += b.x * e.x; L[q].y += b.y * e.y; L[q].z += b.z * e.z; L[q].w += b.w * e.w;
-            }
-        } else {
-#pragma unroll
-            for (int q = 0; q < NQ; ++q) {
-                float4 b = beta[q * c];
-                L[q].x += b.x * 0.f; L[q].y += b.y * 0.f; L[q].z += b.z * 0.f; L[q].w += b.w * 0.f;
-            }
-        }
+        la->emit = true;
+        la->emitOff = (al >= 0 && vdot(is.dg.nn, vneg(ray.d)) > 0.f) ? S.lights[al].spec : -1;
     }
+    PGD_T0(BSDF);
     const uint32_t hp = P.hp[slot], s = P.smp[slot], spp = (uint32_t)S.spp;
     // only the camera ray carries differentials (path.cpp:107 drops them); they matter only
     // to textured materials
@@ -402,6 +432,7 @@ PGD_INLINE Pushes shade_vertex(const DevScene &S, const PathSoA &P, int slot, in
     BSDF bs;
     V p, n;
     get_bsdf<FEAT>(S, is, diff, kb, c, bs, &p, &n);
+    PGD_T1(BSDF);
     const V wo = vneg(ray.d);
     MT rng;
     const bool useMT = vb >= 3;
@@ -417,6 +448,7 @@ PGD_INLINE Pushes shade_vertex(const DevScene &S, const PathSoA &P, int slot, in
 #else
     if (nLights > 0) {
 #endif
+        PGD_T0(LIGHT);
         float ul[3], ub[3], ulnum;
         if (!useMT) {
             float u2[2];
@@ -452,7 +484,7 @@ PGD_INLINE Pushes shade_vertex(const DevScene &S, const PathSoA &P, int slot, in
                 sc = fabsf(vdot(wi, n)) * weight / lightPdf;
             }
             // A_i = (f_i * Li_i) * sc ; written while testing f for black (A unused if black)
-            float4 *A = P.A + slot;
+            float4 *A = A_of<NB>(P, vb, slot);
             bool black = true;
 #pragma unroll
             for (int q = 0; q < NQ; ++q) {
@@ -472,6 +504,8 @@ PGD_INLINE Pushes shade_vertex(const DevScene &S, const PathSoA &P, int slot, in
                 out.s = true;
             }
         }
+        PGD_T1(LIGHT);
+        PGD_T0(MIS);
         // ---- BSDF sample with MIS -> B (added if the MIS ray reaches this light: hits it
         // facing, for an area light; escapes the scene, for the environment)
         if (!em.point) {
@@ -494,7 +528,7 @@ PGD_INLINE Pushes shade_vertex(const DevScene &S, const PathSoA &P, int slot, in
                 }
                 if (go && !emit_black<NB, FEAT>(S, eb)) {
                     const float ad = fabsf(vdot(wi, n));
-                    float4 *B = P.B + slot;
+                    float4 *B = B_of<NB>(P, vb, slot);
                     bool black = true;
 #pragma unroll
                     for (int q = 0; q < NQ; ++q) {
@@ -516,24 +550,15 @@ PGD_INLINE Pushes shade_vertex(const DevScene &S, const PathSoA &P, int slot, in
                 }
             }
         }
+        PGD_T1(MIS);
         if (!(fl & (PF_PA | PF_PB))) {
-            // nothing can add to Ld: finish now (L += beta * (nLights * 0))
-            const float z = (float)nLights * 0.f;
-#pragma unroll
-            for (int q = 0; q < NQ; ++q) {
-                float4 b = beta[q * c];
-                L[q].x += b.x * z; L[q].y += b.y * z; L[q].z += b.z * z; L[q].w += b.w * z;
-            }
+            // nothing can add to Ld: finish now (L += beta * (nLights * 0), nLights * 0 == 0)
+            la->zero = true;
             fl &= ~PF_PEND;
         }
-    } else {
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) {
-            float4 b = beta[q * c];
-            L[q].x += b.x * 0.f; L[q].y += b.y * 0.f; L[q].z += b.z * 0.f; L[q].w += b.w * 0.f;
-        }
-    }
+    } else la->zero = true;   // L += beta * 0
     // ---- path continuation
+    PGD_T0(CONT);
     float up[3];
     if (!useMT) {
         float u2[2];
@@ -550,7 +575,7 @@ PGD_INLINE Pushes shade_vertex(const DevScene &S, const PathSoA &P, int slot, in
     if (cont) {
         fval_prepare<NB, FEAT>(S, F, mb, c);
         const float ad = fabsf(vdot(wi, n));
-        float4 *bn = P.beta + (size_t)((vb + 1) & 1) * NQ * c + slot;
+        float4 *bn = beta_of<NB>(P, vb + 1, slot);
         float4 nb4[NQ];
         bool black = true;
 #pragma unroll
@@ -594,25 +619,32 @@ PGD_INLINE Pushes shade_vertex(const DevScene &S, const PathSoA &P, int slot, in
         mt_store(P, slot, rng);
         if (rng.init) fl |= PF_MTINIT;
     }
+    PGD_T1(CONT);
     return out;
 }
 
 // k_shade body for one slot: finish pending direct light, process the next vertex.
-// Returns the ray requests; *done when the path has produced its radiance.
+// Returns the ray requests; *done when the path has produced its radiance.  L is read and
+// updated once, after the vertex: the finish of vertex b (beta_b, A_b, B_b), then the
+// vertex's own additions -- the order of PathIntegrator::Li.  Keeping L out of registers
+// through shade_vertex is what lets the kernel fit its occupancy target.
 template <int NB, int FEAT>
 PGD_INLINE Pushes shade_slot(const DevScene &S, const PathSoA &P, int slot, float *__restrict__ Lout, bool *done,
                              bool *zeroed) {
     constexpr int NQ = Bands<NB>::NQ;
     const size_t c = P.cap;
+    PGD_T0(LOAD);
     uint32_t fl = P.flags[slot];
-    int b = P.bounce[slot];
-    float4 L[NQ];
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) L[q] = P.L[q * c + slot];
+    const int b = P.bounce[slot];
     Pushes out = {false, false, false};
-    if (fl & PF_PEND) {
-        const bool useA = (fl & PF_PA) && !P.occ[slot];
-        bool useB = false;
+    PGD_T1(LOAD);
+    PGD_T0(FINISH);
+    // which terms of vertex b's direct light arrived (decided before shade_vertex reuses the
+    // slot's MIS ray)
+    const bool fin = (fl & PF_PEND) != 0;
+    bool useA = false, useB = false;
+    if (fin) {
+        useA = (fl & PF_PA) && !P.occ[slot];
         if (fl & PF_PB) {
             const int ln = (int)(fl >> PF_LIGHT_SHIFT);
             int mp = P.hitPrim[c + slot];
@@ -624,13 +656,35 @@ PGD_INLINE Pushes shade_slot(const DevScene &S, const PathSoA &P, int slot, floa
                 useB = vdot(lis.dg.nn, vneg(mr.d)) > 0.f;
             }
         }
+        fl &= ~(PF_PEND | PF_PA | PF_PB);
+    }
+    PGD_T1(FINISH);
+    LAdds la = {false, -1, false};
+    int esc = 0;   // continuation ray escaped: 1 camera ray (sum of Le), 2 after a specular bounce
+    int vb = b;
+    if (fl & PF_CONT) {
+        vb = b + 1;
+        const int prim = P.hitPrim[slot];
+        fl &= ~PF_CONT;
+        if (prim < 0) esc = vb == 0 ? 1 : ((fl & PF_SPEC) ? 2 : 0);
+        else {
+            Ray ray = ray_load(P, RAY_C, slot);
+            out = shade_vertex<NB, FEAT>(S, P, slot, vb, ray, prim, P.hitT[slot], fl, &la);
+            P.bounce[slot] = vb;
+        }
+    }
+    PGD_T0(OUT);
+    float4 L[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) L[q] = P.L[q * c + slot];
+    if (fin) {   // L += beta_b * (nLights * Ld), Ld = (0 [+ A]) [+ B]
         const float nl = (float)S.nLights;
-        const float4 *beta = P.beta + (size_t)(b & 1) * NQ * c + slot;
+        const float4 *beta = beta_of<NB>(P, b, slot), *A = A_of<NB>(P, b, slot), *B = B_of<NB>(P, b, slot);
 #pragma unroll
         for (int q = 0; q < NQ; ++q) {
             float4 bt = beta[q * c];
-            float4 a = useA ? P.A[q * c + slot] : make_float4(0.f, 0.f, 0.f, 0.f);
-            float4 bb = useB ? P.B[q * c + slot] : make_float4(0.f, 0.f, 0.f, 0.f);
+            float4 a = useA ? A[q * c] : make_float4(0.f, 0.f, 0.f, 0.f);
+            float4 bb = useB ? B[q * c] : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 float Ld = 0.f;
@@ -639,48 +693,49 @@ PGD_INLINE Pushes shade_slot(const DevScene &S, const PathSoA &P, int slot, floa
                 cmp(L[q], k) += cmp(bt, k) * (nl * Ld);
             }
         }
-        fl &= ~(PF_PEND | PF_PA | PF_PB);
     }
-    if (fl & PF_CONT) {
-        const int vb = b + 1;
-        const int prim = P.hitPrim[slot];
-        fl &= ~PF_CONT;
-        if (prim < 0) {
-            if (vb == 0) {
-                // SamplerRenderer::Li (samplerrenderer.cpp:237-240): Li = sum of the lights' Le,
-                // zero for area and point lights
-                if ((FEAT & FEAT_INF) && S.nInf > 0) {
-                    const Ray ray = ray_load(P, RAY_C, slot);
-                    for (int l = 0; l < S.nLights; ++l)
-                        if (S.lights[l].type == PBRTGPU_LIGHT_INFINITE) {
-                            const Emit e = inf_Le(S.lights[l], ray.d);
+    if (la.emit || la.zero) {   // vertex vb: L += beta * Le, then L += beta * (nLights * 0)
+        const float4 *beta = beta_of<NB>(P, vb, slot);
+        const float *Ls = S.spectra + (la.emitOff >= 0 ? la.emitOff : 0);
 #pragma unroll
-                            for (int q = 0; q < NQ; ++q) {
-                                float4 v = emit4<FEAT>(S, e, q);
-                                L[q].x += v.x; L[q].y += v.y; L[q].z += v.z; L[q].w += v.w;
-                            }
-                        }
-                }
-            } else if (fl & PF_SPEC) {
-                // path.cpp:92-96: L += beta * Le(ray) for every light
-                const float4 *beta = P.beta + (size_t)(vb & 1) * NQ * c + slot;
-                V d = v3(0.f, 0.f, 0.f);
-                if ((FEAT & FEAT_INF) && S.nInf > 0) d = ray_load(P, RAY_C, slot).d;
-                for (int l = 0; l < S.nLights; ++l) {
-                    Emit e;
-                    e.mode = EM_BLACK;
-                    if ((FEAT & FEAT_INF) && S.lights[l].type == PBRTGPU_LIGHT_INFINITE) e = inf_Le(S.lights[l], d);
+        for (int q = 0; q < NQ; ++q) {
+            const float4 bt = beta[q * c];
+            if (la.emit) {
+                const float4 e = la.emitOff >= 0 ? ld4(Ls + 4 * q) : make_float4(0.f, 0.f, 0.f, 0.f);
+                L[q].x += bt.x * e.x; L[q].y += bt.y * e.y; L[q].z += bt.z * e.z; L[q].w += bt.w * e.w;
+            }
+            if (la.zero) { L[q].x += bt.x * 0.f; L[q].y += bt.y * 0.f; L[q].z += bt.z * 0.f; L[q].w += bt.w * 0.f; }
+        }
+    }
+    if (esc == 1) {
+        // SamplerRenderer::Li (samplerrenderer.cpp:237-240): Li = sum of the lights' Le, zero
+        // for area and point lights
+        if ((FEAT & FEAT_INF) && S.nInf > 0) {
+            const Ray ray = ray_load(P, RAY_C, slot);
+            for (int l = 0; l < S.nLights; ++l)
+                if (S.lights[l].type == PBRTGPU_LIGHT_INFINITE) {
+                    const Emit e = inf_Le(S.lights[l], ray.d);
 #pragma unroll
                     for (int q = 0; q < NQ; ++q) {
-                        float4 bt = beta[q * c], v = emit4<FEAT>(S, e, q);
-                        L[q].x += bt.x * v.x; L[q].y += bt.y * v.y; L[q].z += bt.z * v.z; L[q].w += bt.w * v.w;
+                        float4 v = emit4<FEAT>(S, e, q);
+                        L[q].x += v.x; L[q].y += v.y; L[q].z += v.z; L[q].w += v.w;
                     }
                 }
+        }
+    } else if (esc == 2) {
+        // path.cpp:92-96: L += beta * Le(ray) for every light
+        const float4 *beta = beta_of<NB>(P, vb, slot);
+        V d = v3(0.f, 0.f, 0.f);
+        if ((FEAT & FEAT_INF) && S.nInf > 0) d = ray_load(P, RAY_C, slot).d;
+        for (int l = 0; l < S.nLights; ++l) {
+            Emit e;
+            e.mode = EM_BLACK;
+            if ((FEAT & FEAT_INF) && S.lights[l].type == PBRTGPU_LIGHT_INFINITE) e = inf_Le(S.lights[l], d);
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                float4 bt = beta[q * c], v = emit4<FEAT>(S, e, q);
+                L[q].x += bt.x * v.x; L[q].y += bt.y * v.y; L[q].z += bt.z * v.z; L[q].w += bt.w * v.w;
             }
-        } else {
-            Ray ray = ray_load(P, RAY_C, slot);
-            out = shade_vertex<NB, FEAT>(S, P, slot, vb, ray, prim, P.hitT[slot], fl, L);
-            P.bounce[slot] = vb;
         }
     }
     *done = !(fl & (PF_CONT | PF_PEND));
@@ -691,6 +746,7 @@ PGD_INLINE Pushes shade_slot(const DevScene &S, const PathSoA &P, int slot, floa
         for (int q = 0; q < NQ; ++q) P.L[q * c + slot] = L[q];
     }
     P.flags[slot] = fl;
+    PGD_T1(OUT);
     return out;
 }
 
