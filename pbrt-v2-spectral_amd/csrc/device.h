@@ -406,7 +406,10 @@ PGD_INLINE Ray to_object(const pbrtgpu_quadric &q, const Ray &r) {
     return o;
 }
 // Sphere::Intersect (sphere.cpp:50-150)
-PGD_INLINE bool sphere_intersect(const pbrtgpu_quadric &q, const Ray &r, float *tHit, float *rayEps, DG *dg) {
+// nnOnly: the caller uses only dg->nn (light sampling / pdf / MIS facing tests); nn is
+// computed exactly as dg_init would, the rest of the differential geometry is skipped
+PGD_INLINE bool sphere_intersect(const pbrtgpu_quadric &q, const Ray &r, float *tHit, float *rayEps, DG *dg,
+                                 bool nnOnly = false) {
     float phi;
     V phit;
     Ray ray = to_object(q, r);
@@ -442,6 +445,19 @@ PGD_INLINE bool sphere_intersect(const pbrtgpu_quadric &q, const Ray &r, float *
             return false;
     }
     if (!dg) { *tHit = thit; return true; }
+    if (nnOnly) {
+        const float theta = ACOSF(clampf(phit.z / q.radius, -1.f, 1.f));
+        const float zradius = sqrtf(phit.x * phit.x + phit.y * phit.y);
+        const float invzradius = 1.f / zradius;
+        const float cosphi = phit.x * invzradius, sinphi = phit.y * invzradius;
+        const V dpdu = v3(-q.phi_max * phit.y, q.phi_max * phit.x, 0);
+        const V dpdv = vmul(v3(phit.z * cosphi, phit.z * sinphi, -q.radius * SINF(theta)), q.theta_max - q.theta_min);
+        dg->nn = vnorm(vcross(xvec(q.o2w_m, dpdu), xvec(q.o2w_m, dpdv)));
+        if (q.reverse_orientation ^ q.swaps_handedness) dg->nn = vmul(dg->nn, -1.f);
+        *tHit = thit;
+        *rayEps = 5e-4f * *tHit;
+        return true;
+    }
     float u = phi / q.phi_max;
     float theta = ACOSF(clampf(phit.z / q.radius, -1.f, 1.f));
     float v = (theta - q.theta_min) / (q.theta_max - q.theta_min);
@@ -466,7 +482,8 @@ PGD_INLINE bool sphere_intersect(const pbrtgpu_quadric &q, const Ray &r, float *
     return true;
 }
 // Disk::Intersect (disk.cpp:48-96)
-PGD_INLINE bool disk_intersect(const pbrtgpu_quadric &q, const Ray &r, float *tHit, float *rayEps, DG *dg) {
+PGD_INLINE bool disk_intersect(const pbrtgpu_quadric &q, const Ray &r, float *tHit, float *rayEps, DG *dg,
+                               bool nnOnly = false) {
     Ray ray = to_object(q, r);
     if (fabsf(ray.d.z) < 1e-7) return false;
     float thit = (q.height - ray.o.z) / ray.d.z;
@@ -474,8 +491,30 @@ PGD_INLINE bool disk_intersect(const pbrtgpu_quadric &q, const Ray &r, float *tH
     V phit = rayat(ray, thit);
     float dist2 = phit.x * phit.x + phit.y * phit.y;
     if (dist2 > q.radius * q.radius || dist2 < q.inner_radius * q.inner_radius) return false;
-    // phi <= (float)(2pi) always: with phi_max >= that bound a hit-only query skips the atan2
-    if (!dg && q.phi_max >= 2.f * kPi) { *tHit = thit; return true; }
+    // phi <= (float)(2pi) always: with phi_max >= that bound the phi test cannot fail, and a
+    // hit-only (or nn-only) query skips the atan2
+    const bool phiFree = q.phi_max >= 2.f * kPi;
+    if (!dg && phiFree) { *tHit = thit; return true; }
+    if (nnOnly) {
+        if (!phiFree) {
+            float phi = ATAN2F(phit.y, phit.x);
+            if (phi < 0) phi = (float)((double)phi + 2. * (double)kPi);
+            if (phi > q.phi_max) return false;
+        }
+        const float oneMinusV = ((sqrtf(dist2) - q.inner_radius) / (q.radius - q.inner_radius));
+        const float invOneMinusV = (oneMinusV > 0.f) ? (1.f / oneMinusV) : 0.f;
+        V dpdu = v3(-q.phi_max * phit.y, q.phi_max * phit.x, 0.);
+        V dpdv = v3(-phit.x * invOneMinusV, -phit.y * invOneMinusV, 0.);
+        const float su = q.phi_max * kInvTwoPi;
+        dpdu = v3(dpdu.x * su, dpdu.y * su, dpdu.z * su);
+        const float sc = (q.radius - q.inner_radius) / q.radius;
+        dpdv = v3(dpdv.x * sc, dpdv.y * sc, dpdv.z * sc);
+        dg->nn = vnorm(vcross(xvec(q.o2w_m, dpdu), xvec(q.o2w_m, dpdv)));
+        if (q.reverse_orientation ^ q.swaps_handedness) dg->nn = vmul(dg->nn, -1.f);
+        *tHit = thit;
+        *rayEps = 5e-4f * *tHit;
+        return true;
+    }
     float phi = ATAN2F(phit.y, phit.x);
     if (phi < 0) phi = (float)((double)phi + 2. * (double)kPi);
     if (phi > q.phi_max) return false;
@@ -507,10 +546,11 @@ PGD_INLINE float shape_area(const DevScene &S, int type, int idx) {
     if (type == PBRTGPU_SHAPE_SPHERE) return q.phi_max * q.radius * (q.zmax - q.zmin);
     return q.phi_max * 0.5f * (q.radius * q.radius - q.inner_radius * q.inner_radius);
 }
-PGD_HEAVY bool shape_intersect(const DevScene &S, int type, int idx, const Ray &r, float *tHit, float *eps, DG *dg) {
+PGD_HEAVY bool shape_intersect(const DevScene &S, int type, int idx, const Ray &r, float *tHit, float *eps, DG *dg,
+                               bool nnOnly = false) {
     if (type == PBRTGPU_SHAPE_TRIANGLE) return tri_intersect(S, idx, r, tHit, eps, dg);
-    if (type == PBRTGPU_SHAPE_SPHERE) return sphere_intersect(S.quads[idx], r, tHit, eps, dg);
-    return disk_intersect(S.quads[idx], r, tHit, eps, dg);
+    if (type == PBRTGPU_SHAPE_SPHERE) return sphere_intersect(S.quads[idx], r, tHit, eps, dg, nnOnly);
+    return disk_intersect(S.quads[idx], r, tHit, eps, dg, nnOnly);
 }
 
 // ------------------------------------------------------------------ BVH traversal
@@ -827,6 +867,22 @@ PGD_INLINE bool bvh_intersectP(const DevScene &S, Stack &st, const Ray &ray) {
     return bvh_walk<true, INST>(S, st, 0, 0u, r, &hp, &ht);
 }
 struct Isect { DG dg; float rayEps; int prim; int inst; float time; };
+PGD_HEAVY void isect_fill(const DevScene &S, const Ray &ray, int prim, float t, Isect &is);
+// geometric normal dg.nn of a recorded closest hit (the field isect_fill would produce)
+PGD_INLINE V isect_nn(const DevScene &S, const Ray &ray, int prim, float t) {
+    if (!S.nInsts || S.primInst[prim] < 0) {
+        const pbrtgpu_prim pr = S.prims[prim];
+        Ray r = ray;
+        r.maxt = t;
+        float th, e;
+        DG dg;
+        shape_intersect(S, pr.shape_type, pr.shape_index, r, &th, &e, &dg, true);
+        return dg.nn;
+    }
+    Isect is;
+    isect_fill(S, ray, prim, t, is);
+    return is.dg.nn;
+}
 // full intersection record for a recorded closest hit; primitives of a transformed instance
 // are intersected in primitive space and moved to world space (primitive.cpp:94-110)
 PGD_HEAVY void isect_fill(const DevScene &S, const Ray &ray, int prim, float t, Isect &is) {
@@ -1568,9 +1624,8 @@ PGD_INLINE V sphere_sample_p(const pbrtgpu_quadric &q, V p, float u1, float u2, 
     float phi = u2 * 2.f * kPi;
     V dir = vadd(vadd(vmul(wcX, COSF(phi) * sintheta), vmul(wcY, SINF(phi) * sintheta)), vmul(wc, costheta));
     Ray r; r.o = p; r.d = dir; r.mint = 1e-3f; r.maxt = INFINITY; r.time = 0.f;
-    float thit, eps;
-    DG dgs;
-    if (!sphere_intersect(q, r, &thit, &eps, &dgs)) thit = vdot(vsub(Pcenter, p), vnorm(r.d));
+    float thit, eps;   // sphere.cpp:245-247 uses only thit of the intersection
+    if (!sphere_intersect(q, r, &thit, &eps, nullptr)) thit = vdot(vsub(Pcenter, p), vnorm(r.d));
     V ps = rayat(r, thit);
     *ns = vnorm(vsub(ps, Pcenter));
     if (q.reverse_orientation) *ns = vmul(*ns, -1.f);
@@ -1580,7 +1635,7 @@ PGD_INLINE float shape_pdf_generic(const DevScene &S, int type, int idx, V p, V 
     Ray ray; ray.o = p; ray.d = wi; ray.mint = 1e-3f; ray.maxt = INFINITY; ray.time = 0.f;
     float thit, eps;
     DG dg;
-    if (!shape_intersect(S, type, idx, ray, &thit, &eps, &dg)) return 0.;
+    if (!shape_intersect(S, type, idx, ray, &thit, &eps, &dg, true)) return 0.;
     float pdf = vlen2(vsub(p, rayat(ray, thit))) / (fabsf(vdot(dg.nn, vneg(wi))) * shape_area(S, type, idx));
     if (isinf(pdf)) pdf = 0.f;
     return pdf;
@@ -1689,7 +1744,7 @@ PGD_HEAVY void light_sample_L(const DevScene &S, const pbrtgpu_light &L, V p, fl
     for (int i = 0; i < L.n_shapes; ++i) {
         float th, e;
         DG d2;
-        if (shape_intersect(S, shs[i].shape_type, shs[i].shape_index, r, &th, &e, &d2)) { anyHit = true; thit = th; hitNN = d2.nn; }
+        if (shape_intersect(S, shs[i].shape_type, shs[i].shape_index, r, &th, &e, &d2, true)) { anyHit = true; thit = th; hitNN = d2.nn; }
     }
     if (anyHit) ns = hitNN;
     V ps = rayat(r, thit);

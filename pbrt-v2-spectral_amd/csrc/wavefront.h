@@ -651,9 +651,7 @@ PGD_INLINE Pushes shade_slot(const DevScene &S, const PathSoA &P, int slot, floa
             if ((FEAT & FEAT_INF) && S.lights[ln].type == PBRTGPU_LIGHT_INFINITE) useB = mp < 0;   // Li = light->Le(ray)
             else if (mp >= 0 && S.prims[mp].area_light == ln) {
                 Ray mr = ray_load(P, RAY_M, slot);
-                Isect lis;
-                isect_fill(S, mr, mp, P.hitT[c + slot], lis);
-                useB = vdot(lis.dg.nn, vneg(mr.d)) > 0.f;
+                useB = vdot(isect_nn(S, mr, mp, P.hitT[c + slot]), vneg(mr.d)) > 0.f;   // DiffuseAreaLight::L
             }
         }
         fl &= ~(PF_PEND | PF_PA | PF_PB);

@@ -6,6 +6,7 @@ mkdir -p $OUT
 timeout -k 10 300 python3 -m pytest tests -m gpu -x -q > $OUT/pytest_gpu.log 2>&1 || { tail -30 $OUT/pytest_gpu.log; exit 1; }
 tail -1 $OUT/pytest_gpu.log
 timeout -k 10 200 python3 bench.py --steps 2 --warmup 1 --no-cpu > $OUT/base.json
+shopt -s nullglob
 for v in pbrt-v2-spectral_amd/lib/exp/*.so; do
   n=$(basename $v .so)
   PBRTGPU_LIB=$PWD/$v timeout -k 10 200 python3 bench.py --steps 2 --warmup 1 --no-cpu > $OUT/$n.json
