@@ -103,6 +103,20 @@ PBRT_FM_FN double pbrt_fm_cos(double x) {
         default: return pbrt_fm_ksin(r);
     }
 }
+/* sin and cos of one argument: exactly pbrt_fm_sin(x) and pbrt_fm_cos(x) */
+PBRT_FM_FN void pbrt_fm_sincos(double x, double *s, double *c) {
+    if (pbrt_fm_isnan(x) || pbrt_fm_isinf(x)) { *s = x - x; *c = x - x; return; }
+    double r;
+    int q = pbrt_fm_reduce(x, &r);
+    double ks = pbrt_fm_ksin(r), kc = pbrt_fm_kcos(r);
+    switch (q) {
+        case 0: *s = ks; *c = kc; break;
+        case 1: *s = kc; *c = -ks; break;
+        case 2: *s = -ks; *c = -kc; break;
+        default: *s = -kc; *c = ks; break;
+    }
+    if (pbrt_fm_fabs(x) < 0x1p-27) *s = x;
+}
 PBRT_FM_FN double pbrt_fm_tan(double x) {
     if (pbrt_fm_isnan(x) || pbrt_fm_isinf(x)) return x - x;
     if (pbrt_fm_fabs(x) < 0x1p-27) return x;

@@ -51,7 +51,14 @@ PGD_TFN float ATAN2F(float y, float x) { return (float)pbrt_fm_atan2((double)y, 
 PGD_TFN float TANF(float x) { return (float)pbrt_fm_tan((double)x); }
 PGD_TFN float ATANF(float x) { return (float)pbrt_fm_atan((double)x); }
 PGD_TFN float LOGF(float x) { return (float)pbrt_fm_log_any((double)x); }
+// (SINF(x), COSF(x)) from one argument reduction -- the same two values, one call
+PGD_TFN float2 SINCOSF(float x) {
+    double s, c;
+    pbrt_fm_sincos((double)x, &s, &c);
+    return make_float2((float)s, (float)c);
+}
 #else
+PGD_INLINE float2 SINCOSF(float x) { return make_float2(__sinf(x), __cosf(x)); }
 PGD_INLINE float LOGF(float x) { return __logf(x); }   // timing experiment only (not the parity definition): float library functions
 PGD_INLINE float SINF(float x) { return __sinf(x); }
 PGD_INLINE float COSF(float x) { return __cosf(x); }
@@ -203,8 +210,9 @@ PGD_INLINE void concentric_disk(float u1, float u2, float *dx, float *dy) {
         else { r = -sy; theta = 6.0f + sx / r; }
     }
     theta *= kPi / 4.f;
-    *dx = r * COSF(theta);
-    *dy = r * SINF(theta);
+    const float2 sc = SINCOSF(theta);
+    *dx = r * sc.y;
+    *dy = r * sc.x;
 }
 PGD_INLINE V cosine_hemisphere(float u1, float u2) {
     V r;
@@ -216,7 +224,8 @@ PGD_INLINE V uniform_sphere(float u1, float u2) {
     float z = 1.f - 2.f * u1;
     float r = sqrtf(pmax(0.f, 1.f - z * z));
     float phi = 2.f * kPi * u2;
-    return v3(r * COSF(phi), r * SINF(phi), z);
+    const float2 sc = SINCOSF(phi);
+    return v3(r * sc.y, r * sc.x, z);
 }
 PGD_INLINE float power_heuristic(float fPdf, float gPdf) {
     float f = 1 * fPdf, g = 1 * gPdf;
@@ -697,7 +706,8 @@ PGD_INLINE Quat slerp(float t, Quat q1, Quat q2) {   // quaternion.cpp:39-49
     float theta = ACOSF(clampf(cosTheta, -1.f, 1.f));
     float thetap = theta * t;
     Quat qperp = qnormalize(qsub(q2, qscale(q1, cosTheta)));
-    return qadd(qscale(q1, COSF(thetap)), qscale(qperp, SINF(thetap)));
+    const float2 sc = SINCOSF(thetap);
+    return qadd(qscale(q1, sc.y), qscale(qperp, sc.x));
 }
 // AnimatedTransform::Interpolate (transform.cpp:356-381): world->primitive m (and mInv)
 PGD_INLINE void inst_interp(const pbrtgpu_instance &I, float time, float *m, float *minv) {
@@ -946,15 +956,29 @@ PGD_INLINE float fr_dielectric(float cosi, float eta_i, float eta_t) {
     float Rperp = ((ei * ci) - (et * cost)) / ((ei * ci) + (et * cost));
     return (Rparl * Rparl + Rperp * Rperp) / 2.f;
 }
-PGD_INLINE float blinn_D(float e, V wh) { return (e + 2) * kInvTwoPi * POWF(abscos(wh), e); }
+// The microfacet distribution D(wh) and the matching pdf raise the same |cos theta_h| to the
+// same exponent when BSDF::f and BSDF::Pdf (or Sample_f's other-component pdf) look at one
+// (wo, wi); a one-entry memo per vertex returns the identical powf instead of recomputing it
+struct PowMemo {
+    uint32_t x = 0xffffffffu, e = 0xffffffffu;   // a NaN key: never matches
+    float r = 0.f;
+};
+PGD_INLINE float dpow(PowMemo &m, float x, float e) {
+    const uint32_t xb = __float_as_uint(x), eb = __float_as_uint(e);
+    if (xb == m.x && eb == m.e) return m.r;
+    const float r = POWF(x, e);
+    m.x = xb; m.e = eb; m.r = r;
+    return r;
+}
+PGD_INLINE float blinn_D(PowMemo &pm, float e, V wh) { return (e + 2) * kInvTwoPi * dpow(pm, abscos(wh), e); }
 PGD_INLINE float micro_G(V wo, V wi, V wh) {
     float NdotWh = abscos(wh), NdotWo = abscos(wo), NdotWi = abscos(wi), WOdotWh = fabsf(vdot(wo, wh));
     return pmin(1.f, pmin((2.f * NdotWh * NdotWo / WOdotWh), (2.f * NdotWh * NdotWi / WOdotWh)));
 }
-PGD_INLINE float blinn_pdf(float e, V wo, V wi) {
+PGD_INLINE float blinn_pdf(PowMemo &pm, float e, V wo, V wi) {
     V wh = vnorm(vadd(wo, wi));
     float costheta = abscos(wh);
-    float p = ((e + 1.f) * POWF(costheta, e)) / (2.f * kPi * 4.f * vdot(wo, wh));
+    float p = ((e + 1.f) * dpow(pm, costheta, e)) / (2.f * kPi * 4.f * vdot(wo, wh));
     if (vdot(wo, wh) <= 0.f) p = 0.f;
     return p;
 }
@@ -962,28 +986,29 @@ PGD_INLINE void blinn_sample(float e, V wo, V *wi, float u1, float u2, float *pd
     float costheta = POWF(u1, 1.f / (e + 1));
     float sintheta = sqrtf(pmax(0.f, 1.f - costheta * costheta));
     float phi = u2 * 2.f * kPi;
-    V wh = v3(sintheta * COSF(phi), sintheta * SINF(phi), costheta);
+    const float2 sc = SINCOSF(phi);
+    V wh = v3(sintheta * sc.y, sintheta * sc.x, costheta);
     if (!samehemi(wo, wh)) wh = vneg(wh);
     *wi = vadd(vneg(wo), vmul(wh, 2.f * vdot(wo, wh)));
     float p = ((e + 1.f) * POWF(costheta, e)) / (2.f * kPi * 4.f * vdot(wo, wh));
     if (vdot(wo, wh) <= 0.f) p = 0.f;
     *pdf = p;
 }
-PGD_INLINE float aniso_D(float ex, float ey, V wh) {
+PGD_INLINE float aniso_D(PowMemo &pm, float ex, float ey, V wh) {
     float costhetah = abscos(wh);
     float d = 1.f - costhetah * costhetah;
     if (d == 0.f) return 0.f;
     float e = (ex * wh.x * wh.x + ey * wh.y * wh.y) / d;
-    return sqrtf((ex + 2.f) * (ey + 2.f)) * kInvTwoPi * POWF(costhetah, e);
+    return sqrtf((ex + 2.f) * (ey + 2.f)) * kInvTwoPi * dpow(pm, costhetah, e);
 }
-PGD_INLINE float aniso_pdf(float ex, float ey, V wo, V wi) {
+PGD_INLINE float aniso_pdf(PowMemo &pm, float ex, float ey, V wo, V wi) {
     V wh = vnorm(vadd(wo, wi));
     float costhetah = abscos(wh);
     float ds = 1.f - costhetah * costhetah;
     float p = 0.f;
     if (ds > 0.f && vdot(wo, wh) > 0.f) {
         float e = (ex * wh.x * wh.x + ey * wh.y * wh.y) / ds;
-        float d = sqrtf((ex + 1.f) * (ey + 1.f)) * kInvTwoPi * POWF(costhetah, e);
+        float d = sqrtf((ex + 1.f) * (ey + 1.f)) * kInvTwoPi * dpow(pm, costhetah, e);
         p = d / (4.f * vdot(wo, wh));
     }
     return p;
@@ -991,7 +1016,8 @@ PGD_INLINE float aniso_pdf(float ex, float ey, V wo, V wi) {
 PGD_INLINE void aniso_first_quadrant(float ex, float ey, float u1, float u2, float *phi, float *costheta) {
     if (ex == ey) *phi = kPi * u1 * 0.5f;
     else *phi = ATANF(sqrtf((ex + 1.f) / (ey + 1.f)) * TANF(kPi * u1 * 0.5f));
-    float cp = COSF(*phi), sp = SINF(*phi);
+    const float2 scp = SINCOSF(*phi);
+    float cp = scp.y, sp = scp.x;
     *costheta = POWF(u2, 1.f / (ex * cp * cp + ey * sp * sp + 1));
 }
 PGD_INLINE void aniso_sample(float ex, float ey, V wo, V *wi, float u1, float u2, float *pdf) {
@@ -1001,7 +1027,8 @@ PGD_INLINE void aniso_sample(float ex, float ey, V wo, V *wi, float u1, float u2
     else if (u1 < .75f) { u1 = 4.f * (u1 - .5f); aniso_first_quadrant(ex, ey, u1, u2, &phi, &costheta); phi += kPi; }
     else { u1 = 4.f * (1.f - u1); aniso_first_quadrant(ex, ey, u1, u2, &phi, &costheta); phi = 2.f * kPi - phi; }
     float sintheta = sqrtf(pmax(0.f, 1.f - costheta * costheta));
-    V wh = v3(sintheta * COSF(phi), sintheta * SINF(phi), costheta);
+    const float2 sc = SINCOSF(phi);
+    V wh = v3(sintheta * sc.y, sintheta * sc.x, costheta);
     if (!samehemi(wo, wh)) wh = vneg(wh);
     *wi = vadd(vneg(wo), vmul(wh, 2.f * vdot(wo, wh)));
     float costhetah = abscos(wh);
@@ -1049,7 +1076,7 @@ PGD_INLINE V brdf_remap(V wo, V wi) {
     if (dphi > kPi) dphi = 2.f * kPi - dphi;
     return v3(sini * sino, dphi / kPi, cosi * coso);
 }
-PGD_INLINE FTerm bx_term(const BxDF &b, V wo, V wi) {
+PGD_INLINE FTerm bx_term(PowMemo &pm, const BxDF &b, V wo, V wi) {
     FTerm t;
     t.kind = T_ZERO; t.R = b.R; t.R2 = b.R2; t.s0 = t.s1 = t.s2 = t.s3 = 0.f;
     switch (b.kind) {
@@ -1079,7 +1106,7 @@ PGD_INLINE FTerm bx_term(const BxDF &b, V wo, V wi) {
             float cosThetaH = vdot(wi, wh);
             if (b.kind == BX_MICRO_BLINN_DIEL) { t.kind = T_BLINN; t.s2 = fr_dielectric(cosThetaH, 1.5f, 1.f); }
             else { t.kind = T_BLINNC; t.s2 = fabsf(cosThetaH); }   // FresnelConductor::Evaluate
-            t.s0 = blinn_D(b.a, wh);
+            t.s0 = blinn_D(pm, b.a, wh);
             t.s1 = micro_G(wo, wi, wh);
             t.s3 = 4.f * cosThetaI * cosThetaO;
             break;
@@ -1089,7 +1116,7 @@ PGD_INLINE FTerm bx_term(const BxDF &b, V wo, V wi) {
             V wh = vadd(wi, wo);
             if (wh.x == 0. && wh.y == 0. && wh.z == 0.) break;
             wh = vnorm(wh);
-            float D = aniso_D(b.a, b.b, wh);
+            float D = aniso_D(pm, b.a, b.b, wh);
             float den = (4.f * fabsf(vdot(wi, wh)) * pmax(abscos(wi), abscos(wo)));
             t.kind = T_FB;
             t.s0 = ta; t.s1 = tb;
@@ -1107,28 +1134,28 @@ PGD_INLINE FTerm bx_term(const BxDF &b, V wo, V wi) {
     }
     return t;
 }
-PGD_INLINE float bx_pdf(const BxDF &b, V wo, V wi) {
+PGD_INLINE float bx_pdf(PowMemo &pm, const BxDF &b, V wo, V wi) {
     switch (b.kind) {
         case BX_MICRO_BLINN_DIEL:
-        case BX_MICRO_BLINN_COND: if (!samehemi(wo, wi)) return 0.f; return blinn_pdf(b.a, wo, wi);
+        case BX_MICRO_BLINN_COND: if (!samehemi(wo, wi)) return 0.f; return blinn_pdf(pm, b.a, wo, wi);
         case BX_SPEC_REFL_NOOP:
         case BX_SPEC_REFL_DIEL:
         case BX_SPEC_TRANS: return 0.;
         case BX_FRESNEL_BLEND_ANISO:
             if (!samehemi(wo, wi)) return 0.f;
-            return .5f * (abscos(wi) * kInvPi + aniso_pdf(b.a, b.b, wo, wi));
+            return .5f * (abscos(wi) * kInvPi + aniso_pdf(pm, b.a, b.b, wo, wi));
         default: return samehemi(wo, wi) ? abscos(wi) * kInvPi : 0.f;
     }
 }
 // BxDF::Sample_f: direction + pdf; f as a one-term sum (or the specular spectrum)
-PGD_INLINE void bx_sample_f(const BxDF &b, V wo, V *wi, float u1, float u2, float *pdf, FVal &F) {
+PGD_INLINE void bx_sample_f(PowMemo &pm, const BxDF &b, V wo, V *wi, float u1, float u2, float *pdf, FVal &F) {
     fval_zero(F);
     switch (b.kind) {
         case BX_MICRO_BLINN_DIEL:
         case BX_MICRO_BLINN_COND:
             blinn_sample(b.a, wo, wi, u1, u2, pdf);
             if (!samehemi(wo, *wi)) return;
-            F.n = 1; F.t[0] = bx_term(b, wo, *wi);
+            F.n = 1; F.t[0] = bx_term(pm, b, wo, *wi);
             return;
         case BX_SPEC_REFL_NOOP:    // SpecularReflection with FresnelNoOp: Spectrum(1) * R / |cos|
         case BX_SPEC_REFL_DIEL:    // ... with FresnelDielectric(1, ior)
@@ -1164,39 +1191,39 @@ PGD_INLINE void bx_sample_f(const BxDF &b, V wo, V *wi, float u1, float u2, floa
                 aniso_sample(b.a, b.b, wo, wi, u1, u2, pdf);
                 if (!samehemi(wo, *wi)) return;
             }
-            *pdf = bx_pdf(b, wo, *wi);
-            F.n = 1; F.t[0] = bx_term(b, wo, *wi);
+            *pdf = bx_pdf(pm, b, wo, *wi);
+            F.n = 1; F.t[0] = bx_term(pm, b, wo, *wi);
             return;
         default:
             *wi = cosine_hemisphere(u1, u2);
             if (wo.z < 0.) wi->z *= -1.f;
-            *pdf = bx_pdf(b, wo, *wi);
-            F.n = 1; F.t[0] = bx_term(b, wo, *wi);
+            *pdf = bx_pdf(pm, b, wo, *wi);
+            F.n = 1; F.t[0] = bx_term(pm, b, wo, *wi);
             return;
     }
 }
 // BSDF::f (reflection.cpp:478-494)
-PGD_INLINE void bsdf_f(const BSDF &bs, V woW, V wiW, int flags, FVal &F) {
+PGD_INLINE void bsdf_f(PowMemo &pm, const BSDF &bs, V woW, V wiW, int flags, FVal &F) {
     V wi = to_local(bs, wiW), wo = to_local(bs, woW);
     if (vdot(wiW, bs.ng) * vdot(woW, bs.ng) > 0) flags &= ~BSDF_TRANSMISSION;
     else flags &= ~BSDF_REFLECTION;
     fval_zero(F);
 #pragma unroll
     for (int k = 0; k < 2; ++k)
-        if (k < bs.n && matches(bs.bx[k], flags)) fval_push(F, bx_term(bs.bx[k], wo, wi));
+        if (k < bs.n && matches(bs.bx[k], flags)) fval_push(F, bx_term(pm, bs.bx[k], wo, wi));
 }
-PGD_INLINE float bsdf_pdf(const BSDF &bs, V woW, V wiW, int flags) {
+PGD_INLINE float bsdf_pdf(PowMemo &pm, const BSDF &bs, V woW, V wiW, int flags) {
     if (bs.n == 0.) return 0.;
     V wo = to_local(bs, woW), wi = to_local(bs, wiW);
     float pdf = 0.f;
     int m = 0;
 #pragma unroll
     for (int k = 0; k < 2; ++k)
-        if (k < bs.n && matches(bs.bx[k], flags)) { ++m; pdf += bx_pdf(bs.bx[k], wo, wi); }
+        if (k < bs.n && matches(bs.bx[k], flags)) { ++m; pdf += bx_pdf(pm, bs.bx[k], wo, wi); }
     return m > 0 ? pdf / m : 0.f;
 }
 // BSDF::Sample_f (reflection.cpp:514-568)
-PGD_HEAVY void bsdf_sample_f(const BSDF &bs, V woW, V *wiW, float u0, float u1, float uc, float *pdf, int flags,
+PGD_HEAVY void bsdf_sample_f(PowMemo &pm, const BSDF &bs, V woW, V *wiW, float u0, float u1, float uc, float *pdf, int flags,
                               int *sampledType, FVal &F) {
     int matching = 0;
 #pragma unroll
@@ -1215,7 +1242,7 @@ PGD_HEAVY void bsdf_sample_f(const BSDF &bs, V woW, V *wiW, float u0, float u1, 
     const BxDF bx = sel == 0 ? bs.bx[0] : bs.bx[1];
     V wo = to_local(bs, woW), wi;
     *pdf = 0.f;
-    bx_sample_f(bx, wo, &wi, u0, u1, pdf, F);
+    bx_sample_f(pm, bx, wo, &wi, u0, u1, pdf, F);
     if (*pdf == 0.f) {
         *sampledType = 0;
         fval_zero(F);
@@ -1226,7 +1253,7 @@ PGD_HEAVY void bsdf_sample_f(const BSDF &bs, V woW, V *wiW, float u0, float u1, 
     if (!(bx.type & BSDF_SPECULAR) && matching > 1)
 #pragma unroll
         for (int k = 0; k < 2; ++k)
-            if (k < bs.n && k != sel && matches(bs.bx[k], flags)) *pdf += bx_pdf(bs.bx[k], wo, wi);
+            if (k < bs.n && k != sel && matches(bs.bx[k], flags)) *pdf += bx_pdf(pm, bs.bx[k], wo, wi);
     if (matching > 1) *pdf /= matching;
     if (!(bx.type & BSDF_SPECULAR)) {
         fval_zero(F);
@@ -1234,7 +1261,7 @@ PGD_HEAVY void bsdf_sample_f(const BSDF &bs, V woW, V *wiW, float u0, float u1, 
         else flags &= ~BSDF_REFLECTION;
 #pragma unroll
         for (int k = 0; k < 2; ++k)
-            if (k < bs.n && matches(bs.bx[k], flags)) fval_push(F, bx_term(bs.bx[k], wo, wi));
+            if (k < bs.n && matches(bs.bx[k], flags)) fval_push(F, bx_term(pm, bs.bx[k], wo, wi));
     }
 }
 
@@ -1622,7 +1649,8 @@ PGD_INLINE V sphere_sample_p(const pbrtgpu_quadric &q, V p, float u1, float u2, 
     float costheta = lerpf(u1, cosThetaMax, 1.f);
     float sintheta = sqrtf(1.f - costheta * costheta);
     float phi = u2 * 2.f * kPi;
-    V dir = vadd(vadd(vmul(wcX, COSF(phi) * sintheta), vmul(wcY, SINF(phi) * sintheta)), vmul(wc, costheta));
+    const float2 sc = SINCOSF(phi);
+    V dir = vadd(vadd(vmul(wcX, sc.y * sintheta), vmul(wcY, sc.x * sintheta)), vmul(wc, costheta));
     Ray r; r.o = p; r.d = dir; r.mint = 1e-3f; r.maxt = INFINITY; r.time = 0.f;
     float thit, eps;   // sphere.cpp:245-247 uses only thit of the intersection
     if (!sphere_intersect(q, r, &thit, &eps, nullptr)) thit = vdot(vsub(Pcenter, p), vnorm(r.d));
@@ -1714,8 +1742,9 @@ PGD_HEAVY void light_sample_L(const DevScene &S, const pbrtgpu_light &L, V p, fl
         float uv0 = u[0], uv1 = u[1], mapPdf = L.map_pdf;
         if (mapPdf == 0.f) { *pdf = 0.f; return; }
         float theta = uv1 * kPi, phi = uv0 * 2.f * kPi;
-        float costheta = COSF(theta), sintheta = SINF(theta);
-        float sinphi = SINF(phi), cosphi = COSF(phi);
+        const float2 st = SINCOSF(theta), sp = SINCOSF(phi);
+        float costheta = st.y, sintheta = st.x;
+        float sinphi = sp.x, cosphi = sp.y;
         *wi = xvec(L.l2w_m, v3(sintheta * cosphi, sintheta * sinphi, costheta));
         *pdf = mapPdf / (2.f * kPi * kPi * sintheta);
         if (sintheta == 0.f) *pdf = 0.f;

@@ -434,6 +434,7 @@ PGD_INLINE Pushes shade_vertex(const DevScene &S, const PathSoA &P, int slot, in
     get_bsdf<FEAT>(S, is, diff, kb, c, bs, &p, &n);
     PGD_T1(BSDF);
     const V wo = vneg(ray.d);
+    PowMemo pm;   // powf memo of this vertex's BSDF evaluations
     MT rng;
     const bool useMT = vb >= 3;
     if (useMT) {
@@ -474,12 +475,12 @@ PGD_INLINE Pushes shade_vertex(const DevScene &S, const PathSoA &P, int slot, in
         Emit em;
         light_sample_L<FEAT>(S, Lt, p, is.rayEps, ul, &wi, &lightPdf, &vis, &em);
         if (lightPdf > 0. && !emit_black<NB, FEAT>(S, em)) {
-            bsdf_f(bs, wo, wi, flags, F);
+            bsdf_f(pm, bs, wo, wi, flags, F);
             fval_prepare<NB, FEAT>(S, F, mb, c);
             float sc;
             if (em.point) sc = fabsf(vdot(wi, n)) / lightPdf;
             else {
-                bsdfPdf = bsdf_pdf(bs, wo, wi, flags);
+                bsdfPdf = bsdf_pdf(pm, bs, wo, wi, flags);
                 float weight = power_heuristic(lightPdf, bsdfPdf);
                 sc = fabsf(vdot(wi, n)) * weight / lightPdf;
             }
@@ -510,7 +511,7 @@ PGD_INLINE Pushes shade_vertex(const DevScene &S, const PathSoA &P, int slot, in
         // facing, for an area light; escapes the scene, for the environment)
         if (!em.point) {
             int sampledType;
-            bsdf_sample_f(bs, wo, &wi, ub[0], ub[1], ub[2], &bsdfPdf, flags, &sampledType, F);
+            bsdf_sample_f(pm, bs, wo, &wi, ub[0], ub[1], ub[2], &bsdfPdf, flags, &sampledType, F);
             if (bsdfPdf > 0. && !(F.mode == FV_SUM && F.n == 0)) {
                 fval_prepare<NB, FEAT>(S, F, mb, c);
                 float weight = 1.f;
@@ -570,7 +571,7 @@ PGD_INLINE Pushes shade_vertex(const DevScene &S, const PathSoA &P, int slot, in
     V wi;
     float pdf;
     int sflags;
-    bsdf_sample_f(bs, wo, &wi, up[0], up[1], up[2], &pdf, BSDF_ALL, &sflags, F);
+    bsdf_sample_f(pm, bs, wo, &wi, up[0], up[1], up[2], &pdf, BSDF_ALL, &sflags, F);
     bool cont = pdf != 0. && !(F.mode == FV_SUM && F.n == 0);
     if (cont) {
         fval_prepare<NB, FEAT>(S, F, mb, c);
