@@ -47,8 +47,11 @@ enum {
     PF_PB = 8,        // BSDF-sample term B waits on the MIS ray
     PF_SPEC = 16,     // specularBounce
     PF_MTINIT = 32,   // MT19937 recurrence window initialised
+    PF_LZ = 64,       // L is still all zero (not stored yet)
+    PF_NF0 = 128,     // bits 7..9: beta buffer k (PF_NF0 << k) holds a non-finite band
 };
-#define PF_LIGHT_SHIFT 8
+#define PF_LIGHT_SHIFT 12
+#define PF_LIGHT_MASK 0xfffffu
 
 enum { RAY_C = 0, RAY_M = 1, RAY_S = 2 };
 // counters (u32 words), each on its own 128-byte line so that the per-block atomics of
@@ -125,6 +128,12 @@ template <int NB> struct Bands { static constexpr int NQ = (NB + 3) / 4; };
 template <int NB> PGD_INLINE float4 *beta_of(const PathSoA &P, int v, int slot) {
     return P.beta + (size_t)(v % 3) * Bands<NB>::NQ * P.cap + slot;
 }
+// band quad q of beta at vertex v: beta_0 = 1 is never stored
+template <int NB> PGD_INLINE float4 beta_ld(const PathSoA &P, int v, int slot, int q) {
+    return v == 0 ? make_float4(1.f, 1.f, 1.f, 1.f) : beta_of<NB>(P, v, slot)[(size_t)q * P.cap];
+}
+// beta of vertex v has a non-finite band (then L += beta * 0 is NaN and cannot be skipped)
+PGD_INLINE bool beta_nonfinite(uint32_t fl, int v) { return v > 0 && ((fl >> (7 + v % 3)) & 1u); }
 template <int NB> PGD_INLINE float4 *A_of(const PathSoA &P, int v, int slot) {
     return P.A + (size_t)(v & 1) * Bands<NB>::NQ * P.cap + slot;
 }
@@ -304,7 +313,6 @@ PGD_INLINE void fval_prepare(const DevScene &S, FVal &F, float4 *mb, size_t c) {
 // samplerrenderer.cpp:86-108 + the fixed-seed sampler of DESIGN.md §3.1)
 template <int NB>
 PGD_INLINE void path_start(const DevScene &S, const PathSoA &P, const ItemSrc &src, int slot, uint32_t item) {
-    constexpr int NQ = Bands<NB>::NQ;
     int px, py;
     uint32_t s;
     if (src.keys) { int3 k = src.keys[item]; px = k.x; py = k.y; s = (uint32_t)k.z; }
@@ -328,15 +336,9 @@ PGD_INLINE void path_start(const DevScene &S, const PathSoA &P, const ItemSrc &s
     P.pix[slot] = ((uint32_t)py << 16) | (uint32_t)px;
     P.smp[slot] = s;
     P.bounce[slot] = -1;
-    P.flags[slot] = PF_CONT;
+    P.flags[slot] = PF_CONT | PF_LZ;   // L = 0 and beta_0 = 1 are implicit (not stored)
     P.mt[slot] = 0;
     P.mt[4 * (size_t)P.cap + slot] = path_seed(hp, s);
-    const size_t c = P.cap;
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-        P.L[q * c + slot] = make_float4(0.f, 0.f, 0.f, 0.f);
-        P.beta[q * c + slot] = make_float4(1.f, 1.f, 1.f, 1.f);
-    }
 }
 
 // finished path -> guard (samplerrenderer.cpp:111-128) -> Lout[item]; returns "zeroed"
@@ -397,7 +399,6 @@ PGD_INLINE Pushes shade_vertex(const DevScene &S, const PathSoA &P, int slot, in
     const size_t c = P.cap;
     const float *sp = S.spectra;
     Pushes out = {false, false, false};
-    const float4 *beta = beta_of<NB>(P, vb, slot);
     float4 *mb = P.M + slot;
     Isect is;
     PGD_T0(ISECT);
@@ -442,7 +443,7 @@ PGD_INLINE Pushes shade_vertex(const DevScene &S, const PathSoA &P, int slot, in
         if (!rng.init) mt_init(rng);
     }
     const int nLights = S.nLights;
-    fl &= ~(PF_PEND | PF_PA | PF_PB | PF_CONT | (0xffffffu << PF_LIGHT_SHIFT));
+    fl &= ~(PF_PEND | PF_PA | PF_PB | PF_CONT | (PF_LIGHT_MASK << PF_LIGHT_SHIFT));
     FVal F;
 #ifdef PGD_EXPERIMENT_NO_NEE
     if (false) {
@@ -581,7 +582,7 @@ PGD_INLINE Pushes shade_vertex(const DevScene &S, const PathSoA &P, int slot, in
         bool black = true;
 #pragma unroll
         for (int q = 0; q < NQ; ++q) {
-            float4 f = fval4<FEAT>(sp, F, q, mb, kb, c), b = beta[q * c];
+            float4 f = fval4<FEAT>(sp, F, q, mb, kb, c), b = beta_ld<NB>(P, vb, slot, q);
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 cmp(nb4[q], k) = cmp(b, k) * ((cmp(f, k) * ad) / pdf);
@@ -607,8 +608,16 @@ PGD_INLINE Pushes shade_vertex(const DevScene &S, const PathSoA &P, int slot, in
             if (vb == S.maxDepth) cont = false;
         }
         if (cont) {
+            bool nf = false;
 #pragma unroll
-            for (int q = 0; q < NQ; ++q) bn[q * c] = nb4[q];
+            for (int q = 0; q < NQ; ++q) {
+                bn[q * c] = nb4[q];
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    if (4 * q + k < NB) nf = nf || !(fabsf(cmp(nb4[q], k)) < INFINITY);
+            }
+            const uint32_t nfBit = (uint32_t)PF_NF0 << ((vb + 1) % 3);
+            fl = nf ? (fl | nfBit) : (fl & ~nfBit);
             Ray nray;
             nray.o = p; nray.d = wi; nray.mint = is.rayEps; nray.maxt = INFINITY; nray.time = ray.time;
             ray_store(P, RAY_C, slot, nray);
@@ -673,15 +682,31 @@ PGD_INLINE Pushes shade_slot(const DevScene &S, const PathSoA &P, int slot, floa
         }
     }
     PGD_T0(OUT);
+    // L += beta * 0 leaves L unchanged for a finite beta (up to the sign of a zero, which
+    // path_output's "+ 0.f" erases), so those additions are skipped unless beta is
+    // non-finite (NaN result); L is read and written only when something changes it
+    const bool addFin = fin && (useA || useB || beta_nonfinite(fl, b));
+    const bool addEmit = la.emit && (la.emitOff >= 0 || beta_nonfinite(fl, vb));
+    const bool addZero = la.zero && beta_nonfinite(fl, vb);
+    const bool infLe = (FEAT & FEAT_INF) && S.nInf > 0;
+    const bool addEsc = esc == 1 ? infLe : (esc == 2 && (infLe || beta_nonfinite(fl, vb)));
+    *done = !(fl & (PF_CONT | PF_PEND));
+    *zeroed = false;
+    if (!(addFin || addEmit || addZero || addEsc || *done)) {
+        P.flags[slot] = fl;
+        PGD_T1(OUT);
+        return out;
+    }
     float4 L[NQ];
+    const bool lz = (fl & PF_LZ) != 0;
 #pragma unroll
-    for (int q = 0; q < NQ; ++q) L[q] = P.L[q * c + slot];
-    if (fin) {   // L += beta_b * (nLights * Ld), Ld = (0 [+ A]) [+ B]
+    for (int q = 0; q < NQ; ++q) L[q] = lz ? make_float4(0.f, 0.f, 0.f, 0.f) : P.L[q * c + slot];
+    if (addFin) {   // L += beta_b * (nLights * Ld), Ld = (0 [+ A]) [+ B]
         const float nl = (float)S.nLights;
-        const float4 *beta = beta_of<NB>(P, b, slot), *A = A_of<NB>(P, b, slot), *B = B_of<NB>(P, b, slot);
+        const float4 *A = A_of<NB>(P, b, slot), *B = B_of<NB>(P, b, slot);
 #pragma unroll
         for (int q = 0; q < NQ; ++q) {
-            float4 bt = beta[q * c];
+            float4 bt = beta_ld<NB>(P, b, slot, q);
             float4 a = useA ? A[q * c] : make_float4(0.f, 0.f, 0.f, 0.f);
             float4 bb = useB ? B[q * c] : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
@@ -693,20 +718,19 @@ PGD_INLINE Pushes shade_slot(const DevScene &S, const PathSoA &P, int slot, floa
             }
         }
     }
-    if (la.emit || la.zero) {   // vertex vb: L += beta * Le, then L += beta * (nLights * 0)
-        const float4 *beta = beta_of<NB>(P, vb, slot);
+    if (addEmit || addZero) {   // vertex vb: L += beta * Le, then L += beta * (nLights * 0)
         const float *Ls = S.spectra + (la.emitOff >= 0 ? la.emitOff : 0);
 #pragma unroll
         for (int q = 0; q < NQ; ++q) {
-            const float4 bt = beta[q * c];
-            if (la.emit) {
+            const float4 bt = beta_ld<NB>(P, vb, slot, q);
+            if (addEmit) {
                 const float4 e = la.emitOff >= 0 ? ld4(Ls + 4 * q) : make_float4(0.f, 0.f, 0.f, 0.f);
                 L[q].x += bt.x * e.x; L[q].y += bt.y * e.y; L[q].z += bt.z * e.z; L[q].w += bt.w * e.w;
             }
-            if (la.zero) { L[q].x += bt.x * 0.f; L[q].y += bt.y * 0.f; L[q].z += bt.z * 0.f; L[q].w += bt.w * 0.f; }
+            if (addZero) { L[q].x += bt.x * 0.f; L[q].y += bt.y * 0.f; L[q].z += bt.z * 0.f; L[q].w += bt.w * 0.f; }
         }
     }
-    if (esc == 1) {
+    if (addEsc && esc == 1) {
         // SamplerRenderer::Li (samplerrenderer.cpp:237-240): Li = sum of the lights' Le, zero
         // for area and point lights
         if ((FEAT & FEAT_INF) && S.nInf > 0) {
@@ -721,9 +745,8 @@ PGD_INLINE Pushes shade_slot(const DevScene &S, const PathSoA &P, int slot, floa
                     }
                 }
         }
-    } else if (esc == 2) {
+    } else if (addEsc && esc == 2) {
         // path.cpp:92-96: L += beta * Le(ray) for every light
-        const float4 *beta = beta_of<NB>(P, vb, slot);
         V d = v3(0.f, 0.f, 0.f);
         if ((FEAT & FEAT_INF) && S.nInf > 0) d = ray_load(P, RAY_C, slot).d;
         for (int l = 0; l < S.nLights; ++l) {
@@ -732,17 +755,16 @@ PGD_INLINE Pushes shade_slot(const DevScene &S, const PathSoA &P, int slot, floa
             if ((FEAT & FEAT_INF) && S.lights[l].type == PBRTGPU_LIGHT_INFINITE) e = inf_Le(S.lights[l], d);
 #pragma unroll
             for (int q = 0; q < NQ; ++q) {
-                float4 bt = beta[q * c], v = emit4<FEAT>(S, e, q);
+                float4 bt = beta_ld<NB>(P, vb, slot, q), v = emit4<FEAT>(S, e, q);
                 L[q].x += bt.x * v.x; L[q].y += bt.y * v.y; L[q].z += bt.z * v.z; L[q].w += bt.w * v.w;
             }
         }
     }
-    *done = !(fl & (PF_CONT | PF_PEND));
-    *zeroed = false;
     if (*done) *zeroed = path_output<NB>(S, L, Lout, P.item[slot]);
     else {
 #pragma unroll
         for (int q = 0; q < NQ; ++q) P.L[q * c + slot] = L[q];
+        fl &= ~PF_LZ;
     }
     P.flags[slot] = fl;
     PGD_T1(OUT);
