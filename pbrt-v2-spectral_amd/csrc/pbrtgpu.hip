@@ -51,7 +51,13 @@ static int fail(int code, const std::string &msg) { g_err = msg; return code; }
 
 // ------------------------------------------------------------------ kernels
 static const int kTraceBlock = 128;
-static const int kStackLDS = 16;   // k_trace_pt: traversal-stack entries per lane kept in LDS (power of two)
+#ifndef PGD_STACK_LDS
+#define PGD_STACK_LDS 8   // C2: 8 -> closest 161 -> 145 ms/frame vs 16 (r01m ablation)
+#endif
+static const int kStackLDS = PGD_STACK_LDS;   // k_trace_pt: traversal-stack entries per lane kept in LDS (power of two)
+#ifndef PGD_TRACE_ATTR   // occupancy experiments (tools/build_exp.sh)
+#define PGD_TRACE_ATTR
+#endif
 
 // closest-hit queries of one pass (BVHAccel::Intersect, bvh.cpp:380-432): persistent grid,
 // one ray per lane per iteration, LDS traversal stack (column per lane)
@@ -121,7 +127,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_shadow(DevScene S, PathSo
 // then, if the lane stands on a leaf, that leaf's primitives.  Per ray the nodes visited,
 // primitives tested and their order are bvh_walk's.
 template <bool ANY, bool STATS>
-__global__ __launch_bounds__(kTraceBlock) void k_trace_pt(DevScene S, PathSoA P, int q, int refill, int ring, uint2 *__restrict__ spill) {
+__global__ __launch_bounds__(kTraceBlock) PGD_TRACE_ATTR void k_trace_pt(DevScene S, PathSoA P, int q, int refill, int ring, uint2 *__restrict__ spill) {
     // traversal stack: the top kStackLDS entries of each lane in LDS (a ring, column per
     // lane: refs, then entry distances), deeper entries in the lane's spill area in HBM
     __shared__ uint32_t sref[kStackLDS * kTraceBlock];
@@ -142,6 +148,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_pt(DevScene S, PathSoA P,
     Ray ray;
     V invDir = v3(0.f, 0.f, 0.f);
     int neg[3] = {0, 0, 0};
+    uint32_t negMask = 0;
     uint32_t nM = 0, hM = 0;
     for (;;) {
         const unsigned long long idle = __ballot(!active);
@@ -156,6 +163,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_pt(DevScene S, PathSoA P,
                     ray = ray_load(P, kind, slot);
                     invDir = v3(1.f / ray.d.x, 1.f / ray.d.y, 1.f / ray.d.z);
                     neg[0] = invDir.x < 0; neg[1] = invDir.y < 0; neg[2] = invDir.z < 0;
+                    negMask = (uint32_t)neg[0] | ((uint32_t)neg[1] << 1) | ((uint32_t)neg[2] << 2);
                     prim = -1;
                     thit = INFINITY;
                     todo = 0;
@@ -189,7 +197,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_pt(DevScene S, PathSoA P,
                 const bool hl = slab_enter(l0, l1, ray, invDir, neg, &tl) && tl < ray.maxt;
                 const bool hr = slab_enter(r0, r1, ray, invDir, neg, &tr) && tr < ray.maxt;
                 const uint32_t refL = __float_as_uint(l0.w), refR = __float_as_uint(l1.w);
-                const bool swap = neg[__float_as_uint(r0.w)] != 0;
+                const bool swap = ((negMask >> __float_as_uint(r0.w)) & 1u) != 0;   // no indexed private array
                 const bool hn = swap ? hr : hl, hf = swap ? hl : hr;
                 const uint32_t rn = swap ? refR : refL, rf = swap ? refL : refR;
                 if (hn) {
@@ -403,7 +411,7 @@ template <class T> static hipError_t upload(pbrtgpu_ctx *c, const T *src, size_t
 static int slot_target() {
     const char *e = getenv("PBRTGPU_SLOTS");
     int v = e ? atoi(e) : 0;
-    return v > 0 ? v : (1 << 21);
+    return v > 0 ? v : (1 << 22);   // 4 M slots (C2: 2 M -> 4 M shortens the per-pass tails, 228 -> 236 Mpaths/s)
 }
 
 static int ensure_slots(pbrtgpu_ctx *c, int cap, int NB) {

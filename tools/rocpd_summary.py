@@ -64,16 +64,21 @@ def main():
         print("\n".join(pl))
         out = {"source": "%s: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of bench.py --steps 1 --warmup 0; "
                           "FETCH_SIZE x2 (gfx950 correction, MI355X_MICROARCH.md) + WRITE_SIZE" % tag}
-        for k in ("k_trace_closest<false>", "k_trace_shadow<false>", "k_shade<32>"):
-            fetch = pm.get((k, "FETCH_SIZE"))
-            write = pm.get((k, "WRITE_SIZE"))
+        # timing names of pbrtgpu_last_timing <- device kernel names (the uninstrumented
+        # template instances a bench frame runs)
+        names = {"k_trace_closest": ("k_trace_pt<false, false>", "k_trace_closest<false, false>"),
+                 "k_trace_shadow": ("k_trace_pt<true, false>", "k_trace_shadow<false, false>"),
+                 "k_shade": tuple(sorted({kk for kk, _ in pm if kk.split("<")[0].endswith("k_shade")}))}
+        for k, srcs in names.items():
+            fetch = [x for s in srcs for x in pm.get((s, "FETCH_SIZE"), [])]
+            write = [x for s in srcs for x in pm.get((s, "WRITE_SIZE"), [])]
             if not fetch or not write:
                 continue
             # one frame was rendered per pass: total over its launches / launches
             fb = sum(fetch) * 1024.0
             wb = sum(write) * 1024.0
             n = len(fetch)
-            out[k.split("<")[0]] = {"res": 700, "spp": 256, "launches": n, "fetch_bytes_raw_per_launch": fb / n,
+            out[k] = {"res": 700, "spp": 256, "launches": n, "fetch_bytes_raw_per_launch": fb / n,
                                     "write_bytes_per_launch": wb / len(write),
                                     "hbm_bytes_per_launch": (2.0 * fb + wb) / n}
         json.dump(out, open(os.path.join(prof, "hbm_traffic.json"), "w"), indent=1)
