@@ -59,7 +59,7 @@ def shade_bytes(work, paths, bands):
     per_cont = S + 36 + 4                                  # beta_{b+1}, ray, queue entry
     per_shadow = S + 36 + 4 + S                            # A write, ray, queue, A read at finish
     per_mis = S + 36 + 4 + S + 8                           # B write, ray, queue, B read, hit
-    per_cam = 2 * S + 36 + 4 + slot_state                  # L, beta init, camera ray
+    per_cam = 36 + 4 + slot_state                          # camera ray (L = 0, beta = 1 implicit)
     per_out = S
     return (verts * per_vertex + cont * per_cont + work["shadow_rays"] * per_shadow
             + work["mis_rays"] * per_mis + cams * (per_cam + per_out))
