@@ -50,7 +50,10 @@ static int fail(int code, const std::string &msg) { g_err = msg; return code; }
 
 
 // ------------------------------------------------------------------ kernels
-static const int kTraceBlock = 128;
+#ifndef PGD_TRACE_BLOCK
+#define PGD_TRACE_BLOCK 128
+#endif
+static const int kTraceBlock = PGD_TRACE_BLOCK;
 #ifndef PGD_STACK_LDS
 #define PGD_STACK_LDS 8   // C2: 8 -> closest 161 -> 145 ms/frame vs 16 (r01m ablation)
 #endif
@@ -376,7 +379,9 @@ struct Timing {
 struct pbrtgpu_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
+    hipStream_t stream2 = nullptr;   // shadow queries beside the closest-hit queries
     hipEvent_t ev[8] = {};
+    hipEvent_t pev[6 * 4] = {};      // per-pass events of one batch of run_wavefront passes
     bool hasScene = false;
     DevScene S{};
     int nb = 0, spp = 0, stackDepth = 0;
@@ -452,6 +457,7 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
     HIPCHK(hipMemsetAsync(P.cnt, 0, CNT_WORDS * 4, c->stream));
     // LDS stack: child refs and (closest-hit) entry distances, one column per lane
     const size_t ldsS = (size_t)c->stackDepth * kTraceBlock * sizeof(uint32_t), lds = 2 * ldsS;
+    static const int kPassBatch = 4;
     const int perCU = std::max(1, std::min(16, (int)(160 * 1024 / std::max<size_t>(lds, 1))));
     const int traceGrid = c->numCUs * perCU;
     const int shadeGrid = (cap + kShadeBlock - 1) / kShadeBlock;
@@ -463,71 +469,77 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
     auto kShade = c->feat ? launch_shade<NB, FEAT_ALL> : launch_shade<NB, 0>;
     HIPCHK(kShade(shadeGrid, c->stream, c->S, P, src, q, Lout));
     HIPCHK(hipEventRecord(c->ev[5], c->stream));
-    bool pending = false;   // events ev[0..3] of the previous pass still to be read
+    // Passes are enqueued kPassBatch at a time between counter read-backs: the kernels read
+    // their queue sizes on the device, and passes after the queues have drained are empty
+    // launches.  The shadow queries run on a second stream beside the closest-hit queries
+    // (their tails overlap); shade waits for both.
+    const bool inst = c->S.nInsts > 0;
+    if (!c->ptBlocksPerCU) {   // resident blocks of the persistent kernels (registers, LDS)
+        int b0 = 0, b1 = 0;
+        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&b0, k_trace_pt<false, false>, kTraceBlock, 0));
+        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&b1, k_trace_pt<true, false>, kTraceBlock, 0));
+        c->ptBlocksPerCU = std::max(1, std::min(b0, b1));
+    }
+    const uint32_t ptGrid = (uint32_t)(c->numCUs * c->ptBlocksPerCU);
+    const size_t spillLane = (size_t)ptGrid * kTraceBlock * c->stackDepth;   // uint2 per kernel
+    HIPCHK(c->spill.ensure(2 * spillLane * sizeof(uint2)));
+    uint2 *spillC = (uint2 *)c->spill.p, *spillS = spillC + spillLane;
+    int batch = 0;   // passes of the last batch whose events are still to be read
     float m;
     for (;;) {
         HIPCHK(hipMemcpyAsync(c->hostCnt, P.cnt, CNT_WORK * 4, hipMemcpyDeviceToHost, c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
-        if (pending) {
-            HIPCHK(hipEventElapsedTime(&m, c->ev[0], c->ev[1])); T.ms[K_CLOSEST] += m;
-            HIPCHK(hipEventElapsedTime(&m, c->ev[1], c->ev[2])); T.ms[K_SHADOW] += m;
-            HIPCHK(hipEventElapsedTime(&m, c->ev[2], c->ev[3])); T.ms[K_SHADE] += m;
-        } else {
+        if (batch == 0) {
             HIPCHK(hipEventElapsedTime(&m, c->ev[4], c->ev[5])); T.ms[K_SHADE] += m;
             T.launches[K_SHADE]++;
+        }
+        for (int j = 0; j < batch; ++j) {
+            hipEvent_t *e = c->pev + 6 * j;
+            HIPCHK(hipEventElapsedTime(&m, e[0], e[1])); T.ms[K_CLOSEST] += m;
+            HIPCHK(hipEventElapsedTime(&m, e[2], e[3])); T.ms[K_SHADOW] += m;
+            HIPCHK(hipEventElapsedTime(&m, e[4], e[5])); T.ms[K_SHADE] += m;
         }
         const uint32_t nC = c->hostCnt[CNT_QC(q)], nS = c->hostCnt[CNT_QS(q)];
         if (nC == 0 && nS == 0) break;
         if (T.passes > 4096) return fail(PBRTGPU_E_STATE, "wavefront did not drain");
-        const int nq = q ^ 1;
-        HIPCHK(hipMemsetAsync(P.cnt + CNT_QC(nq), 0, 4, c->stream));
-        HIPCHK(hipMemsetAsync(P.cnt + CNT_QS(nq), 0, 4, c->stream));
-        HIPCHK(hipEventRecord(c->ev[0], c->stream));
-        const bool inst = c->S.nInsts > 0;
-        // instanced scenes walk nested BVHs (bvh_walk); the others run the persistent
-        // ray-replacement kernels over the whole (wave-partitioned) queue
-        if (!c->ptBlocksPerCU) {   // resident blocks of the persistent kernels (registers, LDS)
-            int b0 = 0, b1 = 0;
-            HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&b0, k_trace_pt<false, false>, kTraceBlock, 0));
-            HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&b1, k_trace_pt<true, false>, kTraceBlock, 0));
-            c->ptBlocksPerCU = std::max(1, std::min(b0, b1));
-        }
-        const uint32_t ptGrid = (uint32_t)(c->numCUs * c->ptBlocksPerCU);
-        HIPCHK(c->spill.ensure((size_t)ptGrid * kTraceBlock * c->stackDepth * sizeof(uint2)));
-        int gC = (int)std::min<uint32_t>((nC + kTraceBlock - 1) / kTraceBlock, (uint32_t)traceGrid);
-        if (gC > 0) {
+        batch = kPassBatch;
+        for (int j = 0; j < batch; ++j) {
+            hipEvent_t *e = c->pev + 6 * j;
+            const int nq = q ^ 1;
+            HIPCHK(hipMemsetAsync(P.cnt + CNT_QC(nq), 0, 4, c->stream));
+            HIPCHK(hipMemsetAsync(P.cnt + CNT_QS(nq), 0, 4, c->stream));
+            HIPCHK(hipEventRecord(e[0], c->stream));
+            // shadow queries of queue set q on stream2, after the counter resets
+            HIPCHK(hipStreamWaitEvent(c->stream2, e[0], 0));
+            HIPCHK(hipEventRecord(e[2], c->stream2));
+            // instanced scenes walk nested BVHs (bvh_walk); the others run the persistent
+            // ray-replacement kernels over the whole (wave-partitioned) queue
             if (inst) {
-                if (countWork) hipLaunchKernelGGL((k_trace_closest<true, true>), dim3(gC), dim3(kTraceBlock), lds, c->stream, c->S, P, q);
-                else hipLaunchKernelGGL((k_trace_closest<false, true>), dim3(gC), dim3(kTraceBlock), lds, c->stream, c->S, P, q);
+                if (countWork) hipLaunchKernelGGL((k_trace_closest<true, true>), dim3(traceGrid), dim3(kTraceBlock), lds, c->stream, c->S, P, q);
+                else hipLaunchKernelGGL((k_trace_closest<false, true>), dim3(traceGrid), dim3(kTraceBlock), lds, c->stream, c->S, P, q);
+                HIPCHK(hipGetLastError());
+                if (countWork) hipLaunchKernelGGL((k_trace_shadow<true, true>), dim3(traceGrid), dim3(kTraceBlock), ldsS, c->stream2, c->S, P, q);
+                else hipLaunchKernelGGL((k_trace_shadow<false, true>), dim3(traceGrid), dim3(kTraceBlock), ldsS, c->stream2, c->S, P, q);
             } else {
-                const uint32_t g = std::min<uint32_t>(ptGrid, (nC + 63) / 64 * 64 / kTraceBlock + 1);
-                if (countWork) hipLaunchKernelGGL((k_trace_pt<false, true>), dim3(g), dim3(kTraceBlock), 0, c->stream, c->S, P, q, c->refill, c->ring, (uint2 *)c->spill.p);
-                else hipLaunchKernelGGL((k_trace_pt<false, false>), dim3(g), dim3(kTraceBlock), 0, c->stream, c->S, P, q, c->refill, c->ring, (uint2 *)c->spill.p);
+                if (countWork) hipLaunchKernelGGL((k_trace_pt<false, true>), dim3(ptGrid), dim3(kTraceBlock), 0, c->stream, c->S, P, q, c->refill, c->ring, spillC);
+                else hipLaunchKernelGGL((k_trace_pt<false, false>), dim3(ptGrid), dim3(kTraceBlock), 0, c->stream, c->S, P, q, c->refill, c->ring, spillC);
+                HIPCHK(hipGetLastError());
+                if (countWork) hipLaunchKernelGGL((k_trace_pt<true, true>), dim3(ptGrid), dim3(kTraceBlock), 0, c->stream2, c->S, P, q, c->refill, c->ring, spillS);
+                else hipLaunchKernelGGL((k_trace_pt<true, false>), dim3(ptGrid), dim3(kTraceBlock), 0, c->stream2, c->S, P, q, c->refill, c->ring, spillS);
             }
             HIPCHK(hipGetLastError());
             T.launches[K_CLOSEST]++;
-        }
-        HIPCHK(hipEventRecord(c->ev[1], c->stream));
-        int gS = (int)std::min<uint32_t>((nS + kTraceBlock - 1) / kTraceBlock, (uint32_t)traceGrid);
-        if (gS > 0) {
-            if (inst) {
-                if (countWork) hipLaunchKernelGGL((k_trace_shadow<true, true>), dim3(gS), dim3(kTraceBlock), ldsS, c->stream, c->S, P, q);
-                else hipLaunchKernelGGL((k_trace_shadow<false, true>), dim3(gS), dim3(kTraceBlock), ldsS, c->stream, c->S, P, q);
-            } else {
-                const uint32_t g = std::min<uint32_t>(ptGrid, (nS + 63) / 64 * 64 / kTraceBlock + 1);
-                if (countWork) hipLaunchKernelGGL((k_trace_pt<true, true>), dim3(g), dim3(kTraceBlock), 0, c->stream, c->S, P, q, c->refill, c->ring, (uint2 *)c->spill.p);
-                else hipLaunchKernelGGL((k_trace_pt<true, false>), dim3(g), dim3(kTraceBlock), 0, c->stream, c->S, P, q, c->refill, c->ring, (uint2 *)c->spill.p);
-            }
-            HIPCHK(hipGetLastError());
             T.launches[K_SHADOW]++;
+            HIPCHK(hipEventRecord(e[1], c->stream));
+            HIPCHK(hipEventRecord(e[3], c->stream2));
+            HIPCHK(hipStreamWaitEvent(c->stream, e[3], 0));
+            HIPCHK(hipEventRecord(e[4], c->stream));
+            HIPCHK(kShade(shadeGrid, c->stream, c->S, P, src, nq, Lout));
+            T.launches[K_SHADE]++;
+            HIPCHK(hipEventRecord(e[5], c->stream));
+            T.passes++;
+            q = nq;
         }
-        HIPCHK(hipEventRecord(c->ev[2], c->stream));
-        HIPCHK(kShade(shadeGrid, c->stream, c->S, P, src, nq, Lout));
-        T.launches[K_SHADE]++;
-        HIPCHK(hipEventRecord(c->ev[3], c->stream));
-        pending = true;
-        T.passes++;
-        q = nq;
     }
     uint64_t w[W_COUNT];
     HIPCHK(hipMemcpy(w, P.cnt + CNT_WORK, sizeof(w), hipMemcpyDeviceToHost));
@@ -603,7 +615,9 @@ int pbrtgpu_context_create(int device, pbrtgpu_ctx **out) {
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->numCUs = prop.multiProcessorCount;
     bool ok = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess;
+    ok = ok && hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) == hipSuccess;
     for (int i = 0; i < 8 && ok; ++i) ok = hipEventCreate(&c->ev[i]) == hipSuccess;
+    for (int i = 0; i < 24 && ok; ++i) ok = hipEventCreate(&c->pev[i]) == hipSuccess;
     ok = ok && hipHostMalloc((void **)&c->hostCnt, CNT_WORDS * 4, hipHostMallocDefault) == hipSuccess;
     if (!ok) {
         delete c;
@@ -623,6 +637,8 @@ int pbrtgpu_context_destroy(pbrtgpu_ctx *c) {
                       &c->scratch[1], &c->scratch[2], &c->slots, &c->spill};
     for (DevBuf *b : bufs) b->release();
     for (int i = 0; i < 8; ++i) if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
+    for (int i = 0; i < 24; ++i) if (c->pev[i]) (void)hipEventDestroy(c->pev[i]);
+    if (c->stream2) (void)hipStreamDestroy(c->stream2);
     if (c->hostCnt) (void)hipHostFree(c->hostCnt);
     (void)hipStreamDestroy(c->stream);
     delete c;

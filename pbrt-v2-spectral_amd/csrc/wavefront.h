@@ -771,7 +771,10 @@ PGD_INLINE Pushes shade_slot(const DevScene &S, const PathSoA &P, int slot, floa
     return out;
 }
 
-static const int kShadeBlock = 256;
+#ifndef PGD_SHADE_BLOCK
+#define PGD_SHADE_BLOCK 256
+#endif
+static const int kShadeBlock = PGD_SHADE_BLOCK;
 // k_shade<NB, FEAT> launch (defined in shade.hip, one translation unit per variant)
 template <int NB, int FEAT>
 hipError_t launch_shade(int grid, hipStream_t stream, const DevScene &S, const PathSoA &P, const ItemSrc &src, int qout,
