@@ -50,6 +50,9 @@ static int fail(int code, const std::string &msg) { g_err = msg; return code; }
 
 
 // ------------------------------------------------------------------ kernels
+#ifndef PGD_PASS_BATCH   // wavefront passes enqueued per counter read-back (<= 8)
+#define PGD_PASS_BATCH 4
+#endif
 #ifndef PGD_TRACE_BLOCK
 #define PGD_TRACE_BLOCK 128
 #endif
@@ -381,7 +384,7 @@ struct pbrtgpu_ctx {
     hipStream_t stream = nullptr;
     hipStream_t stream2 = nullptr;   // shadow queries beside the closest-hit queries
     hipEvent_t ev[8] = {};
-    hipEvent_t pev[6 * 4] = {};      // per-pass events of one batch of run_wavefront passes
+    hipEvent_t pev[6 * 8] = {};      // per-pass events of one batch of run_wavefront passes
     bool hasScene = false;
     DevScene S{};
     int nb = 0, spp = 0, stackDepth = 0;
@@ -457,7 +460,7 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
     HIPCHK(hipMemsetAsync(P.cnt, 0, CNT_WORDS * 4, c->stream));
     // LDS stack: child refs and (closest-hit) entry distances, one column per lane
     const size_t ldsS = (size_t)c->stackDepth * kTraceBlock * sizeof(uint32_t), lds = 2 * ldsS;
-    static const int kPassBatch = 4;
+    static const int kPassBatch = PGD_PASS_BATCH;
     const int perCU = std::max(1, std::min(16, (int)(160 * 1024 / std::max<size_t>(lds, 1))));
     const int traceGrid = c->numCUs * perCU;
     const int shadeGrid = (cap + kShadeBlock - 1) / kShadeBlock;
@@ -617,7 +620,7 @@ int pbrtgpu_context_create(int device, pbrtgpu_ctx **out) {
     bool ok = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess;
     ok = ok && hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) == hipSuccess;
     for (int i = 0; i < 8 && ok; ++i) ok = hipEventCreate(&c->ev[i]) == hipSuccess;
-    for (int i = 0; i < 24 && ok; ++i) ok = hipEventCreate(&c->pev[i]) == hipSuccess;
+    for (int i = 0; i < 48 && ok; ++i) ok = hipEventCreate(&c->pev[i]) == hipSuccess;
     ok = ok && hipHostMalloc((void **)&c->hostCnt, CNT_WORDS * 4, hipHostMallocDefault) == hipSuccess;
     if (!ok) {
         delete c;
@@ -637,7 +640,7 @@ int pbrtgpu_context_destroy(pbrtgpu_ctx *c) {
                       &c->scratch[1], &c->scratch[2], &c->slots, &c->spill};
     for (DevBuf *b : bufs) b->release();
     for (int i = 0; i < 8; ++i) if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
-    for (int i = 0; i < 24; ++i) if (c->pev[i]) (void)hipEventDestroy(c->pev[i]);
+    for (int i = 0; i < 48; ++i) if (c->pev[i]) (void)hipEventDestroy(c->pev[i]);
     if (c->stream2) (void)hipStreamDestroy(c->stream2);
     if (c->hostCnt) (void)hipHostFree(c->hostCnt);
     (void)hipStreamDestroy(c->stream);
