@@ -382,12 +382,24 @@ struct Timing {
     uint64_t work[W_COUNT] = {0};
 };
 
+// One wavefront instance: path slots, queues and counters, its two streams (closest-hit
+// queries + shading; shadow queries beside them) and the events of one batch of passes.
+struct Lane {
+    DevBuf slots;            // PathSoA storage
+    DevBuf spill;            // k_trace_pt stack spill areas (closest, shadow)
+    int slotCap = 0, slotNb = 0;
+    PathSoA P{};
+    hipStream_t s = nullptr, s2 = nullptr;
+    hipEvent_t ev[2 + 6 * 8] = {};
+    uint32_t *hostCnt = nullptr;   // pinned mirror of the queue counters
+};
+static const int kLanes = 2;
+
 struct pbrtgpu_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
-    hipStream_t stream2 = nullptr;   // shadow queries beside the closest-hit queries
     hipEvent_t ev[8] = {};
-    hipEvent_t pev[6 * 8] = {};      // per-pass events of one batch of run_wavefront passes
+    Lane lane[kLanes];       // lane[0].s is `stream`
     bool hasScene = false;
     DevScene S{};
     int nb = 0, spp = 0, stackDepth = 0;
@@ -395,11 +407,6 @@ struct pbrtgpu_ctx {
     pbrtgpu_camera cam{};
     std::vector<DevBuf> sceneBufs;
     DevBuf film, Lbuf, pix, filmIdx, mask, keys, counter, spillL, lists[4], scratch[3];
-    DevBuf slots;            // PathSoA storage
-    DevBuf spill;            // k_trace_pt stack spill areas (persistent lanes x stack depth)
-    int slotCap = 0, slotNb = 0;
-    PathSoA P{};
-    uint32_t *hostCnt = nullptr;   // pinned mirror of the queue counters
     int numCUs = 256;
     int ptBlocksPerCU = 0;    // occupancy of k_trace_pt (computed on first use)
     int ring = kStackLDS;     // LDS ring entries in use (PBRTGPU_STACK_LDS: tests force HBM spills)
@@ -422,10 +429,10 @@ template <class T> static hipError_t upload(pbrtgpu_ctx *c, const T *src, size_t
 static int slot_target() {
     const char *e = getenv("PBRTGPU_SLOTS");
     int v = e ? atoi(e) : 0;
-    return v > 0 ? v : (1 << 22);   // 4 M slots (C2: 2 M -> 4 M shortens the per-pass tails, 228 -> 236 Mpaths/s)
+    return v > 0 ? v : (1 << 23);   // 8 M slots = 2 lanes x 4 M (C2 r01p: 289 -> 301 Mpaths/s vs 2 x 2 M)
 }
 
-static int ensure_slots(pbrtgpu_ctx *c, int cap, int NB) {
+static int ensure_slots(Lane *c, int cap, int NB) {
     if (c->slotCap == cap && c->slotNb == NB) return 0;
     const size_t C = (size_t)cap;
     const int NBP = (NB + 3) / 4 * 4;   // bands padded to whole float4 quads
@@ -452,33 +459,21 @@ static int ensure_slots(pbrtgpu_ctx *c, int cap, int NB) {
 }
 
 // Runs every item of src through the wavefront pipeline; radiance of item i -> Lout[i][NB].
+// The items are split into kLanes independent halves, each run by its own lane (slots,
+// queues, streams), so one lane's shading overlaps the other's ray queries.  Within a lane,
+// passes are enqueued kPassBatch at a time between counter read-backs: the kernels read
+// their queue sizes on the device, and passes after the queues have drained are empty
+// launches.  The shadow queries run on the lane's second stream beside the closest-hit
+// queries (their tails overlap); shade waits for both.
 template <int NB>
 static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool countWork, Timing &T,
                          unsigned int *zeroedOut) {
     if (src.nItems == 0) return 0;
-    const int cap = (int)std::min<uint32_t>(src.nItems, (uint32_t)slot_target());
-    if (int e = ensure_slots(c, cap, NB)) return e;
-    PathSoA &P = c->P;
-    HIPCHK(hipMemsetAsync(P.item, 0xff, (size_t)cap * 4, c->stream));
-    HIPCHK(hipMemsetAsync(P.cnt, 0, CNT_WORDS * 4, c->stream));
-    // LDS stack: child refs and (closest-hit) entry distances, one column per lane
-    const size_t ldsS = (size_t)c->stackDepth * kTraceBlock * sizeof(uint32_t), lds = 2 * ldsS;
     static const int kPassBatch = PGD_PASS_BATCH;
+    // LDS stack of the instanced-scene kernels: child refs and (closest-hit) entry distances
+    const size_t ldsS = (size_t)c->stackDepth * kTraceBlock * sizeof(uint32_t), lds = 2 * ldsS;
     const int perCU = std::max(1, std::min(16, (int)(160 * 1024 / std::max<size_t>(lds, 1))));
     const int traceGrid = c->numCUs * perCU;
-    const int shadeGrid = (cap + kShadeBlock - 1) / kShadeBlock;
-    int q = 0;
-    // pass 0: every slot is free -> regeneration fills them with camera rays (queue 0)
-    HIPCHK(hipEventRecord(c->ev[4], c->stream));
-    // scenes without measured BRDFs, textures and environment lights run the variant with
-    // that code compiled out (fewer registers, no kd-tree stack)
-    auto kShade = c->feat ? launch_shade<NB, FEAT_ALL> : launch_shade<NB, 0>;
-    HIPCHK(kShade(shadeGrid, c->stream, c->S, P, src, q, Lout));
-    HIPCHK(hipEventRecord(c->ev[5], c->stream));
-    // Passes are enqueued kPassBatch at a time between counter read-backs: the kernels read
-    // their queue sizes on the device, and passes after the queues have drained are empty
-    // launches.  The shadow queries run on a second stream beside the closest-hit queries
-    // (their tails overlap); shade waits for both.
     const bool inst = c->S.nInsts > 0;
     if (!c->ptBlocksPerCU) {   // resident blocks of the persistent kernels (registers, LDS)
         int b0 = 0, b1 = 0;
@@ -488,70 +483,111 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
     }
     const uint32_t ptGrid = (uint32_t)(c->numCUs * c->ptBlocksPerCU);
     const size_t spillLane = (size_t)ptGrid * kTraceBlock * c->stackDepth;   // uint2 per kernel
-    HIPCHK(c->spill.ensure(2 * spillLane * sizeof(uint2)));
-    uint2 *spillC = (uint2 *)c->spill.p, *spillS = spillC + spillLane;
-    int batch = 0;   // passes of the last batch whose events are still to be read
+    // scenes without measured BRDFs, textures and environment lights run the variant with
+    // that code compiled out (fewer registers, no kd-tree stack)
+    auto kShade = c->feat ? launch_shade<NB, FEAT_ALL> : launch_shade<NB, 0>;
+    struct Run { Lane *L; ItemSrc src; int cap, grid, q, batch; bool done; };
+    Run R[kLanes];
+    const int nl = src.nItems >= 8192u ? kLanes : 1;
+    HIPCHK(hipEventRecord(c->ev[0], c->stream));   // the other lanes start after the work queued so far
+    for (int l = 0; l < nl; ++l) {
+        Run &r = R[l];
+        Lane &L = c->lane[l];
+        r.L = &L;
+        r.src = src;
+        const uint32_t lo = (uint32_t)((uint64_t)src.nItems * l / nl), hi = (uint32_t)((uint64_t)src.nItems * (l + 1) / nl);
+        r.src.base = src.base + lo;
+        r.src.nItems = hi - lo;
+        r.cap = (int)std::min<uint32_t>(r.src.nItems, (uint32_t)std::max(64, slot_target() / nl));
+        r.grid = (r.cap + kShadeBlock - 1) / kShadeBlock;
+        r.q = 0;
+        r.batch = 0;
+        r.done = false;
+        if (int e = ensure_slots(&L, r.cap, NB)) return e;
+        HIPCHK(L.spill.ensure(2 * spillLane * sizeof(uint2)));
+        if (l > 0) HIPCHK(hipStreamWaitEvent(L.s, c->ev[0], 0));
+        HIPCHK(hipMemsetAsync(L.P.item, 0xff, (size_t)r.cap * 4, L.s));
+        HIPCHK(hipMemsetAsync(L.P.cnt, 0, CNT_WORDS * 4, L.s));
+        // pass 0: every slot is free -> regeneration fills them with camera rays (queue 0)
+        HIPCHK(hipEventRecord(L.ev[0], L.s));
+        HIPCHK(kShade(r.grid, L.s, c->S, L.P, r.src, 0, Lout));
+        HIPCHK(hipEventRecord(L.ev[1], L.s));
+        HIPCHK(hipMemcpyAsync(L.hostCnt, L.P.cnt, CNT_WORK * 4, hipMemcpyDeviceToHost, L.s));
+    }
+    int live = nl;
     float m;
-    for (;;) {
-        HIPCHK(hipMemcpyAsync(c->hostCnt, P.cnt, CNT_WORK * 4, hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(hipStreamSynchronize(c->stream));
-        if (batch == 0) {
-            HIPCHK(hipEventElapsedTime(&m, c->ev[4], c->ev[5])); T.ms[K_SHADE] += m;
-            T.launches[K_SHADE]++;
-        }
-        for (int j = 0; j < batch; ++j) {
-            hipEvent_t *e = c->pev + 6 * j;
-            HIPCHK(hipEventElapsedTime(&m, e[0], e[1])); T.ms[K_CLOSEST] += m;
-            HIPCHK(hipEventElapsedTime(&m, e[2], e[3])); T.ms[K_SHADOW] += m;
-            HIPCHK(hipEventElapsedTime(&m, e[4], e[5])); T.ms[K_SHADE] += m;
-        }
-        const uint32_t nC = c->hostCnt[CNT_QC(q)], nS = c->hostCnt[CNT_QS(q)];
-        if (nC == 0 && nS == 0) break;
-        if (T.passes > 4096) return fail(PBRTGPU_E_STATE, "wavefront did not drain");
-        batch = kPassBatch;
-        for (int j = 0; j < batch; ++j) {
-            hipEvent_t *e = c->pev + 6 * j;
-            const int nq = q ^ 1;
-            HIPCHK(hipMemsetAsync(P.cnt + CNT_QC(nq), 0, 4, c->stream));
-            HIPCHK(hipMemsetAsync(P.cnt + CNT_QS(nq), 0, 4, c->stream));
-            HIPCHK(hipEventRecord(e[0], c->stream));
-            // shadow queries of queue set q on stream2, after the counter resets
-            HIPCHK(hipStreamWaitEvent(c->stream2, e[0], 0));
-            HIPCHK(hipEventRecord(e[2], c->stream2));
-            // instanced scenes walk nested BVHs (bvh_walk); the others run the persistent
-            // ray-replacement kernels over the whole (wave-partitioned) queue
-            if (inst) {
-                if (countWork) hipLaunchKernelGGL((k_trace_closest<true, true>), dim3(traceGrid), dim3(kTraceBlock), lds, c->stream, c->S, P, q);
-                else hipLaunchKernelGGL((k_trace_closest<false, true>), dim3(traceGrid), dim3(kTraceBlock), lds, c->stream, c->S, P, q);
-                HIPCHK(hipGetLastError());
-                if (countWork) hipLaunchKernelGGL((k_trace_shadow<true, true>), dim3(traceGrid), dim3(kTraceBlock), ldsS, c->stream2, c->S, P, q);
-                else hipLaunchKernelGGL((k_trace_shadow<false, true>), dim3(traceGrid), dim3(kTraceBlock), ldsS, c->stream2, c->S, P, q);
-            } else {
-                if (countWork) hipLaunchKernelGGL((k_trace_pt<false, true>), dim3(ptGrid), dim3(kTraceBlock), 0, c->stream, c->S, P, q, c->refill, c->ring, spillC);
-                else hipLaunchKernelGGL((k_trace_pt<false, false>), dim3(ptGrid), dim3(kTraceBlock), 0, c->stream, c->S, P, q, c->refill, c->ring, spillC);
-                HIPCHK(hipGetLastError());
-                if (countWork) hipLaunchKernelGGL((k_trace_pt<true, true>), dim3(ptGrid), dim3(kTraceBlock), 0, c->stream2, c->S, P, q, c->refill, c->ring, spillS);
-                else hipLaunchKernelGGL((k_trace_pt<true, false>), dim3(ptGrid), dim3(kTraceBlock), 0, c->stream2, c->S, P, q, c->refill, c->ring, spillS);
+    while (live > 0) {
+        for (int l = 0; l < nl; ++l) {
+            Run &r = R[l];
+            if (r.done) continue;
+            Lane &L = *r.L;
+            const PathSoA &P = L.P;
+            HIPCHK(hipStreamSynchronize(L.s));
+            if (r.batch == 0) {
+                HIPCHK(hipEventElapsedTime(&m, L.ev[0], L.ev[1])); T.ms[K_SHADE] += m;
+                T.launches[K_SHADE]++;
             }
-            HIPCHK(hipGetLastError());
-            T.launches[K_CLOSEST]++;
-            T.launches[K_SHADOW]++;
-            HIPCHK(hipEventRecord(e[1], c->stream));
-            HIPCHK(hipEventRecord(e[3], c->stream2));
-            HIPCHK(hipStreamWaitEvent(c->stream, e[3], 0));
-            HIPCHK(hipEventRecord(e[4], c->stream));
-            HIPCHK(kShade(shadeGrid, c->stream, c->S, P, src, nq, Lout));
-            T.launches[K_SHADE]++;
-            HIPCHK(hipEventRecord(e[5], c->stream));
-            T.passes++;
-            q = nq;
+            for (int j = 0; j < r.batch; ++j) {
+                hipEvent_t *e = L.ev + 2 + 6 * j;
+                HIPCHK(hipEventElapsedTime(&m, e[0], e[1])); T.ms[K_CLOSEST] += m;
+                HIPCHK(hipEventElapsedTime(&m, e[2], e[3])); T.ms[K_SHADOW] += m;
+                HIPCHK(hipEventElapsedTime(&m, e[4], e[5])); T.ms[K_SHADE] += m;
+            }
+            int q = r.q;
+            if (L.hostCnt[CNT_QC(q)] == 0 && L.hostCnt[CNT_QS(q)] == 0) {
+                r.done = true;
+                --live;
+                uint64_t w[W_COUNT];
+                HIPCHK(hipMemcpy(w, P.cnt + CNT_WORK, sizeof(w), hipMemcpyDeviceToHost));
+                if (countWork)
+                    for (int i = 0; i < W_COUNT; ++i) T.work[i] += w[i];
+                if (zeroedOut) *zeroedOut += L.hostCnt[CNT_ZEROED];
+                continue;
+            }
+            if (T.passes > 4096) return fail(PBRTGPU_E_STATE, "wavefront did not drain");
+            uint2 *spillC = (uint2 *)L.spill.p, *spillS = spillC + spillLane;
+            r.batch = kPassBatch;
+            for (int j = 0; j < r.batch; ++j) {
+                hipEvent_t *e = L.ev + 2 + 6 * j;
+                const int nq = q ^ 1;
+                HIPCHK(hipMemsetAsync(P.cnt + CNT_QC(nq), 0, 4, L.s));
+                HIPCHK(hipMemsetAsync(P.cnt + CNT_QS(nq), 0, 4, L.s));
+                HIPCHK(hipEventRecord(e[0], L.s));
+                // shadow queries of queue set q on s2, after the counter resets
+                HIPCHK(hipStreamWaitEvent(L.s2, e[0], 0));
+                HIPCHK(hipEventRecord(e[2], L.s2));
+                // instanced scenes walk nested BVHs (bvh_walk); the others run the persistent
+                // ray-replacement kernels over the whole (wave-partitioned) queue
+                if (inst) {
+                    if (countWork) hipLaunchKernelGGL((k_trace_closest<true, true>), dim3(traceGrid), dim3(kTraceBlock), lds, L.s, c->S, P, q);
+                    else hipLaunchKernelGGL((k_trace_closest<false, true>), dim3(traceGrid), dim3(kTraceBlock), lds, L.s, c->S, P, q);
+                    HIPCHK(hipGetLastError());
+                    if (countWork) hipLaunchKernelGGL((k_trace_shadow<true, true>), dim3(traceGrid), dim3(kTraceBlock), ldsS, L.s2, c->S, P, q);
+                    else hipLaunchKernelGGL((k_trace_shadow<false, true>), dim3(traceGrid), dim3(kTraceBlock), ldsS, L.s2, c->S, P, q);
+                } else {
+                    if (countWork) hipLaunchKernelGGL((k_trace_pt<false, true>), dim3(ptGrid), dim3(kTraceBlock), 0, L.s, c->S, P, q, c->refill, c->ring, spillC);
+                    else hipLaunchKernelGGL((k_trace_pt<false, false>), dim3(ptGrid), dim3(kTraceBlock), 0, L.s, c->S, P, q, c->refill, c->ring, spillC);
+                    HIPCHK(hipGetLastError());
+                    if (countWork) hipLaunchKernelGGL((k_trace_pt<true, true>), dim3(ptGrid), dim3(kTraceBlock), 0, L.s2, c->S, P, q, c->refill, c->ring, spillS);
+                    else hipLaunchKernelGGL((k_trace_pt<true, false>), dim3(ptGrid), dim3(kTraceBlock), 0, L.s2, c->S, P, q, c->refill, c->ring, spillS);
+                }
+                HIPCHK(hipGetLastError());
+                T.launches[K_CLOSEST]++;
+                T.launches[K_SHADOW]++;
+                HIPCHK(hipEventRecord(e[1], L.s));
+                HIPCHK(hipEventRecord(e[3], L.s2));
+                HIPCHK(hipStreamWaitEvent(L.s, e[3], 0));
+                HIPCHK(hipEventRecord(e[4], L.s));
+                HIPCHK(kShade(r.grid, L.s, c->S, P, r.src, nq, Lout));
+                T.launches[K_SHADE]++;
+                HIPCHK(hipEventRecord(e[5], L.s));
+                T.passes++;
+                q = nq;
+            }
+            r.q = q;
+            HIPCHK(hipMemcpyAsync(L.hostCnt, P.cnt, CNT_WORK * 4, hipMemcpyDeviceToHost, L.s));
         }
     }
-    uint64_t w[W_COUNT];
-    HIPCHK(hipMemcpy(w, P.cnt + CNT_WORK, sizeof(w), hipMemcpyDeviceToHost));
-    if (countWork)
-        for (int i = 0; i < W_COUNT; ++i) T.work[i] += w[i];
-    if (zeroedOut) *zeroedOut += c->hostCnt[CNT_ZEROED];
     return 0;
 }
 
@@ -621,10 +657,15 @@ int pbrtgpu_context_create(int device, pbrtgpu_ctx **out) {
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->numCUs = prop.multiProcessorCount;
     bool ok = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess;
-    ok = ok && hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) == hipSuccess;
     for (int i = 0; i < 8 && ok; ++i) ok = hipEventCreate(&c->ev[i]) == hipSuccess;
-    for (int i = 0; i < 48 && ok; ++i) ok = hipEventCreate(&c->pev[i]) == hipSuccess;
-    ok = ok && hipHostMalloc((void **)&c->hostCnt, CNT_WORDS * 4, hipHostMallocDefault) == hipSuccess;
+    for (int l = 0; l < kLanes && ok; ++l) {
+        Lane &L = c->lane[l];
+        if (l == 0) L.s = c->stream;
+        else ok = hipStreamCreateWithFlags(&L.s, hipStreamNonBlocking) == hipSuccess;
+        ok = ok && hipStreamCreateWithFlags(&L.s2, hipStreamNonBlocking) == hipSuccess;
+        for (int i = 0; i < 2 + 6 * 8 && ok; ++i) ok = hipEventCreate(&L.ev[i]) == hipSuccess;
+        ok = ok && hipHostMalloc((void **)&L.hostCnt, CNT_WORDS * 4, hipHostMallocDefault) == hipSuccess;
+    }
     if (!ok) {
         delete c;
         return fail(PBRTGPU_E_NODEVICE, "stream/event creation failed");
@@ -640,12 +681,19 @@ int pbrtgpu_context_destroy(pbrtgpu_ctx *c) {
     for (auto &b : c->sceneBufs) b.release();
     DevBuf *bufs[] = {&c->film, &c->Lbuf, &c->pix, &c->filmIdx, &c->mask, &c->keys, &c->counter, &c->spillL,
                       &c->lists[0], &c->lists[1], &c->lists[2], &c->lists[3], &c->scratch[0],
-                      &c->scratch[1], &c->scratch[2], &c->slots, &c->spill};
+                      &c->scratch[1], &c->scratch[2]};
     for (DevBuf *b : bufs) b->release();
     for (int i = 0; i < 8; ++i) if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
-    for (int i = 0; i < 48; ++i) if (c->pev[i]) (void)hipEventDestroy(c->pev[i]);
-    if (c->stream2) (void)hipStreamDestroy(c->stream2);
-    if (c->hostCnt) (void)hipHostFree(c->hostCnt);
+    for (Lane &L : c->lane) {
+        if (L.s && L.s != c->stream) (void)hipStreamSynchronize(L.s);
+        if (L.s2) (void)hipStreamSynchronize(L.s2);
+        L.slots.release();
+        L.spill.release();
+        for (hipEvent_t e : L.ev) if (e) (void)hipEventDestroy(e);
+        if (L.s2) (void)hipStreamDestroy(L.s2);
+        if (L.s && L.s != c->stream) (void)hipStreamDestroy(L.s);
+        if (L.hostCnt) (void)hipHostFree(L.hostCnt);
+    }
     (void)hipStreamDestroy(c->stream);
     delete c;
     return 0;

@@ -91,7 +91,8 @@ struct ItemSrc {
     int sb;             // samples per pixel in this batch
     int s0;             // first sample index
     const int3 *keys;   // explicit (x, y, s) keys instead (trace_paths / spill samples), or null
-    uint32_t nItems;
+    uint32_t nItems;    // items of this run: global items base .. base + nItems - 1
+    uint32_t base;
 };
 
 PGD_INLINE void ray_store(const PathSoA &P, int kind, int slot, const Ray &r) {
@@ -312,7 +313,8 @@ PGD_INLINE void fval_prepare(const DevScene &S, FVal &F, float4 *mb, size_t c) {
 // camera sample of an item -> fresh path in `slot` (SamplerRendererTask::Run,
 // samplerrenderer.cpp:86-108 + the fixed-seed sampler of DESIGN.md §3.1)
 template <int NB>
-PGD_INLINE void path_start(const DevScene &S, const PathSoA &P, const ItemSrc &src, int slot, uint32_t item) {
+PGD_INLINE void path_start(const DevScene &S, const PathSoA &P, const ItemSrc &src, int slot, uint32_t it) {
+    const uint32_t item = src.base + it;
     int px, py;
     uint32_t s;
     if (src.keys) { int3 k = src.keys[item]; px = k.x; py = k.y; s = (uint32_t)k.z; }
