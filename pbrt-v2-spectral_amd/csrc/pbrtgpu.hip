@@ -393,7 +393,10 @@ struct Lane {
     hipEvent_t ev[2 + 6 * 8] = {};
     uint32_t *hostCnt = nullptr;   // pinned mirror of the queue counters
 };
-static const int kLanes = 2;
+#ifndef PGD_LANES
+#define PGD_LANES 2
+#endif
+static const int kLanes = PGD_LANES;
 
 struct pbrtgpu_ctx {
     int device = 0;

@@ -310,6 +310,25 @@ PGD_INLINE void fval_prepare(const DevScene &S, FVal &F, float4 *mb, size_t c) {
         }
 }
 
+// The BSDF-sampled term B of a vertex counts only if the MIS ray's closest hit is a
+// primitive of light Lt (DiffuseAreaLight::L, integrator.cpp:150-160).  A ray that misses
+// every shape of the light -- the hit test BVHAccel runs on them, with maxt = inf, whose
+// hit set contains that of any shorter ray -- cannot reach it: B is never added, so that
+// ray is not traced.  Lights with triangle shapes (or many shapes) are always traced.
+template <int FEAT>
+PGD_INLINE bool mis_may_reach(const DevScene &S, const pbrtgpu_light &Lt, const Ray &r) {
+    if ((FEAT & FEAT_INF) && Lt.type == PBRTGPU_LIGHT_INFINITE) return true;
+    if (Lt.n_shapes > 8) return true;
+    const pbrtgpu_light_shape *shs = S.lightShapes + Lt.shape_offset;
+    for (int i = 0; i < Lt.n_shapes; ++i) {
+        const int ty = shs[i].shape_type;
+        if (ty == PBRTGPU_SHAPE_TRIANGLE) return true;
+        float t;
+        if (quadric_test(S, ty, shs[i].shape_index, r, &t)) return true;
+    }
+    return false;
+}
+
 // camera sample of an item -> fresh path in `slot` (SamplerRendererTask::Run,
 // samplerrenderer.cpp:86-108 + the fixed-seed sampler of DESIGN.md §3.1)
 template <int NB>
@@ -530,7 +549,9 @@ PGD_INLINE Pushes shade_vertex(const DevScene &S, const PathSoA &P, int slot, in
                 } else {
                     eb.mode = Lt.is_black ? EM_BLACK : EM_POOL; eb.off = Lt.spec; eb.div = 1.f; eb.point = false;
                 }
-                if (go && !emit_black<NB, FEAT>(S, eb)) {
+                Ray mr;
+                mr.o = p; mr.d = wi; mr.mint = is.rayEps; mr.maxt = INFINITY; mr.time = ray.time;
+                if (go && !emit_black<NB, FEAT>(S, eb) && mis_may_reach<FEAT>(S, Lt, mr)) {
                     const float ad = fabsf(vdot(wi, n));
                     float4 *B = B_of<NB>(P, vb, slot);
                     bool black = true;
@@ -545,8 +566,6 @@ PGD_INLINE Pushes shade_vertex(const DevScene &S, const PathSoA &P, int slot, in
                         B[q * c] = b;
                     }
                     if (!black) {
-                        Ray mr;
-                        mr.o = p; mr.d = wi; mr.mint = is.rayEps; mr.maxt = INFINITY; mr.time = ray.time;
                         ray_store(P, RAY_M, slot, mr);
                         fl |= PF_PB;
                         out.m = true;
