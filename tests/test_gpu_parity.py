@@ -293,3 +293,23 @@ def test_traversal_stack_spill_and_ray_replacement(pg, killeroo64, dev, monkeypa
     assert np.array_equal(ref.view(np.int32), got.view(np.int32))
     for k in ("rays", "shadow_rays", "nodes_closest", "nodes_shadow", "tris_closest", "tris_shadow", "hits"):
         assert w[k] == w0[k], k
+
+
+@pytest.mark.parametrize("name,exact", [("bunny", True), ("coverage", False)])
+def test_mis_rays_that_can_reach_the_light_are_traced(pg, name, exact):
+    """k_shade skips only MIS rays that miss every shape of the sampled area light
+    (wavefront.h mis_may_reach).  In scenes whose BSDF samples do reach the light some MIS
+    rays are still traced, and per-path radiance stays identical to the oracle, which traces
+    every MIS ray."""
+    from conftest import PACKS
+    scene = pg.Scene.load(os.path.join(PACKS, name + ".pack"), xres=48, yres=32, spp=8)
+    keys = _keys(scene)
+    with pg.Device(0) as d:
+        d.upload(scene)
+        d.render(count_work=True)
+        w = d.timing()["work"]
+        Lg = d.trace_paths(keys)
+    assert w["mis_rays"] > 0
+    Lo = pg.oracle().trace_paths(scene, keys)
+    same = np.all(Lg.view(np.int32) == Lo.view(np.int32), axis=1).mean()
+    assert same == 1.0 if exact else same >= 1 - 1e-4
