@@ -1223,15 +1223,21 @@ PGD_INLINE float bsdf_pdf(PowMemo &pm, const BSDF &bs, V woW, V wiW, int flags) 
     return m > 0 ? pdf / m : 0.f;
 }
 // BSDF::Sample_f (reflection.cpp:514-568)
-PGD_HEAVY void bsdf_sample_f(PowMemo &pm, const BSDF &bs, V woW, V *wiW, float u0, float u1, float uc, float *pdf, int flags,
-                              int *sampledType, FVal &F) {
+// BSDF::Sample_f (reflection.cpp:555-611) in two steps: bsdf_sample_dir picks the component
+// and samples the direction (pdf of that component, F of a specular one); bsdf_sample_rest
+// adds the other matching components' pdfs and, for a non-specular sample, the BSDF value.
+// Callers that may discard the direction (the MIS ray, mis_may_reach) run the second step
+// only when they keep it; bsdf_sample_f runs both.
+struct BSDFSampleState { int sel, matching; V wo, wi; };
+PGD_HEAVY bool bsdf_sample_dir(PowMemo &pm, const BSDF &bs, V woW, V *wiW, float u0, float u1, float uc, float *pdf,
+                               int flags, int *sampledType, FVal &F, BSDFSampleState &st) {
     int matching = 0;
 #pragma unroll
     for (int k = 0; k < 2; ++k) if (k < bs.n && matches(bs.bx[k], flags)) ++matching;
     if (matching == 0) {
         *pdf = 0.f; *sampledType = 0;
         fval_zero(F);
-        return;
+        return false;
     }
     int which = (int)floorf(uc * matching);
     if (which > matching - 1) which = matching - 1;
@@ -1246,23 +1252,36 @@ PGD_HEAVY void bsdf_sample_f(PowMemo &pm, const BSDF &bs, V woW, V *wiW, float u
     if (*pdf == 0.f) {
         *sampledType = 0;
         fval_zero(F);
-        return;
+        return false;
     }
     *sampledType = bx.type;
     *wiW = to_world(bs, wi);
-    if (!(bx.type & BSDF_SPECULAR) && matching > 1)
+    st.sel = sel; st.matching = matching; st.wo = wo; st.wi = wi;
+    return true;
+}
+PGD_HEAVY void bsdf_sample_rest(PowMemo &pm, const BSDF &bs, V woW, V wiW, const BSDFSampleState &st, float *pdf,
+                                int flags, int sampledType, FVal &F) {
+    const int sel = st.sel, matching = st.matching;
+    const V wo = st.wo, wi = st.wi;
+    if (!(sampledType & BSDF_SPECULAR) && matching > 1)
 #pragma unroll
         for (int k = 0; k < 2; ++k)
             if (k < bs.n && k != sel && matches(bs.bx[k], flags)) *pdf += bx_pdf(pm, bs.bx[k], wo, wi);
     if (matching > 1) *pdf /= matching;
-    if (!(bx.type & BSDF_SPECULAR)) {
+    if (!(sampledType & BSDF_SPECULAR)) {
         fval_zero(F);
-        if (vdot(*wiW, bs.ng) * vdot(woW, bs.ng) > 0) flags &= ~BSDF_TRANSMISSION;
+        if (vdot(wiW, bs.ng) * vdot(woW, bs.ng) > 0) flags &= ~BSDF_TRANSMISSION;
         else flags &= ~BSDF_REFLECTION;
 #pragma unroll
         for (int k = 0; k < 2; ++k)
             if (k < bs.n && matches(bs.bx[k], flags)) fval_push(F, bx_term(pm, bs.bx[k], wo, wi));
     }
+}
+PGD_INLINE void bsdf_sample_f(PowMemo &pm, const BSDF &bs, V woW, V *wiW, float u0, float u1, float uc, float *pdf,
+                              int flags, int *sampledType, FVal &F) {
+    BSDFSampleState st;
+    if (bsdf_sample_dir(pm, bs, woW, wiW, u0, u1, uc, pdf, flags, sampledType, F, st))
+        bsdf_sample_rest(pm, bs, woW, *wiW, st, pdf, flags, *sampledType, F);
 }
 
 

@@ -533,8 +533,14 @@ PGD_INLINE Pushes shade_vertex(const DevScene &S, const PathSoA &P, int slot, in
         // facing, for an area light; escapes the scene, for the environment)
         if (!em.point) {
             int sampledType;
-            bsdf_sample_f(pm, bs, wo, &wi, ub[0], ub[1], ub[2], &bsdfPdf, flags, &sampledType, F);
-            if (bsdfPdf > 0. && !(F.mode == FV_SUM && F.n == 0)) {
+            BSDFSampleState sst;
+            bool keep = bsdf_sample_dir(pm, bs, wo, &wi, ub[0], ub[1], ub[2], &bsdfPdf, flags, &sampledType, F, sst);
+            Ray mr;
+            mr.o = p; mr.d = wi; mr.mint = is.rayEps; mr.maxt = INFINITY; mr.time = ray.time;
+            // a direction whose MIS ray cannot reach the light contributes nothing (B unused)
+            if (keep) keep = mis_may_reach<FEAT>(S, Lt, mr);
+            if (keep) bsdf_sample_rest(pm, bs, wo, wi, sst, &bsdfPdf, flags, sampledType, F);
+            if (keep && bsdfPdf > 0. && !(F.mode == FV_SUM && F.n == 0)) {
                 fval_prepare<NB, FEAT>(S, F, mb, c);
                 float weight = 1.f;
                 bool go = true;
@@ -549,9 +555,7 @@ PGD_INLINE Pushes shade_vertex(const DevScene &S, const PathSoA &P, int slot, in
                 } else {
                     eb.mode = Lt.is_black ? EM_BLACK : EM_POOL; eb.off = Lt.spec; eb.div = 1.f; eb.point = false;
                 }
-                Ray mr;
-                mr.o = p; mr.d = wi; mr.mint = is.rayEps; mr.maxt = INFINITY; mr.time = ray.time;
-                if (go && !emit_black<NB, FEAT>(S, eb) && mis_may_reach<FEAT>(S, Lt, mr)) {
+                if (go && !emit_black<NB, FEAT>(S, eb)) {
                     const float ad = fabsf(vdot(wi, n));
                     float4 *B = B_of<NB>(P, vb, slot);
                     bool black = true;
