@@ -618,7 +618,10 @@ struct Stack {
 // quadric hit test kept out of line: its double-precision transcendentals would otherwise
 // set the register budget of every traversal loop.  Scalars in, t out (-inf: miss), so
 // the call passes everything in VGPRs and the traversal kernels need no private memory.
-__device__ __attribute__((noinline)) float quadric_hit(const pbrtgpu_quadric *quads, int type, int idx, float ox,
+#ifndef PGD_QUAD_ATTR   // quadric hit test out of line (traversal register budget); experiments may inline it
+#define PGD_QUAD_ATTR __attribute__((noinline))
+#endif
+__device__ PGD_QUAD_ATTR float quadric_hit(const pbrtgpu_quadric *quads, int type, int idx, float ox,
                                                        float oy, float oz, float dx, float dy, float dz, float mint,
                                                        float maxt, float time) {
     Ray ray;
