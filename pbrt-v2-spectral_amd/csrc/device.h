@@ -621,9 +621,8 @@ struct Stack {
 #ifndef PGD_QUAD_ATTR   // quadric hit test out of line (traversal register budget); experiments may inline it
 #define PGD_QUAD_ATTR __attribute__((noinline))
 #endif
-__device__ PGD_QUAD_ATTR float quadric_hit(const pbrtgpu_quadric *quads, int type, int idx, float ox,
-                                                       float oy, float oz, float dx, float dy, float dz, float mint,
-                                                       float maxt, float time) {
+PGD_INLINE float quadric_hit_inl(const pbrtgpu_quadric *quads, int type, int idx, float ox, float oy, float oz, float dx,
+                                 float dy, float dz, float mint, float maxt, float time) {
     Ray ray;
     ray.o = v3(ox, oy, oz); ray.d = v3(dx, dy, dz); ray.mint = mint; ray.maxt = maxt; ray.time = time;
     float t, e;
@@ -631,8 +630,16 @@ __device__ PGD_QUAD_ATTR float quadric_hit(const pbrtgpu_quadric *quads, int typ
                                                   : disk_intersect(quads[idx], ray, &t, &e, nullptr);
     return hit ? t : -INFINITY;   // a hit has t >= mint >= 0 (or NaN)
 }
+__device__ PGD_QUAD_ATTR float quadric_hit(const pbrtgpu_quadric *quads, int type, int idx, float ox, float oy, float oz,
+                                           float dx, float dy, float dz, float mint, float maxt, float time) {
+    return quadric_hit_inl(quads, type, idx, ox, oy, oz, dx, dy, dz, mint, maxt, time);
+}
+// INL: the persistent traversal kernels inline the hit-only test (fewer VGPRs than the call
+// there); the shading kernel calls it (inlined, it costs k_shade registers)
+template <bool INL = false>
 PGD_INLINE bool quadric_test(const DevScene &S, int type, int idx, const Ray &r, float *t) {
-    const float th = quadric_hit(S.quads, type, idx, r.o.x, r.o.y, r.o.z, r.d.x, r.d.y, r.d.z, r.mint, r.maxt, r.time);
+    const float th = INL ? quadric_hit_inl(S.quads, type, idx, r.o.x, r.o.y, r.o.z, r.d.x, r.d.y, r.d.z, r.mint, r.maxt, r.time)
+                         : quadric_hit(S.quads, type, idx, r.o.x, r.o.y, r.o.z, r.d.x, r.d.y, r.d.z, r.mint, r.maxt, r.time);
     *t = th;
     return th != -INFINITY;
 }
@@ -784,7 +791,7 @@ PGD_INLINE bool prim_test(const DevScene &S, Stack &st, int base, int pi, Ray &r
         if (!tri_hit(S.primTri[pi], ray, &t)) return false;
     } else if (!INST || pr.shape_type != PBRTGPU_SHAPE_INSTANCE) {
         st.cQuads++;
-        if (!quadric_test(S, pr.shape_type, pr.shape_index, ray, &t)) return false;
+        if (!quadric_test<true>(S, pr.shape_type, pr.shape_index, ray, &t)) return false;
     } else {
         if constexpr (INST) {
             const pbrtgpu_instance &I = S.insts[pr.shape_index];
