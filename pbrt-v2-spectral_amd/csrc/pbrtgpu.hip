@@ -411,7 +411,8 @@ struct pbrtgpu_ctx {
     std::vector<DevBuf> sceneBufs;
     DevBuf film, Lbuf, pix, filmIdx, mask, keys, counter, spillL, lists[4], scratch[3];
     int numCUs = 256;
-    int ptBlocksPerCU = 0;    // occupancy of k_trace_pt (computed on first use)
+    int ptBlocksPerCU = 0;    // occupancy of k_trace_pt closest (computed on first use)
+    int ptBlocksPerCUS = 0;   // occupancy of k_trace_pt shadow
     int ring = kStackLDS;     // LDS ring entries in use (PBRTGPU_STACK_LDS: tests force HBM spills)
     int refill = 16;          // idle lanes that trigger ray replacement in k_trace_pt (PBRTGPU_REFILL)
     Timing last;
@@ -482,10 +483,11 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
         int b0 = 0, b1 = 0;
         HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&b0, k_trace_pt<false, false>, kTraceBlock, 0));
         HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&b1, k_trace_pt<true, false>, kTraceBlock, 0));
-        c->ptBlocksPerCU = std::max(1, std::min(b0, b1));
+        c->ptBlocksPerCU = std::max(1, b0);
+        c->ptBlocksPerCUS = std::max(1, b1);
     }
-    const uint32_t ptGrid = (uint32_t)(c->numCUs * c->ptBlocksPerCU);
-    const size_t spillLane = (size_t)ptGrid * kTraceBlock * c->stackDepth;   // uint2 per kernel
+    const uint32_t ptGrid = (uint32_t)(c->numCUs * c->ptBlocksPerCU), ptGridS = (uint32_t)(c->numCUs * c->ptBlocksPerCUS);
+    const size_t spillLane = (size_t)std::max(ptGrid, ptGridS) * kTraceBlock * c->stackDepth;   // uint2 per kernel
     // scenes without measured BRDFs, textures and environment lights run the variant with
     // that code compiled out (fewer registers, no kd-tree stack)
     auto kShade = c->feat ? launch_shade<NB, FEAT_ALL> : launch_shade<NB, 0>;
@@ -571,8 +573,8 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
                     if (countWork) hipLaunchKernelGGL((k_trace_pt<false, true>), dim3(ptGrid), dim3(kTraceBlock), 0, L.s, c->S, P, q, c->refill, c->ring, spillC);
                     else hipLaunchKernelGGL((k_trace_pt<false, false>), dim3(ptGrid), dim3(kTraceBlock), 0, L.s, c->S, P, q, c->refill, c->ring, spillC);
                     HIPCHK(hipGetLastError());
-                    if (countWork) hipLaunchKernelGGL((k_trace_pt<true, true>), dim3(ptGrid), dim3(kTraceBlock), 0, L.s2, c->S, P, q, c->refill, c->ring, spillS);
-                    else hipLaunchKernelGGL((k_trace_pt<true, false>), dim3(ptGrid), dim3(kTraceBlock), 0, L.s2, c->S, P, q, c->refill, c->ring, spillS);
+                    if (countWork) hipLaunchKernelGGL((k_trace_pt<true, true>), dim3(ptGridS), dim3(kTraceBlock), 0, L.s2, c->S, P, q, c->refill, c->ring, spillS);
+                    else hipLaunchKernelGGL((k_trace_pt<true, false>), dim3(ptGridS), dim3(kTraceBlock), 0, L.s2, c->S, P, q, c->refill, c->ring, spillS);
                 }
                 HIPCHK(hipGetLastError());
                 T.launches[K_CLOSEST]++;
