@@ -1,21 +1,38 @@
-"""bench.py -- Mpaths/s of the MI355X spectral path tracer on BASELINE.json configs[1].
+"""bench.py -- Mpaths/s of the MI355X spectral path tracer on BASELINE.json's configs.
 
-Workload (N=1): killeroo-simple, SampledSpectrum 32 bands (the reference build's
-nSpectralSamples; BASELINE's "30 bands" names the same config), 'path' integrator
-maxdepth 5, 700x700 film, 256 spp -> 125.44 M camera paths per step.  One step = one
-full-frame render through the C-ABI (pbrtgpu_render_tiles): every path traced, every
-sample accumulated into the film in the reference's order.  The scene is uploaded once;
-its BVH/meshes stay resident in HBM, so the timed region starts with inputs in HBM.
+Workload (default --config c2 = BASELINE.json configs[1], the metric's configuration):
+killeroo-simple, SampledSpectrum 32 bands (the reference build's nSpectralSamples;
+BASELINE's "30 bands" names the same config), 'path' integrator maxdepth 5, 700x700 film,
+256 spp -> 125.44 M camera paths per step.  --config c3 | c4 | c5 runs the other packaged
+configs at their stated sizes (bunny 1920x1080@1024 measured BRDF; metal 400x400@4096 60 bands;
+anim-killeroos-moving 600x600@512 motion blur).
 
-Multi-GPU (python -m torch.distributed.run ... bench.py --gpus N): one process per GPU.
-Image tiles / frames shard with no data-path collective.  Default "weak": every rank
-renders its own full frame with per-rank seed (fixed per-GPU work);  "--shard tiles"
-splits ONE frame's tiles round-robin over ranks (strong).  The only collectives are the
-barrier around the timed region and the max-over-ranks of the elapsed time.
+One step = one frame: every camera path traced, every sample added to the film in the
+reference's order, and the film back on the host (first kernel launch ->
+film tiles on the host).  The scene is uploaded once before timing, so inputs are resident
+in HBM when the timed region starts.
 
-Extra JSON fields: "roofline" for the dominant kernel (k_render, the path megakernel)
-and "cpu_baseline" (the CPU restatement in oracle/, timed on this host's cores over a
-bounded, representative sample of the same workload).  See DESIGN.md §5.
+Multi-GPU: ONE frame's 16x16 film-pixel tiles are dealt into interleaved
+slices (pbrtgpu.tile_slice), one per GPU; every GPU renders its slice and gathers its pixels
+into one host film (pbrtgpu_film_gather).  Nothing is exchanged between GPUs (no RCCL).
+  * python -m torch.distributed.run --nproc-per-node N bench.py --gpus N: one process per
+    GPU (LOCAL_RANK); the film is a shared-memory file every rank writes its own pixels into;
+    the barrier around the timed region and the max over ranks of the elapsed time go over
+    gloo (host only).  value = the frame's paths x steps / max elapsed ("strong": the total
+    work of a step is one frame whatever N is).
+  * python bench.py --gpus N (no launcher): one process, N contexts, one host thread each
+    (pbrtgpu_render_multi).
+--shard frames instead gives every rank its own frame (seed = rank; "weak").
+
+Extra JSON fields:
+  roofline     the dominant kernel's algorithmic bytes per launch / its EXCLUSIVE average
+               launch time, from one untimed frame in serial mode (PBRTGPU_SERIAL=1: one
+               lane, no concurrent kernels, so each kernel's HIP-event spans are its own
+               device time); per-kernel table beside it (ms, GB/s, frac, PMC traffic from
+               profiles/hbm_traffic.json when it holds this config).  DESIGN.md §5.
+  cpu_baseline the CPU restatement (oracle/liboracle.so, TEST INFRASTRUCTURE) timed on this
+               host: every core this process may use, and one core, over a bounded sample of
+               the same frame (all spp of pseudo-randomly spread pixels).
 """
 import argparse
 import json
@@ -32,10 +49,21 @@ import pbrtgpu as pg  # noqa: E402
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md "HBM [CDNA4]": 8 TB/s peak
 NODE_BYTES, TRI_BYTES, QUAD_BYTES = 32, 48, 176
 RAY_BYTES, HIT_BYTES, QENTRY_BYTES = 36, 8, 4     # SoA ray record read, hit / occlusion written, queue entry
+METRIC = "Mpaths/sec (whole node) + HBM GB/s; spectral path tracer at 1/2/4/8 MI355X"
+
+# BASELINE.json configs -> scene packs (built from the reference's scene files with SURVEY.md
+# App. B overrides: 'path' integrator maxdepth 5, lowdiscrepancy spp, resolution, bands)
+CONFIGS = {
+    "c2": ("killeroo-simple.pack", "killeroo-simple SampledSpectrum %d bands, path maxdepth %d, %dspp, %dx%d"),
+    "c3": ("bunny.pack", "bunny (mystique measured BRDF) SampledSpectrum %d bands, path maxdepth %d, %dspp, %dx%d"),
+    "c4": ("metal.pack", "metal (Au conductor, env light) SampledSpectrum %d bands, path maxdepth %d, %dspp, %dx%d"),
+    "c5": ("anim-killeroos-moving.pack",
+           "anim-killeroos-moving (motion-blur BVHs) SampledSpectrum %d bands, path maxdepth %d, %dspp, %dx%d"),
+}
 
 
 def trace_bytes(work, kernel):
-    """DESIGN.md §5.1: algorithmic bytes of a traversal kernel = every BVH node it visits
+    """DESIGN.md §5: algorithmic bytes of a traversal kernel = every BVH node it visits
     (32 B), every primitive it tests (48 B pre-gathered triangle, 176 B quadric record),
     plus the ray it reads, the answer it writes and its queue entry."""
     if kernel == "k_trace_closest":
@@ -46,7 +74,7 @@ def trace_bytes(work, kernel):
 
 
 def shade_bytes(work, paths, bands):
-    """DESIGN.md §5.1: algorithmic bytes of k_shade over a frame, from the event counts of
+    """DESIGN.md §5: algorithmic bytes of k_shade over a frame, from the event counts of
     the instrumented render.  S = 4*bands (one spectrum); scene gathers per vertex:
     prim 16 + triangle 16 + 3 vertices x (P 12, N 12, uv 8) + material 64 = 192 B, plus three
     BSDF-spectrum reads and one emitted-spectrum read."""
@@ -65,35 +93,61 @@ def shade_bytes(work, paths, bands):
             + work["mis_rays"] * per_mis + cams * (per_cam + per_out))
 
 
+def accum_bytes(paths, bands):
+    """k_accum: every per-sample radiance read once (4 B per band); film read+write per pixel
+    is negligible next to it (1/spp)."""
+    return 4.0 * bands * paths
+
+
+def cpu_info():
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    model = ln.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    ncpu = os.cpu_count() or 1
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else ncpu
+    return model, ncpu, aff
+
+
 def cpu_baseline(scene, target_s):
-    """CPU restatement (oracle/liboracle.so, TEST INFRASTRUCTURE) on the host cores: all
-    samples of pseudo-randomly spread pixels, sized to ~target_s seconds of work."""
-    ncpu = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
-    threads = max(1, min(16, ncpu))
+    """CPU restatement (oracle/liboracle.so, TEST INFRASTRUCTURE) on the host: all spp of
+    pseudo-randomly spread pixels of the same frame, sized to ~target_s seconds on every core
+    this process may use (the affinity mask, capped by OMP_NUM_THREADS where the box sets a
+    CPU share), then ~target_s / 3 on one core."""
+    model, ncpu, aff = cpu_info()
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    threads = max(1, min(aff, share) if share > 0 else aff)
     o = pg.oracle()
     spp = scene.spp
-    probe = 256 * spp // 16 * threads
-    t = time.perf_counter()
-    o.trace_range(scene, 0, probe, threads)
-    dt = time.perf_counter() - t
-    count = int(max(probe, probe * target_s / max(dt, 1e-3)))
-    count = (count + spp - 1) // spp * spp
-    t = time.perf_counter()
-    n = o.trace_range(scene, 0, count, threads)
-    dt = time.perf_counter() - t
-    return {"value": n / dt / 1e6, "unit": "Mpaths/s", "cores": threads, "kind": "port",
-            "sample": "%d paths = all %d samples of %d pseudo-randomly spread pixels of the same frame, "
-                      "%.1f s on %d threads" % (n, spp, n // spp, dt, threads)}
+
+    def timed(nthreads, seconds):
+        probe = max(spp, 64 * spp // 16 * nthreads)
+        t = time.perf_counter()
+        o.trace_range(scene, 0, probe, nthreads)
+        dt = time.perf_counter() - t
+        count = int(max(probe, probe * seconds / max(dt, 1e-3)))
+        count = (count + spp - 1) // spp * spp
+        t = time.perf_counter()
+        n = o.trace_range(scene, 0, count, nthreads)
+        return n, time.perf_counter() - t
+
+    n, dt = timed(threads, target_s)
+    n1, dt1 = timed(1, target_s / 3.0)
+    per_core = n1 / dt1 / 1e6
+    return {"value": round(n / dt / 1e6, 4), "unit": "Mpaths/s", "cores": threads, "kind": "port",
+            "one_core": round(per_core, 4), "host_cpus": ncpu, "affinity_cpus": aff, "cpu_model": model,
+            "sample": "%d paths = all %d samples of %d pseudo-randomly spread pixels of the same frame, %.1f s on "
+                      "%d threads; 1-core leg %d paths in %.1f s" % (n, spp, n // spp, dt, threads, n1, dt1),
+            "calibration": "port vs reference per core, same box: profiles/cpu_calibration.json"}
 
 
-def shard_tiles(ntiles, rank, world):
-    """Tile ids of one rank when ONE frame's tiles are split over ranks (--shard tiles):
-    round-robin, so every rank gets a spread of cheap and expensive image regions."""
-    return np.arange(rank, ntiles, world, dtype=np.int32)
-
-
-def reduce_over_ranks(dist, elapsed, paths, device):
-    """(max elapsed over ranks, total paths over ranks) -- the only collectives of the run."""
+def reduce_over_ranks(dist, elapsed, paths, device="cpu"):
+    """(max elapsed over ranks, total paths over ranks) -- host-side (gloo) reductions."""
     if dist is None:
         return elapsed, paths
     import torch
@@ -104,131 +158,196 @@ def reduce_over_ranks(dist, elapsed, paths, device):
     return float(mx[0]), float(t[1])
 
 
+def shared_film(shape, rank, dist, tag):
+    """A host film every rank of one node writes its own pixels into (/dev/shm file):
+    the host gather of SURVEY.md §8(e) without any collective."""
+    path = "/dev/shm/pbrtgpu_film_%s" % tag
+    n = int(np.prod(shape)) * 4
+    if rank == 0:
+        with open(path, "wb") as f:
+            f.truncate(n)
+    if dist is not None:
+        dist.barrier()
+    return path, np.memmap(path, dtype=np.float32, mode="r+", shape=shape)
+
+
+def exclusive_roofline(dev, scene, tiles, tile, frame_paths, cfg):
+    """Per-kernel exclusive device time (serial mode) and algorithmic bytes (instrumented
+    frame), both over one frame of this rank's tiles, untimed."""
+    os.environ["PBRTGPU_SERIAL"] = "1"
+    try:
+        dev.render(tiles=tiles, tile=tile)
+        tm = dev.timing()
+        serial_wall = None
+        t = time.perf_counter()
+        dev.render(tiles=tiles, tile=tile)
+        serial_wall = time.perf_counter() - t
+        tm = dev.timing()
+    finally:
+        del os.environ["PBRTGPU_SERIAL"]
+    dev.render(tiles=tiles, tile=tile, count_work=True)
+    work = dev.timing()["work"]
+    byts = {"k_trace_closest": trace_bytes(work, "k_trace_closest"),
+            "k_trace_shadow": trace_bytes(work, "k_trace_shadow"),
+            "k_shade": shade_bytes(work, frame_paths, scene.bands),
+            "k_accum": accum_bytes(frame_paths, scene.bands)}
+    traffic = {}
+    tf = os.path.join(ROOT, "profiles", "hbm_traffic.json")
+    if os.path.exists(tf):
+        with open(tf) as f:
+            tr = json.load(f)
+        traffic = tr.get("configs", {}).get(cfg, {})
+    per = {}
+    for k in pg.Timing.KERNELS:
+        ms, nl = tm[k]["ms"], max(tm[k]["launches"], 1)
+        avg = ms / nl
+        bpl = byts[k] / nl
+        gbs = bpl / (avg * 1e-3) / 1e9 if avg > 0 else 0.0
+        ent = traffic.get(k)
+        per[k] = {"ms_per_frame": round(ms, 2), "launches": tm[k]["launches"], "avg_launch_ms": round(avg, 4),
+                  "alg_bytes_per_launch": round(bpl), "alg_GBps": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4),
+                  "pmc_bytes_per_launch": ent.get("hbm_bytes_per_launch") if ent else None}
+    dom = max(("k_trace_closest", "k_trace_shadow", "k_shade"), key=lambda k: per[k]["ms_per_frame"])
+    d = per[dom]
+    roof = {"bound": "hbm", "achieved": d["alg_GBps"], "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": d["frac"],
+            "traffic": d["pmc_bytes_per_launch"], "kernel": dom, "avg_launch_ms": d["avg_launch_ms"],
+            "alg_bytes_per_launch": d["alg_bytes_per_launch"],
+            "timing": "exclusive: PBRTGPU_SERIAL=1 frame (one lane, no concurrent kernels), HIP events",
+            "serial_frame_ms": round(serial_wall * 1e3, 2), "kernels": per,
+            "per_path": {k: round(v / frame_paths, 3) for k, v in work.items()},
+            "traffic_source": (traffic.get("source") if traffic else None)}
+    return roof
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--scene", default=os.path.join(ROOT, "scenes", "killeroo-simple.pack"))
-    ap.add_argument("--res", type=int, default=700)
-    ap.add_argument("--spp", type=int, default=256)
-    ap.add_argument("--shard", choices=["frames", "tiles"], default="frames")
+    ap.add_argument("--config", choices=sorted(CONFIGS), default="c2")
+    ap.add_argument("--scene", default=None, help="scene pack (default: the config's)")
+    ap.add_argument("--res", type=int, default=-1, help="square resolution override (default: the config's)")
+    ap.add_argument("--spp", type=int, default=-1, help="spp override (default: the config's)")
+    ap.add_argument("--shard", choices=["tiles", "frames"], default="tiles")
     ap.add_argument("--tile", type=int, default=16)
+    ap.add_argument("--slices", type=int, default=1, help="tile slices per GPU (single-process --gpus N)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--serial", action="store_true", help="timed frames in serial mode (profiling runs)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1 and args.gpus not in (1, world):
+        raise SystemExit("--gpus %d but WORLD_SIZE %d" % (args.gpus, world))
+    threads_mode = world == 1 and args.gpus > 1
+    n_gpus = world if world > 1 else args.gpus
+    if args.serial:
+        os.environ["PBRTGPU_SERIAL"] = "1"
     dist = None
     if world > 1:
-        import torch
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dist.init_process_group("gloo")          # host-side barrier / max only (no RCCL needed)
 
-    scene = pg.Scene.load(args.scene, xres=args.res, yres=args.res, spp=args.spp,
-                          seed=rank if args.shard == "frames" else 0)
+    pack, desc = CONFIGS[args.config]
+    scene = pg.Scene.load(args.scene or os.path.join(ROOT, "scenes", pack), xres=args.res, yres=args.res,
+                          spp=args.spp, seed=rank if args.shard == "frames" else 0)
     info = scene.info()
-    dev = pg.Device(local)
-    dev.upload(scene)
+    tile = (args.tile, args.tile)
+    ntx, nty = pg.tile_grid(scene, tile)
+    shape = (scene.height, scene.width, scene.bands)
 
-    tiles = None
-    if args.shard == "tiles" and world > 1:
-        c = scene.flat.camera
-        tw = (c.sx_end - c.sx_start + args.tile - 1) // args.tile
-        th = (c.sy_end - c.sy_start + args.tile - 1) // args.tile
-        tiles = shard_tiles(tw * th, rank, world)
+    if threads_mode:
+        if pg.gpu_lib().pbrtgpu_device_count() < args.gpus:
+            raise SystemExit("--gpus %d: only %d devices visible" % (args.gpus, pg.gpu_lib().pbrtgpu_device_count()))
+        devs = [pg.Device(i) for i in range(args.gpus)]
+        for d in devs:
+            d.upload(scene)
+        film = np.zeros(shape, np.float32)
+        dev, tiles = devs[0], None
 
-    def step():
-        return dev.render(tiles=tiles, tile=(args.tile, args.tile))
+        def step():
+            _, st = pg.render_multi(devs, tile=tile, slices_per_device=args.slices, out=film)
+            return st[:, pg.STAT_PATHS].sum()
+    else:
+        dev = pg.Device(local)
+        dev.upload(scene)
+        if world > 1 and args.shard == "tiles":
+            tiles = pg.tile_slice(ntx * nty, rank, world)
+            tag = os.environ.get("TORCHELASTIC_RUN_ID", "") + "_" + os.environ.get("MASTER_PORT", "0")
+            film_path, film = shared_film(shape, rank, dist, tag)
+        else:
+            tiles, film_path = None, None
+            film = np.zeros(shape, np.float32)
+
+        def step():
+            st = dev.render(tiles=tiles, tile=tile)
+            dev.gather(film, tiles=tiles, tile=tile)      # film tiles back on the host
+            return st[pg.STAT_PATHS]
 
     for _ in range(args.warmup):
         step()
-
-    def sync_all():
-        if dist is not None:
-            import torch
-            torch.cuda.synchronize()
-            dist.barrier()
-
-    sync_all()
+    if dist is not None:
+        dist.barrier()
     t0 = time.perf_counter()
     paths = 0.0
-    kern = {}
     for _ in range(args.steps):
-        st = step()                      # returns after the film is complete (device synced)
-        paths += st[pg.STAT_PATHS]
-        tm = dev.timing()
-        for k in pg.Timing.KERNELS:
-            a = kern.setdefault(k, [0.0, 0])
-            a[0] += tm[k]["ms"]
-            a[1] += tm[k]["launches"]
+        paths += step()                  # returns after the film is on the host (device synced)
     elapsed = time.perf_counter() - t0
-    sync_all()
-    elapsed, total_paths = reduce_over_ranks(dist, elapsed, paths, "cuda")
+    my_elapsed = elapsed
+    if dist is not None:
+        dist.barrier()
+    elapsed, total_paths = reduce_over_ranks(dist, elapsed, paths)
+    per_rank = None
+    if dist is not None:
+        import torch
+        g = [torch.zeros(1, dtype=torch.float64) for _ in range(world)]
+        dist.all_gather(g, torch.tensor([my_elapsed], dtype=torch.float64))
+        per_rank = [round(float(x[0]) / args.steps * 1e3, 2) for x in g]
 
-    # roofline of the dominant kernel: algorithmic bytes (from one instrumented, untimed
-    # render of the same frame) / its device time (HIP events around every launch)
-    dom = max(("k_trace_closest", "k_trace_shadow", "k_shade"), key=lambda k: kern[k][0])
-    dev.render(tiles=tiles, tile=(args.tile, args.tile), count_work=True)
-    work = dev.timing()["work"]
-    frame_paths = paths / args.steps
-    if dom == "k_shade":
-        byts = shade_bytes(work, frame_paths, scene.bands)
-    else:
-        byts = trace_bytes(work, dom)                     # per frame
-    sec = kern[dom][0] / args.steps * 1e-3                # per frame
-    achieved = byts / sec / 1e9
-    launches = kern[dom][1] / args.steps
-    roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "kernel": dom,
-            "avg_launch_ms": round(kern[dom][0] / max(kern[dom][1], 1), 4),
-            "launches_per_step": launches, "alg_bytes_per_launch": round(byts / max(launches, 1)),
-            "per_path": {k: round(v / frame_paths, 3) for k, v in work.items()},
-            "kernel_ms_per_step": {k: round(v[0] / args.steps, 2) for k, v in kern.items()},
-            "kernel_alg_GBps": {
-                "k_trace_closest": round(trace_bytes(work, "k_trace_closest") / (kern["k_trace_closest"][0] / args.steps * 1e-3) / 1e9, 1),
-                "k_trace_shadow": round(trace_bytes(work, "k_trace_shadow") / (kern["k_trace_shadow"][0] / args.steps * 1e-3) / 1e9, 1),
-                "k_shade": round(shade_bytes(work, frame_paths, scene.bands) / (kern["k_shade"][0] / args.steps * 1e-3) / 1e9, 1)},
-            # the two wavefront lanes and the shadow stream run kernels concurrently, so the
-            # per-kernel event spans above overlap; this is all three kernels' algorithmic
-            # bytes of a frame over the wall time of a step
-            "pipeline_alg_GBps": round((trace_bytes(work, "k_trace_closest") + trace_bytes(work, "k_trace_shadow")
-                                        + shade_bytes(work, frame_paths, scene.bands)) / (elapsed / args.steps) / 1e9, 1)}
-    tf = os.path.join(ROOT, "profiles", "hbm_traffic.json")
-    if os.path.exists(tf):
-        with open(tf) as f:
-            tr = json.load(f)
-        ent = tr.get(dom)
-        if ent and ent.get("res") == args.res and ent.get("spp") == args.spp:
-            roof["traffic"] = ent.get("hbm_bytes_per_launch")
-            roof["traffic_source"] = tr.get("source")
+    frame_paths = paths / args.steps    # this rank's share of a frame
+    roof = None
+    if rank == 0 and not args.no_roofline:
+        roof = exclusive_roofline(dev, scene, tiles, tile, frame_paths, args.config)
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu:
+    if rank == 0 and n_gpus == 1 and not args.no_cpu:
         cpu = cpu_baseline(scene, args.cpu_seconds)
 
     if rank == 0:
         value = total_paths / elapsed / 1e6
         line = {
-            "metric": "Mpaths/sec (whole node) + HBM GB/s; spectral path tracer at 1/2/4/8 MI355X",
-            "value": round(value, 3), "unit": "Mpaths/s", "n_gpus": world, "steps": args.steps,
+            "metric": METRIC,
+            "value": round(value, 3), "unit": "Mpaths/s", "n_gpus": n_gpus, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
             "higher_is_better": True, "scaling": "weak" if args.shard == "frames" else "strong",
-            "vs_baseline": None, "dtype": "f32", "data": "packaged scene killeroo-simple "
-            "(scene pack built from the reference's scene file), fixed per-path seeds",
-            "config": {"workload": "killeroo-simple SampledSpectrum %d bands, path maxdepth %d, %dspp, %dx%d"
-                       % (scene.bands, info["maxdepth"], scene.spp, scene.width, scene.height),
-                       "paths_per_step_per_gpu": int(paths / args.steps), "shard": args.shard,
-                       "parallelism": "%s x%d" % ("frames" if args.shard == "frames" else "tiles", world)},
+            "vs_baseline": None, "dtype": "f32",
+            "data": "packaged scene %s (scene pack built from the reference's scene file), fixed per-path seeds"
+                    % pack.replace(".pack", ""),
+            "config": {"workload": desc % (scene.bands, info["maxdepth"], scene.spp, scene.width, scene.height),
+                       "config": args.config, "paths_per_frame": int(scene.width * scene.height * scene.spp),
+                       "shard": args.shard, "tile": args.tile,
+                       "parallelism": "%s x%d%s" % ("tiles" if args.shard == "tiles" else "frames", n_gpus,
+                                                    " (threads, one process)" if threads_mode else "")},
             "roofline": roof,
             "cpu_baseline": cpu,
         }
+        if per_rank is not None:
+            line["per_gpu_ms_per_step"] = per_rank
+        if args.serial:
+            line["note"] = "serial mode (profiling): one lane, no concurrent kernels"
         print(json.dumps(line), flush=True)
-    dev.close()
+    if threads_mode:
+        for d in devs:
+            d.close()
+    else:
+        dev.close()
     if dist is not None:
+        dist.barrier()
+        if rank == 0 and film_path:
+            os.unlink(film_path)
         dist.destroy_process_group()
 
 

@@ -227,9 +227,15 @@ typedef struct pbrtgpu_flat_scene {
 } pbrtgpu_flat_scene;
 
 /* ---- render description ----------------------------------------------------------- */
+/* Tiles are tile_w x tile_h blocks of the FILM pixel window (camera px_count x py_count;
+ * the sample extent's half-pixel border belongs to no tile): tile id = ty * ntx + tx with
+ * ntx = ceil(px_count / tile_w), nty = ceil(py_count / tile_h); the last row / column may be
+ * ragged.  Rendering a tile renders the camera samples of its pixels, plus the samples of any
+ * other sample pixel whose box footprint reaches one of them (spectralImage.cpp:80-92), so
+ * films of disjoint tile sets are disjoint and sum to the full-frame film. */
 typedef struct pbrtgpu_render_desc {
     int32_t spp_begin, spp_end;   /* sample index range [begin,end) of this call */
-    int32_t tile_w, tile_h;       /* tile size in sample pixels (tile ids index this grid) */
+    int32_t tile_w, tile_h;       /* tile size in film pixels (<= 0: 16) */
     int32_t flags;                /* PBRTGPU_F_* */
     int32_t reserved[3];
 } pbrtgpu_render_desc;
@@ -257,11 +263,35 @@ int pbrtgpu_context_destroy(pbrtgpu_ctx *ctx);
 const char *pbrtgpu_last_error(void);
 /* copies the flattened scene into device memory owned by ctx */
 int pbrtgpu_scene_upload(pbrtgpu_ctx *ctx, const pbrtgpu_flat_scene *scene);
-/* Renders the listed tiles of the sample extent for samples [spp_begin, spp_end) and
- * accumulates into the context's film (film pixels touched by those tiles).
- * tile_ids == NULL means every tile. stats_out may be NULL. */
+/* Renders the listed tiles for samples [spp_begin, spp_end) into the context's film (the
+ * film is cleared first unless PBRTGPU_F_ACCUMULATE is set or spp_begin > 0).
+ * tile_ids == NULL means every tile. stats_out ([PBRTGPU_STAT_COUNT]) may be NULL.
+ * One call over the whole sample range adds every pixel's samples in the reference's order
+ * (SamplerRendererTask::Run + AddSample).  A frame split into sample ranges and accumulated
+ * adds the same contributions range by range: its film equals the one-call film up to float
+ * summation order.
+ * Replaces SamplerRenderer::Render (renderers/samplerrenderer.cpp:188-222) for the tiles'
+ * share of the frame; the tiles play the role of ComputeSubWindow's task windows
+ * (core/sampler.cpp:47-67). */
 int pbrtgpu_render_tiles(pbrtgpu_ctx *ctx, const pbrtgpu_render_desc *desc,
                          const int32_t *tile_ids, int32_t ntiles, double *stats_out);
+/* Host gather of a tile list: writes the film pixels of the listed tiles (grid as in
+ * pbrtgpu_render_desc) into film_out (float32 [py_count][px_count][n_bands], n_floats >= its
+ * size); other pixels of film_out are left untouched.  tile_ids == NULL copies the whole film. */
+int pbrtgpu_film_gather(pbrtgpu_ctx *ctx, int32_t tile_w, int32_t tile_h, const int32_t *tile_ids,
+                        int32_t ntiles, float *film_out, int64_t n_floats);
+/* One frame over n contexts (one per GPU, each holding the same uploaded scene; no RCCL, no
+ * device-to-device traffic).  The tile list (tile_ids, or every tile when NULL) is dealt into
+ * m = n * max(1, slices_per_ctx) interleaved slices (slice j = list[j], list[j + m], ...);
+ * one host thread per context pulls slices from a shared atomic counter and renders each
+ * with pbrtgpu_render_tiles (its first slice clears the context film unless desc asks to
+ * accumulate), then gathers its tiles into film_out (pbrtgpu_film_gather).  Films of
+ * different contexts cover disjoint pixels, so film_out is the full-frame film bit for bit.
+ * stats_out ([n][PBRTGPU_STAT_COUNT], may be NULL): per-context sums.  Returns the first
+ * context's error, if any. */
+int pbrtgpu_render_multi(pbrtgpu_ctx *const *ctxs, int32_t n, const pbrtgpu_render_desc *desc,
+                         const int32_t *tile_ids, int32_t ntiles, int32_t slices_per_ctx,
+                         float *film_out, int64_t n_floats, double *stats_out);
 /* Copies the film (float32 [py_count][px_count][n_bands], Σ L per pixel -- the
  * reference film does not normalise) to host memory. */
 int pbrtgpu_film_read(pbrtgpu_ctx *ctx, float *film_out, int64_t n_floats);

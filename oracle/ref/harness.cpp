@@ -19,6 +19,17 @@
 // render loop of SamplerRendererTask::Run (samplerrenderer.cpp:60-164) with the
 // build's fixed per-path seeding instead of per-task RNG streams.
 // No header or library is stubbed: everything it links is reference code or this file.
+//
+// --refdat additionally feeds every sample to the reference's own SpectralImageNoCameraFilm
+// (film/spectralImageNoCamera.cpp, which builds here: it does not include the lens-camera
+// headers).  Its AddSample c[] accumulation (:36-75 of that file) and WriteImage payload
+// (clamp-index quirk, splat pad, identity conversion matrix, x-major band planes as float64)
+// are those of SpectralImageFilm (spectralImage.cpp:77-152, 267-378); it writes header line
+// 1 only (no "focal fStop fov" line) and attempts a _depth.exr side image, which this
+// OpenEXR-less build cannot write.  So the .dat it writes pins the payload and line 1 of the
+// spectral film's .dat with reference code.
+// --keys traces an explicit (x, y, s) key list (int32 triples) at the scene's full
+// resolution and sample count -- the configs' real spp -- without a film.
 
 #include "stdafx.h"
 #include "pbrt.h"
@@ -42,6 +53,7 @@
 #include "accelerators/bvh.h"
 #include "cameras/perspective.h"
 #include "filters/box.h"
+#include "film/spectralImageNoCamera.h"
 #include "integrators/path.h"
 #include "integrators/emission.h"
 #include "lights/diffuse.h"
@@ -317,6 +329,7 @@ static int ovW = -1, ovH = -1, ovMaxDepth = -1;
 static Scene *gScene = NULL;
 static Camera *gCamera = NULL;
 static HarnessFilm *gFilm = NULL;
+static Filter *gFilter = NULL;
 static SurfaceIntegrator *gSurf = NULL;
 static VolumeIntegrator *gVol = NULL;
 static int gSppParam = 4;
@@ -487,6 +500,7 @@ void pbrtWorldEnd() {
         crop[2] = Clamp(min(cr[2], cr[3]), 0., 1.); crop[3] = Clamp(max(cr[2], cr[3]), 0., 1.);
     }
     Filter *filter = CreateBoxFilter(filterParams);
+    gFilter = filter;
     gFilm = new HarnessFilm(xres, yres, filter, crop, "harness");
     Transform *c2w[2];
     tcache.Lookup(cameraToWorld[0], &c2w[0], NULL);
@@ -519,7 +533,8 @@ static void KatMT(const char *fn) {
 static void usage() {
     fprintf(stderr, "usage: harness scene.pbrt [--res W H] [--spp N] [--maxdepth D] [--seed S]\n"
                     "   [--window x0 x1 y0 y1] [--raw film.f32] [--dat film.dat] [--paths paths.bin]\n"
-                    "   [--path-every K] [--kat-mt out.bin] [--spectra out.bin] [--tris out.bin]\n");
+                    "   [--path-every K] [--kat-mt out.bin] [--spectra out.bin] [--tris out.bin]\n"
+                    "   [--keys keys.i32 (with --paths)] [--refdat film.dat]\n");
     exit(1);
 }
 
@@ -528,6 +543,7 @@ int main(int argc, char **argv) {
     const char *scene = argv[1];
     int spp = -1, seed = 0, win[4] = { -1, -1, -1, -1 }, pathEvery = 0;
     const char *rawOut = NULL, *datOut = NULL, *pathsOut = NULL, *katMt = NULL, *specOut = NULL, *trisOut = NULL;
+    const char *keysIn = NULL, *refDat = NULL;
     for (int i = 2; i < argc; ++i) {
         string a = argv[i];
         if (a == "--res") { ovW = atoi(argv[++i]); ovH = atoi(argv[++i]); }
@@ -542,10 +558,31 @@ int main(int argc, char **argv) {
         else if (a == "--kat-mt") katMt = argv[++i];
         else if (a == "--spectra") specOut = argv[++i];
         else if (a == "--tris") trisOut = argv[++i];
+        else if (a == "--keys") keysIn = argv[++i];
+        else if (a == "--refdat") refDat = argv[++i];
         else usage();
     }
     Options opt; opt.quiet = true;
     pbrtInit(opt);
+    // the reference's own spectral film beside the restatement (--refdat).  WriteImage adds
+    // splatScale * splatC[nSpectralSamples] -- the Pixel's `pad` member, which the Pixel
+    // constructor never initialises (spectralImageNoCamera.h:72-82, spectralImage.h:74-84) --
+    // to every band.  A config-size film (tens of MB) comes from fresh mmap pages, where pad
+    // is 0; a small film allocated after the scene would reuse freed heap.  So the film is
+    // created here, on the fresh heap, before the scene is parsed: the fixture sees the
+    // config-size behaviour (pad == 0).  Film parameters: the --res override and the box
+    // filter's defaults (the harness's film uses the same, pbrtPixelFilter keeps only the name).
+    Film *refFilm = NULL;
+    if (refDat) {
+        if (ovW <= 0) { fprintf(stderr, "harness: --refdat needs --res\n"); return 1; }
+        ParamSet fp;
+        int w = ovW, h = ovH;
+        fp.AddInt("xresolution", &w, 1);
+        fp.AddInt("yresolution", &h, 1);
+        string fn(refDat);
+        fp.AddString("filename", &fn, 1);
+        refFilm = CreateSpectralImageNoCameraFilm(fp, CreateBoxFilter(ParamSet()));
+    }
     if (katMt) KatMT(katMt);
     if (specOut) {
         // 'color' parameters -> FromRGB(REFLECTANCE) (paramset.cpp:89-98); band table dump
@@ -596,37 +633,68 @@ int main(int argc, char **argv) {
     if (pf) { int hdr[4] = { nSpectralSamples, spp, seed, 0 }; fwrite(hdr, 4, 4, pf); }
     MemoryArena arena;
     long nPath = 0, nBad = 0;
+    // one camera sample of SamplerRendererTask::Run (samplerrenderer.cpp:86-133) with the
+    // fixed-seed sampler and per-path RNG
+    auto trace = [&](int x, int y, int s, RayDifferential *ray) -> Spectrum {
+        FillSample(smp, x, y, (uint32_t)s, (uint32_t)spp, (uint32_t)seed, gCamera->shutterOpen, gCamera->shutterClose);
+        float rayWeight = gCamera->GenerateRayDifferential(*smp, ray);
+        ray->ScaleDifferentials(1.f / sqrtf(spp));
+        RNG rng(path_seed(pixel_hash((uint32_t)seed, x, y), (uint32_t)s));
+        Spectrum L;
+        Intersection isect;
+        Spectrum T;
+        if (rayWeight > 0.f) L = rayWeight * renderer.Li(gScene, *ray, smp, rng, arena, &isect, &T);
+        else L = 0.f;
+        if (L.HasNaNs()) { L = Spectrum(0.f); ++nBad; }
+        else if (L.y() < -1e-5) { L = Spectrum(0.f); ++nBad; }
+        else if (isinf(L.y())) { L = Spectrum(0.f); ++nBad; }
+        return L;
+    };
+    auto emit = [&](int x, int y, int s, const Spectrum &L) {
+        int key[3] = { x, y, s };
+        float c[nSpectralSamples];
+        L.GetOrigC(c);
+        fwrite(key, 4, 3, pf);
+        fwrite(c, 4, nSpectralSamples, pf);
+    };
+    if (keysIn) {
+        if (!pf) { fprintf(stderr, "harness: --keys needs --paths\n"); return 1; }
+        FILE *kf = fopen(keysIn, "rb");
+        if (!kf) { fprintf(stderr, "harness: cannot open %s\n", keysIn); return 1; }
+        int key[3];
+        while (fread(key, 4, 3, kf) == 3) {
+            int gx0, gx1, gy0, gy1;
+            gFilm->GetSampleExtent(&gx0, &gx1, &gy0, &gy1);
+            if (key[0] < gx0 || key[0] >= gx1 || key[1] < gy0 || key[1] >= gy1 || key[2] < 0 || key[2] >= spp) {
+                fprintf(stderr, "harness: key (%d %d %d) outside the sample extent\n", key[0], key[1], key[2]);
+                return 1;
+            }
+            RayDifferential ray;
+            Spectrum L = trace(key[0], key[1], key[2], &ray);
+            emit(key[0], key[1], key[2], L);
+            ++nPath;
+            arena.FreeAll();
+        }
+        fclose(kf);
+        fclose(pf);
+        fprintf(stderr, "harness: %ld keyed paths traced (%d spp), %ld zeroed by NaN/inf guards\n", nPath, spp, nBad);
+        return 0;
+    }
     for (int y = ys; y < ye; ++y)
         for (int x = xs; x < xe; ++x)
             for (int s = 0; s < spp; ++s) {
-                FillSample(smp, x, y, (uint32_t)s, (uint32_t)spp, (uint32_t)seed,
-                           gCamera->shutterOpen, gCamera->shutterClose);
                 RayDifferential ray;
-                float rayWeight = gCamera->GenerateRayDifferential(*smp, &ray);
-                ray.ScaleDifferentials(1.f / sqrtf(spp));
-                RNG rng(path_seed(pixel_hash((uint32_t)seed, x, y), (uint32_t)s));
-                Spectrum L;
-                Intersection isect;
-                Spectrum T;
-                if (rayWeight > 0.f) L = rayWeight * renderer.Li(gScene, ray, smp, rng, arena, &isect, &T);
-                else L = 0.f;
-                if (L.HasNaNs()) { L = Spectrum(0.f); ++nBad; }
-                else if (L.y() < -1e-5) { L = Spectrum(0.f); ++nBad; }
-                else if (isinf(L.y())) { L = Spectrum(0.f); ++nBad; }
+                Spectrum L = trace(x, y, s, &ray);
                 gFilm->AddSample(*smp, L, ray);
-                if (pf && (pathEvery <= 1 || (nPath % pathEvery) == 0)) {
-                    int key[3] = { x, y, s };
-                    float c[nSpectralSamples];
-                    L.GetOrigC(c);
-                    fwrite(key, 4, 3, pf);
-                    fwrite(c, 4, nSpectralSamples, pf);
-                }
+                if (refFilm) refFilm->AddSample(*smp, L, ray);
+                if (pf && (pathEvery <= 1 || (nPath % pathEvery) == 0)) emit(x, y, s, L);
                 ++nPath;
                 arena.FreeAll();
             }
     if (pf) fclose(pf);
     if (rawOut) gFilm->WriteRaw(rawOut);
     if (datOut) gFilm->WriteDat(datOut);
+    if (refFilm) refFilm->WriteImage(1.f);
     fprintf(stderr, "harness: %ld paths traced (%d spp), %ld zeroed by NaN/inf guards\n", nPath, spp, nBad);
     return 0;
 }

@@ -22,6 +22,8 @@
 #include <cstring>
 #include <cstdio>
 #include <mutex>
+#include <thread>
+#include <atomic>
 #include "pbrtgpu.h"
 #include "device.h"
 #include "wavefront.h"
@@ -53,7 +55,8 @@ static int fail(int code, const std::string &msg) { g_err = msg; return code; }
 #ifndef PGD_PASS_BATCH   // wavefront passes enqueued per counter read-back (<= 8)
 #define PGD_PASS_BATCH 4
 #endif
-#ifndef PGD_LBUF_GIB   // per-sample radiance buffer of one spp batch (GiB)
+static_assert(PGD_PASS_BATCH >= 1 && PGD_PASS_BATCH <= 8, "Lane::ev holds the events of at most 8 passes");
+#ifndef PGD_LBUF_GIB   // default per-sample radiance buffer of one spp batch (GiB); PBRTGPU_LBUF_MB overrides
 #define PGD_LBUF_GIB 16   // C2: one 256-spp batch per frame (one drain instead of four): 265 -> 288 Mpaths/s
 #endif
 #ifndef PGD_TRACE_BLOCK
@@ -298,13 +301,14 @@ __global__ void k_accum(const float *__restrict__ Lbuf, const int *__restrict__ 
 
 // spill scan over the sample extent: queue samples that land on a masked film pixel
 // other than their own sample pixel (spectralImage.cpp:80-92, box filter width 0.5)
-__global__ void k_spill_scan(pbrtgpu_camera cam, uint32_t seed, int spp, const uint8_t *__restrict__ mask,
+// over the samples [s0, s1) of a render call
+__global__ void k_spill_scan(pbrtgpu_camera cam, uint32_t seed, int spp, int s0, int s1, const uint8_t *__restrict__ mask,
                              int3 *__restrict__ keys, unsigned int *__restrict__ count, unsigned int cap) {
-    const int ew = cam.sx_end - cam.sx_start, eh = cam.sy_end - cam.sy_start;
-    const long n = (long)ew * eh * spp;
+    const int ew = cam.sx_end - cam.sx_start, eh = cam.sy_end - cam.sy_start, ns = s1 - s0;
+    const long n = (long)ew * eh * ns;
     for (long it = (long)blockIdx.x * blockDim.x + threadIdx.x; it < n; it += (long)gridDim.x * blockDim.x) {
-        long pi = it / spp;
-        int s = (int)(it - pi * spp);
+        long pi = it / ns;
+        int s = s0 + (int)(it - pi * ns);
         int x = cam.sx_start + (int)(pi % ew), y = cam.sy_start + (int)(pi / ew);
         uint32_t hp = pixel_hash(seed, x, y);
         float u[2];
@@ -336,6 +340,15 @@ __global__ void k_apply(int nTargets, const int *__restrict__ tgt, const int *__
     float acc = film[(long)tgt[q] * nb + b];
     for (int e = start[q]; e < start[q + 1]; ++e) acc += 1.f * Lsp[(long)src[e] * nb + b];
     film[(long)tgt[q] * nb + b] = acc;
+}
+
+// film gather: out[p][b] = film[fidx[p]][b] (the pixels of a tile list, packed for one copy)
+__global__ void k_pack(const float *__restrict__ film, const int *__restrict__ fidx, int nPix, int nb,
+                       float *__restrict__ out) {
+    long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (long)nPix * nb) return;
+    int p = (int)(t / nb), b = (int)(t - (long)p * nb);
+    out[t] = film[(long)fidx[p] * nb + b];
 }
 
 __global__ __launch_bounds__(kTraceBlock) void k_intersect(DevScene S, const float *__restrict__ rays, int n,
@@ -409,7 +422,7 @@ struct pbrtgpu_ctx {
     int feat = 0;   // FEAT_* of the uploaded scene: selects the k_shade variant
     pbrtgpu_camera cam{};
     std::vector<DevBuf> sceneBufs;
-    DevBuf film, Lbuf, pix, filmIdx, mask, keys, counter, spillL, lists[4], scratch[3];
+    DevBuf film, Lbuf, pix, filmIdx, mask, keys, counter, spillL, lists[4], scratch[3], gather[2];
     int numCUs = 256;
     int ptBlocksPerCU = 0;    // occupancy of k_trace_pt closest (computed on first use)
     int ptBlocksPerCUS = 0;   // occupancy of k_trace_pt shadow
@@ -429,11 +442,24 @@ template <class T> static hipError_t upload(pbrtgpu_ctx *c, const T *src, size_t
     return e;
 }
 
-// path slots: PATH_SLOTS env override (tests use small capacities to exercise regeneration)
+// path slots: PBRTGPU_SLOTS env override (tests use small capacities to exercise regeneration)
 static int slot_target() {
     const char *e = getenv("PBRTGPU_SLOTS");
     int v = e ? atoi(e) : 0;
     return v > 0 ? v : (1 << 23);   // 8 M slots = 2 lanes x 4 M (C2 r01p: 289 -> 301 Mpaths/s vs 2 x 2 M)
+}
+// per-sample radiance budget of one spp batch: PBRTGPU_LBUF_MB env override (tests force
+// many batches per frame with a tiny budget)
+static size_t lbuf_budget() {
+    const char *e = getenv("PBRTGPU_LBUF_MB");
+    long v = e ? atol(e) : 0;
+    return v > 0 ? ((size_t)v << 20) : ((size_t)PGD_LBUF_GIB << 30);
+}
+// PBRTGPU_SERIAL=1: one lane, shadow queries on the lane's main stream -- no two kernels of
+// a render overlap, so each kernel's event spans are its exclusive device time (roofline)
+static bool serial_mode() {
+    const char *e = getenv("PBRTGPU_SERIAL");
+    return e && atoi(e) != 0;
 }
 
 static int ensure_slots(Lane *c, int cap, int NB) {
@@ -491,9 +517,10 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
     // scenes without measured BRDFs, textures and environment lights run the variant with
     // that code compiled out (fewer registers, no kd-tree stack)
     auto kShade = c->feat ? launch_shade<NB, FEAT_ALL> : launch_shade<NB, 0>;
-    struct Run { Lane *L; ItemSrc src; int cap, grid, q, batch; bool done; };
+    struct Run { Lane *L; ItemSrc src; int cap, grid, q, batch, passes, maxPasses; bool done; };
     Run R[kLanes];
-    const int nl = src.nItems >= 8192u ? kLanes : 1;
+    const bool serial = serial_mode();
+    const int nl = (src.nItems >= 8192u && !serial) ? kLanes : 1;
     HIPCHK(hipEventRecord(c->ev[0], c->stream));   // the other lanes start after the work queued so far
     for (int l = 0; l < nl; ++l) {
         Run &r = R[l];
@@ -508,6 +535,12 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
         r.q = 0;
         r.batch = 0;
         r.done = false;
+        // drain bound of this run: a path lives at most maxDepth + 3 passes (camera ray,
+        // maxDepth + 1 vertices, the finish of the last one), so every slot takes a new item
+        // at least once per maxDepth + 3 passes while items remain; twice that, plus the
+        // overshoot of one enqueued batch, means the wavefront is stuck
+        r.passes = 0;
+        r.maxPasses = 2 * (int)((r.src.nItems + r.cap - 1) / r.cap + 1) * (c->S.maxDepth + 3) + 2 * kPassBatch;
         if (int e = ensure_slots(&L, r.cap, NB)) return e;
         HIPCHK(L.spill.ensure(2 * spillLane * sizeof(uint2)));
         if (l > 0) HIPCHK(hipStreamWaitEvent(L.s, c->ev[0], 0));
@@ -549,8 +582,10 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
                 if (zeroedOut) *zeroedOut += L.hostCnt[CNT_ZEROED];
                 continue;
             }
-            if (T.passes > 4096) return fail(PBRTGPU_E_STATE, "wavefront did not drain");
+            if (r.passes > r.maxPasses) return fail(PBRTGPU_E_STATE, "wavefront did not drain");
             uint2 *spillC = (uint2 *)L.spill.p, *spillS = spillC + spillLane;
+            // serial mode: the shadow queries follow the closest-hit queries on the main stream
+            hipStream_t s2 = serial ? L.s : L.s2;
             r.batch = kPassBatch;
             for (int j = 0; j < r.batch; ++j) {
                 hipEvent_t *e = L.ev + 2 + 6 * j;
@@ -558,9 +593,36 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
                 HIPCHK(hipMemsetAsync(P.cnt + CNT_QC(nq), 0, 4, L.s));
                 HIPCHK(hipMemsetAsync(P.cnt + CNT_QS(nq), 0, 4, L.s));
                 HIPCHK(hipEventRecord(e[0], L.s));
+                if (serial) {   // closest-hit queries first, alone on the device
+                    if (inst) {
+                        if (countWork) hipLaunchKernelGGL((k_trace_closest<true, true>), dim3(traceGrid), dim3(kTraceBlock), lds, L.s, c->S, P, q);
+                        else hipLaunchKernelGGL((k_trace_closest<false, true>), dim3(traceGrid), dim3(kTraceBlock), lds, L.s, c->S, P, q);
+                    } else if (countWork) hipLaunchKernelGGL((k_trace_pt<false, true>), dim3(ptGrid), dim3(kTraceBlock), 0, L.s, c->S, P, q, c->refill, c->ring, spillC);
+                    else hipLaunchKernelGGL((k_trace_pt<false, false>), dim3(ptGrid), dim3(kTraceBlock), 0, L.s, c->S, P, q, c->refill, c->ring, spillC);
+                    HIPCHK(hipGetLastError());
+                    HIPCHK(hipEventRecord(e[1], L.s));
+                    HIPCHK(hipEventRecord(e[2], L.s));
+                    if (inst) {
+                        if (countWork) hipLaunchKernelGGL((k_trace_shadow<true, true>), dim3(traceGrid), dim3(kTraceBlock), ldsS, L.s, c->S, P, q);
+                        else hipLaunchKernelGGL((k_trace_shadow<false, true>), dim3(traceGrid), dim3(kTraceBlock), ldsS, L.s, c->S, P, q);
+                    } else if (countWork) hipLaunchKernelGGL((k_trace_pt<true, true>), dim3(ptGridS), dim3(kTraceBlock), 0, L.s, c->S, P, q, c->refill, c->ring, spillS);
+                    else hipLaunchKernelGGL((k_trace_pt<true, false>), dim3(ptGridS), dim3(kTraceBlock), 0, L.s, c->S, P, q, c->refill, c->ring, spillS);
+                    HIPCHK(hipGetLastError());
+                    T.launches[K_CLOSEST]++;
+                    T.launches[K_SHADOW]++;
+                    HIPCHK(hipEventRecord(e[3], L.s));
+                    HIPCHK(hipEventRecord(e[4], L.s));
+                    HIPCHK(kShade(r.grid, L.s, c->S, P, r.src, nq, Lout));
+                    T.launches[K_SHADE]++;
+                    HIPCHK(hipEventRecord(e[5], L.s));
+                    T.passes++;
+                    r.passes++;
+                    q = nq;
+                    continue;
+                }
                 // shadow queries of queue set q on s2, after the counter resets
-                HIPCHK(hipStreamWaitEvent(L.s2, e[0], 0));
-                HIPCHK(hipEventRecord(e[2], L.s2));
+                HIPCHK(hipStreamWaitEvent(s2, e[0], 0));
+                HIPCHK(hipEventRecord(e[2], s2));
                 // instanced scenes walk nested BVHs (bvh_walk); the others run the persistent
                 // ray-replacement kernels over the whole (wave-partitioned) queue
                 if (inst) {
@@ -573,20 +635,21 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
                     if (countWork) hipLaunchKernelGGL((k_trace_pt<false, true>), dim3(ptGrid), dim3(kTraceBlock), 0, L.s, c->S, P, q, c->refill, c->ring, spillC);
                     else hipLaunchKernelGGL((k_trace_pt<false, false>), dim3(ptGrid), dim3(kTraceBlock), 0, L.s, c->S, P, q, c->refill, c->ring, spillC);
                     HIPCHK(hipGetLastError());
-                    if (countWork) hipLaunchKernelGGL((k_trace_pt<true, true>), dim3(ptGridS), dim3(kTraceBlock), 0, L.s2, c->S, P, q, c->refill, c->ring, spillS);
-                    else hipLaunchKernelGGL((k_trace_pt<true, false>), dim3(ptGridS), dim3(kTraceBlock), 0, L.s2, c->S, P, q, c->refill, c->ring, spillS);
+                    if (countWork) hipLaunchKernelGGL((k_trace_pt<true, true>), dim3(ptGridS), dim3(kTraceBlock), 0, s2, c->S, P, q, c->refill, c->ring, spillS);
+                    else hipLaunchKernelGGL((k_trace_pt<true, false>), dim3(ptGridS), dim3(kTraceBlock), 0, s2, c->S, P, q, c->refill, c->ring, spillS);
                 }
                 HIPCHK(hipGetLastError());
                 T.launches[K_CLOSEST]++;
                 T.launches[K_SHADOW]++;
                 HIPCHK(hipEventRecord(e[1], L.s));
-                HIPCHK(hipEventRecord(e[3], L.s2));
+                HIPCHK(hipEventRecord(e[3], s2));
                 HIPCHK(hipStreamWaitEvent(L.s, e[3], 0));
                 HIPCHK(hipEventRecord(e[4], L.s));
                 HIPCHK(kShade(r.grid, L.s, c->S, P, r.src, nq, Lout));
                 T.launches[K_SHADE]++;
                 HIPCHK(hipEventRecord(e[5], L.s));
                 T.passes++;
+                r.passes++;
                 q = nq;
             }
             r.q = q;
@@ -686,7 +749,7 @@ int pbrtgpu_context_destroy(pbrtgpu_ctx *c) {
     for (auto &b : c->sceneBufs) b.release();
     DevBuf *bufs[] = {&c->film, &c->Lbuf, &c->pix, &c->filmIdx, &c->mask, &c->keys, &c->counter, &c->spillL,
                       &c->lists[0], &c->lists[1], &c->lists[2], &c->lists[3], &c->scratch[0],
-                      &c->scratch[1], &c->scratch[2]};
+                      &c->scratch[1], &c->scratch[2], &c->gather[0], &c->gather[1]};
     for (DevBuf *b : bufs) b->release();
     for (int i = 0; i < 8; ++i) if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
     for (Lane &L : c->lane) {
@@ -934,37 +997,52 @@ int pbrtgpu_film_read(pbrtgpu_ctx *c, float *out, int64_t n) {
 
 }  // extern "C"
 
+// Film pixels of a tile list.  Tiles are tile_w x tile_h blocks of the FILM pixel window
+// (px_count x py_count, row-major tile ids, ragged last row / column); tile_ids == NULL
+// means every tile.  fidx = film indices (y * px_count + x) in tile order without repeats,
+// mask = 1 on those pixels.
+static int tile_pixels(const pbrtgpu_camera &cam, int tile_w, int tile_h, const int32_t *tiles, int32_t ntiles,
+                       std::vector<int> *fidx, std::vector<uint8_t> *mask) {
+    const int tw = tile_w > 0 ? tile_w : 16, th = tile_h > 0 ? tile_h : 16;
+    const int ntx = (cam.px_count + tw - 1) / tw, nty = (cam.py_count + th - 1) / th;
+    mask->assign((size_t)cam.px_count * cam.py_count, 0);
+    fidx->clear();
+    auto addTile = [&](int t) {
+        int tx = t % ntx, ty = t / ntx;
+        for (int y = ty * th; y < std::min(cam.py_count, (ty + 1) * th); ++y)
+            for (int x = tx * tw; x < std::min(cam.px_count, (tx + 1) * tw); ++x) {
+                size_t fi = (size_t)y * cam.px_count + x;
+                if ((*mask)[fi]) continue;
+                (*mask)[fi] = 1;
+                fidx->push_back((int)fi);
+            }
+    };
+    if (!tiles) for (int t = 0; t < ntx * nty; ++t) addTile(t);
+    else {
+        if (ntiles < 0) return fail(PBRTGPU_E_INVALID, "negative tile count");
+        for (int i = 0; i < ntiles; ++i) {
+            if (tiles[i] < 0 || tiles[i] >= ntx * nty) return fail(PBRTGPU_E_INVALID, "tile id out of range");
+            addTile(tiles[i]);
+        }
+    }
+    return 0;
+}
+
 template <int NB>
 static int render_impl(pbrtgpu_ctx *c, const pbrtgpu_render_desc *d, const int32_t *tiles, int32_t ntiles, double *stats) {
     const pbrtgpu_camera &cam = c->cam;
     const int spp = c->spp;
     int s0 = d->spp_begin, s1 = d->spp_end;
     if (s0 < 0 || s1 > spp || s0 >= s1) return fail(PBRTGPU_E_INVALID, "bad sample range");
-    int tw = d->tile_w > 0 ? d->tile_w : 16, th = d->tile_h > 0 ? d->tile_h : 16;
-    int ntx = (cam.px_count + tw - 1) / tw, nty = (cam.py_count + th - 1) / th;
     const bool countWork = (d->flags & PBRTGPU_F_COUNT_WORK) != 0;
     Timing T;
     // pixel list of the requested tiles (film pixels; own sample pixel == film pixel)
-    std::vector<int2> pix;
     std::vector<int> fidx;
-    std::vector<uint8_t> mask((size_t)cam.px_count * cam.py_count, 0);
-    auto addTile = [&](int t) {
-        int tx = t % ntx, ty = t / ntx;
-        for (int y = ty * th; y < std::min(cam.py_count, (ty + 1) * th); ++y)
-            for (int x = tx * tw; x < std::min(cam.px_count, (tx + 1) * tw); ++x) {
-                size_t fi = (size_t)y * cam.px_count + x;
-                if (mask[fi]) continue;
-                mask[fi] = 1;
-                pix.push_back(make_int2(cam.px_start + x, cam.py_start + y));
-                fidx.push_back((int)fi);
-            }
-    };
-    if (!tiles) for (int t = 0; t < ntx * nty; ++t) addTile(t);
-    else
-        for (int i = 0; i < ntiles; ++i) {
-            if (tiles[i] < 0 || tiles[i] >= ntx * nty) return fail(PBRTGPU_E_INVALID, "tile id out of range");
-            addTile(tiles[i]);
-        }
+    std::vector<uint8_t> mask;
+    if (int e = tile_pixels(cam, d->tile_w, d->tile_h, tiles, ntiles, &fidx, &mask)) return e;
+    std::vector<int2> pix(fidx.size());
+    for (size_t i = 0; i < fidx.size(); ++i)
+        pix[i] = make_int2(cam.px_start + fidx[i] % cam.px_count, cam.py_start + fidx[i] / cam.px_count);
     const int nPix = (int)pix.size();
     double st[PBRTGPU_STAT_COUNT] = {0};
     if (!(d->flags & PBRTGPU_F_ACCUMULATE) && s0 == 0)
@@ -976,20 +1054,22 @@ static int render_impl(pbrtgpu_ctx *c, const pbrtgpu_render_desc *d, const int32
     HIPCHK(hipMemcpyAsync(c->filmIdx.p, fidx.data(), fidx.size() * sizeof(int), hipMemcpyHostToDevice, c->stream));
     unsigned int zeroed = 0;
 
-    // ---- spill samples (only meaningful when the whole sample range is rendered)
+    // ---- spill samples of the call's sample range [s0, s1).  A frame rendered as one call
+    // adds every pixel's contributions in the reference's order; a frame split into sample
+    // ranges (F_ACCUMULATE) adds the same contributions, range by range, so its sums differ
+    // from the one-call film only in float summation order
     std::vector<int> preT, preStart, preSrc, postT, postStart, postSrc;
     int nSpill = 0;
-    bool doSpills = (s0 == 0 && s1 == spp);
-    if (doSpills) {
+    {
         HIPCHK(c->mask.ensure(mask.size()));
         HIPCHK(hipMemcpyAsync(c->mask.p, mask.data(), mask.size(), hipMemcpyHostToDevice, c->stream));
         unsigned int cap = 1u << 20;
         HIPCHK(c->keys.ensure((size_t)cap * sizeof(int3)));
         HIPCHK(c->counter.ensure(16));
         HIPCHK(hipMemsetAsync(c->counter.p, 0, 16, c->stream));
-        long nsamp = (long)(cam.sx_end - cam.sx_start) * (cam.sy_end - cam.sy_start) * spp;
+        long nsamp = (long)(cam.sx_end - cam.sx_start) * (cam.sy_end - cam.sy_start) * (s1 - s0);
         int grid = (int)std::min<long>((nsamp + 255) / 256, (long)c->numCUs * 16);
-        hipLaunchKernelGGL(k_spill_scan, dim3(grid), dim3(256), 0, c->stream, cam, c->S.seed, spp,
+        hipLaunchKernelGGL(k_spill_scan, dim3(grid), dim3(256), 0, c->stream, cam, c->S.seed, spp, s0, s1,
                            (const uint8_t *)c->mask.p, (int3 *)c->keys.p, (unsigned int *)c->counter.p, cap);
         HIPCHK(hipGetLastError());
         unsigned int cnt = 0;
@@ -1074,7 +1154,7 @@ static int render_impl(pbrtgpu_ctx *c, const pbrtgpu_render_desc *d, const int32
     if (int e = applyLists(preT, preStart, preSrc)) return e;
 
     // ---- main batches: per-sample radiance for (pixels x batch samples), then the ordered film sum
-    const size_t lbudget = (size_t)PGD_LBUF_GIB << 30;   // per-sample radiance per batch
+    const size_t lbudget = lbuf_budget();   // per-sample radiance per batch
     int sb = (int)std::max<long>(1, std::min<long>(s1 - s0, (long)(lbudget / ((size_t)nPix * NB * 4))));
     if ((uint64_t)nPix * sb > 0x7fffffffull) sb = std::max(1, (int)(0x7fffffffll / nPix));
     HIPCHK(c->Lbuf.ensure((size_t)nPix * sb * NB * 4));
@@ -1135,6 +1215,96 @@ int pbrtgpu_render_tiles(pbrtgpu_ctx *c, const pbrtgpu_render_desc *d, const int
         case 30: return render_impl<30>(c, d, tile_ids, ntiles, stats);
     }
     return fail(PBRTGPU_E_UNSUPPORTED, "band count");
+}
+
+int pbrtgpu_film_gather(pbrtgpu_ctx *c, int32_t tile_w, int32_t tile_h, const int32_t *tile_ids, int32_t ntiles,
+                        float *film_out, int64_t n_floats) {
+    if (!c || !c->hasScene || !film_out) return fail(PBRTGPU_E_STATE, "no scene / null out");
+    if (!tile_ids) return pbrtgpu_film_read(c, film_out, n_floats);
+    const size_t need = (size_t)c->cam.px_count * c->cam.py_count * c->nb;
+    if (n_floats < 0 || (size_t)n_floats < need) return fail(PBRTGPU_E_INVALID, "film buffer too small");
+    std::vector<int> fidx;
+    std::vector<uint8_t> mask;
+    if (int e = tile_pixels(c->cam, tile_w, tile_h, tile_ids, ntiles, &fidx, &mask)) return e;
+    if (fidx.empty()) return 0;
+    HIPCHK(hipSetDevice(c->device));
+    const int nb = c->nb, nPix = (int)fidx.size();
+    HIPCHK(c->gather[0].ensure(fidx.size() * sizeof(int)));
+    HIPCHK(c->gather[1].ensure((size_t)nPix * nb * 4));
+    HIPCHK(hipMemcpyAsync(c->gather[0].p, fidx.data(), fidx.size() * sizeof(int), hipMemcpyHostToDevice, c->stream));
+    const long n = (long)nPix * nb;
+    hipLaunchKernelGGL(k_pack, dim3((n + 255) / 256), dim3(256), 0, c->stream, (const float *)c->film.p,
+                       (const int *)c->gather[0].p, nPix, nb, (float *)c->gather[1].p);
+    HIPCHK(hipGetLastError());
+    std::vector<float> packed((size_t)n);
+    HIPCHK(hipMemcpyAsync(packed.data(), c->gather[1].p, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    for (int p = 0; p < nPix; ++p) memcpy(film_out + (size_t)fidx[p] * nb, packed.data() + (size_t)p * nb, (size_t)nb * 4);
+    return 0;
+}
+
+int pbrtgpu_render_multi(pbrtgpu_ctx *const *ctxs, int32_t n, const pbrtgpu_render_desc *desc, const int32_t *tile_ids,
+                         int32_t ntiles, int32_t slices_per_ctx, float *film_out, int64_t n_floats, double *stats_out) {
+    if (!ctxs || n <= 0 || !desc || !film_out) return fail(PBRTGPU_E_INVALID, "bad arguments");
+    for (int i = 0; i < n; ++i) {
+        if (!ctxs[i] || !ctxs[i]->hasScene) return fail(PBRTGPU_E_STATE, "context without a scene");
+        for (int j = 0; j < i; ++j)
+            if (ctxs[j] == ctxs[i]) return fail(PBRTGPU_E_INVALID, "a context is listed twice");
+        const pbrtgpu_camera &a = ctxs[0]->cam, &b = ctxs[i]->cam;
+        if (ctxs[i]->nb != ctxs[0]->nb || ctxs[i]->spp != ctxs[0]->spp || a.px_count != b.px_count ||
+            a.py_count != b.py_count || a.px_start != b.px_start || a.py_start != b.py_start)
+            return fail(PBRTGPU_E_INVALID, "contexts hold different scenes / films");
+    }
+    const pbrtgpu_camera &cam = ctxs[0]->cam;
+    if (n_floats < 0 || (size_t)n_floats < (size_t)cam.px_count * cam.py_count * ctxs[0]->nb)
+        return fail(PBRTGPU_E_INVALID, "film buffer too small");
+    // the frame's tile list, dealt into m interleaved slices (slice j = list[j], list[j + m], ...):
+    // each slice spreads over the whole image, so slices cost about the same
+    const int tw = desc->tile_w > 0 ? desc->tile_w : 16, th = desc->tile_h > 0 ? desc->tile_h : 16;
+    const int ntx = (cam.px_count + tw - 1) / tw, nty = (cam.py_count + th - 1) / th;
+    std::vector<int32_t> list;
+    if (tile_ids) {
+        if (ntiles < 0) return fail(PBRTGPU_E_INVALID, "negative tile count");
+        list.assign(tile_ids, tile_ids + ntiles);
+    } else
+        for (int t = 0; t < ntx * nty; ++t) list.push_back(t);
+    for (int32_t t : list)
+        if (t < 0 || t >= ntx * nty) return fail(PBRTGPU_E_INVALID, "tile id out of range");
+    const int m = n * std::max(1, (int)slices_per_ctx);
+    std::atomic<int> next(0);
+    std::vector<int> rc(n, 0);
+    std::vector<std::string> msg(n);
+    std::vector<double> st((size_t)n * PBRTGPU_STAT_COUNT, 0.0);
+    auto worker = [&](int i) {
+        pbrtgpu_ctx *c = ctxs[i];
+        std::vector<int32_t> mine;
+        bool first = true;
+        for (int j; (j = next.fetch_add(1)) < m;) {
+            std::vector<int32_t> slice;
+            for (size_t k = (size_t)j; k < list.size(); k += (size_t)m) slice.push_back(list[k]);
+            if (slice.empty()) continue;
+            pbrtgpu_render_desc d = *desc;
+            if (!first) d.flags |= PBRTGPU_F_ACCUMULATE;   // the slices of one context share its film
+            double s8[PBRTGPU_STAT_COUNT] = {0};
+            int e = pbrtgpu_render_tiles(c, &d, slice.data(), (int32_t)slice.size(), s8);
+            if (e) { rc[i] = e; msg[i] = g_err; return; }
+            for (int k = 0; k < PBRTGPU_STAT_COUNT; ++k) st[(size_t)i * PBRTGPU_STAT_COUNT + k] += s8[k];
+            mine.insert(mine.end(), slice.begin(), slice.end());
+            first = false;
+        }
+        if (mine.empty()) return;
+        // host gather: this context's film pixels (disjoint from every other context's)
+        int e = pbrtgpu_film_gather(c, tw, th, mine.data(), (int32_t)mine.size(), film_out, n_floats);
+        if (e) { rc[i] = e; msg[i] = g_err; }
+    };
+    std::vector<std::thread> threads;
+    for (int i = 1; i < n; ++i) threads.emplace_back(worker, i);
+    worker(0);
+    for (auto &t : threads) t.join();
+    if (stats_out) memcpy(stats_out, st.data(), st.size() * sizeof(double));
+    for (int i = 0; i < n; ++i)
+        if (rc[i]) return fail(rc[i], "context " + std::to_string(i) + ": " + msg[i]);
+    return 0;
 }
 
 }  // extern "C"

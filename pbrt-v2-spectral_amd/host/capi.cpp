@@ -1,6 +1,7 @@
 // capi.cpp -- C ABI of the host library (libpbrthost.so): scene loading (pbrt files or
 // scene packs), flattening, and the reference's multispectral .dat writer.
 // Declarations: include/pbrthost.h.
+#include <sstream>
 #include "pbrthost.h"
 #include "scene.h"
 #include <cstring>
@@ -80,6 +81,17 @@ int pbrthost_info(pbrthost_scene *h, int64_t *info, int n) {
 
 // SpectralImageFilm::WriteImage (spectralImage.cpp:267-378), identity conversion matrix.
 // film: [H][W][N] float32 raw sums; weight: [H][W] (filter weight sums, may be NULL = all 1).
+// "focal fStop fov\n" with fov = 2 atan(sensorWidth / (2 focal)) / pi * 180 in the film's
+// float / double mix, formatted by an ostream (default precision 6, "-nan" for the sign-set
+// NaN x86 produces for 0 / 0)
+static std::string dat_lens_line(float focal, float fStop, float sensorWidth) {
+    volatile float den = 2 * focal;   // evaluated at run time, as in the reference
+    const float fov = (float)(2 * atanf(sensorWidth / den) / 3.1415926539 * 180);
+    std::ostringstream os;
+    os << focal << " " << fStop << " " << fov << "\n";
+    return os.str();
+}
+
 int pbrthost_write_dat(const char *path, const float *film, const float *weight, int W, int H, int N) {
     int nPix = W * H;
     std::vector<float> finalC((size_t)N * nPix);
@@ -104,7 +116,11 @@ int pbrthost_write_dat(const char *path, const float *film, const float *weight,
     FILE *f = fopen(path, "w");
     if (!f) return -1;
     fprintf(f, "%d %d %d\n", W, H, N);
-    fprintf(f, "0 0 0\n");   // focalLength fStop fov (0 for a perspective camera)
+    // line 2: focalLength fStop fov as the film's ofstream formats them
+    // (spectralImage.cpp:356-360).  CreateSpectralImageFilm leaves focal length, f-stop and
+    // sensor width at 0 for every camera but RealisticDiffraction (:400-429), so the field
+    // of view is 2 atan(0 / 0) ... = the x86 default NaN, printed "-nan"
+    fputs(dat_lens_line(0.f, 0.f, 0.f).c_str(), f);
     for (int i = 0; i < N; ++i)
         for (int j = 0; j < nPix; ++j) { double r = outv[(size_t)N * j + i]; fwrite(&r, 8, 1, f); }
     fclose(f);

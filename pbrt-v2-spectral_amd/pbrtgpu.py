@@ -145,6 +145,8 @@ def gpu_lib():
         g.pbrtgpu_intersect.argtypes = [P, P, I32, P, P]
         g.pbrtgpu_path_stats.argtypes = [P, P, I32, P]
         g.pbrtgpu_last_timing.argtypes = [P, ctypes.POINTER(Timing)]
+        g.pbrtgpu_film_gather.argtypes = [P, I32, I32, P, I32, P, ctypes.c_int64]
+        g.pbrtgpu_render_multi.argtypes = [P, I32, ctypes.POINTER(RenderDesc), P, I32, I32, P, ctypes.c_int64, P]
     return _gpu
 
 
@@ -153,7 +155,21 @@ def gpu_symbols():
     return ["pbrtgpu_abi_version", "pbrtgpu_device_count", "pbrtgpu_context_create",
             "pbrtgpu_context_destroy", "pbrtgpu_last_error", "pbrtgpu_scene_upload",
             "pbrtgpu_render_tiles", "pbrtgpu_film_read", "pbrtgpu_film_clear",
-            "pbrtgpu_trace_paths", "pbrtgpu_intersect", "pbrtgpu_path_stats", "pbrtgpu_last_timing"]
+            "pbrtgpu_trace_paths", "pbrtgpu_intersect", "pbrtgpu_path_stats", "pbrtgpu_last_timing",
+            "pbrtgpu_film_gather", "pbrtgpu_render_multi"]
+
+
+def tile_grid(scene, tile=16):
+    """(ntx, nty) of the film-pixel tile grid the C ABI uses (pbrtgpu.h, pbrtgpu_render_desc)."""
+    tw, th = (tile, tile) if isinstance(tile, int) else tile
+    return (scene.width + tw - 1) // tw, (scene.height + th - 1) // th
+
+
+def tile_slice(ntiles, j, m):
+    """Slice j of m of a frame's tiles: tiles j, j + m, j + 2m, ... (interleaved, so every
+    slice spreads over the whole image and slices cost about the same).  The same dealing as
+    pbrtgpu_render_multi; a rank of a multi-process render takes slice `rank` of `world`."""
+    return np.arange(j, ntiles, m, dtype=np.int32)
 
 
 class Scene:
@@ -270,6 +286,19 @@ class Device:
         _check(self.lib.pbrtgpu_film_read(self.ctx, out.ctypes.data, out.size))
         return out
 
+    def gather(self, out, tiles=None, tile=(16, 16)):
+        """Host gather: writes the film pixels of `tiles` (all when None) into `out` (a float32
+        [H][W][bands] array, e.g. a shared-memory film), leaving its other pixels untouched."""
+        s = self.scene
+        assert out.dtype == np.float32 and out.flags.c_contiguous and out.size >= s.height * s.width * s.bands
+        if tiles is None:
+            _check(self.lib.pbrtgpu_film_gather(self.ctx, tile[0], tile[1], None, 0, out.ctypes.data, out.size))
+        else:
+            t = np.ascontiguousarray(tiles, dtype=np.int32)
+            _check(self.lib.pbrtgpu_film_gather(self.ctx, tile[0], tile[1], t.ctypes.data, len(t), out.ctypes.data,
+                                                out.size))
+        return out
+
     def clear(self):
         _check(self.lib.pbrtgpu_film_clear(self.ctx))
 
@@ -303,6 +332,29 @@ class Device:
             out[k] = {"ms": t.ms[i], "launches": t.launches[i]}
         out["work"] = {k: int(t.work[i]) for i, k in enumerate(Timing.WORK)}
         return out
+
+
+def render_multi(devices, spp_begin=0, spp_end=None, tiles=None, tile=(16, 16), slices_per_device=1, out=None,
+                 accumulate=False):
+    """One frame over several Devices (one per GPU, same scene uploaded): pbrtgpu_render_multi
+    -- one host thread per device pulls interleaved tile slices, then gathers its tiles into
+    the returned film.  Returns (film, per-device stats [n][8])."""
+    s = devices[0].scene
+    n = len(devices)
+    arr = (P * n)(*[d.ctx for d in devices])
+    desc = RenderDesc(spp_begin, s.spp if spp_end is None else spp_end, tile[0], tile[1],
+                      F_ACCUMULATE if accumulate else 0, (I32 * 3)())
+    if out is None:
+        out = np.zeros((s.height, s.width, s.bands), dtype=np.float32)
+    st = np.zeros((n, 8), dtype=np.float64)
+    if tiles is None:
+        tp, nt = None, 0
+    else:
+        t = np.ascontiguousarray(tiles, dtype=np.int32)
+        tp, nt = t.ctypes.data, len(t)
+    _check(gpu_lib().pbrtgpu_render_multi(arr, n, ctypes.byref(desc), tp, nt, slices_per_device, out.ctypes.data,
+                                          out.size, st.ctypes.data))
+    return out, st
 
 
 # ---------------------------------------------------------------- test infrastructure

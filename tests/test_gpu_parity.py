@@ -110,9 +110,12 @@ def _golden_scene(pg, cfg, name="killeroo"):
 
 @pytest.mark.parametrize("name", ["killeroo_paths_64x64s4", "killeroo_paths_48x48s8_seed7_md7", "anim_paths_48x48s4",
                                   "bunny_paths_64x36s4", "metal_paths_48x48s4",
-                                  "coverage_paths_64x48s8"])
+                                  "coverage_paths_64x48s8", "killeroo_keys_c2_700x700s256",
+                                  "bunny_keys_c3_1920x1080s1024", "metal_keys_c4_400x400s4096",
+                                  "anim_keys_c5_600x600s512"])
 def test_paths_vs_reference_golden(pg, name):
-    """GPU against the reference harness's own per-path radiance (fixed seeds)."""
+    """GPU against the reference harness's own per-path radiance (fixed seeds); the *_keys_*
+    fixtures are the configs at their real resolution and sample count."""
     from conftest import GOLDEN
     g = np.load(os.path.join(GOLDEN, name + ".npz"))
     scene = _golden_scene(pg, g["config"], name)
@@ -158,8 +161,8 @@ def test_tile_shards_compose_to_full_frame(pg, killeroo64, dev):
     the full-frame film bit for bit."""
     dev.render()
     full = dev.film()
-    c = killeroo64.flat.camera
-    ntiles = ((c.px_count + 15) // 16) * ((c.py_count + 15) // 16)
+    ntx, nty = pg.tile_grid(killeroo64)
+    ntiles = ntx * nty
     dev.render(tiles=np.arange(0, ntiles, 2))
     dev.render(tiles=np.arange(1, ntiles, 2), accumulate=True)
     assert np.array_equal(full.view(np.int32), dev.film().view(np.int32))

@@ -101,6 +101,32 @@ def test_write_dat_layout(pg, tmp_path):
         for y in range(H):
             expect[:, x * H + y] = finalC[y * W + x]
     assert np.array_equal(data.reshape(N, W * H), expect)
+    # line 2: focal length, f-stop, field of view of a non-RealisticDiffraction camera
+    # (0, 0, 2 atan(0 / 0) ...), as the film's ofstream prints them
+    assert raw[l1 + 1:l2] == b"0 0 -nan"
+
+
+def test_write_dat_vs_reference_film(pg, tmp_path):
+    """The .dat of the reference's own spectral film (SpectralImageNoCameraFilm, compiled from
+    film/spectralImageNoCamera.cpp into the harness; same AddSample sums and WriteImage payload
+    as SpectralImageFilm, spectralImage.cpp:77-152, 267-378, but no lens line) against
+    pbrthost_write_dat of the harness's restatement film of the same render
+    (tests/golden/killeroo_dat_40x32s4.npz, tools/make_golden.py --only dat)."""
+    from conftest import GOLDEN
+    g = np.load(os.path.join(GOLDEN, "killeroo_dat_40x32s4.npz"))
+    film, ref = g["film"], g["dat"].tobytes()
+    H, W, N = film.shape
+    s = pg.Scene.load(PACK, xres=W, yres=H, spp=1)
+    fn = str(tmp_path / "k.dat")
+    s.write_dat(fn, film)
+    mine = open(fn, "rb").read()
+    r1 = ref.index(b"\n") + 1
+    m1 = mine.index(b"\n") + 1
+    m2 = mine.index(b"\n", m1) + 1
+    assert ref[:r1] == mine[:m1] == b"%d %d %d\n" % (W, H, N)
+    assert mine[m1:m2] == b"0 0 -nan\n"
+    assert len(ref) - r1 == W * H * N * 8
+    assert ref[r1:] == mine[m2:]          # payload bit for bit (float64 planes)
 
 
 @pytest.mark.reference

@@ -37,6 +37,11 @@ def exact_rate(name):
 
 PATHS = ["killeroo_paths_64x64s4", "killeroo_paths_48x48s8_seed7_md7", "anim_paths_48x48s4", "bunny_paths_64x36s4",
          "metal_paths_48x48s4", "coverage_paths_64x48s8"]
+# the configs at their real size and sample count (BASELINE.json configs 2-5; harness --keys):
+# every sample of a few pixels plus random keys of the whole sample extent
+KEYS = ["killeroo_keys_c2_700x700s256", "bunny_keys_c3_1920x1080s1024", "metal_keys_c4_400x400s4096",
+        "anim_keys_c5_600x600s512"]
+PATHS += KEYS
 
 
 @pytest.fixture(scope="module")

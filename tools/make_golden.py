@@ -25,7 +25,15 @@ Fixtures (numpy .npz, inputs + expected outputs only):
                                   floor with imagemap Kd + scaled imagemap bump (1x1 fallback
                                   texels, EWA filtering with camera ray differentials), infinite
                                   light (one-texel environment map)
-Usage: python tools/make_golden.py   (after `make -C oracle ref` and `make -C oracle ref60`)
+  <scene>_keys_<cfg>_*.npz         per-path radiance at the configs' REAL size and sample count
+                                  (C2 killeroo 700x700@256, C3 bunny 1920x1080@1024, C4 metal
+                                  400x400@4096 60 bands, C5 anim 600x600@512): every sample of a
+                                  few pixels (all of the sampler's permutation masks at that spp)
+                                  plus 2048 random (x, y, s) keys of the sample extent (--keys)
+  killeroo_dat_40x32s4.npz        the raw film of the restatement film AND the .dat the
+                                  reference's own SpectralImageNoCameraFilm wrote for the same
+                                  samples (--refdat): pins AddSample and the WriteImage payload
+Usage: python tools/make_golden.py [--only keys|dat]   (after `make -C oracle ref` and `make -C oracle ref60`)
 """
 import os
 import subprocess
@@ -74,10 +82,65 @@ def film_fixture(name, res, spp, seed, maxdepth, tmp, scene="killeroo-simple.pbr
     print(name, film.shape)
 
 
+# (name, scene file, pack, W, H, spp, bands, key seed): BASELINE.json configs 2-5 at full size
+KEY_CONFIGS = [("killeroo_keys_c2_700x700s256", "killeroo-simple.pbrt", 700, 700, 256, 32, 2),
+               ("bunny_keys_c3_1920x1080s1024", "bunny.pbrt", 1920, 1080, 1024, 32, 3),
+               ("metal_keys_c4_400x400s4096", "metal.pbrt", 400, 400, 4096, 60, 4),
+               ("anim_keys_c5_600x600s512", "anim-killeroos-moving.pbrt", 600, 600, 512, 32, 5)]
+
+
+def config_keys(W, H, spp, seed, n_random=2048):
+    """Every sample of max(1, 4096 // spp) random pixels, then n_random random keys, over the
+    box filter's sample extent [0, W + 1) x [0, H + 1) (spectralImage.cpp:176-185)."""
+    rng = np.random.RandomState(seed)
+    npx = max(1, 4096 // spp)
+    px = np.stack([rng.randint(0, W + 1, npx), rng.randint(0, H + 1, npx)], 1)
+    full = np.array([(x, y, s) for x, y in px for s in range(spp)], np.int32).reshape(-1, 3)
+    rnd = np.stack([rng.randint(0, W + 1, n_random), rng.randint(0, H + 1, n_random), rng.randint(0, spp, n_random)], 1)
+    return np.concatenate([full, rnd.astype(np.int32)])
+
+
+def keys_fixture(name, scene, W, H, spp, bands, kseed, tmp):
+    keys = config_keys(W, H, spp, kseed)
+    kf = os.path.join(tmp, name + ".keys")
+    keys.astype(np.int32).tofile(kf)
+    fn = os.path.join(tmp, name + ".bin")
+    run([os.path.join(SCENES, scene), "--res", str(W), str(H), "--spp", str(spp), "--seed", "0", "--maxdepth", "5",
+         "--keys", kf, "--paths", fn], bands)
+    k2, L, _, _ = read_paths(fn)
+    assert np.array_equal(k2, keys)
+    np.savez_compressed(os.path.join(OUT, name + ".npz"), keys=keys, L=L, config=np.array([W, H, spp, 0, 5], np.int32))
+    print(name, keys.shape)
+
+
+def dat_fixture(name, res, spp, tmp, scene="killeroo-simple.pbrt"):
+    """The restatement film (--raw) and the reference film's .dat (--refdat) of one render."""
+    raw, dat = os.path.join(tmp, name + ".f32"), os.path.join(tmp, name + ".dat")
+    run([os.path.join(SCENES, scene), "--res", str(res[0]), str(res[1]), "--spp", str(spp), "--seed", "0", "--maxdepth",
+         "5", "--raw", raw, "--refdat", dat])
+    r = np.fromfile(raw, dtype=np.int32)
+    W, H, N = r[:3]
+    film = r[3:].view(np.float32).reshape(H, W, N)
+    np.savez_compressed(os.path.join(OUT, name + ".npz"), film=film, dat=np.fromfile(dat, dtype=np.uint8),
+                        config=np.array([res[0], res[1], spp, 0, 5], np.int32))
+    print(name, film.shape, os.path.getsize(dat))
+
+
 def main():
     if not os.path.exists(HARNESS):
         sys.exit("build the reference harness first: make -C oracle ref")
     os.makedirs(OUT, exist_ok=True)
+    only = sys.argv[2] if len(sys.argv) > 2 and sys.argv[1] == "--only" else None
+    if only:
+        with tempfile.TemporaryDirectory() as tmp:
+            if only == "keys":
+                for cfg in KEY_CONFIGS:
+                    if cfg[5] == 60 and not os.path.exists(HARNESS60):
+                        sys.exit("make -C oracle ref60 first")
+                    keys_fixture(*cfg, tmp)
+            elif only == "dat":
+                dat_fixture("killeroo_dat_40x32s4", (40, 32), 4, tmp)
+        return
     with tempfile.TemporaryDirectory() as tmp:
         paths_fixture("killeroo_paths_64x64s4", (64, 64), 4, 0, 5, 5, tmp)
         paths_fixture("killeroo_paths_48x48s8_seed7_md7", (48, 48), 8, 7, 7, 3, tmp)
@@ -99,6 +162,10 @@ def main():
             rec = raw[1:].reshape(n, 3 + 60 + 60).view(np.float32)
             np.savez_compressed(os.path.join(OUT, "fromrgb_60.npz"), rgb=rec[:, :3].copy(), refl=rec[:, 3:63].copy(),
                                 illum=rec[:, 63:].copy())
+        for cfg in KEY_CONFIGS:
+            if cfg[5] != 60 or os.path.exists(HARNESS60):
+                keys_fixture(*cfg, tmp)
+        dat_fixture("killeroo_dat_40x32s4", (40, 32), 4, tmp)
         fn = os.path.join(tmp, "mt.bin")
         run(["-", "--kat-mt", fn])
         raw = np.fromfile(fn, dtype=np.uint32).reshape(6, 65)
