@@ -1,0 +1,85 @@
+// integration/gpupathrenderer.cpp -- see gpupathrenderer.h.
+#include "stdafx.h"
+#include "gpupathrenderer.h"
+#include "camera.h"
+#include "film.h"
+#include "spectrum.h"
+#include "pbrthost.h"
+#include "pbrtgpu.h"
+#include <vector>
+
+static string gSceneFile;
+
+void GpuPathRenderer::SetSceneFile(const string &file) { gSceneFile = file; }
+const string &GpuPathRenderer::SceneFile() { return gSceneFile; }
+
+GpuPathRenderer::GpuPathRenderer(Camera *c, const ParamSet &params)
+    : camera(c), status(0) {
+    ngpu = params.FindOneInt("gpus", 0);
+    slices = params.FindOneInt("slices", 1);
+    seed = (uint32_t)params.FindOneInt("seed", 0);
+    sceneFile = params.FindOneString("scenefile", gSceneFile);
+    // the spectral film writes <imageOutputName stem>.dat (spectralImage.cpp:348-350)
+    const string &img = camera ? camera->film->imageOutputName : string("pbrt.exr");
+    outFile = img.substr(0, img.find_last_of(".")) + ".dat";
+}
+
+GpuPathRenderer::~GpuPathRenderer() { delete camera; }
+
+void GpuPathRenderer::Render(const Scene *) {
+    status = 0;
+    if (sceneFile.empty()) {
+        Error("gpupath: top-level scene file unknown (GpuPathRenderer::SetSceneFile or \"string scenefile\")");
+        status = PBRTGPU_E_INVALID;
+        return;
+    }
+    int ndev = pbrtgpu_device_count();
+    if (ndev <= 0) {   // no CPU fallback: the core is the GPU path
+        Error("gpupath: no MI355X device (pbrtgpu_device_count() == 0); nothing rendered");
+        status = PBRTGPU_E_NODEVICE;
+        return;
+    }
+    int n = ngpu > 0 ? min(ngpu, ndev) : ndev;
+    pbrthost_overrides ov = { -1, -1, -1, -1, nSpectralSamples, seed };
+    pbrthost_scene *hs = NULL;
+    char err[1024];
+    if ((status = pbrthost_load(sceneFile.c_str(), &ov, &hs, err, sizeof(err))) != 0) {
+        Error("gpupath: %s", err);
+        return;
+    }
+    pbrtgpu_flat_scene fs;
+    pbrthost_flat(hs, &fs);
+    const int W = fs.camera.px_count, H = fs.camera.py_count, N = fs.n_bands;
+    std::vector<pbrtgpu_ctx *> ctx(n, (pbrtgpu_ctx *)NULL);
+    for (int d = 0; d < n && status == 0; ++d)
+        if ((status = pbrtgpu_context_create(d, &ctx[d])) == 0) status = pbrtgpu_scene_upload(ctx[d], &fs);
+    std::vector<float> film((size_t)W * H * N, 0.f);
+    if (status == 0) {
+        // one host thread per GPU, interleaved 16x16 film tiles, host gather (no RCCL)
+        pbrtgpu_render_desc rd = { 0, fs.spp, 16, 16, 0, { 0, 0, 0 } };
+        status = pbrtgpu_render_multi(ctx.data(), n, &rd, NULL, 0, slices, film.data(), (int64_t)film.size(), NULL);
+    }
+    if (status != 0) Error("gpupath: %s", pbrtgpu_last_error());
+    for (int d = 0; d < n; ++d)
+        if (ctx[d]) pbrtgpu_context_destroy(ctx[d]);
+    if (status == 0 && pbrthost_write_dat(outFile.c_str(), film.data(), NULL, W, H, N) != 0) {
+        Error("gpupath: cannot write \"%s\"", outFile.c_str());
+        status = PBRTGPU_E_INVALID;
+    }
+    pbrthost_free(hs);
+}
+
+Spectrum GpuPathRenderer::Li(const Scene *, const RayDifferential &, const Sample *, RNG &, MemoryArena &,
+                             Intersection *, Spectrum *) const {
+    Error("gpupath renders whole frames only (Renderer::Li is not available)");
+    return Spectrum(0.f);
+}
+
+Spectrum GpuPathRenderer::Transmittance(const Scene *, const RayDifferential &, const Sample *, RNG &,
+                                        MemoryArena &) const {
+    return Spectrum(1.f);   // no participating media on this path (EmissionIntegrator: T = 1)
+}
+
+GpuPathRenderer *CreateGpuPathRenderer(Camera *camera, const ParamSet &params) {
+    return new GpuPathRenderer(camera, params);
+}

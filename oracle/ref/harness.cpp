@@ -54,6 +54,9 @@
 #include "cameras/perspective.h"
 #include "filters/box.h"
 #include "film/spectralImageNoCamera.h"
+#ifdef HARNESS_GPUPATH
+#include "gpupathrenderer.h"   // integration/: the reference-side binding of the MI355X core
+#endif
 #include "integrators/path.h"
 #include "integrators/emission.h"
 #include "lights/diffuse.h"
@@ -534,7 +537,7 @@ static void usage() {
     fprintf(stderr, "usage: harness scene.pbrt [--res W H] [--spp N] [--maxdepth D] [--seed S]\n"
                     "   [--window x0 x1 y0 y1] [--raw film.f32] [--dat film.dat] [--paths paths.bin]\n"
                     "   [--path-every K] [--kat-mt out.bin] [--spectra out.bin] [--tris out.bin]\n"
-                    "   [--keys keys.i32 (with --paths)] [--refdat film.dat]\n");
+                    "   [--keys keys.i32 (with --paths)] [--refdat film.dat] [--gpupath]\n");
     exit(1);
 }
 
@@ -544,6 +547,7 @@ int main(int argc, char **argv) {
     int spp = -1, seed = 0, win[4] = { -1, -1, -1, -1 }, pathEvery = 0;
     const char *rawOut = NULL, *datOut = NULL, *pathsOut = NULL, *katMt = NULL, *specOut = NULL, *trisOut = NULL;
     const char *keysIn = NULL, *refDat = NULL;
+    bool gpupath = false;
     for (int i = 2; i < argc; ++i) {
         string a = argv[i];
         if (a == "--res") { ovW = atoi(argv[++i]); ovH = atoi(argv[++i]); }
@@ -560,6 +564,7 @@ int main(int argc, char **argv) {
         else if (a == "--tris") trisOut = argv[++i];
         else if (a == "--keys") keysIn = argv[++i];
         else if (a == "--refdat") refDat = argv[++i];
+        else if (a == "--gpupath") gpupath = true;
         else usage();
     }
     Options opt; opt.quiet = true;
@@ -604,6 +609,21 @@ int main(int argc, char **argv) {
     if (string(scene) == "-") return 0;
     if (!ParseFile(scene)) { fprintf(stderr, "harness: cannot parse %s\n", scene); return 1; }
     if (!gScene) { fprintf(stderr, "harness: no WorldEnd\n"); return 1; }
+#ifdef HARNESS_GPUPATH
+    if (gpupath) {
+        // Renderer "gpupath" as the binding's MakeRenderer branch creates it (INTEGRATION.md
+        // §1): the renderer owns the camera; Render() reports failures through Error()
+        GpuPathRenderer::SetSceneFile(scene);
+        GpuPathRenderer *r = CreateGpuPathRenderer(gCamera, ParamSet());
+        r->Render(gScene);
+        fprintf(stderr, "harness: gpupath status %d\n", r->LastStatus());
+        int st = r->LastStatus();
+        delete r;
+        return st == 0 ? 0 : 3;
+    }
+#else
+    if (gpupath) { fprintf(stderr, "harness: built without the gpupath binding (make -C oracle/ref gpupath)\n"); return 1; }
+#endif
     if (spp <= 0) spp = gSppParam;
     spp = (int)RoundUpPow2(spp);   // LDSampler rounds up (lowdiscrepancy.cpp:33-39)
 

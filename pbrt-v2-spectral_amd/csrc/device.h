@@ -258,6 +258,8 @@ struct DevScene {
     const int *primInst;              // per prim: owning instance or -1
     int nInsts;
     const pbrtgpu_kdnode *kd;         // measured BRDF kd-trees
+    const float4 *kdPack;             // kd nodes packed for the lookup walk (kd_lookup, wavefront.h)
+    int nKd, kdInLds;                 // kd nodes in all trees; 1: k_shade copies them to LDS
     const pbrtgpu_texture *tex;       // texture nodes (one-texel image maps, scale, constants)
     const float *ewa;                 // [128] MIPMap::weightLut
     const float *basis;               // [14][nbp] FromRGB basis spectra, band-quad padded

@@ -953,9 +953,43 @@ int pbrtgpu_scene_upload(pbrtgpu_ctx *c, const pbrtgpu_flat_scene *s) {
         for (auto &k : kd)
             if (!remap(k.spec, &k.spec)) return fail(PBRTGPU_E_INVALID, "kd-tree spectrum offset");
         for (auto &m : mats)
-            if (m.type == PBRTGPU_MAT_MEASURED && (m.aux < 0 || m.aux2 < 0 || m.aux + m.aux2 > (int)kd.size()))
+            if (m.type == PBRTGPU_MAT_MEASURED && (m.aux < 0 || m.aux2 <= 0 || m.aux + m.aux2 > (int)kd.size()))
                 return fail(PBRTGPU_E_INVALID, "measured material kd-tree range");
         HIPCHK(upload(c, kd.data(), kd.size(), &S.kd));
+        // packed nodes with parent links (relative indices; left child = node + 1) for the
+        // stackless lookup walk (kd_lookup, wavefront.h)
+        std::vector<float4> pack(2 * kd.size(), make_float4(0.f, 0.f, 0.f, 0.f));
+        std::vector<int> par(kd.size(), -1);
+        for (auto &m : mats) {
+            if (m.type != PBRTGPU_MAT_MEASURED) continue;
+            for (int i = 0; i < m.aux2; ++i) {
+                const pbrtgpu_kdnode &k = kd[(size_t)m.aux + i];
+                if (k.split_axis < 0 || k.split_axis > 3) return fail(PBRTGPU_E_INVALID, "kd-tree split axis");
+                if (k.split_axis == 3) continue;
+                if (k.has_left) {
+                    if (i + 1 >= m.aux2) return fail(PBRTGPU_E_INVALID, "kd-tree left child out of range");
+                    par[(size_t)m.aux + i + 1] = i;
+                }
+                if (k.right_child < m.aux2) {
+                    if (k.right_child <= i) return fail(PBRTGPU_E_INVALID, "kd-tree right child order");
+                    par[(size_t)m.aux + k.right_child] = i;
+                }
+            }
+            for (int i = 0; i < m.aux2; ++i) {
+                const pbrtgpu_kdnode &k = kd[(size_t)m.aux + i];
+                const int rc = (k.split_axis != 3 && k.right_child < m.aux2) ? k.right_child : -1;
+                const int meta = k.split_axis | (k.has_left && k.split_axis != 3 ? 4 : 0);
+                pack[2 * ((size_t)m.aux + i)] = make_float4(k.p[0], k.p[1], k.p[2], k.split_pos);
+                pack[2 * ((size_t)m.aux + i) + 1] =
+                    make_float4(bits_f((uint32_t)k.spec), bits_f((uint32_t)rc), bits_f((uint32_t)par[(size_t)m.aux + i]),
+                                bits_f((uint32_t)meta));
+            }
+        }
+        HIPCHK(upload(c, pack.data(), pack.size(), &S.kdPack));
+        S.nKd = (int)kd.size();
+        S.kdInLds = (S.nKd > 0 && S.nKd <= kKdLdsNodes) ? 1 : 0;
+        if (const char *e = getenv("PBRTGPU_KD_LDS"))   // tests: force the global-memory walk
+            if (atoi(e) == 0) S.kdInLds = 0;
     }
     c->feat = S.nInf > 0 ? FEAT_INF : 0;
     for (int i = 0; i < s->n_materials; ++i) {

@@ -67,6 +67,7 @@ __global__ __launch_bounds__(kShadeBlock) PGD_SHADE_ATTR void k_shade(DevScene S
     if (threadIdx.x < SEC_N) pgd_secs[threadIdx.x] = 0;
     __syncthreads();
 #endif
+    if (FEAT & FEAT_MEAS) kd_lds_fill(S);   // the measured-BRDF kd-trees, once per block
     const int slot = blockIdx.x * blockDim.x + threadIdx.x;
     const bool inRange = slot < P.cap;
     Pushes pu = {false, false, false};
@@ -106,7 +107,8 @@ __global__ __launch_bounds__(kShadeBlock) PGD_SHADE_ATTR void k_shade(DevScene S
 template <int NB, int FEAT>
 hipError_t launch_shade(int grid, hipStream_t stream, const DevScene &S, const PathSoA &P, const ItemSrc &src, int qout,
                         float *Lout) {
-    hipLaunchKernelGGL((k_shade<NB, FEAT>), dim3(grid), dim3(kShadeBlock), 0, stream, S, P, src, qout, Lout);
+    const size_t lds = ((FEAT & FEAT_MEAS) && S.kdInLds) ? (size_t)S.nKd * 32 : 0;
+    hipLaunchKernelGGL((k_shade<NB, FEAT>), dim3(grid), dim3(kShadeBlock), lds, stream, S, P, src, qout, Lout);
     return hipGetLastError();
 }
 template hipError_t launch_shade<SHADE_NB, SHADE_FEAT>(int, hipStream_t, const DevScene &, const PathSoA &,

@@ -232,71 +232,115 @@ PGD_INLINE bool emit_black(const DevScene &S, const Emit &e) {
 }
 
 // IrregIsotropicBRDF::f (reflection.cpp:251-264): KdTree::Lookup (kdtree.h:160-185) with
-// IrregIsoProc (reflection.cpp:34-47), accumulating the spectrum in the slot's M bands in
-// the reference's visiting order; an iterative walk of the recursive post-order lookup
-template <int NB>
-PGD_INLINE void measured_lookup(const DevScene &S, const FTerm &t, float4 *mb, size_t c) {
+// IrregIsoProc (reflection.cpp:34-47), retried with the radius doubled until more than 2
+// samples are found, in the reference's visiting order (children first, near child before
+// far child, the far child only when the split plane is within reach, then the node).
+//   * The walk is stackless: it climbs back over parent links, so there is no private stack
+//     in scratch memory.
+//   * Nodes are packed as 2 float4 (kd_pack, host-built): {p.xyz, splitPos},
+//     {spec offset, rightChild, parent, axis | hasLeft << 2}; indices relative to the tree.
+//   * When every tree of the scene fits (kKdLdsNodes), each shade block copies them to LDS
+//     once and the walk's dependent node loads are LDS reads (~100 cycles) instead of L2
+//     round trips -- the walk is a chain of ~100-200 dependent loads per lookup, and a wave
+//     waits for its slowest lane (C3: lookups were 2/3 of the frame).
+//   * The spectrum sum stays in registers and is written to the slot's M bands once.
+// Out of line: the walk's registers do not add to the shade kernel's at its 3 call sites.
+static const int kKdLdsNodes = 1536;            // 48 KB of LDS per shade block
+extern __shared__ float4 pgd_kd_lds[];          // dynamic LDS of k_shade (FEAT_MEAS variants)
+typedef float F4N __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) const F4N LdsF4;   // an LDS float4 (ds_read_b128)
+PGD_INLINE float4 kd_node(const float4 *__restrict__ p, int i) { return p[i]; }
+PGD_INLINE float4 kd_node(LdsF4 *p, int i) { const F4N v = p[i]; return make_float4(v.x, v.y, v.z, v.w); }
+
+template <int NB, class NodePtr>
+PGD_INLINE void kd_lookup(NodePtr nodes, const float *__restrict__ spectra, float p0, float p1, float p2,
+                          float4 *__restrict__ mb, size_t c) {
     constexpr int NQ = Bands<NB>::NQ;
-    const pbrtgpu_kdnode *nodes = S.kd + t.R;
-    const int nNodes = t.R2;
-    const float p[3] = {t.s0, t.s1, t.s2};
     float lastMaxDist2 = .001f;
     for (;;) {
+        float4 acc[NQ];
 #pragma unroll
-        for (int q = 0; q < NQ; ++q) mb[q * c] = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int q = 0; q < NQ; ++q) acc[q] = make_float4(0.f, 0.f, 0.f, 0.f);
         float sumWeights = 0.f;
         int nFound = 0;
         const float maxD2 = lastMaxDist2;
-        uint32_t stk[64];   // node << 2 | state
-        int top = 0;
-        if (nNodes > 0) stk[top++] = 0u;
-        while (top > 0) {
-            const uint32_t e = stk[--top];
-            const uint32_t n = e >> 2, state = e & 3u;
-            const pbrtgpu_kdnode nd = nodes[n];
-            const int axis = nd.split_axis;
-            const float pa = axis == 0 ? p[0] : (axis == 1 ? p[1] : p[2]);
-            const bool leftFirst = pa <= nd.split_pos;
-            const float dist2s = (pa - nd.split_pos) * (pa - nd.split_pos);
-            const bool hasRight = nd.right_child < nNodes, hasLeft = nd.has_left != 0;
-            if (state == 0u && axis != 3) {
-                stk[top++] = (n << 2) | 1u;
-                if (leftFirst ? hasLeft : hasRight) stk[top++] = (leftFirst ? n + 1 : (uint32_t)nd.right_child) << 2;
+        int cur = 0, prev = -1;
+        bool down = true;
+        for (;;) {
+            const float4 a = kd_node(nodes, 2 * cur), b = kd_node(nodes, 2 * cur + 1);
+            const int meta = __float_as_int(b.w), axis = meta & 3;
+            int nxt = -1;
+            if (axis != 3) {
+                const float pa = axis == 0 ? p0 : (axis == 1 ? p1 : p2);
+                const bool leftFirst = pa <= a.w;
+                const float dist2s = (pa - a.w) * (pa - a.w);
+                const int L = (meta & 4) ? cur + 1 : -1, R = __float_as_int(b.y);   // -1: no right child
+                const int first = leftFirst ? L : R, second = leftFirst ? R : L;
+                if (down && first >= 0) nxt = first;
+                else if ((down || prev == first) && second >= 0 && dist2s < maxD2) nxt = second;
+            }
+            if (nxt >= 0) {
+                prev = cur;
+                cur = nxt;
+                down = true;
                 continue;
             }
-            if (state == 1u) {
-                stk[top++] = (n << 2) | 2u;
-                if (dist2s < maxD2 && (leftFirst ? hasRight : hasLeft))
-                    stk[top++] = (leftFirst ? (uint32_t)nd.right_child : n + 1) << 2;
-                continue;
-            }
-            // process the node (after its children)
-            V d = vsub(v3(nd.p[0], nd.p[1], nd.p[2]), v3(p[0], p[1], p[2]));
-            float dist2 = vlen2(d);
+            // the node itself, after its children
+            const V d = vsub(v3(a.x, a.y, a.z), v3(p0, p1, p2));
+            const float dist2 = vlen2(d);
             if (dist2 < maxD2) {
-                float weight = (float)pbrt_fm_exp((double)(-100.f * dist2));   // expf
-                const float *sv = S.spectra + nd.spec;
+                const float weight = (float)pbrt_fm_exp((double)(-100.f * dist2));   // expf
+                const float4 *sv = reinterpret_cast<const float4 *>(spectra + __float_as_int(b.x));
 #pragma unroll
                 for (int q = 0; q < NQ; ++q) {
-                    float4 a = mb[q * c], s = ld4(sv + 4 * q);
-                    a.x += weight * s.x; a.y += weight * s.y; a.z += weight * s.z; a.w += weight * s.w;
-                    mb[q * c] = a;
+                    const float4 sq = sv[q];
+                    acc[q].x += weight * sq.x; acc[q].y += weight * sq.y;
+                    acc[q].z += weight * sq.z; acc[q].w += weight * sq.w;
                 }
                 sumWeights += weight;
                 ++nFound;
             }
+            if (cur == 0) break;
+            prev = cur;
+            cur = __float_as_int(b.z);
+            down = false;
         }
         if (nFound > 2 || lastMaxDist2 > 1.5f) {
 #pragma unroll
             for (int q = 0; q < NQ; ++q) {
-                float4 a = mb[q * c];
-                mb[q * c] = make_float4(clampf(a.x, 0.f, INFINITY) / sumWeights, clampf(a.y, 0.f, INFINITY) / sumWeights,
-                                        clampf(a.z, 0.f, INFINITY) / sumWeights, clampf(a.w, 0.f, INFINITY) / sumWeights);
+                const float4 v = acc[q];
+                mb[q * c] = make_float4(clampf(v.x, 0.f, INFINITY) / sumWeights, clampf(v.y, 0.f, INFINITY) / sumWeights,
+                                        clampf(v.z, 0.f, INFINITY) / sumWeights, clampf(v.w, 0.f, INFINITY) / sumWeights);
             }
             return;
         }
         lastMaxDist2 *= 2.f;
     }
+}
+template <int NB>
+__device__ __attribute__((noinline)) void kd_lookup_lds(LdsF4 *nodes, const float *__restrict__ spectra, float p0,
+                                                        float p1, float p2, float4 *__restrict__ mb, size_t c) {
+    kd_lookup<NB>(nodes, spectra, p0, p1, p2, mb, c);
+}
+template <int NB>
+__device__ __attribute__((noinline)) void kd_lookup_global(const float4 *__restrict__ nodes, const float *__restrict__ spectra,
+                                                           float p0, float p1, float p2, float4 *__restrict__ mb, size_t c) {
+    kd_lookup<NB>(nodes, spectra, p0, p1, p2, mb, c);
+}
+template <int NB>
+PGD_INLINE void measured_lookup(const DevScene &S, const FTerm &t, float4 *mb, size_t c) {
+#ifdef PGD_EXP_MEAS_CHEAP   // timing experiment only: the lookup's cost share (wrong radiance)
+    for (int q = 0; q < Bands<NB>::NQ; ++q) mb[q * c] = ld4(S.spectra + S.kd[t.R].spec + 4 * q);
+    return;
+#endif
+    if (S.kdInLds) kd_lookup_lds<NB>((LdsF4 *)pgd_kd_lds + 2 * t.R, S.spectra, t.s0, t.s1, t.s2, mb, c);
+    else kd_lookup_global<NB>(S.kdPack + 2 * t.R, S.spectra, t.s0, t.s1, t.s2, mb, c);
+}
+// k_shade prologue of the FEAT_MEAS variants: the block's copy of the kd-trees in LDS
+PGD_INLINE void kd_lds_fill(const DevScene &S) {
+    if (!S.kdInLds) return;
+    for (int i = threadIdx.x; i < 2 * S.nKd; i += blockDim.x) pgd_kd_lds[i] = S.kdPack[i];
+    __syncthreads();
 }
 // materialise a measured term of F into the slot's M bands (T_MEAS -> T_BUF)
 template <int NB, int FEAT>

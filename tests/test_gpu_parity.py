@@ -206,10 +206,13 @@ def test_motion_blur_instances_match_oracle(pg):
     assert np.array_equal(og, oo)
 
 
-def test_measured_brdf_matches_oracle(pg):
+@pytest.mark.parametrize("kd_lds", ["1", "0"])
+def test_measured_brdf_matches_oracle(pg, monkeypatch, kd_lds):
     """C3: measured (mystique) BRDF through the kd-tree, point light, disk light -- GPU
-    against the oracle path by path and film."""
+    against the oracle path by path and film; kd-tree walk over the LDS copy of the tree
+    (default) and over global memory (PBRTGPU_KD_LDS=0, trees too large for LDS)."""
     from conftest import PACKS
+    monkeypatch.setenv("PBRTGPU_KD_LDS", kd_lds)
     scene = pg.Scene.load(os.path.join(PACKS, "bunny.pack"), xres=48, yres=27, spp=4)
     assert scene.flat.n_kdnodes > 0
     keys = _keys(scene)
