@@ -235,6 +235,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--serial", action="store_true", help="timed frames in serial mode (profiling runs)")
+    ap.add_argument("--dump-film", default=None, help="rank 0 saves the gathered film (.npy) after the timed steps")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -272,7 +273,9 @@ def main():
             _, st = pg.render_multi(devs, tile=tile, slices_per_device=args.slices, out=film)
             return st[:, pg.STAT_PATHS].sum()
     else:
-        dev = pg.Device(local)
+        # one GPU per rank; ranks beyond the visible devices share them (a 1-GPU box running a
+        # 2-rank rehearsal of the multi-GPU path)
+        dev = pg.Device(local % max(1, pg.gpu_lib().pbrtgpu_device_count()))
         dev.upload(scene)
         if world > 1 and args.shard == "tiles":
             tiles = pg.tile_slice(ntx * nty, rank, world)
@@ -307,6 +310,8 @@ def main():
         dist.all_gather(g, torch.tensor([my_elapsed], dtype=torch.float64))
         per_rank = [round(float(x[0]) / args.steps * 1e3, 2) for x in g]
 
+    if args.dump_film and rank == 0:
+        np.save(args.dump_film, np.asarray(film))
     frame_paths = paths / args.steps    # this rank's share of a frame
     roof = None
     if rank == 0 and not args.no_roofline:

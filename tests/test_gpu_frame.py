@@ -115,3 +115,30 @@ def test_serial_mode_same_film(pg, k64, full, monkeypatch):
         assert _same(d.film(), full[0])
         t = d.timing()
         assert t["k_shade"]["ms"] > 0 and t["k_trace_closest"]["ms"] > 0
+
+
+def test_bench_two_ranks_gather_one_frame(pg, tmp_path):
+    """bench.py's multi-process path on real hardware: torch.distributed.run with 2 ranks (on a
+    1-GPU box both ranks share the GPU), each rendering its interleaved tile slice and writing
+    its pixels into the shared host film -- the gathered film is the single-device film bit
+    for bit."""
+    import subprocess
+    import sys
+    from conftest import ROOT
+    out = str(tmp_path / "film.npy")
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr=127.0.0.1",
+           "--master-port=%d" % (29500 + os.getpid() % 1000), os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps",
+           "1", "--warmup", "0", "--no-cpu", "--no-roofline", "--res", "96", "--spp", "8", "--dump-film", out]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
+    import json
+    d = json.loads(line)
+    assert d["n_gpus"] == 2 and d["config"]["shard"] == "tiles" and len(d["per_gpu_ms_per_step"]) == 2
+    scene = pg.Scene.load(os.path.join(PACKS, "killeroo-simple.pack"), xres=96, yres=96, spp=8)
+    with pg.Device(0) as dv:
+        dv.upload(scene)
+        dv.render()
+        ref = dv.film()
+    assert _same(np.load(out), ref)

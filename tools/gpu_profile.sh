@@ -1,15 +1,19 @@
 #!/bin/bash
-# GPU-box recipe: parity tests, smoke, bench, rocprofv3 kernel trace + PMC passes.
-# Usage (from the repo root, on the GPU box): bash tools/gpu_profile.sh TAG
+# GPU-box profiling recipe for one config: rocprofv3 kernel trace + stats of the bench
+# command (default mode and serial mode), then separate PMC passes (FETCH_SIZE, WRITE_SIZE,
+# two SQ groups) over one serial-mode frame (no concurrent kernels: one frame's launches,
+# each counted once).  Usage (repo root, GPU box): bash tools/gpu_profile.sh TAG [config]
 set -e
-TAG=${1:-r01}
+TAG=${1:-r02}
+CFG=${2:-c2}
 OUT=$PWD/gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
-timeout -k 10 300 python3 -m pytest tests -m gpu -x -q > $OUT/pytest_gpu.log 2>&1
-timeout -k 10 120 python3 -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1
-timeout -k 10 300 python3 bench.py > $OUT/bench.json 2> $OUT/bench.err
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu > $OUT/bench_trace.json 2> $OUT/trace.err
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch -o run -- python3 bench.py --steps 1 --warmup 0 --no-cpu > $OUT/bench_pmc1.json 2> $OUT/pmc1.err
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_write -o run -- python3 bench.py --steps 1 --warmup 0 --no-cpu > $OUT/bench_pmc2.json 2> $OUT/pmc2.err
+B="bench.py --config $CFG --no-cpu --no-roofline"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run -- python3 $B --steps 2 --warmup 1 > $OUT/bench_trace.json 2> $OUT/trace.err
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace_serial -o run -- python3 $B --steps 1 --warmup 1 --serial > $OUT/bench_trace_serial.json 2> $OUT/trace_serial.err
+timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch -o run -- python3 $B --steps 1 --warmup 0 --serial > $OUT/pmc1.json 2> $OUT/pmc1.err
+timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_write -o run -- python3 $B --steps 1 --warmup 0 --serial > $OUT/pmc2.json 2> $OUT/pmc2.err
+timeout -s KILL 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES -d $OUT/pmc_sq1 -o run -- python3 $B --steps 1 --warmup 0 --serial > $OUT/pmc3.json 2> $OUT/pmc3.err
+timeout -s KILL 300 rocprofv3 --pmc SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INST_CYCLES_VMEM SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE GRBM_COUNT -d $OUT/pmc_sq2 -o run -- python3 $B --steps 1 --warmup 0 --serial > $OUT/pmc4.json 2> $OUT/pmc4.err
 echo done

@@ -1,12 +1,15 @@
-"""Summarise rocprofv3 rocpd databases (kernel trace and PMC passes) into text/JSON under
-profiles/.  Usage:
-  python tools/rocpd_summary.py TAG gpurun_out/TAG   -> profiles/TAG_kernel_stats.txt,
-                                                         profiles/TAG_pmc.txt,
-                                                         profiles/hbm_traffic.json
+"""Summarise rocprofv3 rocpd databases (kernel traces and PMC passes of tools/gpu_profile.sh)
+into profiles/.  Usage:
+  python tools/rocpd_summary.py TAG gpurun_out/TAG CONFIG
+    -> profiles/TAG_kernel_stats.txt   per-kernel calls / total / avg / min / max (ns -> ms) of
+                                       the default-mode trace and of the serial-mode trace
+       profiles/TAG_pmc.txt            per-kernel PMC sums (FETCH, WRITE, SQ groups)
+       profiles/hbm_traffic.json       configs[CONFIG][timing name]: HBM bytes per launch
 Kernel durations are from the 'kernels' view (ns).  HBM traffic per launch follows
 MI355X_MICROARCH.md "HBM [CDNA4]": FETCH_SIZE and WRITE_SIZE come from separate passes
 (TCC slot limits); FETCH_SIZE is doubled (gfx950 tallies 128-B read requests at 64 B),
-WRITE_SIZE is taken as is.  Both counters are in KiB.
+WRITE_SIZE is taken as is.  Both counters are in KiB.  The PMC passes render one serial-mode
+frame, so each launch is counted once and alone on the device.
 """
 import glob
 import json
@@ -14,9 +17,23 @@ import os
 import sqlite3
 import sys
 
+# timing names of pbrtgpu_last_timing <- device kernel name prefixes (uninstrumented instances)
+NAMES = {"k_trace_closest": ("k_trace_pt<false, false>", "k_trace_closest<false, true>"),
+         "k_trace_shadow": ("k_trace_pt<true, false>", "k_trace_shadow<false, true>"),
+         "k_shade": ("k_shade<",),
+         "k_accum": ("k_accum<",)}
+
 
 def short(name):
-    return name.split("(")[0].replace("void ", "")
+    n = name.split("(")[0].replace("void ", "")
+    return n[5:] if n.startswith("pgd::") else n
+
+
+def timing_name(k):
+    for t, pre in NAMES.items():
+        if any(k.startswith(p) for p in pre):
+            return t
+    return None
 
 
 def kernel_rows(db):
@@ -33,55 +50,77 @@ def pmc_rows(db):
     return out
 
 
+def stats_lines(rows, title):
+    tot = sum(sum(v) for v in rows.values())
+    out = ["# " + title, "%-34s %7s %12s %12s %12s %12s %7s" % ("kernel", "calls", "total_ms", "avg_ms", "min_ms", "max_ms", "pct")]
+    for k, v in sorted(rows.items(), key=lambda kv: -sum(kv[1])):
+        out.append("%-34s %7d %12.3f %12.4f %12.4f %12.4f %7.2f" % (
+            k[:34], len(v), sum(v) / 1e6, sum(v) / len(v) / 1e6, min(v) / 1e6, max(v) / 1e6, 100.0 * sum(v) / tot))
+    return out
+
+
 def main():
-    tag, d = sys.argv[1], sys.argv[2]
+    tag, d, cfg = sys.argv[1], sys.argv[2], sys.argv[3]
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     prof = os.path.join(root, "profiles")
-    os.makedirs(prof, exist_ok=True)
-    tr = glob.glob(os.path.join(d, "trace", "*.db"))
     lines = []
-    if tr:
-        rows = kernel_rows(sqlite3.connect(tr[0]))
-        tot = sum(sum(v) for v in rows.values())
-        lines.append("# rocprofv3 --kernel-trace --stats -- python3 bench.py --steps 2 --warmup 1 --no-cpu  (%s)" % tag)
-        lines.append("%-28s %7s %12s %12s %12s %12s %7s" % ("kernel", "calls", "total_ms", "avg_ms", "min_ms", "max_ms", "pct"))
-        for k, v in sorted(rows.items(), key=lambda kv: -sum(kv[1])):
-            lines.append("%-28s %7d %12.3f %12.3f %12.3f %12.3f %7.2f" % (
-                k, len(v), sum(v) / 1e6, sum(v) / len(v) / 1e6, min(v) / 1e6, max(v) / 1e6, 100.0 * sum(v) / tot))
-        open(os.path.join(prof, "%s_kernel_stats.txt" % tag), "w").write("\n".join(lines) + "\n")
+    for sub, title in (("trace", "rocprofv3 --kernel-trace --stats -- python3 bench.py --config %s --no-cpu --no-roofline "
+                                 "--steps 2 --warmup 1   (default mode: two lanes + shadow stream, spans overlap)"),
+                       ("trace_serial", "rocprofv3 --kernel-trace --stats -- python3 bench.py --config %s --no-cpu "
+                                        "--no-roofline --steps 1 --warmup 1 --serial   (exclusive kernel durations)")):
+        f = glob.glob(os.path.join(d, sub, "**", "*.db"), recursive=True)
+        if f:
+            lines += stats_lines(kernel_rows(sqlite3.connect(f[0])), (title % cfg) + "  [%s]" % tag) + [""]
+    if lines:
+        open(os.path.join(prof, "%s_kernel_stats.txt" % tag), "w").write("\n".join(lines))
         print("\n".join(lines))
     pm = {}
-    for sub in ("pmc_fetch", "pmc_write"):
-        f = glob.glob(os.path.join(d, sub, "*.db"))
-        if f:
-            pm.update(pmc_rows(sqlite3.connect(f[0])))
-    if pm:
-        pl = ["# rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) -- python3 bench.py --steps 1 --warmup 0 --no-cpu  (%s)" % tag,
-              "%-28s %-11s %7s %16s" % ("kernel", "counter", "calls", "avg_KiB/launch")]
-        for (k, c), v in sorted(pm.items()):
-            pl.append("%-28s %-11s %7d %16.1f" % (k, c, len(v), sum(v) / len(v)))
-        open(os.path.join(prof, "%s_pmc.txt" % tag), "w").write("\n".join(pl) + "\n")
-        print("\n".join(pl))
-        out = {"source": "%s: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of bench.py --steps 1 --warmup 0; "
-                          "FETCH_SIZE x2 (gfx950 correction, MI355X_MICROARCH.md) + WRITE_SIZE" % tag}
-        # timing names of pbrtgpu_last_timing <- device kernel names (the uninstrumented
-        # template instances a bench frame runs)
-        names = {"k_trace_closest": ("k_trace_pt<false, false>", "k_trace_closest<false, false>"),
-                 "k_trace_shadow": ("k_trace_pt<true, false>", "k_trace_shadow<false, false>"),
-                 "k_shade": tuple(sorted({kk for kk, _ in pm if kk.split("<")[0].endswith("k_shade")}))}
-        for k, srcs in names.items():
-            fetch = [x for s in srcs for x in pm.get((s, "FETCH_SIZE"), [])]
-            write = [x for s in srcs for x in pm.get((s, "WRITE_SIZE"), [])]
-            if not fetch or not write:
-                continue
-            # one frame was rendered per pass: total over its launches / launches
-            fb = sum(fetch) * 1024.0
-            wb = sum(write) * 1024.0
-            n = len(fetch)
-            out[k] = {"res": 700, "spp": 256, "launches": n, "fetch_bytes_raw_per_launch": fb / n,
-                                    "write_bytes_per_launch": wb / len(write),
-                                    "hbm_bytes_per_launch": (2.0 * fb + wb) / n}
-        json.dump(out, open(os.path.join(prof, "hbm_traffic.json"), "w"), indent=1)
+    for sub in ("pmc_fetch", "pmc_write", "pmc_sq1", "pmc_sq2"):
+        for f in glob.glob(os.path.join(d, sub, "**", "*.db"), recursive=True):
+            for kk, v in pmc_rows(sqlite3.connect(f)).items():
+                pm.setdefault(kk, []).extend(v)
+    if not pm:
+        return
+    pl = ["# rocprofv3 --pmc <group> (separate passes) -- python3 bench.py --config %s --steps 1 --warmup 0 --serial "
+          "--no-cpu --no-roofline  [%s]" % (cfg, tag),
+          "%-34s %-22s %7s %18s %18s" % ("kernel", "counter", "calls", "sum", "avg/launch")]
+    per = {}
+    for (k, c), v in sorted(pm.items()):
+        if k.startswith("__amd"):
+            continue
+        pl.append("%-34s %-22s %7d %18.1f %18.1f" % (k[:34], c, len(v), sum(v), sum(v) / len(v)))
+        t = timing_name(k)
+        if t:
+            e = per.setdefault(t, {})
+            e.setdefault(c, [0.0, 0])
+            e[c][0] += sum(v)
+            e[c][1] += len(v)
+    for t, cs in sorted(per.items()):
+        if "SQ_WAVE_CYCLES" in cs:
+            wc = cs["SQ_WAVE_CYCLES"][0]
+            parts = ["%s %.1f%%" % (c, 100.0 * cs[c][0] / wc) for c in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY")
+                     if c in cs]
+            pl.append("# %s: %s of SQ_WAVE_CYCLES" % (t, ", ".join(parts)))
+        if "SQ_INSTS_VALU" in cs and "SQ_WAVES" in cs:
+            pl.append("# %s: VALU insts / wave %.0f, VMEM_RD / wave %.1f, VMEM_WR / wave %.1f" % (
+                t, cs["SQ_INSTS_VALU"][0] / cs["SQ_WAVES"][0], cs.get("SQ_INSTS_VMEM_RD", [0])[0] / cs["SQ_WAVES"][0],
+                cs.get("SQ_INSTS_VMEM_WR", [0])[0] / cs["SQ_WAVES"][0]))
+    open(os.path.join(prof, "%s_pmc.txt" % tag), "w").write("\n".join(pl) + "\n")
+    print("\n".join(pl))
+    tf = os.path.join(prof, "hbm_traffic.json")
+    tr = json.load(open(tf)) if os.path.exists(tf) else {}
+    if "configs" not in tr:
+        tr = {"configs": {}}
+    ent = {"source": "%s: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (separate) of bench.py --config %s --steps 1 "
+                     "--warmup 0 --serial; FETCH_SIZE x2 (gfx950 correction, MI355X_MICROARCH.md) + WRITE_SIZE" % (tag, cfg)}
+    for t, cs in per.items():
+        if "FETCH_SIZE" in cs and "WRITE_SIZE" in cs:
+            fb, n = cs["FETCH_SIZE"][0] * 1024.0, cs["FETCH_SIZE"][1]
+            wb, nw = cs["WRITE_SIZE"][0] * 1024.0, cs["WRITE_SIZE"][1]
+            ent[t] = {"launches": n, "fetch_bytes_raw_per_launch": fb / n, "write_bytes_per_launch": wb / nw,
+                      "hbm_bytes_per_launch": 2.0 * fb / n + wb / nw}
+    tr["configs"][cfg] = ent
+    json.dump(tr, open(tf, "w"), indent=1)
 
 
 if __name__ == "__main__":
