@@ -888,10 +888,25 @@ PGD_INLINE bool bvh_intersectP(const DevScene &S, Stack &st, const Ray &ray) {
     float ht;
     return bvh_walk<true, INST>(S, st, 0, 0u, r, &hp, &ht);
 }
-struct Isect { DG dg; float rayEps; int prim; int inst; float time; };
-PGD_HEAVY void isect_fill(const DevScene &S, const Ray &ray, int prim, float t, Isect &is);
+// im: the path's instance transforms (PathSoA::instM, per instance 8 float4: world->primitive
+// m rows, then its inverse), or null in scenes without instances
+struct Isect { DG dg; float rayEps; int prim; int inst; float time; const float4 *im; };
+// instance transforms of a path, computed once at path start (every ray of a path carries
+// the camera sample's time, so AnimatedTransform::Interpolate gives the same matrices for all
+// of them): m (and mInv) of instance i from the path's record
+PGD_INLINE void inst_load(const float4 *im, int i, float *m, float *minv) {
+    for (int k = 0; k < 4; ++k) {
+        const float4 a = im[8 * i + k];
+        m[4 * k] = a.x; m[4 * k + 1] = a.y; m[4 * k + 2] = a.z; m[4 * k + 3] = a.w;
+        if (minv) {
+            const float4 b = im[8 * i + 4 + k];
+            minv[4 * k] = b.x; minv[4 * k + 1] = b.y; minv[4 * k + 2] = b.z; minv[4 * k + 3] = b.w;
+        }
+    }
+}
+PGD_HEAVY void isect_fill(const DevScene &S, const Ray &ray, int prim, float t, Isect &is, const float4 *im);
 // geometric normal dg.nn of a recorded closest hit (the field isect_fill would produce)
-PGD_INLINE V isect_nn(const DevScene &S, const Ray &ray, int prim, float t) {
+PGD_INLINE V isect_nn(const DevScene &S, const Ray &ray, int prim, float t, const float4 *im) {
     if (!S.nInsts || S.primInst[prim] < 0) {
         const pbrtgpu_prim pr = S.prims[prim];
         Ray r = ray;
@@ -902,12 +917,12 @@ PGD_INLINE V isect_nn(const DevScene &S, const Ray &ray, int prim, float t) {
         return dg.nn;
     }
     Isect is;
-    isect_fill(S, ray, prim, t, is);
+    isect_fill(S, ray, prim, t, is, im);
     return is.dg.nn;
 }
 // full intersection record for a recorded closest hit; primitives of a transformed instance
 // are intersected in primitive space and moved to world space (primitive.cpp:94-110)
-PGD_HEAVY void isect_fill(const DevScene &S, const Ray &ray, int prim, float t, Isect &is) {
+PGD_HEAVY void isect_fill(const DevScene &S, const Ray &ray, int prim, float t, Isect &is, const float4 *im) {
     const pbrtgpu_prim pr = S.prims[prim];
     Ray r = ray;
     r.maxt = t;
@@ -915,13 +930,14 @@ PGD_HEAVY void isect_fill(const DevScene &S, const Ray &ray, int prim, float t, 
     is.prim = prim;
     is.inst = -1;
     is.time = ray.time;
+    is.im = im;
     const int inst = S.nInsts ? S.primInst[prim] : -1;
     if (inst < 0) {
         shape_intersect(S, pr.shape_type, pr.shape_index, r, &th, &is.rayEps, &is.dg);
         return;
     }
     float m[16], minv[16];
-    inst_interp(S.insts[inst], ray.time, m, minv);
+    inst_load(im, inst, m, minv);
     Ray ro = xray(m, r);
     shape_intersect(S, pr.shape_type, pr.shape_index, ro, &th, &is.rayEps, &is.dg);
     if (m4_is_identity(m)) return;
@@ -1514,7 +1530,7 @@ PGD_HEAVY void get_bsdf(const DevScene &S, const Isect &is, const float diff[4],
         else {
             // ObjectToWorld = Inverse(Identity * w2p): its mInv is Mul(Identity, w2p.m)
             float w[16], id[16], nm[16];
-            inst_interp(S.insts[is.inst], is.time, w, nullptr);
+            inst_load(is.im, is.inst, w, nullptr);
             m4_identity(id);
             m4_mul(id, w, nm);
             tri_shading(S, pr.shape_index, nm, is.dg, dgs);

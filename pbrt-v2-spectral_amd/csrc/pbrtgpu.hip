@@ -70,6 +70,9 @@ static const int kStackLDS = PGD_STACK_LDS;   // k_trace_pt: traversal-stack ent
 #ifndef PGD_TRACE_ATTR   // occupancy experiments (tools/build_exp.sh)
 #define PGD_TRACE_ATTR
 #endif
+#ifndef PGD_TRACE_INST_ATTR   // the two-level kernel: the instance transform's peak would give 148 VGPRs (3 waves)
+#define PGD_TRACE_INST_ATTR __attribute__((amdgpu_waves_per_eu(4, 8)))
+#endif
 
 // closest-hit queries of one pass (BVHAccel::Intersect, bvh.cpp:380-432): persistent grid,
 // one ray per lane per iteration, LDS traversal stack (column per lane)
@@ -286,6 +289,239 @@ __global__ __launch_bounds__(kTraceBlock) PGD_TRACE_ATTR void k_trace_pt(DevScen
     }
 }
 
+// Ray queries of one pass WITH instanced primitives (TransformedPrimitive over nested BVHs,
+// primitive.cpp:87-116, C5): k_trace_pt's persistent ray-replacement scheme with a two-level
+// walk per lane.  Level 0 walks the top-level BVH in world space; a top-level leaf's
+// primitives are tested in order, and an instance among them moves the lane to level 1:
+// the ray is transformed to primitive space at ray.time (AnimatedTransform::Interpolate) and
+// the instance's nested BVH is walked with the stack entries above `ibase`.  When that walk
+// runs out of entries the lane returns to level 0 with the shrunken maxt (closest hit) and
+// resumes the leaf after the instance.  Per ray the nodes visited, the primitives tested and
+// their order are bvh_walk<ANY, true>'s; entry distances are parametric t, the same in both
+// spaces.
+template <bool ANY, bool STATS>
+__global__ __launch_bounds__(kTraceBlock) PGD_TRACE_INST_ATTR void k_trace_inst(DevScene S, PathSoA P, int q, int refill, int ring, uint2 *__restrict__ spill) {
+    __shared__ uint32_t sref[kStackLDS * kTraceBlock];
+    __shared__ float stm[ANY ? 1 : kStackLDS * kTraceBlock];
+    uint2 *gsp = spill + (size_t)(blockIdx.x * blockDim.x + threadIdx.x) * S.stackDepth;
+    int bottom = 0;   // entries [0, bottom) live in gsp
+    Stack st;         // work counters only
+    const uint32_t n = ANY ? P.cnt[CNT_QS(q)] : P.cnt[CNT_QC(q)];
+    const uint32_t *Q = ANY ? P.qS + (size_t)q * P.cap : P.qC + (size_t)q * 2 * P.cap;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = (gridDim.x * blockDim.x) >> 6;
+    uint32_t next = (uint32_t)((uint64_t)n * wave / nw);
+    const uint32_t end = (uint32_t)((uint64_t)n * (wave + 1) / nw);
+    bool active = false;
+    int slot = 0, kind = 0, todo = 0, prim = -1;
+    uint32_t ref = 0;
+    float thit = INFINITY;
+    // the ray of the current level: the world ray at level 0, the instance-space ray at level
+    // 1 (the world ray is reloaded from the slot's ray record when the instance is done; only
+    // its maxt, wmaxt, is kept)
+    Ray ray;
+    V invDir = v3(0.f, 0.f, 0.f);
+    uint32_t negMask = 0;
+    float wmaxt = 0.f;
+    int level = 0, ibase = 0;                     // level 1: inside an instance, its entries from ibase
+    uint32_t leafOff = 0, leafN = 0, leafI = 0;   // top-level leaf under test (resumed after an instance)
+    bool inLeaf = false;
+    uint32_t nM = 0, hM = 0;
+    const uint32_t NONE = 0xffffffffu;
+    auto setRay = [&](const Ray &r) {
+        ray = r;
+        invDir = v3(1.f / r.d.x, 1.f / r.d.y, 1.f / r.d.z);
+        negMask = (uint32_t)(invDir.x < 0) | ((uint32_t)(invDir.y < 0) << 1) | ((uint32_t)(invDir.z < 0) << 2);
+    };
+    for (;;) {
+        const unsigned long long idle = __ballot(!active);
+        const uint32_t nIdle = (uint32_t)__popcll(idle);
+        if (next < end && (nIdle >= (uint32_t)refill || nIdle == 64u)) {
+            if (!active) {
+                const uint32_t i = next + (uint32_t)__popcll(idle & ((1ull << lane) - 1ull));
+                if (i < end) {
+                    const uint32_t e = Q[i];
+                    slot = ANY ? (int)e : (int)(e >> 1);
+                    kind = ANY ? RAY_S : (int)(e & 1);
+                    setRay(ray_load(P, kind, slot));
+                    prim = -1;
+                    thit = INFINITY;
+                    todo = 0;
+                    bottom = 0;
+                    level = 0;
+                    inLeaf = false;
+                    if (ANY) st.cShadow++; else st.cRays++;
+                    st.cNodes++;
+                    const int neg[3] = {(int)(negMask & 1u), (int)((negMask >> 1) & 1u), (int)(negMask >> 2)};
+                    if (bbox_hit(S.nodes[0], S.nodes[1], ray, invDir, neg)) {
+                        ref = S.nodeRef[0];
+                        active = true;
+                    } else if (ANY) P.occ[slot] = 0u;
+                    else {
+                        P.hitPrim[(size_t)kind * P.cap + slot] = -1;
+                        P.hitT[(size_t)kind * P.cap + slot] = INFINITY;
+                        if (STATS && kind == RAY_M) nM++;
+                    }
+                }
+            }
+            next = min(end, next + nIdle);
+        }
+        if (!__ballot(active)) {
+            if (next >= end) break;
+            continue;
+        }
+        if (active) {
+            bool occluded = false, done = false;
+            const int neg[3] = {(int)(negMask & 1u), (int)((negMask >> 1) & 1u), (int)(negMask >> 2)};
+            if (level == 1 || !inLeaf) {
+                if (ref != NONE && !(ref & WREF_LEAF)) {
+                    const float4 *w = S.wnodes + 4 * (size_t)ref;
+                    const float4 l0 = w[0], l1 = w[1], r0 = w[2], r1 = w[3];
+                    st.cNodes++;
+                    float tl = 0.f, tr = 0.f;
+                    const bool hl = slab_enter(l0, l1, ray, invDir, neg, &tl) && tl < ray.maxt;
+                    const bool hr = slab_enter(r0, r1, ray, invDir, neg, &tr) && tr < ray.maxt;
+                    const uint32_t refL = __float_as_uint(l0.w), refR = __float_as_uint(l1.w);
+                    const bool swap = ((negMask >> __float_as_uint(r0.w)) & 1u) != 0;
+                    const bool hn = swap ? hr : hl, hf = swap ? hl : hr;
+                    const uint32_t rn = swap ? refR : refL, rf = swap ? refL : refR;
+                    if (hn) {
+                        if (hf) {
+                            if (todo - bottom == ring) {   // ring full: oldest entry to HBM
+                                const int j = (bottom & (ring - 1)) * kTraceBlock + threadIdx.x;
+                                gsp[bottom] = make_uint2(sref[j], ANY ? 0u : __float_as_uint(stm[j]));
+                                ++bottom;
+                            }
+                            const int j = (todo & (ring - 1)) * kTraceBlock + threadIdx.x;
+                            sref[j] = rf;
+                            if (!ANY) stm[j] = swap ? tl : tr;
+                            ++todo;
+                        }
+                        ref = rn;
+                    } else if (hf) ref = rf;
+                    else ref = NONE;
+                }
+                if (ref != NONE && (ref & WREF_LEAF)) {
+                    const uint32_t np = (ref >> WREF_NP_SHIFT) & WREF_NP_MASK, off = ref & WREF_OFF_MASK;
+                    if (level == 1) {   // nested BVH leaf: triangles / quadrics only
+                        for (uint32_t i = 0; i < np; ++i)
+                            if (prim_test<ANY, false>(S, st, todo, (int)(off + i), ray, &prim, &thit) && ANY) {
+                                occluded = true;
+                                break;
+                            }
+                        ref = NONE;
+                    } else {
+                        leafOff = off;
+                        leafN = np;
+                        leafI = 0;
+                        inLeaf = true;
+                    }
+                }
+            }
+            if (level == 0 && inLeaf) {
+                // the top-level leaf's primitives from leafI; an instance suspends the leaf
+                bool entered = false;
+                while (leafI < leafN && !occluded) {
+                    const int pi = (int)(leafOff + leafI);
+                    ++leafI;
+                    const pbrtgpu_prim pr = S.prims[pi];
+                    if (pr.shape_type != PBRTGPU_SHAPE_INSTANCE) {
+                        if (prim_test<ANY, false>(S, st, todo, pi, ray, &prim, &thit) && ANY) occluded = true;
+                        continue;
+                    }
+                    const pbrtgpu_instance &I = S.insts[pr.shape_index];
+                    float m[16];
+                    inst_load(inst_rec(P, slot), pr.shape_index, m, nullptr);   // the path's transform
+                    Ray ir = xray(m, ray);
+                    if (I.single_prim >= 0) {
+                        if (prim_test<ANY, false>(S, st, todo, I.single_prim, ir, &prim, &thit)) {
+                            if (ANY) occluded = true;
+                            else ray.maxt = ir.maxt;
+                        }
+                        continue;
+                    }
+                    // nested BVH (bvh_walk<ANY, false>): its root box, then its walk
+                    wmaxt = ray.maxt;
+                    setRay(ir);
+                    st.cNodes++;
+                    const uint32_t root = (uint32_t)I.root;
+                    const int negI[3] = {(int)(negMask & 1u), (int)((negMask >> 1) & 1u), (int)(negMask >> 2)};
+                    if (!bbox_hit(S.nodes[2 * root], S.nodes[2 * root + 1], ray, invDir, negI)) {
+                        Ray wr = ray_load(P, kind, slot);   // back to the world ray
+                        wr.maxt = wmaxt;
+                        setRay(wr);
+                        continue;
+                    }
+                    level = 1;
+                    ibase = todo;
+                    ref = S.nodeRef[root];
+                    entered = true;
+                    break;
+                }
+                if (!entered && !occluded) {
+                    inLeaf = false;
+                    ref = NONE;
+                }
+            }
+            done = occluded;
+            if (!done && ref == NONE && !(level == 0 && inLeaf)) {
+                // pop the next entry of this level whose box is still entered before maxt
+                for (;;) {
+                    if (todo == (level ? ibase : 0)) {
+                        if (level == 0) { done = true; break; }
+                        // instance walked: back to the world ray (maxt shrunk by its hits),
+                        // resume the suspended leaf
+                        Ray wr = ray_load(P, kind, slot);
+                        wr.maxt = ANY ? wmaxt : ray.maxt;
+                        setRay(wr);
+                        level = 0;
+                        break;
+                    }
+                    --todo;
+                    uint32_t r;
+                    float tm;
+                    if (todo < bottom) {
+                        const uint2 g = gsp[todo];
+                        r = g.x; tm = __uint_as_float(g.y);
+                        bottom = todo;
+                    } else {
+                        const int j = (todo & (ring - 1)) * kTraceBlock + threadIdx.x;
+                        r = sref[j]; tm = ANY ? 0.f : stm[j];
+                    }
+                    if (ANY || tm < ray.maxt) { ref = r; break; }
+                }
+            }
+            if (done) {
+                active = false;
+                if (ANY) P.occ[slot] = occluded ? 1u : 0u;
+                else {
+                    P.hitPrim[(size_t)kind * P.cap + slot] = prim;
+                    P.hitT[(size_t)kind * P.cap + slot] = prim >= 0 ? thit : INFINITY;
+                    st.cHits += prim >= 0 ? 1u : 0u;
+                    if (STATS && kind == RAY_M) { nM++; hM += prim >= 0 ? 1u : 0u; }
+                }
+            }
+        }
+    }
+    if (STATS) {
+        unsigned long long *w = reinterpret_cast<unsigned long long *>(P.cnt + CNT_WORK);
+        if (ANY) {
+            atomicAdd(&w[W_SHADOW], (unsigned long long)st.cShadow);
+            atomicAdd(&w[W_NODES_S], (unsigned long long)st.cNodes);
+            atomicAdd(&w[W_TRIS_S], (unsigned long long)st.cTris);
+            atomicAdd(&w[W_QUADS_S], (unsigned long long)st.cQuads);
+        } else {
+            atomicAdd(&w[W_RAYS], (unsigned long long)st.cRays);
+            atomicAdd(&w[W_NODES_C], (unsigned long long)st.cNodes);
+            atomicAdd(&w[W_TRIS_C], (unsigned long long)st.cTris);
+            atomicAdd(&w[W_QUADS_C], (unsigned long long)st.cQuads);
+            atomicAdd(&w[W_HITS], (unsigned long long)st.cHits);
+            atomicAdd(&w[W_RAYS_M], (unsigned long long)nM);
+            atomicAdd(&w[W_HITS_M], (unsigned long long)hM);
+        }
+    }
+}
+
 // film[filmIdx[p]][b] += L(p, s) for s in batch order (spectralImage.cpp:125-131)
 template <int NB>
 __global__ void k_accum(const float *__restrict__ Lbuf, const int *__restrict__ filmIdx, int nPix, int sb,
@@ -400,7 +636,7 @@ struct Timing {
 struct Lane {
     DevBuf slots;            // PathSoA storage
     DevBuf spill;            // k_trace_pt stack spill areas (closest, shadow)
-    int slotCap = 0, slotNb = 0;
+    int slotCap = 0, slotNb = 0, slotInst = 0;
     PathSoA P{};
     hipStream_t s = nullptr, s2 = nullptr;
     hipEvent_t ev[2 + 6 * 8] = {};
@@ -426,6 +662,7 @@ struct pbrtgpu_ctx {
     int numCUs = 256;
     int ptBlocksPerCU = 0;    // occupancy of k_trace_pt closest (computed on first use)
     int ptBlocksPerCUS = 0;   // occupancy of k_trace_pt shadow
+    int instBlocksPerCU = 0, instBlocksPerCUS = 0;   // occupancy of k_trace_inst closest / shadow
     int ring = kStackLDS;     // LDS ring entries in use (PBRTGPU_STACK_LDS: tests force HBM spills)
     int refill = 16;          // idle lanes that trigger ray replacement in k_trace_pt (PBRTGPU_REFILL)
     Timing last;
@@ -457,13 +694,17 @@ static size_t lbuf_budget() {
 }
 // PBRTGPU_SERIAL=1: one lane, shadow queries on the lane's main stream -- no two kernels of
 // a render overlap, so each kernel's event spans are its exclusive device time (roofline)
+static bool legacy_inst_walk() {
+    const char *e = getenv("PBRTGPU_INST_WALK");
+    return e && !strcmp(e, "legacy");
+}
 static bool serial_mode() {
     const char *e = getenv("PBRTGPU_SERIAL");
     return e && atoi(e) != 0;
 }
 
-static int ensure_slots(Lane *c, int cap, int NB) {
-    if (c->slotCap == cap && c->slotNb == NB) return 0;
+static int ensure_slots(Lane *c, int cap, int NB, int nInst) {
+    if (c->slotCap == cap && c->slotNb == NB && c->slotInst == nInst) return 0;
     const size_t C = (size_t)cap;
     const int NBP = (NB + 3) / 4 * 4;   // bands padded to whole float4 quads
     size_t off = 0;
@@ -471,7 +712,7 @@ static int ensure_slots(Lane *c, int cap, int NB) {
     size_t oItem = take(C * 4), oHp = take(C * 4), oSmp = take(C * 4), oBounce = take(C * 4), oFlags = take(C * 4),
            oMt = take(C * 20), oBeta = take(C * 3 * NBP * 4), oL = take(C * NBP * 4), oA = take(C * 2 * NBP * 4),
            oB = take(C * 2 * NBP * 4), oM = take(C * NBP * 4), oK = take(C * NBP * 4), oPix = take(C * 4), oRay = take(C * 27 * 4), oHitP = take(C * 8), oHitT = take(C * 8), oOcc = take(C * 4),
-           oQC = take(C * 16), oQS = take(C * 8), oCnt = take(CNT_WORDS * 4);
+           oQC = take(C * 16), oQS = take(C * 8), oCnt = take(CNT_WORDS * 4), oInst = take(C * (size_t)nInst * 128);
     HIPCHK(c->slots.ensure(off));
     char *base = (char *)c->slots.p;
     PathSoA &P = c->P;
@@ -483,8 +724,11 @@ static int ensure_slots(Lane *c, int cap, int NB) {
     P.ray = (float *)(base + oRay); P.hitPrim = (int *)(base + oHitP); P.hitT = (float *)(base + oHitT);
     P.occ = (uint32_t *)(base + oOcc); P.qC = (uint32_t *)(base + oQC); P.qS = (uint32_t *)(base + oQS);
     P.cnt = (uint32_t *)(base + oCnt);
+    P.nInst = nInst;
+    P.instM = nInst ? (float4 *)(base + oInst) : nullptr;
     c->slotCap = cap;
     c->slotNb = NB;
+    c->slotInst = nInst;
     return 0;
 }
 
@@ -506,13 +750,21 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
     const int traceGrid = c->numCUs * perCU;
     const bool inst = c->S.nInsts > 0;
     if (!c->ptBlocksPerCU) {   // resident blocks of the persistent kernels (registers, LDS)
-        int b0 = 0, b1 = 0;
+        int b0 = 0, b1 = 0, b2 = 0, b3 = 0;
         HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&b0, k_trace_pt<false, false>, kTraceBlock, 0));
         HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&b1, k_trace_pt<true, false>, kTraceBlock, 0));
+        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&b2, k_trace_inst<false, false>, kTraceBlock, 0));
+        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&b3, k_trace_inst<true, false>, kTraceBlock, 0));
         c->ptBlocksPerCU = std::max(1, b0);
         c->ptBlocksPerCUS = std::max(1, b1);
+        c->instBlocksPerCU = std::max(1, b2);
+        c->instBlocksPerCUS = std::max(1, b3);
     }
-    const uint32_t ptGrid = (uint32_t)(c->numCUs * c->ptBlocksPerCU), ptGridS = (uint32_t)(c->numCUs * c->ptBlocksPerCUS);
+    // instanced scenes: the two-level persistent kernels (PBRTGPU_INST_WALK=legacy: the
+    // one-ray-per-thread bvh_walk kernels, kept for A/B parity tests)
+    const bool instPT = inst && !legacy_inst_walk();
+    const uint32_t ptGrid = (uint32_t)(c->numCUs * (instPT ? c->instBlocksPerCU : c->ptBlocksPerCU));
+    const uint32_t ptGridS = (uint32_t)(c->numCUs * (instPT ? c->instBlocksPerCUS : c->ptBlocksPerCUS));
     const size_t spillLane = (size_t)std::max(ptGrid, ptGridS) * kTraceBlock * c->stackDepth;   // uint2 per kernel
     // scenes without measured BRDFs, textures and environment lights run the variant with
     // that code compiled out (fewer registers, no kd-tree stack)
@@ -541,7 +793,7 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
         // overshoot of one enqueued batch, means the wavefront is stuck
         r.passes = 0;
         r.maxPasses = 2 * (int)((r.src.nItems + r.cap - 1) / r.cap + 1) * (c->S.maxDepth + 3) + 2 * kPassBatch;
-        if (int e = ensure_slots(&L, r.cap, NB)) return e;
+        if (int e = ensure_slots(&L, r.cap, NB, c->S.nInsts)) return e;
         HIPCHK(L.spill.ensure(2 * spillLane * sizeof(uint2)));
         if (l > 0) HIPCHK(hipStreamWaitEvent(L.s, c->ev[0], 0));
         HIPCHK(hipMemsetAsync(L.P.item, 0xff, (size_t)r.cap * 4, L.s));
@@ -594,7 +846,10 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
                 HIPCHK(hipMemsetAsync(P.cnt + CNT_QS(nq), 0, 4, L.s));
                 HIPCHK(hipEventRecord(e[0], L.s));
                 if (serial) {   // closest-hit queries first, alone on the device
-                    if (inst) {
+                    if (instPT) {
+                        if (countWork) hipLaunchKernelGGL((k_trace_inst<false, true>), dim3(ptGrid), dim3(kTraceBlock), 0, L.s, c->S, P, q, c->refill, c->ring, spillC);
+                        else hipLaunchKernelGGL((k_trace_inst<false, false>), dim3(ptGrid), dim3(kTraceBlock), 0, L.s, c->S, P, q, c->refill, c->ring, spillC);
+                    } else if (inst) {
                         if (countWork) hipLaunchKernelGGL((k_trace_closest<true, true>), dim3(traceGrid), dim3(kTraceBlock), lds, L.s, c->S, P, q);
                         else hipLaunchKernelGGL((k_trace_closest<false, true>), dim3(traceGrid), dim3(kTraceBlock), lds, L.s, c->S, P, q);
                     } else if (countWork) hipLaunchKernelGGL((k_trace_pt<false, true>), dim3(ptGrid), dim3(kTraceBlock), 0, L.s, c->S, P, q, c->refill, c->ring, spillC);
@@ -602,7 +857,10 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
                     HIPCHK(hipGetLastError());
                     HIPCHK(hipEventRecord(e[1], L.s));
                     HIPCHK(hipEventRecord(e[2], L.s));
-                    if (inst) {
+                    if (instPT) {
+                        if (countWork) hipLaunchKernelGGL((k_trace_inst<true, true>), dim3(ptGridS), dim3(kTraceBlock), 0, L.s, c->S, P, q, c->refill, c->ring, spillS);
+                        else hipLaunchKernelGGL((k_trace_inst<true, false>), dim3(ptGridS), dim3(kTraceBlock), 0, L.s, c->S, P, q, c->refill, c->ring, spillS);
+                    } else if (inst) {
                         if (countWork) hipLaunchKernelGGL((k_trace_shadow<true, true>), dim3(traceGrid), dim3(kTraceBlock), ldsS, L.s, c->S, P, q);
                         else hipLaunchKernelGGL((k_trace_shadow<false, true>), dim3(traceGrid), dim3(kTraceBlock), ldsS, L.s, c->S, P, q);
                     } else if (countWork) hipLaunchKernelGGL((k_trace_pt<true, true>), dim3(ptGridS), dim3(kTraceBlock), 0, L.s, c->S, P, q, c->refill, c->ring, spillS);
@@ -623,9 +881,15 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
                 // shadow queries of queue set q on s2, after the counter resets
                 HIPCHK(hipStreamWaitEvent(s2, e[0], 0));
                 HIPCHK(hipEventRecord(e[2], s2));
-                // instanced scenes walk nested BVHs (bvh_walk); the others run the persistent
-                // ray-replacement kernels over the whole (wave-partitioned) queue
-                if (inst) {
+                // persistent ray-replacement kernels over the whole (wave-partitioned) queue;
+                // instanced scenes run the two-level variant (or, legacy, bvh_walk per thread)
+                if (instPT) {
+                    if (countWork) hipLaunchKernelGGL((k_trace_inst<false, true>), dim3(ptGrid), dim3(kTraceBlock), 0, L.s, c->S, P, q, c->refill, c->ring, spillC);
+                    else hipLaunchKernelGGL((k_trace_inst<false, false>), dim3(ptGrid), dim3(kTraceBlock), 0, L.s, c->S, P, q, c->refill, c->ring, spillC);
+                    HIPCHK(hipGetLastError());
+                    if (countWork) hipLaunchKernelGGL((k_trace_inst<true, true>), dim3(ptGridS), dim3(kTraceBlock), 0, s2, c->S, P, q, c->refill, c->ring, spillS);
+                    else hipLaunchKernelGGL((k_trace_inst<true, false>), dim3(ptGridS), dim3(kTraceBlock), 0, s2, c->S, P, q, c->refill, c->ring, spillS);
+                } else if (inst) {
                     if (countWork) hipLaunchKernelGGL((k_trace_closest<true, true>), dim3(traceGrid), dim3(kTraceBlock), lds, L.s, c->S, P, q);
                     else hipLaunchKernelGGL((k_trace_closest<false, true>), dim3(traceGrid), dim3(kTraceBlock), lds, L.s, c->S, P, q);
                     HIPCHK(hipGetLastError());

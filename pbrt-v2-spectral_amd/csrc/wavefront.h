@@ -83,7 +83,13 @@ struct PathSoA {
     uint32_t *qC;       // [2][2*cap]: (slot << 1) | kind
     uint32_t *qS;       // [2][cap]
     uint32_t *cnt;      // counters (CNT_*), work counters as u64 from word CNT_WORK
+    float4 *instM;      // [cap][nInst][8]: the path's instance transforms (inst_load), or null
+    int nInst;
 };
+// the path's instance-transform record (null without instances)
+PGD_INLINE const float4 *inst_rec(const PathSoA &P, int slot) {
+    return P.nInst ? P.instM + (size_t)slot * P.nInst * 8 : nullptr;
+}
 
 // where the camera samples of a pass come from
 struct ItemSrc {
@@ -396,6 +402,17 @@ PGD_INLINE void path_start(const DevScene &S, const PathSoA &P, const ItemSrc &s
     float timeU = s1d(hp, 2, s, spp);
     Ray r = camera_ray(S.cam, imageX, imageY, lens[0], lens[1], timeU);
     ray_store(P, RAY_C, slot, r);
+    // AnimatedTransform::Interpolate (transform.cpp:356-381) of every instance at the path's
+    // time, once per path: all of the path's rays carry this time
+    for (int i = 0; i < P.nInst; ++i) {
+        float m[16], minv[16];
+        inst_interp(S.insts[i], r.time, m, minv);
+        float4 *o = P.instM + ((size_t)slot * P.nInst + i) * 8;
+        for (int k = 0; k < 4; ++k) {
+            o[k] = make_float4(m[4 * k], m[4 * k + 1], m[4 * k + 2], m[4 * k + 3]);
+            o[4 + k] = make_float4(minv[4 * k], minv[4 * k + 1], minv[4 * k + 2], minv[4 * k + 3]);
+        }
+    }
     P.item[slot] = (int)item;
     P.hp[slot] = hp;
     P.pix[slot] = ((uint32_t)py << 16) | (uint32_t)px;
@@ -467,7 +484,7 @@ PGD_INLINE Pushes shade_vertex(const DevScene &S, const PathSoA &P, int slot, in
     float4 *mb = P.M + slot;
     Isect is;
     PGD_T0(ISECT);
-    isect_fill(S, ray, prim, thit, is);
+    isect_fill(S, ray, prim, thit, is, inst_rec(P, slot));
     PGD_T1(ISECT);
     la->emit = false;
     la->zero = false;
@@ -730,7 +747,7 @@ PGD_INLINE Pushes shade_slot(const DevScene &S, const PathSoA &P, int slot, floa
             if ((FEAT & FEAT_INF) && S.lights[ln].type == PBRTGPU_LIGHT_INFINITE) useB = mp < 0;   // Li = light->Le(ray)
             else if (mp >= 0 && S.prims[mp].area_light == ln) {
                 Ray mr = ray_load(P, RAY_M, slot);
-                useB = vdot(isect_nn(S, mr, mp, P.hitT[c + slot]), vneg(mr.d)) > 0.f;   // DiffuseAreaLight::L
+                useB = vdot(isect_nn(S, mr, mp, P.hitT[c + slot], inst_rec(P, slot)), vneg(mr.d)) > 0.f;   // DiffuseAreaLight::L
             }
         }
         fl &= ~(PF_PEND | PF_PA | PF_PB);

@@ -142,3 +142,26 @@ def test_bench_two_ranks_gather_one_frame(pg, tmp_path):
         dv.render()
         ref = dv.film()
     assert _same(np.load(out), ref)
+
+
+def test_instanced_walks_agree_with_work_counters(pg, monkeypatch):
+    """k_trace_inst (two-level persistent walk) against the bvh_walk kernels on C5's scene:
+    identical per-path radiance, and identical traversal work (rays, nodes visited, primitive
+    tests, hits) -- the same nodes and primitives per ray, in the reference's order."""
+    scene = pg.Scene.load(os.path.join(PACKS, "anim-killeroos-moving.pack"), xres=64, yres=48, spp=8)
+    c = scene.flat.camera
+    keys = np.array([(x, y, s) for y in range(c.sy_start, c.sy_end, 3) for x in range(c.sx_start, c.sx_end, 2)
+                     for s in range(scene.spp)], np.int32)
+    out = {}
+    for walk in ("persistent", "legacy"):
+        monkeypatch.setenv("PBRTGPU_INST_WALK", walk)
+        with pg.Device(0) as d:
+            d.upload(scene)
+            L = d.trace_paths(keys)
+            d.render(count_work=True)
+            out[walk] = (L, d.timing()["work"], d.film())
+    assert _same(out["persistent"][0], out["legacy"][0])
+    assert _same(out["persistent"][2], out["legacy"][2])
+    for k in ("rays", "shadow_rays", "nodes_closest", "nodes_shadow", "tris_closest", "tris_shadow", "quads_closest",
+              "quads_shadow", "hits"):
+        assert out["persistent"][1][k] == out["legacy"][1][k], k

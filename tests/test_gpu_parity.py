@@ -177,10 +177,14 @@ def test_sample_range_split_and_bad_arguments(pg, killeroo64, dev):
         dev.trace_paths(np.array([[10 ** 5, 0, 0]], np.int32))
 
 
-def test_motion_blur_instances_match_oracle(pg):
+@pytest.mark.parametrize("walk", ["persistent", "legacy"])
+def test_motion_blur_instances_match_oracle(pg, monkeypatch, walk):
     """C5: animated TransformedPrimitives over nested BVHs -- GPU against the oracle, path
-    by path and film, bit for bit (same transcendental definition)."""
+    by path and film, bit for bit (same transcendental definition); the two-level persistent
+    traversal kernel (k_trace_inst, default) and the one-ray-per-thread bvh_walk kernels
+    (PBRTGPU_INST_WALK=legacy)."""
     from conftest import PACKS
+    monkeypatch.setenv("PBRTGPU_INST_WALK", walk)
     scene = pg.Scene.load(os.path.join(PACKS, "anim-killeroos-moving.pack"), xres=40, yres=40, spp=4)
     assert scene.flat.n_instances == 2
     keys = _keys(scene)
