@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define PBRTGPU_ABI_VERSION 5
+#define PBRTGPU_ABI_VERSION 6
 #define PBRTGPU_MAX_BANDS 64
 
 #define PBRTGPU_E_INVALID   (-1)
@@ -86,7 +86,11 @@ enum {
     PBRTGPU_MAT_SUBSTRATE = 3,  /* spec[0]=Kd, spec[1]=Ks; f[0]=uroughness, f[1]=vroughness */
     PBRTGPU_MAT_MIRROR = 4,     /* spec[0]=Kr */
     PBRTGPU_MAT_GLASS = 5,      /* spec[0]=Kr, spec[1]=Kt; f[0]=index */
-    PBRTGPU_MAT_MEASURED = 6    /* IrregIsotropicBRDF: aux = first kd-tree node, aux2 = node count */
+    PBRTGPU_MAT_MEASURED = 6,   /* IrregIsotropicBRDF: aux = first kd-tree node, aux2 = node count */
+    PBRTGPU_MAT_MEASURED_HALFANGLE = 7   /* RegularHalfangleBRDF (.merl): aux = first texel of its
+                                          * 90 x 90 x 180 RGB table in merl[] (3 floats per texel),
+                                          * -1 when the file could not be read (no BxDF, as the
+                                          * reference's MeasuredMaterial then adds none) */
 };
 
 /* Texture<float> / Texture<Spectrum> (texture.h, textures/{constant,scale,imagemap}.cpp).
@@ -224,6 +228,10 @@ typedef struct pbrtgpu_flat_scene {
     const float *ewa_lut;         /* [128] MIPMap::weightLut (mipmap.h:185-193) */
     const float *rgb_basis;       /* [14][n_bands] rgbRefl2Spect{White,Cyan,Magenta,Yellow,Red,
                                    * Green,Blue}, rgbIllum2Spect{...} (FromRGB, spectrum.cpp:93-178) */
+    int32_t n_merl_floats;        /* RegularHalfangleBRDF tables: per texel RGB after the loader's
+                                   * scale and clamp (measured.cpp:133-175), texel index
+                                   * phiD + 180 * (thetaD + 90 * thetaH) */
+    const float *merl;
 } pbrtgpu_flat_scene;
 
 /* ---- render description ----------------------------------------------------------- */

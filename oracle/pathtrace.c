@@ -713,7 +713,8 @@ static void isect_fill(const Ctx *c, const Ray *ray, const Hit *h, Isect *is) {
 enum { BSDF_REFLECTION = 1, BSDF_TRANSMISSION = 2, BSDF_DIFFUSE = 4, BSDF_GLOSSY = 8, BSDF_SPECULAR = 16,
        BSDF_ALL = 31 };
 enum { BX_LAMBERT, BX_OREN, BX_MICRO_BLINN_DIEL, BX_SPEC_REFL_NOOP, BX_FRESNEL_BLEND_ANISO, BX_MEASURED_IRREG,
-       BX_MICRO_BLINN_COND, BX_SPEC_REFL_DIEL, BX_SPEC_TRANS };   /* eta_t = index of refraction for the last two */
+       BX_MICRO_BLINN_COND, BX_SPEC_REFL_DIEL, BX_SPEC_TRANS,    /* eta_t = index of refraction for these two */
+       BX_MEASURED_HALF };                                        /* RegularHalfangleBRDF: merl = its table */
 typedef struct {
     int kind, type;
     const float *R;      /* reflectance spectrum */
@@ -723,6 +724,7 @@ typedef struct {
     const float *eta, *k;   /* FresnelConductor */
     const pbrtgpu_kdnode *kd;   /* IrregIsotropicBRDF: kd-tree nodes */
     int nkd;
+    const float *merl;          /* RegularHalfangleBRDF: RGB table (90 x 90 x 180 texels) */
 } BxDF;
 typedef struct {
     V nn, ng, sn, tn;
@@ -896,9 +898,41 @@ static void irreg_f(const Ctx *c, const BxDF *b, V wo, V wi, float *f) {
         lastMaxDist2 *= 2.f;
     }
 }
+static void from_rgb(const Ctx *c, const float rgb[3], int illum, float *r);
+static inline int clampi_(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
+/* RegularHalfangleBRDF::f (reflection.cpp:267-300); M_PI is a float literal (pbrt.h:179),
+ * REMAP = Clamp(int(V / MAX * COUNT), 0, COUNT - 1) */
+static void halfangle_f(const Ctx *c, const BxDF *b, V WO, V WI, float *f) {
+    V wo = WO, wi = WI, wh = vadd(wo, wi);
+    for (int i = 0; i < c->nb; ++i) f[i] = 0.f;
+    if (wh.z < 0.f) { wo = vneg(wo); wi = vneg(wi); wh = vneg(wh); }
+    if (wh.x == 0.f && wh.y == 0.f && wh.z == 0.f) return;
+    wh = vnorm(wh);
+    float whTheta = ACOSF(clampf(wh.z, -1.f, 1.f));
+    float whCosPhi = cosphi(wh), whSinPhi = sinphi(wh);
+    float whCosTheta = wh.z, whSinTheta = sinth(wh);
+    V whx = v3(whCosPhi * whCosTheta, whSinPhi * whCosTheta, -whSinTheta);
+    V why = v3(-whSinPhi, whCosPhi, 0.f);
+    V wd = v3(vdot(wi, whx), vdot(wi, why), vdot(wi, wh));
+    float wdTheta = ACOSF(clampf(wd.z, -1.f, 1.f));
+    float wdPhi = ATAN2F(wd.y, wd.x);
+    wdPhi = (wdPhi < 0.f) ? wdPhi + 2.f * PI_F : wdPhi;
+    if (wdPhi > PI_F) wdPhi -= PI_F;
+    int whThetaIndex = clampi_((int)(sqrtf(fmaxf_(0.f, whTheta / (PI_F / 2.f))) / 1.f * (float)90), 0, 89);
+    int wdThetaIndex = clampi_((int)(wdTheta / (PI_F / 2.f) * (float)90), 0, 89);
+    int wdPhiIndex = clampi_((int)(wdPhi / PI_F * (float)180), 0, 179);
+    int index = wdPhiIndex + 180 * (wdThetaIndex + whThetaIndex * 90);
+    from_rgb(c, &b->merl[3 * index], 0, f);
+}
 static void bx_f_add(const Ctx *c, const BxDF *b, V wo, V wi, float *out) {
     int nb = c->nb;
     switch (b->kind) {
+        case BX_MEASURED_HALF: {
+            float f[PBRTGPU_MAX_BANDS];
+            halfangle_f(c, b, wo, wi, f);
+            for (int i = 0; i < nb; ++i) out[i] += f[i];
+            break;
+        }
         case BX_MEASURED_IRREG: {
             float f[PBRTGPU_MAX_BANDS];
             irreg_f(c, b, wo, wi, f);
@@ -1385,6 +1419,13 @@ static void get_bsdf(const Ctx *c, const Isect *is, const float diff[4], BSDF *b
             BxDF *x = &bs->bx[bs->n++];
             x->kind = BX_MEASURED_IRREG; x->type = BSDF_REFLECTION | BSDF_GLOSSY;
             x->kd = c->s->kdnodes + mt->aux; x->nkd = mt->aux2;
+            break;
+        }
+        case PBRTGPU_MAT_MEASURED_HALFANGLE: {   /* measured.cpp:196-198: RegularHalfangleBRDF, none without data */
+            if (mt->aux < 0) break;
+            BxDF *x = &bs->bx[bs->n++];
+            x->kind = BX_MEASURED_HALF; x->type = BSDF_REFLECTION | BSDF_GLOSSY;
+            x->merl = c->s->merl + 3 * (size_t)mt->aux;
             break;
         }
         case PBRTGPU_MAT_SUBSTRATE: {   /* substrate.cpp:34-56 */

@@ -260,6 +260,7 @@ struct DevScene {
     const pbrtgpu_kdnode *kd;         // measured BRDF kd-trees
     const float4 *kdPack;             // kd nodes packed for the lookup walk (kd_lookup, wavefront.h)
     int nKd, kdInLds;                 // kd nodes in all trees; 1: k_shade copies them to LDS
+    const float *merl;                // RegularHalfangleBRDF RGB tables (3 floats per texel)
     const pbrtgpu_texture *tex;       // texture nodes (one-texel image maps, scale, constants)
     const float *ewa;                 // [128] MIPMap::weightLut
     const float *basis;               // [14][nbp] FromRGB basis spectra, band-quad padded
@@ -954,7 +955,8 @@ PGD_HEAVY void isect_fill(const DevScene &S, const Ray &ray, int prim, float t, 
 // ------------------------------------------------------------------ BSDF
 enum { BSDF_REFLECTION = 1, BSDF_TRANSMISSION = 2, BSDF_DIFFUSE = 4, BSDF_GLOSSY = 8, BSDF_SPECULAR = 16, BSDF_ALL = 31 };
 enum { BX_LAMBERT, BX_OREN, BX_MICRO_BLINN_DIEL, BX_SPEC_REFL_NOOP, BX_FRESNEL_BLEND_ANISO, BX_MEASURED_IRREG,
-       BX_MICRO_BLINN_COND, BX_SPEC_REFL_DIEL, BX_SPEC_TRANS };   // a = index of refraction for the last two
+       BX_MICRO_BLINN_COND, BX_SPEC_REFL_DIEL, BX_SPEC_TRANS,    // a = index of refraction for these two
+       BX_MEASURED_HALF };                                        // RegularHalfangleBRDF: R = first texel
 // R, R2: offsets into DevScene::spectra, or -1 for the per-slot textured spectrum (K bands)
 struct BxDF { int kind, type; int R, R2; float a, b; };
 struct BSDF { V nn, ng, sn, tn; int n; BxDF bx[2]; };
@@ -1078,7 +1080,9 @@ PGD_INLINE void aniso_sample(float ex, float ey, V wo, V *wi, float u1, float u2
 // T_MEAS: IrregIsotropicBRDF at BRDFRemap point (s0, s1, s2), kd-tree nodes [R, R + R2);
 // once looked up (measured_prepare) it becomes T_BUF: the spectrum in the slot's scratch bands
 // T_BLINNC: Microfacet with FresnelConductor, eta = R, k = R2, s2 = |cos theta_h|
-enum { T_ZERO = 0, T_LAMB, T_OREN, T_BLINN, T_FB, T_MEAS, T_BUF, T_BLINNC };
+// T_MERL: RegularHalfangleBRDF texel R + R2 of DevScene::merl, FromRGB'd into the slot's scratch
+// bands (fval_prepare, like T_MEAS)
+enum { T_ZERO = 0, T_LAMB, T_OREN, T_BLINN, T_FB, T_MEAS, T_BUF, T_BLINNC, T_MERL };
 struct FTerm { int kind; int R, R2; float s0, s1, s2, s3; };
 enum { FV_SUM = 0, FV_SPEC = 1 };
 // FV_SPEC: a specular BxDF's sampled value (fs * R_i) / d (reflection.cpp:130-162)
@@ -1103,6 +1107,32 @@ PGD_INLINE V brdf_remap(V wo, V wi) {
     if (dphi > 2.f * kPi) dphi -= 2.f * kPi;
     if (dphi > kPi) dphi = 2.f * kPi - dphi;
     return v3(sini * sino, dphi / kPi, cosi * coso);
+}
+PGD_INLINE int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }   // Clamp(int) (pbrt.h)
+// RegularHalfangleBRDF::f (reflection.cpp:267-300) up to the table lookup: the texel index
+// of (wo, wi) in the 90 x 90 x 180 (sqrt thetaH, thetaD, phiD) table, or -1 when wo + wi == 0
+// (Spectrum(0.)).  M_PI is a float literal in this reference (pbrt.h:179); REMAP truncates
+// V / MAX * COUNT to int and clamps to [0, COUNT - 1].
+PGD_INLINE int halfangle_index(V WO, V WI) {
+    V wo = WO, wi = WI, wh = vadd(wo, wi);
+    if (wh.z < 0.f) { wo = vneg(wo); wi = vneg(wi); wh = vneg(wh); }
+    if (wh.x == 0.f && wh.y == 0.f && wh.z == 0.f) return -1;
+    wh = vnorm(wh);
+    const float whTheta = ACOSF(clampf(wh.z, -1.f, 1.f));   // SphericalTheta
+    const float whCosPhi = cosphi(wh), whSinPhi = sinphi(wh);
+    const float whCosTheta = wh.z, whSinTheta = sinth(wh);
+    const V whx = v3(whCosPhi * whCosTheta, whSinPhi * whCosTheta, -whSinTheta);
+    const V why = v3(-whSinPhi, whCosPhi, 0.f);
+    const V wd = v3(vdot(wi, whx), vdot(wi, why), vdot(wi, wh));
+    const float wdTheta = ACOSF(clampf(wd.z, -1.f, 1.f));
+    float wdPhi = ATAN2F(wd.y, wd.x);                        // SphericalPhi
+    wdPhi = (wdPhi < 0.f) ? wdPhi + 2.f * kPi : wdPhi;
+    if (wdPhi > kPi) wdPhi -= kPi;
+    auto remap = [](float v, float mx, int count) { return clampi((int)(v / mx * (float)count), 0, count - 1); };
+    const int whThetaIndex = remap(sqrtf(pmax(0.f, whTheta / (kPi / 2.f))), 1.f, 90);
+    const int wdThetaIndex = remap(wdTheta, kPi / 2.f, 90);
+    const int wdPhiIndex = remap(wdPhi, kPi, 180);
+    return wdPhiIndex + 180 * (wdThetaIndex + whThetaIndex * 90);
 }
 PGD_INLINE FTerm bx_term(PowMemo &pm, const BxDF &b, V wo, V wi) {
     FTerm t;
@@ -1156,6 +1186,11 @@ PGD_INLINE FTerm bx_term(PowMemo &pm, const BxDF &b, V wo, V wi) {
             V m = brdf_remap(wo, wi);
             t.kind = T_MEAS;
             t.s0 = m.x; t.s1 = m.y; t.s2 = m.z;
+            break;
+        }
+        case BX_MEASURED_HALF: {
+            const int idx = halfangle_index(wo, wi);
+            if (idx >= 0) { t.kind = T_MERL; t.R2 = idx; }
             break;
         }
         default: break;   // SpecularReflection::f == 0
@@ -1662,6 +1697,14 @@ PGD_HEAVY void get_bsdf(const DevScene &S, const Isect &is, const float diff[4],
             BxDF &x = bs.bx[bs.n++];
             x.kind = BX_MEASURED_IRREG; x.type = BSDF_REFLECTION | BSDF_GLOSSY;
             x.R = mt.aux; x.R2 = mt.aux2;
+            x.a = x.b = 0.f;
+            break;
+        }
+        case PBRTGPU_MAT_MEASURED_HALFANGLE: {   // measured.cpp:196-198: one RegularHalfangleBRDF, none without data
+            if (mt.aux < 0) break;
+            BxDF &x = bs.bx[bs.n++];
+            x.kind = BX_MEASURED_HALF; x.type = BSDF_REFLECTION | BSDF_GLOSSY;
+            x.R = mt.aux; x.R2 = 0;
             x.a = x.b = 0.f;
             break;
         }

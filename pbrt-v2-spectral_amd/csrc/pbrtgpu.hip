@@ -1061,17 +1061,21 @@ int pbrtgpu_scene_upload(pbrtgpu_ctx *c, const pbrtgpu_flat_scene *s) {
     };
     for (int i = 0; i < s->n_materials; ++i) {
         const pbrtgpu_material &m = s->materials[i];
-        if (m.type < PBRTGPU_MAT_MATTE || m.type > PBRTGPU_MAT_MEASURED)
+        if (m.type < PBRTGPU_MAT_MATTE || m.type > PBRTGPU_MAT_MEASURED_HALFANGLE)
             return fail(PBRTGPU_E_UNSUPPORTED, "material type not yet supported on the GPU");
         int nt = 0;
         for (int k = 0; k < 4; ++k)
             if (m.tex[k] >= 0) {
                 ++nt;
-                if (!texOk(m.tex[k], 1, true) || m.type == PBRTGPU_MAT_METAL || m.type == PBRTGPU_MAT_MEASURED)
+                if (!texOk(m.tex[k], 1, true) || m.type == PBRTGPU_MAT_METAL || m.type == PBRTGPU_MAT_MEASURED ||
+                    m.type == PBRTGPU_MAT_MEASURED_HALFANGLE)
                     return fail(PBRTGPU_E_UNSUPPORTED, "material spectrum texture");
             }
         if (nt > 1) return fail(PBRTGPU_E_UNSUPPORTED, "more than one textured spectrum per material");
         if (m.bump_tex >= 0 && !texOk(m.bump_tex, 0, false)) return fail(PBRTGPU_E_INVALID, "bump texture");
+        if (m.type == PBRTGPU_MAT_MEASURED_HALFANGLE && m.aux >= 0 &&
+            (!s->merl || s->n_merl_floats < 0 || (int64_t)m.aux * 3 + 3 * 90 * 90 * 180 > (int64_t)s->n_merl_floats))
+            return fail(PBRTGPU_E_INVALID, "RegularHalfangle table out of range");
     }
     HIPCHK(hipSetDevice(c->device));
     HIPCHK(hipStreamSynchronize(c->stream));
@@ -1250,6 +1254,7 @@ int pbrtgpu_scene_upload(pbrtgpu_ctx *c, const pbrtgpu_flat_scene *s) {
             }
         }
         HIPCHK(upload(c, pack.data(), pack.size(), &S.kdPack));
+        HIPCHK(upload(c, s->merl, (size_t)std::max(0, s->n_merl_floats), &S.merl));
         S.nKd = (int)kd.size();
         S.kdInLds = (S.nKd > 0 && S.nKd <= kKdLdsNodes) ? 1 : 0;
         if (const char *e = getenv("PBRTGPU_KD_LDS"))   // tests: force the global-memory walk
@@ -1258,7 +1263,7 @@ int pbrtgpu_scene_upload(pbrtgpu_ctx *c, const pbrtgpu_flat_scene *s) {
     c->feat = S.nInf > 0 ? FEAT_INF : 0;
     for (int i = 0; i < s->n_materials; ++i) {
         const pbrtgpu_material &m = s->materials[i];
-        if (m.type == PBRTGPU_MAT_MEASURED) c->feat |= FEAT_MEAS;
+        if (m.type == PBRTGPU_MAT_MEASURED || m.type == PBRTGPU_MAT_MEASURED_HALFANGLE) c->feat |= FEAT_MEAS;
         if (m.bump_tex >= 0 || m.tex[0] >= 0 || m.tex[1] >= 0 || m.tex[2] >= 0 || m.tex[3] >= 0) c->feat |= FEAT_TEX;
     }
     if (const char *e = getenv("PBRTGPU_SHADE_FULL"))   // tests: run the full variant on any scene

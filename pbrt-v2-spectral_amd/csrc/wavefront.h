@@ -357,6 +357,14 @@ PGD_INLINE void fval_prepare(const DevScene &S, FVal &F, float4 *mb, size_t c) {
         if (k < F.n && F.t[k].kind == T_MEAS) {
             measured_lookup<NB>(S, F.t[k], mb, c);
             F.t[k].kind = T_BUF;
+        } else if (k < F.n && F.t[k].kind == T_MERL) {
+            // Spectrum::FromRGB(&brdf[3 * index]) (reflection.cpp:299), reflectance
+            const float *rgb = S.merl + 3 * ((size_t)F.t[k].R + (size_t)F.t[k].R2);
+            const float v[3] = {rgb[0], rgb[1], rgb[2]};
+            const RGBPick pk = rgb_pick(v);
+#pragma unroll
+            for (int q = 0; q < Bands<NB>::NQ; ++q) mb[q * c] = from_rgb4(S, pk, false, q);
+            F.t[k].kind = T_BUF;
         }
 }
 
@@ -592,7 +600,11 @@ PGD_INLINE Pushes shade_vertex(const DevScene &S, const PathSoA &P, int slot, in
         PGD_T0(MIS);
         // ---- BSDF sample with MIS -> B (added if the MIS ray reaches this light: hits it
         // facing, for an area light; escapes the scene, for the environment)
+#ifdef PGD_EXPERIMENT_NO_MIS   // timing experiment only: the MIS section's cost (wrong radiance)
+        if (false) {
+#else
         if (!em.point) {
+#endif
             int sampledType;
             BSDFSampleState sst;
             bool keep = bsdf_sample_dir(pm, bs, wo, &wi, ub[0], ub[1], ub[2], &bsdfPdf, flags, &sampledType, F, sst);

@@ -963,11 +963,17 @@ private:
             std::string fn = Resolve(GetString(g, m, "filename", ""));
             size_t dot = fn.rfind('.');
             std::string suf = dot == std::string::npos ? "" : fn.substr(dot);
-            if (suf != ".brdf" && suf != ".BRDF")
-                throw std::runtime_error("measured BRDF '" + fn + "': only the irregular .brdf format is supported");
-            auto it = measuredCache.find(fn);
-            if (it == measuredCache.end()) it = measuredCache.insert(std::make_pair(fn, LoadIrregBrdf(fn))).first;
-            mo->measured = it->second;
+            if (suf == ".brdf" || suf == ".BRDF") {
+                auto it = measuredCache.find(fn);
+                if (it == measuredCache.end()) it = measuredCache.insert(std::make_pair(fn, LoadIrregBrdf(fn))).first;
+                mo->measured = it->second;
+            } else {
+                // any other suffix: the MERL RegularHalfangle format (measured.cpp:131-175)
+                mt.type = PBRTGPU_MAT_MEASURED_HALFANGLE;
+                auto it = merlCache.find(fn);
+                if (it == merlCache.end()) it = merlCache.insert(std::make_pair(fn, LoadMerl(fn))).first;
+                mt.aux = it->second;
+            }
         } else
             throw std::runtime_error("material '" + name + "' is not supported by this build yet");
         return mo;
@@ -999,6 +1005,7 @@ private:
         return spec.FromSampled(wl, kAbsorption ? kk : eta, 56);
     }
     std::map<std::string, std::shared_ptr<MeasuredData> > measuredCache;
+    std::map<std::string, int> merlCache;   // loadedRegularHalfangle (measured.cpp:99)
     // ReadFloatFile (floatfile.cpp:30-74)
     static std::vector<float> ReadFloatFile(const std::string &fn) {
         FILE *fp = fopen(fn.c_str(), "r");
@@ -1033,6 +1040,47 @@ private:
         if (dphi > 2.f * kPiF) dphi -= 2.f * kPiF;
         if (dphi > kPiF) dphi = 2.f * kPiF - dphi;
         return V3(sini * sino, dphi / kPiF, cosi * coso);
+    }
+    // RegularHalfangle data (measured.cpp:131-175): three int dims whose product must be
+    // 90 * 90 * 180, then per RGB channel that many doubles in chunks of 2 * nPhiD, each
+    // scaled (1/1500, 1.15/1500, 1.66/1500 as float constants) and clamped at 0 in double,
+    // stored as float.  Returns the first texel in out->merl, or -1 when the reference's loader
+    // fails (Error(); the material then has no BxDF).
+    int LoadMerl(const std::string &fn) {
+        const uint32_t nThetaH = 90, nThetaD = 90, nPhiD = 180;
+        FILE *f = fopen(fn.c_str(), "rb");
+        if (!f) { out->warnings.push_back("Unable to open BRDF data file " + fn); return -1; }
+        int dims[3];
+        if (fread(dims, sizeof(int), 3, f) != 3) {
+            out->warnings.push_back("Premature end-of-file in measured BRDF data file " + fn);
+            fclose(f);
+            return -1;
+        }
+        const uint32_t n = (uint32_t)dims[0] * (uint32_t)dims[1] * (uint32_t)dims[2];
+        if (n != nThetaH * nThetaD * nPhiD) {
+            out->warnings.push_back("Dimensions don't match in " + fn);
+            fclose(f);
+            return -1;
+        }
+        std::vector<float> tab(3 * (size_t)n);
+        const uint32_t chunkSize = 2 * nPhiD, nChunks = n / chunkSize;
+        std::vector<double> tmp(chunkSize);
+        const float scales[3] = {1.f / 1500.f, 1.15f / 1500.f, 1.66f / 1500.f};
+        for (int c = 0; c < 3; ++c) {
+            size_t offset = 0;
+            for (uint32_t i = 0; i < nChunks; ++i) {
+                if (fread(tmp.data(), sizeof(double), chunkSize, f) != chunkSize) {
+                    out->warnings.push_back("Premature end-of-file in measured BRDF data file " + fn);
+                    fclose(f);
+                    return -1;
+                }
+                for (uint32_t j = 0; j < chunkSize; ++j) tab[3 * offset++ + c] = (float)std::max(0., tmp[j] * scales[c]);
+            }
+        }
+        fclose(f);
+        const int first = (int)(out->merl.size() / 3);
+        out->merl.insert(out->merl.end(), tab.begin(), tab.end());
+        return first;
     }
     std::shared_ptr<MeasuredData> LoadIrregBrdf(const std::string &fn) {
         std::vector<float> values = ReadFloatFile(fn);
@@ -1682,6 +1730,8 @@ void HostScene::Flat(pbrtgpu_flat_scene *f) const {
     f->n_textures = (int)textures.size(); f->textures = textures.empty() ? nullptr : textures.data();
     f->ewa_lut = ewaLut.empty() ? nullptr : ewaLut.data();
     f->rgb_basis = rgbBasis.empty() ? nullptr : rgbBasis.data();
+    f->n_merl_floats = (int)merl.size();
+    f->merl = merl.empty() ? nullptr : merl.data();
 }
 
 }  // namespace pbrtamd

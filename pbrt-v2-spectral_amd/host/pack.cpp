@@ -11,7 +11,7 @@
 namespace pbrtamd {
 
 static const char kMagic[8] = {'P', 'B', 'R', 'T', 'P', 'A', 'C', 'K'};
-static const uint32_t kVersion = 5;
+static const uint32_t kVersion = 6;   // 6: + merl tables (version 5 packs load with none)
 
 static bool W(gzFile f, const void *p, size_t n) {
     const char *c = (const char *)p;
@@ -46,7 +46,7 @@ bool SavePack(const HostScene &s, const std::string &path, std::string *err) {
          WArr(f, s.vertP) && WArr(f, s.vertN) && WArr(f, s.vertUV) && WArr(f, s.quadrics) && WArr(f, s.materials) &&
          WArr(f, s.lights) && WArr(f, s.lightShapes) && WArr(f, s.spectra) && WArr(f, s.instances) &&
          WArr(f, s.primInstance) && WArr(f, s.kdnodes) && WArr(f, s.textures) && WArr(f, s.ewaLut) &&
-         WArr(f, s.rgbBasis);
+         WArr(f, s.rgbBasis) && WArr(f, s.merl);
     ok = (gzclose(f) == Z_OK) && ok;
     if (!ok && err) *err = "write error on " + path;
     return ok;
@@ -57,7 +57,7 @@ bool LoadPack(const std::string &path, HostScene *s, std::string *err) {
     if (!f) { if (err) *err = "cannot open " + path; return false; }
     char magic[8];
     uint32_t ver = 0;
-    bool ok = R(f, magic, 8) && memcmp(magic, kMagic, 8) == 0 && R(f, &ver, 4) && ver == kVersion;
+    bool ok = R(f, magic, 8) && memcmp(magic, kMagic, 8) == 0 && R(f, &ver, 4) && (ver == kVersion || ver == 5);
     int32_t hdr[4];
     ok = ok && R(f, hdr, 16) && R(f, &s->seed, 4) && R(f, &s->yint, 4);
     if (ok) { s->nBands = hdr[0]; s->maxDepth = hdr[1]; s->spp = hdr[2]; s->bvhMaxDepth = hdr[3]; }
@@ -67,6 +67,8 @@ bool LoadPack(const std::string &path, HostScene *s, std::string *err) {
          RArr(f, s->lights) && RArr(f, s->lightShapes) && RArr(f, s->spectra) && RArr(f, s->instances) &&
          RArr(f, s->primInstance) && RArr(f, s->kdnodes) && RArr(f, s->textures) && RArr(f, s->ewaLut) &&
          RArr(f, s->rgbBasis);
+    s->merl.clear();
+    if (ok && ver >= 6) ok = RArr(f, s->merl);
     gzclose(f);
     if (!ok && err) *err = "bad or truncated scene pack " + path;
     return ok;

@@ -57,6 +57,7 @@ struct HostScene {
     std::vector<pbrtgpu_texture> textures;
     std::vector<float> ewaLut;                // [128] MIPMap::weightLut
     std::vector<float> rgbBasis;              // [14][nBands] FromRGB basis spectra
+    std::vector<float> merl;                  // RegularHalfangleBRDF RGB tables (pbrtgpu_flat_scene::merl)
     // diagnostics
     std::vector<std::string> warnings;
     int bvhMaxDepth = 0;

@@ -58,7 +58,8 @@ class FlatScene(ctypes.Structure):
                 ("n_spectra_floats", I32), ("spectra", P),
                 ("n_instances", I32), ("instances", P), ("prim_instance", P),
                 ("n_kdnodes", I32), ("kdnodes", P),
-                ("n_textures", I32), ("textures", P), ("ewa_lut", P), ("rgb_basis", P)]
+                ("n_textures", I32), ("textures", P), ("ewa_lut", P), ("rgb_basis", P),
+                ("n_merl_floats", I32), ("merl", P)]
 
 
 class Overrides(ctypes.Structure):
@@ -74,7 +75,7 @@ class RenderDesc(ctypes.Structure):
 STAT_PATHS, STAT_KERNEL_MS, STAT_ACCUM_MS, STAT_ZEROED, STAT_SPILLS, STAT_PASSES = 0, 1, 2, 3, 4, 5
 F_ACCUMULATE, F_COUNT_WORK = 1, 2
 KEEP_SEED = 0xFFFFFFFF
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 
 class Timing(ctypes.Structure):

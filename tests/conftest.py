@@ -32,3 +32,21 @@ def pg():
 @pytest.fixture(scope="session")
 def killeroo64(pg):
     return pg.Scene.load(os.path.join(PACKS, "killeroo-simple.pack"), xres=64, yres=64, spp=4)
+
+
+@pytest.fixture(scope="session")
+def merl_dir(tmp_path_factory):
+    """tests/scenes/merl.pbrt next to the synthetic MERL table it names (tools/make_merl.py
+    writes the 35 MB table here; it is not committed)."""
+    import shutil
+    d = tmp_path_factory.mktemp("merl")
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import make_merl
+    make_merl.write(str(d / "synthetic.merl"))
+    shutil.copy(os.path.join(ROOT, "tests", "scenes", "merl.pbrt"), str(d))
+    return str(d)
+
+
+def merl_scene(pg, merl_dir, cfg):
+    w, h, spp, seed, md = [int(v) for v in cfg]
+    return pg.Scene.load(os.path.join(merl_dir, "merl.pbrt"), xres=w, yres=h, spp=spp, maxdepth=md, seed=seed)

@@ -136,3 +136,21 @@ def test_frontend_parses_reference_scene_to_pack(pg):
     a, b = flat_arrays(s), flat_arrays(p)
     for k in a:
         assert np.array_equal(a[k], b[k]), k
+
+
+def test_pack_keeps_merl_tables(pg, merl_dir, tmp_path):
+    """Scene packs (version 6) carry the RegularHalfangle tables; the missing-file material
+    keeps aux = -1 (no BxDF)."""
+    import ctypes
+    s = pg.Scene.load(os.path.join(merl_dir, "merl.pbrt"), xres=16, yres=12, spp=1)
+    fn = str(tmp_path / "m.pack")
+    s.save_pack(fn)
+    p = pg.Scene.load(fn)
+    n = s.flat.n_merl_floats
+    assert n == p.flat.n_merl_floats == 3 * 90 * 90 * 180
+    a = np.ctypeslib.as_array(ctypes.cast(s.flat.merl, ctypes.POINTER(ctypes.c_float)), (n,))
+    b = np.ctypeslib.as_array(ctypes.cast(p.flat.merl, ctypes.POINTER(ctypes.c_float)), (n,))
+    assert np.array_equal(a, b) and a.min() == 0.0 and a.max() > 0.5
+    mats = ctypes.cast(s.flat.materials, ctypes.POINTER(ctypes.c_int32 * 24))
+    kinds = [(mats[i][0], mats[i][5]) for i in range(s.flat.n_materials)]   # (type, aux)
+    assert (7, 0) in kinds and (7, -1) in kinds

@@ -112,3 +112,21 @@ def test_metal_scene_contents(pg):
     assert s.bands == 60 and s.flat.n_textures >= 3 and s.flat.n_lights == 1
     import ctypes
     assert ctypes.cast(s.flat.lights, ctypes.POINTER(ctypes.c_int32))[0] == 2   # PBRTGPU_LIGHT_INFINITE
+
+
+@pytest.mark.parametrize("name", ["merl_paths_64x48s8", "merl_film_64x48s8"])
+def test_regular_halfangle_brdf_bit_exact_vs_reference(pg, ora_libm, merl_dir, name):
+    """RegularHalfangleBRDF (reflection.cpp:267-300) from a MERL-format table loaded as
+    measured.cpp:131-175 loads it, and a measured material whose file is missing (no BxDF):
+    the oracle against the reference harness, bit for bit."""
+    from conftest import merl_scene
+    g = np.load(os.path.join(GOLDEN, name + ".npz"))
+    scene = merl_scene(pg, merl_dir, g["config"])
+    assert scene.flat.n_merl_floats == 3 * 90 * 90 * 180
+    if "paths" in name:
+        L = ora_libm.trace_paths(scene, g["keys"])
+        same = np.all(L.view(np.int32) == g["L"].view(np.int32), axis=1)
+        assert same.all(), "paths differing: %d / %d" % ((~same).sum(), len(same))
+    else:
+        film, _ = ora_libm.render(scene, threads=8)
+        assert np.array_equal(film.view(np.int32), g["film"].view(np.int32))

@@ -30,6 +30,10 @@ Fixtures (numpy .npz, inputs + expected outputs only):
                                   400x400@4096 60 bands, C5 anim 600x600@512): every sample of a
                                   few pixels (all of the sampler's permutation masks at that spp)
                                   plus 2048 random (x, y, s) keys of the sample extent (--keys)
+  merl_paths_64x48s8.npz, merl_film_64x48s8.npz   tests/scenes/merl.pbrt: RegularHalfangleBRDF
+                                  (measured.cpp:131-175, reflection.cpp:267-300) from the synthetic
+                                  MERL table of tools/make_merl.py, plus a measured material whose
+                                  .merl file is missing (no BxDF)
   killeroo_dat_40x32s4.npz        the raw film of the restatement film AND the .dat the
                                   reference's own SpectralImageNoCameraFilm wrote for the same
                                   samples (--refdat): pins AddSample and the WriteImage payload
@@ -126,6 +130,16 @@ def dat_fixture(name, res, spp, tmp, scene="killeroo-simple.pbrt"):
     print(name, film.shape, os.path.getsize(dat))
 
 
+def merl_fixtures(tmp):
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import make_merl
+    merl = os.path.join(ROOT, "tests", "scenes", "synthetic.merl")   # git-ignored, regenerated here
+    make_merl.write(merl)
+    scene = os.path.join(ROOT, "tests", "scenes", "merl.pbrt")
+    paths_fixture("merl_paths_64x48s8", (64, 48), 8, 0, 5, 2, tmp, scene=scene)
+    film_fixture("merl_film_64x48s8", (64, 48), 8, 0, 5, tmp, scene=scene)
+
+
 def main():
     if not os.path.exists(HARNESS):
         sys.exit("build the reference harness first: make -C oracle ref")
@@ -140,6 +154,8 @@ def main():
                     keys_fixture(*cfg, tmp)
             elif only == "dat":
                 dat_fixture("killeroo_dat_40x32s4", (40, 32), 4, tmp)
+            elif only == "merl":
+                merl_fixtures(tmp)
         return
     with tempfile.TemporaryDirectory() as tmp:
         paths_fixture("killeroo_paths_64x64s4", (64, 64), 4, 0, 5, 5, tmp)
@@ -166,6 +182,7 @@ def main():
             if cfg[5] != 60 or os.path.exists(HARNESS60):
                 keys_fixture(*cfg, tmp)
         dat_fixture("killeroo_dat_40x32s4", (40, 32), 4, tmp)
+        merl_fixtures(tmp)
         fn = os.path.join(tmp, "mt.bin")
         run(["-", "--kat-mt", fn])
         raw = np.fromfile(fn, dtype=np.uint32).reshape(6, 65)
