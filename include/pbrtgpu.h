@@ -140,7 +140,9 @@ typedef struct pbrtgpu_light {
     float sum_area;        /* ShapeSet::sumArea */
     float pos[3];          /* point light position LightToWorld(0,0,0) */
     int32_t is_black;      /* emitted spectrum IsBlack() */
-    int32_t pad[3];
+    int32_t n_samples;     /* Light::nSamples = max(1, "nsamples") (light.h:45); DirectLighting's
+                            * strategy "all" takes RoundUpPow2 of it (LDSampler::RoundSize) */
+    int32_t pad[2];
     float l2w_m[16];
     float l2w_minv[16];
     /* infinite (InfiniteAreaLight, lights/infinite.cpp): the radiance MIPMap's single texel
@@ -232,7 +234,15 @@ typedef struct pbrtgpu_flat_scene {
                                    * scale and clamp (measured.cpp:133-175), texel index
                                    * phiD + 180 * (thetaD + 90 * thetaH) */
     const float *merl;
+    int32_t integrator;           /* PBRTGPU_INTEGRATOR_*: the scene's SurfaceIntegrator */
+    int32_t dl_strategy;          /* DirectLighting "strategy": PBRTGPU_DL_ALL or PBRTGPU_DL_ONE */
 } pbrtgpu_flat_scene;
+
+/* SurfaceIntegrator of a flattened scene: "path" (integrators/path.cpp:44-115) or
+ * "directlighting" (integrators/directlighting.cpp:73-125, with the specular recursion of
+ * core/integrator.cpp:169-250); max_depth is the integrator's "maxdepth" either way */
+enum { PBRTGPU_INTEGRATOR_PATH = 0, PBRTGPU_INTEGRATOR_DIRECT = 1 };
+enum { PBRTGPU_DL_ALL = 0, PBRTGPU_DL_ONE = 1 };
 
 /* ---- render description ----------------------------------------------------------- */
 /* Tiles are tile_w x tile_h blocks of the FILM pixel window (camera px_count x py_count;

@@ -26,6 +26,9 @@ typedef struct pbrthost_overrides {
     int32_t maxdepth;     /* SurfaceIntegrator "path" "maxdepth" */
     int32_t bands;        /* nSpectralSamples: 32 (reference build), 60 or 30; <= 0: the pack's own, or 32 */
     uint32_t seed;        /* fixed-seed sampler seed; PBRTHOST_KEEP_SEED keeps the pack's (0 for .pbrt) */
+    int32_t integrator;   /* PBRTGPU_INTEGRATOR_* to force, or -1: the scene's own ("path" for packs
+                           * built before integrators were recorded) */
+    int32_t dl_strategy;  /* PBRTGPU_DL_* to force, or -1: the scene's "strategy" */
 } pbrthost_overrides;
 
 /* path: a .pbrt scene file or a .pack scene pack.  Returns 0 or -1 (message in err). */

@@ -1278,7 +1278,32 @@ static void tex_spec(const Ctx *c, int id, const TexPt *q, float *out) {
 }
 /* camera ray differentials (perspective.cpp:98-104 + RayDifferential::ScaleDifferentials) */
 typedef struct { V rxo, rxd, ryo, ryd; int has; } RayDiff;
-/* DifferentialGeometry::ComputeDifferentials (diffgeom.cpp:50-105): out = dudx, dvdx, dudy, dvdy */
+/* DifferentialGeometry::ComputeDifferentials (diffgeom.cpp:50-105): out = dudx, dvdx, dudy, dvdy;
+ * dpdx / dpdy (may be NULL) = px - p, py - p, zero where the reference zeroes them */
+static void compute_differentials2(const DG *dg, const RayDiff *rd, float out[4], V *dpdx, V *dpdy) {
+    out[0] = out[1] = out[2] = out[3] = 0.f;
+    if (dpdx) *dpdx = v3(0.f, 0.f, 0.f);
+    if (dpdy) *dpdy = v3(0.f, 0.f, 0.f);
+    if (!rd || !rd->has) return;
+    float d = -vdot(dg->nn, dg->p);
+    float tx = -(vdot(dg->nn, rd->rxo) + d) / vdot(dg->nn, rd->rxd);
+    if (isnan(tx)) return;
+    V px = vadd(rd->rxo, vmul(rd->rxd, tx));
+    float ty = -(vdot(dg->nn, rd->ryo) + d) / vdot(dg->nn, rd->ryd);
+    if (isnan(ty)) return;
+    V py = vadd(rd->ryo, vmul(rd->ryd, ty));
+    if (dpdx) *dpdx = vsub(px, dg->p);
+    if (dpdy) *dpdy = vsub(py, dg->p);
+    int a0, a1;
+    if (fabsf(dg->nn.x) > fabsf(dg->nn.y) && fabsf(dg->nn.x) > fabsf(dg->nn.z)) { a0 = 1; a1 = 2; }
+    else if (fabsf(dg->nn.y) > fabsf(dg->nn.z)) { a0 = 0; a1 = 2; }
+    else { a0 = 0; a1 = 1; }
+    float A[2][2] = {{vcomp(dg->dpdu, a0), vcomp(dg->dpdv, a0)}, {vcomp(dg->dpdu, a1), vcomp(dg->dpdv, a1)}};
+    float Bx[2] = {vcomp(px, a0) - vcomp(dg->p, a0), vcomp(px, a1) - vcomp(dg->p, a1)};
+    float By[2] = {vcomp(py, a0) - vcomp(dg->p, a0), vcomp(py, a1) - vcomp(dg->p, a1)};
+    if (!solve2x2(A, Bx, &out[0], &out[1])) out[0] = out[1] = 0.f;
+    if (!solve2x2(A, By, &out[2], &out[3])) out[2] = out[3] = 0.f;
+}
 static void compute_differentials(const DG *dg, const RayDiff *rd, float out[4]) {
     out[0] = out[1] = out[2] = out[3] = 0.f;
     if (!rd || !rd->has) return;
@@ -1784,6 +1809,131 @@ static void radiance(const Ctx *c, Ray ray, const RayDiff *rd, PathSampler *ps, 
     for (int i = 0; i < nb; ++i) Lout[i] = (1.f * L[i]) + 0.f;   /* T * Li + Lvi */
 }
 
+/* ------------------------------------------------------------------ DirectLightingIntegrator */
+/* Sample layout of DirectLightingIntegrator::RequestSamples (directlighting.cpp:46-70) + the
+ * emission integrator's 2 x 1D: strategy "all": per light i 1D [lightComp 2i, bsdfComp 2i+1],
+ * 2D [lightPos 2i, bsdfDir 2i+1], each with RoundUpPow2(nSamples) values; "one": 1D
+ * [lightComp 0, lightNum 1, bsdfComp 2], 2D [lightPos 0, bsdfDir 1].  Value k of a slot of
+ * count n is sample index s * n + k of a sequence of length spp * n. */
+static uint32_t pow2_up(uint32_t v) { v--; v |= v >> 1; v |= v >> 2; v |= v >> 4; v |= v >> 8; v |= v >> 16; return v + 1; }
+static int dl_n1d(const Ctx *c) { return c->s->dl_strategy == PBRTGPU_DL_ONE ? 5 : 2 * c->s->n_lights + 2; }
+static int dl_count(const Ctx *c, int i) { int n = c->s->lights[i].n_samples; return (int)pow2_up((uint32_t)(n > 1 ? n : 1)); }
+static void dl_light_sample(const Ctx *c, const PathSampler *ps, int i, int j, float ul[3], float ub[3], float *ulnum) {
+    uint32_t n1 = (uint32_t)dl_n1d(c), u2i[2];
+    float u2[2];
+    (void)u2i;
+    if (c->s->dl_strategy == PBRTGPU_DL_ONE) {
+        *ulnum = s1d(ps->hp, 3u + 1u, ps->s, ps->spp);
+        s2d(ps->hp, 3u + n1 + 0u, ps->s, ps->spp, u2); ul[0] = u2[0]; ul[1] = u2[1];
+        ul[2] = s1d(ps->hp, 3u + 0u, ps->s, ps->spp);
+        s2d(ps->hp, 3u + n1 + 1u, ps->s, ps->spp, u2); ub[0] = u2[0]; ub[1] = u2[1];
+        ub[2] = s1d(ps->hp, 3u + 2u, ps->s, ps->spp);
+        return;
+    }
+    uint32_t n = (uint32_t)dl_count(c, i), k = ps->s * n + (uint32_t)j, len = ps->spp * n;
+    s2d(ps->hp, 3u + n1 + 2u * i, k, len, u2); ul[0] = u2[0]; ul[1] = u2[1];
+    ul[2] = s1d(ps->hp, 3u + 2u * i, k, len);
+    s2d(ps->hp, 3u + n1 + 2u * i + 1u, k, len, u2); ub[0] = u2[0]; ub[1] = u2[1];
+    ub[2] = s1d(ps->hp, 3u + 2u * i + 1u, k, len);
+    *ulnum = 0.f;
+}
+/* DirectLightingIntegrator::Li (directlighting.cpp:73-109) for a ray of depth `depth`, via
+ * SamplerRenderer::Li (samplerrenderer.cpp:225-247: miss -> sum of the lights' Le), with
+ * SpecularReflect / SpecularTransmit (integrator.cpp:169-250) and their ray differentials */
+static void dl_radiance(const Ctx *c, Ray ray, const RayDiff *rd, int depth, PathSampler *ps, float *Lout) {
+    int nb = c->nb, nLights = c->s->n_lights;
+    float L[MAXB], tmp[MAXB], Ld[MAXB], ed[MAXB], f[MAXB], Lc[MAXB];
+    for (int i = 0; i < nb; ++i) L[i] = 0.f;
+    Hit h;
+    Isect is;
+    if (!bvh_intersect(c, &ray, &h)) {
+        for (int k = 0; k < nLights; ++k)
+            if (c->s->lights[k].type == PBRTGPU_LIGHT_INFINITE) {
+                inf_Le(c, &c->s->lights[k], ray.d, tmp);
+                for (int i = 0; i < nb; ++i) L[i] += tmp[i];
+            }
+        for (int i = 0; i < nb; ++i) Lout[i] = (1.f * L[i]) + 0.f;
+        return;
+    }
+    isect_fill(c, &ray, &h, &is);
+    float diff[4];
+    V dpdx, dpdy;
+    compute_differentials2(&is.dg, rd, diff, &dpdx, &dpdy);
+    BSDF bs;
+    DG dgs;
+    get_bsdf(c, &is, diff, &bs, &dgs);
+    V wo = vneg(ray.d), p = dgs.p, n = dgs.nn;
+    isect_Le(c, &is, wo, tmp);
+    for (int i = 0; i < nb; ++i) L[i] += tmp[i];
+    if (nLights > 0) {
+        float ul[3], ub[3], ulnum;
+        if (c->s->dl_strategy == PBRTGPU_DL_ONE) {   /* UniformSampleOneLight (integrator.cpp:74-106) */
+            dl_light_sample(c, ps, 0, 0, ul, ub, &ulnum);
+            int lightNum = (int)floorf(ulnum * nLights);
+            if (lightNum > nLights - 1) lightNum = nLights - 1;
+            estimate_direct(c, lightNum, p, n, wo, is.rayEps, ray.time, &bs, ul, ub, ed);
+            for (int i = 0; i < nb; ++i) L[i] += ed[i] * (float)nLights;
+        } else {                                       /* UniformSampleAllLights (integrator.cpp:39-71) */
+            float La[MAXB];                            /* its own sum, added to L once */
+            for (int i = 0; i < nb; ++i) La[i] = 0.f;
+            for (int li = 0; li < nLights; ++li) {
+                int ns = dl_count(c, li);
+                for (int i = 0; i < nb; ++i) Ld[i] = 0.f;
+                for (int j = 0; j < ns; ++j) {
+                    dl_light_sample(c, ps, li, j, ul, ub, &ulnum);
+                    estimate_direct(c, li, p, n, wo, is.rayEps, ray.time, &bs, ul, ub, ed);
+                    for (int i = 0; i < nb; ++i) Ld[i] += ed[i];
+                }
+                for (int i = 0; i < nb; ++i) La[i] += Ld[i] / (float)ns;
+            }
+            for (int i = 0; i < nb; ++i) L[i] += La[i];
+        }
+    }
+    if (depth + 1 < c->s->max_depth) {
+        const pbrtgpu_material *mt = &c->s->materials[c->s->prims[is.prim].material];
+        float bsdfEta = mt->type == PBRTGPU_MAT_GLASS ? mt->f[0] : 1.f;   /* BSDF::eta (glass.cpp:48) */
+        for (int pass = 0; pass < 2; ++pass) {   /* SpecularReflect, then SpecularTransmit */
+            float u0 = rng_float(&ps->rng), u1 = rng_float(&ps->rng), uc = rng_float(&ps->rng);   /* BSDFSample(rng) */
+            int flags = BSDF_SPECULAR | (pass ? BSDF_TRANSMISSION : BSDF_REFLECTION), st;
+            V wi;
+            float pdf;
+            bsdf_sample_f(c, &bs, wo, &wi, u0, u1, uc, &pdf, flags, &st, f);
+            float ad = fabsf(vdot(wi, n));
+            if (!(pdf > 0.f) || spec_black(c, f) || ad == 0.f) continue;
+            Ray cr; cr.o = p; cr.d = wi; cr.mint = is.rayEps; cr.maxt = INFINITY; cr.time = ray.time;
+            RayDiff crd;
+            crd.has = 0;
+            if (rd && rd->has) {
+                crd.has = 1;
+                crd.rxo = vadd(p, dpdx);
+                crd.ryo = vadd(p, dpdy);
+                V dndx = vadd(vmul(dgs.dndu, diff[0]), vmul(dgs.dndv, diff[1]));
+                V dndy = vadd(vmul(dgs.dndu, diff[2]), vmul(dgs.dndv, diff[3]));
+                V dwodx = vsub(vneg(rd->rxd), wo), dwody = vsub(vneg(rd->ryd), wo);
+                float dDNdx = vdot(dwodx, n) + vdot(wo, dndx);
+                float dDNdy = vdot(dwody, n) + vdot(wo, dndy);
+                if (pass == 0) {
+                    float won = vdot(wo, n);
+                    crd.rxd = vadd(vsub(wi, dwodx), vmul(vadd(vmul(dndx, won), vmul(n, dDNdx)), 2.f));
+                    crd.ryd = vadd(vsub(wi, dwody), vmul(vadd(vmul(dndy, won), vmul(n, dDNdy)), 2.f));
+                } else {
+                    float eta = bsdfEta;
+                    V w = vneg(wo);
+                    if (vdot(wo, n) < 0) eta = 1.f / eta;
+                    float mu = eta * vdot(w, n) - vdot(wi, n);
+                    float dmudx = (eta - (eta * eta * vdot(w, n)) / vdot(wi, n)) * dDNdx;
+                    float dmudy = (eta - (eta * eta * vdot(w, n)) / vdot(wi, n)) * dDNdy;
+                    crd.rxd = vsub(vadd(wi, vmul(dwodx, eta)), vadd(vmul(dndx, mu), vmul(n, dmudx)));
+                    crd.ryd = vsub(vadd(wi, vmul(dwody, eta)), vadd(vmul(dndy, mu), vmul(n, dmudy)));
+                }
+            }
+            dl_radiance(c, cr, &crd, depth + 1, ps, Lc);
+            for (int i = 0; i < nb; ++i) L[i] += ((f[i] * Lc[i]) * ad) / pdf;
+        }
+    }
+    for (int i = 0; i < nb; ++i) Lout[i] = (1.f * L[i]) + 0.f;
+}
+
 /* camera sample -> world ray (perspective.cpp:73-106, transform.h:253-262) */
 static Ray camera_ray(const Ctx *c, float imageX, float imageY, float lensU, float lensV, float timeU, RayDiff *rd) {
     const pbrtgpu_camera *cam = &c->s->camera;
@@ -1853,7 +2003,8 @@ static int trace_path(const Ctx *c, int px, int py, uint32_t s, float *L, float 
     RayDiff rd;
     Ray r = camera_ray(c, imageX, imageY, lens[0], lens[1], timeU, &rd);
     float Lr[MAXB];
-    radiance(c, r, &rd, &ps, Lr);
+    if (c->s->integrator == PBRTGPU_INTEGRATOR_DIRECT) dl_radiance(c, r, &rd, 0, &ps, Lr);
+    else radiance(c, r, &rd, &ps, Lr);
     int nb = c->nb, bad = 0;
     for (int i = 0; i < nb; ++i) L[i] = 1.f * Lr[i];   /* rayWeight * Li */
     int nan = 0;

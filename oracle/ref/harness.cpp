@@ -58,6 +58,8 @@
 #include "gpupathrenderer.h"   // integration/: the reference-side binding of the MI355X core
 #endif
 #include "integrators/path.h"
+#include "integrators/directlighting.h"
+#include "samplers/lowdiscrepancy.h"
 #include "integrators/emission.h"
 #include "lights/diffuse.h"
 #include "lights/point.h"
@@ -129,12 +131,15 @@ static void FillSample(Sample *smp, int px, int py, uint32_t s, uint32_t spp, ui
     smp->lensU = u[0]; smp->lensV = u[1];
     smp->time = Lerp(sample1D(hp, 2, s, spp), shutterOpen, shutterClose);
     uint32_t n1 = smp->n1D.size(), n2 = smp->n2D.size();
+    // a slot requested with count n (DirectLighting "all": a light's nSamples, rounded to a
+    // power of two by LDSampler::RoundSize) holds the n values of sample index s * n + k of
+    // the same dimension's sequence of length spp * n; with n == 1 that is (s, spp)
     for (uint32_t j = 0; j < n1; ++j)
-        for (uint32_t k = 0; k < smp->n1D[j]; ++k)      // all counts are 1 for path
-            smp->oneD[j][k] = sample1D(hp, 3 + j, s, spp);
+        for (uint32_t k = 0; k < smp->n1D[j]; ++k)
+            smp->oneD[j][k] = sample1D(hp, 3 + j, s * smp->n1D[j] + k, spp * smp->n1D[j]);
     for (uint32_t j = 0; j < n2; ++j)
         for (uint32_t k = 0; k < smp->n2D[j]; ++k)
-            sample2D(hp, 3 + n1 + j, s, spp, &smp->twoD[j][2 * k]);
+            sample2D(hp, 3 + n1 + j, s * smp->n2D[j] + k, spp * smp->n2D[j], &smp->twoD[j][2 * k]);
 }
 
 // ---------------------------------------------------------------------------------
@@ -328,6 +333,8 @@ static std::vector<Light *> lights;
 static std::vector<Reference<Primitive> > primitives;
 // overrides from the command line
 static int ovW = -1, ovH = -1, ovMaxDepth = -1;
+static const char *surfOv = "path";   // --surf: the SurfaceIntegrator to create
+static const char *dlStrategyOv = NULL;
 // results of WorldEnd
 static Scene *gScene = NULL;
 static Camera *gCamera = NULL;
@@ -512,7 +519,16 @@ void pbrtWorldEnd() {
     if (cameraName != "perspective") { fprintf(stderr, "harness: camera %s unsupported\n", cameraName.c_str()); exit(2); }
     gCamera = CreatePerspectiveCamera(cameraParams, ac2w, gFilm);
     if (ovMaxDepth >= 0) { int v = ovMaxDepth; surfParams.AddInt("maxdepth", &v, 1); }
-    gSurf = CreatePathSurfaceIntegrator(surfParams);   // configs override to "path" 
+    // the configs override the scene's integrator to "path" (SURVEY App. B), the harness's
+    // default; --surf directlighting creates the DirectLightingIntegrator from the scene's
+    // SurfaceIntegrator parameters (maxdepth, strategy; --dl-strategy overrides the latter),
+    // --surf scene the one the scene names (api.cpp:551-583)
+    string sn = string(surfOv) == "scene" ? surfName : string(surfOv);
+    if (sn == "directlighting") {
+        if (dlStrategyOv) { string st(dlStrategyOv); surfParams.AddString("strategy", &st, 1); }
+        gSurf = CreateDirectLightingIntegrator(surfParams);
+    } else if (sn == "path") gSurf = CreatePathSurfaceIntegrator(surfParams);
+    else { fprintf(stderr, "harness: surface integrator %s unsupported\n", sn.c_str()); exit(2); }
     gVol = CreateEmissionVolumeIntegrator(ParamSet());
     gSppParam = samplerParams.FindOneInt("pixelsamples", 4);
     Primitive *accel = CreateBVHAccelerator(primitives, accelParams);
@@ -537,7 +553,8 @@ static void usage() {
     fprintf(stderr, "usage: harness scene.pbrt [--res W H] [--spp N] [--maxdepth D] [--seed S]\n"
                     "   [--window x0 x1 y0 y1] [--raw film.f32] [--dat film.dat] [--paths paths.bin]\n"
                     "   [--path-every K] [--kat-mt out.bin] [--spectra out.bin] [--tris out.bin]\n"
-                    "   [--keys keys.i32 (with --paths)] [--refdat film.dat] [--gpupath]\n");
+                    "   [--keys keys.i32 (with --paths)] [--refdat film.dat] [--gpupath]\n"
+                    "   [--surf path|directlighting|scene] [--dl-strategy all|one]\n");
     exit(1);
 }
 
@@ -565,6 +582,8 @@ int main(int argc, char **argv) {
         else if (a == "--keys") keysIn = argv[++i];
         else if (a == "--refdat") refDat = argv[++i];
         else if (a == "--gpupath") gpupath = true;
+        else if (a == "--surf") surfOv = argv[++i];
+        else if (a == "--dl-strategy") dlStrategyOv = argv[++i];
         else usage();
     }
     Options opt; opt.quiet = true;
@@ -645,7 +664,11 @@ int main(int argc, char **argv) {
     int xs, xe, ys, ye;
     gFilm->GetSampleExtent(&xs, &xe, &ys, &ye);
     if (win[0] >= 0) { xs = max(xs, win[0]); xe = min(xe, win[1]); ys = max(ys, win[2]); ye = min(ye, win[3]); }
-    Sample *smp = new Sample(NULL, gSurf, gVol, gScene);
+    // the renderer's sampler only sizes the request here (LDSampler::RoundSize rounds a
+    // DirectLighting light's nSamples to a power of two, directlighting.cpp:51); the sample
+    // values come from FillSample
+    LDSampler sizer(xs, xe, ys, ye, spp, gCamera->shutterOpen, gCamera->shutterClose);
+    Sample *smp = new Sample(&sizer, gSurf, gVol, gScene);
     HarnessRenderer renderer(gSurf, gVol);
     gSurf->Preprocess(gScene, gCamera, &renderer);
     gVol->Preprocess(gScene, gCamera, &renderer);

@@ -1039,6 +1039,10 @@ int pbrtgpu_scene_upload(pbrtgpu_ctx *c, const pbrtgpu_flat_scene *s) {
     if (s->max_depth < 0 || s->max_depth > 20)
         return fail(PBRTGPU_E_UNSUPPORTED, "maxdepth > 20 exceeds the first MT19937 block (DESIGN.md §3.1)");
     if (s->n_nodes <= 0 || s->n_prims <= 0) return fail(PBRTGPU_E_INVALID, "empty scene");
+    if (s->integrator != PBRTGPU_INTEGRATOR_PATH && s->integrator != PBRTGPU_INTEGRATOR_DIRECT)
+        return fail(PBRTGPU_E_INVALID, "unknown SurfaceIntegrator");
+    if (s->integrator == PBRTGPU_INTEGRATOR_DIRECT && s->dl_strategy != PBRTGPU_DL_ALL && s->dl_strategy != PBRTGPU_DL_ONE)
+        return fail(PBRTGPU_E_INVALID, "unknown DirectLighting strategy");
     for (int i = 0; i < s->n_lights; ++i)
         if (s->lights[i].type < PBRTGPU_LIGHT_AREA || s->lights[i].type > PBRTGPU_LIGHT_INFINITE)
             return fail(PBRTGPU_E_INVALID, "bad light type");

@@ -28,6 +28,7 @@ int pbrthost_load(const char *path, const pbrthost_overrides *ov, pbrthost_scene
         if (ov) {
             o.xres = ov->xres; o.yres = ov->yres; o.spp = ov->spp; o.maxdepth = ov->maxdepth;
             o.bands = ov->bands > 0 ? ov->bands : 32; o.seed = ov->seed;
+            o.integrator = ov->integrator; o.dl_strategy = ov->dl_strategy;
         }
         ok = LoadPbrtScene(p, o, s, &e);
     }
@@ -42,6 +43,8 @@ int pbrthost_load(const char *path, const pbrthost_overrides *ov, pbrthost_scene
         if (ov->spp > 0) { uint32_t v = ov->spp; v--; v |= v >> 1; v |= v >> 2; v |= v >> 4; v |= v >> 8; v |= v >> 16; s->spp = v + 1; }
         if (ov->maxdepth >= 0) s->maxDepth = ov->maxdepth;
         if (ov->seed != PBRTHOST_KEEP_SEED) s->seed = ov->seed;
+        if (ov->integrator >= 0) s->integrator = ov->integrator;
+        if (ov->dl_strategy >= 0) s->dlStrategy = ov->dl_strategy;
     }
     *out = reinterpret_cast<pbrthost_scene *>(s);
     return 0;

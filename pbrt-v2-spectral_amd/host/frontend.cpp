@@ -547,6 +547,7 @@ private:
     std::map<Xform, std::pair<Xform, Xform> > tcache;   // key compares m only (first wins)
     float tStart = 0.f, tEnd = 1.f;
     ParamSet filmParams, cameraParams, samplerParams, surfParams, accelParams;
+    std::string surfName = "directlighting";   // RenderOptions::SurfIntegratorName default (api.cpp:222)
     std::string cameraName = "perspective";
     TransformSet cameraToWorld;
     std::vector<std::shared_ptr<LightObj> > lights;
@@ -709,7 +710,7 @@ private:
             else if (d == "Film") { Str(); filmParams = Params(); }
             else if (d == "Sampler") { Str(); samplerParams = Params(); }
             else if (d == "Accelerator") { Str(); accelParams = Params(); }
-            else if (d == "SurfaceIntegrator") { Str(); surfParams = Params(); }
+            else if (d == "SurfaceIntegrator") { surfName = Str(); surfParams = Params(); }
             else if (d == "VolumeIntegrator") { Str(); Params(); }
             else if (d == "Renderer") { Str(); Params(); }
             else if (d == "Camera") {
@@ -1200,6 +1201,8 @@ private:
         } else
             throw std::runtime_error("light '" + name + "' is not supported by this build yet");
         lo->l.is_black = SpecIsBlack(lo->L);
+        // Light::nSamples (light.h:45): point lights take none, infinite "nsamples" (infinite.cpp:181)
+        lo->l.n_samples = std::max(1, name == "point" ? 1 : p.FindOneInt("nsamples", 1));
         lights.push_back(lo);
     }
     // ShapeSet (light.cpp:114-135): refine with a LIFO todo list
@@ -1328,6 +1331,7 @@ private:
             Spec sc = gs.areaLightParams.FindOneSpectrum("scale", spec.Const(1.0f));
             alo->L = SpecMul(L, sc);
             alo->l.is_black = SpecIsBlack(alo->L);
+            alo->l.n_samples = std::max(1, gs.areaLightParams.FindOneInt("nsamples", 1));   // diffuse.cpp:55
             ShapeSetOf(shape, &alo->shapeSet);
             Xform l2w = curT.t[0];
             memcpy(alo->l.l2w_m, l2w.m.m, 64); memcpy(alo->l.l2w_minv, l2w.mInv.m, 64);
@@ -1547,6 +1551,16 @@ private:
         ComputeCamera(cp, xres, yres, &out->camera);
         // ---- integrator / sampler
         out->maxDepth = ov.maxdepth >= 0 ? ov.maxdepth : surfParams.FindOneInt("maxdepth", 5);
+        // SurfaceIntegrator (api.cpp:551-583): "path" or "directlighting" (strategy "all" / "one",
+        // unknown strategies -> "all" with a warning, directlighting.cpp:115-125); others are
+        // rejected rather than rendered as something else
+        if (ov.integrator >= 0) out->integrator = ov.integrator;
+        else if (surfName == "path") out->integrator = PBRTGPU_INTEGRATOR_PATH;
+        else if (surfName == "directlighting") out->integrator = PBRTGPU_INTEGRATOR_DIRECT;
+        else throw std::runtime_error("SurfaceIntegrator '" + surfName + "' is not supported by this build");
+        std::string st = surfParams.FindOneString("strategy", "all");
+        if (st != "all" && st != "one") out->warnings.push_back("Strategy \"" + st + "\" for direct lighting unknown");
+        out->dlStrategy = ov.dl_strategy >= 0 ? ov.dl_strategy : (st == "one" ? PBRTGPU_DL_ONE : PBRTGPU_DL_ALL);
         int nsamp = ov.spp > 0 ? ov.spp : samplerParams.FindOneInt("pixelsamples", 4);
         out->spp = (int)RoundUpPow2((uint32_t)nsamp);
         out->seed = ov.seed == 0xffffffffu ? 0u : ov.seed;   // PBRTHOST_KEEP_SEED
@@ -1732,6 +1746,8 @@ void HostScene::Flat(pbrtgpu_flat_scene *f) const {
     f->rgb_basis = rgbBasis.empty() ? nullptr : rgbBasis.data();
     f->n_merl_floats = (int)merl.size();
     f->merl = merl.empty() ? nullptr : merl.data();
+    f->integrator = integrator;
+    f->dl_strategy = dlStrategy;
 }
 
 }  // namespace pbrtamd

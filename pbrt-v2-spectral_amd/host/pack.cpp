@@ -47,6 +47,8 @@ bool SavePack(const HostScene &s, const std::string &path, std::string *err) {
          WArr(f, s.lights) && WArr(f, s.lightShapes) && WArr(f, s.spectra) && WArr(f, s.instances) &&
          WArr(f, s.primInstance) && WArr(f, s.kdnodes) && WArr(f, s.textures) && WArr(f, s.ewaLut) &&
          WArr(f, s.rgbBasis) && WArr(f, s.merl);
+    int32_t integ[2] = {s.integrator, s.dlStrategy};
+    ok = ok && W(f, integ, 8);
     ok = (gzclose(f) == Z_OK) && ok;
     if (!ok && err) *err = "write error on " + path;
     return ok;
@@ -68,7 +70,13 @@ bool LoadPack(const std::string &path, HostScene *s, std::string *err) {
          RArr(f, s->primInstance) && RArr(f, s->kdnodes) && RArr(f, s->textures) && RArr(f, s->ewaLut) &&
          RArr(f, s->rgbBasis);
     s->merl.clear();
-    if (ok && ver >= 6) ok = RArr(f, s->merl);
+    s->integrator = 0;   // packs before v6: the configs' "path" 
+    s->dlStrategy = 0;
+    if (ok && ver >= 6) {
+        int32_t integ[2];
+        ok = RArr(f, s->merl) && R(f, integ, 8);
+        if (ok) { s->integrator = integ[0]; s->dlStrategy = integ[1]; }
+    }
     gzclose(f);
     if (!ok && err) *err = "bad or truncated scene pack " + path;
     return ok;

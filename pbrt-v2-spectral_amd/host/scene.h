@@ -15,6 +15,8 @@ struct RenderOverrides {
     int maxdepth = -1;            // SurfaceIntegrator "path" maxdepth
     int bands = 32;               // nSpectralSamples (32 = reference build, 60 = C4 variant)
     uint32_t seed = 0;
+    int integrator = -1;          // PBRTGPU_INTEGRATOR_* to force, -1: the scene's SurfaceIntegrator
+    int dl_strategy = -1;         // PBRTGPU_DL_* to force, -1: the scene's "strategy"
 };
 
 // Resolution-independent camera description (perspective.cpp:110-147 parameters); the
@@ -58,6 +60,8 @@ struct HostScene {
     std::vector<float> ewaLut;                // [128] MIPMap::weightLut
     std::vector<float> rgbBasis;              // [14][nBands] FromRGB basis spectra
     std::vector<float> merl;                  // RegularHalfangleBRDF RGB tables (pbrtgpu_flat_scene::merl)
+    int integrator = 0;                       // PBRTGPU_INTEGRATOR_* (packs older than v6: path)
+    int dlStrategy = 0;                       // PBRTGPU_DL_*
     // diagnostics
     std::vector<std::string> warnings;
     int bvhMaxDepth = 0;

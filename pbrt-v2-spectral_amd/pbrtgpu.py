@@ -59,12 +59,16 @@ class FlatScene(ctypes.Structure):
                 ("n_instances", I32), ("instances", P), ("prim_instance", P),
                 ("n_kdnodes", I32), ("kdnodes", P),
                 ("n_textures", I32), ("textures", P), ("ewa_lut", P), ("rgb_basis", P),
-                ("n_merl_floats", I32), ("merl", P)]
+                ("n_merl_floats", I32), ("merl", P), ("integrator", I32), ("dl_strategy", I32)]
 
 
 class Overrides(ctypes.Structure):
     _fields_ = [("xres", I32), ("yres", I32), ("spp", I32), ("maxdepth", I32), ("bands", I32),
-                ("seed", ctypes.c_uint32)]
+                ("seed", ctypes.c_uint32), ("integrator", I32), ("dl_strategy", I32)]
+
+
+INTEGRATORS = {"path": 0, "directlighting": 1}
+DL_STRATEGIES = {"all": 0, "one": 1}
 
 
 class RenderDesc(ctypes.Structure):
@@ -182,11 +186,15 @@ class Scene:
         host_lib().pbrthost_flat(self._h, ctypes.byref(self.flat))
 
     @staticmethod
-    def load(path, xres=-1, yres=-1, spp=-1, maxdepth=-1, bands=0, seed=None):
-        """bands <= 0: the pack's own band count, or 32 (the reference build) for a .pbrt file."""
+    def load(path, xres=-1, yres=-1, spp=-1, maxdepth=-1, bands=0, seed=None, integrator=None, strategy=None):
+        """bands <= 0: the pack's own band count, or 32 (the reference build) for a .pbrt file.
+        integrator / strategy: None keeps the scene's SurfaceIntegrator ("path" or
+        "directlighting") and DirectLighting "strategy" ("all" or "one")."""
         h = P()
         err = ctypes.create_string_buffer(1024)
-        ov = Overrides(xres, yres, spp, maxdepth, bands, KEEP_SEED if seed is None else seed)
+        ov = Overrides(xres, yres, spp, maxdepth, bands, KEEP_SEED if seed is None else seed,
+                       -1 if integrator is None else INTEGRATORS[integrator],
+                       -1 if strategy is None else DL_STRATEGIES[strategy])
         if host_lib().pbrthost_load(path.encode(), ctypes.byref(ov), ctypes.byref(h), err, 1024) != 0:
             raise RuntimeError("scene load failed: %s" % err.value.decode())
         return Scene(h)

@@ -130,3 +130,37 @@ def test_regular_halfangle_brdf_bit_exact_vs_reference(pg, ora_libm, merl_dir, n
     else:
         film, _ = ora_libm.render(scene, threads=8)
         assert np.array_equal(film.view(np.int32), g["film"].view(np.int32))
+
+
+DL = ["killeroo_dl_%s_48x40s4", "bunny_dl_%s_48x27s4", "anim_dl_%s_40x40s4", "coverage_dl_%s_64x48s4",
+      "coverage_dlone_%s_64x48s4"]
+
+
+def dl_scene(pg, g, name):
+    """The pack of a DirectLightingIntegrator fixture, rendered with the integrator the scene
+    files name (packs record "path", the configs' override)."""
+    w, h, spp, seed, md = [int(v) for v in g["config"]]
+    pack = {"anim": "anim-killeroos-moving.pack", "bunny": "bunny.pack", "coverage": "coverage.pack"}.get(
+        name.split("_")[0], "killeroo-simple.pack")
+    return pg.Scene.load(os.path.join(PACKS, pack), xres=w, yres=h, spp=spp, maxdepth=md, seed=seed,
+                         integrator="directlighting", strategy="one" if "_dlone_" in name else "all")
+
+
+@pytest.mark.parametrize("name", [d % "paths" for d in DL])
+def test_direct_lighting_paths_bit_exact_vs_reference(pg, ora_libm, name):
+    """DirectLightingIntegrator (directlighting.cpp:73-109; UniformSampleAllLights /
+    UniformSampleOneLight, integrator.cpp:39-106; SpecularReflect / SpecularTransmit with ray
+    differentials, integrator.cpp:169-250): the oracle against the reference harness."""
+    g = np.load(os.path.join(GOLDEN, name + ".npz"))
+    scene = dl_scene(pg, g, name)
+    assert scene.flat.integrator == pg.INTEGRATORS["directlighting"]
+    L = ora_libm.trace_paths(scene, g["keys"])
+    same = np.all(L.view(np.int32) == g["L"].view(np.int32), axis=1)
+    assert same.all(), "paths differing: %d / %d" % ((~same).sum(), len(same))
+
+
+@pytest.mark.parametrize("name", [d % "film" for d in DL])
+def test_direct_lighting_film_bit_exact_vs_reference(pg, ora_libm, name):
+    g = np.load(os.path.join(GOLDEN, name + ".npz"))
+    film, _ = ora_libm.render(dl_scene(pg, g, name), threads=8)
+    assert np.array_equal(film.view(np.int32), g["film"].view(np.int32))

@@ -34,6 +34,11 @@ Fixtures (numpy .npz, inputs + expected outputs only):
                                   (measured.cpp:131-175, reflection.cpp:267-300) from the synthetic
                                   MERL table of tools/make_merl.py, plus a measured material whose
                                   .merl file is missing (no BxDF)
+  *_dl_paths_*, *_dl_film_*, coverage_dlone_*   DirectLightingIntegrator (directlighting.cpp, with
+                                  UniformSampleAll/OneLight and the specular recursion of
+                                  integrator.cpp:169-250): killeroo (strategy all, light nsamples 8),
+                                  bunny, anim, and the coverage scene (mirror / glass recursion,
+                                  textures) with strategies all and one
   killeroo_dat_40x32s4.npz        the raw film of the restatement film AND the .dat the
                                   reference's own SpectralImageNoCameraFilm wrote for the same
                                   samples (--refdat): pins AddSample and the WriteImage payload
@@ -64,20 +69,20 @@ def read_paths(fn):
     return rec[:, :3].copy(), rec[:, 3:].copy().view(np.float32), int(spp), int(seed)
 
 
-def paths_fixture(name, res, spp, seed, maxdepth, every, tmp, scene="killeroo-simple.pbrt", bands=32):
+def paths_fixture(name, res, spp, seed, maxdepth, every, tmp, scene="killeroo-simple.pbrt", bands=32, extra=()):
     fn = os.path.join(tmp, name + ".bin")
     run([os.path.join(SCENES, scene), "--res", str(res[0]), str(res[1]), "--spp", str(spp), "--seed", str(seed), "--maxdepth",
-         str(maxdepth), "--paths", fn, "--path-every", str(every)], bands)
+         str(maxdepth), "--paths", fn, "--path-every", str(every)] + list(extra), bands)
     keys, L, _, _ = read_paths(fn)
     np.savez_compressed(os.path.join(OUT, name + ".npz"), keys=keys, L=L,
                         config=np.array([res[0], res[1], spp, seed, maxdepth], np.int32))
     print(name, keys.shape)
 
 
-def film_fixture(name, res, spp, seed, maxdepth, tmp, scene="killeroo-simple.pbrt", bands=32):
+def film_fixture(name, res, spp, seed, maxdepth, tmp, scene="killeroo-simple.pbrt", bands=32, extra=()):
     fn = os.path.join(tmp, name + ".f32")
     run([os.path.join(SCENES, scene), "--res", str(res[0]), str(res[1]), "--spp", str(spp), "--seed", str(seed), "--maxdepth",
-         str(maxdepth), "--raw", fn], bands)
+         str(maxdepth), "--raw", fn] + list(extra), bands)
     raw = np.fromfile(fn, dtype=np.int32)
     W, H, N = raw[:3]
     film = raw[3:].view(np.float32).reshape(H, W, N)
@@ -130,6 +135,28 @@ def dat_fixture(name, res, spp, tmp, scene="killeroo-simple.pbrt"):
     print(name, film.shape, os.path.getsize(dat))
 
 
+# DirectLightingIntegrator (the integrator the packaged scene files name): (fixture stem, scene,
+# res, spp, maxdepth, path stride, harness extra args).  Python loads the matching pack with
+# integrator="directlighting" (and strategy="one" for the dlone fixtures).
+DL_FIXTURES = [
+    ("killeroo_dl", "killeroo-simple.pbrt", (48, 40), 4, 5, 2, ()),            # strategy all, nsamples 8
+    ("bunny_dl", "bunny.pbrt", (48, 27), 4, 5, 2, ()),                        # point + disk (nsamples 4)
+    ("anim_dl", "anim-killeroos-moving.pbrt", (40, 40), 4, 5, 2, ()),         # instances, motion blur
+    ("coverage_dl", "COVERAGE", (64, 48), 4, 6, 1, ()),                       # mirror / glass recursion, textures
+    ("coverage_dlone", "COVERAGE", (64, 48), 4, 6, 1, ("--dl-strategy", "one")),
+]
+
+
+def dl_fixtures(tmp):
+    for stem, scene, res, spp, md, every, extra in DL_FIXTURES:
+        if scene == "COVERAGE":
+            scene = os.path.join(ROOT, "tests", "scenes", "coverage.pbrt")
+        ex = ("--surf", "directlighting") + tuple(extra)
+        tag = "%dx%ds%d" % (res[0], res[1], spp)
+        paths_fixture("%s_paths_%s" % (stem, tag), res, spp, 0, md, every, tmp, scene=scene, extra=ex)
+        film_fixture("%s_film_%s" % (stem, tag), res, spp, 0, md, tmp, scene=scene, extra=ex)
+
+
 def merl_fixtures(tmp):
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     import make_merl
@@ -156,6 +183,8 @@ def main():
                 dat_fixture("killeroo_dat_40x32s4", (40, 32), 4, tmp)
             elif only == "merl":
                 merl_fixtures(tmp)
+            elif only == "dl":
+                dl_fixtures(tmp)
         return
     with tempfile.TemporaryDirectory() as tmp:
         paths_fixture("killeroo_paths_64x64s4", (64, 64), 4, 0, 5, 5, tmp)
@@ -183,6 +212,7 @@ def main():
                 keys_fixture(*cfg, tmp)
         dat_fixture("killeroo_dat_40x32s4", (40, 32), 4, tmp)
         merl_fixtures(tmp)
+        dl_fixtures(tmp)
         fn = os.path.join(tmp, "mt.bin")
         run(["-", "--kat-mt", fn])
         raw = np.fromfile(fn, dtype=np.uint32).reshape(6, 65)

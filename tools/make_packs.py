@@ -27,8 +27,10 @@ def main():
     out = os.path.join(ROOT, "scenes")
     os.makedirs(out, exist_ok=True)
     for name, fn, bands, xr, yr, spp in PACKS:
+        # the configs render with "path" (SURVEY App. B); load a pack with integrator="directlighting"
+        # to render it with the DirectLightingIntegrator the scene files name
         s = pg.Scene.load(os.path.join(REF, fn), xres=xr, yres=yr, spp=spp, maxdepth=-1 if name == "coverage" else 5,
-                          bands=bands)
+                          bands=bands, integrator="path")
         path = os.path.join(out, name + ".pack")
         s.save_pack(path)
         print(name, s.info(), os.path.getsize(path))
