@@ -266,6 +266,8 @@ struct DevScene {
     const float *basis;               // [14][nbp] FromRGB basis spectra, band-quad padded
     int nbp;                          // padded band count (multiple of 4)
     int nInf;                         // infinite lights among lights[]
+    int integrator, dlStrategy;       // PBRTGPU_INTEGRATOR_*, PBRTGPU_DL_*
+    int dlK;                          // DirectLighting light samples per vertex (sum of RoundUpPow2(nSamples))
 };
 
 // scene features a shade kernel is specialised for (k_shade<NB, FEAT>): a scene without
@@ -1528,8 +1530,11 @@ PGD_INLINE float4 tex_spec4(const DevScene &S, const SpecTex &t, int q) {
 // offset rays; out = dudx, dvdx, dudy, dvdy
 struct RayDiff { V rxo, rxd, ryo, ryd; };
 PGD_INLINE float vcomp(V a, int i) { return i == 0 ? a.x : (i == 1 ? a.y : a.z); }
-PGD_HEAVY void compute_differentials(const DG &dg, const RayDiff &rd, float out[4]) {
+// dpdx / dpdy (optional) = px - p, py - p, zero where the reference leaves them zero
+PGD_HEAVY void compute_differentials(const DG &dg, const RayDiff &rd, float out[4], V *dpdx = nullptr,
+                                     V *dpdy = nullptr) {
     out[0] = out[1] = out[2] = out[3] = 0.f;
+    if (dpdx) { *dpdx = v3(0.f, 0.f, 0.f); *dpdy = v3(0.f, 0.f, 0.f); }
     float d = -vdot(dg.nn, dg.p);
     float tx = -(vdot(dg.nn, rd.rxo) + d) / vdot(dg.nn, rd.rxd);
     if (isnan(tx)) return;
@@ -1537,6 +1542,7 @@ PGD_HEAVY void compute_differentials(const DG &dg, const RayDiff &rd, float out[
     float ty = -(vdot(dg.nn, rd.ryo) + d) / vdot(dg.nn, rd.ryd);
     if (isnan(ty)) return;
     V py = vadd(rd.ryo, vmul(rd.ryd, ty));
+    if (dpdx) { *dpdx = vsub(px, dg.p); *dpdy = vsub(py, dg.p); }
     int a0, a1;
     if (fabsf(dg.nn.x) > fabsf(dg.nn.y) && fabsf(dg.nn.x) > fabsf(dg.nn.z)) { a0 = 1; a1 = 2; }
     else if (fabsf(dg.nn.y) > fabsf(dg.nn.z)) { a0 = 0; a1 = 2; }
@@ -1552,9 +1558,11 @@ PGD_HEAVY void compute_differentials(const DG &dg, const RayDiff &rd, float out[
 // diff: dudx, dvdx, dudy, dvdy of the hit (zero without ray differentials); the material's
 // textured spectrum, if any, is written clamped into the slot's K bands (kb[q * c]) and its
 // BxDF refers to it with offset -1
+// dnOut (optional): dndu, dndv of the shading geometry (SpecularReflect / SpecularTransmit ray
+// differentials, integrator.cpp:190-192)
 template <int FEAT>
 PGD_HEAVY void get_bsdf(const DevScene &S, const Isect &is, const float diff[4], float4 *kb, size_t c, BSDF &bs,
-                        V *pOut, V *nOut) {
+                        V *pOut, V *nOut, V *dnOut = nullptr) {
     const pbrtgpu_prim pr = S.prims[is.prim];
     const pbrtgpu_material &mt = S.mats[pr.material];
     DG dgs;
@@ -1607,6 +1615,7 @@ PGD_HEAVY void get_bsdf(const DevScene &S, const Isect &is, const float diff[4],
     bs.n = 0;
     *pOut = dgs.p;
     *nOut = nn;
+    if (dnOut) { dnOut[0] = dgs.dndu; dnOut[1] = dgs.dndv; }
     // material spectra: constant offsets, or the textured slot materialised in K
     int off[4];
     bool black0 = (mt.black_mask & 1) != 0, black1 = (mt.black_mask & 2) != 0;

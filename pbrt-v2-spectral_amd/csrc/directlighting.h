@@ -1,0 +1,421 @@
+// directlighting.h -- DirectLightingIntegrator::Li (directlighting.cpp:73-109) as a wavefront
+// shading step: k_shade<NB, FEAT, DL = true> calls shade_slot_dl once per live slot and pass.
+//
+// The reference recurses: a vertex adds its emission and its direct light (strategy "all":
+// UniformSampleAllLights, integrator.cpp:39-71, RoundUpPow2(nSamples) samples per light;
+// "one": UniformSampleOneLight, integrator.cpp:74-106), then, while depth + 1 < maxDepth,
+// SpecularReflect and SpecularTransmit (integrator.cpp:169-250) trace a child ray each and add
+// (f * Li_child) * |wi . n| / pdf.  Here a slot keeps that recursion as an explicit stack of
+// frames in HBM (PathSoA::f*, frame d = the vertex at ray depth d) and advances it one ray
+// round trip per pass:
+//   - a light sample of the top vertex queues its shadow / MIS rays (estimate_direct, the
+//     path integrator's EstimateDirect) and the next pass adds (0 [+ A]) [+ B] to the sums;
+//   - a specular child queues its continuation ray; the pass that receives its hit pushes a
+//     frame, the pass that completes the child pops it into the parent.
+// Every other step (several zero-contribution light samples, a child that misses, a chain of
+// completed frames) is done within one pass.  The vertex's BSDF is rebuilt from the frame's
+// incoming ray whenever a pass needs it (isect_fill + get_bsdf are pure functions of the ray,
+// the hit and the differentials).  The specular samples draw BSDFSample(rng) from the path's
+// MT19937 stream in the reference's order (reflect, its subtree, transmit).
+#pragma once
+#include "wavefront.h"
+
+namespace pgd {
+
+template <int NB> PGD_INLINE float4 *dl_L(const PathSoA &P, int d, int slot) {
+    return P.fL + (size_t)d * Bands<NB>::NQ * P.cap + slot;
+}
+template <int NB> PGD_INLINE float4 *dl_F(const PathSoA &P, int d, int slot) {
+    return P.fF + (size_t)d * Bands<NB>::NQ * P.cap + slot;
+}
+PGD_INLINE void dl_vec_store(float *b, size_t c, V v) { b[0] = v.x; b[c] = v.y; b[2 * c] = v.z; }
+PGD_INLINE V dl_vec_load(const float *b, size_t c) { return v3(b[0], b[c], b[2 * c]); }
+
+// RoundUpPow2(max(1, nSamples)) samples of light i (directlighting.cpp:53-55)
+PGD_INLINE int dl_count(const DevScene &S, int i) {
+    uint32_t v = (uint32_t)max(1, S.lights[i].n_samples) - 1u;
+    v |= v >> 1; v |= v >> 2; v |= v >> 4; v |= v >> 8; v |= v >> 16;
+    return (int)(v + 1u);
+}
+
+// strategy "all": light-sample k of a vertex is sample j of light i (of n)
+PGD_INLINE void dl_cursor(const DevScene &S, int k, int *i, int *j, int *n) {
+    int li = 0, jj = k, nn = dl_count(S, 0);
+    while (jj >= nn) { jj -= nn; ++li; nn = dl_count(S, li); }
+    *i = li; *j = jj; *n = nn;
+}
+
+// sample values of light-sample k of a vertex (DirectLightingIntegrator::RequestSamples,
+// directlighting.cpp:46-70 + the emission integrator's two 1D values): "all": per light i 1D
+// [lightComp 2i, bsdfComp 2i+1], 2D [lightPos 2i, bsdfDir 2i+1], RoundUpPow2(nSamples) values
+// each (value j of a count-n slot = sample s * n + j of a length spp * n sequence); "one":
+// 1D [lightComp 0, lightNum 1, bsdfComp 2], 2D [lightPos 0, bsdfDir 1].  Returns the light.
+PGD_INLINE int dl_sample(const DevScene &S, uint32_t hp, uint32_t s, int k, float ul[3], float ub[3], int *jOut,
+                         int *nsOut) {
+    const uint32_t spp = (uint32_t)S.spp;
+    float u2[2];
+    if (S.dlStrategy == PBRTGPU_DL_ONE) {
+        const uint32_t n1 = 5u;
+        const float ulnum = s1d(hp, 3u + 1u, s, spp);
+        s2d(hp, 3u + n1 + 0u, s, spp, u2); ul[0] = u2[0]; ul[1] = u2[1];
+        ul[2] = s1d(hp, 3u + 0u, s, spp);
+        s2d(hp, 3u + n1 + 1u, s, spp, u2); ub[0] = u2[0]; ub[1] = u2[1];
+        ub[2] = s1d(hp, 3u + 2u, s, spp);
+        int ln = (int)floorf(ulnum * S.nLights);
+        if (ln > S.nLights - 1) ln = S.nLights - 1;
+        *jOut = 0; *nsOut = 1;
+        return ln;
+    }
+    const uint32_t n1 = 2u * (uint32_t)S.nLights + 2u;
+    int i, j, n;
+    dl_cursor(S, k, &i, &j, &n);
+    const uint32_t kk = s * (uint32_t)n + (uint32_t)j, len = spp * (uint32_t)n;
+    s2d(hp, 3u + n1 + 2u * i, kk, len, u2); ul[0] = u2[0]; ul[1] = u2[1];
+    ul[2] = s1d(hp, 3u + 2u * i, kk, len);
+    s2d(hp, 3u + n1 + 2u * i + 1u, kk, len, u2); ub[0] = u2[0]; ub[1] = u2[1];
+    ub[2] = s1d(hp, 3u + 2u * i + 1u, kk, len);
+    *jOut = j; *nsOut = n;
+    return i;
+}
+
+// the top vertex rebuilt from its frame: intersection, differentials, BSDF
+struct DLVertex {
+    Ray ray;
+    RayDiff rd;
+    Isect is;
+    BSDF bs;
+    V p, n, wo, dpdx, dpdy, dn[2];
+    float diff[4];
+};
+template <int NB, int FEAT>
+PGD_INLINE void dl_vertex(const DevScene &S, const PathSoA &P, int slot, int d, DLVertex &v) {
+    const size_t c = P.cap;
+    const float *fr = P.fRay + (size_t)d * 9 * c + slot;
+    v.ray.o = dl_vec_load(fr, c);
+    v.ray.d = dl_vec_load(fr + 3 * c, c);
+    v.ray.mint = fr[6 * c]; v.ray.maxt = fr[7 * c]; v.ray.time = fr[8 * c];
+    const int prim = P.fHit[(size_t)2 * d * c + slot];
+    const float t = __int_as_float(P.fHit[(size_t)(2 * d + 1) * c + slot]);
+    isect_fill(S, v.ray, prim, t, v.is, inst_rec(P, slot));
+    if (d == 0) {   // the camera ray's differentials are re-derived from its sample
+        const uint32_t hp = P.hp[slot], s = P.smp[slot], spp = (uint32_t)S.spp, pxy = P.pix[slot];
+        float u[2], lens[2];
+        s2d(hp, 0, s, spp, u);
+        s2d(hp, 1, s, spp, lens);
+        const float timeU = s1d(hp, 2, s, spp);
+        v.rd = camera_diff(S.cam, S.spp, (int)(pxy & 0xffffu) + u[0], (int)(pxy >> 16) + u[1], lens[0], lens[1], timeU);
+    } else {
+        const float *fd = P.fDiff + (size_t)d * 12 * c + slot;
+        v.rd.rxo = dl_vec_load(fd, c);
+        v.rd.rxd = dl_vec_load(fd + 3 * c, c);
+        v.rd.ryo = dl_vec_load(fd + 6 * c, c);
+        v.rd.ryd = dl_vec_load(fd + 9 * c, c);
+    }
+    compute_differentials(v.is.dg, v.rd, v.diff, &v.dpdx, &v.dpdy);
+    get_bsdf<FEAT>(S, v.is, v.diff, P.K + slot, c, v.bs, &v.p, &v.n, v.dn);
+    v.wo = vneg(v.ray.d);
+}
+
+// k_shade body of the DirectLighting integrator for one slot (see the file comment).
+// Returns the ray requests; *done when the camera sample's radiance is in Lout.
+template <int NB, int FEAT>
+PGD_INLINE Pushes shade_slot_dl(const DevScene &S, const PathSoA &P, int slot, float *__restrict__ Lout, bool *done,
+                                bool *zeroed) {
+    constexpr int NQ = Bands<NB>::NQ;
+    const size_t c = P.cap;
+    const float *sp = S.spectra;
+    uint32_t fl = P.flags[slot];
+    int d = P.bounce[slot];   // depth of the top frame (-1: camera ray in flight)
+    Pushes out = {false, false, false};
+    *done = false;
+    *zeroed = false;
+    const int nLights = S.nLights;
+    const bool all = S.dlStrategy != PBRTGPU_DL_ONE;
+    const int K = all ? S.dlK : 1;
+    const uint32_t hp = P.hp[slot], s = P.smp[slot];
+    float4 *La = P.beta + slot, *Ld = P.beta + (size_t)NQ * c + slot;   // UniformSampleAllLights sums
+    int k = (int)P.dlk[slot];
+    DLVertex vx;
+    bool have = false;   // vx holds the top frame's vertex
+    MT rng;
+    bool rngLoaded = false;
+    float4 Lr[NQ];       // radiance of a completed frame, handed to its parent (pop)
+    // stage: 1 light sample k of the top vertex, 2 its specular branches, 3 pop Lr
+    int stage;
+#ifdef PGD_DL_TRACE_ITEM   // debugging aid: the step of one item per pass
+    const bool trc = P.item[slot] == PGD_DL_TRACE_ITEM;
+    if (trc) printf("[dl] slot %d d %d fl %x k %d K %d prim %d occ %u hitM %d\n", slot, d, fl, k, K, P.hitPrim[slot],
+                    P.occ[slot], P.hitPrim[c + slot]);
+#endif
+    if (fl & PF_PEND) {
+        // ---- the answered light sample k: ED = (0 [+ A]) [+ B] (EstimateDirect)
+        const bool useA = (fl & PF_PA) && !P.occ[slot];
+        bool useB = false;
+        const int ln = (int)(fl >> PF_LIGHT_SHIFT);
+        if (fl & PF_PB) {
+            const int mp = P.hitPrim[c + slot];
+            if ((FEAT & FEAT_INF) && S.lights[ln].type == PBRTGPU_LIGHT_INFINITE) useB = mp < 0;
+            else if (mp >= 0 && S.prims[mp].area_light == ln) {
+                const Ray mr = ray_load(P, RAY_M, slot);
+                useB = vdot(isect_nn(S, mr, mp, P.hitT[c + slot], inst_rec(P, slot)), vneg(mr.d)) > 0.f;
+            }
+        }
+        fl &= ~(PF_PEND | PF_PA | PF_PB | (PF_LIGHT_MASK << PF_LIGHT_SHIFT));
+        const float4 *A = A_of<NB>(P, 0, slot), *B = B_of<NB>(P, 0, slot);
+        int li = 0, j = 0, ns = 1;
+        if (all) dl_cursor(S, k, &li, &j, &ns);
+        float4 *Lv = dl_L<NB>(P, d, slot);
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            const float4 a = useA ? A[q * c] : make_float4(0.f, 0.f, 0.f, 0.f);
+            const float4 bb = useB ? B[q * c] : make_float4(0.f, 0.f, 0.f, 0.f);
+            float4 ed;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                float e = 0.f;
+                if (useA) e += cmp(a, i);
+                if (useB) e += cmp(bb, i);
+                cmp(ed, i) = e;
+            }
+            if (!all) {   // L += UniformSampleOneLight = ED * nLights
+                float4 l = Lv[q * c];
+                const float nl = (float)nLights;
+                l.x += ed.x * nl; l.y += ed.y * nl; l.z += ed.z * nl; l.w += ed.w * nl;
+                Lv[q * c] = l;
+            } else {      // Ld += ED; after the light's last sample La += Ld / ns
+                float4 ld = j == 0 ? make_float4(0.f, 0.f, 0.f, 0.f) : Ld[q * c];
+                ld.x += ed.x; ld.y += ed.y; ld.z += ed.z; ld.w += ed.w;
+                if (j == ns - 1) {
+                    float4 la = k + 1 == ns ? make_float4(0.f, 0.f, 0.f, 0.f) : La[q * c];   // first light
+                    const float fn = (float)ns;
+                    la.x += ld.x / fn; la.y += ld.y / fn; la.z += ld.z / fn; la.w += ld.w / fn;
+                    La[q * c] = la;
+                } else Ld[q * c] = ld;
+            }
+        }
+        ++k;
+        stage = k < K ? 1 : 2;
+        if (stage == 2 && all) {   // L += La
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                float4 l = Lv[q * c];
+                const float4 la = La[q * c];
+                l.x += la.x; l.y += la.y; l.z += la.z; l.w += la.w;
+                Lv[q * c] = l;
+            }
+        }
+    } else {
+        // ---- the camera ray or a specular child ray was answered (PF_CONT)
+        fl &= ~PF_CONT;
+        const int prim = P.hitPrim[slot];
+        const Ray ray = ray_load(P, RAY_C, slot);
+        if (prim < 0) {
+            // SamplerRenderer::Li (samplerrenderer.cpp:237-240): Li = sum of the lights' Le
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) Lr[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if ((FEAT & FEAT_INF) && S.nInf > 0)
+                for (int l = 0; l < nLights; ++l)
+                    if (S.lights[l].type == PBRTGPU_LIGHT_INFINITE) {
+                        const Emit e = inf_Le(S.lights[l], ray.d);
+#pragma unroll
+                        for (int q = 0; q < NQ; ++q) {
+                            const float4 v = emit4<FEAT>(S, e, q);
+                            Lr[q].x += v.x; Lr[q].y += v.y; Lr[q].z += v.z; Lr[q].w += v.w;
+                        }
+                    }
+            d = d + 1;   // the missing ray's frame, popped at once
+            stage = 3;
+        } else {
+            // push frame d + 1: its incoming ray and hit; L = 0 + Le(wo)
+            d = d + 1;
+            float *fr = P.fRay + (size_t)d * 9 * c + slot;
+            dl_vec_store(fr, c, ray.o);
+            dl_vec_store(fr + 3 * c, c, ray.d);
+            fr[6 * c] = ray.mint; fr[7 * c] = ray.maxt; fr[8 * c] = ray.time;
+            P.fHit[(size_t)2 * d * c + slot] = prim;
+            P.fHit[(size_t)(2 * d + 1) * c + slot] = __float_as_int(P.hitT[slot]);
+            P.fBr[(size_t)d * c + slot] = 0u;
+            k = 0;
+            dl_vertex<NB, FEAT>(S, P, slot, d, vx);
+            have = true;
+            const int al = S.prims[vx.is.prim].area_light;
+            const int eo = (al >= 0 && vdot(vx.is.dg.nn, vx.wo) > 0.f) ? S.lights[al].spec : -1;   // AreaLight::L
+            float4 *Lv = dl_L<NB>(P, d, slot);
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                const float4 e = eo >= 0 ? ld4(sp + eo + 4 * q) : make_float4(0.f, 0.f, 0.f, 0.f);
+                Lv[q * c] = make_float4(0.f + e.x, 0.f + e.y, 0.f + e.z, 0.f + e.w);
+            }
+            stage = nLights > 0 ? 1 : 2;
+        }
+    }
+    for (;;) {
+        if (stage == 1) {
+            // ---- light sample k of the top vertex
+            if (!have) { dl_vertex<NB, FEAT>(S, P, slot, d, vx); have = true; }
+            float ul[3], ub[3];
+            int j, ns;
+            const int ln = dl_sample(S, hp, s, k, ul, ub, &j, &ns);
+            PowMemo pm;
+            FVal F;
+            estimate_direct<NB, FEAT>(S, P, slot, 0, ln, vx.bs, pm, vx.p, vx.n, vx.wo, vx.is.rayEps, vx.ray.time, ul, ub,
+                                      F, fl, out);
+            if (fl & (PF_PA | PF_PB)) break;   // the next pass adds ED
+            // nothing queued: ED = 0, added now
+            fl &= ~(PF_PEND | (PF_LIGHT_MASK << PF_LIGHT_SHIFT));
+            float4 *Lv = dl_L<NB>(P, d, slot);
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                if (!all) {
+                    float4 l = Lv[q * c];
+                    const float z = 0.f * (float)nLights;
+                    l.x += z; l.y += z; l.z += z; l.w += z;
+                    Lv[q * c] = l;
+                } else {
+                    float4 ld = j == 0 ? make_float4(0.f, 0.f, 0.f, 0.f) : Ld[q * c];
+                    ld.x += 0.f; ld.y += 0.f; ld.z += 0.f; ld.w += 0.f;
+                    if (j == ns - 1) {
+                        float4 la = k + 1 == ns ? make_float4(0.f, 0.f, 0.f, 0.f) : La[q * c];
+                        const float fn = (float)ns;
+                        la.x += ld.x / fn; la.y += ld.y / fn; la.z += ld.z / fn; la.w += ld.w / fn;
+                        La[q * c] = la;
+                    } else Ld[q * c] = ld;
+                }
+            }
+            ++k;
+            if (k < K) continue;
+            if (all) {
+#pragma unroll
+                for (int q = 0; q < NQ; ++q) {
+                    float4 l = Lv[q * c];
+                    const float4 la = La[q * c];
+                    l.x += la.x; l.y += la.y; l.z += la.z; l.w += la.w;
+                    Lv[q * c] = l;
+                }
+            }
+            stage = 2;
+        }
+        if (stage == 2) {
+            // ---- SpecularReflect, then SpecularTransmit (integrator.cpp:169-250)
+            uint32_t br = P.fBr[(size_t)d * c + slot];
+            bool spawned = false;
+            while (d + 1 < S.maxDepth && br < 2u) {
+                if (!have) { dl_vertex<NB, FEAT>(S, P, slot, d, vx); have = true; }
+                if (!rngLoaded) {
+                    mt_load(P, slot, fl, rng);
+                    if (!rng.init) mt_init(rng);
+                    rngLoaded = true;
+                }
+                const float u0 = mt_float(rng), u1 = mt_float(rng), uc = mt_float(rng);   // BSDFSample(rng)
+                const bool refl = br == 0u;
+                ++br;
+                const int flags = BSDF_SPECULAR | (refl ? BSDF_REFLECTION : BSDF_TRANSMISSION);
+                PowMemo pm;
+                FVal F;
+                V wi;
+                float pdf;
+                int st;
+                bsdf_sample_f(pm, vx.bs, vx.wo, &wi, u0, u1, uc, &pdf, flags, &st, F);
+                const float ad = fabsf(vdot(wi, vx.n));
+                if (!(pdf > 0.f) || ad == 0.f || (F.mode == FV_SUM && F.n == 0)) continue;
+                float4 *mb = P.M + slot, *kb = P.K + slot;
+                fval_prepare<NB, FEAT>(S, F, mb, c);
+                float4 *Fo = dl_F<NB>(P, d, slot);
+                bool black = true;
+#pragma unroll
+                for (int q = 0; q < NQ; ++q) {
+                    const float4 f = fval4<FEAT>(sp, F, q, mb, kb, c);
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+                        if (4 * q + i < NB) black = black && (cmp(f, i) == 0.);
+                    Fo[q * c] = f;
+                }
+                if (black) continue;
+                P.fS[(size_t)2 * d * c + slot] = ad;
+                P.fS[(size_t)(2 * d + 1) * c + slot] = pdf;
+                // the child ray and its differentials (the camera's rays always carry them)
+                Ray cr;
+                cr.o = vx.p; cr.d = wi; cr.mint = vx.is.rayEps; cr.maxt = INFINITY; cr.time = vx.ray.time;
+                ray_store(P, RAY_C, slot, cr);
+                const V n = vx.n, wo = vx.wo;
+                const V rxo = vadd(vx.p, vx.dpdx), ryo = vadd(vx.p, vx.dpdy);
+                const V dndx = vadd(vmul(vx.dn[0], vx.diff[0]), vmul(vx.dn[1], vx.diff[1]));
+                const V dndy = vadd(vmul(vx.dn[0], vx.diff[2]), vmul(vx.dn[1], vx.diff[3]));
+                const V dwodx = vsub(vneg(vx.rd.rxd), wo), dwody = vsub(vneg(vx.rd.ryd), wo);
+                const float dDNdx = vdot(dwodx, n) + vdot(wo, dndx);
+                const float dDNdy = vdot(dwody, n) + vdot(wo, dndy);
+                V rxd, ryd;
+                if (refl) {
+                    const float won = vdot(wo, n);
+                    rxd = vadd(vsub(wi, dwodx), vmul(vadd(vmul(dndx, won), vmul(n, dDNdx)), 2.f));
+                    ryd = vadd(vsub(wi, dwody), vmul(vadd(vmul(dndy, won), vmul(n, dDNdy)), 2.f));
+                } else {
+                    // BSDF::eta: the glass material's index, 1 otherwise (glass.cpp:48)
+                    const pbrtgpu_material &mt = S.mats[S.prims[vx.is.prim].material];
+                    float eta = mt.type == PBRTGPU_MAT_GLASS ? mt.f[0] : 1.f;
+                    const V w = vneg(wo);
+                    if (vdot(wo, n) < 0) eta = 1.f / eta;
+                    const float mu = eta * vdot(w, n) - vdot(wi, n);
+                    const float dmudx = (eta - (eta * eta * vdot(w, n)) / vdot(wi, n)) * dDNdx;
+                    const float dmudy = (eta - (eta * eta * vdot(w, n)) / vdot(wi, n)) * dDNdy;
+                    rxd = vsub(vadd(wi, vmul(dwodx, eta)), vadd(vmul(dndx, mu), vmul(n, dmudx)));
+                    ryd = vsub(vadd(wi, vmul(dwody, eta)), vadd(vmul(dndy, mu), vmul(n, dmudy)));
+                }
+                float *fd = P.fDiff + (size_t)(d + 1) * 12 * c + slot;
+                dl_vec_store(fd, c, rxo);
+                dl_vec_store(fd + 3 * c, c, rxd);
+                dl_vec_store(fd + 6 * c, c, ryo);
+                dl_vec_store(fd + 9 * c, c, ryd);
+                fl |= PF_CONT;
+                out.c = true;
+                spawned = true;
+                break;
+            }
+            P.fBr[(size_t)d * c + slot] = br;
+            if (spawned) break;
+            // the frame is complete: Li = (1 * L) + 0 goes to the parent
+            const float4 *Lv = dl_L<NB>(P, d, slot);
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) Lr[q] = Lv[q * c];
+            stage = 3;
+        }
+        // ---- pop frame d with raw radiance Lr
+        if (d == 0) {
+            *zeroed = path_output<NB>(S, Lr, Lout, P.item[slot]);   // rayWeight * ((1 * L) + 0), guarded
+            *done = true;
+            break;
+        }
+        --d;
+        have = false;
+        {
+            float4 *Lv = dl_L<NB>(P, d, slot);
+            const float4 *Fo = dl_F<NB>(P, d, slot);
+            const float ad = P.fS[(size_t)2 * d * c + slot], pdf = P.fS[(size_t)(2 * d + 1) * c + slot];
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                float4 l = Lv[q * c];
+                const float4 f = Fo[q * c];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const float li = (1.f * cmp(Lr[q], i)) + 0.f;
+                    cmp(l, i) += ((cmp(f, i) * li) * ad) / pdf;
+                }
+                Lv[q * c] = l;
+            }
+        }
+        stage = 2;
+    }
+    if (rngLoaded) {
+        mt_store(P, slot, rng);
+        if (rng.init) fl |= PF_MTINIT;
+    }
+#ifdef PGD_DL_TRACE_ITEM
+    if (trc) printf("[dl]   -> d %d fl %x k %d push %d%d%d done %d\n", d, fl, k, out.c, out.m, out.s, *done);
+#endif
+    P.bounce[slot] = d;
+    P.dlk[slot] = (uint32_t)k;
+    P.flags[slot] = fl;
+    return out;
+}
+
+}  // namespace pgd

@@ -636,7 +636,7 @@ struct Timing {
 struct Lane {
     DevBuf slots;            // PathSoA storage
     DevBuf spill;            // k_trace_pt stack spill areas (closest, shadow)
-    int slotCap = 0, slotNb = 0, slotInst = 0;
+    int slotCap = 0, slotNb = 0, slotInst = 0, slotFrames = 0;
     PathSoA P{};
     hipStream_t s = nullptr, s2 = nullptr;
     hipEvent_t ev[2 + 6 * 8] = {};
@@ -703,8 +703,10 @@ static bool serial_mode() {
     return e && atoi(e) != 0;
 }
 
-static int ensure_slots(Lane *c, int cap, int NB, int nInst) {
-    if (c->slotCap == cap && c->slotNb == NB && c->slotInst == nInst) return 0;
+// DirectLighting frame bytes per slot and frame (PathSoA::f*)
+static size_t frame_bytes(int NB) { return (size_t)8 * ((NB + 3) / 4 * 4) + 104; }
+static int ensure_slots(Lane *c, int cap, int NB, int nInst, int nFrames) {
+    if (c->slotCap == cap && c->slotNb == NB && c->slotInst == nInst && c->slotFrames == nFrames) return 0;
     const size_t C = (size_t)cap;
     const int NBP = (NB + 3) / 4 * 4;   // bands padded to whole float4 quads
     size_t off = 0;
@@ -713,6 +715,9 @@ static int ensure_slots(Lane *c, int cap, int NB, int nInst) {
            oMt = take(C * 20), oBeta = take(C * 3 * NBP * 4), oL = take(C * NBP * 4), oA = take(C * 2 * NBP * 4),
            oB = take(C * 2 * NBP * 4), oM = take(C * NBP * 4), oK = take(C * NBP * 4), oPix = take(C * 4), oRay = take(C * 27 * 4), oHitP = take(C * 8), oHitT = take(C * 8), oOcc = take(C * 4),
            oQC = take(C * 16), oQS = take(C * 8), oCnt = take(CNT_WORDS * 4), oInst = take(C * (size_t)nInst * 128);
+    const size_t F = (size_t)nFrames;
+    size_t oFL = take(C * F * NBP * 4), oFF = take(C * F * NBP * 4), oFRay = take(C * F * 36), oFDiff = take(C * F * 48),
+           oFS = take(C * F * 8), oFHit = take(C * F * 8), oFBr = take(C * F * 4), oDlk = take(nFrames ? C * 4 : 0);
     HIPCHK(c->slots.ensure(off));
     char *base = (char *)c->slots.p;
     PathSoA &P = c->P;
@@ -726,6 +731,16 @@ static int ensure_slots(Lane *c, int cap, int NB, int nInst) {
     P.cnt = (uint32_t *)(base + oCnt);
     P.nInst = nInst;
     P.instM = nInst ? (float4 *)(base + oInst) : nullptr;
+    P.nFrames = nFrames;
+    P.fL = nFrames ? (float4 *)(base + oFL) : nullptr;
+    P.fF = nFrames ? (float4 *)(base + oFF) : nullptr;
+    P.fRay = nFrames ? (float *)(base + oFRay) : nullptr;
+    P.fDiff = nFrames ? (float *)(base + oFDiff) : nullptr;
+    P.fS = nFrames ? (float *)(base + oFS) : nullptr;
+    P.fHit = nFrames ? (int *)(base + oFHit) : nullptr;
+    P.fBr = nFrames ? (uint32_t *)(base + oFBr) : nullptr;
+    P.dlk = nFrames ? (uint32_t *)(base + oDlk) : nullptr;
+    c->slotFrames = nFrames;
     c->slotCap = cap;
     c->slotNb = NB;
     c->slotInst = nInst;
@@ -768,7 +783,14 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
     const size_t spillLane = (size_t)std::max(ptGrid, ptGridS) * kTraceBlock * c->stackDepth;   // uint2 per kernel
     // scenes without measured BRDFs, textures and environment lights run the variant with
     // that code compiled out (fewer registers, no kd-tree stack)
-    auto kShade = c->feat ? launch_shade<NB, FEAT_ALL> : launch_shade<NB, 0>;
+    // the DirectLighting integrator has its own step (all features compiled in)
+    const bool dl = c->S.integrator == PBRTGPU_INTEGRATOR_DIRECT;
+    auto kShade = dl ? launch_shade_dl<NB> : c->feat ? launch_shade<NB, FEAT_ALL> : launch_shade<NB, 0>;
+    const int nFrames = dl ? std::max(1, c->S.maxDepth) : 0;
+    // passes one path can take: the camera ray + maxdepth + 1 vertices + 1 finish (path); per
+    // vertex of the DirectLighting recursion (at most 2^maxdepth - 1) its hit + one pass per
+    // light sample, + the output
+    const int64_t pathPasses = dl ? (((int64_t)1 << nFrames) - 1) * (c->S.dlK + 1) + 2 : c->S.maxDepth + 3;
     struct Run { Lane *L; ItemSrc src; int cap, grid, q, batch, passes, maxPasses; bool done; };
     Run R[kLanes];
     const bool serial = serial_mode();
@@ -783,17 +805,19 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
         r.src.base = src.base + lo;
         r.src.nItems = hi - lo;
         r.cap = (int)std::min<uint32_t>(r.src.nItems, (uint32_t)std::max(64, slot_target() / nl));
+        if (dl)   // the frame stacks: at most 16 GiB per lane
+            r.cap = (int)std::max<size_t>(64, std::min<size_t>((size_t)r.cap, ((size_t)16 << 30) / (frame_bytes(NB) * nFrames)));
         r.grid = (r.cap + kShadeBlock - 1) / kShadeBlock;
         r.q = 0;
         r.batch = 0;
         r.done = false;
-        // drain bound of this run: a path lives at most maxDepth + 3 passes (camera ray,
-        // maxDepth + 1 vertices, the finish of the last one), so every slot takes a new item
-        // at least once per maxDepth + 3 passes while items remain; twice that, plus the
-        // overshoot of one enqueued batch, means the wavefront is stuck
+        // drain bound of this run: a path lives at most pathPasses passes, so every slot
+        // takes a new item at least once per pathPasses passes while items remain; twice
+        // that, plus the overshoot of one enqueued batch, means the wavefront is stuck
         r.passes = 0;
-        r.maxPasses = 2 * (int)((r.src.nItems + r.cap - 1) / r.cap + 1) * (c->S.maxDepth + 3) + 2 * kPassBatch;
-        if (int e = ensure_slots(&L, r.cap, NB, c->S.nInsts)) return e;
+        r.maxPasses = (int)std::min<int64_t>(INT32_MAX / 2, 2 * ((r.src.nItems + r.cap - 1) / r.cap + 1) * pathPasses) +
+                      2 * kPassBatch;
+        if (int e = ensure_slots(&L, r.cap, NB, c->S.nInsts, nFrames)) return e;
         HIPCHK(L.spill.ensure(2 * spillLane * sizeof(uint2)));
         if (l > 0) HIPCHK(hipStreamWaitEvent(L.s, c->ev[0], 0));
         HIPCHK(hipMemsetAsync(L.P.item, 0xff, (size_t)r.cap * 4, L.s));
@@ -1043,6 +1067,10 @@ int pbrtgpu_scene_upload(pbrtgpu_ctx *c, const pbrtgpu_flat_scene *s) {
         return fail(PBRTGPU_E_INVALID, "unknown SurfaceIntegrator");
     if (s->integrator == PBRTGPU_INTEGRATOR_DIRECT && s->dl_strategy != PBRTGPU_DL_ALL && s->dl_strategy != PBRTGPU_DL_ONE)
         return fail(PBRTGPU_E_INVALID, "unknown DirectLighting strategy");
+    // DirectLighting draws 6 MT19937 values at each of up to 2^(maxdepth-1) - 1 specular
+    // vertices; the device stream covers the first 227
+    if (s->integrator == PBRTGPU_INTEGRATOR_DIRECT && s->max_depth > 6)
+        return fail(PBRTGPU_E_UNSUPPORTED, "DirectLighting maxdepth > 6 exceeds the first MT19937 block");
     for (int i = 0; i < s->n_lights; ++i)
         if (s->lights[i].type < PBRTGPU_LIGHT_AREA || s->lights[i].type > PBRTGPU_LIGHT_INFINITE)
             return fail(PBRTGPU_E_INVALID, "bad light type");
@@ -1095,6 +1123,15 @@ int pbrtgpu_scene_upload(pbrtgpu_ctx *c, const pbrtgpu_flat_scene *s) {
     S.yint = s->y_int;
     S.cam = s->camera;
     S.nLights = s->n_lights;
+    S.integrator = s->integrator;
+    S.dlStrategy = s->dl_strategy;
+    S.dlK = 0;
+    for (int i = 0; i < s->n_lights; ++i) {   // RoundUpPow2(max(1, nSamples)) per light
+        uint32_t v = (uint32_t)std::max(1, s->lights[i].n_samples) - 1u;
+        v |= v >> 1; v |= v >> 2; v |= v >> 4; v |= v >> 8; v |= v >> 16;
+        if (v + 1u > (1u << 16)) return fail(PBRTGPU_E_UNSUPPORTED, "light nsamples > 65536");
+        S.dlK += (int)(v + 1u);
+    }
     // BVH: verify topology and measure the stack depth traversal needs (top level, plus the
     // deepest nested instance BVH whose walk stacks above it)
     if (s->n_instances < 0 || (s->n_instances > 0 && (!s->instances || !s->prim_instance)))

@@ -6,9 +6,13 @@
 #include "pbrtgpu.h"
 #include "device.h"
 #include "wavefront.h"
+#include "directlighting.h"
 
 #if !defined(SHADE_NB) || !defined(SHADE_FEAT)
-#error "compile with -DSHADE_NB=<30|32|60> -DSHADE_FEAT=<0|7>"
+#error "compile with -DSHADE_NB=<30|32|60> -DSHADE_FEAT=<0|7> [-DSHADE_DL=1]"
+#endif
+#ifndef SHADE_DL
+#define SHADE_DL 0
 #endif
 
 namespace pgd {
@@ -18,6 +22,7 @@ namespace pgd {
 #define PGD_CAT2(a, b, c) a##b##_##c
 #define PGD_CAT(a, b, c) PGD_CAT2(a, b, c)
 static __device__ unsigned long long pgd_sec_total[8 * SEC_N * 16];
+#if !SHADE_DL
 extern "C" int PGD_CAT(pgd_sections_read_, SHADE_NB, SHADE_FEAT)(unsigned long long *out, int reset) {
     unsigned long long h[8 * SEC_N * 16];
     if (hipMemcpyFromSymbol(h, HIP_SYMBOL(pgd_sec_total), sizeof(h)) != hipSuccess) return -1;
@@ -29,6 +34,7 @@ extern "C" int PGD_CAT(pgd_sections_read_, SHADE_NB, SHADE_FEAT)(unsigned long l
     }
     return 0;
 }
+#endif
 #endif
 
 // Block-wide exclusive prefix of a per-thread flag with ONE atomicAdd per block on
@@ -56,10 +62,18 @@ __device__ __forceinline__ uint32_t block_push(bool flag, uint32_t *counter, uin
 // occupancy target: 3 waves/SIMD (<= 168 VGPRs) for <= 32 bands costs a few spilled
 // registers and beats the unconstrained 200-VGPR / 2-wave build (C2 shade 372 -> 335
 // ms/frame, r01l ablation; 4 waves spills ~90 registers and loses); 60 bands: 2 waves
+// The DirectLighting step is left unconstrained: forced to 3 waves it spills ~1400 VGPRs and
+// gave non-deterministic radiance on coverage.pbrt (tools/dbg/dl_debug4.py); unconstrained
+// (1 wave/SIMD, 32 spills) it is bit-exact and deterministic
 #ifndef PGD_SHADE_ATTR
+#if SHADE_DL
+#define PGD_SHADE_ATTR
+#else
 #define PGD_SHADE_ATTR __attribute__((amdgpu_waves_per_eu(SHADE_NB > 32 ? 2 : 3, SHADE_NB > 32 ? 2 : 3)))
 #endif
-template <int NB, int FEAT>
+#endif
+// DL: the DirectLightingIntegrator's step (directlighting.h) instead of PathIntegrator's
+template <int NB, int FEAT, bool DL>
 __global__ __launch_bounds__(kShadeBlock) PGD_SHADE_ATTR void k_shade(DevScene S, PathSoA P, ItemSrc src, int qout,
                                                        float *__restrict__ Lout) {
     __shared__ uint32_t lds4[16];
@@ -75,7 +89,8 @@ __global__ __launch_bounds__(kShadeBlock) PGD_SHADE_ATTR void k_shade(DevScene S
     bool zeroed = false;
     if (inRange && !freeSlot) {
         bool done;
-        pu = shade_slot<NB, FEAT>(S, P, slot, Lout, &done, &zeroed);
+        if (DL) pu = shade_slot_dl<NB, FEAT>(S, P, slot, Lout, &done, &zeroed);
+        else pu = shade_slot<NB, FEAT>(S, P, slot, Lout, &done, &zeroed);
         if (done) { P.item[slot] = -1; freeSlot = true; }
     }
     if (__ballot(zeroed)) {
@@ -104,14 +119,29 @@ __global__ __launch_bounds__(kShadeBlock) PGD_SHADE_ATTR void k_shade(DevScene S
 #endif
 }
 
+template <int NB, int FEAT, bool DL>
+static hipError_t launch(int grid, hipStream_t stream, const DevScene &S, const PathSoA &P, const ItemSrc &src, int qout,
+                         float *Lout) {
+    const size_t lds = ((FEAT & FEAT_MEAS) && S.kdInLds) ? (size_t)S.nKd * 32 : 0;
+    hipLaunchKernelGGL((k_shade<NB, FEAT, DL>), dim3(grid), dim3(kShadeBlock), lds, stream, S, P, src, qout, Lout);
+    return hipGetLastError();
+}
+#if SHADE_DL
+template <int NB>
+hipError_t launch_shade_dl(int grid, hipStream_t stream, const DevScene &S, const PathSoA &P, const ItemSrc &src,
+                           int qout, float *Lout) {
+    return launch<NB, SHADE_FEAT, true>(grid, stream, S, P, src, qout, Lout);
+}
+template hipError_t launch_shade_dl<SHADE_NB>(int, hipStream_t, const DevScene &, const PathSoA &, const ItemSrc &, int,
+                                              float *);
+#else
 template <int NB, int FEAT>
 hipError_t launch_shade(int grid, hipStream_t stream, const DevScene &S, const PathSoA &P, const ItemSrc &src, int qout,
                         float *Lout) {
-    const size_t lds = ((FEAT & FEAT_MEAS) && S.kdInLds) ? (size_t)S.nKd * 32 : 0;
-    hipLaunchKernelGGL((k_shade<NB, FEAT>), dim3(grid), dim3(kShadeBlock), lds, stream, S, P, src, qout, Lout);
-    return hipGetLastError();
+    return launch<NB, FEAT, false>(grid, stream, S, P, src, qout, Lout);
 }
 template hipError_t launch_shade<SHADE_NB, SHADE_FEAT>(int, hipStream_t, const DevScene &, const PathSoA &,
                                                        const ItemSrc &, int, float *);
+#endif
 
 }  // namespace pgd

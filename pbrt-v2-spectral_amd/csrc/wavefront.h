@@ -85,6 +85,17 @@ struct PathSoA {
     uint32_t *cnt;      // counters (CNT_*), work counters as u64 from word CNT_WORK
     float4 *instM;      // [cap][nInst][8]: the path's instance transforms (inst_load), or null
     int nInst;
+    // DirectLightingIntegrator only (null for the path integrator): the slot's stack of the
+    // SpecularReflect / SpecularTransmit recursion, frame d = the vertex at ray depth d
+    int nFrames;
+    float4 *fL;         // [nFrames][NQ][cap]: the vertex's radiance so far
+    float4 *fF;         // [nFrames][NQ][cap]: BSDF value of its pending specular child
+    float *fRay;        // [nFrames][9][cap]: its incoming ray
+    float *fDiff;       // [nFrames][12][cap]: that ray's differentials rxo, rxd, ryo, ryd (depth >= 1)
+    float *fS;          // [nFrames][2][cap]: |wi . n| and pdf of the pending child
+    int *fHit;          // [nFrames][2][cap]: hit primitive, hit t (bits) of the incoming ray
+    uint32_t *fBr;      // [nFrames][cap]: specular branches tried (0, 1 reflect, 2 transmit)
+    uint32_t *dlk;      // [cap]: light-sample cursor of the top vertex
 };
 // the path's instance-transform record (null without instances)
 PGD_INLINE const float4 *inst_rec(const PathSoA &P, int slot) {
@@ -478,6 +489,116 @@ struct LAdds {
     bool zero;      // L += beta * (nLights * 0)
 };
 
+// EstimateDirect (integrator.cpp:109-166) of light lightNum at a vertex (point p, shading
+// normal n, BSDF bs): the light-sample term goes to A_vb with its shadow ray (PF_PA), the
+// BSDF-sample term with MIS to B_vb with its MIS ray (PF_PB); the caller adds (0 [+ A]) [+ B]
+// when the rays are answered.  Sets PF_PEND and the light index in fl.
+template <int NB, int FEAT>
+PGD_INLINE void estimate_direct(const DevScene &S, const PathSoA &P, int slot, int vb, int lightNum, const BSDF &bs,
+                                PowMemo &pm, V p, V n, V wo, float rayEps, float time, const float ul[3],
+                                const float ub[3], FVal &F, uint32_t &fl, Pushes &out) {
+    constexpr int NQ = Bands<NB>::NQ;
+    const size_t c = P.cap;
+    const float *sp = S.spectra;
+    float4 *mb = P.M + slot, *kb = P.K + slot;
+    PGD_T0(LIGHT);
+    const pbrtgpu_light &Lt = S.lights[lightNum];
+    const int flags = BSDF_ALL & ~BSDF_SPECULAR;
+    fl |= PF_PEND | ((uint32_t)lightNum << PF_LIGHT_SHIFT);
+    // ---- light sample -> A (added if the shadow ray is unoccluded)
+    V wi;
+    float lightPdf, bsdfPdf;
+    Seg vis;
+    Emit em;
+    light_sample_L<FEAT>(S, Lt, p, rayEps, ul, &wi, &lightPdf, &vis, &em);
+    if (lightPdf > 0. && !emit_black<NB, FEAT>(S, em)) {
+        bsdf_f(pm, bs, wo, wi, flags, F);
+        fval_prepare<NB, FEAT>(S, F, mb, c);
+        float sc;
+        if (em.point) sc = fabsf(vdot(wi, n)) / lightPdf;
+        else {
+            bsdfPdf = bsdf_pdf(pm, bs, wo, wi, flags);
+            float weight = power_heuristic(lightPdf, bsdfPdf);
+            sc = fabsf(vdot(wi, n)) * weight / lightPdf;
+        }
+        // A_i = (f_i * Li_i) * sc ; written while testing f for black (A unused if black)
+        float4 *A = A_of<NB>(P, vb, slot);
+        bool black = true;
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            float4 f = fval4<FEAT>(sp, F, q, mb, kb, c), e = emit4<FEAT>(S, em, q), a;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                cmp(a, k) = (cmp(f, k) * cmp(e, k)) * sc;
+                if (4 * q + k < NB) black = black && (cmp(f, k) == 0.);
+            }
+            A[q * c] = a;
+        }
+        if (!black) {
+            Ray sr;
+            sr.o = vis.o; sr.d = vis.d; sr.mint = vis.mint; sr.maxt = vis.maxt; sr.time = time;
+            ray_store(P, RAY_S, slot, sr);
+            fl |= PF_PA;
+            out.s = true;
+        }
+    }
+    PGD_T1(LIGHT);
+    PGD_T0(MIS);
+    // ---- BSDF sample with MIS -> B (added if the MIS ray reaches this light: hits it
+    // facing, for an area light; escapes the scene, for the environment)
+#ifdef PGD_EXPERIMENT_NO_MIS   // timing experiment only: the MIS section's cost (wrong radiance)
+    if (false) {
+#else
+    if (!em.point) {
+#endif
+        int sampledType;
+        BSDFSampleState sst;
+        bool keep = bsdf_sample_dir(pm, bs, wo, &wi, ub[0], ub[1], ub[2], &bsdfPdf, flags, &sampledType, F, sst);
+        Ray mr;
+        mr.o = p; mr.d = wi; mr.mint = rayEps; mr.maxt = INFINITY; mr.time = time;
+        // a direction whose MIS ray cannot reach the light contributes nothing (B unused)
+        if (keep) keep = mis_may_reach<FEAT>(S, Lt, mr);
+        if (keep) bsdf_sample_rest(pm, bs, wo, wi, sst, &bsdfPdf, flags, sampledType, F);
+        if (keep && bsdfPdf > 0. && !(F.mode == FV_SUM && F.n == 0)) {
+            fval_prepare<NB, FEAT>(S, F, mb, c);
+            float weight = 1.f;
+            bool go = true;
+            if (!(sampledType & BSDF_SPECULAR)) {
+                lightPdf = light_pdf<FEAT>(S, Lt, p, wi);
+                if (lightPdf == 0.) go = false;
+                else weight = power_heuristic(bsdfPdf, lightPdf);
+            }
+            Emit eb;
+            if ((FEAT & FEAT_INF) && Lt.type == PBRTGPU_LIGHT_INFINITE) {
+                if (go) eb = inf_Le(Lt, wi);
+            } else {
+                eb.mode = Lt.is_black ? EM_BLACK : EM_POOL; eb.off = Lt.spec; eb.div = 1.f; eb.point = false;
+            }
+            if (go && !emit_black<NB, FEAT>(S, eb)) {
+                const float ad = fabsf(vdot(wi, n));
+                float4 *B = B_of<NB>(P, vb, slot);
+                bool black = true;
+#pragma unroll
+                for (int q = 0; q < NQ; ++q) {
+                    float4 f = fval4<FEAT>(sp, F, q, mb, kb, c), e = emit4<FEAT>(S, eb, q), b;
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        cmp(b, k) = (((cmp(f, k) * cmp(e, k)) * ad) * weight) / bsdfPdf;
+                        if (4 * q + k < NB) black = black && (cmp(f, k) == 0.);
+                    }
+                    B[q * c] = b;
+                }
+                if (!black) {
+                    ray_store(P, RAY_M, slot, mr);
+                    fl |= PF_PB;
+                    out.m = true;
+                }
+            }
+        }
+    }
+    PGD_T1(MIS);
+}
+
 // One vertex of PathIntegrator::Li at bounce `vb` for the path in `slot`, whose
 // continuation ray `ray` hit primitive `prim` at `thit`.  L stays in HBM: the vertex's own
 // additions to L are returned in *la.  beta_vb is beta_of(vb) in HBM.  BSDF values are
@@ -540,7 +661,6 @@ PGD_INLINE Pushes shade_vertex(const DevScene &S, const PathSoA &P, int slot, in
 #else
     if (nLights > 0) {
 #endif
-        PGD_T0(LIGHT);
         float ul[3], ub[3], ulnum;
         if (!useMT) {
             float u2[2];
@@ -556,101 +676,7 @@ PGD_INLINE Pushes shade_vertex(const DevScene &S, const PathSoA &P, int slot, in
         }
         int lightNum = (int)floorf(ulnum * nLights);
         if (lightNum > nLights - 1) lightNum = nLights - 1;
-        const pbrtgpu_light &Lt = S.lights[lightNum];
-        const int flags = BSDF_ALL & ~BSDF_SPECULAR;
-        fl |= PF_PEND | ((uint32_t)lightNum << PF_LIGHT_SHIFT);
-        // ---- light sample -> A (added if the shadow ray is unoccluded)
-        V wi;
-        float lightPdf, bsdfPdf;
-        Seg vis;
-        Emit em;
-        light_sample_L<FEAT>(S, Lt, p, is.rayEps, ul, &wi, &lightPdf, &vis, &em);
-        if (lightPdf > 0. && !emit_black<NB, FEAT>(S, em)) {
-            bsdf_f(pm, bs, wo, wi, flags, F);
-            fval_prepare<NB, FEAT>(S, F, mb, c);
-            float sc;
-            if (em.point) sc = fabsf(vdot(wi, n)) / lightPdf;
-            else {
-                bsdfPdf = bsdf_pdf(pm, bs, wo, wi, flags);
-                float weight = power_heuristic(lightPdf, bsdfPdf);
-                sc = fabsf(vdot(wi, n)) * weight / lightPdf;
-            }
-            // A_i = (f_i * Li_i) * sc ; written while testing f for black (A unused if black)
-            float4 *A = A_of<NB>(P, vb, slot);
-            bool black = true;
-#pragma unroll
-            for (int q = 0; q < NQ; ++q) {
-                float4 f = fval4<FEAT>(sp, F, q, mb, kb, c), e = emit4<FEAT>(S, em, q), a;
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    cmp(a, k) = (cmp(f, k) * cmp(e, k)) * sc;
-                    if (4 * q + k < NB) black = black && (cmp(f, k) == 0.);
-                }
-                A[q * c] = a;
-            }
-            if (!black) {
-                Ray sr;
-                sr.o = vis.o; sr.d = vis.d; sr.mint = vis.mint; sr.maxt = vis.maxt; sr.time = ray.time;
-                ray_store(P, RAY_S, slot, sr);
-                fl |= PF_PA;
-                out.s = true;
-            }
-        }
-        PGD_T1(LIGHT);
-        PGD_T0(MIS);
-        // ---- BSDF sample with MIS -> B (added if the MIS ray reaches this light: hits it
-        // facing, for an area light; escapes the scene, for the environment)
-#ifdef PGD_EXPERIMENT_NO_MIS   // timing experiment only: the MIS section's cost (wrong radiance)
-        if (false) {
-#else
-        if (!em.point) {
-#endif
-            int sampledType;
-            BSDFSampleState sst;
-            bool keep = bsdf_sample_dir(pm, bs, wo, &wi, ub[0], ub[1], ub[2], &bsdfPdf, flags, &sampledType, F, sst);
-            Ray mr;
-            mr.o = p; mr.d = wi; mr.mint = is.rayEps; mr.maxt = INFINITY; mr.time = ray.time;
-            // a direction whose MIS ray cannot reach the light contributes nothing (B unused)
-            if (keep) keep = mis_may_reach<FEAT>(S, Lt, mr);
-            if (keep) bsdf_sample_rest(pm, bs, wo, wi, sst, &bsdfPdf, flags, sampledType, F);
-            if (keep && bsdfPdf > 0. && !(F.mode == FV_SUM && F.n == 0)) {
-                fval_prepare<NB, FEAT>(S, F, mb, c);
-                float weight = 1.f;
-                bool go = true;
-                if (!(sampledType & BSDF_SPECULAR)) {
-                    lightPdf = light_pdf<FEAT>(S, Lt, p, wi);
-                    if (lightPdf == 0.) go = false;
-                    else weight = power_heuristic(bsdfPdf, lightPdf);
-                }
-                Emit eb;
-                if ((FEAT & FEAT_INF) && Lt.type == PBRTGPU_LIGHT_INFINITE) {
-                    if (go) eb = inf_Le(Lt, wi);
-                } else {
-                    eb.mode = Lt.is_black ? EM_BLACK : EM_POOL; eb.off = Lt.spec; eb.div = 1.f; eb.point = false;
-                }
-                if (go && !emit_black<NB, FEAT>(S, eb)) {
-                    const float ad = fabsf(vdot(wi, n));
-                    float4 *B = B_of<NB>(P, vb, slot);
-                    bool black = true;
-#pragma unroll
-                    for (int q = 0; q < NQ; ++q) {
-                        float4 f = fval4<FEAT>(sp, F, q, mb, kb, c), e = emit4<FEAT>(S, eb, q), b;
-#pragma unroll
-                        for (int k = 0; k < 4; ++k) {
-                            cmp(b, k) = (((cmp(f, k) * cmp(e, k)) * ad) * weight) / bsdfPdf;
-                            if (4 * q + k < NB) black = black && (cmp(f, k) == 0.);
-                        }
-                        B[q * c] = b;
-                    }
-                    if (!black) {
-                        ray_store(P, RAY_M, slot, mr);
-                        fl |= PF_PB;
-                        out.m = true;
-                    }
-                }
-            }
-        }
-        PGD_T1(MIS);
+        estimate_direct<NB, FEAT>(S, P, slot, vb, lightNum, bs, pm, p, n, wo, is.rayEps, ray.time, ul, ub, F, fl, out);
         if (!(fl & (PF_PA | PF_PB))) {
             // nothing can add to Ld: finish now (L += beta * (nLights * 0), nLights * 0 == 0)
             la->zero = true;
@@ -877,5 +903,9 @@ static const int kShadeBlock = PGD_SHADE_BLOCK;
 template <int NB, int FEAT>
 hipError_t launch_shade(int grid, hipStream_t stream, const DevScene &S, const PathSoA &P, const ItemSrc &src, int qout,
                         float *Lout);
+// k_shade with the DirectLightingIntegrator step (all features compiled in)
+template <int NB>
+hipError_t launch_shade_dl(int grid, hipStream_t stream, const DevScene &S, const PathSoA &P, const ItemSrc &src,
+                           int qout, float *Lout);
 
 }  // namespace pgd

@@ -345,3 +345,59 @@ def test_regular_halfangle_brdf_vs_reference_golden(pg, merl_dir):
     assert np.abs(film - gf["film"]).max() / np.abs(gf["film"]).max() < 1e-4
     Lo = pg.oracle().trace_paths(scene, g["keys"])
     assert np.all(L.view(np.int32) == Lo.view(np.int32), axis=1).mean() >= 1 - 1e-4
+
+
+DL = ["killeroo_dl_%s_48x40s4", "bunny_dl_%s_48x27s4", "anim_dl_%s_40x40s4", "coverage_dl_%s_64x48s4",
+      "coverage_dlone_%s_64x48s4"]
+
+
+@pytest.mark.parametrize("base", DL)
+def test_direct_lighting_vs_reference_golden(pg, base):
+    """DirectLightingIntegrator on the GPU (directlighting.h: light samples one pass each,
+    SpecularReflect / SpecularTransmit as a per-slot frame stack) against the reference
+    harness's per-path radiance and film, and path by path against the oracle."""
+    from conftest import GOLDEN
+    from test_oracle_golden import dl_scene
+    g = np.load(os.path.join(GOLDEN, base % "paths" + ".npz"))
+    gf = np.load(os.path.join(GOLDEN, base % "film" + ".npz"))
+    scene = dl_scene(pg, g, base % "paths")
+    with pg.Device(0) as d:
+        d.upload(scene)
+        L = d.trace_paths(g["keys"])
+        d.render()
+        film = d.film()
+    ref = g["L"]
+    same = np.all(L.view(np.int32) == ref.view(np.int32), axis=1)
+    rel = np.abs(L - ref).max(axis=1) / np.maximum(np.abs(ref).max(axis=1), 1e-30)
+    # last-ulp transcendental differences (DESIGN.md §3.2): coverage.pbrt samples three lights
+    # per vertex ("all"), so more of its paths meet one (path integrator there: 0.955)
+    assert same.mean() >= (0.90 if base.startswith("coverage") else 0.97), "bit-exact paths %d/%d" % (same.sum(), len(same))
+    assert (rel > 1e-4).mean() <= 5e-4
+    assert np.abs(film - gf["film"]).max() / np.abs(gf["film"]).max() < 1e-4
+    Lo = pg.oracle().trace_paths(scene, g["keys"])
+    assert np.all(L.view(np.int32) == Lo.view(np.int32), axis=1).mean() >= 1 - 1e-4
+
+
+@pytest.mark.parametrize("strategy,md", [("all", 6), ("one", 3)])
+def test_direct_lighting_recursion_and_regeneration(pg, monkeypatch, strategy, md):
+    """Deep specular recursion (coverage.pbrt's glass and mirror, maxdepth up to 6: every
+    vertex may push both children) and a tiny slot pool (many regenerations per slot) give the
+    oracle's radiance; the film does not depend on the slot count."""
+    from conftest import PACKS
+    scene = pg.Scene.load(os.path.join(PACKS, "coverage.pack"), xres=40, yres=30, spp=4, maxdepth=md,
+                          integrator="directlighting", strategy=strategy)
+    keys = _keys(scene)
+    with pg.Device(0) as d:
+        d.upload(scene)
+        L = d.trace_paths(keys)
+        d.render()
+        film = d.film()
+        monkeypatch.setenv("PBRTGPU_SLOTS", "193")
+        Ls = d.trace_paths(keys)
+        d.render()
+        films = d.film()
+    assert np.array_equal(L.view(np.int32), Ls.view(np.int32))
+    assert np.array_equal(film.view(np.int32), films.view(np.int32))
+    Lo = pg.oracle().trace_paths(scene, keys)
+    assert np.all(L.view(np.int32) == Lo.view(np.int32), axis=1).mean() >= 1 - 1e-4
+    assert np.abs(L - Lo).max() / np.abs(Lo).max() < 1e-4

@@ -10,6 +10,7 @@ H="/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=
 pids=()
 for v in 32_0 32_7 60_0 60_7 30_0 30_7; do
   $H "$@" -DSHADE_NB=${v%_*} -DSHADE_FEAT=${v#*_} -c csrc/shade.hip -o $T/s$v.o & pids+=($!)
+  if [ ${v#*_} = 7 ]; then $H "$@" -DSHADE_NB=${v%_*} -DSHADE_FEAT=7 -DSHADE_DL=1 -c csrc/shade.hip -o $T/d$v.o & pids+=($!); fi
 done
 $H "$@" -c csrc/pbrtgpu.hip -o $T/p.o & pids+=($!)
 for p in ${pids[@]}; do wait $p; done
