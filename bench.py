@@ -228,6 +228,9 @@ def main():
     ap.add_argument("--scene", default=None, help="scene pack (default: the config's)")
     ap.add_argument("--res", type=int, default=-1, help="square resolution override (default: the config's)")
     ap.add_argument("--spp", type=int, default=-1, help="spp override (default: the config's)")
+    ap.add_argument("--integrator", choices=["path", "directlighting"], default="path",
+                    help="SurfaceIntegrator (BASELINE configs: path; directlighting = SURVEY §8(f) row)")
+    ap.add_argument("--strategy", choices=["all", "one"], default="all", help="DirectLighting strategy")
     ap.add_argument("--shard", choices=["tiles", "frames"], default="tiles")
     ap.add_argument("--tile", type=int, default=16)
     ap.add_argument("--slices", type=int, default=1, help="tile slices per GPU (single-process --gpus N)")
@@ -254,7 +257,10 @@ def main():
 
     pack, desc = CONFIGS[args.config]
     scene = pg.Scene.load(args.scene or os.path.join(ROOT, "scenes", pack), xres=args.res, yres=args.res,
-                          spp=args.spp, seed=rank if args.shard == "frames" else 0)
+                          spp=args.spp, seed=rank if args.shard == "frames" else 0,
+                          integrator=args.integrator, strategy=args.strategy)
+    if args.integrator != "path":
+        desc = desc.replace("path maxdepth", "directlighting (%s) maxdepth" % args.strategy)
     info = scene.info()
     tile = (args.tile, args.tile)
     ntx, nty = pg.tile_grid(scene, tile)
@@ -315,7 +321,7 @@ def main():
     frame_paths = paths / args.steps    # this rank's share of a frame
     roof = None
     if rank == 0 and not args.no_roofline:
-        roof = exclusive_roofline(dev, scene, tiles, tile, frame_paths, args.config)
+        roof = exclusive_roofline(dev, scene, tiles, tile, frame_paths, args.config if args.integrator == "path" else args.config + "_dl")
 
     cpu = None
     if rank == 0 and n_gpus == 1 and not args.no_cpu:
