@@ -243,6 +243,7 @@ struct DevScene {
     const float4 *nodes;              // 2 x float4 per node (the flattened scene's BVH; roots are tested here)
     const float4 *wnodes;             // child-in-parent BVH: 4 x float4 per interior node (wide_bvh)
     const uint32_t *nodeRef;          // per node: its wide-node index, or a leaf reference (WREF_*)
+    int nTop;                         // wide nodes [0, nTop): the BVH's top levels, breadth-first (LDS in k_trace_pt)
     const pbrtgpu_prim *prims;
     const DevTri *primTri;            // per prim (triangles only meaningful)
     const pbrtgpu_triangle *tris;

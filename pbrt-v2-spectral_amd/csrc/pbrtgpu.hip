@@ -66,7 +66,14 @@ static const int kTraceBlock = PGD_TRACE_BLOCK;
 #ifndef PGD_STACK_LDS
 #define PGD_STACK_LDS 8   // C2: 8 -> closest 161 -> 145 ms/frame vs 16 (r01m ablation)
 #endif
-static const int kStackLDS = PGD_STACK_LDS;   // k_trace_pt: traversal-stack entries per lane kept in LDS (power of two)
+static const int kStackLDS = PGD_STACK_LDS;
+// k_trace_pt: top-level wide nodes held in LDS per block.  Off: measured on C2 (r02k), the
+// top levels are L1/L2-resident already and the LDS tile costs occupancy -- closest-hit
+// 82 ms/frame without, 91 with 128 nodes, 113 with 256
+#ifndef PGD_TOP_NODES
+#define PGD_TOP_NODES 0
+#endif
+static const int kTopNodes = PGD_TOP_NODES;   // k_trace_pt: traversal-stack entries per lane kept in LDS (power of two)
 #ifndef PGD_TRACE_ATTR   // occupancy experiments (tools/build_exp.sh)
 #define PGD_TRACE_ATTR
 #endif
@@ -147,6 +154,12 @@ __global__ __launch_bounds__(kTraceBlock) PGD_TRACE_ATTR void k_trace_pt(DevScen
     // lane: refs, then entry distances), deeper entries in the lane's spill area in HBM
     __shared__ uint32_t sref[kStackLDS * kTraceBlock];
     __shared__ float stm[ANY ? 1 : kStackLDS * kTraceBlock];
+    // the top levels of the BVH (wide nodes [0, S.nTop), breadth-first), once per block
+    __shared__ float4 stop[kTopNodes > 0 ? 4 * kTopNodes : 1];
+    if (kTopNodes > 0) {
+        for (int i = threadIdx.x; i < 4 * S.nTop; i += blockDim.x) stop[i] = S.wnodes[i];
+        __syncthreads();
+    }
     uint2 *gsp = spill + (size_t)(blockIdx.x * blockDim.x + threadIdx.x) * S.stackDepth;
     int bottom = 0;   // entries [0, bottom) live in gsp
     Stack st;         // work counters only
@@ -205,8 +218,14 @@ __global__ __launch_bounds__(kTraceBlock) PGD_TRACE_ATTR void k_trace_pt(DevScen
         if (active) {
             bool done = false, occluded = false;
             if (!(ref & WREF_LEAF)) {
-                const float4 *w = S.wnodes + 4 * (size_t)ref;
-                const float4 l0 = w[0], l1 = w[1], r0 = w[2], r1 = w[3];
+                float4 l0, l1, r0, r1;
+                if (kTopNodes > 0 && ref < (uint32_t)S.nTop) {
+                    const float4 *w = stop + 4 * ref;
+                    l0 = w[0]; l1 = w[1]; r0 = w[2]; r1 = w[3];
+                } else {
+                    const float4 *w = S.wnodes + 4 * (size_t)ref;
+                    l0 = w[0]; l1 = w[1]; r0 = w[2]; r1 = w[3];
+                }
                 st.cNodes++;
                 float tl = 0.f, tr = 0.f;
                 const bool hl = slab_enter(l0, l1, ray, invDir, neg, &tl) && tl < ray.maxt;
@@ -698,6 +717,12 @@ static bool legacy_inst_walk() {
     const char *e = getenv("PBRTGPU_INST_WALK");
     return e && !strcmp(e, "legacy");
 }
+// top-level wide BVH nodes k_trace_pt copies to LDS (PBRTGPU_TOP_NODES: fewer, for tests)
+static int top_nodes() {
+    const char *e = getenv("PBRTGPU_TOP_NODES");
+    const int v = e ? atoi(e) : kTopNodes;
+    return std::max(0, std::min(v, kTopNodes));
+}
 static bool serial_mode() {
     const char *e = getenv("PBRTGPU_SERIAL");
     return e && atoi(e) != 0;
@@ -954,14 +979,30 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
 // reference (wide index or WREF_LEAF record); the roots of the top-level and instance BVHs
 // are looked up there.
 static float bits_f(uint32_t u) { float f; memcpy(&f, &u, 4); return f; }
-static int wide_bvh(const pbrtgpu_flat_scene *s, std::vector<float4> *wn, std::vector<uint32_t> *ref) {
+// Wide indices: the first `top` interior nodes of the top-level BVH in breadth-first order
+// (the top levels, which k_trace_pt keeps in LDS), then every other interior node in the
+// reference's depth-first order.  Indices only name nodes: the traversal order is the same.
+static int wide_bvh(const pbrtgpu_flat_scene *s, int top, std::vector<float4> *wn, std::vector<uint32_t> *ref,
+                    int *nTopOut) {
     const int n = s->n_nodes;
-    ref->assign(n, 0u);
+    ref->assign(n, 0xffffffffu);
     uint32_t nw = 0;
+    if (top > 0 && n > 0 && !(s->nodes[0].meta & 0xff)) {
+        std::vector<int> bfs(1, 0);
+        for (size_t h = 0; h < bfs.size() && (int)nw < top; ++h) {
+            const int i = bfs[h];
+            const pbrtgpu_bvh_node &b = s->nodes[i];
+            if (b.meta & 0xff) continue;
+            (*ref)[i] = nw++;
+            if (i + 1 < n) bfs.push_back(i + 1);
+            if (b.offset < (uint32_t)n) bfs.push_back((int)b.offset);
+        }
+    }
+    *nTopOut = (int)nw;
     for (int i = 0; i < n; ++i) {
         const pbrtgpu_bvh_node &b = s->nodes[i];
         const uint32_t np = b.meta & 0xff;
-        if (np == 0) (*ref)[i] = nw++;
+        if (np == 0) { if ((*ref)[i] == 0xffffffffu) (*ref)[i] = nw++; }
         else {
             if (np > WREF_NP_MASK || b.offset > WREF_OFF_MASK)
                 return fail(PBRTGPU_E_UNSUPPORTED, "BVH leaf beyond the 2^24-primitive reference range");
@@ -1179,7 +1220,7 @@ int pbrtgpu_scene_upload(pbrtgpu_ctx *c, const pbrtgpu_flat_scene *s) {
     {
         std::vector<float4> wn;
         std::vector<uint32_t> ref;
-        if (int e = wide_bvh(s, &wn, &ref)) return e;
+        if (int e = wide_bvh(s, top_nodes(), &wn, &ref, &S.nTop)) return e;
         HIPCHK(upload(c, wn.data(), wn.size(), &S.wnodes));
         HIPCHK(upload(c, ref.data(), ref.size(), &S.nodeRef));
     }
