@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define PBRTGPU_ABI_VERSION 6
+#define PBRTGPU_ABI_VERSION 7
 #define PBRTGPU_MAX_BANDS 64
 
 #define PBRTGPU_E_INVALID   (-1)
@@ -236,13 +236,22 @@ typedef struct pbrtgpu_flat_scene {
     const float *merl;
     int32_t integrator;           /* PBRTGPU_INTEGRATOR_*: the scene's SurfaceIntegrator */
     int32_t dl_strategy;          /* DirectLighting "strategy": PBRTGPU_DL_ALL or PBRTGPU_DL_ONE */
+    int32_t meta_strategy;        /* MetadataIntegrator "strategy": PBRTGPU_META_* */
+    const uint32_t *prim_meta;    /* [n_prims][2]: the Intersection::primitiveId and ::materialId a hit
+                                   * on the primitive reports (core/primitive.cpp:87-166; the
+                                   * Primitive / Material constructor counters, primitive.h:40,
+                                   * material.h:39), or NULL */
 } pbrtgpu_flat_scene;
 
-/* SurfaceIntegrator of a flattened scene: "path" (integrators/path.cpp:44-115) or
+/* SurfaceIntegrator of a flattened scene: "path" (integrators/path.cpp:44-115),
  * "directlighting" (integrators/directlighting.cpp:73-125, with the specular recursion of
- * core/integrator.cpp:169-250); max_depth is the integrator's "maxdepth" either way */
-enum { PBRTGPU_INTEGRATOR_PATH = 0, PBRTGPU_INTEGRATOR_DIRECT = 1 };
+ * core/integrator.cpp:169-250; max_depth is the integrator's "maxdepth" for both) or
+ * "metadata" (integrators/metadata.cpp) */
+enum { PBRTGPU_INTEGRATOR_PATH = 0, PBRTGPU_INTEGRATOR_DIRECT = 1, PBRTGPU_INTEGRATOR_METADATA = 2 };
 enum { PBRTGPU_DL_ALL = 0, PBRTGPU_DL_ONE = 1 };
+/* MetadataIntegrator (integrators/metadata.cpp:41-98): L = Spectrum(primitiveId),
+ * Spectrum(materialId) or Spectrum(|hit point - ray origin|) at the camera ray's first hit */
+enum { PBRTGPU_META_MESH = 0, PBRTGPU_META_MATERIAL = 1, PBRTGPU_META_DEPTH = 2 };
 
 /* ---- render description ----------------------------------------------------------- */
 /* Tiles are tile_w x tile_h blocks of the FILM pixel window (camera px_count x py_count;

@@ -29,6 +29,7 @@ typedef struct pbrthost_overrides {
     int32_t integrator;   /* PBRTGPU_INTEGRATOR_* to force, or -1: the scene's own ("path" for packs
                            * built before integrators were recorded) */
     int32_t dl_strategy;  /* PBRTGPU_DL_* to force, or -1: the scene's "strategy" */
+    int32_t meta_strategy;   /* PBRTGPU_META_* to force, or -1: the scene's metadata "strategy" */
 } pbrthost_overrides;
 
 /* path: a .pbrt scene file or a .pack scene pack.  Returns 0 or -1 (message in err). */
@@ -40,6 +41,12 @@ int pbrthost_set_render(pbrthost_scene *s, int spp, int maxdepth, uint32_t seed)
 /* info[0..15]: bands, spp, maxdepth, nodes, prims, tris, meshes, verts, quadrics,
  * materials, lights, bvh depth, film W, film H, warnings, 0 */
 int pbrthost_info(pbrthost_scene *s, int64_t *info, int n);
+/* pbrtWorldEnd's metadata text file (api.cpp:1228-1282) for the scene's SurfaceIntegrator
+ * "strategy": "mesh" -> <stem>_mesh.txt ("primitiveId shape-name" per top-level primitive, in
+ * scene order), "material" -> <stem>_materials.txt ("materialId name" per named material, by
+ * name); any other strategy writes nothing.  image_file: the film's output name (its stem is
+ * kept).  Returns 1 if a file was written, 0 if none, -1 on error. */
+int pbrthost_write_metadata(pbrthost_scene *s, const char *image_file);
 /* reference .dat writer; film [H][W][N] float32 (raw sums), weight [H][W] or NULL */
 int pbrthost_write_dat(const char *path, const float *film, const float *weight, int W, int H, int N);
 

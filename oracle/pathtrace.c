@@ -1934,6 +1934,36 @@ static void dl_radiance(const Ctx *c, Ray ray, const RayDiff *rd, int depth, Pat
     for (int i = 0; i < nb; ++i) Lout[i] = (1.f * L[i]) + 0.f;
 }
 
+/* MetadataIntegrator::Li (metadata.cpp:41-80) via SamplerRenderer::Li (samplerrenderer.cpp:225-247):
+ * first hit -> Spectrum(primitiveId), Spectrum(materialId) or Spectrum(|p - ray.o|); a miss ->
+ * the lights' Le */
+static void meta_radiance(const Ctx *c, Ray ray, float *Lout) {
+    int nb = c->nb;
+    float L[MAXB], tmp[MAXB];
+    for (int i = 0; i < nb; ++i) L[i] = 0.f;
+    Hit h;
+    if (!bvh_intersect(c, &ray, &h)) {
+        for (int k = 0; k < c->s->n_lights; ++k)
+            if (c->s->lights[k].type == PBRTGPU_LIGHT_INFINITE) {
+                inf_Le(c, &c->s->lights[k], ray.d, tmp);
+                for (int i = 0; i < nb; ++i) L[i] += tmp[i];
+            }
+    } else {
+        float v;
+        if (c->s->meta_strategy == PBRTGPU_META_DEPTH) {
+            Isect is;
+            isect_fill(c, &ray, &h, &is);
+            V d = vsub(is.dg.p, ray.o);
+            v = sqrtf(d.x * d.x + d.y * d.y + d.z * d.z);
+        } else {
+            const uint32_t *m = c->s->prim_meta;
+            v = m ? (float)m[2 * h.prim + (c->s->meta_strategy == PBRTGPU_META_MATERIAL)] : 0.f;
+        }
+        for (int i = 0; i < nb; ++i) L[i] = v;
+    }
+    for (int i = 0; i < nb; ++i) Lout[i] = (1.f * L[i]) + 0.f;
+}
+
 /* camera sample -> world ray (perspective.cpp:73-106, transform.h:253-262) */
 static Ray camera_ray(const Ctx *c, float imageX, float imageY, float lensU, float lensV, float timeU, RayDiff *rd) {
     const pbrtgpu_camera *cam = &c->s->camera;
@@ -2004,6 +2034,7 @@ static int trace_path(const Ctx *c, int px, int py, uint32_t s, float *L, float 
     Ray r = camera_ray(c, imageX, imageY, lens[0], lens[1], timeU, &rd);
     float Lr[MAXB];
     if (c->s->integrator == PBRTGPU_INTEGRATOR_DIRECT) dl_radiance(c, r, &rd, 0, &ps, Lr);
+    else if (c->s->integrator == PBRTGPU_INTEGRATOR_METADATA) meta_radiance(c, r, Lr);
     else radiance(c, r, &rd, &ps, Lr);
     int nb = c->nb, bad = 0;
     for (int i = 0; i < nb; ++i) L[i] = 1.f * Lr[i];   /* rayWeight * Li */

@@ -59,6 +59,7 @@
 #endif
 #include "integrators/path.h"
 #include "integrators/directlighting.h"
+#include "integrators/metadata.h"
 #include "samplers/lowdiscrepancy.h"
 #include "integrators/emission.h"
 #include "lights/diffuse.h"
@@ -335,6 +336,7 @@ static std::vector<Reference<Primitive> > primitives;
 static int ovW = -1, ovH = -1, ovMaxDepth = -1;
 static const char *surfOv = "path";   // --surf: the SurfaceIntegrator to create
 static const char *dlStrategyOv = NULL;
+static const char *metaStrategyOv = NULL;   // --meta-strategy: MetadataIntegrator "strategy" 
 // results of WorldEnd
 static Scene *gScene = NULL;
 static Camera *gCamera = NULL;
@@ -527,6 +529,9 @@ void pbrtWorldEnd() {
     if (sn == "directlighting") {
         if (dlStrategyOv) { string st(dlStrategyOv); surfParams.AddString("strategy", &st, 1); }
         gSurf = CreateDirectLightingIntegrator(surfParams);
+    } else if (sn == "metadata") {   // integrators/metadata.cpp:83-97
+        if (metaStrategyOv) { string st(metaStrategyOv); surfParams.AddString("strategy", &st, 1); }
+        gSurf = CreateMetadataIntegrator(surfParams);
     } else if (sn == "path") gSurf = CreatePathSurfaceIntegrator(surfParams);
     else { fprintf(stderr, "harness: surface integrator %s unsupported\n", sn.c_str()); exit(2); }
     gVol = CreateEmissionVolumeIntegrator(ParamSet());
@@ -554,7 +559,8 @@ static void usage() {
                     "   [--window x0 x1 y0 y1] [--raw film.f32] [--dat film.dat] [--paths paths.bin]\n"
                     "   [--path-every K] [--kat-mt out.bin] [--spectra out.bin] [--tris out.bin]\n"
                     "   [--keys keys.i32 (with --paths)] [--refdat film.dat] [--gpupath]\n"
-                    "   [--surf path|directlighting|scene] [--dl-strategy all|one]\n");
+                    "   [--surf path|directlighting|metadata|scene] [--dl-strategy all|one]\n"
+                    "   [--meta-strategy mesh|material|depth]\n");
     exit(1);
 }
 
@@ -584,6 +590,7 @@ int main(int argc, char **argv) {
         else if (a == "--gpupath") gpupath = true;
         else if (a == "--surf") surfOv = argv[++i];
         else if (a == "--dl-strategy") dlStrategyOv = argv[++i];
+        else if (a == "--meta-strategy") metaStrategyOv = argv[++i];
         else usage();
     }
     Options opt; opt.quiet = true;

@@ -269,6 +269,8 @@ struct DevScene {
     int nInf;                         // infinite lights among lights[]
     int integrator, dlStrategy;       // PBRTGPU_INTEGRATOR_*, PBRTGPU_DL_*
     int dlK;                          // DirectLighting light samples per vertex (sum of RoundUpPow2(nSamples))
+    int metaStrategy;                 // PBRTGPU_META_* (MetadataIntegrator)
+    const uint32_t *primMeta;         // [prims][2]: primitiveId, materialId a hit reports
 };
 
 // scene features a shade kernel is specialised for (k_shade<NB, FEAT>): a scene without

@@ -810,7 +810,9 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
     // that code compiled out (fewer registers, no kd-tree stack)
     // the DirectLighting integrator has its own step (all features compiled in)
     const bool dl = c->S.integrator == PBRTGPU_INTEGRATOR_DIRECT;
-    auto kShade = dl ? launch_shade_dl<NB> : c->feat ? launch_shade<NB, FEAT_ALL> : launch_shade<NB, 0>;
+    auto kShade = dl ? launch_shade_dl<NB>
+                  : c->S.integrator == PBRTGPU_INTEGRATOR_METADATA ? launch_shade_meta<NB>
+                  : c->feat ? launch_shade<NB, FEAT_ALL> : launch_shade<NB, 0>;
     const int nFrames = dl ? std::max(1, c->S.maxDepth) : 0;
     // passes one path can take: the camera ray + maxdepth + 1 vertices + 1 finish (path); per
     // vertex of the DirectLighting recursion (at most 2^maxdepth - 1) its hit + one pass per
@@ -1104,8 +1106,15 @@ int pbrtgpu_scene_upload(pbrtgpu_ctx *c, const pbrtgpu_flat_scene *s) {
     if (s->max_depth < 0 || s->max_depth > 20)
         return fail(PBRTGPU_E_UNSUPPORTED, "maxdepth > 20 exceeds the first MT19937 block (DESIGN.md §3.1)");
     if (s->n_nodes <= 0 || s->n_prims <= 0) return fail(PBRTGPU_E_INVALID, "empty scene");
-    if (s->integrator != PBRTGPU_INTEGRATOR_PATH && s->integrator != PBRTGPU_INTEGRATOR_DIRECT)
+    if (s->integrator != PBRTGPU_INTEGRATOR_PATH && s->integrator != PBRTGPU_INTEGRATOR_DIRECT &&
+        s->integrator != PBRTGPU_INTEGRATOR_METADATA)
         return fail(PBRTGPU_E_INVALID, "unknown SurfaceIntegrator");
+    if (s->integrator == PBRTGPU_INTEGRATOR_METADATA) {
+        if (s->meta_strategy < PBRTGPU_META_MESH || s->meta_strategy > PBRTGPU_META_DEPTH)
+            return fail(PBRTGPU_E_INVALID, "unknown metadata strategy");
+        if (s->meta_strategy != PBRTGPU_META_DEPTH && !s->prim_meta)
+            return fail(PBRTGPU_E_INVALID, "metadata mesh / material ids need prim_meta");
+    }
     if (s->integrator == PBRTGPU_INTEGRATOR_DIRECT && s->dl_strategy != PBRTGPU_DL_ALL && s->dl_strategy != PBRTGPU_DL_ONE)
         return fail(PBRTGPU_E_INVALID, "unknown DirectLighting strategy");
     // DirectLighting draws 6 MT19937 values at each of up to 2^(maxdepth-1) - 1 specular
@@ -1166,6 +1175,9 @@ int pbrtgpu_scene_upload(pbrtgpu_ctx *c, const pbrtgpu_flat_scene *s) {
     S.nLights = s->n_lights;
     S.integrator = s->integrator;
     S.dlStrategy = s->dl_strategy;
+    S.metaStrategy = s->meta_strategy;
+    S.primMeta = nullptr;
+    if (s->prim_meta) HIPCHK(upload(c, s->prim_meta, (size_t)2 * s->n_prims, &S.primMeta));
     S.dlK = 0;
     for (int i = 0; i < s->n_lights; ++i) {   // RoundUpPow2(max(1, nSamples)) per light
         uint32_t v = (uint32_t)std::max(1, s->lights[i].n_samples) - 1u;

@@ -7,6 +7,7 @@
 #include "device.h"
 #include "wavefront.h"
 #include "directlighting.h"
+#include "metadata.h"
 
 #if !defined(SHADE_NB) || !defined(SHADE_FEAT)
 #error "compile with -DSHADE_NB=<30|32|60> -DSHADE_FEAT=<0|7> [-DSHADE_DL=1]"
@@ -72,8 +73,10 @@ __device__ __forceinline__ uint32_t block_push(bool flag, uint32_t *counter, uin
 #define PGD_SHADE_ATTR __attribute__((amdgpu_waves_per_eu(SHADE_NB > 32 ? 2 : 3, SHADE_NB > 32 ? 2 : 3)))
 #endif
 #endif
-// DL: the DirectLightingIntegrator's step (directlighting.h) instead of PathIntegrator's
-template <int NB, int FEAT, bool DL>
+// MODE: the SurfaceIntegrator's step -- PathIntegrator (wavefront.h), DirectLightingIntegrator
+// (directlighting.h) or MetadataIntegrator (metadata.h)
+enum { MODE_PATH = 0, MODE_DL = 1, MODE_META = 2 };
+template <int NB, int FEAT, int MODE>
 __global__ __launch_bounds__(kShadeBlock) PGD_SHADE_ATTR void k_shade(DevScene S, PathSoA P, ItemSrc src, int qout,
                                                        float *__restrict__ Lout) {
     __shared__ uint32_t lds4[16];
@@ -89,7 +92,8 @@ __global__ __launch_bounds__(kShadeBlock) PGD_SHADE_ATTR void k_shade(DevScene S
     bool zeroed = false;
     if (inRange && !freeSlot) {
         bool done;
-        if (DL) pu = shade_slot_dl<NB, FEAT>(S, P, slot, Lout, &done, &zeroed);
+        if (MODE == MODE_DL) pu = shade_slot_dl<NB, FEAT>(S, P, slot, Lout, &done, &zeroed);
+        else if (MODE == MODE_META) pu = shade_slot_meta<NB, FEAT>(S, P, slot, Lout, &done, &zeroed);
         else pu = shade_slot<NB, FEAT>(S, P, slot, Lout, &done, &zeroed);
         if (done) { P.item[slot] = -1; freeSlot = true; }
     }
@@ -119,26 +123,33 @@ __global__ __launch_bounds__(kShadeBlock) PGD_SHADE_ATTR void k_shade(DevScene S
 #endif
 }
 
-template <int NB, int FEAT, bool DL>
+template <int NB, int FEAT, int MODE>
 static hipError_t launch(int grid, hipStream_t stream, const DevScene &S, const PathSoA &P, const ItemSrc &src, int qout,
                          float *Lout) {
     const size_t lds = ((FEAT & FEAT_MEAS) && S.kdInLds) ? (size_t)S.nKd * 32 : 0;
-    hipLaunchKernelGGL((k_shade<NB, FEAT, DL>), dim3(grid), dim3(kShadeBlock), lds, stream, S, P, src, qout, Lout);
+    hipLaunchKernelGGL((k_shade<NB, FEAT, MODE>), dim3(grid), dim3(kShadeBlock), lds, stream, S, P, src, qout, Lout);
     return hipGetLastError();
 }
 #if SHADE_DL
 template <int NB>
 hipError_t launch_shade_dl(int grid, hipStream_t stream, const DevScene &S, const PathSoA &P, const ItemSrc &src,
                            int qout, float *Lout) {
-    return launch<NB, SHADE_FEAT, true>(grid, stream, S, P, src, qout, Lout);
+    return launch<NB, SHADE_FEAT, MODE_DL>(grid, stream, S, P, src, qout, Lout);
+}
+template <int NB>
+hipError_t launch_shade_meta(int grid, hipStream_t stream, const DevScene &S, const PathSoA &P, const ItemSrc &src,
+                             int qout, float *Lout) {
+    return launch<NB, SHADE_FEAT, MODE_META>(grid, stream, S, P, src, qout, Lout);
 }
 template hipError_t launch_shade_dl<SHADE_NB>(int, hipStream_t, const DevScene &, const PathSoA &, const ItemSrc &, int,
                                               float *);
+template hipError_t launch_shade_meta<SHADE_NB>(int, hipStream_t, const DevScene &, const PathSoA &, const ItemSrc &,
+                                                int, float *);
 #else
 template <int NB, int FEAT>
 hipError_t launch_shade(int grid, hipStream_t stream, const DevScene &S, const PathSoA &P, const ItemSrc &src, int qout,
                         float *Lout) {
-    return launch<NB, FEAT, false>(grid, stream, S, P, src, qout, Lout);
+    return launch<NB, FEAT, MODE_PATH>(grid, stream, S, P, src, qout, Lout);
 }
 template hipError_t launch_shade<SHADE_NB, SHADE_FEAT>(int, hipStream_t, const DevScene &, const PathSoA &,
                                                        const ItemSrc &, int, float *);

@@ -907,5 +907,9 @@ hipError_t launch_shade(int grid, hipStream_t stream, const DevScene &S, const P
 template <int NB>
 hipError_t launch_shade_dl(int grid, hipStream_t stream, const DevScene &S, const PathSoA &P, const ItemSrc &src,
                            int qout, float *Lout);
+// k_shade with the MetadataIntegrator step (all features compiled in)
+template <int NB>
+hipError_t launch_shade_meta(int grid, hipStream_t stream, const DevScene &S, const PathSoA &P, const ItemSrc &src,
+                             int qout, float *Lout);
 
 }  // namespace pgd

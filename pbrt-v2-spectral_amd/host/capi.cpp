@@ -28,7 +28,7 @@ int pbrthost_load(const char *path, const pbrthost_overrides *ov, pbrthost_scene
         if (ov) {
             o.xres = ov->xres; o.yres = ov->yres; o.spp = ov->spp; o.maxdepth = ov->maxdepth;
             o.bands = ov->bands > 0 ? ov->bands : 32; o.seed = ov->seed;
-            o.integrator = ov->integrator; o.dl_strategy = ov->dl_strategy;
+            o.integrator = ov->integrator; o.dl_strategy = ov->dl_strategy; o.meta_strategy = ov->meta_strategy;
         }
         ok = LoadPbrtScene(p, o, s, &e);
     }
@@ -45,6 +45,7 @@ int pbrthost_load(const char *path, const pbrthost_overrides *ov, pbrthost_scene
         if (ov->seed != PBRTHOST_KEEP_SEED) s->seed = ov->seed;
         if (ov->integrator >= 0) s->integrator = ov->integrator;
         if (ov->dl_strategy >= 0) s->dlStrategy = ov->dl_strategy;
+        if (ov->meta_strategy >= 0) s->metaStrategy = ov->meta_strategy;
     }
     *out = reinterpret_cast<pbrthost_scene *>(s);
     return 0;
@@ -80,6 +81,23 @@ int pbrthost_info(pbrthost_scene *h, int64_t *info, int n) {
                      s->bvhMaxDepth, s->camera.px_count, s->camera.py_count, (int64_t)s->warnings.size(), 0};
     for (int i = 0; i < n && i < 16; ++i) info[i] = v[i];
     return 0;
+}
+
+int pbrthost_write_metadata(pbrthost_scene *h, const char *image_file) {
+    HostScene *s = reinterpret_cast<HostScene *>(h);
+    if (!s || !image_file) return -1;
+    // api.cpp:1235-1279: the output image name's stem + _mesh.txt / _materials.txt
+    std::string fn(image_file);
+    const std::string stem = fn.substr(0, fn.find_last_of("."));
+    const std::vector<std::pair<uint32_t, std::string> > *list;
+    std::string path;
+    if (s->surfStrategy == "mesh") { list = &s->metaMesh; path = stem + "_mesh.txt"; }
+    else if (s->surfStrategy == "material") { list = &s->metaMaterials; path = stem + "_materials.txt"; }
+    else return 0;
+    FILE *f = fopen(path.c_str(), "w");
+    if (!f) return -1;
+    for (auto &e : *list) fprintf(f, "%u %s\n", e.first, e.second.c_str());
+    return fclose(f) == 0 ? 1 : -1;
 }
 
 // SpectralImageFilm::WriteImage (spectralImage.cpp:267-378), identity conversion matrix.

@@ -212,6 +212,7 @@ struct MaterialObj {
     std::vector<Spec> spectra;
     std::shared_ptr<MeasuredData> measured;
     int flatIndex = -1;
+    uint32_t refId = 0;   // Material::materialId (material.h:39: constructor counter from 1)
 };
 struct LightObj {
     pbrtgpu_light l{};
@@ -223,6 +224,8 @@ struct PrimObj {
     std::shared_ptr<MaterialObj> mtl;
     int areaLight = -1;
     int instance = -1;    // animated shape -> TransformedPrimitive (index into instanceObjs)
+    uint32_t refId = 0;   // Primitive::primitiveId of the GeometricPrimitive / TransformedPrimitive
+    std::string name;     // the Shape directive's name (api.cpp:1117 primitiveNames)
 };
 
 struct SDVertex { V3 P; int startFace = -1; int child = -1; bool regular = false, boundary = false; };
@@ -552,6 +555,9 @@ private:
     TransformSet cameraToWorld;
     std::vector<std::shared_ptr<LightObj> > lights;
     std::vector<PrimObj> primitives;
+    // Primitive / Material constructor counters (primitive.cpp:32, material.cpp:34): the ids
+    // the MetadataIntegrator reports, replayed in the reference's construction order
+    uint32_t nextPrimId = 1, nextMatId = 1;
     std::vector<std::shared_ptr<TriMesh> > allMeshes;
     std::vector<std::shared_ptr<Quadric> > allQuads;
 
@@ -977,6 +983,7 @@ private:
             }
         } else
             throw std::runtime_error("material '" + name + "' is not supported by this build yet");
+        mo->refId = nextMatId++;
         return mo;
     }
     // default metal eta / k: copper, sampled at 56 wavelengths (metal.cpp:71-97), FromSampled
@@ -1303,6 +1310,16 @@ private:
             auto shape = MakeShape(name, id, idInv, gs.reverseOrientation, params);
             if (!shape) return;
             auto mtl = CreateMaterialFromState(params);
+            // api.cpp:1094-1105: GeometricPrimitive, its FullyRefine (one GeometricPrimitive per
+            // refined shape: a mesh's triangles, a subdivision surface's mesh and then its
+            // triangles), a BVHAccel over more than one, then the TransformedPrimitive
+            nextPrimId++;
+            if (shape->kind != ShapeObj::QUADRIC) {
+                std::vector<Isect> r;
+                RefineShape(shape, &r);
+                nextPrimId += (uint32_t)r.size() + (shape->kind == ShapeObj::LOOP ? 1u : 0u);
+                if (r.size() > 1) nextPrimId++;
+            }
             Xform w2o0, w2o1;
             LookupCache(curT.t[0], nullptr, &w2o0);
             LookupCache(curT.t[1], nullptr, &w2o1);
@@ -1311,6 +1328,8 @@ private:
             io.anim = AnimXform(w2o0, tStart, w2o1, tEnd);
             instanceObjs.push_back(io);
             PrimObj po; po.instance = (int)instanceObjs.size() - 1;
+            po.refId = nextPrimId++;
+            po.name = name;
             primitives.push_back(po);
             return;
         }
@@ -1337,12 +1356,14 @@ private:
             memcpy(alo->l.l2w_m, l2w.m.m, 64); memcpy(alo->l.l2w_minv, l2w.mInv.m, 64);
         }
         PrimObj po; po.shape = shape; po.mtl = mtl;
+        po.refId = nextPrimId++;   // api.cpp:1070 GeometricPrimitive
+        po.name = name;
         if (alo) { lights.push_back(alo); po.areaLight = (int)lights.size() - 1; }
         primitives.push_back(po);
     }
 
     // ------------------------------ WorldEnd ---------------------------------------
-    struct BuildPrim { Isect is; int material; int areaLight; };
+    struct BuildPrim { Isect is; int material; int areaLight; uint32_t primId = 0, matId = 0; };
     struct PrimInfo { int primitiveNumber; V3 centroid; BBox bounds; };
     struct BuildNode { BBox bounds; int children[2] = {-1, -1}; uint32_t splitAxis = 0, firstPrimOffset = 0, nPrimitives = 0; };
     struct InstanceObj {
@@ -1461,6 +1482,8 @@ private:
             fp.area_light = bp.areaLight;
             out->prims.push_back(fp);
             out->primInstance.push_back(inst);
+            out->primMeta.push_back(bp.primId);
+            out->primMeta.push_back(bp.matId);
         }
     }
 
@@ -1557,10 +1580,20 @@ private:
         if (ov.integrator >= 0) out->integrator = ov.integrator;
         else if (surfName == "path") out->integrator = PBRTGPU_INTEGRATOR_PATH;
         else if (surfName == "directlighting") out->integrator = PBRTGPU_INTEGRATOR_DIRECT;
+        else if (surfName == "metadata") out->integrator = PBRTGPU_INTEGRATOR_METADATA;
         else throw std::runtime_error("SurfaceIntegrator '" + surfName + "' is not supported by this build");
+        out->surfStrategy = surfParams.FindOneString("strategy", "");
         std::string st = surfParams.FindOneString("strategy", "all");
-        if (st != "all" && st != "one") out->warnings.push_back("Strategy \"" + st + "\" for direct lighting unknown");
+        if (out->integrator == PBRTGPU_INTEGRATOR_DIRECT && st != "all" && st != "one")
+            out->warnings.push_back("Strategy \"" + st + "\" for direct lighting unknown");
         out->dlStrategy = ov.dl_strategy >= 0 ? ov.dl_strategy : (st == "one" ? PBRTGPU_DL_ONE : PBRTGPU_DL_ALL);
+        // CreateMetadataIntegrator (metadata.cpp:83-97): "mesh", "material", "depth" (default;
+        // unknown strategies -> "depth" with a warning)
+        std::string ms = surfParams.FindOneString("strategy", "depth");
+        out->metaStrategy = ms == "mesh" ? PBRTGPU_META_MESH : ms == "material" ? PBRTGPU_META_MATERIAL : PBRTGPU_META_DEPTH;
+        if (out->integrator == PBRTGPU_INTEGRATOR_METADATA && ms != "mesh" && ms != "material" && ms != "depth")
+            out->warnings.push_back("Strategy \"" + ms + "\" for metadata unknown");
+        if (ov.meta_strategy >= 0) out->metaStrategy = ov.meta_strategy;
         int nsamp = ov.spp > 0 ? ov.spp : samplerParams.FindOneInt("pixelsamples", 4);
         out->spp = (int)RoundUpPow2((uint32_t)nsamp);
         out->seed = ov.seed == 0xffffffffu ? 0u : ov.seed;   // PBRTHOST_KEEP_SEED
@@ -1568,25 +1601,41 @@ private:
         out->bandY.assign(spec.Y(), spec.Y() + spec.n());
         out->yint = spec.yint();
         // ---- refine primitives (primitive.cpp:40-53, LIFO) and build the BVHs
+        // ids: hits on a top-level primitive report its refined GeometricPrimitive's id (created
+        // in triangle order by Refine, primitive.cpp:137-148, after the subdivision mesh's own);
+        // hits inside a TransformedPrimitive report the TransformedPrimitive's (primitive.cpp:95)
         auto refineInto = [&](const std::shared_ptr<ShapeObj> &shape, MaterialObj *mtl, int areaLight,
-                              std::vector<BuildPrim> *dst) {
+                              uint32_t fixedId, std::vector<BuildPrim> *dst) {
             std::vector<Isect> r;
             RefineShape(shape, &r);
+            uint32_t base = fixedId;
+            if (!fixedId) {
+                if (shape->kind == ShapeObj::LOOP) nextPrimId++;
+                base = nextPrimId;
+                nextPrimId += (uint32_t)r.size();
+            }
             // single intersectable shape -> itself; refinable -> children popped in reverse
-            for (auto it = r.rbegin(); it != r.rend(); ++it) {
-                BuildPrim bp; bp.is = *it; bp.material = EmitMaterial(mtl); bp.areaLight = areaLight;
+            for (size_t k = r.size(); k-- > 0;) {
+                BuildPrim bp; bp.is = r[k]; bp.material = EmitMaterial(mtl); bp.areaLight = areaLight;
+                bp.primId = fixedId ? fixedId : base + (uint32_t)k;
+                bp.matId = mtl->refId;
                 dst->push_back(bp);
             }
         };
+        nextPrimId++;   // the scene's BVHAccel (MakeScene -> MakeAccelerator, api.cpp:1318)
         blas.assign(instanceObjs.size(), BvhBuild());
         for (auto &po : primitives) {
-            if (po.instance < 0) { refineInto(po.shape, po.mtl.get(), po.areaLight, &top.prims); continue; }
+            if (po.instance < 0) {
+                refineInto(po.shape, po.mtl.get(), po.areaLight, po.shape->kind == ShapeObj::QUADRIC ? po.refId : 0u,
+                           &top.prims);
+                continue;
+            }
             // TransformedPrimitive (api.cpp:1101-1118): nested BVHAccel(refined) with the
             // default maxPrims 1, or the single refined primitive itself
             InstanceObj &io = instanceObjs[po.instance];
             BvhBuild &B = blas[po.instance];
             B.maxPrimsInNode = 1;
-            refineInto(io.shape, io.mtl.get(), -1, &B.prims);
+            refineInto(io.shape, io.mtl.get(), -1, po.refId, &B.prims);
             if (B.prims.empty()) continue;
             BBox objBound;
             if (B.prims.size() > 1) { B.Build(); objBound = B.bnodes[0].bounds; }
@@ -1596,9 +1645,14 @@ private:
             tp.is.inst = po.instance;
             tp.is.instBound = io.anim.MotionBounds(objBound, true);   // TransformedPrimitive::WorldBound
             tp.material = -1; tp.areaLight = -1;
+            tp.primId = po.refId; tp.matId = io.mtl->refId;
             top.prims.push_back(tp);
         }
         if (top.prims.empty()) throw std::runtime_error("scene has no primitives");
+        // pbrtWorldEnd's metadata lists (api.cpp:1252-1276)
+        for (auto &po : primitives) out->metaMesh.push_back(std::make_pair(po.refId, po.name));
+        for (auto &nm : gs.namedMaterials)
+            if (nm.second) out->metaMaterials.push_back(std::make_pair(nm.second->refId, nm.first));
         top.Build();
         out->bvhMaxDepth = top.maxDepth;
         size_t nNodes = top.bnodes.size();
@@ -1748,6 +1802,8 @@ void HostScene::Flat(pbrtgpu_flat_scene *f) const {
     f->merl = merl.empty() ? nullptr : merl.data();
     f->integrator = integrator;
     f->dl_strategy = dlStrategy;
+    f->meta_strategy = metaStrategy;
+    f->prim_meta = primMeta.size() == 2 * prims.size() && !prims.empty() ? primMeta.data() : nullptr;
 }
 
 }  // namespace pbrtamd

@@ -11,7 +11,7 @@
 namespace pbrtamd {
 
 static const char kMagic[8] = {'P', 'B', 'R', 'T', 'P', 'A', 'C', 'K'};
-static const uint32_t kVersion = 6;   // 6: + merl tables (version 5 packs load with none)
+static const uint32_t kVersion = 7;   // 6: + merl tables; 7: + metadata ids (5 and 6 still load)
 
 static bool W(gzFile f, const void *p, size_t n) {
     const char *c = (const char *)p;
@@ -35,6 +35,32 @@ template <class T> static bool RArr(gzFile f, std::vector<T> &v) {
     return n == 0 || R(f, v.data(), sizeof(T) * n);
 }
 
+static bool WStr(gzFile f, const std::string &v) {
+    uint64_t n = v.size();
+    return W(f, &n, 8) && (n == 0 || W(f, v.data(), n));
+}
+static bool RStr(gzFile f, std::string &v) {
+    uint64_t n;
+    if (!R(f, &n, 8) || n > (1u << 20)) return false;
+    v.assign(n, '\0');
+    return n == 0 || R(f, &v[0], n);
+}
+typedef std::vector<std::pair<uint32_t, std::string> > IdList;
+static bool WList(gzFile f, const IdList &v) {
+    uint64_t n = v.size();
+    bool ok = W(f, &n, 8);
+    for (size_t i = 0; ok && i < v.size(); ++i) ok = W(f, &v[i].first, 4) && WStr(f, v[i].second);
+    return ok;
+}
+static bool RList(gzFile f, IdList &v) {
+    uint64_t n;
+    if (!R(f, &n, 8) || n > (1u << 26)) return false;
+    v.resize(n);
+    bool ok = true;
+    for (size_t i = 0; ok && i < n; ++i) ok = R(f, &v[i].first, 4) && RStr(f, v[i].second);
+    return ok;
+}
+
 bool SavePack(const HostScene &s, const std::string &path, std::string *err) {
     gzFile f = gzopen(path.c_str(), "wb6");
     if (!f) { if (err) *err = "cannot write " + path; return false; }
@@ -49,6 +75,10 @@ bool SavePack(const HostScene &s, const std::string &path, std::string *err) {
          WArr(f, s.rgbBasis) && WArr(f, s.merl);
     int32_t integ[2] = {s.integrator, s.dlStrategy};
     ok = ok && W(f, integ, 8);
+    // v7: metadata strategy, per-prim ids, the metadata text lists
+    int32_t ms = s.metaStrategy;
+    ok = ok && W(f, &ms, 4) && WStr(f, s.surfStrategy) && WArr(f, s.primMeta) && WList(f, s.metaMesh) &&
+         WList(f, s.metaMaterials);
     ok = (gzclose(f) == Z_OK) && ok;
     if (!ok && err) *err = "write error on " + path;
     return ok;
@@ -59,7 +89,7 @@ bool LoadPack(const std::string &path, HostScene *s, std::string *err) {
     if (!f) { if (err) *err = "cannot open " + path; return false; }
     char magic[8];
     uint32_t ver = 0;
-    bool ok = R(f, magic, 8) && memcmp(magic, kMagic, 8) == 0 && R(f, &ver, 4) && (ver == kVersion || ver == 5);
+    bool ok = R(f, magic, 8) && memcmp(magic, kMagic, 8) == 0 && R(f, &ver, 4) && ver >= 5 && ver <= kVersion;
     int32_t hdr[4];
     ok = ok && R(f, hdr, 16) && R(f, &s->seed, 4) && R(f, &s->yint, 4);
     if (ok) { s->nBands = hdr[0]; s->maxDepth = hdr[1]; s->spp = hdr[2]; s->bvhMaxDepth = hdr[3]; }
@@ -76,6 +106,15 @@ bool LoadPack(const std::string &path, HostScene *s, std::string *err) {
         int32_t integ[2];
         ok = RArr(f, s->merl) && R(f, integ, 8);
         if (ok) { s->integrator = integ[0]; s->dlStrategy = integ[1]; }
+    }
+    s->metaStrategy = PBRTGPU_META_DEPTH;
+    s->surfStrategy.clear();
+    s->primMeta.clear(); s->metaMesh.clear(); s->metaMaterials.clear();
+    if (ok && ver >= 7) {
+        int32_t ms;
+        ok = R(f, &ms, 4) && RStr(f, s->surfStrategy) && RArr(f, s->primMeta) && RList(f, s->metaMesh) &&
+             RList(f, s->metaMaterials);
+        if (ok) s->metaStrategy = ms;
     }
     gzclose(f);
     if (!ok && err) *err = "bad or truncated scene pack " + path;

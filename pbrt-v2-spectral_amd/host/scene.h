@@ -17,6 +17,7 @@ struct RenderOverrides {
     uint32_t seed = 0;
     int integrator = -1;          // PBRTGPU_INTEGRATOR_* to force, -1: the scene's SurfaceIntegrator
     int dl_strategy = -1;         // PBRTGPU_DL_* to force, -1: the scene's "strategy"
+    int meta_strategy = -1;       // PBRTGPU_META_* to force, -1: the scene's metadata "strategy"
 };
 
 // Resolution-independent camera description (perspective.cpp:110-147 parameters); the
@@ -62,6 +63,11 @@ struct HostScene {
     std::vector<float> merl;                  // RegularHalfangleBRDF RGB tables (pbrtgpu_flat_scene::merl)
     int integrator = 0;                       // PBRTGPU_INTEGRATOR_* (packs older than v6: path)
     int dlStrategy = 0;                       // PBRTGPU_DL_*
+    int metaStrategy = PBRTGPU_META_DEPTH;    // PBRTGPU_META_*
+    std::string surfStrategy;                 // the SurfaceIntegrator's "strategy" string (metadata files)
+    std::vector<uint32_t> primMeta;           // [prims][2]: primitiveId, materialId a hit reports
+    std::vector<std::pair<uint32_t, std::string> > metaMesh;        // top-level primitives: id, shape name
+    std::vector<std::pair<uint32_t, std::string> > metaMaterials;   // named materials: id, name (by name)
     // diagnostics
     std::vector<std::string> warnings;
     int bvhMaxDepth = 0;

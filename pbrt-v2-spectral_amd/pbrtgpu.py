@@ -59,16 +59,18 @@ class FlatScene(ctypes.Structure):
                 ("n_instances", I32), ("instances", P), ("prim_instance", P),
                 ("n_kdnodes", I32), ("kdnodes", P),
                 ("n_textures", I32), ("textures", P), ("ewa_lut", P), ("rgb_basis", P),
-                ("n_merl_floats", I32), ("merl", P), ("integrator", I32), ("dl_strategy", I32)]
+                ("n_merl_floats", I32), ("merl", P), ("integrator", I32), ("dl_strategy", I32),
+                ("meta_strategy", I32), ("prim_meta", P)]
 
 
 class Overrides(ctypes.Structure):
     _fields_ = [("xres", I32), ("yres", I32), ("spp", I32), ("maxdepth", I32), ("bands", I32),
-                ("seed", ctypes.c_uint32), ("integrator", I32), ("dl_strategy", I32)]
+                ("seed", ctypes.c_uint32), ("integrator", I32), ("dl_strategy", I32), ("meta_strategy", I32)]
 
 
-INTEGRATORS = {"path": 0, "directlighting": 1}
+INTEGRATORS = {"path": 0, "directlighting": 1, "metadata": 2}
 DL_STRATEGIES = {"all": 0, "one": 1}
+META_STRATEGIES = {"mesh": 0, "material": 1, "depth": 2}
 
 
 class RenderDesc(ctypes.Structure):
@@ -79,7 +81,7 @@ class RenderDesc(ctypes.Structure):
 STAT_PATHS, STAT_KERNEL_MS, STAT_ACCUM_MS, STAT_ZEROED, STAT_SPILLS, STAT_PASSES = 0, 1, 2, 3, 4, 5
 F_ACCUMULATE, F_COUNT_WORK = 1, 2
 KEEP_SEED = 0xFFFFFFFF
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 
 class Timing(ctypes.Structure):
@@ -115,13 +117,14 @@ def host_lib():
         _host.pbrthost_info.argtypes = [P, ctypes.POINTER(ctypes.c_int64), ctypes.c_int]
         _host.pbrthost_write_dat.argtypes = [ctypes.c_char_p, P, P, ctypes.c_int, ctypes.c_int, ctypes.c_int]
         _host.pbrthost_spectrum_from_rgb.argtypes = [ctypes.c_int, P, ctypes.c_int, P]
+        _host.pbrthost_write_metadata.argtypes = [P, ctypes.c_char_p]
     return _host
 
 
 def host_symbols():
     """Symbols declared in include/pbrthost.h."""
     return ["pbrthost_load", "pbrthost_free", "pbrthost_flat", "pbrthost_save_pack", "pbrthost_set_render",
-            "pbrthost_info", "pbrthost_write_dat", "pbrthost_spectrum_from_rgb"]
+            "pbrthost_info", "pbrthost_write_dat", "pbrthost_spectrum_from_rgb", "pbrthost_write_metadata"]
 
 
 def spectrum_from_rgb(rgb, bands=32, illuminant=False):
@@ -188,13 +191,16 @@ class Scene:
     @staticmethod
     def load(path, xres=-1, yres=-1, spp=-1, maxdepth=-1, bands=0, seed=None, integrator=None, strategy=None):
         """bands <= 0: the pack's own band count, or 32 (the reference build) for a .pbrt file.
-        integrator / strategy: None keeps the scene's SurfaceIntegrator ("path" or
-        "directlighting") and DirectLighting "strategy" ("all" or "one")."""
+        integrator / strategy: None keeps the scene's SurfaceIntegrator ("path",
+        "directlighting" or "metadata") and its "strategy" (DirectLighting "all" / "one",
+        metadata "mesh" / "material" / "depth")."""
         h = P()
         err = ctypes.create_string_buffer(1024)
         ov = Overrides(xres, yres, spp, maxdepth, bands, KEEP_SEED if seed is None else seed,
                        -1 if integrator is None else INTEGRATORS[integrator],
-                       -1 if strategy is None else DL_STRATEGIES[strategy])
+                       DL_STRATEGIES.get(strategy, -1), META_STRATEGIES.get(strategy, -1))
+        if strategy is not None and strategy not in DL_STRATEGIES and strategy not in META_STRATEGIES:
+            raise ValueError("unknown strategy %r" % strategy)
         if host_lib().pbrthost_load(path.encode(), ctypes.byref(ov), ctypes.byref(h), err, 1024) != 0:
             raise RuntimeError("scene load failed: %s" % err.value.decode())
         return Scene(h)
@@ -230,6 +236,21 @@ class Scene:
     @property
     def spp(self):
         return self.flat.spp
+
+    def write_metadata(self, image_file):
+        """pbrtWorldEnd's _mesh.txt / _materials.txt beside image_file; True if one was written."""
+        r = host_lib().pbrthost_write_metadata(self._h, image_file.encode())
+        if r < 0:
+            raise RuntimeError("cannot write metadata for %s" % image_file)
+        return r == 1
+
+    def prim_meta(self):
+        """[n_prims][2] uint32: the primitiveId / materialId a hit on each primitive reports."""
+        n = self.flat.n_prims
+        if not self.flat.prim_meta:
+            return np.zeros((n, 2), np.uint32)
+        buf = (ctypes.c_uint32 * (2 * n)).from_address(self.flat.prim_meta)
+        return np.frombuffer(buf, dtype=np.uint32).reshape(n, 2).copy()
 
     def write_dat(self, path, film):
         film = np.ascontiguousarray(film, dtype=np.float32)

@@ -154,3 +154,39 @@ def test_pack_keeps_merl_tables(pg, merl_dir, tmp_path):
     mats = ctypes.cast(s.flat.materials, ctypes.POINTER(ctypes.c_int32 * 24))
     kinds = [(mats[i][0], mats[i][5]) for i in range(s.flat.n_materials)]   # (type, aux)
     assert (7, 0) in kinds and (7, -1) in kinds
+
+
+def test_metadata_ids_and_text_files(pg, tmp_path):
+    """pbrtWorldEnd's metadata files (api.cpp:1228-1282) list the ids the hits report: the
+    quadrics' and the animated shape's primitive ids (the mesh file, scene order) and the named
+    materials' ids (the materials file, by name) appear in the per-prim hit ids."""
+    scn = os.path.join(os.path.dirname(os.path.abspath(__file__)), "scenes", "metadata.pbrt")
+    s = pg.Scene.load(scn, integrator="metadata", strategy="mesh")
+    meta = s.prim_meta()
+    assert meta.shape == (s.flat.n_prims, 2) and meta.min() >= 1
+    # the scene file says "material": that is the strategy the text file follows
+    assert s.write_metadata(str(tmp_path / "img.exr"))
+    mats = [l.split() for l in open(tmp_path / "img_materials.txt").read().splitlines()]
+    assert [m[1] for m in mats] == ["floor", "shiny"]
+    assert {int(m[0]) for m in mats} <= set(meta[:, 1].tolist())
+    # per-shape materials get fresh ids (GraphicsState::CreateMaterial), so 5 distinct ids
+    assert len(set(meta[:, 1].tolist())) == 5
+    pack = str(tmp_path / "m.pack")
+    s.save_pack(pack)
+    p = pg.Scene.load(pack)
+    assert np.array_equal(p.prim_meta(), meta)
+    assert p.write_metadata(str(tmp_path / "again.dat"))
+    assert open(tmp_path / "again_materials.txt").read() == open(tmp_path / "img_materials.txt").read()
+    # the mesh list: 5 top-level primitives in scene order; quadric / animated ids are hit ids
+    d = pg.Scene.load(scn, integrator="metadata")
+    d2 = str(tmp_path / "mesh.pbrt")
+    open(d2, "w").write(open(scn).read().replace('"string strategy" "material"', '"string strategy" "mesh"'))
+    m = pg.Scene.load(d2)
+    assert m.flat.integrator == pg.INTEGRATORS["metadata"] and m.flat.meta_strategy == pg.META_STRATEGIES["mesh"]
+    assert m.write_metadata(str(tmp_path / "x.exr"))
+    rows = [l.split() for l in open(tmp_path / "x_mesh.txt").read().splitlines()]
+    assert [r[1] for r in rows] == ["trianglemesh", "sphere", "loopsubdiv", "disk", "trianglemesh"]
+    ids = set(m.prim_meta()[:, 0].tolist())
+    assert int(rows[1][0]) in ids and int(rows[3][0]) in ids and int(rows[4][0]) in ids
+    assert int(rows[0][0]) not in ids          # a refined mesh reports its triangles' ids
+    assert d.flat.meta_strategy == pg.META_STRATEGIES["material"]

@@ -164,3 +164,38 @@ def test_direct_lighting_film_bit_exact_vs_reference(pg, ora_libm, name):
     g = np.load(os.path.join(GOLDEN, name + ".npz"))
     film, _ = ora_libm.render(dl_scene(pg, g, name), threads=8)
     assert np.array_equal(film.view(np.int32), g["film"].view(np.int32))
+
+
+META = ["metadata_material_%s_48x36s4", "metadata_mesh_%s_48x36s4", "metadata_depth_%s_48x36s4",
+        "killeroo_meta_mesh_%s_40x32s2", "anim_meta_mesh_%s_40x32s2", "bunny_meta_depth_%s_40x32s2"]
+
+
+def meta_scene(pg, g, name):
+    """The scene of a MetadataIntegrator fixture: tests/scenes/metadata.pbrt itself, or a config
+    scene's pack rendered with integrator "metadata" and the fixture's strategy."""
+    w, h, spp, seed, md = [int(v) for v in g["config"]]
+    st = "mesh" if "_mesh_" in name else "material" if "_material_" in name else "depth"
+    if name.startswith("metadata_"):
+        path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "scenes", "metadata.pbrt")
+    else:
+        path = os.path.join(PACKS, {"anim": "anim-killeroos-moving.pack", "bunny": "bunny.pack"}.get(
+            name.split("_")[0], "killeroo-simple.pack"))
+    return pg.Scene.load(path, xres=w, yres=h, spp=spp, seed=seed, integrator="metadata", strategy=st)
+
+
+@pytest.mark.parametrize("name", [m % "paths" for m in META])
+def test_metadata_paths_bit_exact_vs_reference(pg, ora_libm, name):
+    """MetadataIntegrator (metadata.cpp:41-98): Spectrum(primitiveId / materialId / depth) of
+    the first hit, the ids replayed from the reference's Primitive / Material constructor
+    counters by the front end; the oracle against the reference harness, bit for bit."""
+    g = np.load(os.path.join(GOLDEN, name + ".npz"))
+    scene = meta_scene(pg, g, name)
+    L = ora_libm.trace_paths(scene, g["keys"])
+    assert np.array_equal(L.view(np.int32), g["L"].view(np.int32))
+
+
+@pytest.mark.parametrize("name", [m % "film" for m in META])
+def test_metadata_film_bit_exact_vs_reference(pg, ora_libm, name):
+    g = np.load(os.path.join(GOLDEN, name + ".npz"))
+    film, _ = ora_libm.render(meta_scene(pg, g, name), threads=8)
+    assert np.array_equal(film.view(np.int32), g["film"].view(np.int32))

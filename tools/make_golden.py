@@ -39,10 +39,14 @@ Fixtures (numpy .npz, inputs + expected outputs only):
                                   integrator.cpp:169-250): killeroo (strategy all, light nsamples 8),
                                   bunny, anim, and the coverage scene (mirror / glass recursion,
                                   textures) with strategies all and one
+  metadata_*, *_meta_*            MetadataIntegrator (integrators/metadata.cpp) with strategies
+                                  material / mesh / depth: tests/scenes/metadata.pbrt (named and
+                                  per-shape materials, mesh, subdivision, quadric and animated
+                                  primitives), killeroo and anim (mesh ids), bunny (depth)
   killeroo_dat_40x32s4.npz        the raw film of the restatement film AND the .dat the
                                   reference's own SpectralImageNoCameraFilm wrote for the same
                                   samples (--refdat): pins AddSample and the WriteImage payload
-Usage: python tools/make_golden.py [--only keys|dat]   (after `make -C oracle ref` and `make -C oracle ref60`)
+Usage: python tools/make_golden.py [--only keys|dat|merl|dl|meta]   (after `make -C oracle ref` and `make -C oracle ref60`)
 """
 import os
 import subprocess
@@ -157,6 +161,29 @@ def dl_fixtures(tmp):
         film_fixture("%s_film_%s" % (stem, tag), res, spp, 0, md, tmp, scene=scene, extra=ex)
 
 
+# MetadataIntegrator (integrators/metadata.cpp): (fixture stem, scene, res, spp, strategy, stride).
+# Python loads tests/scenes/metadata.pbrt directly and the config scenes from their packs with
+# integrator="metadata" and the strategy.
+META_FIXTURES = [
+    ("metadata_material", "METADATA", (48, 36), 4, "material", 1),   # named + per-shape materials
+    ("metadata_mesh", "METADATA", (48, 36), 4, "mesh", 1),           # mesh / subdivision / quadric / animated ids
+    ("metadata_depth", "METADATA", (48, 36), 4, "depth", 1),
+    ("killeroo_meta_mesh", "killeroo-simple.pbrt", (40, 32), 2, "mesh", 1),
+    ("anim_meta_mesh", "anim-killeroos-moving.pbrt", (40, 32), 2, "mesh", 1),
+    ("bunny_meta_depth", "bunny.pbrt", (40, 32), 2, "depth", 1),
+]
+
+
+def meta_fixtures(tmp):
+    for stem, scene, res, spp, st, every in META_FIXTURES:
+        if scene == "METADATA":
+            scene = os.path.join(ROOT, "tests", "scenes", "metadata.pbrt")
+        ex = ("--surf", "metadata", "--meta-strategy", st)
+        tag = "%dx%ds%d" % (res[0], res[1], spp)
+        paths_fixture("%s_paths_%s" % (stem, tag), res, spp, 0, 5, every, tmp, scene=scene, extra=ex)
+        film_fixture("%s_film_%s" % (stem, tag), res, spp, 0, 5, tmp, scene=scene, extra=ex)
+
+
 def merl_fixtures(tmp):
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     import make_merl
@@ -185,6 +212,8 @@ def main():
                 merl_fixtures(tmp)
             elif only == "dl":
                 dl_fixtures(tmp)
+            elif only == "meta":
+                meta_fixtures(tmp)
         return
     with tempfile.TemporaryDirectory() as tmp:
         paths_fixture("killeroo_paths_64x64s4", (64, 64), 4, 0, 5, 5, tmp)
