@@ -40,7 +40,7 @@ void GpuPathRenderer::Render(const Scene *) {
         return;
     }
     int n = ngpu > 0 ? min(ngpu, ndev) : ndev;
-    pbrthost_overrides ov = { -1, -1, -1, -1, nSpectralSamples, seed, -1, -1 };   // the scene's own integrator
+    pbrthost_overrides ov = { -1, -1, -1, -1, nSpectralSamples, seed, -1, -1, -1 };   // the scene's own integrator
     pbrthost_scene *hs = NULL;
     char err[1024];
     if ((status = pbrthost_load(sceneFile.c_str(), &ov, &hs, err, sizeof(err))) != 0) {
@@ -62,6 +62,9 @@ void GpuPathRenderer::Render(const Scene *) {
     if (status != 0) Error("gpupath: %s", pbrtgpu_last_error());
     for (int d = 0; d < n; ++d)
         if (ctx[d]) pbrtgpu_context_destroy(ctx[d]);
+    // (the metadata text file of a "metadata" SurfaceIntegrator is written by the reference's own
+    // pbrtWorldEnd, api.cpp:1228-1282, before the renderer runs; pbrthost_write_metadata is that
+    // writer for callers without api.cpp)
     if (status == 0 && pbrthost_write_dat(outFile.c_str(), film.data(), NULL, W, H, N) != 0) {
         Error("gpupath: cannot write \"%s\"", outFile.c_str());
         status = PBRTGPU_E_INVALID;
