@@ -116,6 +116,54 @@ PGD_INLINE void dl_vertex(const DevScene &S, const PathSoA &P, int slot, int d, 
     v.wo = vneg(v.ray.d);
 }
 
+// adds light sample kk's ED = (0 [+ A]) [+ B] of the top vertex (frame d): strategy one
+// L += ED * nLights (UniformSampleOneLight); strategy all Ld += ED, La += Ld / nSamples after a
+// light's last sample and L += La after the last light (UniformSampleAllLights), the sums in the
+// slot's beta buffers 0 (La) and 1 (Ld)
+template <int NB>
+PGD_INLINE void dl_add(const DevScene &S, const PathSoA &P, int slot, int d, int kk, int K, bool all, bool useA,
+                       bool useB, const float4 *A, const float4 *B) {
+    constexpr int NQ = Bands<NB>::NQ;
+    const size_t c = P.cap;
+    float4 *La = P.beta + slot, *Ld = P.beta + (size_t)NQ * c + slot;
+    float4 *Lv = dl_L<NB>(P, d, slot);
+    int li = 0, j = 0, ns = 1;
+    if (all) dl_cursor(S, kk, &li, &j, &ns);
+    const bool last = kk == K - 1;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+        const float4 a = useA ? A[q * c] : make_float4(0.f, 0.f, 0.f, 0.f);
+        const float4 bb = useB ? B[q * c] : make_float4(0.f, 0.f, 0.f, 0.f);
+        float4 ed;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            float e = 0.f;
+            if (useA) e += cmp(a, i);
+            if (useB) e += cmp(bb, i);
+            cmp(ed, i) = e;
+        }
+        if (!all) {
+            float4 l = Lv[q * c];
+            const float nl = (float)S.nLights;
+            l.x += ed.x * nl; l.y += ed.y * nl; l.z += ed.z * nl; l.w += ed.w * nl;
+            Lv[q * c] = l;
+        } else {
+            float4 ld = j == 0 ? make_float4(0.f, 0.f, 0.f, 0.f) : Ld[q * c];
+            ld.x += ed.x; ld.y += ed.y; ld.z += ed.z; ld.w += ed.w;
+            if (j == ns - 1) {
+                float4 la = kk + 1 == ns ? make_float4(0.f, 0.f, 0.f, 0.f) : La[q * c];   // the first light
+                const float fn = (float)ns;
+                la.x += ld.x / fn; la.y += ld.y / fn; la.z += ld.z / fn; la.w += ld.w / fn;
+                if (last) {
+                    float4 l = Lv[q * c];
+                    l.x += la.x; l.y += la.y; l.z += la.z; l.w += la.w;
+                    Lv[q * c] = l;
+                } else La[q * c] = la;
+            } else Ld[q * c] = ld;
+        }
+    }
+}
+
 // k_shade body of the DirectLighting integrator for one slot (see the file comment).
 // Returns the ray requests; *done when the camera sample's radiance is in Lout.
 template <int NB, int FEAT>
@@ -126,14 +174,13 @@ PGD_INLINE Pushes shade_slot_dl(const DevScene &S, const PathSoA &P, int slot, f
     const float *sp = S.spectra;
     uint32_t fl = P.flags[slot];
     int d = P.bounce[slot];   // depth of the top frame (-1: camera ray in flight)
-    Pushes out = {false, false, false};
+    Pushes out = {false, false, false, 0u, 0u};
     *done = false;
     *zeroed = false;
     const int nLights = S.nLights;
     const bool all = S.dlStrategy != PBRTGPU_DL_ONE;
     const int K = all ? S.dlK : 1;
     const uint32_t hp = P.hp[slot], s = P.smp[slot];
-    float4 *La = P.beta + slot, *Ld = P.beta + (size_t)NQ * c + slot;   // UniformSampleAllLights sums
     int k = (int)P.dlk[slot];
     DLVertex vx;
     bool have = false;   // vx holds the top frame's vertex
@@ -145,65 +192,34 @@ PGD_INLINE Pushes shade_slot_dl(const DevScene &S, const PathSoA &P, int slot, f
 #ifdef PGD_DL_TRACE_ITEM   // debugging aid: the step of one item per pass
     const bool trc = P.item[slot] == PGD_DL_TRACE_ITEM;
     if (trc) printf("[dl] slot %d d %d fl %x k %d K %d prim %d occ %u hitM %d\n", slot, d, fl, k, K, P.hitPrim[slot],
-                    P.occ[slot], P.hitPrim[c + slot]);
+                    P.occ[slot], P.hitPrim[P.rcap + slot]);
 #endif
     if (fl & PF_PEND) {
-        // ---- the answered light sample k: ED = (0 [+ A]) [+ B] (EstimateDirect)
-        const bool useA = (fl & PF_PA) && !P.occ[slot];
-        bool useB = false;
-        const int ln = (int)(fl >> PF_LIGHT_SHIFT);
-        if (fl & PF_PB) {
-            const int mp = P.hitPrim[c + slot];
-            if ((FEAT & FEAT_INF) && S.lights[ln].type == PBRTGPU_LIGHT_INFINITE) useB = mp < 0;
-            else if (mp >= 0 && S.prims[mp].area_light == ln) {
-                const Ray mr = ray_load(P, RAY_M, slot);
-                useB = vdot(isect_nn(S, mr, mp, P.hitT[c + slot], inst_rec(P, slot)), vneg(mr.d)) > 0.f;
-            }
-        }
+        // ---- the answered batch of light samples [k, kEnd): ED = (0 [+ A]) [+ B] each
+        // (EstimateDirect), added in sample order
+        const uint32_t msk = P.dlMask[slot];
+        const int kEnd = min(k + P.dlBatch, K);
+        const int lnOne = (int)(fl >> PF_LIGHT_SHIFT);
         fl &= ~(PF_PEND | PF_PA | PF_PB | (PF_LIGHT_MASK << PF_LIGHT_SHIFT));
-        const float4 *A = A_of<NB>(P, 0, slot), *B = B_of<NB>(P, 0, slot);
-        int li = 0, j = 0, ns = 1;
-        if (all) dl_cursor(S, k, &li, &j, &ns);
-        float4 *Lv = dl_L<NB>(P, d, slot);
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) {
-            const float4 a = useA ? A[q * c] : make_float4(0.f, 0.f, 0.f, 0.f);
-            const float4 bb = useB ? B[q * c] : make_float4(0.f, 0.f, 0.f, 0.f);
-            float4 ed;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                float e = 0.f;
-                if (useA) e += cmp(a, i);
-                if (useB) e += cmp(bb, i);
-                cmp(ed, i) = e;
+        for (int kk = k; kk < kEnd; ++kk) {
+            const int jb = kk - k, rs = slot + jb * (int)c;
+            int ln = lnOne;
+            if (all) { int j, ns; dl_cursor(S, kk, &ln, &j, &ns); }
+            const bool useA = ((msk >> jb) & 1u) && !P.occ[rs];
+            bool useB = false;
+            if ((msk >> (16 + jb)) & 1u) {
+                const int mp = P.hitPrim[P.rcap + rs];
+                if ((FEAT & FEAT_INF) && S.lights[ln].type == PBRTGPU_LIGHT_INFINITE) useB = mp < 0;
+                else if (mp >= 0 && S.prims[mp].area_light == ln) {
+                    const Ray mr = ray_load(P, RAY_M, rs);
+                    useB = vdot(isect_nn(S, mr, mp, P.hitT[P.rcap + rs], inst_rec(P, slot)), vneg(mr.d)) > 0.f;
+                }
             }
-            if (!all) {   // L += UniformSampleOneLight = ED * nLights
-                float4 l = Lv[q * c];
-                const float nl = (float)nLights;
-                l.x += ed.x * nl; l.y += ed.y * nl; l.z += ed.z * nl; l.w += ed.w * nl;
-                Lv[q * c] = l;
-            } else {      // Ld += ED; after the light's last sample La += Ld / ns
-                float4 ld = j == 0 ? make_float4(0.f, 0.f, 0.f, 0.f) : Ld[q * c];
-                ld.x += ed.x; ld.y += ed.y; ld.z += ed.z; ld.w += ed.w;
-                if (j == ns - 1) {
-                    float4 la = k + 1 == ns ? make_float4(0.f, 0.f, 0.f, 0.f) : La[q * c];   // first light
-                    const float fn = (float)ns;
-                    la.x += ld.x / fn; la.y += ld.y / fn; la.z += ld.z / fn; la.w += ld.w / fn;
-                    La[q * c] = la;
-                } else Ld[q * c] = ld;
-            }
+            dl_add<NB>(S, P, slot, d, kk, K, all, useA, useB, P.A + (size_t)jb * NQ * c + slot,
+                       P.B + (size_t)jb * NQ * c + slot);
         }
-        ++k;
+        k = kEnd;
         stage = k < K ? 1 : 2;
-        if (stage == 2 && all) {   // L += La
-#pragma unroll
-            for (int q = 0; q < NQ; ++q) {
-                float4 l = Lv[q * c];
-                const float4 la = La[q * c];
-                l.x += la.x; l.y += la.y; l.z += la.z; l.w += la.w;
-                Lv[q * c] = l;
-            }
-        }
     } else {
         // ---- the camera ray or a specular child ray was answered (PF_CONT)
         fl &= ~PF_CONT;
@@ -251,48 +267,40 @@ PGD_INLINE Pushes shade_slot_dl(const DevScene &S, const PathSoA &P, int slot, f
     }
     for (;;) {
         if (stage == 1) {
-            // ---- light sample k of the top vertex
+            // ---- a batch of light samples [k, kEnd) of the top vertex: shadow and MIS rays of
+            // sample k + j at ray slot slot + j * cap, terms in A_j, B_j
             if (!have) { dl_vertex<NB, FEAT>(S, P, slot, d, vx); have = true; }
-            float ul[3], ub[3];
-            int j, ns;
-            const int ln = dl_sample(S, hp, s, k, ul, ub, &j, &ns);
-            PowMemo pm;
-            FVal F;
-            estimate_direct<NB, FEAT>(S, P, slot, 0, ln, vx.bs, pm, vx.p, vx.n, vx.wo, vx.is.rayEps, vx.ray.time, ul, ub,
-                                      F, fl, out);
-            if (fl & (PF_PA | PF_PB)) break;   // the next pass adds ED
-            // nothing queued: ED = 0, added now
-            fl &= ~(PF_PEND | (PF_LIGHT_MASK << PF_LIGHT_SHIFT));
-            float4 *Lv = dl_L<NB>(P, d, slot);
-#pragma unroll
-            for (int q = 0; q < NQ; ++q) {
-                if (!all) {
-                    float4 l = Lv[q * c];
-                    const float z = 0.f * (float)nLights;
-                    l.x += z; l.y += z; l.z += z; l.w += z;
-                    Lv[q * c] = l;
-                } else {
-                    float4 ld = j == 0 ? make_float4(0.f, 0.f, 0.f, 0.f) : Ld[q * c];
-                    ld.x += 0.f; ld.y += 0.f; ld.z += 0.f; ld.w += 0.f;
-                    if (j == ns - 1) {
-                        float4 la = k + 1 == ns ? make_float4(0.f, 0.f, 0.f, 0.f) : La[q * c];
-                        const float fn = (float)ns;
-                        la.x += ld.x / fn; la.y += ld.y / fn; la.z += ld.z / fn; la.w += ld.w / fn;
-                        La[q * c] = la;
-                    } else Ld[q * c] = ld;
-                }
+            const int kEnd = min(k + P.dlBatch, K);
+            uint32_t mA = 0u, mB = 0u;
+            int lnOne = 0;
+            for (int kk = k; kk < kEnd; ++kk) {
+                const int jb = kk - k;
+                float ul[3], ub[3];
+                int j, ns;
+                const int ln = dl_sample(S, hp, s, kk, ul, ub, &j, &ns);
+                PowMemo pm;
+                FVal F;
+                uint32_t f2 = 0u;
+                Pushes o2 = {false, false, false, 0u, 0u};
+                estimate_direct<NB, FEAT>(S, P, slot, slot + jb * (int)c, P.A + (size_t)jb * NQ * c + slot,
+                                          P.B + (size_t)jb * NQ * c + slot, ln, vx.bs, pm, vx.p, vx.n, vx.wo,
+                                          vx.is.rayEps, vx.ray.time, ul, ub, F, f2, o2);
+                if (f2 & PF_PA) mA |= 1u << jb;
+                if (f2 & PF_PB) mB |= 1u << jb;
+                lnOne = ln;
             }
-            ++k;
+            if (mA | mB) {   // the next pass adds the batch
+                out.sMask = mA;
+                out.mMask = mB;
+                fl |= PF_PEND | (all ? 0u : (uint32_t)lnOne << PF_LIGHT_SHIFT);
+                P.dlMask[slot] = mA | (mB << 16);
+                break;
+            }
+            // nothing queued: every ED of the batch is 0, added now
+            for (int kk = k; kk < kEnd; ++kk)
+                dl_add<NB>(S, P, slot, d, kk, K, all, false, false, P.A + slot, P.B + slot);
+            k = kEnd;
             if (k < K) continue;
-            if (all) {
-#pragma unroll
-                for (int q = 0; q < NQ; ++q) {
-                    float4 l = Lv[q * c];
-                    const float4 la = La[q * c];
-                    l.x += la.x; l.y += la.y; l.z += la.z; l.w += la.w;
-                    Lv[q * c] = l;
-                }
-            }
             stage = 2;
         }
         if (stage == 2) {

@@ -67,6 +67,11 @@ static const int kTraceBlock = PGD_TRACE_BLOCK;
 #define PGD_STACK_LDS 8   // C2: 8 -> closest 161 -> 145 ms/frame vs 16 (r01m ablation)
 #endif
 static const int kStackLDS = PGD_STACK_LDS;
+#ifndef PGD_DL_BATCH
+#define PGD_DL_BATCH 8
+#endif
+static const int kDlBatch = PGD_DL_BATCH;   // DirectLighting light samples issued per pass (<= 16)
+static_assert(PGD_DL_BATCH >= 1 && PGD_DL_BATCH <= 16, "the batch masks hold 16 samples");
 // k_trace_pt: top-level wide nodes held in LDS per block.  Off: measured on C2 (r02k), the
 // top levels are L1/L2-resident already and the LDS tile costs occupancy -- closest-hit
 // 82 ms/frame without, 91 with 128 nodes, 113 with 256
@@ -91,7 +96,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_closest(DevScene S, PathS
     st.tbase = reinterpret_cast<float *>(lds + (size_t)S.stackDepth * blockDim.x) + threadIdx.x;
     st.stride = blockDim.x;
     const uint32_t n = P.cnt[CNT_QC(q)];
-    const uint32_t *Q = P.qC + (size_t)q * 2 * P.cap;
+    const uint32_t *Q = P.qC + (size_t)q * 2 * P.rcap;
     uint32_t nM = 0, hM = 0;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const uint32_t e = Q[i];
@@ -100,8 +105,8 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_closest(DevScene S, PathS
         int prim = -1;
         float t = INFINITY;
         if (!bvh_intersect<INST>(S, st, r, &prim, &t)) prim = -1;
-        P.hitPrim[(size_t)kind * P.cap + slot] = prim;
-        P.hitT[(size_t)kind * P.cap + slot] = t;
+        P.hitPrim[(size_t)kind * P.rcap + slot] = prim;
+        P.hitT[(size_t)kind * P.rcap + slot] = t;
         if (STATS && kind == RAY_M) { nM++; hM += prim >= 0 ? 1u : 0u; }
     }
     if (STATS) {
@@ -125,7 +130,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_shadow(DevScene S, PathSo
     st.tbase = reinterpret_cast<float *>(lds + (size_t)S.stackDepth * blockDim.x) + threadIdx.x;
     st.stride = blockDim.x;
     const uint32_t n = P.cnt[CNT_QS(q)];
-    const uint32_t *Q = P.qS + (size_t)q * P.cap;
+    const uint32_t *Q = P.qS + (size_t)q * P.rcap;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const int slot = (int)Q[i];
         Ray r = ray_load(P, RAY_S, slot);
@@ -164,7 +169,7 @@ __global__ __launch_bounds__(kTraceBlock) PGD_TRACE_ATTR void k_trace_pt(DevScen
     int bottom = 0;   // entries [0, bottom) live in gsp
     Stack st;         // work counters only
     const uint32_t n = ANY ? P.cnt[CNT_QS(q)] : P.cnt[CNT_QC(q)];
-    const uint32_t *Q = ANY ? P.qS + (size_t)q * P.cap : P.qC + (size_t)q * 2 * P.cap;
+    const uint32_t *Q = ANY ? P.qS + (size_t)q * P.rcap : P.qC + (size_t)q * 2 * P.rcap;
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = (gridDim.x * blockDim.x) >> 6;
     uint32_t next = (uint32_t)((uint64_t)n * wave / nw);
@@ -203,8 +208,8 @@ __global__ __launch_bounds__(kTraceBlock) PGD_TRACE_ATTR void k_trace_pt(DevScen
                         active = true;
                     } else if (ANY) P.occ[slot] = 0u;
                     else {
-                        P.hitPrim[(size_t)kind * P.cap + slot] = -1;
-                        P.hitT[(size_t)kind * P.cap + slot] = INFINITY;
+                        P.hitPrim[(size_t)kind * P.rcap + slot] = -1;
+                        P.hitT[(size_t)kind * P.rcap + slot] = INFINITY;
                         if (STATS && kind == RAY_M) nM++;
                     }
                 }
@@ -281,8 +286,8 @@ __global__ __launch_bounds__(kTraceBlock) PGD_TRACE_ATTR void k_trace_pt(DevScen
                 active = false;
                 if (ANY) P.occ[slot] = occluded ? 1u : 0u;
                 else {
-                    P.hitPrim[(size_t)kind * P.cap + slot] = prim;
-                    P.hitT[(size_t)kind * P.cap + slot] = prim >= 0 ? thit : INFINITY;
+                    P.hitPrim[(size_t)kind * P.rcap + slot] = prim;
+                    P.hitT[(size_t)kind * P.rcap + slot] = prim >= 0 ? thit : INFINITY;
                     st.cHits += prim >= 0 ? 1u : 0u;
                     if (STATS && kind == RAY_M) { nM++; hM += prim >= 0 ? 1u : 0u; }
                 }
@@ -326,7 +331,7 @@ __global__ __launch_bounds__(kTraceBlock) PGD_TRACE_INST_ATTR void k_trace_inst(
     int bottom = 0;   // entries [0, bottom) live in gsp
     Stack st;         // work counters only
     const uint32_t n = ANY ? P.cnt[CNT_QS(q)] : P.cnt[CNT_QC(q)];
-    const uint32_t *Q = ANY ? P.qS + (size_t)q * P.cap : P.qC + (size_t)q * 2 * P.cap;
+    const uint32_t *Q = ANY ? P.qS + (size_t)q * P.rcap : P.qC + (size_t)q * 2 * P.rcap;
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = (gridDim.x * blockDim.x) >> 6;
     uint32_t next = (uint32_t)((uint64_t)n * wave / nw);
@@ -377,8 +382,8 @@ __global__ __launch_bounds__(kTraceBlock) PGD_TRACE_INST_ATTR void k_trace_inst(
                         active = true;
                     } else if (ANY) P.occ[slot] = 0u;
                     else {
-                        P.hitPrim[(size_t)kind * P.cap + slot] = -1;
-                        P.hitT[(size_t)kind * P.cap + slot] = INFINITY;
+                        P.hitPrim[(size_t)kind * P.rcap + slot] = -1;
+                        P.hitT[(size_t)kind * P.rcap + slot] = INFINITY;
                         if (STATS && kind == RAY_M) nM++;
                     }
                 }
@@ -450,7 +455,7 @@ __global__ __launch_bounds__(kTraceBlock) PGD_TRACE_INST_ATTR void k_trace_inst(
                     }
                     const pbrtgpu_instance &I = S.insts[pr.shape_index];
                     float m[16];
-                    inst_load(inst_rec(P, slot), pr.shape_index, m, nullptr);   // the path's transform
+                    inst_load(inst_rec(P, slot_of_ray(P, slot)), pr.shape_index, m, nullptr);   // the path's transform
                     Ray ir = xray(m, ray);
                     if (I.single_prim >= 0) {
                         if (prim_test<ANY, false>(S, st, todo, I.single_prim, ir, &prim, &thit)) {
@@ -514,8 +519,8 @@ __global__ __launch_bounds__(kTraceBlock) PGD_TRACE_INST_ATTR void k_trace_inst(
                 active = false;
                 if (ANY) P.occ[slot] = occluded ? 1u : 0u;
                 else {
-                    P.hitPrim[(size_t)kind * P.cap + slot] = prim;
-                    P.hitT[(size_t)kind * P.cap + slot] = prim >= 0 ? thit : INFINITY;
+                    P.hitPrim[(size_t)kind * P.rcap + slot] = prim;
+                    P.hitT[(size_t)kind * P.rcap + slot] = prim >= 0 ? thit : INFINITY;
                     st.cHits += prim >= 0 ? 1u : 0u;
                     if (STATS && kind == RAY_M) { nM++; hM += prim >= 0 ? 1u : 0u; }
                 }
@@ -655,7 +660,7 @@ struct Timing {
 struct Lane {
     DevBuf slots;            // PathSoA storage
     DevBuf spill;            // k_trace_pt stack spill areas (closest, shadow)
-    int slotCap = 0, slotNb = 0, slotInst = 0, slotFrames = 0;
+    int slotCap = 0, slotNb = 0, slotInst = 0, slotFrames = 0, slotBatch = 0;
     PathSoA P{};
     hipStream_t s = nullptr, s2 = nullptr;
     hipEvent_t ev[2 + 6 * 8] = {};
@@ -730,16 +735,23 @@ static bool serial_mode() {
 
 // DirectLighting frame bytes per slot and frame (PathSoA::f*)
 static size_t frame_bytes(int NB) { return (size_t)8 * ((NB + 3) / 4 * 4) + 104; }
-static int ensure_slots(Lane *c, int cap, int NB, int nInst, int nFrames) {
-    if (c->slotCap == cap && c->slotNb == NB && c->slotInst == nInst && c->slotFrames == nFrames) return 0;
-    const size_t C = (size_t)cap;
+// DirectLighting bytes per slot and batched light sample: A, B terms and the ray records
+static size_t batch_bytes(int NB) { return (size_t)8 * ((NB + 3) / 4 * 4) + 27 * 4 + 8 + 8 + 4 + 24; }
+// batch: ray slots per slot (light samples a DirectLighting pass issues; 1 for the other integrators)
+static int ensure_slots(Lane *c, int cap, int NB, int nInst, int nFrames, int batch) {
+    if (c->slotCap == cap && c->slotNb == NB && c->slotInst == nInst && c->slotFrames == nFrames &&
+        c->slotBatch == batch)
+        return 0;
+    const size_t C = (size_t)cap, R = C * (size_t)batch, AB = (size_t)std::max(2, batch);
     const int NBP = (NB + 3) / 4 * 4;   // bands padded to whole float4 quads
     size_t off = 0;
     auto take = [&](size_t bytes) { size_t o = off; off += (bytes + 255) & ~(size_t)255; return o; };
     size_t oItem = take(C * 4), oHp = take(C * 4), oSmp = take(C * 4), oBounce = take(C * 4), oFlags = take(C * 4),
-           oMt = take(C * 20), oBeta = take(C * 3 * NBP * 4), oL = take(C * NBP * 4), oA = take(C * 2 * NBP * 4),
-           oB = take(C * 2 * NBP * 4), oM = take(C * NBP * 4), oK = take(C * NBP * 4), oPix = take(C * 4), oRay = take(C * 27 * 4), oHitP = take(C * 8), oHitT = take(C * 8), oOcc = take(C * 4),
-           oQC = take(C * 16), oQS = take(C * 8), oCnt = take(CNT_WORDS * 4), oInst = take(C * (size_t)nInst * 128);
+           oMt = take(C * 20), oBeta = take(C * 3 * NBP * 4), oL = take(C * NBP * 4), oA = take(C * AB * NBP * 4),
+           oB = take(C * AB * NBP * 4), oM = take(C * NBP * 4), oK = take(C * NBP * 4), oPix = take(C * 4),
+           oRay = take(R * 27 * 4), oHitP = take(R * 8), oHitT = take(R * 8), oOcc = take(R * 4), oQC = take(R * 16),
+           oQS = take(R * 8), oCnt = take(CNT_WORDS * 4), oInst = take(C * (size_t)nInst * 128),
+           oMask = take(nFrames ? C * 4 : 0);
     const size_t F = (size_t)nFrames;
     size_t oFL = take(C * F * NBP * 4), oFF = take(C * F * NBP * 4), oFRay = take(C * F * 36), oFDiff = take(C * F * 48),
            oFS = take(C * F * 8), oFHit = take(C * F * 8), oFBr = take(C * F * 4), oDlk = take(nFrames ? C * 4 : 0);
@@ -747,6 +759,9 @@ static int ensure_slots(Lane *c, int cap, int NB, int nInst, int nFrames) {
     char *base = (char *)c->slots.p;
     PathSoA &P = c->P;
     P.cap = cap;
+    P.rcap = (int)R;
+    P.dlBatch = batch;
+    P.dlMask = nFrames ? (uint32_t *)(base + oMask) : nullptr;
     P.item = (int *)(base + oItem); P.hp = (uint32_t *)(base + oHp); P.smp = (uint32_t *)(base + oSmp);
     P.bounce = (int *)(base + oBounce); P.flags = (uint32_t *)(base + oFlags); P.mt = (uint32_t *)(base + oMt);
     P.beta = (float4 *)(base + oBeta); P.L = (float4 *)(base + oL); P.A = (float4 *)(base + oA); P.B = (float4 *)(base + oB);
@@ -766,6 +781,7 @@ static int ensure_slots(Lane *c, int cap, int NB, int nInst, int nFrames) {
     P.fBr = nFrames ? (uint32_t *)(base + oFBr) : nullptr;
     P.dlk = nFrames ? (uint32_t *)(base + oDlk) : nullptr;
     c->slotFrames = nFrames;
+    c->slotBatch = batch;
     c->slotCap = cap;
     c->slotNb = NB;
     c->slotInst = nInst;
@@ -814,6 +830,8 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
                   : c->S.integrator == PBRTGPU_INTEGRATOR_METADATA ? launch_shade_meta<NB>
                   : c->feat ? launch_shade<NB, FEAT_ALL> : launch_shade<NB, 0>;
     const int nFrames = dl ? std::max(1, c->S.maxDepth) : 0;
+    // DirectLighting issues up to kDlBatch light samples of a vertex per pass
+    const int batch = dl ? std::max(1, std::min(c->S.dlStrategy == PBRTGPU_DL_ONE ? 1 : c->S.dlK, kDlBatch)) : 1;
     // passes one path can take: the camera ray + maxdepth + 1 vertices + 1 finish (path); per
     // vertex of the DirectLighting recursion (at most 2^maxdepth - 1) its hit + one pass per
     // light sample, + the output
@@ -832,8 +850,9 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
         r.src.base = src.base + lo;
         r.src.nItems = hi - lo;
         r.cap = (int)std::min<uint32_t>(r.src.nItems, (uint32_t)std::max(64, slot_target() / nl));
-        if (dl)   // the frame stacks: at most 16 GiB per lane
-            r.cap = (int)std::max<size_t>(64, std::min<size_t>((size_t)r.cap, ((size_t)16 << 30) / (frame_bytes(NB) * nFrames)));
+        if (dl)   // the frame stacks and light-sample batches: at most 24 GiB per lane
+            r.cap = (int)std::max<size_t>(64, std::min<size_t>((size_t)r.cap, ((size_t)24 << 30) /
+                                                               (frame_bytes(NB) * nFrames + batch_bytes(NB) * batch)));
         r.grid = (r.cap + kShadeBlock - 1) / kShadeBlock;
         r.q = 0;
         r.batch = 0;
@@ -844,7 +863,7 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
         r.passes = 0;
         r.maxPasses = (int)std::min<int64_t>(INT32_MAX / 2, 2 * ((r.src.nItems + r.cap - 1) / r.cap + 1) * pathPasses) +
                       2 * kPassBatch;
-        if (int e = ensure_slots(&L, r.cap, NB, c->S.nInsts, nFrames)) return e;
+        if (int e = ensure_slots(&L, r.cap, NB, c->S.nInsts, nFrames, batch)) return e;
         HIPCHK(L.spill.ensure(2 * spillLane * sizeof(uint2)));
         if (l > 0) HIPCHK(hipStreamWaitEvent(L.s, c->ev[0], 0));
         HIPCHK(hipMemsetAsync(L.P.item, 0xff, (size_t)r.cap * 4, L.s));

@@ -58,6 +58,28 @@ __device__ __forceinline__ uint32_t block_push(bool flag, uint32_t *counter, uin
     return idx;
 }
 
+// block_push for n >= 0 entries per thread: returns the index of this thread's first entry
+__device__ __forceinline__ uint32_t block_push_n(uint32_t n, uint32_t *counter, uint32_t *lds4) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t x = n;   // inclusive scan over the wave
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) lds4[wave] = x;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t tot = 0;
+        for (int w = 0; w < (int)(blockDim.x >> 6); ++w) { uint32_t v = lds4[w]; lds4[w] = tot; tot += v; }
+        lds4[15] = tot ? atomicAdd(counter, tot) : 0u;
+    }
+    __syncthreads();
+    const uint32_t idx = lds4[15] + lds4[wave] + (x - n);
+    __syncthreads();
+    return idx;
+}
+
 // shading pass over every slot: finish / advance live paths, regenerate free slots, and
 // queue the next pass's rays into queue set qout (block-aggregated queue pushes)
 // occupancy target: 3 waves/SIMD (<= 168 VGPRs) for <= 32 bands costs a few spilled
@@ -110,12 +132,21 @@ __global__ __launch_bounds__(kShadeBlock) PGD_SHADE_ATTR void k_shade(DevScene S
     }
     PGD_T1(REGEN);
     PGD_T0(PUSH);
+    uint32_t *qC = P.qC + (size_t)qout * 2 * P.rcap, *qS = P.qS + (size_t)qout * P.rcap;
     const uint32_t kc = block_push(pu.c, &P.cnt[CNT_QC(qout)], lds4);
-    if (pu.c) P.qC[(size_t)qout * 2 * P.cap + kc] = (uint32_t)slot << 1;
-    const uint32_t km = block_push(pu.m, &P.cnt[CNT_QC(qout)], lds4);
-    if (pu.m) P.qC[(size_t)qout * 2 * P.cap + km] = ((uint32_t)slot << 1) | 1u;
-    const uint32_t ks = block_push(pu.s, &P.cnt[CNT_QS(qout)], lds4);
-    if (pu.s) P.qS[(size_t)qout * P.cap + ks] = (uint32_t)slot;
+    if (pu.c) qC[kc] = (uint32_t)slot << 1;
+    if (MODE == MODE_DL) {   // a batch of light samples: ray slots slot + j * cap
+        uint32_t km = block_push_n((uint32_t)__popc(pu.mMask), &P.cnt[CNT_QC(qout)], lds4);
+        for (uint32_t m = pu.mMask; m; m &= m - 1u)
+            qC[km++] = ((uint32_t)(slot + (__ffs(m) - 1) * P.cap) << 1) | 1u;
+        uint32_t ks = block_push_n((uint32_t)__popc(pu.sMask), &P.cnt[CNT_QS(qout)], lds4);
+        for (uint32_t m = pu.sMask; m; m &= m - 1u) qS[ks++] = (uint32_t)(slot + (__ffs(m) - 1) * P.cap);
+    } else {
+        const uint32_t km = block_push(pu.m, &P.cnt[CNT_QC(qout)], lds4);
+        if (pu.m) qC[km] = ((uint32_t)slot << 1) | 1u;
+        const uint32_t ks = block_push(pu.s, &P.cnt[CNT_QS(qout)], lds4);
+        if (pu.s) qS[ks] = (uint32_t)slot;
+    }
     PGD_T1(PUSH);
 #ifdef PGD_SECTIONS
     __syncthreads();

@@ -76,12 +76,15 @@ struct PathSoA {
     float4 *A, *B;      // [2][NQ][cap]: pending direct-light terms of vertex v in buffer v & 1
     float4 *M;          // [NQ][cap]: measured-BRDF spectrum of the BSDF value being consumed
     float4 *K;          // [NQ][cap]: the material's textured spectrum at the current vertex
-    float *ray;         // [3][9][cap]: o.xyz, d.xyz, mint, maxt, time  for RAY_C, RAY_M, RAY_S
-    int *hitPrim;       // [2][cap]  (RAY_C, RAY_M)
-    float *hitT;        // [2][cap]
-    uint32_t *occ;      // [cap]
-    uint32_t *qC;       // [2][2*cap]: (slot << 1) | kind
-    uint32_t *qS;       // [2][cap]
+    // ray records are indexed by ray slot rs: the slot itself, or (DirectLighting, a batch of
+    // light samples per pass) slot + j * cap for the batch's sample j; rcap = cap x batch
+    int rcap;
+    float *ray;         // [3][9][rcap]: o.xyz, d.xyz, mint, maxt, time  for RAY_C, RAY_M, RAY_S
+    int *hitPrim;       // [2][rcap]  (RAY_C, RAY_M)
+    float *hitT;        // [2][rcap]
+    uint32_t *occ;      // [rcap]
+    uint32_t *qC;       // [2][2*rcap]: (ray slot << 1) | kind
+    uint32_t *qS;       // [2][rcap]: ray slot
     uint32_t *cnt;      // counters (CNT_*), work counters as u64 from word CNT_WORK
     float4 *instM;      // [cap][nInst][8]: the path's instance transforms (inst_load), or null
     int nInst;
@@ -95,8 +98,12 @@ struct PathSoA {
     float *fS;          // [nFrames][2][cap]: |wi . n| and pdf of the pending child
     int *fHit;          // [nFrames][2][cap]: hit primitive, hit t (bits) of the incoming ray
     uint32_t *fBr;      // [nFrames][cap]: specular branches tried (0, 1 reflect, 2 transmit)
-    uint32_t *dlk;      // [cap]: light-sample cursor of the top vertex
+    uint32_t *dlk;      // [cap]: light-sample cursor of the top vertex (first sample of its batch)
+    uint32_t *dlMask;   // [cap]: the batch's queued shadow rays (bits 0-15) and MIS rays (16-31)
+    int dlBatch;        // light samples issued per pass (<= 16); A, B hold [dlBatch][NQ][cap]
 };
+// the slot a ray slot belongs to
+PGD_INLINE int slot_of_ray(const PathSoA &P, int rs) { return rs < P.cap ? rs : rs % P.cap; }
 // the path's instance-transform record (null without instances)
 PGD_INLINE const float4 *inst_rec(const PathSoA &P, int slot) {
     return P.nInst ? P.instM + (size_t)slot * P.nInst * 8 : nullptr;
@@ -112,16 +119,16 @@ struct ItemSrc {
     uint32_t base;
 };
 
-PGD_INLINE void ray_store(const PathSoA &P, int kind, int slot, const Ray &r) {
-    float *b = P.ray + (size_t)kind * 9 * P.cap + slot;
-    const size_t c = P.cap;
+PGD_INLINE void ray_store(const PathSoA &P, int kind, int rs, const Ray &r) {
+    float *b = P.ray + (size_t)kind * 9 * P.rcap + rs;
+    const size_t c = P.rcap;
     b[0] = r.o.x; b[c] = r.o.y; b[2 * c] = r.o.z;
     b[3 * c] = r.d.x; b[4 * c] = r.d.y; b[5 * c] = r.d.z;
     b[6 * c] = r.mint; b[7 * c] = r.maxt; b[8 * c] = r.time;
 }
-PGD_INLINE Ray ray_load(const PathSoA &P, int kind, int slot) {
-    const float *b = P.ray + (size_t)kind * 9 * P.cap + slot;
-    const size_t c = P.cap;
+PGD_INLINE Ray ray_load(const PathSoA &P, int kind, int rs) {
+    const float *b = P.ray + (size_t)kind * 9 * P.rcap + rs;
+    const size_t c = P.rcap;
     Ray r;
     r.o = v3(b[0], b[c], b[2 * c]);
     r.d = v3(b[3 * c], b[4 * c], b[5 * c]);
@@ -476,8 +483,9 @@ PGD_INLINE bool path_output(const DevScene &S, const float4 (&L)[Bands<NB>::NQ],
     return bad;
 }
 
-// ray requests produced by one shade step
-struct Pushes { bool c, m, s; };
+// ray requests produced by one shade step (DirectLighting batches: the MIS / shadow rays of
+// batch samples j at ray slots slot + j * cap, bit j of mMask / sMask)
+struct Pushes { bool c, m, s; uint32_t mMask, sMask; };
 
 // Additions to L a vertex makes before its direct light is known, in order: emitted
 // radiance (path.cpp:67-68; bounce 0 or after a specular bounce) and the zero direct light
@@ -493,10 +501,11 @@ struct LAdds {
 // normal n, BSDF bs): the light-sample term goes to A_vb with its shadow ray (PF_PA), the
 // BSDF-sample term with MIS to B_vb with its MIS ray (PF_PB); the caller adds (0 [+ A]) [+ B]
 // when the rays are answered.  Sets PF_PEND and the light index in fl.
+// A, B: the slot's term buffers for this sample; rs: the ray slot its shadow / MIS rays use.
 template <int NB, int FEAT>
-PGD_INLINE void estimate_direct(const DevScene &S, const PathSoA &P, int slot, int vb, int lightNum, const BSDF &bs,
-                                PowMemo &pm, V p, V n, V wo, float rayEps, float time, const float ul[3],
-                                const float ub[3], FVal &F, uint32_t &fl, Pushes &out) {
+PGD_INLINE void estimate_direct(const DevScene &S, const PathSoA &P, int slot, int rs, float4 *A, float4 *B,
+                                int lightNum, const BSDF &bs, PowMemo &pm, V p, V n, V wo, float rayEps, float time,
+                                const float ul[3], const float ub[3], FVal &F, uint32_t &fl, Pushes &out) {
     constexpr int NQ = Bands<NB>::NQ;
     const size_t c = P.cap;
     const float *sp = S.spectra;
@@ -522,7 +531,6 @@ PGD_INLINE void estimate_direct(const DevScene &S, const PathSoA &P, int slot, i
             sc = fabsf(vdot(wi, n)) * weight / lightPdf;
         }
         // A_i = (f_i * Li_i) * sc ; written while testing f for black (A unused if black)
-        float4 *A = A_of<NB>(P, vb, slot);
         bool black = true;
 #pragma unroll
         for (int q = 0; q < NQ; ++q) {
@@ -537,7 +545,7 @@ PGD_INLINE void estimate_direct(const DevScene &S, const PathSoA &P, int slot, i
         if (!black) {
             Ray sr;
             sr.o = vis.o; sr.d = vis.d; sr.mint = vis.mint; sr.maxt = vis.maxt; sr.time = time;
-            ray_store(P, RAY_S, slot, sr);
+            ray_store(P, RAY_S, rs, sr);
             fl |= PF_PA;
             out.s = true;
         }
@@ -576,7 +584,6 @@ PGD_INLINE void estimate_direct(const DevScene &S, const PathSoA &P, int slot, i
             }
             if (go && !emit_black<NB, FEAT>(S, eb)) {
                 const float ad = fabsf(vdot(wi, n));
-                float4 *B = B_of<NB>(P, vb, slot);
                 bool black = true;
 #pragma unroll
                 for (int q = 0; q < NQ; ++q) {
@@ -589,7 +596,7 @@ PGD_INLINE void estimate_direct(const DevScene &S, const PathSoA &P, int slot, i
                     B[q * c] = b;
                 }
                 if (!black) {
-                    ray_store(P, RAY_M, slot, mr);
+                    ray_store(P, RAY_M, rs, mr);
                     fl |= PF_PB;
                     out.m = true;
                 }
@@ -676,7 +683,8 @@ PGD_INLINE Pushes shade_vertex(const DevScene &S, const PathSoA &P, int slot, in
         }
         int lightNum = (int)floorf(ulnum * nLights);
         if (lightNum > nLights - 1) lightNum = nLights - 1;
-        estimate_direct<NB, FEAT>(S, P, slot, vb, lightNum, bs, pm, p, n, wo, is.rayEps, ray.time, ul, ub, F, fl, out);
+        estimate_direct<NB, FEAT>(S, P, slot, slot, A_of<NB>(P, vb, slot), B_of<NB>(P, vb, slot), lightNum, bs, pm, p, n,
+                                  wo, is.rayEps, ray.time, ul, ub, F, fl, out);
         if (!(fl & (PF_PA | PF_PB))) {
             // nothing can add to Ld: finish now (L += beta * (nLights * 0), nLights * 0 == 0)
             la->zero = true;
@@ -781,11 +789,11 @@ PGD_INLINE Pushes shade_slot(const DevScene &S, const PathSoA &P, int slot, floa
         useA = (fl & PF_PA) && !P.occ[slot];
         if (fl & PF_PB) {
             const int ln = (int)(fl >> PF_LIGHT_SHIFT);
-            int mp = P.hitPrim[c + slot];
+            int mp = P.hitPrim[P.rcap + slot];
             if ((FEAT & FEAT_INF) && S.lights[ln].type == PBRTGPU_LIGHT_INFINITE) useB = mp < 0;   // Li = light->Le(ray)
             else if (mp >= 0 && S.prims[mp].area_light == ln) {
                 Ray mr = ray_load(P, RAY_M, slot);
-                useB = vdot(isect_nn(S, mr, mp, P.hitT[c + slot], inst_rec(P, slot)), vneg(mr.d)) > 0.f;   // DiffuseAreaLight::L
+                useB = vdot(isect_nn(S, mr, mp, P.hitT[P.rcap + slot], inst_rec(P, slot)), vneg(mr.d)) > 0.f;   // DiffuseAreaLight::L
             }
         }
         fl &= ~(PF_PEND | PF_PA | PF_PB);
