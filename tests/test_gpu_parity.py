@@ -392,6 +392,7 @@ def test_direct_lighting_recursion_and_regeneration(pg, monkeypatch, strategy, m
         L = d.trace_paths(keys)
         d.render()
         film = d.film()
+        assert np.array_equal(L.view(np.int32), d.trace_paths(keys).view(np.int32))   # deterministic
         monkeypatch.setenv("PBRTGPU_SLOTS", "193")
         Ls = d.trace_paths(keys)
         d.render()
