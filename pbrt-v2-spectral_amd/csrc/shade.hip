@@ -38,46 +38,15 @@ extern "C" int PGD_CAT(pgd_sections_read_, SHADE_NB, SHADE_FEAT)(unsigned long l
 #endif
 #endif
 
-// Block-wide exclusive prefix of a per-thread flag with ONE atomicAdd per block on
-// *counter; returns this thread's index (valid where flag is set).  All threads of the
-// block must call it (it contains barriers).
-__device__ __forceinline__ uint32_t block_push(bool flag, uint32_t *counter, uint32_t *lds4) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const unsigned long long m = __ballot(flag);
-    const uint32_t before = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-    if (lane == 0) lds4[wave] = (uint32_t)__popcll(m);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t tot = 0;
-        for (int w = 0; w < (int)(blockDim.x >> 6); ++w) { uint32_t v = lds4[w]; lds4[w] = tot; tot += v; }
-        lds4[15] = tot ? atomicAdd(counter, tot) : 0u;
-    }
-    __syncthreads();
-    const uint32_t idx = lds4[15] + lds4[wave] + before;
-    __syncthreads();   // lds4 is reused by the next call
-    return idx;
-}
-
-// block_push for n >= 0 entries per thread: returns the index of this thread's first entry
-__device__ __forceinline__ uint32_t block_push_n(uint32_t n, uint32_t *counter, uint32_t *lds4) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    uint32_t x = n;   // inclusive scan over the wave
+// inclusive prefix sum over the wave's 64 lanes
+__device__ __forceinline__ uint32_t wave_scan(uint32_t x) {
+    const int lane = threadIdx.x & 63;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
         const uint32_t y = __shfl_up(x, o);
         if (lane >= o) x += y;
     }
-    if (lane == 63) lds4[wave] = x;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t tot = 0;
-        for (int w = 0; w < (int)(blockDim.x >> 6); ++w) { uint32_t v = lds4[w]; lds4[w] = tot; tot += v; }
-        lds4[15] = tot ? atomicAdd(counter, tot) : 0u;
-    }
-    __syncthreads();
-    const uint32_t idx = lds4[15] + lds4[wave] + (x - n);
-    __syncthreads();
-    return idx;
+    return x;
 }
 
 // shading pass over every slot: finish / advance live paths, regenerate free slots, and
@@ -102,7 +71,6 @@ enum { MODE_PATH = 0, MODE_DL = 1, MODE_META = 2 };
 template <int NB, int FEAT, int MODE>
 __global__ __launch_bounds__(kShadeBlock) PGD_SHADE_ATTR void k_shade(DevScene S, PathSoA P, ItemSrc src, int qout,
                                                        float *__restrict__ Lout) {
-    __shared__ uint32_t lds4[16];
 #ifdef PGD_SECTIONS
     if (threadIdx.x < SEC_N) pgd_secs[threadIdx.x] = 0;
     __syncthreads();
@@ -110,7 +78,7 @@ __global__ __launch_bounds__(kShadeBlock) PGD_SHADE_ATTR void k_shade(DevScene S
     if (FEAT & FEAT_MEAS) kd_lds_fill(S);   // the measured-BRDF kd-trees, once per block
     const int slot = blockIdx.x * blockDim.x + threadIdx.x;
     const bool inRange = slot < P.cap;
-    Pushes pu = {false, false, false};
+    Pushes pu = {false, false, false, 0u, 0u};
     bool freeSlot = inRange && P.item[slot] < 0;
     bool zeroed = false;
     if (inRange && !freeSlot) {
@@ -124,28 +92,60 @@ __global__ __launch_bounds__(kShadeBlock) PGD_SHADE_ATTR void k_shade(DevScene S
         const unsigned long long m = __ballot(zeroed);
         if ((threadIdx.x & 63) == 0) atomicAdd(&P.cnt[CNT_ZEROED], (uint32_t)__popcll(m));
     }
-    // regeneration: free slots take the next camera samples
-    PGD_T0(REGEN);
-    const bool want = freeSlot && *(volatile uint32_t *)&P.cnt[CNT_NEXT] < src.nItems;
-    if (__syncthreads_or(want)) {
-        const uint32_t it = block_push(want, &P.cnt[CNT_NEXT], lds4);
-        if (want && it < src.nItems) { path_start<NB>(S, P, src, slot, it); pu.c = true; }
-    }
-    PGD_T1(REGEN);
+    // Regeneration and the queue pushes of the block in one step -- one pair of barriers and at
+    // most three atomics per block: free slots take the next camera samples; the closest-hit
+    // queue gets the block's continuation / child rays, then the regenerated camera rays, then
+    // the MIS rays; the shadow queue the shadow rays.  Entries are in block order.
     PGD_T0(PUSH);
+    __shared__ uint32_t qsh[24];   // per wave [w][4]: want, C, M, S (totals -> offsets); bases
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    const bool want = freeSlot && *(volatile uint32_t *)&P.cnt[CNT_NEXT] < src.nItems;
+    const unsigned long long bW = __ballot(want), bC = __ballot(pu.c);
+    uint32_t pm, ps, tm, ts;   // this thread's prefix and the wave total, MIS / shadow entries
+    if (MODE == MODE_DL) {   // a batch of light samples per slot: ray slots slot + j * cap
+        const uint32_t nm = (uint32_t)__popc(pu.mMask), ns = (uint32_t)__popc(pu.sMask);
+        const uint32_t im = wave_scan(nm), is = wave_scan(ns);
+        pm = im - nm; ps = is - ns;
+        tm = __shfl(im, 63); ts = __shfl(is, 63);
+    } else {
+        const unsigned long long bM = __ballot(pu.m), bS = __ballot(pu.s);
+        pm = (uint32_t)__popcll(bM & lt); ps = (uint32_t)__popcll(bS & lt);
+        tm = (uint32_t)__popcll(bM); ts = (uint32_t)__popcll(bS);
+    }
+    if (lane == 0) {
+        qsh[4 * wave + 0] = (uint32_t)__popcll(bW); qsh[4 * wave + 1] = (uint32_t)__popcll(bC);
+        qsh[4 * wave + 2] = tm; qsh[4 * wave + 3] = ts;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t[4] = {0u, 0u, 0u, 0u};
+        for (int w = 0; w < (int)(blockDim.x >> 6); ++w)
+            for (int k = 0; k < 4; ++k) { const uint32_t v = qsh[4 * w + k]; qsh[4 * w + k] = t[k]; t[k] += v; }
+        const uint32_t nb = t[0] ? atomicAdd(&P.cnt[CNT_NEXT], t[0]) : 0u;
+        const uint32_t nReg = nb >= src.nItems ? 0u : min(t[0], src.nItems - nb);
+        const uint32_t nQC = t[1] + nReg + t[2];
+        qsh[16] = nb; qsh[17] = nReg; qsh[18] = nQC ? atomicAdd(&P.cnt[CNT_QC(qout)], nQC) : 0u;
+        qsh[19] = t[3] ? atomicAdd(&P.cnt[CNT_QS(qout)], t[3]) : 0u;
+        qsh[20] = t[1];
+    }
+    __syncthreads();
     uint32_t *qC = P.qC + (size_t)qout * 2 * P.rcap, *qS = P.qS + (size_t)qout * P.rcap;
-    const uint32_t kc = block_push(pu.c, &P.cnt[CNT_QC(qout)], lds4);
-    if (pu.c) qC[kc] = (uint32_t)slot << 1;
-    if (MODE == MODE_DL) {   // a batch of light samples: ray slots slot + j * cap
-        uint32_t km = block_push_n((uint32_t)__popc(pu.mMask), &P.cnt[CNT_QC(qout)], lds4);
-        for (uint32_t m = pu.mMask; m; m &= m - 1u)
-            qC[km++] = ((uint32_t)(slot + (__ffs(m) - 1) * P.cap) << 1) | 1u;
-        uint32_t ks = block_push_n((uint32_t)__popc(pu.sMask), &P.cnt[CNT_QS(qout)], lds4);
+    const uint32_t qcBase = qsh[18], nC = qsh[20], nReg = qsh[17];
+    if (pu.c) qC[qcBase + qsh[4 * wave + 1] + (uint32_t)__popcll(bC & lt)] = (uint32_t)slot << 1;
+    if (want) {
+        const uint32_t r = qsh[4 * wave + 0] + (uint32_t)__popcll(bW & lt);   // block order among free slots
+        if (r < nReg) {
+            path_start<NB>(S, P, src, slot, qsh[16] + r);
+            qC[qcBase + nC + r] = (uint32_t)slot << 1;
+        }
+    }
+    uint32_t km = qcBase + nC + nReg + qsh[4 * wave + 2] + pm, ks = qsh[19] + qsh[4 * wave + 3] + ps;
+    if (MODE == MODE_DL) {
+        for (uint32_t m = pu.mMask; m; m &= m - 1u) qC[km++] = ((uint32_t)(slot + (__ffs(m) - 1) * P.cap) << 1) | 1u;
         for (uint32_t m = pu.sMask; m; m &= m - 1u) qS[ks++] = (uint32_t)(slot + (__ffs(m) - 1) * P.cap);
     } else {
-        const uint32_t km = block_push(pu.m, &P.cnt[CNT_QC(qout)], lds4);
         if (pu.m) qC[km] = ((uint32_t)slot << 1) | 1u;
-        const uint32_t ks = block_push(pu.s, &P.cnt[CNT_QS(qout)], lds4);
         if (pu.s) qS[ks] = (uint32_t)slot;
     }
     PGD_T1(PUSH);
