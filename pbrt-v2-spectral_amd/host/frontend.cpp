@@ -25,6 +25,7 @@
 #include <memory>
 #include <stdexcept>
 #include <algorithm>
+#include <chrono>
 #include <functional>
 
 namespace pbrtamd {
@@ -508,6 +509,7 @@ public:
         searchDir = sl == std::string::npos ? std::string(".") : path.substr(0, sl);
     }
     void Run(const std::string &path) {
+        tLoad0 = std::chrono::steady_clock::now();
         if (!lex.Open(path)) throw std::runtime_error("cannot open scene file " + path);
         Parse();
         if (!worldEnded) throw std::runtime_error("scene has no WorldEnd");
@@ -533,6 +535,7 @@ private:
 
     RenderOverrides ov;
     HostScene *out;
+    std::chrono::steady_clock::time_point tLoad0;
     SpectrumCtx spec;
     Lexer lex;
     std::string searchDir;
@@ -1653,7 +1656,12 @@ private:
         for (auto &po : primitives) out->metaMesh.push_back(std::make_pair(po.refId, po.name));
         for (auto &nm : gs.namedMaterials)
             if (nm.second) out->metaMaterials.push_back(std::make_pair(nm.second->refId, nm.first));
+        const auto tb0 = std::chrono::steady_clock::now();
         top.Build();
+        if (getenv("PBRTHOST_TIMING"))
+            fprintf(stderr, "pbrthost: parse+refine %.1f ms, top-level BVH build %.1f ms\n",
+                    std::chrono::duration<double, std::milli>(tb0 - tLoad0).count(),
+                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tb0).count());
         out->bvhMaxDepth = top.maxDepth;
         size_t nNodes = top.bnodes.size();
         for (auto &B : blas) nNodes += B.bnodes.size();

@@ -2,14 +2,17 @@
 # GPU-box profiling recipe for one config: rocprofv3 kernel trace + stats of the bench
 # command (default mode and serial mode), then separate PMC passes (FETCH_SIZE, WRITE_SIZE,
 # two SQ groups) over one serial-mode frame (no concurrent kernels: one frame's launches,
-# each counted once).  Usage (repo root, GPU box): bash tools/gpu_profile.sh TAG [config]
+# each counted once).  Usage (repo root, GPU box): bash tools/gpu_profile.sh TAG [config [bench args]]
+# (e.g. bash tools/gpu_profile.sh r02n_dl c2 --integrator directlighting)
 set -e
 TAG=${1:-r02}
 CFG=${2:-c2}
+shift 2 || true
+EXTRA="$*"
 OUT=$PWD/gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
-B="bench.py --config $CFG --no-cpu --no-roofline"
+B="bench.py --config $CFG --no-cpu --no-roofline $EXTRA"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run -- python3 $B --steps 2 --warmup 1 > $OUT/bench_trace.json 2> $OUT/trace.err
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace_serial -o run -- python3 $B --steps 1 --warmup 1 --serial > $OUT/bench_trace_serial.json 2> $OUT/trace_serial.err
 timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch -o run -- python3 $B --steps 1 --warmup 0 --serial > $OUT/pmc1.json 2> $OUT/pmc1.err
