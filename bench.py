@@ -228,9 +228,10 @@ def main():
     ap.add_argument("--scene", default=None, help="scene pack (default: the config's)")
     ap.add_argument("--res", type=int, default=-1, help="square resolution override (default: the config's)")
     ap.add_argument("--spp", type=int, default=-1, help="spp override (default: the config's)")
-    ap.add_argument("--integrator", choices=["path", "directlighting"], default="path",
-                    help="SurfaceIntegrator (BASELINE configs: path; directlighting = SURVEY §8(f) row)")
-    ap.add_argument("--strategy", choices=["all", "one"], default="all", help="DirectLighting strategy")
+    ap.add_argument("--integrator", choices=["path", "directlighting", "metadata"], default="path",
+                    help="SurfaceIntegrator (BASELINE configs: path; directlighting / metadata = SURVEY §8(f) rows)")
+    ap.add_argument("--strategy", choices=["all", "one", "mesh", "material", "depth"], default=None,
+                    help="DirectLighting (all / one) or metadata (mesh / material / depth) strategy")
     ap.add_argument("--shard", choices=["tiles", "frames"], default="tiles")
     ap.add_argument("--tile", type=int, default=16)
     ap.add_argument("--slices", type=int, default=1, help="tile slices per GPU (single-process --gpus N)")
@@ -260,7 +261,7 @@ def main():
                           spp=args.spp, seed=rank if args.shard == "frames" else 0,
                           integrator=args.integrator, strategy=args.strategy)
     if args.integrator != "path":
-        desc = desc.replace("path maxdepth", "directlighting (%s) maxdepth" % args.strategy)
+        desc = desc.replace("path maxdepth", "%s (%s) maxdepth" % (args.integrator, args.strategy or "scene"))
     info = scene.info()
     tile = (args.tile, args.tile)
     ntx, nty = pg.tile_grid(scene, tile)
