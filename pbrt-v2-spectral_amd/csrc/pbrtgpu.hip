@@ -1503,11 +1503,9 @@ static int render_impl(pbrtgpu_ctx *c, const pbrtgpu_render_desc *d, const int32
                 return a.z < b.z;
             });
             HIPCHK(hipMemcpy(c->keys.p, keys.data(), nSpill * sizeof(int3), hipMemcpyHostToDevice));
+            // the spill samples are traced with the first batch (items after its pixel
+            // samples), so they cost no wavefront fill and drain of their own
             HIPCHK(c->spillL.ensure((size_t)nSpill * NB * 4));
-            ItemSrc ks{};
-            ks.keys = (const int3 *)c->keys.p;
-            ks.nItems = (uint32_t)nSpill;
-            if (int e = run_wavefront<NB>(c, ks, (float *)c->spillL.p, countWork, T, nullptr)) return e;
             // contributions per target pixel, split into pre (source before the target's own
             // sample pixel in row-major order) and post
             const int ew = cam.sx_end - cam.sx_start;
@@ -1567,13 +1565,12 @@ static int render_impl(pbrtgpu_ctx *c, const pbrtgpu_render_desc *d, const int32
         HIPCHK(hipStreamSynchronize(c->stream));   // host vectors are reused right after
         return 0;
     };
-    if (int e = applyLists(preT, preStart, preSrc)) return e;
 
     // ---- main batches: per-sample radiance for (pixels x batch samples), then the ordered film sum
     const size_t lbudget = lbuf_budget();   // per-sample radiance per batch
     int sb = (int)std::max<long>(1, std::min<long>(s1 - s0, (long)(lbudget / ((size_t)nPix * NB * 4))));
-    if ((uint64_t)nPix * sb > 0x7fffffffull) sb = std::max(1, (int)(0x7fffffffll / nPix));
-    HIPCHK(c->Lbuf.ensure((size_t)nPix * sb * NB * 4));
+    if ((uint64_t)nPix * sb + nSpill > 0x7fffffffull) sb = std::max(1, (int)((0x7fffffffll - nSpill) / nPix));
+    HIPCHK(c->Lbuf.ensure(((size_t)nPix * sb + nSpill) * NB * 4));
     for (int b0 = s0; b0 < s1; b0 += sb) {
         int n = std::min(sb, s1 - b0);
         ItemSrc src{};
@@ -1581,7 +1578,18 @@ static int render_impl(pbrtgpu_ctx *c, const pbrtgpu_render_desc *d, const int32
         src.sb = n;
         src.s0 = b0;
         src.nItems = (uint32_t)((long)nPix * n);
+        const bool withSpills = b0 == s0 && nSpill > 0;
+        if (withSpills) {
+            src.keys = (const int3 *)c->keys.p;
+            src.keyBase = src.nItems;
+            src.nItems += (uint32_t)nSpill;
+        }
         if (int e = run_wavefront<NB>(c, src, (float *)c->Lbuf.p, countWork, T, &zeroed)) return e;
+        if (withSpills) {   // keep the spill radiance (later batches reuse Lbuf), add the pre lists
+            HIPCHK(hipMemcpyAsync(c->spillL.p, (const float *)c->Lbuf.p + (size_t)src.keyBase * NB,
+                                  (size_t)nSpill * NB * 4, hipMemcpyDeviceToDevice, c->stream));
+            if (int e = applyLists(preT, preStart, preSrc)) return e;
+        }
         long na = (long)nPix * NB;
         HIPCHK(hipEventRecord(c->ev[6], c->stream));
         hipLaunchKernelGGL(k_accum<NB>, dim3((na + 255) / 256), dim3(256), 0, c->stream, (const float *)c->Lbuf.p,
@@ -1593,7 +1601,7 @@ static int render_impl(pbrtgpu_ctx *c, const pbrtgpu_render_desc *d, const int32
         HIPCHK(hipEventElapsedTime(&m2, c->ev[6], c->ev[7]));
         T.ms[K_ACCUM] += m2;
         T.launches[K_ACCUM]++;
-        st[PBRTGPU_STAT_PATHS] += (double)src.nItems;
+        st[PBRTGPU_STAT_PATHS] += (double)((long)nPix * n);
     }
     if (int e = applyLists(postT, postStart, postSrc)) return e;
     HIPCHK(hipStreamSynchronize(c->stream));

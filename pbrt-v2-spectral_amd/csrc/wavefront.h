@@ -114,7 +114,8 @@ struct ItemSrc {
     const int2 *pix;    // film pixels (sample x, y) of the render call
     int sb;             // samples per pixel in this batch
     int s0;             // first sample index
-    const int3 *keys;   // explicit (x, y, s) keys instead (trace_paths / spill samples), or null
+    const int3 *keys;   // explicit (x, y, s) keys for items >= keyBase (trace_paths, spill samples), or null
+    uint32_t keyBase;   // items [0, keyBase) are (pixel, sample) items, the rest keys[item - keyBase]
     uint32_t nItems;    // items of this run: global items base .. base + nItems - 1
     uint32_t base;
 };
@@ -412,7 +413,10 @@ PGD_INLINE void path_start(const DevScene &S, const PathSoA &P, const ItemSrc &s
     const uint32_t item = src.base + it;
     int px, py;
     uint32_t s;
-    if (src.keys) { int3 k = src.keys[item]; px = k.x; py = k.y; s = (uint32_t)k.z; }
+    if (src.keys && item >= src.keyBase) {
+        const int3 k = src.keys[item - src.keyBase];
+        px = k.x; py = k.y; s = (uint32_t)k.z;
+    }
     else {
         uint32_t p = item / (uint32_t)src.sb;
         int2 xy = src.pix[p];
