@@ -524,8 +524,9 @@ PGD_INLINE void estimate_direct(const DevScene &S, const PathSoA &P, int slot, i
     Seg vis;
     Emit em;
     light_sample_L<FEAT>(S, Lt, p, rayEps, ul, &wi, &lightPdf, &vis, &em);
-    if (lightPdf > 0. && !emit_black<NB, FEAT>(S, em)) {
-        bsdf_f(pm, bs, wo, wi, flags, F);
+    if (lightPdf > 0. && !emit_black<NB, FEAT>(S, em)) bsdf_f(pm, bs, wo, wi, flags, F);
+    // no matching BxDF (e.g. the light below the surface): f is black, A unused
+    if (lightPdf > 0. && !emit_black<NB, FEAT>(S, em) && !(F.mode == FV_SUM && F.n == 0)) {
         fval_prepare<NB, FEAT>(S, F, mb, c);
         float sc;
         if (em.point) sc = fabsf(vdot(wi, n)) / lightPdf;
