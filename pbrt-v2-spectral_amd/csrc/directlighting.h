@@ -307,8 +307,13 @@ PGD_INLINE Pushes shade_slot_dl(const DevScene &S, const PathSoA &P, int slot, f
             // ---- SpecularReflect, then SpecularTransmit (integrator.cpp:169-250)
             uint32_t br = P.fBr[(size_t)d * c + slot];
             bool spawned = false;
+            // only mirror and glass have specular BxDFs: elsewhere the two BSDFSample(rng) draws
+            // still happen (the reference constructs them) but no child can be sampled, and the
+            // vertex need not be rebuilt
+            const int vprim = P.fHit[(size_t)2 * d * c + slot];
+            const int vtype = S.mats[S.prims[vprim].material].type;
+            const bool canSpec = vtype == PBRTGPU_MAT_MIRROR || vtype == PBRTGPU_MAT_GLASS;
             while (d + 1 < S.maxDepth && br < 2u) {
-                if (!have) { dl_vertex<NB, FEAT>(S, P, slot, d, vx); have = true; }
                 if (!rngLoaded) {
                     mt_load(P, slot, fl, rng);
                     if (!rng.init) mt_init(rng);
@@ -317,6 +322,8 @@ PGD_INLINE Pushes shade_slot_dl(const DevScene &S, const PathSoA &P, int slot, f
                 const float u0 = mt_float(rng), u1 = mt_float(rng), uc = mt_float(rng);   // BSDFSample(rng)
                 const bool refl = br == 0u;
                 ++br;
+                if (!canSpec) continue;
+                if (!have) { dl_vertex<NB, FEAT>(S, P, slot, d, vx); have = true; }
                 const int flags = BSDF_SPECULAR | (refl ? BSDF_REFLECTION : BSDF_TRANSMISSION);
                 PowMemo pm;
                 FVal F;
