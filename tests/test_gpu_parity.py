@@ -437,3 +437,28 @@ def test_metadata_vs_reference_golden(pg, base):
     assert np.abs(film - gf["film"]).max() / np.abs(gf["film"]).max() < 1e-6
     of, _ = o.render(scene)
     assert np.array_equal(film.view(np.int32), of.view(np.int32))
+
+
+def test_integrator_scene_checks(pg):
+    """pbrtgpu_scene_upload refuses what the integrator steps cannot render exactly: a
+    DirectLighting maxdepth beyond the first MT19937 block (> 6), an unknown metadata strategy,
+    mesh / material ids without the per-primitive id table."""
+    from conftest import PACKS
+    import ctypes
+    pack = os.path.join(PACKS, "coverage.pack")
+    with pg.Device(0) as d:
+        s = pg.Scene.load(pack, xres=8, yres=8, spp=1, maxdepth=7, integrator="directlighting")
+        with pytest.raises(RuntimeError, match="maxdepth"):
+            d.upload(s)
+        s = pg.Scene.load(pack, xres=8, yres=8, spp=1, maxdepth=6, integrator="directlighting")
+        d.upload(s)
+        m = pg.Scene.load(pack, xres=8, yres=8, spp=1, integrator="metadata", strategy="mesh")
+        m.flat.meta_strategy = 7
+        with pytest.raises(RuntimeError, match="strategy"):
+            d.upload(m)
+        m.flat.meta_strategy = pg.META_STRATEGIES["material"]
+        m.flat.prim_meta = None
+        with pytest.raises(RuntimeError, match="prim_meta"):
+            d.upload(m)
+        m.flat.meta_strategy = pg.META_STRATEGIES["depth"]   # depth needs no ids
+        d.upload(m)
