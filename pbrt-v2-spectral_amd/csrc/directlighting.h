@@ -164,6 +164,70 @@ PGD_INLINE void dl_add(const DevScene &S, const PathSoA &P, int slot, int d, int
     }
 }
 
+// DirectLighting slot states beside wavefront.h's PF_* (bits 10, 11 are free there)
+enum {
+    PF_DLNEE = 1u << 10,   // the top vertex's next light-sample batch is due (k_dl_nee, this pass)
+    PF_DLS2 = 1u << 11,    // its light samples are done, its specular branches come next (k_shade)
+};
+
+// the light-sample batches of a slot marked PF_DLNEE, run by k_dl_nee right after k_shade in
+// the same pass: the vertex, then batches [k, kEnd) until one queues a ray (PF_PEND: the next
+// k_shade adds it) or the last one is added (PF_DLS2).  Returns true if the slot is left without
+// a queued ray (PF_DLS2), so the pass must not count as the wavefront's last.
+template <int NB, int FEAT>
+PGD_INLINE bool dl_light_batches(const DevScene &S, const PathSoA &P, int slot, Pushes &out) {
+    constexpr int NQ = Bands<NB>::NQ;
+    const size_t c = P.cap;
+    uint32_t fl = P.flags[slot] & ~PF_DLNEE;
+    const int d = P.bounce[slot];
+    const bool all = S.dlStrategy != PBRTGPU_DL_ONE;
+    const int K = all ? S.dlK : 1;
+    const uint32_t hp = P.hp[slot], s = P.smp[slot];
+    int k = (int)P.dlk[slot];
+    DLVertex vx;
+    dl_vertex<NB, FEAT>(S, P, slot, d, vx);
+    bool idle = false;
+    for (;;) {
+        const int kEnd = min(k + P.dlBatch, K);
+        uint32_t mA = 0u, mB = 0u;
+        int lnOne = 0;
+        for (int kk = k; kk < kEnd; ++kk) {
+            const int jb = kk - k;
+            float ul[3], ub[3];
+            int j, ns;
+            const int ln = dl_sample(S, hp, s, kk, ul, ub, &j, &ns);
+            PowMemo pm;
+            FVal F;
+            uint32_t f2 = 0u;
+            Pushes o2 = {false, false, false, 0u, 0u};
+            estimate_direct<NB, FEAT>(S, P, slot, slot + jb * (int)c, P.A + (size_t)jb * NQ * c + slot,
+                                      P.B + (size_t)jb * NQ * c + slot, ln, vx.bs, pm, vx.p, vx.n, vx.wo,
+                                      vx.is.rayEps, vx.ray.time, ul, ub, F, f2, o2);
+            if (f2 & PF_PA) mA |= 1u << jb;
+            if (f2 & PF_PB) mB |= 1u << jb;
+            lnOne = ln;
+        }
+        if (mA | mB) {   // the next k_shade adds the batch
+            out.sMask = mA;
+            out.mMask = mB;
+            fl |= PF_PEND | (all ? 0u : (uint32_t)lnOne << PF_LIGHT_SHIFT);
+            P.dlMask[slot] = mA | (mB << 16);
+            break;
+        }
+        // nothing queued: every ED of the batch is 0, added now
+        for (int kk = k; kk < kEnd; ++kk)
+            dl_add<NB>(S, P, slot, d, kk, K, all, false, false, P.A + slot, P.B + slot);
+        k = kEnd;
+        if (k < K) continue;
+        fl |= PF_DLS2;
+        idle = true;
+        break;
+    }
+    P.dlk[slot] = (uint32_t)k;
+    P.flags[slot] = fl;
+    return idle;
+}
+
 // k_shade body of the DirectLighting integrator for one slot (see the file comment).
 // Returns the ray requests; *done when the camera sample's radiance is in Lout.
 template <int NB, int FEAT>
@@ -180,7 +244,6 @@ PGD_INLINE Pushes shade_slot_dl(const DevScene &S, const PathSoA &P, int slot, f
     const int nLights = S.nLights;
     const bool all = S.dlStrategy != PBRTGPU_DL_ONE;
     const int K = all ? S.dlK : 1;
-    const uint32_t hp = P.hp[slot], s = P.smp[slot];
     int k = (int)P.dlk[slot];
     DLVertex vx;
     bool have = false;   // vx holds the top frame's vertex
@@ -194,7 +257,10 @@ PGD_INLINE Pushes shade_slot_dl(const DevScene &S, const PathSoA &P, int slot, f
     if (trc) printf("[dl] slot %d d %d fl %x k %d K %d prim %d occ %u hitM %d\n", slot, d, fl, k, K, P.hitPrim[slot],
                     P.occ[slot], P.hitPrim[P.rcap + slot]);
 #endif
-    if (fl & PF_PEND) {
+    if (fl & PF_DLS2) {   // light samples done in k_dl_nee: the specular branches
+        fl &= ~PF_DLS2;
+        stage = 2;
+    } else if (fl & PF_PEND) {
         // ---- the answered batch of light samples [k, kEnd): ED = (0 [+ A]) [+ B] each
         // (EstimateDirect), added in sample order
         const uint32_t msk = P.dlMask[slot];
@@ -252,10 +318,10 @@ PGD_INLINE Pushes shade_slot_dl(const DevScene &S, const PathSoA &P, int slot, f
             P.fHit[(size_t)(2 * d + 1) * c + slot] = __float_as_int(P.hitT[slot]);
             P.fBr[(size_t)d * c + slot] = 0u;
             k = 0;
-            dl_vertex<NB, FEAT>(S, P, slot, d, vx);
-            have = true;
-            const int al = S.prims[vx.is.prim].area_light;
-            const int eo = (al >= 0 && vdot(vx.is.dg.nn, vx.wo) > 0.f) ? S.lights[al].spec : -1;   // AreaLight::L
+            Isect is0;   // the hit alone decides the emission
+            isect_fill(S, ray, prim, P.hitT[slot], is0, inst_rec(P, slot));
+            const int al = S.prims[is0.prim].area_light;
+            const int eo = (al >= 0 && vdot(is0.dg.nn, vneg(ray.d)) > 0.f) ? S.lights[al].spec : -1;   // AreaLight::L
             float4 *Lv = dl_L<NB>(P, d, slot);
 #pragma unroll
             for (int q = 0; q < NQ; ++q) {
@@ -266,42 +332,9 @@ PGD_INLINE Pushes shade_slot_dl(const DevScene &S, const PathSoA &P, int slot, f
         }
     }
     for (;;) {
-        if (stage == 1) {
-            // ---- a batch of light samples [k, kEnd) of the top vertex: shadow and MIS rays of
-            // sample k + j at ray slot slot + j * cap, terms in A_j, B_j
-            if (!have) { dl_vertex<NB, FEAT>(S, P, slot, d, vx); have = true; }
-            const int kEnd = min(k + P.dlBatch, K);
-            uint32_t mA = 0u, mB = 0u;
-            int lnOne = 0;
-            for (int kk = k; kk < kEnd; ++kk) {
-                const int jb = kk - k;
-                float ul[3], ub[3];
-                int j, ns;
-                const int ln = dl_sample(S, hp, s, kk, ul, ub, &j, &ns);
-                PowMemo pm;
-                FVal F;
-                uint32_t f2 = 0u;
-                Pushes o2 = {false, false, false, 0u, 0u};
-                estimate_direct<NB, FEAT>(S, P, slot, slot + jb * (int)c, P.A + (size_t)jb * NQ * c + slot,
-                                          P.B + (size_t)jb * NQ * c + slot, ln, vx.bs, pm, vx.p, vx.n, vx.wo,
-                                          vx.is.rayEps, vx.ray.time, ul, ub, F, f2, o2);
-                if (f2 & PF_PA) mA |= 1u << jb;
-                if (f2 & PF_PB) mB |= 1u << jb;
-                lnOne = ln;
-            }
-            if (mA | mB) {   // the next pass adds the batch
-                out.sMask = mA;
-                out.mMask = mB;
-                fl |= PF_PEND | (all ? 0u : (uint32_t)lnOne << PF_LIGHT_SHIFT);
-                P.dlMask[slot] = mA | (mB << 16);
-                break;
-            }
-            // nothing queued: every ED of the batch is 0, added now
-            for (int kk = k; kk < kEnd; ++kk)
-                dl_add<NB>(S, P, slot, d, kk, K, all, false, false, P.A + slot, P.B + slot);
-            k = kEnd;
-            if (k < K) continue;
-            stage = 2;
+        if (stage == 1) {   // the next light-sample batch: k_dl_nee, later in this pass
+            fl |= PF_DLNEE;
+            break;
         }
         if (stage == 2) {
             // ---- SpecularReflect, then SpecularTransmit (integrator.cpp:169-250)

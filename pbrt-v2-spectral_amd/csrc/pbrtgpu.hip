@@ -830,6 +830,7 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
                   : c->S.integrator == PBRTGPU_INTEGRATOR_METADATA ? launch_shade_meta<NB>
                   : c->feat ? launch_shade<NB, FEAT_ALL> : launch_shade<NB, 0>;
     const int nFrames = dl ? std::max(1, c->S.maxDepth) : 0;
+    auto kNee = c->feat ? launch_dl_nee<NB> : launch_dl_nee<NB>;
     // DirectLighting issues up to kDlBatch light samples of a vertex per pass
     const int batch = dl ? std::max(1, std::min(c->S.dlStrategy == PBRTGPU_DL_ONE ? 1 : c->S.dlK, kDlBatch)) : 1;
     // passes one path can take: the camera ray + maxdepth + 1 vertices + 1 finish (path); per
@@ -872,7 +873,7 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
         HIPCHK(hipEventRecord(L.ev[0], L.s));
         HIPCHK(kShade(r.grid, L.s, c->S, L.P, r.src, 0, Lout));
         HIPCHK(hipEventRecord(L.ev[1], L.s));
-        HIPCHK(hipMemcpyAsync(L.hostCnt, L.P.cnt, CNT_WORK * 4, hipMemcpyDeviceToHost, L.s));
+        HIPCHK(hipMemcpyAsync(L.hostCnt, L.P.cnt, CNT_WORDS * 4, hipMemcpyDeviceToHost, L.s));
     }
     int live = nl;
     float m;
@@ -894,7 +895,7 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
                 HIPCHK(hipEventElapsedTime(&m, e[4], e[5])); T.ms[K_SHADE] += m;
             }
             int q = r.q;
-            if (L.hostCnt[CNT_QC(q)] == 0 && L.hostCnt[CNT_QS(q)] == 0) {
+            if (L.hostCnt[CNT_QC(q)] == 0 && L.hostCnt[CNT_QS(q)] == 0 && L.hostCnt[CNT_IDLE(q)] == 0) {
                 r.done = true;
                 --live;
                 uint64_t w[W_COUNT];
@@ -914,6 +915,7 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
                 const int nq = q ^ 1;
                 HIPCHK(hipMemsetAsync(P.cnt + CNT_QC(nq), 0, 4, L.s));
                 HIPCHK(hipMemsetAsync(P.cnt + CNT_QS(nq), 0, 4, L.s));
+                if (dl) HIPCHK(hipMemsetAsync(P.cnt + CNT_IDLE(nq), 0, 4, L.s));
                 HIPCHK(hipEventRecord(e[0], L.s));
                 if (serial) {   // closest-hit queries first, alone on the device
                     if (instPT) {
@@ -941,6 +943,7 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
                     HIPCHK(hipEventRecord(e[3], L.s));
                     HIPCHK(hipEventRecord(e[4], L.s));
                     HIPCHK(kShade(r.grid, L.s, c->S, P, r.src, nq, Lout));
+                    if (dl) HIPCHK(kNee(r.grid, L.s, c->S, P, nq));
                     T.launches[K_SHADE]++;
                     HIPCHK(hipEventRecord(e[5], L.s));
                     T.passes++;
@@ -980,6 +983,7 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
                 HIPCHK(hipStreamWaitEvent(L.s, e[3], 0));
                 HIPCHK(hipEventRecord(e[4], L.s));
                 HIPCHK(kShade(r.grid, L.s, c->S, P, r.src, nq, Lout));
+                if (dl) HIPCHK(kNee(r.grid, L.s, c->S, P, nq));
                 T.launches[K_SHADE]++;
                 HIPCHK(hipEventRecord(e[5], L.s));
                 T.passes++;
@@ -987,7 +991,7 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
                 q = nq;
             }
             r.q = q;
-            HIPCHK(hipMemcpyAsync(L.hostCnt, P.cnt, CNT_WORK * 4, hipMemcpyDeviceToHost, L.s));
+            HIPCHK(hipMemcpyAsync(L.hostCnt, P.cnt, CNT_WORDS * 4, hipMemcpyDeviceToHost, L.s));
         }
     }
     return 0;

@@ -163,6 +163,47 @@ static hipError_t launch(int grid, hipStream_t stream, const DevScene &S, const 
     return hipGetLastError();
 }
 #if SHADE_DL
+// The light-sample batches of the DirectLighting slots this pass's k_shade marked PF_DLNEE
+// (directlighting.h dl_light_batches), in a kernel of their own so that neither step carries the
+// other's registers; their shadow / MIS rays join the pass's queues.
+#ifndef PGD_NEE_ATTR
+#define PGD_NEE_ATTR __attribute__((amdgpu_waves_per_eu(2, 2)))
+#endif
+template <int NB, int FEAT>
+__global__ __launch_bounds__(kShadeBlock) PGD_NEE_ATTR void k_dl_nee(DevScene S, PathSoA P, int qout) {
+    if (FEAT & FEAT_MEAS) kd_lds_fill(S);   // measured-BRDF lookups read the LDS copy (as in k_shade)
+    const int slot = blockIdx.x * blockDim.x + threadIdx.x;
+    Pushes pu = {false, false, false, 0u, 0u};
+    bool idle = false;
+    if (slot < P.cap && P.item[slot] >= 0 && (P.flags[slot] & PF_DLNEE)) idle = dl_light_batches<NB, FEAT>(S, P, slot, pu);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const unsigned long long bI = __ballot(idle);
+    if (bI && lane == 0) atomicAdd(&P.cnt[CNT_IDLE(qout)], (uint32_t)__popcll(bI));
+    __shared__ uint32_t qsh[12];   // per wave: M, S totals -> offsets; bases
+    const uint32_t nm = (uint32_t)__popc(pu.mMask), ns = (uint32_t)__popc(pu.sMask);
+    const uint32_t im = wave_scan(nm), is = wave_scan(ns);
+    if (lane == 63) { qsh[2 * wave] = im; qsh[2 * wave + 1] = is; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t[2] = {0u, 0u};
+        for (int w = 0; w < (int)(blockDim.x >> 6); ++w)
+            for (int k = 0; k < 2; ++k) { const uint32_t v = qsh[2 * w + k]; qsh[2 * w + k] = t[k]; t[k] += v; }
+        qsh[8] = t[0] ? atomicAdd(&P.cnt[CNT_QC(qout)], t[0]) : 0u;
+        qsh[9] = t[1] ? atomicAdd(&P.cnt[CNT_QS(qout)], t[1]) : 0u;
+    }
+    __syncthreads();
+    uint32_t *qC = P.qC + (size_t)qout * 2 * P.rcap, *qS = P.qS + (size_t)qout * P.rcap;
+    uint32_t km = qsh[8] + qsh[2 * wave] + im - nm, ks = qsh[9] + qsh[2 * wave + 1] + is - ns;
+    for (uint32_t m = pu.mMask; m; m &= m - 1u) qC[km++] = ((uint32_t)(slot + (__ffs(m) - 1) * P.cap) << 1) | 1u;
+    for (uint32_t m = pu.sMask; m; m &= m - 1u) qS[ks++] = (uint32_t)(slot + (__ffs(m) - 1) * P.cap);
+}
+template <int NB>
+hipError_t launch_dl_nee(int grid, hipStream_t stream, const DevScene &S, const PathSoA &P, int qout) {
+    const size_t lds = ((SHADE_FEAT & FEAT_MEAS) && S.kdInLds) ? (size_t)S.nKd * 32 : 0;
+    hipLaunchKernelGGL((k_dl_nee<NB, SHADE_FEAT>), dim3(grid), dim3(kShadeBlock), lds, stream, S, P, qout);
+    return hipGetLastError();
+}
+template hipError_t launch_dl_nee<SHADE_NB>(int, hipStream_t, const DevScene &, const PathSoA &, int);
 template <int NB>
 hipError_t launch_shade_dl(int grid, hipStream_t stream, const DevScene &S, const PathSoA &P, const ItemSrc &src,
                            int qout, float *Lout) {
