@@ -54,13 +54,14 @@ __device__ __forceinline__ uint32_t wave_scan(uint32_t x) {
 // occupancy target: 3 waves/SIMD (<= 168 VGPRs) for <= 32 bands costs a few spilled
 // registers and beats the unconstrained 200-VGPR / 2-wave build (C2 shade 372 -> 335
 // ms/frame, r01l ablation; 4 waves spills ~90 registers and loses); 60 bands: 2 waves
-// The DirectLighting / metadata step at 2 waves/SIMD: C2 DL 137 (unconstrained, 1 wave) -> 156-161
-// (2 waves) vs 148 (3 waves) Mpaths/s (r02m).  Before light samples were batched, the 3-wave build
-// gave non-deterministic radiance on coverage.pbrt (tools/dbg/dl_debug4.py); every variant since
-// passes tools/dbg/dl_determinism.py (3 identical runs, oracle bit for bit)
+// The DirectLighting / metadata step at 3 waves/SIMD since its light-sample batches moved to
+// k_dl_nee (C2 DL shade 409 -> 396 ms/frame; k_dl_nee itself is fastest at 2 waves: 3 waves 421,
+// unconstrained 561).  Before the batches existed, a 3-wave build gave non-deterministic radiance
+// on coverage.pbrt (tools/dbg/dl_debug4.py); every variant since passes
+// tools/dbg/dl_determinism.py (3 identical runs, oracle bit for bit)
 #ifndef PGD_SHADE_ATTR
 #if SHADE_DL
-#define PGD_SHADE_ATTR __attribute__((amdgpu_waves_per_eu(2, 2)))
+#define PGD_SHADE_ATTR __attribute__((amdgpu_waves_per_eu(3, 3)))
 #else
 #define PGD_SHADE_ATTR __attribute__((amdgpu_waves_per_eu(SHADE_NB > 32 ? 2 : 3, SHADE_NB > 32 ? 2 : 3)))
 #endif
