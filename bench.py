@@ -124,6 +124,7 @@ def cpu_baseline(scene, target_s):
     threads = max(1, min(aff, share) if share > 0 else aff)
     o = pg.oracle()
     spp = scene.spp
+    pps = scene.paths_per_sample()   # SpectralRenderer singleDirection: a sample is nWaveBands paths
 
     def timed(nthreads, seconds):
         probe = max(spp, 64 * spp // 16 * nthreads)
@@ -138,11 +139,12 @@ def cpu_baseline(scene, target_s):
 
     n, dt = timed(threads, target_s)
     n1, dt1 = timed(1, target_s / 3.0)
+    n, n1 = n * pps, n1 * pps
     per_core = n1 / dt1 / 1e6
     return {"value": round(n / dt / 1e6, 4), "unit": "Mpaths/s", "cores": threads, "kind": "port",
             "one_core": round(per_core, 4), "host_cpus": ncpu, "affinity_cpus": aff, "cpu_model": model,
             "sample": "%d paths = all %d samples of %d pseudo-randomly spread pixels of the same frame, %.1f s on "
-                      "%d threads; 1-core leg %d paths in %.1f s" % (n, spp, n // spp, dt, threads, n1, dt1),
+                      "%d threads; 1-core leg %d paths in %.1f s" % (n, spp, n // spp // pps, dt, threads, n1, dt1),
             "calibration": "port vs reference per core, same box: profiles/cpu_calibration.json"}
 
 
@@ -171,7 +173,7 @@ def shared_film(shape, rank, dist, tag):
     return path, np.memmap(path, dtype=np.float32, mode="r+", shape=shape)
 
 
-def exclusive_roofline(dev, scene, tiles, tile, frame_paths, cfg):
+def exclusive_roofline(dev, scene, tiles, tile, frame_paths, cfg, pps=1):
     """Per-kernel exclusive device time (serial mode) and algorithmic bytes (instrumented
     frame), both over one frame of this rank's tiles, untimed."""
     os.environ["PBRTGPU_SERIAL"] = "1"
@@ -190,7 +192,7 @@ def exclusive_roofline(dev, scene, tiles, tile, frame_paths, cfg):
     byts = {"k_trace_closest": trace_bytes(work, "k_trace_closest"),
             "k_trace_shadow": trace_bytes(work, "k_trace_shadow"),
             "k_shade": shade_bytes(work, frame_paths, scene.bands),
-            "k_accum": accum_bytes(frame_paths, scene.bands)}
+            "k_accum": accum_bytes(frame_paths / pps, scene.bands)}   # one row per camera sample
     traffic = {}
     tf = os.path.join(ROOT, "profiles", "hbm_traffic.json")
     if os.path.exists(tf):
@@ -232,6 +234,11 @@ def main():
                     help="SurfaceIntegrator (BASELINE configs: path; directlighting / metadata = SURVEY §8(f) rows)")
     ap.add_argument("--strategy", choices=["all", "one", "mesh", "material", "depth"], default=None,
                     help="DirectLighting (all / one) or metadata (mesh / material / depth) strategy")
+    ap.add_argument("--renderer", choices=["sampler", "spectral"], default="sampler",
+                    help="Renderer (BASELINE configs: sampler; spectral = SpectralRenderer, SURVEY §8(f) row 2)")
+    ap.add_argument("--wave-bands", type=int, default=0, help="SpectralRenderer nWaveBands (default: 32)")
+    ap.add_argument("--sampling", choices=["single", "sampler"], default=None,
+                    help="SpectralRenderer samplingMethod singleDirection / samplerDirection (default: single)")
     ap.add_argument("--shard", choices=["tiles", "frames"], default="tiles")
     ap.add_argument("--tile", type=int, default=16)
     ap.add_argument("--slices", type=int, default=1, help="tile slices per GPU (single-process --gpus N)")
@@ -259,9 +266,15 @@ def main():
     pack, desc = CONFIGS[args.config]
     scene = pg.Scene.load(args.scene or os.path.join(ROOT, "scenes", pack), xres=args.res, yres=args.res,
                           spp=args.spp, seed=rank if args.shard == "frames" else 0,
-                          integrator=args.integrator, strategy=args.strategy)
+                          integrator=args.integrator, strategy=args.strategy,
+                          renderer=None if args.renderer == "sampler" else "spectral", wave_bands=args.wave_bands,
+                          sampling=args.sampling)
     if args.integrator != "path":
         desc = desc.replace("path maxdepth", "%s (%s) maxdepth" % (args.integrator, args.strategy or "scene"))
+    pps = scene.paths_per_sample()
+    if args.renderer == "spectral":
+        desc += ", SpectralRenderer nWaveBands %d %sDirection (%d paths per camera sample)" % (
+            scene.flat.wave_bands, "single" if scene.flat.spectral_sampling == 0 else "sampler", pps)
     info = scene.info()
     tile = (args.tile, args.tile)
     ntx, nty = pg.tile_grid(scene, tile)
@@ -322,7 +335,8 @@ def main():
     frame_paths = paths / args.steps    # this rank's share of a frame
     roof = None
     if rank == 0 and not args.no_roofline:
-        roof = exclusive_roofline(dev, scene, tiles, tile, frame_paths, args.config if args.integrator == "path" else args.config + "_dl")
+        cfg = args.config + ("" if args.integrator == "path" else "_dl") + ("" if args.renderer == "sampler" else "_spec")
+        roof = exclusive_roofline(dev, scene, tiles, tile, frame_paths, cfg, pps)
 
     cpu = None
     if rank == 0 and n_gpus == 1 and not args.no_cpu:
@@ -339,7 +353,7 @@ def main():
             "data": "packaged scene %s (scene pack built from the reference's scene file), fixed per-path seeds"
                     % pack.replace(".pack", ""),
             "config": {"workload": desc % (scene.bands, info["maxdepth"], scene.spp, scene.width, scene.height),
-                       "config": args.config, "paths_per_frame": int(scene.width * scene.height * scene.spp),
+                       "config": args.config, "paths_per_frame": int(scene.width * scene.height * scene.spp * pps),
                        "shard": args.shard, "tile": args.tile,
                        "parallelism": "%s x%d%s" % ("tiles" if args.shard == "tiles" else "frames", n_gpus,
                                                     " (threads, one process)" if threads_mode else "")},

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define PBRTGPU_ABI_VERSION 7
+#define PBRTGPU_ABI_VERSION 8
 #define PBRTGPU_MAX_BANDS 64
 
 #define PBRTGPU_E_INVALID   (-1)
@@ -241,6 +241,10 @@ typedef struct pbrtgpu_flat_scene {
                                    * on the primitive reports (core/primitive.cpp:87-166; the
                                    * Primitive / Material constructor counters, primitive.h:40,
                                    * material.h:39), or NULL */
+    int32_t renderer;             /* PBRTGPU_RENDERER_*: the scene's Renderer */
+    int32_t wave_bands;           /* SpectralRenderer "nWaveBands" (api.cpp:1378, default 32) */
+    int32_t spectral_sampling;    /* SpectralRenderer "samplingMethod": PBRTGPU_SPECTRAL_* */
+    int32_t pad_r;
 } pbrtgpu_flat_scene;
 
 /* SurfaceIntegrator of a flattened scene: "path" (integrators/path.cpp:44-115),
@@ -252,6 +256,16 @@ enum { PBRTGPU_DL_ALL = 0, PBRTGPU_DL_ONE = 1 };
 /* MetadataIntegrator (integrators/metadata.cpp:41-98): L = Spectrum(primitiveId),
  * Spectrum(materialId) or Spectrum(|hit point - ray origin|) at the camera ray's first hit */
 enum { PBRTGPU_META_MESH = 0, PBRTGPU_META_MATERIAL = 1, PBRTGPU_META_DEPTH = 2 };
+/* Renderer: "sampler" (renderers/samplerrenderer.cpp:60-247) or "spectralrenderer"
+ * (renderers/spectralrenderer.cpp:60-223): per camera sample and wave band b of
+ * nWaveBands, a path of wavelength 395 + dW b + dW / 2 (dW = 320 / nWaveBands, integer
+ * division) whose radiance's value at that wavelength (Spectrum::GetValueAtWavelength,
+ * spectrum.h:384-405) fills the sample's indices [dI b, min(dI (b + 1), N - 1)),
+ * dI = N / nWaveBands.  singleDirection traces every band of every sample (nWaveBands paths
+ * per sample, path b drawing from RNG(path_seed(hp, s nWaveBands + b))); samplerDirection
+ * traces band s % nWaveBands of sample s only.  A sample's unassigned indices are 0. */
+enum { PBRTGPU_RENDERER_SAMPLER = 0, PBRTGPU_RENDERER_SPECTRAL = 1 };
+enum { PBRTGPU_SPECTRAL_SINGLE = 0, PBRTGPU_SPECTRAL_SAMPLER = 1 };
 
 /* ---- render description ----------------------------------------------------------- */
 /* Tiles are tile_w x tile_h blocks of the FILM pixel window (camera px_count x py_count;
@@ -272,7 +286,7 @@ typedef struct pbrtgpu_render_desc {
 
 /* stats_out layout (doubles) */
 enum {
-    PBRTGPU_STAT_PATHS = 0,       /* camera paths traced */
+    PBRTGPU_STAT_PATHS = 0,       /* paths traced: camera samples x SpectralRenderer bands per sample */
     PBRTGPU_STAT_KERNEL_MS = 1,   /* device time of the path kernels (trace + shade) */
     PBRTGPU_STAT_ACCUM_MS = 2,    /* device time of the film accumulation */
     PBRTGPU_STAT_ZEROED = 3,      /* samples zeroed by the NaN/negative/inf guard */

@@ -30,6 +30,9 @@ typedef struct pbrthost_overrides {
                            * built before integrators were recorded) */
     int32_t dl_strategy;  /* PBRTGPU_DL_* to force, or -1: the scene's "strategy" */
     int32_t meta_strategy;   /* PBRTGPU_META_* to force, or -1: the scene's metadata "strategy" */
+    int32_t renderer;        /* PBRTGPU_RENDERER_* to force, or -1: the scene's Renderer */
+    int32_t wave_bands;      /* SpectralRenderer nWaveBands to force, or <= 0: the scene's */
+    int32_t spectral_sampling;   /* PBRTGPU_SPECTRAL_* to force, or -1: the scene's samplingMethod */
 } pbrthost_overrides;
 
 /* path: a .pbrt scene file or a .pack scene pack.  Returns 0 or -1 (message in err). */

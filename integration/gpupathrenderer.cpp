@@ -40,7 +40,7 @@ void GpuPathRenderer::Render(const Scene *) {
         return;
     }
     int n = ngpu > 0 ? min(ngpu, ndev) : ndev;
-    pbrthost_overrides ov = { -1, -1, -1, -1, nSpectralSamples, seed, -1, -1, -1 };   // the scene's own integrator
+    pbrthost_overrides ov = { -1, -1, -1, -1, nSpectralSamples, seed, -1, -1, -1, -1, 0, -1 };   // the scene's own integrator
     pbrthost_scene *hs = NULL;
     char err[1024];
     if ((status = pbrthost_load(sceneFile.c_str(), &ov, &hs, err, sizeof(err))) != 0) {

@@ -2016,8 +2016,9 @@ static Ray camera_ray(const Ctx *c, float imageX, float imageY, float lensU, flo
     return o;
 }
 
-/* One camera path: sample -> ray -> radiance -> guard (samplerrenderer.cpp:86-133) */
-static int trace_path(const Ctx *c, int px, int py, uint32_t s, float *L, float *imgX, float *imgY) {
+/* One camera path: sample -> ray -> rayWeight * Li (samplerrenderer.cpp:86-110), the path
+ * drawing from RNG(path_seed(hp, rngIdx)) */
+static void camera_path(const Ctx *c, int px, int py, uint32_t s, uint32_t rngIdx, float *L, float *imgX, float *imgY) {
     uint32_t spp = (uint32_t)c->s->spp;
     PathSampler ps;
     ps.hp = pixel_hash(c->s->seed, px, py);
@@ -2028,7 +2029,7 @@ static int trace_path(const Ctx *c, int px, int py, uint32_t s, float *L, float 
     float imageX = px + u[0], imageY = py + u[1];
     s2d(ps.hp, 1, s, spp, lens);
     float timeU = s1d(ps.hp, 2, s, spp);
-    rng_seed(&ps.rng, path_seed(ps.hp, s));
+    rng_seed(&ps.rng, path_seed(ps.hp, rngIdx));
     ps.rng.mti = 624;   /* RNG ctor: Seed() leaves mti == N, first draw regenerates */
     RayDiff rd;
     Ray r = camera_ray(c, imageX, imageY, lens[0], lens[1], timeU, &rd);
@@ -2036,8 +2037,16 @@ static int trace_path(const Ctx *c, int px, int py, uint32_t s, float *L, float 
     if (c->s->integrator == PBRTGPU_INTEGRATOR_DIRECT) dl_radiance(c, r, &rd, 0, &ps, Lr);
     else if (c->s->integrator == PBRTGPU_INTEGRATOR_METADATA) meta_radiance(c, r, Lr);
     else radiance(c, r, &rd, &ps, Lr);
+    for (int i = 0; i < c->nb; ++i) L[i] = 1.f * Lr[i];   /* rayWeight * Li */
+    if (imgX) *imgX = imageX;
+    if (imgY) *imgY = imageY;
+}
+
+/* SamplerRenderer: the path and the NaN / negative / infinite luminance guard
+ * (samplerrenderer.cpp:111-128) */
+static int sampler_sample(const Ctx *c, int px, int py, uint32_t s, float *L, float *imgX, float *imgY) {
+    camera_path(c, px, py, s, s, L, imgX, imgY);
     int nb = c->nb, bad = 0;
-    for (int i = 0; i < nb; ++i) L[i] = 1.f * Lr[i];   /* rayWeight * Li */
     int nan = 0;
     for (int i = 0; i < nb; ++i) if (isnan(L[i])) nan = 1;
     if (nan) bad = 1;
@@ -2047,9 +2056,76 @@ static int trace_path(const Ctx *c, int px, int py, uint32_t s, float *L, float 
         else if (isinf(yv)) bad = 1;
     }
     if (bad) for (int i = 0; i < nb; ++i) L[i] = 0.f;
-    if (imgX) *imgX = imageX;
-    if (imgY) *imgY = imageY;
     return bad;
+}
+
+/* SpectralRenderer: one camera sample of SpectralRendererTask::Run (spectralrenderer.cpp:
+ * 98-190).  sampledLambdaStart / End are the ints 395 / 715 (spectrum.h:41-42), so
+ * deltaWave = float(320 / nWaveBands) and GetValueAtWavelength's step float(320 / N).
+ * singleDirection: band b = 0 .. nWaveBands-1 traces the sample's camera path with
+ * RNG(path_seed(hp, s nWaveBands + b)); samplerDirection: band s % nWaveBands only, with
+ * RNG(path_seed(hp, s)).  A band's radiance: NaN -> 0; the luminance guard on the sample's
+ * spectrum as assigned so far (it starts at 0 per sample); its value at the band's
+ * wavelength (spectrum.h:384-405, Lerp(t, c[i], c[i+1])) into indices
+ * [dI b, min(dI (b+1), N-1)), dI = round(N / nWaveBands).  Returns the bands zeroed. */
+static int spectral_sample(const Ctx *c, int px, int py, uint32_t s, float *L, float *imgX, float *imgY) {
+    const int N = c->nb, nWB = c->s->wave_bands;
+    const int single = c->s->spectral_sampling == PBRTGPU_SPECTRAL_SINGLE;
+    const int mm = single ? nWB : 1;
+    const int dI = (int)round(N / nWB);
+    const float dW = (float)((715 - 395) / nWB), step = (float)((715 - 395) / N);
+    int bad = 0;
+    for (int i = 0; i < N; ++i) L[i] = 0.f;
+    for (int sb = 0; sb < mm; ++sb) {
+        const int b = single ? sb : (int)(s % (uint32_t)nWB);
+        float Lr[MAXB];
+        camera_path(c, px, py, s, single ? s * (uint32_t)nWB + (uint32_t)b : s, Lr, imgX, imgY);
+        int nan = 0;
+        for (int i = 0; i < N; ++i) if (isnan(Lr[i])) nan = 1;
+        int zero = nan;
+        if (!nan) {
+            float yv = spec_y(c, L);
+            if (yv < -1e-5) zero = 1;
+            else if (isinf(yv)) zero = 1;
+        }
+        if (zero) { for (int i = 0; i < N; ++i) Lr[i] = 0.f; ++bad; }
+        const float wl = 395 + dW * b + (dW / 2);
+        const int lo = dI * b, hi = (dI * (b + 1) < N - 1) ? dI * (b + 1) : N - 1;
+        if (hi <= lo) continue;
+        float v = 0.f;
+        for (int i = 0; i < N; ++i) {
+            const float w0 = 395 + i * step, w1 = 395 + (i + 1) * step;
+            if (wl >= w0 && wl < w1) {
+                if (i + 1 >= N) abort();   /* c[N]: rejected by oracle_spectral_ok */
+                v = lerpf((wl - w0) / (w1 - w0), Lr[i], Lr[i + 1]);
+                break;
+            }
+        }
+        for (int k = lo; k < hi; ++k) L[k] = v;
+    }
+    return bad;
+}
+
+/* a SpectralRenderer band whose indices need c[N] reads past the spectrum: such scenes are
+ * rejected (as by pbrtgpu_scene_upload) */
+static int spectral_ok(const pbrtgpu_flat_scene *s) {
+    if (s->renderer != PBRTGPU_RENDERER_SPECTRAL) return 1;
+    const int N = s->n_bands, nWB = s->wave_bands;
+    if (nWB < 1) return 0;
+    const int dI = (int)round(N / nWB);
+    const float dW = (float)((715 - 395) / nWB), step = (float)((715 - 395) / N);
+    for (int b = 0; b < nWB; ++b) {
+        const int lo = dI * b, hi = (dI * (b + 1) < N - 1) ? dI * (b + 1) : N - 1;
+        if (hi <= lo) continue;
+        const float wl = 395 + dW * b + (dW / 2);
+        if (wl >= 395 + (N - 1) * step) return 0;
+    }
+    return 1;
+}
+
+static int trace_path(const Ctx *c, int px, int py, uint32_t s, float *L, float *imgX, float *imgY) {
+    if (c->s->renderer == PBRTGPU_RENDERER_SPECTRAL) return spectral_sample(c, px, py, s, L, imgX, imgY);
+    return sampler_sample(c, px, py, s, L, imgX, imgY);
 }
 
 /* ------------------------------------------------------------------ exported API */
@@ -2072,6 +2148,7 @@ int oracle_mt_first(uint32_t seed, int n, uint32_t *out) {
 }
 int oracle_trace_paths(const pbrtgpu_flat_scene *s, const int32_t *keys, int32_t n, float *out) {
     Ctx c = {s, s->n_bands};
+    if (!spectral_ok(s)) return -1;
     for (int k = 0; k < n; ++k) trace_path(&c, keys[3 * k], keys[3 * k + 1], (uint32_t)keys[3 * k + 2], out + (size_t)k * s->n_bands, NULL, NULL);
     return 0;
 }
@@ -2201,6 +2278,7 @@ static void run_phase(Job *j, int phase, int nthreads) {
 int oracle_render(const pbrtgpu_flat_scene *s, int x0, int x1, int y0, int y1, float *film, int nthreads,
                   double *stats) {
     Ctx c = {s, s->n_bands};
+    if (!spectral_ok(s)) return -1;
     const pbrtgpu_camera *cam = &s->camera;
     int nb = s->n_bands;
     Job j;
@@ -2293,6 +2371,7 @@ static void *tworker(void *arg) {
 }
 long oracle_trace_range(const pbrtgpu_flat_scene *s, long first, long count, int nthreads) {
     Ctx c = {s, s->n_bands};
+    if (!spectral_ok(s)) return -1;
     TJob t;
     t.c = &c; t.n0 = first; t.n1 = first + count; t.next = first; t.W = s->camera.px_count; t.H = s->camera.py_count;
     pthread_mutex_init(&t.mu, NULL);

@@ -337,6 +337,10 @@ static int ovW = -1, ovH = -1, ovMaxDepth = -1;
 static const char *surfOv = "path";   // --surf: the SurfaceIntegrator to create
 static const char *dlStrategyOv = NULL;
 static const char *metaStrategyOv = NULL;   // --meta-strategy: MetadataIntegrator "strategy" 
+// --spectral N [single|sampler]: Renderer "spectralrenderer" with nWaveBands N and samplingMethod
+// singleDirection / samplerDirection (api.cpp:1377-1403)
+static int specBands = 0;
+static bool specSampler = false;
 // results of WorldEnd
 static Scene *gScene = NULL;
 static Camera *gCamera = NULL;
@@ -560,7 +564,7 @@ static void usage() {
                     "   [--path-every K] [--kat-mt out.bin] [--spectra out.bin] [--tris out.bin]\n"
                     "   [--keys keys.i32 (with --paths)] [--refdat film.dat] [--gpupath]\n"
                     "   [--surf path|directlighting|metadata|scene] [--dl-strategy all|one]\n"
-                    "   [--meta-strategy mesh|material|depth]\n");
+                    "   [--meta-strategy mesh|material|depth] [--spectral N single|sampler]\n");
     exit(1);
 }
 
@@ -591,6 +595,7 @@ int main(int argc, char **argv) {
         else if (a == "--surf") surfOv = argv[++i];
         else if (a == "--dl-strategy") dlStrategyOv = argv[++i];
         else if (a == "--meta-strategy") metaStrategyOv = argv[++i];
+        else if (a == "--spectral") { specBands = atoi(argv[++i]); specSampler = string(argv[++i]) == "sampler"; }
         else usage();
     }
     Options opt; opt.quiet = true;
@@ -650,6 +655,22 @@ int main(int argc, char **argv) {
 #else
     if (gpupath) { fprintf(stderr, "harness: built without the gpupath binding (make -C oracle/ref gpupath)\n"); return 1; }
 #endif
+    if (specBands) {
+        // bands whose assigned indices need GetValueAtWavelength's c[i + 1] past the last
+        // sample (spectrum.h:397) read outside the spectrum: rejected, as the GPU core does
+        const int dI = round(nSpectralSamples / specBands);
+        const float dW = (sampledLambdaEnd - sampledLambdaStart) / specBands;
+        const float step = (sampledLambdaEnd - sampledLambdaStart) / nSpectralSamples;
+        for (int b = 0; specBands > 0 && b < specBands; ++b) {
+            if (min(dI * (b + 1), nSpectralSamples - 1) <= dI * b) continue;
+            float wl = sampledLambdaStart + dW * b + (dW / 2);
+            if (wl >= sampledLambdaStart + (nSpectralSamples - 1) * step) {
+                fprintf(stderr, "harness: nWaveBands %d reads past the spectrum\n", specBands);
+                return 1;
+            }
+        }
+        if (specBands < 1) { fprintf(stderr, "harness: nWaveBands must be >= 1\n"); return 1; }
+    }
     if (spp <= 0) spp = gSppParam;
     spp = (int)RoundUpPow2(spp);   // LDSampler rounds up (lowdiscrepancy.cpp:33-39)
 
@@ -700,6 +721,56 @@ int main(int argc, char **argv) {
         else if (isinf(L.y())) { L = Spectrum(0.f); ++nBad; }
         return L;
     };
+    // one camera sample of SpectralRendererTask::Run (spectralrenderer.cpp:98-190): per wave
+    // band b a ray of wavelength 395 + dW b + dW / 2 (integer dW = 320 / nWaveBands), its
+    // radiance's value at that wavelength (Spectrum::GetValueAtWavelength, spectrum.h:384-405)
+    // assigned to indices [dI b, min(dI (b+1), N-1)).  singleDirection traces every band of the
+    // sample; samplerDirection only band s % nWaveBands.  Fixed-seed re-specification: the
+    // sample's Ls starts at 0 (the reference reuses a per-batch-slot array across samples) and
+    // band b's path draws from RNG(path_seed(hp, s nWaveBands + b)) (singleDirection) or
+    // RNG(path_seed(hp, s)) (samplerDirection) instead of the task's shared stream.
+    auto traceSpectral = [&](int x, int y, int s, RayDifferential *ray) -> Spectrum {
+        const int nWaveBands = specBands;
+        FillSample(smp, x, y, (uint32_t)s, (uint32_t)spp, (uint32_t)seed, gCamera->shutterOpen, gCamera->shutterClose);
+        const int methodMultiplier = specSampler ? 1 : nWaveBands;
+        int deltaIndex = round(nSpectralSamples / nWaveBands);
+        float deltaWave = (sampledLambdaEnd - sampledLambdaStart) / nWaveBands;
+        const uint32_t hp = pixel_hash((uint32_t)seed, x, y);
+        Spectrum Ls(0.f);
+        for (int sb = 0; sb < methodMultiplier; ++sb) {
+            const int b = specSampler ? s % nWaveBands : sb;
+            Spectrum Lr;
+            ray->wavelength = sampledLambdaStart + deltaWave * b + (deltaWave / 2);
+            const float wlSet = ray->wavelength;
+            float rayWeight = gCamera->GenerateRayDifferential(*smp, ray);
+            ray->ScaleDifferentials(1.f / sqrtf(spp));
+            if (x == xs && y == ys && s == 0 && b == 0)
+                fprintf(stderr, "harness: wavelength %g set, %g after GenerateRayDifferential\n", wlSet, ray->wavelength);
+            // the camera may leave the wavelength indeterminate (the perspective camera's Ray
+            // constructor does not set it, geometry.h:319-321); the band's wavelength is what
+            // the renderer reads
+            ray->wavelength = wlSet;
+            RNG rng(path_seed(hp, specSampler ? (uint32_t)s : (uint32_t)s * (uint32_t)nWaveBands + (uint32_t)b));
+            Intersection isect;
+            Spectrum T;
+            if (rayWeight > 0.f) {
+                Lr = rayWeight * renderer.Li(gScene, *ray, smp, rng, arena, &isect, &T);
+                if (Lr.HasNaNs()) { Lr = Spectrum(0.f); ++nBad; }
+                else if (Ls.y() < -1e-5) { Lr = Spectrum(0.f); ++nBad; }
+                else if (isinf(Ls.y())) { Lr = Spectrum(0.f); ++nBad; }
+            }
+            else Lr = 0.f;
+            int bottomIndex = deltaIndex * b;
+            int topIndex = min(deltaIndex * (b + 1), nSpectralSamples - 1);
+            float v;
+            if (topIndex > bottomIndex) {
+                Lr.GetValueAtWavelength(ray->wavelength, &v);
+                for (int k = bottomIndex; k < topIndex; ++k) Ls.AssignValueAtIndex(k, v);
+            }
+            arena.FreeAll();
+        }
+        return Ls;
+    };
     auto emit = [&](int x, int y, int s, const Spectrum &L) {
         int key[3] = { x, y, s };
         float c[nSpectralSamples];
@@ -720,7 +791,7 @@ int main(int argc, char **argv) {
                 return 1;
             }
             RayDifferential ray;
-            Spectrum L = trace(key[0], key[1], key[2], &ray);
+            Spectrum L = specBands ? traceSpectral(key[0], key[1], key[2], &ray) : trace(key[0], key[1], key[2], &ray);
             emit(key[0], key[1], key[2], L);
             ++nPath;
             arena.FreeAll();
@@ -734,7 +805,7 @@ int main(int argc, char **argv) {
         for (int x = xs; x < xe; ++x)
             for (int s = 0; s < spp; ++s) {
                 RayDifferential ray;
-                Spectrum L = trace(x, y, s, &ray);
+                Spectrum L = specBands ? traceSpectral(x, y, s, &ray) : trace(x, y, s, &ray);
                 gFilm->AddSample(*smp, L, ray);
                 if (refFilm) refFilm->AddSample(*smp, L, ray);
                 if (pf && (pathEvery <= 1 || (nPath % pathEvery) == 0)) emit(x, y, s, L);

@@ -271,6 +271,12 @@ struct DevScene {
     int dlK;                          // DirectLighting light samples per vertex (sum of RoundUpPow2(nSamples))
     int metaStrategy;                 // PBRTGPU_META_* (MetadataIntegrator)
     const uint32_t *primMeta;         // [prims][2]: primitiveId, materialId a hit reports
+    // SpectralRenderer (spectralrenderer.cpp:60-223): specItems paths per camera sample
+    // (nWaveBands for singleDirection, 1 for samplerDirection and the SamplerRenderer)
+    int specMode;                     // 0: SamplerRenderer, 1: singleDirection, 2: samplerDirection
+    int specBands;                    // nWaveBands
+    int specItems;
+    const int4 *specTab;              // [nWaveBands]: assigned indices [x, y), interval z (-1: none), t (bits)
 };
 
 // scene features a shade kernel is specialised for (k_shade<NB, FEAT>): a scene without

@@ -429,7 +429,7 @@ PGD_INLINE Pushes shade_slot_dl(const DevScene &S, const PathSoA &P, int slot, f
         }
         // ---- pop frame d with raw radiance Lr
         if (d == 0) {
-            *zeroed = path_output<NB>(S, Lr, Lout, P.item[slot]);   // rayWeight * ((1 * L) + 0), guarded
+            *zeroed = path_output<NB>(S, Lr, Lout, P.item[slot], P.smp[slot]);   // rayWeight * ((1 * L) + 0), guarded
             *done = true;
             break;
         }

@@ -42,7 +42,7 @@ PGD_INLINE Pushes shade_slot_meta(const DevScene &S, const PathSoA &P, int slot,
         for (int q = 0; q < NQ; ++q) L[q] = make_float4(v, v, v, v);
     }
     // rayWeight * ((1 * Li) + 0), guarded (samplerrenderer.cpp:111-128)
-    *zeroed = path_output<NB>(S, L, Lout, P.item[slot]);
+    *zeroed = path_output<NB>(S, L, Lout, P.item[slot], P.smp[slot]);
     *done = true;
     return Pushes{false, false, false};
 }

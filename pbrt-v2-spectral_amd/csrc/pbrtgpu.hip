@@ -546,6 +546,30 @@ __global__ __launch_bounds__(kTraceBlock) PGD_TRACE_INST_ATTR void k_trace_inst(
     }
 }
 
+// SpectralRenderer singleDirection: band b's luminance guard (spectralrenderer.cpp:163-172)
+// looks at the sample's spectrum as assigned by bands 0 .. b-1 (the rest still 0): its
+// y() = sum_i Y_i c_i / yint (spectrum.h:417-422) < -1e-5 or infinite zeroes band b.  The
+// bands' index ranges are contiguous from 0, so y() is the running sum over the indices
+// already final.  One thread per sample row.
+template <int NB>
+__global__ void k_spec_guard(const DevScene S, float *__restrict__ Lout, uint32_t rows) {
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= rows) return;
+    float *o = Lout + (size_t)r * NB;
+    float yy = 0.f;
+    for (int b = 0; b < S.specBands; ++b) {
+        const int4 tb = S.specTab[b];
+        if (tb.y <= tb.x) continue;
+        const float yv = yy / S.yint;
+        const bool bad = (yv < -1e-5f) || isinf(yv);
+        for (int i = tb.x; i < tb.y; ++i) {
+            float v = o[i];
+            if (bad) o[i] = v = 0.f;
+            yy += S.bandY[i] * v;
+        }
+    }
+}
+
 // film[filmIdx[p]][b] += L(p, s) for s in batch order (spectralImage.cpp:125-131)
 template <int NB>
 __global__ void k_accum(const float *__restrict__ Lbuf, const int *__restrict__ filmIdx, int nPix, int sb,
@@ -994,6 +1018,15 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
             HIPCHK(hipMemcpyAsync(L.hostCnt, P.cnt, CNT_WORDS * 4, hipMemcpyDeviceToHost, L.s));
         }
     }
+    if (c->S.specMode == 1) {   // the rows' luminance guard once every band of them is in
+        for (int l = 1; l < nl; ++l) {
+            HIPCHK(hipEventRecord(c->ev[1], c->lane[l].s));
+            HIPCHK(hipStreamWaitEvent(c->stream, c->ev[1], 0));
+        }
+        const uint32_t rows = src.nItems / (uint32_t)c->S.specItems;
+        hipLaunchKernelGGL(k_spec_guard<NB>, dim3((rows + 255) / 256), dim3(256), 0, c->stream, c->S, Lout, rows);
+        HIPCHK(hipGetLastError());
+    }
     return 0;
 }
 
@@ -1048,6 +1081,36 @@ static int wide_bvh(const pbrtgpu_flat_scene *s, int top, std::vector<float4> *w
         w[2] = make_float4(r.bmin[0], r.bmin[1], r.bmin[2], bits_f((b.meta >> 8) & 0xff));
         w[3] = make_float4(r.bmax[0], r.bmax[1], r.bmax[2], 0.f);
         if (((b.meta >> 8) & 0xff) > 2) return fail(PBRTGPU_E_INVALID, "BVH split axis");
+    }
+    return 0;
+}
+
+// SpectralRendererTask::Run's wave bands (spectralrenderer.cpp:99-100, 124, 180-188) in the
+// reference's own int / float arithmetic (sampledLambdaStart 395, sampledLambdaEnd 715 are
+// ints, spectrum.h:41-42): band b's wavelength 395 + dW b + dW / 2 with dW = float(320 / nWB),
+// its interval i of GetValueAtWavelength (spectrum.h:384-405: step float(320 / N), first i with
+// w0 <= wl < w1) and t = (wl - w0) / (w1 - w0), and its indices [dI b, min(dI (b+1), N-1)),
+// dI = round(N / nWB).  A band with indices whose interval is the last reads c[N], past the
+// spectrum: rejected.
+static int spectral_table(int N, int nWB, std::vector<int4> *tab) {
+    const int lStart = 395, lEnd = 715;
+    const int dI = (int)round(N / nWB);
+    const float dW = (float)((lEnd - lStart) / nWB);
+    const float step = (float)((lEnd - lStart) / N);
+    tab->resize(nWB);
+    for (int b = 0; b < nWB; ++b) {
+        const float wl = lStart + dW * b + (dW / 2);
+        int iv = -1;
+        float t = 0.f;
+        for (int i = 0; i < N; ++i) {
+            const float w0 = lStart + i * step, w1 = lStart + (i + 1) * step;
+            if (wl >= w0 && wl < w1) { iv = i; t = (wl - w0) / (w1 - w0); break; }
+        }
+        const int lo = dI * b, hi = std::max(lo, std::min(dI * (b + 1), N - 1));
+        if (hi > lo && iv == N - 1) return fail(PBRTGPU_E_UNSUPPORTED, "nWaveBands: a band reads past the spectrum (spectrum.h:397)");
+        uint32_t tb;
+        memcpy(&tb, &t, 4);
+        (*tab)[b] = make_int4(lo, hi, iv, (int)tb);
     }
     return 0;
 }
@@ -1138,6 +1201,15 @@ int pbrtgpu_scene_upload(pbrtgpu_ctx *c, const pbrtgpu_flat_scene *s) {
         if (s->meta_strategy != PBRTGPU_META_DEPTH && !s->prim_meta)
             return fail(PBRTGPU_E_INVALID, "metadata mesh / material ids need prim_meta");
     }
+    if (s->renderer != PBRTGPU_RENDERER_SAMPLER && s->renderer != PBRTGPU_RENDERER_SPECTRAL)
+        return fail(PBRTGPU_E_INVALID, "unknown Renderer");
+    std::vector<int4> specTab;
+    if (s->renderer == PBRTGPU_RENDERER_SPECTRAL) {
+        if (s->spectral_sampling != PBRTGPU_SPECTRAL_SINGLE && s->spectral_sampling != PBRTGPU_SPECTRAL_SAMPLER)
+            return fail(PBRTGPU_E_INVALID, "unknown spectral sampling method");
+        if (s->wave_bands < 1 || s->wave_bands > 1024) return fail(PBRTGPU_E_INVALID, "nWaveBands must be 1..1024");
+        if (int e = spectral_table(s->n_bands, s->wave_bands, &specTab)) return e;
+    }
     if (s->integrator == PBRTGPU_INTEGRATOR_DIRECT && s->dl_strategy != PBRTGPU_DL_ALL && s->dl_strategy != PBRTGPU_DL_ONE)
         return fail(PBRTGPU_E_INVALID, "unknown DirectLighting strategy");
     // DirectLighting draws 6 MT19937 values at each of up to 2^(maxdepth-1) - 1 specular
@@ -1201,6 +1273,11 @@ int pbrtgpu_scene_upload(pbrtgpu_ctx *c, const pbrtgpu_flat_scene *s) {
     S.metaStrategy = s->meta_strategy;
     S.primMeta = nullptr;
     if (s->prim_meta) HIPCHK(upload(c, s->prim_meta, (size_t)2 * s->n_prims, &S.primMeta));
+    S.specMode = s->renderer != PBRTGPU_RENDERER_SPECTRAL ? 0 : s->spectral_sampling == PBRTGPU_SPECTRAL_SINGLE ? 1 : 2;
+    S.specBands = S.specMode ? s->wave_bands : 1;
+    S.specItems = S.specMode == 1 ? s->wave_bands : 1;
+    S.specTab = nullptr;
+    if (S.specMode) HIPCHK(upload(c, specTab.data(), specTab.size(), &S.specTab));
     S.dlK = 0;
     for (int i = 0; i < s->n_lights; ++i) {   // RoundUpPow2(max(1, nSamples)) per light
         uint32_t v = (uint32_t)std::max(1, s->lights[i].n_samples) - 1u;
@@ -1573,7 +1650,9 @@ static int render_impl(pbrtgpu_ctx *c, const pbrtgpu_render_desc *d, const int32
     // ---- main batches: per-sample radiance for (pixels x batch samples), then the ordered film sum
     const size_t lbudget = lbuf_budget();   // per-sample radiance per batch
     int sb = (int)std::max<long>(1, std::min<long>(s1 - s0, (long)(lbudget / ((size_t)nPix * NB * 4))));
-    if ((uint64_t)nPix * sb + nSpill > 0x7fffffffull) sb = std::max(1, (int)((0x7fffffffll - nSpill) / nPix));
+    const uint64_t bi = (uint64_t)c->S.specItems;   // paths per camera sample (SpectralRenderer bands)
+    if (((uint64_t)nPix * sb + nSpill) * bi > 0x7fffffffull) sb = (int)((0x7fffffffll / bi - nSpill) / nPix);
+    if (sb < 1) return fail(PBRTGPU_E_UNSUPPORTED, "render call too large for 31-bit path items");
     HIPCHK(c->Lbuf.ensure(((size_t)nPix * sb + nSpill) * NB * 4));
     for (int b0 = s0; b0 < s1; b0 += sb) {
         int n = std::min(sb, s1 - b0);
@@ -1588,6 +1667,7 @@ static int render_impl(pbrtgpu_ctx *c, const pbrtgpu_render_desc *d, const int32
             src.keyBase = src.nItems;
             src.nItems += (uint32_t)nSpill;
         }
+        src.nItems *= (uint32_t)bi;   // keyBase stays in samples
         if (int e = run_wavefront<NB>(c, src, (float *)c->Lbuf.p, countWork, T, &zeroed)) return e;
         if (withSpills) {   // keep the spill radiance (later batches reuse Lbuf), add the pre lists
             HIPCHK(hipMemcpyAsync(c->spillL.p, (const float *)c->Lbuf.p + (size_t)src.keyBase * NB,
@@ -1605,7 +1685,7 @@ static int render_impl(pbrtgpu_ctx *c, const pbrtgpu_render_desc *d, const int32
         HIPCHK(hipEventElapsedTime(&m2, c->ev[6], c->ev[7]));
         T.ms[K_ACCUM] += m2;
         T.launches[K_ACCUM]++;
-        st[PBRTGPU_STAT_PATHS] += (double)((long)nPix * n);
+        st[PBRTGPU_STAT_PATHS] += (double)((long)nPix * n) * (double)bi;
     }
     if (int e = applyLists(postT, postStart, postSrc)) return e;
     HIPCHK(hipStreamSynchronize(c->stream));
@@ -1749,9 +1829,10 @@ static int trace_impl(pbrtgpu_ctx *c, const int32_t *keys, int32_t n, float *out
     HIPCHK(c->scratch[0].ensure((size_t)n * sizeof(int3)));
     HIPCHK(c->scratch[1].ensure((size_t)n * NB * 4));
     HIPCHK(hipMemcpyAsync(c->scratch[0].p, keys, (size_t)n * 12, hipMemcpyHostToDevice, c->stream));
+    if ((uint64_t)n * (uint64_t)c->S.specItems > 0x7fffffffull) return fail(PBRTGPU_E_INVALID, "too many keys");
     ItemSrc ks{};
     ks.keys = (const int3 *)c->scratch[0].p;
-    ks.nItems = (uint32_t)n;
+    ks.nItems = (uint32_t)n * (uint32_t)c->S.specItems;
     Timing T;
     if (int e = run_wavefront<NB>(c, ks, (float *)c->scratch[1].p, countWork, T, nullptr)) return e;
     c->last = T;

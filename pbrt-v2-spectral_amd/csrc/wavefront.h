@@ -410,21 +410,25 @@ PGD_INLINE bool mis_may_reach(const DevScene &S, const pbrtgpu_light &Lt, const 
 }
 
 // camera sample of an item -> fresh path in `slot` (SamplerRendererTask::Run,
-// samplerrenderer.cpp:86-108 + the fixed-seed sampler of DESIGN.md §3.1)
+// samplerrenderer.cpp:86-108 + the fixed-seed sampler of DESIGN.md §3.1).  With the
+// SpectralRenderer's singleDirection method item = sample * nWaveBands + band: the band's
+// path repeats the sample's camera ray and sample values and draws from its own RNG
+// (spectralrenderer.cpp:116-151)
 template <int NB>
 PGD_INLINE void path_start(const DevScene &S, const PathSoA &P, const ItemSrc &src, int slot, uint32_t it) {
     const uint32_t item = src.base + it;
+    const uint32_t sitem = S.specItems > 1 ? item / (uint32_t)S.specItems : item;
     int px, py;
     uint32_t s;
-    if (src.keys && item >= src.keyBase) {
-        const int3 k = src.keys[item - src.keyBase];
+    if (src.keys && sitem >= src.keyBase) {
+        const int3 k = src.keys[sitem - src.keyBase];
         px = k.x; py = k.y; s = (uint32_t)k.z;
     }
     else {
-        uint32_t p = item / (uint32_t)src.sb;
+        uint32_t p = sitem / (uint32_t)src.sb;
         int2 xy = src.pix[p];
         px = xy.x; py = xy.y;
-        s = (uint32_t)src.s0 + (item - p * (uint32_t)src.sb);
+        s = (uint32_t)src.s0 + (sitem - p * (uint32_t)src.sb);
     }
     const uint32_t spp = (uint32_t)S.spp;
     uint32_t hp = pixel_hash(S.seed, px, py);
@@ -453,13 +457,51 @@ PGD_INLINE void path_start(const DevScene &S, const PathSoA &P, const ItemSrc &s
     P.bounce[slot] = -1;
     P.flags[slot] = PF_CONT | PF_LZ;   // L = 0 and beta_0 = 1 are implicit (not stored)
     P.mt[slot] = 0;
-    P.mt[4 * (size_t)P.cap + slot] = path_seed(hp, s);
+    P.mt[4 * (size_t)P.cap + slot] =
+        path_seed(hp, S.specItems > 1 ? s * (uint32_t)S.specItems + (item - sitem * (uint32_t)S.specItems) : s);
+}
+
+// SpectralRenderer output of one band's path (spectralrenderer.cpp:158-188): a NaN
+// radiance -> 0; else the value at the band's wavelength, Lerp(t, c[i], c[i+1]), into the
+// band's indices of the sample's row; samplerDirection rows (one band per sample) and the
+// last band of a singleDirection row also write the unassigned indices' zeros.  The
+// luminance guard on the partly assigned spectrum runs per row after the wavefront
+// (k_spec_guard).  Returns "zeroed".
+template <int NB>
+PGD_INLINE bool spectral_output(const DevScene &S, const float4 (&L)[Bands<NB>::NQ], float *__restrict__ Lout, int item,
+                                uint32_t smp) {
+    const int bi = S.specItems;
+    const int row = bi > 1 ? item / bi : item;
+    const int band = S.specMode == 1 ? item - row * bi : (int)(smp % (uint32_t)S.specBands);
+    const int4 tb = S.specTab[band];
+    bool nan = false;
+    float a = 0.f, b = 0.f;
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+        const float v = 1.f * ((1.f * cmp(L[i / 4], i % 4)) + 0.f);
+        nan = nan || isnan(v);
+        if (i == tb.z) a = v;
+        if (i == tb.z + 1) b = v;
+    }
+    const float t = __int_as_float(tb.w);
+    const float val = (nan || tb.z < 0) ? 0.f : (1.f - t) * a + t * b;
+    float *o = Lout + (size_t)row * NB;
+    const bool tail = S.specMode == 2 || band == S.specBands - 1;
+    // the bands' index ranges are contiguous from 0 up to the last band's end
+    const int tailLo = S.specMode == 2 ? 0 : S.specTab[S.specBands - 1].y;
+    for (int i = tb.x; i < tb.y; ++i) o[i] = val;
+    if (tail)
+        for (int i = tailLo; i < NB; ++i)
+            if (i < tb.x || i >= tb.y) o[i] = 0.f;
+    return nan;
 }
 
 // finished path -> guard (samplerrenderer.cpp:111-128) -> Lout[item]; returns "zeroed"
 template <int NB>
-PGD_INLINE bool path_output(const DevScene &S, const float4 (&L)[Bands<NB>::NQ], float *__restrict__ Lout, int item) {
+PGD_INLINE bool path_output(const DevScene &S, const float4 (&L)[Bands<NB>::NQ], float *__restrict__ Lout, int item,
+                            uint32_t smp) {
     constexpr int NQ = Bands<NB>::NQ;
+    if (S.specMode) return spectral_output<NB>(S, L, Lout, item, smp);
     bool nan = false;
     float yy = 0.f;
 #pragma unroll
@@ -900,7 +942,7 @@ PGD_INLINE Pushes shade_slot(const DevScene &S, const PathSoA &P, int slot, floa
             }
         }
     }
-    if (*done) *zeroed = path_output<NB>(S, L, Lout, P.item[slot]);
+    if (*done) *zeroed = path_output<NB>(S, L, Lout, P.item[slot], P.smp[slot]);
     else {
 #pragma unroll
         for (int q = 0; q < NQ; ++q) P.L[q * c + slot] = L[q];

@@ -29,6 +29,7 @@ int pbrthost_load(const char *path, const pbrthost_overrides *ov, pbrthost_scene
             o.xres = ov->xres; o.yres = ov->yres; o.spp = ov->spp; o.maxdepth = ov->maxdepth;
             o.bands = ov->bands > 0 ? ov->bands : 32; o.seed = ov->seed;
             o.integrator = ov->integrator; o.dl_strategy = ov->dl_strategy; o.meta_strategy = ov->meta_strategy;
+            o.renderer = ov->renderer; o.wave_bands = ov->wave_bands; o.spectral_sampling = ov->spectral_sampling;
         }
         ok = LoadPbrtScene(p, o, s, &e);
     }
@@ -46,6 +47,9 @@ int pbrthost_load(const char *path, const pbrthost_overrides *ov, pbrthost_scene
         if (ov->integrator >= 0) s->integrator = ov->integrator;
         if (ov->dl_strategy >= 0) s->dlStrategy = ov->dl_strategy;
         if (ov->meta_strategy >= 0) s->metaStrategy = ov->meta_strategy;
+        if (ov->renderer >= 0) s->renderer = ov->renderer;
+        if (ov->wave_bands > 0) s->waveBands = ov->wave_bands;
+        if (ov->spectral_sampling >= 0) s->spectralSampling = ov->spectral_sampling;
     }
     *out = reinterpret_cast<pbrthost_scene *>(s);
     return 0;

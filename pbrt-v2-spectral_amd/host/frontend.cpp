@@ -554,6 +554,8 @@ private:
     float tStart = 0.f, tEnd = 1.f;
     ParamSet filmParams, cameraParams, samplerParams, surfParams, accelParams;
     std::string surfName = "directlighting";   // RenderOptions::SurfIntegratorName default (api.cpp:222)
+    std::string rendererName = "sampler";      // RenderOptions::RendererName default (api.cpp:225)
+    ParamSet rendererParams;
     std::string cameraName = "perspective";
     TransformSet cameraToWorld;
     std::vector<std::shared_ptr<LightObj> > lights;
@@ -721,7 +723,7 @@ private:
             else if (d == "Accelerator") { Str(); accelParams = Params(); }
             else if (d == "SurfaceIntegrator") { surfName = Str(); surfParams = Params(); }
             else if (d == "VolumeIntegrator") { Str(); Params(); }
-            else if (d == "Renderer") { Str(); Params(); }
+            else if (d == "Renderer") { rendererName = Str(); rendererParams = Params(); }
             else if (d == "Camera") {
                 cameraName = Str(); cameraParams = Params();
                 for (int i = 0; i < MAXT; ++i) cameraToWorld.t[i] = Inverse(curT.t[i]);
@@ -1597,6 +1599,21 @@ private:
         if (out->integrator == PBRTGPU_INTEGRATOR_METADATA && ms != "mesh" && ms != "material" && ms != "depth")
             out->warnings.push_back("Strategy \"" + ms + "\" for metadata unknown");
         if (ov.meta_strategy >= 0) out->metaStrategy = ov.meta_strategy;
+        // Renderer (api.cpp:1369-1407): "spectralrenderer" with "nWaveBands" (default 32) and
+        // "samplingMethod" ("singleDirection" default, or "samplerDirection"); every other
+        // name renders as "sampler" (the configs override "metropolis")
+        out->renderer = PBRTGPU_RENDERER_SAMPLER;
+        if (rendererName == "spectralrenderer") {
+            out->renderer = PBRTGPU_RENDERER_SPECTRAL;
+            out->waveBands = rendererParams.FindOneInt("nWaveBands", 32);
+            std::string sm = rendererParams.FindOneString("samplingMethod", "singleDirection");
+            if (sm == "singleDirection") out->spectralSampling = PBRTGPU_SPECTRAL_SINGLE;
+            else if (sm == "samplerDirection") out->spectralSampling = PBRTGPU_SPECTRAL_SAMPLER;
+            else throw std::runtime_error("Unrecognized spectral sampling method \"" + sm + "\"");
+        }
+        if (ov.renderer >= 0) out->renderer = ov.renderer;
+        if (ov.wave_bands > 0) out->waveBands = ov.wave_bands;
+        if (ov.spectral_sampling >= 0) out->spectralSampling = ov.spectral_sampling;
         int nsamp = ov.spp > 0 ? ov.spp : samplerParams.FindOneInt("pixelsamples", 4);
         out->spp = (int)RoundUpPow2((uint32_t)nsamp);
         out->seed = ov.seed == 0xffffffffu ? 0u : ov.seed;   // PBRTHOST_KEEP_SEED
@@ -1812,6 +1829,10 @@ void HostScene::Flat(pbrtgpu_flat_scene *f) const {
     f->dl_strategy = dlStrategy;
     f->meta_strategy = metaStrategy;
     f->prim_meta = primMeta.size() == 2 * prims.size() && !prims.empty() ? primMeta.data() : nullptr;
+    f->renderer = renderer;
+    f->wave_bands = waveBands;
+    f->spectral_sampling = spectralSampling;
+    f->pad_r = 0;
 }
 
 }  // namespace pbrtamd

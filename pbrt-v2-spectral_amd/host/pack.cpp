@@ -11,7 +11,7 @@
 namespace pbrtamd {
 
 static const char kMagic[8] = {'P', 'B', 'R', 'T', 'P', 'A', 'C', 'K'};
-static const uint32_t kVersion = 7;   // 6: + merl tables; 7: + metadata ids (5 and 6 still load)
+static const uint32_t kVersion = 8;   // 6: + merl tables; 7: + metadata ids; 8: + Renderer (5-7 still load)
 
 static bool W(gzFile f, const void *p, size_t n) {
     const char *c = (const char *)p;
@@ -79,6 +79,9 @@ bool SavePack(const HostScene &s, const std::string &path, std::string *err) {
     int32_t ms = s.metaStrategy;
     ok = ok && W(f, &ms, 4) && WStr(f, s.surfStrategy) && WArr(f, s.primMeta) && WList(f, s.metaMesh) &&
          WList(f, s.metaMaterials);
+    // v8: the Renderer
+    int32_t rnd[3] = {s.renderer, s.waveBands, s.spectralSampling};
+    ok = ok && W(f, rnd, 12);
     ok = (gzclose(f) == Z_OK) && ok;
     if (!ok && err) *err = "write error on " + path;
     return ok;
@@ -115,6 +118,14 @@ bool LoadPack(const std::string &path, HostScene *s, std::string *err) {
         ok = R(f, &ms, 4) && RStr(f, s->surfStrategy) && RArr(f, s->primMeta) && RList(f, s->metaMesh) &&
              RList(f, s->metaMaterials);
         if (ok) s->metaStrategy = ms;
+    }
+    s->renderer = PBRTGPU_RENDERER_SAMPLER;
+    s->waveBands = 32;
+    s->spectralSampling = PBRTGPU_SPECTRAL_SINGLE;
+    if (ok && ver >= 8) {
+        int32_t rnd[3];
+        ok = R(f, rnd, 12);
+        if (ok) { s->renderer = rnd[0]; s->waveBands = rnd[1]; s->spectralSampling = rnd[2]; }
     }
     gzclose(f);
     if (!ok && err) *err = "bad or truncated scene pack " + path;

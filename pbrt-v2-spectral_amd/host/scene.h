@@ -18,6 +18,9 @@ struct RenderOverrides {
     int integrator = -1;          // PBRTGPU_INTEGRATOR_* to force, -1: the scene's SurfaceIntegrator
     int dl_strategy = -1;         // PBRTGPU_DL_* to force, -1: the scene's "strategy"
     int meta_strategy = -1;       // PBRTGPU_META_* to force, -1: the scene's metadata "strategy"
+    int renderer = -1;            // PBRTGPU_RENDERER_* to force, -1: the scene's Renderer
+    int wave_bands = 0;           // SpectralRenderer nWaveBands to force, <= 0: the scene's
+    int spectral_sampling = -1;   // PBRTGPU_SPECTRAL_* to force, -1: the scene's samplingMethod
 };
 
 // Resolution-independent camera description (perspective.cpp:110-147 parameters); the
@@ -65,6 +68,9 @@ struct HostScene {
     int dlStrategy = 0;                       // PBRTGPU_DL_*
     int metaStrategy = PBRTGPU_META_DEPTH;    // PBRTGPU_META_*
     std::string surfStrategy;                 // the SurfaceIntegrator's "strategy" string (metadata files)
+    int renderer = PBRTGPU_RENDERER_SAMPLER;  // PBRTGPU_RENDERER_* (packs older than v8: sampler)
+    int waveBands = 32;                       // SpectralRenderer nWaveBands
+    int spectralSampling = PBRTGPU_SPECTRAL_SINGLE;
     std::vector<uint32_t> primMeta;           // [prims][2]: primitiveId, materialId a hit reports
     std::vector<std::pair<uint32_t, std::string> > metaMesh;        // top-level primitives: id, shape name
     std::vector<std::pair<uint32_t, std::string> > metaMaterials;   // named materials: id, name (by name)

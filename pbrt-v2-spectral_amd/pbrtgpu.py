@@ -60,17 +60,21 @@ class FlatScene(ctypes.Structure):
                 ("n_kdnodes", I32), ("kdnodes", P),
                 ("n_textures", I32), ("textures", P), ("ewa_lut", P), ("rgb_basis", P),
                 ("n_merl_floats", I32), ("merl", P), ("integrator", I32), ("dl_strategy", I32),
-                ("meta_strategy", I32), ("prim_meta", P)]
+                ("meta_strategy", I32), ("prim_meta", P), ("renderer", I32), ("wave_bands", I32),
+                ("spectral_sampling", I32), ("pad_r", I32)]
 
 
 class Overrides(ctypes.Structure):
     _fields_ = [("xres", I32), ("yres", I32), ("spp", I32), ("maxdepth", I32), ("bands", I32),
-                ("seed", ctypes.c_uint32), ("integrator", I32), ("dl_strategy", I32), ("meta_strategy", I32)]
+                ("seed", ctypes.c_uint32), ("integrator", I32), ("dl_strategy", I32), ("meta_strategy", I32),
+                ("renderer", I32), ("wave_bands", I32), ("spectral_sampling", I32)]
 
 
 INTEGRATORS = {"path": 0, "directlighting": 1, "metadata": 2}
 DL_STRATEGIES = {"all": 0, "one": 1}
 META_STRATEGIES = {"mesh": 0, "material": 1, "depth": 2}
+RENDERERS = {"sampler": 0, "spectral": 1}
+SPECTRAL_SAMPLING = {"single": 0, "sampler": 1}   # samplingMethod singleDirection / samplerDirection
 
 
 class RenderDesc(ctypes.Structure):
@@ -81,7 +85,7 @@ class RenderDesc(ctypes.Structure):
 STAT_PATHS, STAT_KERNEL_MS, STAT_ACCUM_MS, STAT_ZEROED, STAT_SPILLS, STAT_PASSES = 0, 1, 2, 3, 4, 5
 F_ACCUMULATE, F_COUNT_WORK = 1, 2
 KEEP_SEED = 0xFFFFFFFF
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 
 class Timing(ctypes.Structure):
@@ -189,21 +193,32 @@ class Scene:
         host_lib().pbrthost_flat(self._h, ctypes.byref(self.flat))
 
     @staticmethod
-    def load(path, xres=-1, yres=-1, spp=-1, maxdepth=-1, bands=0, seed=None, integrator=None, strategy=None):
+    def load(path, xres=-1, yres=-1, spp=-1, maxdepth=-1, bands=0, seed=None, integrator=None, strategy=None,
+             renderer=None, wave_bands=0, sampling=None):
         """bands <= 0: the pack's own band count, or 32 (the reference build) for a .pbrt file.
         integrator / strategy: None keeps the scene's SurfaceIntegrator ("path",
         "directlighting" or "metadata") and its "strategy" (DirectLighting "all" / "one",
-        metadata "mesh" / "material" / "depth")."""
+        metadata "mesh" / "material" / "depth").  renderer ("sampler" / "spectral"),
+        wave_bands and sampling ("single" / "sampler"): None / 0 keep the scene's Renderer
+        and its "nWaveBands" / "samplingMethod"."""
         h = P()
         err = ctypes.create_string_buffer(1024)
         ov = Overrides(xres, yres, spp, maxdepth, bands, KEEP_SEED if seed is None else seed,
                        -1 if integrator is None else INTEGRATORS[integrator],
-                       DL_STRATEGIES.get(strategy, -1), META_STRATEGIES.get(strategy, -1))
+                       DL_STRATEGIES.get(strategy, -1), META_STRATEGIES.get(strategy, -1),
+                       -1 if renderer is None else RENDERERS[renderer], wave_bands,
+                       -1 if sampling is None else SPECTRAL_SAMPLING[sampling])
         if strategy is not None and strategy not in DL_STRATEGIES and strategy not in META_STRATEGIES:
             raise ValueError("unknown strategy %r" % strategy)
         if host_lib().pbrthost_load(path.encode(), ctypes.byref(ov), ctypes.byref(h), err, 1024) != 0:
             raise RuntimeError("scene load failed: %s" % err.value.decode())
         return Scene(h)
+
+    def paths_per_sample(self):
+        """paths traced per camera sample: nWaveBands for the SpectralRenderer's
+        singleDirection method, else 1"""
+        f = self.flat
+        return f.wave_bands if f.renderer == RENDERERS["spectral"] and f.spectral_sampling == 0 else 1
 
     def set_render(self, spp=-1, maxdepth=-1, seed=0):
         host_lib().pbrthost_set_render(self._h, spp, maxdepth, seed)

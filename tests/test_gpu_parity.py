@@ -439,6 +439,72 @@ def test_metadata_vs_reference_golden(pg, base):
     assert np.array_equal(film.view(np.int32), of.view(np.int32))
 
 
+SPEC = ["killeroo_spec32_%s_40x32s4", "coverage_spec3_%s_48x36s4", "coverage_specsampler8_%s_48x36s8",
+        "killeroo_spec5_dl_%s_32x24s2"]
+
+
+@pytest.mark.parametrize("base", SPEC)
+def test_spectral_renderer_vs_reference_golden(pg, base):
+    """SpectralRenderer on the GPU (singleDirection: nWaveBands paths per camera sample, each
+    writing its band's indices of the sample's row, then k_spec_guard; samplerDirection: band
+    s % nWaveBands) against the reference harness's per-sample spectra and film, and sample by
+    sample against the oracle."""
+    from conftest import GOLDEN
+    from test_oracle_golden import spec_scene
+    g = np.load(os.path.join(GOLDEN, base % "paths" + ".npz"))
+    gf = np.load(os.path.join(GOLDEN, base % "film" + ".npz"))
+    scene = spec_scene(pg, g, base % "paths")
+    with pg.Device(0) as d:
+        d.upload(scene)
+        L = d.trace_paths(g["keys"])
+        d.render()
+        film = d.film()
+    ref = g["L"]
+    same = np.all(L.view(np.int32) == ref.view(np.int32), axis=1)
+    rel = np.abs(L - ref).max(axis=1) / np.maximum(np.abs(ref).max(axis=1), 1e-30)
+    # a singleDirection sample is nWaveBands paths: one last-ulp transcendental difference
+    # (DESIGN.md §3.2) in any of them shows in its row
+    assert same.mean() >= 0.80, "bit-exact samples %d/%d" % (same.sum(), len(same))
+    assert (rel > 1e-4).mean() <= 2e-3
+    assert np.abs(film - gf["film"]).max() / np.abs(gf["film"]).max() < 1e-4
+    o = pg.oracle()
+    Lo = o.trace_paths(scene, g["keys"])
+    assert np.all(L.view(np.int32) == Lo.view(np.int32), axis=1).mean() >= 1 - 1e-3
+    assert np.abs(L - Lo).max() / np.abs(Lo).max() < 1e-4
+
+
+def test_spectral_renderer_lanes_batches_and_rejects(pg, monkeypatch):
+    """The bands of a sample land in its row whatever lane, slot or Lbuf batch traces them: a
+    tiny slot pool and a tiny Lbuf give the same samples and film bit for bit; nWaveBands whose
+    band reads past the spectrum (60 bands at the default 32 wave bands, spectrum.h:397) and
+    unknown sampling methods are refused."""
+    from conftest import PACKS
+    scene = pg.Scene.load(os.path.join(PACKS, "coverage.pack"), xres=40, yres=30, spp=4, maxdepth=6,
+                          renderer="spectral", wave_bands=7, sampling="single")
+    keys = _keys(scene)
+    with pg.Device(0) as d:
+        d.upload(scene)
+        L = d.trace_paths(keys)
+        d.render()
+        film = d.film()
+        monkeypatch.setenv("PBRTGPU_SLOTS", "193")
+        monkeypatch.setenv("PBRTGPU_LBUF_MB", "1")
+        Ls = d.trace_paths(keys)
+        d.render()
+        films = d.film()
+        assert np.array_equal(L.view(np.int32), Ls.view(np.int32))
+        assert np.array_equal(film.view(np.int32), films.view(np.int32))
+        Lo = pg.oracle().trace_paths(scene, keys)
+        assert np.all(L.view(np.int32) == Lo.view(np.int32), axis=1).mean() >= 1 - 1e-3
+        m = pg.Scene.load(os.path.join(PACKS, "metal.pack"), xres=8, yres=8, spp=1, renderer="spectral")
+        assert m.flat.n_bands == 60 and m.flat.wave_bands == 32
+        with pytest.raises(RuntimeError, match="past the spectrum"):
+            d.upload(m)
+        scene.flat.spectral_sampling = 5
+        with pytest.raises(RuntimeError, match="sampling"):
+            d.upload(scene)
+
+
 def test_integrator_scene_checks(pg):
     """pbrtgpu_scene_upload refuses what the integrator steps cannot render exactly: a
     DirectLighting maxdepth beyond the first MT19937 block (> 6), an unknown metadata strategy,

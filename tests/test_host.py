@@ -190,3 +190,35 @@ def test_metadata_ids_and_text_files(pg, tmp_path):
     assert int(rows[1][0]) in ids and int(rows[3][0]) in ids and int(rows[4][0]) in ids
     assert int(rows[0][0]) not in ids          # a refined mesh reports its triangles' ids
     assert d.flat.meta_strategy == pg.META_STRATEGIES["material"]
+
+
+def test_spectral_renderer_directive(pg, tmp_path):
+    """Renderer "spectralrenderer" (api.cpp:1377-1403): nWaveBands (default 32) and
+    samplingMethod (singleDirection default, samplerDirection; others refused) reach the flat
+    scene; the pack keeps them; the overrides replace them; other renderers render as sampler."""
+    here = os.path.dirname(os.path.abspath(__file__))
+    src = open(os.path.join(here, "scenes", "metadata.pbrt")).read()
+    assert "Renderer" not in src
+
+    def scene_with(line):
+        p = tmp_path / ("r%d.pbrt" % abs(hash(line)))
+        p.write_text(src.replace("WorldBegin", line + "\nWorldBegin", 1))
+        return str(p)
+    s = pg.Scene.load(scene_with('Renderer "spectralrenderer"'))
+    assert (s.flat.renderer, s.flat.wave_bands, s.flat.spectral_sampling) == (1, 32, 0)
+    assert s.paths_per_sample() == 32
+    s = pg.Scene.load(scene_with('Renderer "spectralrenderer" "integer nWaveBands" [5] '
+                                 '"string samplingMethod" "samplerDirection"'))
+    assert (s.flat.renderer, s.flat.wave_bands, s.flat.spectral_sampling) == (1, 5, 1)
+    assert s.paths_per_sample() == 1
+    out = str(tmp_path / "spec.pack")
+    s.save_pack(out)
+    t = pg.Scene.load(out)
+    assert (t.flat.renderer, t.flat.wave_bands, t.flat.spectral_sampling) == (1, 5, 1)
+    t = pg.Scene.load(out, renderer="spectral", wave_bands=9, sampling="single")
+    assert (t.flat.renderer, t.flat.wave_bands, t.flat.spectral_sampling) == (1, 9, 0)
+    assert pg.Scene.load(out, renderer="sampler").flat.renderer == 0
+    with pytest.raises(RuntimeError, match="spectral sampling"):
+        pg.Scene.load(scene_with('Renderer "spectralrenderer" "string samplingMethod" "diagonal"'))
+    assert pg.Scene.load(scene_with('Renderer "metropolis"')).flat.renderer == 0
+    assert pg.Scene.load(PACK).flat.renderer == 0    # packs before v8: the SamplerRenderer

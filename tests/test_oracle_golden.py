@@ -199,3 +199,39 @@ def test_metadata_film_bit_exact_vs_reference(pg, ora_libm, name):
     g = np.load(os.path.join(GOLDEN, name + ".npz"))
     film, _ = ora_libm.render(meta_scene(pg, g, name), threads=8)
     assert np.array_equal(film.view(np.int32), g["film"].view(np.int32))
+
+
+SPEC = ["killeroo_spec32_%s_40x32s4", "coverage_spec3_%s_48x36s4", "coverage_specsampler8_%s_48x36s8",
+        "killeroo_spec5_dl_%s_32x24s2"]
+
+
+def spec_scene(pg, g, name):
+    """The scene of a SpectralRenderer fixture: the pack (or tests/scenes/coverage.pbrt's pack)
+    rendered with renderer "spectral", the fixture's nWaveBands and samplingMethod (and the
+    DirectLightingIntegrator for the _dl fixture)."""
+    w, h, spp, seed, md = [int(v) for v in g["config"]]
+    pack = "coverage.pack" if name.startswith("coverage") else "killeroo-simple.pack"
+    nwb = int(name.split("_")[1].replace("specsampler", "").replace("spec", ""))
+    return pg.Scene.load(os.path.join(PACKS, pack), xres=w, yres=h, spp=spp, maxdepth=md, seed=seed,
+                         integrator="directlighting" if "_dl_" in name else "path", renderer="spectral", wave_bands=nwb,
+                         sampling="sampler" if "specsampler" in name else "single")
+
+
+@pytest.mark.parametrize("name", [m % "paths" for m in SPEC])
+def test_spectral_renderer_paths_bit_exact_vs_reference(pg, ora_libm, name):
+    """SpectralRenderer (spectralrenderer.cpp:98-190): per camera sample and wave band a path
+    whose radiance at the band's wavelength (Spectrum::GetValueAtWavelength, spectrum.h:384-405)
+    fills the band's indices; the oracle against the reference harness, bit for bit."""
+    g = np.load(os.path.join(GOLDEN, name + ".npz"))
+    scene = spec_scene(pg, g, name)
+    assert scene.flat.renderer == pg.RENDERERS["spectral"]
+    L = ora_libm.trace_paths(scene, g["keys"])
+    same = np.all(L.view(np.int32) == g["L"].view(np.int32), axis=1)
+    assert same.all(), "samples differing: %d / %d" % ((~same).sum(), len(same))
+
+
+@pytest.mark.parametrize("name", [m % "film" for m in SPEC])
+def test_spectral_renderer_film_bit_exact_vs_reference(pg, ora_libm, name):
+    g = np.load(os.path.join(GOLDEN, name + ".npz"))
+    film, _ = ora_libm.render(spec_scene(pg, g, name), threads=8)
+    assert np.array_equal(film.view(np.int32), g["film"].view(np.int32))

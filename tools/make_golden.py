@@ -46,7 +46,7 @@ Fixtures (numpy .npz, inputs + expected outputs only):
   killeroo_dat_40x32s4.npz        the raw film of the restatement film AND the .dat the
                                   reference's own SpectralImageNoCameraFilm wrote for the same
                                   samples (--refdat): pins AddSample and the WriteImage payload
-Usage: python tools/make_golden.py [--only keys|dat|merl|dl|meta]   (after `make -C oracle ref` and `make -C oracle ref60`)
+Usage: python tools/make_golden.py [--only keys|dat|merl|dl|meta|spec]   (after `make -C oracle ref` and `make -C oracle ref60`)
 """
 import os
 import subprocess
@@ -184,6 +184,28 @@ def meta_fixtures(tmp):
         film_fixture("%s_film_%s" % (stem, tag), res, spp, 0, 5, tmp, scene=scene, extra=ex)
 
 
+# SpectralRenderer (renderers/spectralrenderer.cpp): (fixture stem, scene, res, spp, nWaveBands,
+# samplingMethod, surface integrator, path stride).  Python loads the packs / coverage scene with
+# renderer="spectral", wave_bands and sampling (and the integrator).
+SPEC_FIXTURES = [
+    ("killeroo_spec32", "killeroo-simple.pbrt", (40, 32), 4, 32, "single", "path", 1),   # the defaults
+    ("coverage_spec3", "COVERAGE", (48, 36), 4, 3, "single", "path", 1),
+    ("coverage_specsampler8", "COVERAGE", (48, 36), 8, 8, "sampler", "path", 1),
+    ("killeroo_spec5_dl", "killeroo-simple.pbrt", (32, 24), 2, 5, "single", "directlighting", 1),
+]
+
+
+def spec_fixtures(tmp):
+    for stem, scene, res, spp, nwb, method, surf, every in SPEC_FIXTURES:
+        if scene == "COVERAGE":
+            scene = os.path.join(ROOT, "tests", "scenes", "coverage.pbrt")
+        ex = ("--spectral", str(nwb), method, "--surf", surf)
+        md = 6 if "coverage" in stem else 5
+        tag = "%dx%ds%d" % (res[0], res[1], spp)
+        paths_fixture("%s_paths_%s" % (stem, tag), res, spp, 0, md, every, tmp, scene=scene, extra=ex)
+        film_fixture("%s_film_%s" % (stem, tag), res, spp, 0, md, tmp, scene=scene, extra=ex)
+
+
 def merl_fixtures(tmp):
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     import make_merl
@@ -214,6 +236,8 @@ def main():
                 dl_fixtures(tmp)
             elif only == "meta":
                 meta_fixtures(tmp)
+            elif only == "spec":
+                spec_fixtures(tmp)
         return
     with tempfile.TemporaryDirectory() as tmp:
         paths_fixture("killeroo_paths_64x64s4", (64, 64), 4, 0, 5, 5, tmp)
@@ -242,6 +266,8 @@ def main():
         dat_fixture("killeroo_dat_40x32s4", (40, 32), 4, tmp)
         merl_fixtures(tmp)
         dl_fixtures(tmp)
+        meta_fixtures(tmp)
+        spec_fixtures(tmp)
         fn = os.path.join(tmp, "mt.bin")
         run(["-", "--kat-mt", fn])
         raw = np.fromfile(fn, dtype=np.uint32).reshape(6, 65)
