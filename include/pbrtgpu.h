@@ -202,6 +202,25 @@ typedef struct pbrtgpu_camera {
     int32_t pad[2];
 } pbrtgpu_camera;
 
+/* RealisticDiffractionCamera (cameras/realisticDiffraction.cpp:32-94 parameters, 99-193
+ * lens file, 347-468 Snell's law and element intersection, 478-1164 GenerateRay; ray
+ * differentials by Camera::GenerateRayDifferential, camera.cpp:52-81): film rays traced from
+ * the sensor through the lens elements, last element first.  Diffraction, pinhole arrays /
+ * microlenses and the eye IOR curves are not part of this build (pbrthost refuses them). */
+typedef struct pbrtgpu_lens {
+    int32_t n_elements;           /* lens-file elements, scene side first */
+    int32_t chromatic;            /* chromaticAberrationEnabled: n + (lambda - 550) * -0.04 / 300 where n != 1 */
+    float film_distance;          /* "filmdistance" */
+    float film_diag;              /* "filmdiag" */
+    float curve_radius;           /* "curveRadius" (0: flat sensor) */
+    float aperture_offset[2];     /* "x_aperture_offset", "y_aperture_offset" */
+    float film_center[2];         /* "film_center_x", "film_center_y" */
+    float pinhole_exit[3];        /* "pinhole_exit_x/y/z": rays aim there unless one is -1 */
+    float focal_length, fstop;    /* the lens file's first value; focal_length / "aperture_diameter" */
+    const float *elements;        /* [n_elements][4] radius, separation, n, aperture (an aperture stop,
+                                   * radius 0, carries "aperture_diameter") */
+} pbrtgpu_lens;
+
 typedef struct pbrtgpu_flat_scene {
     int32_t abi_version;
     int32_t n_bands;              /* nSpectralSamples */
@@ -244,7 +263,8 @@ typedef struct pbrtgpu_flat_scene {
     int32_t renderer;             /* PBRTGPU_RENDERER_*: the scene's Renderer */
     int32_t wave_bands;           /* SpectralRenderer "nWaveBands" (api.cpp:1378, default 32) */
     int32_t spectral_sampling;    /* SpectralRenderer "samplingMethod": PBRTGPU_SPECTRAL_* */
-    int32_t pad_r;
+    int32_t camera_type;          /* PBRTGPU_CAMERA_*: "perspective" (camera) or "realisticDiffraction" (lens) */
+    pbrtgpu_lens lens;
 } pbrtgpu_flat_scene;
 
 /* SurfaceIntegrator of a flattened scene: "path" (integrators/path.cpp:44-115),
@@ -265,6 +285,7 @@ enum { PBRTGPU_META_MESH = 0, PBRTGPU_META_MATERIAL = 1, PBRTGPU_META_DEPTH = 2 
  * per sample, path b drawing from RNG(path_seed(hp, s nWaveBands + b))); samplerDirection
  * traces band s % nWaveBands of sample s only.  A sample's unassigned indices are 0. */
 enum { PBRTGPU_RENDERER_SAMPLER = 0, PBRTGPU_RENDERER_SPECTRAL = 1 };
+enum { PBRTGPU_CAMERA_PERSPECTIVE = 0, PBRTGPU_CAMERA_REALISTIC = 1 };
 enum { PBRTGPU_SPECTRAL_SINGLE = 0, PBRTGPU_SPECTRAL_SAMPLER = 1 };
 
 /* ---- render description ----------------------------------------------------------- */

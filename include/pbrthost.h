@@ -52,6 +52,9 @@ int pbrthost_info(pbrthost_scene *s, int64_t *info, int n);
 int pbrthost_write_metadata(pbrthost_scene *s, const char *image_file);
 /* reference .dat writer; film [H][W][N] float32 (raw sums), weight [H][W] or NULL */
 int pbrthost_write_dat(const char *path, const float *film, const float *weight, int W, int H, int N);
+/* the same for a scene's film (its crop window's W x H, its bands), line 2 holding the
+ * RealisticDiffractionCamera's focal length, f-stop and field of view (spectralImage.cpp:356-360) */
+int pbrthost_write_dat_scene(const pbrthost_scene *s, const char *path, const float *film, const float *weight);
 
 /* SampledSpectrum::FromRGB (spectrum.cpp:93-178) at the given band count (32, 60 or 30);
  * illuminant != 0 selects SPECTRUM_ILLUMINANT.  out[bands]. */

@@ -2016,9 +2016,138 @@ static Ray camera_ray(const Ctx *c, float imageX, float imageY, float lensU, flo
     return o;
 }
 
+/* ---- RealisticDiffractionCamera (cameras/realisticDiffraction.cpp), diffraction off.
+ * PARITY UNPINNED: the camera's TU includes GSL headers this image lacks, so the reference
+ * harness cannot run it; this restatement and the GPU's are checked against each other. */
+/* IntersectLensEl (realisticDiffraction.cpp:412-468) */
+static int lens_el_hit(const Ray *r, float radius, V dist, float *tHit, V *nrm) {
+    float m[16] = {1.f, 0.f, 0.f, dist.x, 0.f, 1.f, 0.f, dist.y, 0.f, 0.f, 1.f, dist.z, 0.f, 0.f, 0.f, 1.f};
+    V o = xpoint(m, r->o), d = xvec(m, r->d);
+    if (radius < 0) radius = -radius;
+    float A = d.x * d.x + d.y * d.y + d.z * d.z;
+    float B = 2 * (d.x * o.x + d.y * o.y + d.z * o.z);
+    float C = o.x * o.x + o.y * o.y + o.z * o.z - radius * radius;
+    float t0, t1;
+    if (!quadratic(A, B, C, &t0, &t1)) return 0;
+    if (t0 > r->maxt || t1 < r->mint) return 0;
+    float th = t0;
+    if (t0 < r->mint) {
+        th = t1;
+        if (th > r->maxt) return 0;
+    }
+    *tHit = th;
+    *nrm = vnorm(v3(d.x * th + o.x, d.y * th + o.y, d.z * th + o.z));
+    return 1;
+}
+/* applySnellsLaw (realisticDiffraction.cpp:347-410), chromatic model in double (-.04) */
+static void lens_snell(float n1, float n2, float lensRadius, V nrm, Ray *ray, float wl, int chromatic) {
+    if (chromatic) {
+        if (n1 != 1) n1 = (float)((double)(wl - 550) * -.04 / (300) + (double)n1);
+        if (n2 != 1) n2 = (float)((double)(wl - 550) * -.04 / (300) + (double)n2);
+    }
+    V s1 = ray->d;
+    if (lensRadius > 0) nrm = vneg(nrm);
+    V cr = vcross(nrm, s1);
+    float radicand = 1 - (n1 / n2) * (n1 / n2) * vdot(cr, cr);
+    if (radicand < 0) { ray->d = v3(0.f, 0.f, 0.f); return; }
+    V s2 = vsub(vmul(vcross(nrm, vcross(vmul(nrm, -1.f), s1)), n1 / n2), vmul(nrm, sqrtf(radicand)));
+    ray->d = vnorm(s2);
+}
+/* GenerateRay (realisticDiffraction.cpp:478-1164) without diffraction / pinhole arrays /
+ * microlenses: returns the weight (0: blocked) */
+static float lens_ray(const Ctx *c, float imageX, float imageY, float lensU, float lensV, float timeU, float wl, Ray *out) {
+    const pbrtgpu_camera *cam = &c->s->camera;
+    const pbrtgpu_lens *Ls = &c->s->lens;
+    const float xr2 = (float)cam->xres / 2.f, yr2 = (float)cam->yres / 2.f;
+    V sp;
+    sp.x = (float)(-((double)(imageX - xr2) - .25) / (double)xr2);
+    sp.y = (float)(((double)(imageY - yr2) - .25) / (double)yr2);
+    sp.z = -Ls->film_distance;
+    float aspect = (float)cam->xres / (float)cam->yres;
+    float width = Ls->film_diag / sqrtf((1.f + 1.f / (aspect * aspect)));
+    float height = width / aspect;
+    sp.x = sp.x * width / 2.f + Ls->film_center[0];
+    sp.y = sp.y * height / 2.f + Ls->film_center[1];
+    if (Ls->curve_radius != 0) {
+        float R = Ls->curve_radius, th = sp.x / R, ph = sp.y / R;
+        sp.x = R * COSF(ph) * SINF(th);
+        sp.z = R * COSF(ph) * COSF(th);
+        sp.y = R * SINF(ph);
+        float sc = (-Ls->film_distance - R);
+        sp.z = sc + sp.z;
+    }
+    float lu, lv;
+    concentric_disk(lensU, lensV, &lu, &lv);
+    const int n = Ls->n_elements;
+    const float *E = Ls->elements;
+    float firstAp = E[4 * (n - 1) + 3] / 2, firstR = E[4 * (n - 1)];
+    float zI = firstR == 0 ? 0.f : (-firstR - sqrtf(firstR * firstR - firstAp * firstAp));
+    lu *= firstAp;
+    lv *= firstAp;
+    V pol = v3(lu, lv, zI);
+    if (Ls->pinhole_exit[0] != -1 && Ls->pinhole_exit[1] != -1 && Ls->pinhole_exit[2] != -1)
+        pol = v3(Ls->pinhole_exit[0], Ls->pinhole_exit[1], Ls->pinhole_exit[2]);
+    Ray r;
+    r.o = sp;
+    r.d = vnorm(vsub(pol, r.o));
+    r.mint = 0.f; r.maxt = INFINITY; r.time = 0.f;
+    float lensDist = 0.f;
+    for (int i = n - 1; i >= 0; --i) {
+        float rad = E[4 * i], ap = E[4 * i + 3];
+        lensDist += E[4 * i + 1];
+        r.o = sp;
+        if (rad == 0) {
+            float tA = (i == n - 1) ? Ls->film_distance / r.d.z : (lensDist - r.o.z) / (r.d.z);
+            V ai = v3(r.o.x + r.d.x * tA, r.o.y + r.d.y * tA, r.o.z + r.d.z * tA);
+            float dx = ai.x - Ls->aperture_offset[0], dy = ai.y - Ls->aperture_offset[1];
+            if ((double)(dx * dx + dy * dy) > (double)(ap * ap) * .25) return 0.f;
+            sp = ai;
+        } else {
+            float tHit = 0.f;
+            V nrm = v3(0.f, 0.f, 1.f);
+            if (!lens_el_hit(&r, rad, v3(0.f, 0.f, rad - lensDist), &tHit, &nrm)) return 0.f;
+            V ip = v3(tHit * r.d.x + r.o.x, tHit * r.d.y + r.o.y, tHit * r.d.z + r.o.z);
+            if (ip.x * ip.x + ip.y * ip.y >= ap * ap / 4.f) return 0.f;
+            float n1 = E[4 * i + 2], n2 = 1;
+            if (i - 1 >= 0) {
+                n2 = E[4 * (i - 1) + 2];
+                if (n2 == 0) n2 = E[4 * (i - 2) + 2];
+            }
+            lens_snell(n1, n2, rad, nrm, &r, wl, Ls->chromatic);
+            sp = ip;
+        }
+    }
+    r.o = sp;
+    r.time = lerpf(timeU, cam->shutter_open, cam->shutter_close);
+    out->o = xpoint(cam->cam2world_m, r.o);
+    out->d = vnorm(xvec(cam->cam2world_m, r.d));
+    out->mint = r.mint; out->maxt = r.maxt; out->time = r.time;
+    return 1.f;
+}
+/* Camera::GenerateRayDifferential (camera.cpp:52-81) + ScaleDifferentials(1 / sqrtf(spp)) */
+static float lens_ray_diff(const Ctx *c, float imageX, float imageY, float lensU, float lensV, float timeU, float wl,
+                           Ray *ray, RayDiff *rd) {
+    float wt = lens_ray(c, imageX, imageY, lensU, lensV, timeU, wl, ray);
+    Ray rx, ry;
+    float sx = imageX + 1.f;
+    float wtx = lens_ray(c, sx, imageY, lensU, lensV, timeU, wl, &rx);
+    sx = sx - 1.f;
+    float wty = lens_ray(c, sx, imageY + 1.f, lensU, lensV, timeU, wl, &ry);
+    if (wtx == 0.f || wty == 0.f) return 0.f;
+    float sc = 1.f / sqrtf((float)c->s->spp);
+    rd->rxo = vadd(ray->o, vmul(vsub(rx.o, ray->o), sc));
+    rd->ryo = vadd(ray->o, vmul(vsub(ry.o, ray->o), sc));
+    rd->rxd = vadd(ray->d, vmul(vsub(rx.d, ray->d), sc));
+    rd->ryd = vadd(ray->d, vmul(vsub(ry.d, ray->d), sc));
+    rd->has = 1;
+    return wt;
+}
+
 /* One camera path: sample -> ray -> rayWeight * Li (samplerrenderer.cpp:86-110), the path
- * drawing from RNG(path_seed(hp, rngIdx)) */
-static void camera_path(const Ctx *c, int px, int py, uint32_t s, uint32_t rngIdx, float *L, float *imgX, float *imgY) {
+ * drawing from RNG(path_seed(hp, rngIdx)); wl is the ray's wavelength (0 under the
+ * SamplerRenderer, Ray() in geometry.h:317) */
+static void camera_path(const Ctx *c, int px, int py, uint32_t s, uint32_t rngIdx, float wl, float *L, float *imgX,
+                        float *imgY) {
     uint32_t spp = (uint32_t)c->s->spp;
     PathSampler ps;
     ps.hp = pixel_hash(c->s->seed, px, py);
@@ -2032,8 +2161,16 @@ static void camera_path(const Ctx *c, int px, int py, uint32_t s, uint32_t rngId
     rng_seed(&ps.rng, path_seed(ps.hp, rngIdx));
     ps.rng.mti = 624;   /* RNG ctor: Seed() leaves mti == N, first draw regenerates */
     RayDiff rd;
-    Ray r = camera_ray(c, imageX, imageY, lens[0], lens[1], timeU, &rd);
+    Ray r;
     float Lr[MAXB];
+    if (c->s->camera_type == PBRTGPU_CAMERA_REALISTIC &&
+        lens_ray_diff(c, imageX, imageY, lens[0], lens[1], timeU, wl, &r, &rd) == 0.f) {
+        for (int i = 0; i < c->nb; ++i) L[i] = 0.f;   /* rayWeight 0: L = 0, nothing traced */
+        if (imgX) *imgX = imageX;
+        if (imgY) *imgY = imageY;
+        return;
+    }
+    if (c->s->camera_type != PBRTGPU_CAMERA_REALISTIC) r = camera_ray(c, imageX, imageY, lens[0], lens[1], timeU, &rd);
     if (c->s->integrator == PBRTGPU_INTEGRATOR_DIRECT) dl_radiance(c, r, &rd, 0, &ps, Lr);
     else if (c->s->integrator == PBRTGPU_INTEGRATOR_METADATA) meta_radiance(c, r, Lr);
     else radiance(c, r, &rd, &ps, Lr);
@@ -2045,7 +2182,7 @@ static void camera_path(const Ctx *c, int px, int py, uint32_t s, uint32_t rngId
 /* SamplerRenderer: the path and the NaN / negative / infinite luminance guard
  * (samplerrenderer.cpp:111-128) */
 static int sampler_sample(const Ctx *c, int px, int py, uint32_t s, float *L, float *imgX, float *imgY) {
-    camera_path(c, px, py, s, s, L, imgX, imgY);
+    camera_path(c, px, py, s, s, 0.f, L, imgX, imgY);
     int nb = c->nb, bad = 0;
     int nan = 0;
     for (int i = 0; i < nb; ++i) if (isnan(L[i])) nan = 1;
@@ -2079,7 +2216,8 @@ static int spectral_sample(const Ctx *c, int px, int py, uint32_t s, float *L, f
     for (int sb = 0; sb < mm; ++sb) {
         const int b = single ? sb : (int)(s % (uint32_t)nWB);
         float Lr[MAXB];
-        camera_path(c, px, py, s, single ? s * (uint32_t)nWB + (uint32_t)b : s, Lr, imgX, imgY);
+        const float wl = 395 + dW * b + (dW / 2);
+        camera_path(c, px, py, s, single ? s * (uint32_t)nWB + (uint32_t)b : s, wl, Lr, imgX, imgY);
         int nan = 0;
         for (int i = 0; i < N; ++i) if (isnan(Lr[i])) nan = 1;
         int zero = nan;
@@ -2089,7 +2227,6 @@ static int spectral_sample(const Ctx *c, int px, int py, uint32_t s, float *L, f
             else if (isinf(yv)) zero = 1;
         }
         if (zero) { for (int i = 0; i < N; ++i) Lr[i] = 0.f; ++bad; }
-        const float wl = 395 + dW * b + (dW / 2);
         const int lo = dI * b, hi = (dI * (b + 1) < N - 1) ? dI * (b + 1) : N - 1;
         if (hi <= lo) continue;
         float v = 0.f;

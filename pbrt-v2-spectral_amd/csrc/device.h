@@ -277,6 +277,11 @@ struct DevScene {
     int specBands;                    // nWaveBands
     int specItems;
     const int4 *specTab;              // [nWaveBands]: assigned indices [x, y), interval z (-1: none), t (bits)
+    const float *specWl;              // [nWaveBands]: the band's ray wavelength
+    int camType;                      // PBRTGPU_CAMERA_*
+    int lensN, lensChromatic;         // RealisticDiffractionCamera: elements, chromaticAberrationEnabled
+    float lensFilmDist, lensFilmDiag, lensCurveR, lensApOff[2], lensFilmC[2], lensPinhole[3];
+    const float4 *lensEl;             // [lensN]: radius, separation, n, aperture
 };
 
 // scene features a shade kernel is specialised for (k_shade<NB, FEAT>): a scene without
@@ -1972,6 +1977,164 @@ PGD_INLINE Ray camera_ray(const pbrtgpu_camera &cam, float imageX, float imageY,
     o.o = cam_point(cw, r.o);
     o.d = xvec(cw, r.d);
     return o;
+}
+
+// ---- RealisticDiffractionCamera (cameras/realisticDiffraction.cpp), diffraction off
+// IntersectLensEl (realisticDiffraction.cpp:412-468): the sphere of |radius| centred by
+// Translate(dist); tHit, and the normalised hit point (in the shifted frame) as the normal
+PGD_INLINE bool lens_el_hit(const Ray &r, float radius, V dist, float *tHit, V *nrm) {
+    const float m[16] = {1.f, 0.f, 0.f, dist.x, 0.f, 1.f, 0.f, dist.y, 0.f, 0.f, 1.f, dist.z, 0.f, 0.f, 0.f, 1.f};
+    const V o = cam_point(m, r.o), d = xvec(m, r.d);
+    if (radius < 0) radius = -radius;
+    const float A = d.x * d.x + d.y * d.y + d.z * d.z;
+    const float B = 2 * (d.x * o.x + d.y * o.y + d.z * o.z);
+    const float C = o.x * o.x + o.y * o.y + o.z * o.z - radius * radius;
+    float t0, t1;
+    if (!quadratic(A, B, C, &t0, &t1)) return false;
+    if (t0 > r.maxt || t1 < r.mint) return false;
+    float th = t0;
+    if (t0 < r.mint) {
+        th = t1;
+        if (th > r.maxt) return false;
+    }
+    *tHit = th;
+    *nrm = vnorm(v3(d.x * th + o.x, d.y * th + o.y, d.z * th + o.z));
+    return true;
+}
+// applySnellsLaw (realisticDiffraction.cpp:347-410) without the eye IOR curves; the
+// chromatic model's arithmetic is double (the -.04 literal)
+PGD_INLINE void lens_snell(float n1, float n2, float lensRadius, V nrm, Ray *ray, float wl, int chromatic) {
+    if (chromatic) {
+        if (n1 != 1) n1 = (float)((double)(wl - 550) * -.04 / (300) + (double)n1);
+        if (n2 != 1) n2 = (float)((double)(wl - 550) * -.04 / (300) + (double)n2);
+    }
+    const V s1 = ray->d;
+    if (lensRadius > 0) nrm = vneg(nrm);
+    const V c = vcross(nrm, s1);
+    const float radicand = 1 - (n1 / n2) * (n1 / n2) * vdot(c, c);
+    if (radicand < 0) {
+        ray->d = v3(0.f, 0.f, 0.f);
+        return;
+    }
+    const V s2 = vsub(vmul(vcross(nrm, vcross(vmul(nrm, -1.f), s1)), n1 / n2), vmul(nrm, sqrtf(radicand)));
+    ray->d = vnorm(s2);
+}
+// RealisticDiffractionCamera::GenerateRay (realisticDiffraction.cpp:478-1164 without the
+// diffraction, pinhole-array and microlens branches): film point -> toward the sampled point
+// of the last element's aperture disk (or the pinhole exit point) -> every element, last
+// first; a blocked or missed element returns weight 0.  The ray ends in world space with a
+// normalised direction.
+PGD_INLINE float lens_ray(const DevScene &S, float imageX, float imageY, float lensU, float lensV, float timeU, float wl,
+                          Ray *out) {
+    const pbrtgpu_camera &cam = S.cam;
+    const float xr2 = (float)cam.xres / 2.f, yr2 = (float)cam.yres / 2.f;
+    V sp;
+    sp.x = (float)(-((double)(imageX - xr2) - .25) / (double)xr2);
+    sp.y = (float)(((double)(imageY - yr2) - .25) / (double)yr2);
+    sp.z = -S.lensFilmDist;
+    const float aspect = (float)cam.xres / (float)cam.yres;
+    const float width = S.lensFilmDiag / sqrtf((1.f + 1.f / (aspect * aspect)));
+    const float height = width / aspect;
+    sp.x = sp.x * width / 2.f + S.lensFilmC[0];
+    sp.y = sp.y * height / 2.f + S.lensFilmC[1];
+    if (S.lensCurveR != 0) {   // curved sensor
+        const float R = S.lensCurveR, th = sp.x / R, ph = sp.y / R;
+        sp.x = R * COSF(ph) * SINF(th);
+        sp.z = R * COSF(ph) * COSF(th);
+        sp.y = R * SINF(ph);
+        const float sc = (-S.lensFilmDist - R);
+        sp.z = sc + sp.z;
+    }
+    float lu, lv;
+    concentric_disk(lensU, lensV, &lu, &lv);
+    const float4 last = S.lensEl[S.lensN - 1];
+    const float firstAp = last.w / 2, firstR = last.x;
+    const float zI = firstR == 0 ? 0.f : (-firstR - sqrtf(firstR * firstR - firstAp * firstAp));
+    lu *= firstAp;
+    lv *= firstAp;
+    V pol = v3(lu, lv, zI);
+    if (S.lensPinhole[0] != -1 && S.lensPinhole[1] != -1 && S.lensPinhole[2] != -1)
+        pol = v3(S.lensPinhole[0], S.lensPinhole[1], S.lensPinhole[2]);
+    Ray r;
+    r.o = sp;
+    r.d = vnorm(vsub(pol, r.o));
+    r.mint = 0.f;
+    r.maxt = INFINITY;
+    r.time = 0.f;
+    float lensDist = 0.f;
+    for (int i = S.lensN - 1; i >= 0; --i) {
+        const float4 e = S.lensEl[i];
+        const float rad = e.x, ap = e.w;
+        lensDist += e.y;
+        r.o = sp;
+        if (rad == 0) {   // aperture stop
+            const float tA = (i == S.lensN - 1) ? S.lensFilmDist / r.d.z : (lensDist - r.o.z) / (r.d.z);
+            const V ai = v3(r.o.x + r.d.x * tA, r.o.y + r.d.y * tA, r.o.z + r.d.z * tA);
+            const float dx = ai.x - S.lensApOff[0], dy = ai.y - S.lensApOff[1];
+            if ((double)(dx * dx + dy * dy) > (double)(ap * ap) * .25) return 0.f;
+            sp = ai;
+        } else {
+            float tHit = 0.f;
+            V nrm = v3(0.f, 0.f, 1.f);
+            if (!lens_el_hit(r, rad, v3(0.f, 0.f, rad - lensDist), &tHit, &nrm)) return 0.f;
+            const V ip = v3(tHit * r.d.x + r.o.x, tHit * r.d.y + r.o.y, tHit * r.d.z + r.o.z);
+            if (ip.x * ip.x + ip.y * ip.y >= ap * ap / 4.f) return 0.f;
+            const float n1 = e.z;
+            float n2 = 1;
+            if (i - 1 >= 0) {
+                n2 = S.lensEl[i - 1].z;
+                if (n2 == 0) n2 = S.lensEl[i - 2].z;
+            }
+            lens_snell(n1, n2, rad, nrm, &r, wl, S.lensChromatic);
+            sp = ip;
+        }
+    }
+    r.o = sp;
+    r.time = lerpf(timeU, cam.shutter_open, cam.shutter_close);
+    const float *cw = cam.cam2world_m;
+    out->o = cam_point(cw, r.o);
+    out->d = vnorm(xvec(cw, r.d));
+    out->mint = r.mint;
+    out->maxt = r.maxt;
+    out->time = r.time;
+    return 1.f;
+}
+// Camera::GenerateRayDifferential (camera.cpp:52-81) for the lens camera: the ray, then the
+// rays one pixel over in x and in y (the sample's imageX restored as (x + 1) - 1), weight 0
+// if any of them is blocked; the offsets scaled by 1 / sqrtf(spp) (samplerrenderer.cpp:91)
+PGD_INLINE float lens_ray_diff(const DevScene &S, float imageX, float imageY, float lensU, float lensV, float timeU,
+                               float wl, Ray *ray, RayDiff *rd) {
+    const float wt = lens_ray(S, imageX, imageY, lensU, lensV, timeU, wl, ray);
+    Ray rx, ry;
+    float sx = imageX + 1.f;
+    const float wtx = lens_ray(S, sx, imageY, lensU, lensV, timeU, wl, &rx);
+    sx = sx - 1.f;
+    const float wty = lens_ray(S, sx, imageY + 1.f, lensU, lensV, timeU, wl, &ry);
+    if (wtx == 0.f || wty == 0.f) return 0.f;
+    const float sc = 1.f / sqrtf((float)S.spp);
+    rd->rxo = vadd(ray->o, vmul(vsub(rx.o, ray->o), sc));
+    rd->ryo = vadd(ray->o, vmul(vsub(ry.o, ray->o), sc));
+    rd->rxd = vadd(ray->d, vmul(vsub(rx.d, ray->d), sc));
+    rd->ryd = vadd(ray->d, vmul(vsub(ry.d, ray->d), sc));
+    return wt;
+}
+// the ray wavelength of a path: the SpectralRenderer band's, 0 under the SamplerRenderer
+// (its RayDifferentials start from Ray(), geometry.h:317)
+PGD_INLINE float path_wavelength(const DevScene &S, int item, uint32_t smp) {
+    if (!S.specMode) return 0.f;
+    const int band = S.specMode == 1 ? item % S.specItems : (int)(smp % (uint32_t)S.specBands);
+    return S.specWl[band];
+}
+// the camera ray's differentials for a path (first-hit texture filtering)
+PGD_INLINE RayDiff path_camera_diff(const DevScene &S, int item, uint32_t smp, float imageX, float imageY, float lensU,
+                                    float lensV, float timeU) {
+    if (S.camType == PBRTGPU_CAMERA_REALISTIC) {
+        Ray r;
+        RayDiff rd;
+        (void)lens_ray_diff(S, imageX, imageY, lensU, lensV, timeU, path_wavelength(S, item, smp), &r, &rd);
+        return rd;
+    }
+    return camera_diff(S.cam, S.spp, imageX, imageY, lensU, lensV, timeU);
 }
 
 }  // namespace pgd

@@ -1092,14 +1092,16 @@ static int wide_bvh(const pbrtgpu_flat_scene *s, int top, std::vector<float4> *w
 // w0 <= wl < w1) and t = (wl - w0) / (w1 - w0), and its indices [dI b, min(dI (b+1), N-1)),
 // dI = round(N / nWB).  A band with indices whose interval is the last reads c[N], past the
 // spectrum: rejected.
-static int spectral_table(int N, int nWB, std::vector<int4> *tab) {
+static int spectral_table(int N, int nWB, std::vector<int4> *tab, std::vector<float> *wls) {
     const int lStart = 395, lEnd = 715;
     const int dI = (int)round(N / nWB);
     const float dW = (float)((lEnd - lStart) / nWB);
     const float step = (float)((lEnd - lStart) / N);
     tab->resize(nWB);
+    wls->resize(nWB);
     for (int b = 0; b < nWB; ++b) {
         const float wl = lStart + dW * b + (dW / 2);
+        (*wls)[b] = wl;
         int iv = -1;
         float t = 0.f;
         for (int i = 0; i < N; ++i) {
@@ -1204,11 +1206,22 @@ int pbrtgpu_scene_upload(pbrtgpu_ctx *c, const pbrtgpu_flat_scene *s) {
     if (s->renderer != PBRTGPU_RENDERER_SAMPLER && s->renderer != PBRTGPU_RENDERER_SPECTRAL)
         return fail(PBRTGPU_E_INVALID, "unknown Renderer");
     std::vector<int4> specTab;
+    std::vector<float> specWl;
     if (s->renderer == PBRTGPU_RENDERER_SPECTRAL) {
         if (s->spectral_sampling != PBRTGPU_SPECTRAL_SINGLE && s->spectral_sampling != PBRTGPU_SPECTRAL_SAMPLER)
             return fail(PBRTGPU_E_INVALID, "unknown spectral sampling method");
         if (s->wave_bands < 1 || s->wave_bands > 1024) return fail(PBRTGPU_E_INVALID, "nWaveBands must be 1..1024");
-        if (int e = spectral_table(s->n_bands, s->wave_bands, &specTab)) return e;
+        if (int e = spectral_table(s->n_bands, s->wave_bands, &specTab, &specWl)) return e;
+    }
+    if (s->camera_type != PBRTGPU_CAMERA_PERSPECTIVE && s->camera_type != PBRTGPU_CAMERA_REALISTIC)
+        return fail(PBRTGPU_E_INVALID, "unknown camera type");
+    if (s->camera_type == PBRTGPU_CAMERA_REALISTIC) {
+        const pbrtgpu_lens &L = s->lens;
+        if (L.n_elements < 1 || L.n_elements > 4096 || !L.elements) return fail(PBRTGPU_E_INVALID, "lens camera without elements");
+        // element 1 refracting into element 0 of n == 0 would read lensEls[-1] (realisticDiffraction.cpp:960-966)
+        if (L.n_elements >= 2 && L.elements[2] == 0 && L.elements[4] != 0)
+            return fail(PBRTGPU_E_INVALID, "lens element 0 has n == 0");
+        if (s->camera.xres <= 0 || s->camera.yres <= 0) return fail(PBRTGPU_E_INVALID, "lens camera without film resolution");
     }
     if (s->integrator == PBRTGPU_INTEGRATOR_DIRECT && s->dl_strategy != PBRTGPU_DL_ALL && s->dl_strategy != PBRTGPU_DL_ONE)
         return fail(PBRTGPU_E_INVALID, "unknown DirectLighting strategy");
@@ -1277,7 +1290,25 @@ int pbrtgpu_scene_upload(pbrtgpu_ctx *c, const pbrtgpu_flat_scene *s) {
     S.specBands = S.specMode ? s->wave_bands : 1;
     S.specItems = S.specMode == 1 ? s->wave_bands : 1;
     S.specTab = nullptr;
-    if (S.specMode) HIPCHK(upload(c, specTab.data(), specTab.size(), &S.specTab));
+    S.specWl = nullptr;
+    if (S.specMode) {
+        HIPCHK(upload(c, specTab.data(), specTab.size(), &S.specTab));
+        HIPCHK(upload(c, specWl.data(), specWl.size(), &S.specWl));
+    }
+    S.camType = s->camera_type;
+    S.lensN = 0;
+    S.lensEl = nullptr;
+    if (S.camType == PBRTGPU_CAMERA_REALISTIC) {
+        const pbrtgpu_lens &L = s->lens;
+        S.lensN = L.n_elements;
+        S.lensChromatic = L.chromatic;
+        S.lensFilmDist = L.film_distance;
+        S.lensFilmDiag = L.film_diag;
+        S.lensCurveR = L.curve_radius;
+        for (int k = 0; k < 2; ++k) { S.lensApOff[k] = L.aperture_offset[k]; S.lensFilmC[k] = L.film_center[k]; }
+        for (int k = 0; k < 3; ++k) S.lensPinhole[k] = L.pinhole_exit[k];
+        HIPCHK(upload(c, reinterpret_cast<const float4 *>(L.elements), (size_t)L.n_elements, &S.lensEl));
+    }
     S.dlK = 0;
     for (int i = 0; i < s->n_lights; ++i) {   // RoundUpPow2(max(1, nSamples)) per light
         uint32_t v = (uint32_t)std::max(1, s->lights[i].n_samples) - 1u;

@@ -84,7 +84,14 @@ __global__ __launch_bounds__(kShadeBlock) PGD_SHADE_ATTR void k_shade(DevScene S
     bool zeroed = false;
     if (inRange && !freeSlot) {
         bool done;
-        if (MODE == MODE_DL) pu = shade_slot_dl<NB, FEAT>(S, P, slot, Lout, &done, &zeroed);
+        if (P.bounce[slot] == -2) {   // a camera ray of weight 0 (lens camera): radiance 0
+            float4 Z[Bands<NB>::NQ];
+#pragma unroll
+            for (int q = 0; q < Bands<NB>::NQ; ++q) Z[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+            (void)path_output<NB>(S, Z, Lout, P.item[slot], P.smp[slot]);
+            done = true;
+        }
+        else if (MODE == MODE_DL) pu = shade_slot_dl<NB, FEAT>(S, P, slot, Lout, &done, &zeroed);
         else if (MODE == MODE_META) pu = shade_slot_meta<NB, FEAT>(S, P, slot, Lout, &done, &zeroed);
         else pu = shade_slot<NB, FEAT>(S, P, slot, Lout, &done, &zeroed);
         if (done) { P.item[slot] = -1; freeSlot = true; }

@@ -437,7 +437,19 @@ PGD_INLINE void path_start(const DevScene &S, const PathSoA &P, const ItemSrc &s
     float imageX = px + u[0], imageY = py + u[1];
     s2d(hp, 1, s, spp, lens);
     float timeU = s1d(hp, 2, s, spp);
-    Ray r = camera_ray(S.cam, imageX, imageY, lens[0], lens[1], timeU);
+    Ray r;
+    bool dead = false;   // rayWeight 0: the sample's radiance is 0 (samplerrenderer.cpp:105-110)
+    if (S.camType == PBRTGPU_CAMERA_REALISTIC) {
+        RayDiff rd;
+        dead = lens_ray_diff(S, imageX, imageY, lens[0], lens[1], timeU, path_wavelength(S, (int)item, s), &r, &rd) == 0.f;
+        if (dead) {   // a ray no traversal hits; k_shade writes the zero radiance
+            r.o = v3(0.f, 0.f, 0.f);
+            r.d = v3(0.f, 0.f, 1.f);
+            r.mint = 1.f;
+            r.maxt = 0.f;
+        }
+    }
+    else r = camera_ray(S.cam, imageX, imageY, lens[0], lens[1], timeU);
     ray_store(P, RAY_C, slot, r);
     // AnimatedTransform::Interpolate (transform.cpp:356-381) of every instance at the path's
     // time, once per path: all of the path's rays carry this time
@@ -454,7 +466,7 @@ PGD_INLINE void path_start(const DevScene &S, const PathSoA &P, const ItemSrc &s
     P.hp[slot] = hp;
     P.pix[slot] = ((uint32_t)py << 16) | (uint32_t)px;
     P.smp[slot] = s;
-    P.bounce[slot] = -1;
+    P.bounce[slot] = dead ? -2 : -1;
     P.flags[slot] = PF_CONT | PF_LZ;   // L = 0 and beta_0 = 1 are implicit (not stored)
     P.mt[slot] = 0;
     P.mt[4 * (size_t)P.cap + slot] =
@@ -692,8 +704,8 @@ PGD_INLINE Pushes shade_vertex(const DevScene &S, const PathSoA &P, int slot, in
             s2d(hp, 0, s, spp, u);
             s2d(hp, 1, s, spp, lens);
             const float timeU = s1d(hp, 2, s, spp);
-            RayDiff rd = camera_diff(S.cam, S.spp, (int)(pxy & 0xffffu) + u[0], (int)(pxy >> 16) + u[1], lens[0], lens[1],
-                                     timeU);
+            RayDiff rd = path_camera_diff(S, P.item[slot], s, (int)(pxy & 0xffffu) + u[0], (int)(pxy >> 16) + u[1],
+                                          lens[0], lens[1], timeU);
             compute_differentials(is.dg, rd, diff);
         }
     }

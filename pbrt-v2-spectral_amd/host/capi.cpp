@@ -117,7 +117,8 @@ static std::string dat_lens_line(float focal, float fStop, float sensorWidth) {
     return os.str();
 }
 
-int pbrthost_write_dat(const char *path, const float *film, const float *weight, int W, int H, int N) {
+static int write_dat(const char *path, const float *film, const float *weight, int W, int H, int N,
+                     const std::string &lensLine) {
     int nPix = W * H;
     std::vector<float> finalC((size_t)N * nPix);
     int offset = 0;
@@ -145,11 +146,31 @@ int pbrthost_write_dat(const char *path, const float *film, const float *weight,
     // (spectralImage.cpp:356-360).  CreateSpectralImageFilm leaves focal length, f-stop and
     // sensor width at 0 for every camera but RealisticDiffraction (:400-429), so the field
     // of view is 2 atan(0 / 0) ... = the x86 default NaN, printed "-nan"
-    fputs(dat_lens_line(0.f, 0.f, 0.f).c_str(), f);
+    fputs(lensLine.c_str(), f);
     for (int i = 0; i < N; ++i)
         for (int j = 0; j < nPix; ++j) { double r = outv[(size_t)N * j + i]; fwrite(&r, 8, 1, f); }
     fclose(f);
     return 0;
+}
+
+int pbrthost_write_dat(const char *path, const float *film, const float *weight, int W, int H, int N) {
+    return write_dat(path, film, weight, W, H, N, dat_lens_line(0.f, 0.f, 0.f));
+}
+
+// the scene's film: its resolution and band count; line 2 from a RealisticDiffractionCamera's
+// getFocalLength / getFStop / getSensorWidth (spectralImage.cpp:400-429, realisticDiffraction.cpp:
+// 316-324, 470-476), zeros (and the NaN field of view) for every other camera
+int pbrthost_write_dat_scene(const pbrthost_scene *h, const char *path, const float *film, const float *weight) {
+    if (!h || !path || !film) return -1;
+    const HostScene *s = reinterpret_cast<const HostScene *>(h);
+    const int W = s->camera.px_count, H = s->camera.py_count;
+    std::string line = dat_lens_line(0.f, 0.f, 0.f);
+    if (s->cameraType == PBRTGPU_CAMERA_REALISTIC) {
+        const float aspect = (float)s->camera.xres / (float)s->camera.yres;
+        const float width = s->lens.film_diag / sqrtf((1.f + 1.f / (aspect * aspect)));
+        line = dat_lens_line(s->lens.focal_length, s->lens.fstop, width);
+    }
+    return write_dat(path, film, weight, W, H, s->nBands, line);
 }
 
 int pbrthost_spectrum_from_rgb(int bands, const float rgb[3], int illuminant, float *out) {

@@ -1542,6 +1542,58 @@ private:
         return m->flatIndex;
     }
 
+    // CreateRealisticDiffractionCamera + the constructor's lens file (realisticDiffraction.cpp:
+    // 32-193): shutter times default to -1 (not swapped); the lens file is ReadFloatFile's
+    // floats, the focal length then (radius, separation, n, aperture) per element, an aperture
+    // stop (radius 0) taking "aperture_diameter".  What GenerateRay does only with GSL
+    // (diffraction, on by default), the pinhole-array / microlens light-field modes and the
+    // eye IOR curves are refused.
+    void RealisticCamera(CameraParams *cp) {
+        const ParamSet &p = cameraParams;
+        cp->shutterOpen = p.FindOneFloat("shutteropen", -1.f);
+        cp->shutterClose = p.FindOneFloat("shutterclose", -1.f);
+        std::string spec = p.FindOneString("specfile", "");
+        if (spec.empty()) throw std::runtime_error("No lens spec file supplied!");
+        if (p.FindOneBool("diffractionEnabled", true))
+            throw std::runtime_error("realisticDiffraction: diffractionEnabled (GSL Gaussian noise) is not supported; "
+                                     "set \"bool diffractionEnabled\" \"false\"");
+        if (p.FindOneBool("IORforEyeEnabled", false))
+            throw std::runtime_error("realisticDiffraction: IORforEyeEnabled is not supported");
+        if ((int)p.FindOneFloat("num_pinholes_w", -1) > 0 && (int)p.FindOneFloat("num_pinholes_h", -1) > 0)
+            throw std::runtime_error("realisticDiffraction: pinhole arrays / microlenses are not supported");
+        pbrtgpu_lens &L = out->lens;
+        memset(&L, 0, sizeof(L));
+        L.chromatic = p.FindOneBool("chromaticAberrationEnabled", false) ? 1 : 0;
+        L.film_distance = p.FindOneFloat("filmdistance", 70.f);
+        const float apDiam = p.FindOneFloat("aperture_diameter", 1.f);
+        L.film_diag = p.FindOneFloat("filmdiag", 35.f);
+        L.curve_radius = p.FindOneFloat("curveRadius", 0.f);
+        L.aperture_offset[0] = p.FindOneFloat("x_aperture_offset", 0.f);
+        L.aperture_offset[1] = p.FindOneFloat("y_aperture_offset", 0.f);
+        L.film_center[0] = p.FindOneFloat("film_center_x", 0.f);
+        L.film_center[1] = p.FindOneFloat("film_center_y", 0.f);
+        L.pinhole_exit[0] = p.FindOneFloat("pinhole_exit_x", -1.f);
+        L.pinhole_exit[1] = p.FindOneFloat("pinhole_exit_y", -1.f);
+        L.pinhole_exit[2] = p.FindOneFloat("pinhole_exit_z", -1.f);
+        std::vector<float> vals = ReadFloatFile(Resolve(spec));
+        if (vals.empty()) throw std::runtime_error("Unable to read lens file " + spec);
+        if ((vals.size() - 1) % 4 != 0) throw std::runtime_error("Wrong number of float values in lens file " + spec);
+        L.focal_length = vals[0];
+        L.fstop = L.focal_length / apDiam;
+        out->lensEl.clear();
+        for (size_t i = 1; i < vals.size(); i += 4) {
+            float el[4] = {vals[i], vals[i + 1], vals[i + 2], vals[i + 3]};
+            if (el[0] == 0) el[3] = apDiam;
+            out->lensEl.insert(out->lensEl.end(), el, el + 4);
+        }
+        const int n = (int)out->lensEl.size() / 4;
+        if (n == 0) throw std::runtime_error("lens file " + spec + " has no elements");
+        // GenerateRay reads lensEls[i - 2].n when element i - 1 has n == 0 (realisticDiffraction.cpp:960-966)
+        if (n >= 2 && out->lensEl[2] == 0 && out->lensEl[4] != 0)
+            throw std::runtime_error("lens file " + spec + ": element 0 has n == 0");
+        out->cameraType = PBRTGPU_CAMERA_REALISTIC;
+    }
+
     void WorldEnd() {
         while (!pushedGS.empty()) { gs = pushedGS.back(); pushedGS.pop_back(); }
         // ---- film (spectralImage.cpp:452-475) and sample extent (176-185)
@@ -1554,7 +1606,8 @@ private:
             crop[2] = Clamp(pmin(cr->f[2], cr->f[3]), 0., 1.); crop[3] = Clamp(pmax(cr->f[2], cr->f[3]), 0., 1.);
         }
         // ---- camera (perspective.cpp:110-147) -- parameters kept resolution independent
-        if (cameraName != "perspective") throw std::runtime_error("camera '" + cameraName + "' is not supported by this build");
+        if (cameraName != "perspective" && cameraName != "realisticDiffraction")
+            throw std::runtime_error("camera '" + cameraName + "' is not supported by this build");
         Xform c2w[2];
         for (int i = 0; i < 2; ++i) LookupCache(cameraToWorld.t[i], &c2w[i], nullptr);
         if (c2w[0] != c2w[1]) throw std::runtime_error("animated cameras are not supported yet");
@@ -1562,6 +1615,8 @@ private:
         cp.shutterOpen = cameraParams.FindOneFloat("shutteropen", 0.f);
         cp.shutterClose = cameraParams.FindOneFloat("shutterclose", 1.f);
         if (cp.shutterClose < cp.shutterOpen) std::swap(cp.shutterOpen, cp.shutterClose);
+        out->cameraType = PBRTGPU_CAMERA_PERSPECTIVE;
+        if (cameraName == "realisticDiffraction") RealisticCamera(&cp);
         cp.lensRadius = cameraParams.FindOneFloat("lensradius", 0.f);
         cp.focalDistance = cameraParams.FindOneFloat("focaldistance", 1e30f);
         const Param *fa = cameraParams.Find(P_FLOAT, "frameaspectratio");
@@ -1832,7 +1887,10 @@ void HostScene::Flat(pbrtgpu_flat_scene *f) const {
     f->renderer = renderer;
     f->wave_bands = waveBands;
     f->spectral_sampling = spectralSampling;
-    f->pad_r = 0;
+    f->camera_type = cameraType;
+    f->lens = lens;
+    f->lens.n_elements = (int)lensEl.size() / 4;
+    f->lens.elements = lensEl.empty() ? nullptr : lensEl.data();
 }
 
 }  // namespace pbrtamd

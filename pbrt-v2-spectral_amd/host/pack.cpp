@@ -82,6 +82,9 @@ bool SavePack(const HostScene &s, const std::string &path, std::string *err) {
     // v8: the Renderer
     int32_t rnd[3] = {s.renderer, s.waveBands, s.spectralSampling};
     ok = ok && W(f, rnd, 12);
+    // v8: the camera type and RealisticDiffractionCamera
+    int32_t ct = s.cameraType;
+    ok = ok && W(f, &ct, 4) && W(f, &s.lens, sizeof(s.lens)) && WArr(f, s.lensEl);
     ok = (gzclose(f) == Z_OK) && ok;
     if (!ok && err) *err = "write error on " + path;
     return ok;
@@ -120,12 +123,19 @@ bool LoadPack(const std::string &path, HostScene *s, std::string *err) {
         if (ok) s->metaStrategy = ms;
     }
     s->renderer = PBRTGPU_RENDERER_SAMPLER;
+    s->cameraType = PBRTGPU_CAMERA_PERSPECTIVE;
+    memset(&s->lens, 0, sizeof(s->lens));
+    s->lensEl.clear();
     s->waveBands = 32;
     s->spectralSampling = PBRTGPU_SPECTRAL_SINGLE;
     if (ok && ver >= 8) {
         int32_t rnd[3];
         ok = R(f, rnd, 12);
         if (ok) { s->renderer = rnd[0]; s->waveBands = rnd[1]; s->spectralSampling = rnd[2]; }
+        int32_t ct = 0;
+        ok = ok && R(f, &ct, 4) && R(f, &s->lens, sizeof(s->lens)) && RArr(f, s->lensEl);
+        if (ok) s->cameraType = ct;
+        s->lens.elements = nullptr;
     }
     gzclose(f);
     if (!ok && err) *err = "bad or truncated scene pack " + path;

@@ -71,6 +71,9 @@ struct HostScene {
     int renderer = PBRTGPU_RENDERER_SAMPLER;  // PBRTGPU_RENDERER_* (packs older than v8: sampler)
     int waveBands = 32;                       // SpectralRenderer nWaveBands
     int spectralSampling = PBRTGPU_SPECTRAL_SINGLE;
+    int cameraType = PBRTGPU_CAMERA_PERSPECTIVE;   // PBRTGPU_CAMERA_*
+    pbrtgpu_lens lens = {};                   // RealisticDiffractionCamera (elements: lensEl)
+    std::vector<float> lensEl;                // [elements][4]
     std::vector<uint32_t> primMeta;           // [prims][2]: primitiveId, materialId a hit reports
     std::vector<std::pair<uint32_t, std::string> > metaMesh;        // top-level primitives: id, shape name
     std::vector<std::pair<uint32_t, std::string> > metaMaterials;   // named materials: id, name (by name)

@@ -46,6 +46,14 @@ P = ctypes.c_void_p
 I32 = ctypes.c_int32
 
 
+class Lens(ctypes.Structure):
+    _fields_ = [("n_elements", I32), ("chromatic", I32), ("film_distance", ctypes.c_float),
+                ("film_diag", ctypes.c_float), ("curve_radius", ctypes.c_float),
+                ("aperture_offset", ctypes.c_float * 2), ("film_center", ctypes.c_float * 2),
+                ("pinhole_exit", ctypes.c_float * 3), ("focal_length", ctypes.c_float), ("fstop", ctypes.c_float),
+                ("elements", P)]
+
+
 class FlatScene(ctypes.Structure):
     _fields_ = [("abi_version", I32), ("n_bands", I32), ("max_depth", I32), ("spp", I32),
                 ("seed", ctypes.c_uint32), ("y_int", ctypes.c_float), ("band_Y", P),
@@ -61,7 +69,7 @@ class FlatScene(ctypes.Structure):
                 ("n_textures", I32), ("textures", P), ("ewa_lut", P), ("rgb_basis", P),
                 ("n_merl_floats", I32), ("merl", P), ("integrator", I32), ("dl_strategy", I32),
                 ("meta_strategy", I32), ("prim_meta", P), ("renderer", I32), ("wave_bands", I32),
-                ("spectral_sampling", I32), ("pad_r", I32)]
+                ("spectral_sampling", I32), ("camera_type", I32), ("lens", Lens)]
 
 
 class Overrides(ctypes.Structure):
@@ -120,6 +128,7 @@ def host_lib():
         _host.pbrthost_set_render.argtypes = [P, ctypes.c_int, ctypes.c_int, ctypes.c_uint32]
         _host.pbrthost_info.argtypes = [P, ctypes.POINTER(ctypes.c_int64), ctypes.c_int]
         _host.pbrthost_write_dat.argtypes = [ctypes.c_char_p, P, P, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+        _host.pbrthost_write_dat_scene.argtypes = [P, ctypes.c_char_p, P, P]
         _host.pbrthost_spectrum_from_rgb.argtypes = [ctypes.c_int, P, ctypes.c_int, P]
         _host.pbrthost_write_metadata.argtypes = [P, ctypes.c_char_p]
     return _host
@@ -128,7 +137,8 @@ def host_lib():
 def host_symbols():
     """Symbols declared in include/pbrthost.h."""
     return ["pbrthost_load", "pbrthost_free", "pbrthost_flat", "pbrthost_save_pack", "pbrthost_set_render",
-            "pbrthost_info", "pbrthost_write_dat", "pbrthost_spectrum_from_rgb", "pbrthost_write_metadata"]
+            "pbrthost_info", "pbrthost_write_dat", "pbrthost_write_dat_scene", "pbrthost_spectrum_from_rgb",
+            "pbrthost_write_metadata"]
 
 
 def spectrum_from_rgb(rgb, bands=32, illuminant=False):
@@ -269,7 +279,9 @@ class Scene:
 
     def write_dat(self, path, film):
         film = np.ascontiguousarray(film, dtype=np.float32)
-        host_lib().pbrthost_write_dat(path.encode(), film.ctypes.data, None, self.width, self.height, self.bands)
+        assert film.shape == (self.height, self.width, self.bands)
+        if host_lib().pbrthost_write_dat_scene(self._h, path.encode(), film.ctypes.data, None) != 0:
+            raise RuntimeError("cannot write %s" % path)
 
     def __del__(self):
         try:

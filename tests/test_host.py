@@ -222,3 +222,47 @@ def test_spectral_renderer_directive(pg, tmp_path):
         pg.Scene.load(scene_with('Renderer "spectralrenderer" "string samplingMethod" "diagonal"'))
     assert pg.Scene.load(scene_with('Renderer "metropolis"')).flat.renderer == 0
     assert pg.Scene.load(PACK).flat.renderer == 0    # packs before v8: the SamplerRenderer
+
+
+def test_realistic_diffraction_camera(pg, tmp_path):
+    """Camera "realisticDiffraction" (realisticDiffraction.cpp:32-193): the lens file's focal
+    length and elements (an aperture stop takes aperture_diameter), the camera parameters and
+    its -1 shutter defaults reach the flat scene and the pack; what needs GSL (diffraction, on
+    by default), the eye IOR curves and pinhole arrays are refused; the .dat header's line 2
+    carries focal length, f-stop and field of view (spectralImage.cpp:356-360)."""
+    here = os.path.join(os.path.dirname(os.path.abspath(__file__)), "scenes")
+    s = pg.Scene.load(os.path.join(here, "lens.pbrt"))
+    f = s.flat
+    assert f.camera_type == 1 and f.lens.n_elements == 11 and f.lens.chromatic == 1
+    assert (f.lens.focal_length, f.lens.film_distance) == (50.0, np.float32(36.77))
+    assert f.lens.fstop == np.float32(np.float32(50.0) / np.float32(12.0))
+    el = np.ctypeslib.as_array(ctypes.cast(f.lens.elements, ctypes.POINTER(ctypes.c_float)), (11, 4))
+    assert el[5].tolist() == [0.0, 4.5, 0.0, 12.0] and el[0, 0] == np.float32(29.475)
+    assert (f.camera.shutter_open, f.camera.shutter_close) == (-1.0, -1.0)
+    assert tuple(f.lens.pinhole_exit) == (-1.0, -1.0, -1.0)
+    out = str(tmp_path / "lens.pack")
+    s.save_pack(out)
+    t = pg.Scene.load(out)
+    el2 = np.ctypeslib.as_array(ctypes.cast(t.flat.lens.elements, ctypes.POINTER(ctypes.c_float)), (11, 4))
+    assert t.flat.camera_type == 1 and np.array_equal(el, el2) and t.flat.lens.fstop == f.lens.fstop
+    src = open(os.path.join(here, "lens.pbrt")).read()
+    for bad, msg in [('"bool diffractionEnabled" "false"', "diffractionEnabled"),
+                     ('"bool diffractionEnabled" "false" "bool IORforEyeEnabled" "true"', "IORforEye"),
+                     ('"bool diffractionEnabled" "false" "float num_pinholes_w" [4] "float num_pinholes_h" [4]',
+                      "pinhole")]:
+        body = src.replace('"bool diffractionEnabled" "false"', bad if msg != "diffractionEnabled" else "")
+        p = os.path.join(here, "_lens_bad.pbrt")   # next to the lens file it names
+        try:
+            open(p, "w").write(body)
+            with pytest.raises(RuntimeError, match=msg):
+                pg.Scene.load(p)
+        finally:
+            os.remove(p)
+    film = np.zeros((s.height, s.width, s.bands), np.float32)
+    dat = str(tmp_path / "lens.dat")
+    s.write_dat(dat, film)
+    line2 = open(dat, "rb").read().split(b"\n")[1].decode()
+    a = np.float32(64) / np.float32(48)
+    w = np.float32(43.27) / np.sqrt(np.float32(1) + np.float32(1) / (a * a))
+    fov = np.float32(2 * float(np.arctan(np.float32(w / np.float32(100.0)))) / 3.1415926539 * 180)
+    assert line2 == "%g %g %g" % (50.0, f.lens.fstop, fov)
