@@ -19,6 +19,11 @@ GpuPathRenderer::GpuPathRenderer(Camera *c, const ParamSet &params)
     slices = params.FindOneInt("slices", 1);
     seed = (uint32_t)params.FindOneInt("seed", 0);
     sceneFile = params.FindOneString("scenefile", gSceneFile);
+    // the SpectralRenderer's parameters (api.cpp:1378-1379): "integer nWaveBands" > 0 renders
+    // as Renderer "spectralrenderer" would
+    waveBands = params.FindOneInt("nWaveBands", 0);
+    string sm = params.FindOneString("samplingMethod", "singleDirection");
+    spectralSampling = sm == "samplerDirection" ? PBRTGPU_SPECTRAL_SAMPLER : PBRTGPU_SPECTRAL_SINGLE;
     // the spectral film writes <imageOutputName stem>.dat (spectralImage.cpp:348-350)
     const string &img = camera ? camera->film->imageOutputName : string("pbrt.exr");
     outFile = img.substr(0, img.find_last_of(".")) + ".dat";
@@ -40,7 +45,10 @@ void GpuPathRenderer::Render(const Scene *) {
         return;
     }
     int n = ngpu > 0 ? min(ngpu, ndev) : ndev;
-    pbrthost_overrides ov = { -1, -1, -1, -1, nSpectralSamples, seed, -1, -1, -1, -1, 0, -1 };   // the scene's own integrator
+    // the scene's own integrator and camera; the SpectralRenderer if asked for
+    pbrthost_overrides ov = { -1, -1, -1, -1, nSpectralSamples, seed, -1, -1, -1,
+                              waveBands > 0 ? PBRTGPU_RENDERER_SPECTRAL : -1, waveBands,
+                              waveBands > 0 ? spectralSampling : -1 };
     pbrthost_scene *hs = NULL;
     char err[1024];
     if ((status = pbrthost_load(sceneFile.c_str(), &ov, &hs, err, sizeof(err))) != 0) {
@@ -65,7 +73,8 @@ void GpuPathRenderer::Render(const Scene *) {
     // (the metadata text file of a "metadata" SurfaceIntegrator is written by the reference's own
     // pbrtWorldEnd, api.cpp:1228-1282, before the renderer runs; pbrthost_write_metadata is that
     // writer for callers without api.cpp)
-    if (status == 0 && pbrthost_write_dat(outFile.c_str(), film.data(), NULL, W, H, N) != 0) {
+    // line 2 of the header: the lens camera's focal length, f-stop, field of view
+    if (status == 0 && pbrthost_write_dat_scene(hs, outFile.c_str(), film.data(), NULL) != 0) {
         Error("gpupath: cannot write \"%s\"", outFile.c_str());
         status = PBRTGPU_E_INVALID;
     }

@@ -24,7 +24,8 @@ public:
     // camera: as MakeRenderer creates it for SamplerRenderer (the renderer owns it; its film
     // names the output, Film::imageOutputName).  params: the Renderer directive's
     //   "integer gpus" (0: every visible device), "integer seed" (fixed-seed sampler seed),
-    //   "integer slices" (tile slices per GPU), "string scenefile" (overrides SceneFile()).
+    //   "integer slices" (tile slices per GPU), "string scenefile" (overrides SceneFile()),
+    //   "integer nWaveBands" / "string samplingMethod" (the SpectralRenderer's, api.cpp:1378-1379).
     GpuPathRenderer(Camera *camera, const ParamSet &params);
     ~GpuPathRenderer();
     // Renderer::Render: one frame over all GPUs, .dat written; on failure Error() and no file
@@ -48,6 +49,7 @@ private:
     Camera *camera;
     string sceneFile, outFile;
     int ngpu, slices, status;
+    int waveBands, spectralSampling;   // "nWaveBands" (> 0: SpectralRenderer), "samplingMethod"
     uint32_t seed;
 };
 
