@@ -54,6 +54,7 @@ METRIC = "Mpaths/sec (whole node) + HBM GB/s; spectral path tracer at 1/2/4/8 MI
 # BASELINE.json configs -> scene packs (built from the reference's scene files with SURVEY.md
 # App. B overrides: 'path' integrator maxdepth 5, lowdiscrepancy spp, resolution, bands)
 CONFIGS = {
+    "c1": ("killeroo-simple-rgb.pack", "killeroo-simple RGBSpectrum (%d channels), path maxdepth %d, %dspp, %dx%d"),
     "c2": ("killeroo-simple.pack", "killeroo-simple SampledSpectrum %d bands, path maxdepth %d, %dspp, %dx%d"),
     "c3": ("bunny.pack", "bunny (mystique measured BRDF) SampledSpectrum %d bands, path maxdepth %d, %dspp, %dx%d"),
     "c4": ("metal.pack", "metal (Au conductor, env light) SampledSpectrum %d bands, path maxdepth %d, %dspp, %dx%d"),

@@ -53,7 +53,9 @@
 #include "accelerators/bvh.h"
 #include "cameras/perspective.h"
 #include "filters/box.h"
+#ifndef HARNESS_RGB
 #include "film/spectralImageNoCamera.h"
+#endif
 #ifdef HARNESS_GPUPATH
 #include "gpupathrenderer.h"   // integration/: the reference-side binding of the MI355X core
 #endif
@@ -73,6 +75,15 @@
 #include "materials/mirror.h"
 #include "materials/glass.h"
 #include "shapes/sphere.h"
+// output channels of a radiance: the spectrum's bands, or RGB in the C1 build (HARNESS_RGB:
+// Spectrum = RGBSpectrum, pbrt.h:144)
+#ifdef HARNESS_RGB
+static const int NOUT = 3;
+static inline void spec_out(const Spectrum &L, float *c) { L.ToRGB(c); }
+#else
+static const int NOUT = nSpectralSamples;
+static inline void spec_out(const Spectrum &L, float *c) { L.GetOrigC(c); }
+#endif
 #include "shapes/disk.h"
 #include "shapes/trianglemesh.h"
 #include "shapes/loopsubdiv.h"
@@ -155,7 +166,7 @@ public:
         xPixelCount = max(1, Ceil2Int(xResolution * cropWindow[1]) - xPixelStart);
         yPixelStart = Ceil2Int(yResolution * cropWindow[2]);
         yPixelCount = max(1, Ceil2Int(yResolution * cropWindow[3]) - yPixelStart);
-        c.assign((size_t)xPixelCount * yPixelCount * nSpectralSamples, 0.f);
+        c.assign((size_t)xPixelCount * yPixelCount * NOUT, 0.f);
         wsum.assign((size_t)xPixelCount * yPixelCount, 0.f);
         for (int y = 0; y < 16; ++y) {
             float fy = ((float)y + .5f) * filter->yWidth / 16;
@@ -175,8 +186,8 @@ public:
         x0 = max(x0, xPixelStart); x1 = min(x1, xPixelStart + xPixelCount - 1);
         y0 = max(y0, yPixelStart); y1 = min(y1, yPixelStart + yPixelCount - 1);
         if ((x1 - x0) < 0 || (y1 - y0) < 0) return;
-        float origC[nSpectralSamples];
-        L.GetOrigC(origC);
+        float origC[NOUT];
+        spec_out(L, origC);
         for (int y = y0; y <= y1; ++y) {
             float fy = fabsf((y - dimageY) * filter->invYWidth * 16);
             int iy = min(Floor2Int(fy), 15);
@@ -185,7 +196,7 @@ public:
                 int ix = min(Floor2Int(fx), 15);
                 float w = table[iy * 16 + ix];
                 size_t pix = (size_t)(y - yPixelStart) * xPixelCount + (x - xPixelStart);
-                for (int i = 0; i < nSpectralSamples; ++i) c[pix * nSpectralSamples + i] += w * origC[i];
+                for (int i = 0; i < NOUT; ++i) c[pix * NOUT + i] += w * origC[i];
                 wsum[pix] += w;
             }
         }
@@ -205,14 +216,14 @@ public:
     // raw accumulator, [y][x][band] float32
     void WriteRaw(const char *fn) const {
         FILE *f = fopen(fn, "wb");
-        int hdr[3] = { xPixelCount, yPixelCount, nSpectralSamples };
+        int hdr[3] = { xPixelCount, yPixelCount, NOUT };
         fwrite(hdr, sizeof(int), 3, f);
         fwrite(&c[0], sizeof(float), c.size(), f);
         fclose(f);
     }
     // .dat exactly as SpectralImageFilm::WriteImage (identity conversion matrix)
     void WriteDat(const char *fn) const {
-        int W = xPixelCount, H = yPixelCount, N = nSpectralSamples, nPix = W * H;
+        int W = xPixelCount, H = yPixelCount, N = NOUT, nPix = W * H;
         std::vector<float> finalC((size_t)N * nPix);
         int offset = 0;
         for (int x = 0; x < W; ++x)
@@ -609,6 +620,7 @@ int main(int argc, char **argv) {
     // config-size behaviour (pad == 0).  Film parameters: the --res override and the box
     // filter's defaults (the harness's film uses the same, pbrtPixelFilter keeps only the name).
     Film *refFilm = NULL;
+#ifndef HARNESS_RGB
     if (refDat) {
         if (ovW <= 0) { fprintf(stderr, "harness: --refdat needs --res\n"); return 1; }
         ParamSet fp;
@@ -619,7 +631,11 @@ int main(int argc, char **argv) {
         fp.AddString("filename", &fn, 1);
         refFilm = CreateSpectralImageNoCameraFilm(fp, CreateBoxFilter(ParamSet()));
     }
+#else
+    if (refDat) { fprintf(stderr, "harness: --refdat needs the SampledSpectrum build\n"); return 1; }
+#endif
     if (katMt) KatMT(katMt);
+#ifndef HARNESS_RGB
     if (specOut) {
         // 'color' parameters -> FromRGB(REFLECTANCE) (paramset.cpp:89-98); band table dump
         FILE *f = fopen(specOut, "wb");
@@ -637,6 +653,9 @@ int main(int argc, char **argv) {
         }
         fclose(f);
     }
+#else
+    if (specOut) { fprintf(stderr, "harness: --spectra needs the SampledSpectrum build\n"); return 1; }
+#endif
     if (string(scene) == "-") return 0;
     if (!ParseFile(scene)) { fprintf(stderr, "harness: cannot parse %s\n", scene); return 1; }
     if (!gScene) { fprintf(stderr, "harness: no WorldEnd\n"); return 1; }
@@ -655,6 +674,7 @@ int main(int argc, char **argv) {
 #else
     if (gpupath) { fprintf(stderr, "harness: built without the gpupath binding (make -C oracle/ref gpupath)\n"); return 1; }
 #endif
+#ifndef HARNESS_RGB
     if (specBands) {
         // bands whose assigned indices need GetValueAtWavelength's c[i + 1] past the last
         // sample (spectrum.h:397) read outside the spectrum: rejected, as the GPU core does
@@ -671,6 +691,9 @@ int main(int argc, char **argv) {
         }
         if (specBands < 1) { fprintf(stderr, "harness: nWaveBands must be >= 1\n"); return 1; }
     }
+#else
+    if (specBands) { fprintf(stderr, "harness: --spectral needs the SampledSpectrum build\n"); return 1; }
+#endif
     if (spp <= 0) spp = gSppParam;
     spp = (int)RoundUpPow2(spp);   // LDSampler rounds up (lowdiscrepancy.cpp:33-39)
 
@@ -701,7 +724,7 @@ int main(int argc, char **argv) {
     gSurf->Preprocess(gScene, gCamera, &renderer);
     gVol->Preprocess(gScene, gCamera, &renderer);
     FILE *pf = pathsOut ? fopen(pathsOut, "wb") : NULL;
-    if (pf) { int hdr[4] = { nSpectralSamples, spp, seed, 0 }; fwrite(hdr, 4, 4, pf); }
+    if (pf) { int hdr[4] = { NOUT, spp, seed, 0 }; fwrite(hdr, 4, 4, pf); }
     MemoryArena arena;
     long nPath = 0, nBad = 0;
     // one camera sample of SamplerRendererTask::Run (samplerrenderer.cpp:86-133) with the
@@ -721,6 +744,7 @@ int main(int argc, char **argv) {
         else if (isinf(L.y())) { L = Spectrum(0.f); ++nBad; }
         return L;
     };
+#ifndef HARNESS_RGB
     // one camera sample of SpectralRendererTask::Run (spectralrenderer.cpp:98-190): per wave
     // band b a ray of wavelength 395 + dW b + dW / 2 (integer dW = 320 / nWaveBands), its
     // radiance's value at that wavelength (Spectrum::GetValueAtWavelength, spectrum.h:384-405)
@@ -771,12 +795,15 @@ int main(int argc, char **argv) {
         }
         return Ls;
     };
+#else
+    auto traceSpectral = [&](int x, int y, int s, RayDifferential *ray) -> Spectrum { return trace(x, y, s, ray); };
+#endif
     auto emit = [&](int x, int y, int s, const Spectrum &L) {
         int key[3] = { x, y, s };
-        float c[nSpectralSamples];
-        L.GetOrigC(c);
+        float c[NOUT];
+        spec_out(L, c);
         fwrite(key, 4, 3, pf);
-        fwrite(c, 4, nSpectralSamples, pf);
+        fwrite(c, 4, NOUT, pf);
     };
     if (keysIn) {
         if (!pf) { fprintf(stderr, "harness: --keys needs --paths\n"); return 1; }

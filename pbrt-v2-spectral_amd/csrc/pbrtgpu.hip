@@ -1188,8 +1188,19 @@ int pbrtgpu_context_destroy(pbrtgpu_ctx *c) {
 int pbrtgpu_scene_upload(pbrtgpu_ctx *c, const pbrtgpu_flat_scene *s) {
     if (!c || !s) return fail(PBRTGPU_E_INVALID, "null argument");
     if (s->abi_version != PBRTGPU_ABI_VERSION) return fail(PBRTGPU_E_INVALID, "ABI version mismatch");
-    if (!(s->n_bands == 32 || s->n_bands == 60 || s->n_bands == 30))
-        return fail(PBRTGPU_E_UNSUPPORTED, "n_bands must be 30, 32 or 60");
+    if (!(s->n_bands == 32 || s->n_bands == 60 || s->n_bands == 30 || s->n_bands == 3))
+        return fail(PBRTGPU_E_UNSUPPORTED, "n_bands must be 30, 32, 60 or 3 (RGB)");
+    // the RGB build (C1): image textures, the environment light and MERL tables convert RGB with
+    // SampledSpectrum::FromRGB's basis on the device; the host front end refuses them there
+    if (s->n_bands == 3 && (s->n_textures > 0 || s->n_merl_floats > 0))
+        for (int i = 0; i < s->n_textures; ++i)
+            if (s->textures[i].type == PBRTGPU_TEX_IMAGE) return fail(PBRTGPU_E_UNSUPPORTED, "RGB build: image textures");
+    if (s->n_bands == 3 && s->n_merl_floats > 0) return fail(PBRTGPU_E_UNSUPPORTED, "RGB build: MERL BRDFs");
+    if (s->n_bands == 3)
+        for (int i = 0; i < s->n_lights; ++i)
+            if (s->lights[i].type == PBRTGPU_LIGHT_INFINITE) return fail(PBRTGPU_E_UNSUPPORTED, "RGB build: infinite lights");
+    if (s->n_bands == 3 && s->renderer == PBRTGPU_RENDERER_SPECTRAL)
+        return fail(PBRTGPU_E_UNSUPPORTED, "RGB build: the SpectralRenderer needs SampledSpectrum");
     if (s->spp <= 0 || (s->spp & (s->spp - 1))) return fail(PBRTGPU_E_INVALID, "spp must be a power of two");
     if (s->max_depth < 0 || s->max_depth > 20)
         return fail(PBRTGPU_E_UNSUPPORTED, "maxdepth > 20 exceeds the first MT19937 block (DESIGN.md §3.1)");
@@ -1751,6 +1762,7 @@ int pbrtgpu_render_tiles(pbrtgpu_ctx *c, const pbrtgpu_render_desc *d, const int
     switch (c->nb) {
         case 32: return render_impl<32>(c, d, tile_ids, ntiles, stats);
         case 60: return render_impl<60>(c, d, tile_ids, ntiles, stats);
+        case 3: return render_impl<3>(c, d, tile_ids, ntiles, stats);
         case 30: return render_impl<30>(c, d, tile_ids, ntiles, stats);
     }
     return fail(PBRTGPU_E_UNSUPPORTED, "band count");
@@ -1881,6 +1893,7 @@ int pbrtgpu_trace_paths(pbrtgpu_ctx *c, const int32_t *keys, int32_t n, float *o
     switch (c->nb) {
         case 32: return trace_impl<32>(c, keys, n, out, false);
         case 60: return trace_impl<60>(c, keys, n, out, false);
+        case 3: return trace_impl<3>(c, keys, n, out, false);
         case 30: return trace_impl<30>(c, keys, n, out, false);
     }
     return fail(PBRTGPU_E_UNSUPPORTED, "band count");
@@ -1893,6 +1906,7 @@ int pbrtgpu_path_stats(pbrtgpu_ctx *c, const int32_t *keys, int32_t n, uint64_t 
     switch (c->nb) {
         case 32: e = trace_impl<32>(c, keys, n, nullptr, true); break;
         case 60: e = trace_impl<60>(c, keys, n, nullptr, true); break;
+        case 3: e = trace_impl<3>(c, keys, n, nullptr, true); break;
         case 30: e = trace_impl<30>(c, keys, n, nullptr, true); break;
     }
     if (e) return e;

@@ -802,6 +802,7 @@ private:
     }
     // ImageTexture (imagemap.cpp:47-73 GetTexture, :97-160 Create*): a one-texel MIPMap
     int MakeImageTexture(const ParamSet &p, bool spectral) {
+        if (spec.rgb()) throw std::runtime_error("image textures are not supported in the RGB build");
         pbrtgpu_texture t = TexNode(PBRTGPU_TEX_IMAGE, spectral);
         std::string mapping = GetString(p, p, "mapping", "uv");
         if (mapping != "uv") throw std::runtime_error("texture mapping '" + mapping + "' is not supported yet");
@@ -1060,6 +1061,7 @@ private:
     // stored as float.  Returns the first texel in out->merl, or -1 when the reference's loader
     // fails (Error(); the material then has no BxDF).
     int LoadMerl(const std::string &fn) {
+        if (spec.rgb()) throw std::runtime_error("measured (MERL) BRDFs are not supported in the RGB build");
         const uint32_t nThetaH = 90, nThetaD = 90, nPhiD = 180;
         FILE *f = fopen(fn.c_str(), "rb");
         if (!f) { out->warnings.push_back("Unable to open BRDF data file " + fn); return -1; }
@@ -1188,6 +1190,7 @@ private:
             lo->l.pos[0] = lp.x; lo->l.pos[1] = lp.y; lo->l.pos[2] = lp.z;
             memcpy(lo->l.l2w_m, l2w.m.m, 64); memcpy(lo->l.l2w_minv, l2w.mInv.m, 64);
         } else if (name == "infinite" || name == "exinfinite") {   // infinite.cpp:41-80, 232-245
+            if (spec.rgb()) throw std::runtime_error("infinite lights are not supported in the RGB build");
             Spec L = p.FindOneSpectrum("L", spec.Const(1.0f));
             Spec sc = p.FindOneSpectrum("scale", spec.Const(1.0f));
             std::string texmap = p.FindOneString("mapname", "");

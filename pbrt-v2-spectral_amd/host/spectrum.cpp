@@ -8,7 +8,17 @@
 
 namespace pbrtamd {
 
+// RGBSpectrum::y (spectrum.h:489-492): YWeight[0] c0 + YWeight[1] c1 + YWeight[2] c2, here as
+// ((0 + w0 c0) + w1 c1) + w2 c2, divided by yint = 1 -- the same float result
+static const float kRgbY[3] = {0.212671f, 0.715160f, 0.072169f};
+static const float kRgbZero[3] = {0.f, 0.f, 0.f};
+
 SpectrumCtx::SpectrumCtx(int nBands, int lambdaStart, int lambdaEnd) : nb(nBands), l0(lambdaStart), l1(lambdaEnd) {
+    if (nBands == 3) {
+        tX = kRgbZero; tY = kRgbY; tZ = kRgbZero; tyint = 1.f;
+        for (int k = 0; k < 14; ++k) basis[k] = kRgbZero;   // FromRGB is the identity (no basis)
+        return;
+    }
     const SpectralTableSet *t = nullptr;
     if (nBands == 32 && l0 == 395 && l1 == 715) t = &kTables_32_395_715;
     else if (nBands == 60 && l0 == 395 && l1 == 715) t = &kTables_60_395_715;
@@ -25,6 +35,7 @@ static inline void addScaled(Spec &r, float a, const float *B) {
 
 // spectrum.cpp:93-178 ; basis order: W C M Y R G B (reflectance 0-6, illuminant 7-13)
 Spec SpectrumCtx::FromRGB(const float rgb[3], bool illum) const {
+    if (this->rgb()) return Spec(rgb, rgb + 3);   // RGBSpectrum::FromRGB (spectrum.h:463-470): no clamp
     Spec r(nb, 0.f);
     const float *const *b = basis + (illum ? 7 : 0);
     enum { W, C, M, Yy, R, G, B };
@@ -47,7 +58,7 @@ Spec SpectrumCtx::FromRGB(const float rgb[3], bool illum) const {
 }
 
 Spec SpectrumCtx::FromXYZ(const float xyz[3], bool illum) const {
-    float rgb[3];   // spectrum.h:48-52
+    float rgb[3];   // spectrum.h:48-52 (RGBSpectrum::FromXYZ: XYZToRGB, no clamp)
     rgb[0] = 3.240479f * xyz[0] - 1.537150f * xyz[1] - 0.498535f * xyz[2];
     rgb[1] = -0.969256f * xyz[0] + 1.875991f * xyz[1] + 0.041556f * xyz[2];
     rgb[2] = 0.055648f * xyz[0] - 0.204043f * xyz[1] + 1.057311f * xyz[2];
@@ -55,6 +66,8 @@ Spec SpectrumCtx::FromXYZ(const float xyz[3], bool illum) const {
 }
 
 Spec SpectrumCtx::FromSampled(const float *lambda, const float *v, int n) const {
+    if (rgb()) throw std::runtime_error("sampled spectra (SPD files, default metal, measured BRDFs, blackbody) are not "
+                                        "supported in the RGB build");
     bool sorted = true;
     for (int i = 0; i < n - 1; ++i) if (lambda[i] > lambda[i + 1]) { sorted = false; break; }
     if (!sorted) {
@@ -98,6 +111,7 @@ float SpectrumCtx::y(const Spec &s) const {
 }
 
 void SpectrumCtx::ToRGB(const Spec &s, float rgb[3]) const {
+    if (this->rgb()) { for (int k = 0; k < 3; ++k) rgb[k] = s[k]; return; }
     float xyz[3] = {0.f, 0.f, 0.f};
     for (int i = 0; i < nb; ++i) {
         xyz[0] += tX[i] * s[i];

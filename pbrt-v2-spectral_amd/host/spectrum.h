@@ -13,9 +13,12 @@ struct SpectralTables;   // opaque, see spectrum.cpp
 
 class SpectrumCtx {
 public:
-    // n = 32 (395-715 nm, the reference build), 60 (395-715) or 30 (400-700)
+    // n = 32 (395-715 nm, the reference build), 60 (395-715) or 30 (400-700); n = 3 is the
+    // reference's RGB build (Spectrum = RGBSpectrum, pbrt.h:144; spectrum.h:453-530): FromRGB
+    // keeps the triple, y() weighs it with YWeight (yint 1)
     explicit SpectrumCtx(int nBands, int lambdaStart = 395, int lambdaEnd = 715);
     int n() const { return nb; }
+    bool rgb() const { return nb == 3; }
     int lambdaStart() const { return l0; }
     int lambdaEnd() const { return l1; }
     typedef std::vector<float> Spec;

@@ -539,6 +539,36 @@ def test_realistic_diffraction_camera_vs_oracle(pg, monkeypatch, kw):
     assert np.abs(film - of).max() / np.abs(of).max() < 1e-4
 
 
+@pytest.mark.parametrize("name", ["killeroo_rgb_paths_48x40s4", "killeroo_rgb_keys_c1_400x400s64"])
+def test_rgb_build_vs_reference_golden(pg, name):
+    """C1 (BASELINE configs[0]): the RGBSpectrum build (3 channels, NB = 3 kernels) against the
+    reference's RGB harness per path -- keys at C1's 400x400 at 64 spp included -- and the film,
+    and against the oracle."""
+    from conftest import GOLDEN
+    from test_oracle_golden import rgb_scene
+    g = np.load(os.path.join(GOLDEN, name + ".npz"))
+    scene = rgb_scene(pg, g)
+    with pg.Device(0) as d:
+        d.upload(scene)
+        L = d.trace_paths(g["keys"])
+        film = None
+        if "paths" in name:
+            gf = np.load(os.path.join(GOLDEN, "killeroo_rgb_film_40x32s8.npz"))
+            fs = rgb_scene(pg, gf)
+            d.upload(fs)
+            d.render()
+            film = d.film()
+    ref = g["L"]
+    same = np.all(L.view(np.int32) == ref.view(np.int32), axis=1)
+    rel = np.abs(L - ref).max(axis=1) / np.maximum(np.abs(ref).max(axis=1), 1e-30)
+    assert same.mean() >= 0.97, "bit-exact paths %d / %d" % (same.sum(), len(same))
+    assert (rel > 1e-4).mean() <= 5e-4
+    Lo = pg.oracle().trace_paths(scene, g["keys"])
+    assert np.all(L.view(np.int32) == Lo.view(np.int32), axis=1).mean() >= 1 - 1e-4
+    if film is not None:
+        assert np.abs(film - gf["film"]).max() / np.abs(gf["film"]).max() < 1e-4
+
+
 def test_integrator_scene_checks(pg):
     """pbrtgpu_scene_upload refuses what the integrator steps cannot render exactly: a
     DirectLighting maxdepth beyond the first MT19937 block (> 6), an unknown metadata strategy,

@@ -266,3 +266,17 @@ def test_realistic_diffraction_camera(pg, tmp_path):
     w = np.float32(43.27) / np.sqrt(np.float32(1) + np.float32(1) / (a * a))
     fov = np.float32(2 * float(np.arctan(np.float32(w / np.float32(100.0)))) / 3.1415926539 * 180)
     assert line2 == "%g %g %g" % (50.0, f.lens.fstop, fov)
+
+
+def test_rgb_build_front_end(pg):
+    """bands=3 is the reference's RGB build: 'color' parameters stay RGB triples (no basis, no
+    clamp), y() uses RGBSpectrum's YWeight with yint 1; what converts spectra on the device
+    (image textures, the environment light) or needs sampled spectra is refused."""
+    s = pg.Scene.load(os.path.join(PACKS, "killeroo-simple-rgb.pack"))
+    assert s.bands == 3 and s.flat.y_int == 1.0
+    y = np.ctypeslib.as_array(ctypes.cast(s.flat.band_Y, ctypes.POINTER(ctypes.c_float)), (3,))
+    assert y.tolist() == [np.float32(0.212671), np.float32(0.715160), np.float32(0.072169)]
+    here = os.path.join(os.path.dirname(os.path.abspath(__file__)), "scenes")
+    with pytest.raises(RuntimeError, match="RGB build"):
+        pg.Scene.load(os.path.join(here, "coverage.pbrt"), bands=3)
+    assert s.flat.n_lights == 1

@@ -235,3 +235,30 @@ def test_spectral_renderer_film_bit_exact_vs_reference(pg, ora_libm, name):
     g = np.load(os.path.join(GOLDEN, name + ".npz"))
     film, _ = ora_libm.render(spec_scene(pg, g, name), threads=8)
     assert np.array_equal(film.view(np.int32), g["film"].view(np.int32))
+
+
+RGB = ["killeroo_rgb_paths_48x40s4", "killeroo_rgb_film_40x32s8", "killeroo_rgb_keys_c1_400x400s64"]
+
+
+def rgb_scene(pg, g):
+    """C1: killeroo-simple in the reference's RGB build (Spectrum = RGBSpectrum, pbrt.h:144), from
+    its 3-channel pack."""
+    w, h, spp, seed, md = [int(v) for v in g["config"]]
+    return pg.Scene.load(os.path.join(PACKS, "killeroo-simple-rgb.pack"), xres=w, yres=h, spp=spp, maxdepth=md,
+                         seed=seed)
+
+
+@pytest.mark.parametrize("name", RGB)
+def test_rgb_build_bit_exact_vs_reference(pg, ora_libm, name):
+    """C1 (BASELINE configs[0]): the RGBSpectrum build of the reference harness (oracle/ref
+    BANDS=rgb) against the oracle with 3 channels -- FromRGB keeps the triple, y() weighs it
+    with RGBSpectrum's YWeight -- per path (including keys at C1's 400x400 at 64 spp) and film."""
+    g = np.load(os.path.join(GOLDEN, name + ".npz"))
+    scene = rgb_scene(pg, g)
+    assert scene.bands == 3
+    if "film" in name:
+        film, _ = ora_libm.render(scene, threads=8)
+        assert np.array_equal(film.view(np.int32), g["film"].view(np.int32))
+    else:
+        L = ora_libm.trace_paths(scene, g["keys"])
+        assert np.array_equal(L.view(np.int32), g["L"].view(np.int32))

@@ -46,7 +46,7 @@ Fixtures (numpy .npz, inputs + expected outputs only):
   killeroo_dat_40x32s4.npz        the raw film of the restatement film AND the .dat the
                                   reference's own SpectralImageNoCameraFilm wrote for the same
                                   samples (--refdat): pins AddSample and the WriteImage payload
-Usage: python tools/make_golden.py [--only keys|dat|merl|dl|meta|spec]   (after `make -C oracle ref` and `make -C oracle ref60`)
+Usage: python tools/make_golden.py [--only keys|dat|merl|dl|meta|spec|rgb]   (after `make -C oracle ref` and `make -C oracle ref60`)
 """
 import os
 import subprocess
@@ -58,12 +58,14 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HARNESS = os.path.join(ROOT, "oracle", "_ref", "b32", "pbrt_ref_harness")
 HARNESS60 = os.path.join(ROOT, "oracle", "_ref", "b60", "pbrt_ref_harness")   # make -C oracle ref60
+HARNESSRGB = os.path.join(ROOT, "oracle", "_ref", "brgb", "pbrt_ref_harness")  # make -C oracle refrgb
 SCENES = "/root/reference/scenes"
 OUT = os.path.join(ROOT, "tests", "golden")
 
 
 def run(args, bands=32):
-    subprocess.run([HARNESS60 if bands == 60 else HARNESS] + args, check=True, cwd=SCENES)
+    exe = HARNESS60 if bands == 60 else HARNESSRGB if bands == 3 else HARNESS
+    subprocess.run([exe] + args, check=True, cwd=SCENES)
 
 
 def read_paths(fn):
@@ -111,6 +113,14 @@ def config_keys(W, H, spp, seed, n_random=2048):
     full = np.array([(x, y, s) for x, y in px for s in range(spp)], np.int32).reshape(-1, 3)
     rnd = np.stack([rng.randint(0, W + 1, n_random), rng.randint(0, H + 1, n_random), rng.randint(0, spp, n_random)], 1)
     return np.concatenate([full, rnd.astype(np.int32)])
+
+
+def rgb_fixtures(tmp):
+    """C1: the reference's RGB build (Spectrum = RGBSpectrum) on killeroo-simple -- per-path RGB
+    radiance, a film, and keys at C1's real size (400x400 at 64 spp)."""
+    paths_fixture("killeroo_rgb_paths_48x40s4", (48, 40), 4, 0, 5, 1, tmp, bands=3)
+    film_fixture("killeroo_rgb_film_40x32s8", (40, 32), 8, 0, 5, tmp, bands=3)
+    keys_fixture("killeroo_rgb_keys_c1_400x400s64", "killeroo-simple.pbrt", 400, 400, 64, 3, 1, tmp)
 
 
 def keys_fixture(name, scene, W, H, spp, bands, kseed, tmp):
@@ -238,6 +248,8 @@ def main():
                 meta_fixtures(tmp)
             elif only == "spec":
                 spec_fixtures(tmp)
+            elif only == "rgb":
+                rgb_fixtures(tmp)
         return
     with tempfile.TemporaryDirectory() as tmp:
         paths_fixture("killeroo_paths_64x64s4", (64, 64), 4, 0, 5, 5, tmp)
@@ -268,6 +280,8 @@ def main():
         dl_fixtures(tmp)
         meta_fixtures(tmp)
         spec_fixtures(tmp)
+        if os.path.exists(HARNESSRGB):
+            rgb_fixtures(tmp)
         fn = os.path.join(tmp, "mt.bin")
         run(["-", "--kat-mt", fn])
         raw = np.fromfile(fn, dtype=np.uint32).reshape(6, 65)

@@ -20,13 +20,18 @@ PACKS = [
     ("bunny", "bunny.pbrt", 32, 1920, 1080, 1024),
     ("metal", "metal.pbrt", 60, 400, 400, 4096),
     ("coverage", os.path.join(ROOT, "tests", "scenes", "coverage.pbrt"), 32, 64, 48, 8),
+    # C1: the reference's RGB build (Spectrum = RGBSpectrum), 400x400 at 64 spp
+    ("killeroo-simple-rgb", "killeroo-simple.pbrt", 3, 400, 400, 64),
 ]
 
 
 def main():
     out = os.path.join(ROOT, "scenes")
     os.makedirs(out, exist_ok=True)
+    only = sys.argv[2:] if len(sys.argv) > 2 and sys.argv[1] == "--only" else None   # --only NAME ...
     for name, fn, bands, xr, yr, spp in PACKS:
+        if only and name not in only:
+            continue
         # the configs render with "path" (SURVEY App. B); load a pack with integrator="directlighting"
         # to render it with the DirectLightingIntegrator the scene files name
         s = pg.Scene.load(os.path.join(REF, fn), xres=xr, yres=yr, spp=spp, maxdepth=-1 if name == "coverage" else 5,
