@@ -733,6 +733,15 @@ static int slot_target() {
     int v = e ? atoi(e) : 0;
     return v > 0 ? v : (1 << 23);   // 8 M slots = 2 lanes x 4 M (C2 r01p: 289 -> 301 Mpaths/s vs 2 x 2 M)
 }
+// slots of a lane running `items` paths: the target, but without the override at most a quarter
+// of the lane's items (>= 1 M), so that a small render -- one GPU's 1/8 of a frame -- runs a few
+// slot generations rather than one long fill and drain (C2 1/8 frame: 4 M slots per lane 330,
+// 2 M 344 Mpaths/s; whole frame: 4 M 393, 2 M 384; profiles/r02q_slots.txt)
+static int lane_slots(uint32_t items, int nl) {
+    const int t = std::max(64, slot_target() / nl);
+    if (getenv("PBRTGPU_SLOTS")) return (int)std::min<uint32_t>(items, (uint32_t)t);
+    return (int)std::min<uint32_t>(items, (uint32_t)std::min(t, std::max(1 << 20, (int)(items / 4u))));
+}
 // per-sample radiance budget of one spp batch: PBRTGPU_LBUF_MB env override (tests force
 // many batches per frame with a tiny budget)
 static size_t lbuf_budget() {
@@ -874,7 +883,7 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
         const uint32_t lo = (uint32_t)((uint64_t)src.nItems * l / nl), hi = (uint32_t)((uint64_t)src.nItems * (l + 1) / nl);
         r.src.base = src.base + lo;
         r.src.nItems = hi - lo;
-        r.cap = (int)std::min<uint32_t>(r.src.nItems, (uint32_t)std::max(64, slot_target() / nl));
+        r.cap = lane_slots(r.src.nItems, nl);
         if (dl)   // the frame stacks and light-sample batches: at most 24 GiB per lane
             r.cap = (int)std::max<size_t>(64, std::min<size_t>((size_t)r.cap, ((size_t)24 << 30) /
                                                                (frame_bytes(NB) * nFrames + batch_bytes(NB) * batch)));
