@@ -247,6 +247,9 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--serial", action="store_true", help="timed frames in serial mode (profiling runs)")
+    ap.add_argument("--bvh", choices=["host", "gpu"], default="host",
+                    help="host: the front end's SAH build (node for node the reference's, the default); "
+                         "gpu: the linear BVH built on the GPU (pbrtgpu_build_bvh, SURVEY 8(f) row 3)")
     ap.add_argument("--dump-film", default=None, help="rank 0 saves the gathered film (.npy) after the timed steps")
     args = ap.parse_args()
 
@@ -285,6 +288,8 @@ def main():
         if pg.gpu_lib().pbrtgpu_device_count() < args.gpus:
             raise SystemExit("--gpus %d: only %d devices visible" % (args.gpus, pg.gpu_lib().pbrtgpu_device_count()))
         devs = [pg.Device(i) for i in range(args.gpus)]
+        if args.bvh == "gpu":
+            scene = devs[0].build_bvh(scene)
         for d in devs:
             d.upload(scene)
         film = np.zeros(shape, np.float32)
@@ -297,6 +302,8 @@ def main():
         # one GPU per rank; ranks beyond the visible devices share them (a 1-GPU box running a
         # 2-rank rehearsal of the multi-GPU path)
         dev = pg.Device(local % max(1, pg.gpu_lib().pbrtgpu_device_count()))
+        if args.bvh == "gpu":
+            scene = dev.build_bvh(scene)
         dev.upload(scene)
         if world > 1 and args.shard == "tiles":
             tiles = pg.tile_slice(ntx * nty, rank, world)
@@ -363,6 +370,9 @@ def main():
         }
         if per_rank is not None:
             line["per_gpu_ms_per_step"] = per_rank
+        if args.bvh == "gpu":
+            line["config"]["bvh"] = "GPU linear BVH (%d nodes): build %.2f ms device, %.2f ms call" % (
+                scene.flat.n_nodes, scene.build_ms[0], scene.build_ms[1])
         if args.serial:
             line["note"] = "serial mode (profiling): one lane, no concurrent kernels"
         print(json.dumps(line), flush=True)

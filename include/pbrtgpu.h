@@ -366,6 +366,17 @@ int pbrtgpu_trace_paths(pbrtgpu_ctx *ctx, const int32_t *keys, int32_t n, float 
  * prim = -1 on miss; occluded_out [n] (may be NULL). */
 int pbrtgpu_intersect(pbrtgpu_ctx *ctx, const float *rays, int32_t n, float *hits_out,
                       int32_t *occluded_out);
+/* GPU BVH build (the host front end's SAH build restates
+ * accelerators/bvh.cpp:145-351 node for node and stays the default, since the bit-exact
+ * traversal order rests on it).  A linear BVH (Morton codes, radix sort, Karras radix tree,
+ * bottom-up bounds) over n primitives' world bounds [n][6] = bmin.xyz, bmax.xyz, returned in
+ * the LinearBVHNode layout above with one primitive per leaf: nodes_out [2n-1];
+ * order_out [n] = the original index of the primitive at leaf position j, i.e. the new
+ * orderedPrims (prims[], prim_instance[] and prim_meta[] are permuted by it).  Deterministic.
+ * ms_out [2] (may be NULL): device time of the build, wall time of the call.  Returns the
+ * node count (2n - 1) or a negative error.  Scenes with instances keep the host build. */
+int pbrtgpu_build_bvh(pbrtgpu_ctx *ctx, int32_t n, const float *bounds, pbrtgpu_bvh_node *nodes_out,
+                      int32_t *order_out, double *ms_out);
 /* Instrumented traversal statistics for a list of path keys (roofline model): counters_out
  * [6] = closest-hit rays, shadow rays, BVH nodes visited, triangle tests, quadric tests,
  * closest hits. */

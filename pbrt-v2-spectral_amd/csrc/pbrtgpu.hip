@@ -42,6 +42,13 @@ static int pgd_sections_read(unsigned long long *out, int reset) {
 }
 #endif
 
+namespace pgd {
+// GPU linear BVH build (lbvh.hip)
+int lbvh_build(hipStream_t stream, int n, const float *bounds, pbrtgpu_bvh_node *nodes_out, int32_t *order_out,
+               double *ms_out, std::string *err);
+}
+using pgd::lbvh_build;
+
 static thread_local std::string g_err;
 static int fail(int code, const std::string &msg) { g_err = msg; return code; }
 #define HIPCHK(x)                                                                          \
@@ -1923,6 +1930,16 @@ int pbrtgpu_path_stats(pbrtgpu_ctx *c, const int32_t *keys, int32_t n, uint64_t 
     counters_out[0] = w[W_RAYS]; counters_out[1] = w[W_SHADOW]; counters_out[2] = w[W_NODES_C] + w[W_NODES_S];
     counters_out[3] = w[W_TRIS_C] + w[W_TRIS_S]; counters_out[4] = w[W_QUADS_C] + w[W_QUADS_S]; counters_out[5] = w[W_HITS];
     return 0;
+}
+
+int pbrtgpu_build_bvh(pbrtgpu_ctx *c, int32_t n, const float *bounds, pbrtgpu_bvh_node *nodes_out, int32_t *order_out,
+                      double *ms_out) {
+    if (!c || !bounds || !nodes_out || !order_out || n < 1) return fail(PBRTGPU_E_INVALID, "bad arguments");
+    if (n > (1 << 24)) return fail(PBRTGPU_E_UNSUPPORTED, "BVH leaf beyond the 2^24-primitive reference range");
+    HIPCHK(hipSetDevice(c->device));
+    std::string err;
+    const int e = lbvh_build(c->stream, n, bounds, nodes_out, order_out, ms_out, &err);
+    return e ? fail(e, "pbrtgpu_build_bvh: " + err) : 2 * n - 1;
 }
 
 int pbrtgpu_intersect(pbrtgpu_ctx *c, const float *rays, int32_t n, float *hits, int32_t *occ) {

@@ -169,6 +169,7 @@ def gpu_lib():
         g.pbrtgpu_last_timing.argtypes = [P, ctypes.POINTER(Timing)]
         g.pbrtgpu_film_gather.argtypes = [P, I32, I32, P, I32, P, ctypes.c_int64]
         g.pbrtgpu_render_multi.argtypes = [P, I32, ctypes.POINTER(RenderDesc), P, I32, I32, P, ctypes.c_int64, P]
+        g.pbrtgpu_build_bvh.argtypes = [P, I32, P, P, P, P]
     return _gpu
 
 
@@ -178,7 +179,7 @@ def gpu_symbols():
             "pbrtgpu_context_destroy", "pbrtgpu_last_error", "pbrtgpu_scene_upload",
             "pbrtgpu_render_tiles", "pbrtgpu_film_read", "pbrtgpu_film_clear",
             "pbrtgpu_trace_paths", "pbrtgpu_intersect", "pbrtgpu_path_stats", "pbrtgpu_last_timing",
-            "pbrtgpu_film_gather", "pbrtgpu_render_multi"]
+            "pbrtgpu_film_gather", "pbrtgpu_render_multi", "pbrtgpu_build_bvh"]
 
 
 def tile_grid(scene, tile=16):
@@ -291,6 +292,76 @@ class Scene:
             pass
 
 
+def _arr(ptr, ctype, n):
+    return np.frombuffer((ctype * n).from_address(ptr), dtype=np.dtype(ctype)).copy() if n else np.zeros(0, np.dtype(ctype))
+
+
+def prim_bounds(scene):
+    """[n_prims][6] float32 world bounds of the scene's primitives (bmin, bmax): a triangle's
+    three world-space vertices (Triangle::WorldBound, trianglemesh.cpp:97-103); a sphere's or
+    disk's object bound (sphere.cpp:42-46, disk.cpp:41-45) through ObjectToWorld's eight corners
+    (transform.cpp:144-156), evaluated in double and rounded outward to float.  The input of
+    the GPU BVH build (pbrtgpu_build_bvh)."""
+    f = scene.flat
+    if f.n_instances:
+        raise ValueError("the GPU BVH build covers scenes without instances")
+    n = f.n_prims
+    prims = _arr(f.prims, ctypes.c_int32, 4 * n).reshape(n, 4)
+    out = np.zeros((n, 6), np.float32)
+    tri = prims[:, 0] == SHAPE_TRIANGLE
+    if tri.any():
+        tv = _arr(f.tris, ctypes.c_int32, 4 * f.n_tris).reshape(-1, 4)[:, 1:]
+        vp = _arr(f.vert_p, ctypes.c_float, 3 * f.n_verts).reshape(-1, 3)
+        pts = vp[tv[prims[tri, 1]]]                      # [k][3 vertices][xyz]
+        out[tri, :3] = pts.min(axis=1)
+        out[tri, 3:] = pts.max(axis=1)
+    quads = np.nonzero(~tri)[0]
+    if len(quads):
+        q = _arr(f.quadrics, ctypes.c_float, 44 * f.n_quadrics).reshape(-1, 44)
+        qt = q[:, 0].view(np.int32)
+        for i in quads:
+            r = q[prims[i, 1]]
+            rad, zmin, zmax, h = float(r[36]), float(r[37]), float(r[38]), float(r[42])
+            if qt[prims[i, 1]] == SHAPE_SPHERE:
+                lo, hi = (-rad, -rad, zmin), (rad, rad, zmax)
+            else:
+                lo, hi = (-rad, -rad, h), (rad, rad, h)
+            m = r[4:20].astype(np.float64).reshape(4, 4)
+            c = np.array([[x, y, z, 1.0] for x in (lo[0], hi[0]) for y in (lo[1], hi[1]) for z in (lo[2], hi[2])])
+            w = c @ m.T
+            p = w[:, :3] / np.where(w[:, 3:] == 1.0, 1.0, w[:, 3:])
+            out[i, :3] = np.nextafter(p.min(axis=0).astype(np.float32), np.float32(-np.inf))
+            out[i, 3:] = np.nextafter(p.max(axis=0).astype(np.float32), np.float32(np.inf))
+    return out
+
+
+class BvhScene(Scene):
+    """A scene over a BVH built on the GPU (pbrtgpu_build_bvh): the parent's flattened scene
+    with new nodes and its per-primitive arrays (prims, prim_instance, prim_meta) permuted
+    into the new leaf order.  Everything else is shared with the parent."""
+
+    def __init__(self, parent, nodes, order, build_ms):
+        self.parent = parent
+        self._h = parent._h
+        self.build_ms = build_ms
+        self.order = order
+        self.flat = FlatScene.from_buffer_copy(parent.flat)
+        f, n = parent.flat, parent.flat.n_prims
+        self._nodes = nodes
+        self._prims = np.ascontiguousarray(_arr(f.prims, ctypes.c_int32, 4 * n).reshape(n, 4)[order])
+        self.flat.n_nodes, self.flat.nodes = len(nodes), nodes.ctypes.data
+        self.flat.prims = self._prims.ctypes.data
+        if f.prim_instance:
+            self._pi = np.ascontiguousarray(_arr(f.prim_instance, ctypes.c_int32, n)[order])
+            self.flat.prim_instance = self._pi.ctypes.data
+        if f.prim_meta:
+            self._pm = np.ascontiguousarray(_arr(f.prim_meta, ctypes.c_uint32, 2 * n).reshape(n, 2)[order])
+            self.flat.prim_meta = self._pm.ctypes.data
+
+    def __del__(self):
+        pass   # the parent owns the host scene
+
+
 def _check(rc):
     if rc != 0:
         msg = gpu_lib().pbrtgpu_last_error()
@@ -320,6 +391,21 @@ class Device:
     def upload(self, scene):
         _check(self.lib.pbrtgpu_scene_upload(self.ctx, ctypes.byref(scene.flat)))
         self.scene = scene
+
+    def build_bvh(self, scene):
+        """The scene over a BVH built on this GPU (pbrtgpu_build_bvh) -> BvhScene with
+        build_ms = (device ms, call wall ms).  Needs no uploaded scene."""
+        b = prim_bounds(scene)
+        n = len(b)
+        nodes = np.zeros(2 * n - 1, dtype=np.dtype([("bmin", "<f4", 3), ("bmax", "<f4", 3), ("offset", "<u4"),
+                                                     ("meta", "<u4")]))
+        order = np.zeros(n, np.int32)
+        ms = np.zeros(2, np.float64)
+        rc = self.lib.pbrtgpu_build_bvh(self.ctx, n, b.ctypes.data, nodes.ctypes.data, order.ctypes.data, ms.ctypes.data)
+        if rc < 0:
+            _check(rc)
+        assert rc == 2 * n - 1
+        return BvhScene(scene, nodes, order, (float(ms[0]), float(ms[1])))
 
     def render(self, spp_begin=0, spp_end=None, tiles=None, tile=(16, 16), accumulate=False, stats=None,
                count_work=False):
