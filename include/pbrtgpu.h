@@ -377,6 +377,19 @@ int pbrtgpu_intersect(pbrtgpu_ctx *ctx, const float *rays, int32_t n, float *hit
  * node count (2n - 1) or a negative error.  Scenes with instances keep the host build. */
 int pbrtgpu_build_bvh(pbrtgpu_ctx *ctx, int32_t n, const float *bounds, pbrtgpu_bvh_node *nodes_out,
                       int32_t *order_out, double *ms_out);
+/* GPU Loop subdivision (shapes/loopsubdiv.cpp:147-437): the control mesh
+ * vi [nf][3] over P [nv][3] (object space) refined by n_levels levels to its limit surface,
+ * with every float operation in the reference's order (csrc/loopsubdiv.hip): *n_verts_out
+ * vertices, P_out / N_out [*n_verts_out][3] limit positions and normals (object space),
+ * vi_out [nf * 4^n_levels][3]; with P_out NULL only *n_verts_out is set.  ms_out [2] (may be
+ * NULL): device time, wall time of the call.  Every vertex must belong to a face. */
+int pbrtgpu_loop_subdivide(pbrtgpu_ctx *ctx, int32_t nf, int32_t nv, const int32_t *vi, const float *P,
+                           int32_t n_levels, int32_t *n_verts_out, float *P_out, float *N_out, int32_t *vi_out,
+                           double *ms_out);
+/* The same with pbrthost_set_loop_subdivider's signature (user = the pbrtgpu_ctx), so the
+ * host front end refines its loopsubdiv shapes on the GPU. */
+int pbrtgpu_loop_subdivide_hook(void *ctx, int32_t nf, int32_t nv, const int32_t *vi, const float *P,
+                                int32_t n_levels, int32_t *n_verts_out, float *P_out, float *N_out, int32_t *vi_out);
 /* Instrumented traversal statistics for a list of path keys (roofline model): counters_out
  * [6] = closest-hit rays, shadow rays, BVH nodes visited, triangle tests, quadric tests,
  * closest hits. */

@@ -58,6 +58,18 @@ int pbrthost_write_dat_scene(const pbrthost_scene *s, const char *path, const fl
 
 /* SampledSpectrum::FromRGB (spectrum.cpp:93-178) at the given band count (32, 60 or 30);
  * illuminant != 0 selects SPECTRUM_ILLUMINANT.  out[bands]. */
+/* Loop subdivision (shapes/loopsubdiv.cpp:147-437).  A subdivider refines a control mesh
+ * (nf faces vi[nf][3] over nv vertices P[nv][3], object space) by `levels` levels to the
+ * limit surface: *nv_out vertices, P_out / N_out [*nv_out][3] limit positions and normals,
+ * vi_out [nf * 4^levels][3]; with P_out NULL it only sets *nv_out.  Returns 0 or an error.
+ * pbrthost_set_loop_subdivider(fn, user) makes the front end refine loopsubdiv shapes with fn
+ * (e.g. pbrtgpu_loop_subdivide_hook with user = a pbrtgpu context); NULL restores the host
+ * refinement.  pbrthost_loop_refine is the host refinement itself (tests). */
+typedef int (*pbrthost_loop_subdivider)(void *user, int32_t nf, int32_t nv, const int32_t *vi, const float *P,
+                                        int32_t levels, int32_t *nv_out, float *P_out, float *N_out, int32_t *vi_out);
+int pbrthost_set_loop_subdivider(pbrthost_loop_subdivider fn, void *user);
+int pbrthost_loop_refine(int32_t nf, int32_t nv, const int32_t *vi, const float *P, int32_t levels, int32_t *nv_out,
+                         float *P_out, float *N_out, int32_t *vi_out);
 int pbrthost_spectrum_from_rgb(int bands, const float rgb[3], int illuminant, float *out);
 
 #ifdef __cplusplus

@@ -46,8 +46,12 @@ namespace pgd {
 // GPU linear BVH build (lbvh.hip)
 int lbvh_build(hipStream_t stream, int n, const float *bounds, pbrtgpu_bvh_node *nodes_out, int32_t *order_out,
                double *ms_out, std::string *err);
+// GPU Loop subdivision (loopsubdiv.hip)
+int loop_subdivide(hipStream_t stream, int nf, int nv, const int32_t *vi, const float *P, int levels, int32_t *nv_out,
+                   float *P_out, float *N_out, int32_t *vi_out, double *ms_out, std::string *err);
 }
 using pgd::lbvh_build;
+using pgd::loop_subdivide;
 
 static thread_local std::string g_err;
 static int fail(int code, const std::string &msg) { g_err = msg; return code; }
@@ -1940,6 +1944,21 @@ int pbrtgpu_build_bvh(pbrtgpu_ctx *c, int32_t n, const float *bounds, pbrtgpu_bv
     std::string err;
     const int e = lbvh_build(c->stream, n, bounds, nodes_out, order_out, ms_out, &err);
     return e ? fail(e, "pbrtgpu_build_bvh: " + err) : 2 * n - 1;
+}
+
+int pbrtgpu_loop_subdivide(pbrtgpu_ctx *c, int32_t nf, int32_t nv, const int32_t *vi, const float *P, int32_t levels,
+                           int32_t *nv_out, float *P_out, float *N_out, int32_t *vi_out, double *ms_out) {
+    if (!c || nf < 1 || nv < 1 || !vi || !P || !nv_out || levels < 0 || levels > 12 || (P_out && (!N_out || !vi_out)))
+        return fail(PBRTGPU_E_INVALID, "bad arguments");
+    HIPCHK(hipSetDevice(c->device));
+    std::string err;
+    const int e = loop_subdivide(c->stream, nf, nv, vi, P, levels, nv_out, P_out, N_out, vi_out, ms_out, &err);
+    return e ? fail(e < -1 ? e : PBRTGPU_E_INVALID, "pbrtgpu_loop_subdivide: " + err) : 0;
+}
+
+int pbrtgpu_loop_subdivide_hook(void *ctx, int32_t nf, int32_t nv, const int32_t *vi, const float *P, int32_t levels,
+                                int32_t *nv_out, float *P_out, float *N_out, int32_t *vi_out) {
+    return pbrtgpu_loop_subdivide((pbrtgpu_ctx *)ctx, nf, nv, vi, P, levels, nv_out, P_out, N_out, vi_out, nullptr);
 }
 
 int pbrtgpu_intersect(pbrtgpu_ctx *c, const float *rays, int32_t n, float *hits, int32_t *occ) {

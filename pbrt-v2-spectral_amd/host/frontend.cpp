@@ -15,6 +15,7 @@
 //                                          film/spectralImage.cpp:40-50,176-185
 // Float expressions keep the reference's operand order (compile with -ffp-contract=off).
 #include "scene.h"
+#include "pbrthost.h"
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -351,8 +352,9 @@ static void LoopInit(ShapeObj &s, int nfaces, int nvertices, const int *vi, cons
     }
 }
 
-// LoopSubdiv::Refine (loopsubdiv.cpp:222-437) -> TriangleMesh with limit normals
-static std::shared_ptr<TriMesh> LoopRefine(ShapeObj &s) {
+// LoopSubdiv::Refine (loopsubdiv.cpp:222-437): limit positions (object space), limit normals
+// and the refined faces' vertex indices
+static void LoopRefineCore(ShapeObj &s, std::vector<V3> &Plimit, std::vector<V3> &Ns, std::vector<int> &vi) {
     std::vector<SDVertex> V = s.verts;
     std::vector<SDFace> F = s.faces;
     std::vector<int> f(F.size()), v(V.size());
@@ -446,14 +448,14 @@ static std::shared_ptr<TriMesh> LoopRefine(ShapeObj &s) {
         v = newVertices;
     }
     // limit surface
-    std::vector<V3> Plimit(v.size());
+    Plimit.assign(v.size(), V3());
     for (size_t i = 0; i < v.size(); ++i) {
         if (V[v[i]].boundary) Plimit[i] = lm.weightBoundary(v[i], 1.f / 5.f);
         else Plimit[i] = lm.weightOneRing(v[i], LoopGamma(lm.valence(v[i])));
     }
     for (size_t i = 0; i < v.size(); ++i) V[v[i]].P = Plimit[i];
     // tangents -> normals
-    std::vector<V3> Ns;
+    Ns.clear();
     Ns.reserve(v.size());
     std::vector<V3> Pring;
     for (size_t i = 0; i < v.size(); ++i) {
@@ -484,20 +486,87 @@ static std::shared_ptr<TriMesh> LoopRefine(ShapeObj &s) {
         }
         Ns.push_back(Cross(S, T));
     }
+    std::map<int, int> used;
+    for (size_t i = 0; i < v.size(); ++i) used[v[i]] = (int)i;
+    vi.clear();
+    for (size_t i = 0; i < f.size(); ++i)
+        for (int j = 0; j < 3; ++j) vi.push_back(used[F[f[i]].v[j]]);
+}
+
+// the refinement of a loopsubdiv shape: on the GPU when a subdivider is set
+// (pbrthost_set_loop_subdivider; pbrtgpu_loop_subdivide_hook), else LoopRefineCore
+static pbrthost_loop_subdivider g_loopFn = nullptr;
+static void *g_loopUser = nullptr;
+static std::shared_ptr<TriMesh> LoopRefine(ShapeObj &s) {
+    std::vector<V3> Plimit, Ns;
+    std::vector<int> vi;
+    if (g_loopFn) {
+        const int nf = (int)s.faces.size(), nv = (int)s.verts.size();
+        std::vector<int> cvi(3 * (size_t)nf);
+        std::vector<float> cP(3 * (size_t)nv);
+        for (int i = 0; i < nf; ++i)
+            for (int j = 0; j < 3; ++j) cvi[3 * i + j] = s.faces[i].v[j];
+        for (int i = 0; i < nv; ++i) { cP[3 * i] = s.verts[i].P.x; cP[3 * i + 1] = s.verts[i].P.y; cP[3 * i + 2] = s.verts[i].P.z; }
+        int nvOut = 0;
+        if (g_loopFn(g_loopUser, nf, nv, cvi.data(), cP.data(), s.nLevels, &nvOut, nullptr, nullptr, nullptr) != 0)
+            throw std::runtime_error("loopsubdiv: the GPU subdivider failed (sizes)");
+        const size_t nfOut = (size_t)nf << (2 * s.nLevels);
+        std::vector<float> P(3 * (size_t)nvOut), N(3 * (size_t)nvOut);
+        vi.resize(3 * nfOut);
+        if (g_loopFn(g_loopUser, nf, nv, cvi.data(), cP.data(), s.nLevels, &nvOut, P.data(), N.data(), vi.data()) != 0)
+            throw std::runtime_error("loopsubdiv: the GPU subdivider failed");
+        Plimit.resize(nvOut);
+        Ns.resize(nvOut);
+        for (int i = 0; i < nvOut; ++i) {
+            Plimit[i] = V3(P[3 * i], P[3 * i + 1], P[3 * i + 2]);
+            Ns[i] = V3(N[3 * i], N[3 * i + 1], N[3 * i + 2]);
+        }
+    } else LoopRefineCore(s, Plimit, Ns, vi);
     auto mesh = std::make_shared<TriMesh>();
     mesh->o2w = s.o2w;
     mesh->ro = s.ro;
     mesh->swaps = s.o2w.SwapsHandedness();
-    mesh->ntris = (int)f.size();
-    mesh->nverts = (int)v.size();
-    std::map<int, int> used;
-    for (size_t i = 0; i < v.size(); ++i) used[v[i]] = (int)i;
-    for (size_t i = 0; i < f.size(); ++i)
-        for (int j = 0; j < 3; ++j) mesh->vi.push_back(used[F[f[i]].v[j]]);
-    mesh->p.resize(v.size());
-    for (size_t i = 0; i < v.size(); ++i) mesh->p[i] = s.o2w.Point(Plimit[i]);
+    mesh->ntris = (int)vi.size() / 3;
+    mesh->nverts = (int)Plimit.size();
+    mesh->vi = vi;
+    mesh->p.resize(Plimit.size());
+    for (size_t i = 0; i < Plimit.size(); ++i) mesh->p[i] = s.o2w.Point(Plimit[i]);
     mesh->n = Ns;
     return mesh;
+}
+
+extern "C" int pbrthost_set_loop_subdivider(pbrthost_loop_subdivider fn, void *user) {
+    g_loopFn = fn;
+    g_loopUser = user;
+    return 0;
+}
+
+// the host refinement of a control mesh (object space), for tests of the GPU subdivider
+extern "C" int pbrthost_loop_refine(int32_t nf, int32_t nv, const int32_t *vi, const float *P, int32_t levels,
+                                    int32_t *nv_out, float *P_out, float *N_out, int32_t *vi_out) {
+    try {
+        if (nf < 1 || nv < 1 || levels < 0 || !vi || !P || !nv_out) return -1;
+        std::vector<V3> cp(nv);
+        for (int i = 0; i < nv; ++i) cp[i] = V3(P[3 * i], P[3 * i + 1], P[3 * i + 2]);
+        ShapeObj s;
+        s.kind = ShapeObj::LOOP;
+        s.nLevels = levels;
+        LoopInit(s, nf, nv, vi, cp.data());
+        std::vector<V3> Pl, Ns;
+        std::vector<int> fvi;
+        LoopRefineCore(s, Pl, Ns, fvi);
+        *nv_out = (int32_t)Pl.size();
+        if (P_out) {
+            for (size_t i = 0; i < Pl.size(); ++i) {
+                P_out[3 * i] = Pl[i].x; P_out[3 * i + 1] = Pl[i].y; P_out[3 * i + 2] = Pl[i].z;
+                N_out[3 * i] = Ns[i].x; N_out[3 * i + 1] = Ns[i].y; N_out[3 * i + 2] = Ns[i].z;
+            }
+            std::copy(fvi.begin(), fvi.end(), vi_out);
+        }
+        return 0;
+    } catch (const std::exception &) {
+        return -1;
+    }
 }
 
 // ------------------------------------------------------------------------------------

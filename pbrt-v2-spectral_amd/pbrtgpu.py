@@ -131,6 +131,8 @@ def host_lib():
         _host.pbrthost_write_dat_scene.argtypes = [P, ctypes.c_char_p, P, P]
         _host.pbrthost_spectrum_from_rgb.argtypes = [ctypes.c_int, P, ctypes.c_int, P]
         _host.pbrthost_write_metadata.argtypes = [P, ctypes.c_char_p]
+        _host.pbrthost_set_loop_subdivider.argtypes = [P, P]
+        _host.pbrthost_loop_refine.argtypes = [I32, I32, P, P, I32, P, P, P, P]
     return _host
 
 
@@ -138,7 +140,39 @@ def host_symbols():
     """Symbols declared in include/pbrthost.h."""
     return ["pbrthost_load", "pbrthost_free", "pbrthost_flat", "pbrthost_save_pack", "pbrthost_set_render",
             "pbrthost_info", "pbrthost_write_dat", "pbrthost_write_dat_scene", "pbrthost_spectrum_from_rgb",
-            "pbrthost_write_metadata"]
+            "pbrthost_write_metadata", "pbrthost_set_loop_subdivider", "pbrthost_loop_refine"]
+
+
+def _loop_call(fn, vi, P, levels, *lead):
+    """Run a subdivider with the pbrthost_loop_subdivider convention -> (P, N, vi)."""
+    vi = np.ascontiguousarray(vi, np.int32).reshape(-1, 3)
+    P = np.ascontiguousarray(P, np.float32).reshape(-1, 3)
+    nv = np.zeros(1, np.int32)
+    rc = fn(*lead, len(vi), len(P), vi.ctypes.data, P.ctypes.data, levels, nv.ctypes.data, None, None, None)
+    if rc != 0:
+        raise RuntimeError("loop subdivision failed (%d)" % rc)
+    Po, No = np.zeros((nv[0], 3), np.float32), np.zeros((nv[0], 3), np.float32)
+    vo = np.zeros((len(vi) << (2 * levels), 3), np.int32)
+    rc = fn(*lead, len(vi), len(P), vi.ctypes.data, P.ctypes.data, levels, nv.ctypes.data, Po.ctypes.data,
+            No.ctypes.data, vo.ctypes.data)
+    if rc != 0:
+        raise RuntimeError("loop subdivision failed (%d)" % rc)
+    return Po, No, vo
+
+
+def loop_refine_host(vi, P, levels):
+    """The front end's LoopSubdiv::Refine of a control mesh (object space): (P, N, vi)."""
+    return _loop_call(host_lib().pbrthost_loop_refine, vi, P, levels)
+
+
+def use_gpu_subdivision(device):
+    """Scenes loaded from now on refine their loopsubdiv shapes on `device` (a Device), or on
+    the host again with None (pbrthost_set_loop_subdivider + pbrtgpu_loop_subdivide_hook)."""
+    if device is None:
+        host_lib().pbrthost_set_loop_subdivider(None, None)
+    else:
+        fn = ctypes.cast(gpu_lib().pbrtgpu_loop_subdivide_hook, P)
+        host_lib().pbrthost_set_loop_subdivider(fn, device.ctx)
 
 
 def spectrum_from_rgb(rgb, bands=32, illuminant=False):
@@ -170,6 +204,8 @@ def gpu_lib():
         g.pbrtgpu_film_gather.argtypes = [P, I32, I32, P, I32, P, ctypes.c_int64]
         g.pbrtgpu_render_multi.argtypes = [P, I32, ctypes.POINTER(RenderDesc), P, I32, I32, P, ctypes.c_int64, P]
         g.pbrtgpu_build_bvh.argtypes = [P, I32, P, P, P, P]
+        g.pbrtgpu_loop_subdivide.argtypes = [P, I32, I32, P, P, I32, P, P, P, P, P]
+        g.pbrtgpu_loop_subdivide_hook.argtypes = [P, I32, I32, P, P, I32, P, P, P, P]
     return _gpu
 
 
@@ -179,7 +215,8 @@ def gpu_symbols():
             "pbrtgpu_context_destroy", "pbrtgpu_last_error", "pbrtgpu_scene_upload",
             "pbrtgpu_render_tiles", "pbrtgpu_film_read", "pbrtgpu_film_clear",
             "pbrtgpu_trace_paths", "pbrtgpu_intersect", "pbrtgpu_path_stats", "pbrtgpu_last_timing",
-            "pbrtgpu_film_gather", "pbrtgpu_render_multi", "pbrtgpu_build_bvh"]
+            "pbrtgpu_film_gather", "pbrtgpu_render_multi", "pbrtgpu_build_bvh", "pbrtgpu_loop_subdivide",
+            "pbrtgpu_loop_subdivide_hook"]
 
 
 def tile_grid(scene, tile=16):
@@ -406,6 +443,10 @@ class Device:
             _check(rc)
         assert rc == 2 * n - 1
         return BvhScene(scene, nodes, order, (float(ms[0]), float(ms[1])))
+
+    def loop_subdivide(self, vi, P, levels):
+        """Loop subdivision of a control mesh on this GPU (pbrtgpu_loop_subdivide): (P, N, vi)."""
+        return _loop_call(self.lib.pbrtgpu_loop_subdivide_hook, vi, P, levels, self.ctx)
 
     def render(self, spp_begin=0, spp_end=None, tiles=None, tile=(16, 16), accumulate=False, stats=None,
                count_work=False):
