@@ -22,6 +22,9 @@ GpuPathRenderer::GpuPathRenderer(Camera *c, const ParamSet &params)
     // the SpectralRenderer's parameters (api.cpp:1378-1379): "integer nWaveBands" > 0 renders
     // as Renderer "spectralrenderer" would
     waveBands = params.FindOneInt("nWaveBands", 0);
+    // "bool gpusetup": the front end refines the scene's loopsubdiv shapes on the first GPU
+    // (positions bit-identical to the host refinement, normals up to last-ulp cosf / sinf cases)
+    gpuSetup = params.FindOneBool("gpusetup", false);
     string sm = params.FindOneString("samplingMethod", "singleDirection");
     spectralSampling = sm == "samplerDirection" ? PBRTGPU_SPECTRAL_SAMPLER : PBRTGPU_SPECTRAL_SINGLE;
     // the spectral film writes <imageOutputName stem>.dat (spectralImage.cpp:348-350)
@@ -51,16 +54,23 @@ void GpuPathRenderer::Render(const Scene *) {
                               waveBands > 0 ? spectralSampling : -1 };
     pbrthost_scene *hs = NULL;
     char err[1024];
-    if ((status = pbrthost_load(sceneFile.c_str(), &ov, &hs, err, sizeof(err))) != 0) {
-        Error("gpupath: %s", err);
+    std::vector<pbrtgpu_ctx *> ctx(n, (pbrtgpu_ctx *)NULL);
+    for (int d = 0; d < n && status == 0; ++d) status = pbrtgpu_context_create(d, &ctx[d]);
+    if (status == 0) {
+        if (gpuSetup) pbrthost_set_loop_subdivider(pbrtgpu_loop_subdivide_hook, ctx[0]);
+        status = pbrthost_load(sceneFile.c_str(), &ov, &hs, err, sizeof(err));
+        if (gpuSetup) pbrthost_set_loop_subdivider(NULL, NULL);
+        if (status != 0) Error("gpupath: %s", err);
+    } else Error("gpupath: %s", pbrtgpu_last_error());
+    if (status != 0) {
+        for (int d = 0; d < n; ++d)
+            if (ctx[d]) pbrtgpu_context_destroy(ctx[d]);
         return;
     }
     pbrtgpu_flat_scene fs;
     pbrthost_flat(hs, &fs);
     const int W = fs.camera.px_count, H = fs.camera.py_count, N = fs.n_bands;
-    std::vector<pbrtgpu_ctx *> ctx(n, (pbrtgpu_ctx *)NULL);
-    for (int d = 0; d < n && status == 0; ++d)
-        if ((status = pbrtgpu_context_create(d, &ctx[d])) == 0) status = pbrtgpu_scene_upload(ctx[d], &fs);
+    for (int d = 0; d < n && status == 0; ++d) status = pbrtgpu_scene_upload(ctx[d], &fs);
     std::vector<float> film((size_t)W * H * N, 0.f);
     if (status == 0) {
         // one host thread per GPU, interleaved 16x16 film tiles, host gather (no RCCL)

@@ -26,6 +26,7 @@ public:
     //   "integer gpus" (0: every visible device), "integer seed" (fixed-seed sampler seed),
     //   "integer slices" (tile slices per GPU), "string scenefile" (overrides SceneFile()),
     //   "integer nWaveBands" / "string samplingMethod" (the SpectralRenderer's, api.cpp:1378-1379).
+    //   "bool gpusetup" (refine loopsubdiv shapes on the GPU, pbrtgpu_loop_subdivide).
     GpuPathRenderer(Camera *camera, const ParamSet &params);
     ~GpuPathRenderer();
     // Renderer::Render: one frame over all GPUs, .dat written; on failure Error() and no file
@@ -49,6 +50,7 @@ private:
     Camera *camera;
     string sceneFile, outFile;
     int ngpu, slices, status;
+    bool gpuSetup;   // "bool gpusetup": refine loopsubdiv shapes on the GPU (pbrtgpu_loop_subdivide)
     int waveBands, spectralSampling;   // "nWaveBands" (> 0: SpectralRenderer), "samplingMethod"
     uint32_t seed;
 };
