@@ -93,7 +93,7 @@ __global__ __launch_bounds__(kShadeBlock) PGD_SHADE_ATTR void k_shade(DevScene S
         }
         else if (MODE == MODE_DL) pu = shade_slot_dl<NB, FEAT>(S, P, slot, Lout, &done, &zeroed);
         else if (MODE == MODE_META) pu = shade_slot_meta<NB, FEAT>(S, P, slot, Lout, &done, &zeroed);
-        else pu = shade_slot<NB, FEAT>(S, P, slot, Lout, &done, &zeroed);
+        else pu = shade_slot<NB, FEAT>(S, P, slot, Lout, &done, &zeroed, qout);
         if (done) { P.item[slot] = -1; freeSlot = true; }
     }
     if (__ballot(zeroed)) {

@@ -77,6 +77,9 @@ struct PathSoA {
     float4 *beta;       // [3][NQ][cap]: beta at vertex v in buffer v % 3
     float4 *L;          // [NQ][cap]
     float4 *A, *B;      // [2][NQ][cap]: pending direct-light terms of vertex v in buffer v & 1
+                        // (path integrator: A of a pass in buffer qout, compacted per wave, see aMask)
+    unsigned long long *aMask;   // [2][cap/64]: path integrator, the lanes of each wave that wrote
+                                 // an A term in the pass with queue set q (A = wave region + rank)
     float4 *M;          // [NQ][cap]: measured-BRDF spectrum of the BSDF value being consumed
     float4 *K;          // [NQ][cap]: the material's textured spectrum at the current vertex
     // ray records are indexed by ray slot rs: the slot itself, or (DirectLighting, a batch of
@@ -168,6 +171,19 @@ template <int NB> PGD_INLINE float4 *A_of(const PathSoA &P, int v, int slot) {
 }
 template <int NB> PGD_INLINE float4 *B_of(const PathSoA &P, int v, int slot) {
     return P.B + (size_t)(v & 1) * Bands<NB>::NQ * P.cap + slot;
+}
+
+// path integrator: the A region of slot's wave in the buffer of queue set q, and that wave's
+// writer mask; the reader of the next pass finds its term at the region + its rank
+template <int NB> PGD_INLINE float4 *A_reg(const PathSoA &P, int q, int slot) {
+    return P.A + (size_t)q * Bands<NB>::NQ * P.cap + (slot & ~63);
+}
+PGD_INLINE unsigned long long *A_mask(const PathSoA &P, int q, int slot) {
+    return P.aMask + (size_t)q * ((P.cap + 63) >> 6) + (slot >> 6);
+}
+template <int NB> PGD_INLINE const float4 *A_read(const PathSoA &P, int q, int slot) {
+    const unsigned long long m = *A_mask(P, q, slot);
+    return A_reg<NB>(P, q, slot) + __popcll(m & ((1ull << (slot & 63)) - 1ull));
 }
 
 PGD_INLINE float4 ld4(const float *p) { return *reinterpret_cast<const float4 *>(p); }
@@ -564,9 +580,13 @@ struct LAdds {
 // when the rays are answered.  Sets PF_PEND and the light index in fl.
 // A, B: the slot's term buffers for this sample; rs: the ray slot its shadow / MIS rays use.
 template <int NB, int FEAT>
+// aMask (path integrator): A is the wave's region of the pass's A buffer; the lanes that write
+// a term take its entries in lane order (whole 64-B lines instead of the scattered lines of
+// divergent lanes) and *aMask records them for the reader of the next pass
 PGD_INLINE void estimate_direct(const DevScene &S, const PathSoA &P, int slot, int rs, float4 *A, float4 *B,
                                 int lightNum, const BSDF &bs, PowMemo &pm, V p, V n, V wo, float rayEps, float time,
-                                const float ul[3], const float ub[3], FVal &F, uint32_t &fl, Pushes &out) {
+                                const float ul[3], const float ub[3], FVal &F, uint32_t &fl, Pushes &out,
+                                unsigned long long *aMask) {
     constexpr int NQ = Bands<NB>::NQ;
     const size_t c = P.cap;
     const float *sp = S.spectra;
@@ -583,7 +603,14 @@ PGD_INLINE void estimate_direct(const DevScene &S, const PathSoA &P, int slot, i
     light_sample_L<FEAT>(S, Lt, p, rayEps, ul, &wi, &lightPdf, &vis, &em);
     if (lightPdf > 0. && !emit_black<NB, FEAT>(S, em)) bsdf_f(pm, bs, wo, wi, flags, F);
     // no matching BxDF (e.g. the light below the surface): f is black, A unused
-    if (lightPdf > 0. && !emit_black<NB, FEAT>(S, em) && !(F.mode == FV_SUM && F.n == 0)) {
+    const bool withA = lightPdf > 0. && !emit_black<NB, FEAT>(S, em) && !(F.mode == FV_SUM && F.n == 0);
+    if (aMask) {
+        const unsigned long long m = __ballot(withA), act = __ballot(true);
+        const int lane = threadIdx.x & 63;
+        if (lane == __ffsll((long long)act) - 1) *aMask = m;
+        A += __popcll(m & ((1ull << lane) - 1ull));
+    }
+    if (withA) {
         fval_prepare<NB, FEAT>(S, F, mb, c);
         float sc;
         if (em.point) sc = fabsf(vdot(wi, n)) / lightPdf;
@@ -674,7 +701,7 @@ PGD_INLINE void estimate_direct(const DevScene &S, const PathSoA &P, int slot, i
 // evaluated lazily per band quad (fval4).  Updates fl.
 template <int NB, int FEAT>
 PGD_INLINE Pushes shade_vertex(const DevScene &S, const PathSoA &P, int slot, int vb, const Ray &ray, int prim,
-                               float thit, uint32_t &fl, LAdds *la) {
+                               float thit, uint32_t &fl, LAdds *la, int qout) {
     constexpr int NQ = Bands<NB>::NQ;
     const size_t c = P.cap;
     const float *sp = S.spectra;
@@ -745,8 +772,8 @@ PGD_INLINE Pushes shade_vertex(const DevScene &S, const PathSoA &P, int slot, in
         }
         int lightNum = (int)floorf(ulnum * nLights);
         if (lightNum > nLights - 1) lightNum = nLights - 1;
-        estimate_direct<NB, FEAT>(S, P, slot, slot, A_of<NB>(P, vb, slot), B_of<NB>(P, vb, slot), lightNum, bs, pm, p, n,
-                                  wo, is.rayEps, ray.time, ul, ub, F, fl, out);
+        estimate_direct<NB, FEAT>(S, P, slot, slot, A_reg<NB>(P, qout, slot), B_of<NB>(P, vb, slot), lightNum, bs, pm, p,
+                                  n, wo, is.rayEps, ray.time, ul, ub, F, fl, out, A_mask(P, qout, slot));
         if (!(fl & (PF_PA | PF_PB))) {
             // nothing can add to Ld: finish now (L += beta * (nLights * 0), nLights * 0 == 0)
             la->zero = true;
@@ -834,7 +861,7 @@ PGD_INLINE Pushes shade_vertex(const DevScene &S, const PathSoA &P, int slot, in
 // through shade_vertex is what lets the kernel fit its occupancy target.
 template <int NB, int FEAT>
 PGD_INLINE Pushes shade_slot(const DevScene &S, const PathSoA &P, int slot, float *__restrict__ Lout, bool *done,
-                             bool *zeroed) {
+                             bool *zeroed, int qout) {
     constexpr int NQ = Bands<NB>::NQ;
     const size_t c = P.cap;
     PGD_T0(LOAD);
@@ -871,7 +898,7 @@ PGD_INLINE Pushes shade_slot(const DevScene &S, const PathSoA &P, int slot, floa
         if (prim < 0) esc = vb == 0 ? 1 : ((fl & PF_SPEC) ? 2 : 0);
         else {
             Ray ray = ray_load(P, RAY_C, slot);
-            out = shade_vertex<NB, FEAT>(S, P, slot, vb, ray, prim, P.hitT[slot], fl, &la);
+            out = shade_vertex<NB, FEAT>(S, P, slot, vb, ray, prim, P.hitT[slot], fl, &la, qout);
             P.bounce[slot] = vb;
         }
     }
@@ -897,7 +924,8 @@ PGD_INLINE Pushes shade_slot(const DevScene &S, const PathSoA &P, int slot, floa
     for (int q = 0; q < NQ; ++q) L[q] = lz ? make_float4(0.f, 0.f, 0.f, 0.f) : P.L[q * c + slot];
     if (addFin) {   // L += beta_b * (nLights * Ld), Ld = (0 [+ A]) [+ B]
         const float nl = (float)S.nLights;
-        const float4 *A = A_of<NB>(P, b, slot), *B = B_of<NB>(P, b, slot);
+        // A of vertex b: written by the previous pass (queue set qout ^ 1), compacted per wave
+        const float4 *A = useA ? A_read<NB>(P, qout ^ 1, slot) : nullptr, *B = B_of<NB>(P, b, slot);
 #pragma unroll
         for (int q = 0; q < NQ; ++q) {
             float4 bt = beta_ld<NB>(P, b, slot, q);
