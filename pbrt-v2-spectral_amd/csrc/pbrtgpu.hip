@@ -795,7 +795,8 @@ static int ensure_slots(Lane *c, int cap, int NB, int nInst, int nFrames, int ba
            oB = take(C * AB * NBP * 4), oM = take(C * NBP * 4), oK = take(C * NBP * 4), oPix = take(C * 4),
            oRay = take(R * 27 * 4), oHitP = take(R * 8), oHitT = take(R * 8), oOcc = take(R * 4), oQC = take(R * 16),
            oQS = take(R * 8), oCnt = take(CNT_WORDS * 4), oInst = take(C * (size_t)nInst * 128),
-           oMask = take(nFrames ? C * 4 : 0), oAMask = take(2 * ((C + 63) / 64) * 8);
+           oMask = take(nFrames ? C * 4 : 0), oAMask = take(2 * ((C + 63) / 64) * 8),
+           oBMask = take(3 * ((C + 63) / 64) * 8);
     const size_t F = (size_t)nFrames;
     size_t oFL = take(C * F * NBP * 4), oFF = take(C * F * NBP * 4), oFRay = take(C * F * 36), oFDiff = take(C * F * 48),
            oFS = take(C * F * 8), oFHit = take(C * F * 8), oFBr = take(C * F * 4), oDlk = take(nFrames ? C * 4 : 0);
@@ -807,6 +808,8 @@ static int ensure_slots(Lane *c, int cap, int NB, int nInst, int nFrames, int ba
     P.dlBatch = batch;
     P.dlMask = nFrames ? (uint32_t *)(base + oMask) : nullptr;
     P.aMask = (unsigned long long *)(base + oAMask);
+    P.bMask = (unsigned long long *)(base + oBMask);
+    P.pass = 0;
     P.item = (int *)(base + oItem); P.hp = (uint32_t *)(base + oHp); P.smp = (uint32_t *)(base + oSmp);
     P.bounce = (int *)(base + oBounce); P.flags = (uint32_t *)(base + oFlags); P.mt = (uint32_t *)(base + oMt);
     P.beta = (float4 *)(base + oBeta); P.L = (float4 *)(base + oL); P.A = (float4 *)(base + oA); P.B = (float4 *)(base + oB);
@@ -916,6 +919,7 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
         HIPCHK(hipMemsetAsync(L.P.cnt, 0, CNT_WORDS * 4, L.s));
         // pass 0: every slot is free -> regeneration fills them with camera rays (queue 0)
         HIPCHK(hipEventRecord(L.ev[0], L.s));
+        L.P.pass = 0;   // k_shade pass index (mod 3) of this run: the beta buffers rotate with it
         HIPCHK(kShade(r.grid, L.s, c->S, L.P, r.src, 0, Lout));
         HIPCHK(hipEventRecord(L.ev[1], L.s));
         HIPCHK(hipMemcpyAsync(L.hostCnt, L.P.cnt, CNT_WORDS * 4, hipMemcpyDeviceToHost, L.s));
@@ -987,6 +991,7 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
                     T.launches[K_SHADOW]++;
                     HIPCHK(hipEventRecord(e[3], L.s));
                     HIPCHK(hipEventRecord(e[4], L.s));
+                    L.P.pass = (L.P.pass + 1) % 3;
                     HIPCHK(kShade(r.grid, L.s, c->S, P, r.src, nq, Lout));
                     if (dl) HIPCHK(kNee(r.grid, L.s, c->S, P, nq));
                     T.launches[K_SHADE]++;
@@ -1027,6 +1032,7 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
                 HIPCHK(hipEventRecord(e[3], s2));
                 HIPCHK(hipStreamWaitEvent(L.s, e[3], 0));
                 HIPCHK(hipEventRecord(e[4], L.s));
+                L.P.pass = (L.P.pass + 1) % 3;
                 HIPCHK(kShade(r.grid, L.s, c->S, P, r.src, nq, Lout));
                 if (dl) HIPCHK(kNee(r.grid, L.s, c->S, P, nq));
                 T.launches[K_SHADE]++;

@@ -80,6 +80,9 @@ struct PathSoA {
                         // (path integrator: A of a pass in buffer qout, compacted per wave, see aMask)
     unsigned long long *aMask;   // [2][cap/64]: path integrator, the lanes of each wave that wrote
                                  // an A term in the pass with queue set q (A = wave region + rank)
+    unsigned long long *bMask;   // [3][cap/64]: path integrator, the lanes of each wave that wrote
+                                 // a beta in the pass with index pass % 3 (beta = wave region + rank)
+    int pass;                    // index of this k_shade pass within the run (host counter)
     float4 *M;          // [NQ][cap]: measured-BRDF spectrum of the BSDF value being consumed
     float4 *K;          // [NQ][cap]: the material's textured spectrum at the current vertex
     // ray records are indexed by ray slot rs: the slot itself, or (DirectLighting, a batch of
@@ -155,15 +158,25 @@ PGD_INLINE void mt_store(const PathSoA &P, int slot, const MT &r) {
 }
 
 template <int NB> struct Bands { static constexpr int NQ = (NB + 3) / 4; };
-// path-state spectra of vertex v (v >= 0): beta in three buffers, so that a pass can read
-// beta_b (finishing vertex b), beta_{b+1} (shading it) and write beta_{b+2}; A, B in two
-template <int NB> PGD_INLINE float4 *beta_of(const PathSoA &P, int v, int slot) {
-    return P.beta + (size_t)(v % 3) * Bands<NB>::NQ * P.cap + slot;
+// path-state spectra: beta in three buffers, so that a pass can read beta_b (finishing vertex
+// b), beta_{b+1} (shading it) and write beta_{b+2}; A, B in two
+// Path integrator: beta of a vertex is written by the pass that samples its direction (buffer
+// pass % 3, compacted per wave like A) and read by the next pass (shading the vertex) and the one
+// after (finishing its direct light): ago = 1 or 2 passes.  Vertex 0 (beta = 1) is not stored.
+PGD_INLINE int pass_buf(const PathSoA &P, int ago) { return (P.pass + 3 - ago) % 3; }
+template <int NB> PGD_INLINE float4 *beta_reg(const PathSoA &P, int buf, int slot) {
+    return P.beta + (size_t)buf * Bands<NB>::NQ * P.cap + (slot & ~63);
 }
-// band quad q of beta at vertex v: beta_0 = 1 is never stored
-template <int NB> PGD_INLINE float4 beta_ld(const PathSoA &P, int v, int slot, int q) {
-    return v == 0 ? make_float4(1.f, 1.f, 1.f, 1.f) : beta_of<NB>(P, v, slot)[(size_t)q * P.cap];
+PGD_INLINE unsigned long long *beta_mask(const PathSoA &P, int buf, int slot) {
+    return P.bMask + (size_t)buf * ((P.cap + 63) >> 6) + (slot >> 6);
 }
+// the slot's beta written `ago` passes back (null for vertex 0)
+template <int NB> PGD_INLINE const float4 *beta_rd(const PathSoA &P, int v, int ago, int slot) {
+    if (v == 0) return nullptr;
+    const int buf = pass_buf(P, ago);
+    return beta_reg<NB>(P, buf, slot) + __popcll(*beta_mask(P, buf, slot) & ((1ull << (slot & 63)) - 1ull));
+}
+PGD_INLINE float4 beta_q(const float4 *bp, int q, size_t c) { return bp ? bp[q * c] : make_float4(1.f, 1.f, 1.f, 1.f); }
 // beta of vertex v has a non-finite band (then L += beta * 0 is NaN and cannot be skipped)
 PGD_INLINE bool beta_nonfinite(uint32_t fl, int v) { return v > 0 && ((fl >> (7 + v % 3)) & 1u); }
 template <int NB> PGD_INLINE float4 *A_of(const PathSoA &P, int v, int slot) {
@@ -798,12 +811,12 @@ PGD_INLINE Pushes shade_vertex(const DevScene &S, const PathSoA &P, int slot, in
     if (cont) {
         fval_prepare<NB, FEAT>(S, F, mb, c);
         const float ad = fabsf(vdot(wi, n));
-        float4 *bn = beta_of<NB>(P, vb + 1, slot);
+        const float4 *bv = beta_rd<NB>(P, vb, 1, slot);
         float4 nb4[NQ];
         bool black = true;
 #pragma unroll
         for (int q = 0; q < NQ; ++q) {
-            float4 f = fval4<FEAT>(sp, F, q, mb, kb, c), b = beta_ld<NB>(P, vb, slot, q);
+            float4 f = fval4<FEAT>(sp, F, q, mb, kb, c), b = beta_q(bv, q, c);
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 cmp(nb4[q], k) = cmp(b, k) * ((cmp(f, k) * ad) / pdf);
@@ -828,7 +841,12 @@ PGD_INLINE Pushes shade_vertex(const DevScene &S, const PathSoA &P, int slot, in
             }
             if (vb == S.maxDepth) cont = false;
         }
+        // beta_{vb+1}: the continuing lanes take the wave region's entries in lane order
+        const unsigned long long bm = __ballot(cont), act = __ballot(true);
+        const int buf = pass_buf(P, 0), lane = threadIdx.x & 63;
+        if (lane == __ffsll((long long)act) - 1) *beta_mask(P, buf, slot) = bm;
         if (cont) {
+            float4 *bn = beta_reg<NB>(P, buf, slot) + __popcll(bm & ((1ull << lane) - 1ull));
             bool nf = false;
 #pragma unroll
             for (int q = 0; q < NQ; ++q) {
@@ -926,9 +944,10 @@ PGD_INLINE Pushes shade_slot(const DevScene &S, const PathSoA &P, int slot, floa
         const float nl = (float)S.nLights;
         // A of vertex b: written by the previous pass (queue set qout ^ 1), compacted per wave
         const float4 *A = useA ? A_read<NB>(P, qout ^ 1, slot) : nullptr, *B = B_of<NB>(P, b, slot);
+        const float4 *bb4 = beta_rd<NB>(P, b, 2, slot);
 #pragma unroll
         for (int q = 0; q < NQ; ++q) {
-            float4 bt = beta_ld<NB>(P, b, slot, q);
+            float4 bt = beta_q(bb4, q, c);
             float4 a = useA ? A[q * c] : make_float4(0.f, 0.f, 0.f, 0.f);
             float4 bb = useB ? B[q * c] : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
@@ -942,9 +961,10 @@ PGD_INLINE Pushes shade_slot(const DevScene &S, const PathSoA &P, int slot, floa
     }
     if (addEmit || addZero) {   // vertex vb: L += beta * Le, then L += beta * (nLights * 0)
         const float *Ls = S.spectra + (la.emitOff >= 0 ? la.emitOff : 0);
+        const float4 *bv4 = beta_rd<NB>(P, vb, 1, slot);
 #pragma unroll
         for (int q = 0; q < NQ; ++q) {
-            const float4 bt = beta_ld<NB>(P, vb, slot, q);
+            const float4 bt = beta_q(bv4, q, c);
             if (addEmit) {
                 const float4 e = la.emitOff >= 0 ? ld4(Ls + 4 * q) : make_float4(0.f, 0.f, 0.f, 0.f);
                 L[q].x += bt.x * e.x; L[q].y += bt.y * e.y; L[q].z += bt.z * e.z; L[q].w += bt.w * e.w;
@@ -977,7 +997,7 @@ PGD_INLINE Pushes shade_slot(const DevScene &S, const PathSoA &P, int slot, floa
             if ((FEAT & FEAT_INF) && S.lights[l].type == PBRTGPU_LIGHT_INFINITE) e = inf_Le(S.lights[l], d);
 #pragma unroll
             for (int q = 0; q < NQ; ++q) {
-                float4 bt = beta_ld<NB>(P, vb, slot, q), v = emit4<FEAT>(S, e, q);
+                float4 bt = beta_q(beta_rd<NB>(P, vb, 1, slot), q, c), v = emit4<FEAT>(S, e, q);
                 L[q].x += bt.x * v.x; L[q].y += bt.y * v.y; L[q].z += bt.z * v.z; L[q].w += bt.w * v.w;
             }
         }
