@@ -203,7 +203,7 @@ PGD_INLINE bool dl_light_batches(const DevScene &S, const PathSoA &P, int slot, 
             Pushes o2 = {false, false, false, 0u, 0u};
             estimate_direct<NB, FEAT>(S, P, slot, slot + jb * (int)c, P.A + (size_t)jb * NQ * c + slot,
                                       P.B + (size_t)jb * NQ * c + slot, ln, vx.bs, pm, vx.p, vx.n, vx.wo,
-                                      vx.is.rayEps, vx.ray.time, ul, ub, F, f2, o2, nullptr);
+                                      vx.is.rayEps, vx.ray.time, ul, ub, F, f2, o2, nullptr, nullptr);
             if (f2 & PF_PA) mA |= 1u << jb;
             if (f2 & PF_PB) mB |= 1u << jb;
             lnOne = ln;

@@ -796,7 +796,7 @@ static int ensure_slots(Lane *c, int cap, int NB, int nInst, int nFrames, int ba
            oRay = take(R * 27 * 4), oHitP = take(R * 8), oHitT = take(R * 8), oOcc = take(R * 4), oQC = take(R * 16),
            oQS = take(R * 8), oCnt = take(CNT_WORDS * 4), oInst = take(C * (size_t)nInst * 128),
            oMask = take(nFrames ? C * 4 : 0), oAMask = take(2 * ((C + 63) / 64) * 8),
-           oBMask = take(3 * ((C + 63) / 64) * 8);
+           oBMask = take(3 * ((C + 63) / 64) * 8), oMMask = take(2 * ((C + 63) / 64) * 8);
     const size_t F = (size_t)nFrames;
     size_t oFL = take(C * F * NBP * 4), oFF = take(C * F * NBP * 4), oFRay = take(C * F * 36), oFDiff = take(C * F * 48),
            oFS = take(C * F * 8), oFHit = take(C * F * 8), oFBr = take(C * F * 4), oDlk = take(nFrames ? C * 4 : 0);
@@ -809,6 +809,7 @@ static int ensure_slots(Lane *c, int cap, int NB, int nInst, int nFrames, int ba
     P.dlMask = nFrames ? (uint32_t *)(base + oMask) : nullptr;
     P.aMask = (unsigned long long *)(base + oAMask);
     P.bMask = (unsigned long long *)(base + oBMask);
+    P.mMask = (unsigned long long *)(base + oMMask);
     P.pass = 0;
     P.item = (int *)(base + oItem); P.hp = (uint32_t *)(base + oHp); P.smp = (uint32_t *)(base + oSmp);
     P.bounce = (int *)(base + oBounce); P.flags = (uint32_t *)(base + oFlags); P.mt = (uint32_t *)(base + oMt);

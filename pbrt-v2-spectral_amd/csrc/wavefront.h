@@ -80,6 +80,7 @@ struct PathSoA {
                         // (path integrator: A of a pass in buffer qout, compacted per wave, see aMask)
     unsigned long long *aMask;   // [2][cap/64]: path integrator, the lanes of each wave that wrote
                                  // an A term in the pass with queue set q (A = wave region + rank)
+    unsigned long long *mMask;   // [2][cap/64]: the same for the B (MIS) terms
     unsigned long long *bMask;   // [3][cap/64]: path integrator, the lanes of each wave that wrote
                                  // a beta in the pass with index pass % 3 (beta = wave region + rank)
     int pass;                    // index of this k_shade pass within the run (host counter)
@@ -197,6 +198,17 @@ PGD_INLINE unsigned long long *A_mask(const PathSoA &P, int q, int slot) {
 template <int NB> PGD_INLINE const float4 *A_read(const PathSoA &P, int q, int slot) {
     const unsigned long long m = *A_mask(P, q, slot);
     return A_reg<NB>(P, q, slot) + __popcll(m & ((1ull << (slot & 63)) - 1ull));
+}
+// the B (MIS) terms likewise
+template <int NB> PGD_INLINE float4 *B_reg(const PathSoA &P, int q, int slot) {
+    return P.B + (size_t)q * Bands<NB>::NQ * P.cap + (slot & ~63);
+}
+PGD_INLINE unsigned long long *B_mask(const PathSoA &P, int q, int slot) {
+    return P.mMask + (size_t)q * ((P.cap + 63) >> 6) + (slot >> 6);
+}
+template <int NB> PGD_INLINE const float4 *B_read(const PathSoA &P, int q, int slot) {
+    const unsigned long long m = *B_mask(P, q, slot);
+    return B_reg<NB>(P, q, slot) + __popcll(m & ((1ull << (slot & 63)) - 1ull));
 }
 
 PGD_INLINE float4 ld4(const float *p) { return *reinterpret_cast<const float4 *>(p); }
@@ -599,7 +611,7 @@ template <int NB, int FEAT>
 PGD_INLINE void estimate_direct(const DevScene &S, const PathSoA &P, int slot, int rs, float4 *A, float4 *B,
                                 int lightNum, const BSDF &bs, PowMemo &pm, V p, V n, V wo, float rayEps, float time,
                                 const float ul[3], const float ub[3], FVal &F, uint32_t &fl, Pushes &out,
-                                unsigned long long *aMask) {
+                                unsigned long long *aMask, unsigned long long *mMask) {
     constexpr int NQ = Bands<NB>::NQ;
     const size_t c = P.cap;
     const float *sp = S.spectra;
@@ -684,7 +696,14 @@ PGD_INLINE void estimate_direct(const DevScene &S, const PathSoA &P, int slot, i
             } else {
                 eb.mode = Lt.is_black ? EM_BLACK : EM_POOL; eb.off = Lt.spec; eb.div = 1.f; eb.point = false;
             }
-            if (go && !emit_black<NB, FEAT>(S, eb)) {
+            const bool withB = go && !emit_black<NB, FEAT>(S, eb);
+            if (mMask) {   // path integrator: B in the wave's compacted region (as A)
+                const unsigned long long m = __ballot(withB), act = __ballot(true);
+                const int lane = threadIdx.x & 63;
+                if (lane == __ffsll((long long)act) - 1) *mMask = m;
+                B += __popcll(m & ((1ull << lane) - 1ull));
+            }
+            if (withB) {
                 const float ad = fabsf(vdot(wi, n));
                 bool black = true;
 #pragma unroll
@@ -785,8 +804,9 @@ PGD_INLINE Pushes shade_vertex(const DevScene &S, const PathSoA &P, int slot, in
         }
         int lightNum = (int)floorf(ulnum * nLights);
         if (lightNum > nLights - 1) lightNum = nLights - 1;
-        estimate_direct<NB, FEAT>(S, P, slot, slot, A_reg<NB>(P, qout, slot), B_of<NB>(P, vb, slot), lightNum, bs, pm, p,
-                                  n, wo, is.rayEps, ray.time, ul, ub, F, fl, out, A_mask(P, qout, slot));
+        estimate_direct<NB, FEAT>(S, P, slot, slot, A_reg<NB>(P, qout, slot), B_reg<NB>(P, qout, slot), lightNum, bs, pm,
+                                  p, n, wo, is.rayEps, ray.time, ul, ub, F, fl, out, A_mask(P, qout, slot),
+                                  B_mask(P, qout, slot));
         if (!(fl & (PF_PA | PF_PB))) {
             // nothing can add to Ld: finish now (L += beta * (nLights * 0), nLights * 0 == 0)
             la->zero = true;
@@ -943,7 +963,7 @@ PGD_INLINE Pushes shade_slot(const DevScene &S, const PathSoA &P, int slot, floa
     if (addFin) {   // L += beta_b * (nLights * Ld), Ld = (0 [+ A]) [+ B]
         const float nl = (float)S.nLights;
         // A of vertex b: written by the previous pass (queue set qout ^ 1), compacted per wave
-        const float4 *A = useA ? A_read<NB>(P, qout ^ 1, slot) : nullptr, *B = B_of<NB>(P, b, slot);
+        const float4 *A = useA ? A_read<NB>(P, qout ^ 1, slot) : nullptr, *B = useB ? B_read<NB>(P, qout ^ 1, slot) : nullptr;
         const float4 *bb4 = beta_rd<NB>(P, b, 2, slot);
 #pragma unroll
         for (int q = 0; q < NQ; ++q) {
