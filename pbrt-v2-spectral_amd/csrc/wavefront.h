@@ -171,11 +171,24 @@ template <int NB> PGD_INLINE float4 *beta_reg(const PathSoA &P, int buf, int slo
 PGD_INLINE unsigned long long *beta_mask(const PathSoA &P, int buf, int slot) {
     return P.bMask + (size_t)buf * ((P.cap + 63) >> 6) + (slot >> 6);
 }
-// the slot's beta written `ago` passes back (null for vertex 0)
-template <int NB> PGD_INLINE const float4 *beta_rd(const PathSoA &P, int v, int ago, int slot) {
+// the writer masks a k_shade wave reads, loaded once at the start of the slot's step (scalar
+// loads: the wave index is uniform), so that no spectrum load waits on its mask
+struct WaveMasks { unsigned long long a, b, b1, b2; };   // A, B of the last pass; beta 1, 2 passes back
+PGD_INLINE WaveMasks wave_masks(const PathSoA &P, int qout, int slot) {
+    const size_t W = (size_t)((P.cap + 63) >> 6);
+    const int w = __builtin_amdgcn_readfirstlane(slot >> 6);
+    WaveMasks m;
+    m.a = P.aMask[(size_t)(qout ^ 1) * W + w];
+    m.b = P.mMask[(size_t)(qout ^ 1) * W + w];
+    m.b1 = P.bMask[(size_t)pass_buf(P, 1) * W + w];
+    m.b2 = P.bMask[(size_t)pass_buf(P, 2) * W + w];
+    return m;
+}
+PGD_INLINE int wave_rank(unsigned long long m, int slot) { return __popcll(m & ((1ull << (slot & 63)) - 1ull)); }
+// the slot's beta written `ago` passes back (null for vertex 0); m = that pass's writer mask
+template <int NB> PGD_INLINE const float4 *beta_rd(const PathSoA &P, int v, int ago, int slot, unsigned long long m) {
     if (v == 0) return nullptr;
-    const int buf = pass_buf(P, ago);
-    return beta_reg<NB>(P, buf, slot) + __popcll(*beta_mask(P, buf, slot) & ((1ull << (slot & 63)) - 1ull));
+    return beta_reg<NB>(P, pass_buf(P, ago), slot) + wave_rank(m, slot);
 }
 PGD_INLINE float4 beta_q(const float4 *bp, int q, size_t c) { return bp ? bp[q * c] : make_float4(1.f, 1.f, 1.f, 1.f); }
 // beta of vertex v has a non-finite band (then L += beta * 0 is NaN and cannot be skipped)
@@ -195,20 +208,12 @@ template <int NB> PGD_INLINE float4 *A_reg(const PathSoA &P, int q, int slot) {
 PGD_INLINE unsigned long long *A_mask(const PathSoA &P, int q, int slot) {
     return P.aMask + (size_t)q * ((P.cap + 63) >> 6) + (slot >> 6);
 }
-template <int NB> PGD_INLINE const float4 *A_read(const PathSoA &P, int q, int slot) {
-    const unsigned long long m = *A_mask(P, q, slot);
-    return A_reg<NB>(P, q, slot) + __popcll(m & ((1ull << (slot & 63)) - 1ull));
-}
 // the B (MIS) terms likewise
 template <int NB> PGD_INLINE float4 *B_reg(const PathSoA &P, int q, int slot) {
     return P.B + (size_t)q * Bands<NB>::NQ * P.cap + (slot & ~63);
 }
 PGD_INLINE unsigned long long *B_mask(const PathSoA &P, int q, int slot) {
     return P.mMask + (size_t)q * ((P.cap + 63) >> 6) + (slot >> 6);
-}
-template <int NB> PGD_INLINE const float4 *B_read(const PathSoA &P, int q, int slot) {
-    const unsigned long long m = *B_mask(P, q, slot);
-    return B_reg<NB>(P, q, slot) + __popcll(m & ((1ull << (slot & 63)) - 1ull));
 }
 
 PGD_INLINE float4 ld4(const float *p) { return *reinterpret_cast<const float4 *>(p); }
@@ -733,7 +738,7 @@ PGD_INLINE void estimate_direct(const DevScene &S, const PathSoA &P, int slot, i
 // evaluated lazily per band quad (fval4).  Updates fl.
 template <int NB, int FEAT>
 PGD_INLINE Pushes shade_vertex(const DevScene &S, const PathSoA &P, int slot, int vb, const Ray &ray, int prim,
-                               float thit, uint32_t &fl, LAdds *la, int qout) {
+                               float thit, uint32_t &fl, LAdds *la, int qout, unsigned long long mb1) {
     constexpr int NQ = Bands<NB>::NQ;
     const size_t c = P.cap;
     const float *sp = S.spectra;
@@ -831,7 +836,7 @@ PGD_INLINE Pushes shade_vertex(const DevScene &S, const PathSoA &P, int slot, in
     if (cont) {
         fval_prepare<NB, FEAT>(S, F, mb, c);
         const float ad = fabsf(vdot(wi, n));
-        const float4 *bv = beta_rd<NB>(P, vb, 1, slot);
+        const float4 *bv = beta_rd<NB>(P, vb, 1, slot, mb1);
         float4 nb4[NQ];
         bool black = true;
 #pragma unroll
@@ -905,6 +910,7 @@ PGD_INLINE Pushes shade_slot(const DevScene &S, const PathSoA &P, int slot, floa
     PGD_T0(LOAD);
     uint32_t fl = P.flags[slot];
     const int b = P.bounce[slot];
+    const WaveMasks wm = wave_masks(P, qout, slot);
     Pushes out = {false, false, false};
     PGD_T1(LOAD);
     PGD_T0(FINISH);
@@ -936,7 +942,7 @@ PGD_INLINE Pushes shade_slot(const DevScene &S, const PathSoA &P, int slot, floa
         if (prim < 0) esc = vb == 0 ? 1 : ((fl & PF_SPEC) ? 2 : 0);
         else {
             Ray ray = ray_load(P, RAY_C, slot);
-            out = shade_vertex<NB, FEAT>(S, P, slot, vb, ray, prim, P.hitT[slot], fl, &la, qout);
+            out = shade_vertex<NB, FEAT>(S, P, slot, vb, ray, prim, P.hitT[slot], fl, &la, qout, wm.b1);
             P.bounce[slot] = vb;
         }
     }
@@ -963,8 +969,9 @@ PGD_INLINE Pushes shade_slot(const DevScene &S, const PathSoA &P, int slot, floa
     if (addFin) {   // L += beta_b * (nLights * Ld), Ld = (0 [+ A]) [+ B]
         const float nl = (float)S.nLights;
         // A of vertex b: written by the previous pass (queue set qout ^ 1), compacted per wave
-        const float4 *A = useA ? A_read<NB>(P, qout ^ 1, slot) : nullptr, *B = useB ? B_read<NB>(P, qout ^ 1, slot) : nullptr;
-        const float4 *bb4 = beta_rd<NB>(P, b, 2, slot);
+        const float4 *A = A_reg<NB>(P, qout ^ 1, slot) + wave_rank(wm.a, slot),
+                     *B = B_reg<NB>(P, qout ^ 1, slot) + wave_rank(wm.b, slot);
+        const float4 *bb4 = beta_rd<NB>(P, b, 2, slot, wm.b2);
 #pragma unroll
         for (int q = 0; q < NQ; ++q) {
             float4 bt = beta_q(bb4, q, c);
@@ -981,7 +988,7 @@ PGD_INLINE Pushes shade_slot(const DevScene &S, const PathSoA &P, int slot, floa
     }
     if (addEmit || addZero) {   // vertex vb: L += beta * Le, then L += beta * (nLights * 0)
         const float *Ls = S.spectra + (la.emitOff >= 0 ? la.emitOff : 0);
-        const float4 *bv4 = beta_rd<NB>(P, vb, 1, slot);
+        const float4 *bv4 = beta_rd<NB>(P, vb, 1, slot, wm.b1);
 #pragma unroll
         for (int q = 0; q < NQ; ++q) {
             const float4 bt = beta_q(bv4, q, c);
@@ -1017,7 +1024,7 @@ PGD_INLINE Pushes shade_slot(const DevScene &S, const PathSoA &P, int slot, floa
             if ((FEAT & FEAT_INF) && S.lights[l].type == PBRTGPU_LIGHT_INFINITE) e = inf_Le(S.lights[l], d);
 #pragma unroll
             for (int q = 0; q < NQ; ++q) {
-                float4 bt = beta_q(beta_rd<NB>(P, vb, 1, slot), q, c), v = emit4<FEAT>(S, e, q);
+                float4 bt = beta_q(beta_rd<NB>(P, vb, 1, slot, wm.b1), q, c), v = emit4<FEAT>(S, e, q);
                 L[q].x += bt.x * v.x; L[q].y += bt.y * v.y; L[q].z += bt.z * v.z; L[q].w += bt.w * v.w;
             }
         }
