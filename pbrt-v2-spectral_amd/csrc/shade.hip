@@ -154,7 +154,7 @@ __global__ __launch_bounds__(kShadeBlock) PGD_SHADE_ATTR void k_shade(DevScene S
         for (uint32_t m = pu.sMask; m; m &= m - 1u) qS[ks++] = (uint32_t)(slot + (__ffs(m) - 1) * P.cap);
     } else {
         if (pu.m) qC[km] = ((uint32_t)slot << 1) | 1u;
-        if (pu.s) qS[ks] = (uint32_t)slot;
+        if (pu.s) qS[ks] = (uint32_t)(MODE == MODE_PATH ? pu.sIdx : slot);
     }
     PGD_T1(PUSH);
 #ifdef PGD_SECTIONS

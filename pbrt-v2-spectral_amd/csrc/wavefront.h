@@ -592,7 +592,7 @@ PGD_INLINE bool path_output(const DevScene &S, const float4 (&L)[Bands<NB>::NQ],
 
 // ray requests produced by one shade step (DirectLighting batches: the MIS / shadow rays of
 // batch samples j at ray slots slot + j * cap, bit j of mMask / sMask)
-struct Pushes { bool c, m, s; uint32_t mMask, sMask; };
+struct Pushes { bool c, m, s; uint32_t mMask, sMask; int sIdx; };   // sIdx: the shadow ray's ray slot (path)
 
 // Additions to L a vertex makes before its direct light is known, in order: emitted
 // radiance (path.cpp:67-68; bounce 0 or after a specular bounce) and the zero direct light
@@ -634,11 +634,14 @@ PGD_INLINE void estimate_direct(const DevScene &S, const PathSoA &P, int slot, i
     if (lightPdf > 0. && !emit_black<NB, FEAT>(S, em)) bsdf_f(pm, bs, wo, wi, flags, F);
     // no matching BxDF (e.g. the light below the surface): f is black, A unused
     const bool withA = lightPdf > 0. && !emit_black<NB, FEAT>(S, em) && !(F.mode == FV_SUM && F.n == 0);
+    int rsS = rs;   // the shadow ray's record: path integrator without instances, at A's compacted entry
     if (aMask) {
         const unsigned long long m = __ballot(withA), act = __ballot(true);
         const int lane = threadIdx.x & 63;
         if (lane == __ffsll((long long)act) - 1) *aMask = m;
-        A += __popcll(m & ((1ull << lane) - 1ull));
+        const int rank = __popcll(m & ((1ull << lane) - 1ull));
+        A += rank;
+        if (!P.nInst) rsS = (slot & ~63) + rank;
     }
     if (withA) {
         fval_prepare<NB, FEAT>(S, F, mb, c);
@@ -664,9 +667,10 @@ PGD_INLINE void estimate_direct(const DevScene &S, const PathSoA &P, int slot, i
         if (!black) {
             Ray sr;
             sr.o = vis.o; sr.d = vis.d; sr.mint = vis.mint; sr.maxt = vis.maxt; sr.time = time;
-            ray_store(P, RAY_S, rs, sr);
+            ray_store(P, RAY_S, rsS, sr);
             fl |= PF_PA;
             out.s = true;
+            out.sIdx = rsS;
         }
     }
     PGD_T1(LIGHT);
@@ -919,7 +923,8 @@ PGD_INLINE Pushes shade_slot(const DevScene &S, const PathSoA &P, int slot, floa
     const bool fin = (fl & PF_PEND) != 0;
     bool useA = false, useB = false;
     if (fin) {
-        useA = (fl & PF_PA) && !P.occ[slot];
+        // the shadow ray's answer: at A's compacted entry (path integrator without instances)
+        useA = (fl & PF_PA) && !P.occ[P.nInst ? slot : (slot & ~63) + wave_rank(wm.a, slot)];
         if (fl & PF_PB) {
             const int ln = (int)(fl >> PF_LIGHT_SHIFT);
             int mp = P.hitPrim[P.rcap + slot];
