@@ -153,7 +153,7 @@ __global__ __launch_bounds__(kShadeBlock) PGD_SHADE_ATTR void k_shade(DevScene S
         for (uint32_t m = pu.mMask; m; m &= m - 1u) qC[km++] = ((uint32_t)(slot + (__ffs(m) - 1) * P.cap) << 1) | 1u;
         for (uint32_t m = pu.sMask; m; m &= m - 1u) qS[ks++] = (uint32_t)(slot + (__ffs(m) - 1) * P.cap);
     } else {
-        if (pu.m) qC[km] = ((uint32_t)slot << 1) | 1u;
+        if (pu.m) qC[km] = ((uint32_t)(MODE == MODE_PATH ? pu.mIdx : slot) << 1) | 1u;
         if (pu.s) qS[ks] = (uint32_t)(MODE == MODE_PATH ? pu.sIdx : slot);
     }
     PGD_T1(PUSH);

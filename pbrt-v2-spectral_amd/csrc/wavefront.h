@@ -592,7 +592,7 @@ PGD_INLINE bool path_output(const DevScene &S, const float4 (&L)[Bands<NB>::NQ],
 
 // ray requests produced by one shade step (DirectLighting batches: the MIS / shadow rays of
 // batch samples j at ray slots slot + j * cap, bit j of mMask / sMask)
-struct Pushes { bool c, m, s; uint32_t mMask, sMask; int sIdx; };   // sIdx: the shadow ray's ray slot (path)
+struct Pushes { bool c, m, s; uint32_t mMask, sMask; int sIdx, mIdx; };   // the shadow / MIS ray's ray slot (path)
 
 // Additions to L a vertex makes before its direct light is known, in order: emitted
 // radiance (path.cpp:67-68; bounce 0 or after a specular bounce) and the zero direct light
@@ -706,11 +706,14 @@ PGD_INLINE void estimate_direct(const DevScene &S, const PathSoA &P, int slot, i
                 eb.mode = Lt.is_black ? EM_BLACK : EM_POOL; eb.off = Lt.spec; eb.div = 1.f; eb.point = false;
             }
             const bool withB = go && !emit_black<NB, FEAT>(S, eb);
+            int rsM = rs;   // the MIS ray's record: without instances, at B's compacted entry
             if (mMask) {   // path integrator: B in the wave's compacted region (as A)
                 const unsigned long long m = __ballot(withB), act = __ballot(true);
                 const int lane = threadIdx.x & 63;
                 if (lane == __ffsll((long long)act) - 1) *mMask = m;
-                B += __popcll(m & ((1ull << lane) - 1ull));
+                const int rank = __popcll(m & ((1ull << lane) - 1ull));
+                B += rank;
+                if (!P.nInst) rsM = (slot & ~63) + rank;
             }
             if (withB) {
                 const float ad = fabsf(vdot(wi, n));
@@ -726,9 +729,10 @@ PGD_INLINE void estimate_direct(const DevScene &S, const PathSoA &P, int slot, i
                     B[q * c] = b;
                 }
                 if (!black) {
-                    ray_store(P, RAY_M, rs, mr);
+                    ray_store(P, RAY_M, rsM, mr);
                     fl |= PF_PB;
                     out.m = true;
+                    out.mIdx = rsM;
                 }
             }
         }
@@ -927,11 +931,12 @@ PGD_INLINE Pushes shade_slot(const DevScene &S, const PathSoA &P, int slot, floa
         useA = (fl & PF_PA) && !P.occ[P.nInst ? slot : (slot & ~63) + wave_rank(wm.a, slot)];
         if (fl & PF_PB) {
             const int ln = (int)(fl >> PF_LIGHT_SHIFT);
-            int mp = P.hitPrim[P.rcap + slot];
+            const int mi = P.nInst ? slot : (slot & ~63) + wave_rank(wm.b, slot);   // the MIS ray's record
+            int mp = P.hitPrim[P.rcap + mi];
             if ((FEAT & FEAT_INF) && S.lights[ln].type == PBRTGPU_LIGHT_INFINITE) useB = mp < 0;   // Li = light->Le(ray)
             else if (mp >= 0 && S.prims[mp].area_light == ln) {
-                Ray mr = ray_load(P, RAY_M, slot);
-                useB = vdot(isect_nn(S, mr, mp, P.hitT[P.rcap + slot], inst_rec(P, slot)), vneg(mr.d)) > 0.f;   // DiffuseAreaLight::L
+                Ray mr = ray_load(P, RAY_M, mi);
+                useB = vdot(isect_nn(S, mr, mp, P.hitT[P.rcap + mi], inst_rec(P, slot)), vneg(mr.d)) > 0.f;   // DiffuseAreaLight::L
             }
         }
         fl &= ~(PF_PEND | PF_PA | PF_PB);
