@@ -1226,16 +1226,9 @@ PGD_INLINE float bx_pdf(PowMemo &pm, const BxDF &b, V wo, V wi) {
         default: return samehemi(wo, wi) ? abscos(wi) * kInvPi : 0.f;
     }
 }
-// BxDF::Sample_f: direction + pdf; f as a one-term sum (or the specular spectrum)
-PGD_INLINE void bx_sample_f(PowMemo &pm, const BxDF &b, V wo, V *wi, float u1, float u2, float *pdf, FVal &F) {
-    fval_zero(F);
+// the specular BxDFs' Sample_f (reflection.cpp SpecularReflection / SpecularTransmission::Sample_f)
+PGD_INLINE void bx_sample_specular(const BxDF &b, V wo, V *wi, float *pdf, FVal &F) {
     switch (b.kind) {
-        case BX_MICRO_BLINN_DIEL:
-        case BX_MICRO_BLINN_COND:
-            blinn_sample(b.a, wo, wi, u1, u2, pdf);
-            if (!samehemi(wo, *wi)) return;
-            F.n = 1; F.t[0] = bx_term(pm, b, wo, *wi);
-            return;
         case BX_SPEC_REFL_NOOP:    // SpecularReflection with FresnelNoOp: Spectrum(1) * R / |cos|
         case BX_SPEC_REFL_DIEL:    // ... with FresnelDielectric(1, ior)
             *wi = v3(-wo.x, -wo.y, wo.z);
@@ -1260,6 +1253,24 @@ PGD_INLINE void bx_sample_f(PowMemo &pm, const BxDF &b, V wo, V *wi, float u1, f
             F.fs = 1.f - fr_dielectric(wo.z, 1.f, b.a);
             return;
         }
+        default: return;
+    }
+}
+// BxDF::Sample_f: direction + pdf; f as a one-term sum (or the specular spectrum)
+PGD_INLINE void bx_sample_f(PowMemo &pm, const BxDF &b, V wo, V *wi, float u1, float u2, float *pdf, FVal &F) {
+    fval_zero(F);
+    switch (b.kind) {
+        case BX_MICRO_BLINN_DIEL:
+        case BX_MICRO_BLINN_COND:
+            blinn_sample(b.a, wo, wi, u1, u2, pdf);
+            if (!samehemi(wo, *wi)) return;
+            F.n = 1; F.t[0] = bx_term(pm, b, wo, *wi);
+            return;
+        case BX_SPEC_REFL_NOOP:
+        case BX_SPEC_REFL_DIEL:
+        case BX_SPEC_TRANS:
+            bx_sample_specular(b, wo, wi, pdf, F);
+            return;
         case BX_FRESNEL_BLEND_ANISO:
             if (u1 < .5) {
                 u1 = 2.f * u1;
@@ -1361,6 +1372,30 @@ PGD_INLINE void bsdf_sample_f(PowMemo &pm, const BSDF &bs, V woW, V *wiW, float 
     BSDFSampleState st;
     if (bsdf_sample_dir(pm, bs, woW, wiW, u0, u1, uc, pdf, flags, sampledType, F, st))
         bsdf_sample_rest(pm, bs, woW, *wiW, st, pdf, flags, *sampledType, F);
+}
+// BSDF::Sample_f for flags that select specular BxDFs only (SpecularReflect / SpecularTransmit,
+// integrator.cpp:169-250): bsdf_sample_f's arithmetic for the components such flags can match
+// (the microfacet / diffuse cases compiled out).  pdf 0: nothing sampled (wi not set).
+PGD_INLINE void bsdf_sample_specular(const BSDF &bs, V woW, V *wiW, float uc, float *pdf, int flags, FVal &F) {
+    int matching = 0;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) if (k < bs.n && matches(bs.bx[k], flags)) ++matching;
+    fval_zero(F);
+    *pdf = 0.f;
+    if (matching == 0) return;
+    int which = (int)floorf(uc * matching);
+    if (which > matching - 1) which = matching - 1;
+    int sel = -1, count = which;
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+        if (sel < 0 && k < bs.n && matches(bs.bx[k], flags) && count-- == 0) sel = k;
+    const BxDF bx = sel == 0 ? bs.bx[0] : bs.bx[1];
+    const V wo = to_local(bs, woW);
+    V wi;
+    bx_sample_specular(bx, wo, &wi, pdf, F);
+    if (*pdf == 0.f) { fval_zero(F); return; }
+    *wiW = to_world(bs, wi);
+    if (matching > 1) *pdf /= matching;   // a specular sample adds no other pdfs (bsdf_sample_rest)
 }
 
 

@@ -168,15 +168,14 @@ PGD_INLINE void dl_add(const DevScene &S, const PathSoA &P, int slot, int d, int
 // DirectLighting slot states beside wavefront.h's PF_* (bits 10, 11 are free there)
 enum {
     PF_DLNEE = 1u << 10,   // the top vertex's next light-sample batch is due (k_dl_nee, this pass)
-    PF_DLS2 = 1u << 11,    // its light samples are done, its specular branches come next (k_shade)
+    PF_DLSPEC = 1u << 11,  // its light samples are done: its specular branches (k_dl_spec, this pass)
 };
 
 // the light-sample batches of a slot marked PF_DLNEE, run by k_dl_nee right after k_shade in
 // the same pass: the vertex, then batches [k, kEnd) until one queues a ray (PF_PEND: the next
-// k_shade adds it) or the last one is added (PF_DLS2).  Returns true if the slot is left without
-// a queued ray (PF_DLS2), so the pass must not count as the wavefront's last.
+// k_shade adds it) or the last one is added (PF_DLSPEC: k_dl_spec takes the slot next).
 template <int NB, int FEAT>
-PGD_INLINE bool dl_light_batches(const DevScene &S, const PathSoA &P, int slot, Pushes &out) {
+PGD_INLINE void dl_light_batches(const DevScene &S, const PathSoA &P, int slot, Pushes &out) {
     constexpr int NQ = Bands<NB>::NQ;
     const size_t c = P.cap;
     uint32_t fl = P.flags[slot] & ~PF_DLNEE;
@@ -187,7 +186,6 @@ PGD_INLINE bool dl_light_batches(const DevScene &S, const PathSoA &P, int slot, 
     int k = (int)P.dlk[slot];
     DLVertex vx;
     dl_vertex<NB, FEAT>(S, P, slot, d, vx);
-    bool idle = false;
     for (;;) {
         const int kEnd = min(k + P.dlBatch, K);
         uint32_t mA = 0u, mB = 0u;
@@ -220,17 +218,44 @@ PGD_INLINE bool dl_light_batches(const DevScene &S, const PathSoA &P, int slot, 
             dl_add<NB>(S, P, slot, d, kk, K, all, false, false, P.A + slot, P.B + slot);
         k = kEnd;
         if (k < K) continue;
-        fl |= PF_DLS2;
-        idle = true;
+        fl |= PF_DLSPEC;
         break;
     }
     P.dlk[slot] = (uint32_t)k;
     P.flags[slot] = fl;
-    return idle;
 }
 
-// k_shade body of the DirectLighting integrator for one slot (see the file comment).
-// Returns the ray requests; *done when the camera sample's radiance is in Lout.
+// L of frame d += (f * ((1 * Lr) + 0)) * |wi . n| / pdf: the completed child frame's radiance Lr
+// into its parent d (integrator.cpp:199-200, 243-244; f, |wi . n| and pdf kept with the frame)
+template <int NB>
+PGD_INLINE void dl_pop(const PathSoA &P, int d, int slot, const float4 (&Lr)[Bands<NB>::NQ]) {
+    constexpr int NQ = Bands<NB>::NQ;
+    const size_t c = P.cap;
+    float4 *Lv = dl_L<NB>(P, d, slot);
+    const float4 *Fo = dl_F<NB>(P, d, slot);
+    const float ad = P.fS[(size_t)2 * d * c + slot], pdf = P.fS[(size_t)(2 * d + 1) * c + slot];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+        float4 l = Lv[q * c];
+        const float4 f = Fo[q * c];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const float li = (1.f * cmp(Lr[q], i)) + 0.f;
+            cmp(l, i) += ((cmp(f, i) * li) * ad) / pdf;
+        }
+        Lv[q * c] = l;
+    }
+}
+
+// k_shade body of the DirectLighting integrator for one slot (see the file comment): the
+// answers of the last pass -- a light-sample batch's shadow / MIS rays (added in sample order),
+// or the camera / specular child ray (a hit pushes its frame, a miss pops straight into the
+// parent) -- then the slot is handed to this pass's k_dl_nee (PF_DLNEE: the next light-sample
+// batch) or k_dl_spec (PF_DLSPEC: the specular branches).  The specular branches and the
+// frame pops they lead to run in k_dl_spec, a kernel of their own: inlined here they raised this
+// step's register peak from 162 to ~330 VGPRs (559 spilled at 3 waves/SIMD).
+// Returns the ray requests (none: the step queues no rays); *done when the camera ray missed
+// and the sample's radiance is in Lout.
 template <int NB, int FEAT>
 PGD_INLINE Pushes shade_slot_dl(const DevScene &S, const PathSoA &P, int slot, float *__restrict__ Lout, bool *done,
                                 bool *zeroed) {
@@ -246,22 +271,13 @@ PGD_INLINE Pushes shade_slot_dl(const DevScene &S, const PathSoA &P, int slot, f
     const bool all = S.dlStrategy != PBRTGPU_DL_ONE;
     const int K = all ? S.dlK : 1;
     int k = (int)P.dlk[slot];
-    DLVertex vx;
-    bool have = false;   // vx holds the top frame's vertex
-    MT rng;
-    bool rngLoaded = false;
-    float4 Lr[NQ];       // radiance of a completed frame, handed to its parent (pop)
-    // stage: 1 light sample k of the top vertex, 2 its specular branches, 3 pop Lr
-    int stage;
+    bool spec;   // next: the specular branches (k_dl_spec), else a light-sample batch (k_dl_nee)
 #ifdef PGD_DL_TRACE_ITEM   // debugging aid: the step of one item per pass
     const bool trc = P.item[slot] == PGD_DL_TRACE_ITEM;
     if (trc) printf("[dl] slot %d d %d fl %x k %d K %d prim %d occ %u hitM %d\n", slot, d, fl, k, K, P.hitPrim[slot],
                     P.occ[slot], P.hitPrim[P.rcap + slot]);
 #endif
-    if (fl & PF_DLS2) {   // light samples done in k_dl_nee: the specular branches
-        fl &= ~PF_DLS2;
-        stage = 2;
-    } else if (fl & PF_PEND) {
+    if (fl & PF_PEND) {
         // ---- the answered batch of light samples [k, kEnd): ED = (0 [+ A]) [+ B] each
         // (EstimateDirect), added in sample order
         const uint32_t msk = P.dlMask[slot];
@@ -286,7 +302,7 @@ PGD_INLINE Pushes shade_slot_dl(const DevScene &S, const PathSoA &P, int slot, f
                        P.B + (size_t)jb * NQ * c + slot);
         }
         k = kEnd;
-        stage = k < K ? 1 : 2;
+        spec = k >= K;
     } else {
         // ---- the camera ray or a specular child ray was answered (PF_CONT)
         fl &= ~PF_CONT;
@@ -294,6 +310,7 @@ PGD_INLINE Pushes shade_slot_dl(const DevScene &S, const PathSoA &P, int slot, f
         const Ray ray = ray_load(P, RAY_C, slot);
         if (prim < 0) {
             // SamplerRenderer::Li (samplerrenderer.cpp:237-240): Li = sum of the lights' Le
+            float4 Lr[NQ];
 #pragma unroll
             for (int q = 0; q < NQ; ++q) Lr[q] = make_float4(0.f, 0.f, 0.f, 0.f);
             if ((FEAT & FEAT_INF) && S.nInf > 0)
@@ -306,8 +323,14 @@ PGD_INLINE Pushes shade_slot_dl(const DevScene &S, const PathSoA &P, int slot, f
                             Lr[q].x += v.x; Lr[q].y += v.y; Lr[q].z += v.z; Lr[q].w += v.w;
                         }
                     }
-            d = d + 1;   // the missing ray's frame, popped at once
-            stage = 3;
+            if (d < 0) {   // the camera ray: rayWeight * ((1 * L) + 0), guarded
+                *zeroed = path_output<NB>(S, Lr, Lout, P.item[slot], P.smp[slot]);
+                *done = true;
+                P.flags[slot] = fl;
+                return out;
+            }
+            dl_pop<NB>(P, d, slot, Lr);   // the missing child's frame, popped at once
+            spec = true;                  // the parent's remaining branches
         } else {
             // push frame d + 1: its incoming ray and hit; L = 0 + Le(wo)
             d = d + 1;
@@ -329,140 +352,142 @@ PGD_INLINE Pushes shade_slot_dl(const DevScene &S, const PathSoA &P, int slot, f
                 const float4 e = eo >= 0 ? ld4(sp + eo + 4 * q) : make_float4(0.f, 0.f, 0.f, 0.f);
                 Lv[q * c] = make_float4(0.f + e.x, 0.f + e.y, 0.f + e.z, 0.f + e.w);
             }
-            stage = nLights > 0 ? 1 : 2;
+            spec = nLights == 0;
         }
     }
+    fl |= spec ? PF_DLSPEC : PF_DLNEE;
+#ifdef PGD_DL_TRACE_ITEM
+    if (trc) printf("[dl]   -> d %d fl %x k %d\n", d, fl, k);
+#endif
+    P.bounce[slot] = d;
+    P.dlk[slot] = (uint32_t)k;
+    P.flags[slot] = fl;
+    return out;
+}
+
+// k_dl_spec body for a slot marked PF_DLSPEC: SpecularReflect, then SpecularTransmit
+// (integrator.cpp:169-250) of the top frame d -- each draws BSDFSample(rng) (3 MT19937 values,
+// in the reference's order: reflect, its whole subtree, transmit) and queues its child ray with
+// the ray differentials -- and, once a frame has no branch left, its pop into the parent and the
+// parent's remaining branches, down to the camera sample's output at depth 0.
+// Returns the ray requests; *done when the sample's radiance is in Lout.
+template <int NB, int FEAT>
+PGD_INLINE Pushes dl_spec_step(const DevScene &S, const PathSoA &P, int slot, float *__restrict__ Lout, bool *done,
+                               bool *zeroed) {
+    constexpr int NQ = Bands<NB>::NQ;
+    const size_t c = P.cap;
+    const float *sp = S.spectra;
+    uint32_t fl = P.flags[slot] & ~PF_DLSPEC;
+    int d = P.bounce[slot];
+    Pushes out = {false, false, false, 0u, 0u};
+    *done = false;
+    *zeroed = false;
+    MT rng;
+    bool rngLoaded = false;
     for (;;) {
-        if (stage == 1) {   // the next light-sample batch: k_dl_nee, later in this pass
-            fl |= PF_DLNEE;
+        // ---- the specular branches of frame d
+        uint32_t br = P.fBr[(size_t)d * c + slot];
+        bool spawned = false;
+        // only mirror and glass have specular BxDFs: elsewhere the two BSDFSample(rng) draws
+        // still happen (the reference constructs them) but no child can be sampled, and the
+        // vertex need not be rebuilt
+        const int vprim = P.fHit[(size_t)2 * d * c + slot];
+        const int vtype = S.mats[S.prims[vprim].material].type;
+        const bool canSpec = vtype == PBRTGPU_MAT_MIRROR || vtype == PBRTGPU_MAT_GLASS;
+        while (d + 1 < S.maxDepth && br < 2u) {
+            if (!rngLoaded) {
+                mt_load(P, slot, fl, rng);
+                if (!rng.init) mt_init(rng);
+                rngLoaded = true;
+            }
+            const float u0 = mt_float(rng), u1 = mt_float(rng), uc = mt_float(rng);   // BSDFSample(rng)
+            const bool refl = br == 0u;
+            ++br;
+            if (!canSpec) continue;
+            DLVertex vx;
+            dl_vertex<NB, FEAT>(S, P, slot, d, vx);
+            const int flags = BSDF_SPECULAR | (refl ? BSDF_REFLECTION : BSDF_TRANSMISSION);
+            FVal F;
+            V wi;
+            float pdf;
+            (void)u0; (void)u1;   // the specular BxDFs ignore the two direction values
+            bsdf_sample_specular(vx.bs, vx.wo, &wi, uc, &pdf, flags, F);
+            if (!(pdf > 0.f)) continue;   // no matching BxDF: wi is not set
+            const float ad = fabsf(vdot(wi, vx.n));
+            if (ad == 0.f || (F.mode == FV_SUM && F.n == 0)) continue;
+            float4 *mb = P.M + slot, *kb = P.K + slot;
+            fval_prepare<NB, FEAT>(S, F, mb, c);
+            float4 *Fo = dl_F<NB>(P, d, slot);
+            bool black = true;
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                const float4 f = fval4<FEAT>(sp, F, q, mb, kb, c);
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    if (4 * q + i < NB) black = black && (cmp(f, i) == 0.);
+                Fo[q * c] = f;
+            }
+            if (black) continue;
+            P.fS[(size_t)2 * d * c + slot] = ad;
+            P.fS[(size_t)(2 * d + 1) * c + slot] = pdf;
+            // the child ray and its differentials (the camera's rays always carry them)
+            Ray cr;
+            cr.o = vx.p; cr.d = wi; cr.mint = vx.is.rayEps; cr.maxt = INFINITY; cr.time = vx.ray.time;
+            ray_store(P, RAY_C, slot, cr);
+            const V n = vx.n, wo = vx.wo;
+            const V rxo = vadd(vx.p, vx.dpdx), ryo = vadd(vx.p, vx.dpdy);
+            const V dndx = vadd(vmul(vx.dn[0], vx.diff[0]), vmul(vx.dn[1], vx.diff[1]));
+            const V dndy = vadd(vmul(vx.dn[0], vx.diff[2]), vmul(vx.dn[1], vx.diff[3]));
+            const V dwodx = vsub(vneg(vx.rd.rxd), wo), dwody = vsub(vneg(vx.rd.ryd), wo);
+            const float dDNdx = vdot(dwodx, n) + vdot(wo, dndx);
+            const float dDNdy = vdot(dwody, n) + vdot(wo, dndy);
+            V rxd, ryd;
+            if (refl) {
+                const float won = vdot(wo, n);
+                rxd = vadd(vsub(wi, dwodx), vmul(vadd(vmul(dndx, won), vmul(n, dDNdx)), 2.f));
+                ryd = vadd(vsub(wi, dwody), vmul(vadd(vmul(dndy, won), vmul(n, dDNdy)), 2.f));
+            } else {
+                // BSDF::eta: the glass material's index, 1 otherwise (glass.cpp:48)
+                const pbrtgpu_material &mt = S.mats[S.prims[vx.is.prim].material];
+                float eta = mt.type == PBRTGPU_MAT_GLASS ? mt.f[0] : 1.f;
+                const V w = vneg(wo);
+                if (vdot(wo, n) < 0) eta = 1.f / eta;
+                const float mu = eta * vdot(w, n) - vdot(wi, n);
+                const float dmudx = (eta - (eta * eta * vdot(w, n)) / vdot(wi, n)) * dDNdx;
+                const float dmudy = (eta - (eta * eta * vdot(w, n)) / vdot(wi, n)) * dDNdy;
+                rxd = vsub(vadd(wi, vmul(dwodx, eta)), vadd(vmul(dndx, mu), vmul(n, dmudx)));
+                ryd = vsub(vadd(wi, vmul(dwody, eta)), vadd(vmul(dndy, mu), vmul(n, dmudy)));
+            }
+            float *fd = P.fDiff + (size_t)(d + 1) * 12 * c + slot;
+            dl_vec_store(fd, c, rxo);
+            dl_vec_store(fd + 3 * c, c, rxd);
+            dl_vec_store(fd + 6 * c, c, ryo);
+            dl_vec_store(fd + 9 * c, c, ryd);
+            fl |= PF_CONT;
+            out.c = true;
+            spawned = true;
             break;
         }
-        if (stage == 2) {
-            // ---- SpecularReflect, then SpecularTransmit (integrator.cpp:169-250)
-            uint32_t br = P.fBr[(size_t)d * c + slot];
-            bool spawned = false;
-            // only mirror and glass have specular BxDFs: elsewhere the two BSDFSample(rng) draws
-            // still happen (the reference constructs them) but no child can be sampled, and the
-            // vertex need not be rebuilt
-            const int vprim = P.fHit[(size_t)2 * d * c + slot];
-            const int vtype = S.mats[S.prims[vprim].material].type;
-            const bool canSpec = vtype == PBRTGPU_MAT_MIRROR || vtype == PBRTGPU_MAT_GLASS;
-            while (d + 1 < S.maxDepth && br < 2u) {
-                if (!rngLoaded) {
-                    mt_load(P, slot, fl, rng);
-                    if (!rng.init) mt_init(rng);
-                    rngLoaded = true;
-                }
-                const float u0 = mt_float(rng), u1 = mt_float(rng), uc = mt_float(rng);   // BSDFSample(rng)
-                const bool refl = br == 0u;
-                ++br;
-                if (!canSpec) continue;
-                if (!have) { dl_vertex<NB, FEAT>(S, P, slot, d, vx); have = true; }
-                const int flags = BSDF_SPECULAR | (refl ? BSDF_REFLECTION : BSDF_TRANSMISSION);
-                PowMemo pm;
-                FVal F;
-                V wi;
-                float pdf;
-                int st;
-                bsdf_sample_f(pm, vx.bs, vx.wo, &wi, u0, u1, uc, &pdf, flags, &st, F);
-                const float ad = fabsf(vdot(wi, vx.n));
-                if (!(pdf > 0.f) || ad == 0.f || (F.mode == FV_SUM && F.n == 0)) continue;
-                float4 *mb = P.M + slot, *kb = P.K + slot;
-                fval_prepare<NB, FEAT>(S, F, mb, c);
-                float4 *Fo = dl_F<NB>(P, d, slot);
-                bool black = true;
+        P.fBr[(size_t)d * c + slot] = br;
+        if (spawned) break;
+        // ---- frame d is complete: Li = (1 * L) + 0 goes to its parent, or is the sample's
+        float4 Lr[NQ];
+        const float4 *Lv = dl_L<NB>(P, d, slot);
 #pragma unroll
-                for (int q = 0; q < NQ; ++q) {
-                    const float4 f = fval4<FEAT>(sp, F, q, mb, kb, c);
-#pragma unroll
-                    for (int i = 0; i < 4; ++i)
-                        if (4 * q + i < NB) black = black && (cmp(f, i) == 0.);
-                    Fo[q * c] = f;
-                }
-                if (black) continue;
-                P.fS[(size_t)2 * d * c + slot] = ad;
-                P.fS[(size_t)(2 * d + 1) * c + slot] = pdf;
-                // the child ray and its differentials (the camera's rays always carry them)
-                Ray cr;
-                cr.o = vx.p; cr.d = wi; cr.mint = vx.is.rayEps; cr.maxt = INFINITY; cr.time = vx.ray.time;
-                ray_store(P, RAY_C, slot, cr);
-                const V n = vx.n, wo = vx.wo;
-                const V rxo = vadd(vx.p, vx.dpdx), ryo = vadd(vx.p, vx.dpdy);
-                const V dndx = vadd(vmul(vx.dn[0], vx.diff[0]), vmul(vx.dn[1], vx.diff[1]));
-                const V dndy = vadd(vmul(vx.dn[0], vx.diff[2]), vmul(vx.dn[1], vx.diff[3]));
-                const V dwodx = vsub(vneg(vx.rd.rxd), wo), dwody = vsub(vneg(vx.rd.ryd), wo);
-                const float dDNdx = vdot(dwodx, n) + vdot(wo, dndx);
-                const float dDNdy = vdot(dwody, n) + vdot(wo, dndy);
-                V rxd, ryd;
-                if (refl) {
-                    const float won = vdot(wo, n);
-                    rxd = vadd(vsub(wi, dwodx), vmul(vadd(vmul(dndx, won), vmul(n, dDNdx)), 2.f));
-                    ryd = vadd(vsub(wi, dwody), vmul(vadd(vmul(dndy, won), vmul(n, dDNdy)), 2.f));
-                } else {
-                    // BSDF::eta: the glass material's index, 1 otherwise (glass.cpp:48)
-                    const pbrtgpu_material &mt = S.mats[S.prims[vx.is.prim].material];
-                    float eta = mt.type == PBRTGPU_MAT_GLASS ? mt.f[0] : 1.f;
-                    const V w = vneg(wo);
-                    if (vdot(wo, n) < 0) eta = 1.f / eta;
-                    const float mu = eta * vdot(w, n) - vdot(wi, n);
-                    const float dmudx = (eta - (eta * eta * vdot(w, n)) / vdot(wi, n)) * dDNdx;
-                    const float dmudy = (eta - (eta * eta * vdot(w, n)) / vdot(wi, n)) * dDNdy;
-                    rxd = vsub(vadd(wi, vmul(dwodx, eta)), vadd(vmul(dndx, mu), vmul(n, dmudx)));
-                    ryd = vsub(vadd(wi, vmul(dwody, eta)), vadd(vmul(dndy, mu), vmul(n, dmudy)));
-                }
-                float *fd = P.fDiff + (size_t)(d + 1) * 12 * c + slot;
-                dl_vec_store(fd, c, rxo);
-                dl_vec_store(fd + 3 * c, c, rxd);
-                dl_vec_store(fd + 6 * c, c, ryo);
-                dl_vec_store(fd + 9 * c, c, ryd);
-                fl |= PF_CONT;
-                out.c = true;
-                spawned = true;
-                break;
-            }
-            P.fBr[(size_t)d * c + slot] = br;
-            if (spawned) break;
-            // the frame is complete: Li = (1 * L) + 0 goes to the parent
-            const float4 *Lv = dl_L<NB>(P, d, slot);
-#pragma unroll
-            for (int q = 0; q < NQ; ++q) Lr[q] = Lv[q * c];
-            stage = 3;
-        }
-        // ---- pop frame d with raw radiance Lr
+        for (int q = 0; q < NQ; ++q) Lr[q] = Lv[q * c];
         if (d == 0) {
             *zeroed = path_output<NB>(S, Lr, Lout, P.item[slot], P.smp[slot]);   // rayWeight * ((1 * L) + 0), guarded
             *done = true;
             break;
         }
         --d;
-        have = false;
-        {
-            float4 *Lv = dl_L<NB>(P, d, slot);
-            const float4 *Fo = dl_F<NB>(P, d, slot);
-            const float ad = P.fS[(size_t)2 * d * c + slot], pdf = P.fS[(size_t)(2 * d + 1) * c + slot];
-#pragma unroll
-            for (int q = 0; q < NQ; ++q) {
-                float4 l = Lv[q * c];
-                const float4 f = Fo[q * c];
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const float li = (1.f * cmp(Lr[q], i)) + 0.f;
-                    cmp(l, i) += ((cmp(f, i) * li) * ad) / pdf;
-                }
-                Lv[q * c] = l;
-            }
-        }
-        stage = 2;
+        dl_pop<NB>(P, d, slot, Lr);
     }
     if (rngLoaded) {
         mt_store(P, slot, rng);
         if (rng.init) fl |= PF_MTINIT;
     }
-#ifdef PGD_DL_TRACE_ITEM
-    if (trc) printf("[dl]   -> d %d fl %x k %d push %d%d%d done %d\n", d, fl, k, out.c, out.m, out.s, *done);
-#endif
     P.bounce[slot] = d;
-    P.dlk[slot] = (uint32_t)k;
     P.flags[slot] = fl;
     return out;
 }

@@ -27,6 +27,7 @@
 #include "pbrtgpu.h"
 #include "device.h"
 #include "wavefront.h"
+#include "scene_build.h"
 
 using namespace pgd;
 #ifdef PGD_SECTIONS
@@ -776,6 +777,13 @@ static bool serial_mode() {
     const char *e = getenv("PBRTGPU_SERIAL");
     return e && atoi(e) != 0;
 }
+// PBRTGPU_POISON=<byte> (debugging / tests): every path-slot array and the traversal stack spill
+// area are filled with that byte before each wavefront run, so a read of state no pass wrote
+// gives a result that changes with the byte; -1 (unset): left as they are
+static int poison_byte() {
+    const char *e = getenv("PBRTGPU_POISON");
+    return e && *e ? (int)(strtol(e, nullptr, 0) & 0xff) : -1;
+}
 
 // DirectLighting frame bytes per slot and frame (PathSoA::f*)
 static size_t frame_bytes(int NB) { return (size_t)8 * ((NB + 3) / 4 * 4) + 104; }
@@ -879,7 +887,8 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
                   : c->S.integrator == PBRTGPU_INTEGRATOR_METADATA ? launch_shade_meta<NB>
                   : c->feat ? launch_shade<NB, FEAT_ALL> : launch_shade<NB, 0>;
     const int nFrames = dl ? std::max(1, c->S.maxDepth) : 0;
-    auto kNee = c->feat ? launch_dl_nee<NB> : launch_dl_nee<NB>;
+    auto kNee = launch_dl_nee<NB>;
+    auto kSpec = launch_dl_spec<NB>;
     // DirectLighting issues up to kDlBatch light samples of a vertex per pass
     const int batch = dl ? std::max(1, std::min(c->S.dlStrategy == PBRTGPU_DL_ONE ? 1 : c->S.dlK, kDlBatch)) : 1;
     // passes one path can take: the camera ray + maxdepth + 1 vertices + 1 finish (path); per
@@ -916,8 +925,19 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
         if (int e = ensure_slots(&L, r.cap, NB, c->S.nInsts, nFrames, batch)) return e;
         HIPCHK(L.spill.ensure(2 * spillLane * sizeof(uint2)));
         if (l > 0) HIPCHK(hipStreamWaitEvent(L.s, c->ev[0], 0));
+        if (const int pb = poison_byte(); pb >= 0) {
+            HIPCHK(hipMemsetAsync(L.slots.p, pb, L.slots.n, L.s));
+            HIPCHK(hipMemsetAsync(L.spill.p, pb, L.spill.n, L.s));
+        }
         HIPCHK(hipMemsetAsync(L.P.item, 0xff, (size_t)r.cap * 4, L.s));
         HIPCHK(hipMemsetAsync(L.P.cnt, 0, CNT_WORDS * 4, L.s));
+        {   // the per-wave writer masks start empty: k_shade loads a wave's masks before it knows
+            // which of them its lanes will use (wave_masks), so none is read unwritten
+            const size_t W = (size_t)((r.cap + 63) / 64) * 8;
+            HIPCHK(hipMemsetAsync(L.P.aMask, 0, 2 * W, L.s));
+            HIPCHK(hipMemsetAsync(L.P.bMask, 0, 3 * W, L.s));
+            HIPCHK(hipMemsetAsync(L.P.mMask, 0, 2 * W, L.s));
+        }
         // pass 0: every slot is free -> regeneration fills them with camera rays (queue 0)
         HIPCHK(hipEventRecord(L.ev[0], L.s));
         L.P.pass = 0;   // k_shade pass index (mod 3) of this run: the beta buffers rotate with it
@@ -994,7 +1014,7 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
                     HIPCHK(hipEventRecord(e[4], L.s));
                     L.P.pass = (L.P.pass + 1) % 3;
                     HIPCHK(kShade(r.grid, L.s, c->S, P, r.src, nq, Lout));
-                    if (dl) HIPCHK(kNee(r.grid, L.s, c->S, P, nq));
+                    if (dl) { HIPCHK(kNee(r.grid, L.s, c->S, P, nq)); HIPCHK(kSpec(r.grid, L.s, c->S, P, nq, Lout)); }
                     T.launches[K_SHADE]++;
                     HIPCHK(hipEventRecord(e[5], L.s));
                     T.passes++;
@@ -1035,7 +1055,7 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
                 HIPCHK(hipEventRecord(e[4], L.s));
                 L.P.pass = (L.P.pass + 1) % 3;
                 HIPCHK(kShade(r.grid, L.s, c->S, P, r.src, nq, Lout));
-                if (dl) HIPCHK(kNee(r.grid, L.s, c->S, P, nq));
+                if (dl) { HIPCHK(kNee(r.grid, L.s, c->S, P, nq)); HIPCHK(kSpec(r.grid, L.s, c->S, P, nq, Lout)); }
                 T.launches[K_SHADE]++;
                 HIPCHK(hipEventRecord(e[5], L.s));
                 T.passes++;
@@ -1058,92 +1078,6 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
     return 0;
 }
 
-// Child-in-parent copy of the flattened BVH (LinearBVHNode, bvh.cpp:105-115) for
-// bvh_walk: wide node k of interior node i = {left box lo, ref(left)} {left box hi,
-// ref(right)} {right box lo, axis} {right box hi, 0}, with left = i + 1 and right =
-// secondChildOffset as in the reference's depth-first layout.  ref[] maps every node to its
-// reference (wide index or WREF_LEAF record); the roots of the top-level and instance BVHs
-// are looked up there.
-static float bits_f(uint32_t u) { float f; memcpy(&f, &u, 4); return f; }
-// Wide indices: the first `top` interior nodes of the top-level BVH in breadth-first order
-// (the top levels, which k_trace_pt keeps in LDS), then every other interior node in the
-// reference's depth-first order.  Indices only name nodes: the traversal order is the same.
-static int wide_bvh(const pbrtgpu_flat_scene *s, int top, std::vector<float4> *wn, std::vector<uint32_t> *ref,
-                    int *nTopOut) {
-    const int n = s->n_nodes;
-    ref->assign(n, 0xffffffffu);
-    uint32_t nw = 0;
-    if (top > 0 && n > 0 && !(s->nodes[0].meta & 0xff)) {
-        std::vector<int> bfs(1, 0);
-        for (size_t h = 0; h < bfs.size() && (int)nw < top; ++h) {
-            const int i = bfs[h];
-            const pbrtgpu_bvh_node &b = s->nodes[i];
-            if (b.meta & 0xff) continue;
-            (*ref)[i] = nw++;
-            if (i + 1 < n) bfs.push_back(i + 1);
-            if (b.offset < (uint32_t)n) bfs.push_back((int)b.offset);
-        }
-    }
-    *nTopOut = (int)nw;
-    for (int i = 0; i < n; ++i) {
-        const pbrtgpu_bvh_node &b = s->nodes[i];
-        const uint32_t np = b.meta & 0xff;
-        if (np == 0) { if ((*ref)[i] == 0xffffffffu) (*ref)[i] = nw++; }
-        else {
-            if (np > WREF_NP_MASK || b.offset > WREF_OFF_MASK)
-                return fail(PBRTGPU_E_UNSUPPORTED, "BVH leaf beyond the 2^24-primitive reference range");
-            (*ref)[i] = WREF_LEAF | (np << WREF_NP_SHIFT) | b.offset;
-        }
-    }
-    if (nw >= WREF_LEAF) return fail(PBRTGPU_E_UNSUPPORTED, "BVH too large");
-    wn->assign((size_t)nw * 4, make_float4(0.f, 0.f, 0.f, 0.f));
-    for (int i = 0; i < n; ++i) {
-        const pbrtgpu_bvh_node &b = s->nodes[i];
-        if (b.meta & 0xff) continue;
-        const uint32_t L = (uint32_t)i + 1, R = b.offset;
-        if (L >= (uint32_t)n || R >= (uint32_t)n) return fail(PBRTGPU_E_INVALID, "BVH child out of range");
-        const pbrtgpu_bvh_node &l = s->nodes[L], &r = s->nodes[R];
-        float4 *w = wn->data() + (size_t)(*ref)[i] * 4;
-        w[0] = make_float4(l.bmin[0], l.bmin[1], l.bmin[2], bits_f((*ref)[L]));
-        w[1] = make_float4(l.bmax[0], l.bmax[1], l.bmax[2], bits_f((*ref)[R]));
-        w[2] = make_float4(r.bmin[0], r.bmin[1], r.bmin[2], bits_f((b.meta >> 8) & 0xff));
-        w[3] = make_float4(r.bmax[0], r.bmax[1], r.bmax[2], 0.f);
-        if (((b.meta >> 8) & 0xff) > 2) return fail(PBRTGPU_E_INVALID, "BVH split axis");
-    }
-    return 0;
-}
-
-// SpectralRendererTask::Run's wave bands (spectralrenderer.cpp:99-100, 124, 180-188) in the
-// reference's own int / float arithmetic (sampledLambdaStart 395, sampledLambdaEnd 715 are
-// ints, spectrum.h:41-42): band b's wavelength 395 + dW b + dW / 2 with dW = float(320 / nWB),
-// its interval i of GetValueAtWavelength (spectrum.h:384-405: step float(320 / N), first i with
-// w0 <= wl < w1) and t = (wl - w0) / (w1 - w0), and its indices [dI b, min(dI (b+1), N-1)),
-// dI = round(N / nWB).  A band with indices whose interval is the last reads c[N], past the
-// spectrum: rejected.
-static int spectral_table(int N, int nWB, std::vector<int4> *tab, std::vector<float> *wls) {
-    const int lStart = 395, lEnd = 715;
-    const int dI = (int)round(N / nWB);
-    const float dW = (float)((lEnd - lStart) / nWB);
-    const float step = (float)((lEnd - lStart) / N);
-    tab->resize(nWB);
-    wls->resize(nWB);
-    for (int b = 0; b < nWB; ++b) {
-        const float wl = lStart + dW * b + (dW / 2);
-        (*wls)[b] = wl;
-        int iv = -1;
-        float t = 0.f;
-        for (int i = 0; i < N; ++i) {
-            const float w0 = lStart + i * step, w1 = lStart + (i + 1) * step;
-            if (wl >= w0 && wl < w1) { iv = i; t = (wl - w0) / (w1 - w0); break; }
-        }
-        const int lo = dI * b, hi = std::max(lo, std::min(dI * (b + 1), N - 1));
-        if (hi > lo && iv == N - 1) return fail(PBRTGPU_E_UNSUPPORTED, "nWaveBands: a band reads past the spectrum (spectrum.h:397)");
-        uint32_t tb;
-        memcpy(&tb, &t, 4);
-        (*tab)[b] = make_int4(lo, hi, iv, (int)tb);
-    }
-    return 0;
-}
 
 extern "C" {
 
@@ -1215,97 +1149,8 @@ int pbrtgpu_context_destroy(pbrtgpu_ctx *c) {
 }
 int pbrtgpu_scene_upload(pbrtgpu_ctx *c, const pbrtgpu_flat_scene *s) {
     if (!c || !s) return fail(PBRTGPU_E_INVALID, "null argument");
-    if (s->abi_version != PBRTGPU_ABI_VERSION) return fail(PBRTGPU_E_INVALID, "ABI version mismatch");
-    if (!(s->n_bands == 32 || s->n_bands == 60 || s->n_bands == 30 || s->n_bands == 3))
-        return fail(PBRTGPU_E_UNSUPPORTED, "n_bands must be 30, 32, 60 or 3 (RGB)");
-    // the RGB build (C1): image textures, the environment light and MERL tables convert RGB with
-    // SampledSpectrum::FromRGB's basis on the device; the host front end refuses them there
-    if (s->n_bands == 3 && (s->n_textures > 0 || s->n_merl_floats > 0))
-        for (int i = 0; i < s->n_textures; ++i)
-            if (s->textures[i].type == PBRTGPU_TEX_IMAGE) return fail(PBRTGPU_E_UNSUPPORTED, "RGB build: image textures");
-    if (s->n_bands == 3 && s->n_merl_floats > 0) return fail(PBRTGPU_E_UNSUPPORTED, "RGB build: MERL BRDFs");
-    if (s->n_bands == 3)
-        for (int i = 0; i < s->n_lights; ++i)
-            if (s->lights[i].type == PBRTGPU_LIGHT_INFINITE) return fail(PBRTGPU_E_UNSUPPORTED, "RGB build: infinite lights");
-    if (s->n_bands == 3 && s->renderer == PBRTGPU_RENDERER_SPECTRAL)
-        return fail(PBRTGPU_E_UNSUPPORTED, "RGB build: the SpectralRenderer needs SampledSpectrum");
-    if (s->spp <= 0 || (s->spp & (s->spp - 1))) return fail(PBRTGPU_E_INVALID, "spp must be a power of two");
-    if (s->max_depth < 0 || s->max_depth > 20)
-        return fail(PBRTGPU_E_UNSUPPORTED, "maxdepth > 20 exceeds the first MT19937 block (DESIGN.md §3.1)");
-    if (s->n_nodes <= 0 || s->n_prims <= 0) return fail(PBRTGPU_E_INVALID, "empty scene");
-    if (s->integrator != PBRTGPU_INTEGRATOR_PATH && s->integrator != PBRTGPU_INTEGRATOR_DIRECT &&
-        s->integrator != PBRTGPU_INTEGRATOR_METADATA)
-        return fail(PBRTGPU_E_INVALID, "unknown SurfaceIntegrator");
-    if (s->integrator == PBRTGPU_INTEGRATOR_METADATA) {
-        if (s->meta_strategy < PBRTGPU_META_MESH || s->meta_strategy > PBRTGPU_META_DEPTH)
-            return fail(PBRTGPU_E_INVALID, "unknown metadata strategy");
-        if (s->meta_strategy != PBRTGPU_META_DEPTH && !s->prim_meta)
-            return fail(PBRTGPU_E_INVALID, "metadata mesh / material ids need prim_meta");
-    }
-    if (s->renderer != PBRTGPU_RENDERER_SAMPLER && s->renderer != PBRTGPU_RENDERER_SPECTRAL)
-        return fail(PBRTGPU_E_INVALID, "unknown Renderer");
-    std::vector<int4> specTab;
-    std::vector<float> specWl;
-    if (s->renderer == PBRTGPU_RENDERER_SPECTRAL) {
-        if (s->spectral_sampling != PBRTGPU_SPECTRAL_SINGLE && s->spectral_sampling != PBRTGPU_SPECTRAL_SAMPLER)
-            return fail(PBRTGPU_E_INVALID, "unknown spectral sampling method");
-        if (s->wave_bands < 1 || s->wave_bands > 1024) return fail(PBRTGPU_E_INVALID, "nWaveBands must be 1..1024");
-        if (int e = spectral_table(s->n_bands, s->wave_bands, &specTab, &specWl)) return e;
-    }
-    if (s->camera_type != PBRTGPU_CAMERA_PERSPECTIVE && s->camera_type != PBRTGPU_CAMERA_REALISTIC)
-        return fail(PBRTGPU_E_INVALID, "unknown camera type");
-    if (s->camera_type == PBRTGPU_CAMERA_REALISTIC) {
-        const pbrtgpu_lens &L = s->lens;
-        if (L.n_elements < 1 || L.n_elements > 4096 || !L.elements) return fail(PBRTGPU_E_INVALID, "lens camera without elements");
-        // element 1 refracting into element 0 of n == 0 would read lensEls[-1] (realisticDiffraction.cpp:960-966)
-        if (L.n_elements >= 2 && L.elements[2] == 0 && L.elements[4] != 0)
-            return fail(PBRTGPU_E_INVALID, "lens element 0 has n == 0");
-        if (s->camera.xres <= 0 || s->camera.yres <= 0) return fail(PBRTGPU_E_INVALID, "lens camera without film resolution");
-    }
-    if (s->integrator == PBRTGPU_INTEGRATOR_DIRECT && s->dl_strategy != PBRTGPU_DL_ALL && s->dl_strategy != PBRTGPU_DL_ONE)
-        return fail(PBRTGPU_E_INVALID, "unknown DirectLighting strategy");
-    // DirectLighting draws 6 MT19937 values at each of up to 2^(maxdepth-1) - 1 specular
-    // vertices; the device stream covers the first 227
-    if (s->integrator == PBRTGPU_INTEGRATOR_DIRECT && s->max_depth > 6)
-        return fail(PBRTGPU_E_UNSUPPORTED, "DirectLighting maxdepth > 6 exceeds the first MT19937 block");
-    for (int i = 0; i < s->n_lights; ++i)
-        if (s->lights[i].type < PBRTGPU_LIGHT_AREA || s->lights[i].type > PBRTGPU_LIGHT_INFINITE)
-            return fail(PBRTGPU_E_INVALID, "bad light type");
-    if (!s->rgb_basis || !s->ewa_lut) return fail(PBRTGPU_E_INVALID, "rgb_basis / ewa_lut missing");
-    // texture graph: SCALE nodes combine CONST / IMAGE leaves; a material's spectrum slot is an
-    // IMAGE or SCALE(IMAGE, CONST) spectrum texture, its bump a float texture
-    auto texOk = [&](int id, int spectral, bool slot) -> bool {
-        if (id < 0 || id >= s->n_textures || !s->textures) return false;
-        const pbrtgpu_texture &t = s->textures[id];
-        if (t.spectral != spectral || t.type < PBRTGPU_TEX_CONST || t.type > PBRTGPU_TEX_SCALE) return false;
-        if (t.type == PBRTGPU_TEX_SCALE) {
-            for (int o : {t.tex1, t.tex2}) {
-                if (o < 0 || o >= s->n_textures || s->textures[o].spectral != spectral) return false;
-                if (s->textures[o].type == PBRTGPU_TEX_SCALE) return false;
-            }
-            if (spectral && (s->textures[t.tex1].type == PBRTGPU_TEX_CONST) == (s->textures[t.tex2].type == PBRTGPU_TEX_CONST))
-                return false;
-        }
-        return !(slot && spectral && t.type == PBRTGPU_TEX_CONST);
-    };
-    for (int i = 0; i < s->n_materials; ++i) {
-        const pbrtgpu_material &m = s->materials[i];
-        if (m.type < PBRTGPU_MAT_MATTE || m.type > PBRTGPU_MAT_MEASURED_HALFANGLE)
-            return fail(PBRTGPU_E_UNSUPPORTED, "material type not yet supported on the GPU");
-        int nt = 0;
-        for (int k = 0; k < 4; ++k)
-            if (m.tex[k] >= 0) {
-                ++nt;
-                if (!texOk(m.tex[k], 1, true) || m.type == PBRTGPU_MAT_METAL || m.type == PBRTGPU_MAT_MEASURED ||
-                    m.type == PBRTGPU_MAT_MEASURED_HALFANGLE)
-                    return fail(PBRTGPU_E_UNSUPPORTED, "material spectrum texture");
-            }
-        if (nt > 1) return fail(PBRTGPU_E_UNSUPPORTED, "more than one textured spectrum per material");
-        if (m.bump_tex >= 0 && !texOk(m.bump_tex, 0, false)) return fail(PBRTGPU_E_INVALID, "bump texture");
-        if (m.type == PBRTGPU_MAT_MEASURED_HALFANGLE && m.aux >= 0 &&
-            (!s->merl || s->n_merl_floats < 0 || (int64_t)m.aux * 3 + 3 * 90 * 90 * 180 > (int64_t)s->n_merl_floats))
-            return fail(PBRTGPU_E_INVALID, "RegularHalfangle table out of range");
-    }
+    std::string err;
+    if (int e = scene_check(s, &err)) return fail(e, err);
     HIPCHK(hipSetDevice(c->device));
     HIPCHK(hipStreamSynchronize(c->stream));
     c->hasScene = false;
@@ -1313,223 +1158,18 @@ int pbrtgpu_scene_upload(pbrtgpu_ctx *c, const pbrtgpu_flat_scene *s) {
     c->sceneBufs.clear();
     c->sceneBufs.reserve(64);
     DevScene &S = c->S;
-    S.nb = s->n_bands;
-    S.maxDepth = s->max_depth;
-    S.spp = s->spp;
-    S.seed = s->seed;
-    S.yint = s->y_int;
-    S.cam = s->camera;
-    S.nLights = s->n_lights;
-    S.integrator = s->integrator;
-    S.dlStrategy = s->dl_strategy;
-    S.metaStrategy = s->meta_strategy;
-    S.primMeta = nullptr;
-    if (s->prim_meta) HIPCHK(upload(c, s->prim_meta, (size_t)2 * s->n_prims, &S.primMeta));
-    S.specMode = s->renderer != PBRTGPU_RENDERER_SPECTRAL ? 0 : s->spectral_sampling == PBRTGPU_SPECTRAL_SINGLE ? 1 : 2;
-    S.specBands = S.specMode ? s->wave_bands : 1;
-    S.specItems = S.specMode == 1 ? s->wave_bands : 1;
-    S.specTab = nullptr;
-    S.specWl = nullptr;
-    if (S.specMode) {
-        HIPCHK(upload(c, specTab.data(), specTab.size(), &S.specTab));
-        HIPCHK(upload(c, specWl.data(), specWl.size(), &S.specWl));
-    }
-    S.camType = s->camera_type;
-    S.lensN = 0;
-    S.lensEl = nullptr;
-    if (S.camType == PBRTGPU_CAMERA_REALISTIC) {
-        const pbrtgpu_lens &L = s->lens;
-        S.lensN = L.n_elements;
-        S.lensChromatic = L.chromatic;
-        S.lensFilmDist = L.film_distance;
-        S.lensFilmDiag = L.film_diag;
-        S.lensCurveR = L.curve_radius;
-        for (int k = 0; k < 2; ++k) { S.lensApOff[k] = L.aperture_offset[k]; S.lensFilmC[k] = L.film_center[k]; }
-        for (int k = 0; k < 3; ++k) S.lensPinhole[k] = L.pinhole_exit[k];
-        HIPCHK(upload(c, reinterpret_cast<const float4 *>(L.elements), (size_t)L.n_elements, &S.lensEl));
-    }
-    S.dlK = 0;
-    for (int i = 0; i < s->n_lights; ++i) {   // RoundUpPow2(max(1, nSamples)) per light
-        uint32_t v = (uint32_t)std::max(1, s->lights[i].n_samples) - 1u;
-        v |= v >> 1; v |= v >> 2; v |= v >> 4; v |= v >> 8; v |= v >> 16;
-        if (v + 1u > (1u << 16)) return fail(PBRTGPU_E_UNSUPPORTED, "light nsamples > 65536");
-        S.dlK += (int)(v + 1u);
-    }
-    // BVH: verify topology and measure the stack depth traversal needs (top level, plus the
-    // deepest nested instance BVH whose walk stacks above it)
-    if (s->n_instances < 0 || (s->n_instances > 0 && (!s->instances || !s->prim_instance)))
-        return fail(PBRTGPU_E_INVALID, "instance arrays missing");
-    auto walkDepth = [&](uint32_t root, int *depthOut) -> int {
-        int maxD = 0;
-        std::vector<std::pair<uint32_t, int> > todo;
-        todo.push_back(std::make_pair(root, 0));
-        while (!todo.empty()) {
-            auto q = todo.back();
-            todo.pop_back();
-            if (q.first >= (uint32_t)s->n_nodes) return fail(PBRTGPU_E_INVALID, "BVH node index out of range");
-            const pbrtgpu_bvh_node &n = s->nodes[q.first];
-            maxD = std::max(maxD, q.second);
-            if ((n.meta & 0xff) == 0) {
-                if (q.second > 62) return fail(PBRTGPU_E_UNSUPPORTED, "BVH deeper than 63 levels");
-                todo.push_back(std::make_pair(q.first + 1, q.second + 1));
-                todo.push_back(std::make_pair(n.offset, q.second + 1));
-            } else if (n.offset + (n.meta & 0xff) > (uint32_t)s->n_prims)
-                return fail(PBRTGPU_E_INVALID, "BVH leaf out of range");
-        }
-        *depthOut = maxD;
-        return 0;
+    hipError_t he = hipSuccess;
+    auto put = [&](auto *src, size_t count, auto **dst) -> int {
+        he = upload(c, src, count, dst);
+        return he == hipSuccess ? 0 : PBRTGPU_E_NODEVICE;
     };
-    int maxDepth = 0, instDepth = 0;
-    if (int e = walkDepth(0, &maxDepth)) return e;
-    for (int i = 0; i < s->n_instances; ++i) {
-        const pbrtgpu_instance &I = s->instances[i];
-        if (I.root >= 0) {
-            int dd = 0;
-            if (int e = walkDepth((uint32_t)I.root, &dd)) return e;
-            instDepth = std::max(instDepth, dd + 1);
-        } else if (I.single_prim < 0 || I.single_prim >= s->n_prims)
-            return fail(PBRTGPU_E_INVALID, "instance without primitives");
+    if (int e = scene_build(s, top_nodes(), S, &c->feat, put, &err)) {
+        if (he != hipSuccess) return fail(-(1000 + (int)he), std::string("scene upload: ") + hipGetErrorString(he));
+        return fail(e, err);
     }
-    for (int i = 0; i < s->n_prims; ++i)
-        if (s->prims[i].shape_type == PBRTGPU_SHAPE_INSTANCE &&
-            (s->prims[i].shape_index < 0 || s->prims[i].shape_index >= s->n_instances))
-            return fail(PBRTGPU_E_INVALID, "bad instance index");
-    maxDepth += instDepth;
-    c->stackDepth = maxDepth + 1;
-    S.stackDepth = c->stackDepth;
-    HIPCHK(upload(c, s->band_Y, (size_t)s->n_bands, &S.bandY));
-    HIPCHK(upload(c, reinterpret_cast<const float4 *>(s->nodes), (size_t)s->n_nodes * 2, &S.nodes));
-    {
-        std::vector<float4> wn;
-        std::vector<uint32_t> ref;
-        if (int e = wide_bvh(s, top_nodes(), &wn, &ref, &S.nTop)) return e;
-        HIPCHK(upload(c, wn.data(), wn.size(), &S.wnodes));
-        HIPCHK(upload(c, ref.data(), ref.size(), &S.nodeRef));
-    }
-    HIPCHK(upload(c, s->prims, (size_t)s->n_prims, &S.prims));
-    std::vector<DevTri> pt(s->n_prims);
-    for (int i = 0; i < s->n_prims; ++i) {
-        const pbrtgpu_prim &p = s->prims[i];
-        DevTri t{};
-        if (p.shape_type == PBRTGPU_SHAPE_INSTANCE) {
-            pt[i] = t;
-            continue;
-        }
-        if (p.shape_type == PBRTGPU_SHAPE_TRIANGLE) {
-            if (p.shape_index < 0 || p.shape_index >= s->n_tris) return fail(PBRTGPU_E_INVALID, "bad triangle index");
-            const pbrtgpu_triangle &tr = s->tris[p.shape_index];
-            const float *a = s->vert_p + 3 * tr.v[0], *b = s->vert_p + 3 * tr.v[1], *cc = s->vert_p + 3 * tr.v[2];
-            t.a = make_float4(a[0], a[1], a[2], 0.f);
-            t.b = make_float4(b[0], b[1], b[2], 0.f);
-            t.c = make_float4(cc[0], cc[1], cc[2], 0.f);
-        } else if (p.shape_index < 0 || p.shape_index >= s->n_quadrics)
-            return fail(PBRTGPU_E_INVALID, "bad quadric index");
-        pt[i] = t;
-    }
-    // spectrum pool re-laid out with a stride of whole float4 quads (16-byte aligned band
-    // quads for the shading loads); every offset in the flattened scene is a multiple of
-    // n_bands (front end emits whole spectra)
-    const int nbp = (s->n_bands + 3) / 4 * 4;
-    if (s->n_spectra_floats % s->n_bands) return fail(PBRTGPU_E_INVALID, "spectrum pool is not whole spectra");
-    auto remap = [&](int32_t off, int32_t *out) -> bool {
-        if (off < 0) { *out = off; return true; }
-        if (off % s->n_bands || off >= s->n_spectra_floats) return false;
-        *out = off / s->n_bands * nbp;
-        return true;
-    };
-    std::vector<float> pool((size_t)s->n_spectra_floats / s->n_bands * nbp, 0.f);
-    for (int k = 0; k < s->n_spectra_floats / s->n_bands; ++k)
-        for (int i = 0; i < s->n_bands; ++i) pool[(size_t)k * nbp + i] = s->spectra[(size_t)k * s->n_bands + i];
-    std::vector<pbrtgpu_material> mats(s->materials, s->materials + s->n_materials);
-    for (auto &m : mats)
-        for (int k = 0; k < 4; ++k)
-            if (!remap(m.spec[k], &m.spec[k])) return fail(PBRTGPU_E_INVALID, "material spectrum offset");
-    std::vector<pbrtgpu_light> lts(s->lights, s->lights + s->n_lights);
-    S.nInf = 0;
-    for (auto &l : lts) {
-        if (!remap(l.spec, &l.spec)) return fail(PBRTGPU_E_INVALID, "light spectrum offset");
-        if (l.type == PBRTGPU_LIGHT_INFINITE) ++S.nInf;
-    }
-    std::vector<pbrtgpu_texture> texs(s->textures, s->textures + std::max(0, s->n_textures));
-    for (auto &t : texs)
-        if (t.type == PBRTGPU_TEX_CONST && t.spectral && !remap(t.spec, &t.spec))
-            return fail(PBRTGPU_E_INVALID, "texture spectrum offset");
-    // FromRGB basis, each of the 14 spectra padded to whole quads
-    std::vector<float> basis((size_t)14 * nbp, 0.f);
-    for (int k = 0; k < 14; ++k)
-        for (int i = 0; i < s->n_bands; ++i) basis[(size_t)k * nbp + i] = s->rgb_basis[(size_t)k * s->n_bands + i];
-    S.nbp = nbp;
-    HIPCHK(upload(c, texs.data(), texs.size(), &S.tex));
-    HIPCHK(upload(c, basis.data(), basis.size(), &S.basis));
-    HIPCHK(upload(c, s->ewa_lut, (size_t)128, &S.ewa));
-    HIPCHK(upload(c, pt.data(), pt.size(), &S.primTri));
-    HIPCHK(upload(c, s->tris, (size_t)s->n_tris, &S.tris));
-    HIPCHK(upload(c, s->meshes, (size_t)s->n_meshes, &S.meshes));
-    HIPCHK(upload(c, s->vert_p, (size_t)s->n_verts * 3, &S.vertP));
-    HIPCHK(upload(c, s->vert_n, (size_t)s->n_verts * 3, &S.vertN));
-    HIPCHK(upload(c, s->vert_uv, (size_t)s->n_verts * 2, &S.vertUV));
-    HIPCHK(upload(c, s->quadrics, (size_t)s->n_quadrics, &S.quads));
-    HIPCHK(upload(c, mats.data(), mats.size(), &S.mats));
-    HIPCHK(upload(c, lts.data(), lts.size(), &S.lights));
-    HIPCHK(upload(c, s->light_shapes, (size_t)s->n_light_shapes, &S.lightShapes));
-    S.nInsts = s->n_instances;
-    HIPCHK(upload(c, s->instances, (size_t)s->n_instances, &S.insts));
-    {
-        std::vector<int> pi(s->n_prims, -1);
-        if (s->n_instances > 0) for (int i = 0; i < s->n_prims; ++i) pi[i] = s->prim_instance[i];
-        HIPCHK(upload(c, pi.data(), pi.size(), &S.primInst));
-    }
-    HIPCHK(upload(c, pool.data(), pool.size(), &S.spectra));
-    {
-        std::vector<pbrtgpu_kdnode> kd(s->kdnodes, s->kdnodes + std::max(0, s->n_kdnodes));
-        for (auto &k : kd)
-            if (!remap(k.spec, &k.spec)) return fail(PBRTGPU_E_INVALID, "kd-tree spectrum offset");
-        for (auto &m : mats)
-            if (m.type == PBRTGPU_MAT_MEASURED && (m.aux < 0 || m.aux2 <= 0 || m.aux + m.aux2 > (int)kd.size()))
-                return fail(PBRTGPU_E_INVALID, "measured material kd-tree range");
-        HIPCHK(upload(c, kd.data(), kd.size(), &S.kd));
-        // packed nodes with parent links (relative indices; left child = node + 1) for the
-        // stackless lookup walk (kd_lookup, wavefront.h)
-        std::vector<float4> pack(2 * kd.size(), make_float4(0.f, 0.f, 0.f, 0.f));
-        std::vector<int> par(kd.size(), -1);
-        for (auto &m : mats) {
-            if (m.type != PBRTGPU_MAT_MEASURED) continue;
-            for (int i = 0; i < m.aux2; ++i) {
-                const pbrtgpu_kdnode &k = kd[(size_t)m.aux + i];
-                if (k.split_axis < 0 || k.split_axis > 3) return fail(PBRTGPU_E_INVALID, "kd-tree split axis");
-                if (k.split_axis == 3) continue;
-                if (k.has_left) {
-                    if (i + 1 >= m.aux2) return fail(PBRTGPU_E_INVALID, "kd-tree left child out of range");
-                    par[(size_t)m.aux + i + 1] = i;
-                }
-                if (k.right_child < m.aux2) {
-                    if (k.right_child <= i) return fail(PBRTGPU_E_INVALID, "kd-tree right child order");
-                    par[(size_t)m.aux + k.right_child] = i;
-                }
-            }
-            for (int i = 0; i < m.aux2; ++i) {
-                const pbrtgpu_kdnode &k = kd[(size_t)m.aux + i];
-                const int rc = (k.split_axis != 3 && k.right_child < m.aux2) ? k.right_child : -1;
-                const int meta = k.split_axis | (k.has_left && k.split_axis != 3 ? 4 : 0);
-                pack[2 * ((size_t)m.aux + i)] = make_float4(k.p[0], k.p[1], k.p[2], k.split_pos);
-                pack[2 * ((size_t)m.aux + i) + 1] =
-                    make_float4(bits_f((uint32_t)k.spec), bits_f((uint32_t)rc), bits_f((uint32_t)par[(size_t)m.aux + i]),
-                                bits_f((uint32_t)meta));
-            }
-        }
-        HIPCHK(upload(c, pack.data(), pack.size(), &S.kdPack));
-        HIPCHK(upload(c, s->merl, (size_t)std::max(0, s->n_merl_floats), &S.merl));
-        S.nKd = (int)kd.size();
-        S.kdInLds = (S.nKd > 0 && S.nKd <= kKdLdsNodes) ? 1 : 0;
-        if (const char *e = getenv("PBRTGPU_KD_LDS"))   // tests: force the global-memory walk
-            if (atoi(e) == 0) S.kdInLds = 0;
-    }
-    c->feat = S.nInf > 0 ? FEAT_INF : 0;
-    for (int i = 0; i < s->n_materials; ++i) {
-        const pbrtgpu_material &m = s->materials[i];
-        if (m.type == PBRTGPU_MAT_MEASURED || m.type == PBRTGPU_MAT_MEASURED_HALFANGLE) c->feat |= FEAT_MEAS;
-        if (m.bump_tex >= 0 || m.tex[0] >= 0 || m.tex[1] >= 0 || m.tex[2] >= 0 || m.tex[3] >= 0) c->feat |= FEAT_TEX;
-    }
+    c->stackDepth = S.stackDepth;
+    if (const char *e = getenv("PBRTGPU_KD_LDS"))   // tests: force the global-memory walk
+        if (atoi(e) == 0) S.kdInLds = 0;
     if (const char *e = getenv("PBRTGPU_SHADE_FULL"))   // tests: run the full variant on any scene
         if (atoi(e) != 0) c->feat = FEAT_ALL;
     c->nb = s->n_bands;

@@ -171,22 +171,30 @@ static hipError_t launch(int grid, hipStream_t stream, const DevScene &S, const 
     return hipGetLastError();
 }
 #if SHADE_DL
-// The light-sample batches of the DirectLighting slots this pass's k_shade marked PF_DLNEE
-// (directlighting.h dl_light_batches), in a kernel of their own so that neither step carries the
-// other's registers; their shadow / MIS rays join the pass's queues.
+// The DirectLighting step's two kernels after k_shade in each pass, in kernels of their own so
+// that no step carries another's registers (k_shade with the specular branches inlined peaked at
+// ~330 VGPRs: 559 spilled at 3 waves/SIMD); their rays join the pass's queues.
+//   k_dl_nee:  the light-sample batches of the slots k_shade marked PF_DLNEE
+//              (directlighting.h dl_light_batches);
+//   k_dl_spec: the specular branches and frame pops of the slots marked PF_DLSPEC by k_shade or
+//              by k_dl_nee (dl_spec_step).  A slot whose sample completes here is free from the
+//              next pass's k_shade on; it is counted in CNT_IDLE so that this pass is not taken
+//              for the wavefront's last while items may remain.
+// 2 waves/SIMD for <= 32 bands (k_dl_nee: 47 VGPRs spilled, k_dl_spec: 148); the 60-band
+// builds need 1 wave/SIMD to stay within tools/kernel_budget.py (at 2 waves k_dl_nee spilled 682)
 #ifndef PGD_NEE_ATTR
-#define PGD_NEE_ATTR __attribute__((amdgpu_waves_per_eu(2, 2)))
+#define PGD_NEE_ATTR __attribute__((amdgpu_waves_per_eu(SHADE_NB > 32 ? 1 : 2, SHADE_NB > 32 ? 1 : 2)))
+#endif
+#ifndef PGD_SPEC_ATTR
+#define PGD_SPEC_ATTR __attribute__((amdgpu_waves_per_eu(SHADE_NB > 32 ? 1 : 2, SHADE_NB > 32 ? 1 : 2)))
 #endif
 template <int NB, int FEAT>
 __global__ __launch_bounds__(kShadeBlock) PGD_NEE_ATTR void k_dl_nee(DevScene S, PathSoA P, int qout) {
     if (FEAT & FEAT_MEAS) kd_lds_fill(S);   // measured-BRDF lookups read the LDS copy (as in k_shade)
     const int slot = blockIdx.x * blockDim.x + threadIdx.x;
     Pushes pu = {false, false, false, 0u, 0u};
-    bool idle = false;
-    if (slot < P.cap && P.item[slot] >= 0 && (P.flags[slot] & PF_DLNEE)) idle = dl_light_batches<NB, FEAT>(S, P, slot, pu);
+    if (slot < P.cap && P.item[slot] >= 0 && (P.flags[slot] & PF_DLNEE)) dl_light_batches<NB, FEAT>(S, P, slot, pu);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const unsigned long long bI = __ballot(idle);
-    if (bI && lane == 0) atomicAdd(&P.cnt[CNT_IDLE(qout)], (uint32_t)__popcll(bI));
     __shared__ uint32_t qsh[12];   // per wave: M, S totals -> offsets; bases
     const uint32_t nm = (uint32_t)__popc(pu.mMask), ns = (uint32_t)__popc(pu.sMask);
     const uint32_t im = wave_scan(nm), is = wave_scan(ns);
@@ -205,13 +213,51 @@ __global__ __launch_bounds__(kShadeBlock) PGD_NEE_ATTR void k_dl_nee(DevScene S,
     for (uint32_t m = pu.mMask; m; m &= m - 1u) qC[km++] = ((uint32_t)(slot + (__ffs(m) - 1) * P.cap) << 1) | 1u;
     for (uint32_t m = pu.sMask; m; m &= m - 1u) qS[ks++] = (uint32_t)(slot + (__ffs(m) - 1) * P.cap);
 }
+template <int NB, int FEAT>
+__global__ __launch_bounds__(kShadeBlock) PGD_SPEC_ATTR void k_dl_spec(DevScene S, PathSoA P, int qout,
+                                                                      float *__restrict__ Lout) {
+    if (FEAT & FEAT_MEAS) kd_lds_fill(S);
+    const int slot = blockIdx.x * blockDim.x + threadIdx.x;
+    Pushes pu = {false, false, false, 0u, 0u};
+    bool done = false, zeroed = false;
+    if (slot < P.cap && P.item[slot] >= 0 && (P.flags[slot] & PF_DLSPEC)) {
+        pu = dl_spec_step<NB, FEAT>(S, P, slot, Lout, &done, &zeroed);
+        if (done) P.item[slot] = -1;
+    }
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const unsigned long long bD = __ballot(done), bZ = __ballot(zeroed), bC = __ballot(pu.c);
+    if (lane == 0) {
+        if (bD) atomicAdd(&P.cnt[CNT_IDLE(qout)], (uint32_t)__popcll(bD));
+        if (bZ) atomicAdd(&P.cnt[CNT_ZEROED], (uint32_t)__popcll(bZ));
+    }
+    __shared__ uint32_t qsh[8];   // per wave: child rays -> offsets; base
+    if (lane == 0) qsh[wave] = (uint32_t)__popcll(bC);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = 0u;
+        for (int w = 0; w < (int)(blockDim.x >> 6); ++w) { const uint32_t v = qsh[w]; qsh[w] = t; t += v; }
+        qsh[7] = t ? atomicAdd(&P.cnt[CNT_QC(qout)], t) : 0u;
+    }
+    __syncthreads();
+    if (pu.c) {
+        uint32_t *qC = P.qC + (size_t)qout * 2 * P.rcap;
+        qC[qsh[7] + qsh[wave] + (uint32_t)__popcll(bC & ((1ull << lane) - 1ull))] = (uint32_t)slot << 1;
+    }
+}
 template <int NB>
 hipError_t launch_dl_nee(int grid, hipStream_t stream, const DevScene &S, const PathSoA &P, int qout) {
     const size_t lds = ((SHADE_FEAT & FEAT_MEAS) && S.kdInLds) ? (size_t)S.nKd * 32 : 0;
     hipLaunchKernelGGL((k_dl_nee<NB, SHADE_FEAT>), dim3(grid), dim3(kShadeBlock), lds, stream, S, P, qout);
     return hipGetLastError();
 }
+template <int NB>
+hipError_t launch_dl_spec(int grid, hipStream_t stream, const DevScene &S, const PathSoA &P, int qout, float *Lout) {
+    const size_t lds = ((SHADE_FEAT & FEAT_MEAS) && S.kdInLds) ? (size_t)S.nKd * 32 : 0;
+    hipLaunchKernelGGL((k_dl_spec<NB, SHADE_FEAT>), dim3(grid), dim3(kShadeBlock), lds, stream, S, P, qout, Lout);
+    return hipGetLastError();
+}
 template hipError_t launch_dl_nee<SHADE_NB>(int, hipStream_t, const DevScene &, const PathSoA &, int);
+template hipError_t launch_dl_spec<SHADE_NB>(int, hipStream_t, const DevScene &, const PathSoA &, int, float *);
 template <int NB>
 hipError_t launch_shade_dl(int grid, hipStream_t stream, const DevScene &S, const PathSoA &P, const ItemSrc &src,
                            int qout, float *Lout) {

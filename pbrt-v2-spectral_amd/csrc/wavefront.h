@@ -322,7 +322,10 @@ PGD_INLINE bool emit_black(const DevScene &S, const Emit &e) {
 static const int kKdLdsNodes = 1536;            // 48 KB of LDS per shade block
 extern __shared__ float4 pgd_kd_lds[];          // dynamic LDS of k_shade (FEAT_MEAS variants)
 typedef float F4N __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(3))) const F4N LdsF4;   // an LDS float4 (ds_read_b128)
+#ifndef PGD_LDS_AS   // the LDS address space (the host replay of tools/hostsan defines it empty)
+#define PGD_LDS_AS __attribute__((address_space(3)))
+#endif
+typedef PGD_LDS_AS const F4N LdsF4;   // an LDS float4 (ds_read_b128)
 PGD_INLINE float4 kd_node(const float4 *__restrict__ p, int i) { return p[i]; }
 PGD_INLINE float4 kd_node(LdsF4 *p, int i) { const F4N v = p[i]; return make_float4(v.x, v.y, v.z, v.w); }
 
@@ -1065,6 +1068,9 @@ hipError_t launch_shade_dl(int grid, hipStream_t stream, const DevScene &S, cons
 // k_dl_nee: the light-sample batches of the DirectLighting slots k_shade marked (PF_DLNEE)
 template <int NB>
 hipError_t launch_dl_nee(int grid, hipStream_t stream, const DevScene &S, const PathSoA &P, int qout);
+// k_dl_spec: their specular branches and frame pops (PF_DLSPEC)
+template <int NB>
+hipError_t launch_dl_spec(int grid, hipStream_t stream, const DevScene &S, const PathSoA &P, int qout, float *Lout);
 // k_shade with the MetadataIntegrator step (all features compiled in)
 template <int NB>
 hipError_t launch_shade_meta(int grid, hipStream_t stream, const DevScene &S, const PathSoA &P, const ItemSrc &src,

@@ -404,6 +404,33 @@ def test_direct_lighting_recursion_and_regeneration(pg, monkeypatch, strategy, m
     assert np.abs(L - Lo).max() / np.abs(Lo).max() < 1e-4
 
 
+@pytest.mark.parametrize("integ,strategy,md", [("directlighting", "all", 6), ("directlighting", "one", 4),
+                                               ("path", None, 5)])
+def test_independent_of_unwritten_state_and_slot_layout(pg, monkeypatch, integ, strategy, md):
+    """PBRTGPU_POISON fills every path-slot array (and the traversal stack spill area) with a byte
+    before each run, so a read of state no pass wrote changes the radiance; the slot pool size
+    changes which items share a wave and in what order slots are regenerated.  Every combination
+    gives the same bits, and the oracle's (the DirectLighting non-determinism of
+    the first 3-wave build)."""
+    from conftest import PACKS
+    kw = dict(integrator=integ, strategy=strategy) if strategy else {}
+    scene = pg.Scene.load(os.path.join(PACKS, "coverage.pack"), xres=40, yres=30, spp=4, maxdepth=md, **kw)
+    keys = _keys(scene)
+    runs = []
+    with pg.Device(0) as d:
+        d.upload(scene)
+        for poison in ("0x00", "0xff", "0x7f"):
+            for slots in (None, "193", "4096"):
+                monkeypatch.setenv("PBRTGPU_POISON", poison)
+                if slots: monkeypatch.setenv("PBRTGPU_SLOTS", slots)
+                else: monkeypatch.delenv("PBRTGPU_SLOTS", raising=False)
+                runs.append(d.trace_paths(keys))
+    for r in runs[1:]:
+        assert np.array_equal(r.view(np.int32), runs[0].view(np.int32))
+    Lo = pg.oracle().trace_paths(scene, keys)
+    assert np.all(runs[0].view(np.int32) == Lo.view(np.int32), axis=1).mean() >= 1 - 1e-4
+
+
 META = ["metadata_material_%s_48x36s4", "metadata_mesh_%s_48x36s4", "metadata_depth_%s_48x36s4",
         "killeroo_meta_mesh_%s_40x32s2", "anim_meta_mesh_%s_40x32s2", "bunny_meta_depth_%s_40x32s2"]
 

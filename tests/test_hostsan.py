@@ -1,0 +1,122 @@
+"""The GPU's device shading code replayed on the CPU (tools/hostsan/shade_host.cpp) against the
+oracle, and under the host sanitizers.
+
+shade_host compiles csrc/wavefront.h, directlighting.h, metadata.h, device.h and scene_build.h
+as host C++ (tools/hostsan/hip/hip_runtime.h stands in for the HIP header) and drives the
+wavefront pass by pass as pbrtgpu.hip does.  It is test infrastructure: these tests pin the
+device source itself, independently of the GPU --
+  * bit-exact with the C oracle (liboracle.so, the transcendental definition the GPU uses) for
+    every integrator and the packaged scenes, and at config C2's real size (golden keys);
+  * no read of state a pass did not write: MSan reports none, and the radiance does not change
+    with the byte the path-slot arrays are filled with (--poison);
+  * no out-of-bounds access or undefined behaviour: ASan + UBSan report none.
+This is how the DirectLighting non-determinism of the first 3-wave build was localised to that
+build's machine code rather than its source.
+"""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, PACKS, ROOT
+
+HS = os.path.join(ROOT, "tools", "hostsan")
+
+
+def _build(target):
+    subprocess.run(["make", "-s", "-C", HS, target], check=True, capture_output=True)
+    return os.path.join(HS, target)
+
+
+def _keys(scene):
+    c = scene.flat.camera
+    return np.array([(x, y, s) for y in range(c.sy_start, c.sy_end) for x in range(c.sx_start, c.sx_end)
+                     for s in range(scene.spp)], np.int32)
+
+
+def _replay(exe, pack, tmp_path, keys=None, poison=None, **a):
+    out = str(tmp_path / "L.f32")
+    cmd = [exe, pack, "--out", out]
+    for k, v in a.items():
+        cmd += ["--" + k, str(v)]
+    if poison is not None:
+        cmd += ["--poison", str(poison)]
+    if keys is not None:
+        kf = str(tmp_path / "keys.i32")
+        np.ascontiguousarray(keys, np.int32).tofile(kf)
+        cmd += ["--keys", kf]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+    for bad in ("ERROR: AddressSanitizer", "runtime error:", "WARNING: MemorySanitizer", "LeakSanitizer"):
+        assert bad not in r.stderr, r.stderr[-4000:]
+    assert r.returncode == 0, r.stderr[-4000:]
+    return np.fromfile(out, np.float32)
+
+
+CASES = [
+    ("coverage.pack", dict(xres=40, yres=30, spp=4, maxdepth=6, integrator="directlighting", strategy="all")),
+    ("coverage.pack", dict(xres=40, yres=30, spp=4, maxdepth=5, integrator="directlighting", strategy="one")),
+    ("killeroo-simple.pack", dict(xres=32, yres=24, spp=4, maxdepth=5, integrator="directlighting", strategy="all")),
+    ("coverage.pack", dict(xres=40, yres=30, spp=8, maxdepth=5)),
+    ("anim-killeroos-moving.pack", dict(xres=24, yres=24, spp=4, maxdepth=5)),
+    ("bunny.pack", dict(xres=24, yres=16, spp=4, maxdepth=5)),
+    ("metal.pack", dict(xres=24, yres=24, spp=4, maxdepth=5)),
+    ("coverage.pack", dict(xres=40, yres=30, spp=2, integrator="metadata", strategy="depth")),
+]
+
+
+@pytest.mark.parametrize("pack,a", CASES, ids=["dl_all_md6", "dl_one", "dl_killeroo", "path_coverage", "path_anim",
+                                               "path_bunny", "path_metal60", "metadata"])
+def test_replay_matches_oracle(pg, tmp_path, pack, a):
+    exe = _build("shade_host")
+    scene = pg.Scene.load(os.path.join(PACKS, pack), **a)
+    keys = _keys(scene)
+    Lo = pg.oracle().trace_paths(scene, keys)
+    L = _replay(exe, os.path.join(PACKS, pack), tmp_path, **a).reshape(Lo.shape)
+    assert np.array_equal(L.view(np.int32), Lo.view(np.int32))
+
+
+KEYS = [("killeroo_keys_c2_700x700s256", "killeroo-simple.pack"), ("bunny_keys_c3_1920x1080s1024", "bunny.pack"),
+        ("metal_keys_c4_400x400s4096", "metal.pack"), ("anim_keys_c5_600x600s512", "anim-killeroos-moving.pack")]
+
+
+@pytest.mark.parametrize("name,pack", KEYS, ids=["c2", "c3", "c4", "c5"])
+def test_replay_config_golden_keys(pg, tmp_path, name, pack):
+    """Configs C2-C5 at their real size and sample count: the reference harness's golden keys."""
+    from test_oracle_golden import exact_rate
+    exe = _build("shade_host")
+    g = np.load(os.path.join(GOLDEN, name + ".npz"))
+    w, h, spp, seed, md = [int(v) for v in g["config"]]
+    assert seed == 0   # the packs' own seed
+    pack = os.path.join(PACKS, pack)
+    scene = pg.Scene.load(pack, xres=w, yres=h, spp=spp, maxdepth=md, seed=seed)
+    Lo = pg.oracle().trace_paths(scene, g["keys"])
+    L = _replay(exe, pack, tmp_path, keys=g["keys"], xres=w, yres=h, spp=spp, maxdepth=md).reshape(Lo.shape)
+    assert np.array_equal(L.view(np.int32), Lo.view(np.int32))
+    assert np.all(L.view(np.int32) == g["L"].view(np.int32), axis=1).mean() >= exact_rate(name)
+
+
+def test_replay_independent_of_unwritten_state(pg, tmp_path):
+    """Path-slot arrays filled with 0x00, 0xff or 0x7f (NaN patterns) before the run: the same bits."""
+    exe = _build("shade_host")
+    pack, a = CASES[0]
+    runs = [_replay(exe, os.path.join(PACKS, pack), tmp_path, poison=p, **a) for p in (0x00, 0xff, 0x7f)]
+    pack2, a2 = CASES[3]
+    runs2 = [_replay(exe, os.path.join(PACKS, pack2), tmp_path, poison=p, **a2) for p in (0x00, 0xff, 0x7f)]
+    for r in runs[1:]:
+        assert np.array_equal(r.view(np.int32), runs[0].view(np.int32))
+    for r in runs2[1:]:
+        assert np.array_equal(r.view(np.int32), runs2[0].view(np.int32))
+
+
+@pytest.mark.parametrize("variant", ["shade_host_asan", "shade_host_msan"])
+def test_replay_under_sanitizers(pg, tmp_path, variant):
+    """Every case above (DirectLighting's specular recursion and light-sample batches, the path
+    integrator on every packaged scene and coverage.pbrt's features, metadata) under ASan + UBSan
+    and under MSan: no report, oracle bits."""
+    exe = _build(variant)
+    for pack, a in CASES:
+        scene = pg.Scene.load(os.path.join(PACKS, pack), **a)
+        Lo = pg.oracle().trace_paths(scene, _keys(scene))
+        L = _replay(exe, os.path.join(PACKS, pack), tmp_path, **a).reshape(Lo.shape)
+        assert np.array_equal(L.view(np.int32), Lo.view(np.int32))

@@ -1,0 +1,362 @@
+// shade_host.cpp -- TEST INFRASTRUCTURE (never part of the product): the GPU wavefront's device
+// code replayed on the CPU, so that it can run under the host sanitizers.
+//
+// The device shading steps (csrc/wavefront.h shade_slot / path_start, directlighting.h
+// shade_slot_dl / dl_light_batches, metadata.h shade_slot_meta), the ray queries
+// (device.h bvh_intersect / bvh_intersectP: the legacy one-ray walk, same primitives in the same
+// order as the persistent kernels) and the DevScene layout (csrc/scene_build.h) are compiled as
+// host C++ against tools/hostsan/hip/hip_runtime.h and driven pass by pass the way
+// pbrtgpu.hip run_wavefront drives them: regeneration, closest-hit and shadow queries of the
+// queued rays, one shading step per live slot (+ k_dl_nee's light batches for DirectLighting).
+//   * Every path-slot array is its own heap block (ASan redzones per array) and is left as
+//     malloc returns it (MSan tracks it as uninitialised) or filled with --poison BYTE, as the
+//     GPU leaves hipMalloc memory unwritten: a read of state no pass wrote shows up as an MSan
+//     report or as a radiance that changes with the poison byte.
+//   * Each slot is lane 0 of its own 64-slot wave (slot = 64 i): the wave intrinsics of the
+//     stand-in header then see one active lane.
+//
+// usage: shade_host SCENE [--xres N] [--yres N] [--spp N] [--maxdepth N] [--bands N]
+//                         [--integrator path|directlighting|metadata] [--strategy all|one|mesh|material|depth]
+//                         [--slots N] [--poison BYTE] [--keys FILE] --out FILE
+// Items: every (x, y, s) of the camera's sample extent in row-major order, or the int32
+// (x, y, s) triples of --keys.  Writes float32 [items][bands] radiance to --out.
+#include <hip/hip_runtime.h>   // the stand-in of tools/hostsan/hip
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <type_traits>
+#include <vector>
+#include "pbrthost.h"
+#include "scene_build.h"
+#include "directlighting.h"
+#include "metadata.h"
+
+#if defined(__has_feature)
+#if __has_feature(memory_sanitizer)
+#include <sanitizer/msan_interface.h>
+#define HS_MSAN 1
+#endif
+#endif
+#ifndef HS_MSAN
+#define HS_MSAN 0
+#endif
+
+namespace pgd {
+float4 pgd_kd_lds[2 * kKdLdsNodes];   // k_shade's dynamic LDS (the measured-BRDF kd-trees)
+}
+using namespace pgd;
+
+static std::vector<void *> g_blocks;
+static int g_poison = -1;   // -1: leave heap blocks as allocated
+
+static void *halloc(size_t bytes, bool poison) {
+    const size_t n = std::max<size_t>(64, (bytes + 63) & ~(size_t)63);
+    void *p = aligned_alloc(64, n);
+    if (!p) { fprintf(stderr, "out of memory\n"); exit(2); }
+    if (poison && g_poison >= 0) memset(p, g_poison, n);
+    g_blocks.push_back(p);
+    return p;
+}
+template <class T> static T *arr(size_t n) { return static_cast<T *>(halloc(n * sizeof(T), true)); }
+
+#if HS_MSAN
+// the flattened scene comes from libpbrthost (not instrumented): its arrays are initialised
+static void unpoison_flat(const pbrtgpu_flat_scene *s) {
+    auto u = [](const void *p, size_t b) { if (p && b) __msan_unpoison(p, b); };
+    u(s, sizeof(*s));
+    u(s->band_Y, 4 * (size_t)s->n_bands);
+    u(s->nodes, sizeof(*s->nodes) * (size_t)s->n_nodes);
+    u(s->prims, sizeof(*s->prims) * (size_t)s->n_prims);
+    u(s->tris, sizeof(*s->tris) * (size_t)s->n_tris);
+    u(s->meshes, sizeof(*s->meshes) * (size_t)s->n_meshes);
+    u(s->vert_p, 12 * (size_t)s->n_verts);
+    u(s->vert_n, 12 * (size_t)s->n_verts);
+    u(s->vert_uv, 8 * (size_t)s->n_verts);
+    u(s->quadrics, sizeof(*s->quadrics) * (size_t)s->n_quadrics);
+    u(s->materials, sizeof(*s->materials) * (size_t)s->n_materials);
+    u(s->lights, sizeof(*s->lights) * (size_t)s->n_lights);
+    u(s->light_shapes, sizeof(*s->light_shapes) * (size_t)s->n_light_shapes);
+    u(s->spectra, 4 * (size_t)s->n_spectra_floats);
+    u(s->instances, sizeof(*s->instances) * (size_t)std::max(0, s->n_instances));
+    if (s->n_instances > 0) u(s->prim_instance, 4 * (size_t)s->n_prims);
+    u(s->kdnodes, sizeof(*s->kdnodes) * (size_t)std::max(0, s->n_kdnodes));
+    u(s->textures, sizeof(*s->textures) * (size_t)std::max(0, s->n_textures));
+    u(s->ewa_lut, 4 * 128);
+    u(s->rgb_basis, 4 * 14 * (size_t)s->n_bands);
+    u(s->merl, 4 * (size_t)std::max(0, s->n_merl_floats));
+    u(s->prim_meta, 8 * (size_t)s->n_prims);
+    u(s->lens.elements, 16 * (size_t)std::max(0, s->lens.n_elements));
+}
+#endif
+
+// PathSoA as pbrtgpu.hip ensure_slots lays it out, one heap block per array
+static PathSoA make_soa(int cap, int NB, int nInst, int nFrames, int batch) {
+    const size_t C = (size_t)cap, R = C * (size_t)batch, AB = (size_t)std::max(2, batch), W = (C + 63) / 64;
+    const size_t NQ = (size_t)(NB + 3) / 4, F = (size_t)nFrames;
+    PathSoA P{};
+    P.cap = cap;
+    P.rcap = (int)R;
+    P.dlBatch = batch;
+    P.item = arr<int>(C); P.hp = arr<uint32_t>(C); P.smp = arr<uint32_t>(C); P.bounce = arr<int>(C);
+    P.flags = arr<uint32_t>(C); P.mt = arr<uint32_t>(5 * C); P.pix = arr<uint32_t>(C);
+    P.beta = arr<float4>(3 * NQ * C); P.L = arr<float4>(NQ * C);
+    P.A = arr<float4>(AB * NQ * C); P.B = arr<float4>(AB * NQ * C);
+    P.M = arr<float4>(NQ * C); P.K = arr<float4>(NQ * C);
+    P.aMask = arr<unsigned long long>(2 * W); P.bMask = arr<unsigned long long>(3 * W);
+    P.mMask = arr<unsigned long long>(2 * W);
+    P.ray = arr<float>(3 * 9 * R); P.hitPrim = arr<int>(2 * R); P.hitT = arr<float>(2 * R); P.occ = arr<uint32_t>(R);
+    P.qC = arr<uint32_t>(2 * 2 * R); P.qS = arr<uint32_t>(2 * R);
+    P.cnt = arr<uint32_t>(CNT_WORDS);
+    memset(P.cnt, 0, CNT_WORDS * 4);
+    P.nInst = nInst;
+    P.instM = nInst ? arr<float4>(C * (size_t)nInst * 8) : nullptr;
+    P.nFrames = nFrames;
+    if (nFrames) {
+        P.dlMask = arr<uint32_t>(C);
+        P.fL = arr<float4>(F * NQ * C); P.fF = arr<float4>(F * NQ * C);
+        P.fRay = arr<float>(F * 9 * C); P.fDiff = arr<float>(F * 12 * C); P.fS = arr<float>(F * 2 * C);
+        P.fHit = arr<int>(F * 2 * C); P.fBr = arr<uint32_t>(F * C); P.dlk = arr<uint32_t>(C);
+    }
+    for (size_t i = 0; i < C; ++i) P.item[i] = -1;   // run_wavefront: hipMemset(item, 0xff) and the masks' 0
+    memset(P.aMask, 0, 2 * W * 8);
+    memset(P.bMask, 0, 3 * W * 8);
+    memset(P.mMask, 0, 2 * W * 8);
+    return P;
+}
+
+struct Queues { std::vector<uint32_t> c, s; };
+
+template <int NB, int FEAT, int MODE>
+static int run(const DevScene &S, PathSoA &P, const ItemSrc &src, int nSlots, float *Lout, std::string *err) {
+    enum { MODE_PATH = 0, MODE_DL = 1, MODE_META = 2 };
+    const int cap = P.cap;
+    uint32_t next = 0, finished = 0;
+    Queues Q[2];
+    std::vector<uint32_t> stk((size_t)S.stackDepth + 1);
+    std::vector<float> stkT((size_t)S.stackDepth + 1);
+    const int64_t pathPasses = MODE == MODE_DL ? (((int64_t)1 << P.nFrames) - 1) * (S.dlK + 1) + 2 : S.maxDepth + 3;
+    const int64_t maxPasses = 2 * ((src.nItems + nSlots - 1) / nSlots + 1) * pathPasses + 8;
+    auto push = [&](int q, const Pushes &pu, int slot) {
+        if (pu.c) Q[q].c.push_back((uint32_t)slot << 1);
+        if (MODE == MODE_DL) {
+            for (uint32_t m = pu.mMask; m; m &= m - 1u) Q[q].c.push_back(((uint32_t)(slot + (__builtin_ctz(m)) * cap) << 1) | 1u);
+            for (uint32_t m = pu.sMask; m; m &= m - 1u) Q[q].s.push_back((uint32_t)(slot + (__builtin_ctz(m)) * cap));
+        } else {
+            if (pu.m) Q[q].c.push_back(((uint32_t)(MODE == MODE_PATH ? pu.mIdx : slot) << 1) | 1u);
+            if (pu.s) Q[q].s.push_back((uint32_t)(MODE == MODE_PATH ? pu.sIdx : slot));
+        }
+    };
+    // one k_shade pass (+ k_dl_nee): the per-thread body of shade.hip k_shade for every slot
+    auto shade = [&](int qout) -> uint32_t {
+        Q[qout].c.clear();
+        Q[qout].s.clear();
+        for (int i = 0; i < nSlots; ++i) {
+            const int slot = 64 * i;
+            threadIdx.x = (unsigned)(slot & 63);
+            Pushes pu = {false, false, false, 0u, 0u};
+            bool freeSlot = P.item[slot] < 0, zeroed = false;
+            if (!freeSlot) {
+                bool done;
+                if (P.bounce[slot] == -2) {
+                    float4 Z[Bands<NB>::NQ];
+                    for (int q = 0; q < Bands<NB>::NQ; ++q) Z[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+                    (void)path_output<NB>(S, Z, Lout, P.item[slot], P.smp[slot]);
+                    done = true;
+                } else if (MODE == MODE_DL) pu = shade_slot_dl<NB, FEAT>(S, P, slot, Lout, &done, &zeroed);
+                else if (MODE == MODE_META) pu = shade_slot_meta<NB, FEAT>(S, P, slot, Lout, &done, &zeroed);
+                else pu = shade_slot<NB, FEAT>(S, P, slot, Lout, &done, &zeroed, qout);
+                if (done) { P.item[slot] = -1; freeSlot = true; ++finished; }
+            }
+            push(qout, pu, slot);
+            if (freeSlot && next < src.nItems) {
+                path_start<NB>(S, P, src, slot, next++);
+                Q[qout].c.push_back((uint32_t)slot << 1);
+            }
+        }
+        uint32_t idle = 0;
+        if (MODE == MODE_DL) {
+            for (int i = 0; i < nSlots; ++i) {   // k_dl_nee
+                const int slot = 64 * i;
+                threadIdx.x = (unsigned)(slot & 63);
+                Pushes pu = {false, false, false, 0u, 0u};
+                if (P.item[slot] >= 0 && (P.flags[slot] & PF_DLNEE)) dl_light_batches<NB, FEAT>(S, P, slot, pu);
+                push(qout, pu, slot);
+            }
+            for (int i = 0; i < nSlots; ++i) {   // k_dl_spec
+                const int slot = 64 * i;
+                threadIdx.x = (unsigned)(slot & 63);
+                Pushes pu = {false, false, false, 0u, 0u};
+                bool done = false, zeroed = false;
+                if (P.item[slot] >= 0 && (P.flags[slot] & PF_DLSPEC)) {
+                    pu = dl_spec_step<NB, FEAT>(S, P, slot, Lout, &done, &zeroed);
+                    if (done) { P.item[slot] = -1; ++finished; ++idle; }
+                }
+                push(qout, pu, slot);
+            }
+        }
+        return idle;
+    };
+    // the ray queries of queue set q (k_trace_pt / k_trace_inst: hit or miss, t = inf on a miss)
+    auto trace = [&](int q) {
+        Stack st;
+        st.base = stk.data();
+        st.tbase = stkT.data();
+        st.stride = 1;
+        for (uint32_t e : Q[q].c) {
+            const int rs = (int)(e >> 1), kind = (int)(e & 1u);
+            Ray r = ray_load(P, kind, rs);
+            int prim = -1;
+            float t = INFINITY;
+            const bool hit = S.nInsts > 0 ? bvh_intersect<true>(S, st, r, &prim, &t) : bvh_intersect<false>(S, st, r, &prim, &t);
+            if (!hit) prim = -1;
+            P.hitPrim[(size_t)kind * P.rcap + rs] = prim;
+            P.hitT[(size_t)kind * P.rcap + rs] = prim >= 0 ? t : INFINITY;
+        }
+        for (uint32_t rs : Q[q].s) {
+            const Ray r = ray_load(P, RAY_S, (int)rs);
+            P.occ[rs] = (S.nInsts > 0 ? bvh_intersectP<true>(S, st, r) : bvh_intersectP<false>(S, st, r)) ? 1u : 0u;
+        }
+    };
+    P.pass = 0;
+    (void)shade(0);
+    int q = 0;
+    for (int64_t pass = 0;; ++pass) {
+        if (pass > maxPasses) { *err = "wavefront did not drain"; return 3; }
+        trace(q);
+        const int nq = q ^ 1;
+        P.pass = (P.pass + 1) % 3;
+        const uint32_t idle = shade(nq);
+        q = nq;
+        if (Q[q].c.empty() && Q[q].s.empty() && idle == 0) break;
+    }
+    if (finished != src.nItems || next != src.nItems) {
+        *err = "items left unfinished: " + std::to_string(src.nItems - finished);
+        return 3;
+    }
+    return 0;
+}
+
+template <int NB>
+static int run_nb(const DevScene &S, PathSoA &P, const ItemSrc &src, int nSlots, int feat, float *Lout, std::string *err) {
+    if (S.integrator == PBRTGPU_INTEGRATOR_DIRECT) return run<NB, FEAT_ALL, 1>(S, P, src, nSlots, Lout, err);
+    if (S.integrator == PBRTGPU_INTEGRATOR_METADATA) return run<NB, FEAT_ALL, 2>(S, P, src, nSlots, Lout, err);
+    return feat ? run<NB, FEAT_ALL, 0>(S, P, src, nSlots, Lout, err) : run<NB, 0, 0>(S, P, src, nSlots, Lout, err);
+}
+
+int main(int argc, char **argv) {
+    if (argc < 2) {
+        fprintf(stderr, "usage: %s SCENE [--xres N] [--yres N] [--spp N] [--maxdepth N] [--bands N] [--integrator I] "
+                        "[--strategy S] [--slots N] [--poison BYTE] [--keys FILE] --out FILE\n", argv[0]);
+        return 2;
+    }
+    pbrthost_overrides ov = {-1, -1, -1, -1, 0, PBRTHOST_KEEP_SEED, -1, -1, -1, -1, -1, -1};
+    int nSlots = 256;
+    const char *out = nullptr, *keyFile = nullptr, *strategy = nullptr;
+    for (int i = 2; i + 1 < argc; i += 2) {
+        const std::string a = argv[i];
+        const char *v = argv[i + 1];
+        if (a == "--xres") ov.xres = atoi(v);
+        else if (a == "--yres") ov.yres = atoi(v);
+        else if (a == "--spp") ov.spp = atoi(v);
+        else if (a == "--maxdepth") ov.maxdepth = atoi(v);
+        else if (a == "--bands") ov.bands = atoi(v);
+        else if (a == "--slots") nSlots = std::max(1, atoi(v));
+        else if (a == "--poison") g_poison = (int)strtol(v, nullptr, 0) & 0xff;
+        else if (a == "--out") out = v;
+        else if (a == "--keys") keyFile = v;
+        else if (a == "--strategy") strategy = v;
+        else if (a == "--integrator")
+            ov.integrator = !strcmp(v, "directlighting") ? PBRTGPU_INTEGRATOR_DIRECT
+                            : !strcmp(v, "metadata")     ? PBRTGPU_INTEGRATOR_METADATA
+                                                         : PBRTGPU_INTEGRATOR_PATH;
+        else { fprintf(stderr, "unknown option %s\n", a.c_str()); return 2; }
+    }
+    if (strategy) {
+        if (!strcmp(strategy, "all")) ov.dl_strategy = PBRTGPU_DL_ALL;
+        else if (!strcmp(strategy, "one")) ov.dl_strategy = PBRTGPU_DL_ONE;
+        else if (!strcmp(strategy, "mesh")) ov.meta_strategy = PBRTGPU_META_MESH;
+        else if (!strcmp(strategy, "material")) ov.meta_strategy = PBRTGPU_META_MATERIAL;
+        else if (!strcmp(strategy, "depth")) ov.meta_strategy = PBRTGPU_META_DEPTH;
+    }
+    if (!out) { fprintf(stderr, "--out FILE is required\n"); return 2; }
+    char msg[512] = {0};
+    pbrthost_scene *hs = nullptr;
+    pbrtgpu_flat_scene fs;
+#if HS_MSAN
+    // libpbrthost and libz are not instrumented: no interceptor checks while they run (their
+    // writes are not tracked), then their output counts as initialised
+    __msan_scoped_disable_interceptor_checks();
+#endif
+    const int lrc = pbrthost_load(argv[1], &ov, &hs, msg, sizeof(msg));
+    const int frc = lrc ? -1 : pbrthost_flat(hs, &fs);
+#if HS_MSAN
+    __msan_scoped_enable_interceptor_checks();
+    __msan_unpoison(msg, sizeof(msg));
+#endif
+    if (lrc) { fprintf(stderr, "load: %s\n", msg); return 1; }
+    if (frc) { fprintf(stderr, "flat scene failed\n"); return 1; }
+#if HS_MSAN
+    unpoison_flat(&fs);
+#endif
+    std::string err;
+    if (int e = scene_check(&fs, &err)) { fprintf(stderr, "scene: %s (%d)\n", err.c_str(), e); return 1; }
+    DevScene S{};
+    int feat = 0;
+    auto put = [&](auto *src, size_t count, auto **dst) -> int {
+        using T = std::remove_const_t<std::remove_pointer_t<decltype(src)>>;
+        T *p = static_cast<T *>(halloc(std::max<size_t>(count, 1) * sizeof(T), false));
+        if (count) memcpy(p, src, count * sizeof(T));
+        *dst = p;
+        return 0;
+    };
+    if (int e = scene_build(&fs, 0, S, &feat, put, &err)) { fprintf(stderr, "scene: %s (%d)\n", err.c_str(), e); return 1; }
+    if (S.kdInLds) memcpy(pgd_kd_lds, S.kdPack, (size_t)S.nKd * 32);
+    // items
+    std::vector<int3> keys;
+    if (keyFile) {
+        FILE *f = fopen(keyFile, "rb");
+        if (!f) { fprintf(stderr, "cannot open %s\n", keyFile); return 1; }
+        int3 k;
+        while (fread(&k, 12, 1, f) == 1) keys.push_back(k);
+        fclose(f);
+    } else {
+        const pbrtgpu_camera &c = fs.camera;
+        for (int y = c.sy_start; y < c.sy_end; ++y)
+            for (int x = c.sx_start; x < c.sx_end; ++x)
+                for (int s = 0; s < fs.spp; ++s) keys.push_back(make_int3(x, y, s));
+    }
+    const uint32_t nItems = (uint32_t)keys.size() * (uint32_t)S.specItems;
+    ItemSrc src{};
+    src.pix = nullptr;
+    src.sb = 1;
+    src.s0 = 0;
+    src.keys = keys.data();
+    src.keyBase = 0;
+    src.nItems = nItems;
+    src.base = 0;
+    const bool dl = S.integrator == PBRTGPU_INTEGRATOR_DIRECT;
+    const int nFrames = dl ? std::max(1, S.maxDepth) : 0;
+    const int batch = dl ? std::max(1, std::min(S.dlStrategy == PBRTGPU_DL_ONE ? 1 : S.dlK, 8)) : 1;
+    PathSoA P = make_soa(64 * nSlots, S.nb, S.nInsts, nFrames, batch);
+    const size_t rows = S.specMode == 1 ? keys.size() : nItems;
+    std::vector<float> Lout(rows * (size_t)S.nb, NAN);
+    int rc;
+    switch (S.nb) {
+        case 32: rc = run_nb<32>(S, P, src, nSlots, feat, Lout.data(), &err); break;
+        case 60: rc = run_nb<60>(S, P, src, nSlots, feat, Lout.data(), &err); break;
+        case 30: rc = run_nb<30>(S, P, src, nSlots, feat, Lout.data(), &err); break;
+        case 3: rc = run_nb<3>(S, P, src, nSlots, feat, Lout.data(), &err); break;
+        default: err = "band count"; rc = 2;
+    }
+    if (rc) { fprintf(stderr, "replay: %s\n", err.c_str()); return rc; }
+    FILE *f = fopen(out, "wb");
+    if (!f || fwrite(Lout.data(), 4, Lout.size(), f) != Lout.size()) { fprintf(stderr, "cannot write %s\n", out); return 1; }
+    fclose(f);
+    printf("shade_host: %u items, %d bands, integrator %d, %d slots, poison %d\n", nItems, S.nb, S.integrator, nSlots,
+           g_poison);
+    for (void *p : g_blocks) free(p);
+    pbrthost_free(hs);
+    return 0;
+}
