@@ -366,6 +366,11 @@ int pbrtgpu_trace_paths(pbrtgpu_ctx *ctx, const int32_t *keys, int32_t n, float 
  * prim = -1 on miss; occluded_out [n] (may be NULL). */
 int pbrtgpu_intersect(pbrtgpu_ctx *ctx, const float *rays, int32_t n, float *hits_out,
                       int32_t *occluded_out);
+/* The first n outputs of the path RNG as the device draws them (parity hook for RNG,
+ * core/rng.cpp:35-100: Seed(seed) then n RandomUInt()): the 5-word window for outputs 0-226,
+ * the full 624-word state rebuilt at output 227 and twisted every 624 after it (device.h
+ * mt_uint_ext).  out [n] uint32.  Needs no scene. */
+int pbrtgpu_mt_sequence(pbrtgpu_ctx *ctx, uint32_t seed, int32_t n, uint32_t *out);
 /* GPU BVH build (the host front end's SAH build restates
  * accelerators/bvh.cpp:145-351 node for node and stays the default, since the bit-exact
  * traversal order rests on it).  A linear BVH (Morton codes, radix sort, Karras radix tree,

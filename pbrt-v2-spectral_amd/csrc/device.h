@@ -166,9 +166,10 @@ struct MT {
     uint32_t m;        // mt[k+397]
     bool init;
     uint32_t seed;
+    uint32_t *ext;     // the slot's full 624-word state for outputs k >= 227, or null (mt_ext)
 };
 PGD_INLINE uint32_t mt_next_word(uint32_t prev, uint32_t idx) { return 1812433253U * (prev ^ (prev >> 30)) + idx; }
-PGD_INLINE void mt_begin(MT &r, uint32_t seed) { r.seed = seed; r.init = false; r.k = 0; }
+PGD_INLINE void mt_begin(MT &r, uint32_t seed) { r.seed = seed; r.init = false; r.k = 0; r.ext = nullptr; }
 // the seed recurrence up to mt[397]: once per path, before its first draw (one copy; a
 // fully unrolled 396-step loop at every draw site would dominate the shade kernel's code)
 __device__ __attribute__((noinline)) void mt_init(MT &r) {
@@ -180,19 +181,48 @@ __device__ __attribute__((noinline)) void mt_init(MT &r) {
     r.m = w;
     r.init = true;
 }
-PGD_INLINE uint32_t mt_uint(MT &r) {   // requires r.init (mt_init)
-    uint32_t y = (r.a & 0x80000000U) | (r.b & 0x7fffffffU);
-    y = r.m ^ (y >> 1) ^ ((y & 1U) ? 0x9908b0dfU : 0U);
-    // advance the recurrence windows
-    r.a = r.b;
-    r.b = mt_next_word(r.b, r.k + 2);
-    r.m = mt_next_word(r.m, r.k + 398);
-    r.k++;
+PGD_INLINE uint32_t mt_temper(uint32_t y) {
     y ^= (y >> 11);
     y ^= (y << 7) & 0x9d2c5680U;
     y ^= (y << 15) & 0xefc60000U;
     y ^= (y >> 18);
     return y;
+}
+PGD_INLINE uint32_t mt_mix(uint32_t a, uint32_t b, uint32_t m) {   // one twist step (rng.cpp:68-78)
+    const uint32_t y = (a & 0x80000000U) | (b & 0x7fffffffU);
+    return m ^ (y >> 1) ^ ((y & 1U) ? 0x9908b0dfU : 0U);
+}
+// Outputs k >= 227 of RNG (rng.cpp:60-100): from there on a twist step reads words the same
+// generation already rewrote, so the 5-word window no longer suffices.  The path's full state
+// lives in its slot's ext row (PathSoA::mtExt, allocated when maxdepth allows so many draws):
+// at k = 227 it is rebuilt from the seed (Seed + the first twist of the whole array), at
+// k = 624 j (j >= 1) twisted in place, exactly as RNG::RandomUInt regenerates; output k is
+// the tempered word k mod 624.  Out of line: paths get here only beyond ~20 bounces.
+__device__ __attribute__((noinline)) uint32_t mt_uint_ext(MT &r) {
+    uint32_t *mt = r.ext;
+    if (r.k == 227 || r.k % 624 == 0) {
+        if (r.k == 227) {
+            mt[0] = r.seed;
+            for (uint32_t i = 1; i < 624; ++i) mt[i] = mt_next_word(mt[i - 1], i);
+        }
+        int kk = 0;
+        for (; kk < 624 - 397; ++kk) mt[kk] = mt_mix(mt[kk], mt[kk + 1], mt[kk + 397]);
+        for (; kk < 623; ++kk) mt[kk] = mt_mix(mt[kk], mt[kk + 1], mt[kk + (397 - 624)]);
+        mt[623] = mt_mix(mt[623], mt[0], mt[396]);
+    }
+    const uint32_t y = mt[r.k % 624];
+    r.k++;
+    return mt_temper(y);
+}
+PGD_INLINE uint32_t mt_uint(MT &r) {   // requires r.init (mt_init)
+    if (r.k >= 227) return r.ext ? mt_uint_ext(r) : 0u;   // no ext row: refused at upload (maxdepth)
+    uint32_t y = mt_mix(r.a, r.b, r.m);
+    // advance the recurrence windows
+    r.a = r.b;
+    r.b = mt_next_word(r.b, r.k + 2);
+    r.m = mt_next_word(r.m, r.k + 398);
+    r.k++;
+    return mt_temper(y);
 }
 PGD_INLINE float mt_float(MT &r) { return (mt_uint(r) & 0xffffff) / (float)(1 << 24); }
 

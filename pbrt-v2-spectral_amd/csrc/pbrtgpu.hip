@@ -667,6 +667,16 @@ __global__ __launch_bounds__(kTraceBlock) void k_intersect(DevScene S, const flo
     occ[k] = bvh_intersectP(S, st, r2) ? 1 : 0;
 }
 
+// pbrtgpu_mt_sequence: one lane draws the RNG's first n outputs with the shading code's MT
+__global__ void k_mt_sequence(uint32_t seed, int n, uint32_t *out, uint32_t *ext) {
+    if (threadIdx.x != 0) return;
+    MT r;
+    mt_begin(r, seed);
+    mt_init(r);
+    r.ext = ext;
+    for (int i = 0; i < n; ++i) out[i] = mt_uint(r);
+}
+
 // ------------------------------------------------------------------ context
 struct DevBuf {
     void *p = nullptr;
@@ -697,6 +707,7 @@ struct Lane {
     DevBuf slots;            // PathSoA storage
     DevBuf spill;            // k_trace_pt stack spill areas (closest, shadow)
     int slotCap = 0, slotNb = 0, slotInst = 0, slotFrames = 0, slotBatch = 0;
+    bool slotMtExt = false;
     PathSoA P{};
     hipStream_t s = nullptr, s2 = nullptr;
     hipEvent_t ev[2 + 6 * 8] = {};
@@ -773,6 +784,10 @@ static int top_nodes() {
     const int v = e ? atoi(e) : kTopNodes;
     return std::max(0, std::min(v, kTopNodes));
 }
+static bool mt_ext_forced() {
+    const char *e = getenv("PBRTGPU_MT_EXT");
+    return e && atoi(e) != 0;
+}
 static bool serial_mode() {
     const char *e = getenv("PBRTGPU_SERIAL");
     return e && atoi(e) != 0;
@@ -790,9 +805,9 @@ static size_t frame_bytes(int NB) { return (size_t)8 * ((NB + 3) / 4 * 4) + 104;
 // DirectLighting bytes per slot and batched light sample: A, B terms and the ray records
 static size_t batch_bytes(int NB) { return (size_t)8 * ((NB + 3) / 4 * 4) + 27 * 4 + 8 + 8 + 4 + 24; }
 // batch: ray slots per slot (light samples a DirectLighting pass issues; 1 for the other integrators)
-static int ensure_slots(Lane *c, int cap, int NB, int nInst, int nFrames, int batch) {
+static int ensure_slots(Lane *c, int cap, int NB, int nInst, int nFrames, int batch, bool mtExt) {
     if (c->slotCap == cap && c->slotNb == NB && c->slotInst == nInst && c->slotFrames == nFrames &&
-        c->slotBatch == batch)
+        c->slotBatch == batch && c->slotMtExt == mtExt)
         return 0;
     const size_t C = (size_t)cap, R = C * (size_t)batch, AB = (size_t)std::max(2, batch);
     const int NBP = (NB + 3) / 4 * 4;   // bands padded to whole float4 quads
@@ -807,7 +822,8 @@ static int ensure_slots(Lane *c, int cap, int NB, int nInst, int nFrames, int ba
            oBMask = take(3 * ((C + 63) / 64) * 8), oMMask = take(2 * ((C + 63) / 64) * 8);
     const size_t F = (size_t)nFrames;
     size_t oFL = take(C * F * NBP * 4), oFF = take(C * F * NBP * 4), oFRay = take(C * F * 36), oFDiff = take(C * F * 48),
-           oFS = take(C * F * 8), oFHit = take(C * F * 8), oFBr = take(C * F * 4), oDlk = take(nFrames ? C * 4 : 0);
+           oFS = take(C * F * 8), oFHit = take(C * F * 8), oFBr = take(C * F * 4), oDlk = take(nFrames ? C * 4 : 0),
+           oMtExt = take(mtExt ? C * 624 * 4 : 0);
     HIPCHK(c->slots.ensure(off));
     char *base = (char *)c->slots.p;
     PathSoA &P = c->P;
@@ -837,6 +853,8 @@ static int ensure_slots(Lane *c, int cap, int NB, int nInst, int nFrames, int ba
     P.fHit = nFrames ? (int *)(base + oFHit) : nullptr;
     P.fBr = nFrames ? (uint32_t *)(base + oFBr) : nullptr;
     P.dlk = nFrames ? (uint32_t *)(base + oDlk) : nullptr;
+    P.mtExt = mtExt ? (uint32_t *)(base + oMtExt) : nullptr;
+    c->slotMtExt = mtExt;
     c->slotFrames = nFrames;
     c->slotBatch = batch;
     c->slotCap = cap;
@@ -894,7 +912,13 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
     // passes one path can take: the camera ray + maxdepth + 1 vertices + 1 finish (path); per
     // vertex of the DirectLighting recursion (at most 2^maxdepth - 1) its hit + one pass per
     // light sample, + the output
-    const int64_t pathPasses = dl ? (((int64_t)1 << nFrames) - 1) * (c->S.dlK + 1) + 2 : c->S.maxDepth + 3;
+    const int64_t pathPasses = dl ? (nFrames >= 40 ? ((int64_t)1 << 60) : (((int64_t)1 << nFrames) - 1) * (c->S.dlK + 1) + 2)
+                                  : c->S.maxDepth + 3;
+    // paths that may draw past the first 227 MT19937 outputs keep their full state in an ext row
+    // (device.h mt_uint_ext): path integrator maxdepth > 20 (at most 11 draws per vertex beyond
+    // the sampler's 3 bounces), DirectLighting maxdepth > 6 (6 per specular vertex, up to
+    // 2^(maxdepth-1) - 1 of them); PBRTGPU_MT_EXT=1 forces the rows (tests)
+    const bool mtExt = (dl ? c->S.maxDepth > 6 : c->S.maxDepth > 20) || mt_ext_forced();
     struct Run { Lane *L; ItemSrc src; int cap, grid, q, batch, passes, maxPasses; bool done; };
     Run R[kLanes];
     const bool serial = serial_mode();
@@ -912,6 +936,7 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
         if (dl)   // the frame stacks and light-sample batches: at most 24 GiB per lane
             r.cap = (int)std::max<size_t>(64, std::min<size_t>((size_t)r.cap, ((size_t)24 << 30) /
                                                                (frame_bytes(NB) * nFrames + batch_bytes(NB) * batch)));
+        if (mtExt && !getenv("PBRTGPU_SLOTS")) r.cap = std::min(r.cap, 1 << 20);   // 2.5 KiB of MT state per slot
         r.grid = (r.cap + kShadeBlock - 1) / kShadeBlock;
         r.q = 0;
         r.batch = 0;
@@ -922,7 +947,7 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
         r.passes = 0;
         r.maxPasses = (int)std::min<int64_t>(INT32_MAX / 2, 2 * ((r.src.nItems + r.cap - 1) / r.cap + 1) * pathPasses) +
                       2 * kPassBatch;
-        if (int e = ensure_slots(&L, r.cap, NB, c->S.nInsts, nFrames, batch)) return e;
+        if (int e = ensure_slots(&L, r.cap, NB, c->S.nInsts, nFrames, batch, mtExt)) return e;
         HIPCHK(L.spill.ensure(2 * spillLane * sizeof(uint2)));
         if (l > 0) HIPCHK(hipStreamWaitEvent(L.s, c->ev[0], 0));
         if (const int pb = poison_byte(); pb >= 0) {
@@ -1607,6 +1632,19 @@ int pbrtgpu_loop_subdivide(pbrtgpu_ctx *c, int32_t nf, int32_t nv, const int32_t
 int pbrtgpu_loop_subdivide_hook(void *ctx, int32_t nf, int32_t nv, const int32_t *vi, const float *P, int32_t levels,
                                 int32_t *nv_out, float *P_out, float *N_out, int32_t *vi_out) {
     return pbrtgpu_loop_subdivide((pbrtgpu_ctx *)ctx, nf, nv, vi, P, levels, nv_out, P_out, N_out, vi_out, nullptr);
+}
+
+int pbrtgpu_mt_sequence(pbrtgpu_ctx *c, uint32_t seed, int32_t n, uint32_t *out) {
+    if (!c || !out || n < 0) return fail(PBRTGPU_E_INVALID, "bad arguments");
+    if (n == 0) return 0;
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(c->scratch[0].ensure((size_t)n * 4 + 624 * 4));
+    uint32_t *d = (uint32_t *)c->scratch[0].p;
+    hipLaunchKernelGGL(k_mt_sequence, dim3(1), dim3(64), 0, c->stream, seed, n, d, d + n);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(out, d, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return 0;
 }
 
 int pbrtgpu_intersect(pbrtgpu_ctx *c, const float *rays, int32_t n, float *hits, int32_t *occ) {

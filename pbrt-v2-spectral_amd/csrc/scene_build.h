@@ -133,8 +133,7 @@ static inline int scene_check(const pbrtgpu_flat_scene *s, std::string *err) {
     if (s->n_bands == 3 && s->renderer == PBRTGPU_RENDERER_SPECTRAL)
         SB_FAIL(PBRTGPU_E_UNSUPPORTED, "RGB build: the SpectralRenderer needs SampledSpectrum");
     if (s->spp <= 0 || (s->spp & (s->spp - 1))) SB_FAIL(PBRTGPU_E_INVALID, "spp must be a power of two");
-    if (s->max_depth < 0 || s->max_depth > 20)
-        SB_FAIL(PBRTGPU_E_UNSUPPORTED, "maxdepth > 20 exceeds the first MT19937 block (DESIGN.md §3.1)");
+    if (s->max_depth < 0 || s->max_depth > 100000) SB_FAIL(PBRTGPU_E_INVALID, "maxdepth out of range");
     if (s->n_nodes <= 0 || s->n_prims <= 0) SB_FAIL(PBRTGPU_E_INVALID, "empty scene");
     if (s->integrator != PBRTGPU_INTEGRATOR_PATH && s->integrator != PBRTGPU_INTEGRATOR_DIRECT &&
         s->integrator != PBRTGPU_INTEGRATOR_METADATA)
@@ -167,10 +166,6 @@ static inline int scene_check(const pbrtgpu_flat_scene *s, std::string *err) {
     }
     if (s->integrator == PBRTGPU_INTEGRATOR_DIRECT && s->dl_strategy != PBRTGPU_DL_ALL && s->dl_strategy != PBRTGPU_DL_ONE)
         SB_FAIL(PBRTGPU_E_INVALID, "unknown DirectLighting strategy");
-    // DirectLighting draws 6 MT19937 values at each of up to 2^(maxdepth-1) - 1 specular
-    // vertices; the device stream covers the first 227
-    if (s->integrator == PBRTGPU_INTEGRATOR_DIRECT && s->max_depth > 6)
-        SB_FAIL(PBRTGPU_E_UNSUPPORTED, "DirectLighting maxdepth > 6 exceeds the first MT19937 block");
     for (int i = 0; i < s->n_lights; ++i)
         if (s->lights[i].type < PBRTGPU_LIGHT_AREA || s->lights[i].type > PBRTGPU_LIGHT_INFINITE)
             SB_FAIL(PBRTGPU_E_INVALID, "bad light type");

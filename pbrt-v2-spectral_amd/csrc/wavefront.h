@@ -74,6 +74,8 @@ struct PathSoA {
     int *bounce;        // vertex index of the last processed vertex (-1: camera ray in flight)
     uint32_t *flags;
     uint32_t *mt;       // [5][cap]: k, a, b, m, seed
+    uint32_t *mtExt;    // [cap][624]: the full MT19937 state of a path past 227 draws (device.h
+                        // mt_uint_ext), or null when the scene's maxdepth cannot get there
     float4 *beta;       // [3][NQ][cap]: beta at vertex v in buffer v % 3
     float4 *L;          // [NQ][cap]
     float4 *A, *B;      // [2][NQ][cap]: pending direct-light terms of vertex v in buffer v & 1
@@ -152,6 +154,7 @@ PGD_INLINE void mt_load(const PathSoA &P, int slot, uint32_t fl, MT &r) {
     r.k = P.mt[slot]; r.a = P.mt[c + slot]; r.b = P.mt[2 * c + slot]; r.m = P.mt[3 * c + slot];
     r.seed = P.mt[4 * c + slot];
     r.init = (fl & PF_MTINIT) != 0;
+    r.ext = P.mtExt ? P.mtExt + (size_t)slot * 624 : nullptr;
 }
 PGD_INLINE void mt_store(const PathSoA &P, int slot, const MT &r) {
     const size_t c = P.cap;

@@ -199,6 +199,7 @@ def gpu_lib():
         g.pbrtgpu_film_clear.argtypes = [P]
         g.pbrtgpu_trace_paths.argtypes = [P, P, I32, P]
         g.pbrtgpu_intersect.argtypes = [P, P, I32, P, P]
+        g.pbrtgpu_mt_sequence.argtypes = [P, ctypes.c_uint32, I32, P]
         g.pbrtgpu_path_stats.argtypes = [P, P, I32, P]
         g.pbrtgpu_last_timing.argtypes = [P, ctypes.POINTER(Timing)]
         g.pbrtgpu_film_gather.argtypes = [P, I32, I32, P, I32, P, ctypes.c_int64]
@@ -214,7 +215,7 @@ def gpu_symbols():
     return ["pbrtgpu_abi_version", "pbrtgpu_device_count", "pbrtgpu_context_create",
             "pbrtgpu_context_destroy", "pbrtgpu_last_error", "pbrtgpu_scene_upload",
             "pbrtgpu_render_tiles", "pbrtgpu_film_read", "pbrtgpu_film_clear",
-            "pbrtgpu_trace_paths", "pbrtgpu_intersect", "pbrtgpu_path_stats", "pbrtgpu_last_timing",
+            "pbrtgpu_trace_paths", "pbrtgpu_intersect", "pbrtgpu_mt_sequence", "pbrtgpu_path_stats", "pbrtgpu_last_timing",
             "pbrtgpu_film_gather", "pbrtgpu_render_multi", "pbrtgpu_build_bvh", "pbrtgpu_loop_subdivide",
             "pbrtgpu_loop_subdivide_hook"]
 
@@ -490,6 +491,12 @@ class Device:
         keys = np.ascontiguousarray(keys, dtype=np.int32).reshape(-1, 3)
         out = np.zeros((len(keys), self.scene.bands), dtype=np.float32)
         _check(self.lib.pbrtgpu_trace_paths(self.ctx, keys.ctypes.data, len(keys), out.ctypes.data))
+        return out
+
+    def mt_sequence(self, seed, n):
+        """The first n outputs of RNG(seed) as the shading kernels draw them (pbrtgpu_mt_sequence)."""
+        out = np.zeros(n, np.uint32)
+        _check(self.lib.pbrtgpu_mt_sequence(self.ctx, seed, n, out.ctypes.data))
         return out
 
     def intersect(self, rays):

@@ -404,6 +404,33 @@ def test_direct_lighting_recursion_and_regeneration(pg, monkeypatch, strategy, m
     assert np.abs(L - Lo).max() / np.abs(Lo).max() < 1e-4
 
 
+def test_rng_sequence_matches_reference(pg):
+    """The device RNG (5-word window for outputs 0-226, then the full state rebuilt and twisted
+    every 624 outputs) against the oracle's MT19937, itself pinned to the reference's
+    (test_oracle_golden.py), over 4 generations."""
+    ora = pg.oracle()
+    with pg.Device(0) as d:
+        for seed in (0, 1, 5489, 123456789, 0xdeadbeef):
+            assert np.array_equal(d.mt_sequence(seed, 2600), ora.mt_first(seed, 2600))
+
+
+@pytest.mark.parametrize("integ,md,strategy", [("directlighting", 16, "all"), ("directlighting", 20, "one"),
+                                               ("path", 60, None)])
+def test_deep_paths_past_the_first_rng_block(pg, integ, md, strategy):
+    """maxdepth beyond the first MT19937 block: DirectLighting's specular recursion on
+    coverage.pbrt's glass and mirrors at maxdepth 16 / 20 draws up to ~300 values per path, so
+    paths continue on the rebuilt full state; the path integrator at maxdepth 60.  Oracle bits."""
+    from conftest import PACKS
+    kw = dict(integrator=integ, strategy=strategy) if strategy else {}
+    scene = pg.Scene.load(os.path.join(PACKS, "coverage.pack"), xres=40, yres=30, spp=4, maxdepth=md, **kw)
+    keys = _keys(scene)
+    with pg.Device(0) as d:
+        d.upload(scene)
+        L = d.trace_paths(keys)
+    Lo = pg.oracle().trace_paths(scene, keys)
+    assert np.all(L.view(np.int32) == Lo.view(np.int32), axis=1).mean() >= 1 - 1e-4
+
+
 @pytest.mark.parametrize("integ,strategy,md", [("directlighting", "all", 6), ("directlighting", "one", 4),
                                                ("path", None, 5)])
 def test_independent_of_unwritten_state_and_slot_layout(pg, monkeypatch, integ, strategy, md):
@@ -598,18 +625,21 @@ def test_rgb_build_vs_reference_golden(pg, name):
 
 
 def test_integrator_scene_checks(pg):
-    """pbrtgpu_scene_upload refuses what the integrator steps cannot render exactly: a
-    DirectLighting maxdepth beyond the first MT19937 block (> 6), an unknown metadata strategy,
-    mesh / material ids without the per-primitive id table."""
+    """pbrtgpu_scene_upload refuses what the integrator steps cannot render: a negative
+    maxdepth, an unknown metadata strategy, mesh / material ids without the per-primitive id
+    table.  Any maxdepth the reference reads is accepted (the RNG's full state is kept once a
+    path passes 227 draws)."""
     from conftest import PACKS
     import ctypes
     pack = os.path.join(PACKS, "coverage.pack")
     with pg.Device(0) as d:
         s = pg.Scene.load(pack, xres=8, yres=8, spp=1, maxdepth=7, integrator="directlighting")
+        s.flat.max_depth = -1
         with pytest.raises(RuntimeError, match="maxdepth"):
             d.upload(s)
-        s = pg.Scene.load(pack, xres=8, yres=8, spp=1, maxdepth=6, integrator="directlighting")
-        d.upload(s)
+        for md in (6, 7, 25):
+            d.upload(pg.Scene.load(pack, xres=8, yres=8, spp=1, maxdepth=md, integrator="directlighting"))
+        d.upload(pg.Scene.load(pack, xres=8, yres=8, spp=1, maxdepth=60))
         m = pg.Scene.load(pack, xres=8, yres=8, spp=1, integrator="metadata", strategy="mesh")
         m.flat.meta_strategy = 7
         with pytest.raises(RuntimeError, match="strategy"):

@@ -96,6 +96,28 @@ def test_replay_config_golden_keys(pg, tmp_path, name, pack):
     assert np.all(L.view(np.int32) == g["L"].view(np.int32), axis=1).mean() >= exact_rate(name)
 
 
+def test_device_rng_matches_oracle(pg, tmp_path):
+    """device.h's MT19937 (5-word window, then the full state rebuilt at output 227 and twisted
+    every 624) against the oracle's, over 4 generations."""
+    exe = _build("shade_host")
+    out = str(tmp_path / "mt.u32")
+    for seed in (0, 1, 5489, 123456789, 0xdeadbeef):
+        subprocess.run([exe, str(seed), "--mt-kat", "2600", "--out", out], check=True, capture_output=True)
+        assert np.array_equal(np.fromfile(out, np.uint32), pg.oracle().mt_first(seed, 2600))
+
+
+@pytest.mark.parametrize("md,strategy", [(16, "all"), (20, "one")])
+def test_replay_deep_directlighting(pg, tmp_path, md, strategy):
+    """DirectLighting recursion deep enough that paths draw past the RNG's first 227 outputs."""
+    exe = _build("shade_host")
+    a = dict(xres=40, yres=30, spp=4, maxdepth=md, integrator="directlighting", strategy=strategy)
+    pack = os.path.join(PACKS, "coverage.pack")
+    scene = pg.Scene.load(pack, **a)
+    Lo = pg.oracle().trace_paths(scene, _keys(scene))
+    L = _replay(exe, pack, tmp_path, **a).reshape(Lo.shape)
+    assert np.array_equal(L.view(np.int32), Lo.view(np.int32))
+
+
 def test_replay_independent_of_unwritten_state(pg, tmp_path):
     """Path-slot arrays filled with 0x00, 0xff or 0x7f (NaN patterns) before the run: the same bits."""
     exe = _build("shade_host")

@@ -18,6 +18,7 @@
 // usage: shade_host SCENE [--xres N] [--yres N] [--spp N] [--maxdepth N] [--bands N]
 //                         [--integrator path|directlighting|metadata] [--strategy all|one|mesh|material|depth]
 //                         [--slots N] [--poison BYTE] [--keys FILE] --out FILE
+//        shade_host SEED --mt-kat N --out FILE     (the device RNG's first N outputs, uint32)
 // Items: every (x, y, s) of the camera's sample extent in row-major order, or the int32
 // (x, y, s) triples of --keys.  Writes float32 [items][bands] radiance to --out.
 #include <hip/hip_runtime.h>   // the stand-in of tools/hostsan/hip
@@ -50,6 +51,7 @@ using namespace pgd;
 
 static std::vector<void *> g_blocks;
 static int g_poison = -1;   // -1: leave heap blocks as allocated
+static uint32_t g_maxDraws = 0;
 
 static void *halloc(size_t bytes, bool poison) {
     const size_t n = std::max<size_t>(64, (bytes + 63) & ~(size_t)63);
@@ -92,7 +94,7 @@ static void unpoison_flat(const pbrtgpu_flat_scene *s) {
 #endif
 
 // PathSoA as pbrtgpu.hip ensure_slots lays it out, one heap block per array
-static PathSoA make_soa(int cap, int NB, int nInst, int nFrames, int batch) {
+static PathSoA make_soa(int cap, int NB, int nInst, int nFrames, int batch, bool mtExt) {
     const size_t C = (size_t)cap, R = C * (size_t)batch, AB = (size_t)std::max(2, batch), W = (C + 63) / 64;
     const size_t NQ = (size_t)(NB + 3) / 4, F = (size_t)nFrames;
     PathSoA P{};
@@ -112,6 +114,7 @@ static PathSoA make_soa(int cap, int NB, int nInst, int nFrames, int batch) {
     memset(P.cnt, 0, CNT_WORDS * 4);
     P.nInst = nInst;
     P.instM = nInst ? arr<float4>(C * (size_t)nInst * 8) : nullptr;
+    P.mtExt = mtExt ? arr<uint32_t>(C * 624) : nullptr;
     P.nFrames = nFrames;
     if (nFrames) {
         P.dlMask = arr<uint32_t>(C);
@@ -136,7 +139,8 @@ static int run(const DevScene &S, PathSoA &P, const ItemSrc &src, int nSlots, fl
     Queues Q[2];
     std::vector<uint32_t> stk((size_t)S.stackDepth + 1);
     std::vector<float> stkT((size_t)S.stackDepth + 1);
-    const int64_t pathPasses = MODE == MODE_DL ? (((int64_t)1 << P.nFrames) - 1) * (S.dlK + 1) + 2 : S.maxDepth + 3;
+    const int64_t pathPasses = MODE == MODE_DL ? (P.nFrames >= 40 ? ((int64_t)1 << 60) : (((int64_t)1 << P.nFrames) - 1) * (S.dlK + 1) + 2)
+                                               : S.maxDepth + 3;
     const int64_t maxPasses = 2 * ((src.nItems + nSlots - 1) / nSlots + 1) * pathPasses + 8;
     auto push = [&](int q, const Pushes &pu, int slot) {
         if (pu.c) Q[q].c.push_back((uint32_t)slot << 1);
@@ -147,6 +151,10 @@ static int run(const DevScene &S, PathSoA &P, const ItemSrc &src, int nSlots, fl
             if (pu.m) Q[q].c.push_back(((uint32_t)(MODE == MODE_PATH ? pu.mIdx : slot) << 1) | 1u);
             if (pu.s) Q[q].s.push_back((uint32_t)(MODE == MODE_PATH ? pu.sIdx : slot));
         }
+    };
+    // MT19937 outputs a finished path drew (the most of any path is reported: > 227 exercises mt_uint_ext)
+    auto note_draws = [&](int slot) {
+        if (P.flags[slot] & PF_MTINIT) g_maxDraws = std::max(g_maxDraws, P.mt[slot]);
     };
     // one k_shade pass (+ k_dl_nee): the per-thread body of shade.hip k_shade for every slot
     auto shade = [&](int qout) -> uint32_t {
@@ -167,7 +175,7 @@ static int run(const DevScene &S, PathSoA &P, const ItemSrc &src, int nSlots, fl
                 } else if (MODE == MODE_DL) pu = shade_slot_dl<NB, FEAT>(S, P, slot, Lout, &done, &zeroed);
                 else if (MODE == MODE_META) pu = shade_slot_meta<NB, FEAT>(S, P, slot, Lout, &done, &zeroed);
                 else pu = shade_slot<NB, FEAT>(S, P, slot, Lout, &done, &zeroed, qout);
-                if (done) { P.item[slot] = -1; freeSlot = true; ++finished; }
+                if (done) { P.item[slot] = -1; freeSlot = true; ++finished; note_draws(slot); }
             }
             push(qout, pu, slot);
             if (freeSlot && next < src.nItems) {
@@ -191,7 +199,7 @@ static int run(const DevScene &S, PathSoA &P, const ItemSrc &src, int nSlots, fl
                 bool done = false, zeroed = false;
                 if (P.item[slot] >= 0 && (P.flags[slot] & PF_DLSPEC)) {
                     pu = dl_spec_step<NB, FEAT>(S, P, slot, Lout, &done, &zeroed);
-                    if (done) { P.item[slot] = -1; ++finished; ++idle; }
+                    if (done) { P.item[slot] = -1; ++finished; ++idle; note_draws(slot); }
                 }
                 push(qout, pu, slot);
             }
@@ -252,7 +260,7 @@ int main(int argc, char **argv) {
         return 2;
     }
     pbrthost_overrides ov = {-1, -1, -1, -1, 0, PBRTHOST_KEEP_SEED, -1, -1, -1, -1, -1, -1};
-    int nSlots = 256;
+    int nSlots = 256, mtKat = 0;
     const char *out = nullptr, *keyFile = nullptr, *strategy = nullptr;
     for (int i = 2; i + 1 < argc; i += 2) {
         const std::string a = argv[i];
@@ -267,6 +275,7 @@ int main(int argc, char **argv) {
         else if (a == "--out") out = v;
         else if (a == "--keys") keyFile = v;
         else if (a == "--strategy") strategy = v;
+        else if (a == "--mt-kat") mtKat = atoi(v);
         else if (a == "--integrator")
             ov.integrator = !strcmp(v, "directlighting") ? PBRTGPU_INTEGRATOR_DIRECT
                             : !strcmp(v, "metadata")     ? PBRTGPU_INTEGRATOR_METADATA
@@ -281,6 +290,19 @@ int main(int argc, char **argv) {
         else if (!strcmp(strategy, "depth")) ov.meta_strategy = PBRTGPU_META_DEPTH;
     }
     if (!out) { fprintf(stderr, "--out FILE is required\n"); return 2; }
+    if (mtKat) {   // the device RNG's first n outputs (mt_uint / mt_uint_ext) for seed = argv[1]
+        const uint32_t seed = (uint32_t)strtoul(argv[1], nullptr, 0);
+        std::vector<uint32_t> ext(624), seq((size_t)mtKat);
+        MT r;
+        mt_begin(r, seed);
+        mt_init(r);
+        r.ext = ext.data();
+        for (int i = 0; i < mtKat; ++i) seq[(size_t)i] = mt_uint(r);
+        FILE *f = fopen(out, "wb");
+        if (!f || fwrite(seq.data(), 4, seq.size(), f) != seq.size()) { fprintf(stderr, "cannot write %s\n", out); return 1; }
+        fclose(f);
+        return 0;
+    }
     char msg[512] = {0};
     pbrthost_scene *hs = nullptr;
     pbrtgpu_flat_scene fs;
@@ -339,7 +361,8 @@ int main(int argc, char **argv) {
     const bool dl = S.integrator == PBRTGPU_INTEGRATOR_DIRECT;
     const int nFrames = dl ? std::max(1, S.maxDepth) : 0;
     const int batch = dl ? std::max(1, std::min(S.dlStrategy == PBRTGPU_DL_ONE ? 1 : S.dlK, 8)) : 1;
-    PathSoA P = make_soa(64 * nSlots, S.nb, S.nInsts, nFrames, batch);
+    const bool mtExt = dl ? S.maxDepth > 6 : S.maxDepth > 20;   // as pbrtgpu.hip run_wavefront
+    PathSoA P = make_soa(64 * nSlots, S.nb, S.nInsts, nFrames, batch, mtExt);
     const size_t rows = S.specMode == 1 ? keys.size() : nItems;
     std::vector<float> Lout(rows * (size_t)S.nb, NAN);
     int rc;
@@ -354,8 +377,8 @@ int main(int argc, char **argv) {
     FILE *f = fopen(out, "wb");
     if (!f || fwrite(Lout.data(), 4, Lout.size(), f) != Lout.size()) { fprintf(stderr, "cannot write %s\n", out); return 1; }
     fclose(f);
-    printf("shade_host: %u items, %d bands, integrator %d, %d slots, poison %d\n", nItems, S.nb, S.integrator, nSlots,
-           g_poison);
+    printf("shade_host: %u items, %d bands, integrator %d, %d slots, poison %d, most MT draws of a path %u\n", nItems,
+           S.nb, S.integrator, nSlots, g_poison, g_maxDraws);
     for (void *p : g_blocks) free(p);
     pbrthost_free(hs);
     return 0;
