@@ -197,12 +197,12 @@ PGD_INLINE uint32_t mt_mix(uint32_t a, uint32_t b, uint32_t m) {   // one twist 
 // lives in its slot's ext row (PathSoA::mtExt, allocated when maxdepth allows so many draws):
 // at k = 227 it is rebuilt from the seed (Seed + the first twist of the whole array), at
 // k = 624 j (j >= 1) twisted in place, exactly as RNG::RandomUInt regenerates; output k is
-// the tempered word k mod 624.  Out of line: paths get here only beyond ~20 bounces.
-__device__ __attribute__((noinline)) uint32_t mt_uint_ext(MT &r) {
-    uint32_t *mt = r.ext;
-    if (r.k == 227 || r.k % 624 == 0) {
-        if (r.k == 227) {
-            mt[0] = r.seed;
+// the tempered word k mod 624.  Out of line, scalars in and out (no MT in private memory at
+// the draw sites): paths get here only beyond ~20 bounces.
+__device__ __attribute__((noinline)) uint32_t mt_ext_draw(uint32_t k, uint32_t seed, uint32_t *mt) {
+    if (k == 227 || k % 624 == 0) {
+        if (k == 227) {
+            mt[0] = seed;
             for (uint32_t i = 1; i < 624; ++i) mt[i] = mt_next_word(mt[i - 1], i);
         }
         int kk = 0;
@@ -210,12 +210,14 @@ __device__ __attribute__((noinline)) uint32_t mt_uint_ext(MT &r) {
         for (; kk < 623; ++kk) mt[kk] = mt_mix(mt[kk], mt[kk + 1], mt[kk + (397 - 624)]);
         mt[623] = mt_mix(mt[623], mt[0], mt[396]);
     }
-    const uint32_t y = mt[r.k % 624];
-    r.k++;
-    return mt_temper(y);
+    return mt_temper(mt[k % 624]);
 }
 PGD_INLINE uint32_t mt_uint(MT &r) {   // requires r.init (mt_init)
-    if (r.k >= 227) return r.ext ? mt_uint_ext(r) : 0u;   // no ext row: refused at upload (maxdepth)
+    if (__builtin_expect(r.k >= 227, 0)) {   // no ext row: refused at upload (maxdepth)
+        const uint32_t y = r.ext ? mt_ext_draw(r.k, r.seed, r.ext) : 0u;
+        r.k++;
+        return y;
+    }
     uint32_t y = mt_mix(r.a, r.b, r.m);
     // advance the recurrence windows
     r.a = r.b;

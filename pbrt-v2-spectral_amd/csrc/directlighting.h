@@ -247,6 +247,140 @@ PGD_INLINE void dl_pop(const PathSoA &P, int d, int slot, const float4 (&Lr)[Ban
     }
 }
 
+// k_dl_spec body for a slot marked PF_DLSPEC: SpecularReflect, then SpecularTransmit
+// (integrator.cpp:169-250) of the top frame d -- each draws BSDFSample(rng) (3 MT19937 values,
+// in the reference's order: reflect, its whole subtree, transmit) and queues its child ray with
+// the ray differentials -- and, once a frame has no branch left, its pop into the parent and the
+// parent's remaining branches, down to the camera sample's output at depth 0.
+// Returns the ray requests; *done when the sample's radiance is in Lout.
+// SPAWN = false (k_shade): only frames that cannot sample a specular child (not mirror or glass,
+// or at maxdepth) are completed and popped -- the common case, cheap enough to run inline -- and
+// the first frame that could branch is left to k_dl_spec (PF_DLSPEC).
+template <int NB, int FEAT, bool SPAWN = true>
+PGD_INLINE Pushes dl_spec_step(const DevScene &S, const PathSoA &P, int slot, float *__restrict__ Lout, bool *done,
+                               bool *zeroed) {
+    constexpr int NQ = Bands<NB>::NQ;
+    const size_t c = P.cap;
+    const float *sp = S.spectra;
+    uint32_t fl = P.flags[slot] & ~PF_DLSPEC;
+    int d = P.bounce[slot];
+    Pushes out = {false, false, false, 0u, 0u};
+    *done = false;
+    *zeroed = false;
+    MT rng;
+    bool rngLoaded = false;
+    for (;;) {
+        // ---- the specular branches of frame d
+        uint32_t br = P.fBr[(size_t)d * c + slot];
+        bool spawned = false;
+        // only mirror and glass have specular BxDFs: elsewhere the two BSDFSample(rng) draws
+        // still happen (the reference constructs them) but no child can be sampled, and the
+        // vertex need not be rebuilt
+        const int vprim = P.fHit[(size_t)2 * d * c + slot];
+        const int vtype = S.mats[S.prims[vprim].material].type;
+        const bool canSpec = vtype == PBRTGPU_MAT_MIRROR || vtype == PBRTGPU_MAT_GLASS;
+        if (!SPAWN && canSpec && d + 1 < S.maxDepth && br < 2u) {
+            fl |= PF_DLSPEC;
+            break;
+        }
+        while (d + 1 < S.maxDepth && br < 2u) {
+            if (!rngLoaded) {
+                mt_load(P, slot, fl, rng);
+                if (!rng.init) mt_init(rng);
+                rngLoaded = true;
+            }
+            const float u0 = mt_float(rng), u1 = mt_float(rng), uc = mt_float(rng);   // BSDFSample(rng)
+            const bool refl = br == 0u;
+            ++br;
+            if (!SPAWN || !canSpec) continue;
+            DLVertex vx;
+            dl_vertex<NB, FEAT>(S, P, slot, d, vx);
+            const int flags = BSDF_SPECULAR | (refl ? BSDF_REFLECTION : BSDF_TRANSMISSION);
+            FVal F;
+            V wi;
+            float pdf;
+            (void)u0; (void)u1;   // the specular BxDFs ignore the two direction values
+            bsdf_sample_specular(vx.bs, vx.wo, &wi, uc, &pdf, flags, F);
+            if (!(pdf > 0.f)) continue;   // no matching BxDF: wi is not set
+            const float ad = fabsf(vdot(wi, vx.n));
+            if (ad == 0.f || (F.mode == FV_SUM && F.n == 0)) continue;
+            float4 *mb = P.M + slot, *kb = P.K + slot;
+            fval_prepare<NB, FEAT>(S, F, mb, c);
+            float4 *Fo = dl_F<NB>(P, d, slot);
+            bool black = true;
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                const float4 f = fval4<FEAT>(sp, F, q, mb, kb, c);
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    if (4 * q + i < NB) black = black && (cmp(f, i) == 0.);
+                Fo[q * c] = f;
+            }
+            if (black) continue;
+            P.fS[(size_t)2 * d * c + slot] = ad;
+            P.fS[(size_t)(2 * d + 1) * c + slot] = pdf;
+            // the child ray and its differentials (the camera's rays always carry them)
+            Ray cr;
+            cr.o = vx.p; cr.d = wi; cr.mint = vx.is.rayEps; cr.maxt = INFINITY; cr.time = vx.ray.time;
+            ray_store(P, RAY_C, slot, cr);
+            const V n = vx.n, wo = vx.wo;
+            const V rxo = vadd(vx.p, vx.dpdx), ryo = vadd(vx.p, vx.dpdy);
+            const V dndx = vadd(vmul(vx.dn[0], vx.diff[0]), vmul(vx.dn[1], vx.diff[1]));
+            const V dndy = vadd(vmul(vx.dn[0], vx.diff[2]), vmul(vx.dn[1], vx.diff[3]));
+            const V dwodx = vsub(vneg(vx.rd.rxd), wo), dwody = vsub(vneg(vx.rd.ryd), wo);
+            const float dDNdx = vdot(dwodx, n) + vdot(wo, dndx);
+            const float dDNdy = vdot(dwody, n) + vdot(wo, dndy);
+            V rxd, ryd;
+            if (refl) {
+                const float won = vdot(wo, n);
+                rxd = vadd(vsub(wi, dwodx), vmul(vadd(vmul(dndx, won), vmul(n, dDNdx)), 2.f));
+                ryd = vadd(vsub(wi, dwody), vmul(vadd(vmul(dndy, won), vmul(n, dDNdy)), 2.f));
+            } else {
+                // BSDF::eta: the glass material's index, 1 otherwise (glass.cpp:48)
+                const pbrtgpu_material &mt = S.mats[S.prims[vx.is.prim].material];
+                float eta = mt.type == PBRTGPU_MAT_GLASS ? mt.f[0] : 1.f;
+                const V w = vneg(wo);
+                if (vdot(wo, n) < 0) eta = 1.f / eta;
+                const float mu = eta * vdot(w, n) - vdot(wi, n);
+                const float dmudx = (eta - (eta * eta * vdot(w, n)) / vdot(wi, n)) * dDNdx;
+                const float dmudy = (eta - (eta * eta * vdot(w, n)) / vdot(wi, n)) * dDNdy;
+                rxd = vsub(vadd(wi, vmul(dwodx, eta)), vadd(vmul(dndx, mu), vmul(n, dmudx)));
+                ryd = vsub(vadd(wi, vmul(dwody, eta)), vadd(vmul(dndy, mu), vmul(n, dmudy)));
+            }
+            float *fd = P.fDiff + (size_t)(d + 1) * 12 * c + slot;
+            dl_vec_store(fd, c, rxo);
+            dl_vec_store(fd + 3 * c, c, rxd);
+            dl_vec_store(fd + 6 * c, c, ryo);
+            dl_vec_store(fd + 9 * c, c, ryd);
+            fl |= PF_CONT;
+            out.c = true;
+            spawned = true;
+            break;
+        }
+        P.fBr[(size_t)d * c + slot] = br;
+        if (spawned) break;
+        // ---- frame d is complete: Li = (1 * L) + 0 goes to its parent, or is the sample's
+        float4 Lr[NQ];
+        const float4 *Lv = dl_L<NB>(P, d, slot);
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) Lr[q] = Lv[q * c];
+        if (d == 0) {
+            *zeroed = path_output<NB>(S, Lr, Lout, P.item[slot], P.smp[slot]);   // rayWeight * ((1 * L) + 0), guarded
+            *done = true;
+            break;
+        }
+        --d;
+        dl_pop<NB>(P, d, slot, Lr);
+    }
+    if (rngLoaded) {
+        mt_store(P, slot, rng);
+        if (rng.init) fl |= PF_MTINIT;
+    }
+    P.bounce[slot] = d;
+    P.flags[slot] = fl;
+    return out;
+}
+
 // k_shade body of the DirectLighting integrator for one slot (see the file comment): the
 // answers of the last pass -- a light-sample batch's shadow / MIS rays (added in sample order),
 // or the camera / specular child ray (a hit pushes its frame, a miss pops straight into the
@@ -355,141 +489,18 @@ PGD_INLINE Pushes shade_slot_dl(const DevScene &S, const PathSoA &P, int slot, f
             spec = nLights == 0;
         }
     }
-    fl |= spec ? PF_DLSPEC : PF_DLNEE;
 #ifdef PGD_DL_TRACE_ITEM
-    if (trc) printf("[dl]   -> d %d fl %x k %d\n", d, fl, k);
+    if (trc) printf("[dl]   -> d %d fl %x k %d spec %d\n", d, fl, k, (int)spec);
 #endif
     P.bounce[slot] = d;
     P.dlk[slot] = (uint32_t)k;
-    P.flags[slot] = fl;
-    return out;
-}
-
-// k_dl_spec body for a slot marked PF_DLSPEC: SpecularReflect, then SpecularTransmit
-// (integrator.cpp:169-250) of the top frame d -- each draws BSDFSample(rng) (3 MT19937 values,
-// in the reference's order: reflect, its whole subtree, transmit) and queues its child ray with
-// the ray differentials -- and, once a frame has no branch left, its pop into the parent and the
-// parent's remaining branches, down to the camera sample's output at depth 0.
-// Returns the ray requests; *done when the sample's radiance is in Lout.
-template <int NB, int FEAT>
-PGD_INLINE Pushes dl_spec_step(const DevScene &S, const PathSoA &P, int slot, float *__restrict__ Lout, bool *done,
-                               bool *zeroed) {
-    constexpr int NQ = Bands<NB>::NQ;
-    const size_t c = P.cap;
-    const float *sp = S.spectra;
-    uint32_t fl = P.flags[slot] & ~PF_DLSPEC;
-    int d = P.bounce[slot];
-    Pushes out = {false, false, false, 0u, 0u};
-    *done = false;
-    *zeroed = false;
-    MT rng;
-    bool rngLoaded = false;
-    for (;;) {
-        // ---- the specular branches of frame d
-        uint32_t br = P.fBr[(size_t)d * c + slot];
-        bool spawned = false;
-        // only mirror and glass have specular BxDFs: elsewhere the two BSDFSample(rng) draws
-        // still happen (the reference constructs them) but no child can be sampled, and the
-        // vertex need not be rebuilt
-        const int vprim = P.fHit[(size_t)2 * d * c + slot];
-        const int vtype = S.mats[S.prims[vprim].material].type;
-        const bool canSpec = vtype == PBRTGPU_MAT_MIRROR || vtype == PBRTGPU_MAT_GLASS;
-        while (d + 1 < S.maxDepth && br < 2u) {
-            if (!rngLoaded) {
-                mt_load(P, slot, fl, rng);
-                if (!rng.init) mt_init(rng);
-                rngLoaded = true;
-            }
-            const float u0 = mt_float(rng), u1 = mt_float(rng), uc = mt_float(rng);   // BSDFSample(rng)
-            const bool refl = br == 0u;
-            ++br;
-            if (!canSpec) continue;
-            DLVertex vx;
-            dl_vertex<NB, FEAT>(S, P, slot, d, vx);
-            const int flags = BSDF_SPECULAR | (refl ? BSDF_REFLECTION : BSDF_TRANSMISSION);
-            FVal F;
-            V wi;
-            float pdf;
-            (void)u0; (void)u1;   // the specular BxDFs ignore the two direction values
-            bsdf_sample_specular(vx.bs, vx.wo, &wi, uc, &pdf, flags, F);
-            if (!(pdf > 0.f)) continue;   // no matching BxDF: wi is not set
-            const float ad = fabsf(vdot(wi, vx.n));
-            if (ad == 0.f || (F.mode == FV_SUM && F.n == 0)) continue;
-            float4 *mb = P.M + slot, *kb = P.K + slot;
-            fval_prepare<NB, FEAT>(S, F, mb, c);
-            float4 *Fo = dl_F<NB>(P, d, slot);
-            bool black = true;
-#pragma unroll
-            for (int q = 0; q < NQ; ++q) {
-                const float4 f = fval4<FEAT>(sp, F, q, mb, kb, c);
-#pragma unroll
-                for (int i = 0; i < 4; ++i)
-                    if (4 * q + i < NB) black = black && (cmp(f, i) == 0.);
-                Fo[q * c] = f;
-            }
-            if (black) continue;
-            P.fS[(size_t)2 * d * c + slot] = ad;
-            P.fS[(size_t)(2 * d + 1) * c + slot] = pdf;
-            // the child ray and its differentials (the camera's rays always carry them)
-            Ray cr;
-            cr.o = vx.p; cr.d = wi; cr.mint = vx.is.rayEps; cr.maxt = INFINITY; cr.time = vx.ray.time;
-            ray_store(P, RAY_C, slot, cr);
-            const V n = vx.n, wo = vx.wo;
-            const V rxo = vadd(vx.p, vx.dpdx), ryo = vadd(vx.p, vx.dpdy);
-            const V dndx = vadd(vmul(vx.dn[0], vx.diff[0]), vmul(vx.dn[1], vx.diff[1]));
-            const V dndy = vadd(vmul(vx.dn[0], vx.diff[2]), vmul(vx.dn[1], vx.diff[3]));
-            const V dwodx = vsub(vneg(vx.rd.rxd), wo), dwody = vsub(vneg(vx.rd.ryd), wo);
-            const float dDNdx = vdot(dwodx, n) + vdot(wo, dndx);
-            const float dDNdy = vdot(dwody, n) + vdot(wo, dndy);
-            V rxd, ryd;
-            if (refl) {
-                const float won = vdot(wo, n);
-                rxd = vadd(vsub(wi, dwodx), vmul(vadd(vmul(dndx, won), vmul(n, dDNdx)), 2.f));
-                ryd = vadd(vsub(wi, dwody), vmul(vadd(vmul(dndy, won), vmul(n, dDNdy)), 2.f));
-            } else {
-                // BSDF::eta: the glass material's index, 1 otherwise (glass.cpp:48)
-                const pbrtgpu_material &mt = S.mats[S.prims[vx.is.prim].material];
-                float eta = mt.type == PBRTGPU_MAT_GLASS ? mt.f[0] : 1.f;
-                const V w = vneg(wo);
-                if (vdot(wo, n) < 0) eta = 1.f / eta;
-                const float mu = eta * vdot(w, n) - vdot(wi, n);
-                const float dmudx = (eta - (eta * eta * vdot(w, n)) / vdot(wi, n)) * dDNdx;
-                const float dmudy = (eta - (eta * eta * vdot(w, n)) / vdot(wi, n)) * dDNdy;
-                rxd = vsub(vadd(wi, vmul(dwodx, eta)), vadd(vmul(dndx, mu), vmul(n, dmudx)));
-                ryd = vsub(vadd(wi, vmul(dwody, eta)), vadd(vmul(dndy, mu), vmul(n, dmudy)));
-            }
-            float *fd = P.fDiff + (size_t)(d + 1) * 12 * c + slot;
-            dl_vec_store(fd, c, rxo);
-            dl_vec_store(fd + 3 * c, c, rxd);
-            dl_vec_store(fd + 6 * c, c, ryo);
-            dl_vec_store(fd + 9 * c, c, ryd);
-            fl |= PF_CONT;
-            out.c = true;
-            spawned = true;
-            break;
-        }
-        P.fBr[(size_t)d * c + slot] = br;
-        if (spawned) break;
-        // ---- frame d is complete: Li = (1 * L) + 0 goes to its parent, or is the sample's
-        float4 Lr[NQ];
-        const float4 *Lv = dl_L<NB>(P, d, slot);
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) Lr[q] = Lv[q * c];
-        if (d == 0) {
-            *zeroed = path_output<NB>(S, Lr, Lout, P.item[slot], P.smp[slot]);   // rayWeight * ((1 * L) + 0), guarded
-            *done = true;
-            break;
-        }
-        --d;
-        dl_pop<NB>(P, d, slot, Lr);
+    if (!spec) {
+        P.flags[slot] = fl | PF_DLNEE;
+        return out;
     }
-    if (rngLoaded) {
-        mt_store(P, slot, rng);
-        if (rng.init) fl |= PF_MTINIT;
-    }
-    P.bounce[slot] = d;
+    // the top frame's branches: completed here if it cannot branch, else in k_dl_spec
     P.flags[slot] = fl;
-    return out;
+    return dl_spec_step<NB, FEAT, false>(S, P, slot, Lout, done, zeroed);
 }
 
 }  // namespace pgd

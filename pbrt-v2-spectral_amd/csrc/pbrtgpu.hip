@@ -990,7 +990,7 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
                 HIPCHK(hipEventElapsedTime(&m, e[4], e[5])); T.ms[K_SHADE] += m;
             }
             int q = r.q;
-            if (L.hostCnt[CNT_QC(q)] == 0 && L.hostCnt[CNT_QS(q)] == 0 && L.hostCnt[CNT_IDLE(q)] == 0) {
+            if (L.hostCnt[CNT_QC(q)] == 0 && L.hostCnt[CNT_QS(q)] == 0) {
                 r.done = true;
                 --live;
                 uint64_t w[W_COUNT];
@@ -1010,7 +1010,6 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
                 const int nq = q ^ 1;
                 HIPCHK(hipMemsetAsync(P.cnt + CNT_QC(nq), 0, 4, L.s));
                 HIPCHK(hipMemsetAsync(P.cnt + CNT_QS(nq), 0, 4, L.s));
-                if (dl) HIPCHK(hipMemsetAsync(P.cnt + CNT_IDLE(nq), 0, 4, L.s));
                 HIPCHK(hipEventRecord(e[0], L.s));
                 if (serial) {   // closest-hit queries first, alone on the device
                     if (instPT) {
@@ -1039,7 +1038,7 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
                     HIPCHK(hipEventRecord(e[4], L.s));
                     L.P.pass = (L.P.pass + 1) % 3;
                     HIPCHK(kShade(r.grid, L.s, c->S, P, r.src, nq, Lout));
-                    if (dl) { HIPCHK(kNee(r.grid, L.s, c->S, P, nq)); HIPCHK(kSpec(r.grid, L.s, c->S, P, nq, Lout)); }
+                    if (dl) { HIPCHK(kNee(r.grid, L.s, c->S, P, nq)); HIPCHK(kSpec(r.grid, L.s, c->S, P, r.src, nq, Lout)); }
                     T.launches[K_SHADE]++;
                     HIPCHK(hipEventRecord(e[5], L.s));
                     T.passes++;
@@ -1080,7 +1079,7 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
                 HIPCHK(hipEventRecord(e[4], L.s));
                 L.P.pass = (L.P.pass + 1) % 3;
                 HIPCHK(kShade(r.grid, L.s, c->S, P, r.src, nq, Lout));
-                if (dl) { HIPCHK(kNee(r.grid, L.s, c->S, P, nq)); HIPCHK(kSpec(r.grid, L.s, c->S, P, nq, Lout)); }
+                if (dl) { HIPCHK(kNee(r.grid, L.s, c->S, P, nq)); HIPCHK(kSpec(r.grid, L.s, c->S, P, r.src, nq, Lout)); }
                 T.launches[K_SHADE]++;
                 HIPCHK(hipEventRecord(e[5], L.s));
                 T.passes++;

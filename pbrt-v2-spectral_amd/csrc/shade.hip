@@ -177,9 +177,10 @@ static hipError_t launch(int grid, hipStream_t stream, const DevScene &S, const 
 //   k_dl_nee:  the light-sample batches of the slots k_shade marked PF_DLNEE
 //              (directlighting.h dl_light_batches);
 //   k_dl_spec: the specular branches and frame pops of the slots marked PF_DLSPEC by k_shade or
-//              by k_dl_nee (dl_spec_step).  A slot whose sample completes here is free from the
-//              next pass's k_shade on; it is counted in CNT_IDLE so that this pass is not taken
-//              for the wavefront's last while items may remain.
+//              by k_dl_nee (dl_spec_step);
+//   k_regen:   the slots whose sample completed in k_dl_spec take the next camera samples in the
+//              same pass (as k_shade's regeneration does for the others), so a slot is not left
+//              idle for a pass -- without it a C2 frame took 76 passes instead of 52.
 // 2 waves/SIMD for <= 32 bands (k_dl_nee: 47 VGPRs spilled, k_dl_spec: 148); the 60-band
 // builds need 1 wave/SIMD to stay within tools/kernel_budget.py (at 2 waves k_dl_nee spilled 682)
 #ifndef PGD_NEE_ATTR
@@ -225,11 +226,8 @@ __global__ __launch_bounds__(kShadeBlock) PGD_SPEC_ATTR void k_dl_spec(DevScene 
         if (done) P.item[slot] = -1;
     }
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const unsigned long long bD = __ballot(done), bZ = __ballot(zeroed), bC = __ballot(pu.c);
-    if (lane == 0) {
-        if (bD) atomicAdd(&P.cnt[CNT_IDLE(qout)], (uint32_t)__popcll(bD));
-        if (bZ) atomicAdd(&P.cnt[CNT_ZEROED], (uint32_t)__popcll(bZ));
-    }
+    const unsigned long long bZ = __ballot(zeroed), bC = __ballot(pu.c);
+    if (lane == 0 && bZ) atomicAdd(&P.cnt[CNT_ZEROED], (uint32_t)__popcll(bZ));
     __shared__ uint32_t qsh[8];   // per wave: child rays -> offsets; base
     if (lane == 0) qsh[wave] = (uint32_t)__popcll(bC);
     __syncthreads();
@@ -244,6 +242,32 @@ __global__ __launch_bounds__(kShadeBlock) PGD_SPEC_ATTR void k_dl_spec(DevScene 
         qC[qsh[7] + qsh[wave] + (uint32_t)__popcll(bC & ((1ull << lane) - 1ull))] = (uint32_t)slot << 1;
     }
 }
+// regeneration of free slots (the tail of k_shade's queue step, for the slots k_dl_spec freed)
+template <int NB>
+__global__ __launch_bounds__(kShadeBlock) void k_regen(DevScene S, PathSoA P, ItemSrc src, int qout) {
+    const int slot = blockIdx.x * blockDim.x + threadIdx.x;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const bool want = slot < P.cap && P.item[slot] < 0 && *(volatile uint32_t *)&P.cnt[CNT_NEXT] < src.nItems;
+    const unsigned long long bW = __ballot(want);
+    __shared__ uint32_t qsh[8];   // per wave: wanting slots -> offsets; next item, regenerated, queue base
+    if (lane == 0) qsh[wave] = (uint32_t)__popcll(bW);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = 0u;
+        for (int w = 0; w < (int)(blockDim.x >> 6); ++w) { const uint32_t v = qsh[w]; qsh[w] = t; t += v; }
+        const uint32_t nb = t ? atomicAdd(&P.cnt[CNT_NEXT], t) : 0u;
+        const uint32_t nReg = nb >= src.nItems ? 0u : min(t, src.nItems - nb);
+        qsh[4] = nb; qsh[5] = nReg; qsh[6] = nReg ? atomicAdd(&P.cnt[CNT_QC(qout)], nReg) : 0u;
+    }
+    __syncthreads();
+    if (want) {
+        const uint32_t r = qsh[wave] + (uint32_t)__popcll(bW & ((1ull << lane) - 1ull));   // block order
+        if (r < qsh[5]) {
+            path_start<NB>(S, P, src, slot, qsh[4] + r);
+            P.qC[(size_t)qout * 2 * P.rcap + qsh[6] + r] = (uint32_t)slot << 1;
+        }
+    }
+}
 template <int NB>
 hipError_t launch_dl_nee(int grid, hipStream_t stream, const DevScene &S, const PathSoA &P, int qout) {
     const size_t lds = ((SHADE_FEAT & FEAT_MEAS) && S.kdInLds) ? (size_t)S.nKd * 32 : 0;
@@ -251,13 +275,17 @@ hipError_t launch_dl_nee(int grid, hipStream_t stream, const DevScene &S, const 
     return hipGetLastError();
 }
 template <int NB>
-hipError_t launch_dl_spec(int grid, hipStream_t stream, const DevScene &S, const PathSoA &P, int qout, float *Lout) {
+hipError_t launch_dl_spec(int grid, hipStream_t stream, const DevScene &S, const PathSoA &P, const ItemSrc &src, int qout,
+                          float *Lout) {
     const size_t lds = ((SHADE_FEAT & FEAT_MEAS) && S.kdInLds) ? (size_t)S.nKd * 32 : 0;
     hipLaunchKernelGGL((k_dl_spec<NB, SHADE_FEAT>), dim3(grid), dim3(kShadeBlock), lds, stream, S, P, qout, Lout);
+    if (hipError_t e = hipGetLastError()) return e;
+    hipLaunchKernelGGL((k_regen<NB>), dim3(grid), dim3(kShadeBlock), 0, stream, S, P, src, qout);
     return hipGetLastError();
 }
 template hipError_t launch_dl_nee<SHADE_NB>(int, hipStream_t, const DevScene &, const PathSoA &, int);
-template hipError_t launch_dl_spec<SHADE_NB>(int, hipStream_t, const DevScene &, const PathSoA &, int, float *);
+template hipError_t launch_dl_spec<SHADE_NB>(int, hipStream_t, const DevScene &, const PathSoA &, const ItemSrc &, int,
+                                              float *);
 template <int NB>
 hipError_t launch_shade_dl(int grid, hipStream_t stream, const DevScene &S, const PathSoA &P, const ItemSrc &src,
                            int qout, float *Lout) {

@@ -59,9 +59,6 @@ enum { RAY_C = 0, RAY_M = 1, RAY_S = 2 };
 #define CNT_QC(q) (32 * (q))          // closest-hit queue size, queue set q = 0, 1
 #define CNT_QS(q) (64 + 32 * (q))     // shadow queue size
 enum { CNT_NEXT = 128, CNT_ZEROED = 160, CNT_WORK = 192, CNT_WORDS = 288 };
-// slots a pass leaves alive without a queued ray (DirectLighting, PF_DLS2), queue set q = 0, 1:
-// the wavefront has not drained while any remain
-#define CNT_IDLE(q) (224 + 32 * (q))
 enum { W_RAYS = 0, W_SHADOW = 1, W_NODES_C = 2, W_NODES_S = 3, W_TRIS_C = 4, W_TRIS_S = 5, W_QUADS_C = 6, W_QUADS_S = 7,
        W_HITS = 8, W_RAYS_M = 9, W_HITS_M = 10, W_COUNT = 12 };
 
@@ -1071,9 +1068,11 @@ hipError_t launch_shade_dl(int grid, hipStream_t stream, const DevScene &S, cons
 // k_dl_nee: the light-sample batches of the DirectLighting slots k_shade marked (PF_DLNEE)
 template <int NB>
 hipError_t launch_dl_nee(int grid, hipStream_t stream, const DevScene &S, const PathSoA &P, int qout);
-// k_dl_spec: their specular branches and frame pops (PF_DLSPEC)
+// k_dl_spec: their specular branches and frame pops (PF_DLSPEC), then k_regen: the slots it
+// freed take the next camera samples
 template <int NB>
-hipError_t launch_dl_spec(int grid, hipStream_t stream, const DevScene &S, const PathSoA &P, int qout, float *Lout);
+hipError_t launch_dl_spec(int grid, hipStream_t stream, const DevScene &S, const PathSoA &P, const ItemSrc &src, int qout,
+                          float *Lout);
 // k_shade with the MetadataIntegrator step (all features compiled in)
 template <int NB>
 hipError_t launch_shade_meta(int grid, hipStream_t stream, const DevScene &S, const PathSoA &P, const ItemSrc &src,

@@ -199,7 +199,8 @@ def gpu_lib():
         g.pbrtgpu_film_clear.argtypes = [P]
         g.pbrtgpu_trace_paths.argtypes = [P, P, I32, P]
         g.pbrtgpu_intersect.argtypes = [P, P, I32, P, P]
-        g.pbrtgpu_mt_sequence.argtypes = [P, ctypes.c_uint32, I32, P]
+        if hasattr(g, "pbrtgpu_mt_sequence"):   # (experiment libraries of earlier builds lack it)
+            g.pbrtgpu_mt_sequence.argtypes = [P, ctypes.c_uint32, I32, P]
         g.pbrtgpu_path_stats.argtypes = [P, P, I32, P]
         g.pbrtgpu_last_timing.argtypes = [P, ctypes.POINTER(Timing)]
         g.pbrtgpu_film_gather.argtypes = [P, I32, I32, P, I32, P, ctypes.c_int64]

@@ -157,7 +157,7 @@ static int run(const DevScene &S, PathSoA &P, const ItemSrc &src, int nSlots, fl
         if (P.flags[slot] & PF_MTINIT) g_maxDraws = std::max(g_maxDraws, P.mt[slot]);
     };
     // one k_shade pass (+ k_dl_nee): the per-thread body of shade.hip k_shade for every slot
-    auto shade = [&](int qout) -> uint32_t {
+    auto shade = [&](int qout) {
         Q[qout].c.clear();
         Q[qout].s.clear();
         for (int i = 0; i < nSlots; ++i) {
@@ -183,7 +183,6 @@ static int run(const DevScene &S, PathSoA &P, const ItemSrc &src, int nSlots, fl
                 Q[qout].c.push_back((uint32_t)slot << 1);
             }
         }
-        uint32_t idle = 0;
         if (MODE == MODE_DL) {
             for (int i = 0; i < nSlots; ++i) {   // k_dl_nee
                 const int slot = 64 * i;
@@ -199,12 +198,18 @@ static int run(const DevScene &S, PathSoA &P, const ItemSrc &src, int nSlots, fl
                 bool done = false, zeroed = false;
                 if (P.item[slot] >= 0 && (P.flags[slot] & PF_DLSPEC)) {
                     pu = dl_spec_step<NB, FEAT>(S, P, slot, Lout, &done, &zeroed);
-                    if (done) { P.item[slot] = -1; ++finished; ++idle; note_draws(slot); }
+                    if (done) { P.item[slot] = -1; ++finished; note_draws(slot); }
                 }
                 push(qout, pu, slot);
             }
+            for (int i = 0; i < nSlots; ++i) {   // k_regen
+                const int slot = 64 * i;
+                if (P.item[slot] < 0 && next < src.nItems) {
+                    path_start<NB>(S, P, src, slot, next++);
+                    Q[qout].c.push_back((uint32_t)slot << 1);
+                }
+            }
         }
-        return idle;
     };
     // the ray queries of queue set q (k_trace_pt / k_trace_inst: hit or miss, t = inf on a miss)
     auto trace = [&](int q) {
@@ -228,16 +233,16 @@ static int run(const DevScene &S, PathSoA &P, const ItemSrc &src, int nSlots, fl
         }
     };
     P.pass = 0;
-    (void)shade(0);
+    shade(0);
     int q = 0;
     for (int64_t pass = 0;; ++pass) {
         if (pass > maxPasses) { *err = "wavefront did not drain"; return 3; }
         trace(q);
         const int nq = q ^ 1;
         P.pass = (P.pass + 1) % 3;
-        const uint32_t idle = shade(nq);
+        shade(nq);
         q = nq;
-        if (Q[q].c.empty() && Q[q].s.empty() && idle == 0) break;
+        if (Q[q].c.empty() && Q[q].s.empty()) break;
     }
     if (finished != src.nItems || next != src.nItems) {
         *err = "items left unfinished: " + std::to_string(src.nItems - finished);
