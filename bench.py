@@ -161,9 +161,25 @@ def reduce_over_ranks(dist, elapsed, paths, device="cpu"):
     return float(mx[0]), float(t[1])
 
 
+def one_node(world):
+    """All ranks on one node (torchrun's LOCAL_WORLD_SIZE == WORLD_SIZE): the shared-memory film
+    can be used.  Otherwise every rank keeps a film of its own (compose_film)."""
+    return int(os.environ.get("LOCAL_WORLD_SIZE", world)) == world
+
+
+def compose_film(film, dist, device="cpu"):
+    """Multi-node: the ranks' private films (each holding only its own tiles; the others 0) summed
+    onto rank 0 over gloo -- exact, as the tile sets are disjoint.  After the timed steps only."""
+    import torch
+    t = torch.from_numpy(np.ascontiguousarray(film))
+    dist.reduce(t, dst=0, op=dist.ReduceOp.SUM)
+    return t.numpy()
+
+
 def shared_film(shape, rank, dist, tag):
-    """A host film every rank of one node writes its own pixels into (/dev/shm file):
-    the host gather of SURVEY.md §8(e) without any collective."""
+    """A host film every rank of ONE node writes its own pixels into (/dev/shm file): the host
+    gather of SURVEY.md §8(e) without any collective.  Only valid when all ranks share the node
+    (one_node); a /dev/shm file is invisible to other nodes."""
     path = "/dev/shm/pbrtgpu_film_%s" % tag
     n = int(np.prod(shape)) * 4
     if rank == 0:
@@ -307,8 +323,11 @@ def main():
         dev.upload(scene)
         if world > 1 and args.shard == "tiles":
             tiles = pg.tile_slice(ntx * nty, rank, world)
-            tag = os.environ.get("TORCHELASTIC_RUN_ID", "") + "_" + os.environ.get("MASTER_PORT", "0")
-            film_path, film = shared_film(shape, rank, dist, tag)
+            if one_node(world):
+                tag = os.environ.get("TORCHELASTIC_RUN_ID", "") + "_" + os.environ.get("MASTER_PORT", "0")
+                film_path, film = shared_film(shape, rank, dist, tag)
+            else:
+                film_path, film = None, np.zeros(shape, np.float32)
         else:
             tiles, film_path = None, None
             film = np.zeros(shape, np.float32)
@@ -338,6 +357,8 @@ def main():
         dist.all_gather(g, torch.tensor([my_elapsed], dtype=torch.float64))
         per_rank = [round(float(x[0]) / args.steps * 1e3, 2) for x in g]
 
+    if dist is not None and args.shard == "tiles" and not one_node(world):
+        film = compose_film(film, dist)   # multi-node: private films -> rank 0
     if args.dump_film and rank == 0:
         np.save(args.dump_film, np.asarray(film))
     frame_paths = paths / args.steps    # this rank's share of a frame

@@ -18,9 +18,14 @@ extern "C" {
 typedef struct pbrthost_scene pbrthost_scene;
 
 #define PBRTHOST_KEEP_SEED 0xffffffffu
+/* Layout version of pbrthost_overrides: the caller writes it into abi_version, and
+ * pbrthost_load refuses a struct of another layout (a caller built against an older header
+ * passes a shorter struct) */
+#define PBRTHOST_ABI_VERSION 2
 
 /* Overrides of scene-file values: -1 keeps the file's value. */
 typedef struct pbrthost_overrides {
+    int32_t abi_version;  /* PBRTHOST_ABI_VERSION */
     int32_t xres, yres;   /* Film "xresolution"/"yresolution" */
     int32_t spp;          /* Sampler "pixelsamples" (rounded up to a power of two) */
     int32_t maxdepth;     /* SurfaceIntegrator "path" "maxdepth" */
@@ -35,7 +40,10 @@ typedef struct pbrthost_overrides {
     int32_t spectral_sampling;   /* PBRTGPU_SPECTRAL_* to force, or -1: the scene's samplingMethod */
 } pbrthost_overrides;
 
-/* path: a .pbrt scene file or a .pack scene pack.  Returns 0 or -1 (message in err). */
+/* PBRTHOST_ABI_VERSION of the library */
+int pbrthost_abi_version(void);
+/* path: a .pbrt scene file or a .pack scene pack; ov may be NULL (the file's values) or must
+ * carry abi_version == PBRTHOST_ABI_VERSION.  Returns 0 or -1 (message in err). */
 int pbrthost_load(const char *path, const pbrthost_overrides *ov, pbrthost_scene **out, char *err, int errlen);
 int pbrthost_free(pbrthost_scene *s);
 int pbrthost_flat(pbrthost_scene *s, pbrtgpu_flat_scene *out);   /* pointers stay owned by s */

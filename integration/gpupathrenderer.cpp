@@ -49,7 +49,7 @@ void GpuPathRenderer::Render(const Scene *) {
     }
     int n = ngpu > 0 ? min(ngpu, ndev) : ndev;
     // the scene's own integrator and camera; the SpectralRenderer if asked for
-    pbrthost_overrides ov = { -1, -1, -1, -1, nSpectralSamples, seed, -1, -1, -1,
+    pbrthost_overrides ov = { PBRTHOST_ABI_VERSION, -1, -1, -1, -1, nSpectralSamples, seed, -1, -1, -1,
                               waveBands > 0 ? PBRTGPU_RENDERER_SPECTRAL : -1, waveBands,
                               waveBands > 0 ? spectralSampling : -1 };
     pbrthost_scene *hs = NULL;

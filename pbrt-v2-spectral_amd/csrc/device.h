@@ -171,14 +171,18 @@ struct MT {
 PGD_INLINE uint32_t mt_next_word(uint32_t prev, uint32_t idx) { return 1812433253U * (prev ^ (prev >> 30)) + idx; }
 PGD_INLINE void mt_begin(MT &r, uint32_t seed) { r.seed = seed; r.init = false; r.k = 0; r.ext = nullptr; }
 // the seed recurrence up to mt[397]: once per path, before its first draw (one copy; a
-// fully unrolled 396-step loop at every draw site would dominate the shade kernel's code)
-__device__ __attribute__((noinline)) void mt_init(MT &r) {
-    r.a = r.seed;
-    r.b = mt_next_word(r.a, 1);
-    uint32_t w = r.b;
+// fully unrolled 396-step loop at every draw site would dominate the shade kernel's code).
+// Scalars in and out: an MT passed by reference to an out-of-line function would live in
+// scratch memory at every draw site.
+__device__ __attribute__((noinline)) uint32_t mt_word397(uint32_t w) {
 #pragma unroll 4
     for (uint32_t i = 2; i <= 397; ++i) w = mt_next_word(w, i);
-    r.m = w;
+    return w;
+}
+PGD_INLINE void mt_init(MT &r) {
+    r.a = r.seed;
+    r.b = mt_next_word(r.a, 1);
+    r.m = mt_word397(r.b);
     r.init = true;
 }
 PGD_INLINE uint32_t mt_temper(uint32_t y) {
@@ -1134,11 +1138,25 @@ enum { T_ZERO = 0, T_LAMB, T_OREN, T_BLINN, T_FB, T_MEAS, T_BUF, T_BLINNC, T_MER
 struct FTerm { int kind; int R, R2; float s0, s1, s2, s3; };
 enum { FV_SUM = 0, FV_SPEC = 1 };
 // FV_SPEC: a specular BxDF's sampled value (fs * R_i) / d (reflection.cpp:130-162)
-struct FVal { int mode, n; FTerm t[2]; float d, fs; int R; };   // FV_SUM with n == 0: zero spectrum
+// The two terms are named members, not an array: any access through a runtime index (or an
+// address the compiler selects between them) keeps the whole FVal in scratch memory, and the
+// band loops then reload its terms from there (r03: 3 x 64 scratch loads in k_shade's band loops)
+struct FVal { int mode, n; FTerm t0, t1; float d, fs; int R; };   // FV_SUM with n == 0: zero spectrum
 
 PGD_INLINE void fval_zero(FVal &F) { F.mode = FV_SUM; F.n = 0; }
-PGD_INLINE void fval_push(FVal &F, const FTerm &t) {   // static indices only (no scratch)
-    if (F.n == 0) F.t[0] = t; else F.t[1] = t;
+// Field by field, as value selects: `if (F.n == 0) F.t[0] = t; else F.t[1] = t;` was folded into
+// a store through a selected address, a dynamic index that kept every FVal in scratch memory (and
+// the band loops reloading its terms from there)
+PGD_INLINE FTerm fterm_sel(bool c, const FTerm &a, const FTerm &b) {
+    FTerm r;
+    r.kind = c ? a.kind : b.kind; r.R = c ? a.R : b.R; r.R2 = c ? a.R2 : b.R2;
+    r.s0 = c ? a.s0 : b.s0; r.s1 = c ? a.s1 : b.s1; r.s2 = c ? a.s2 : b.s2; r.s3 = c ? a.s3 : b.s3;
+    return r;
+}
+PGD_INLINE void fval_push(FVal &F, const FTerm &t) {
+    const bool first = F.n == 0;
+    F.t1 = fterm_sel(first, F.t1, t);
+    F.t0 = fterm_sel(first, t, F.t0);
     F.n++;
 }
 
@@ -1296,7 +1314,7 @@ PGD_INLINE void bx_sample_f(PowMemo &pm, const BxDF &b, V wo, V *wi, float u1, f
         case BX_MICRO_BLINN_COND:
             blinn_sample(b.a, wo, wi, u1, u2, pdf);
             if (!samehemi(wo, *wi)) return;
-            F.n = 1; F.t[0] = bx_term(pm, b, wo, *wi);
+            F.n = 1; F.t0 = bx_term(pm, b, wo, *wi);
             return;
         case BX_SPEC_REFL_NOOP:
         case BX_SPEC_REFL_DIEL:
@@ -1314,13 +1332,13 @@ PGD_INLINE void bx_sample_f(PowMemo &pm, const BxDF &b, V wo, V *wi, float u1, f
                 if (!samehemi(wo, *wi)) return;
             }
             *pdf = bx_pdf(pm, b, wo, *wi);
-            F.n = 1; F.t[0] = bx_term(pm, b, wo, *wi);
+            F.n = 1; F.t0 = bx_term(pm, b, wo, *wi);
             return;
         default:
             *wi = cosine_hemisphere(u1, u2);
             if (wo.z < 0.) wi->z *= -1.f;
             *pdf = bx_pdf(pm, b, wo, *wi);
-            F.n = 1; F.t[0] = bx_term(pm, b, wo, *wi);
+            F.n = 1; F.t0 = bx_term(pm, b, wo, *wi);
             return;
     }
 }

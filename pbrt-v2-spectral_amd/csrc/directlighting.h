@@ -199,8 +199,8 @@ PGD_INLINE void dl_light_batches(const DevScene &S, const PathSoA &P, int slot, 
             FVal F;
             uint32_t f2 = 0u;
             Pushes o2 = {false, false, false, 0u, 0u};
-            estimate_direct<NB, FEAT>(S, P, slot, slot + jb * (int)c, P.A + (size_t)jb * NQ * c + slot,
-                                      P.B + (size_t)jb * NQ * c + slot, ln, vx.bs, pm, vx.p, vx.n, vx.wo,
+            estimate_direct<NB, FEAT>(S, P, slot, slot + jb * (int)c, Col<float4>{P.A, (uint32_t)(jb * NQ * c + slot)},
+                                      Col<float4>{P.B, (uint32_t)(jb * NQ * c + slot)}, ln, vx.bs, pm, vx.p, vx.n, vx.wo,
                                       vx.is.rayEps, vx.ray.time, ul, ub, F, f2, o2, nullptr, nullptr);
             if (f2 & PF_PA) mA |= 1u << jb;
             if (f2 & PF_PB) mB |= 1u << jb;

@@ -18,7 +18,7 @@
 //
 // A ray's closest hit is the same primitive at the same t under any BVH except for exact
 // ties in t (the traversal visits them in another order), so a render over this BVH equals
-// the reference's up to those ties (tests/test_gpu_lbvh.py measures it).
+// the reference's up to those ties (tests/test_lbvh.py measures it).
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 #include <chrono>

@@ -31,15 +31,22 @@
 
 using namespace pgd;
 #ifdef PGD_SECTIONS
+// weak: an experiment build may compile only some shade variants with PGD_SECTIONS
 extern "C" {
-int pgd_sections_read_32_0(unsigned long long *, int); int pgd_sections_read_32_7(unsigned long long *, int);
-int pgd_sections_read_60_0(unsigned long long *, int); int pgd_sections_read_60_7(unsigned long long *, int);
-int pgd_sections_read_30_0(unsigned long long *, int); int pgd_sections_read_30_7(unsigned long long *, int);
+__attribute__((weak)) int pgd_sections_read_32_0(unsigned long long *, int);
+__attribute__((weak)) int pgd_sections_read_32_7(unsigned long long *, int);
+__attribute__((weak)) int pgd_sections_read_60_0(unsigned long long *, int);
+__attribute__((weak)) int pgd_sections_read_60_7(unsigned long long *, int);
+__attribute__((weak)) int pgd_sections_read_30_0(unsigned long long *, int);
+__attribute__((weak)) int pgd_sections_read_30_7(unsigned long long *, int);
 }
 static int pgd_sections_read(unsigned long long *out, int reset) {
     for (int k = 0; k < SEC_N; ++k) out[k] = 0;
-    int e = pgd_sections_read_32_0(out, reset) | pgd_sections_read_32_7(out, reset) | pgd_sections_read_60_0(out, reset);
-    return e | pgd_sections_read_60_7(out, reset) | pgd_sections_read_30_0(out, reset) | pgd_sections_read_30_7(out, reset);
+    int e = 0;
+    for (auto f : {pgd_sections_read_32_0, pgd_sections_read_32_7, pgd_sections_read_60_0, pgd_sections_read_60_7,
+                   pgd_sections_read_30_0, pgd_sections_read_30_7})
+        if (f) e |= f(out, reset);
+    return e;
 }
 #endif
 
@@ -804,11 +811,20 @@ static int poison_byte() {
 static size_t frame_bytes(int NB) { return (size_t)8 * ((NB + 3) / 4 * 4) + 104; }
 // DirectLighting bytes per slot and batched light sample: A, B terms and the ray records
 static size_t batch_bytes(int NB) { return (size_t)8 * ((NB + 3) / 4 * 4) + 27 * 4 + 8 + 8 + 4 + 24; }
+// The shading step addresses the slot arrays through 32-bit byte offsets (wavefront.h sa / Col):
+// the largest of them -- A / B at max(2, batch) x padded bands, beta at 3 x, the ray records at
+// 27 floats per ray slot -- must stay below 4 GiB, which bounds a lane's slots
+static int max_slots_32bit(int NB, int batch) {
+    const size_t NBP = (size_t)(NB + 3) / 4 * 4;
+    const size_t per = std::max({(size_t)std::max(2, batch) * NBP * 4, 3 * NBP * 4, (size_t)batch * 27 * 4});
+    return (int)std::min<size_t>(INT32_MAX / 2, (((size_t)1 << 32) - 1) / per);
+}
 // batch: ray slots per slot (light samples a DirectLighting pass issues; 1 for the other integrators)
 static int ensure_slots(Lane *c, int cap, int NB, int nInst, int nFrames, int batch, bool mtExt) {
     if (c->slotCap == cap && c->slotNb == NB && c->slotInst == nInst && c->slotFrames == nFrames &&
         c->slotBatch == batch && c->slotMtExt == mtExt)
         return 0;
+    if (cap > max_slots_32bit(NB, batch)) return fail(PBRTGPU_E_INVALID, "slot arrays beyond 32-bit offsets");
     const size_t C = (size_t)cap, R = C * (size_t)batch, AB = (size_t)std::max(2, batch);
     const int NBP = (NB + 3) / 4 * 4;   // bands padded to whole float4 quads
     size_t off = 0;
@@ -937,6 +953,7 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
             r.cap = (int)std::max<size_t>(64, std::min<size_t>((size_t)r.cap, ((size_t)24 << 30) /
                                                                (frame_bytes(NB) * nFrames + batch_bytes(NB) * batch)));
         if (mtExt && !getenv("PBRTGPU_SLOTS")) r.cap = std::min(r.cap, 1 << 20);   // 2.5 KiB of MT state per slot
+        r.cap = std::min(r.cap, max_slots_32bit(NB, batch));
         r.grid = (r.cap + kShadeBlock - 1) / kShadeBlock;
         r.q = 0;
         r.batch = 0;
@@ -1427,11 +1444,12 @@ static int render_impl(pbrtgpu_ctx *c, const pbrtgpu_render_desc *d, const int32
     {   // timing experiment: wave-cycles per k_shade section of this render
         unsigned long long sec[SEC_N];
         if (pgd_sections_read(sec, 1) == 0) {
-            static const char *nm[] = {"load", "finish", "isect", "bsdf", "light", "mis", "cont", "out", "regen", "push"};
+            static const char *nm[] = {"load", "finish", "isect", "bsdf", "light", "mis", "cont", "out", "regen", "push",
+                                       "[light: sample", "eval", "store]", "[cont: sample", "bands]"};
             unsigned long long tot = 0;
             for (int k = 0; k < SEC_PUSH + 1; ++k) tot += sec[k];
             fprintf(stderr, "sections:");
-            for (int k = 0; k < SEC_PUSH + 1; ++k) fprintf(stderr, " %s %.1f%%", nm[k], 100.0 * sec[k] / std::max(1ull, tot));
+            for (int k = 0; k < SEC_CBAND + 1; ++k) fprintf(stderr, " %s %.1f%%", nm[k], 100.0 * sec[k] / std::max(1ull, tot));
             fprintf(stderr, "  (total %.3e wave-cycles)\n", (double)tot);
         }
     }

@@ -27,11 +27,22 @@ namespace pgd {
 // Timing experiment only (-DPGD_SECTIONS, never in the product build): wave-cycles per
 // section of k_shade, summed per block in LDS and written to a per-block array.
 #ifdef PGD_SECTIONS
-enum { SEC_LOAD, SEC_FINISH, SEC_ISECT, SEC_BSDF, SEC_LIGHT, SEC_MIS, SEC_CONT, SEC_OUT, SEC_REGEN, SEC_PUSH, SEC_N = 16 };
+// Sub-sections of LIGHT (light_sample_L, the BSDF value / pdf, the A bands + shadow ray) and of
+// CONT (the direction sample, the beta bands + roulette + continuation ray).  -DPGD_SECTIONS_DRAIN
+// waits for every outstanding memory operation at each section's end, so a section is charged
+// the latency of its own loads and stores (the total then exceeds an undrained run's).
+enum { SEC_LOAD, SEC_FINISH, SEC_ISECT, SEC_BSDF, SEC_LIGHT, SEC_MIS, SEC_CONT, SEC_OUT, SEC_REGEN, SEC_PUSH,
+       SEC_LSAMP, SEC_LEVAL, SEC_LSTORE, SEC_CSAMP, SEC_CBAND, SEC_N = 16 };
 __shared__ unsigned long long pgd_secs[SEC_N];
+#ifdef PGD_SECTIONS_DRAIN
+#define PGD_SEC_DRAIN() __builtin_amdgcn_s_waitcnt(0)
+#else
+#define PGD_SEC_DRAIN() do {} while (0)
+#endif
 #define PGD_T0(k) const unsigned long long pgd_t_##k = clock64()
 #define PGD_T1(k)                                                                                 \
     do {                                                                                          \
+        PGD_SEC_DRAIN();                                                                          \
         const unsigned long long d_ = clock64() - pgd_t_##k;                                      \
         if (__builtin_amdgcn_readfirstlane(threadIdx.x) == threadIdx.x) atomicAdd(&pgd_secs[SEC_##k], d_); \
     } while (0)
@@ -129,33 +140,52 @@ struct ItemSrc {
     uint32_t base;
 };
 
+// Slot arrays are addressed through a 32-bit element index from their base: the base is a
+// kernel argument (wave-uniform, in SGPRs) and the byte offset a 32-bit value, so a load or store
+// takes one VGPR of address (global saddr mode) instead of a 64-bit per-lane pointer -- fewer
+// registers live across k_shade and no 64-bit address arithmetic.  Every array the path step
+// addresses this way is < 4 GiB (pbrtgpu.hip ensure_slots checks it).
+template <class T> PGD_INLINE T *sa(T *base, uint32_t i) {
+    return reinterpret_cast<T *>(reinterpret_cast<char *>(base) + (uint32_t)(i * (uint32_t)sizeof(T)));
+}
+template <class T> PGD_INLINE const T *sa(const T *base, uint32_t i) {
+    return reinterpret_cast<const T *>(reinterpret_cast<const char *>(base) + (uint32_t)(i * (uint32_t)sizeof(T)));
+}
+// a column of a slot array: element i (+ k) of base
+template <class T> struct Col {
+    T *base;
+    uint32_t i;
+    PGD_INLINE T &operator[](uint32_t k) const { return *sa(base, i + k); }
+};
+static constexpr uint32_t kNoCol = 0xffffffffu;
+
 PGD_INLINE void ray_store(const PathSoA &P, int kind, int rs, const Ray &r) {
-    float *b = P.ray + (size_t)kind * 9 * P.rcap + rs;
-    const size_t c = P.rcap;
-    b[0] = r.o.x; b[c] = r.o.y; b[2 * c] = r.o.z;
-    b[3 * c] = r.d.x; b[4 * c] = r.d.y; b[5 * c] = r.d.z;
-    b[6 * c] = r.mint; b[7 * c] = r.maxt; b[8 * c] = r.time;
+    const uint32_t c = (uint32_t)P.rcap, b = (uint32_t)kind * 9u * c + (uint32_t)rs;
+    float *R = P.ray;
+    *sa(R, b) = r.o.x; *sa(R, b + c) = r.o.y; *sa(R, b + 2 * c) = r.o.z;
+    *sa(R, b + 3 * c) = r.d.x; *sa(R, b + 4 * c) = r.d.y; *sa(R, b + 5 * c) = r.d.z;
+    *sa(R, b + 6 * c) = r.mint; *sa(R, b + 7 * c) = r.maxt; *sa(R, b + 8 * c) = r.time;
 }
 PGD_INLINE Ray ray_load(const PathSoA &P, int kind, int rs) {
-    const float *b = P.ray + (size_t)kind * 9 * P.rcap + rs;
-    const size_t c = P.rcap;
+    const uint32_t c = (uint32_t)P.rcap, b = (uint32_t)kind * 9u * c + (uint32_t)rs;
+    const float *R = P.ray;
     Ray r;
-    r.o = v3(b[0], b[c], b[2 * c]);
-    r.d = v3(b[3 * c], b[4 * c], b[5 * c]);
-    r.mint = b[6 * c]; r.maxt = b[7 * c]; r.time = b[8 * c];
+    r.o = v3(*sa(R, b), *sa(R, b + c), *sa(R, b + 2 * c));
+    r.d = v3(*sa(R, b + 3 * c), *sa(R, b + 4 * c), *sa(R, b + 5 * c));
+    r.mint = *sa(R, b + 6 * c); r.maxt = *sa(R, b + 7 * c); r.time = *sa(R, b + 8 * c);
     return r;
 }
 
 PGD_INLINE void mt_load(const PathSoA &P, int slot, uint32_t fl, MT &r) {
-    const size_t c = P.cap;
-    r.k = P.mt[slot]; r.a = P.mt[c + slot]; r.b = P.mt[2 * c + slot]; r.m = P.mt[3 * c + slot];
-    r.seed = P.mt[4 * c + slot];
+    const uint32_t c = (uint32_t)P.cap, s = (uint32_t)slot;
+    r.k = *sa(P.mt, s); r.a = *sa(P.mt, c + s); r.b = *sa(P.mt, 2 * c + s); r.m = *sa(P.mt, 3 * c + s);
+    r.seed = *sa(P.mt, 4 * c + s);
     r.init = (fl & PF_MTINIT) != 0;
     r.ext = P.mtExt ? P.mtExt + (size_t)slot * 624 : nullptr;
 }
 PGD_INLINE void mt_store(const PathSoA &P, int slot, const MT &r) {
-    const size_t c = P.cap;
-    P.mt[slot] = r.k; P.mt[c + slot] = r.a; P.mt[2 * c + slot] = r.b; P.mt[3 * c + slot] = r.m;
+    const uint32_t c = (uint32_t)P.cap, s = (uint32_t)slot;
+    *sa(P.mt, s) = r.k; *sa(P.mt, c + s) = r.a; *sa(P.mt, 2 * c + s) = r.b; *sa(P.mt, 3 * c + s) = r.m;
 }
 
 template <int NB> struct Bands { static constexpr int NQ = (NB + 3) / 4; };
@@ -165,8 +195,8 @@ template <int NB> struct Bands { static constexpr int NQ = (NB + 3) / 4; };
 // pass % 3, compacted per wave like A) and read by the next pass (shading the vertex) and the one
 // after (finishing its direct light): ago = 1 or 2 passes.  Vertex 0 (beta = 1) is not stored.
 PGD_INLINE int pass_buf(const PathSoA &P, int ago) { return (P.pass + 3 - ago) % 3; }
-template <int NB> PGD_INLINE float4 *beta_reg(const PathSoA &P, int buf, int slot) {
-    return P.beta + (size_t)buf * Bands<NB>::NQ * P.cap + (slot & ~63);
+template <int NB> PGD_INLINE Col<float4> beta_reg(const PathSoA &P, int buf, int slot) {
+    return Col<float4>{P.beta, (uint32_t)buf * Bands<NB>::NQ * (uint32_t)P.cap + ((uint32_t)slot & ~63u)};
 }
 PGD_INLINE unsigned long long *beta_mask(const PathSoA &P, int buf, int slot) {
     return P.bMask + (size_t)buf * ((P.cap + 63) >> 6) + (slot >> 6);
@@ -185,38 +215,48 @@ PGD_INLINE WaveMasks wave_masks(const PathSoA &P, int qout, int slot) {
     return m;
 }
 PGD_INLINE int wave_rank(unsigned long long m, int slot) { return __popcll(m & ((1ull << (slot & 63)) - 1ull)); }
-// the slot's beta written `ago` passes back (null for vertex 0); m = that pass's writer mask
-template <int NB> PGD_INLINE const float4 *beta_rd(const PathSoA &P, int v, int ago, int slot, unsigned long long m) {
-    if (v == 0) return nullptr;
-    return beta_reg<NB>(P, pass_buf(P, ago), slot) + wave_rank(m, slot);
+// the slot's beta written `ago` passes back (i = kNoCol for vertex 0: beta = 1, not stored);
+// m = that pass's writer mask
+template <int NB> PGD_INLINE Col<float4> beta_rd(const PathSoA &P, int v, int ago, int slot, unsigned long long m) {
+    Col<float4> r = beta_reg<NB>(P, pass_buf(P, ago), slot);
+    r.i = v == 0 ? kNoCol : r.i + (uint32_t)wave_rank(m, slot);
+    return r;
 }
-PGD_INLINE float4 beta_q(const float4 *bp, int q, size_t c) { return bp ? bp[q * c] : make_float4(1.f, 1.f, 1.f, 1.f); }
+#ifdef PGD_EXP_NOBETA   // timing experiment only: beta not loaded (wrong radiance)
+PGD_INLINE float4 beta_q(const Col<float4> &bp, int q, uint32_t c) {
+    return make_float4(1.f, 1.f, 1.f, bp.i != kNoCol ? 0.5f : 1.f);
+}
+#else
+PGD_INLINE float4 beta_q(const Col<float4> &bp, int q, uint32_t c) {
+    return bp.i != kNoCol ? bp[(uint32_t)q * c] : make_float4(1.f, 1.f, 1.f, 1.f);
+}
+#endif
 // beta of vertex v has a non-finite band (then L += beta * 0 is NaN and cannot be skipped)
 PGD_INLINE bool beta_nonfinite(uint32_t fl, int v) { return v > 0 && ((fl >> (7 + v % 3)) & 1u); }
-template <int NB> PGD_INLINE float4 *A_of(const PathSoA &P, int v, int slot) {
-    return P.A + (size_t)(v & 1) * Bands<NB>::NQ * P.cap + slot;
-}
-template <int NB> PGD_INLINE float4 *B_of(const PathSoA &P, int v, int slot) {
-    return P.B + (size_t)(v & 1) * Bands<NB>::NQ * P.cap + slot;
-}
-
 // path integrator: the A region of slot's wave in the buffer of queue set q, and that wave's
 // writer mask; the reader of the next pass finds its term at the region + its rank
-template <int NB> PGD_INLINE float4 *A_reg(const PathSoA &P, int q, int slot) {
-    return P.A + (size_t)q * Bands<NB>::NQ * P.cap + (slot & ~63);
+template <int NB> PGD_INLINE Col<float4> A_reg(const PathSoA &P, int q, int slot) {
+    return Col<float4>{P.A, (uint32_t)q * Bands<NB>::NQ * (uint32_t)P.cap + ((uint32_t)slot & ~63u)};
 }
 PGD_INLINE unsigned long long *A_mask(const PathSoA &P, int q, int slot) {
     return P.aMask + (size_t)q * ((P.cap + 63) >> 6) + (slot >> 6);
 }
 // the B (MIS) terms likewise
-template <int NB> PGD_INLINE float4 *B_reg(const PathSoA &P, int q, int slot) {
-    return P.B + (size_t)q * Bands<NB>::NQ * P.cap + (slot & ~63);
+template <int NB> PGD_INLINE Col<float4> B_reg(const PathSoA &P, int q, int slot) {
+    return Col<float4>{P.B, (uint32_t)q * Bands<NB>::NQ * (uint32_t)P.cap + ((uint32_t)slot & ~63u)};
 }
 PGD_INLINE unsigned long long *B_mask(const PathSoA &P, int q, int slot) {
     return P.mMask + (size_t)q * ((P.cap + 63) >> 6) + (slot >> 6);
 }
 
+#ifdef PGD_EXP_NOSPEC   // timing experiment only: scene spectra not loaded (wrong radiance)
+PGD_INLINE float4 ld4(const float *p) { return make_float4(0.5f, 0.5f, 0.5f, (float)((uintptr_t)p & 1)); }
+PGD_INLINE float4 ld4(const float *p, int off) { return make_float4(0.5f, 0.5f, 0.5f, (float)(off & 1)); }
+#else
 PGD_INLINE float4 ld4(const float *p) { return *reinterpret_cast<const float4 *>(p); }
+// band quad at float offset off of the spectrum pool p (32-bit offset from the uniform base)
+PGD_INLINE float4 ld4(const float *p, int off) { return *reinterpret_cast<const float4 *>(sa(p, (uint32_t)off)); }
+#endif
 PGD_INLINE float &cmp(float4 &v, int k) { return k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w; }
 PGD_INLINE float cmp(const float4 &v, int k) { return k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w; }
 
@@ -246,39 +286,39 @@ PGD_INLINE float term_val(const FTerm &t, float r, float r2) {
 }
 // band quad q of a spectrum reference: pool offset, or -1 = the slot's K bands
 PGD_INLINE float4 spec4(const float *sp, int off, int q, const float4 *kb, size_t c) {
-    return off >= 0 ? ld4(sp + off + 4 * q) : kb[q * c];
+    return off >= 0 ? ld4(sp, off + 4 * q) : kb[q * c];
+}
+// one term's share of four bands (quad q), added to v
+template <int FEAT>
+PGD_INLINE void term4(const float *sp, const FTerm &t, int q, const float4 *mb, const float4 *kb, size_t c, float4 &v) {
+    if ((FEAT & FEAT_MEAS) && t.kind == T_BUF) {
+        const float4 m = mb[q * c];
+        v.x += m.x; v.y += m.y; v.z += m.z; v.w += m.w;
+        return;
+    }
+    float4 r, r2;
+    if (FEAT & FEAT_TEX) {
+        r = spec4(sp, t.R, q, kb, c);
+        r2 = (t.kind == T_FB || t.kind == T_BLINNC) ? spec4(sp, t.R2, q, kb, c) : r;
+    } else {
+        r = ld4(sp, t.R + 4 * q);
+        r2 = (t.kind == T_FB || t.kind == T_BLINNC) ? ld4(sp, t.R2 + 4 * q) : r;
+    }
+    v.x += term_val(t, r.x, r2.x);
+    v.y += term_val(t, r.y, r2.y);
+    v.z += term_val(t, r.z, r2.z);
+    v.w += term_val(t, r.w, r2.w);
 }
 // BSDF value of four bands (quad q): mb = measured scratch, kb = texture scratch of the slot
 template <int FEAT>
 PGD_INLINE float4 fval4(const float *sp, const FVal &F, int q, const float4 *mb, const float4 *kb, size_t c) {
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
     if (F.mode == FV_SPEC) {
-        float4 r = (FEAT & FEAT_TEX) ? spec4(sp, F.R, q, kb, c) : ld4(sp + F.R + 4 * q);
+        float4 r = (FEAT & FEAT_TEX) ? spec4(sp, F.R, q, kb, c) : ld4(sp, F.R + 4 * q);
         return make_float4((F.fs * r.x) / F.d, (F.fs * r.y) / F.d, (F.fs * r.z) / F.d, (F.fs * r.w) / F.d);
     }
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-        if (k < F.n) {
-            const FTerm &t = F.t[k];
-            if ((FEAT & FEAT_MEAS) && t.kind == T_BUF) {
-                float4 m = mb[q * c];
-                v.x += m.x; v.y += m.y; v.z += m.z; v.w += m.w;
-                continue;
-            }
-            float4 r, r2;
-            if (FEAT & FEAT_TEX) {
-                r = spec4(sp, t.R, q, kb, c);
-                r2 = (t.kind == T_FB || t.kind == T_BLINNC) ? spec4(sp, t.R2, q, kb, c) : r;
-            } else {
-                r = ld4(sp + t.R + 4 * q);
-                r2 = (t.kind == T_FB || t.kind == T_BLINNC) ? ld4(sp + t.R2 + 4 * q) : r;
-            }
-            v.x += term_val(t, r.x, r2.x);
-            v.y += term_val(t, r.y, r2.y);
-            v.z += term_val(t, r.z, r2.z);
-            v.w += term_val(t, r.w, r2.w);
-        }
-    }
+    if (F.n > 0) term4<FEAT>(sp, F.t0, q, mb, kb, c, v);
+    if (F.n > 1) term4<FEAT>(sp, F.t1, q, mb, kb, c, v);
     return v;
 }
 // band quad q of an emitted radiance (Emit, device.h)
@@ -286,7 +326,7 @@ template <int FEAT>
 PGD_INLINE float4 emit4(const DevScene &S, const Emit &e, int q) {
     if ((FEAT & FEAT_INF) && e.mode == EM_RGB) return from_rgb4(S, e.pick, true, q);
     if (e.mode == EM_BLACK) return make_float4(0.f, 0.f, 0.f, 0.f);
-    float4 v = ld4(S.spectra + e.off + 4 * q);
+    float4 v = ld4(S.spectra, e.off + 4 * q);
     if (e.point) v = make_float4(v.x / e.div, v.y / e.div, v.z / e.div, v.w / e.div);
     return v;
 }
@@ -420,23 +460,26 @@ PGD_INLINE void kd_lds_fill(const DevScene &S) {
     __syncthreads();
 }
 // materialise a measured term of F into the slot's M bands (T_MEAS -> T_BUF)
+template <int NB>
+PGD_INLINE void term_prepare(const DevScene &S, FTerm &t, float4 *mb, size_t c) {
+    if (t.kind == T_MEAS) {
+        measured_lookup<NB>(S, t, mb, c);
+        t.kind = T_BUF;
+    } else if (t.kind == T_MERL) {
+        // Spectrum::FromRGB(&brdf[3 * index]) (reflection.cpp:299), reflectance
+        const float *rgb = S.merl + 3 * ((size_t)t.R + (size_t)t.R2);
+        const float v[3] = {rgb[0], rgb[1], rgb[2]};
+        const RGBPick pk = rgb_pick(v);
+#pragma unroll
+        for (int q = 0; q < Bands<NB>::NQ; ++q) mb[q * c] = from_rgb4(S, pk, false, q);
+        t.kind = T_BUF;
+    }
+}
 template <int NB, int FEAT>
 PGD_INLINE void fval_prepare(const DevScene &S, FVal &F, float4 *mb, size_t c) {
     if (!(FEAT & FEAT_MEAS) || F.mode != FV_SUM) return;
-#pragma unroll
-    for (int k = 0; k < 2; ++k)
-        if (k < F.n && F.t[k].kind == T_MEAS) {
-            measured_lookup<NB>(S, F.t[k], mb, c);
-            F.t[k].kind = T_BUF;
-        } else if (k < F.n && F.t[k].kind == T_MERL) {
-            // Spectrum::FromRGB(&brdf[3 * index]) (reflection.cpp:299), reflectance
-            const float *rgb = S.merl + 3 * ((size_t)F.t[k].R + (size_t)F.t[k].R2);
-            const float v[3] = {rgb[0], rgb[1], rgb[2]};
-            const RGBPick pk = rgb_pick(v);
-#pragma unroll
-            for (int q = 0; q < Bands<NB>::NQ; ++q) mb[q * c] = from_rgb4(S, pk, false, q);
-            F.t[k].kind = T_BUF;
-        }
+    if (F.n > 0) term_prepare<NB>(S, F.t0, mb, c);
+    if (F.n > 1) term_prepare<NB>(S, F.t1, mb, c);
 }
 
 // The BSDF-sampled term B of a vertex counts only if the MIS ray's closest hit is a
@@ -511,14 +554,15 @@ PGD_INLINE void path_start(const DevScene &S, const PathSoA &P, const ItemSrc &s
             o[4 + k] = make_float4(minv[4 * k], minv[4 * k + 1], minv[4 * k + 2], minv[4 * k + 3]);
         }
     }
-    P.item[slot] = (int)item;
-    P.hp[slot] = hp;
-    P.pix[slot] = ((uint32_t)py << 16) | (uint32_t)px;
-    P.smp[slot] = s;
-    P.bounce[slot] = dead ? -2 : -1;
-    P.flags[slot] = PF_CONT | PF_LZ;   // L = 0 and beta_0 = 1 are implicit (not stored)
-    P.mt[slot] = 0;
-    P.mt[4 * (size_t)P.cap + slot] =
+    const uint32_t us = (uint32_t)slot;
+    *sa(P.item, us) = (int)item;
+    *sa(P.hp, us) = hp;
+    *sa(P.pix, us) = ((uint32_t)py << 16) | (uint32_t)px;
+    *sa(P.smp, us) = s;
+    *sa(P.bounce, us) = dead ? -2 : -1;
+    *sa(P.flags, us) = PF_CONT | PF_LZ;   // L = 0 and beta_0 = 1 are implicit (not stored)
+    *sa(P.mt, us) = 0;
+    *sa(P.mt, 4 * (uint32_t)P.cap + us) =
         path_seed(hp, S.specItems > 1 ? s * (uint32_t)S.specItems + (item - sitem * (uint32_t)S.specItems) : s);
 }
 
@@ -615,13 +659,17 @@ struct LAdds {
 template <int NB, int FEAT>
 // aMask (path integrator): A is the wave's region of the pass's A buffer; the lanes that write
 // a term take its entries in lane order (whole 64-B lines instead of the scattered lines of
-// divergent lanes) and *aMask records them for the reader of the next pass
-PGD_INLINE void estimate_direct(const DevScene &S, const PathSoA &P, int slot, int rs, float4 *A, float4 *B,
+// divergent lanes) and *aMask records them for the reader of the next pass.  With masks it must
+// stay ONE call site per k_shade pass (shade_vertex): the first active lane overwrites the wave's
+// mask, and the next pass's readers rank themselves in it (PF_PA / PF_PB are set in the same
+// pass).  A second call site, or a persistent k_shade reusing a wave for other slots, would read
+// another lane's entry.  (DirectLighting passes null masks: its batches are indexed per slot.)
+PGD_INLINE void estimate_direct(const DevScene &S, const PathSoA &P, int slot, int rs, Col<float4> A, Col<float4> B,
                                 int lightNum, const BSDF &bs, PowMemo &pm, V p, V n, V wo, float rayEps, float time,
                                 const float ul[3], const float ub[3], FVal &F, uint32_t &fl, Pushes &out,
                                 unsigned long long *aMask, unsigned long long *mMask) {
     constexpr int NQ = Bands<NB>::NQ;
-    const size_t c = P.cap;
+    const uint32_t c = (uint32_t)P.cap;
     const float *sp = S.spectra;
     float4 *mb = P.M + slot, *kb = P.K + slot;
     PGD_T0(LIGHT);
@@ -633,7 +681,10 @@ PGD_INLINE void estimate_direct(const DevScene &S, const PathSoA &P, int slot, i
     float lightPdf, bsdfPdf;
     Seg vis;
     Emit em;
+    PGD_T0(LSAMP);
     light_sample_L<FEAT>(S, Lt, p, rayEps, ul, &wi, &lightPdf, &vis, &em);
+    PGD_T1(LSAMP);
+    PGD_T0(LEVAL);
     if (lightPdf > 0. && !emit_black<NB, FEAT>(S, em)) bsdf_f(pm, bs, wo, wi, flags, F);
     // no matching BxDF (e.g. the light below the surface): f is black, A unused
     const bool withA = lightPdf > 0. && !emit_black<NB, FEAT>(S, em) && !(F.mode == FV_SUM && F.n == 0);
@@ -643,7 +694,7 @@ PGD_INLINE void estimate_direct(const DevScene &S, const PathSoA &P, int slot, i
         const int lane = threadIdx.x & 63;
         if (lane == __ffsll((long long)act) - 1) *aMask = m;
         const int rank = __popcll(m & ((1ull << lane) - 1ull));
-        A += rank;
+        A.i += (uint32_t)rank;
         if (!P.nInst) rsS = (slot & ~63) + rank;
     }
     if (withA) {
@@ -655,6 +706,8 @@ PGD_INLINE void estimate_direct(const DevScene &S, const PathSoA &P, int slot, i
             float weight = power_heuristic(lightPdf, bsdfPdf);
             sc = fabsf(vdot(wi, n)) * weight / lightPdf;
         }
+        PGD_T1(LEVAL);
+        PGD_T0(LSTORE);
         // A_i = (f_i * Li_i) * sc ; written while testing f for black (A unused if black)
         bool black = true;
 #pragma unroll
@@ -665,7 +718,10 @@ PGD_INLINE void estimate_direct(const DevScene &S, const PathSoA &P, int slot, i
                 cmp(a, k) = (cmp(f, k) * cmp(e, k)) * sc;
                 if (4 * q + k < NB) black = black && (cmp(f, k) == 0.);
             }
-            A[q * c] = a;
+#ifdef PGD_EXP_NO_AB   // timing experiment only: the A / B band stores suppressed (wrong radiance)
+            if (__float_as_uint(a.x) == 0x7fc01234u)
+#endif
+            A[(uint32_t)q * c] = a;
         }
         if (!black) {
             Ray sr;
@@ -675,6 +731,7 @@ PGD_INLINE void estimate_direct(const DevScene &S, const PathSoA &P, int slot, i
             out.s = true;
             out.sIdx = rsS;
         }
+        PGD_T1(LSTORE);
     }
     PGD_T1(LIGHT);
     PGD_T0(MIS);
@@ -715,7 +772,7 @@ PGD_INLINE void estimate_direct(const DevScene &S, const PathSoA &P, int slot, i
                 const int lane = threadIdx.x & 63;
                 if (lane == __ffsll((long long)act) - 1) *mMask = m;
                 const int rank = __popcll(m & ((1ull << lane) - 1ull));
-                B += rank;
+                B.i += (uint32_t)rank;
                 if (!P.nInst) rsM = (slot & ~63) + rank;
             }
             if (withB) {
@@ -729,7 +786,10 @@ PGD_INLINE void estimate_direct(const DevScene &S, const PathSoA &P, int slot, i
                         cmp(b, k) = (((cmp(f, k) * cmp(e, k)) * ad) * weight) / bsdfPdf;
                         if (4 * q + k < NB) black = black && (cmp(f, k) == 0.);
                     }
-                    B[q * c] = b;
+#ifdef PGD_EXP_NO_AB
+                    if (__float_as_uint(b.x) == 0x7fc01234u)
+#endif
+                    B[(uint32_t)q * c] = b;
                 }
                 if (!black) {
                     ray_store(P, RAY_M, rsM, mr);
@@ -751,7 +811,7 @@ template <int NB, int FEAT>
 PGD_INLINE Pushes shade_vertex(const DevScene &S, const PathSoA &P, int slot, int vb, const Ray &ray, int prim,
                                float thit, uint32_t &fl, LAdds *la, int qout, unsigned long long mb1) {
     constexpr int NQ = Bands<NB>::NQ;
-    const size_t c = P.cap;
+    const uint32_t c = (uint32_t)P.cap, us = (uint32_t)slot;
     const float *sp = S.spectra;
     Pushes out = {false, false, false};
     float4 *mb = P.M + slot;
@@ -767,7 +827,7 @@ PGD_INLINE Pushes shade_vertex(const DevScene &S, const PathSoA &P, int slot, in
         la->emitOff = (al >= 0 && vdot(is.dg.nn, vneg(ray.d)) > 0.f) ? S.lights[al].spec : -1;
     }
     PGD_T0(BSDF);
-    const uint32_t hp = P.hp[slot], s = P.smp[slot], spp = (uint32_t)S.spp;
+    const uint32_t hp = *sa(P.hp, us), s = *sa(P.smp, us), spp = (uint32_t)S.spp;
     // only the camera ray carries differentials (path.cpp:107 drops them); they matter only
     // to textured materials
     float diff[4] = {0.f, 0.f, 0.f, 0.f};
@@ -842,12 +902,15 @@ PGD_INLINE Pushes shade_vertex(const DevScene &S, const PathSoA &P, int slot, in
     V wi;
     float pdf;
     int sflags;
+    PGD_T0(CSAMP);
     bsdf_sample_f(pm, bs, wo, &wi, up[0], up[1], up[2], &pdf, BSDF_ALL, &sflags, F);
+    PGD_T1(CSAMP);
+    PGD_T0(CBAND);
     bool cont = pdf != 0. && !(F.mode == FV_SUM && F.n == 0);
     if (cont) {
         fval_prepare<NB, FEAT>(S, F, mb, c);
         const float ad = fabsf(vdot(wi, n));
-        const float4 *bv = beta_rd<NB>(P, vb, 1, slot, mb1);
+        const Col<float4> bv = beta_rd<NB>(P, vb, 1, slot, mb1);
         float4 nb4[NQ];
         bool black = true;
 #pragma unroll
@@ -882,11 +945,12 @@ PGD_INLINE Pushes shade_vertex(const DevScene &S, const PathSoA &P, int slot, in
         const int buf = pass_buf(P, 0), lane = threadIdx.x & 63;
         if (lane == __ffsll((long long)act) - 1) *beta_mask(P, buf, slot) = bm;
         if (cont) {
-            float4 *bn = beta_reg<NB>(P, buf, slot) + __popcll(bm & ((1ull << lane) - 1ull));
+            Col<float4> bn = beta_reg<NB>(P, buf, slot);
+            bn.i += (uint32_t)__popcll(bm & ((1ull << lane) - 1ull));
             bool nf = false;
 #pragma unroll
             for (int q = 0; q < NQ; ++q) {
-                bn[q * c] = nb4[q];
+                bn[(uint32_t)q * c] = nb4[q];
 #pragma unroll
                 for (int k = 0; k < 4; ++k)
                     if (4 * q + k < NB) nf = nf || !(fabsf(cmp(nb4[q], k)) < INFINITY);
@@ -904,6 +968,7 @@ PGD_INLINE Pushes shade_vertex(const DevScene &S, const PathSoA &P, int slot, in
         mt_store(P, slot, rng);
         if (rng.init) fl |= PF_MTINIT;
     }
+    PGD_T1(CBAND);
     PGD_T1(CONT);
     return out;
 }
@@ -917,10 +982,10 @@ template <int NB, int FEAT>
 PGD_INLINE Pushes shade_slot(const DevScene &S, const PathSoA &P, int slot, float *__restrict__ Lout, bool *done,
                              bool *zeroed, int qout) {
     constexpr int NQ = Bands<NB>::NQ;
-    const size_t c = P.cap;
+    const uint32_t c = (uint32_t)P.cap, us = (uint32_t)slot, rc = (uint32_t)P.rcap;
     PGD_T0(LOAD);
-    uint32_t fl = P.flags[slot];
-    const int b = P.bounce[slot];
+    uint32_t fl = *sa(P.flags, us);
+    const int b = *sa(P.bounce, us);
     const WaveMasks wm = wave_masks(P, qout, slot);
     Pushes out = {false, false, false};
     PGD_T1(LOAD);
@@ -931,15 +996,15 @@ PGD_INLINE Pushes shade_slot(const DevScene &S, const PathSoA &P, int slot, floa
     bool useA = false, useB = false;
     if (fin) {
         // the shadow ray's answer: at A's compacted entry (path integrator without instances)
-        useA = (fl & PF_PA) && !P.occ[P.nInst ? slot : (slot & ~63) + wave_rank(wm.a, slot)];
+        useA = (fl & PF_PA) && !*sa(P.occ, P.nInst ? us : (us & ~63u) + (uint32_t)wave_rank(wm.a, slot));
         if (fl & PF_PB) {
             const int ln = (int)(fl >> PF_LIGHT_SHIFT);
             const int mi = P.nInst ? slot : (slot & ~63) + wave_rank(wm.b, slot);   // the MIS ray's record
-            int mp = P.hitPrim[P.rcap + mi];
+            int mp = *sa(P.hitPrim, rc + (uint32_t)mi);
             if ((FEAT & FEAT_INF) && S.lights[ln].type == PBRTGPU_LIGHT_INFINITE) useB = mp < 0;   // Li = light->Le(ray)
             else if (mp >= 0 && S.prims[mp].area_light == ln) {
                 Ray mr = ray_load(P, RAY_M, mi);
-                useB = vdot(isect_nn(S, mr, mp, P.hitT[P.rcap + mi], inst_rec(P, slot)), vneg(mr.d)) > 0.f;   // DiffuseAreaLight::L
+                useB = vdot(isect_nn(S, mr, mp, *sa(P.hitT, rc + (uint32_t)mi), inst_rec(P, slot)), vneg(mr.d)) > 0.f;   // DiffuseAreaLight::L
             }
         }
         fl &= ~(PF_PEND | PF_PA | PF_PB);
@@ -950,13 +1015,13 @@ PGD_INLINE Pushes shade_slot(const DevScene &S, const PathSoA &P, int slot, floa
     int vb = b;
     if (fl & PF_CONT) {
         vb = b + 1;
-        const int prim = P.hitPrim[slot];
+        const int prim = *sa(P.hitPrim, us);
         fl &= ~PF_CONT;
         if (prim < 0) esc = vb == 0 ? 1 : ((fl & PF_SPEC) ? 2 : 0);
         else {
             Ray ray = ray_load(P, RAY_C, slot);
-            out = shade_vertex<NB, FEAT>(S, P, slot, vb, ray, prim, P.hitT[slot], fl, &la, qout, wm.b1);
-            P.bounce[slot] = vb;
+            out = shade_vertex<NB, FEAT>(S, P, slot, vb, ray, prim, *sa(P.hitT, us), fl, &la, qout, wm.b1);
+            *sa(P.bounce, us) = vb;
         }
     }
     PGD_T0(OUT);
@@ -971,25 +1036,26 @@ PGD_INLINE Pushes shade_slot(const DevScene &S, const PathSoA &P, int slot, floa
     *done = !(fl & (PF_CONT | PF_PEND));
     *zeroed = false;
     if (!(addFin || addEmit || addZero || addEsc || *done)) {
-        P.flags[slot] = fl;
+        *sa(P.flags, us) = fl;
         PGD_T1(OUT);
         return out;
     }
     float4 L[NQ];
     const bool lz = (fl & PF_LZ) != 0;
 #pragma unroll
-    for (int q = 0; q < NQ; ++q) L[q] = lz ? make_float4(0.f, 0.f, 0.f, 0.f) : P.L[q * c + slot];
+    for (int q = 0; q < NQ; ++q) L[q] = lz ? make_float4(0.f, 0.f, 0.f, 0.f) : *sa(P.L, (uint32_t)q * c + us);
     if (addFin) {   // L += beta_b * (nLights * Ld), Ld = (0 [+ A]) [+ B]
         const float nl = (float)S.nLights;
         // A of vertex b: written by the previous pass (queue set qout ^ 1), compacted per wave
-        const float4 *A = A_reg<NB>(P, qout ^ 1, slot) + wave_rank(wm.a, slot),
-                     *B = B_reg<NB>(P, qout ^ 1, slot) + wave_rank(wm.b, slot);
-        const float4 *bb4 = beta_rd<NB>(P, b, 2, slot, wm.b2);
+        Col<float4> A = A_reg<NB>(P, qout ^ 1, slot), B = B_reg<NB>(P, qout ^ 1, slot);
+        A.i += (uint32_t)wave_rank(wm.a, slot);
+        B.i += (uint32_t)wave_rank(wm.b, slot);
+        const Col<float4> bb4 = beta_rd<NB>(P, b, 2, slot, wm.b2);
 #pragma unroll
         for (int q = 0; q < NQ; ++q) {
             float4 bt = beta_q(bb4, q, c);
-            float4 a = useA ? A[q * c] : make_float4(0.f, 0.f, 0.f, 0.f);
-            float4 bb = useB ? B[q * c] : make_float4(0.f, 0.f, 0.f, 0.f);
+            float4 a = useA ? A[(uint32_t)q * c] : make_float4(0.f, 0.f, 0.f, 0.f);
+            float4 bb = useB ? B[(uint32_t)q * c] : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 float Ld = 0.f;
@@ -1000,13 +1066,12 @@ PGD_INLINE Pushes shade_slot(const DevScene &S, const PathSoA &P, int slot, floa
         }
     }
     if (addEmit || addZero) {   // vertex vb: L += beta * Le, then L += beta * (nLights * 0)
-        const float *Ls = S.spectra + (la.emitOff >= 0 ? la.emitOff : 0);
-        const float4 *bv4 = beta_rd<NB>(P, vb, 1, slot, wm.b1);
+        const Col<float4> bv4 = beta_rd<NB>(P, vb, 1, slot, wm.b1);
 #pragma unroll
         for (int q = 0; q < NQ; ++q) {
             const float4 bt = beta_q(bv4, q, c);
             if (addEmit) {
-                const float4 e = la.emitOff >= 0 ? ld4(Ls + 4 * q) : make_float4(0.f, 0.f, 0.f, 0.f);
+                const float4 e = la.emitOff >= 0 ? ld4(S.spectra, la.emitOff + 4 * q) : make_float4(0.f, 0.f, 0.f, 0.f);
                 L[q].x += bt.x * e.x; L[q].y += bt.y * e.y; L[q].z += bt.z * e.z; L[q].w += bt.w * e.w;
             }
             if (addZero) { L[q].x += bt.x * 0.f; L[q].y += bt.y * 0.f; L[q].z += bt.z * 0.f; L[q].w += bt.w * 0.f; }
@@ -1042,13 +1107,13 @@ PGD_INLINE Pushes shade_slot(const DevScene &S, const PathSoA &P, int slot, floa
             }
         }
     }
-    if (*done) *zeroed = path_output<NB>(S, L, Lout, P.item[slot], P.smp[slot]);
+    if (*done) *zeroed = path_output<NB>(S, L, Lout, *sa(P.item, us), *sa(P.smp, us));
     else {
 #pragma unroll
-        for (int q = 0; q < NQ; ++q) P.L[q * c + slot] = L[q];
+        for (int q = 0; q < NQ; ++q) *sa(P.L, (uint32_t)q * c + us) = L[q];
         fl &= ~PF_LZ;
     }
-    P.flags[slot] = fl;
+    *sa(P.flags, us) = fl;
     PGD_T1(OUT);
     return out;
 }
@@ -1057,6 +1122,10 @@ PGD_INLINE Pushes shade_slot(const DevScene &S, const PathSoA &P, int slot, floa
 #define PGD_SHADE_BLOCK 256
 #endif
 static const int kShadeBlock = PGD_SHADE_BLOCK;
+// The per-wave compaction of A / B / beta and of the shadow / MIS ray records (wave region =
+// slot & ~63, rank = lanes below that wrote) needs whole 64-lane waves with slot = block * blockDim
+// + lane, every pass
+static_assert(kShadeBlock % 64 == 0, "k_shade blocks must be whole waves");
 // k_shade<NB, FEAT> launch (defined in shade.hip, one translation unit per variant)
 template <int NB, int FEAT>
 hipError_t launch_shade(int grid, hipStream_t stream, const DevScene &S, const PathSoA &P, const ItemSrc &src, int qout,

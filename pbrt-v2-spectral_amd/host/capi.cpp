@@ -17,8 +17,14 @@ static void SetErr(char *err, int errlen, const std::string &msg) {
 
 extern "C" {
 
+int pbrthost_abi_version(void) { return PBRTHOST_ABI_VERSION; }
+
 int pbrthost_load(const char *path, const pbrthost_overrides *ov, pbrthost_scene **out, char *err, int errlen) {
     if (!path || !out) { SetErr(err, errlen, "null argument"); return -1; }
+    if (ov && ov->abi_version != PBRTHOST_ABI_VERSION) {
+        SetErr(err, errlen, "pbrthost_overrides ABI version mismatch (caller built against another pbrthost.h)");
+        return -1;
+    }
     HostScene *s = new HostScene();
     std::string e, p(path);
     bool ok;

@@ -1395,6 +1395,7 @@ private:
                 std::vector<Isect> r;
                 RefineShape(shape, &r);
                 nextPrimId += (uint32_t)r.size() + (shape->kind == ShapeObj::LOOP ? 1u : 0u);
+                if (r.empty()) return;   // api.cpp:1099: no TransformedPrimitive (and no id) then
                 if (r.size() > 1) nextPrimId++;
             }
             Xform w2o0, w2o1;

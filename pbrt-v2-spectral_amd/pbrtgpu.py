@@ -72,8 +72,11 @@ class FlatScene(ctypes.Structure):
                 ("spectral_sampling", I32), ("camera_type", I32), ("lens", Lens)]
 
 
+PBRTHOST_ABI_VERSION = 2   # include/pbrthost.h
+
+
 class Overrides(ctypes.Structure):
-    _fields_ = [("xres", I32), ("yres", I32), ("spp", I32), ("maxdepth", I32), ("bands", I32),
+    _fields_ = [("abi_version", I32), ("xres", I32), ("yres", I32), ("spp", I32), ("maxdepth", I32), ("bands", I32),
                 ("seed", ctypes.c_uint32), ("integrator", I32), ("dl_strategy", I32), ("meta_strategy", I32),
                 ("renderer", I32), ("wave_bands", I32), ("spectral_sampling", I32)]
 
@@ -120,6 +123,9 @@ def host_lib():
     global _host
     if _host is None:
         _host = _load("libpbrthost.so")
+        if _host.pbrthost_abi_version() != PBRTHOST_ABI_VERSION:
+            raise RuntimeError("libpbrthost.so ABI %d, this mirror expects %d" % (_host.pbrthost_abi_version(),
+                                                                                 PBRTHOST_ABI_VERSION))
         _host.pbrthost_load.argtypes = [ctypes.c_char_p, ctypes.POINTER(Overrides), ctypes.POINTER(P),
                                         ctypes.c_char_p, ctypes.c_int]
         _host.pbrthost_flat.argtypes = [P, ctypes.POINTER(FlatScene)]
@@ -138,7 +144,7 @@ def host_lib():
 
 def host_symbols():
     """Symbols declared in include/pbrthost.h."""
-    return ["pbrthost_load", "pbrthost_free", "pbrthost_flat", "pbrthost_save_pack", "pbrthost_set_render",
+    return ["pbrthost_abi_version", "pbrthost_load", "pbrthost_free", "pbrthost_flat", "pbrthost_save_pack", "pbrthost_set_render",
             "pbrthost_info", "pbrthost_write_dat", "pbrthost_write_dat_scene", "pbrthost_spectrum_from_rgb",
             "pbrthost_write_metadata", "pbrthost_set_loop_subdivider", "pbrthost_loop_refine"]
 
@@ -253,7 +259,7 @@ class Scene:
         and its "nWaveBands" / "samplingMethod"."""
         h = P()
         err = ctypes.create_string_buffer(1024)
-        ov = Overrides(xres, yres, spp, maxdepth, bands, KEEP_SEED if seed is None else seed,
+        ov = Overrides(PBRTHOST_ABI_VERSION, xres, yres, spp, maxdepth, bands, KEEP_SEED if seed is None else seed,
                        -1 if integrator is None else INTEGRATORS[integrator],
                        DL_STRATEGIES.get(strategy, -1), META_STRATEGIES.get(strategy, -1),
                        -1 if renderer is None else RENDERERS[renderer], wave_bands,

@@ -518,7 +518,7 @@ def test_spectral_renderer_vs_reference_golden(pg, base):
     rel = np.abs(L - ref).max(axis=1) / np.maximum(np.abs(ref).max(axis=1), 1e-30)
     # a singleDirection sample is nWaveBands paths: one last-ulp transcendental difference
     #  in any of them shows in its row (measured: 0.970 - 1.0 bit-exact,
-    # tools/dbg/exact_rates.py; the oracle 1.0)
+    # tools/exact_rates.py; the oracle 1.0)
     assert same.mean() >= 0.95, "bit-exact samples %d/%d" % (same.sum(), len(same))
     assert (rel > 1e-4).mean() <= 5e-4
     assert np.abs(film - gf["film"]).max() / np.abs(gf["film"]).max() < 1e-4

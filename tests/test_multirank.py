@@ -35,7 +35,7 @@ def tile_mask(pg, scene, tiles, tile=16):
     return m
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, mode="shared"):
     import sys
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "pbrt-v2-spectral_amd"))
@@ -47,17 +47,24 @@ def _worker(rank, world, port, q):
     ntx, nty = pg.tile_grid(scene)
     tiles = pg.tile_slice(ntx * nty, rank, world)
     shape = (scene.height, scene.width, scene.bands)
-    path, film = bench.shared_film(shape, rank, dist, "test_%d" % port)
+    if mode == "shared":   # all ranks on one node: the /dev/shm film
+        path, film = bench.shared_film(shape, rank, dist, "test_%d" % port)
+    else:                  # ranks on several nodes: private films, summed onto rank 0 afterwards
+        path, film = None, np.zeros(shape, np.float32)
     mine, _ = pg.oracle().render(scene, threads=2)       # this rank's film (stands in for its GPU)
     m = tile_mask(pg, scene, tiles)
     film[m] = mine[m]                                    # host gather of the slice's pixels
-    film.flush()
+    if mode == "shared":
+        film.flush()
+    else:
+        film = bench.compose_film(film, dist)
     elapsed, total = bench.reduce_over_ranks(dist, 1.0 + rank, 100.0 * (rank + 1))
     dist.barrier()
     if rank == 0:
         full, _ = pg.oracle().render(scene, threads=2)
         same = bool(np.array_equal(np.asarray(film).view(np.int32), full.view(np.int32)))
-        os.unlink(path)
+        if path:
+            os.unlink(path)
     else:
         same = None
     q.put((rank, tiles.tolist(), int(ntx * nty), elapsed, total, same))
@@ -65,12 +72,12 @@ def _worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_tile_slices_gather_and_reduction(world):
+@pytest.mark.parametrize("world,mode", [(2, "shared"), (3, "shared"), (2, "compose")])
+def test_tile_slices_gather_and_reduction(world, mode):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    ps = [ctx.Process(target=_worker, args=(r, world, port, q, mode)) for r in range(world)]
     for p in ps:
         p.start()
     res = sorted(q.get(timeout=180) for _ in range(world))
@@ -93,3 +100,15 @@ def test_tile_slices_match_render_multi_dealing(pg):
         assert sorted(got.tolist()) == list(range(n))
         for j in range(m):
             assert pg.tile_slice(n, j, m).tolist() == list(range(n))[j::m]
+
+
+def test_one_node_detection(monkeypatch):
+    """bench.py uses the /dev/shm film only when every rank is on this node (torchrun's
+    LOCAL_WORLD_SIZE == WORLD_SIZE); otherwise each rank keeps its own film (compose_film)."""
+    import sys
+    sys.path.insert(0, ROOT)
+    import bench
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "8")
+    assert bench.one_node(8) and not bench.one_node(16)
+    monkeypatch.delenv("LOCAL_WORLD_SIZE")
+    assert bench.one_node(4)

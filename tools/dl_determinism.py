@@ -1,7 +1,7 @@
-# scratch: DirectLighting determinism + oracle agreement on coverage.pbrt (PBRTGPU_LIB variants)
+# DirectLighting determinism + oracle agreement on coverage.pbrt (PBRTGPU_LIB variants)
 import os, sys
 import numpy as np
-R = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "..")
+R = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
 sys.path.insert(0, os.path.join(R, "pbrt-v2-spectral_amd"))
 import pbrtgpu as pg
 scene = pg.Scene.load(os.path.join(R, "scenes", "coverage.pack"), xres=40, yres=30, spp=4, maxdepth=3,

@@ -1,0 +1,7 @@
+#!/bin/bash
+set -e
+OUT=$PWD/gpurun_out/r03k
+mkdir -p $OUT
+timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 || { tail -40 $OUT/pytest_gpu.log; exit 1; }
+tail -1 $OUT/pytest_gpu.log
+bash tools/gpu_exp_bench.sh r03k/c2

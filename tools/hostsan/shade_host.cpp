@@ -264,7 +264,7 @@ int main(int argc, char **argv) {
                         "[--strategy S] [--slots N] [--poison BYTE] [--keys FILE] --out FILE\n", argv[0]);
         return 2;
     }
-    pbrthost_overrides ov = {-1, -1, -1, -1, 0, PBRTHOST_KEEP_SEED, -1, -1, -1, -1, -1, -1};
+    pbrthost_overrides ov = {PBRTHOST_ABI_VERSION, -1, -1, -1, -1, 0, PBRTHOST_KEEP_SEED, -1, -1, -1, -1, -1, -1};
     int nSlots = 256, mtKat = 0;
     const char *out = nullptr, *keyFile = nullptr, *strategy = nullptr;
     for (int i = 2; i + 1 < argc; i += 2) {

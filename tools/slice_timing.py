@@ -1,7 +1,7 @@
-# scratch: per-GPU step time for 1/N of the C2 frame (what each rank renders at N GPUs)
+# per-GPU step time for 1/N of the C2 frame (what each rank renders at N GPUs)
 import os, sys, time
 import numpy as np
-R = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "..")
+R = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
 sys.path.insert(0, os.path.join(R, "pbrt-v2-spectral_amd"))
 import pbrtgpu as pg
 scene = pg.Scene.load(os.path.join(R, "scenes", "killeroo-simple.pack"))
