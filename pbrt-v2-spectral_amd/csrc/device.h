@@ -69,6 +69,18 @@ PGD_INLINE float TANF(float x) { return __tanf(x); }
 PGD_INLINE float ATANF(float x) { return atanf(x); }
 #endif
 
+// Scene and slot arrays are addressed through a 32-bit element index from their base: the base
+// is a kernel argument (wave-uniform, in SGPRs) and the byte offset a 32-bit value, so a load or
+// store takes one VGPR of address (global saddr mode) instead of a 64-bit per-lane pointer --
+// fewer registers live across the kernels and no 64-bit address arithmetic.  Every array
+// addressed this way is < 4 GiB (scene_build.h and pbrtgpu.hip ensure_slots check it).
+template <class T> PGD_INLINE T *sa(T *base, uint32_t i) {
+    return reinterpret_cast<T *>(reinterpret_cast<char *>(base) + (uint32_t)(i * (uint32_t)sizeof(T)));
+}
+template <class T> PGD_INLINE const T *sa(const T *base, uint32_t i) {
+    return reinterpret_cast<const T *>(reinterpret_cast<const char *>(base) + (uint32_t)(i * (uint32_t)sizeof(T)));
+}
+
 // ------------------------------------------------------------------ vectors
 struct V { float x, y, z; };
 PGD_INLINE V v3(float x, float y, float z) { V r; r.x = x; r.y = y; r.z = z; return r; }
@@ -353,17 +365,17 @@ PGD_INLINE bool tri_hit(const DevTri &t, const Ray &ray, float *tHit) {
     return true;
 }
 PGD_INLINE void tri_uvs(const DevScene &S, const pbrtgpu_triangle &t, float uv[3][2]) {
-    const pbrtgpu_mesh &m = S.meshes[t.mesh];
+    const pbrtgpu_mesh &m = (*sa(S.meshes, (uint32_t)(t.mesh)));
     if (m.has_uvs) {
-        for (int k = 0; k < 3; ++k) { uv[k][0] = S.vertUV[2 * t.v[k]]; uv[k][1] = S.vertUV[2 * t.v[k] + 1]; }
+        for (int k = 0; k < 3; ++k) { uv[k][0] = (*sa(S.vertUV, (uint32_t)(2 * t.v[k]))); uv[k][1] = (*sa(S.vertUV, (uint32_t)(2 * t.v[k] + 1))); }
     } else {
         uv[0][0] = 0.; uv[0][1] = 0.; uv[1][0] = 1.; uv[1][1] = 0.; uv[2][0] = 1.; uv[2][1] = 1.;
     }
 }
 // full Triangle::Intersect (dg + rayEpsilon) for a known-hit triangle
 PGD_INLINE bool tri_intersect(const DevScene &S, int ti, const Ray &ray, float *tHit, float *rayEps, DG *dg) {
-    const pbrtgpu_triangle t = S.tris[ti];
-    V p1 = ldv(S.vertP + 3 * t.v[0]), p2 = ldv(S.vertP + 3 * t.v[1]), p3 = ldv(S.vertP + 3 * t.v[2]);
+    const pbrtgpu_triangle t = (*sa(S.tris, (uint32_t)(ti)));
+    V p1 = ldv(sa(S.vertP, (uint32_t)(3 * t.v[0]))), p2 = ldv(sa(S.vertP, (uint32_t)(3 * t.v[1]))), p3 = ldv(sa(S.vertP, (uint32_t)(3 * t.v[2])));
     V e1 = vsub(p2, p1), e2 = vsub(p3, p1);
     V s1 = vcross(ray.d, e2);
     float divisor = vdot(s1, e1);
@@ -394,7 +406,7 @@ PGD_INLINE bool tri_intersect(const DevScene &S, int ti, const Ray &ray, float *
     float b0 = 1 - b1 - b2;
     float tu = b0 * uvs[0][0] + b1 * uvs[1][0] + b2 * uvs[2][0];
     float tv = b0 * uvs[0][1] + b1 * uvs[1][1] + b2 * uvs[2][1];
-    const pbrtgpu_mesh &m = S.meshes[t.mesh];
+    const pbrtgpu_mesh &m = (*sa(S.meshes, (uint32_t)(t.mesh)));
     dg_init(*dg, rayat(ray, tt), dpdu, dpdv, v3(0, 0, 0), v3(0, 0, 0), tu, tv, m.reverse_orientation ^ m.swaps_handedness);
     *tHit = tt;
     *rayEps = 1e-3f * *tHit;
@@ -412,8 +424,8 @@ PGD_INLINE bool solve2x2(const float A[2][2], const float B[2], float *x0, float
 // nmat: mInv of the ObjectToWorld handed to GetShadingGeometry (the mesh's, or the instance-
 // composed one of TransformedPrimitive::Intersect)
 PGD_INLINE void tri_shading(const DevScene &S, int ti, const float *nmat, const DG &dg, DG &dgs) {
-    const pbrtgpu_triangle t = S.tris[ti];
-    const pbrtgpu_mesh &m = S.meshes[t.mesh];
+    const pbrtgpu_triangle t = (*sa(S.tris, (uint32_t)(ti)));
+    const pbrtgpu_mesh &m = (*sa(S.meshes, (uint32_t)(t.mesh)));
     if (!m.has_normals) { dgs = dg; return; }
     float b[3];
     float uv[3][2];
@@ -422,7 +434,7 @@ PGD_INLINE void tri_shading(const DevScene &S, int ti, const float *nmat, const 
     float C[2] = {dg.u - uv[0][0], dg.v - uv[0][1]};
     if (!solve2x2(A, C, &b[1], &b[2])) b[0] = b[1] = b[2] = 1.f / 3.f;
     else b[0] = 1.f - b[1] - b[2];
-    V n0 = ldv(S.vertN + 3 * t.v[0]), n1 = ldv(S.vertN + 3 * t.v[1]), n2 = ldv(S.vertN + 3 * t.v[2]);
+    V n0 = ldv(sa(S.vertN, (uint32_t)(3 * t.v[0]))), n1 = ldv(sa(S.vertN, (uint32_t)(3 * t.v[1]))), n2 = ldv(sa(S.vertN, (uint32_t)(3 * t.v[2])));
     V ni = vadd(vadd(vmul(n0, b[0]), vmul(n1, b[1])), vmul(n2, b[2]));
     V ns = vnorm(xnormal(nmat, ni));
     V ss = vnorm(dg.dpdu);
@@ -602,19 +614,19 @@ PGD_INLINE bool disk_intersect(const pbrtgpu_quadric &q, const Ray &r, float *tH
 }
 PGD_INLINE float shape_area(const DevScene &S, int type, int idx) {
     if (type == PBRTGPU_SHAPE_TRIANGLE) {
-        const pbrtgpu_triangle t = S.tris[idx];
-        V p1 = ldv(S.vertP + 3 * t.v[0]), p2 = ldv(S.vertP + 3 * t.v[1]), p3 = ldv(S.vertP + 3 * t.v[2]);
+        const pbrtgpu_triangle t = (*sa(S.tris, (uint32_t)(idx)));
+        V p1 = ldv(sa(S.vertP, (uint32_t)(3 * t.v[0]))), p2 = ldv(sa(S.vertP, (uint32_t)(3 * t.v[1]))), p3 = ldv(sa(S.vertP, (uint32_t)(3 * t.v[2])));
         return 0.5f * vlen(vcross(vsub(p2, p1), vsub(p3, p1)));
     }
-    const pbrtgpu_quadric &q = S.quads[idx];
+    const pbrtgpu_quadric &q = (*sa(S.quads, (uint32_t)(idx)));
     if (type == PBRTGPU_SHAPE_SPHERE) return q.phi_max * q.radius * (q.zmax - q.zmin);
     return q.phi_max * 0.5f * (q.radius * q.radius - q.inner_radius * q.inner_radius);
 }
 PGD_HEAVY bool shape_intersect(const DevScene &S, int type, int idx, const Ray &r, float *tHit, float *eps, DG *dg,
                                bool nnOnly = false) {
     if (type == PBRTGPU_SHAPE_TRIANGLE) return tri_intersect(S, idx, r, tHit, eps, dg);
-    if (type == PBRTGPU_SHAPE_SPHERE) return sphere_intersect(S.quads[idx], r, tHit, eps, dg, nnOnly);
-    return disk_intersect(S.quads[idx], r, tHit, eps, dg, nnOnly);
+    if (type == PBRTGPU_SHAPE_SPHERE) return sphere_intersect((*sa(S.quads, (uint32_t)(idx))), r, tHit, eps, dg, nnOnly);
+    return disk_intersect((*sa(S.quads, (uint32_t)(idx))), r, tHit, eps, dg, nnOnly);
 }
 
 // ------------------------------------------------------------------ BVH traversal
@@ -699,8 +711,8 @@ PGD_INLINE bool quadric_test(const DevScene &S, int type, int idx, const Ray &r,
     return th != -INFINITY;
 }
 PGD_INLINE bool prim_hit(const DevScene &S, Stack &st, int pi, const Ray &ray, float *t) {
-    const pbrtgpu_prim pr = S.prims[pi];
-    if (pr.shape_type == PBRTGPU_SHAPE_TRIANGLE) { st.cTris++; return tri_hit(S.primTri[pi], ray, t); }
+    const pbrtgpu_prim pr = (*sa(S.prims, (uint32_t)(pi)));
+    if (pr.shape_type == PBRTGPU_SHAPE_TRIANGLE) { st.cTris++; return tri_hit((*sa(S.primTri, (uint32_t)(pi))), ray, t); }
     st.cQuads++;
     return quadric_test(S, pr.shape_type, pr.shape_index, ray, t);
 }
@@ -839,17 +851,17 @@ PGD_INLINE bool bvh_walk(const DevScene &S, Stack &st, int base, uint32_t root, 
 
 template <bool ANY, bool INST>
 PGD_INLINE bool prim_test(const DevScene &S, Stack &st, int base, int pi, Ray &ray, int *hitPrim, float *hitT) {
-    const pbrtgpu_prim pr = S.prims[pi];
+    const pbrtgpu_prim pr = (*sa(S.prims, (uint32_t)(pi)));
     float t;
     if (pr.shape_type == PBRTGPU_SHAPE_TRIANGLE) {
         st.cTris++;
-        if (!tri_hit(S.primTri[pi], ray, &t)) return false;
+        if (!tri_hit((*sa(S.primTri, (uint32_t)(pi))), ray, &t)) return false;
     } else if (!INST || pr.shape_type != PBRTGPU_SHAPE_INSTANCE) {
         st.cQuads++;
         if (!quadric_test<true>(S, pr.shape_type, pr.shape_index, ray, &t)) return false;
     } else {
         if constexpr (INST) {
-            const pbrtgpu_instance &I = S.insts[pr.shape_index];
+            const pbrtgpu_instance &I = (*sa(S.insts, (uint32_t)(pr.shape_index)));
             float m[16];
             inst_interp(I, ray.time, m, nullptr);
             Ray r = xray(m, ray);
@@ -879,12 +891,12 @@ PGD_INLINE bool bvh_walk(const DevScene &S, Stack &st, int base, uint32_t root, 
     int neg[3] = {invDir.x < 0, invDir.y < 0, invDir.z < 0};
     if (ANY) st.cShadow += INST ? 1u : 0u; else st.cRays += INST ? 1u : 0u;
     {
-        const float4 n0 = S.nodes[2 * root], n1 = S.nodes[2 * root + 1];
+        const float4 n0 = (*sa(S.nodes, (uint32_t)(2 * root))), n1 = (*sa(S.nodes, (uint32_t)(2 * root + 1)));
         st.cNodes++;
         if (!bbox_hit(n0, n1, ray, invDir, neg)) return false;
     }
     int todo = base;
-    uint32_t ref = S.nodeRef[root];
+    uint32_t ref = (*sa(S.nodeRef, (uint32_t)(root)));
     bool found = false;
     for (;;) {
         if (ref & WREF_LEAF) {
@@ -895,7 +907,7 @@ PGD_INLINE bool bvh_walk(const DevScene &S, Stack &st, int base, uint32_t root, 
                     found = true;
                 }
         } else {
-            const float4 *w = S.wnodes + 4 * (size_t)ref;
+            const float4 *w = sa(S.wnodes, (uint32_t)(4 * (size_t)ref));
             const float4 l0 = w[0], l1 = w[1], r0 = w[2], r1 = w[3];
             st.cNodes++;
             float tl = 0.f, tr = 0.f;
@@ -960,8 +972,8 @@ PGD_INLINE void inst_load(const float4 *im, int i, float *m, float *minv) {
 PGD_HEAVY void isect_fill(const DevScene &S, const Ray &ray, int prim, float t, Isect &is, const float4 *im);
 // geometric normal dg.nn of a recorded closest hit (the field isect_fill would produce)
 PGD_INLINE V isect_nn(const DevScene &S, const Ray &ray, int prim, float t, const float4 *im) {
-    if (!S.nInsts || S.primInst[prim] < 0) {
-        const pbrtgpu_prim pr = S.prims[prim];
+    if (!S.nInsts || (*sa(S.primInst, (uint32_t)(prim))) < 0) {
+        const pbrtgpu_prim pr = (*sa(S.prims, (uint32_t)(prim)));
         Ray r = ray;
         r.maxt = t;
         float th, e;
@@ -976,7 +988,7 @@ PGD_INLINE V isect_nn(const DevScene &S, const Ray &ray, int prim, float t, cons
 // full intersection record for a recorded closest hit; primitives of a transformed instance
 // are intersected in primitive space and moved to world space (primitive.cpp:94-110)
 PGD_HEAVY void isect_fill(const DevScene &S, const Ray &ray, int prim, float t, Isect &is, const float4 *im) {
-    const pbrtgpu_prim pr = S.prims[prim];
+    const pbrtgpu_prim pr = (*sa(S.prims, (uint32_t)(prim)));
     Ray r = ray;
     r.maxt = t;
     float th;
@@ -984,7 +996,7 @@ PGD_HEAVY void isect_fill(const DevScene &S, const Ray &ray, int prim, float t, 
     is.inst = -1;
     is.time = ray.time;
     is.im = im;
-    const int inst = S.nInsts ? S.primInst[prim] : -1;
+    const int inst = S.nInsts ? (*sa(S.primInst, (uint32_t)(prim))) : -1;
     if (inst < 0) {
         shape_intersect(S, pr.shape_type, pr.shape_index, r, &th, &is.rayEps, &is.dg);
         return;
@@ -1473,7 +1485,7 @@ PGD_INLINE RGBPick rgb_pick(const float rgb[3]) {
     return p;
 }
 PGD_INLINE float4 from_rgb4(const DevScene &S, const RGBPick &p, bool illum, int q) {
-    const float *b = S.basis + (illum ? 7 : 0) * S.nbp + 4 * q;
+    const float *b = sa(S.basis, (uint32_t)((illum ? 7 : 0) * S.nbp + 4 * q));
     const float4 x = *reinterpret_cast<const float4 *>(b + p.k0 * S.nbp);
     const float4 y = *reinterpret_cast<const float4 *>(b + p.k1 * S.nbp);
     const float4 z = *reinterpret_cast<const float4 *>(b + p.k2 * S.nbp);
@@ -1531,7 +1543,7 @@ PGD_INLINE void mip_ewa0(const DevScene &S, const float *T, int wrap, float s, f
             float r2 = A * ss * ss + B * ss * tt + C * tt * tt;
             if (r2 < 1.) {
                 int li = (int)(r2 * 128);
-                float weight = S.ewa[li < 127 ? li : 127];
+                float weight = (*sa(S.ewa, (uint32_t)(li < 127 ? li : 127)));
 #pragma unroll
                 for (int k = 0; k < NC; ++k) sum[k] += texel_c(T, wrap, is, it, k) * weight;
                 sumWts += weight;
@@ -1587,7 +1599,7 @@ PGD_INLINE void tex_image(const DevScene &S, const pbrtgpu_texture &tx, const Te
     mip_lookup<NC>(S, tx, s, t, dsdx, dtdx, dsdy, dtdy, out);
 }
 PGD_INLINE float tex_leaf_float(const DevScene &S, int id, const TexPt &q) {
-    const pbrtgpu_texture &tx = S.tex[id];
+    const pbrtgpu_texture &tx = (*sa(S.tex, (uint32_t)(id)));
     if (tx.type == PBRTGPU_TEX_CONST) return tx.value;
     float v;
     tex_image<1>(S, tx, q, &v);
@@ -1595,7 +1607,7 @@ PGD_INLINE float tex_leaf_float(const DevScene &S, int id, const TexPt &q) {
 }
 // Texture<float>: CONST, IMAGE, or ScaleTexture of two leaves (front end guarantees the depth)
 PGD_HEAVY float tex_float(const DevScene &S, int id, const TexPt &q) {
-    const pbrtgpu_texture &tx = S.tex[id];
+    const pbrtgpu_texture &tx = (*sa(S.tex, (uint32_t)(id)));
     if (tx.type != PBRTGPU_TEX_SCALE) return tex_leaf_float(S, id, q);
     return tex_leaf_float(S, tx.tex1, q) * tex_leaf_float(S, tx.tex2, q);
 }
@@ -1606,22 +1618,22 @@ PGD_HEAVY SpecTex tex_spec_prepare(const DevScene &S, int id, const TexPt &q) {
     SpecTex r;
     r.constOff = -1; r.constFirst = false;
     int img = id;
-    const pbrtgpu_texture &tx = S.tex[id];
+    const pbrtgpu_texture &tx = (*sa(S.tex, (uint32_t)(id)));
     if (tx.type == PBRTGPU_TEX_SCALE) {
-        const bool firstConst = S.tex[tx.tex1].type == PBRTGPU_TEX_CONST;
+        const bool firstConst = (*sa(S.tex, (uint32_t)(tx.tex1))).type == PBRTGPU_TEX_CONST;
         img = firstConst ? tx.tex2 : tx.tex1;
-        r.constOff = S.tex[firstConst ? tx.tex1 : tx.tex2].spec;
+        r.constOff = (*sa(S.tex, (uint32_t)(firstConst ? tx.tex1 : tx.tex2))).spec;
         r.constFirst = firstConst;
     }
     float rgb[3];
-    tex_image<3>(S, S.tex[img], q, rgb);
+    tex_image<3>(S, (*sa(S.tex, (uint32_t)(img))), q, rgb);
     r.pick = rgb_pick(rgb);
     return r;
 }
 PGD_INLINE float4 tex_spec4(const DevScene &S, const SpecTex &t, int q) {
     float4 a = from_rgb4(S, t.pick, false, q);
     if (t.constOff < 0) return a;
-    float4 b = *reinterpret_cast<const float4 *>(S.spectra + t.constOff + 4 * q);
+    float4 b = *reinterpret_cast<const float4 *>(sa(S.spectra, (uint32_t)(t.constOff + 4 * q)));
     return t.constFirst ? make_float4(b.x * a.x, b.y * a.y, b.z * a.z, b.w * a.w)
                         : make_float4(a.x * b.x, a.y * b.y, a.z * b.z, a.w * b.w);
 }
@@ -1662,12 +1674,12 @@ PGD_HEAVY void compute_differentials(const DG &dg, const RayDiff &rd, float out[
 template <int FEAT>
 PGD_HEAVY void get_bsdf(const DevScene &S, const Isect &is, const float diff[4], float4 *kb, size_t c, BSDF &bs,
                         V *pOut, V *nOut, V *dnOut = nullptr) {
-    const pbrtgpu_prim pr = S.prims[is.prim];
-    const pbrtgpu_material &mt = S.mats[pr.material];
+    const pbrtgpu_prim pr = (*sa(S.prims, (uint32_t)(is.prim)));
+    const pbrtgpu_material &mt = (*sa(S.mats, (uint32_t)(pr.material)));
     DG dgs;
     int ro, swaps;
     if (pr.shape_type == PBRTGPU_SHAPE_TRIANGLE) {
-        const pbrtgpu_mesh &m = S.meshes[S.tris[pr.shape_index].mesh];
+        const pbrtgpu_mesh &m = (*sa(S.meshes, (uint32_t)((*sa(S.tris, (uint32_t)(pr.shape_index))).mesh)));
         if (is.inst < 0) tri_shading(S, pr.shape_index, m.o2w_minv, is.dg, dgs);
         else {
             // ObjectToWorld = Inverse(Identity * w2p): its mInv is Mul(Identity, w2p.m)
@@ -1680,7 +1692,7 @@ PGD_HEAVY void get_bsdf(const DevScene &S, const Isect &is, const float diff[4],
         ro = m.reverse_orientation; swaps = m.swaps_handedness;
     } else {
         dgs = is.dg;
-        const pbrtgpu_quadric &q = S.quads[pr.shape_index];
+        const pbrtgpu_quadric &q = (*sa(S.quads, (uint32_t)(pr.shape_index)));
         ro = q.reverse_orientation; swaps = q.swaps_handedness;
     }
     TexPt tq;
@@ -1868,7 +1880,7 @@ PGD_INLINE float shape_pdf_generic(const DevScene &S, int type, int idx, V p, V 
 }
 PGD_INLINE float shape_pdf(const DevScene &S, int type, int idx, V p, V wi) {
     if (type == PBRTGPU_SHAPE_SPHERE) {
-        const pbrtgpu_quadric &q = S.quads[idx];
+        const pbrtgpu_quadric &q = (*sa(S.quads, (uint32_t)(idx)));
         V Pcenter = xpoint(q.o2w_m, v3(0, 0, 0));
         if (vlen2(vsub(p, Pcenter)) - q.radius * q.radius < 1e-4f) return shape_pdf_generic(S, type, idx, p, wi);
         float sinThetaMax2 = q.radius * q.radius / vlen2(vsub(p, Pcenter));
@@ -1878,9 +1890,9 @@ PGD_INLINE float shape_pdf(const DevScene &S, int type, int idx, V p, V wi) {
     return shape_pdf_generic(S, type, idx, p, wi);
 }
 PGD_INLINE V shape_sample_p(const DevScene &S, int type, int idx, V p, float u1, float u2, V *ns) {
-    if (type == PBRTGPU_SHAPE_SPHERE) return sphere_sample_p(S.quads[idx], p, u1, u2, ns);
+    if (type == PBRTGPU_SHAPE_SPHERE) return sphere_sample_p((*sa(S.quads, (uint32_t)(idx))), p, u1, u2, ns);
     if (type == PBRTGPU_SHAPE_DISK) {
-        const pbrtgpu_quadric &q = S.quads[idx];
+        const pbrtgpu_quadric &q = (*sa(S.quads, (uint32_t)(idx)));
         V pp;
         concentric_disk(u1, u2, &pp.x, &pp.y);
         pp.x *= q.radius; pp.y *= q.radius; pp.z = q.height;
@@ -1888,11 +1900,11 @@ PGD_INLINE V shape_sample_p(const DevScene &S, int type, int idx, V p, float u1,
         if (q.reverse_orientation) *ns = vmul(*ns, -1.f);
         return xpoint(q.o2w_m, pp);
     }
-    const pbrtgpu_triangle t = S.tris[idx];
-    const pbrtgpu_mesh &m = S.meshes[t.mesh];
+    const pbrtgpu_triangle t = (*sa(S.tris, (uint32_t)(idx)));
+    const pbrtgpu_mesh &m = (*sa(S.meshes, (uint32_t)(t.mesh)));
     float su1 = sqrtf(u1);
     float b1 = 1.f - su1, b2 = u2 * su1;
-    V p1 = ldv(S.vertP + 3 * t.v[0]), p2 = ldv(S.vertP + 3 * t.v[1]), p3 = ldv(S.vertP + 3 * t.v[2]);
+    V p1 = ldv(sa(S.vertP, (uint32_t)(3 * t.v[0]))), p2 = ldv(sa(S.vertP, (uint32_t)(3 * t.v[1]))), p3 = ldv(sa(S.vertP, (uint32_t)(3 * t.v[2])));
     V pp = vadd(vadd(vmul(p1, b1), vmul(p2, b2)), vmul(p3, (1.f - b1 - b2)));
     *ns = vnorm(vcross(vsub(p2, p1), vsub(p3, p1)));
     if (m.reverse_orientation) *ns = vmul(*ns, -1.f);
@@ -1960,7 +1972,7 @@ PGD_HEAVY void light_sample_L(const DevScene &S, const pbrtgpu_light &L, V p, fl
         em->div = vlen2(vsub(lp, p));   // Intensity / DistanceSquared
         return;
     }
-    const pbrtgpu_light_shape *shs = S.lightShapes + L.shape_offset;
+    const pbrtgpu_light_shape *shs = sa(S.lightShapes, (uint32_t)(L.shape_offset));
     int sn = sample_discrete(shs, L.n_shapes, u[2]);
     V ns;
     V pt = shape_sample_p(S, shs[sn].shape_type, shs[sn].shape_index, p, u[0], u[1], &ns);
@@ -1992,7 +2004,7 @@ PGD_HEAVY float light_pdf(const DevScene &S, const pbrtgpu_light &L, V p, V wi) 
         if (sintheta == 0.f) return 0.f;
         return L.dist_pdf / (2.f * kPi * kPi * sintheta);
     }
-    const pbrtgpu_light_shape *shs = S.lightShapes + L.shape_offset;
+    const pbrtgpu_light_shape *shs = sa(S.lightShapes, (uint32_t)(L.shape_offset));
     float pp = 0.f;
     for (int i = 0; i < L.n_shapes; ++i) pp += shs[i].area * shape_pdf(S, shs[i].shape_type, shs[i].shape_index, p, wi);
     return pp / L.sum_area;
@@ -2132,7 +2144,7 @@ PGD_INLINE float lens_ray(const DevScene &S, float imageX, float imageY, float l
     }
     float lu, lv;
     concentric_disk(lensU, lensV, &lu, &lv);
-    const float4 last = S.lensEl[S.lensN - 1];
+    const float4 last = (*sa(S.lensEl, (uint32_t)(S.lensN - 1)));
     const float firstAp = last.w / 2, firstR = last.x;
     const float zI = firstR == 0 ? 0.f : (-firstR - sqrtf(firstR * firstR - firstAp * firstAp));
     lu *= firstAp;
@@ -2148,7 +2160,7 @@ PGD_INLINE float lens_ray(const DevScene &S, float imageX, float imageY, float l
     r.time = 0.f;
     float lensDist = 0.f;
     for (int i = S.lensN - 1; i >= 0; --i) {
-        const float4 e = S.lensEl[i];
+        const float4 e = (*sa(S.lensEl, (uint32_t)(i)));
         const float rad = e.x, ap = e.w;
         lensDist += e.y;
         r.o = sp;
@@ -2167,8 +2179,8 @@ PGD_INLINE float lens_ray(const DevScene &S, float imageX, float imageY, float l
             const float n1 = e.z;
             float n2 = 1;
             if (i - 1 >= 0) {
-                n2 = S.lensEl[i - 1].z;
-                if (n2 == 0) n2 = S.lensEl[i - 2].z;
+                n2 = (*sa(S.lensEl, (uint32_t)(i - 1))).z;
+                if (n2 == 0) n2 = (*sa(S.lensEl, (uint32_t)(i - 2))).z;
             }
             lens_snell(n1, n2, rad, nrm, &r, wl, S.lensChromatic);
             sp = ip;
@@ -2208,7 +2220,7 @@ PGD_INLINE float lens_ray_diff(const DevScene &S, float imageX, float imageY, fl
 PGD_INLINE float path_wavelength(const DevScene &S, int item, uint32_t smp) {
     if (!S.specMode) return 0.f;
     const int band = S.specMode == 1 ? item % S.specItems : (int)(smp % (uint32_t)S.specBands);
-    return S.specWl[band];
+    return (*sa(S.specWl, (uint32_t)(band)));
 }
 // the camera ray's differentials for a path (first-hit texture filtering)
 PGD_INLINE RayDiff path_camera_diff(const DevScene &S, int item, uint32_t smp, float imageX, float imageY, float lensU,

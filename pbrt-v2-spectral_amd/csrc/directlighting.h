@@ -33,7 +33,7 @@ PGD_INLINE V dl_vec_load(const float *b, size_t c) { return v3(b[0], b[c], b[2 *
 
 // RoundUpPow2(max(1, nSamples)) samples of light i (directlighting.cpp:53-55)
 PGD_INLINE int dl_count(const DevScene &S, int i) {
-    uint32_t v = (uint32_t)max(1, S.lights[i].n_samples) - 1u;
+    uint32_t v = (uint32_t)max(1, (*sa(S.lights, (uint32_t)(i))).n_samples) - 1u;
     v |= v >> 1; v |= v >> 2; v |= v >> 4; v |= v >> 8; v |= v >> 16;
     return (int)(v + 1u);
 }
@@ -277,7 +277,7 @@ PGD_INLINE Pushes dl_spec_step(const DevScene &S, const PathSoA &P, int slot, fl
         // still happen (the reference constructs them) but no child can be sampled, and the
         // vertex need not be rebuilt
         const int vprim = P.fHit[(size_t)2 * d * c + slot];
-        const int vtype = S.mats[S.prims[vprim].material].type;
+        const int vtype = (*sa(S.mats, (uint32_t)((*sa(S.prims, (uint32_t)(vprim))).material))).type;
         const bool canSpec = vtype == PBRTGPU_MAT_MIRROR || vtype == PBRTGPU_MAT_GLASS;
         if (!SPAWN && canSpec && d + 1 < S.maxDepth && br < 2u) {
             fl |= PF_DLSPEC;
@@ -337,7 +337,7 @@ PGD_INLINE Pushes dl_spec_step(const DevScene &S, const PathSoA &P, int slot, fl
                 ryd = vadd(vsub(wi, dwody), vmul(vadd(vmul(dndy, won), vmul(n, dDNdy)), 2.f));
             } else {
                 // BSDF::eta: the glass material's index, 1 otherwise (glass.cpp:48)
-                const pbrtgpu_material &mt = S.mats[S.prims[vx.is.prim].material];
+                const pbrtgpu_material &mt = (*sa(S.mats, (uint32_t)((*sa(S.prims, (uint32_t)(vx.is.prim))).material)));
                 float eta = mt.type == PBRTGPU_MAT_GLASS ? mt.f[0] : 1.f;
                 const V w = vneg(wo);
                 if (vdot(wo, n) < 0) eta = 1.f / eta;
@@ -426,8 +426,8 @@ PGD_INLINE Pushes shade_slot_dl(const DevScene &S, const PathSoA &P, int slot, f
             bool useB = false;
             if ((msk >> (16 + jb)) & 1u) {
                 const int mp = P.hitPrim[P.rcap + rs];
-                if ((FEAT & FEAT_INF) && S.lights[ln].type == PBRTGPU_LIGHT_INFINITE) useB = mp < 0;
-                else if (mp >= 0 && S.prims[mp].area_light == ln) {
+                if ((FEAT & FEAT_INF) && (*sa(S.lights, (uint32_t)(ln))).type == PBRTGPU_LIGHT_INFINITE) useB = mp < 0;
+                else if (mp >= 0 && (*sa(S.prims, (uint32_t)(mp))).area_light == ln) {
                     const Ray mr = ray_load(P, RAY_M, rs);
                     useB = vdot(isect_nn(S, mr, mp, P.hitT[P.rcap + rs], inst_rec(P, slot)), vneg(mr.d)) > 0.f;
                 }
@@ -449,8 +449,8 @@ PGD_INLINE Pushes shade_slot_dl(const DevScene &S, const PathSoA &P, int slot, f
             for (int q = 0; q < NQ; ++q) Lr[q] = make_float4(0.f, 0.f, 0.f, 0.f);
             if ((FEAT & FEAT_INF) && S.nInf > 0)
                 for (int l = 0; l < nLights; ++l)
-                    if (S.lights[l].type == PBRTGPU_LIGHT_INFINITE) {
-                        const Emit e = inf_Le(S.lights[l], ray.d);
+                    if ((*sa(S.lights, (uint32_t)(l))).type == PBRTGPU_LIGHT_INFINITE) {
+                        const Emit e = inf_Le((*sa(S.lights, (uint32_t)(l))), ray.d);
 #pragma unroll
                         for (int q = 0; q < NQ; ++q) {
                             const float4 v = emit4<FEAT>(S, e, q);
@@ -478,8 +478,8 @@ PGD_INLINE Pushes shade_slot_dl(const DevScene &S, const PathSoA &P, int slot, f
             k = 0;
             Isect is0;   // the hit alone decides the emission
             isect_fill(S, ray, prim, P.hitT[slot], is0, inst_rec(P, slot));
-            const int al = S.prims[is0.prim].area_light;
-            const int eo = (al >= 0 && vdot(is0.dg.nn, vneg(ray.d)) > 0.f) ? S.lights[al].spec : -1;   // AreaLight::L
+            const int al = (*sa(S.prims, (uint32_t)(is0.prim))).area_light;
+            const int eo = (al >= 0 && vdot(is0.dg.nn, vneg(ray.d)) > 0.f) ? (*sa(S.lights, (uint32_t)(al))).spec : -1;   // AreaLight::L
             float4 *Lv = dl_L<NB>(P, d, slot);
 #pragma unroll
             for (int q = 0; q < NQ; ++q) {

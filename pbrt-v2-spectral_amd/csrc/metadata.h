@@ -21,8 +21,8 @@ PGD_INLINE Pushes shade_slot_meta(const DevScene &S, const PathSoA &P, int slot,
     if (prim < 0) {
         if ((FEAT & FEAT_INF) && S.nInf > 0)
             for (int l = 0; l < S.nLights; ++l)
-                if (S.lights[l].type == PBRTGPU_LIGHT_INFINITE) {
-                    const Emit e = inf_Le(S.lights[l], ray.d);
+                if ((*sa(S.lights, (uint32_t)(l))).type == PBRTGPU_LIGHT_INFINITE) {
+                    const Emit e = inf_Le((*sa(S.lights, (uint32_t)(l))), ray.d);
 #pragma unroll
                     for (int q = 0; q < NQ; ++q) {
                         const float4 v = emit4<FEAT>(S, e, q);
@@ -37,7 +37,7 @@ PGD_INLINE Pushes shade_slot_meta(const DevScene &S, const PathSoA &P, int slot,
             const V d = vsub(is.dg.p, ray.o);
             v = sqrtf(d.x * d.x + d.y * d.y + d.z * d.z);
         } else
-            v = (float)S.primMeta[2 * prim + (S.metaStrategy == PBRTGPU_META_MATERIAL ? 1 : 0)];
+            v = (float)(*sa(S.primMeta, (uint32_t)(2 * prim + (S.metaStrategy == PBRTGPU_META_MATERIAL ? 1 : 0))));
 #pragma unroll
         for (int q = 0; q < NQ; ++q) L[q] = make_float4(v, v, v, v);
     }

@@ -181,7 +181,7 @@ __global__ __launch_bounds__(kTraceBlock) PGD_TRACE_ATTR void k_trace_pt(DevScen
     // the top levels of the BVH (wide nodes [0, S.nTop), breadth-first), once per block
     __shared__ float4 stop[kTopNodes > 0 ? 4 * kTopNodes : 1];
     if (kTopNodes > 0) {
-        for (int i = threadIdx.x; i < 4 * S.nTop; i += blockDim.x) stop[i] = S.wnodes[i];
+        for (int i = threadIdx.x; i < 4 * S.nTop; i += blockDim.x) stop[i] = (*sa(S.wnodes, (uint32_t)(i)));
         __syncthreads();
     }
     uint2 *gsp = spill + (size_t)(blockIdx.x * blockDim.x + threadIdx.x) * S.stackDepth;
@@ -222,8 +222,8 @@ __global__ __launch_bounds__(kTraceBlock) PGD_TRACE_ATTR void k_trace_pt(DevScen
                     bottom = 0;
                     if (ANY) st.cShadow++; else st.cRays++;
                     st.cNodes++;
-                    if (bbox_hit(S.nodes[0], S.nodes[1], ray, invDir, neg)) {
-                        ref = S.nodeRef[0];
+                    if (bbox_hit((*sa(S.nodes, (uint32_t)(0))), (*sa(S.nodes, (uint32_t)(1))), ray, invDir, neg)) {
+                        ref = (*sa(S.nodeRef, (uint32_t)(0)));
                         active = true;
                     } else if (ANY) P.occ[slot] = 0u;
                     else {
@@ -247,7 +247,7 @@ __global__ __launch_bounds__(kTraceBlock) PGD_TRACE_ATTR void k_trace_pt(DevScen
                     const float4 *w = stop + 4 * ref;
                     l0 = w[0]; l1 = w[1]; r0 = w[2]; r1 = w[3];
                 } else {
-                    const float4 *w = S.wnodes + 4 * (size_t)ref;
+                    const float4 *w = sa(S.wnodes, (uint32_t)(4 * (size_t)ref));
                     l0 = w[0]; l1 = w[1]; r0 = w[2]; r1 = w[3];
                 }
                 st.cNodes++;
@@ -396,8 +396,8 @@ __global__ __launch_bounds__(kTraceBlock) PGD_TRACE_INST_ATTR void k_trace_inst(
                     if (ANY) st.cShadow++; else st.cRays++;
                     st.cNodes++;
                     const int neg[3] = {(int)(negMask & 1u), (int)((negMask >> 1) & 1u), (int)(negMask >> 2)};
-                    if (bbox_hit(S.nodes[0], S.nodes[1], ray, invDir, neg)) {
-                        ref = S.nodeRef[0];
+                    if (bbox_hit((*sa(S.nodes, (uint32_t)(0))), (*sa(S.nodes, (uint32_t)(1))), ray, invDir, neg)) {
+                        ref = (*sa(S.nodeRef, (uint32_t)(0)));
                         active = true;
                     } else if (ANY) P.occ[slot] = 0u;
                     else {
@@ -418,7 +418,7 @@ __global__ __launch_bounds__(kTraceBlock) PGD_TRACE_INST_ATTR void k_trace_inst(
             const int neg[3] = {(int)(negMask & 1u), (int)((negMask >> 1) & 1u), (int)(negMask >> 2)};
             if (level == 1 || !inLeaf) {
                 if (ref != NONE && !(ref & WREF_LEAF)) {
-                    const float4 *w = S.wnodes + 4 * (size_t)ref;
+                    const float4 *w = sa(S.wnodes, (uint32_t)(4 * (size_t)ref));
                     const float4 l0 = w[0], l1 = w[1], r0 = w[2], r1 = w[3];
                     st.cNodes++;
                     float tl = 0.f, tr = 0.f;
@@ -467,12 +467,12 @@ __global__ __launch_bounds__(kTraceBlock) PGD_TRACE_INST_ATTR void k_trace_inst(
                 while (leafI < leafN && !occluded) {
                     const int pi = (int)(leafOff + leafI);
                     ++leafI;
-                    const pbrtgpu_prim pr = S.prims[pi];
+                    const pbrtgpu_prim pr = (*sa(S.prims, (uint32_t)(pi)));
                     if (pr.shape_type != PBRTGPU_SHAPE_INSTANCE) {
                         if (prim_test<ANY, false>(S, st, todo, pi, ray, &prim, &thit) && ANY) occluded = true;
                         continue;
                     }
-                    const pbrtgpu_instance &I = S.insts[pr.shape_index];
+                    const pbrtgpu_instance &I = (*sa(S.insts, (uint32_t)(pr.shape_index)));
                     float m[16];
                     inst_load(inst_rec(P, slot_of_ray(P, slot)), pr.shape_index, m, nullptr);   // the path's transform
                     Ray ir = xray(m, ray);
@@ -489,7 +489,7 @@ __global__ __launch_bounds__(kTraceBlock) PGD_TRACE_INST_ATTR void k_trace_inst(
                     st.cNodes++;
                     const uint32_t root = (uint32_t)I.root;
                     const int negI[3] = {(int)(negMask & 1u), (int)((negMask >> 1) & 1u), (int)(negMask >> 2)};
-                    if (!bbox_hit(S.nodes[2 * root], S.nodes[2 * root + 1], ray, invDir, negI)) {
+                    if (!bbox_hit((*sa(S.nodes, (uint32_t)(2 * root))), (*sa(S.nodes, (uint32_t)(2 * root + 1))), ray, invDir, negI)) {
                         Ray wr = ray_load(P, kind, slot);   // back to the world ray
                         wr.maxt = wmaxt;
                         setRay(wr);
@@ -497,7 +497,7 @@ __global__ __launch_bounds__(kTraceBlock) PGD_TRACE_INST_ATTR void k_trace_inst(
                     }
                     level = 1;
                     ibase = todo;
-                    ref = S.nodeRef[root];
+                    ref = (*sa(S.nodeRef, (uint32_t)(root)));
                     entered = true;
                     break;
                 }
@@ -577,14 +577,14 @@ __global__ void k_spec_guard(const DevScene S, float *__restrict__ Lout, uint32_
     float *o = Lout + (size_t)r * NB;
     float yy = 0.f;
     for (int b = 0; b < S.specBands; ++b) {
-        const int4 tb = S.specTab[b];
+        const int4 tb = (*sa(S.specTab, (uint32_t)(b)));
         if (tb.y <= tb.x) continue;
         const float yv = yy / S.yint;
         const bool bad = (yv < -1e-5f) || isinf(yv);
         for (int i = tb.x; i < tb.y; ++i) {
             float v = o[i];
             if (bad) o[i] = v = 0.f;
-            yy += S.bandY[i] * v;
+            yy += (*sa(S.bandY, (uint32_t)(i))) * v;
         }
     }
 }

@@ -22,9 +22,11 @@ namespace pgd {
         if (err) *err = (msg);         \
         return (code);                 \
     } while (0)
-#define SB_PUT(src, n, dst)                                         \
-    do {                                                            \
-        if (int e_ = put((src), (size_t)(n), (dst))) return e_;     \
+// every array is < 4 GiB: the device addresses them through 32-bit byte offsets (device.h sa)
+#define SB_PUT(src, n, dst)                                                                          \
+    do {                                                                                             \
+        if ((size_t)(n) * sizeof(*(src)) >= ((size_t)1 << 32)) SB_FAIL(PBRTGPU_E_UNSUPPORTED, "scene array >= 4 GiB"); \
+        if (int e_ = put((src), (size_t)(n), (dst))) return e_;                                      \
     } while (0)
 
 // Child-in-parent copy of the flattened BVH (LinearBVHNode, bvh.cpp:105-115) for

@@ -140,18 +140,7 @@ struct ItemSrc {
     uint32_t base;
 };
 
-// Slot arrays are addressed through a 32-bit element index from their base: the base is a
-// kernel argument (wave-uniform, in SGPRs) and the byte offset a 32-bit value, so a load or store
-// takes one VGPR of address (global saddr mode) instead of a 64-bit per-lane pointer -- fewer
-// registers live across k_shade and no 64-bit address arithmetic.  Every array the path step
-// addresses this way is < 4 GiB (pbrtgpu.hip ensure_slots checks it).
-template <class T> PGD_INLINE T *sa(T *base, uint32_t i) {
-    return reinterpret_cast<T *>(reinterpret_cast<char *>(base) + (uint32_t)(i * (uint32_t)sizeof(T)));
-}
-template <class T> PGD_INLINE const T *sa(const T *base, uint32_t i) {
-    return reinterpret_cast<const T *>(reinterpret_cast<const char *>(base) + (uint32_t)(i * (uint32_t)sizeof(T)));
-}
-// a column of a slot array: element i (+ k) of base
+// a column of a slot array (32-bit addressing, device.h sa): element i (+ k) of base
 template <class T> struct Col {
     T *base;
     uint32_t i;
@@ -189,6 +178,13 @@ PGD_INLINE void mt_store(const PathSoA &P, int slot, const MT &r) {
 }
 
 template <int NB> struct Bands { static constexpr int NQ = (NB + 3) / 4; };
+// unrolling of the band loops that stream the light-sample and MIS terms A, B to memory: by 4
+// quads (U=3 keeps every variant within the kernel budget; fully unrolled, all quads' loads were hoisted, and the FEAT 0 kernel reloaded a spilled
+// BSDF parameter from scratch in every band: 213 scratch loads, 11 by 3 or 4 quads); the beta loop
+// stays unrolled, its quads are kept for the roulette
+#ifndef PGD_UNROLL_BANDS
+#define PGD_UNROLL_BANDS _Pragma("unroll 3")
+#endif
 // path-state spectra: beta in three buffers, so that a pass can read beta_b (finishing vertex
 // b), beta_{b+1} (shading it) and write beta_{b+2}; A, B in two
 // Path integrator: beta of a vertex is written by the pass that samples its direction (buffer
@@ -447,16 +443,16 @@ __device__ __attribute__((noinline)) void kd_lookup_global(const float4 *__restr
 template <int NB>
 PGD_INLINE void measured_lookup(const DevScene &S, const FTerm &t, float4 *mb, size_t c) {
 #ifdef PGD_EXP_MEAS_CHEAP   // timing experiment only: the lookup's cost share (wrong radiance)
-    for (int q = 0; q < Bands<NB>::NQ; ++q) mb[q * c] = ld4(S.spectra + S.kd[t.R].spec + 4 * q);
+    for (int q = 0; q < Bands<NB>::NQ; ++q) mb[q * c] = ld4(sa(S.spectra, (uint32_t)((*sa(S.kd, (uint32_t)(t.R))).spec + 4 * q)));
     return;
 #endif
     if (S.kdInLds) kd_lookup_lds<NB>((LdsF4 *)pgd_kd_lds + 2 * t.R, S.spectra, t.s0, t.s1, t.s2, mb, c);
-    else kd_lookup_global<NB>(S.kdPack + 2 * t.R, S.spectra, t.s0, t.s1, t.s2, mb, c);
+    else kd_lookup_global<NB>(sa(S.kdPack, (uint32_t)(2 * t.R)), S.spectra, t.s0, t.s1, t.s2, mb, c);
 }
 // k_shade prologue of the FEAT_MEAS variants: the block's copy of the kd-trees in LDS
 PGD_INLINE void kd_lds_fill(const DevScene &S) {
     if (!S.kdInLds) return;
-    for (int i = threadIdx.x; i < 2 * S.nKd; i += blockDim.x) pgd_kd_lds[i] = S.kdPack[i];
+    for (int i = threadIdx.x; i < 2 * S.nKd; i += blockDim.x) pgd_kd_lds[i] = (*sa(S.kdPack, (uint32_t)(i)));
     __syncthreads();
 }
 // materialise a measured term of F into the slot's M bands (T_MEAS -> T_BUF)
@@ -467,7 +463,7 @@ PGD_INLINE void term_prepare(const DevScene &S, FTerm &t, float4 *mb, size_t c) 
         t.kind = T_BUF;
     } else if (t.kind == T_MERL) {
         // Spectrum::FromRGB(&brdf[3 * index]) (reflection.cpp:299), reflectance
-        const float *rgb = S.merl + 3 * ((size_t)t.R + (size_t)t.R2);
+        const float *rgb = sa(S.merl, (uint32_t)(3 * ((size_t)t.R + (size_t)t.R2)));
         const float v[3] = {rgb[0], rgb[1], rgb[2]};
         const RGBPick pk = rgb_pick(v);
 #pragma unroll
@@ -491,7 +487,7 @@ template <int FEAT>
 PGD_INLINE bool mis_may_reach(const DevScene &S, const pbrtgpu_light &Lt, const Ray &r) {
     if ((FEAT & FEAT_INF) && Lt.type == PBRTGPU_LIGHT_INFINITE) return true;
     if (Lt.n_shapes > 8) return true;
-    const pbrtgpu_light_shape *shs = S.lightShapes + Lt.shape_offset;
+    const pbrtgpu_light_shape *shs = sa(S.lightShapes, (uint32_t)(Lt.shape_offset));
     for (int i = 0; i < Lt.n_shapes; ++i) {
         const int ty = shs[i].shape_type;
         if (ty == PBRTGPU_SHAPE_TRIANGLE) return true;
@@ -547,7 +543,7 @@ PGD_INLINE void path_start(const DevScene &S, const PathSoA &P, const ItemSrc &s
     // time, once per path: all of the path's rays carry this time
     for (int i = 0; i < P.nInst; ++i) {
         float m[16], minv[16];
-        inst_interp(S.insts[i], r.time, m, minv);
+        inst_interp((*sa(S.insts, (uint32_t)(i))), r.time, m, minv);
         float4 *o = P.instM + ((size_t)slot * P.nInst + i) * 8;
         for (int k = 0; k < 4; ++k) {
             o[k] = make_float4(m[4 * k], m[4 * k + 1], m[4 * k + 2], m[4 * k + 3]);
@@ -578,7 +574,7 @@ PGD_INLINE bool spectral_output(const DevScene &S, const float4 (&L)[Bands<NB>::
     const int bi = S.specItems;
     const int row = bi > 1 ? item / bi : item;
     const int band = S.specMode == 1 ? item - row * bi : (int)(smp % (uint32_t)S.specBands);
-    const int4 tb = S.specTab[band];
+    const int4 tb = (*sa(S.specTab, (uint32_t)(band)));
     bool nan = false;
     float a = 0.f, b = 0.f;
 #pragma unroll
@@ -593,7 +589,7 @@ PGD_INLINE bool spectral_output(const DevScene &S, const float4 (&L)[Bands<NB>::
     float *o = Lout + (size_t)row * NB;
     const bool tail = S.specMode == 2 || band == S.specBands - 1;
     // the bands' index ranges are contiguous from 0 up to the last band's end
-    const int tailLo = S.specMode == 2 ? 0 : S.specTab[S.specBands - 1].y;
+    const int tailLo = S.specMode == 2 ? 0 : (*sa(S.specTab, (uint32_t)(S.specBands - 1))).y;
     for (int i = tb.x; i < tb.y; ++i) o[i] = val;
     if (tail)
         for (int i = tailLo; i < NB; ++i)
@@ -613,7 +609,7 @@ PGD_INLINE bool path_output(const DevScene &S, const float4 (&L)[Bands<NB>::NQ],
     for (int i = 0; i < NB; ++i) {
         float v = 1.f * ((1.f * cmp(L[i / 4], i % 4)) + 0.f);
         nan = nan || isnan(v);
-        yy += S.bandY[i] * v;
+        yy += (*sa(S.bandY, (uint32_t)(i))) * v;
     }
     bool bad = nan;
     if (!bad) {
@@ -673,7 +669,7 @@ PGD_INLINE void estimate_direct(const DevScene &S, const PathSoA &P, int slot, i
     const float *sp = S.spectra;
     float4 *mb = P.M + slot, *kb = P.K + slot;
     PGD_T0(LIGHT);
-    const pbrtgpu_light &Lt = S.lights[lightNum];
+    const pbrtgpu_light &Lt = (*sa(S.lights, (uint32_t)(lightNum)));
     const int flags = BSDF_ALL & ~BSDF_SPECULAR;
     fl |= PF_PEND | ((uint32_t)lightNum << PF_LIGHT_SHIFT);
     // ---- light sample -> A (added if the shadow ray is unoccluded)
@@ -710,7 +706,7 @@ PGD_INLINE void estimate_direct(const DevScene &S, const PathSoA &P, int slot, i
         PGD_T0(LSTORE);
         // A_i = (f_i * Li_i) * sc ; written while testing f for black (A unused if black)
         bool black = true;
-#pragma unroll
+PGD_UNROLL_BANDS
         for (int q = 0; q < NQ; ++q) {
             float4 f = fval4<FEAT>(sp, F, q, mb, kb, c), e = emit4<FEAT>(S, em, q), a;
 #pragma unroll
@@ -778,7 +774,7 @@ PGD_INLINE void estimate_direct(const DevScene &S, const PathSoA &P, int slot, i
             if (withB) {
                 const float ad = fabsf(vdot(wi, n));
                 bool black = true;
-#pragma unroll
+PGD_UNROLL_BANDS
                 for (int q = 0; q < NQ; ++q) {
                     float4 f = fval4<FEAT>(sp, F, q, mb, kb, c), e = emit4<FEAT>(S, eb, q), b;
 #pragma unroll
@@ -822,9 +818,9 @@ PGD_INLINE Pushes shade_vertex(const DevScene &S, const PathSoA &P, int slot, in
     la->emit = false;
     la->zero = false;
     if (vb == 0 || (fl & PF_SPEC)) {
-        int al = S.prims[is.prim].area_light;
+        int al = (*sa(S.prims, (uint32_t)(is.prim))).area_light;
         la->emit = true;
-        la->emitOff = (al >= 0 && vdot(is.dg.nn, vneg(ray.d)) > 0.f) ? S.lights[al].spec : -1;
+        la->emitOff = (al >= 0 && vdot(is.dg.nn, vneg(ray.d)) > 0.f) ? (*sa(S.lights, (uint32_t)(al))).spec : -1;
     }
     PGD_T0(BSDF);
     const uint32_t hp = *sa(P.hp, us), s = *sa(P.smp, us), spp = (uint32_t)S.spp;
@@ -832,7 +828,7 @@ PGD_INLINE Pushes shade_vertex(const DevScene &S, const PathSoA &P, int slot, in
     // to textured materials
     float diff[4] = {0.f, 0.f, 0.f, 0.f};
     if ((FEAT & FEAT_TEX) && vb == 0) {
-        const pbrtgpu_material &mt = S.mats[S.prims[is.prim].material];
+        const pbrtgpu_material &mt = (*sa(S.mats, (uint32_t)((*sa(S.prims, (uint32_t)(is.prim))).material)));
         if (mt.bump_tex >= 0 || mt.tex[0] >= 0 || mt.tex[1] >= 0 || mt.tex[2] >= 0 || mt.tex[3] >= 0) {
             const uint32_t pxy = P.pix[slot];
             float u[2], lens[2];
@@ -928,7 +924,7 @@ PGD_INLINE Pushes shade_vertex(const DevScene &S, const PathSoA &P, int slot, in
             if (vb > 3) {
                 float yy = 0.f;
 #pragma unroll
-                for (int i = 0; i < NB; ++i) yy += S.bandY[i] * cmp(nb4[i / 4], i % 4);
+                for (int i = 0; i < NB; ++i) yy += (*sa(S.bandY, (uint32_t)(i))) * cmp(nb4[i / 4], i % 4);
                 float cp = pmin(.5f, yy / S.yint);
                 if (mt_float(rng) > cp) cont = false;
                 else {
@@ -1001,8 +997,8 @@ PGD_INLINE Pushes shade_slot(const DevScene &S, const PathSoA &P, int slot, floa
             const int ln = (int)(fl >> PF_LIGHT_SHIFT);
             const int mi = P.nInst ? slot : (slot & ~63) + wave_rank(wm.b, slot);   // the MIS ray's record
             int mp = *sa(P.hitPrim, rc + (uint32_t)mi);
-            if ((FEAT & FEAT_INF) && S.lights[ln].type == PBRTGPU_LIGHT_INFINITE) useB = mp < 0;   // Li = light->Le(ray)
-            else if (mp >= 0 && S.prims[mp].area_light == ln) {
+            if ((FEAT & FEAT_INF) && (*sa(S.lights, (uint32_t)(ln))).type == PBRTGPU_LIGHT_INFINITE) useB = mp < 0;   // Li = light->Le(ray)
+            else if (mp >= 0 && (*sa(S.prims, (uint32_t)(mp))).area_light == ln) {
                 Ray mr = ray_load(P, RAY_M, mi);
                 useB = vdot(isect_nn(S, mr, mp, *sa(P.hitT, rc + (uint32_t)mi), inst_rec(P, slot)), vneg(mr.d)) > 0.f;   // DiffuseAreaLight::L
             }
@@ -1083,8 +1079,8 @@ PGD_INLINE Pushes shade_slot(const DevScene &S, const PathSoA &P, int slot, floa
         if ((FEAT & FEAT_INF) && S.nInf > 0) {
             const Ray ray = ray_load(P, RAY_C, slot);
             for (int l = 0; l < S.nLights; ++l)
-                if (S.lights[l].type == PBRTGPU_LIGHT_INFINITE) {
-                    const Emit e = inf_Le(S.lights[l], ray.d);
+                if ((*sa(S.lights, (uint32_t)(l))).type == PBRTGPU_LIGHT_INFINITE) {
+                    const Emit e = inf_Le((*sa(S.lights, (uint32_t)(l))), ray.d);
 #pragma unroll
                     for (int q = 0; q < NQ; ++q) {
                         float4 v = emit4<FEAT>(S, e, q);
@@ -1099,7 +1095,7 @@ PGD_INLINE Pushes shade_slot(const DevScene &S, const PathSoA &P, int slot, floa
         for (int l = 0; l < S.nLights; ++l) {
             Emit e;
             e.mode = EM_BLACK;
-            if ((FEAT & FEAT_INF) && S.lights[l].type == PBRTGPU_LIGHT_INFINITE) e = inf_Le(S.lights[l], d);
+            if ((FEAT & FEAT_INF) && (*sa(S.lights, (uint32_t)(l))).type == PBRTGPU_LIGHT_INFINITE) e = inf_Le((*sa(S.lights, (uint32_t)(l))), d);
 #pragma unroll
             for (int q = 0; q < NQ; ++q) {
                 float4 bt = beta_q(beta_rd<NB>(P, vb, 1, slot, wm.b1), q, c), v = emit4<FEAT>(S, e, q);
