@@ -105,6 +105,8 @@ def _golden_scene(pg, cfg, name="killeroo"):
     pack = {"anim": "anim-killeroos-moving.pack", "bunny": "bunny.pack", "metal": "metal.pack",
             "coverage": "coverage.pack"}.get(name.split("_")[0],
                                                                                               "killeroo-simple.pack")
+    if "_b30_" in name:
+        pack = pack.replace(".pack", "-b30.pack")
     return pg.Scene.load(os.path.join(PACKS, pack), xres=w, yres=h, spp=spp, maxdepth=md, seed=seed)
 
 
@@ -112,7 +114,8 @@ def _golden_scene(pg, cfg, name="killeroo"):
                                   "bunny_paths_64x36s4", "metal_paths_48x48s4",
                                   "coverage_paths_64x48s8", "killeroo_keys_c2_700x700s256",
                                   "bunny_keys_c3_1920x1080s1024", "metal_keys_c4_400x400s4096",
-                                  "anim_keys_c5_600x600s512"])
+                                  "anim_keys_c5_600x600s512", "killeroo_b30_paths_48x40s4",
+                                  "coverage_b30_paths_48x36s4"])
 def test_paths_vs_reference_golden(pg, name):
     """GPU against the reference harness's own per-path radiance (fixed seeds); the *_keys_*
     fixtures are the configs at their real resolution and sample count."""
@@ -133,7 +136,8 @@ def test_paths_vs_reference_golden(pg, name):
 
 
 @pytest.mark.parametrize("name", ["killeroo_film_96x72s16", "anim_film_40x40s8", "bunny_film_48x27s8",
-                                  "metal_film_40x40s8", "coverage_film_64x48s8"])
+                                  "metal_film_40x40s8", "coverage_film_64x48s8", "killeroo_b30_film_40x32s8",
+                                  "coverage_b30_film_40x30s4"])
 def test_film_vs_reference_golden(pg, name):
     """Whole-film render against the reference's film (raw sums, incl. neighbour-pixel
     samples): image L-inf relative error < 1e-4 (BASELINE.json north star)."""
@@ -145,7 +149,7 @@ def test_film_vs_reference_golden(pg, name):
         st = d.render()
         film = d.film()
     ref = g["film"]
-    if name.startswith("killeroo"):
+    if name.startswith("killeroo_film"):
         assert st[pg.STAT_SPILLS] > 0
     assert np.abs(film - ref).max() / np.abs(ref).max() < 1e-4
     # a fraction 1 - r of paths differs from glibc-float transcendentals in the last ulp

@@ -62,11 +62,12 @@ CASES = [
     ("bunny.pack", dict(xres=24, yres=16, spp=4, maxdepth=5)),
     ("metal.pack", dict(xres=24, yres=24, spp=4, maxdepth=5)),
     ("coverage.pack", dict(xres=40, yres=30, spp=2, integrator="metadata", strategy="depth")),
+    ("coverage-b30.pack", dict(xres=40, yres=30, spp=4, maxdepth=6)),
 ]
 
 
 @pytest.mark.parametrize("pack,a", CASES, ids=["dl_all_md6", "dl_one", "dl_killeroo", "path_coverage", "path_anim",
-                                               "path_bunny", "path_metal60", "metadata"])
+                                               "path_bunny", "path_metal60", "metadata", "path_coverage_b30"])
 def test_replay_matches_oracle(pg, tmp_path, pack, a):
     exe = _build("shade_host")
     scene = pg.Scene.load(os.path.join(PACKS, pack), **a)

@@ -20,6 +20,9 @@ def _scene(pg, cfg, name="killeroo"):
     pack = {"anim": "anim-killeroos-moving.pack", "bunny": "bunny.pack", "metal": "metal.pack",
             "coverage": "coverage.pack"}.get(name.split("_")[0],
                                                                                               "killeroo-simple.pack")
+    # *_b30_*: the upstream 30-band, 400-700 nm build (b30 harness, spectrum.h.original:36-38)
+    if "_b30_" in name:
+        pack = pack.replace(".pack", "-b30.pack")
     return pg.Scene.load(os.path.join(PACKS, pack), xres=w, yres=h, spp=spp, maxdepth=md, seed=seed)
 
 
@@ -36,7 +39,7 @@ def exact_rate(name):
 
 
 PATHS = ["killeroo_paths_64x64s4", "killeroo_paths_48x48s8_seed7_md7", "anim_paths_48x48s4", "bunny_paths_64x36s4",
-         "metal_paths_48x48s4", "coverage_paths_64x48s8"]
+         "metal_paths_48x48s4", "coverage_paths_64x48s8", "killeroo_b30_paths_48x40s4", "coverage_b30_paths_48x36s4"]
 # the configs at their real size and sample count (BASELINE.json configs 2-5; harness --keys):
 # every sample of a few pixels plus random keys of the whole sample extent
 KEYS = ["killeroo_keys_c2_700x700s256", "bunny_keys_c3_1920x1080s1024", "metal_keys_c4_400x400s4096",
@@ -78,12 +81,13 @@ def test_paths_double_rounded_definition(pg, name):
 
 
 @pytest.mark.parametrize("name", ["killeroo_film_96x72s16", "anim_film_40x40s8", "bunny_film_48x27s8",
-                                  "metal_film_40x40s8", "coverage_film_64x48s8"])
+                                  "metal_film_40x40s8", "coverage_film_64x48s8", "killeroo_b30_film_40x32s8",
+                                  "coverage_b30_film_40x30s4"])
 def test_film_bit_exact_vs_reference(pg, ora_libm, name):
     g = np.load(os.path.join(GOLDEN, name + ".npz"))
     scene = _scene(pg, g["config"], name)
     film, st = ora_libm.render(scene, threads=8)
-    if name.startswith("killeroo"):
+    if name.startswith("killeroo_film"):
         assert st[2] > 0, "fixture should contain samples landing on neighbour pixels"
     assert np.array_equal(film.view(np.int32), g["film"].view(np.int32))
 
@@ -97,7 +101,7 @@ def test_mt19937_known_answers(pg):
     assert int(o.mt_first(5489, 10000)[-1]) == 4123659995
 
 
-@pytest.mark.parametrize("bands", [32, 60])
+@pytest.mark.parametrize("bands", [32, 60, 30])
 def test_host_fromrgb_bit_exact(pg, bands):
     g = np.load(os.path.join(GOLDEN, "fromrgb_%d.npz" % bands))
     for rgb, refl, illum in zip(g["rgb"], g["refl"], g["illum"]):

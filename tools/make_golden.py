@@ -46,7 +46,9 @@ Fixtures (numpy .npz, inputs + expected outputs only):
   killeroo_dat_40x32s4.npz        the raw film of the restatement film AND the .dat the
                                   reference's own SpectralImageNoCameraFilm wrote for the same
                                   samples (--refdat): pins AddSample and the WriteImage payload
-Usage: python tools/make_golden.py [--only keys|dat|merl|dl|meta|spec|rgb]   (after `make -C oracle ref` and `make -C oracle ref60`)
+  *_b30_*, fromrgb_30.npz         the upstream 30-band build (b30 harness, 400-700 nm)
+Usage: python tools/make_golden.py [--only keys|dat|merl|dl|meta|spec|rgb|b30]
+       (after `make -C oracle ref`, `ref60`, `ref30` and `refrgb`)
 """
 import os
 import subprocess
@@ -59,12 +61,13 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HARNESS = os.path.join(ROOT, "oracle", "_ref", "b32", "pbrt_ref_harness")
 HARNESS60 = os.path.join(ROOT, "oracle", "_ref", "b60", "pbrt_ref_harness")   # make -C oracle ref60
 HARNESSRGB = os.path.join(ROOT, "oracle", "_ref", "brgb", "pbrt_ref_harness")  # make -C oracle refrgb
+HARNESS30 = os.path.join(ROOT, "oracle", "_ref", "b30", "pbrt_ref_harness")    # make -C oracle ref30
 SCENES = "/root/reference/scenes"
 OUT = os.path.join(ROOT, "tests", "golden")
 
 
 def run(args, bands=32):
-    exe = HARNESS60 if bands == 60 else HARNESSRGB if bands == 3 else HARNESS
+    exe = {60: HARNESS60, 30: HARNESS30, 3: HARNESSRGB}.get(bands, HARNESS)
     subprocess.run([exe] + args, check=True, cwd=SCENES)
 
 
@@ -121,6 +124,29 @@ def rgb_fixtures(tmp):
     paths_fixture("killeroo_rgb_paths_48x40s4", (48, 40), 4, 0, 5, 1, tmp, bands=3)
     film_fixture("killeroo_rgb_film_40x32s8", (40, 32), 8, 0, 5, tmp, bands=3)
     keys_fixture("killeroo_rgb_keys_c1_400x400s64", "killeroo-simple.pbrt", 400, 400, 64, 3, 1, tmp)
+
+
+def spectra_fixture(bands, tmp):
+    """SampledSpectrum::FromRGB (reflectance and illuminant) of the harness's RGB triples."""
+    fn = os.path.join(tmp, "spec%d.bin" % bands)
+    run(["-", "--spectra", fn], bands)
+    raw = np.fromfile(fn, dtype=np.int32)
+    n = raw[0]
+    rec = raw[1:].reshape(n, 3 + 2 * bands).view(np.float32)
+    np.savez_compressed(os.path.join(OUT, "fromrgb_%d.npz" % bands), rgb=rec[:, :3].copy(), refl=rec[:, 3:3 + bands].copy(),
+                        illum=rec[:, 3 + bands:].copy())
+
+
+def b30_fixtures(tmp):
+    """The upstream 30-band build (400-700 nm, spectrum.h.original:36-38; BASELINE's literal
+    "30 bands"): killeroo (C2's scene) and the coverage scene (SPD metals, textures, every light
+    type), per-path radiance and film, and FromRGB."""
+    paths_fixture("killeroo_b30_paths_48x40s4", (48, 40), 4, 0, 5, 2, tmp, bands=30)
+    film_fixture("killeroo_b30_film_40x32s8", (40, 32), 8, 0, 5, tmp, bands=30)
+    cov = os.path.join(ROOT, "tests", "scenes", "coverage.pbrt")
+    paths_fixture("coverage_b30_paths_48x36s4", (48, 36), 4, 0, 6, 1, tmp, scene=cov, bands=30)
+    film_fixture("coverage_b30_film_40x30s4", (40, 30), 4, 0, 6, tmp, scene=cov, bands=30)
+    spectra_fixture(30, tmp)
 
 
 def keys_fixture(name, scene, W, H, spp, bands, kseed, tmp):
@@ -250,6 +276,8 @@ def main():
                 spec_fixtures(tmp)
             elif only == "rgb":
                 rgb_fixtures(tmp)
+            elif only == "b30":
+                b30_fixtures(tmp)
         return
     with tempfile.TemporaryDirectory() as tmp:
         paths_fixture("killeroo_paths_64x64s4", (64, 64), 4, 0, 5, 5, tmp)
@@ -282,6 +310,8 @@ def main():
         spec_fixtures(tmp)
         if os.path.exists(HARNESSRGB):
             rgb_fixtures(tmp)
+        if os.path.exists(HARNESS30):
+            b30_fixtures(tmp)
         fn = os.path.join(tmp, "mt.bin")
         run(["-", "--kat-mt", fn])
         raw = np.fromfile(fn, dtype=np.uint32).reshape(6, 65)
