@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define PBRTGPU_ABI_VERSION 8
+#define PBRTGPU_ABI_VERSION 9
 #define PBRTGPU_MAX_BANDS 64
 
 #define PBRTGPU_E_INVALID   (-1)
@@ -205,7 +205,9 @@ typedef struct pbrtgpu_camera {
 /* RealisticDiffractionCamera (cameras/realisticDiffraction.cpp:32-94 parameters, 99-193
  * lens file, 347-468 Snell's law and element intersection, 478-1164 GenerateRay; ray
  * differentials by Camera::GenerateRayDifferential, camera.cpp:52-81): film rays traced from
- * the sensor through the lens elements, last element first.  Diffraction, pinhole arrays /
+ * the sensor through the lens elements, last element first; with "diffractionEnabled" each
+ * element's exit direction is perturbed by a bivariate Gaussian (realisticDiffraction.cpp:
+ * 1057-1150) drawn from the camera sample's own stream.  Pinhole arrays /
  * microlenses and the eye IOR curves are not part of this build (pbrthost refuses them). */
 typedef struct pbrtgpu_lens {
     int32_t n_elements;           /* lens-file elements, scene side first */
@@ -217,6 +219,8 @@ typedef struct pbrtgpu_lens {
     float film_center[2];         /* "film_center_x", "film_center_y" */
     float pinhole_exit[3];        /* "pinhole_exit_x/y/z": rays aim there unless one is -1 */
     float focal_length, fstop;    /* the lens file's first value; focal_length / "aperture_diameter" */
+    int32_t diffraction;          /* "diffractionEnabled" (default true) */
+    int32_t reserved;
     const float *elements;        /* [n_elements][4] radius, separation, n, aperture (an aperture stop,
                                    * radius 0, carries "aperture_diameter") */
 } pbrtgpu_lens;

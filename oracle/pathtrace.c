@@ -52,6 +52,11 @@
 #define ATAN2F atan2f
 #define TANF tanf
 #define ATANF atanf
+#define DSIN sin   /* double: the lens camera's diffraction (realisticDiffraction.cpp:1057-1150) */
+#define DCOS cos
+#define DACOS acos
+#define DATAN atan
+#define DLOG log
 #else
 /* the parity definition shared with the GPU: include/pbrt_fmath.h */
 static inline float SINF(float x) { return (float)pbrt_fm_sin((double)x); }
@@ -62,6 +67,11 @@ static inline float ACOSF(float x) { return (float)pbrt_fm_acos((double)x); }
 static inline float ATAN2F(float y, float x) { return (float)pbrt_fm_atan2((double)y, (double)x); }
 static inline float TANF(float x) { return (float)pbrt_fm_tan((double)x); }
 static inline float ATANF(float x) { return (float)pbrt_fm_atan((double)x); }
+#define DSIN pbrt_fm_sin
+#define DCOS pbrt_fm_cos
+#define DACOS pbrt_fm_acos
+#define DATAN pbrt_fm_atan
+#define DLOG pbrt_fm_log
 #endif
 
 /* ------------------------------------------------------------------ vector math */
@@ -2016,9 +2026,80 @@ static Ray camera_ray(const Ctx *c, float imageX, float imageY, float lensU, flo
     return o;
 }
 
-/* ---- RealisticDiffractionCamera (cameras/realisticDiffraction.cpp), diffraction off.
+/* ---- RealisticDiffractionCamera (cameras/realisticDiffraction.cpp).
  * PARITY UNPINNED: the camera's TU includes GSL headers this image lacks, so the reference
  * harness cannot run it; this restatement and the GPU's are checked against each other. */
+
+/* Diffraction's Gaussian draws (realisticDiffraction.cpp:1091, gsl_ran_bivariate_gaussian over
+ * one GSL generator shared by the render threads): here each camera sample has its own
+ * counter-based stream, uniform number n = top 32 bits of
+ * splitmix64(key + n * 0x9E3779B97F4A7C15) / 2^32, n = 1, 2, ... */
+typedef struct { uint64_t key; uint32_t n; } DiffStream;
+static double diff_next(DiffStream *st) {
+    st->n += 1;
+    uint64_t z = st->key + (uint64_t)st->n * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z = z ^ (z >> 31);
+    return (double)(uint32_t)(z >> 32) / 4294967296.0;
+}
+/* GSL randist/bigauss.c, rho = 0: polar Box-Muller, at most 64 tries (then no noise) */
+static void diff_bigauss(DiffStream *st, double sigma_x, double sigma_y, double *x, double *y) {
+    int tries;
+    *x = 0.0;
+    *y = 0.0;
+    for (tries = 0; tries < 64; ++tries) {
+        double u = -1 + 2 * diff_next(st);
+        double v = -1 + 2 * diff_next(st);
+        double r2 = u * u + v * v;
+        if (r2 > 1.0 || r2 == 0) continue;
+        double scale = sqrt(-2.0 * DLOG(r2) / r2);
+        *x = sigma_x * u * scale;
+        *y = sigma_y * (0.0 * u + 1.0 * v) * scale;   /* rho u + sqrt(1 - rho^2) v */
+        return;
+    }
+}
+/* realisticDiffraction.cpp:1057-1150 after an element: p its intersection point, ap its aperture,
+ * wl the ray's wavelength.  C++'s float overloads (sqrt of a float expression) are sqrtf here.
+ * Returns 0 when the new direction has a NaN (the ray's weight is 0). */
+static int lens_diffraction(DiffStream *st, V p, float ap, float wl, V *dir_io) {
+    double radius = sqrtf(p.x * p.x + p.y * p.y);
+    V ea = v3(p.x, p.y, 0.f), eb = v3(-p.y, p.x, 0.f);
+    double a = ap / 2 - radius;
+    double b = sqrt(ap / 2 * ap / 2 - radius * radius);
+    double pi = 3.14159265359;
+    double lambda = wl * 1e-9;
+    double sigma_x = DATAN(1 / (sqrt(2.0) * a * .001 * 2 * pi / lambda));
+    double sigma_y = DATAN(1 / (sqrt(2.0) * b * .001 * 2 * pi / lambda));
+    double gx, gy;
+    diff_bigauss(st, sigma_x, sigma_y, &gx, &gy);
+    ea = vnorm(ea);
+    eb = vnorm(eb);
+    float noiseA = (float)gx, noiseB = (float)gy;
+    V d = *dir_io;
+    double projA = (d.x * ea.x + d.y * ea.y) / sqrtf(ea.x * ea.x + ea.y * ea.y);
+    double projB = (d.x * eb.x + d.y * eb.y) / sqrtf(eb.x * eb.x + eb.y * eb.y);
+    double projC = d.z;
+    double rA = sqrt(projA * projA + projC * projC);
+    double rB = sqrt(projB * projB + projC * projC);
+    double thetaA = DACOS(projA / rA) + noiseA;
+    double thetaB = DACOS(projB / rB) + noiseB;   /* recomputed below without the noise */
+    double newA = DCOS(thetaA) * rA;
+    d.z = (float)(DSIN(thetaA) * rA);
+    projC = d.z;
+    rB = sqrt(projB * projB + projC * projC);
+    thetaB = DACOS(projB / rB);
+    double newB = DCOS(thetaB) * rB;
+    d.z = (float)(DSIN(thetaB) * rB);
+    d.x = (float)(ea.x * newA + eb.x * newB);
+    d.y = (float)(ea.y * newA + eb.y * newB);
+    if (isnan(d.x) || isnan(d.y) || isnan(d.z)) {
+        *dir_io = v3(0.f, 0.f, 0.f);
+        return 0;
+    }
+    *dir_io = vnorm(d);
+    return 1;
+}
 /* IntersectLensEl (realisticDiffraction.cpp:412-468) */
 static int lens_el_hit(const Ray *r, float radius, V dist, float *tHit, V *nrm) {
     float m[16] = {1.f, 0.f, 0.f, dist.x, 0.f, 1.f, 0.f, dist.y, 0.f, 0.f, 1.f, dist.z, 0.f, 0.f, 0.f, 1.f};
@@ -2055,7 +2136,8 @@ static void lens_snell(float n1, float n2, float lensRadius, V nrm, Ray *ray, fl
 }
 /* GenerateRay (realisticDiffraction.cpp:478-1164) without diffraction / pinhole arrays /
  * microlenses: returns the weight (0: blocked) */
-static float lens_ray(const Ctx *c, float imageX, float imageY, float lensU, float lensV, float timeU, float wl, Ray *out) {
+static float lens_ray(const Ctx *c, float imageX, float imageY, float lensU, float lensV, float timeU, float wl,
+                      DiffStream *st, Ray *out) {
     const pbrtgpu_camera *cam = &c->s->camera;
     const pbrtgpu_lens *Ls = &c->s->lens;
     const float xr2 = (float)cam->xres / 2.f, yr2 = (float)cam->yres / 2.f;
@@ -2102,6 +2184,7 @@ static float lens_ray(const Ctx *c, float imageX, float imageY, float lensU, flo
             float dx = ai.x - Ls->aperture_offset[0], dy = ai.y - Ls->aperture_offset[1];
             if ((double)(dx * dx + dy * dy) > (double)(ap * ap) * .25) return 0.f;
             sp = ai;
+            if (Ls->diffraction && !lens_diffraction(st, ai, ap, wl, &r.d)) return 0.f;
         } else {
             float tHit = 0.f;
             V nrm = v3(0.f, 0.f, 1.f);
@@ -2115,6 +2198,7 @@ static float lens_ray(const Ctx *c, float imageX, float imageY, float lensU, flo
             }
             lens_snell(n1, n2, rad, nrm, &r, wl, Ls->chromatic);
             sp = ip;
+            if (Ls->diffraction && !lens_diffraction(st, ip, ap, wl, &r.d)) return 0.f;
         }
     }
     r.o = sp;
@@ -2126,13 +2210,16 @@ static float lens_ray(const Ctx *c, float imageX, float imageY, float lensU, flo
 }
 /* Camera::GenerateRayDifferential (camera.cpp:52-81) + ScaleDifferentials(1 / sqrtf(spp)) */
 static float lens_ray_diff(const Ctx *c, float imageX, float imageY, float lensU, float lensV, float timeU, float wl,
-                           Ray *ray, RayDiff *rd) {
-    float wt = lens_ray(c, imageX, imageY, lensU, lensV, timeU, wl, ray);
+                           uint64_t dkey, Ray *ray, RayDiff *rd) {
+    DiffStream st;
+    st.key = dkey;
+    st.n = 0;
+    float wt = lens_ray(c, imageX, imageY, lensU, lensV, timeU, wl, &st, ray);
     Ray rx, ry;
     float sx = imageX + 1.f;
-    float wtx = lens_ray(c, sx, imageY, lensU, lensV, timeU, wl, &rx);
+    float wtx = lens_ray(c, sx, imageY, lensU, lensV, timeU, wl, &st, &rx);
     sx = sx - 1.f;
-    float wty = lens_ray(c, sx, imageY + 1.f, lensU, lensV, timeU, wl, &ry);
+    float wty = lens_ray(c, sx, imageY + 1.f, lensU, lensV, timeU, wl, &st, &ry);
     if (wtx == 0.f || wty == 0.f) return 0.f;
     float sc = 1.f / sqrtf((float)c->s->spp);
     rd->rxo = vadd(ray->o, vmul(vsub(rx.o, ray->o), sc));
@@ -2164,7 +2251,7 @@ static void camera_path(const Ctx *c, int px, int py, uint32_t s, uint32_t rngId
     Ray r;
     float Lr[MAXB];
     if (c->s->camera_type == PBRTGPU_CAMERA_REALISTIC &&
-        lens_ray_diff(c, imageX, imageY, lens[0], lens[1], timeU, wl, &r, &rd) == 0.f) {
+        lens_ray_diff(c, imageX, imageY, lens[0], lens[1], timeU, wl, ((uint64_t)ps.hp << 32) | rngIdx, &r, &rd) == 0.f) {
         for (int i = 0; i < c->nb; ++i) L[i] = 0.f;   /* rayWeight 0: L = 0, nothing traced */
         if (imgX) *imgX = imageX;
         if (imgY) *imgY = imageY;

@@ -328,6 +328,7 @@ struct DevScene {
     const float *specWl;              // [nWaveBands]: the band's ray wavelength
     int camType;                      // PBRTGPU_CAMERA_*
     int lensN, lensChromatic;         // RealisticDiffractionCamera: elements, chromaticAberrationEnabled
+    int lensDiffraction;              // diffractionEnabled
     float lensFilmDist, lensFilmDiag, lensCurveR, lensApOff[2], lensFilmC[2], lensPinhole[3];
     const float4 *lensEl;             // [lensN]: radius, separation, n, aperture
 };
@@ -2116,13 +2117,98 @@ PGD_INLINE void lens_snell(float n1, float n2, float lensRadius, V nrm, Ray *ray
     const V s2 = vsub(vmul(vcross(nrm, vcross(vmul(nrm, -1.f), s1)), n1 / n2), vmul(nrm, sqrtf(radicand)));
     ray->d = vnorm(s2);
 }
+// ---- diffraction (realisticDiffraction.cpp:1057-1150).  PARITY UNPINNED: the reference draws
+// the Gaussian from one GSL generator (gsl_rng_default, mt19937) shared by every render thread,
+// so which values a ray receives depends on thread scheduling, and GSL is absent here (the
+// reference camera cannot be built).  The oracle restates the same stream; GPU = oracle.
+// The camera sample's stream: each camera sample (and SpectralRenderer band) draws from its own
+// counter-based stream, uniform j = (top 32 bits of splitmix64(key + (j + 1) * golden)) / 2^32
+// (gsl_rng_uniform's 32-bit resolution), key = pixel hash << 32 | the path's RNG index.  Being
+// counter based, the camera differentials re-derived at the first hit (path_camera_diff) see
+// the same values as the camera ray.
+struct DiffStream {
+    uint64_t key;
+    uint32_t j;
+};
+PGD_INLINE double diff_uniform(DiffStream *st) {
+    uint64_t z = st->key + (uint64_t)(++st->j) * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    return (double)(uint32_t)(z >> 32) / 4294967296.0;
+}
+// gsl_ran_bivariate_gaussian (GSL randist/bigauss.c, the polar Box-Muller method) with rho = 0:
+// (u, v) uniform in the square [-1, 1)^2 until 0 < r2 = u^2 + v^2 <= 1, s = sqrt(-2 ln r2 / r2),
+// x = sigma_x u s, y = sigma_y (rho u + sqrt(1 - rho^2) v) s.  The rejection loop is bounded
+// (64 tries, each accepted with probability pi / 4): after that, no noise.
+PGD_INLINE void diff_gaussian(DiffStream *st, double sx, double sy, double *x, double *y) {
+    *x = 0.0;
+    *y = 0.0;
+    for (int k = 0; k < 64; ++k) {
+        const double u = -1 + 2 * diff_uniform(st);
+        const double v = -1 + 2 * diff_uniform(st);
+        const double r2 = u * u + v * v;
+        if (r2 > 1.0 || r2 == 0) continue;
+        const double scale = __builtin_sqrt(-2.0 * pbrt_fm_log(r2) / r2);
+        *x = sx * u * scale;
+        *y = sy * (0.0 * u + 1.0 * v) * scale;
+        return;
+    }
+}
+// The perturbation after element i (aperture stop or lens surface): ip the element's
+// intersection point, ap its aperture, wl the ray's wavelength (0 under the SamplerRenderer:
+// sigma = atan(1 / inf) = 0, the draws are still made).  The expressions keep the reference's
+// float / double mix (float Vector arithmetic and sqrtf where its operands are float).  false:
+// the direction became NaN (weight 0, realisticDiffraction.cpp:1141-1147).  Out of line: its
+// double arithmetic is not inlined into the 2 x 3 element steps of a camera differential.
+__device__ __attribute__((noinline)) bool lens_diffract(DiffStream *st, V ip, float ap, float wl, V *dp) {
+    const double radius = (double)sqrtf(ip.x * ip.x + ip.y * ip.y);
+    V dir = v3(ip.x, ip.y, 0.f), orth = v3(-ip.y, ip.x, 0.f);
+    const double a = (double)(ap / 2) - radius;
+    const double b = __builtin_sqrt((double)(ap / 2 * ap / 2) - radius * radius);
+    const double pi = 3.14159265359;
+    const double lambda = (double)wl * 1e-9;
+    const double sqrt2 = 1.4142135623730951;   // sqrt(2)
+    const double sigx = pbrt_fm_atan(1 / (sqrt2 * a * .001 * 2 * pi / lambda));
+    const double sigy = pbrt_fm_atan(1 / (sqrt2 * b * .001 * 2 * pi / lambda));
+    double nx, ny;
+    diff_gaussian(st, sigx, sigy, &nx, &ny);
+    dir = vnorm(dir);
+    orth = vnorm(orth);
+    const float noiseA = (float)nx, noiseB = (float)ny;
+    V d = *dp;
+    const double projA = (double)((d.x * dir.x + d.y * dir.y) / sqrtf(dir.x * dir.x + dir.y * dir.y));
+    const double projB = (double)((d.x * orth.x + d.y * orth.y) / sqrtf(orth.x * orth.x + orth.y * orth.y));
+    double projC = (double)d.z;
+    const double rA = __builtin_sqrt(projA * projA + projC * projC);
+    double rB = __builtin_sqrt(projB * projB + projC * projC);
+    double thetaA = pbrt_fm_acos(projA / rA);
+    double thetaB = pbrt_fm_acos(projB / rB);
+    thetaA = thetaA + (double)noiseA;
+    thetaB = thetaB + (double)noiseB;   // overwritten below, as in the reference
+    const double newProjA = pbrt_fm_cos(thetaA) * rA;
+    d.z = (float)(pbrt_fm_sin(thetaA) * rA);
+    projC = (double)d.z;
+    rB = __builtin_sqrt(projB * projB + projC * projC);
+    thetaB = pbrt_fm_acos(projB / rB);
+    const double newProjB = pbrt_fm_cos(thetaB) * rB;
+    d.z = (float)(pbrt_fm_sin(thetaB) * rB);
+    d.x = (float)((double)dir.x * newProjA + (double)orth.x * newProjB);
+    d.y = (float)((double)dir.y * newProjA + (double)orth.y * newProjB);
+    if (d.x != d.x || d.y != d.y || d.z != d.z) {
+        *dp = v3(0.f, 0.f, 0.f);
+        return false;
+    }
+    *dp = vnorm(d);
+    return true;
+}
 // RealisticDiffractionCamera::GenerateRay (realisticDiffraction.cpp:478-1164 without the
-// diffraction, pinhole-array and microlens branches): film point -> toward the sampled point
+// pinhole-array and microlens branches): film point -> toward the sampled point
 // of the last element's aperture disk (or the pinhole exit point) -> every element, last
 // first; a blocked or missed element returns weight 0.  The ray ends in world space with a
 // normalised direction.
 PGD_INLINE float lens_ray(const DevScene &S, float imageX, float imageY, float lensU, float lensV, float timeU, float wl,
-                          Ray *out) {
+                          DiffStream *st, Ray *out) {
     const pbrtgpu_camera &cam = S.cam;
     const float xr2 = (float)cam.xres / 2.f, yr2 = (float)cam.yres / 2.f;
     V sp;
@@ -2170,6 +2256,7 @@ PGD_INLINE float lens_ray(const DevScene &S, float imageX, float imageY, float l
             const float dx = ai.x - S.lensApOff[0], dy = ai.y - S.lensApOff[1];
             if ((double)(dx * dx + dy * dy) > (double)(ap * ap) * .25) return 0.f;
             sp = ai;
+            if (S.lensDiffraction && !lens_diffract(st, ai, ap, wl, &r.d)) return 0.f;
         } else {
             float tHit = 0.f;
             V nrm = v3(0.f, 0.f, 1.f);
@@ -2184,6 +2271,7 @@ PGD_INLINE float lens_ray(const DevScene &S, float imageX, float imageY, float l
             }
             lens_snell(n1, n2, rad, nrm, &r, wl, S.lensChromatic);
             sp = ip;
+            if (S.lensDiffraction && !lens_diffract(st, ip, ap, wl, &r.d)) return 0.f;
         }
     }
     r.o = sp;
@@ -2199,14 +2287,16 @@ PGD_INLINE float lens_ray(const DevScene &S, float imageX, float imageY, float l
 // Camera::GenerateRayDifferential (camera.cpp:52-81) for the lens camera: the ray, then the
 // rays one pixel over in x and in y (the sample's imageX restored as (x + 1) - 1), weight 0
 // if any of them is blocked; the offsets scaled by 1 / sqrtf(spp) (samplerrenderer.cpp:91)
+// (the three rays draw from the sample's diffraction stream in that order)
 PGD_INLINE float lens_ray_diff(const DevScene &S, float imageX, float imageY, float lensU, float lensV, float timeU,
-                               float wl, Ray *ray, RayDiff *rd) {
-    const float wt = lens_ray(S, imageX, imageY, lensU, lensV, timeU, wl, ray);
+                               float wl, uint64_t diffKey, Ray *ray, RayDiff *rd) {
+    DiffStream st = {diffKey, 0u};
+    const float wt = lens_ray(S, imageX, imageY, lensU, lensV, timeU, wl, &st, ray);
     Ray rx, ry;
     float sx = imageX + 1.f;
-    const float wtx = lens_ray(S, sx, imageY, lensU, lensV, timeU, wl, &rx);
+    const float wtx = lens_ray(S, sx, imageY, lensU, lensV, timeU, wl, &st, &rx);
     sx = sx - 1.f;
-    const float wty = lens_ray(S, sx, imageY + 1.f, lensU, lensV, timeU, wl, &ry);
+    const float wty = lens_ray(S, sx, imageY + 1.f, lensU, lensV, timeU, wl, &st, &ry);
     if (wtx == 0.f || wty == 0.f) return 0.f;
     const float sc = 1.f / sqrtf((float)S.spp);
     rd->rxo = vadd(ray->o, vmul(vsub(rx.o, ray->o), sc));
@@ -2222,13 +2312,21 @@ PGD_INLINE float path_wavelength(const DevScene &S, int item, uint32_t smp) {
     const int band = S.specMode == 1 ? item % S.specItems : (int)(smp % (uint32_t)S.specBands);
     return (*sa(S.specWl, (uint32_t)(band)));
 }
+// the RNG index of a path (path_seed's): its sample, or under the SpectralRenderer's
+// singleDirection method sample * nWaveBands + band
+PGD_INLINE uint32_t path_rng_index(const DevScene &S, uint32_t item, uint32_t smp) {
+    return S.specItems > 1 ? smp * (uint32_t)S.specItems + item % (uint32_t)S.specItems : smp;
+}
+// the key of a camera sample's diffraction stream
+PGD_INLINE uint64_t diff_key(uint32_t hp, uint32_t rngIdx) { return ((uint64_t)hp << 32) | rngIdx; }
 // the camera ray's differentials for a path (first-hit texture filtering)
-PGD_INLINE RayDiff path_camera_diff(const DevScene &S, int item, uint32_t smp, float imageX, float imageY, float lensU,
-                                    float lensV, float timeU) {
+PGD_INLINE RayDiff path_camera_diff(const DevScene &S, int item, uint32_t hp, uint32_t smp, float imageX, float imageY,
+                                    float lensU, float lensV, float timeU) {
     if (S.camType == PBRTGPU_CAMERA_REALISTIC) {
         Ray r;
         RayDiff rd;
-        (void)lens_ray_diff(S, imageX, imageY, lensU, lensV, timeU, path_wavelength(S, item, smp), &r, &rd);
+        (void)lens_ray_diff(S, imageX, imageY, lensU, lensV, timeU, path_wavelength(S, item, smp),
+                            diff_key(hp, path_rng_index(S, (uint32_t)item, smp)), &r, &rd);
         return rd;
     }
     return camera_diff(S.cam, S.spp, imageX, imageY, lensU, lensV, timeU);

@@ -103,7 +103,7 @@ PGD_INLINE void dl_vertex(const DevScene &S, const PathSoA &P, int slot, int d, 
         s2d(hp, 0, s, spp, u);
         s2d(hp, 1, s, spp, lens);
         const float timeU = s1d(hp, 2, s, spp);
-        v.rd = path_camera_diff(S, P.item[slot], s, (int)(pxy & 0xffffu) + u[0], (int)(pxy >> 16) + u[1], lens[0], lens[1],
+        v.rd = path_camera_diff(S, P.item[slot], hp, s, (int)(pxy & 0xffffu) + u[0], (int)(pxy >> 16) + u[1], lens[0], lens[1],
                                 timeU);
     } else {
         const float *fd = P.fDiff + (size_t)d * 12 * c + slot;

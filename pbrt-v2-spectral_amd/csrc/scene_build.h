@@ -245,6 +245,7 @@ static int scene_build(const pbrtgpu_flat_scene *s, int topNodes, DevScene &S, i
         const pbrtgpu_lens &L = s->lens;
         S.lensN = L.n_elements;
         S.lensChromatic = L.chromatic;
+        S.lensDiffraction = L.diffraction;
         S.lensFilmDist = L.film_distance;
         S.lensFilmDiag = L.film_diag;
         S.lensCurveR = L.curve_radius;

@@ -343,7 +343,8 @@ PGD_INLINE bool emit_black(const DevScene &S, const Emit &e) {
 
 // IrregIsotropicBRDF::f (reflection.cpp:251-264): KdTree::Lookup (kdtree.h:160-185) with
 // IrregIsoProc (reflection.cpp:34-47), retried with the radius doubled until more than 2
-// samples are found, in the reference's visiting order (children first, near child before
+// samples are found (here: the final radius found first, kd_final_radius), in the reference's
+// visiting order (children first, near child before
 // far child, the far child only when the split plane is within reach, then the node).
 //   * The walk is stackless: it climbs back over parent links, so there is no private stack
 //     in scratch memory.
@@ -365,33 +366,82 @@ typedef PGD_LDS_AS const F4N LdsF4;   // an LDS float4 (ds_read_b128)
 PGD_INLINE float4 kd_node(const float4 *__restrict__ p, int i) { return p[i]; }
 PGD_INLINE float4 kd_node(LdsF4 *p, int i) { const F4N v = p[i]; return make_float4(v.x, v.y, v.z, v.w); }
 
+// One step of the walk from node cur (children first, near child before far child, the far child
+// only when its split plane is within maxD2, then the node): the next node to visit, or -1 when
+// the node itself is next.
+PGD_INLINE int kd_next(const float4 &a, const float4 &b, int cur, int prev, bool down, float p0, float p1, float p2,
+                       float maxD2) {
+    const int meta = __float_as_int(b.w), axis = meta & 3;
+    if (axis == 3) return -1;
+    const float pa = axis == 0 ? p0 : (axis == 1 ? p1 : p2);
+    const bool leftFirst = pa <= a.w;
+    const float dist2s = (pa - a.w) * (pa - a.w);
+    const int L = (meta & 4) ? cur + 1 : -1, R = __float_as_int(b.y);   // -1: no right child
+    const int first = leftFirst ? L : R, second = leftFirst ? R : L;
+    if (down && first >= 0) return first;
+    if ((down || prev == first) && second >= 0 && dist2s < maxD2) return second;
+    return -1;
+}
+// The radius the reference's retry loop ends at, without its retries: the loop walks at
+// maxDist2 = .001f * 2^k for k = 0, 1, ... and stops at the first k with more than 2 samples
+// strictly inside, or at k = 11 (maxDist2 = 2.048 > 1.5).  That k is the first with
+// d3 < .001f * 2^k, d3 the third-smallest sample distance^2, which one 3-nearest walk finds
+// (pruning far children at the current third-best: a sample beyond a split plane is at least
+// the plane's float distance^2 away, the float subtraction and sums being monotonic).  The
+// samples found are then accumulated by the reference's own walk at that radius, so the sum and
+// its order are the reference's.  C3's points needed ~3-4 walks of growing radius each.
+template <class NodePtr>
+PGD_INLINE float kd_final_radius(NodePtr nodes, float p0, float p1, float p2) {
+    const float capD2 = .001f * 1024.f;   // k = 10; beyond it the loop ends at k = 11 regardless
+    float d1 = capD2, d2 = capD2, d3 = capD2;
+    int cur = 0, prev = -1;
+    bool down = true;
+    for (;;) {
+        const float4 a = kd_node(nodes, 2 * cur), b = kd_node(nodes, 2 * cur + 1);
+        const int nxt = kd_next(a, b, cur, prev, down, p0, p1, p2, d3);
+        if (nxt >= 0) {
+            prev = cur;
+            cur = nxt;
+            down = true;
+            continue;
+        }
+        const V d = vsub(v3(a.x, a.y, a.z), v3(p0, p1, p2));
+        const float dist2 = vlen2(d);
+        if (dist2 < d3) {   // keep d1 <= d2 <= d3 the three smallest
+            d3 = fminf(fmaxf(dist2, d2), d3);
+            d2 = fminf(fmaxf(dist2, d1), d2);
+            d1 = fminf(dist2, d1);
+        }
+        if (cur == 0) break;
+        prev = cur;
+        cur = __float_as_int(b.z);
+        down = false;
+    }
+    float maxD2 = .001f;
+    for (int k = 0; k < 11 && !(d3 < maxD2); ++k) maxD2 *= 2.f;
+    return maxD2;
+}
 template <int NB, class NodePtr>
 PGD_INLINE void kd_lookup(NodePtr nodes, const float *__restrict__ spectra, float p0, float p1, float p2,
                           float4 *__restrict__ mb, size_t c) {
     constexpr int NQ = Bands<NB>::NQ;
-    float lastMaxDist2 = .001f;
+#ifdef PGD_KD_RETRY   // the reference's retry loop (timing comparison)
+    float maxD2 = .001f;
     for (;;) {
+#else
+    const float maxD2 = kd_final_radius(nodes, p0, p1, p2);
+    {
+#endif
         float4 acc[NQ];
 #pragma unroll
         for (int q = 0; q < NQ; ++q) acc[q] = make_float4(0.f, 0.f, 0.f, 0.f);
         float sumWeights = 0.f;
         int nFound = 0;
-        const float maxD2 = lastMaxDist2;
         int cur = 0, prev = -1;
         bool down = true;
         for (;;) {
             const float4 a = kd_node(nodes, 2 * cur), b = kd_node(nodes, 2 * cur + 1);
-            const int meta = __float_as_int(b.w), axis = meta & 3;
-            int nxt = -1;
-            if (axis != 3) {
-                const float pa = axis == 0 ? p0 : (axis == 1 ? p1 : p2);
-                const bool leftFirst = pa <= a.w;
-                const float dist2s = (pa - a.w) * (pa - a.w);
-                const int L = (meta & 4) ? cur + 1 : -1, R = __float_as_int(b.y);   // -1: no right child
-                const int first = leftFirst ? L : R, second = leftFirst ? R : L;
-                if (down && first >= 0) nxt = first;
-                else if ((down || prev == first) && second >= 0 && dist2s < maxD2) nxt = second;
-            }
+            const int nxt = kd_next(a, b, cur, prev, down, p0, p1, p2, maxD2);
             if (nxt >= 0) {
                 prev = cur;
                 cur = nxt;
@@ -418,16 +468,21 @@ PGD_INLINE void kd_lookup(NodePtr nodes, const float *__restrict__ spectra, floa
             cur = __float_as_int(b.z);
             down = false;
         }
-        if (nFound > 2 || lastMaxDist2 > 1.5f) {
-#pragma unroll
-            for (int q = 0; q < NQ; ++q) {
-                const float4 v = acc[q];
-                mb[q * c] = make_float4(clampf(v.x, 0.f, INFINITY) / sumWeights, clampf(v.y, 0.f, INFINITY) / sumWeights,
-                                        clampf(v.z, 0.f, INFINITY) / sumWeights, clampf(v.w, 0.f, INFINITY) / sumWeights);
-            }
-            return;
+#ifdef PGD_KD_RETRY
+        if (!(nFound > 2 || maxD2 > 1.5f)) {
+            maxD2 *= 2.f;
+            continue;
         }
-        lastMaxDist2 *= 2.f;
+#endif
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            const float4 v = acc[q];
+            mb[q * c] = make_float4(clampf(v.x, 0.f, INFINITY) / sumWeights, clampf(v.y, 0.f, INFINITY) / sumWeights,
+                                    clampf(v.z, 0.f, INFINITY) / sumWeights, clampf(v.w, 0.f, INFINITY) / sumWeights);
+        }
+#ifdef PGD_KD_RETRY
+        return;
+#endif
     }
 }
 template <int NB>
@@ -529,7 +584,8 @@ PGD_INLINE void path_start(const DevScene &S, const PathSoA &P, const ItemSrc &s
     bool dead = false;   // rayWeight 0: the sample's radiance is 0 (samplerrenderer.cpp:105-110)
     if (S.camType == PBRTGPU_CAMERA_REALISTIC) {
         RayDiff rd;
-        dead = lens_ray_diff(S, imageX, imageY, lens[0], lens[1], timeU, path_wavelength(S, (int)item, s), &r, &rd) == 0.f;
+        dead = lens_ray_diff(S, imageX, imageY, lens[0], lens[1], timeU, path_wavelength(S, (int)item, s),
+                             diff_key(hp, path_rng_index(S, item, s)), &r, &rd) == 0.f;
         if (dead) {   // a ray no traversal hits; k_shade writes the zero radiance
             r.o = v3(0.f, 0.f, 0.f);
             r.d = v3(0.f, 0.f, 1.f);
@@ -558,8 +614,7 @@ PGD_INLINE void path_start(const DevScene &S, const PathSoA &P, const ItemSrc &s
     *sa(P.bounce, us) = dead ? -2 : -1;
     *sa(P.flags, us) = PF_CONT | PF_LZ;   // L = 0 and beta_0 = 1 are implicit (not stored)
     *sa(P.mt, us) = 0;
-    *sa(P.mt, 4 * (uint32_t)P.cap + us) =
-        path_seed(hp, S.specItems > 1 ? s * (uint32_t)S.specItems + (item - sitem * (uint32_t)S.specItems) : s);
+    *sa(P.mt, 4 * (uint32_t)P.cap + us) = path_seed(hp, path_rng_index(S, item, s));
 }
 
 // SpectralRenderer output of one band's path (spectralrenderer.cpp:158-188): a NaN
@@ -835,7 +890,7 @@ PGD_INLINE Pushes shade_vertex(const DevScene &S, const PathSoA &P, int slot, in
             s2d(hp, 0, s, spp, u);
             s2d(hp, 1, s, spp, lens);
             const float timeU = s1d(hp, 2, s, spp);
-            RayDiff rd = path_camera_diff(S, P.item[slot], s, (int)(pxy & 0xffffu) + u[0], (int)(pxy >> 16) + u[1],
+            RayDiff rd = path_camera_diff(S, P.item[slot], hp, s, (int)(pxy & 0xffffu) + u[0], (int)(pxy >> 16) + u[1],
                                           lens[0], lens[1], timeU);
             compute_differentials(is.dg, rd, diff);
         }

@@ -1618,18 +1618,15 @@ private:
     // CreateRealisticDiffractionCamera + the constructor's lens file (realisticDiffraction.cpp:
     // 32-193): shutter times default to -1 (not swapped); the lens file is ReadFloatFile's
     // floats, the focal length then (radius, separation, n, aperture) per element, an aperture
-    // stop (radius 0) taking "aperture_diameter".  What GenerateRay does only with GSL
-    // (diffraction, on by default), the pinhole-array / microlens light-field modes and the
-    // eye IOR curves are refused.
+    // stop (radius 0) taking "aperture_diameter"; "diffractionEnabled" (on by default) is
+    // GenerateRay's Gaussian perturbation per element.  The pinhole-array / microlens
+    // light-field modes and the eye IOR curves are refused.
     void RealisticCamera(CameraParams *cp) {
         const ParamSet &p = cameraParams;
         cp->shutterOpen = p.FindOneFloat("shutteropen", -1.f);
         cp->shutterClose = p.FindOneFloat("shutterclose", -1.f);
         std::string spec = p.FindOneString("specfile", "");
         if (spec.empty()) throw std::runtime_error("No lens spec file supplied!");
-        if (p.FindOneBool("diffractionEnabled", true))
-            throw std::runtime_error("realisticDiffraction: diffractionEnabled (GSL Gaussian noise) is not supported; "
-                                     "set \"bool diffractionEnabled\" \"false\"");
         if (p.FindOneBool("IORforEyeEnabled", false))
             throw std::runtime_error("realisticDiffraction: IORforEyeEnabled is not supported");
         if ((int)p.FindOneFloat("num_pinholes_w", -1) > 0 && (int)p.FindOneFloat("num_pinholes_h", -1) > 0)
@@ -1637,6 +1634,7 @@ private:
         pbrtgpu_lens &L = out->lens;
         memset(&L, 0, sizeof(L));
         L.chromatic = p.FindOneBool("chromaticAberrationEnabled", false) ? 1 : 0;
+        L.diffraction = p.FindOneBool("diffractionEnabled", true) ? 1 : 0;   // realisticDiffraction.cpp:61,128
         L.film_distance = p.FindOneFloat("filmdistance", 70.f);
         const float apDiam = p.FindOneFloat("aperture_diameter", 1.f);
         L.film_diag = p.FindOneFloat("filmdiag", 35.f);

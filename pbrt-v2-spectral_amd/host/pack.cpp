@@ -11,7 +11,7 @@
 namespace pbrtamd {
 
 static const char kMagic[8] = {'P', 'B', 'R', 'T', 'P', 'A', 'C', 'K'};
-static const uint32_t kVersion = 8;   // 6: + merl tables; 7: + metadata ids; 8: + Renderer (5-7 still load)
+static const uint32_t kVersion = 9;   // 6: + merl tables; 7: + metadata ids; 8: + Renderer; 9: + lens diffraction (5-8 still load)
 
 static bool W(gzFile f, const void *p, size_t n) {
     const char *c = (const char *)p;
@@ -133,7 +133,11 @@ bool LoadPack(const std::string &path, HostScene *s, std::string *err) {
         ok = R(f, rnd, 12);
         if (ok) { s->renderer = rnd[0]; s->waveBands = rnd[1]; s->spectralSampling = rnd[2]; }
         int32_t ct = 0;
-        ok = ok && R(f, &ct, 4) && R(f, &s->lens, sizeof(s->lens)) && RArr(f, s->lensEl);
+        // v8's pbrtgpu_lens ended at fstop (56 bytes) + the elements pointer
+        const size_t lensBytes = ver >= 9 ? sizeof(s->lens) : 64;
+        char lensBuf[sizeof(s->lens) > 64 ? sizeof(s->lens) : 64];
+        ok = ok && R(f, &ct, 4) && R(f, lensBuf, (unsigned)lensBytes) && RArr(f, s->lensEl);
+        memcpy(&s->lens, lensBuf, ver >= 9 ? sizeof(s->lens) : 56);
         if (ok) s->cameraType = ct;
         s->lens.elements = nullptr;
     }

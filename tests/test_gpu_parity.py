@@ -564,19 +564,25 @@ def test_spectral_renderer_lanes_batches_and_rejects(pg, monkeypatch):
             d.upload(scene)
 
 
-@pytest.mark.parametrize("kw", [dict(), dict(integrator="directlighting"),
-                                dict(renderer="spectral", wave_bands=8, sampling="single"),
-                                dict(renderer="spectral", wave_bands=10, sampling="sampler")])
-def test_realistic_diffraction_camera_vs_oracle(pg, monkeypatch, kw):
+@pytest.mark.parametrize("scene_file,kw", [
+    ("lens.pbrt", dict()), ("lens.pbrt", dict(integrator="directlighting")),
+    ("lens.pbrt", dict(renderer="spectral", wave_bands=8, sampling="single")),
+    ("lens.pbrt", dict(renderer="spectral", wave_bands=10, sampling="sampler")),
+    ("lens_diffraction.pbrt", dict()),
+    ("lens_diffraction.pbrt", dict(renderer="spectral", wave_bands=8, sampling="single")),
+    ("lens_diffraction.pbrt", dict(renderer="spectral", wave_bands=10, sampling="sampler", integrator="directlighting"))])
+def test_realistic_diffraction_camera_vs_oracle(pg, monkeypatch, scene_file, kw):
     """RealisticDiffractionCamera (tests/scenes/lens.pbrt: a double-Gauss lens, chromatic
     aberration on, so every SpectralRenderer band refracts with its own n) on the GPU against
     the oracle, sample by sample and film.  PARITY UNPINNED vs the reference: the camera's TU
     includes GSL headers this image lacks.  About 60 % of the camera rays are
     blocked by the stop (weight 0: radiance 0 without a trace); the differentials come from the
     rays one pixel over (camera.cpp:52-81), which the textured materials use.  A tiny slot pool
-    gives the same bits."""
+    gives the same bits.  lens_diffraction.pbrt: diffraction on (realisticDiffraction.cpp:
+    1057-1150), the Gaussian drawn from each camera sample's own stream, also
+    re-derived for the first hit's differentials."""
     here = os.path.join(os.path.dirname(os.path.abspath(__file__)), "scenes")
-    scene = pg.Scene.load(os.path.join(here, "lens.pbrt"), xres=40, yres=30, spp=4, maxdepth=5, **kw)
+    scene = pg.Scene.load(os.path.join(here, scene_file), xres=40, yres=30, spp=4, maxdepth=5, **kw)
     keys = _keys(scene)
     with pg.Device(0) as d:
         d.upload(scene)

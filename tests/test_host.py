@@ -227,8 +227,8 @@ def test_spectral_renderer_directive(pg, tmp_path):
 def test_realistic_diffraction_camera(pg, tmp_path):
     """Camera "realisticDiffraction" (realisticDiffraction.cpp:32-193): the lens file's focal
     length and elements (an aperture stop takes aperture_diameter), the camera parameters and
-    its -1 shutter defaults reach the flat scene and the pack; what needs GSL (diffraction, on
-    by default), the eye IOR curves and pinhole arrays are refused; the .dat header's line 2
+    its -1 shutter defaults reach the flat scene and the pack (diffractionEnabled: false here,
+    true by default); the eye IOR curves and pinhole arrays are refused; the .dat header's line 2
     carries focal length, f-stop and field of view (spectralImage.cpp:356-360)."""
     here = os.path.join(os.path.dirname(os.path.abspath(__file__)), "scenes")
     s = pg.Scene.load(os.path.join(here, "lens.pbrt"))
@@ -245,12 +245,13 @@ def test_realistic_diffraction_camera(pg, tmp_path):
     t = pg.Scene.load(out)
     el2 = np.ctypeslib.as_array(ctypes.cast(t.flat.lens.elements, ctypes.POINTER(ctypes.c_float)), (11, 4))
     assert t.flat.camera_type == 1 and np.array_equal(el, el2) and t.flat.lens.fstop == f.lens.fstop
+    assert f.lens.diffraction == 0 and t.flat.lens.diffraction == 0
+    assert pg.Scene.load(os.path.join(here, "lens_diffraction.pbrt")).flat.lens.diffraction == 1
     src = open(os.path.join(here, "lens.pbrt")).read()
-    for bad, msg in [('"bool diffractionEnabled" "false"', "diffractionEnabled"),
-                     ('"bool diffractionEnabled" "false" "bool IORforEyeEnabled" "true"', "IORforEye"),
+    for bad, msg in [('"bool diffractionEnabled" "false" "bool IORforEyeEnabled" "true"', "IORforEye"),
                      ('"bool diffractionEnabled" "false" "float num_pinholes_w" [4] "float num_pinholes_h" [4]',
                       "pinhole")]:
-        body = src.replace('"bool diffractionEnabled" "false"', bad if msg != "diffractionEnabled" else "")
+        body = src.replace('"bool diffractionEnabled" "false"', bad)
         p = os.path.join(here, "_lens_bad.pbrt")   # next to the lens file it names
         try:
             open(p, "w").write(body)

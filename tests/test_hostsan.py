@@ -22,6 +22,8 @@ import pytest
 from conftest import GOLDEN, PACKS, ROOT
 
 HS = os.path.join(ROOT, "tools", "hostsan")
+# the RealisticDiffractionCamera with diffraction on (an absolute path: os.path.join keeps it)
+LENS_D = os.path.join(ROOT, "tests", "scenes", "lens_diffraction.pbrt")
 
 
 def _build(target):
@@ -63,11 +65,14 @@ CASES = [
     ("metal.pack", dict(xres=24, yres=24, spp=4, maxdepth=5)),
     ("coverage.pack", dict(xres=40, yres=30, spp=2, integrator="metadata", strategy="depth")),
     ("coverage-b30.pack", dict(xres=40, yres=30, spp=4, maxdepth=6)),
+    (LENS_D, dict(xres=40, yres=30, spp=4, maxdepth=5)),
+    (LENS_D, dict(xres=32, yres=24, spp=2, maxdepth=5, renderer="spectral", wave_bands=8, sampling="single")),
 ]
 
 
 @pytest.mark.parametrize("pack,a", CASES, ids=["dl_all_md6", "dl_one", "dl_killeroo", "path_coverage", "path_anim",
-                                               "path_bunny", "path_metal60", "metadata", "path_coverage_b30"])
+                                               "path_bunny", "path_metal60", "metadata", "path_coverage_b30",
+                                               "lens_diffraction", "lens_diffraction_spectral"])
 def test_replay_matches_oracle(pg, tmp_path, pack, a):
     exe = _build("shade_host")
     scene = pg.Scene.load(os.path.join(PACKS, pack), **a)

@@ -261,7 +261,8 @@ static int run_nb(const DevScene &S, PathSoA &P, const ItemSrc &src, int nSlots,
 int main(int argc, char **argv) {
     if (argc < 2) {
         fprintf(stderr, "usage: %s SCENE [--xres N] [--yres N] [--spp N] [--maxdepth N] [--bands N] [--integrator I] "
-                        "[--strategy S] [--slots N] [--poison BYTE] [--keys FILE] --out FILE\n", argv[0]);
+                        "[--strategy S] [--renderer R --wave_bands N --sampling M] [--slots N] [--poison BYTE] [--keys FILE] "
+                        "--out FILE\n", argv[0]);
         return 2;
     }
     pbrthost_overrides ov = {PBRTHOST_ABI_VERSION, -1, -1, -1, -1, 0, PBRTHOST_KEEP_SEED, -1, -1, -1, -1, -1, -1};
@@ -281,6 +282,9 @@ int main(int argc, char **argv) {
         else if (a == "--keys") keyFile = v;
         else if (a == "--strategy") strategy = v;
         else if (a == "--mt-kat") mtKat = atoi(v);
+        else if (a == "--renderer") ov.renderer = !strcmp(v, "spectral") ? PBRTGPU_RENDERER_SPECTRAL : PBRTGPU_RENDERER_SAMPLER;
+        else if (a == "--wave_bands") ov.wave_bands = atoi(v);
+        else if (a == "--sampling") ov.spectral_sampling = !strcmp(v, "sampler") ? PBRTGPU_SPECTRAL_SAMPLER : PBRTGPU_SPECTRAL_SINGLE;
         else if (a == "--integrator")
             ov.integrator = !strcmp(v, "directlighting") ? PBRTGPU_INTEGRATOR_DIRECT
                             : !strcmp(v, "metadata")     ? PBRTGPU_INTEGRATOR_METADATA
