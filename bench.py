@@ -30,7 +30,7 @@ Extra JSON fields:
                lane, no concurrent kernels, so each kernel's HIP-event spans are its own
                device time); per-kernel table beside it (ms, GB/s, frac, PMC traffic from
                profiles/hbm_traffic.json when it holds this config).  DESIGN.md §5.
-  cpu_baseline the CPU restatement (oracle/liboracle.so, TEST INFRASTRUCTURE) timed on this
+  cpu_baseline the CPU restatement (oracle/liboracle_libm.so, TEST INFRASTRUCTURE) timed on this
                host: every core this process may use, and one core, over a bounded sample of
                the same frame (all spp of pseudo-randomly spread pixels).
 """
@@ -116,14 +116,16 @@ def cpu_info():
 
 
 def cpu_baseline(scene, target_s):
-    """CPU restatement (oracle/liboracle.so, TEST INFRASTRUCTURE) on the host: all spp of
+    """CPU restatement (oracle/liboracle_libm.so, TEST INFRASTRUCTURE: the build with glibc's float
+    transcendentals, whose per-core rate profiles/cpu_calibration.json measured against the
+    reference harness itself on one box) on the host: all spp of
     pseudo-randomly spread pixels of the same frame, sized to ~target_s seconds on every core
     this process may use (the affinity mask, capped by OMP_NUM_THREADS where the box sets a
     CPU share), then ~target_s / 3 on one core."""
     model, ncpu, aff = cpu_info()
     share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
     threads = max(1, min(aff, share) if share > 0 else aff)
-    o = pg.oracle()
+    o = pg.oracle(libm_float=True)
     spp = scene.spp
     pps = scene.paths_per_sample()   # SpectralRenderer singleDirection: a sample is nWaveBands paths
 
@@ -146,7 +148,8 @@ def cpu_baseline(scene, target_s):
             "one_core": round(per_core, 4), "host_cpus": ncpu, "affinity_cpus": aff, "cpu_model": model,
             "sample": "%d paths = all %d samples of %d pseudo-randomly spread pixels of the same frame, %.1f s on "
                       "%d threads; 1-core leg %d paths in %.1f s" % (n, spp, n // spp // pps, dt, threads, n1, dt1),
-            "calibration": "port vs reference per core, same box: profiles/cpu_calibration.json"}
+            "calibration": "this build (liboracle_libm.so) vs the reference harness per core, same box: "
+                           "profiles/cpu_calibration.json (port_over_reference)"}
 
 
 def reduce_over_ranks(dist, elapsed, paths, device="cpu"):
@@ -238,6 +241,35 @@ def exclusive_roofline(dev, scene, tiles, tile, frame_paths, cfg, pps=1):
     return roof
 
 
+def slice_efficiency(dev, scene, tile, full_ms, full_paths, reps=2):
+    """What one GPU does at N GPUs, on this GPU: the 1/N interleaved tile slice of the frame
+    (pbrtgpu.tile_slice, as rank 0 of N renders it), rendered and gathered like a timed step,
+    best of `reps`; its rate over the full-frame rate of the timed steps.  Wall time and the
+    call's device time (trace + shade + accum) are both given, so the per-call fixed cost
+    (host setup, spill scan, the wavefront's fill and drain) shows."""
+    ntx, nty = pg.tile_grid(scene, tile)
+    full_rate = full_paths / (full_ms * 1e-3)
+    film = np.zeros((scene.height, scene.width, scene.bands), np.float32)
+    out = {"what": "rank 0's share at N GPUs (1/N interleaved tiles) on one GPU: its Mpaths/s / the full frame's",
+           "full_frame_ms": round(full_ms, 2)}
+    for n in (2, 4, 8):
+        tiles = pg.tile_slice(ntx * nty, 0, n)
+        best, paths = None, 0.0
+        for _ in range(reps + 1):   # the first call sizes the slot pools
+            t = time.perf_counter()
+            st = dev.render(tiles=tiles, tile=tile)
+            dev.gather(film, tiles=tiles, tile=tile)
+            dt = time.perf_counter() - t
+            paths = st[pg.STAT_PATHS]
+            best = dt if best is None else min(best, dt)
+        tm = dev.timing()
+        dev_ms = sum(tm[k]["ms"] for k in pg.Timing.KERNELS)
+        out["1/%d" % n] = {"efficiency": round(paths / best / full_rate, 4), "ms": round(best * 1e3, 2),
+                           "device_ms": round(dev_ms, 2), "passes": tm["passes"],
+                           "Mpaths_s": round(paths / best / 1e6, 2)}
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -262,6 +294,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--no-slices", action="store_true", help="skip the slice_efficiency block")
     ap.add_argument("--serial", action="store_true", help="timed frames in serial mode (profiling runs)")
     ap.add_argument("--bvh", choices=["host", "gpu"], default="host",
                     help="host: the front end's SAH build (node for node the reference's, the default); "
@@ -367,6 +400,10 @@ def main():
         cfg = args.config + ("" if args.integrator == "path" else "_dl") + ("" if args.renderer == "sampler" else "_spec")
         roof = exclusive_roofline(dev, scene, tiles, tile, frame_paths, cfg, pps)
 
+    slices = None
+    if rank == 0 and n_gpus == 1 and not threads_mode and args.shard == "tiles" and not args.no_slices:
+        slices = slice_efficiency(dev, scene, tile, elapsed / args.steps * 1e3, frame_paths)
+
     cpu = None
     if rank == 0 and n_gpus == 1 and not args.no_cpu:
         cpu = cpu_baseline(scene, args.cpu_seconds)
@@ -389,6 +426,8 @@ def main():
             "roofline": roof,
             "cpu_baseline": cpu,
         }
+        if slices is not None:
+            line["slice_efficiency"] = slices
         if per_rank is not None:
             line["per_gpu_ms_per_step"] = per_rank
         if args.bvh == "gpu":

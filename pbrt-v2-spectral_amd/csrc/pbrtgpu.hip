@@ -604,33 +604,40 @@ __global__ void k_accum(const float *__restrict__ Lbuf, const int *__restrict__ 
 
 // spill scan over the sample extent: queue samples that land on a masked film pixel
 // other than their own sample pixel (spectralImage.cpp:80-92, box filter width 0.5)
-// over the samples [s0, s1) of a render call
+// over the samples [s0, s1) of a render call.  One thread per sample pixel: a pixel none of
+// whose 8 neighbours is masked (most of the frame when a call renders a tile slice) is skipped
+// without evaluating its samples.
 __global__ void k_spill_scan(pbrtgpu_camera cam, uint32_t seed, int spp, int s0, int s1, const uint8_t *__restrict__ mask,
                              int3 *__restrict__ keys, unsigned int *__restrict__ count, unsigned int cap) {
-    const int ew = cam.sx_end - cam.sx_start, eh = cam.sy_end - cam.sy_start, ns = s1 - s0;
-    const long n = (long)ew * eh * ns;
-    for (long it = (long)blockIdx.x * blockDim.x + threadIdx.x; it < n; it += (long)gridDim.x * blockDim.x) {
-        long pi = it / ns;
-        int s = s0 + (int)(it - pi * ns);
-        int x = cam.sx_start + (int)(pi % ew), y = cam.sy_start + (int)(pi / ew);
-        uint32_t hp = pixel_hash(seed, x, y);
-        float u[2];
-        s2d(hp, 0, (uint32_t)s, (uint32_t)spp, u);
-        float ix = x + u[0], iy = y + u[1];
-        float dx = ix - 0.5f, dy = iy - 0.5f;
-        int fx0 = (int)ceilf(dx - 0.5f), fx1 = (int)floorf(dx + 0.5f);
-        int fy0 = (int)ceilf(dy - 0.5f), fy1 = (int)floorf(dy + 0.5f);
-        fx0 = max(fx0, cam.px_start); fx1 = min(fx1, cam.px_start + cam.px_count - 1);
-        fy0 = max(fy0, cam.py_start); fy1 = min(fy1, cam.py_start + cam.py_count - 1);
-        if (fx1 - fx0 < 0 || fy1 - fy0 < 0) continue;
-        if (fx0 == x && fx1 == x && fy0 == y && fy1 == y) continue;
-        bool any = false;
-        for (int fy = fy0; fy <= fy1; ++fy)
-            for (int fx = fx0; fx <= fx1; ++fx)
-                if (!(fx == x && fy == y) && mask[(long)(fy - cam.py_start) * cam.px_count + (fx - cam.px_start)]) any = true;
-        if (!any) continue;
-        unsigned int k = atomicAdd(count, 1u);
-        if (k < cap) keys[k] = make_int3(x, y, s);
+    const int ew = cam.sx_end - cam.sx_start, eh = cam.sy_end - cam.sy_start;
+    const long n = (long)ew * eh;
+    for (long pi = (long)blockIdx.x * blockDim.x + threadIdx.x; pi < n; pi += (long)gridDim.x * blockDim.x) {
+        const int x = cam.sx_start + (int)(pi % ew), y = cam.sy_start + (int)(pi / ew);
+        bool near = false;
+        for (int fy = max(y - 1, cam.py_start); fy <= min(y + 1, cam.py_start + cam.py_count - 1); ++fy)
+            for (int fx = max(x - 1, cam.px_start); fx <= min(x + 1, cam.px_start + cam.px_count - 1); ++fx)
+                if (!(fx == x && fy == y) && mask[(long)(fy - cam.py_start) * cam.px_count + (fx - cam.px_start)]) near = true;
+        if (!near) continue;
+        const uint32_t hp = pixel_hash(seed, x, y);
+        for (int s = s0; s < s1; ++s) {
+            float u[2];
+            s2d(hp, 0, (uint32_t)s, (uint32_t)spp, u);
+            float ix = x + u[0], iy = y + u[1];
+            float dx = ix - 0.5f, dy = iy - 0.5f;
+            int fx0 = (int)ceilf(dx - 0.5f), fx1 = (int)floorf(dx + 0.5f);
+            int fy0 = (int)ceilf(dy - 0.5f), fy1 = (int)floorf(dy + 0.5f);
+            fx0 = max(fx0, cam.px_start); fx1 = min(fx1, cam.px_start + cam.px_count - 1);
+            fy0 = max(fy0, cam.py_start); fy1 = min(fy1, cam.py_start + cam.py_count - 1);
+            if (fx1 - fx0 < 0 || fy1 - fy0 < 0) continue;
+            if (fx0 == x && fx1 == x && fy0 == y && fy1 == y) continue;
+            bool any = false;
+            for (int fy = fy0; fy <= fy1; ++fy)
+                for (int fx = fx0; fx <= fx1; ++fx)
+                    if (!(fx == x && fy == y) && mask[(long)(fy - cam.py_start) * cam.px_count + (fx - cam.px_start)]) any = true;
+            if (!any) continue;
+            unsigned int k = atomicAdd(count, 1u);
+            if (k < cap) keys[k] = make_int3(x, y, s);
+        }
     }
 }
 
@@ -791,6 +798,11 @@ static int top_nodes() {
     const int v = e ? atoi(e) : kTopNodes;
     return std::max(0, std::min(v, kTopNodes));
 }
+// PBRTGPU_PASS_LOG=1: per-pass kernel times and queue sizes on stderr (diagnostics)
+static bool pass_log() {
+    static const bool on = getenv("PBRTGPU_PASS_LOG") != nullptr;
+    return on;
+}
 static bool mt_ext_forced() {
     const char *e = getenv("PBRTGPU_MT_EXT");
     return e && atoi(e) != 0;
@@ -917,12 +929,13 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
     // that code compiled out (fewer registers, no kd-tree stack)
     // the DirectLighting integrator has its own step (all features compiled in)
     const bool dl = c->S.integrator == PBRTGPU_INTEGRATOR_DIRECT;
-    auto kShade = dl ? launch_shade_dl<NB>
-                  : c->S.integrator == PBRTGPU_INTEGRATOR_METADATA ? launch_shade_meta<NB>
+    auto kShade = dl ? (c->feat ? launch_shade_dl<NB, FEAT_ALL> : launch_shade_dl<NB, 0>)
+                  : c->S.integrator == PBRTGPU_INTEGRATOR_METADATA
+                      ? (c->feat ? launch_shade_meta<NB, FEAT_ALL> : launch_shade_meta<NB, 0>)
                   : c->feat ? launch_shade<NB, FEAT_ALL> : launch_shade<NB, 0>;
     const int nFrames = dl ? std::max(1, c->S.maxDepth) : 0;
-    auto kNee = launch_dl_nee<NB>;
-    auto kSpec = launch_dl_spec<NB>;
+    auto kNee = c->feat ? launch_dl_nee<NB, FEAT_ALL> : launch_dl_nee<NB, 0>;
+    auto kSpec = c->feat ? launch_dl_spec<NB, FEAT_ALL> : launch_dl_spec<NB, 0>;
     // DirectLighting issues up to kDlBatch light samples of a vertex per pass
     const int batch = dl ? std::max(1, std::min(c->S.dlStrategy == PBRTGPU_DL_ONE ? 1 : c->S.dlK, kDlBatch)) : 1;
     // passes one path can take: the camera ray + maxdepth + 1 vertices + 1 finish (path); per
@@ -1002,10 +1015,17 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
             }
             for (int j = 0; j < r.batch; ++j) {
                 hipEvent_t *e = L.ev + 2 + 6 * j;
-                HIPCHK(hipEventElapsedTime(&m, e[0], e[1])); T.ms[K_CLOSEST] += m;
-                HIPCHK(hipEventElapsedTime(&m, e[2], e[3])); T.ms[K_SHADOW] += m;
-                HIPCHK(hipEventElapsedTime(&m, e[4], e[5])); T.ms[K_SHADE] += m;
+                float mc, ms, mh;
+                HIPCHK(hipEventElapsedTime(&mc, e[0], e[1])); T.ms[K_CLOSEST] += mc;
+                HIPCHK(hipEventElapsedTime(&ms, e[2], e[3])); T.ms[K_SHADOW] += ms;
+                HIPCHK(hipEventElapsedTime(&mh, e[4], e[5])); T.ms[K_SHADE] += mh;
+                if (pass_log())   // diagnostics: per-pass device time of each lane
+                    fprintf(stderr, "pass_log lane %d pass %d closest %.3f shadow %.3f shade %.3f\n", l,
+                            r.passes - r.batch + j, mc, ms, mh);
             }
+            if (pass_log() && r.batch)
+                fprintf(stderr, "pass_log lane %d after pass %d: closest queue %u shadow queue %u items taken %u of %u\n", l,
+                        r.passes - 1, L.hostCnt[CNT_QC(r.q)], L.hostCnt[CNT_QS(r.q)], L.hostCnt[CNT_NEXT], r.src.nItems);
             int q = r.q;
             if (L.hostCnt[CNT_QC(q)] == 0 && L.hostCnt[CNT_QS(q)] == 0) {
                 r.done = true;
@@ -1315,8 +1335,8 @@ static int render_impl(pbrtgpu_ctx *c, const pbrtgpu_render_desc *d, const int32
         HIPCHK(c->keys.ensure((size_t)cap * sizeof(int3)));
         HIPCHK(c->counter.ensure(16));
         HIPCHK(hipMemsetAsync(c->counter.p, 0, 16, c->stream));
-        long nsamp = (long)(cam.sx_end - cam.sx_start) * (cam.sy_end - cam.sy_start) * (s1 - s0);
-        int grid = (int)std::min<long>((nsamp + 255) / 256, (long)c->numCUs * 16);
+        long npx = (long)(cam.sx_end - cam.sx_start) * (cam.sy_end - cam.sy_start);
+        int grid = (int)std::min<long>((npx + 255) / 256, (long)c->numCUs * 16);
         hipLaunchKernelGGL(k_spill_scan, dim3(grid), dim3(256), 0, c->stream, cam, c->S.seed, spp, s0, s1,
                            (const uint8_t *)c->mask.p, (int3 *)c->keys.p, (unsigned int *)c->counter.p, cap);
         HIPCHK(hipGetLastError());

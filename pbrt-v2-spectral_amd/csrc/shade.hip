@@ -268,38 +268,45 @@ __global__ __launch_bounds__(kShadeBlock) void k_regen(DevScene S, PathSoA P, It
         }
     }
 }
-template <int NB>
+template <int NB, int FEAT>
 hipError_t launch_dl_nee(int grid, hipStream_t stream, const DevScene &S, const PathSoA &P, int qout) {
-    const size_t lds = ((SHADE_FEAT & FEAT_MEAS) && S.kdInLds) ? (size_t)S.nKd * 32 : 0;
-    hipLaunchKernelGGL((k_dl_nee<NB, SHADE_FEAT>), dim3(grid), dim3(kShadeBlock), lds, stream, S, P, qout);
+    const size_t lds = ((FEAT & FEAT_MEAS) && S.kdInLds) ? (size_t)S.nKd * 32 : 0;
+    hipLaunchKernelGGL((k_dl_nee<NB, FEAT>), dim3(grid), dim3(kShadeBlock), lds, stream, S, P, qout);
     return hipGetLastError();
 }
+#if SHADE_FEAT == FEAT_ALL   // one k_regen per band count
 template <int NB>
-hipError_t launch_dl_spec(int grid, hipStream_t stream, const DevScene &S, const PathSoA &P, const ItemSrc &src, int qout,
-                          float *Lout) {
-    const size_t lds = ((SHADE_FEAT & FEAT_MEAS) && S.kdInLds) ? (size_t)S.nKd * 32 : 0;
-    hipLaunchKernelGGL((k_dl_spec<NB, SHADE_FEAT>), dim3(grid), dim3(kShadeBlock), lds, stream, S, P, qout, Lout);
-    if (hipError_t e = hipGetLastError()) return e;
+hipError_t launch_regen(int grid, hipStream_t stream, const DevScene &S, const PathSoA &P, const ItemSrc &src, int qout) {
     hipLaunchKernelGGL((k_regen<NB>), dim3(grid), dim3(kShadeBlock), 0, stream, S, P, src, qout);
     return hipGetLastError();
 }
-template hipError_t launch_dl_nee<SHADE_NB>(int, hipStream_t, const DevScene &, const PathSoA &, int);
-template hipError_t launch_dl_spec<SHADE_NB>(int, hipStream_t, const DevScene &, const PathSoA &, const ItemSrc &, int,
-                                              float *);
-template <int NB>
+template hipError_t launch_regen<SHADE_NB>(int, hipStream_t, const DevScene &, const PathSoA &, const ItemSrc &, int);
+#endif
+template <int NB, int FEAT>
+hipError_t launch_dl_spec(int grid, hipStream_t stream, const DevScene &S, const PathSoA &P, const ItemSrc &src, int qout,
+                          float *Lout) {
+    const size_t lds = ((FEAT & FEAT_MEAS) && S.kdInLds) ? (size_t)S.nKd * 32 : 0;
+    hipLaunchKernelGGL((k_dl_spec<NB, FEAT>), dim3(grid), dim3(kShadeBlock), lds, stream, S, P, qout, Lout);
+    if (hipError_t e = hipGetLastError()) return e;
+    return launch_regen<NB>(grid, stream, S, P, src, qout);
+}
+template hipError_t launch_dl_nee<SHADE_NB, SHADE_FEAT>(int, hipStream_t, const DevScene &, const PathSoA &, int);
+template hipError_t launch_dl_spec<SHADE_NB, SHADE_FEAT>(int, hipStream_t, const DevScene &, const PathSoA &,
+                                                         const ItemSrc &, int, float *);
+template <int NB, int FEAT>
 hipError_t launch_shade_dl(int grid, hipStream_t stream, const DevScene &S, const PathSoA &P, const ItemSrc &src,
                            int qout, float *Lout) {
-    return launch<NB, SHADE_FEAT, MODE_DL>(grid, stream, S, P, src, qout, Lout);
+    return launch<NB, FEAT, MODE_DL>(grid, stream, S, P, src, qout, Lout);
 }
-template <int NB>
+template <int NB, int FEAT>
 hipError_t launch_shade_meta(int grid, hipStream_t stream, const DevScene &S, const PathSoA &P, const ItemSrc &src,
                              int qout, float *Lout) {
-    return launch<NB, SHADE_FEAT, MODE_META>(grid, stream, S, P, src, qout, Lout);
+    return launch<NB, FEAT, MODE_META>(grid, stream, S, P, src, qout, Lout);
 }
-template hipError_t launch_shade_dl<SHADE_NB>(int, hipStream_t, const DevScene &, const PathSoA &, const ItemSrc &, int,
-                                              float *);
-template hipError_t launch_shade_meta<SHADE_NB>(int, hipStream_t, const DevScene &, const PathSoA &, const ItemSrc &,
-                                                int, float *);
+template hipError_t launch_shade_dl<SHADE_NB, SHADE_FEAT>(int, hipStream_t, const DevScene &, const PathSoA &,
+                                                          const ItemSrc &, int, float *);
+template hipError_t launch_shade_meta<SHADE_NB, SHADE_FEAT>(int, hipStream_t, const DevScene &, const PathSoA &,
+                                                            const ItemSrc &, int, float *);
 #else
 template <int NB, int FEAT>
 hipError_t launch_shade(int grid, hipStream_t stream, const DevScene &S, const PathSoA &P, const ItemSrc &src, int qout,

@@ -428,6 +428,9 @@ PGD_INLINE void kd_lookup(NodePtr nodes, const float *__restrict__ spectra, floa
 #ifdef PGD_KD_RETRY   // the reference's retry loop (timing comparison)
     float maxD2 = .001f;
     for (;;) {
+#elif defined(PGD_EXP_KD_FIXED)   // timing experiment only: no radius walk (wrong radiance)
+    const float maxD2 = PGD_EXP_KD_FIXED;
+    {
 #else
     const float maxD2 = kd_final_radius(nodes, p0, p1, p2);
     {
@@ -1181,20 +1184,23 @@ static_assert(kShadeBlock % 64 == 0, "k_shade blocks must be whole waves");
 template <int NB, int FEAT>
 hipError_t launch_shade(int grid, hipStream_t stream, const DevScene &S, const PathSoA &P, const ItemSrc &src, int qout,
                         float *Lout);
-// k_shade with the DirectLightingIntegrator step (all features compiled in)
-template <int NB>
+// k_shade with the DirectLightingIntegrator step (FEAT as for the path integrator)
+template <int NB, int FEAT>
 hipError_t launch_shade_dl(int grid, hipStream_t stream, const DevScene &S, const PathSoA &P, const ItemSrc &src,
                            int qout, float *Lout);
 // k_dl_nee: the light-sample batches of the DirectLighting slots k_shade marked (PF_DLNEE)
-template <int NB>
+template <int NB, int FEAT>
 hipError_t launch_dl_nee(int grid, hipStream_t stream, const DevScene &S, const PathSoA &P, int qout);
 // k_dl_spec: their specular branches and frame pops (PF_DLSPEC), then k_regen: the slots it
 // freed take the next camera samples
-template <int NB>
+template <int NB, int FEAT>
 hipError_t launch_dl_spec(int grid, hipStream_t stream, const DevScene &S, const PathSoA &P, const ItemSrc &src, int qout,
                           float *Lout);
-// k_shade with the MetadataIntegrator step (all features compiled in)
+// k_regen alone (instantiated once per band count, in the FEAT_ALL DirectLighting object)
 template <int NB>
+hipError_t launch_regen(int grid, hipStream_t stream, const DevScene &S, const PathSoA &P, const ItemSrc &src, int qout);
+// k_shade with the MetadataIntegrator step
+template <int NB, int FEAT>
 hipError_t launch_shade_meta(int grid, hipStream_t stream, const DevScene &S, const PathSoA &P, const ItemSrc &src,
                              int qout, float *Lout);
 

@@ -1,6 +1,6 @@
 """Summarise rocprofv3 rocpd databases (kernel traces and PMC passes of tools/gpu_profile.sh)
 into profiles/.  Usage:
-  python tools/rocpd_summary.py TAG gpurun_out/TAG CONFIG
+  python tools/rocpd_summary.py TAG gpurun_out/TAG CONFIG [OUTDIR (default profiles/)]
     -> profiles/TAG_kernel_stats.txt   per-kernel calls / total / avg / min / max (ns -> ms) of
                                        the default-mode trace and of the serial-mode trace
        profiles/TAG_pmc.txt            per-kernel PMC sums (FETCH, WRITE, SQ groups)
@@ -63,6 +63,8 @@ def main():
     tag, d, cfg = sys.argv[1], sys.argv[2], sys.argv[3]
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     prof = os.path.join(root, "profiles")
+    out = sys.argv[4] if len(sys.argv) > 4 else prof   # the GPU box: a directory under gpurun_out
+    os.makedirs(out, exist_ok=True)
     lines = []
     for sub, title in (("trace", "rocprofv3 --kernel-trace --stats -- python3 bench.py --config %s --no-cpu --no-roofline "
                                  "--steps 2 --warmup 1   (default mode: two lanes + shadow stream, spans overlap)"),
@@ -72,10 +74,10 @@ def main():
         if f:
             lines += stats_lines(kernel_rows(sqlite3.connect(f[0])), (title % cfg) + "  [%s]" % tag) + [""]
     if lines:
-        open(os.path.join(prof, "%s_kernel_stats.txt" % tag), "w").write("\n".join(lines))
+        open(os.path.join(out, "%s_kernel_stats.txt" % tag), "w").write("\n".join(lines))
         print("\n".join(lines))
     pm = {}
-    for sub in ("pmc_fetch", "pmc_write", "pmc_sq1", "pmc_sq2"):
+    for sub in ("pmc_fetch", "pmc_write", "pmc_sq1", "pmc_sq2", "pmc_lds"):
         for f in glob.glob(os.path.join(d, sub, "**", "*.db"), recursive=True):
             for kk, v in pmc_rows(sqlite3.connect(f)).items():
                 pm.setdefault(kk, []).extend(v)
@@ -105,10 +107,13 @@ def main():
             pl.append("# %s: VALU insts / wave %.0f, VMEM_RD / wave %.1f, VMEM_WR / wave %.1f" % (
                 t, cs["SQ_INSTS_VALU"][0] / cs["SQ_WAVES"][0], cs.get("SQ_INSTS_VMEM_RD", [0])[0] / cs["SQ_WAVES"][0],
                 cs.get("SQ_INSTS_VMEM_WR", [0])[0] / cs["SQ_WAVES"][0]))
-    open(os.path.join(prof, "%s_pmc.txt" % tag), "w").write("\n".join(pl) + "\n")
+    open(os.path.join(out, "%s_pmc.txt" % tag), "w").write("\n".join(pl) + "\n")
     print("\n".join(pl))
     tf = os.path.join(prof, "hbm_traffic.json")
     tr = json.load(open(tf)) if os.path.exists(tf) else {}
+    tf = os.path.join(out, "hbm_traffic.json")
+    if os.path.exists(tf):   # an earlier config of the same run
+        tr = json.load(open(tf))
     if "configs" not in tr:
         tr = {"configs": {}}
     ent = {"source": "%s: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (separate) of bench.py --config %s --steps 1 "
