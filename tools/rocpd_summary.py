@@ -18,9 +18,9 @@ import sqlite3
 import sys
 
 # timing names of pbrtgpu_last_timing <- device kernel name prefixes (uninstrumented instances)
-NAMES = {"k_trace_closest": ("k_trace_pt<false, false>", "k_trace_closest<false, true>"),
-         "k_trace_shadow": ("k_trace_pt<true, false>", "k_trace_shadow<false, true>"),
-         "k_shade": ("k_shade<",),
+NAMES = {"k_trace_closest": ("k_trace_pt<false, false>", "k_trace_closest<false, true>", "k_trace_inst<false, false>"),
+         "k_trace_shadow": ("k_trace_pt<true, false>", "k_trace_shadow<false, true>", "k_trace_inst<true, false>"),
+         "k_shade": ("k_shade<", "k_dl_nee<", "k_dl_spec<", "k_regen<"),
          "k_accum": ("k_accum<",)}
 
 
