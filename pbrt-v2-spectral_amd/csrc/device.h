@@ -187,6 +187,10 @@ PGD_INLINE void mt_begin(MT &r, uint32_t seed) { r.seed = seed; r.init = false; 
 // Scalars in and out: an MT passed by reference to an out-of-line function would live in
 // scratch memory at every draw site.
 __device__ __attribute__((noinline)) uint32_t mt_word397(uint32_t w) {
+#ifdef PGD_EXP_MT_CHEAP   // timing experiment only: the recurrence's cost (wrong MT values)
+    for (uint32_t i = 2; i <= 5; ++i) w = mt_next_word(w, i);
+    return w;
+#endif
 #pragma unroll 4
     for (uint32_t i = 2; i <= 397; ++i) w = mt_next_word(w, i);
     return w;

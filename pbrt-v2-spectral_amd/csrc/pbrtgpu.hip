@@ -589,6 +589,22 @@ __global__ void k_spec_guard(const DevScene S, float *__restrict__ Lout, uint32_
     }
 }
 
+// MT windows of the slots k_shade (path integrator) listed in qT set q, one lane per entry (the
+// list is compacted, so every lane of a wave runs the recurrence for a path); clears set q ^ 1's
+// count, which the previous pass's k_mt_init consumed and the next k_shade fills
+__global__ __launch_bounds__(256) void k_mt_init(PathSoA P, int q) {
+    const uint32_t n = P.cnt[CNT_QT(q)];
+    const uint32_t *list = P.qT + (size_t)q * P.cap;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+        mt_window_init(P, list[i]);
+    if (blockIdx.x == 0 && threadIdx.x == 0) P.cnt[CNT_QT(q ^ 1)] = 0u;
+}
+static const int kMtInitGrid = 1024;   // 4 blocks per CU; a pass lists ~1 M slots at most (C2)
+static hipError_t launch_mt_init(hipStream_t s, const PathSoA &P, int q) {
+    hipLaunchKernelGGL(k_mt_init, dim3(kMtInitGrid), dim3(256), 0, s, P, q);
+    return hipGetLastError();
+}
+
 // film[filmIdx[p]][b] += L(p, s) for s in batch order (spectralImage.cpp:125-131)
 template <int NB>
 __global__ void k_accum(const float *__restrict__ Lbuf, const int *__restrict__ filmIdx, int nPix, int sb,
@@ -845,7 +861,7 @@ static int ensure_slots(Lane *c, int cap, int NB, int nInst, int nFrames, int ba
            oMt = take(C * 20), oBeta = take(C * 3 * NBP * 4), oL = take(C * NBP * 4), oA = take(C * AB * NBP * 4),
            oB = take(C * AB * NBP * 4), oM = take(C * NBP * 4), oK = take(C * NBP * 4), oPix = take(C * 4),
            oRay = take(R * 27 * 4), oHitP = take(R * 8), oHitT = take(R * 8), oOcc = take(R * 4), oQC = take(R * 16),
-           oQS = take(R * 8), oCnt = take(CNT_WORDS * 4), oInst = take(C * (size_t)nInst * 128),
+           oQS = take(R * 8), oQT = take(C * 8), oCnt = take(CNT_WORDS * 4), oInst = take(C * (size_t)nInst * 128),
            oMask = take(nFrames ? C * 4 : 0), oAMask = take(2 * ((C + 63) / 64) * 8),
            oBMask = take(3 * ((C + 63) / 64) * 8), oMMask = take(2 * ((C + 63) / 64) * 8);
     const size_t F = (size_t)nFrames;
@@ -869,6 +885,7 @@ static int ensure_slots(Lane *c, int cap, int NB, int nInst, int nFrames, int ba
     P.M = (float4 *)(base + oM); P.K = (float4 *)(base + oK); P.pix = (uint32_t *)(base + oPix);
     P.ray = (float *)(base + oRay); P.hitPrim = (int *)(base + oHitP); P.hitT = (float *)(base + oHitT);
     P.occ = (uint32_t *)(base + oOcc); P.qC = (uint32_t *)(base + oQC); P.qS = (uint32_t *)(base + oQS);
+    P.qT = (uint32_t *)(base + oQT);
     P.cnt = (uint32_t *)(base + oCnt);
     P.nInst = nInst;
     P.instM = nInst ? (float4 *)(base + oInst) : nullptr;
@@ -934,6 +951,8 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
                       ? (c->feat ? launch_shade_meta<NB, FEAT_ALL> : launch_shade_meta<NB, 0>)
                   : c->feat ? launch_shade<NB, FEAT_ALL> : launch_shade<NB, 0>;
     const int nFrames = dl ? std::max(1, c->S.maxDepth) : 0;
+    // the path integrator's k_shade lists the slots about to make their first MT draws (k_mt_init)
+    const bool mtList = c->S.integrator != PBRTGPU_INTEGRATOR_DIRECT && c->S.integrator != PBRTGPU_INTEGRATOR_METADATA;
     auto kNee = c->feat ? launch_dl_nee<NB, FEAT_ALL> : launch_dl_nee<NB, 0>;
     auto kSpec = c->feat ? launch_dl_spec<NB, FEAT_ALL> : launch_dl_spec<NB, 0>;
     // DirectLighting issues up to kDlBatch light samples of a vertex per pass
@@ -1076,6 +1095,7 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
                     L.P.pass = (L.P.pass + 1) % 3;
                     HIPCHK(kShade(r.grid, L.s, c->S, P, r.src, nq, Lout));
                     if (dl) { HIPCHK(kNee(r.grid, L.s, c->S, P, nq)); HIPCHK(kSpec(r.grid, L.s, c->S, P, r.src, nq, Lout)); }
+                    if (mtList) HIPCHK(launch_mt_init(L.s, P, nq));
                     T.launches[K_SHADE]++;
                     HIPCHK(hipEventRecord(e[5], L.s));
                     T.passes++;
@@ -1117,6 +1137,7 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
                 L.P.pass = (L.P.pass + 1) % 3;
                 HIPCHK(kShade(r.grid, L.s, c->S, P, r.src, nq, Lout));
                 if (dl) { HIPCHK(kNee(r.grid, L.s, c->S, P, nq)); HIPCHK(kSpec(r.grid, L.s, c->S, P, r.src, nq, Lout)); }
+                if (mtList) HIPCHK(launch_mt_init(L.s, P, nq));
                 T.launches[K_SHADE]++;
                 HIPCHK(hipEventRecord(e[5], L.s));
                 T.passes++;

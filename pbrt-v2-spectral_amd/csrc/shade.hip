@@ -106,10 +106,13 @@ __global__ __launch_bounds__(kShadeBlock) PGD_SHADE_ATTR void k_shade(DevScene S
     // the MIS rays; the shadow queue the shadow rays.  Entries are in block order.
     PGD_T0(PUSH);
     __shared__ uint32_t qsh[24];   // per wave [w][4]: want, C, M, S (totals -> offsets); bases
+    __shared__ uint32_t qtw[5];    // path integrator: per wave the MT-window list entries -> offsets; base
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const unsigned long long lt = (1ull << lane) - 1ull;
     const bool want = freeSlot && *(volatile uint32_t *)&P.cnt[CNT_NEXT] < src.nItems;
     const unsigned long long bW = __ballot(want), bC = __ballot(pu.c);
+    const unsigned long long bT = MODE == MODE_PATH ? __ballot(pu.t) : 0ull;
+    if (MODE == MODE_PATH && lane == 0) qtw[wave] = (uint32_t)__popcll(bT);
     uint32_t pm, ps, tm, ts;   // this thread's prefix and the wave total, MIS / shadow entries
     if (MODE == MODE_DL) {   // a batch of light samples per slot: ray slots slot + j * cap
         const uint32_t nm = (uint32_t)__popc(pu.mMask), ns = (uint32_t)__popc(pu.sMask);
@@ -121,6 +124,24 @@ __global__ __launch_bounds__(kShadeBlock) PGD_SHADE_ATTR void k_shade(DevScene S
         pm = (uint32_t)__popcll(bM & lt); ps = (uint32_t)__popcll(bS & lt);
         tm = (uint32_t)__popcll(bM); ts = (uint32_t)__popcll(bS);
     }
+#ifdef PGD_QC_OCT
+    // path integrator: the block's continuation and MIS entries grouped by direction octant
+    // (octant-major, then wave, then lane), so a trace wave's queue range holds runs of rays
+    // that leave nearby vertices in the same octant
+    constexpr int kW = kShadeBlock / 64;
+    __shared__ uint32_t qoc[2 * 8 * kW];   // [C / M][octant][wave]: counts -> offsets in the block's C / M entries
+    uint32_t rC = 0u, rM = 0u;             // the lane's rank among its wave's entries of its octant
+    if (MODE == MODE_PATH) {
+#pragma unroll
+        for (int o = 0; o < 8; ++o) {
+            const bool ic = pu.c && pu.octC == (uint32_t)o, im = pu.m && pu.octM == (uint32_t)o;
+            const unsigned long long bo = __ballot(ic), bmo = __ballot(im);
+            if (ic) rC = (uint32_t)__popcll(bo & lt);
+            if (im) rM = (uint32_t)__popcll(bmo & lt);
+            if (lane == 0) { qoc[o * kW + wave] = (uint32_t)__popcll(bo); qoc[(8 + o) * kW + wave] = (uint32_t)__popcll(bmo); }
+        }
+    }
+#endif
     if (lane == 0) {
         qsh[4 * wave + 0] = (uint32_t)__popcll(bW); qsh[4 * wave + 1] = (uint32_t)__popcll(bC);
         qsh[4 * wave + 2] = tm; qsh[4 * wave + 3] = ts;
@@ -136,11 +157,28 @@ __global__ __launch_bounds__(kShadeBlock) PGD_SHADE_ATTR void k_shade(DevScene S
         qsh[16] = nb; qsh[17] = nReg; qsh[18] = nQC ? atomicAdd(&P.cnt[CNT_QC(qout)], nQC) : 0u;
         qsh[19] = t[3] ? atomicAdd(&P.cnt[CNT_QS(qout)], t[3]) : 0u;
         qsh[20] = t[1];
+        if (MODE == MODE_PATH) {
+            uint32_t tt = 0u;
+            for (int w = 0; w < (int)(blockDim.x >> 6); ++w) { const uint32_t v = qtw[w]; qtw[w] = tt; tt += v; }
+            qtw[4] = tt ? atomicAdd(&P.cnt[CNT_QT(qout)], tt) : 0u;
+#ifdef PGD_QC_OCT
+            for (int k = 0; k < 2; ++k) {
+                uint32_t acc = 0u;
+                for (int i = 0; i < 8 * kW; ++i) { const uint32_t v = qoc[k * 8 * kW + i]; qoc[k * 8 * kW + i] = acc; acc += v; }
+            }
+#endif
+        }
     }
     __syncthreads();
     uint32_t *qC = P.qC + (size_t)qout * 2 * P.rcap, *qS = P.qS + (size_t)qout * P.rcap;
     const uint32_t qcBase = qsh[18], nC = qsh[20], nReg = qsh[17];
+#ifdef PGD_QC_OCT
+    if (MODE == MODE_PATH) {
+        if (pu.c) qC[qcBase + qoc[pu.octC * kW + wave] + rC] = (uint32_t)slot << 1;
+    } else
+#endif
     if (pu.c) qC[qcBase + qsh[4 * wave + 1] + (uint32_t)__popcll(bC & lt)] = (uint32_t)slot << 1;
+    if (MODE == MODE_PATH && pu.t) P.qT[(size_t)qout * P.cap + qtw[4] + qtw[wave] + (uint32_t)__popcll(bT & lt)] = (uint32_t)slot;
     if (want) {
         const uint32_t r = qsh[4 * wave + 0] + (uint32_t)__popcll(bW & lt);   // block order among free slots
         if (r < nReg) {
@@ -153,6 +191,9 @@ __global__ __launch_bounds__(kShadeBlock) PGD_SHADE_ATTR void k_shade(DevScene S
         for (uint32_t m = pu.mMask; m; m &= m - 1u) qC[km++] = ((uint32_t)(slot + (__ffs(m) - 1) * P.cap) << 1) | 1u;
         for (uint32_t m = pu.sMask; m; m &= m - 1u) qS[ks++] = (uint32_t)(slot + (__ffs(m) - 1) * P.cap);
     } else {
+#ifdef PGD_QC_OCT
+        if (MODE == MODE_PATH) km = qcBase + nC + nReg + qoc[(8 + pu.octM) * kW + wave] + rM;
+#endif
         if (pu.m) qC[km] = ((uint32_t)(MODE == MODE_PATH ? pu.mIdx : slot) << 1) | 1u;
         if (pu.s) qS[ks] = (uint32_t)(MODE == MODE_PATH ? pu.sIdx : slot);
     }

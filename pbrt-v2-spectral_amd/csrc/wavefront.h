@@ -69,7 +69,8 @@ enum { RAY_C = 0, RAY_M = 1, RAY_S = 2 };
 // different queues do not serialise on one memory-side atomic unit; work = u64 at CNT_WORK
 #define CNT_QC(q) (32 * (q))          // closest-hit queue size, queue set q = 0, 1
 #define CNT_QS(q) (64 + 32 * (q))     // shadow queue size
-enum { CNT_NEXT = 128, CNT_ZEROED = 160, CNT_WORK = 192, CNT_WORDS = 288 };
+#define CNT_QT(q) (224 + 32 * (q))    // MT-window list size (qT): k_mt_init of set q clears set q ^ 1
+enum { CNT_NEXT = 128,CNT_ZEROED = 160, CNT_WORK = 192, CNT_WORDS = 288 };
 enum { W_RAYS = 0, W_SHADOW = 1, W_NODES_C = 2, W_NODES_S = 3, W_TRIS_C = 4, W_TRIS_S = 5, W_QUADS_C = 6, W_QUADS_S = 7,
        W_HITS = 8, W_RAYS_M = 9, W_HITS_M = 10, W_COUNT = 12 };
 
@@ -105,7 +106,8 @@ struct PathSoA {
     uint32_t *occ;      // [rcap]
     uint32_t *qC;       // [2][2*rcap]: (ray slot << 1) | kind
     uint32_t *qS;       // [2][rcap]: ray slot
-    uint32_t *cnt;      // counters (CNT_*), work counters as u64 from word CNT_WORK
+    uint32_t *qT;       // [2][cap]: path integrator, slots whose MT window k_mt_init computes (mt_window_init)
+    uint32_t *cnt;     // counters (CNT_*), work counters as u64 from word CNT_WORK
     float4 *instM;      // [cap][nInst][8]: the path's instance transforms (inst_load), or null
     int nInst;
     // DirectLightingIntegrator only (null for the path integrator): the slot's stack of the
@@ -175,6 +177,19 @@ PGD_INLINE void mt_load(const PathSoA &P, int slot, uint32_t fl, MT &r) {
 PGD_INLINE void mt_store(const PathSoA &P, int slot, const MT &r) {
     const uint32_t c = (uint32_t)P.cap, s = (uint32_t)slot;
     *sa(P.mt, s) = r.k; *sa(P.mt, c + s) = r.a; *sa(P.mt, 2 * c + s) = r.b; *sa(P.mt, 3 * c + s) = r.m;
+}
+// The recurrence window of a path before its first MT draw (output 0: mt[0], mt[1], mt[397] of its
+// seed), for a path integrator slot that shade_vertex queued in qT when it continued from vertex 2
+// (vertex 3 draws first).  k_mt_init runs it over the pass's compacted list after k_shade: inline
+// at the draw site, the 396 dependent steps of mt_word397 ran once per pass in nearly every wave
+// (one lane in ~10 reaches vertex 3 in a given pass) and made up a large part of k_shade's VALU work
+PGD_INLINE void mt_window_init(const PathSoA &P, uint32_t s) {
+    const uint32_t c = (uint32_t)P.cap;
+    MT r;
+    mt_begin(r, *sa(P.mt, 4 * c + s));
+    mt_init(r);
+    *sa(P.mt, c + s) = r.a; *sa(P.mt, 2 * c + s) = r.b; *sa(P.mt, 3 * c + s) = r.m;
+    *sa(P.flags, s) |= PF_MTINIT;
 }
 
 template <int NB> struct Bands { static constexpr int NQ = (NB + 3) / 4; };
@@ -691,9 +706,12 @@ PGD_INLINE bool path_output(const DevScene &S, const float4 (&L)[Bands<NB>::NQ],
     return bad;
 }
 
+PGD_INLINE uint32_t ray_octant(V d) { return (d.x < 0.f ? 1u : 0u) | (d.y < 0.f ? 2u : 0u) | (d.z < 0.f ? 4u : 0u); }
 // ray requests produced by one shade step (DirectLighting batches: the MIS / shadow rays of
 // batch samples j at ray slots slot + j * cap, bit j of mMask / sMask)
-struct Pushes { bool c, m, s; uint32_t mMask, sMask; int sIdx, mIdx; };   // the shadow / MIS ray's ray slot (path)
+// t (path integrator): the slot's MT window goes to k_mt_init's list (mt_window_init)
+// octC / octM (path integrator): direction octant of the continuation / MIS ray (queue binning)
+struct Pushes { bool c, m, s; uint32_t mMask, sMask; int sIdx, mIdx; bool t; uint32_t octC, octM; };   // the shadow / MIS ray's ray slot (path)
 
 // Additions to L a vertex makes before its direct light is known, in order: emitted
 // radiance (path.cpp:67-68; bounce 0 or after a specular bounce) and the zero direct light
@@ -850,6 +868,7 @@ PGD_UNROLL_BANDS
                     fl |= PF_PB;
                     out.m = true;
                     out.mIdx = rsM;
+                    out.octM = ray_octant(mr.d);
                 }
             }
         }
@@ -1016,6 +1035,10 @@ PGD_INLINE Pushes shade_vertex(const DevScene &S, const PathSoA &P, int slot, in
             ray_store(P, RAY_C, slot, nray);
             fl |= PF_CONT;
             out.c = true;
+            out.octC = ray_octant(nray.d);
+#ifndef PGD_EXP_NO_MT_LIST   // A/B experiment: the window computed inline at vertex 3 instead
+            out.t = vb == 2 && !(fl & PF_MTINIT);   // vertex 3 makes the path's first MT draws
+#endif
         }
     }
     if (useMT) {

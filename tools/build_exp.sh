@@ -10,7 +10,7 @@ H="/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=
 pids=()
 for v in 32_0 32_7 60_0 60_7 30_0 30_7 3_0 3_7; do
   $H "$@" -DSHADE_NB=${v%_*} -DSHADE_FEAT=${v#*_} -c csrc/shade.hip -o $T/s$v.o & pids+=($!)
-  if [ ${v#*_} = 7 ]; then $H "$@" -DSHADE_NB=${v%_*} -DSHADE_FEAT=7 -DSHADE_DL=1 -c csrc/shade.hip -o $T/d$v.o & pids+=($!); fi
+  $H "$@" -DSHADE_NB=${v%_*} -DSHADE_FEAT=${v#*_} -DSHADE_DL=1 -c csrc/shade.hip -o $T/d$v.o & pids+=($!)
 done
 $H "$@" -c csrc/pbrtgpu.hip -o $T/p.o & pids+=($!)
 $H "$@" -c csrc/lbvh.hip -o $T/lbvh.o & pids+=($!)

@@ -151,6 +151,7 @@ static int run(const DevScene &S, PathSoA &P, const ItemSrc &src, int nSlots, fl
             if (pu.m) Q[q].c.push_back(((uint32_t)(MODE == MODE_PATH ? pu.mIdx : slot) << 1) | 1u);
             if (pu.s) Q[q].s.push_back((uint32_t)(MODE == MODE_PATH ? pu.sIdx : slot));
         }
+        if (MODE == MODE_PATH && pu.t) mt_window_init(P, (uint32_t)slot);   // k_mt_init (after the pass on the GPU)
     };
     // MT19937 outputs a finished path drew (the most of any path is reported: > 227 exercises mt_uint_ext)
     auto note_draws = [&](int slot) {
