@@ -599,6 +599,35 @@ __global__ __launch_bounds__(256) void k_mt_init(PathSoA P, int q) {
         mt_window_init(P, list[i]);
     if (blockIdx.x == 0 && threadIdx.x == 0) P.cnt[CNT_QT(q ^ 1)] = 0u;
 }
+// The drain's list of live slots (PathSoA::listMode): block b lists the live slots of
+// [b * chunk, (b + 1) * chunk) in slot order, one device-scope atomic per block
+__global__ __launch_bounds__(256) void k_live_list(PathSoA P, int chunk) {
+    const int lo = blockIdx.x * chunk, hi = min(P.cap, lo + chunk);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    __shared__ uint32_t cnt[4], base;
+    uint32_t mine = 0u;
+    for (int s = lo + (int)threadIdx.x; s < hi; s += 256) mine += P.item[s] >= 0 ? 1u : 0u;
+    if (threadIdx.x == 0) base = 0u;
+    __syncthreads();
+    if (mine) atomicAdd(&base, mine);
+    __syncthreads();
+    if (threadIdx.x == 0) base = base ? atomicAdd(&P.cnt[CNT_LIVE], base) : 0u;
+    __syncthreads();
+    uint32_t off = base;
+    for (int s0 = lo; s0 < hi; s0 += 256) {
+        const int s = s0 + (int)threadIdx.x;
+        const bool lv = s < hi && P.item[s] >= 0;
+        const unsigned long long b = __ballot(lv);
+        if (lane == 0) cnt[wave] = (uint32_t)__popcll(b);
+        __syncthreads();
+        uint32_t pre = 0u, tot = 0u;
+        for (int w = 0; w < 4; ++w) { pre += w < wave ? cnt[w] : 0u; tot += cnt[w]; }
+        if (lv) P.live[off + pre + (uint32_t)__popcll(b & ((1ull << lane) - 1ull))] = (uint32_t)s;
+        off += tot;
+        __syncthreads();
+    }
+}
+static const int kLiveChunk = 4096;
 static const int kMtInitGrid = 1024;   // 4 blocks per CU; a pass lists ~1 M slots at most (C2)
 static hipError_t launch_mt_init(hipStream_t s, const PathSoA &P, int q) {
     hipLaunchKernelGGL(k_mt_init, dim3(kMtInitGrid), dim3(256), 0, s, P, q);
@@ -823,6 +852,18 @@ static bool mt_ext_forced() {
     const char *e = getenv("PBRTGPU_MT_EXT");
     return e && atoi(e) != 0;
 }
+static bool drain_list_on() {
+    const char *e = getenv("PBRTGPU_DRAIN_LIST");
+    return !e || atoi(e) != 0;
+}
+// before a k_shade pass: the drain's live-slot list and PathSoA::listMode (read by the launch)
+static hipError_t drain_list(Lane &L, bool drain, int cap) {
+    L.P.listMode = drain ? 1 : 0;
+    if (!drain) return hipSuccess;
+    if (hipError_t e = hipMemsetAsync(L.P.cnt + CNT_LIVE, 0, 4, L.s)) return e;
+    hipLaunchKernelGGL(k_live_list, dim3((cap + kLiveChunk - 1) / kLiveChunk), dim3(256), 0, L.s, L.P, kLiveChunk);
+    return hipGetLastError();
+}
 static bool serial_mode() {
     const char *e = getenv("PBRTGPU_SERIAL");
     return e && atoi(e) != 0;
@@ -861,7 +902,7 @@ static int ensure_slots(Lane *c, int cap, int NB, int nInst, int nFrames, int ba
            oMt = take(C * 20), oBeta = take(C * 3 * NBP * 4), oL = take(C * NBP * 4), oA = take(C * AB * NBP * 4),
            oB = take(C * AB * NBP * 4), oM = take(C * NBP * 4), oK = take(C * NBP * 4), oPix = take(C * 4),
            oRay = take(R * 27 * 4), oHitP = take(R * 8), oHitT = take(R * 8), oOcc = take(R * 4), oQC = take(R * 16),
-           oQS = take(R * 8), oQT = take(C * 8), oCnt = take(CNT_WORDS * 4), oInst = take(C * (size_t)nInst * 128),
+           oQS = take(R * 8), oQT = take(C * 8), oLive = take(C * 4), oCnt = take(CNT_WORDS * 4), oInst = take(C * (size_t)nInst * 128),
            oMask = take(nFrames ? C * 4 : 0), oAMask = take(2 * ((C + 63) / 64) * 8),
            oBMask = take(3 * ((C + 63) / 64) * 8), oMMask = take(2 * ((C + 63) / 64) * 8);
     const size_t F = (size_t)nFrames;
@@ -886,6 +927,8 @@ static int ensure_slots(Lane *c, int cap, int NB, int nInst, int nFrames, int ba
     P.ray = (float *)(base + oRay); P.hitPrim = (int *)(base + oHitP); P.hitT = (float *)(base + oHitT);
     P.occ = (uint32_t *)(base + oOcc); P.qC = (uint32_t *)(base + oQC); P.qS = (uint32_t *)(base + oQS);
     P.qT = (uint32_t *)(base + oQT);
+    P.live = (uint32_t *)(base + oLive);
+    P.listMode = 0;
     P.cnt = (uint32_t *)(base + oCnt);
     P.nInst = nInst;
     P.instM = nInst ? (float4 *)(base + oInst) : nullptr;
@@ -953,6 +996,9 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
     const int nFrames = dl ? std::max(1, c->S.maxDepth) : 0;
     // the path integrator's k_shade lists the slots about to make their first MT draws (k_mt_init)
     const bool mtList = c->S.integrator != PBRTGPU_INTEGRATOR_DIRECT && c->S.integrator != PBRTGPU_INTEGRATOR_METADATA;
+    // the path and DirectLighting integrators' drain runs on the live slots' list
+    // (PBRTGPU_DRAIN_LIST=0: off, A/B)
+    const bool drainList = c->S.integrator != PBRTGPU_INTEGRATOR_METADATA && drain_list_on();
     auto kNee = c->feat ? launch_dl_nee<NB, FEAT_ALL> : launch_dl_nee<NB, 0>;
     auto kSpec = c->feat ? launch_dl_spec<NB, FEAT_ALL> : launch_dl_spec<NB, 0>;
     // DirectLighting issues up to kDlBatch light samples of a vertex per pass
@@ -967,7 +1013,10 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
     // the sampler's 3 bounces), DirectLighting maxdepth > 6 (6 per specular vertex, up to
     // 2^(maxdepth-1) - 1 of them); PBRTGPU_MT_EXT=1 forces the rows (tests)
     const bool mtExt = (dl ? c->S.maxDepth > 6 : c->S.maxDepth > 20) || mt_ext_forced();
-    struct Run { Lane *L; ItemSrc src; int cap, grid, q, batch, passes, maxPasses; bool done; };
+    // drain: the run's items are all taken; its k_shade passes take the live slots' list
+    // (PathSoA::listMode) on a grid of liveGrid blocks (live slots <= the queued rays at the last
+    // read-back, as every live slot ends a pass with a ray queued)
+    struct Run { Lane *L; ItemSrc src; int cap, grid, q, batch, passes, maxPasses; bool done, drain; int liveGrid; };
     Run R[kLanes];
     const bool serial = serial_mode();
     const int nl = (src.nItems >= 8192u && !serial) ? kLanes : 1;
@@ -990,6 +1039,9 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
         r.q = 0;
         r.batch = 0;
         r.done = false;
+        r.drain = false;
+        r.liveGrid = r.grid;
+        L.P.listMode = 0;
         // drain bound of this run: a path lives at most pathPasses passes, so every slot
         // takes a new item at least once per pathPasses passes while items remain; twice
         // that, plus the overshoot of one enqueued batch, means the wavefront is stuck
@@ -1057,6 +1109,11 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
                 continue;
             }
             if (r.passes > r.maxPasses) return fail(PBRTGPU_E_STATE, "wavefront did not drain");
+            if (drainList && L.hostCnt[CNT_NEXT] >= r.src.nItems) {
+                r.drain = true;
+                const uint64_t bound = std::min<uint64_t>((uint64_t)r.cap, (uint64_t)L.hostCnt[CNT_QC(q)] + L.hostCnt[CNT_QS(q)]);
+                r.liveGrid = (int)std::max<uint64_t>(1, (bound + kShadeBlock - 1) / kShadeBlock);
+            }
             uint2 *spillC = (uint2 *)L.spill.p, *spillS = spillC + spillLane;
             // serial mode: the shadow queries follow the closest-hit queries on the main stream
             hipStream_t s2 = serial ? L.s : L.s2;
@@ -1093,8 +1150,13 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
                     HIPCHK(hipEventRecord(e[3], L.s));
                     HIPCHK(hipEventRecord(e[4], L.s));
                     L.P.pass = (L.P.pass + 1) % 3;
-                    HIPCHK(kShade(r.grid, L.s, c->S, P, r.src, nq, Lout));
-                    if (dl) { HIPCHK(kNee(r.grid, L.s, c->S, P, nq)); HIPCHK(kSpec(r.grid, L.s, c->S, P, r.src, nq, Lout)); }
+                    HIPCHK(drain_list(L, r.drain, r.cap));
+                    HIPCHK(kShade(r.drain ? r.liveGrid : r.grid, L.s, c->S, P, r.src, nq, Lout));
+                    if (dl) {
+                        const int g = r.drain ? r.liveGrid : r.grid;
+                        HIPCHK(kNee(g, L.s, c->S, L.P, nq));
+                        HIPCHK(kSpec(g, L.s, c->S, L.P, r.src, nq, Lout));
+                    }
                     if (mtList) HIPCHK(launch_mt_init(L.s, P, nq));
                     T.launches[K_SHADE]++;
                     HIPCHK(hipEventRecord(e[5], L.s));
@@ -1135,8 +1197,13 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
                 HIPCHK(hipStreamWaitEvent(L.s, e[3], 0));
                 HIPCHK(hipEventRecord(e[4], L.s));
                 L.P.pass = (L.P.pass + 1) % 3;
-                HIPCHK(kShade(r.grid, L.s, c->S, P, r.src, nq, Lout));
-                if (dl) { HIPCHK(kNee(r.grid, L.s, c->S, P, nq)); HIPCHK(kSpec(r.grid, L.s, c->S, P, r.src, nq, Lout)); }
+                HIPCHK(drain_list(L, r.drain, r.cap));
+                HIPCHK(kShade(r.drain ? r.liveGrid : r.grid, L.s, c->S, P, r.src, nq, Lout));
+                if (dl) {
+                    const int g = r.drain ? r.liveGrid : r.grid;
+                    HIPCHK(kNee(g, L.s, c->S, L.P, nq));
+                    HIPCHK(kSpec(g, L.s, c->S, L.P, r.src, nq, Lout));
+                }
                 if (mtList) HIPCHK(launch_mt_init(L.s, P, nq));
                 T.launches[K_SHADE]++;
                 HIPCHK(hipEventRecord(e[5], L.s));

@@ -69,16 +69,25 @@ __device__ __forceinline__ uint32_t wave_scan(uint32_t x) {
 // MODE: the SurfaceIntegrator's step -- PathIntegrator (wavefront.h), DirectLightingIntegrator
 // (directlighting.h) or MetadataIntegrator (metadata.h)
 enum { MODE_PATH = 0, MODE_DL = 1, MODE_META = 2 };
-template <int NB, int FEAT, int MODE>
-__global__ __launch_bounds__(kShadeBlock) PGD_SHADE_ATTR void k_shade(DevScene S, PathSoA P, ItemSrc src, int qout,
+// LIST (path integrator): the drain's instantiation over the live slots' list (PathSoA::listMode);
+// the other one has listMode constant 0, so its compaction code is the per-wave one alone
+template <int NB, int FEAT, int MODE, bool LIST>
+__global__ __launch_bounds__(kShadeBlock) PGD_SHADE_ATTR void k_shade(DevScene S, PathSoA P0, ItemSrc src, int qout,
                                                        float *__restrict__ Lout) {
+    PathSoA P = P0;
+    P.listMode = LIST ? 1 : 0;
 #ifdef PGD_SECTIONS
     if (threadIdx.x < SEC_N) pgd_secs[threadIdx.x] = 0;
     __syncthreads();
 #endif
     if (FEAT & FEAT_MEAS) kd_lds_fill(S);   // the measured-BRDF kd-trees, once per block
-    const int slot = blockIdx.x * blockDim.x + threadIdx.x;
-    const bool inRange = slot < P.cap;
+    int slot = blockIdx.x * blockDim.x + threadIdx.x;
+    bool inRange = slot < P.cap;
+    if (LIST) {   // the drain: thread i takes the i-th live slot
+        const uint32_t i = (uint32_t)slot;
+        inRange = i < P.cnt[CNT_LIVE];
+        slot = inRange ? (int)P.live[i] : 0;
+    }
     Pushes pu = {false, false, false, 0u, 0u};
     bool freeSlot = inRange && P.item[slot] < 0;
     bool zeroed = false;
@@ -124,24 +133,6 @@ __global__ __launch_bounds__(kShadeBlock) PGD_SHADE_ATTR void k_shade(DevScene S
         pm = (uint32_t)__popcll(bM & lt); ps = (uint32_t)__popcll(bS & lt);
         tm = (uint32_t)__popcll(bM); ts = (uint32_t)__popcll(bS);
     }
-#ifdef PGD_QC_OCT
-    // path integrator: the block's continuation and MIS entries grouped by direction octant
-    // (octant-major, then wave, then lane), so a trace wave's queue range holds runs of rays
-    // that leave nearby vertices in the same octant
-    constexpr int kW = kShadeBlock / 64;
-    __shared__ uint32_t qoc[2 * 8 * kW];   // [C / M][octant][wave]: counts -> offsets in the block's C / M entries
-    uint32_t rC = 0u, rM = 0u;             // the lane's rank among its wave's entries of its octant
-    if (MODE == MODE_PATH) {
-#pragma unroll
-        for (int o = 0; o < 8; ++o) {
-            const bool ic = pu.c && pu.octC == (uint32_t)o, im = pu.m && pu.octM == (uint32_t)o;
-            const unsigned long long bo = __ballot(ic), bmo = __ballot(im);
-            if (ic) rC = (uint32_t)__popcll(bo & lt);
-            if (im) rM = (uint32_t)__popcll(bmo & lt);
-            if (lane == 0) { qoc[o * kW + wave] = (uint32_t)__popcll(bo); qoc[(8 + o) * kW + wave] = (uint32_t)__popcll(bmo); }
-        }
-    }
-#endif
     if (lane == 0) {
         qsh[4 * wave + 0] = (uint32_t)__popcll(bW); qsh[4 * wave + 1] = (uint32_t)__popcll(bC);
         qsh[4 * wave + 2] = tm; qsh[4 * wave + 3] = ts;
@@ -161,22 +152,11 @@ __global__ __launch_bounds__(kShadeBlock) PGD_SHADE_ATTR void k_shade(DevScene S
             uint32_t tt = 0u;
             for (int w = 0; w < (int)(blockDim.x >> 6); ++w) { const uint32_t v = qtw[w]; qtw[w] = tt; tt += v; }
             qtw[4] = tt ? atomicAdd(&P.cnt[CNT_QT(qout)], tt) : 0u;
-#ifdef PGD_QC_OCT
-            for (int k = 0; k < 2; ++k) {
-                uint32_t acc = 0u;
-                for (int i = 0; i < 8 * kW; ++i) { const uint32_t v = qoc[k * 8 * kW + i]; qoc[k * 8 * kW + i] = acc; acc += v; }
-            }
-#endif
         }
     }
     __syncthreads();
     uint32_t *qC = P.qC + (size_t)qout * 2 * P.rcap, *qS = P.qS + (size_t)qout * P.rcap;
     const uint32_t qcBase = qsh[18], nC = qsh[20], nReg = qsh[17];
-#ifdef PGD_QC_OCT
-    if (MODE == MODE_PATH) {
-        if (pu.c) qC[qcBase + qoc[pu.octC * kW + wave] + rC] = (uint32_t)slot << 1;
-    } else
-#endif
     if (pu.c) qC[qcBase + qsh[4 * wave + 1] + (uint32_t)__popcll(bC & lt)] = (uint32_t)slot << 1;
     if (MODE == MODE_PATH && pu.t) P.qT[(size_t)qout * P.cap + qtw[4] + qtw[wave] + (uint32_t)__popcll(bT & lt)] = (uint32_t)slot;
     if (want) {
@@ -191,9 +171,6 @@ __global__ __launch_bounds__(kShadeBlock) PGD_SHADE_ATTR void k_shade(DevScene S
         for (uint32_t m = pu.mMask; m; m &= m - 1u) qC[km++] = ((uint32_t)(slot + (__ffs(m) - 1) * P.cap) << 1) | 1u;
         for (uint32_t m = pu.sMask; m; m &= m - 1u) qS[ks++] = (uint32_t)(slot + (__ffs(m) - 1) * P.cap);
     } else {
-#ifdef PGD_QC_OCT
-        if (MODE == MODE_PATH) km = qcBase + nC + nReg + qoc[(8 + pu.octM) * kW + wave] + rM;
-#endif
         if (pu.m) qC[km] = ((uint32_t)(MODE == MODE_PATH ? pu.mIdx : slot) << 1) | 1u;
         if (pu.s) qS[ks] = (uint32_t)(MODE == MODE_PATH ? pu.sIdx : slot);
     }
@@ -208,7 +185,13 @@ template <int NB, int FEAT, int MODE>
 static hipError_t launch(int grid, hipStream_t stream, const DevScene &S, const PathSoA &P, const ItemSrc &src, int qout,
                          float *Lout) {
     const size_t lds = ((FEAT & FEAT_MEAS) && S.kdInLds) ? (size_t)S.nKd * 32 : 0;
-    hipLaunchKernelGGL((k_shade<NB, FEAT, MODE>), dim3(grid), dim3(kShadeBlock), lds, stream, S, P, src, qout, Lout);
+    if constexpr (MODE == MODE_PATH || MODE == MODE_DL) {
+        if (P.listMode) {
+            hipLaunchKernelGGL((k_shade<NB, FEAT, MODE, true>), dim3(grid), dim3(kShadeBlock), lds, stream, S, P, src, qout, Lout);
+            return hipGetLastError();
+        }
+    }
+    hipLaunchKernelGGL((k_shade<NB, FEAT, MODE, false>), dim3(grid), dim3(kShadeBlock), lds, stream, S, P, src, qout, Lout);
     return hipGetLastError();
 }
 #if SHADE_DL
@@ -233,7 +216,8 @@ static hipError_t launch(int grid, hipStream_t stream, const DevScene &S, const 
 template <int NB, int FEAT>
 __global__ __launch_bounds__(kShadeBlock) PGD_NEE_ATTR void k_dl_nee(DevScene S, PathSoA P, int qout) {
     if (FEAT & FEAT_MEAS) kd_lds_fill(S);   // measured-BRDF lookups read the LDS copy (as in k_shade)
-    const int slot = blockIdx.x * blockDim.x + threadIdx.x;
+    int slot = blockIdx.x * blockDim.x + threadIdx.x;
+    if (P.listMode) slot = (uint32_t)slot < P.cnt[CNT_LIVE] ? (int)P.live[slot] : P.cap;   // the drain (k_shade)
     Pushes pu = {false, false, false, 0u, 0u};
     if (slot < P.cap && P.item[slot] >= 0 && (P.flags[slot] & PF_DLNEE)) dl_light_batches<NB, FEAT>(S, P, slot, pu);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -259,7 +243,8 @@ template <int NB, int FEAT>
 __global__ __launch_bounds__(kShadeBlock) PGD_SPEC_ATTR void k_dl_spec(DevScene S, PathSoA P, int qout,
                                                                       float *__restrict__ Lout) {
     if (FEAT & FEAT_MEAS) kd_lds_fill(S);
-    const int slot = blockIdx.x * blockDim.x + threadIdx.x;
+    int slot = blockIdx.x * blockDim.x + threadIdx.x;
+    if (P.listMode) slot = (uint32_t)slot < P.cnt[CNT_LIVE] ? (int)P.live[slot] : P.cap;   // the drain (k_shade)
     Pushes pu = {false, false, false, 0u, 0u};
     bool done = false, zeroed = false;
     if (slot < P.cap && P.item[slot] >= 0 && (P.flags[slot] & PF_DLSPEC)) {

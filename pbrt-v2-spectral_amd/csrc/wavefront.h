@@ -70,7 +70,7 @@ enum { RAY_C = 0, RAY_M = 1, RAY_S = 2 };
 #define CNT_QC(q) (32 * (q))          // closest-hit queue size, queue set q = 0, 1
 #define CNT_QS(q) (64 + 32 * (q))     // shadow queue size
 #define CNT_QT(q) (224 + 32 * (q))    // MT-window list size (qT): k_mt_init of set q clears set q ^ 1
-enum { CNT_NEXT = 128,CNT_ZEROED = 160, CNT_WORK = 192, CNT_WORDS = 288 };
+enum { CNT_NEXT = 128, CNT_ZEROED = 160, CNT_WORK = 192, CNT_LIVE = 288, CNT_WORDS = 320 };
 enum { W_RAYS = 0, W_SHADOW = 1, W_NODES_C = 2, W_NODES_S = 3, W_TRIS_C = 4, W_TRIS_S = 5, W_QUADS_C = 6, W_QUADS_S = 7,
        W_HITS = 8, W_RAYS_M = 9, W_HITS_M = 10, W_COUNT = 12 };
 
@@ -107,6 +107,14 @@ struct PathSoA {
     uint32_t *qC;       // [2][2*rcap]: (ray slot << 1) | kind
     uint32_t *qS;       // [2][rcap]: ray slot
     uint32_t *qT;       // [2][cap]: path integrator, slots whose MT window k_mt_init computes (mt_window_init)
+    // The drain (path integrator, once the run's items are all taken): k_shade's threads take the
+    // live slots listed in `live` (k_live_list, count at CNT_LIVE) instead of slot = thread, so the
+    // last paths run in dense waves.  A wave then holds slots of many regions, and the per-wave
+    // compaction degenerates to the identity: a writer stores at region + (slot & 63) and sets the
+    // region's mask to all ones, so every reader (which ranks itself in the stored mask) finds it
+    // there, whatever mode the writing pass ran in.
+    int listMode;
+    uint32_t *live;     // [cap]
     uint32_t *cnt;     // counters (CNT_*), work counters as u64 from word CNT_WORK
     float4 *instM;      // [cap][nInst][8]: the path's instance transforms (inst_load), or null
     int nInst;
@@ -217,8 +225,16 @@ PGD_INLINE unsigned long long *beta_mask(const PathSoA &P, int buf, int slot) {
 struct WaveMasks { unsigned long long a, b, b1, b2; };   // A, B of the last pass; beta 1, 2 passes back
 PGD_INLINE WaveMasks wave_masks(const PathSoA &P, int qout, int slot) {
     const size_t W = (size_t)((P.cap + 63) >> 6);
-    const int w = __builtin_amdgcn_readfirstlane(slot >> 6);
     WaveMasks m;
+    if (P.listMode) {   // the lanes' slots lie in different regions: per-lane loads
+        const int w = slot >> 6;
+        m.a = P.aMask[(size_t)(qout ^ 1) * W + w];
+        m.b = P.mMask[(size_t)(qout ^ 1) * W + w];
+        m.b1 = P.bMask[(size_t)pass_buf(P, 1) * W + w];
+        m.b2 = P.bMask[(size_t)pass_buf(P, 2) * W + w];
+        return m;
+    }
+    const int w = __builtin_amdgcn_readfirstlane(slot >> 6);
     m.a = P.aMask[(size_t)(qout ^ 1) * W + w];
     m.b = P.mMask[(size_t)(qout ^ 1) * W + w];
     m.b1 = P.bMask[(size_t)pass_buf(P, 1) * W + w];
@@ -706,12 +722,10 @@ PGD_INLINE bool path_output(const DevScene &S, const float4 (&L)[Bands<NB>::NQ],
     return bad;
 }
 
-PGD_INLINE uint32_t ray_octant(V d) { return (d.x < 0.f ? 1u : 0u) | (d.y < 0.f ? 2u : 0u) | (d.z < 0.f ? 4u : 0u); }
 // ray requests produced by one shade step (DirectLighting batches: the MIS / shadow rays of
 // batch samples j at ray slots slot + j * cap, bit j of mMask / sMask)
 // t (path integrator): the slot's MT window goes to k_mt_init's list (mt_window_init)
-// octC / octM (path integrator): direction octant of the continuation / MIS ray (queue binning)
-struct Pushes { bool c, m, s; uint32_t mMask, sMask; int sIdx, mIdx; bool t; uint32_t octC, octM; };   // the shadow / MIS ray's ray slot (path)
+struct Pushes { bool c, m, s; uint32_t mMask, sMask; int sIdx, mIdx; bool t; };   // the shadow / MIS ray's ray slot (path)
 
 // Additions to L a vertex makes before its direct light is known, in order: emitted
 // radiance (path.cpp:67-68; bounce 0 or after a specular bounce) and the zero direct light
@@ -762,10 +776,16 @@ PGD_INLINE void estimate_direct(const DevScene &S, const PathSoA &P, int slot, i
     const bool withA = lightPdf > 0. && !emit_black<NB, FEAT>(S, em) && !(F.mode == FV_SUM && F.n == 0);
     int rsS = rs;   // the shadow ray's record: path integrator without instances, at A's compacted entry
     if (aMask) {
-        const unsigned long long m = __ballot(withA), act = __ballot(true);
-        const int lane = threadIdx.x & 63;
-        if (lane == __ffsll((long long)act) - 1) *aMask = m;
-        const int rank = __popcll(m & ((1ull << lane) - 1ull));
+        int rank;
+        if (P.listMode) {   // identity compaction (PathSoA::listMode)
+            if (withA) *aMask = ~0ull;
+            rank = slot & 63;
+        } else {
+            const unsigned long long m = __ballot(withA), act = __ballot(true);
+            const int lane = threadIdx.x & 63;
+            if (lane == __ffsll((long long)act) - 1) *aMask = m;
+            rank = __popcll(m & ((1ull << lane) - 1ull));
+        }
         A.i += (uint32_t)rank;
         if (!P.nInst) rsS = (slot & ~63) + rank;
     }
@@ -840,10 +860,16 @@ PGD_UNROLL_BANDS
             const bool withB = go && !emit_black<NB, FEAT>(S, eb);
             int rsM = rs;   // the MIS ray's record: without instances, at B's compacted entry
             if (mMask) {   // path integrator: B in the wave's compacted region (as A)
-                const unsigned long long m = __ballot(withB), act = __ballot(true);
-                const int lane = threadIdx.x & 63;
-                if (lane == __ffsll((long long)act) - 1) *mMask = m;
-                const int rank = __popcll(m & ((1ull << lane) - 1ull));
+                int rank;
+                if (P.listMode) {
+                    if (withB) *mMask = ~0ull;
+                    rank = slot & 63;
+                } else {
+                    const unsigned long long m = __ballot(withB), act = __ballot(true);
+                    const int lane = threadIdx.x & 63;
+                    if (lane == __ffsll((long long)act) - 1) *mMask = m;
+                    rank = __popcll(m & ((1ull << lane) - 1ull));
+                }
                 B.i += (uint32_t)rank;
                 if (!P.nInst) rsM = (slot & ~63) + rank;
             }
@@ -868,7 +894,6 @@ PGD_UNROLL_BANDS
                     fl |= PF_PB;
                     out.m = true;
                     out.mIdx = rsM;
-                    out.octM = ray_octant(mr.d);
                 }
             }
         }
@@ -1014,12 +1039,20 @@ PGD_INLINE Pushes shade_vertex(const DevScene &S, const PathSoA &P, int slot, in
             if (vb == S.maxDepth) cont = false;
         }
         // beta_{vb+1}: the continuing lanes take the wave region's entries in lane order
-        const unsigned long long bm = __ballot(cont), act = __ballot(true);
-        const int buf = pass_buf(P, 0), lane = threadIdx.x & 63;
-        if (lane == __ffsll((long long)act) - 1) *beta_mask(P, buf, slot) = bm;
+        const int buf = pass_buf(P, 0);
+        uint32_t bRank;
+        if (P.listMode) {   // identity compaction (PathSoA::listMode)
+            if (cont) *beta_mask(P, buf, slot) = ~0ull;
+            bRank = (uint32_t)(slot & 63);
+        } else {
+            const unsigned long long bm = __ballot(cont), act = __ballot(true);
+            const int lane = threadIdx.x & 63;
+            if (lane == __ffsll((long long)act) - 1) *beta_mask(P, buf, slot) = bm;
+            bRank = (uint32_t)__popcll(bm & ((1ull << lane) - 1ull));
+        }
         if (cont) {
             Col<float4> bn = beta_reg<NB>(P, buf, slot);
-            bn.i += (uint32_t)__popcll(bm & ((1ull << lane) - 1ull));
+            bn.i += bRank;
             bool nf = false;
 #pragma unroll
             for (int q = 0; q < NQ; ++q) {
@@ -1035,7 +1068,6 @@ PGD_INLINE Pushes shade_vertex(const DevScene &S, const PathSoA &P, int slot, in
             ray_store(P, RAY_C, slot, nray);
             fl |= PF_CONT;
             out.c = true;
-            out.octC = ray_octant(nray.d);
 #ifndef PGD_EXP_NO_MT_LIST   // A/B experiment: the window computed inline at vertex 3 instead
             out.t = vb == 2 && !(fl & PF_MTINIT);   // vertex 3 makes the path's first MT draws
 #endif

@@ -241,6 +241,10 @@ static int run(const DevScene &S, PathSoA &P, const ItemSrc &src, int nSlots, fl
         trace(q);
         const int nq = q ^ 1;
         P.pass = (P.pass + 1) % 3;
+        // the drain's list mode (pbrtgpu.hip run_wavefront: once the items are all taken): the
+        // identity compaction and per-lane mask loads of PathSoA::listMode, mixed with the passes
+        // before it; the slot order is the list's (slot order)
+        P.listMode = (MODE == MODE_PATH && next >= src.nItems && !getenv("PBRTGPU_DRAIN_LIST_OFF")) ? 1 : 0;
         shade(nq);
         q = nq;
         if (Q[q].c.empty() && Q[q].s.empty()) break;
