@@ -751,6 +751,33 @@ struct DevBuf {
     void release() { if (p) (void)hipFree(p); p = nullptr; n = 0; }
 };
 
+// Pinned host staging of the film read-back: the device-to-host copy of a step's film (C2:
+// 62.7 MB) runs at PCIe speed into it, where a pageable destination goes through the runtime's
+// bounce buffers; host threads then copy or scatter it into the caller's film (par_for)
+struct PinnedBuf {
+    void *p = nullptr;
+    size_t n = 0;
+    hipError_t ensure(size_t bytes) {
+        if (bytes <= n) return hipSuccess;
+        if (p) (void)hipHostFree(p);
+        p = nullptr; n = 0;
+        hipError_t e = hipHostMalloc(&p, bytes, hipHostMallocDefault);
+        if (e == hipSuccess) n = bytes;
+        return e;
+    }
+    void release() { if (p) (void)hipHostFree(p); p = nullptr; n = 0; }
+};
+// f(lo, hi) over [0, n) split across up to 8 host threads (chunks of at least `grain`)
+template <class F> static void par_for(size_t n, size_t grain, const F &f) {
+    const size_t hw = std::max(1u, std::thread::hardware_concurrency());
+    const size_t nt = std::max<size_t>(1, std::min<size_t>({(size_t)8, hw, n / std::max<size_t>(1, grain)}));
+    if (nt == 1) { f((size_t)0, n); return; }
+    std::vector<std::thread> th;
+    for (size_t t = 1; t < nt; ++t) th.emplace_back([&, t] { f(n * t / nt, n * (t + 1) / nt); });
+    f((size_t)0, n / nt);
+    for (auto &x : th) x.join();
+}
+
 enum { K_CLOSEST = 0, K_SHADOW = 1, K_SHADE = 2, K_ACCUM = 3, K_KINDS = 4 };
 
 struct Timing {
@@ -789,6 +816,7 @@ struct pbrtgpu_ctx {
     pbrtgpu_camera cam{};
     std::vector<DevBuf> sceneBufs;
     DevBuf film, Lbuf, pix, filmIdx, mask, keys, counter, spillL, lists[4], scratch[3], gather[2];
+    PinnedBuf stage;          // film read-back staging (pbrtgpu_film_read / _gather)
     int numCUs = 256;
     int ptBlocksPerCU = 0;    // occupancy of k_trace_pt closest (computed on first use)
     int ptBlocksPerCUS = 0;   // occupancy of k_trace_pt shadow
@@ -1281,6 +1309,7 @@ int pbrtgpu_context_destroy(pbrtgpu_ctx *c) {
                       &c->lists[0], &c->lists[1], &c->lists[2], &c->lists[3], &c->scratch[0],
                       &c->scratch[1], &c->scratch[2], &c->gather[0], &c->gather[1]};
     for (DevBuf *b : bufs) b->release();
+    c->stage.release();
     for (int i = 0; i < 8; ++i) if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
     for (Lane &L : c->lane) {
         if (L.s && L.s != c->stream) (void)hipStreamSynchronize(L.s);
@@ -1346,8 +1375,11 @@ int pbrtgpu_film_read(pbrtgpu_ctx *c, float *out, int64_t n) {
     size_t need = (size_t)c->cam.px_count * c->cam.py_count * c->nb;
     if ((size_t)n < need) return fail(PBRTGPU_E_INVALID, "film buffer too small");
     HIPCHK(hipSetDevice(c->device));
-    HIPCHK(hipMemcpyAsync(out, c->film.p, need * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c->stage.ensure(need * 4));
+    HIPCHK(hipMemcpyAsync(c->stage.p, c->film.p, need * 4, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
+    const char *src = (const char *)c->stage.p;
+    par_for(need * 4, (size_t)4 << 20, [&](size_t lo, size_t hi) { memcpy((char *)out + lo, src + lo, hi - lo); });
     return 0;
 }
 
@@ -1605,10 +1637,13 @@ int pbrtgpu_film_gather(pbrtgpu_ctx *c, int32_t tile_w, int32_t tile_h, const in
     hipLaunchKernelGGL(k_pack, dim3((n + 255) / 256), dim3(256), 0, c->stream, (const float *)c->film.p,
                        (const int *)c->gather[0].p, nPix, nb, (float *)c->gather[1].p);
     HIPCHK(hipGetLastError());
-    std::vector<float> packed((size_t)n);
-    HIPCHK(hipMemcpyAsync(packed.data(), c->gather[1].p, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c->stage.ensure((size_t)n * 4));
+    HIPCHK(hipMemcpyAsync(c->stage.p, c->gather[1].p, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
-    for (int p = 0; p < nPix; ++p) memcpy(film_out + (size_t)fidx[p] * nb, packed.data() + (size_t)p * nb, (size_t)nb * 4);
+    const float *packed = (const float *)c->stage.p;
+    par_for((size_t)nPix, (size_t)1 << 15, [&](size_t lo, size_t hi) {
+        for (size_t p = lo; p < hi; ++p) memcpy(film_out + (size_t)fidx[p] * nb, packed + p * nb, (size_t)nb * 4);
+    });
     return 0;
 }
 

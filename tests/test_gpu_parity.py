@@ -462,6 +462,34 @@ def test_independent_of_unwritten_state_and_slot_layout(pg, monkeypatch, integ, 
     assert np.all(runs[0].view(np.int32) == Lo.view(np.int32), axis=1).mean() >= 1 - 1e-4
 
 
+@pytest.mark.parametrize("integ,strategy,md", [("directlighting", "all", 6), ("path", None, 5), ("path", None, 24)])
+def test_drain_list_mode_is_exact(pg, monkeypatch, integ, strategy, md):
+    """The drain on a live-slot list (once the items are all taken, k_shade and the
+    DirectLighting kernels take the live slots of k_live_list; the per-wave compaction becomes the
+    identity) against the same runs with it off (PBRTGPU_DRAIN_LIST=0): films and per-path
+    radiance bit for bit, with slot pools small enough that most passes run in list mode (193
+    slots: many drains of a few waves) and one large pool."""
+    from conftest import PACKS
+    kw = dict(integrator=integ, strategy=strategy) if strategy else {}
+    scene = pg.Scene.load(os.path.join(PACKS, "coverage.pack"), xres=40, yres=30, spp=4, maxdepth=md, **kw)
+    keys = _keys(scene)
+    out = {}
+    with pg.Device(0) as d:
+        d.upload(scene)
+        for slots in ("193", "4096"):
+            monkeypatch.setenv("PBRTGPU_SLOTS", slots)
+            for on in ("1", "0"):
+                monkeypatch.setenv("PBRTGPU_DRAIN_LIST", on)
+                d.render()
+                out[(slots, on)] = (d.film(), d.trace_paths(keys))
+    ref = out[("4096", "0")]
+    for k, (film, paths) in out.items():
+        assert np.array_equal(film.view(np.int32), ref[0].view(np.int32)), k
+        assert np.array_equal(paths.view(np.int32), ref[1].view(np.int32)), k
+    Lo = pg.oracle().trace_paths(scene, keys)
+    assert np.all(ref[1].view(np.int32) == Lo.view(np.int32), axis=1).mean() >= 1 - 1e-4
+
+
 META = ["metadata_material_%s_48x36s4", "metadata_mesh_%s_48x36s4", "metadata_depth_%s_48x36s4",
         "killeroo_meta_mesh_%s_40x32s2", "anim_meta_mesh_%s_40x32s2", "bunny_meta_depth_%s_40x32s2"]
 

@@ -8,6 +8,8 @@ timeout -k 10 400 python3 -u -m pytest tests -m gpu -x -v --timeout 120 --timeou
 tail -1 $OUT/pytest_gpu.log
 timeout -k 10 120 python3 -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { tail -20 $OUT/smoke.log; exit 1; }
 tail -3 $OUT/smoke.log
+timeout -k 10 120 python3 tools/gather_timing.py > $OUT/gather_timing.log 2>&1 || { tail -5 $OUT/gather_timing.log; exit 1; }
+cat $OUT/gather_timing.log
 b() {   # name, bench args
   local n=$1; shift
   timeout -k 10 300 python3 bench.py "$@" > $OUT/bench_$n.json 2> $OUT/bench_$n.err || { tail -20 $OUT/bench_$n.err; exit 1; }
