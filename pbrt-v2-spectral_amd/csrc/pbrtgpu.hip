@@ -847,10 +847,20 @@ static int slot_target() {
 // of the lane's items (>= 1 M), so that a small render -- one GPU's 1/8 of a frame -- runs a few
 // slot generations rather than one long fill and drain (C2 1/8 frame: 4 M slots per lane 330,
 // 2 M 344 Mpaths/s; whole frame: 4 M 393, 2 M 384; profiles/r02q_slots.txt)
+// A lane's slot pool: every item in a slot at once, up to the slot target.  Before the drain ran
+// on the live-slot list, a lane took at most a quarter of its items in slots (at least 1 M): a
+// pool's drain then cost about a full pass per drain pass.  With the list, the whole pool wins
+// on small renders: one GPU's 1/8 of C2 395 -> 426 Mpaths/s, the full frame unchanged
+// (profiles/r03/slot_rule).  PBRTGPU_SLOT_DIV=d (experiments): at most items / d, at least 1 M.
+static uint32_t slot_div() {
+    const char *e = getenv("PBRTGPU_SLOT_DIV");
+    const long v = e ? atol(e) : 0;
+    return v > 0 ? (uint32_t)v : 1u;
+}
 static int lane_slots(uint32_t items, int nl) {
     const int t = std::max(64, slot_target() / nl);
     if (getenv("PBRTGPU_SLOTS")) return (int)std::min<uint32_t>(items, (uint32_t)t);
-    return (int)std::min<uint32_t>(items, (uint32_t)std::min(t, std::max(1 << 20, (int)(items / 4u))));
+    return (int)std::min<uint32_t>(items, (uint32_t)std::min(t, std::max(1 << 20, (int)(items / slot_div()))));
 }
 // per-sample radiance budget of one spp batch: PBRTGPU_LBUF_MB env override (tests force
 // many batches per frame with a tiny budget)
