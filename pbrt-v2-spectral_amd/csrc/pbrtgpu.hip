@@ -643,6 +643,8 @@ __global__ void k_accum(const float *__restrict__ Lbuf, const int *__restrict__ 
     int p = (int)(t / NB), b = (int)(t - (long)p * NB);
     float acc = film[(long)filmIdx[p] * NB + b];
     const float *src = Lbuf + (long)p * sb * NB + b;
+    // the sum stays in sample order; unrolled so that 16 independent loads are in flight per lane
+#pragma unroll 16
     for (int s = 0; s < sb; ++s) acc += 1.f * src[(long)s * NB];
     film[(long)filmIdx[p] * NB + b] = acc;
 }

@@ -1134,6 +1134,12 @@ PGD_INLINE Pushes shade_slot(const DevScene &S, const PathSoA &P, int slot, floa
         }
     }
     PGD_T0(OUT);
+#ifdef PGD_EXP_NO_OUT   // register-budget experiment only: the L update / output compiled out
+    *sa(P.flags, us) = fl;
+    *done = !(fl & (PF_CONT | PF_PEND));
+    *zeroed = useA && useB;
+    return out;
+#endif
     // L += beta * 0 leaves L unchanged for a finite beta (up to the sign of a zero, which
     // path_output's "+ 0.f" erases), so those additions are skipped unless beta is
     // non-finite (NaN result); L is read and written only when something changes it
