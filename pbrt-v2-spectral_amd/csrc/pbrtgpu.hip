@@ -72,7 +72,7 @@ static int fail(int code, const std::string &msg) { g_err = msg; return code; }
 
 // ------------------------------------------------------------------ kernels
 #ifndef PGD_PASS_BATCH   // wavefront passes enqueued per counter read-back (<= 8)
-#define PGD_PASS_BATCH 4
+#define PGD_PASS_BATCH 8
 #endif
 static_assert(PGD_PASS_BATCH >= 1 && PGD_PASS_BATCH <= 8, "Lane::ev holds the events of at most 8 passes");
 #ifndef PGD_LBUF_GIB   // default per-sample radiance buffer of one spp batch (GiB); PBRTGPU_LBUF_MB overrides
@@ -800,6 +800,7 @@ struct Lane {
     hipStream_t s = nullptr, s2 = nullptr;
     hipEvent_t ev[2 + 6 * 8] = {};
     uint32_t *hostCnt = nullptr;   // pinned mirror of the queue counters
+    hipEvent_t done = nullptr;     // recorded after each batch's counter read-back (polled)
 };
 #ifndef PGD_LANES
 #define PGD_LANES 2
@@ -1110,16 +1111,31 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
         HIPCHK(kShade(r.grid, L.s, c->S, L.P, r.src, 0, Lout));
         HIPCHK(hipEventRecord(L.ev[1], L.s));
         HIPCHK(hipMemcpyAsync(L.hostCnt, L.P.cnt, CNT_WORDS * 4, hipMemcpyDeviceToHost, L.s));
+        HIPCHK(hipEventRecord(L.done, L.s));
     }
     int live = nl;
     float m;
+    int rr = 0;   // round-robin start of the lane poll
     while (live > 0) {
-        for (int l = 0; l < nl; ++l) {
+        // the next lane whose batch has completed: the host never blocks on one lane while the
+        // other lane's queue has run dry (it would idle until that wait ended)
+        int l = -1;
+        for (;;) {
+            for (int k = 0; k < nl && l < 0; ++k) {
+                const int i = (rr + k) % nl;
+                if (R[i].done) continue;
+                const hipError_t qe = hipEventQuery(R[i].L->done);
+                if (qe == hipSuccess) l = i;
+                else if (qe != hipErrorNotReady) HIPCHK(qe);
+            }
+            if (l >= 0) break;
+            std::this_thread::yield();
+        }
+        rr = l + 1;
+        {
             Run &r = R[l];
-            if (r.done) continue;
             Lane &L = *r.L;
             const PathSoA &P = L.P;
-            HIPCHK(hipStreamSynchronize(L.s));
             if (r.batch == 0) {
                 HIPCHK(hipEventElapsedTime(&m, L.ev[0], L.ev[1])); T.ms[K_SHADE] += m;
                 T.launches[K_SHADE]++;
@@ -1253,6 +1269,7 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
             }
             r.q = q;
             HIPCHK(hipMemcpyAsync(L.hostCnt, P.cnt, CNT_WORDS * 4, hipMemcpyDeviceToHost, L.s));
+            HIPCHK(hipEventRecord(L.done, L.s));
         }
     }
     if (c->S.specMode == 1) {   // the rows' luminance guard once every band of them is in
@@ -1302,6 +1319,7 @@ int pbrtgpu_context_create(int device, pbrtgpu_ctx **out) {
         else ok = hipStreamCreateWithFlags(&L.s, hipStreamNonBlocking) == hipSuccess;
         ok = ok && hipStreamCreateWithFlags(&L.s2, hipStreamNonBlocking) == hipSuccess;
         for (int i = 0; i < 2 + 6 * 8 && ok; ++i) ok = hipEventCreate(&L.ev[i]) == hipSuccess;
+        ok = ok && hipEventCreateWithFlags(&L.done, hipEventDisableTiming) == hipSuccess;
         ok = ok && hipHostMalloc((void **)&L.hostCnt, CNT_WORDS * 4, hipHostMallocDefault) == hipSuccess;
     }
     if (!ok) {
@@ -1329,6 +1347,7 @@ int pbrtgpu_context_destroy(pbrtgpu_ctx *c) {
         L.slots.release();
         L.spill.release();
         for (hipEvent_t e : L.ev) if (e) (void)hipEventDestroy(e);
+        if (L.done) (void)hipEventDestroy(L.done);
         if (L.s2) (void)hipStreamDestroy(L.s2);
         if (L.s && L.s != c->stream) (void)hipStreamDestroy(L.s);
         if (L.hostCnt) (void)hipHostFree(L.hostCnt);
