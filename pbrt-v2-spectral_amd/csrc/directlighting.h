@@ -184,8 +184,15 @@ PGD_INLINE void dl_light_batches(const DevScene &S, const PathSoA &P, int slot, 
     const int K = all ? S.dlK : 1;
     const uint32_t hp = P.hp[slot], s = P.smp[slot];
     int k = (int)P.dlk[slot];
-    DLVertex vx;
-    dl_vertex<NB, FEAT>(S, P, slot, d, vx);
+    BSDF bs;
+    V vp, vn, vwo;
+    float vEps, vTime;
+    {   // the vertex (its record is filled through out-of-line calls, so it lives in scratch
+        // memory); the light samples read register copies of the fields they use
+        DLVertex vx;
+        dl_vertex<NB, FEAT>(S, P, slot, d, vx);
+        bs = vx.bs; vp = vx.p; vn = vx.n; vwo = vx.wo; vEps = vx.is.rayEps; vTime = vx.ray.time;
+    }
     for (;;) {
         const int kEnd = min(k + P.dlBatch, K);
         uint32_t mA = 0u, mB = 0u;
@@ -200,8 +207,8 @@ PGD_INLINE void dl_light_batches(const DevScene &S, const PathSoA &P, int slot, 
             uint32_t f2 = 0u;
             Pushes o2 = {false, false, false, 0u, 0u};
             estimate_direct<NB, FEAT>(S, P, slot, slot + jb * (int)c, Col<float4>{P.A, (uint32_t)(jb * NQ * c + slot)},
-                                      Col<float4>{P.B, (uint32_t)(jb * NQ * c + slot)}, ln, vx.bs, pm, vx.p, vx.n, vx.wo,
-                                      vx.is.rayEps, vx.ray.time, ul, ub, F, f2, o2, nullptr, nullptr);
+                                      Col<float4>{P.B, (uint32_t)(jb * NQ * c + slot)}, ln, bs, pm, vp, vn, vwo,
+                                      vEps, vTime, ul, ub, F, f2, o2, nullptr, nullptr);
             if (f2 & PF_PA) mA |= 1u << jb;
             if (f2 & PF_PB) mB |= 1u << jb;
             lnOne = ln;
