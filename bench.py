@@ -397,7 +397,9 @@ def main():
     frame_paths = paths / args.steps    # this rank's share of a frame
     roof = None
     if rank == 0 and not args.no_roofline:
-        cfg = args.config + ("" if args.integrator == "path" else "_dl") + ("" if args.renderer == "sampler" else "_spec")
+        # the profiles/hbm_traffic.json key of this workload (PMC traffic is per integrator / renderer)
+        integ_key = {"path": "", "directlighting": "_dl", "metadata": "_meta"}[args.integrator]
+        cfg = args.config + integ_key + ("" if args.renderer == "sampler" else "_spec")
         roof = exclusive_roofline(dev, scene, tiles, tile, frame_paths, cfg, pps)
 
     slices = None

@@ -820,6 +820,20 @@ struct pbrtgpu_ctx {
     std::vector<DevBuf> sceneBufs;
     DevBuf film, Lbuf, pix, filmIdx, mask, keys, counter, spillL, lists[4], scratch[3], gather[2];
     PinnedBuf stage;          // film read-back staging (pbrtgpu_film_read / _gather)
+    // render_impl's per-call setup of the last call -- its pixel lists (on the device: pix,
+    // filmIdx, mask), its exact-boundary samples (keys, sorted) and their contribution lists --
+    // reused by a call with the same tiles, sample range and scene (repeated frames of one tile
+    // set: the timed steps of a rank)
+    struct CallSetup {
+        bool valid = false;
+        uint64_t gen = 0;
+        int tw = 0, th = 0, s0 = 0, s1 = 0, nPix = 0, nSpill = 0;
+        bool all = false;
+        std::vector<int32_t> tiles;
+        double spills = 0;
+        std::vector<int> preT, preStart, preSrc, postT, postStart, postSrc;
+    } setup;
+    uint64_t sceneGen = 0;    // bumped by every scene upload (invalidates `setup`)
     int numCUs = 256;
     int ptBlocksPerCU = 0;    // occupancy of k_trace_pt closest (computed on first use)
     int ptBlocksPerCUS = 0;   // occupancy of k_trace_pt shadow
@@ -1173,7 +1187,12 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
             uint2 *spillC = (uint2 *)L.spill.p, *spillS = spillC + spillLane;
             // serial mode: the shadow queries follow the closest-hit queries on the main stream
             hipStream_t s2 = serial ? L.s : L.s2;
-            r.batch = kPassBatch;
+            // passes per read-back: kPassBatch while the lane has items for more than one more
+            // pool, then fewer, so that the switch to the drain's list mode and the lane's end
+            // are seen within a few passes (2 in the drain, 4 before it)
+            r.batch = r.drain ? std::min(2, kPassBatch)
+                              : (uint64_t)L.hostCnt[CNT_NEXT] + (uint64_t)r.cap >= r.src.nItems ? std::min(4, kPassBatch)
+                                                                                              : kPassBatch;
             for (int j = 0; j < r.batch; ++j) {
                 hipEvent_t *e = L.ev + 2 + 6 * j;
                 const int nq = q ^ 1;
@@ -1358,6 +1377,8 @@ int pbrtgpu_context_destroy(pbrtgpu_ctx *c) {
 }
 int pbrtgpu_scene_upload(pbrtgpu_ctx *c, const pbrtgpu_flat_scene *s) {
     if (!c || !s) return fail(PBRTGPU_E_INVALID, "null argument");
+    c->sceneGen++;               // the cached render setup belongs to the previous scene
+    c->setup.valid = false;
     std::string err;
     if (int e = scene_check(s, &err)) return fail(e, err);
     HIPCHK(hipSetDevice(c->device));
@@ -1455,31 +1476,46 @@ static int render_impl(pbrtgpu_ctx *c, const pbrtgpu_render_desc *d, const int32
     if (s0 < 0 || s1 > spp || s0 >= s1) return fail(PBRTGPU_E_INVALID, "bad sample range");
     const bool countWork = (d->flags & PBRTGPU_F_COUNT_WORK) != 0;
     Timing T;
-    // pixel list of the requested tiles (film pixels; own sample pixel == film pixel)
-    std::vector<int> fidx;
-    std::vector<uint8_t> mask;
-    if (int e = tile_pixels(cam, d->tile_w, d->tile_h, tiles, ntiles, &fidx, &mask)) return e;
-    std::vector<int2> pix(fidx.size());
-    for (size_t i = 0; i < fidx.size(); ++i)
-        pix[i] = make_int2(cam.px_start + fidx[i] % cam.px_count, cam.py_start + fidx[i] / cam.px_count);
-    const int nPix = (int)pix.size();
     double st[PBRTGPU_STAT_COUNT] = {0};
     if (!(d->flags & PBRTGPU_F_ACCUMULATE) && s0 == 0)
         HIPCHK(hipMemsetAsync(c->film.p, 0, (size_t)cam.px_count * cam.py_count * NB * 4, c->stream));
+    pbrtgpu_ctx::CallSetup &cs = c->setup;
+    const bool same = cs.valid && cs.gen == c->sceneGen && cs.tw == d->tile_w && cs.th == d->tile_h && cs.s0 == s0 &&
+                      cs.s1 == s1 && (tiles ? (!cs.all && cs.tiles.size() == (size_t)std::max(0, ntiles) &&
+                                               std::equal(cs.tiles.begin(), cs.tiles.end(), tiles))
+                                            : cs.all);
+    std::vector<int> fidx;
+    std::vector<uint8_t> mask;
+    if (!same) {
+        cs.valid = false;
+        // pixel list of the requested tiles (film pixels; own sample pixel == film pixel)
+        if (int e = tile_pixels(cam, d->tile_w, d->tile_h, tiles, ntiles, &fidx, &mask)) return e;
+        std::vector<int2> pix(fidx.size());
+        for (size_t i = 0; i < fidx.size(); ++i)
+            pix[i] = make_int2(cam.px_start + fidx[i] % cam.px_count, cam.py_start + fidx[i] / cam.px_count);
+        cs.nPix = (int)pix.size();
+        if (cs.nPix > 0) {
+            HIPCHK(c->pix.ensure(pix.size() * sizeof(int2)));
+            HIPCHK(c->filmIdx.ensure(fidx.size() * sizeof(int)));
+            HIPCHK(hipMemcpyAsync(c->pix.p, pix.data(), pix.size() * sizeof(int2), hipMemcpyHostToDevice, c->stream));
+            HIPCHK(hipMemcpyAsync(c->filmIdx.p, fidx.data(), fidx.size() * sizeof(int), hipMemcpyHostToDevice, c->stream));
+            HIPCHK(hipStreamSynchronize(c->stream));   // the host vectors go out of scope
+        }
+    }
+    const int nPix = cs.nPix;
     if (nPix == 0) { if (stats) memcpy(stats, st, sizeof(st)); c->last = T; return 0; }
-    HIPCHK(c->pix.ensure(pix.size() * sizeof(int2)));
-    HIPCHK(c->filmIdx.ensure(fidx.size() * sizeof(int)));
-    HIPCHK(hipMemcpyAsync(c->pix.p, pix.data(), pix.size() * sizeof(int2), hipMemcpyHostToDevice, c->stream));
-    HIPCHK(hipMemcpyAsync(c->filmIdx.p, fidx.data(), fidx.size() * sizeof(int), hipMemcpyHostToDevice, c->stream));
     unsigned int zeroed = 0;
 
     // ---- spill samples of the call's sample range [s0, s1).  A frame rendered as one call
     // adds every pixel's contributions in the reference's order; a frame split into sample
     // ranges (F_ACCUMULATE) adds the same contributions, range by range, so its sums differ
     // from the one-call film only in float summation order
-    std::vector<int> preT, preStart, preSrc, postT, postStart, postSrc;
-    int nSpill = 0;
-    {
+    std::vector<int> &preT = cs.preT, &preStart = cs.preStart, &preSrc = cs.preSrc, &postT = cs.postT,
+                     &postStart = cs.postStart, &postSrc = cs.postSrc;
+    if (!same) {
+        preT.clear(); preStart.clear(); preSrc.clear(); postT.clear(); postStart.clear(); postSrc.clear();
+        cs.nSpill = 0;
+        cs.spills = 0;
         HIPCHK(c->mask.ensure(mask.size()));
         HIPCHK(hipMemcpyAsync(c->mask.p, mask.data(), mask.size(), hipMemcpyHostToDevice, c->stream));
         unsigned int cap = 1u << 20;
@@ -1495,7 +1531,8 @@ static int render_impl(pbrtgpu_ctx *c, const pbrtgpu_render_desc *d, const int32
         HIPCHK(hipMemcpyAsync(&cnt, c->counter.p, 4, hipMemcpyDeviceToHost, c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
         if (cnt > cap) return fail(PBRTGPU_E_UNSUPPORTED, "too many exact-boundary samples");
-        nSpill = (int)cnt;
+        const int nSpill = (int)cnt;
+        cs.nSpill = nSpill;
         if (nSpill > 0) {
             std::vector<int3> keys(nSpill);
             HIPCHK(hipMemcpy(keys.data(), c->keys.p, nSpill * sizeof(int3), hipMemcpyDeviceToHost));
@@ -1549,9 +1586,17 @@ static int render_impl(pbrtgpu_ctx *c, const pbrtgpu_render_desc *d, const int32
             }
             preStart.push_back((int)preSrc.size());
             postStart.push_back((int)postSrc.size());
-            st[PBRTGPU_STAT_SPILLS] = (double)cbs.size();
+            cs.spills = (double)cbs.size();
         }
+        cs.valid = true;
+        cs.gen = c->sceneGen;
+        cs.tw = d->tile_w; cs.th = d->tile_h; cs.s0 = s0; cs.s1 = s1;
+        cs.all = tiles == nullptr;
+        if (tiles) cs.tiles.assign(tiles, tiles + std::max(0, ntiles));
+        else cs.tiles.clear();
     }
+    const int nSpill = cs.nSpill;
+    st[PBRTGPU_STAT_SPILLS] = cs.spills;
     auto applyLists = [&](std::vector<int> &Tg, std::vector<int> &ST, std::vector<int> &SR) -> int {
         if (Tg.empty()) return 0;
         HIPCHK(c->lists[0].ensure(Tg.size() * 4));

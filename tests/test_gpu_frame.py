@@ -52,6 +52,42 @@ def test_tile_grid_is_film_pixels(pg, k64, full):
         assert _same(d.film(), full[0])
 
 
+def test_repeated_calls_reuse_the_setup(pg, k64, full):
+    """A context keeps its last render call's setup (pixel lists, exact-boundary samples and their
+    contribution lists) for a call with the same tiles, sample range and scene.
+    Alternating tile sets, sample ranges and a scene re-upload must give the films of fresh
+    contexts, spills included."""
+    ref, st_full = full
+    ntx, nty = pg.tile_grid(k64)
+    a, b = np.arange(0, ntx * nty, 2), np.arange(1, ntx * nty, 2)
+    fresh = {}
+    for name, tiles in (("a", a), ("b", b)):
+        with pg.Device(0) as d:
+            d.upload(k64)
+            d.render(tiles=tiles)
+            fresh[name] = d.film()
+    with pg.Device(0) as d:
+        d.upload(k64)
+        for name, tiles in (("a", a), ("a", a), ("b", b), ("a", a)):
+            st = d.render(tiles=tiles)
+            assert _same(d.film(), fresh[name]), name
+        for _ in range(2):
+            st = d.render()
+            assert _same(d.film(), ref)
+            assert st[pg.STAT_SPILLS] == st_full[pg.STAT_SPILLS] > 0
+        d.render(spp_begin=0, spp_end=3)
+        d.render(spp_begin=0, spp_end=8)
+        assert _same(d.film(), ref)
+        small = pg.Scene.load(os.path.join(PACKS, "killeroo-simple.pack"), xres=128, yres=64, spp=4)
+        d.upload(small)            # a new scene: same tiles and range, other samples
+        d.render()
+        f4 = d.film()
+    with pg.Device(0) as d:
+        d.upload(small)
+        d.render()
+        assert _same(d.film(), f4)
+
+
 def test_many_spp_batches_and_runs(pg, k64, full, monkeypatch):
     """128x64 px x 32 bands x 4 B = 1 MiB per sample: a 1 MiB budget gives 8 batches of one
     sample; 300 slots give ~27 regenerations per slot per batch."""
