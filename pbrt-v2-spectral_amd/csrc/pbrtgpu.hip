@@ -858,26 +858,30 @@ template <class T> static hipError_t upload(pbrtgpu_ctx *c, const T *src, size_t
 static int slot_target() {
     const char *e = getenv("PBRTGPU_SLOTS");
     int v = e ? atoi(e) : 0;
-    return v > 0 ? v : (1 << 23);   // 8 M slots = 2 lanes x 4 M (C2 r01p: 289 -> 301 Mpaths/s vs 2 x 2 M)
+    // 16 M slots = 2 lanes x 8 M (C2 456-461 -> 467-468 Mpaths/s vs 2 x 4 M, C4 230 -> 233;
+    // profiles/r03/slot_rule/target16m.txt); a lane's arrays stay below 4 GiB (max_slots_32bit:
+    // 60 bands cap a lane at ~6 M)
+    return v > 0 ? v : (1 << 24);
 }
-// slots of a lane running `items` paths: the target, but without the override at most a quarter
-// of the lane's items (>= 1 M), so that a small render -- one GPU's 1/8 of a frame -- runs a few
-// slot generations rather than one long fill and drain (C2 1/8 frame: 4 M slots per lane 330,
-// 2 M 344 Mpaths/s; whole frame: 4 M 393, 2 M 384; profiles/r02q_slots.txt)
-// A lane's slot pool: every item in a slot at once, up to the slot target.  Before the drain ran
-// on the live-slot list, a lane took at most a quarter of its items in slots (at least 1 M): a
-// pool's drain then cost about a full pass per drain pass.  With the list, the whole pool wins
-// on small renders: one GPU's 1/8 of C2 395 -> 426 Mpaths/s, the full frame unchanged
-// (profiles/r03/slot_rule).  PBRTGPU_SLOT_DIV=d (experiments): at most items / d, at least 1 M.
+// A lane's slot pool: the slot target when the lane has more items than that (two or more slot
+// generations), else half of its items (at least 1 M), so a small render still runs two
+// generations.  Round 2 took a quarter of the items: a pool's drain then cost about a full pass
+// per drain pass.  With the drain on the live-slot list, larger pools win down to two
+// generations (one GPU, min of 3 renders, profiles/r03/slot_rule/rules.txt): C2's 1/8
+// (7.9 M items per lane) 395 (quarter) -> 429 Mpaths/s at 4 M slots, 402 with all its items in
+// slots; its 1/4 (15.9 M) 455 at the 8.4 M target, 394 at exactly half its items (7.9 M: same
+// passes, k_shade 25 % slower, reproducibly -- not understood), 427 at 4 M.
+// PBRTGPU_SLOT_DIV=d (experiments): items / d when the lane has at most the target.
 static uint32_t slot_div() {
     const char *e = getenv("PBRTGPU_SLOT_DIV");
     const long v = e ? atol(e) : 0;
-    return v > 0 ? (uint32_t)v : 1u;
+    return v > 0 ? (uint32_t)v : 2u;
 }
 static int lane_slots(uint32_t items, int nl) {
     const int t = std::max(64, slot_target() / nl);
     if (getenv("PBRTGPU_SLOTS")) return (int)std::min<uint32_t>(items, (uint32_t)t);
-    return (int)std::min<uint32_t>(items, (uint32_t)std::min(t, std::max(1 << 20, (int)(items / slot_div()))));
+    const uint32_t want = items > (uint32_t)t ? (uint32_t)t : std::max<uint32_t>(1u << 20, items / slot_div());
+    return (int)std::min<uint32_t>(items, want);
 }
 // per-sample radiance budget of one spp batch: PBRTGPU_LBUF_MB env override (tests force
 // many batches per frame with a tiny budget)
