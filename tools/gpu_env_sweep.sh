@@ -8,5 +8,5 @@ i=0
 for s in "$@"; do
   i=$((i+1))
   env $s timeout -k 10 200 python3 bench.py --steps 2 --warmup 1 --no-cpu > $OUT/env$i.json
-  python3 -c "import json; d=json.load(open('$OUT/env$i.json')); print('$s', d['value'], d['roofline']['kernel_ms_per_step'])"
+  python3 -c "import json; d=json.load(open('$OUT/env$i.json')); print('$s', d['value'], d['ms_per_step'], {k: v['ms_per_frame'] for k, v in d['roofline']['kernels'].items()})"
 done
