@@ -375,6 +375,14 @@ int pbrtgpu_intersect(pbrtgpu_ctx *ctx, const float *rays, int32_t n, float *hit
  * the full 624-word state rebuilt at output 227 and twisted every 624 after it (device.h
  * mt_uint_ext).  out [n] uint32.  Needs no scene. */
 int pbrtgpu_mt_sequence(pbrtgpu_ctx *ctx, uint32_t seed, int32_t n, uint32_t *out);
+/* Parity hook for the float transcendentals (include/pbrt_libmf.h, the reference's glibc routines
+ * restated): out[i] = f(x[i]) -- or f(x[i], y[i]) for powf / atan2f -- evaluated by
+ * the same device functions the shading kernels call.  fn: PBRTGPU_LIBMF_*; sincosf writes
+ * (sin, cos) pairs (out [2n]).  Needs no scene. */
+enum { PBRTGPU_LIBMF_SINF = 0, PBRTGPU_LIBMF_COSF, PBRTGPU_LIBMF_SINCOSF, PBRTGPU_LIBMF_EXPF, PBRTGPU_LIBMF_LOGF,
+       PBRTGPU_LIBMF_ACOSF, PBRTGPU_LIBMF_ATANF, PBRTGPU_LIBMF_TANF, PBRTGPU_LIBMF_POWF, PBRTGPU_LIBMF_ATAN2F,
+       PBRTGPU_LIBMF_COUNT };
+int pbrtgpu_libmf_eval(pbrtgpu_ctx *ctx, int32_t fn, int64_t n, const float *x, const float *y, float *out);
 /* GPU BVH build (the host front end's SAH build restates
  * accelerators/bvh.cpp:145-351 node for node and stays the default, since the bit-exact
  * traversal order rests on it).  A linear BVH (Morton codes, radix sort, Karras radix tree,

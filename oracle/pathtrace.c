@@ -4,12 +4,13 @@
  * library, and only as the checker / CPU baseline.  The product (libpbrtgpu.so) never
  * links or calls it.
  *
- * Parity pinning: compiled with -DORACLE_LIBM_FLOAT (glibc float transcendentals, as the
- * reference build) it reproduces the reference harness (oracle/_ref, which runs the
- * reference's own PathIntegrator/BVH/BSDF/light/camera code) bit for bit; compiled
- * without it, sinf/cosf/powf/expf/acosf/atan2f/tanf/atanf are the double-precision
- * algorithms of include/pbrt_fmath.h rounded once to float (the definition the HIP
- * kernels implement, from the same header), see DESIGN.md §3.2.
+ * Parity pinning: compiled with -DORACLE_LIBM_FLOAT (calls into glibc's float transcendentals,
+ * as the reference build does) it reproduces the reference harness (oracle/_ref, which runs
+ * the reference's own PathIntegrator/BVH/BSDF/light/camera code) bit for bit; compiled
+ * without it, sinf/cosf/powf/expf/logf/acosf/atan2f/tanf/atanf are include/pbrt_libmf.h, the
+ * restatement of those glibc routines the HIP kernels compile from the same header (pinned to
+ * the system libm over every float input by tools/libmf_check.c), see DESIGN.md §3.2.  The
+ * lens camera's double-precision diffraction terms use include/pbrt_fmath.h in that build.
  *
  * It consumes the flattened scene of include/pbrtgpu.h and follows, function by function:
  *   samplerrenderer.cpp:60-164,225-247  render loop, NaN/inf guard, SamplerRenderer::Li
@@ -58,15 +59,16 @@
 #define DATAN atan
 #define DLOG log
 #else
-/* the parity definition shared with the GPU: include/pbrt_fmath.h */
-static inline float SINF(float x) { return (float)pbrt_fm_sin((double)x); }
-static inline float COSF(float x) { return (float)pbrt_fm_cos((double)x); }
-static inline float POWF(float x, float y) { return (float)pbrt_fm_pow((double)x, (double)y); }
-static inline float EXPF(float x) { return (float)pbrt_fm_exp((double)x); }
-static inline float ACOSF(float x) { return (float)pbrt_fm_acos((double)x); }
-static inline float ATAN2F(float y, float x) { return (float)pbrt_fm_atan2((double)y, (double)x); }
-static inline float TANF(float x) { return (float)pbrt_fm_tan((double)x); }
-static inline float ATANF(float x) { return (float)pbrt_fm_atan((double)x); }
+/* the definition shared with the GPU: glibc's float routines restated, include/pbrt_libmf.h */
+#include "pbrt_libmf.h"
+static inline float SINF(float x) { return libmf_sinf(x); }
+static inline float COSF(float x) { return libmf_cosf(x); }
+static inline float POWF(float x, float y) { return libmf_powf(x, y); }
+static inline float EXPF(float x) { return libmf_expf(x); }
+static inline float ACOSF(float x) { return libmf_acosf(x); }
+static inline float ATAN2F(float y, float x) { return libmf_atan2f(y, x); }
+static inline float TANF(float x) { return libmf_tanf(x); }
+static inline float ATANF(float x) { return libmf_atanf(x); }
 #define DSIN pbrt_fm_sin
 #define DCOS pbrt_fm_cos
 #define DACOS pbrt_fm_acos
@@ -1149,7 +1151,7 @@ static void bsdf_sample_f(const Ctx *c, const BSDF *bs, V woW, V *wiW, float u0,
 #ifdef ORACLE_LIBM_FLOAT
 #define LOGF logf
 #else
-static inline float LOGF(float x) { return (float)pbrt_fm_log_any((double)x); }
+static inline float LOGF(float x) { return libmf_logf(x); }
 #endif
 /* Log2 (pbrt.h:243-246) */
 static inline float log2_(float x) { float invLog2 = 1.f / LOGF(2.f); return LOGF(x) * invLog2; }
@@ -2283,9 +2285,14 @@ static int sampler_sample(const Ctx *c, int px, int py, uint32_t s, float *L, fl
     return bad;
 }
 
+/* sampledLambdaStart / End (ints): 395 / 715 in the 32- and 60-band builds (spectrum.h:41-42),
+ * 400 / 700 in the upstream 30-band one (spectrum.h.original:36-38) */
+static inline int lambda_start(int N) { return N == 30 ? 400 : 395; }
+static inline int lambda_end(int N) { return N == 30 ? 700 : 715; }
+
 /* SpectralRenderer: one camera sample of SpectralRendererTask::Run (spectralrenderer.cpp:
- * 98-190).  sampledLambdaStart / End are the ints 395 / 715 (spectrum.h:41-42), so
- * deltaWave = float(320 / nWaveBands) and GetValueAtWavelength's step float(320 / N).
+ * 98-190).  sampledLambdaStart / End are ints, so deltaWave = float((end - start) / nWaveBands)
+ * and GetValueAtWavelength's step float((end - start) / N).
  * singleDirection: band b = 0 .. nWaveBands-1 traces the sample's camera path with
  * RNG(path_seed(hp, s nWaveBands + b)); samplerDirection: band s % nWaveBands only, with
  * RNG(path_seed(hp, s)).  A band's radiance: NaN -> 0; the luminance guard on the sample's
@@ -2296,14 +2303,14 @@ static int spectral_sample(const Ctx *c, int px, int py, uint32_t s, float *L, f
     const int N = c->nb, nWB = c->s->wave_bands;
     const int single = c->s->spectral_sampling == PBRTGPU_SPECTRAL_SINGLE;
     const int mm = single ? nWB : 1;
-    const int dI = (int)round(N / nWB);
-    const float dW = (float)((715 - 395) / nWB), step = (float)((715 - 395) / N);
+    const int dI = (int)round(N / nWB), l0 = lambda_start(N), l1 = lambda_end(N);
+    const float dW = (float)((l1 - l0) / nWB), step = (float)((l1 - l0) / N);
     int bad = 0;
     for (int i = 0; i < N; ++i) L[i] = 0.f;
     for (int sb = 0; sb < mm; ++sb) {
         const int b = single ? sb : (int)(s % (uint32_t)nWB);
         float Lr[MAXB];
-        const float wl = 395 + dW * b + (dW / 2);
+        const float wl = l0 + dW * b + (dW / 2);
         camera_path(c, px, py, s, single ? s * (uint32_t)nWB + (uint32_t)b : s, wl, Lr, imgX, imgY);
         int nan = 0;
         for (int i = 0; i < N; ++i) if (isnan(Lr[i])) nan = 1;
@@ -2318,7 +2325,7 @@ static int spectral_sample(const Ctx *c, int px, int py, uint32_t s, float *L, f
         if (hi <= lo) continue;
         float v = 0.f;
         for (int i = 0; i < N; ++i) {
-            const float w0 = 395 + i * step, w1 = 395 + (i + 1) * step;
+            const float w0 = l0 + i * step, w1 = l0 + (i + 1) * step;
             if (wl >= w0 && wl < w1) {
                 if (i + 1 >= N) abort();   /* c[N]: rejected by oracle_spectral_ok */
                 v = lerpf((wl - w0) / (w1 - w0), Lr[i], Lr[i + 1]);
@@ -2336,13 +2343,13 @@ static int spectral_ok(const pbrtgpu_flat_scene *s) {
     if (s->renderer != PBRTGPU_RENDERER_SPECTRAL) return 1;
     const int N = s->n_bands, nWB = s->wave_bands;
     if (nWB < 1) return 0;
-    const int dI = (int)round(N / nWB);
-    const float dW = (float)((715 - 395) / nWB), step = (float)((715 - 395) / N);
+    const int dI = (int)round(N / nWB), l0 = lambda_start(N), l1 = lambda_end(N);
+    const float dW = (float)((l1 - l0) / nWB), step = (float)((l1 - l0) / N);
     for (int b = 0; b < nWB; ++b) {
         const int lo = dI * b, hi = (dI * (b + 1) < N - 1) ? dI * (b + 1) : N - 1;
         if (hi <= lo) continue;
-        const float wl = 395 + dW * b + (dW / 2);
-        if (wl >= 395 + (N - 1) * step) return 0;
+        const float wl = l0 + dW * b + (dW / 2);
+        if (wl >= l0 + (N - 1) * step) return 0;
     }
     return 1;
 }
@@ -2622,5 +2629,28 @@ int oracle_measured_f(const pbrtgpu_flat_scene *s, int mat, const float *wo, con
     b.kd = s->kdnodes + mt->aux;
     b.nkd = mt->aux2;
     irreg_f(&c, &b, v3(wo[0], wo[1], wo[2]), v3(wi[0], wi[1], wi[2]), out);
+    return 0;
+}
+
+/* test hook: the float transcendentals of this build (fn: PBRTGPU_LIBMF_*; powf / atan2f take
+ * y; sincosf writes (sin, cos) pairs) -- glibc's own in liboracle_libm.so, include/pbrt_libmf.h
+ * in liboracle.so; tests/test_libmf.py compares the GPU's with both */
+int oracle_libmf_eval(int fn, int64_t n, const float *x, const float *y, float *out) {
+    for (int64_t i = 0; i < n; ++i) {
+        const float a = x[i];
+        switch (fn) {
+        case PBRTGPU_LIBMF_SINF: out[i] = SINF(a); break;
+        case PBRTGPU_LIBMF_COSF: out[i] = COSF(a); break;
+        case PBRTGPU_LIBMF_SINCOSF: out[2 * i] = SINF(a); out[2 * i + 1] = COSF(a); break;
+        case PBRTGPU_LIBMF_EXPF: out[i] = EXPF(a); break;
+        case PBRTGPU_LIBMF_LOGF: out[i] = LOGF(a); break;
+        case PBRTGPU_LIBMF_ACOSF: out[i] = ACOSF(a); break;
+        case PBRTGPU_LIBMF_ATANF: out[i] = ATANF(a); break;
+        case PBRTGPU_LIBMF_TANF: out[i] = TANF(a); break;
+        case PBRTGPU_LIBMF_POWF: out[i] = POWF(a, y[i]); break;
+        case PBRTGPU_LIBMF_ATAN2F: out[i] = ATAN2F(a, y[i]); break;
+        default: return -1;
+        }
+    }
     return 0;
 }

@@ -2,8 +2,8 @@
 //
 // Every function restates the reference arithmetic exactly (same operand order, float vs
 // double promotion, correctly-rounded div/sqrt, no FMA contraction: build with
-// -ffp-contract=off).  Transcendentals are evaluated in double and rounded once, which is
-// the definition shared with the CPU oracle.
+// -ffp-contract=off).  Float transcendentals are the reference's own libm routines restated
+// bit for bit (include/pbrt_libmf.h, shared with the CPU oracle).
 //
 // GPU-specific structure (not in the reference):
 //   * BVH nodes are read as two 16-byte loads; the traversal stack lives in LDS, one
@@ -16,6 +16,18 @@
 #include <stdint.h>
 #include "pbrtgpu.h"
 #include "pbrt_fmath.h"
+#include "pbrt_libmf.h"
+
+// Timing-ablation switches that knowingly change the radiance (PGD_EXP_* / PGD_EXPERIMENT_*,
+// DESIGN.md §4.2, §5) compile only in experiment builds (tools/build_exp*.sh -> lib/exp/, which
+// define PGD_EXPERIMENT_BUILD); the product library refuses them
+#if !defined(PGD_EXPERIMENT_BUILD) &&                                                                   \
+    (defined(PGD_EXPERIMENT_FASTMATH) || defined(PGD_EXPERIMENT_NO_MIS) || defined(PGD_EXPERIMENT_NO_NEE) ||  \
+     defined(PGD_EXP_KD_FIXED) || defined(PGD_EXP_MEAS_CHEAP) || defined(PGD_EXP_MT_CHEAP) ||              \
+     defined(PGD_EXP_NOBETA) || defined(PGD_EXP_NOSPEC) || defined(PGD_EXP_NO_AB) ||                        \
+     defined(PGD_EXP_NO_MT_LIST) || defined(PGD_EXP_NO_OUT))
+#error "PGD_EXP* / PGD_EXPERIMENT_* switches change the radiance: experiment builds only (tools/build_exp.sh)"
+#endif
 
 namespace pgd {
 
@@ -33,29 +45,30 @@ static constexpr float kInvPi = 0.31830988618379067154f;
 static constexpr float kInvTwoPi = 0.15915494309189533577f;
 static constexpr float kOneMinusEps = 0x1.fffffep-1f;
 
-// transcendentals: the parity definition of DESIGN.md §3.2, (float) f((double) x) with the
-// double algorithms of include/pbrt_fmath.h (shared with the CPU oracle).  On the GPU each
-// one is a single out-of-line copy: inlined at every call site they grew the shade kernel's
-// code and register budget (shade 379 -> 361 ms/frame on C2 when outlined, r01f ablation)
+// float transcendentals: the reference's glibc routines restated bit for bit (include/
+// pbrt_libmf.h, shared with the CPU oracle).  On the GPU each one is a single
+// out-of-line copy: inlined at every call site they grew the shade kernel's code and register
+// budget (shade 379 -> 361 ms/frame on C2 when outlined, r01f ablation)
 #ifdef PGD_TRANS_INLINE
 #define PGD_TFN PGD_INLINE
 #else
 #define PGD_TFN __device__ __attribute__((noinline))
 #endif
 #ifndef PGD_EXPERIMENT_FASTMATH
-PGD_TFN float SINF(float x) { return (float)pbrt_fm_sin((double)x); }
-PGD_TFN float COSF(float x) { return (float)pbrt_fm_cos((double)x); }
-PGD_TFN float POWF(float x, float y) { return (float)pbrt_fm_pow((double)x, (double)y); }
-PGD_TFN float ACOSF(float x) { return (float)pbrt_fm_acos((double)x); }
-PGD_TFN float ATAN2F(float y, float x) { return (float)pbrt_fm_atan2((double)y, (double)x); }
-PGD_TFN float TANF(float x) { return (float)pbrt_fm_tan((double)x); }
-PGD_TFN float ATANF(float x) { return (float)pbrt_fm_atan((double)x); }
-PGD_TFN float LOGF(float x) { return (float)pbrt_fm_log_any((double)x); }
-// (SINF(x), COSF(x)) from one argument reduction -- the same two values, one call
+PGD_TFN float SINF(float x) { return libmf_sinf(x); }
+PGD_TFN float COSF(float x) { return libmf_cosf(x); }
+PGD_TFN float POWF(float x, float y) { return libmf_powf(x, y); }
+PGD_TFN float EXPF(float x) { return libmf_expf(x); }
+PGD_TFN float ACOSF(float x) { return libmf_acosf(x); }
+PGD_TFN float ATAN2F(float y, float x) { return libmf_atan2f(y, x); }
+PGD_TFN float TANF(float x) { return libmf_tanf(x); }
+PGD_TFN float ATANF(float x) { return libmf_atanf(x); }
+PGD_TFN float LOGF(float x) { return libmf_logf(x); }
+// (SINF(x), COSF(x)) from one argument reduction -- glibc's sincosf, the same two values
 PGD_TFN float2 SINCOSF(float x) {
-    double s, c;
-    pbrt_fm_sincos((double)x, &s, &c);
-    return make_float2((float)s, (float)c);
+    float s, c;
+    libmf_sincosf(x, &s, &c);
+    return make_float2(s, c);
 }
 #else
 PGD_INLINE float2 SINCOSF(float x) { return make_float2(__sinf(x), __cosf(x)); }

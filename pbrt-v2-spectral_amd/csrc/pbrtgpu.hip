@@ -738,6 +738,25 @@ __global__ void k_mt_sequence(uint32_t seed, int n, uint32_t *out, uint32_t *ext
     for (int i = 0; i < n; ++i) out[i] = mt_uint(r);
 }
 
+// pbrtgpu_libmf_eval: the shading code's transcendental entry points over an input array
+__global__ void k_libmf_eval(int fn, int64_t n, const float *x, const float *y, float *out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float a = x[i];
+    switch (fn) {
+    case PBRTGPU_LIBMF_SINF: out[i] = SINF(a); break;
+    case PBRTGPU_LIBMF_COSF: out[i] = COSF(a); break;
+    case PBRTGPU_LIBMF_SINCOSF: { const float2 sc = SINCOSF(a); out[2 * i] = sc.x; out[2 * i + 1] = sc.y; break; }
+    case PBRTGPU_LIBMF_EXPF: out[i] = EXPF(a); break;
+    case PBRTGPU_LIBMF_LOGF: out[i] = LOGF(a); break;
+    case PBRTGPU_LIBMF_ACOSF: out[i] = ACOSF(a); break;
+    case PBRTGPU_LIBMF_ATANF: out[i] = ATANF(a); break;
+    case PBRTGPU_LIBMF_TANF: out[i] = TANF(a); break;
+    case PBRTGPU_LIBMF_POWF: out[i] = POWF(a, y[i]); break;
+    default: out[i] = ATAN2F(a, y[i]); break;
+    }
+}
+
 // ------------------------------------------------------------------ context
 struct DevBuf {
     void *p = nullptr;
@@ -1883,6 +1902,26 @@ int pbrtgpu_mt_sequence(pbrtgpu_ctx *c, uint32_t seed, int32_t n, uint32_t *out)
     hipLaunchKernelGGL(k_mt_sequence, dim3(1), dim3(64), 0, c->stream, seed, n, d, d + n);
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(out, d, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+int pbrtgpu_libmf_eval(pbrtgpu_ctx *c, int32_t fn, int64_t n, const float *x, const float *y, float *out) {
+    const bool two = fn == PBRTGPU_LIBMF_POWF || fn == PBRTGPU_LIBMF_ATAN2F;
+    if (!c || !x || !out || n < 0 || fn < 0 || fn >= PBRTGPU_LIBMF_COUNT || (two && !y) || n > ((int64_t)1 << 30))
+        return fail(PBRTGPU_E_INVALID, "bad arguments");
+    if (n == 0) return 0;
+    const size_t no = (size_t)n * (fn == PBRTGPU_LIBMF_SINCOSF ? 2 : 1);
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(c->scratch[0].ensure((size_t)n * 4));
+    HIPCHK(c->scratch[1].ensure((size_t)n * 4));
+    HIPCHK(c->scratch[2].ensure(no * 4));
+    HIPCHK(hipMemcpyAsync(c->scratch[0].p, x, (size_t)n * 4, hipMemcpyHostToDevice, c->stream));
+    if (two) HIPCHK(hipMemcpyAsync(c->scratch[1].p, y, (size_t)n * 4, hipMemcpyHostToDevice, c->stream));
+    hipLaunchKernelGGL(k_libmf_eval, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, c->stream, fn, n,
+                       (const float *)c->scratch[0].p, (const float *)c->scratch[1].p, (float *)c->scratch[2].p);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(out, c->scratch[2].p, no * 4, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     return 0;
 }

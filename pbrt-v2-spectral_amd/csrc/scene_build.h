@@ -85,14 +85,15 @@ static inline int wide_bvh(const pbrtgpu_flat_scene *s, int top, std::vector<flo
 }
 
 // SpectralRendererTask::Run's wave bands (spectralrenderer.cpp:99-100, 124, 180-188) in the
-// reference's own int / float arithmetic (sampledLambdaStart 395, sampledLambdaEnd 715 are
-// ints, spectrum.h:41-42): band b's wavelength 395 + dW b + dW / 2 with dW = float(320 / nWB),
-// its interval i of GetValueAtWavelength (spectrum.h:384-405: step float(320 / N), first i with
-// w0 <= wl < w1) and t = (wl - w0) / (w1 - w0), and its indices [dI b, min(dI (b+1), N-1)),
-// dI = round(N / nWB).  A band with indices whose interval is the last reads c[N], past the
-// spectrum: rejected.
+// reference's own int / float arithmetic (sampledLambdaStart / sampledLambdaEnd are ints:
+// 395 / 715 in the 32- and 60-band builds, spectrum.h:41-42; 400 / 700 in the upstream 30-band
+// one, spectrum.h.original:36-38): band b's wavelength start + dW b + dW / 2 with dW =
+// float((end - start) / nWB), its interval i of GetValueAtWavelength (spectrum.h:384-405: step
+// float((end - start) / N), first i with w0 <= wl < w1) and t = (wl - w0) / (w1 - w0), and its
+// indices [dI b, min(dI (b+1), N-1)), dI = round(N / nWB).  A band with indices whose interval is
+// the last reads c[N], past the spectrum: rejected.
 static inline int spectral_table(int N, int nWB, std::vector<int4> *tab, std::vector<float> *wls, std::string *err) {
-    const int lStart = 395, lEnd = 715;
+    const int lStart = N == 30 ? 400 : 395, lEnd = N == 30 ? 700 : 715;
     const int dI = (int)round(N / nWB);
     const float dW = (float)((lEnd - lStart) / nWB);
     const float step = (float)((lEnd - lStart) / N);

@@ -486,7 +486,7 @@ PGD_INLINE void kd_lookup(NodePtr nodes, const float *__restrict__ spectra, floa
             const V d = vsub(v3(a.x, a.y, a.z), v3(p0, p1, p2));
             const float dist2 = vlen2(d);
             if (dist2 < maxD2) {
-                const float weight = (float)pbrt_fm_exp((double)(-100.f * dist2));   // expf
+                const float weight = libmf_expf(-100.f * dist2);   // glibc expf, inline
                 const float4 *sv = reinterpret_cast<const float4 *>(spectra + __float_as_int(b.x));
 #pragma unroll
                 for (int q = 0; q < NQ; ++q) {

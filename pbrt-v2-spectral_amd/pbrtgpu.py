@@ -214,6 +214,7 @@ def gpu_lib():
         g.pbrtgpu_build_bvh.argtypes = [P, I32, P, P, P, P]
         g.pbrtgpu_loop_subdivide.argtypes = [P, I32, I32, P, P, I32, P, P, P, P, P]
         g.pbrtgpu_loop_subdivide_hook.argtypes = [P, I32, I32, P, P, I32, P, P, P, P]
+        g.pbrtgpu_libmf_eval.argtypes = [P, I32, ctypes.c_int64, P, P, P]
     return _gpu
 
 
@@ -224,7 +225,7 @@ def gpu_symbols():
             "pbrtgpu_render_tiles", "pbrtgpu_film_read", "pbrtgpu_film_clear",
             "pbrtgpu_trace_paths", "pbrtgpu_intersect", "pbrtgpu_mt_sequence", "pbrtgpu_path_stats", "pbrtgpu_last_timing",
             "pbrtgpu_film_gather", "pbrtgpu_render_multi", "pbrtgpu_build_bvh", "pbrtgpu_loop_subdivide",
-            "pbrtgpu_loop_subdivide_hook"]
+            "pbrtgpu_loop_subdivide_hook", "pbrtgpu_libmf_eval"]
 
 
 def tile_grid(scene, tile=16):
@@ -506,6 +507,12 @@ class Device:
         _check(self.lib.pbrtgpu_mt_sequence(self.ctx, seed, n, out.ctypes.data))
         return out
 
+    def libmf_eval(self, fn, x, y=None):
+        """The shading kernels' float transcendental `fn` (a LIBMF name) over x (and y for powf /
+        atan2f) on this GPU (pbrtgpu_libmf_eval); sincosf returns [n][2] (sin, cos)."""
+        return _libmf_call(lambda f, n, xp, yp, op: _check(self.lib.pbrtgpu_libmf_eval(self.ctx, f, n, xp, yp, op)),
+                           fn, x, y)
+
     def intersect(self, rays):
         rays = np.ascontiguousarray(rays, dtype=np.float32).reshape(-1, 8)
         hits = np.zeros((len(rays), 4), dtype=np.float32)
@@ -530,6 +537,23 @@ class Device:
             out[k] = {"ms": t.ms[i], "launches": t.launches[i]}
         out["work"] = {k: int(t.work[i]) for i, k in enumerate(Timing.WORK)}
         return out
+
+
+# float transcendentals of include/pbrt_libmf.h (PBRTGPU_LIBMF_* order)
+LIBMF = ["sinf", "cosf", "sincosf", "expf", "logf", "acosf", "atanf", "tanf", "powf", "atan2f"]
+
+
+def _libmf_call(call, fn, x, y):
+    f = LIBMF.index(fn)
+    x = np.ascontiguousarray(x, dtype=np.float32).ravel()
+    yp = None
+    if fn in ("powf", "atan2f"):
+        y = np.ascontiguousarray(y, dtype=np.float32).ravel()
+        assert len(y) == len(x)
+        yp = y.ctypes.data
+    out = np.zeros(2 * len(x) if fn == "sincosf" else len(x), np.float32)
+    call(f, len(x), x.ctypes.data, yp, out.ctypes.data)
+    return out.reshape(-1, 2) if fn == "sincosf" else out
 
 
 def render_multi(devices, spp_begin=0, spp_end=None, tiles=None, tile=(16, 16), slices_per_device=1, out=None,
@@ -573,11 +597,20 @@ class Oracle:
                                                 ctypes.c_int]
         self.lib.oracle_trace_range.restype = ctypes.c_long
         self.lib.oracle_mt_first.argtypes = [ctypes.c_uint32, ctypes.c_int, P]
+        self.lib.oracle_libmf_eval.argtypes = [ctypes.c_int, ctypes.c_int64, P, P, P]
 
     def mt_first(self, seed, n):
         out = np.zeros(n, dtype=np.uint32)
         self.lib.oracle_mt_first(seed, n, out.ctypes.data)
         return out
+
+    def libmf_eval(self, fn, x, y=None):
+        """this build's float transcendental `fn` (glibc's in the libm build, the restatement
+        include/pbrt_libmf.h otherwise)"""
+        def call(f, n, xp, yp, op):
+            if self.lib.oracle_libmf_eval(f, n, xp, yp, op) != 0:
+                raise ValueError(fn)
+        return _libmf_call(call, fn, x, y)
 
     def trace_paths(self, scene, keys):
         keys = np.ascontiguousarray(keys, dtype=np.int32).reshape(-1, 3)

@@ -526,7 +526,7 @@ def test_metadata_vs_reference_golden(pg, base):
 
 
 SPEC = ["killeroo_spec32_%s_40x32s4", "coverage_spec3_%s_48x36s4", "coverage_specsampler8_%s_48x36s8",
-        "killeroo_spec5_dl_%s_32x24s2"]
+        "killeroo_spec5_dl_%s_32x24s2", "killeroo_b30_spec5_%s_32x24s4", "coverage_b30_specsampler6_%s_40x30s8"]
 
 
 @pytest.mark.parametrize("base", SPEC)

@@ -2,10 +2,10 @@
 itself (tools/make_golden.py runs the reference harness built from the unmodified
 reference sources).  This pins the oracle before it is trusted as the GPU's checker.
 
-liboracle_libm.so evaluates transcendentals with glibc float functions -- the reference's
-own -- and must match bit for bit.  liboracle.so uses the double-rounded definition the
-GPU implements; it must agree to within a few float ulps on the rare
-paths where the two definitions of sin/cos/pow/acos/atan2 round differently.
+liboracle_libm.so calls glibc's float transcendentals -- the reference's own -- and must
+match bit for bit.  liboracle.so evaluates them with include/pbrt_libmf.h, the restatement of
+those glibc routines that the GPU kernels compile (pinned over every float input
+by tools/libmf_check.c, tests/test_libmf.py); it must match bit for bit as well.
 """
 import os
 
@@ -26,16 +26,10 @@ def _scene(pg, cfg, name="killeroo"):
     return pg.Scene.load(os.path.join(PACKS, pack), xres=w, yres=h, spp=spp, maxdepth=md, seed=seed)
 
 
-# Fraction of paths expected bit-exact between the double-rounded transcendental definition
-# and glibc's float functions: glibc acosf/atan2f/sinf/cosf are not correctly rounded, so
-# a scene that calls them on every path (C4: the environment light's Le / Pdf / Sample_L)
-# meets last-ulp differences on ~8% of its paths (measured per function: acosf 3.2%,
-# atan2f 1.9%, sinf 1.4%, cosf 0.8%, powf 0.2%); the other scenes on < 1%
-EXACT_RATE = {"metal": 0.90, "coverage": 0.93}
-
-
 def exact_rate(name):
-    return EXACT_RATE.get(name.split("_")[0], 0.97)
+    """Fraction of paths the GPU must reproduce bit for bit: all of them (its transcendentals are
+    the reference's glibc routines restated, include/pbrt_libmf.h)."""
+    return 1.0
 
 
 PATHS = ["killeroo_paths_64x64s4", "killeroo_paths_48x48s8_seed7_md7", "anim_paths_48x48s4", "bunny_paths_64x36s4",
@@ -62,22 +56,14 @@ def test_paths_bit_exact_vs_reference(pg, ora_libm, name):
 
 
 @pytest.mark.parametrize("name", PATHS)
-def test_paths_double_rounded_definition(pg, name):
+def test_paths_restated_libm_bit_exact_vs_reference(pg, name):
+    """The GPU's definition of the float transcendentals (include/pbrt_libmf.h) in the oracle:
+    every path bit for bit the reference's."""
     g = np.load(os.path.join(GOLDEN, name + ".npz"))
     scene = _scene(pg, g["config"], name)
     L = pg.oracle().trace_paths(scene, g["keys"])
-    ref = g["L"]
-    same = np.all(L.view(np.int32) == ref.view(np.int32), axis=1)
-    # a path with many transcendental calls (measured BRDF: 2 atan2 + ~10 exp per lookup)
-    # meets a last-ulp difference more often; the bounds that matter are the two below
-    assert same.mean() >= exact_rate(name)
-    rel = np.abs(L - ref).max(axis=1) / np.maximum(np.abs(ref).max(axis=1), 1e-30)
-    # a path whose sampled direction or roulette decision flips on a last-ulp difference
-    # diverges entirely; such paths must stay rare (<= 1 in 2000) ...
-    assert (rel > 1e-4).mean() <= 5e-4
-    # ... and the estimate they feed stays within the image tolerance (BASELINE: L-inf < 1e-4)
-    tot = np.abs(L.sum(0) - ref.sum(0)).max() / np.abs(ref.sum(0)).max()
-    assert tot < 1e-5
+    same = np.all(L.view(np.int32) == g["L"].view(np.int32), axis=1)
+    assert same.all(), "paths differing: %d / %d" % ((~same).sum(), len(same))
 
 
 @pytest.mark.parametrize("name", ["killeroo_film_96x72s16", "anim_film_40x40s8", "bunny_film_48x27s8",
@@ -206,7 +192,7 @@ def test_metadata_film_bit_exact_vs_reference(pg, ora_libm, name):
 
 
 SPEC = ["killeroo_spec32_%s_40x32s4", "coverage_spec3_%s_48x36s4", "coverage_specsampler8_%s_48x36s8",
-        "killeroo_spec5_dl_%s_32x24s2"]
+        "killeroo_spec5_dl_%s_32x24s2", "killeroo_b30_spec5_%s_32x24s4", "coverage_b30_specsampler6_%s_40x30s8"]
 
 
 def spec_scene(pg, g, name):
@@ -215,7 +201,10 @@ def spec_scene(pg, g, name):
     DirectLightingIntegrator for the _dl fixture)."""
     w, h, spp, seed, md = [int(v) for v in g["config"]]
     pack = "coverage.pack" if name.startswith("coverage") else "killeroo-simple.pack"
-    nwb = int(name.split("_")[1].replace("specsampler", "").replace("spec", ""))
+    if "_b30_" in name:   # the 30-band build: wave bands over 400-700 nm
+        pack = pack.replace(".pack", "-b30.pack")
+    tok = [t for t in name.split("_") if t.startswith("spec")][0]
+    nwb = int(tok.replace("specsampler", "").replace("spec", ""))
     return pg.Scene.load(os.path.join(PACKS, pack), xres=w, yres=h, spp=spp, maxdepth=md, seed=seed,
                          integrator="directlighting" if "_dl_" in name else "path", renderer="spectral", wave_bands=nwb,
                          sampling="sampler" if "specsampler" in name else "single")

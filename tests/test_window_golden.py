@@ -1,0 +1,101 @@
+"""Image-level parity at the configs' REAL resolution and sample count (BASELINE.json configs
+2-5; north star: image L-inf < 1e-4 vs the CPU reference).
+
+The fixtures (tools/make_golden.py --only window) are tile-aligned crops of the reference
+harness's film at full size and spp: C2 killeroo 700x700@256 at the sphere light's edge and at
+a killeroo silhouette (48 x 48 each), C3 bunny 1920x1080@1024, C4 metal 400x400@4096 (60 bands),
+C5 anim 600x600@512 (32 x 32 each).  The harness traced every sample of a window one pixel
+larger on each side, so each cropped pixel holds all of its contributions, including the
+exact-boundary samples of its neighbours (spectralImage.cpp:77-152, samplerrenderer.cpp:119-147).
+
+CPU: the glibc-float oracle renders the same window and must match bit for bit (pins the oracle
+at full spp).  GPU: the tiles covering the crop are rendered at the full config through
+pbrtgpu_render_tiles (which adds the neighbours' spill samples itself); the crop is compared with
+the reference film: L-inf relative to the window's largest value < 1e-4, and per pixel relative
+to that pixel's largest band < 1e-4 as well.  The bit-exact pixel fraction is reported
+(gpurun_out/window_parity.json when run on the box).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, PACKS, ROOT
+
+WINDOWS = ["killeroo_window_c2_light_700x700s256", "killeroo_window_c2_edge_700x700s256",
+           "bunny_window_c3_1920x1080s1024", "metal_window_c4_400x400s4096", "anim_window_c5_600x600s512"]
+PACK = {"killeroo": "killeroo-simple.pack", "bunny": "bunny.pack", "metal": "metal.pack",
+        "anim": "anim-killeroos-moving.pack"}
+
+
+def _load(pg, name):
+    g = np.load(os.path.join(GOLDEN, name + ".npz"))
+    w, h, spp, seed, md = [int(v) for v in g["config"]]
+    scene = pg.Scene.load(os.path.join(PACKS, PACK[name.split("_")[0]]), xres=w, yres=h, spp=spp, maxdepth=md,
+                          seed=seed)
+    return g, scene
+
+
+def window_tiles(scene, window, tile=16):
+    x0, y0, w, h = [int(v) for v in window]
+    assert x0 % tile == 0 and y0 % tile == 0 and w % tile == 0 and h % tile == 0
+    ntx = (scene.width + tile - 1) // tile
+    return np.array([ty * ntx + tx for ty in range(y0 // tile, (y0 + h) // tile)
+                     for tx in range(x0 // tile, (x0 + w) // tile)], np.int32)
+
+
+def window_errors(film, ref):
+    """(L-inf over the window relative to its largest value, largest per-pixel relative error,
+    bit-exact pixel fraction)"""
+    d = np.abs(film.astype(np.float64) - ref.astype(np.float64))
+    linf = d.max() / np.abs(ref).max()
+    px = (d.max(axis=2) / np.maximum(np.abs(ref).max(axis=2), 1e-30)).max()
+    exact = np.all(film.view(np.int32) == ref.view(np.int32), axis=2).mean()
+    return float(linf), float(px), float(exact)
+
+
+@pytest.mark.parametrize("name", WINDOWS)
+def test_window_fixture_shape(name):
+    g = np.load(os.path.join(GOLDEN, name + ".npz"))
+    x0, y0, w, h = g["window"]
+    W, H, spp = g["config"][:3]
+    assert g["film"].shape[:2] == (h, w) and x0 + w <= W and y0 + h <= H
+    assert spp in (256, 512, 1024, 4096) and np.isfinite(g["film"]).all() and g["film"].max() > 0
+
+
+@pytest.mark.parametrize("name", WINDOWS)
+def test_window_oracle_bit_exact_vs_reference(pg, name):
+    """The glibc-float oracle (the reference's transcendentals) renders every sample of the
+    one-pixel-larger window at full spp: bit for bit the reference's film."""
+    g, scene = _load(pg, name)
+    x0, y0, w, h = [int(v) for v in g["window"]]
+    film, _ = pg.oracle(libm_float=True).render(scene, window=(x0 - 1, x0 + w + 1, y0 - 1, y0 + h + 1),
+                                                threads=min(16, os.cpu_count() or 8))
+    crop = film[y0:y0 + h, x0:x0 + w]
+    assert np.array_equal(crop.view(np.int32), g["film"].view(np.int32))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", WINDOWS)
+def test_window_gpu_vs_reference(pg, name):
+    g, scene = _load(pg, name)
+    x0, y0, w, h = [int(v) for v in g["window"]]
+    tiles = window_tiles(scene, g["window"])
+    with pg.Device(0) as d:
+        d.upload(scene)
+        st = d.render(tiles=tiles)
+        film = d.film()
+    crop = film[y0:y0 + h, x0:x0 + w]
+    ref = g["film"]
+    assert st[pg.STAT_PATHS] == w * h * scene.spp
+    linf, px, exact = window_errors(crop, ref)
+    rec = {"name": name, "spp": int(scene.spp), "window": [x0, y0, w, h], "linf_rel_window": linf,
+           "max_pixel_rel": px, "bit_exact_pixels": exact, "spills": float(st[pg.STAT_SPILLS])}
+    out = os.path.join(ROOT, "gpurun_out")
+    if os.path.isdir(out):
+        with open(os.path.join(out, "window_parity.jsonl"), "a") as f:
+            f.write(json.dumps(rec) + "\n")
+    print(rec)
+    assert linf < 1e-4, rec
+    assert px < 1e-4, rec

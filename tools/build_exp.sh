@@ -6,7 +6,7 @@ R=$(cd "$(dirname "$0")/.." && pwd)
 NAME=$1; shift
 cd $R/pbrt-v2-spectral_amd
 T=lib/exp/$NAME.obj; mkdir -p $T
-H="/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -I../include -Ihost -Icsrc"
+H="/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -DPGD_EXPERIMENT_BUILD -I../include -Ihost -Icsrc"
 pids=()
 for v in 32_0 32_7 60_0 60_7 30_0 30_7 3_0 3_7; do
   $H "$@" -DSHADE_NB=${v%_*} -DSHADE_FEAT=${v#*_} -c csrc/shade.hip -o $T/s$v.o & pids+=($!)

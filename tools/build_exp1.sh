@@ -7,7 +7,7 @@ R=$(cd "$(dirname "$0")/.." && pwd)
 NAME=$1; shift
 cd $R/pbrt-v2-spectral_amd
 T=lib/exp/$NAME.obj; rm -rf $T; mkdir -p $T
-H="/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -I../include -Ihost -Icsrc"
+H="/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -DPGD_EXPERIMENT_BUILD -I../include -Ihost -Icsrc"
 $H "$@" -DSHADE_NB=32 -DSHADE_FEAT=0 -c csrc/shade.hip -o $T/s32_0.o &
 p1=$!
 $H "$@" -DSHADE_NB=32 -DSHADE_FEAT=7 -c csrc/shade.hip -o $T/s32_7.o &

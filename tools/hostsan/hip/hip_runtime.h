@@ -20,6 +20,7 @@
 #define __host__
 #define __global__
 #define __shared__
+#define __constant__
 #define __forceinline__ inline
 #define __launch_bounds__(...)
 #define PGD_LDS_AS   // LDS address space qualifier of wavefront.h: ordinary memory here

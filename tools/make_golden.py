@@ -47,7 +47,12 @@ Fixtures (numpy .npz, inputs + expected outputs only):
                                   reference's own SpectralImageNoCameraFilm wrote for the same
                                   samples (--refdat): pins AddSample and the WriteImage payload
   *_b30_*, fromrgb_30.npz         the upstream 30-band build (b30 harness, 400-700 nm)
-Usage: python tools/make_golden.py [--only keys|dat|merl|dl|meta|spec|rgb|b30]
+  <scene>_window_<cfg>_*.npz      film crops at the configs' REAL size and sample count: every
+                                  sample of a one-pixel-larger window (--window), so each cropped
+                                  pixel holds all of its contributions (incl. exact-boundary samples
+                                  of its neighbours, spectralImage.cpp:77-152); C2 at the sphere
+                                  light's edge and at a killeroo silhouette, C3-C5 at an edge each
+Usage: python tools/make_golden.py [--only keys|dat|merl|dl|meta|spec|rgb|b30|window]
        (after `make -C oracle ref`, `ref60`, `ref30` and `refrgb`)
 """
 import os
@@ -147,6 +152,13 @@ def b30_fixtures(tmp):
     paths_fixture("coverage_b30_paths_48x36s4", (48, 36), 4, 0, 6, 1, tmp, scene=cov, bands=30)
     film_fixture("coverage_b30_film_40x30s4", (40, 30), 4, 0, 6, tmp, scene=cov, bands=30)
     spectra_fixture(30, tmp)
+    # the SpectralRenderer at 30 bands: wave-band wavelengths from 400 / 700 nm
+    for stem, scene, res, spp, nwb, method, md in (("killeroo_b30_spec5", "killeroo-simple.pbrt", (32, 24), 4, 5, "single", 5),
+                                                   ("coverage_b30_specsampler6", cov, (40, 30), 8, 6, "sampler", 6)):
+        ex = ("--spectral", str(nwb), method, "--surf", "path")
+        tag = "%dx%ds%d" % (res[0], res[1], spp)
+        paths_fixture("%s_paths_%s" % (stem, tag), res, spp, 0, md, 1, tmp, scene=scene, bands=30, extra=ex)
+        film_fixture("%s_film_%s" % (stem, tag), res, spp, 0, md, tmp, scene=scene, bands=30, extra=ex)
 
 
 def keys_fixture(name, scene, W, H, spp, bands, kseed, tmp):
@@ -160,6 +172,30 @@ def keys_fixture(name, scene, W, H, spp, bands, kseed, tmp):
     assert np.array_equal(k2, keys)
     np.savez_compressed(os.path.join(OUT, name + ".npz"), keys=keys, L=L, config=np.array([W, H, spp, 0, 5], np.int32))
     print(name, keys.shape)
+
+
+# (name, scene file, W, H, spp, bands, film-pixel window x0, y0, w, h): tile-aligned (16 x 16)
+# crops of BASELINE.json configs 2-5 at full resolution and spp
+WINDOW_CONFIGS = [("killeroo_window_c2_light_700x700s256", "killeroo-simple.pbrt", 700, 700, 256, 32, 64, 16, 48, 48),
+                  ("killeroo_window_c2_edge_700x700s256", "killeroo-simple.pbrt", 700, 700, 256, 32, 96, 288, 48, 48),
+                  ("bunny_window_c3_1920x1080s1024", "bunny.pbrt", 1920, 1080, 1024, 32, 1216, 832, 32, 32),
+                  ("metal_window_c4_400x400s4096", "metal.pbrt", 400, 400, 4096, 60, 96, 112, 32, 32),
+                  ("anim_window_c5_600x600s512", "anim-killeroos-moving.pbrt", 600, 600, 512, 32, 112, 240, 32, 32)]
+
+
+def window_fixture(name, scene, W, H, spp, bands, x0, y0, w, h, tmp):
+    """Film pixels [x0, x0 + w) x [y0, y0 + h) of the full-size render.  Film pixel x receives
+    samples of sample pixels x - 1, x, x + 1 only (the box filter's footprint, two pixels wide at
+    an exact boundary), so the harness traces the sample window one pixel larger on each side."""
+    fn = os.path.join(tmp, name + ".f32")
+    run([os.path.join(SCENES, scene), "--res", str(W), str(H), "--spp", str(spp), "--seed", "0", "--maxdepth", "5",
+         "--window", str(x0 - 1), str(x0 + w + 1), str(y0 - 1), str(y0 + h + 1), "--raw", fn], bands)
+    raw = np.fromfile(fn, dtype=np.int32)
+    FW, FH, N = raw[:3]
+    film = raw[3:].view(np.float32).reshape(FH, FW, N)[y0:y0 + h, x0:x0 + w].copy()
+    np.savez_compressed(os.path.join(OUT, name + ".npz"), film=film, window=np.array([x0, y0, w, h], np.int32),
+                        config=np.array([W, H, spp, 0, 5], np.int32))
+    print(name, film.shape)
 
 
 def dat_fixture(name, res, spp, tmp, scene="killeroo-simple.pbrt"):
@@ -278,6 +314,11 @@ def main():
                 rgb_fixtures(tmp)
             elif only == "b30":
                 b30_fixtures(tmp)
+            elif only == "window":
+                sel = sys.argv[3:]
+                for cfg in WINDOW_CONFIGS:
+                    if not sel or cfg[0] in sel:
+                        window_fixture(*cfg, tmp)
         return
     with tempfile.TemporaryDirectory() as tmp:
         paths_fixture("killeroo_paths_64x64s4", (64, 64), 4, 0, 5, 5, tmp)
@@ -304,6 +345,9 @@ def main():
             if cfg[5] != 60 or os.path.exists(HARNESS60):
                 keys_fixture(*cfg, tmp)
         dat_fixture("killeroo_dat_40x32s4", (40, 32), 4, tmp)
+        for cfg in WINDOW_CONFIGS:
+            if cfg[5] != 60 or os.path.exists(HARNESS60):
+                window_fixture(*cfg, tmp)
         merl_fixtures(tmp)
         dl_fixtures(tmp)
         meta_fixtures(tmp)
