@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define PBRTGPU_ABI_VERSION 9
+#define PBRTGPU_ABI_VERSION 10
 #define PBRTGPU_MAX_BANDS 64
 
 #define PBRTGPU_E_INVALID   (-1)
@@ -207,8 +207,11 @@ typedef struct pbrtgpu_camera {
  * differentials by Camera::GenerateRayDifferential, camera.cpp:52-81): film rays traced from
  * the sensor through the lens elements, last element first; with "diffractionEnabled" each
  * element's exit direction is perturbed by a bivariate Gaussian (realisticDiffraction.cpp:
- * 1057-1150) drawn from the camera sample's own stream.  Pinhole arrays /
- * microlenses and the eye IOR curves are not part of this build (pbrthost refuses them). */
+ * 1057-1150) drawn from the camera sample's own stream.  The light-field modes:
+ * a pinhole array between lens and sensor (rays aim at the pinhole of their superpixel,
+ * :248-304, 560-629), optionally with a two-surface microlens per pinhole (:614-876); and the
+ * Gullstrand eye (IORforEyeEnabled, :196-205, 357-377): the ocular media's IOR spectra at the
+ * ray's wavelength. */
 typedef struct pbrtgpu_lens {
     int32_t n_elements;           /* lens-file elements, scene side first */
     int32_t chromatic;            /* chromaticAberrationEnabled: n + (lambda - 550) * -0.04 / 300 where n != 1 */
@@ -223,6 +226,14 @@ typedef struct pbrtgpu_lens {
     int32_t reserved;
     const float *elements;        /* [n_elements][4] radius, separation, n, aperture (an aperture stop,
                                    * radius 0, carries "aperture_diameter") */
+    int32_t num_pinholes_w, num_pinholes_h;   /* "num_pinholes_w/h" (ints of the float parameters); both > 0:
+                                               * the pinhole array */
+    int32_t microlens;            /* "microlens_enabled": a microlens over every pinhole */
+    int32_t ior_eye;              /* "IORforEyeEnabled" */
+    const float *pinholes;        /* [num_pinholes_w][num_pinholes_h][3] the constructor's pinholeArray at the
+                                   * film resolution (realisticDiffraction.cpp:248-304), or NULL */
+    const float *eye_ior;         /* [4][n_bands] cornea, aqueous, lens, vitreous IOR spectra (Spectrum::
+                                   * FromSampled of the camera's curves, :196-205), or NULL */
 } pbrtgpu_lens;
 
 typedef struct pbrtgpu_flat_scene {

@@ -2062,10 +2062,12 @@ static void diff_bigauss(DiffStream *st, double sigma_x, double sigma_y, double 
     }
 }
 /* realisticDiffraction.cpp:1057-1150 after an element: p its intersection point, ap its aperture,
- * wl the ray's wavelength.  C++'s float overloads (sqrt of a float expression) are sqrtf here.
- * Returns 0 when the new direction has a NaN (the ray's weight is 0). */
-static int lens_diffraction(DiffStream *st, V p, float ap, float wl, V *dir_io) {
-    double radius = sqrtf(p.x * p.x + p.y * p.y);
+ * wl the ray's wavelength; the radius is measured from (cx, cy) -- the axis for the main lens, the
+ * microlens centre for the microlens elements (:790-872).  C++'s float overloads (sqrt of a float
+ * expression) are sqrtf here.  nan_out (main lens): a NaN direction returns 0 (the ray's weight is
+ * 0); the microlens step normalises whatever it got (no check there). */
+static int lens_diffraction(DiffStream *st, V p, float cx, float cy, float ap, float wl, V *dir_io, int nan_out) {
+    double radius = sqrtf((p.x - cx) * (p.x - cx) + (p.y - cy) * (p.y - cy));
     V ea = v3(p.x, p.y, 0.f), eb = v3(-p.y, p.x, 0.f);
     double a = ap / 2 - radius;
     double b = sqrt(ap / 2 * ap / 2 - radius * radius);
@@ -2095,7 +2097,7 @@ static int lens_diffraction(DiffStream *st, V p, float ap, float wl, V *dir_io) 
     d.z = (float)(DSIN(thetaB) * rB);
     d.x = (float)(ea.x * newA + eb.x * newB);
     d.y = (float)(ea.y * newA + eb.y * newB);
-    if (isnan(d.x) || isnan(d.y) || isnan(d.z)) {
+    if (nan_out && (isnan(d.x) || isnan(d.y) || isnan(d.z))) {
         *dir_io = v3(0.f, 0.f, 0.f);
         return 0;
     }
@@ -2122,9 +2124,40 @@ static int lens_el_hit(const Ray *r, float radius, V dist, float *tHit, V *nrm) 
     *nrm = vnorm(v3(d.x * th + o.x, d.y * th + o.y, d.z * th + o.z));
     return 1;
 }
-/* applySnellsLaw (realisticDiffraction.cpp:347-410), chromatic model in double (-.04) */
-static void lens_snell(float n1, float n2, float lensRadius, V nrm, Ray *ray, float wl, int chromatic) {
-    if (chromatic) {
+/* Spectrum::GetValueAtWavelength (spectrum.h:384-405): the band interval of wl (int step), Lerp of
+ * its two band values, 0 outside every interval (the front end refuses band wavelengths in the
+ * last interval, which would read c[N]) */
+static float value_at_wavelength(const float *c, int N, float wl) {
+    const int l0 = N == 30 ? 400 : 395, l1 = N == 30 ? 700 : 715;
+    const float step = (float)((l1 - l0) / N);
+    for (int i = 0; i < N; ++i) {
+        const float w0 = l0 + i * step, w1 = l0 + (i + 1) * step;
+        if (wl >= w0 && wl < w1) return lerpf((wl - w0) / (w1 - w0), c[i], c[i + 1]);
+    }
+    return 0.f;
+}
+/* applySnellsLaw (realisticDiffraction.cpp:347-410): with IORforEyeEnabled and a wavelength, the
+ * ocular medium is recognised by the lens file's n (vitreous 1.336, lens 1.42, aqueous 1.3374,
+ * cornea 1.3771; |n1 - n| < .001 in double) and both indices come from the eye IOR spectra
+ * (cornea, aqueous, lens, vitreous) at the wavelength; otherwise the chromatic model, in double
+ * (-.04) */
+static void lens_snell(const pbrtgpu_lens *Ls, int N, float n1, float n2, float lensRadius, V nrm, Ray *ray, float wl) {
+    if (Ls->ior_eye && wl != 0) {
+        const float *cornea = Ls->eye_ior, *aqueous = cornea + N, *lensI = cornea + 2 * N, *vitreous = cornea + 3 * N;
+        if (fabs((double)n1 - 1.336) < 0.001) {
+            n1 = value_at_wavelength(vitreous, N, wl);
+            n2 = value_at_wavelength(lensI, N, wl);
+        } else if (fabs((double)n1 - 1.42) < 0.001) {
+            n1 = value_at_wavelength(lensI, N, wl);
+            n2 = value_at_wavelength(aqueous, N, wl);
+        } else if (fabs((double)n1 - 1.3374) < 0.001) {
+            n1 = value_at_wavelength(aqueous, N, wl);
+            n2 = value_at_wavelength(cornea, N, wl);
+        } else if (fabs((double)n1 - 1.3771) < 0.001) {
+            n1 = value_at_wavelength(cornea, N, wl);
+            n2 = 1;
+        }
+    } else if (Ls->chromatic) {
         if (n1 != 1) n1 = (float)((double)(wl - 550) * -.04 / (300) + (double)n1);
         if (n2 != 1) n2 = (float)((double)(wl - 550) * -.04 / (300) + (double)n2);
     }
@@ -2136,8 +2169,7 @@ static void lens_snell(float n1, float n2, float lensRadius, V nrm, Ray *ray, fl
     V s2 = vsub(vmul(vcross(nrm, vcross(vmul(nrm, -1.f), s1)), n1 / n2), vmul(nrm, sqrtf(radicand)));
     ray->d = vnorm(s2);
 }
-/* GenerateRay (realisticDiffraction.cpp:478-1164) without diffraction / pinhole arrays /
- * microlenses: returns the weight (0: blocked) */
+/* GenerateRay (realisticDiffraction.cpp:478-1164): returns the weight (0: blocked) */
 static float lens_ray(const Ctx *c, float imageX, float imageY, float lensU, float lensV, float timeU, float wl,
                       DiffStream *st, Ray *out) {
     const pbrtgpu_camera *cam = &c->s->camera;
@@ -2166,15 +2198,68 @@ static float lens_ray(const Ctx *c, float imageX, float imageY, float lensU, flo
     const float *E = Ls->elements;
     float firstAp = E[4 * (n - 1) + 3] / 2, firstR = E[4 * (n - 1)];
     float zI = firstR == 0 ? 0.f : (-firstR - sqrtf(firstR * firstR - firstAp * firstAp));
+    const float luNoScale = lu, lvNoScale = lv;
+    float pitch = 0.f;   /* superpixelPitch */
+    int xp = 0, yp = 0;  /* the pinhole under the film point */
+    const int nW = Ls->num_pinholes_w, nH = Ls->num_pinholes_h, pinholes = nW > 0 && nH > 0;
     lu *= firstAp;
     lv *= firstAp;
     V pol = v3(lu, lv, zI);
     if (Ls->pinhole_exit[0] != -1 && Ls->pinhole_exit[1] != -1 && Ls->pinhole_exit[2] != -1)
         pol = v3(Ls->pinhole_exit[0], Ls->pinhole_exit[1], Ls->pinhole_exit[2]);
+    else if (pinholes) {
+        /* the pinhole array (:560-629): the superpixel under the film point, clamped */
+        const int ppW = cam->xres / nW, ppH = cam->yres / nH;
+        xp = (int)(((double)imageX - .25) / ppW);
+        yp = (int)(((double)imageY - .25) / ppH);
+        if (xp > nW - 1) xp = nW - 1;
+        else if (xp < 0) xp = 0;
+        if (yp > nH - 1) yp = nH - 1;
+        else if (yp < 0) yp = 0;
+        const float *ph = Ls->pinholes + 3 * ((size_t)xp * nH + yp);
+        if (Ls->microlens) {
+            /* the microlens's entrance square (:614-623) */
+            pitch = width / nW;
+            pol = v3(luNoScale * pitch / 2.f + ph[0], lvNoScale * pitch / 2.f + ph[1], ph[2]);
+        } else pol = v3(ph[0], ph[1], ph[2]);
+    }
     Ray r;
     r.o = sp;
     r.d = vnorm(vsub(pol, r.o));
     r.mint = 0.f; r.maxt = INFINITY; r.time = 0.f;
+    if (Ls->microlens && pinholes) {
+        /* two spherical microlens surfaces (:634-876): radius from the thick-lens focal length */
+        const float *ph = Ls->pinholes + 3 * ((size_t)xp * nH + yp);
+        const float ap = pitch;
+        const float thick = (float).01;
+        const float mFilmDist = Ls->film_distance + pol.z;
+        const float mFocal = mFilmDist + thick / 2;
+        const float mN = (float)1.67;
+        const double nm1 = (double)(mN - 1);
+        const float oneOverR = (float)((-2 * (mN - 1) + sqrt(4 * (nm1 * nm1) + 4 * (nm1 * nm1) * thick / (mN * mFocal))) /
+                                       (2 * (nm1 * nm1) * thick / mN));
+        float mRad = 1 / oneOverR;
+        float mDist = -Ls->film_distance + mFilmDist;
+        for (int k = 0; k < 2; ++k) {
+            const float cx = ph[0], cy = ph[1];
+            float tHit = 0.f;
+            V nrm = v3(0.f, 0.f, 1.f), ip = v3(0.f, 0.f, 0.f);
+            mRad = -mRad;
+            r.o = sp;
+            if (lens_el_hit(&r, mRad, v3(-cx, -cy, mRad - mDist), &tHit, &nrm)) {
+                ip = v3(tHit * r.d.x + r.o.x, tHit * r.d.y + r.o.y, tHit * r.d.z + r.o.z);
+                if ((ip.x - cx) * (ip.x - cx) + (ip.y - cy) * (ip.y - cy) >= (ap * ap) / (2 * 2)) return 0.f;
+                float n1 = 1, n2 = 1;
+                if (k == 0) {
+                    n2 = mN;
+                    mDist += thick;
+                } else n1 = mN;
+                lens_snell(Ls, c->nb, n1, n2, mRad, nrm, &r, wl);
+                sp = ip;
+            }
+            if (Ls->diffraction) lens_diffraction(st, ip, cx, cy, ap, wl, &r.d, 0);
+        }
+    }
     float lensDist = 0.f;
     for (int i = n - 1; i >= 0; --i) {
         float rad = E[4 * i], ap = E[4 * i + 3];
@@ -2186,7 +2271,7 @@ static float lens_ray(const Ctx *c, float imageX, float imageY, float lensU, flo
             float dx = ai.x - Ls->aperture_offset[0], dy = ai.y - Ls->aperture_offset[1];
             if ((double)(dx * dx + dy * dy) > (double)(ap * ap) * .25) return 0.f;
             sp = ai;
-            if (Ls->diffraction && !lens_diffraction(st, ai, ap, wl, &r.d)) return 0.f;
+            if (Ls->diffraction && !lens_diffraction(st, ai, 0.f, 0.f, ap, wl, &r.d, 1)) return 0.f;
         } else {
             float tHit = 0.f;
             V nrm = v3(0.f, 0.f, 1.f);
@@ -2198,9 +2283,9 @@ static float lens_ray(const Ctx *c, float imageX, float imageY, float lensU, flo
                 n2 = E[4 * (i - 1) + 2];
                 if (n2 == 0) n2 = E[4 * (i - 2) + 2];
             }
-            lens_snell(n1, n2, rad, nrm, &r, wl, Ls->chromatic);
+            lens_snell(Ls, c->nb, n1, n2, rad, nrm, &r, wl);
             sp = ip;
-            if (Ls->diffraction && !lens_diffraction(st, ip, ap, wl, &r.d)) return 0.f;
+            if (Ls->diffraction && !lens_diffraction(st, ip, 0.f, 0.f, ap, wl, &r.d, 1)) return 0.f;
         }
     }
     r.o = sp;
@@ -2351,6 +2436,12 @@ static int spectral_ok(const pbrtgpu_flat_scene *s) {
         const float wl = l0 + dW * b + (dW / 2);
         if (wl >= l0 + (N - 1) * step) return 0;
     }
+    /* the eye IOR lookups read every traced band's interval (spectrum.h:397) */
+    if (s->camera_type == PBRTGPU_CAMERA_REALISTIC && s->lens.ior_eye)
+        for (int b = 0; b < nWB; ++b) {
+            const float wl = l0 + dW * b + (dW / 2);
+            if (wl >= l0 + (N - 1) * step) return 0;
+        }
     return 1;
 }
 

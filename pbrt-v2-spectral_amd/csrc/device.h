@@ -348,6 +348,10 @@ struct DevScene {
     int lensDiffraction;              // diffractionEnabled
     float lensFilmDist, lensFilmDiag, lensCurveR, lensApOff[2], lensFilmC[2], lensPinhole[3];
     const float4 *lensEl;             // [lensN]: radius, separation, n, aperture
+    int lensPinW, lensPinH;           // pinhole array (both > 0), its microlenses, the eye IOR curves
+    int lensMicro, lensEye;
+    const float *lensPinholes;        // [lensPinW][lensPinH][3]
+    const float *lensEyeIor;          // [4][NB]: cornea, aqueous, lens, vitreous
 };
 
 // scene features a shade kernel is specialised for (k_shade<NB, FEAT>): a scene without
@@ -2116,10 +2120,40 @@ PGD_INLINE bool lens_el_hit(const Ray &r, float radius, V dist, float *tHit, V *
     *nrm = vnorm(v3(d.x * th + o.x, d.y * th + o.y, d.z * th + o.z));
     return true;
 }
-// applySnellsLaw (realisticDiffraction.cpp:347-410) without the eye IOR curves; the
-// chromatic model's arithmetic is double (the -.04 literal)
-PGD_INLINE void lens_snell(float n1, float n2, float lensRadius, V nrm, Ray *ray, float wl, int chromatic) {
-    if (chromatic) {
+// Spectrum::GetValueAtWavelength (spectrum.h:384-405) of a spectrum of N bands: the band interval
+// of wl (integer step), Lerp of its two values; 0 outside every interval (band wavelengths in the
+// last interval, which would read c[N], are refused at upload)
+PGD_INLINE float value_at_wavelength(const float *c, int N, float wl) {
+    const int l0 = N == 30 ? 400 : 395, l1 = N == 30 ? 700 : 715;
+    const float step = (float)((l1 - l0) / N);
+    for (int i = 0; i < N; ++i) {
+        const float w0 = l0 + i * step, w1 = l0 + (i + 1) * step;
+        if (wl >= w0 && wl < w1) return lerpf((wl - w0) / (w1 - w0), *sa(c, (uint32_t)i), *sa(c, (uint32_t)(i + 1)));
+    }
+    return 0.f;
+}
+// applySnellsLaw (realisticDiffraction.cpp:347-410).  IORforEyeEnabled with a wavelength: the
+// ocular medium is recognised by the lens file's n (|n1 - n| < .001 in double: vitreous 1.336,
+// lens 1.42, aqueous 1.3374, cornea 1.3771) and both indices come from the eye IOR spectra at the
+// wavelength; otherwise the chromatic model, whose arithmetic is double (the -.04 literal)
+PGD_INLINE void lens_snell(const DevScene &S, float n1, float n2, float lensRadius, V nrm, Ray *ray, float wl) {
+    if (S.lensEye && wl != 0) {
+        const int N = S.nb;
+        const float *cornea = S.lensEyeIor, *aqueous = cornea + N, *lensI = cornea + 2 * N, *vitreous = cornea + 3 * N;
+        if (fabs((double)n1 - 1.336) < 0.001) {
+            n1 = value_at_wavelength(vitreous, N, wl);
+            n2 = value_at_wavelength(lensI, N, wl);
+        } else if (fabs((double)n1 - 1.42) < 0.001) {
+            n1 = value_at_wavelength(lensI, N, wl);
+            n2 = value_at_wavelength(aqueous, N, wl);
+        } else if (fabs((double)n1 - 1.3374) < 0.001) {
+            n1 = value_at_wavelength(aqueous, N, wl);
+            n2 = value_at_wavelength(cornea, N, wl);
+        } else if (fabs((double)n1 - 1.3771) < 0.001) {
+            n1 = value_at_wavelength(cornea, N, wl);
+            n2 = 1;
+        }
+    } else if (S.lensChromatic) {
         if (n1 != 1) n1 = (float)((double)(wl - 550) * -.04 / (300) + (double)n1);
         if (n2 != 1) n2 = (float)((double)(wl - 550) * -.04 / (300) + (double)n2);
     }
@@ -2174,12 +2208,16 @@ PGD_INLINE void diff_gaussian(DiffStream *st, double sx, double sy, double *x, d
 }
 // The perturbation after element i (aperture stop or lens surface): ip the element's
 // intersection point, ap its aperture, wl the ray's wavelength (0 under the SamplerRenderer:
-// sigma = atan(1 / inf) = 0, the draws are still made).  The expressions keep the reference's
-// float / double mix (float Vector arithmetic and sqrtf where its operands are float).  false:
-// the direction became NaN (weight 0, realisticDiffraction.cpp:1141-1147).  Out of line: its
-// double arithmetic is not inlined into the 2 x 3 element steps of a camera differential.
-__device__ __attribute__((noinline)) bool lens_diffract(DiffStream *st, V ip, float ap, float wl, V *dp) {
-    const double radius = (double)sqrtf(ip.x * ip.x + ip.y * ip.y);
+// sigma = atan(1 / inf) = 0, the draws are still made); the radius is measured from (cx, cy):
+// the axis for the main lens, the microlens centre for a microlens surface (:790-872, whose
+// direction vectors still come from the absolute hit point).  The expressions keep the
+// reference's float / double mix (float Vector arithmetic and sqrtf where its operands are
+// float).  nanOut (main lens): a NaN direction returns false (weight 0, realisticDiffraction.cpp:
+// 1141-1147); the microlens step normalises whatever it got.  Out of line: its double arithmetic
+// is not inlined into the element steps of a camera differential.
+__device__ __attribute__((noinline)) bool lens_diffract(DiffStream *st, V ip, float cx, float cy, float ap, float wl, V *dp,
+                                                        bool nanOut) {
+    const double radius = (double)sqrtf((ip.x - cx) * (ip.x - cx) + (ip.y - cy) * (ip.y - cy));
     V dir = v3(ip.x, ip.y, 0.f), orth = v3(-ip.y, ip.x, 0.f);
     const double a = (double)(ap / 2) - radius;
     const double b = __builtin_sqrt((double)(ap / 2 * ap / 2) - radius * radius);
@@ -2212,18 +2250,18 @@ __device__ __attribute__((noinline)) bool lens_diffract(DiffStream *st, V ip, fl
     d.z = (float)(pbrt_fm_sin(thetaB) * rB);
     d.x = (float)((double)dir.x * newProjA + (double)orth.x * newProjB);
     d.y = (float)((double)dir.y * newProjA + (double)orth.y * newProjB);
-    if (d.x != d.x || d.y != d.y || d.z != d.z) {
+    if (nanOut && (d.x != d.x || d.y != d.y || d.z != d.z)) {
         *dp = v3(0.f, 0.f, 0.f);
         return false;
     }
     *dp = vnorm(d);
     return true;
 }
-// RealisticDiffractionCamera::GenerateRay (realisticDiffraction.cpp:478-1164 without the
-// pinhole-array and microlens branches): film point -> toward the sampled point
-// of the last element's aperture disk (or the pinhole exit point) -> every element, last
-// first; a blocked or missed element returns weight 0.  The ray ends in world space with a
-// normalised direction.
+// RealisticDiffractionCamera::GenerateRay (realisticDiffraction.cpp:478-1164): film point ->
+// toward the sampled point of the last element's aperture disk (or the pinhole exit point, or
+// the pinhole of the film point's superpixel, or a point of its microlens's entrance square) ->
+// the two microlens surfaces -> every element, last first; a blocked or missed element returns
+// weight 0.  The ray ends in world space with a normalised direction.
 PGD_INLINE float lens_ray(const DevScene &S, float imageX, float imageY, float lensU, float lensV, float timeU, float wl,
                           DiffStream *st, Ray *out) {
     const pbrtgpu_camera &cam = S.cam;
@@ -2250,46 +2288,107 @@ PGD_INLINE float lens_ray(const DevScene &S, float imageX, float imageY, float l
     const float4 last = (*sa(S.lensEl, (uint32_t)(S.lensN - 1)));
     const float firstAp = last.w / 2, firstR = last.x;
     const float zI = firstR == 0 ? 0.f : (-firstR - sqrtf(firstR * firstR - firstAp * firstAp));
+    const float luNoScale = lu, lvNoScale = lv;
+    float pitch = 0.f;                  // superpixelPitch
+    int xp = 0, yp = 0;                 // the pinhole under the film point
+    const int nW = S.lensPinW, nH = S.lensPinH;
+    const bool pinholes = nW > 0 && nH > 0;
     lu *= firstAp;
     lv *= firstAp;
     V pol = v3(lu, lv, zI);
     if (S.lensPinhole[0] != -1 && S.lensPinhole[1] != -1 && S.lensPinhole[2] != -1)
         pol = v3(S.lensPinhole[0], S.lensPinhole[1], S.lensPinhole[2]);
+    else if (pinholes) {
+        // the pinhole array (:560-629): the superpixel under the film point, clamped
+        const int ppW = cam.xres / nW, ppH = cam.yres / nH;
+        xp = (int)(((double)imageX - .25) / ppW);
+        yp = (int)(((double)imageY - .25) / ppH);
+        xp = xp > nW - 1 ? nW - 1 : (xp < 0 ? 0 : xp);
+        yp = yp > nH - 1 ? nH - 1 : (yp < 0 ? 0 : yp);
+        const float *ph = sa(S.lensPinholes, (uint32_t)(3 * (xp * nH + yp)));
+        if (S.lensMicro) {   // the microlens's entrance square (:614-623)
+            pitch = width / nW;
+            pol = v3(luNoScale * pitch / 2.f + ph[0], lvNoScale * pitch / 2.f + ph[1], ph[2]);
+        } else pol = v3(ph[0], ph[1], ph[2]);
+    }
     Ray r;
     r.o = sp;
     r.d = vnorm(vsub(pol, r.o));
     r.mint = 0.f;
     r.maxt = INFINITY;
     r.time = 0.f;
+    // The surfaces in tracing order: with microlenses first their two spherical surfaces (:634-876;
+    // the radius from the thick-lens focal length, centred on the superpixel's pinhole, a miss
+    // passes unrefracted, diffraction around the microlens centre without the NaN check), then
+    // the lens elements, last first (a miss or a blocked ray has weight 0).  One loop body
+    // serves both, so the kernels that start lens paths carry one copy of it.
+    const int nMicro = (S.lensMicro && pinholes) ? 2 : 0;
+    float mRad = 0.f, mDist = 0.f, mN = 1.f, cx = 0.f, cy = 0.f;
+    const float thick = (float).01;
+    if (nMicro) {
+        const float *ph = sa(S.lensPinholes, (uint32_t)(3 * (xp * nH + yp)));
+        const float mFilmDist = S.lensFilmDist + pol.z;
+        const float mFocal = mFilmDist + thick / 2;
+        mN = (float)1.67;
+        const double nm1 = (double)(mN - 1);   // pow(microlensN - 1, 2): the exact square in double
+        const float oneOverR = (float)((-2 * (mN - 1) + __builtin_sqrt(4 * (nm1 * nm1) + 4 * (nm1 * nm1) * thick / (mN * mFocal))) /
+                                       (2 * (nm1 * nm1) * thick / mN));
+        mRad = 1 / oneOverR;
+        mDist = -S.lensFilmDist + mFilmDist;
+        cx = ph[0];
+        cy = ph[1];
+    }
     float lensDist = 0.f;
-    for (int i = S.lensN - 1; i >= 0; --i) {
-        const float4 e = (*sa(S.lensEl, (uint32_t)(i)));
-        const float rad = e.x, ap = e.w;
-        lensDist += e.y;
+    for (int k = 0; k < nMicro + S.lensN; ++k) {
+        const bool micro = k < nMicro;
+        const int i = S.lensN - 1 - (k - nMicro);   // the lens element (when !micro)
+        float rad, ap;
+        if (micro) {
+            mRad = -mRad;
+            rad = mRad;
+            ap = pitch;
+        } else {
+            const float4 e = (*sa(S.lensEl, (uint32_t)(i)));
+            rad = e.x;
+            ap = e.w;
+            lensDist += e.y;
+            cx = 0.f;
+            cy = 0.f;
+        }
         r.o = sp;
-        if (rad == 0) {   // aperture stop
+        if (!micro && rad == 0) {   // aperture stop
             const float tA = (i == S.lensN - 1) ? S.lensFilmDist / r.d.z : (lensDist - r.o.z) / (r.d.z);
             const V ai = v3(r.o.x + r.d.x * tA, r.o.y + r.d.y * tA, r.o.z + r.d.z * tA);
             const float dx = ai.x - S.lensApOff[0], dy = ai.y - S.lensApOff[1];
             if ((double)(dx * dx + dy * dy) > (double)(ap * ap) * .25) return 0.f;
             sp = ai;
-            if (S.lensDiffraction && !lens_diffract(st, ai, ap, wl, &r.d)) return 0.f;
-        } else {
-            float tHit = 0.f;
-            V nrm = v3(0.f, 0.f, 1.f);
-            if (!lens_el_hit(r, rad, v3(0.f, 0.f, rad - lensDist), &tHit, &nrm)) return 0.f;
-            const V ip = v3(tHit * r.d.x + r.o.x, tHit * r.d.y + r.o.y, tHit * r.d.z + r.o.z);
-            if (ip.x * ip.x + ip.y * ip.y >= ap * ap / 4.f) return 0.f;
-            const float n1 = e.z;
-            float n2 = 1;
-            if (i - 1 >= 0) {
-                n2 = (*sa(S.lensEl, (uint32_t)(i - 1))).z;
-                if (n2 == 0) n2 = (*sa(S.lensEl, (uint32_t)(i - 2))).z;
-            }
-            lens_snell(n1, n2, rad, nrm, &r, wl, S.lensChromatic);
-            sp = ip;
-            if (S.lensDiffraction && !lens_diffract(st, ip, ap, wl, &r.d)) return 0.f;
+            if (S.lensDiffraction && !lens_diffract(st, ai, 0.f, 0.f, ap, wl, &r.d, true)) return 0.f;
+            continue;
         }
+        float tHit = 0.f;
+        V nrm = v3(0.f, 0.f, 1.f), ip = v3(0.f, 0.f, 0.f);
+        const bool hit = lens_el_hit(r, rad, v3(-cx, -cy, rad - (micro ? mDist : lensDist)), &tHit, &nrm);
+        if (!hit && !micro) return 0.f;
+        if (hit) {
+            ip = v3(tHit * r.d.x + r.o.x, tHit * r.d.y + r.o.y, tHit * r.d.z + r.o.z);
+            // (centre 0: (x - 0) (x - 0) is the main lens's x x; (ap ap) / (2 2) its ap ap / 4.f)
+            if ((ip.x - cx) * (ip.x - cx) + (ip.y - cy) * (ip.y - cy) >= (ap * ap) / 4.f) return 0.f;
+            float n1, n2 = 1;
+            if (micro) {
+                n1 = k == 0 ? 1.f : mN;
+                n2 = k == 0 ? mN : 1.f;
+                if (k == 0) mDist += thick;
+            } else {
+                n1 = (*sa(S.lensEl, (uint32_t)(i))).z;
+                if (i - 1 >= 0) {
+                    n2 = (*sa(S.lensEl, (uint32_t)(i - 1))).z;
+                    if (n2 == 0) n2 = (*sa(S.lensEl, (uint32_t)(i - 2))).z;
+                }
+            }
+            lens_snell(S, n1, n2, rad, nrm, &r, wl);
+            sp = ip;
+        }
+        if (S.lensDiffraction && !lens_diffract(st, ip, cx, cy, ap, wl, &r.d, !micro)) return 0.f;
     }
     r.o = sp;
     r.time = lerpf(timeU, cam.shutter_open, cam.shutter_close);

@@ -97,7 +97,9 @@ PGD_INLINE void dl_vertex(const DevScene &S, const PathSoA &P, int slot, int d, 
     const int prim = P.fHit[(size_t)2 * d * c + slot];
     const float t = __int_as_float(P.fHit[(size_t)(2 * d + 1) * c + slot]);
     isect_fill(S, v.ray, prim, t, v.is, inst_rec(P, slot));
-    if (d == 0) {   // the camera ray's differentials are re-derived from its sample
+    if (d == 0 && S.camType != PBRTGPU_CAMERA_REALISTIC) {
+        // the perspective camera's differentials are re-derived from its sample; the lens camera's
+        // were stored in frame 0 by path_start (their lens trace stays out of these kernels)
         const uint32_t hp = P.hp[slot], s = P.smp[slot], spp = (uint32_t)S.spp, pxy = P.pix[slot];
         float u[2], lens[2];
         s2d(hp, 0, s, spp, u);

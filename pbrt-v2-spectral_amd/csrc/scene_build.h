@@ -166,6 +166,20 @@ static inline int scene_check(const pbrtgpu_flat_scene *s, std::string *err) {
         if (L.n_elements >= 2 && L.elements[2] == 0 && L.elements[4] != 0)
             SB_FAIL(PBRTGPU_E_INVALID, "lens element 0 has n == 0");
         if (s->camera.xres <= 0 || s->camera.yres <= 0) SB_FAIL(PBRTGPU_E_INVALID, "lens camera without film resolution");
+        if (L.num_pinholes_w > 0 && L.num_pinholes_h > 0) {
+            // GenerateRay divides by the pixels per superpixel (realisticDiffraction.cpp:566-570)
+            if (L.num_pinholes_w > s->camera.xres || L.num_pinholes_h > s->camera.yres)
+                SB_FAIL(PBRTGPU_E_INVALID, "more pinholes than film pixels");
+            if (!L.pinholes) SB_FAIL(PBRTGPU_E_INVALID, "pinhole array missing");
+        }
+        if (L.ior_eye) {
+            if (!L.eye_ior || s->n_bands == 3) SB_FAIL(PBRTGPU_E_INVALID, "IORforEyeEnabled without SampledSpectrum IOR curves");
+            // a band wavelength in the last interval would read c[N] in GetValueAtWavelength (spectrum.h:397)
+            if (s->renderer == PBRTGPU_RENDERER_SPECTRAL)
+                for (size_t b = 0; b < specTab.size(); ++b)
+                    if (specTab[b].z == s->n_bands - 1)
+                        SB_FAIL(PBRTGPU_E_UNSUPPORTED, "IORforEyeEnabled: a wave band's wavelength reads past the IOR spectra");
+        }
     }
     if (s->integrator == PBRTGPU_INTEGRATOR_DIRECT && s->dl_strategy != PBRTGPU_DL_ALL && s->dl_strategy != PBRTGPU_DL_ONE)
         SB_FAIL(PBRTGPU_E_INVALID, "unknown DirectLighting strategy");
@@ -253,6 +267,15 @@ static int scene_build(const pbrtgpu_flat_scene *s, int topNodes, DevScene &S, i
         for (int k = 0; k < 2; ++k) { S.lensApOff[k] = L.aperture_offset[k]; S.lensFilmC[k] = L.film_center[k]; }
         for (int k = 0; k < 3; ++k) S.lensPinhole[k] = L.pinhole_exit[k];
         SB_PUT(reinterpret_cast<const float4 *>(L.elements), (size_t)L.n_elements, &S.lensEl);
+        S.lensPinW = L.num_pinholes_w;
+        S.lensPinH = L.num_pinholes_h;
+        S.lensMicro = L.microlens;
+        S.lensEye = L.ior_eye;
+        S.lensPinholes = nullptr;
+        S.lensEyeIor = nullptr;
+        if (L.num_pinholes_w > 0 && L.num_pinholes_h > 0)
+            SB_PUT(L.pinholes, (size_t)L.num_pinholes_w * L.num_pinholes_h * 3, &S.lensPinholes);
+        if (L.ior_eye) SB_PUT(L.eye_ior, (size_t)4 * s->n_bands, &S.lensEyeIor);
     }
     S.dlK = 0;
     for (int i = 0; i < s->n_lights; ++i) {   // RoundUpPow2(max(1, nSamples)) per light

@@ -620,6 +620,16 @@ PGD_INLINE void path_start(const DevScene &S, const PathSoA &P, const ItemSrc &s
         RayDiff rd;
         dead = lens_ray_diff(S, imageX, imageY, lens[0], lens[1], timeU, path_wavelength(S, (int)item, s),
                              diff_key(hp, path_rng_index(S, item, s)), &r, &rd) == 0.f;
+        if (P.fDiff) {   // DirectLighting: frame 0's differentials (dl_vertex reads them there)
+            const size_t c = (size_t)P.cap;
+            float *fd = P.fDiff + slot;
+            const V vs[4] = {rd.rxo, rd.rxd, rd.ryo, rd.ryd};
+            for (int k = 0; k < 4; ++k) {
+                fd[(3 * k) * c] = vs[k].x;
+                fd[(3 * k + 1) * c] = vs[k].y;
+                fd[(3 * k + 2) * c] = vs[k].z;
+            }
+        }
         if (dead) {   // a ray no traversal hits; k_shade writes the zero radiance
             r.o = v3(0.f, 0.f, 0.f);
             r.d = v3(0.f, 0.f, 1.f);

@@ -16,6 +16,7 @@
 // Float expressions keep the reference's operand order (compile with -ffp-contract=off).
 #include "scene.h"
 #include "pbrthost.h"
+#include "eye_ior_tables.inc"
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -1619,20 +1620,34 @@ private:
     // 32-193): shutter times default to -1 (not swapped); the lens file is ReadFloatFile's
     // floats, the focal length then (radius, separation, n, aperture) per element, an aperture
     // stop (radius 0) taking "aperture_diameter"; "diffractionEnabled" (on by default) is
-    // GenerateRay's Gaussian perturbation per element.  The pinhole-array / microlens
-    // light-field modes and the eye IOR curves are refused.
+    // GenerateRay's Gaussian perturbation per element.  The light-field modes: "num_pinholes_w/h"
+    // (ints of float parameters, :73-75) a pinhole array whose positions Flat() computes at the film
+    // resolution, "microlens_enabled" (FindOneFloat, :76) a microlens per pinhole; "IORforEyeEnabled"
+    // (:82) the Gullstrand eye's IOR spectra (FromSampled of its curves, :196-205; eye_ior_tables.inc).
     void RealisticCamera(CameraParams *cp) {
         const ParamSet &p = cameraParams;
         cp->shutterOpen = p.FindOneFloat("shutteropen", -1.f);
         cp->shutterClose = p.FindOneFloat("shutterclose", -1.f);
         std::string spec = p.FindOneString("specfile", "");
         if (spec.empty()) throw std::runtime_error("No lens spec file supplied!");
-        if (p.FindOneBool("IORforEyeEnabled", false))
-            throw std::runtime_error("realisticDiffraction: IORforEyeEnabled is not supported");
-        if ((int)p.FindOneFloat("num_pinholes_w", -1) > 0 && (int)p.FindOneFloat("num_pinholes_h", -1) > 0)
-            throw std::runtime_error("realisticDiffraction: pinhole arrays / microlenses are not supported");
         pbrtgpu_lens &L = out->lens;
         memset(&L, 0, sizeof(L));
+        L.num_pinholes_w = (int)p.FindOneFloat("num_pinholes_w", -1);
+        L.num_pinholes_h = (int)p.FindOneFloat("num_pinholes_h", -1);
+        L.microlens = p.FindOneFloat("microlens_enabled", 0) != 0 ? 1 : 0;
+        L.ior_eye = p.FindOneBool("IORforEyeEnabled", false) ? 1 : 0;
+        out->eyeIor.clear();
+        if (L.ior_eye) {
+            const float(*t)[32] = nullptr;
+            const float(*t60)[60] = nullptr;
+            const float(*t30)[30] = nullptr;
+            if (ov.bands == 32) t = kEyeIor_32_395_715;
+            else if (ov.bands == 60) t60 = kEyeIor_60_395_715;
+            else if (ov.bands == 30) t30 = kEyeIor_30_400_700;
+            else throw std::runtime_error("realisticDiffraction: IORforEyeEnabled needs SampledSpectrum (30, 32 or 60 bands)");
+            for (int k = 0; k < 4; ++k)
+                for (int i = 0; i < ov.bands; ++i) out->eyeIor.push_back(t ? t[k][i] : t60 ? t60[k][i] : t30[k][i]);
+        }
         L.chromatic = p.FindOneBool("chromaticAberrationEnabled", false) ? 1 : 0;
         L.diffraction = p.FindOneBool("diffractionEnabled", true) ? 1 : 0;   // realisticDiffraction.cpp:61,128
         L.film_distance = p.FindOneFloat("filmdistance", 70.f);
@@ -1662,6 +1677,8 @@ private:
         // GenerateRay reads lensEls[i - 2].n when element i - 1 has n == 0 (realisticDiffraction.cpp:960-966)
         if (n >= 2 && out->lensEl[2] == 0 && out->lensEl[4] != 0)
             throw std::runtime_error("lens file " + spec + ": element 0 has n == 0");
+        if (L.num_pinholes_w > 0 && L.num_pinholes_h > 0 && (size_t)L.num_pinholes_w * L.num_pinholes_h > (1u << 24))
+            throw std::runtime_error("realisticDiffraction: pinhole array too large");
         out->cameraType = PBRTGPU_CAMERA_REALISTIC;
     }
 
@@ -1962,6 +1979,39 @@ void HostScene::Flat(pbrtgpu_flat_scene *f) const {
     f->lens = lens;
     f->lens.n_elements = (int)lensEl.size() / 4;
     f->lens.elements = lensEl.empty() ? nullptr : lensEl.data();
+    f->lens.eye_ior = lens.ior_eye && (int)eyeIor.size() == 4 * nBands ? eyeIor.data() : nullptr;
+    f->lens.pinholes = nullptr;
+    if (cameraType == PBRTGPU_CAMERA_REALISTIC && lens.num_pinholes_w > 0 && lens.num_pinholes_h > 0 && !lensEl.empty()) {
+        // RealisticDiffractionCamera's pinhole array (realisticDiffraction.cpp:248-304), at the film
+        // resolution the camera sees (getSensorWidth, :470-476): the superpixel pitch, the array's
+        // distance from the sensor by similar triangles with the last element's aperture, then per
+        // pinhole its chief ray from the superpixel centre through the lens centre, cut at that plane
+        const int W = lens.num_pinholes_w, H = lens.num_pinholes_h;
+        const float filmDistance = lens.film_distance;
+        const float aspectRatio = (float)camera.xres / (float)camera.yres;
+        const float width = lens.film_diag / sqrtf((1.f + 1.f / (aspectRatio * aspectRatio)));
+        const float sPixPitch = width / ((float)W);
+        const float lastAperture = lensEl[lensEl.size() - 1];
+        const float pinholeArrayDistance = sPixPitch * filmDistance / (lastAperture + sPixPitch);
+        const float pinholePosition = -filmDistance + pinholeArrayDistance;
+        lensPinholes.assign((size_t)W * H * 3, 0.f);
+        for (int i = 0; i < W; ++i)
+            for (int j = 0; j < H; ++j) {
+                const float cx = (float)(-(i - W / 2.0 + .5) * sPixPitch);
+                const float cy = (float)((j - H / 2.0 + .5) * sPixPitch);
+                const float cz = -filmDistance;
+                // Normalize(lensCenter - centerPos): v / Length() = v * (1 / sqrtf(|v|^2)) (geometry.h)
+                const float vx = 0.f - cx, vy = 0.f - cy, vz = 0.f - cz;
+                const float inv = 1.f / sqrtf(vx * vx + vy * vy + vz * vz);
+                const float dx = vx * inv, dy = vy * inv, dz = vz * inv;
+                const float tHit = pinholePosition / dz;
+                float *o = &lensPinholes[3 * ((size_t)i * H + j)];
+                o[0] = tHit * dx;
+                o[1] = tHit * dy;
+                o[2] = pinholePosition;
+            }
+        f->lens.pinholes = lensPinholes.data();
+    }
 }
 
 }  // namespace pbrtamd

@@ -11,7 +11,8 @@
 namespace pbrtamd {
 
 static const char kMagic[8] = {'P', 'B', 'R', 'T', 'P', 'A', 'C', 'K'};
-static const uint32_t kVersion = 9;   // 6: + merl tables; 7: + metadata ids; 8: + Renderer; 9: + lens diffraction (5-8 still load)
+static const uint32_t kVersion = 10;   // 6: + merl tables; 7: + metadata ids; 8: + Renderer; 9: + lens diffraction;
+                                       // 10: + pinhole array / microlens / eye IOR (5-9 still load)
 
 static bool W(gzFile f, const void *p, size_t n) {
     const char *c = (const char *)p;
@@ -85,6 +86,8 @@ bool SavePack(const HostScene &s, const std::string &path, std::string *err) {
     // v8: the camera type and RealisticDiffractionCamera
     int32_t ct = s.cameraType;
     ok = ok && W(f, &ct, 4) && W(f, &s.lens, sizeof(s.lens)) && WArr(f, s.lensEl);
+    // v10: the eye IOR spectra (the pinhole array is derived at the film resolution, Flat)
+    ok = ok && WArr(f, s.eyeIor);
     ok = (gzclose(f) == Z_OK) && ok;
     if (!ok && err) *err = "write error on " + path;
     return ok;
@@ -133,14 +136,19 @@ bool LoadPack(const std::string &path, HostScene *s, std::string *err) {
         ok = R(f, rnd, 12);
         if (ok) { s->renderer = rnd[0]; s->waveBands = rnd[1]; s->spectralSampling = rnd[2]; }
         int32_t ct = 0;
-        // v8's pbrtgpu_lens ended at fstop (56 bytes) + the elements pointer
-        const size_t lensBytes = ver >= 9 ? sizeof(s->lens) : 64;
-        char lensBuf[sizeof(s->lens) > 64 ? sizeof(s->lens) : 64];
+        // v8's pbrtgpu_lens ended at fstop (56 bytes) + the elements pointer; v9's at the elements
+        // pointer (72 bytes)
+        const size_t lensBytes = ver >= 10 ? sizeof(s->lens) : ver >= 9 ? 72 : 64;
+        char lensBuf[sizeof(s->lens) > 72 ? sizeof(s->lens) : 72];
         ok = ok && R(f, &ct, 4) && R(f, lensBuf, (unsigned)lensBytes) && RArr(f, s->lensEl);
-        memcpy(&s->lens, lensBuf, ver >= 9 ? sizeof(s->lens) : 56);
+        memcpy(&s->lens, lensBuf, ver >= 10 ? sizeof(s->lens) : ver >= 9 ? 64 : 56);
         if (ok) s->cameraType = ct;
         s->lens.elements = nullptr;
+        s->lens.pinholes = nullptr;
+        s->lens.eye_ior = nullptr;
     }
+    s->eyeIor.clear();
+    if (ok && ver >= 10) ok = RArr(f, s->eyeIor);
     gzclose(f);
     if (!ok && err) *err = "bad or truncated scene pack " + path;
     return ok;

@@ -74,6 +74,8 @@ struct HostScene {
     int cameraType = PBRTGPU_CAMERA_PERSPECTIVE;   // PBRTGPU_CAMERA_*
     pbrtgpu_lens lens = {};                   // RealisticDiffractionCamera (elements: lensEl)
     std::vector<float> lensEl;                // [elements][4]
+    std::vector<float> eyeIor;                // [4][nBands] IORforEyeEnabled: cornea, aqueous, lens, vitreous
+    mutable std::vector<float> lensPinholes;  // [w][h][3] pinhole array at the camera's film resolution (Flat)
     std::vector<uint32_t> primMeta;           // [prims][2]: primitiveId, materialId a hit reports
     std::vector<std::pair<uint32_t, std::string> > metaMesh;        // top-level primitives: id, shape name
     std::vector<std::pair<uint32_t, std::string> > metaMaterials;   // named materials: id, name (by name)

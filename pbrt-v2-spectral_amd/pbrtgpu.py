@@ -51,7 +51,9 @@ class Lens(ctypes.Structure):
                 ("film_diag", ctypes.c_float), ("curve_radius", ctypes.c_float),
                 ("aperture_offset", ctypes.c_float * 2), ("film_center", ctypes.c_float * 2),
                 ("pinhole_exit", ctypes.c_float * 3), ("focal_length", ctypes.c_float), ("fstop", ctypes.c_float),
-                ("diffraction", I32), ("reserved", I32), ("elements", P)]
+                ("diffraction", I32), ("reserved", I32), ("elements", P),
+                ("num_pinholes_w", I32), ("num_pinholes_h", I32), ("microlens", I32), ("ior_eye", I32),
+                ("pinholes", P), ("eye_ior", P)]
 
 
 class FlatScene(ctypes.Structure):
@@ -96,7 +98,7 @@ class RenderDesc(ctypes.Structure):
 STAT_PATHS, STAT_KERNEL_MS, STAT_ACCUM_MS, STAT_ZEROED, STAT_SPILLS, STAT_PASSES = 0, 1, 2, 3, 4, 5
 F_ACCUMULATE, F_COUNT_WORK = 1, 2
 KEEP_SEED = 0xFFFFFFFF
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 
 class Timing(ctypes.Structure):

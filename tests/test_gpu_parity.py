@@ -632,6 +632,39 @@ def test_realistic_diffraction_camera_vs_oracle(pg, monkeypatch, scene_file, kw)
     assert np.abs(film - of).max() / np.abs(of).max() < 1e-4
 
 
+@pytest.mark.parametrize("scene_file,kw", [
+    ("lens_pinholes.pbrt", dict()),
+    ("lens_pinholes.pbrt", dict(renderer="spectral", wave_bands=8, sampling="single")),
+    ("lens_microlens.pbrt", dict()),
+    ("lens_microlens.pbrt", dict(renderer="spectral", wave_bands=4, sampling="single", integrator="directlighting")),
+    ("eye.pbrt", dict()),
+    ("eye.pbrt", dict(renderer="spectral", wave_bands=8, sampling="single")),
+    ("eye.pbrt", dict(renderer="spectral", wave_bands=10, sampling="sampler", integrator="directlighting"))])
+def test_light_field_and_eye_cameras_vs_oracle(pg, scene_file, kw):
+    """The RealisticDiffractionCamera's light-field modes and the Gullstrand eye on the GPU
+    against the oracle, sample by sample and film, at the scenes' own film size (the pinhole
+    array depends on it): an 8 x 6 pinhole array (realisticDiffraction.cpp:248-304, 560-629),
+    the same with a two-surface microlens per pinhole and diffraction on every surface
+    (:614-876), and IORforEyeEnabled (:196-205, 357-377: under the SpectralRenderer each band
+    refracts with the ocular media's IOR at its wavelength).  PARITY UNPINNED vs the reference
+    (the camera's TU needs GSL); the device source is also replayed on the CPU
+    against the oracle (tests/test_hostsan.py)."""
+    here = os.path.join(os.path.dirname(os.path.abspath(__file__)), "scenes")
+    scene = pg.Scene.load(os.path.join(here, scene_file), spp=4, maxdepth=5, **kw)
+    keys = _keys(scene)
+    with pg.Device(0) as d:
+        d.upload(scene)
+        L = d.trace_paths(keys)
+        d.render()
+        film = d.film()
+    o = pg.oracle()
+    Lo = o.trace_paths(scene, keys)
+    assert np.any(Lo != 0)
+    assert np.array_equal(L.view(np.int32), Lo.view(np.int32))
+    of, _ = o.render(scene)
+    assert np.array_equal(film.view(np.int32), of.view(np.int32))
+
+
 @pytest.mark.parametrize("name", ["killeroo_rgb_paths_48x40s4", "killeroo_rgb_keys_c1_400x400s64"])
 def test_rgb_build_vs_reference_golden(pg, name):
     """C1 (BASELINE configs[0]): the RGBSpectrum build (3 channels, NB = 3 kernels) against the

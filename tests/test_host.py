@@ -228,7 +228,7 @@ def test_realistic_diffraction_camera(pg, tmp_path):
     """Camera "realisticDiffraction" (realisticDiffraction.cpp:32-193): the lens file's focal
     length and elements (an aperture stop takes aperture_diameter), the camera parameters and
     its -1 shutter defaults reach the flat scene and the pack (diffractionEnabled: false here,
-    true by default); the eye IOR curves and pinhole arrays are refused; the .dat header's line 2
+    true by default; no pinhole array or eye curves); the .dat header's line 2
     carries focal length, f-stop and field of view (spectralImage.cpp:356-360)."""
     here = os.path.join(os.path.dirname(os.path.abspath(__file__)), "scenes")
     s = pg.Scene.load(os.path.join(here, "lens.pbrt"))
@@ -247,18 +247,7 @@ def test_realistic_diffraction_camera(pg, tmp_path):
     assert t.flat.camera_type == 1 and np.array_equal(el, el2) and t.flat.lens.fstop == f.lens.fstop
     assert f.lens.diffraction == 0 and t.flat.lens.diffraction == 0
     assert pg.Scene.load(os.path.join(here, "lens_diffraction.pbrt")).flat.lens.diffraction == 1
-    src = open(os.path.join(here, "lens.pbrt")).read()
-    for bad, msg in [('"bool diffractionEnabled" "false" "bool IORforEyeEnabled" "true"', "IORforEye"),
-                     ('"bool diffractionEnabled" "false" "float num_pinholes_w" [4] "float num_pinholes_h" [4]',
-                      "pinhole")]:
-        body = src.replace('"bool diffractionEnabled" "false"', bad)
-        p = os.path.join(here, "_lens_bad.pbrt")   # next to the lens file it names
-        try:
-            open(p, "w").write(body)
-            with pytest.raises(RuntimeError, match=msg):
-                pg.Scene.load(p)
-        finally:
-            os.remove(p)
+    assert f.lens.num_pinholes_w == -1 and not f.lens.pinholes and not f.lens.ior_eye and not f.lens.eye_ior
     film = np.zeros((s.height, s.width, s.bands), np.float32)
     dat = str(tmp_path / "lens.dat")
     s.write_dat(dat, film)
@@ -267,6 +256,104 @@ def test_realistic_diffraction_camera(pg, tmp_path):
     w = np.float32(43.27) / np.sqrt(np.float32(1) + np.float32(1) / (a * a))
     fov = np.float32(2 * float(np.arctan(np.float32(w / np.float32(100.0)))) / 3.1415926539 * 180)
     assert line2 == "%g %g %g" % (50.0, f.lens.fstop, fov)
+
+
+def _pinhole_array(W, H, xres, yres, film_diag, film_dist, last_ap):
+    """RealisticDiffractionCamera's pinholeArray (realisticDiffraction.cpp:248-304) restated in
+    numpy float32 / double arithmetic"""
+    f = np.float32
+    a = f(xres) / f(yres)
+    width = f(film_diag) / np.sqrt(f(1) + f(1) / (a * a))
+    pitch = width / f(W)
+    dist = pitch * f(film_dist) / (f(last_ap) + pitch)
+    pos = -f(film_dist) + dist
+    out = np.zeros((W, H, 3), np.float32)
+    for i in range(W):
+        for j in range(H):
+            cx = f(-((i - W / 2.0 + .5) * float(pitch)))
+            cy = f((j - H / 2.0 + .5) * float(pitch))
+            v = [f(0) - cx, f(0) - cy, f(0) + f(film_dist)]
+            inv = f(1) / np.sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2])
+            d = [c * inv for c in v]
+            t = pos / d[2]
+            out[i, j] = (t * d[0], t * d[1], pos)
+    return out
+
+
+def test_light_field_and_eye_front_end(pg, tmp_path):
+    """realisticDiffraction's light-field and eye parameters: "num_pinholes_w/h" (ints of floats)
+    give the pinhole array, computed at the film resolution the scene is loaded with (the
+    constructor's similar triangles, realisticDiffraction.cpp:248-304); "microlens_enabled";
+    "IORforEyeEnabled" the four ocular IOR spectra (FromSampled band averages); packs keep them."""
+    here = os.path.join(os.path.dirname(os.path.abspath(__file__)), "scenes")
+    for xres, yres in ((64, 48), (40, 30)):
+        s = pg.Scene.load(os.path.join(here, "lens_pinholes.pbrt"), xres=xres, yres=yres)
+        L = s.flat.lens
+        assert (L.num_pinholes_w, L.num_pinholes_h, L.microlens, L.ior_eye) == (8, 6, 0, 0)
+        ph = np.ctypeslib.as_array(ctypes.cast(L.pinholes, ctypes.POINTER(ctypes.c_float)), (8, 6, 3))
+        ref = _pinhole_array(8, 6, xres, yres, 43.27, 36.77, 20.0)
+        assert np.array_equal(ph.view(np.int32), ref.view(np.int32))
+        assert (ph[:4, :, 0] > 0).all() and (ph[4:, :, 0] < 0).all()   # i = 0: the +x film side
+    m = pg.Scene.load(os.path.join(here, "lens_microlens.pbrt"))
+    assert m.flat.lens.microlens == 1 and m.flat.lens.diffraction == 1
+    out = str(tmp_path / "mic.pack")
+    m.save_pack(out)
+    m2 = pg.Scene.load(out, xres=40, yres=30)
+    assert m2.flat.lens.microlens == 1 and m2.flat.lens.num_pinholes_w == 8
+    ph2 = np.ctypeslib.as_array(ctypes.cast(m2.flat.lens.pinholes, ctypes.POINTER(ctypes.c_float)), (8, 6, 3))
+    assert np.array_equal(ph2, _pinhole_array(8, 6, 40, 30, 43.27, 36.77, 20.0))
+    for bands in (32, 60, 30):
+        e = pg.Scene.load(os.path.join(here, "eye.pbrt"), bands=bands)
+        assert e.flat.lens.ior_eye == 1 and e.flat.lens.n_elements == 5
+        ior = np.ctypeslib.as_array(ctypes.cast(e.flat.lens.eye_ior, ctypes.POINTER(ctypes.c_float)), (4, bands))
+        # cornea, aqueous, lens, vitreous: normal dispersion (n falls with the wavelength)
+        assert (np.diff(ior, axis=1) <= 1e-6).all() and (ior[:, 0] > ior[:, -1]).all()
+        assert 1.37 < ior[0, bands // 2] < 1.38 and 1.41 < ior[2, bands // 2] < 1.43
+        out = str(tmp_path / ("eye%d.pack" % bands))
+        e.save_pack(out)
+        e2 = pg.Scene.load(out)
+        ior2 = np.ctypeslib.as_array(ctypes.cast(e2.flat.lens.eye_ior, ctypes.POINTER(ctypes.c_float)), (4, bands))
+        assert np.array_equal(ior, ior2)
+    with pytest.raises(RuntimeError, match="IORforEye|RGB build"):   # the IOR curves are SampledSpectra
+        pg.Scene.load(os.path.join(here, "eye.pbrt"), bands=3)
+
+
+@pytest.mark.reference
+def test_eye_ior_tables_from_reference_curves(pg):
+    """host/eye_ior_tables.inc (tools/gen_eye_ior.cpp) against an independent numpy float32
+    restatement of Spectrum::FromSampled (AverageSpectrumSamples, spectrum.cpp:50-83) over the
+    curves of the reference's realisticDiffraction.h"""
+    import re
+    src = open("/root/reference/src/cameras/realisticDiffraction.h").read()
+
+    def arr(name):
+        body = re.search(r"const float %s\[\d+\]\s*=\s*\{([^}]*)\}" % name, src).group(1)
+        return np.array([np.float32(float(t)) for t in body.replace("\n", " ").split(",") if t.strip()], np.float32)
+
+    f = np.float32
+    lam = arr("eyeWaveSamples")
+    here = os.path.join(os.path.dirname(os.path.abspath(__file__)), "scenes")
+    for bands, l0, l1 in ((32, 395, 715), (30, 400, 700)):
+        e = pg.Scene.load(os.path.join(here, "eye.pbrt"), bands=bands)
+        ior = np.ctypeslib.as_array(ctypes.cast(e.flat.lens.eye_ior, ctypes.POINTER(ctypes.c_float)), (4, bands))
+        for k, name in enumerate(["corneaIORraw", "aqueousIORraw", "lensIORraw", "vitreousIORraw"]):
+            v = arr(name)
+            for i in range(bands):
+                w0 = (f(1) - f(i) / f(bands)) * f(l0) + (f(i) / f(bands)) * f(l1)
+                w1 = (f(1) - f(i + 1) / f(bands)) * f(l0) + (f(i + 1) / f(bands)) * f(l1)
+                j = 0
+                while w0 > lam[j + 1]:
+                    j += 1
+                acc = f(0)
+                while j + 1 < len(lam) and w1 >= lam[j]:
+                    a, b = max(w0, lam[j]), min(w1, lam[j + 1])
+
+                    def interp(w):
+                        t = (w - lam[j]) / (lam[j + 1] - lam[j])
+                        return (f(1) - t) * v[j] + t * v[j + 1]
+                    acc = acc + (f(0.5) * (interp(a) + interp(b))) * (b - a)
+                    j += 1
+                assert ior[k, i] == acc / (w1 - w0), (name, bands, i)
 
 
 def test_rgb_build_front_end(pg):

@@ -24,6 +24,10 @@ from conftest import GOLDEN, PACKS, ROOT
 HS = os.path.join(ROOT, "tools", "hostsan")
 # the RealisticDiffractionCamera with diffraction on (an absolute path: os.path.join keeps it)
 LENS_D = os.path.join(ROOT, "tests", "scenes", "lens_diffraction.pbrt")
+# its light-field modes (pinhole array; microlenses with diffraction) and the schematic eye
+LF_P = os.path.join(ROOT, "tests", "scenes", "lens_pinholes.pbrt")
+LF_M = os.path.join(ROOT, "tests", "scenes", "lens_microlens.pbrt")
+EYE = os.path.join(ROOT, "tests", "scenes", "eye.pbrt")
 
 
 def _build(target):
@@ -67,12 +71,18 @@ CASES = [
     ("coverage-b30.pack", dict(xres=40, yres=30, spp=4, maxdepth=6)),
     (LENS_D, dict(xres=40, yres=30, spp=4, maxdepth=5)),
     (LENS_D, dict(xres=32, yres=24, spp=2, maxdepth=5, renderer="spectral", wave_bands=8, sampling="single")),
+    (LF_P, dict(xres=64, yres=48, spp=2, maxdepth=5)),
+    (LF_M, dict(xres=64, yres=48, spp=4, maxdepth=5, renderer="spectral", wave_bands=4, sampling="single")),
+    (EYE, dict(xres=48, yres=36, spp=2, maxdepth=5)),
+    (EYE, dict(xres=48, yres=36, spp=2, maxdepth=5, renderer="spectral", wave_bands=8, sampling="single")),
+    (LENS_D, dict(xres=32, yres=24, spp=2, maxdepth=5, integrator="directlighting", strategy="all")),
 ]
 
 
 @pytest.mark.parametrize("pack,a", CASES, ids=["dl_all_md6", "dl_one", "dl_killeroo", "path_coverage", "path_anim",
                                                "path_bunny", "path_metal60", "metadata", "path_coverage_b30",
-                                               "lens_diffraction", "lens_diffraction_spectral"])
+                                               "lens_diffraction", "lens_diffraction_spectral", "lens_pinholes",
+                                               "lens_microlens_spectral", "eye", "eye_spectral", "lens_diffraction_dl"])
 def test_replay_matches_oracle(pg, tmp_path, pack, a):
     exe = _build("shade_host")
     scene = pg.Scene.load(os.path.join(PACKS, pack), **a)

@@ -90,6 +90,9 @@ static void unpoison_flat(const pbrtgpu_flat_scene *s) {
     u(s->merl, 4 * (size_t)std::max(0, s->n_merl_floats));
     u(s->prim_meta, 8 * (size_t)s->n_prims);
     u(s->lens.elements, 16 * (size_t)std::max(0, s->lens.n_elements));
+    if (s->lens.num_pinholes_w > 0 && s->lens.num_pinholes_h > 0)
+        u(s->lens.pinholes, 12 * (size_t)s->lens.num_pinholes_w * (size_t)s->lens.num_pinholes_h);
+    if (s->lens.ior_eye) u(s->lens.eye_ior, 16 * (size_t)s->n_bands);
 }
 #endif
 
