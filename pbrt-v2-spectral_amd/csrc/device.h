@@ -246,7 +246,9 @@ __device__ __attribute__((noinline)) uint32_t mt_ext_draw(uint32_t k, uint32_t s
     return mt_temper(mt[k % 624]);
 }
 PGD_INLINE uint32_t mt_uint(MT &r) {   // requires r.init (mt_init)
-    if (__builtin_expect(r.k >= 227, 0)) {   // no ext row: refused at upload (maxdepth)
+    if (__builtin_expect(r.k >= 227, 0)) {
+        // without an ext row (run_wavefront allocates them when the integrator's maxdepth can get
+        // here) the draw is 0 and mt_store flags the run (CNT_ERR -> PBRTGPU_E_STATE)
         const uint32_t y = r.ext ? mt_ext_draw(r.k, r.seed, r.ext) : 0u;
         r.k++;
         return y;

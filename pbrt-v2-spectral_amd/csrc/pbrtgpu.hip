@@ -23,6 +23,7 @@
 #include <cstdio>
 #include <mutex>
 #include <thread>
+#include <chrono>
 #include <atomic>
 #include "pbrtgpu.h"
 #include "device.h"
@@ -1157,6 +1158,7 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
         // the next lane whose batch has completed: the host never blocks on one lane while the
         // other lane's queue has run dry (it would idle until that wait ended)
         int l = -1;
+        int spins = 0;
         for (;;) {
             for (int k = 0; k < nl && l < 0; ++k) {
                 const int i = (rr + k) % nl;
@@ -1166,7 +1168,10 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
                 else if (qe != hipErrorNotReady) HIPCHK(qe);
             }
             if (l >= 0) break;
-            std::this_thread::yield();
+            // a few empty polls, then short sleeps: a batch of passes takes milliseconds, and a host
+            // thread per device (render_multi) should not burn a core for the whole frame
+            if (++spins > 64) std::this_thread::sleep_for(std::chrono::microseconds(20));
+            else std::this_thread::yield();
         }
         rr = l + 1;
         {
@@ -1191,6 +1196,13 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
                 fprintf(stderr, "pass_log lane %d after pass %d: closest queue %u shadow queue %u items taken %u of %u\n", l,
                         r.passes - 1, L.hostCnt[CNT_QC(r.q)], L.hostCnt[CNT_QS(r.q)], L.hostCnt[CNT_NEXT], r.src.nItems);
             int q = r.q;
+            if (L.hostCnt[CNT_ERR])
+                return fail(PBRTGPU_E_STATE, "a path drew past 227 MT19937 outputs without its state row");
+            // every live slot ends a pass with a ray queued, so the drain's list fits the grid sized
+            // from the last queue sizes; a longer list would leave slots unshaded (their beta / A / B
+            // buffers then rotate under them): refuse instead
+            if (r.drain && (uint64_t)L.hostCnt[CNT_LIVE] > (uint64_t)r.liveGrid * kShadeBlock)
+                return fail(PBRTGPU_E_STATE, "drain: more live slots than the shade grid covers");
             if (L.hostCnt[CNT_QC(q)] == 0 && L.hostCnt[CNT_QS(q)] == 0) {
                 r.done = true;
                 --live;

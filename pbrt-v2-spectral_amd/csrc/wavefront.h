@@ -70,7 +70,9 @@ enum { RAY_C = 0, RAY_M = 1, RAY_S = 2 };
 #define CNT_QC(q) (32 * (q))          // closest-hit queue size, queue set q = 0, 1
 #define CNT_QS(q) (64 + 32 * (q))     // shadow queue size
 #define CNT_QT(q) (224 + 32 * (q))    // MT-window list size (qT): k_mt_init of set q clears set q ^ 1
-enum { CNT_NEXT = 128, CNT_ZEROED = 160, CNT_WORK = 192, CNT_LIVE = 288, CNT_WORDS = 320 };
+// CNT_ERR: nonzero when a path drew past MT output 227 without its full-state row (mt_store), which
+// the host turns into PBRTGPU_E_STATE instead of a silently wrong radiance
+enum { CNT_NEXT = 128, CNT_ZEROED = 160, CNT_WORK = 192, CNT_LIVE = 288, CNT_ERR = 320, CNT_WORDS = 352 };
 enum { W_RAYS = 0, W_SHADOW = 1, W_NODES_C = 2, W_NODES_S = 3, W_TRIS_C = 4, W_TRIS_S = 5, W_QUADS_C = 6, W_QUADS_S = 7,
        W_HITS = 8, W_RAYS_M = 9, W_HITS_M = 10, W_COUNT = 12 };
 
@@ -184,6 +186,7 @@ PGD_INLINE void mt_load(const PathSoA &P, int slot, uint32_t fl, MT &r) {
 }
 PGD_INLINE void mt_store(const PathSoA &P, int slot, const MT &r) {
     const uint32_t c = (uint32_t)P.cap, s = (uint32_t)slot;
+    if (__builtin_expect(r.k >= 227u && !r.ext, 0)) atomicOr(&P.cnt[CNT_ERR], 1u);   // (mt_uint returned 0s)
     *sa(P.mt, s) = r.k; *sa(P.mt, c + s) = r.a; *sa(P.mt, 2 * c + s) = r.b; *sa(P.mt, 3 * c + s) = r.m;
 }
 // The recurrence window of a path before its first MT draw (output 0: mt[0], mt[1], mt[397] of its

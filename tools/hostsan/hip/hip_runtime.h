@@ -67,6 +67,7 @@ inline float __logf(float x) { return std::log(x); }
 inline float __powf(float x, float y) { return std::pow(x, y); }
 
 template <class T> inline T atomicAdd(T *p, T v) { const T o = *p; *p = o + v; return o; }
+template <class T> inline T atomicOr(T *p, T v) { const T o = *p; *p = o | v; return o; }
 
 // HIP's global min / max overloads
 inline int min(int a, int b) { return a < b ? a : b; }

@@ -241,6 +241,7 @@ static int run(const DevScene &S, PathSoA &P, const ItemSrc &src, int nSlots, fl
     int q = 0;
     for (int64_t pass = 0;; ++pass) {
         if (pass > maxPasses) { *err = "wavefront did not drain"; return 3; }
+        if (P.cnt[CNT_ERR]) { *err = "a path drew past 227 MT19937 outputs without its state row"; return 3; }
         trace(q);
         const int nq = q ^ 1;
         P.pass = (P.pass + 1) % 3;
