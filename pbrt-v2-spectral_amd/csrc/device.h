@@ -311,6 +311,8 @@ struct DevScene {
     const float4 *wnodes;             // child-in-parent BVH: 4 x float4 per interior node (wide_bvh)
     const uint32_t *nodeRef;          // per node: its wide-node index, or a leaf reference (WREF_*)
     int nTop;                         // wide nodes [0, nTop): the BVH's top levels, breadth-first (LDS in k_trace_pt)
+    const float4 *w4nodes;            // 4-wide copy for the shadow queries (wide4_bvh): 8 x float4 per node
+    int w4N, w4Stack;                 // its nodes (0: none) and the any-hit stack bound (3 per level + 1)
     const pbrtgpu_prim *prims;
     const DevTri *primTri;            // per prim (triangles only meaningful)
     const pbrtgpu_triangle *tris;
@@ -976,6 +978,35 @@ PGD_INLINE bool bvh_intersectP(const DevScene &S, Stack &st, const Ray &ray) {
     int hp;
     float ht;
     return bvh_walk<true, INST>(S, st, 0, 0u, r, &hp, &ht);
+}
+// The shadow query on the 4-wide BVH copy (scene_build.h wide4_bvh) as one plain walk: the root box,
+// then per node the child boxes k_trace_s4 tests and the same leaves (host replay and tests; the
+// GPU runs k_trace_s4).  st.base must hold S.w4Stack entries.
+PGD_INLINE bool bvh_intersectP4(const DevScene &S, Stack &st, const Ray &ray0) {
+    Ray ray = ray0;
+    const V invDir = v3(1.f / ray.d.x, 1.f / ray.d.y, 1.f / ray.d.z);
+    const int neg[3] = {invDir.x < 0, invDir.y < 0, invDir.z < 0};
+    if (!bbox_hit((*sa(S.nodes, 0u)), (*sa(S.nodes, 1u)), ray, invDir, neg)) return false;
+    int todo = 0, prim = -1;
+    float thit = INFINITY;
+    st.set(todo++, 0u);
+    while (todo > 0) {
+        const uint32_t ref = st.get(--todo);
+        if (ref & WREF_LEAF) {
+            const uint32_t np = (ref >> WREF_NP_SHIFT) & WREF_NP_MASK, off = ref & WREF_OFF_MASK;
+            for (uint32_t i = 0; i < np; ++i)
+                if (prim_test<true, false>(S, st, todo, (int)(off + i), ray, &prim, &thit)) return true;
+            continue;
+        }
+        const float4 *w = sa(S.w4nodes, (uint32_t)(8 * (size_t)ref));
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t r = __float_as_uint(w[2 * k].w);
+            float t = 0.f;
+            if (r != 0xffffffffu && slab_enter(w[2 * k], w[2 * k + 1], ray, invDir, neg, &t) && t < ray.maxt)
+                st.set(todo++, r);
+        }
+    }
+    return false;
 }
 // im: the path's instance transforms (PathSoA::instM, per instance 8 float4: world->primitive
 // m rows, then its inverse), or null in scenes without instances

@@ -333,6 +333,124 @@ __global__ __launch_bounds__(kTraceBlock) PGD_TRACE_ATTR void k_trace_pt(DevScen
     }
 }
 
+// Shadow queries of one pass on the 4-wide BVH copy (BVHAccel::IntersectP, bvh.cpp:435-481;
+// scene_build.h wide4_bvh): k_trace_pt<true>'s persistent ray-replacement scheme, one 4-wide node
+// per loop trip -- its up to four child boxes tested with the reference's slab test, the first hit
+// child taken next and the others pushed -- then, on a leaf, its primitives until one is hit.  The
+// answer (occluded or not) is the reference's: the primitives whose boxes all pass are the same
+// (wide4_bvh), and any-hit does not depend on the order they are tested in.  Half as many
+// dependent node loads per ray as the binary walk.
+template <bool STATS>
+__global__ __launch_bounds__(kTraceBlock) PGD_TRACE_ATTR void k_trace_s4(DevScene S, PathSoA P, int q, int refill, int ring, uint2 *__restrict__ spill) {
+    __shared__ uint32_t sref[kStackLDS * kTraceBlock];
+    uint2 *gsp = spill + (size_t)(blockIdx.x * blockDim.x + threadIdx.x) * S.w4Stack;
+    int bottom = 0;
+    Stack st;
+    const uint32_t n = P.cnt[CNT_QS(q)];
+    const uint32_t *Q = P.qS + (size_t)q * P.rcap;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = (gridDim.x * blockDim.x) >> 6;
+    uint32_t next = (uint32_t)((uint64_t)n * wave / nw);
+    const uint32_t end = (uint32_t)((uint64_t)n * (wave + 1) / nw);
+    bool active = false;
+    int slot = 0, todo = 0, prim = -1;
+    uint32_t ref = 0;
+    float thit = INFINITY;
+    Ray ray;
+    V invDir = v3(0.f, 0.f, 0.f);
+    int neg[3] = {0, 0, 0};
+    const uint32_t NONE = 0xffffffffu;
+    auto push = [&](uint32_t r) {
+        if (todo - bottom == ring) {   // ring full: oldest entry to HBM
+            gsp[bottom] = make_uint2(sref[(bottom & (ring - 1)) * kTraceBlock + threadIdx.x], 0u);
+            ++bottom;
+        }
+        sref[(todo & (ring - 1)) * kTraceBlock + threadIdx.x] = r;
+        ++todo;
+    };
+    for (;;) {
+        const unsigned long long idle = __ballot(!active);
+        const uint32_t nIdle = (uint32_t)__popcll(idle);
+        if (next < end && (nIdle >= (uint32_t)refill || nIdle == 64u)) {
+            if (!active) {
+                const uint32_t i = next + (uint32_t)__popcll(idle & ((1ull << lane) - 1ull));
+                if (i < end) {
+                    slot = (int)Q[i];
+                    ray = ray_load(P, RAY_S, slot);
+                    invDir = v3(1.f / ray.d.x, 1.f / ray.d.y, 1.f / ray.d.z);
+                    neg[0] = invDir.x < 0; neg[1] = invDir.y < 0; neg[2] = invDir.z < 0;
+                    prim = -1;
+                    thit = INFINITY;
+                    todo = 0;
+                    bottom = 0;
+                    st.cShadow++;
+                    st.cNodes++;
+                    if (bbox_hit((*sa(S.nodes, (uint32_t)(0))), (*sa(S.nodes, (uint32_t)(1))), ray, invDir, neg)) {
+                        ref = 0u;   // the 4-wide root (the root's grandchildren)
+                        active = true;
+                    } else P.occ[slot] = 0u;
+                }
+            }
+            next = min(end, next + nIdle);
+        }
+        if (!__ballot(active)) {
+            if (next >= end) break;
+            continue;
+        }
+        if (active) {
+            bool occluded = false;
+            if (!(ref & WREF_LEAF)) {
+                const float4 *w = sa(S.w4nodes, (uint32_t)(8 * (size_t)ref));
+                float4 b[8];
+#pragma unroll
+                for (int k = 0; k < 8; ++k) b[k] = w[k];
+                st.cNodes++;
+                uint32_t nxt = NONE;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const uint32_t r = __float_as_uint(b[2 * k].w);
+                    float t = 0.f;
+                    if (r != NONE && slab_enter(b[2 * k], b[2 * k + 1], ray, invDir, neg, &t) && t < ray.maxt) {
+                        if (nxt == NONE) nxt = r;
+                        else push(r);
+                    }
+                }
+                ref = nxt;
+            }
+            if (ref != NONE && (ref & WREF_LEAF)) {
+                const uint32_t np = (ref >> WREF_NP_SHIFT) & WREF_NP_MASK, off = ref & WREF_OFF_MASK;
+                for (uint32_t i = 0; i < np; ++i)
+                    if (prim_test<true, false>(S, st, todo, (int)(off + i), ray, &prim, &thit)) {
+                        occluded = true;
+                        break;
+                    }
+                ref = NONE;
+            }
+            bool done = occluded;
+            if (!occluded && ref == NONE) {
+                if (todo > 0) {
+                    --todo;
+                    if (todo < bottom) {
+                        ref = gsp[todo].x;
+                        bottom = todo;
+                    } else ref = sref[(todo & (ring - 1)) * kTraceBlock + threadIdx.x];
+                } else done = true;
+            }
+            if (done) {
+                active = false;
+                P.occ[slot] = occluded ? 1u : 0u;
+            }
+        }
+    }
+    if (STATS) {
+        unsigned long long *w = reinterpret_cast<unsigned long long *>(P.cnt + CNT_WORK);
+        atomicAdd(&w[W_SHADOW], (unsigned long long)st.cShadow);
+        atomicAdd(&w[W_NODES_S], (unsigned long long)st.cNodes);
+        atomicAdd(&w[W_TRIS_S], (unsigned long long)st.cTris);
+        atomicAdd(&w[W_QUADS_S], (unsigned long long)st.cQuads);
+    }
+}
+
 // Ray queries of one pass WITH instanced primitives (TransformedPrimitive over nested BVHs,
 // primitive.cpp:87-116, C5): k_trace_pt's persistent ray-replacement scheme with a two-level
 // walk per lane.  Level 0 walks the top-level BVH in world space; a top-level leaf's
@@ -857,6 +975,7 @@ struct pbrtgpu_ctx {
     int numCUs = 256;
     int ptBlocksPerCU = 0;    // occupancy of k_trace_pt closest (computed on first use)
     int ptBlocksPerCUS = 0;   // occupancy of k_trace_pt shadow
+    int s4BlocksPerCU = 0;    // occupancy of k_trace_s4 (shadow queries on the 4-wide BVH)
     int instBlocksPerCU = 0, instBlocksPerCUS = 0;   // occupancy of k_trace_inst closest / shadow
     int ring = kStackLDS;     // LDS ring entries in use (PBRTGPU_STACK_LDS: tests force HBM spills)
     int refill = 16;          // idle lanes that trigger ray replacement in k_trace_pt (PBRTGPU_REFILL)
@@ -930,6 +1049,10 @@ static bool pass_log() {
 static bool mt_ext_forced() {
     const char *e = getenv("PBRTGPU_MT_EXT");
     return e && atoi(e) != 0;
+}
+static bool shadow4_on() {
+    const char *e = getenv("PBRTGPU_SHADOW4");
+    return !e || atoi(e) != 0;
 }
 static bool drain_list_on() {
     const char *e = getenv("PBRTGPU_DRAIN_LIST");
@@ -1053,6 +1176,9 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
         HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&b1, k_trace_pt<true, false>, kTraceBlock, 0));
         HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&b2, k_trace_inst<false, false>, kTraceBlock, 0));
         HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&b3, k_trace_inst<true, false>, kTraceBlock, 0));
+        int b4 = 0;
+        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&b4, k_trace_s4<false>, kTraceBlock, 0));
+        c->s4BlocksPerCU = std::max(1, b4);
         c->ptBlocksPerCU = std::max(1, b0);
         c->ptBlocksPerCUS = std::max(1, b1);
         c->instBlocksPerCU = std::max(1, b2);
@@ -1062,8 +1188,11 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
     // one-ray-per-thread bvh_walk kernels, kept for A/B parity tests)
     const bool instPT = inst && !legacy_inst_walk();
     const uint32_t ptGrid = (uint32_t)(c->numCUs * (instPT ? c->instBlocksPerCU : c->ptBlocksPerCU));
-    const uint32_t ptGridS = (uint32_t)(c->numCUs * (instPT ? c->instBlocksPerCUS : c->ptBlocksPerCUS));
-    const size_t spillLane = (size_t)std::max(ptGrid, ptGridS) * kTraceBlock * c->stackDepth;   // uint2 per kernel
+    // shadow queries on the 4-wide BVH copy (scenes without instances; PBRTGPU_SHADOW4=0: the binary walk)
+    const bool s4 = !inst && c->S.w4N > 0 && shadow4_on();
+    const uint32_t ptGridS = (uint32_t)(c->numCUs * (instPT ? c->instBlocksPerCUS : s4 ? c->s4BlocksPerCU : c->ptBlocksPerCUS));
+    const size_t spillLane = (size_t)std::max(ptGrid, ptGridS) * kTraceBlock *
+                             (size_t)std::max(c->stackDepth, s4 ? c->S.w4Stack : 0);   // uint2 per kernel
     // scenes without measured BRDFs, textures and environment lights run the variant with
     // that code compiled out (fewer registers, no kd-tree stack)
     // the DirectLighting integrator has its own step (all features compiled in)
@@ -1252,7 +1381,9 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
                     } else if (inst) {
                         if (countWork) hipLaunchKernelGGL((k_trace_shadow<true, true>), dim3(traceGrid), dim3(kTraceBlock), ldsS, L.s, c->S, P, q);
                         else hipLaunchKernelGGL((k_trace_shadow<false, true>), dim3(traceGrid), dim3(kTraceBlock), ldsS, L.s, c->S, P, q);
-                    } else if (countWork) hipLaunchKernelGGL((k_trace_pt<true, true>), dim3(ptGridS), dim3(kTraceBlock), 0, L.s, c->S, P, q, c->refill, c->ring, spillS);
+                    } else if (s4 && countWork) hipLaunchKernelGGL((k_trace_s4<true>), dim3(ptGridS), dim3(kTraceBlock), 0, L.s, c->S, P, q, c->refill, c->ring, spillS);
+                    else if (s4) hipLaunchKernelGGL((k_trace_s4<false>), dim3(ptGridS), dim3(kTraceBlock), 0, L.s, c->S, P, q, c->refill, c->ring, spillS);
+                    else if (countWork) hipLaunchKernelGGL((k_trace_pt<true, true>), dim3(ptGridS), dim3(kTraceBlock), 0, L.s, c->S, P, q, c->refill, c->ring, spillS);
                     else hipLaunchKernelGGL((k_trace_pt<true, false>), dim3(ptGridS), dim3(kTraceBlock), 0, L.s, c->S, P, q, c->refill, c->ring, spillS);
                     HIPCHK(hipGetLastError());
                     T.launches[K_CLOSEST]++;
@@ -1296,7 +1427,9 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
                     if (countWork) hipLaunchKernelGGL((k_trace_pt<false, true>), dim3(ptGrid), dim3(kTraceBlock), 0, L.s, c->S, P, q, c->refill, c->ring, spillC);
                     else hipLaunchKernelGGL((k_trace_pt<false, false>), dim3(ptGrid), dim3(kTraceBlock), 0, L.s, c->S, P, q, c->refill, c->ring, spillC);
                     HIPCHK(hipGetLastError());
-                    if (countWork) hipLaunchKernelGGL((k_trace_pt<true, true>), dim3(ptGridS), dim3(kTraceBlock), 0, s2, c->S, P, q, c->refill, c->ring, spillS);
+                    if (s4 && countWork) hipLaunchKernelGGL((k_trace_s4<true>), dim3(ptGridS), dim3(kTraceBlock), 0, s2, c->S, P, q, c->refill, c->ring, spillS);
+                    else if (s4) hipLaunchKernelGGL((k_trace_s4<false>), dim3(ptGridS), dim3(kTraceBlock), 0, s2, c->S, P, q, c->refill, c->ring, spillS);
+                    else if (countWork) hipLaunchKernelGGL((k_trace_pt<true, true>), dim3(ptGridS), dim3(kTraceBlock), 0, s2, c->S, P, q, c->refill, c->ring, spillS);
                     else hipLaunchKernelGGL((k_trace_pt<true, false>), dim3(ptGridS), dim3(kTraceBlock), 0, s2, c->S, P, q, c->refill, c->ring, spillS);
                 }
                 HIPCHK(hipGetLastError());

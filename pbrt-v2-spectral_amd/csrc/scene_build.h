@@ -84,6 +84,72 @@ static inline int wide_bvh(const pbrtgpu_flat_scene *s, int top, std::vector<flo
     return 0;
 }
 
+// 4-wide copy of the top-level BVH for the shadow queries (BVHAccel::IntersectP, bvh.cpp:435-481,
+// k_trace_s4): the node of binary interior node i holds i's grandchildren -- each interior child
+// replaced by its two children, a leaf child kept -- as {box lo, ref} {box hi, 0} pairs, refs as in
+// wide_bvh (interior: 4-wide index, leaf: WREF_LEAF record, empty slot: ~0u).  An any-hit query
+// returns whether any primitive whose boxes all pass is hit, in whatever order: testing a
+// grandchild's box without its parent's tests the same primitives, because the slab test is
+// monotonic in the box (a box inside another box gets slab intervals inside the other's: the
+// float subtractions and products are monotonic), so a child that passes implies its parent
+// passes.  The root's own box is still tested first (nodes[0]), as the reference does.  Returns
+// the stack bound: at most 3 pushes per level.
+static inline int wide4_bvh(const pbrtgpu_flat_scene *s, const std::vector<uint32_t> &ref2, std::vector<float4> *w4,
+                            int *stackOut, std::string *err) {
+    w4->clear();
+    *stackOut = 0;
+    const int n = s->n_nodes;
+    if (n <= 0 || (s->nodes[0].meta & 0xff)) return 0;   // a single-leaf BVH: no 4-wide copy
+    // (binary node, its 4-wide index, its level) in allocation order; DFS by an explicit stack
+    std::vector<std::pair<int, int> > todo(1, std::make_pair(0, 0));
+    std::vector<uint32_t> idx(n, 0xffffffffu);
+    idx[0] = 0;
+    w4->resize(8);
+    int maxLevel = 0;
+    while (!todo.empty()) {
+        const int i = todo.back().first, level = todo.back().second;
+        todo.pop_back();
+        maxLevel = std::max(maxLevel, level);
+        const pbrtgpu_bvh_node &b = s->nodes[i];
+        const int kids[2] = {i + 1, (int)b.offset};
+        int cand[4], nc = 0;
+        for (int k = 0; k < 2; ++k) {
+            const int c = kids[k];
+            if (c < 0 || c >= n) SB_FAIL(PBRTGPU_E_INVALID, "BVH child out of range");
+            if (s->nodes[c].meta & 0xff) cand[nc++] = c;
+            else {
+                const int g[2] = {c + 1, (int)s->nodes[c].offset};
+                for (int m = 0; m < 2; ++m) {
+                    if (g[m] < 0 || g[m] >= n) SB_FAIL(PBRTGPU_E_INVALID, "BVH child out of range");
+                    cand[nc++] = g[m];
+                }
+            }
+        }
+        float4 w[8];
+        for (int k = 0; k < 4; ++k) {
+            w[2 * k] = make_float4(0.f, 0.f, 0.f, sb_bits_f(0xffffffffu));
+            w[2 * k + 1] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        for (int k = 0; k < nc; ++k) {
+            const int c = cand[k];
+            const pbrtgpu_bvh_node &cn = s->nodes[c];
+            uint32_t r;
+            if (cn.meta & 0xff) r = ref2[c];
+            else {
+                if (w4->size() / 8 >= WREF_LEAF) SB_FAIL(PBRTGPU_E_UNSUPPORTED, "BVH too large");
+                r = idx[c] = (uint32_t)(w4->size() / 8);
+                w4->resize(w4->size() + 8);
+                todo.push_back(std::make_pair(c, level + 1));
+            }
+            w[2 * k] = make_float4(cn.bmin[0], cn.bmin[1], cn.bmin[2], sb_bits_f(r));
+            w[2 * k + 1] = make_float4(cn.bmax[0], cn.bmax[1], cn.bmax[2], 0.f);
+        }
+        std::copy(w, w + 8, w4->begin() + (size_t)idx[i] * 8);
+    }
+    *stackOut = 3 * (maxLevel + 1) + 1;
+    return 0;
+}
+
 // SpectralRendererTask::Run's wave bands (spectralrenderer.cpp:99-100, 124, 180-188) in the
 // reference's own int / float arithmetic (sampledLambdaStart / sampledLambdaEnd are ints:
 // 395 / 715 in the 32- and 60-band builds, spectrum.h:41-42; 400 / 700 in the upstream 30-band
@@ -333,6 +399,18 @@ static int scene_build(const pbrtgpu_flat_scene *s, int topNodes, DevScene &S, i
         if (int e = wide_bvh(s, topNodes, &wn, &ref, &S.nTop, err)) return e;
         SB_PUT(wn.data(), wn.size(), &S.wnodes);
         SB_PUT(ref.data(), ref.size(), &S.nodeRef);
+        // the shadow queries' 4-wide copy (scenes without instances)
+        std::vector<float4> w4;
+        S.w4nodes = nullptr;
+        S.w4N = 0;
+        S.w4Stack = 0;
+        if (s->n_instances == 0) {
+            if (int e = wide4_bvh(s, ref, &w4, &S.w4Stack, err)) return e;
+            if (!w4.empty()) {
+                SB_PUT(w4.data(), w4.size(), &S.w4nodes);
+                S.w4N = (int)(w4.size() / 8);
+            }
+        }
     }
     SB_PUT(s->prims, (size_t)s->n_prims, &S.prims);
     std::vector<DevTri> pt(s->n_prims);

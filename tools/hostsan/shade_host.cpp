@@ -140,7 +140,7 @@ static int run(const DevScene &S, PathSoA &P, const ItemSrc &src, int nSlots, fl
     const int cap = P.cap;
     uint32_t next = 0, finished = 0;
     Queues Q[2];
-    std::vector<uint32_t> stk((size_t)S.stackDepth + 1);
+    std::vector<uint32_t> stk((size_t)std::max(S.stackDepth, S.w4Stack) + 1);
     std::vector<float> stkT((size_t)S.stackDepth + 1);
     const int64_t pathPasses = MODE == MODE_DL ? (P.nFrames >= 40 ? ((int64_t)1 << 60) : (((int64_t)1 << P.nFrames) - 1) * (S.dlK + 1) + 2)
                                                : S.maxDepth + 3;
@@ -231,9 +231,14 @@ static int run(const DevScene &S, PathSoA &P, const ItemSrc &src, int nSlots, fl
             P.hitPrim[(size_t)kind * P.rcap + rs] = prim;
             P.hitT[(size_t)kind * P.rcap + rs] = prim >= 0 ? t : INFINITY;
         }
+        // shadow queries: on the 4-wide copy where the GPU uses it (k_trace_s4; PBRTGPU_SHADOW4=0:
+        // the binary walk), so the replay checks its boxes and leaves against the oracle too
+        const char *s4e = getenv("PBRTGPU_SHADOW4");
+        const bool s4 = S.nInsts == 0 && S.w4N > 0 && !(s4e && atoi(s4e) == 0);
         for (uint32_t rs : Q[q].s) {
             const Ray r = ray_load(P, RAY_S, (int)rs);
-            P.occ[rs] = (S.nInsts > 0 ? bvh_intersectP<true>(S, st, r) : bvh_intersectP<false>(S, st, r)) ? 1u : 0u;
+            P.occ[rs] = (s4 ? bvh_intersectP4(S, st, r)
+                            : S.nInsts > 0 ? bvh_intersectP<true>(S, st, r) : bvh_intersectP<false>(S, st, r)) ? 1u : 0u;
         }
     };
     P.pass = 0;
