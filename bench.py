@@ -63,14 +63,29 @@ CONFIGS = {
 }
 
 
-def trace_bytes(work, kernel):
+NODE4_BYTES = 128              # a node of the shadow queries' 4-wide BVH copy (4 child boxes + refs)
+
+
+def wide4_active(scene, kind):
+    """the closest-hit / shadow queries run on the 4-wide BVH copy (k_trace_c4 / k_trace_s4):
+    scenes without instances, unless PBRTGPU_CLOSEST4=0 / PBRTGPU_SHADOW4=0"""
+    var = "PBRTGPU_CLOSEST4" if kind == "closest" else "PBRTGPU_SHADOW4"
+    return scene.flat.n_instances == 0 and os.environ.get(var, "1") != "0"
+
+
+def trace_bytes(work, kernel, wide4=False):
     """algorithmic bytes of a traversal kernel = every BVH node it visits
-    (32 B), every primitive it tests (48 B pre-gathered triangle, 176 B quadric record),
-    plus the ray it reads, the answer it writes and its queue entry."""
+    (32 B; a 4-wide node 128 B, after the root box test of 32 B per ray), every primitive
+    it tests (48 B pre-gathered triangle, 176 B quadric record), plus the ray it reads, the answer
+    it writes and its queue entry."""
     if kernel == "k_trace_closest":
-        return (NODE_BYTES * work["nodes_closest"] + TRI_BYTES * work["tris_closest"]
+        nodes = (NODE_BYTES * work["rays"] + NODE4_BYTES * (work["nodes_closest"] - work["rays"]) if wide4
+                 else NODE_BYTES * work["nodes_closest"])
+        return (nodes + TRI_BYTES * work["tris_closest"]
                 + QUAD_BYTES * work["quads_closest"] + (RAY_BYTES + HIT_BYTES + QENTRY_BYTES) * work["rays"])
-    return (NODE_BYTES * work["nodes_shadow"] + TRI_BYTES * work["tris_shadow"] + QUAD_BYTES * work["quads_shadow"]
+    nodes = (NODE_BYTES * work["shadow_rays"] + NODE4_BYTES * (work["nodes_shadow"] - work["shadow_rays"]) if wide4
+             else NODE_BYTES * work["nodes_shadow"])
+    return (nodes + TRI_BYTES * work["tris_shadow"] + QUAD_BYTES * work["quads_shadow"]
             + (RAY_BYTES + 4 + QENTRY_BYTES) * work["shadow_rays"])
 
 
@@ -209,8 +224,8 @@ def exclusive_roofline(dev, scene, tiles, tile, frame_paths, cfg, pps=1):
         del os.environ["PBRTGPU_SERIAL"]
     dev.render(tiles=tiles, tile=tile, count_work=True)
     work = dev.timing()["work"]
-    byts = {"k_trace_closest": trace_bytes(work, "k_trace_closest"),
-            "k_trace_shadow": trace_bytes(work, "k_trace_shadow"),
+    byts = {"k_trace_closest": trace_bytes(work, "k_trace_closest", wide4_active(scene, "closest")),
+            "k_trace_shadow": trace_bytes(work, "k_trace_shadow", wide4_active(scene, "shadow")),
             "k_shade": shade_bytes(work, frame_paths, scene.bands),
             "k_accum": accum_bytes(frame_paths / pps, scene.bands)}   # one row per camera sample
     traffic = {}

@@ -979,6 +979,70 @@ PGD_INLINE bool bvh_intersectP(const DevScene &S, Stack &st, const Ray &ray) {
     float ht;
     return bvh_walk<true, INST>(S, st, 0, 0u, r, &hp, &ht);
 }
+// The binary walk's visiting order of a 4-wide node's slots (scene_build.h wide4_bvh): the near
+// child's part first by the parent's split axis (bvh.cpp:420-425: dirIsNeg[axis] -> second child
+// first), within each part the near grandchild first by that child's axis (a leaf child: its one
+// slot, the empty one skipped).  negMask: dirIsNeg as bits; meta: the node's axes (2 bits each).
+PGD_INLINE uint32_t w4_order(uint32_t meta, uint32_t negMask) {
+    const uint32_t aP = meta & 3u, aA = (meta >> 2) & 3u, aB = (meta >> 4) & 3u;
+    const uint32_t sP = (negMask >> aP) & 1u, sA = aA < 3u ? (negMask >> aA) & 1u : 0u, sB = aB < 3u ? (negMask >> aB) & 1u : 0u;
+    const uint32_t a0 = sA, a1 = 1u - sA, b0 = 2u + sB, b1 = 3u - sB;
+    // slot of position k in bits 2k..2k+1
+    return sP ? (b0 | b1 << 2 | a0 << 4 | a1 << 6) : (a0 | a1 << 2 | b0 << 4 | b1 << 6);
+}
+// The closest-hit query on the 4-wide copy as one plain walk (host replay and tests; the GPU runs
+// k_trace_c4): the root box, then per node the four child boxes in w4_order, the first passing
+// child next and the others pushed (entry distances re-checked against maxt when popped) -- the
+// primitives tested and their order are bvh_walk's.  st.base / st.tbase must hold S.w4Stack entries.
+PGD_INLINE bool bvh_intersect4(const DevScene &S, Stack &st, Ray &ray, int *hitPrim, float *hitT) {
+    const V invDir = v3(1.f / ray.d.x, 1.f / ray.d.y, 1.f / ray.d.z);
+    const int neg[3] = {invDir.x < 0, invDir.y < 0, invDir.z < 0};
+    const uint32_t negMask = (uint32_t)neg[0] | ((uint32_t)neg[1] << 1) | ((uint32_t)neg[2] << 2);
+    st.cRays++;
+    if (!bbox_hit((*sa(S.nodes, 0u)), (*sa(S.nodes, 1u)), ray, invDir, neg)) return false;
+    int todo = 0;
+    bool found = false;
+    uint32_t ref = 0u;
+    for (;;) {
+        if (ref & WREF_LEAF) {
+            const uint32_t np = (ref >> WREF_NP_SHIFT) & WREF_NP_MASK, off = ref & WREF_OFF_MASK;
+            for (uint32_t i = 0; i < np; ++i)
+                if (prim_test<false, false>(S, st, todo, (int)(off + i), ray, hitPrim, hitT)) found = true;
+        } else {
+            const float4 *w = sa(S.w4nodes, (uint32_t)(8 * (size_t)ref));
+            const uint32_t ord = w4_order(__float_as_uint(w[1].w), negMask);
+            uint32_t rs[4];
+            float ts[4];
+            bool hs[4];
+            for (int k = 0; k < 4; ++k) {
+                const int sl = (int)((ord >> (2 * k)) & 3u);
+                rs[k] = __float_as_uint(w[2 * sl].w);
+                ts[k] = 0.f;
+                hs[k] = rs[k] != 0xffffffffu && slab_enter(w[2 * sl], w[2 * sl + 1], ray, invDir, neg, &ts[k]) &&
+                        ts[k] < ray.maxt;
+            }
+            int first = 4;
+            for (int k = 3; k >= 0; --k)
+                if (hs[k]) first = k;
+            for (int k = 3; k > first; --k)
+                if (hs[k]) {
+                    st.set(todo, rs[k]);
+                    st.setT(todo, ts[k]);
+                    ++todo;
+                }
+            if (first < 4) {
+                ref = rs[first];
+                continue;
+            }
+        }
+        for (;;) {
+            if (todo == 0) return found;
+            --todo;
+            ref = st.get(todo);
+            if (st.getT(todo) < ray.maxt) break;
+        }
+    }
+}
 // The shadow query on the 4-wide BVH copy (scene_build.h wide4_bvh) as one plain walk: the root box,
 // then per node the child boxes k_trace_s4 tests and the same leaves (host replay and tests; the
 // GPU runs k_trace_s4).  st.base must hold S.w4Stack entries.

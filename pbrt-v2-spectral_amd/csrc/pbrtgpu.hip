@@ -451,6 +451,152 @@ __global__ __launch_bounds__(kTraceBlock) PGD_TRACE_ATTR void k_trace_s4(DevScen
     }
 }
 
+// Closest-hit queries of one pass (camera / continuation and MIS rays) on the 4-wide BVH copy
+// (BVHAccel::Intersect, bvh.cpp:380-434; scene_build.h wide4_bvh): k_trace_pt<false>'s persistent
+// ray-replacement scheme, one 4-wide node per loop trip -- its child boxes tested, taken in the
+// binary walk's order (w4_order), the first passing child next and the others pushed with their
+// entry distances, re-checked against the then-current maxt when popped.  The primitives tested
+// and their order are the binary walk's (bvh_intersect4 is the same walk, replayed on the host
+// against the oracle), with half as many dependent node loads per ray.
+template <bool STATS>
+__global__ __launch_bounds__(kTraceBlock) PGD_TRACE_ATTR void k_trace_c4(DevScene S, PathSoA P, int q, int refill, int ring, uint2 *__restrict__ spill) {
+    __shared__ uint32_t sref[kStackLDS * kTraceBlock];
+    __shared__ float stm[kStackLDS * kTraceBlock];
+    uint2 *gsp = spill + (size_t)(blockIdx.x * blockDim.x + threadIdx.x) * S.w4Stack;
+    int bottom = 0;
+    Stack st;
+    const uint32_t n = P.cnt[CNT_QC(q)];
+    const uint32_t *Q = P.qC + (size_t)q * 2 * P.rcap;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = (gridDim.x * blockDim.x) >> 6;
+    uint32_t next = (uint32_t)((uint64_t)n * wave / nw);
+    const uint32_t end = (uint32_t)((uint64_t)n * (wave + 1) / nw);
+    bool active = false;
+    int slot = 0, kind = 0, todo = 0, prim = -1;
+    uint32_t ref = 0;
+    float thit = INFINITY;
+    Ray ray;
+    V invDir = v3(0.f, 0.f, 0.f);
+    int neg[3] = {0, 0, 0};
+    uint32_t negMask = 0;
+    uint32_t nM = 0, hM = 0;
+    const uint32_t NONE = 0xffffffffu;
+    auto push = [&](uint32_t r, float t) {
+        if (todo - bottom == ring) {   // ring full: oldest entry to HBM
+            const int j = (bottom & (ring - 1)) * kTraceBlock + threadIdx.x;
+            gsp[bottom] = make_uint2(sref[j], __float_as_uint(stm[j]));
+            ++bottom;
+        }
+        const int j = (todo & (ring - 1)) * kTraceBlock + threadIdx.x;
+        sref[j] = r;
+        stm[j] = t;
+        ++todo;
+    };
+    for (;;) {
+        const unsigned long long idle = __ballot(!active);
+        const uint32_t nIdle = (uint32_t)__popcll(idle);
+        if (next < end && (nIdle >= (uint32_t)refill || nIdle == 64u)) {
+            if (!active) {
+                const uint32_t i = next + (uint32_t)__popcll(idle & ((1ull << lane) - 1ull));
+                if (i < end) {
+                    const uint32_t e = Q[i];
+                    slot = (int)(e >> 1);
+                    kind = (int)(e & 1);
+                    ray = ray_load(P, kind, slot);
+                    invDir = v3(1.f / ray.d.x, 1.f / ray.d.y, 1.f / ray.d.z);
+                    neg[0] = invDir.x < 0; neg[1] = invDir.y < 0; neg[2] = invDir.z < 0;
+                    negMask = (uint32_t)neg[0] | ((uint32_t)neg[1] << 1) | ((uint32_t)neg[2] << 2);
+                    prim = -1;
+                    thit = INFINITY;
+                    todo = 0;
+                    bottom = 0;
+                    st.cRays++;
+                    st.cNodes++;
+                    if (bbox_hit((*sa(S.nodes, (uint32_t)(0))), (*sa(S.nodes, (uint32_t)(1))), ray, invDir, neg)) {
+                        ref = 0u;   // the 4-wide root (the root's grandchildren)
+                        active = true;
+                    } else {
+                        P.hitPrim[(size_t)kind * P.rcap + slot] = -1;
+                        P.hitT[(size_t)kind * P.rcap + slot] = INFINITY;
+                        if (STATS && kind == RAY_M) nM++;
+                    }
+                }
+            }
+            next = min(end, next + nIdle);
+        }
+        if (!__ballot(active)) {
+            if (next >= end) break;
+            continue;
+        }
+        if (active) {
+            if (!(ref & WREF_LEAF)) {
+                const float4 *w = sa(S.w4nodes, (uint32_t)(8 * (size_t)ref));
+                const float4 b0 = w[0], b1 = w[1], b2 = w[2], b3 = w[3], b4 = w[4], b5 = w[5], b6 = w[6], b7 = w[7];
+                st.cNodes++;
+                // the four slots' tests, then their refs / hits / entries in the binary walk's order
+                float e0 = 0.f, e1 = 0.f, e2 = 0.f, e3 = 0.f;
+                const uint32_t r0 = __float_as_uint(b0.w), r1 = __float_as_uint(b2.w), r2 = __float_as_uint(b4.w),
+                               r3 = __float_as_uint(b6.w);
+                const bool h0 = r0 != NONE && slab_enter(b0, b1, ray, invDir, neg, &e0) && e0 < ray.maxt;
+                const bool h1 = r1 != NONE && slab_enter(b2, b3, ray, invDir, neg, &e1) && e1 < ray.maxt;
+                const bool h2 = r2 != NONE && slab_enter(b4, b5, ray, invDir, neg, &e2) && e2 < ray.maxt;
+                const bool h3 = r3 != NONE && slab_enter(b6, b7, ray, invDir, neg, &e3) && e3 < ray.maxt;
+                const uint32_t ord = w4_order(__float_as_uint(b1.w), negMask);
+                auto pr = [&](uint32_t sl) { return sl == 0 ? r0 : sl == 1 ? r1 : sl == 2 ? r2 : r3; };
+                auto ph = [&](uint32_t sl) { return sl == 0 ? h0 : sl == 1 ? h1 : sl == 2 ? h2 : h3; };
+                auto pe = [&](uint32_t sl) { return sl == 0 ? e0 : sl == 1 ? e1 : sl == 2 ? e2 : e3; };
+                const uint32_t s0 = ord & 3u, s1 = (ord >> 2) & 3u, s2 = (ord >> 4) & 3u, s3 = (ord >> 6) & 3u;
+                const bool k0 = ph(s0), k1 = ph(s1), k2 = ph(s2), k3 = ph(s3);
+                const int first = k0 ? 0 : k1 ? 1 : k2 ? 2 : k3 ? 3 : 4;
+                if (k3 && first < 3) push(pr(s3), pe(s3));
+                if (k2 && first < 2) push(pr(s2), pe(s2));
+                if (k1 && first < 1) push(pr(s1), pe(s1));
+                ref = first == 0 ? pr(s0) : first == 1 ? pr(s1) : first == 2 ? pr(s2) : first == 3 ? pr(s3) : NONE;
+            }
+            if (ref != NONE && (ref & WREF_LEAF)) {
+                const uint32_t np = (ref >> WREF_NP_SHIFT) & WREF_NP_MASK, off = ref & WREF_OFF_MASK;
+                for (uint32_t i = 0; i < np; ++i) prim_test<false, false>(S, st, todo, (int)(off + i), ray, &prim, &thit);
+                ref = NONE;
+            }
+            bool done = false;
+            if (ref == NONE) {
+                done = true;
+                while (todo > 0) {
+                    --todo;
+                    uint32_t r;
+                    float tm;
+                    if (todo < bottom) {
+                        const uint2 g = gsp[todo];
+                        r = g.x; tm = __uint_as_float(g.y);
+                        bottom = todo;
+                    } else {
+                        const int j = (todo & (ring - 1)) * kTraceBlock + threadIdx.x;
+                        r = sref[j]; tm = stm[j];
+                    }
+                    if (tm < ray.maxt) { ref = r; done = false; break; }
+                }
+            }
+            if (done) {
+                active = false;
+                P.hitPrim[(size_t)kind * P.rcap + slot] = prim;
+                P.hitT[(size_t)kind * P.rcap + slot] = prim >= 0 ? thit : INFINITY;
+                st.cHits += prim >= 0 ? 1u : 0u;
+                if (STATS && kind == RAY_M) { nM++; hM += prim >= 0 ? 1u : 0u; }
+            }
+        }
+    }
+    if (STATS) {
+        unsigned long long *w = reinterpret_cast<unsigned long long *>(P.cnt + CNT_WORK);
+        atomicAdd(&w[W_RAYS], (unsigned long long)st.cRays);
+        atomicAdd(&w[W_NODES_C], (unsigned long long)st.cNodes);
+        atomicAdd(&w[W_TRIS_C], (unsigned long long)st.cTris);
+        atomicAdd(&w[W_QUADS_C], (unsigned long long)st.cQuads);
+        atomicAdd(&w[W_HITS], (unsigned long long)st.cHits);
+        atomicAdd(&w[W_RAYS_M], (unsigned long long)nM);
+        atomicAdd(&w[W_HITS_M], (unsigned long long)hM);
+    }
+}
+
 // Ray queries of one pass WITH instanced primitives (TransformedPrimitive over nested BVHs,
 // primitive.cpp:87-116, C5): k_trace_pt's persistent ray-replacement scheme with a two-level
 // walk per lane.  Level 0 walks the top-level BVH in world space; a top-level leaf's
@@ -976,6 +1122,7 @@ struct pbrtgpu_ctx {
     int ptBlocksPerCU = 0;    // occupancy of k_trace_pt closest (computed on first use)
     int ptBlocksPerCUS = 0;   // occupancy of k_trace_pt shadow
     int s4BlocksPerCU = 0;    // occupancy of k_trace_s4 (shadow queries on the 4-wide BVH)
+    int c4BlocksPerCU = 0;    // occupancy of k_trace_c4 (closest-hit queries on the 4-wide BVH)
     int instBlocksPerCU = 0, instBlocksPerCUS = 0;   // occupancy of k_trace_inst closest / shadow
     int ring = kStackLDS;     // LDS ring entries in use (PBRTGPU_STACK_LDS: tests force HBM spills)
     int refill = 16;          // idle lanes that trigger ray replacement in k_trace_pt (PBRTGPU_REFILL)
@@ -1049,6 +1196,10 @@ static bool pass_log() {
 static bool mt_ext_forced() {
     const char *e = getenv("PBRTGPU_MT_EXT");
     return e && atoi(e) != 0;
+}
+static bool closest4_on() {
+    const char *e = getenv("PBRTGPU_CLOSEST4");
+    return !e || atoi(e) != 0;
 }
 static bool shadow4_on() {
     const char *e = getenv("PBRTGPU_SHADOW4");
@@ -1176,9 +1327,11 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
         HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&b1, k_trace_pt<true, false>, kTraceBlock, 0));
         HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&b2, k_trace_inst<false, false>, kTraceBlock, 0));
         HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&b3, k_trace_inst<true, false>, kTraceBlock, 0));
-        int b4 = 0;
+        int b4 = 0, b5 = 0;
         HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&b4, k_trace_s4<false>, kTraceBlock, 0));
+        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&b5, k_trace_c4<false>, kTraceBlock, 0));
         c->s4BlocksPerCU = std::max(1, b4);
+        c->c4BlocksPerCU = std::max(1, b5);
         c->ptBlocksPerCU = std::max(1, b0);
         c->ptBlocksPerCUS = std::max(1, b1);
         c->instBlocksPerCU = std::max(1, b2);
@@ -1187,12 +1340,14 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
     // instanced scenes: the two-level persistent kernels (PBRTGPU_INST_WALK=legacy: the
     // one-ray-per-thread bvh_walk kernels, kept for A/B parity tests)
     const bool instPT = inst && !legacy_inst_walk();
-    const uint32_t ptGrid = (uint32_t)(c->numCUs * (instPT ? c->instBlocksPerCU : c->ptBlocksPerCU));
+    // closest-hit queries on the 4-wide BVH copy likewise (PBRTGPU_CLOSEST4=0: the binary walk)
+    const bool c4 = !inst && c->S.w4N > 0 && closest4_on();
+    const uint32_t ptGrid = (uint32_t)(c->numCUs * (instPT ? c->instBlocksPerCU : c4 ? c->c4BlocksPerCU : c->ptBlocksPerCU));
     // shadow queries on the 4-wide BVH copy (scenes without instances; PBRTGPU_SHADOW4=0: the binary walk)
     const bool s4 = !inst && c->S.w4N > 0 && shadow4_on();
     const uint32_t ptGridS = (uint32_t)(c->numCUs * (instPT ? c->instBlocksPerCUS : s4 ? c->s4BlocksPerCU : c->ptBlocksPerCUS));
     const size_t spillLane = (size_t)std::max(ptGrid, ptGridS) * kTraceBlock *
-                             (size_t)std::max(c->stackDepth, s4 ? c->S.w4Stack : 0);   // uint2 per kernel
+                             (size_t)std::max(c->stackDepth, (s4 || c4) ? c->S.w4Stack : 0);   // uint2 per kernel
     // scenes without measured BRDFs, textures and environment lights run the variant with
     // that code compiled out (fewer registers, no kd-tree stack)
     // the DirectLighting integrator has its own step (all features compiled in)
@@ -1370,7 +1525,9 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
                     } else if (inst) {
                         if (countWork) hipLaunchKernelGGL((k_trace_closest<true, true>), dim3(traceGrid), dim3(kTraceBlock), lds, L.s, c->S, P, q);
                         else hipLaunchKernelGGL((k_trace_closest<false, true>), dim3(traceGrid), dim3(kTraceBlock), lds, L.s, c->S, P, q);
-                    } else if (countWork) hipLaunchKernelGGL((k_trace_pt<false, true>), dim3(ptGrid), dim3(kTraceBlock), 0, L.s, c->S, P, q, c->refill, c->ring, spillC);
+                    } else if (c4 && countWork) hipLaunchKernelGGL((k_trace_c4<true>), dim3(ptGrid), dim3(kTraceBlock), 0, L.s, c->S, P, q, c->refill, c->ring, spillC);
+                    else if (c4) hipLaunchKernelGGL((k_trace_c4<false>), dim3(ptGrid), dim3(kTraceBlock), 0, L.s, c->S, P, q, c->refill, c->ring, spillC);
+                    else if (countWork) hipLaunchKernelGGL((k_trace_pt<false, true>), dim3(ptGrid), dim3(kTraceBlock), 0, L.s, c->S, P, q, c->refill, c->ring, spillC);
                     else hipLaunchKernelGGL((k_trace_pt<false, false>), dim3(ptGrid), dim3(kTraceBlock), 0, L.s, c->S, P, q, c->refill, c->ring, spillC);
                     HIPCHK(hipGetLastError());
                     HIPCHK(hipEventRecord(e[1], L.s));
@@ -1424,7 +1581,9 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
                     if (countWork) hipLaunchKernelGGL((k_trace_shadow<true, true>), dim3(traceGrid), dim3(kTraceBlock), ldsS, L.s2, c->S, P, q);
                     else hipLaunchKernelGGL((k_trace_shadow<false, true>), dim3(traceGrid), dim3(kTraceBlock), ldsS, L.s2, c->S, P, q);
                 } else {
-                    if (countWork) hipLaunchKernelGGL((k_trace_pt<false, true>), dim3(ptGrid), dim3(kTraceBlock), 0, L.s, c->S, P, q, c->refill, c->ring, spillC);
+                    if (c4 && countWork) hipLaunchKernelGGL((k_trace_c4<true>), dim3(ptGrid), dim3(kTraceBlock), 0, L.s, c->S, P, q, c->refill, c->ring, spillC);
+                    else if (c4) hipLaunchKernelGGL((k_trace_c4<false>), dim3(ptGrid), dim3(kTraceBlock), 0, L.s, c->S, P, q, c->refill, c->ring, spillC);
+                    else if (countWork) hipLaunchKernelGGL((k_trace_pt<false, true>), dim3(ptGrid), dim3(kTraceBlock), 0, L.s, c->S, P, q, c->refill, c->ring, spillC);
                     else hipLaunchKernelGGL((k_trace_pt<false, false>), dim3(ptGrid), dim3(kTraceBlock), 0, L.s, c->S, P, q, c->refill, c->ring, spillC);
                     HIPCHK(hipGetLastError());
                     if (s4 && countWork) hipLaunchKernelGGL((k_trace_s4<true>), dim3(ptGridS), dim3(kTraceBlock), 0, s2, c->S, P, q, c->refill, c->ring, spillS);

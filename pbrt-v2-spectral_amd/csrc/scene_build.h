@@ -84,66 +84,75 @@ static inline int wide_bvh(const pbrtgpu_flat_scene *s, int top, std::vector<flo
     return 0;
 }
 
-// 4-wide copy of the top-level BVH for the shadow queries (BVHAccel::IntersectP, bvh.cpp:435-481,
-// k_trace_s4): the node of binary interior node i holds i's grandchildren -- each interior child
-// replaced by its two children, a leaf child kept -- as {box lo, ref} {box hi, 0} pairs, refs as in
-// wide_bvh (interior: 4-wide index, leaf: WREF_LEAF record, empty slot: ~0u).  An any-hit query
-// returns whether any primitive whose boxes all pass is hit, in whatever order: testing a
-// grandchild's box without its parent's tests the same primitives, because the slab test is
-// monotonic in the box (a box inside another box gets slab intervals inside the other's: the
-// float subtractions and products are monotonic), so a child that passes implies its parent
-// passes.  The root's own box is still tested first (nodes[0]), as the reference does.  Returns
-// the stack bound: at most 3 pushes per level.
+// 4-wide copy of the top-level BVH (k_trace_s4 / k_trace_c4, BVHAccel::Intersect / IntersectP,
+// bvh.cpp:380-481): the node of binary interior node i holds i's grandchildren -- slots 0, 1: the
+// left child's children (or the left child itself in slot 0, when it is a leaf), slots 2, 3: the
+// right child's -- as {box lo, ref} {box hi, meta} pairs, refs as in wide_bvh (interior: 4-wide
+// index, leaf: WREF_LEAF record, empty slot: ~0u); slot 0's meta holds the split axes of i, its left
+// and its right child (2 bits each; 3: a leaf).  Testing a grandchild's box without its parent's
+// tests the same primitives, because the slab test is monotonic in the box (a box inside another
+// gets slab intervals inside the other's, entered no earlier: the float subtractions and products
+// are monotonic), so a grandchild that passes implies its parent passes, then or at any later,
+// smaller maxt.  The closest-hit walk visits the grandchildren in the binary walk's order (near
+// child first by the parent's axis, each child's near child first by its own axis) and re-checks a
+// pushed entry distance against the then-current maxt, as the binary walk re-checks the far child
+// it pushed: the primitives tested, and their order, are the binary walk's.  The root's own box is
+// still tested first (nodes[0]).  Returns the stack bound: at most 3 pushes per level.
 static inline int wide4_bvh(const pbrtgpu_flat_scene *s, const std::vector<uint32_t> &ref2, std::vector<float4> *w4,
                             int *stackOut, std::string *err) {
     w4->clear();
     *stackOut = 0;
     const int n = s->n_nodes;
     if (n <= 0 || (s->nodes[0].meta & 0xff)) return 0;   // a single-leaf BVH: no 4-wide copy
-    // (binary node, its 4-wide index, its level) in allocation order; DFS by an explicit stack
+    // (binary node, its level) of the 4-wide nodes to fill; DFS by an explicit stack
     std::vector<std::pair<int, int> > todo(1, std::make_pair(0, 0));
     std::vector<uint32_t> idx(n, 0xffffffffu);
     idx[0] = 0;
     w4->resize(8);
     int maxLevel = 0;
+    auto axisOf = [&](int i) -> uint32_t { return (s->nodes[i].meta & 0xff) ? 3u : ((s->nodes[i].meta >> 8) & 0xff); };
     while (!todo.empty()) {
         const int i = todo.back().first, level = todo.back().second;
         todo.pop_back();
         maxLevel = std::max(maxLevel, level);
         const pbrtgpu_bvh_node &b = s->nodes[i];
         const int kids[2] = {i + 1, (int)b.offset};
-        int cand[4], nc = 0;
-        for (int k = 0; k < 2; ++k) {
-            const int c = kids[k];
-            if (c < 0 || c >= n) SB_FAIL(PBRTGPU_E_INVALID, "BVH child out of range");
-            if (s->nodes[c].meta & 0xff) cand[nc++] = c;
-            else {
-                const int g[2] = {c + 1, (int)s->nodes[c].offset};
-                for (int m = 0; m < 2; ++m) {
-                    if (g[m] < 0 || g[m] >= n) SB_FAIL(PBRTGPU_E_INVALID, "BVH child out of range");
-                    cand[nc++] = g[m];
-                }
-            }
-        }
         float4 w[8];
         for (int k = 0; k < 4; ++k) {
             w[2 * k] = make_float4(0.f, 0.f, 0.f, sb_bits_f(0xffffffffu));
             w[2 * k + 1] = make_float4(0.f, 0.f, 0.f, 0.f);
         }
-        for (int k = 0; k < nc; ++k) {
-            const int c = cand[k];
-            const pbrtgpu_bvh_node &cn = s->nodes[c];
-            uint32_t r;
-            if (cn.meta & 0xff) r = ref2[c];
-            else {
-                if (w4->size() / 8 >= WREF_LEAF) SB_FAIL(PBRTGPU_E_UNSUPPORTED, "BVH too large");
-                r = idx[c] = (uint32_t)(w4->size() / 8);
-                w4->resize(w4->size() + 8);
-                todo.push_back(std::make_pair(c, level + 1));
+        for (int k = 0; k < 2; ++k)
+            if (kids[k] < 0 || kids[k] >= n) SB_FAIL(PBRTGPU_E_INVALID, "BVH child out of range");
+        const uint32_t meta = axisOf(i) | (axisOf(kids[0]) << 2) | (axisOf(kids[1]) << 4);
+        if (axisOf(i) > 2) SB_FAIL(PBRTGPU_E_INVALID, "BVH split axis");
+        for (int k = 0; k < 2; ++k) {
+            const int c = kids[k];
+            int slotc[2] = {c, -1};
+            if (!(s->nodes[c].meta & 0xff)) {
+                slotc[0] = c + 1;
+                slotc[1] = (int)s->nodes[c].offset;
+                if (slotc[1] < 0 || slotc[1] >= n || slotc[0] >= n) SB_FAIL(PBRTGPU_E_INVALID, "BVH child out of range");
+                if (axisOf(c) > 2) SB_FAIL(PBRTGPU_E_INVALID, "BVH split axis");
             }
-            w[2 * k] = make_float4(cn.bmin[0], cn.bmin[1], cn.bmin[2], sb_bits_f(r));
-            w[2 * k + 1] = make_float4(cn.bmax[0], cn.bmax[1], cn.bmax[2], 0.f);
+            for (int m = 0; m < 2; ++m) {
+                const int g = slotc[m];
+                if (g < 0) continue;
+                const pbrtgpu_bvh_node &gn = s->nodes[g];
+                uint32_t r;
+                if (gn.meta & 0xff) r = ref2[g];
+                else {
+                    if (w4->size() / 8 >= WREF_LEAF) SB_FAIL(PBRTGPU_E_UNSUPPORTED, "BVH too large");
+                    r = idx[g] = (uint32_t)(w4->size() / 8);
+                    w4->resize(w4->size() + 8);
+                    todo.push_back(std::make_pair(g, level + 1));
+                }
+                const int sl = 2 * k + m;
+                w[2 * sl] = make_float4(gn.bmin[0], gn.bmin[1], gn.bmin[2], sb_bits_f(r));
+                w[2 * sl + 1] = make_float4(gn.bmax[0], gn.bmax[1], gn.bmax[2], 0.f);
+            }
         }
+        w[1].w = sb_bits_f(meta);
         std::copy(w, w + 8, w4->begin() + (size_t)idx[i] * 8);
     }
     *stackOut = 3 * (maxLevel + 1) + 1;
@@ -399,7 +408,7 @@ static int scene_build(const pbrtgpu_flat_scene *s, int topNodes, DevScene &S, i
         if (int e = wide_bvh(s, topNodes, &wn, &ref, &S.nTop, err)) return e;
         SB_PUT(wn.data(), wn.size(), &S.wnodes);
         SB_PUT(ref.data(), ref.size(), &S.nodeRef);
-        // the shadow queries' 4-wide copy (scenes without instances)
+        // the 4-wide copy (scenes without instances)
         std::vector<float4> w4;
         S.w4nodes = nullptr;
         S.w4N = 0;

@@ -141,7 +141,7 @@ static int run(const DevScene &S, PathSoA &P, const ItemSrc &src, int nSlots, fl
     uint32_t next = 0, finished = 0;
     Queues Q[2];
     std::vector<uint32_t> stk((size_t)std::max(S.stackDepth, S.w4Stack) + 1);
-    std::vector<float> stkT((size_t)S.stackDepth + 1);
+    std::vector<float> stkT((size_t)std::max(S.stackDepth, S.w4Stack) + 1);
     const int64_t pathPasses = MODE == MODE_DL ? (P.nFrames >= 40 ? ((int64_t)1 << 60) : (((int64_t)1 << P.nFrames) - 1) * (S.dlK + 1) + 2)
                                                : S.maxDepth + 3;
     const int64_t maxPasses = 2 * ((src.nItems + nSlots - 1) / nSlots + 1) * pathPasses + 8;
@@ -226,7 +226,10 @@ static int run(const DevScene &S, PathSoA &P, const ItemSrc &src, int nSlots, fl
             Ray r = ray_load(P, kind, rs);
             int prim = -1;
             float t = INFINITY;
-            const bool hit = S.nInsts > 0 ? bvh_intersect<true>(S, st, r, &prim, &t) : bvh_intersect<false>(S, st, r, &prim, &t);
+            const char *c4e = getenv("PBRTGPU_CLOSEST4");
+            const bool c4 = S.nInsts == 0 && S.w4N > 0 && !(c4e && atoi(c4e) == 0);
+            const bool hit = c4 ? bvh_intersect4(S, st, r, &prim, &t)
+                           : S.nInsts > 0 ? bvh_intersect<true>(S, st, r, &prim, &t) : bvh_intersect<false>(S, st, r, &prim, &t);
             if (!hit) prim = -1;
             P.hitPrim[(size_t)kind * P.rcap + rs] = prim;
             P.hitT[(size_t)kind * P.rcap + rs] = prim >= 0 ? t : INFINITY;
