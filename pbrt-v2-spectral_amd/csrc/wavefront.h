@@ -424,6 +424,10 @@ PGD_INLINE int kd_next(const float4 &a, const float4 &b, int cur, int prev, bool
 // the plane's float distance^2 away, the float subtraction and sums being monotonic).  The
 // samples found are then accumulated by the reference's own walk at that radius, so the sum and
 // its order are the reference's.  C3's points needed ~3-4 walks of growing radius each.
+// The 3-nearest walk visits a node's own sample when it first arrives there (pre-order), before
+// its children: the bound d3 tightens on the way down and prunes far children early (the
+// reference's own walk, below, must visit children first; this one only finds d3, which does
+// not depend on the order).
 template <class NodePtr>
 PGD_INLINE float kd_final_radius(NodePtr nodes, float p0, float p1, float p2) {
     const float capD2 = .001f * 1024.f;   // k = 10; beyond it the loop ends at k = 11 regardless
@@ -432,19 +436,21 @@ PGD_INLINE float kd_final_radius(NodePtr nodes, float p0, float p1, float p2) {
     bool down = true;
     for (;;) {
         const float4 a = kd_node(nodes, 2 * cur), b = kd_node(nodes, 2 * cur + 1);
+        if (down) {
+            const V d = vsub(v3(a.x, a.y, a.z), v3(p0, p1, p2));
+            const float dist2 = vlen2(d);
+            if (dist2 < d3) {   // keep d1 <= d2 <= d3 the three smallest
+                d3 = fminf(fmaxf(dist2, d2), d3);
+                d2 = fminf(fmaxf(dist2, d1), d2);
+                d1 = fminf(dist2, d1);
+            }
+        }
         const int nxt = kd_next(a, b, cur, prev, down, p0, p1, p2, d3);
         if (nxt >= 0) {
             prev = cur;
             cur = nxt;
             down = true;
             continue;
-        }
-        const V d = vsub(v3(a.x, a.y, a.z), v3(p0, p1, p2));
-        const float dist2 = vlen2(d);
-        if (dist2 < d3) {   // keep d1 <= d2 <= d3 the three smallest
-            d3 = fminf(fmaxf(dist2, d2), d3);
-            d2 = fminf(fmaxf(dist2, d1), d2);
-            d1 = fminf(dist2, d1);
         }
         if (cur == 0) break;
         prev = cur;
