@@ -821,6 +821,10 @@ PGD_INLINE void estimate_direct(const DevScene &S, const PathSoA &P, int slot, i
         PGD_T0(LSTORE);
         // A_i = (f_i * Li_i) * sc ; written while testing f for black (A unused if black)
         bool black = true;
+#ifdef PGD_EXP_NO_ABLOOP   // timing experiment only: the A / B band loops skipped (wrong radiance)
+        black = sc == 12345.f;
+        if (!black) {} else
+#endif
 PGD_UNROLL_BANDS
         for (int q = 0; q < NQ; ++q) {
             float4 f = fval4<FEAT>(sp, F, q, mb, kb, c), e = emit4<FEAT>(S, em, q), a;
@@ -895,6 +899,10 @@ PGD_UNROLL_BANDS
             if (withB) {
                 const float ad = fabsf(vdot(wi, n));
                 bool black = true;
+#ifdef PGD_EXP_NO_ABLOOP
+                black = ad == 12345.f;
+                if (!black) {} else
+#endif
 PGD_UNROLL_BANDS
                 for (int q = 0; q < NQ; ++q) {
                     float4 f = fval4<FEAT>(sp, F, q, mb, kb, c), e = emit4<FEAT>(S, eb, q), b;
@@ -1188,8 +1196,12 @@ PGD_INLINE Pushes shade_slot(const DevScene &S, const PathSoA &P, int slot, floa
 #pragma unroll
         for (int q = 0; q < NQ; ++q) {
             float4 bt = beta_q(bb4, q, c);
+#ifdef PGD_EXP_NO_ABLOOP
+            float4 a = make_float4(0.1f, 0.f, 0.f, 0.f), bb = a;
+#else
             float4 a = useA ? A[(uint32_t)q * c] : make_float4(0.f, 0.f, 0.f, 0.f);
             float4 bb = useB ? B[(uint32_t)q * c] : make_float4(0.f, 0.f, 0.f, 0.f);
+#endif
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 float Ld = 0.f;

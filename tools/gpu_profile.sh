@@ -20,9 +20,10 @@ timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_write -o run -- pytho
 timeout -s KILL 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES -d $OUT/pmc_sq1 -o run -- python3 $B --steps 1 --warmup 0 --serial > $OUT/pmc3.json 2> $OUT/pmc3.err
 timeout -s KILL 300 rocprofv3 --pmc SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INST_CYCLES_VMEM SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE GRBM_COUNT -d $OUT/pmc_sq2 -o run -- python3 $B --steps 1 --warmup 0 --serial > $OUT/pmc4.json 2> $OUT/pmc4.err
 timeout -s KILL 120 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE -d $OUT/pmc_lds -o run -- python3 $B --steps 1 --warmup 0 --serial > $OUT/pmc5.json 2> $OUT/pmc5.err || echo "LDS pass failed (counter set not available)"
+timeout -s KILL 120 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum -d $OUT/pmc_tcc -o run -- python3 $B --steps 1 --warmup 0 --serial > $OUT/pmc6.json 2> $OUT/pmc6.err || echo "TCC pass failed"
 # summaries next to the run (gpurun_out is copied back only below 64 MiB): the rocpd databases go
 SUMCFG=$CFG; case "$EXTRA" in *directlighting*) SUMCFG=${CFG}_dl;; *metadata*) SUMCFG=${CFG}_meta;; esac
 case "$EXTRA" in *spectral*) SUMCFG=${SUMCFG}_spec;; esac
 python3 tools/rocpd_summary.py $TAG $OUT $SUMCFG $PWD/gpurun_out/summaries > /dev/null
-rm -rf $OUT/trace $OUT/trace_serial $OUT/pmc_fetch $OUT/pmc_write $OUT/pmc_sq1 $OUT/pmc_sq2 $OUT/pmc_lds
+rm -rf $OUT/trace $OUT/trace_serial $OUT/pmc_fetch $OUT/pmc_write $OUT/pmc_sq1 $OUT/pmc_sq2 $OUT/pmc_lds $OUT/pmc_tcc
 echo done

@@ -18,8 +18,10 @@ import sqlite3
 import sys
 
 # timing names of pbrtgpu_last_timing <- device kernel name prefixes (uninstrumented instances)
-NAMES = {"k_trace_closest": ("k_trace_pt<false, false>", "k_trace_closest<false, true>", "k_trace_inst<false, false>"),
-         "k_trace_shadow": ("k_trace_pt<true, false>", "k_trace_shadow<false, true>", "k_trace_inst<true, false>"),
+NAMES = {"k_trace_closest": ("k_trace_pt<false, false>", "k_trace_closest<false, true>", "k_trace_inst<false, false>",
+                             "k_trace_c4<false>"),
+         "k_trace_shadow": ("k_trace_pt<true, false>", "k_trace_shadow<false, true>", "k_trace_inst<true, false>",
+                            "k_trace_s4<false>"),
          "k_shade": ("k_shade<", "k_dl_nee<", "k_dl_spec<", "k_regen<"),
          "k_accum": ("k_accum<",)}
 
@@ -77,7 +79,7 @@ def main():
         open(os.path.join(out, "%s_kernel_stats.txt" % tag), "w").write("\n".join(lines))
         print("\n".join(lines))
     pm = {}
-    for sub in ("pmc_fetch", "pmc_write", "pmc_sq1", "pmc_sq2", "pmc_lds"):
+    for sub in ("pmc_fetch", "pmc_write", "pmc_sq1", "pmc_sq2", "pmc_lds", "pmc_tcc"):
         for f in glob.glob(os.path.join(d, sub, "**", "*.db"), recursive=True):
             for kk, v in pmc_rows(sqlite3.connect(f)).items():
                 pm.setdefault(kk, []).extend(v)
@@ -103,6 +105,9 @@ def main():
             parts = ["%s %.1f%%" % (c, 100.0 * cs[c][0] / wc) for c in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY")
                      if c in cs]
             pl.append("# %s: %s of SQ_WAVE_CYCLES" % (t, ", ".join(parts)))
+        if "TCC_HIT_sum" in cs and "TCC_MISS_sum" in cs:
+            h, m = cs["TCC_HIT_sum"][0], cs["TCC_MISS_sum"][0]
+            pl.append("# %s: TCC (L2) hit rate %.1f%% (%d hits, %d misses)" % (t, 100.0 * h / max(h + m, 1), h, m))
         if "SQ_INSTS_VALU" in cs and "SQ_WAVES" in cs:
             pl.append("# %s: VALU insts / wave %.0f, VMEM_RD / wave %.1f, VMEM_WR / wave %.1f" % (
                 t, cs["SQ_INSTS_VALU"][0] / cs["SQ_WAVES"][0], cs.get("SQ_INSTS_VMEM_RD", [0])[0] / cs["SQ_WAVES"][0],
