@@ -1,0 +1,13 @@
+#!/bin/bash
+# r04f: C2 A/B on one box -- baseline (lib/exp/spectral: the committed shade step), the shade step at
+# 4 waves/SIMD (lib/exp/w4, 208 spilled VGPRs), shared-divisor division without its fallback
+# (lib/exp/divfast, timing only)
+OUT=$PWD/gpurun_out/r04f
+mkdir -p $OUT
+L=$PWD/pbrt-v2-spectral_amd/lib/exp
+run() {   # name lib
+  export PBRTGPU_LIB=$2
+  timeout -k 10 300 python3 bench.py --no-cpu --no-slices > $OUT/bench_$1.json 2> $OUT/bench_$1.err || { tail -20 $OUT/bench_$1.err; return 1; }
+  python3 -c "import json; d=json.load(open('$OUT/bench_$1.json')); k=d['roofline']['kernels']; print('$1', d['value'], {n: v['ms_per_frame'] for n, v in k.items()})"
+}
+run base $L/spectral.so && run w4 $L/w4.so && run divfast $L/divfast.so && run base2 $L/spectral.so && run w4_2 $L/w4.so && run divfast2 $L/divfast.so
