@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define PBRTGPU_ABI_VERSION 10
+#define PBRTGPU_ABI_VERSION 11
 #define PBRTGPU_MAX_BANDS 64
 
 #define PBRTGPU_E_INVALID   (-1)
@@ -94,11 +94,14 @@ enum {
 };
 
 /* Texture<float> / Texture<Spectrum> (texture.h, textures/{constant,scale,imagemap}.cpp).
- * IMAGE textures are the reference's one-texel MIPMap: ReadImage's 1x1 RGB 0.5 fallback for
- * files it cannot decode (imageio.cpp:45-66) or powf(scale, gamma) when a .tga/.pfm is
- * missing (imagemap.cpp:64-70); texels are stored after convertIn.  Lookups follow
- * MIPMap::Lookup (EWA, mipmap.h:278-375, or width-based, :232-259) with the ImageWrap mode,
- * texture coordinates from UVMapping2D (texture.cpp:80-90). */
+ * IMAGE textures are the reference's MIPMap (mipmap.h:119-193): the image ReadImage decodes
+ * (TGA / PFM, imageio.cpp:443-650; a 1x1 RGB 0.5 image for other files, :45-66; the one-valued
+ * powf(scale, gamma) map when a .tga / .pfm cannot be read, imagemap.cpp:64-70) after convertIn,
+ * resampled to powers of two (Lanczos, clamped) and box-filtered into its pyramid; every level in
+ * texels[] from texel_off (level l: max(1, width >> l) x max(1, height >> l) texels, row-major,
+ * 3 floats (RGB) per texel for spectrum textures, 1 for float textures).  Lookups follow
+ * MIPMap::Lookup (EWA, mipmap.h:278-375, or width-based / noFiltering, :232-259) with the
+ * ImageWrap mode, texture coordinates from UVMapping2D (texture.cpp:80-90). */
 enum { PBRTGPU_TEX_CONST = 0, PBRTGPU_TEX_IMAGE = 1, PBRTGPU_TEX_SCALE = 2 };
 enum { PBRTGPU_WRAP_REPEAT = 0, PBRTGPU_WRAP_BLACK = 1, PBRTGPU_WRAP_CLAMP = 2 };
 typedef struct pbrtgpu_texture {
@@ -108,8 +111,11 @@ typedef struct pbrtgpu_texture {
     int32_t spec;          /* CONST spectral: offset into spectra[] */
     int32_t wrap;          /* IMAGE: PBRTGPU_WRAP_* */
     int32_t trilinear;     /* IMAGE: doTrilinear || noFiltering (width-based lookup, no EWA) */
+    int32_t nofilter;      /* IMAGE: noFiltering (the fork's nearest-texel lookup at level 0) */
+    int32_t texel_off;     /* IMAGE: first float of level 0 in texels[] */
+    int32_t width, height; /* IMAGE: level-0 resolution (powers of two) */
+    int32_t levels;        /* IMAGE: nLevels = 1 + Log2Int(max(width, height)) */
     float value;           /* CONST float */
-    float texel[3];        /* IMAGE: the single MIPMap texel (RGB; float textures use [0]) */
     float su, sv, du, dv;  /* UVMapping2D */
     float max_aniso;
 } pbrtgpu_texture;
@@ -280,6 +286,8 @@ typedef struct pbrtgpu_flat_scene {
     int32_t spectral_sampling;    /* SpectralRenderer "samplingMethod": PBRTGPU_SPECTRAL_* */
     int32_t camera_type;          /* PBRTGPU_CAMERA_*: "perspective" (camera) or "realisticDiffraction" (lens) */
     pbrtgpu_lens lens;
+    int32_t n_texel_floats;       /* the MIPMap pyramids of the IMAGE textures (pbrtgpu_texture) */
+    const float *texels;
 } pbrtgpu_flat_scene;
 
 /* SurfaceIntegrator of a flattened scene: "path" (integrators/path.cpp:44-115),
@@ -431,7 +439,9 @@ int pbrtgpu_path_stats(pbrtgpu_ctx *ctx, const int32_t *keys, int32_t n, uint64_
 typedef struct pbrtgpu_timing {
     double ms[4];
     int32_t launches[4];
-    int32_t passes, pad;
+    int32_t passes;
+    int32_t shade_feat;   /* FEAT_* of the k_shade variant the call ran: 0 = lean (no measured BRDF,
+                             texture or environment light), 7 = full (csrc/scene_build.h) */
     uint64_t work[12];
 } pbrtgpu_timing;
 int pbrtgpu_last_timing(pbrtgpu_ctx *ctx, pbrtgpu_timing *out);

@@ -1181,8 +1181,8 @@ static void from_rgb(const Ctx *c, const float rgb[3], int illum, float *r) {
     for (int i = 0; i < nb; ++i) r[i] = clampf(r[i] * sc, 0.f, INFINITY);
 }
 
-/* One-texel MIPMap (mipmap.h): Texel with the wrap mode (:197-222), triangle (:263-274),
- * EWA (:278-375) and the width-based Lookup (:232-259); nc = 3 (RGB) or 1 (float) */
+/* The environment light's one-texel MIPMap (mipmap.h): Texel with the wrap mode (:197-222),
+ * triangle (:263-274); nc = 3 (RGB) or 1 (float) */
 static inline float texel_c(const float *T, int wrap, int s, int t, int k) {
     if (wrap == PBRTGPU_WRAP_BLACK && (s != 0 || t != 0)) return 0.f;
     return T[k];
@@ -1197,11 +1197,57 @@ static void mip_triangle(const float *T, int nc, int wrap, float s, float t, flo
         out[k] = ((w00 * texel_c(T, wrap, s0, t0, k) + w01 * texel_c(T, wrap, s0, t0 + 1, k)) +
                   w10 * texel_c(T, wrap, s0 + 1, t0, k)) + w11 * texel_c(T, wrap, s0 + 1, t0 + 1, k);
 }
-static void mip_ewa0(const Ctx *c, const float *T, int nc, int wrap, float s, float t, float ds0, float dt0, float ds1,
-                     float dt1, float *out) {
-    s = s * 1.f - 0.5f;
-    t = t * 1.f - 0.5f;
-    ds0 *= 1.f; dt0 *= 1.f; ds1 *= 1.f; dt1 *= 1.f;
+/* MIPMap (mipmap.h:119-375) of an IMAGE texture: its pyramid in texels[] from texel_off, level l
+ * max(1, width >> l) x max(1, height >> l) texels of nc floats */
+typedef struct { const float *T; int w, h; } MipLv;
+static MipLv mip_lv(const Ctx *c, const pbrtgpu_texture *tx, int nc, int l) {
+    size_t off = (size_t)tx->texel_off;
+    int w = tx->width, h = tx->height;
+    for (int i = 0; i < l; ++i) {
+        off += (size_t)w * h * nc;
+        w = w > 1 ? w >> 1 : 1;
+        h = h > 1 ? h >> 1 : 1;
+    }
+    MipLv r = {c->s->texels + off, w, h};
+    return r;
+}
+static int mod_i(int a, int b) { int n = a / b; a -= n * b; if (a < 0) a += b; return a; }   /* pbrt.h Mod */
+/* Texel(level, s, t) with the wrap mode (mipmap.h:197-222) */
+static void mip_texel(const MipLv *L, int nc, int wrap, int s, int t, float *out) {
+    if (wrap == PBRTGPU_WRAP_REPEAT) { s = mod_i(s, L->w); t = mod_i(t, L->h); }
+    else if (wrap == PBRTGPU_WRAP_CLAMP) { s = s < 0 ? 0 : (s > L->w - 1 ? L->w - 1 : s); t = t < 0 ? 0 : (t > L->h - 1 ? L->h - 1 : t); }
+    else if (s < 0 || s >= L->w || t < 0 || t >= L->h) { for (int k = 0; k < nc; ++k) out[k] = 0.f; return; }
+    for (int k = 0; k < nc; ++k) out[k] = L->T[((size_t)t * L->w + s) * nc + k];
+}
+/* MIPMap::triangle (mipmap.h:263-274) */
+static void mip_tri(const Ctx *c, const pbrtgpu_texture *tx, int nc, int level, float s, float t, float *out) {
+    level = level < 0 ? 0 : (level > tx->levels - 1 ? tx->levels - 1 : level);
+    const MipLv L = mip_lv(c, tx, nc, level);
+    s = s * (float)(uint32_t)L.w - 0.5f;
+    t = t * (float)(uint32_t)L.h - 0.5f;
+    int s0 = (int)floorf(s), t0 = (int)floorf(t);
+    float ds = s - s0, dt = t - t0;
+    float w00 = (1.f - ds) * (1.f - dt), w01 = (1.f - ds) * dt, w10 = ds * (1.f - dt), w11 = ds * dt;
+    float a[3], b[3], cc[3], d[3];
+    mip_texel(&L, nc, tx->wrap, s0, t0, a);
+    mip_texel(&L, nc, tx->wrap, s0, t0 + 1, b);
+    mip_texel(&L, nc, tx->wrap, s0 + 1, t0, cc);
+    mip_texel(&L, nc, tx->wrap, s0 + 1, t0 + 1, d);
+    for (int k = 0; k < nc; ++k) out[k] = ((w00 * a[k] + w01 * b[k]) + w10 * cc[k]) + w11 * d[k];
+}
+/* MIPMap::EWA (mipmap.h:320-375) */
+static void mip_ewa(const Ctx *c, const pbrtgpu_texture *tx, int nc, int level, float s, float t, float ds0, float dt0,
+                    float ds1, float dt1, float *out) {
+    if (level >= tx->levels) {
+        const MipLv Lt = mip_lv(c, tx, nc, tx->levels - 1);
+        mip_texel(&Lt, nc, tx->wrap, 0, 0, out);
+        return;
+    }
+    const MipLv L = mip_lv(c, tx, nc, level);
+    const float fw = (float)(uint32_t)L.w, fh = (float)(uint32_t)L.h;
+    s = s * fw - 0.5f;
+    t = t * fh - 0.5f;
+    ds0 *= fw; dt0 *= fh; ds1 *= fw; dt1 *= fh;
     float A = dt0 * dt0 + dt1 * dt1 + 1;
     float B = -2.f * (ds0 * dt0 + ds1 * dt1);
     float C = ds0 * ds0 + ds1 * ds1 + 1;
@@ -1220,22 +1266,42 @@ static void mip_ewa0(const Ctx *c, const float *T, int nc, int wrap, float s, fl
             float r2 = A * ss * ss + B * ss * tt + C * tt * tt;
             if (r2 < 1.) {
                 int li = (int)(r2 * 128);
-                float weight = c->s->ewa_lut[li < 127 ? li : 127];
-                for (int k = 0; k < nc; ++k) sum[k] += texel_c(T, wrap, is, it, k) * weight;
+                float weight = c->s->ewa_lut[li < 127 ? li : 127], tv[3];
+                mip_texel(&L, nc, tx->wrap, is, it, tv);
+                for (int k = 0; k < nc; ++k) sum[k] += tv[k] * weight;
                 sumWts += weight;
             }
         }
     }
     for (int k = 0; k < nc; ++k) out[k] = sum[k] / sumWts;
 }
+/* MIPMap::Lookup(s, t, width) (mipmap.h:226-259) with the fork's noFiltering nearest texel */
+static void mip_lookup_w(const Ctx *c, const pbrtgpu_texture *tx, int nc, float s, float t, float width, float *out) {
+    if (tx->nofilter) {
+        const MipLv L = mip_lv(c, tx, nc, 0);
+        s = s * (float)(uint32_t)L.w - 0.5f;
+        t = t * (float)(uint32_t)L.h - 0.5f;
+        mip_texel(&L, nc, tx->wrap, (int)floorf(s + 0.5f), (int)floorf(t + 0.5f), out);   /* Round2Int */
+        return;
+    }
+    float level = (float)(uint32_t)(tx->levels - 1) + log2_(fmaxf_(width, 1e-8f));
+    if (level < 0) mip_tri(c, tx, nc, 0, s, t, out);
+    else if (level >= (float)(uint32_t)(tx->levels - 1)) {
+        const MipLv Lt = mip_lv(c, tx, nc, tx->levels - 1);
+        mip_texel(&Lt, nc, tx->wrap, 0, 0, out);
+    } else {
+        int iLevel = (int)floorf(level);
+        float delta = level - iLevel, a[3], b[3];
+        mip_tri(c, tx, nc, iLevel, s, t, a);
+        mip_tri(c, tx, nc, iLevel + 1, s, t, b);
+        for (int k = 0; k < nc; ++k) out[k] = (1.f - delta) * a[k] + delta * b[k];
+    }
+}
+/* MIPMap::Lookup(s, t, ds0, dt0, ds1, dt1) (mipmap.h:278-318) */
 static void mip_lookup(const Ctx *c, const pbrtgpu_texture *tx, int nc, float s, float t, float ds0, float dt0, float ds1,
                        float dt1, float *out) {
-    const float *T = tx->texel;
-    if (tx->trilinear) {   /* Lookup(s, t, width): level = 0 + Log2(max(width, 1e-8f)) */
-        float width = 2.f * fmaxf_(fmaxf_(fabsf(ds0), fabsf(dt0)), fmaxf_(fabsf(ds1), fabsf(dt1)));
-        float level = 0.f + log2_(fmaxf_(width, 1e-8f));
-        if (level < 0) mip_triangle(T, nc, tx->wrap, s, t, out);
-        else for (int k = 0; k < nc; ++k) out[k] = texel_c(T, tx->wrap, 0, 0, k);
+    if (tx->trilinear) {
+        mip_lookup_w(c, tx, nc, s, t, 2.f * fmaxf_(fmaxf_(fabsf(ds0), fabsf(dt0)), fmaxf_(fabsf(ds1), fabsf(dt1))), out);
         return;
     }
     if (ds0 * ds0 + dt0 * dt0 < ds1 * ds1 + dt1 * dt1) {
@@ -1248,14 +1314,13 @@ static void mip_lookup(const Ctx *c, const pbrtgpu_texture *tx, int nc, float s,
         float scale = majorLength / (minorLength * tx->max_aniso);
         ds1 *= scale; dt1 *= scale; minorLength *= scale;
     }
-    if (minorLength == 0.f) { mip_triangle(T, nc, tx->wrap, s, t, out); return; }
-    float lod = fmaxf_(0.f, 1 - 1.f + log2_(minorLength));
+    if (minorLength == 0.f) { mip_tri(c, tx, nc, 0, s, t, out); return; }
+    float lod = fmaxf_(0.f, (float)(uint32_t)tx->levels - 1.f + log2_(minorLength));
     int ilod = (int)floorf(lod);
-    float d = lod - ilod;
+    float d = lod - (float)(uint32_t)ilod;
     float e0[3], e1[3];
-    if (ilod >= 1) for (int k = 0; k < nc; ++k) e0[k] = texel_c(T, tx->wrap, 0, 0, k);
-    else mip_ewa0(c, T, nc, tx->wrap, s, t, ds0, dt0, ds1, dt1, e0);
-    for (int k = 0; k < nc; ++k) e1[k] = texel_c(T, tx->wrap, 0, 0, k);   /* level ilod + 1 >= nLevels */
+    mip_ewa(c, tx, nc, ilod, s, t, ds0, dt0, ds1, dt1, e0);
+    mip_ewa(c, tx, nc, ilod + 1, s, t, ds0, dt0, ds1, dt1, e1);
     for (int k = 0; k < nc; ++k) out[k] = (1.f - d) * e0[k] + d * e1[k];
 }
 /* texture-space position and screen-space derivatives of the hit (dgs.u, v, dudx, ...) */

@@ -331,8 +331,9 @@ struct DevScene {
     const float4 *kdPack;             // kd nodes packed for the lookup walk (kd_lookup, wavefront.h)
     int nKd, kdInLds;                 // kd nodes in all trees; 1: k_shade copies them to LDS
     const float *merl;                // RegularHalfangleBRDF RGB tables (3 floats per texel)
-    const pbrtgpu_texture *tex;       // texture nodes (one-texel image maps, scale, constants)
+    const pbrtgpu_texture *tex;       // texture nodes (image maps, scale, constants)
     const float *ewa;                 // [128] MIPMap::weightLut
+    const float *texels;              // the image maps' MIPMap pyramids (pbrtgpu_texture::texel_off)
     const float *basis;               // [14][nbp] FromRGB basis spectra, band-quad padded
     int nbp;                          // padded band count (multiple of 4)
     int nInf;                         // infinite lights among lights[]
@@ -1617,8 +1618,8 @@ PGD_INLINE float4 from_rgb4(const DevScene &S, const RGBPick &p, bool illum, int
     return r;
 }
 
-// One-texel MIPMap (mipmap.h): Texel with wrap (:197-222), triangle (:263-274), EWA
-// (:278-375), width-based Lookup (:232-259).  NC = 3 (RGB) or 1 (float).
+// The environment light's one-texel MIPMap (mipmap.h): Texel with wrap (:197-222), triangle
+// (:263-274).  NC = 3 (RGB) or 1 (float).
 PGD_INLINE float log2_(float x) { float invLog2 = 1.f / LOGF(2.f); return LOGF(x) * invLog2; }   // pbrt.h:243-246
 PGD_INLINE float texel_c(const float *T, int wrap, int s, int t, int k) {
     if (wrap == PBRTGPU_WRAP_BLACK && (s != 0 || t != 0)) return 0.f;
@@ -1636,12 +1637,68 @@ PGD_INLINE void mip_triangle(const float *T, int wrap, float s, float t, float *
         out[k] = ((w00 * texel_c(T, wrap, s0, t0, k) + w01 * texel_c(T, wrap, s0, t0 + 1, k)) +
                   w10 * texel_c(T, wrap, s0 + 1, t0, k)) + w11 * texel_c(T, wrap, s0 + 1, t0 + 1, k);
 }
+// MIPMap (mipmap.h:119-375) of an IMAGE texture: its pyramid in S.texels from texel_off,
+// level l max(1, width >> l) x max(1, height >> l) texels of NC floats (3: RGB, 1: float)
+struct MipLv { const float *T; int w, h; };
 template <int NC>
-PGD_INLINE void mip_ewa0(const DevScene &S, const float *T, int wrap, float s, float t, float ds0, float dt0, float ds1,
-                         float dt1, float *out) {
-    s = s * 1.f - 0.5f;
-    t = t * 1.f - 0.5f;
-    ds0 *= 1.f; dt0 *= 1.f; ds1 *= 1.f; dt1 *= 1.f;
+PGD_INLINE MipLv mip_lv(const DevScene &S, const pbrtgpu_texture &tx, int l) {
+    uint32_t off = (uint32_t)tx.texel_off;
+    int w = tx.width, h = tx.height;
+    for (int i = 0; i < l; ++i) {
+        off += (uint32_t)(w * h * NC);
+        w = w > 1 ? w >> 1 : 1;
+        h = h > 1 ? h >> 1 : 1;
+    }
+    MipLv r;
+    r.T = S.texels + off; r.w = w; r.h = h;
+    return r;
+}
+PGD_INLINE int mod_i(int a, int b) { int n = int(a / b); a -= n * b; if (a < 0) a += b; return a; }   // pbrt.h Mod
+// Texel(level, s, t) with the wrap mode (mipmap.h:197-222)
+template <int NC>
+PGD_INLINE void mip_texel(const MipLv &L, int wrap, int s, int t, float *out) {
+    if (wrap == PBRTGPU_WRAP_REPEAT) { s = mod_i(s, L.w); t = mod_i(t, L.h); }
+    else if (wrap == PBRTGPU_WRAP_CLAMP) { s = clampi(s, 0, L.w - 1); t = clampi(t, 0, L.h - 1); }
+    else if (s < 0 || s >= L.w || t < 0 || t >= L.h) {
+#pragma unroll
+        for (int k = 0; k < NC; ++k) out[k] = 0.f;
+        return;
+    }
+    const float *p = L.T + (size_t)(t * L.w + s) * NC;
+#pragma unroll
+    for (int k = 0; k < NC; ++k) out[k] = p[k];
+}
+// MIPMap::triangle (mipmap.h:263-274)
+template <int NC>
+PGD_INLINE void mip_tri(const DevScene &S, const pbrtgpu_texture &tx, int level, float s, float t, float *out) {
+    level = clampi(level, 0, tx.levels - 1);
+    const MipLv L = mip_lv<NC>(S, tx, level);
+    s = s * (float)(uint32_t)L.w - 0.5f;
+    t = t * (float)(uint32_t)L.h - 0.5f;
+    const int s0 = (int)floorf(s), t0 = (int)floorf(t);
+    const float ds = s - s0, dt = t - t0;
+    const float w00 = (1.f - ds) * (1.f - dt), w01 = (1.f - ds) * dt, w10 = ds * (1.f - dt), w11 = ds * dt;
+    float a[NC], b[NC], c[NC], d[NC];
+    mip_texel<NC>(L, tx.wrap, s0, t0, a);
+    mip_texel<NC>(L, tx.wrap, s0, t0 + 1, b);
+    mip_texel<NC>(L, tx.wrap, s0 + 1, t0, c);
+    mip_texel<NC>(L, tx.wrap, s0 + 1, t0 + 1, d);
+#pragma unroll
+    for (int k = 0; k < NC; ++k) out[k] = ((w00 * a[k] + w01 * b[k]) + w10 * c[k]) + w11 * d[k];
+}
+// MIPMap::EWA (mipmap.h:320-375)
+template <int NC>
+PGD_INLINE void mip_ewa(const DevScene &S, const pbrtgpu_texture &tx, int level, float s, float t, float ds0, float dt0,
+                        float ds1, float dt1, float *out) {
+    if (level >= tx.levels) {
+        mip_texel<NC>(mip_lv<NC>(S, tx, tx.levels - 1), tx.wrap, 0, 0, out);
+        return;
+    }
+    const MipLv L = mip_lv<NC>(S, tx, level);
+    const float fw = (float)(uint32_t)L.w, fh = (float)(uint32_t)L.h;
+    s = s * fw - 0.5f;
+    t = t * fh - 0.5f;
+    ds0 *= fw; dt0 *= fh; ds1 *= fw; dt1 *= fh;
     float A = dt0 * dt0 + dt1 * dt1 + 1;
     float B = -2.f * (ds0 * dt0 + ds1 * dt1);
     float C = ds0 * ds0 + ds1 * ds1 + 1;
@@ -1663,8 +1720,10 @@ PGD_INLINE void mip_ewa0(const DevScene &S, const float *T, int wrap, float s, f
             if (r2 < 1.) {
                 int li = (int)(r2 * 128);
                 float weight = (*sa(S.ewa, (uint32_t)(li < 127 ? li : 127)));
+                float tv[NC];
+                mip_texel<NC>(L, tx.wrap, is, it, tv);
 #pragma unroll
-                for (int k = 0; k < NC; ++k) sum[k] += texel_c(T, wrap, is, it, k) * weight;
+                for (int k = 0; k < NC; ++k) sum[k] += tv[k] * weight;
                 sumWts += weight;
             }
         }
@@ -1672,18 +1731,35 @@ PGD_INLINE void mip_ewa0(const DevScene &S, const float *T, int wrap, float s, f
 #pragma unroll
     for (int k = 0; k < NC; ++k) out[k] = sum[k] / sumWts;
 }
+// MIPMap::Lookup(s, t, width) (mipmap.h:226-259), with the fork's noFiltering nearest texel
+template <int NC>
+PGD_INLINE void mip_lookup_w(const DevScene &S, const pbrtgpu_texture &tx, float s, float t, float width, float *out) {
+    if (tx.nofilter) {
+        const MipLv L = mip_lv<NC>(S, tx, 0);
+        s = s * (float)(uint32_t)L.w - 0.5f;
+        t = t * (float)(uint32_t)L.h - 0.5f;
+        mip_texel<NC>(L, tx.wrap, (int)floorf(s + 0.5f), (int)floorf(t + 0.5f), out);   // Round2Int
+        return;
+    }
+    const float level = (float)(uint32_t)(tx.levels - 1) + log2_(pmax(width, 1e-8f));
+    if (level < 0) mip_tri<NC>(S, tx, 0, s, t, out);
+    else if (level >= (float)(uint32_t)(tx.levels - 1)) mip_texel<NC>(mip_lv<NC>(S, tx, tx.levels - 1), tx.wrap, 0, 0, out);
+    else {
+        const int iLevel = (int)floorf(level);
+        const float delta = level - iLevel;
+        float a[NC], b[NC];
+        mip_tri<NC>(S, tx, iLevel, s, t, a);
+        mip_tri<NC>(S, tx, iLevel + 1, s, t, b);
+#pragma unroll
+        for (int k = 0; k < NC; ++k) out[k] = (1.f - delta) * a[k] + delta * b[k];
+    }
+}
+// MIPMap::Lookup(s, t, ds0, dt0, ds1, dt1) (mipmap.h:278-318)
 template <int NC>
 PGD_INLINE void mip_lookup(const DevScene &S, const pbrtgpu_texture &tx, float s, float t, float ds0, float dt0,
                            float ds1, float dt1, float *out) {
-    const float *T = tx.texel;
     if (tx.trilinear) {
-        float width = 2.f * pmax(pmax(fabsf(ds0), fabsf(dt0)), pmax(fabsf(ds1), fabsf(dt1)));
-        float level = 0.f + log2_(pmax(width, 1e-8f));
-        if (level < 0) mip_triangle<NC>(T, tx.wrap, s, t, out);
-        else {
-#pragma unroll
-            for (int k = 0; k < NC; ++k) out[k] = texel_c(T, tx.wrap, 0, 0, k);
-        }
+        mip_lookup_w<NC>(S, tx, s, t, 2.f * pmax(pmax(fabsf(ds0), fabsf(dt0)), pmax(fabsf(ds1), fabsf(dt1))), out);
         return;
     }
     if (ds0 * ds0 + dt0 * dt0 < ds1 * ds1 + dt1 * dt1) {
@@ -1696,17 +1772,15 @@ PGD_INLINE void mip_lookup(const DevScene &S, const pbrtgpu_texture &tx, float s
         float scale = majorLength / (minorLength * tx.max_aniso);
         ds1 *= scale; dt1 *= scale; minorLength *= scale;
     }
-    if (minorLength == 0.f) { mip_triangle<NC>(T, tx.wrap, s, t, out); return; }
-    float lod = pmax(0.f, 1 - 1.f + log2_(minorLength));
+    if (minorLength == 0.f) { mip_tri<NC>(S, tx, 0, s, t, out); return; }
+    float lod = pmax(0.f, (float)(uint32_t)tx.levels - 1.f + log2_(minorLength));
     int ilod = (int)floorf(lod);
-    float d = lod - ilod;
-    float e0[NC];
-    if (ilod >= 1) {
+    float d = lod - (float)(uint32_t)ilod;
+    float e0[NC], e1[NC];
+    mip_ewa<NC>(S, tx, ilod, s, t, ds0, dt0, ds1, dt1, e0);
+    mip_ewa<NC>(S, tx, ilod + 1, s, t, ds0, dt0, ds1, dt1, e1);
 #pragma unroll
-        for (int k = 0; k < NC; ++k) e0[k] = texel_c(T, tx.wrap, 0, 0, k);
-    } else mip_ewa0<NC>(S, T, tx.wrap, s, t, ds0, dt0, ds1, dt1, e0);
-#pragma unroll
-    for (int k = 0; k < NC; ++k) out[k] = (1.f - d) * e0[k] + d * texel_c(T, tx.wrap, 0, 0, k);
+    for (int k = 0; k < NC; ++k) out[k] = (1.f - d) * e0[k] + d * e1[k];
 }
 // hit position in texture space with its screen-space derivatives
 struct TexPt { float u, v, dudx, dvdx, dudy, dvdy; };

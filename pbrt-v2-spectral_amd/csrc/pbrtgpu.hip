@@ -2255,6 +2255,7 @@ int pbrtgpu_last_timing(pbrtgpu_ctx *c, pbrtgpu_timing *out) {
     memset(out, 0, sizeof(*out));
     for (int k = 0; k < K_KINDS; ++k) { out->ms[k] = c->last.ms[k]; out->launches[k] = c->last.launches[k]; }
     out->passes = c->last.passes;
+    out->shade_feat = c->feat;
     for (int i = 0; i < W_COUNT; ++i) out->work[i] = c->last.work[i];
     return 0;
 }

@@ -278,6 +278,21 @@ static inline int scene_check(const pbrtgpu_flat_scene *s, std::string *err) {
         }
         return !(slot && spectral && t.type == PBRTGPU_TEX_CONST);
     };
+    // MIPMap pyramids: power-of-two level 0, nLevels = 1 + floor(log2(max(w, h))), every level
+    // inside the texel pool (the lookups index texels[] without further checks)
+    for (int i = 0; i < s->n_textures; ++i) {
+        const pbrtgpu_texture &t = s->textures[i];
+        if (t.type != PBRTGPU_TEX_IMAGE) continue;
+        const int w = t.width, h = t.height, nc = t.spectral ? 3 : 1;
+        int lv = 0;
+        for (int m = w > h ? w : h; m > 1; m >>= 1) ++lv;
+        if (w < 1 || h < 1 || w > (1 << 24) || h > (1 << 24) || (w & (w - 1)) || (h & (h - 1)) || t.levels != lv + 1 ||
+            t.texel_off < 0 || !s->texels)
+            SB_FAIL(PBRTGPU_E_INVALID, "image texture pyramid");
+        int64_t n = 0;
+        for (int l = 0; l < t.levels; ++l) n += (int64_t)(w >> l > 1 ? w >> l : 1) * (h >> l > 1 ? h >> l : 1) * nc;
+        if ((int64_t)t.texel_off + n > (int64_t)s->n_texel_floats) SB_FAIL(PBRTGPU_E_INVALID, "image texture texels out of range");
+    }
     for (int i = 0; i < s->n_materials; ++i) {
         const pbrtgpu_material &m = s->materials[i];
         if (m.type < PBRTGPU_MAT_MATTE || m.type > PBRTGPU_MAT_MEASURED_HALFANGLE)
@@ -477,6 +492,8 @@ static int scene_build(const pbrtgpu_flat_scene *s, int topNodes, DevScene &S, i
     SB_PUT(texs.data(), texs.size(), &S.tex);
     SB_PUT(basis.data(), basis.size(), &S.basis);
     SB_PUT(s->ewa_lut, (size_t)128, &S.ewa);
+    S.texels = nullptr;
+    if (s->n_texel_floats > 0) SB_PUT(s->texels, (size_t)s->n_texel_floats, &S.texels);
     SB_PUT(pt.data(), pt.size(), &S.primTri);
     SB_PUT(s->tris, (size_t)s->n_tris, &S.tris);
     SB_PUT(s->meshes, (size_t)s->n_meshes, &S.meshes);

@@ -571,6 +571,209 @@ extern "C" int pbrthost_loop_refine(int32_t nf, int32_t nv, const int32_t *vi, c
 }
 
 // ------------------------------------------------------------------------------------
+// Image maps: ReadImage for the formats this build reads without OpenEXR (imageio.cpp:45-66),
+// the decoders' texel values (RGBSpectrum, 3 floats per texel) and MIPMap construction
+// (mipmap.h:119-193).  Float expressions in the reference's operand order.
+// ------------------------------------------------------------------------------------
+// ReadImageTGA (imageio.cpp:443-533): uncompressed true colour (24 / 32 bit) and 8-bit grey;
+// the 18-byte header is followed directly by the pixels (the ID field is not skipped); texels in
+// the file's row order, then the origin bits' horizontal / vertical flips.  false: the reference
+// returns NULL (Error)
+static bool ReadTGA(const std::string &fn, std::vector<float> &rgb, int *w, int *h) {
+    FILE *f = fopen(fn.c_str(), "rb");
+    if (!f) return false;
+    unsigned char hd[18] = {0};
+    const size_t nh = fread(hd, 1, 18, f);
+    (void)nh;   // the reference reads its fields with unchecked fread calls
+    auto s16 = [&](int o) { return (int)(int16_t)(uint16_t)(hd[o] | (hd[o + 1] << 8)); };
+    const int imageType = hd[2], width = s16(12), height = s16(14), depth = hd[16], attr = hd[17];
+    if (((attr & 0xf) != 8 && (attr & 0xf) != 0) || (attr & 0xc0) != 0 ||
+        (imageType == 2 && depth != 32 && depth != 24) || (imageType == 3 && depth != 8) ||
+        (imageType != 2 && imageType != 3) || width <= 0 || height <= 0) {
+        fclose(f);
+        return false;
+    }
+    const int pixbytes = depth == 32 ? 4 : (depth == 24 ? 3 : 1);
+    const size_t size = (size_t)width * height * pixbytes;
+    std::vector<unsigned char> src(size);
+    const bool got = fread(src.data(), 1, size, f) == size;
+    fclose(f);
+    if (!got) return false;   // "Premature end-of-file"
+    rgb.assign((size_t)width * height * 3, 0.f);
+    const unsigned char *p = src.data();
+    for (size_t i = 0; i < (size_t)width * height; ++i) {
+        if (pixbytes == 1) {
+            const float v = (*p++) / 255.f;
+            rgb[3 * i] = rgb[3 * i + 1] = rgb[3 * i + 2] = v;   // RGBSpectrum(v)
+        } else {
+            const float b = (*p++) / 255.f, g = (*p++) / 255.f, r = (*p++) / 255.f;
+            rgb[3 * i] = r; rgb[3 * i + 1] = g; rgb[3 * i + 2] = b;   // FromRGB(c)
+            if (pixbytes == 4) ++p;
+        }
+    }
+    auto swapTexel = [&](size_t a, size_t b) { for (int k = 0; k < 3; ++k) std::swap(rgb[3 * a + k], rgb[3 * b + k]); };
+    if (attr & 0x10)
+        for (int y = 0; y < height; ++y)
+            for (int x = 0; x < width / 2; ++x) swapTexel((size_t)y * width + x, (size_t)y * width + (width - 1 - x));
+    if (attr & 0x20)
+        for (int y = 0; y < height / 2; ++y)
+            for (int x = 0; x < width; ++x) swapTexel((size_t)y * width + x, (size_t)(height - 1 - y) * width + x);
+    *w = width; *h = height;
+    return true;
+}
+// ReadImagePFM (imageio.cpp:574-650): "Pf" (grey) / "PF" (RGB) header words split at ' ', '\n'
+// and '\t', |scale| != 1 multiplies, its sign gives the byte order; no vertical flip
+static bool ReadPFM(const std::string &fn, std::vector<float> &rgb, int *w, int *h) {
+    FILE *f = fopen(fn.c_str(), "rb");
+    if (!f) return false;
+    auto word = [&](std::string &s) -> bool {   // readWord: up to 80 characters before whitespace
+        s.clear();
+        int c = fgetc(f);
+        while (c != EOF && (char)c != ' ' && (char)c != '\n' && (char)c != '\t' && s.size() < 80) {
+            s.push_back((char)c);
+            c = fgetc(f);
+        }
+        return s.size() < 80;
+    };
+    std::string tok;
+    int nc = 0;
+    bool ok = word(tok);
+    if (ok) nc = tok == "Pf" ? 1 : (tok == "PF" ? 3 : 0);
+    ok = ok && nc > 0;
+    int width = 0, height = 0;
+    float scale = 0.f;
+    ok = ok && word(tok);
+    if (ok) width = atoi(tok.c_str());
+    ok = ok && word(tok);
+    if (ok) height = atoi(tok.c_str());
+    ok = ok && word(tok);
+    if (ok) sscanf(tok.c_str(), "%f", &scale);
+    ok = ok && width > 0 && height > 0;
+    std::vector<float> data;
+    if (ok) {
+        data.resize((size_t)nc * width * height);
+        ok = fread(data.data(), sizeof(float), data.size(), f) == data.size();
+    }
+    fclose(f);
+    if (!ok) return false;
+    if (!(scale < 0.f))   // big-endian file on this little-endian host
+        for (float &v : data) {
+            uint8_t b[4];
+            memcpy(b, &v, 4);
+            std::swap(b[0], b[3]); std::swap(b[1], b[2]);
+            memcpy(&v, b, 4);
+        }
+    if (fabsf(scale) != 1.f)
+        for (float &v : data) v *= fabsf(scale);
+    rgb.assign((size_t)width * height * 3, 0.f);
+    for (size_t i = 0; i < (size_t)width * height; ++i)
+        for (int k = 0; k < 3; ++k) rgb[3 * i + k] = nc == 1 ? data[i] : data[3 * i + k];
+    *w = width; *h = height;
+    return true;
+}
+static float Lanczos(float x, float tau = 2.f) {   // texture.cpp:258-266 (M_PI a float literal, pbrt.h:179)
+    x = fabsf(x);
+    if (x < 1e-5) return 1;
+    if (x > 1.) return 0;
+    x *= 3.14159265358979323846f;
+    float s = sinf(x * tau) / (x * tau);
+    float lanczos = sinf(x) / x;
+    return s * lanczos;
+}
+static int ModI(int a, int b) { int n = int(a / b); a -= n * b; if (a < 0) a += b; return a; }   // pbrt.h Mod
+static float Log2f(float x) { static float invLog2 = 1.f / logf(2.f); return logf(x) * invLog2; }   // pbrt.h:243-246
+// MIPMap<T>(sres, tres, img, ..., wrapMode) (mipmap.h:119-193) for NC floats per texel (3: the
+// RGBSpectrum of a spectrum texture, 1: a float texture): every pyramid level appended to `out`,
+// level 0 first; returns (width, height, nLevels)
+static void BuildMipmap(int sres, int tres, std::vector<float> img, int nc, int wrap, std::vector<float> &out, int *W,
+                        int *H, int *levels) {
+    auto isPow2 = [](int v) { return (v & (v - 1)) == 0; };
+    auto roundUpPow2 = [](uint32_t v) { v--; v |= v >> 1; v |= v >> 2; v |= v >> 4; v |= v >> 8; v |= v >> 16; return v + 1; };
+    struct RW { int first; float w[4]; };
+    auto weights = [&](uint32_t oldres, uint32_t newres) {   // resampleWeights (mipmap.h:75-96)
+        std::vector<RW> wt(newres);
+        const float filterwidth = 2.f;
+        for (uint32_t i = 0; i < newres; ++i) {
+            float center = (i + .5f) * oldres / newres;
+            wt[i].first = (int)floorf((center - filterwidth) + 0.5f);
+            for (int j = 0; j < 4; ++j) {
+                float pos = wt[i].first + j + .5f;
+                wt[i].w[j] = Lanczos((pos - center) / filterwidth);
+            }
+            float invSumWts = 1.f / (wt[i].w[0] + wt[i].w[1] + wt[i].w[2] + wt[i].w[3]);
+            for (int j = 0; j < 4; ++j) wt[i].w[j] *= invSumWts;
+        }
+        return wt;
+    };
+    auto wrapIdx = [&](int v, int n) {
+        if (wrap == PBRTGPU_WRAP_REPEAT) return ModI(v, n);
+        if (wrap == PBRTGPU_WRAP_CLAMP) return v < 0 ? 0 : (v > n - 1 ? n - 1 : v);
+        return v;
+    };
+    if (!isPow2(sres) || !isPow2(tres)) {
+        const uint32_t sPow2 = roundUpPow2((uint32_t)sres), tPow2 = roundUpPow2((uint32_t)tres);
+        std::vector<float> res((size_t)sPow2 * tPow2 * nc, 0.f);
+        const std::vector<RW> sw = weights((uint32_t)sres, sPow2);
+        for (int t = 0; t < tres; ++t)
+            for (uint32_t s = 0; s < sPow2; ++s) {
+                float *o = &res[((size_t)t * sPow2 + s) * nc];
+                for (int k = 0; k < nc; ++k) o[k] = 0.f;
+                for (int j = 0; j < 4; ++j) {
+                    const int origS = wrapIdx(sw[s].first + j, sres);
+                    if (origS >= 0 && origS < sres)
+                        for (int k = 0; k < nc; ++k) o[k] += img[((size_t)t * sres + origS) * nc + k] * sw[s].w[j];
+                }
+            }
+        const std::vector<RW> tw = weights((uint32_t)tres, tPow2);
+        std::vector<float> work((size_t)tPow2 * nc);
+        for (uint32_t s = 0; s < sPow2; ++s) {
+            for (uint32_t t = 0; t < tPow2; ++t) {
+                float *o = &work[(size_t)t * nc];
+                for (int k = 0; k < nc; ++k) o[k] = 0.f;
+                for (int j = 0; j < 4; ++j) {
+                    const int off = wrapIdx(tw[t].first + j, tres);
+                    if (off >= 0 && off < tres)
+                        for (int k = 0; k < nc; ++k) o[k] += res[((size_t)off * sPow2 + s) * nc + k] * tw[t].w[j];
+                }
+            }
+            for (uint32_t t = 0; t < tPow2; ++t)
+                for (int k = 0; k < nc; ++k) {   // clamp(v): Clamp(v, 0, INFINITY)
+                    const float v = work[(size_t)t * nc + k];
+                    res[((size_t)t * sPow2 + s) * nc + k] = v < 0.f ? 0.f : (v > INFINITY ? INFINITY : v);
+                }
+        }
+        img.swap(res);
+        sres = (int)sPow2;
+        tres = (int)tPow2;
+    }
+    const int nLevels = 1 + (int)floorf(Log2f(float(std::max(sres, tres))));   // 1 + Log2Int
+    const size_t base = out.size();
+    out.insert(out.end(), img.begin(), img.end());
+    size_t prev = base;
+    int pw = sres, ph = tres;
+    for (int i = 1; i < nLevels; ++i) {
+        const int sR = std::max(1, pw / 2), tR = std::max(1, ph / 2);
+        const size_t cur = out.size();
+        out.resize(cur + (size_t)sR * tR * nc);
+        auto texel = [&](int s, int t, int k) -> float {   // Texel(i - 1, s, t) with the wrap mode
+            if (wrap == PBRTGPU_WRAP_REPEAT) { s = ModI(s, pw); t = ModI(t, ph); }
+            else if (wrap == PBRTGPU_WRAP_CLAMP) { s = s < 0 ? 0 : (s > pw - 1 ? pw - 1 : s); t = t < 0 ? 0 : (t > ph - 1 ? ph - 1 : t); }
+            else if (s < 0 || s >= pw || t < 0 || t >= ph) return 0.f;
+            return out[prev + ((size_t)t * pw + s) * nc + k];
+        };
+        for (int t = 0; t < tR; ++t)
+            for (int s = 0; s < sR; ++s)
+                for (int k = 0; k < nc; ++k)
+                    out[cur + ((size_t)t * sR + s) * nc + k] =
+                        .25f * (texel(2 * s, 2 * t, k) + texel(2 * s + 1, 2 * t, k) + texel(2 * s, 2 * t + 1, k) +
+                                texel(2 * s + 1, 2 * t + 1, k));
+        prev = cur;
+        pw = sR;
+        ph = tR;
+    }
+    *W = sres; *H = tres; *levels = nLevels;
+}
+
 class Builder {
 public:
     Builder(const std::string &path, const RenderOverrides &ov, HostScene *out)
@@ -856,21 +1059,20 @@ private:
         t.su = t.sv = 1.f; t.max_aniso = 8.f;
         return t;
     }
-    // What ReadImage (imageio.cpp:45-66) does with a file in this build (no OpenEXR):
-    // 0 = returns the 1x1 RGB 0.5 image (unknown suffix), 1 = returns NULL (.tga/.pfm that
-    // cannot be opened); a readable .tga/.pfm would be decoded -- not supported yet.
-    int ImageFileKind(const std::string &fn) {
-        if (fn.size() >= 5) {
-            std::string suf = fn.substr(fn.size() - 4);
-            if (suf == ".tga" || suf == ".TGA" || suf == ".pfm" || suf == ".PFM") {
-                FILE *f = fopen(fn.c_str(), "rb");
-                if (f) { fclose(f); throw std::runtime_error("image file " + fn + ": decoded image maps are not supported yet"); }
-                return 1;
-            }
-        }
-        return 0;
+    // ReadImage (imageio.cpp:45-66) in this build (no OpenEXR): a .tga / .pfm is decoded (false:
+    // the decoder returned NULL), any other file gives the 1x1 RGB 0.5 image
+    bool ReadImageFile(const std::string &fn, std::vector<float> &rgb, int *w, int *h) {
+        std::string suf = fn.size() >= 5 ? fn.substr(fn.size() - 4) : std::string();
+        if (suf == ".tga" || suf == ".TGA") return ReadTGA(fn, rgb, w, h);
+        if (suf == ".pfm" || suf == ".PFM") return ReadPFM(fn, rgb, w, h);
+        rgb.assign(3, 0.5f);
+        *w = *h = 1;
+        return true;
     }
-    // ImageTexture (imagemap.cpp:47-73 GetTexture, :97-160 Create*): a one-texel MIPMap
+    // ImageTexture (imagemap.cpp:47-73 GetTexture, :97-160 Create*): the image after convertIn --
+    // Pow(scale * rgb, gamma) per channel, or powf(scale * rgb.y(), gamma) for a float texture --
+    // in a MIPMap pyramid (BuildMipmap) in out->texels; an unreadable .tga / .pfm gives the
+    // one-valued MIPMap(1, 1, powf(scale, gamma)) with the MIPMap defaults
     int MakeImageTexture(const ParamSet &p, bool spectral) {
         if (spec.rgb()) throw std::runtime_error("image textures are not supported in the RGB build");
         pbrtgpu_texture t = TexNode(PBRTGPU_TEX_IMAGE, spectral);
@@ -885,20 +1087,31 @@ private:
         float scale = GetFloat(p, p, "scale", 1.f), gamma = GetFloat(p, p, "gamma", 1.f);
         std::string fn = GetString(p, p, "filename", "");
         if (!fn.empty()) fn = Resolve(fn);
-        if (ImageFileKind(fn) == 0) {
-            // RGB 0.5 texel through convertIn: Pow(scale * rgb, gamma) / powf(scale * rgb.y(), gamma)
-            if (spectral) for (int k = 0; k < 3; ++k) t.texel[k] = powf(scale * 0.5f, gamma);
-            else t.texel[0] = powf(scale * (0.212671f * 0.5f + 0.715160f * 0.5f + 0.072169f * 0.5f), gamma);
+        const int nc = spectral ? 3 : 1;
+        std::vector<float> rgb, img;
+        int w = 0, h = 0;
+        t.texel_off = (int)out->texels.size();
+        if (ReadImageFile(fn, rgb, &w, &h)) {
+            img.resize((size_t)w * h * nc);
+            for (size_t i = 0; i < (size_t)w * h; ++i) {
+                if (spectral)
+                    for (int k = 0; k < 3; ++k) img[3 * i + k] = powf(rgb[3 * i + k] * scale, gamma);
+                else   // RGBSpectrum::y(): YWeight . c
+                    img[i] = powf(scale * (0.212671f * rgb[3 * i] + 0.715160f * rgb[3 * i + 1] + 0.072169f * rgb[3 * i + 2]),
+                                  gamma);
+            }
             t.trilinear = (trilerp || noFilt) ? 1 : 0;
+            t.nofilter = noFilt ? 1 : 0;
             t.max_aniso = maxAniso;
             t.wrap = wm;
         } else {
-            // one-valued MIPMap(1, 1, &powf(scale, gamma)) with the MIPMap defaults
-            float v = powf(scale, gamma);
-            for (int k = 0; k < 3; ++k) t.texel[k] = spectral ? v : 0.f;
-            if (!spectral) t.texel[0] = v;
-            t.trilinear = 0; t.max_aniso = 8.f; t.wrap = PBRTGPU_WRAP_REPEAT;
+            w = h = 1;
+            img.assign((size_t)nc, powf(scale, gamma));
+            t.trilinear = 0; t.nofilter = 0; t.max_aniso = 8.f; t.wrap = PBRTGPU_WRAP_REPEAT;
         }
+        if ((size_t)out->texels.size() + (size_t)w * h * nc * 2 > (size_t)INT32_MAX)
+            throw std::runtime_error("image map " + fn + ": texel pool exceeds 2^31 floats");
+        BuildMipmap(w, h, std::move(img), nc, t.wrap, out->texels, &t.width, &t.height, &t.levels);
         return AddTexture(t);
     }
     // operand of a ScaleTexture: a CONST or IMAGE node
@@ -1269,8 +1482,14 @@ private:
             float rgb[3];
             spec.ToRGB(lo->L, rgb);   // L.ToRGBSpectrum()
             float texel[3] = {rgb[0], rgb[1], rgb[2]};
-            if (texmap != "" && ImageFileKind(Resolve(texmap)) == 0)
-                for (int k = 0; k < 3; ++k) texel[k] = 0.5f * rgb[k];   // RGB 0.5 texel *= L.ToRGBSpectrum()
+            if (texmap != "") {   // ReadImage (imageio.cpp:45-66): NULL keeps the one texel L
+                std::vector<float> img;
+                int w = 0, h = 0;
+                if (ReadImageFile(Resolve(texmap), img, &w, &h)) {
+                    if (w != 1 || h != 1) throw std::runtime_error("environment image maps are not supported yet: " + texmap);
+                    for (int k = 0; k < 3; ++k) texel[k] = img[k] * rgb[k];   // texels[i] *= L.ToRGBSpectrum()
+                }
+            }
             for (int k = 0; k < 3; ++k) lo->l.texel[k] = texel[k];
             lo->l.wrap = PBRTGPU_WRAP_REPEAT;
             // Distribution2D of img[0] = Lookup(0, 0, 1).y() * sinTheta (one texel: Texel(0, 0, 0))
@@ -1977,6 +2196,8 @@ void HostScene::Flat(pbrtgpu_flat_scene *f) const {
     f->spectral_sampling = spectralSampling;
     f->camera_type = cameraType;
     f->lens = lens;
+    f->n_texel_floats = (int32_t)texels.size();
+    f->texels = texels.empty() ? nullptr : texels.data();
     f->lens.n_elements = (int)lensEl.size() / 4;
     f->lens.elements = lensEl.empty() ? nullptr : lensEl.data();
     f->lens.eye_ior = lens.ior_eye && (int)eyeIor.size() == 4 * nBands ? eyeIor.data() : nullptr;

@@ -11,8 +11,15 @@
 namespace pbrtamd {
 
 static const char kMagic[8] = {'P', 'B', 'R', 'T', 'P', 'A', 'C', 'K'};
-static const uint32_t kVersion = 10;   // 6: + merl tables; 7: + metadata ids; 8: + Renderer; 9: + lens diffraction;
-                                       // 10: + pinhole array / microlens / eye IOR (5-9 still load)
+static const uint32_t kVersion = 11;   // 6: + merl tables; 7: + metadata ids; 8: + Renderer; 9: + lens diffraction;
+                                       // 10: + pinhole array / microlens / eye IOR; 11: image maps as MIPMap
+                                       // pyramids (texture records + texel pool; 5-10 still load)
+
+// the texture record of packs before v11: one MIPMap texel inline (the one-texel maps they held)
+struct TexV10 {
+    int32_t type, spectral, tex1, tex2, spec, wrap, trilinear;
+    float value, texel[3], su, sv, du, dv, max_aniso;
+};
 
 static bool W(gzFile f, const void *p, size_t n) {
     const char *c = (const char *)p;
@@ -88,6 +95,8 @@ bool SavePack(const HostScene &s, const std::string &path, std::string *err) {
     ok = ok && W(f, &ct, 4) && W(f, &s.lens, sizeof(s.lens)) && WArr(f, s.lensEl);
     // v10: the eye IOR spectra (the pinhole array is derived at the film resolution, Flat)
     ok = ok && WArr(f, s.eyeIor);
+    // v11: the texel pool of the MIPMap pyramids
+    ok = ok && WArr(f, s.texels);
     ok = (gzclose(f) == Z_OK) && ok;
     if (!ok && err) *err = "write error on " + path;
     return ok;
@@ -106,8 +115,27 @@ bool LoadPack(const std::string &path, HostScene *s, std::string *err) {
     ok = ok && RArr(f, s->bandY) && RArr(f, s->nodes) && RArr(f, s->prims) && RArr(f, s->tris) && RArr(f, s->meshes) &&
          RArr(f, s->vertP) && RArr(f, s->vertN) && RArr(f, s->vertUV) && RArr(f, s->quadrics) && RArr(f, s->materials) &&
          RArr(f, s->lights) && RArr(f, s->lightShapes) && RArr(f, s->spectra) && RArr(f, s->instances) &&
-         RArr(f, s->primInstance) && RArr(f, s->kdnodes) && RArr(f, s->textures) && RArr(f, s->ewaLut) &&
-         RArr(f, s->rgbBasis);
+         RArr(f, s->primInstance) && RArr(f, s->kdnodes);
+    std::vector<TexV10> oldTex;
+    ok = ok && (ver >= 11 ? RArr(f, s->textures) : RArr(f, oldTex));
+    ok = ok && RArr(f, s->ewaLut) && RArr(f, s->rgbBasis);
+    s->texels.clear();
+    if (ok && ver < 11) {   // each one-texel map becomes a 1x1 pyramid in the texel pool
+        s->textures.resize(oldTex.size());
+        for (size_t i = 0; i < oldTex.size(); ++i) {
+            const TexV10 &o = oldTex[i];
+            pbrtgpu_texture &t = s->textures[i];
+            memset(&t, 0, sizeof(t));
+            t.type = o.type; t.spectral = o.spectral; t.tex1 = o.tex1; t.tex2 = o.tex2; t.spec = o.spec; t.wrap = o.wrap;
+            t.trilinear = o.trilinear; t.value = o.value; t.su = o.su; t.sv = o.sv; t.du = o.du; t.dv = o.dv;
+            t.max_aniso = o.max_aniso;
+            if (t.type == PBRTGPU_TEX_IMAGE) {
+                t.texel_off = (int32_t)s->texels.size();
+                t.width = t.height = t.levels = 1;
+                for (int k = 0; k < (o.spectral ? 3 : 1); ++k) s->texels.push_back(o.texel[k]);
+            }
+        }
+    }
     s->merl.clear();
     s->integrator = 0;   // packs before v6: the configs' "path" 
     s->dlStrategy = 0;
@@ -149,6 +177,7 @@ bool LoadPack(const std::string &path, HostScene *s, std::string *err) {
     }
     s->eyeIor.clear();
     if (ok && ver >= 10) ok = RArr(f, s->eyeIor);
+    if (ok && ver >= 11) ok = RArr(f, s->texels);
     gzclose(f);
     if (!ok && err) *err = "bad or truncated scene pack " + path;
     return ok;

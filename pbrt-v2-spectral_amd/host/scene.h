@@ -61,6 +61,7 @@ struct HostScene {
     std::vector<int32_t> primInstance;        // per prim: owning instance or -1
     std::vector<pbrtgpu_kdnode> kdnodes;      // measured BRDF kd-trees
     std::vector<pbrtgpu_texture> textures;
+    std::vector<float> texels;                // MIPMap pyramids of the IMAGE textures (pbrtgpu_texture)
     std::vector<float> ewaLut;                // [128] MIPMap::weightLut
     std::vector<float> rgbBasis;              // [14][nBands] FromRGB basis spectra
     std::vector<float> merl;                  // RegularHalfangleBRDF RGB tables (pbrtgpu_flat_scene::merl)

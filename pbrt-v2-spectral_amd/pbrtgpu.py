@@ -71,7 +71,8 @@ class FlatScene(ctypes.Structure):
                 ("n_textures", I32), ("textures", P), ("ewa_lut", P), ("rgb_basis", P),
                 ("n_merl_floats", I32), ("merl", P), ("integrator", I32), ("dl_strategy", I32),
                 ("meta_strategy", I32), ("prim_meta", P), ("renderer", I32), ("wave_bands", I32),
-                ("spectral_sampling", I32), ("camera_type", I32), ("lens", Lens)]
+                ("spectral_sampling", I32), ("camera_type", I32), ("lens", Lens),
+                ("n_texel_floats", I32), ("texels", P)]
 
 
 PBRTHOST_ABI_VERSION = 2   # include/pbrthost.h
@@ -98,11 +99,11 @@ class RenderDesc(ctypes.Structure):
 STAT_PATHS, STAT_KERNEL_MS, STAT_ACCUM_MS, STAT_ZEROED, STAT_SPILLS, STAT_PASSES = 0, 1, 2, 3, 4, 5
 F_ACCUMULATE, F_COUNT_WORK = 1, 2
 KEEP_SEED = 0xFFFFFFFF
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 
 class Timing(ctypes.Structure):
-    _fields_ = [("ms", ctypes.c_double * 4), ("launches", I32 * 4), ("passes", I32), ("pad", I32),
+    _fields_ = [("ms", ctypes.c_double * 4), ("launches", I32 * 4), ("passes", I32), ("shade_feat", I32),
                 ("work", ctypes.c_uint64 * 12)]
     KERNELS = ("k_trace_closest", "k_trace_shadow", "k_shade", "k_accum")
     WORK = ("rays", "shadow_rays", "nodes_closest", "nodes_shadow", "tris_closest", "tris_shadow", "quads_closest",
@@ -534,7 +535,7 @@ class Device:
         """Per-kernel device ms / launches of the last call, passes, and work counters."""
         t = Timing()
         _check(self.lib.pbrtgpu_last_timing(self.ctx, ctypes.byref(t)))
-        out = {"passes": t.passes}
+        out = {"passes": t.passes, "shade_feat": t.shade_feat}
         for i, k in enumerate(Timing.KERNELS):
             out[k] = {"ms": t.ms[i], "launches": t.launches[i]}
         out["work"] = {k: int(t.work[i]) for i, k in enumerate(Timing.WORK)}

@@ -76,13 +76,16 @@ CASES = [
     (EYE, dict(xres=48, yres=36, spp=2, maxdepth=5)),
     (EYE, dict(xres=48, yres=36, spp=2, maxdepth=5, renderer="spectral", wave_bands=8, sampling="single")),
     (LENS_D, dict(xres=32, yres=24, spp=2, maxdepth=5, integrator="directlighting", strategy="all")),
+    ("imagemap.pack", dict(xres=48, yres=36, spp=4, maxdepth=3)),
+    ("imagemap.pack", dict(xres=40, yres=30, spp=2, maxdepth=3, integrator="directlighting", strategy="all")),
 ]
 
 
 @pytest.mark.parametrize("pack,a", CASES, ids=["dl_all_md6", "dl_one", "dl_killeroo", "path_coverage", "path_anim",
                                                "path_bunny", "path_metal60", "metadata", "path_coverage_b30",
                                                "lens_diffraction", "lens_diffraction_spectral", "lens_pinholes",
-                                               "lens_microlens_spectral", "eye", "eye_spectral", "lens_diffraction_dl"])
+                                               "lens_microlens_spectral", "eye", "eye_spectral", "lens_diffraction_dl",
+                                               "imagemap", "imagemap_dl"])
 def test_replay_matches_oracle(pg, tmp_path, pack, a):
     exe = _build("shade_host")
     scene = pg.Scene.load(os.path.join(PACKS, pack), **a)

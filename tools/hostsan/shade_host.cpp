@@ -85,6 +85,7 @@ static void unpoison_flat(const pbrtgpu_flat_scene *s) {
     if (s->n_instances > 0) u(s->prim_instance, 4 * (size_t)s->n_prims);
     u(s->kdnodes, sizeof(*s->kdnodes) * (size_t)std::max(0, s->n_kdnodes));
     u(s->textures, sizeof(*s->textures) * (size_t)std::max(0, s->n_textures));
+    u(s->texels, 4 * (size_t)std::max(0, s->n_texel_floats));
     u(s->ewa_lut, 4 * 128);
     u(s->rgb_basis, 4 * 14 * (size_t)s->n_bands);
     u(s->merl, 4 * (size_t)std::max(0, s->n_merl_floats));

@@ -47,12 +47,15 @@ Fixtures (numpy .npz, inputs + expected outputs only):
                                   reference's own SpectralImageNoCameraFilm wrote for the same
                                   samples (--refdat): pins AddSample and the WriteImage payload
   *_b30_*, fromrgb_30.npz         the upstream 30-band build (b30 harness, 400-700 nm)
+  imagemap_*                      tests/scenes/imagemap.pbrt: TGA / PFM image maps decoded by the
+                                  reference's imageio.cpp into MIPMap pyramids (mipmap.h): EWA
+                                  over several levels, trilinear, noFiltering, repeat / clamp / black
   <scene>_window_<cfg>_*.npz      film crops at the configs' REAL size and sample count: every
                                   sample of a one-pixel-larger window (--window), so each cropped
                                   pixel holds all of its contributions (incl. exact-boundary samples
                                   of its neighbours, spectralImage.cpp:77-152); C2 at the sphere
                                   light's edge and at a killeroo silhouette, C3-C5 at an edge each
-Usage: python tools/make_golden.py [--only keys|dat|merl|dl|meta|spec|rgb|b30|window]
+Usage: python tools/make_golden.py [--only keys|dat|merl|dl|meta|spec|rgb|b30|window|imagemap]
        (after `make -C oracle ref`, `ref60`, `ref30` and `refrgb`)
 """
 import os
@@ -288,6 +291,15 @@ def merl_fixtures(tmp):
     film_fixture("merl_film_64x48s8", (64, 48), 8, 0, 5, tmp, scene=scene)
 
 
+def imagemap_fixtures(tmp):
+    """tests/scenes/imagemap.pbrt: decoded TGA / PFM image maps in MIPMap pyramids (EWA over
+    several levels, trilinear, noFiltering, the three wrap modes, float and spectrum textures)"""
+    sc = os.path.join(ROOT, "tests", "scenes", "imagemap.pbrt")
+    paths_fixture("imagemap_paths_64x48s4", (64, 48), 4, 0, 3, 1, tmp, scene=sc)
+    film_fixture("imagemap_film_64x48s8", (64, 48), 8, 0, 3, tmp, scene=sc)
+    paths_fixture("imagemap_paths_96x72s2_seed5", (96, 72), 2, 5, 3, 2, tmp, scene=sc)
+
+
 def main():
     if not os.path.exists(HARNESS):
         sys.exit("build the reference harness first: make -C oracle ref")
@@ -314,6 +326,8 @@ def main():
                 rgb_fixtures(tmp)
             elif only == "b30":
                 b30_fixtures(tmp)
+            elif only == "imagemap":
+                imagemap_fixtures(tmp)
             elif only == "window":
                 sel = sys.argv[3:]
                 for cfg in WINDOW_CONFIGS:
@@ -349,6 +363,7 @@ def main():
             if cfg[5] != 60 or os.path.exists(HARNESS60):
                 window_fixture(*cfg, tmp)
         merl_fixtures(tmp)
+        imagemap_fixtures(tmp)
         dl_fixtures(tmp)
         meta_fixtures(tmp)
         spec_fixtures(tmp)

@@ -25,6 +25,8 @@ PACKS = [
     # the upstream 30-band, 400-700 nm sampling (spectrum.h.original:36-38; BASELINE's "30 bands")
     ("killeroo-simple-b30", "killeroo-simple.pbrt", 30, 700, 700, 256),
     ("coverage-b30", os.path.join(ROOT, "tests", "scenes", "coverage.pbrt"), 30, 64, 48, 8),
+    # decoded TGA / PFM image maps in MIPMap pyramids (tests/scenes/textures, tools/make_images.py)
+    ("imagemap", os.path.join(ROOT, "tests", "scenes", "imagemap.pbrt"), 32, 64, 48, 4),
 ]
 
 
@@ -37,7 +39,7 @@ def main():
             continue
         # the configs render with "path" (SURVEY App. B); load a pack with integrator="directlighting"
         # to render it with the DirectLightingIntegrator the scene files name
-        s = pg.Scene.load(os.path.join(REF, fn), xres=xr, yres=yr, spp=spp, maxdepth=-1 if name.startswith("coverage") else 5,
+        s = pg.Scene.load(os.path.join(REF, fn), xres=xr, yres=yr, spp=spp, maxdepth=-1 if name.startswith(("coverage", "imagemap")) else 5,
                           bands=bands, integrator="path")
         path = os.path.join(out, name + ".pack")
         s.save_pack(path)
