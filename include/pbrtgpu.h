@@ -133,7 +133,9 @@ typedef struct pbrtgpu_material {
     float f[8];
     int32_t tex[4];
     int32_t black_mask;
-    int32_t pad[3];
+    int32_t normal_tex;   /* "normalmap" spectrum texture (Material::NormalMap, material.cpp:82-126, used
+                           * where its value is not black), or -1 (the constant-0 default) */
+    int32_t pad[2];
 } pbrtgpu_material;
 
 enum { PBRTGPU_LIGHT_AREA = 0, PBRTGPU_LIGHT_POINT = 1, PBRTGPU_LIGHT_INFINITE = 2 };

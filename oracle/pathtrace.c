@@ -1402,7 +1402,44 @@ static void compute_differentials(const DG *dg, const RayDiff *rd, float out[4])
     if (!solve2x2(A, By, &out[2], &out[3])) out[2] = out[3] = 0.f;
 }
 
-/* Intersection::GetBSDF -> GetShadingGeometry -> Material::GetBSDF (with Bump) */
+/* Texture<Spectrum>::EvaluateMemory of a leaf (the fork's RGB before FromRGB): an image map's
+ * MIPMap lookup, RGB 0 for a constant (constant.h:45-47) */
+static void tex_memory_leaf(const Ctx *c, int id, const TexPt *q, float rgb[3]) {
+    const pbrtgpu_texture *tx = &c->s->textures[id];
+    if (tx->type == PBRTGPU_TEX_IMAGE) tex_image(c, tx, 3, q, rgb);
+    else rgb[0] = rgb[1] = rgb[2] = 0.f;
+}
+/* Material::NormalMap (material.cpp:82-126), taken by every material where the map's Evaluate is
+ * not black (e.g. matte.cpp:40-47); returns 0 when it is black (Bump then), else the rotated
+ * shading normal in *nOut (before the orientation flip and Faceforward) */
+static int normal_map(const Ctx *c, int id, const TexPt *q, V nn, V *nOut) {
+    float sp[MAXB];
+    tex_spec(c, id, q, sp);
+    if (spec_black(c, sp)) return 0;
+    const pbrtgpu_texture *tx = &c->s->textures[id];
+    float rgb[3];
+    if (tx->type == PBRTGPU_TEX_SCALE) {   /* ScaleTexture::EvaluateMemory: tex1 * tex2 (scale.h:47-49) */
+        float a[3], b[3];
+        tex_memory_leaf(c, tx->tex1, q, a);
+        tex_memory_leaf(c, tx->tex2, q, b);
+        for (int k = 0; k < 3; ++k) rgb[k] = a[k] * b[k];
+    } else tex_memory_leaf(c, id, q, rgb);
+    for (int k = 0; k < 3; ++k) rgb[k] = rgb[k] * 2 - 1;
+    V n = vnorm(v3(rgb[0], rgb[1], rgb[2]));
+    V axis = vcross(v3(0.f, 0.f, 1.f), n);
+    float angle = (180.f / (float)M_PI) * ACOSF(vdot(v3(0.f, 0.f, 1.f), n));   /* Degrees */
+    /* Rotate (transform.cpp:197-224), then Transform::operator()(Normal) with mInv = Transpose(m) */
+    V a = vnorm(axis);
+    float s = SINF(((float)M_PI / 180.f) * angle), co = COSF(((float)M_PI / 180.f) * angle);
+    float m[3][3] = {{a.x * a.x + (1.f - a.x * a.x) * co, a.x * a.y * (1.f - co) - a.z * s, a.x * a.z * (1.f - co) + a.y * s},
+                     {a.x * a.y * (1.f - co) + a.z * s, a.y * a.y + (1.f - a.y * a.y) * co, a.y * a.z * (1.f - co) - a.x * s},
+                     {a.x * a.z * (1.f - co) - a.y * s, a.y * a.z * (1.f - co) + a.x * s, a.z * a.z + (1.f - a.z * a.z) * co}};
+    *nOut = v3(m[0][0] * nn.x + m[0][1] * nn.y + m[0][2] * nn.z, m[1][0] * nn.x + m[1][1] * nn.y + m[1][2] * nn.z,
+               m[2][0] * nn.x + m[2][1] * nn.y + m[2][2] * nn.z);
+    return 1;
+}
+
+/* Intersection::GetBSDF -> GetShadingGeometry -> Material::GetBSDF (with Bump or NormalMap) */
 static void get_bsdf(const Ctx *c, const Isect *is, const float diff[4], BSDF *bs, DG *dgsOut) {
     const pbrtgpu_prim *pr = &c->s->prims[is->prim];
     const pbrtgpu_material *mt = &c->s->materials[pr->material];
@@ -1419,7 +1456,11 @@ static void get_bsdf(const Ctx *c, const Isect *is, const float diff[4], BSDF *b
     }
     const TexPt q = {dgs.u, dgs.v, diff[0], diff[1], diff[2], diff[3]};
     DG b = dgs;
-    if (mt->bump_tex < 0) {
+    V nmapN;
+    const int nmap = mt->normal_tex >= 0 && normal_map(c, mt->normal_tex, &q, dgs.nn, &nmapN);
+    if (nmap) {
+        /* dgBump = dgs with the rotated normal */
+    } else if (mt->bump_tex < 0) {
         /* Material::Bump with constant displacement d (material.cpp:39-81); du = dv = .01f
          * gives the identical result for any positive du because (d - d) == 0 */
         float d = mt->f[7];
@@ -1440,7 +1481,7 @@ static void get_bsdf(const Ctx *c, const Isect *is, const float diff[4], BSDF *b
         b.dpdu = vadd(vadd(dgs.dpdu, vmul(dgs.nn, (uDisplace - displace) / du)), vmul(dgs.dndu, displace));
         b.dpdv = vadd(vadd(dgs.dpdv, vmul(dgs.nn, (vDisplace - displace) / dv)), vmul(dgs.dndv, displace));
     }
-    b.nn = vnorm(vcross(b.dpdu, b.dpdv));
+    b.nn = nmap ? nmapN : vnorm(vcross(b.dpdu, b.dpdv));
     if (ro ^ swaps) b.nn = vmul(b.nn, -1.f);
     b.nn = faceforward(b.nn, is->dg.nn);
     /* BSDF ctor (reflection.cpp:593-601) */

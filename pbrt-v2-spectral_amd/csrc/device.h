@@ -1830,6 +1830,55 @@ PGD_INLINE float4 tex_spec4(const DevScene &S, const SpecTex &t, int q) {
     return t.constFirst ? make_float4(b.x * a.x, b.y * a.y, b.z * a.z, b.w * a.w)
                         : make_float4(a.x * b.x, a.y * b.y, a.z * b.z, a.w * b.w);
 }
+// Texture<Spectrum>::EvaluateMemory (the fork's RGB of a texture before FromRGB): an image map's
+// MIPMap lookup, RGB 0 for a constant (constant.h:45-47), the product for a scale (scale.h:47-49)
+PGD_INLINE void tex_memory_leaf(const DevScene &S, int id, const TexPt &q, float rgb[3]) {
+    const pbrtgpu_texture &tx = (*sa(S.tex, (uint32_t)(id)));
+    if (tx.type == PBRTGPU_TEX_IMAGE) tex_image<3>(S, tx, q, rgb);
+    else rgb[0] = rgb[1] = rgb[2] = 0.f;
+}
+// Material::NormalMap (material.cpp:82-126) where the map's spectrum (Evaluate, FromRGB of its
+// texel) is not black (the materials' `!normalSpectrum.IsBlack()`); *nOut = the rotated shading
+// normal before the orientation flip and Faceforward.  false: not black -> Bump instead
+PGD_HEAVY bool normal_map(const DevScene &S, int id, const TexPt &q, V nn, V *nOut) {
+    const pbrtgpu_texture &tx = (*sa(S.tex, (uint32_t)(id)));
+    bool black = true;
+    if (tx.type == PBRTGPU_TEX_CONST) {
+        for (int i = 0; i < S.nb; ++i) black = black && (*sa(S.spectra, (uint32_t)(tx.spec + i))) == 0.f;
+    } else {
+        const SpecTex st = tex_spec_prepare(S, id, q);
+        for (int qq = 0; qq < S.nbp / 4; ++qq) {
+            const float4 v = tex_spec4(S, st, qq);
+            black = black && v.x == 0.f && (4 * qq + 1 >= S.nb || v.y == 0.f) && (4 * qq + 2 >= S.nb || v.z == 0.f) &&
+                    (4 * qq + 3 >= S.nb || v.w == 0.f);
+        }
+    }
+    if (black) return false;
+    float c[3];
+    if (tx.type == PBRTGPU_TEX_SCALE) {
+        float a[3], b[3];
+        tex_memory_leaf(S, tx.tex1, q, a);
+        tex_memory_leaf(S, tx.tex2, q, b);
+        for (int k = 0; k < 3; ++k) c[k] = a[k] * b[k];
+    } else tex_memory_leaf(S, id, q, c);
+    for (int k = 0; k < 3; ++k) c[k] = c[k] * 2.f - 1.f;
+    const V n = vnorm(v3(c[0], c[1], c[2]));
+    const V axis = vcross(v3(0.f, 0.f, 1.f), n);
+    const float angle = (180.f / kPi) * ACOSF(vdot(v3(0.f, 0.f, 1.f), n));   // Degrees(acosf(Dot))
+    // Rotate(angle, axis) (transform.cpp:197-224) applied to the normal: m . nn
+    const V a = vnorm(axis);
+    const float2 sc = SINCOSF((kPi / 180.f) * angle);   // sinf / cosf (Radians)
+    const float s = sc.x, co = sc.y;
+    const float m00 = a.x * a.x + (1.f - a.x * a.x) * co, m01 = a.x * a.y * (1.f - co) - a.z * s,
+                m02 = a.x * a.z * (1.f - co) + a.y * s;
+    const float m10 = a.x * a.y * (1.f - co) + a.z * s, m11 = a.y * a.y + (1.f - a.y * a.y) * co,
+                m12 = a.y * a.z * (1.f - co) - a.x * s;
+    const float m20 = a.x * a.z * (1.f - co) - a.y * s, m21 = a.y * a.z * (1.f - co) + a.x * s,
+                m22 = a.z * a.z + (1.f - a.z * a.z) * co;
+    *nOut = v3(m00 * nn.x + m01 * nn.y + m02 * nn.z, m10 * nn.x + m11 * nn.y + m12 * nn.z,
+               m20 * nn.x + m21 * nn.y + m22 * nn.z);
+    return true;
+}
 // DifferentialGeometry::ComputeDifferentials (diffgeom.cpp:50-105) for the camera ray's
 // offset rays; out = dudx, dvdx, dudy, dvdy
 struct RayDiff { V rxo, rxd, ryo, ryd; };
@@ -1891,7 +1940,12 @@ PGD_HEAVY void get_bsdf(const DevScene &S, const Isect &is, const float diff[4],
     TexPt tq;
     tq.u = dgs.u; tq.v = dgs.v; tq.dudx = diff[0]; tq.dvdx = diff[1]; tq.dudy = diff[2]; tq.dvdy = diff[3];
     V bdpdu, bdpdv;
-    if (!(FEAT & FEAT_TEX) || mt.bump_tex < 0) {
+    V nmapN;
+    const bool nmap = (FEAT & FEAT_TEX) && mt.normal_tex >= 0 && normal_map(S, mt.normal_tex, tq, dgs.nn, &nmapN);
+    if (nmap) {   // dgBump = dgs with the rotated normal (material.cpp:113-114)
+        bdpdu = dgs.dpdu;
+        bdpdv = dgs.dpdv;
+    } else if (!(FEAT & FEAT_TEX) || mt.bump_tex < 0) {
         float d = mt.f[7];
         const float du = .01f, dv = .01f;   // (d - d) / du == +0 for every positive du
         bdpdu = vadd(vadd(dgs.dpdu, vmul(dgs.nn, (d - d) / du)), vmul(dgs.dndu, d));
@@ -1909,7 +1963,7 @@ PGD_HEAVY void get_bsdf(const DevScene &S, const Isect &is, const float diff[4],
         bdpdu = vadd(vadd(dgs.dpdu, vmul(dgs.nn, (uDisplace - displace) / du)), vmul(dgs.dndu, displace));
         bdpdv = vadd(vadd(dgs.dpdv, vmul(dgs.nn, (vDisplace - displace) / dv)), vmul(dgs.dndv, displace));
     }
-    V nn = vnorm(vcross(bdpdu, bdpdv));
+    V nn = nmap ? nmapN : vnorm(vcross(bdpdu, bdpdv));
     if (ro ^ swaps) nn = vmul(nn, -1.f);
     nn = faceforward(nn, is.dg.nn);
     bs.ng = is.dg.nn;

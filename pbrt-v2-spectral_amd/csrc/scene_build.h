@@ -307,6 +307,7 @@ static inline int scene_check(const pbrtgpu_flat_scene *s, std::string *err) {
             }
         if (nt > 1) SB_FAIL(PBRTGPU_E_UNSUPPORTED, "more than one textured spectrum per material");
         if (m.bump_tex >= 0 && !texOk(m.bump_tex, 0, false)) SB_FAIL(PBRTGPU_E_INVALID, "bump texture");
+        if (m.normal_tex >= 0 && (!texOk(m.normal_tex, 1, false) || s->n_bands == 3)) SB_FAIL(PBRTGPU_E_INVALID, "normal map texture");
         if (m.type == PBRTGPU_MAT_MEASURED_HALFANGLE && m.aux >= 0 &&
             (!s->merl || s->n_merl_floats < 0 || (int64_t)m.aux * 3 + 3 * 90 * 90 * 180 > (int64_t)s->n_merl_floats))
             SB_FAIL(PBRTGPU_E_INVALID, "RegularHalfangle table out of range");
@@ -558,7 +559,8 @@ static int scene_build(const pbrtgpu_flat_scene *s, int topNodes, DevScene &S, i
     for (int i = 0; i < s->n_materials; ++i) {
         const pbrtgpu_material &m = s->materials[i];
         if (m.type == PBRTGPU_MAT_MEASURED || m.type == PBRTGPU_MAT_MEASURED_HALFANGLE) *feat |= FEAT_MEAS;
-        if (m.bump_tex >= 0 || m.tex[0] >= 0 || m.tex[1] >= 0 || m.tex[2] >= 0 || m.tex[3] >= 0) *feat |= FEAT_TEX;
+        if (m.bump_tex >= 0 || m.normal_tex >= 0 || m.tex[0] >= 0 || m.tex[1] >= 0 || m.tex[2] >= 0 || m.tex[3] >= 0)
+            *feat |= FEAT_TEX;
     }
     return 0;
 }

@@ -958,7 +958,7 @@ PGD_INLINE Pushes shade_vertex(const DevScene &S, const PathSoA &P, int slot, in
     float diff[4] = {0.f, 0.f, 0.f, 0.f};
     if ((FEAT & FEAT_TEX) && vb == 0) {
         const pbrtgpu_material &mt = (*sa(S.mats, (uint32_t)((*sa(S.prims, (uint32_t)(is.prim))).material)));
-        if (mt.bump_tex >= 0 || mt.tex[0] >= 0 || mt.tex[1] >= 0 || mt.tex[2] >= 0 || mt.tex[3] >= 0) {
+        if (mt.bump_tex >= 0 || mt.normal_tex >= 0 || mt.tex[0] >= 0 || mt.tex[1] >= 0 || mt.tex[2] >= 0 || mt.tex[3] >= 0) {
             const uint32_t pxy = P.pix[slot];
             float u[2], lens[2];
             s2d(hp, 0, s, spp, u);

@@ -1220,9 +1220,18 @@ private:
         pbrtgpu_material &mt = mo->m;
         for (int k = 0; k < 4; ++k) mt.tex[k] = -1;
         mt.bump_tex = -1;
-        // every material: normalmap (constant 0 -> black, skipped) and bumpmap (float texture)
-        Spec nmap = ConstSpecTex(g, m, "normalmap", spec.Const(0.f));
-        if (!SpecIsBlack(nmap)) throw std::runtime_error("normal maps are not supported yet");
+        mt.normal_tex = -1;
+        // every material: normalmap (Material::NormalMap where its value is not black; the default
+        // constant 0 never is) and bumpmap (float texture)
+        SpecTex nmap = GetSpecTex(g, m, "normalmap", spec.Const(0.f));
+        if (nmap.constant) {
+            if (!SpecIsBlack(nmap.value)) {   // EvaluateMemory of a constant is RGB 0 (constant.h:45-47)
+                if (spec.rgb()) throw std::runtime_error("normal maps are not supported in the RGB build");
+                pbrtgpu_texture c = TexNode(PBRTGPU_TEX_CONST, true);
+                c.spec = EmitSpectrum(nmap.value);
+                mt.normal_tex = AddTexture(c);
+            }
+        } else mt.normal_tex = nmap.tex;
         FloatTex bump = GetFloatTex(g, m, "bumpmap", 0.f);
         if (bump.constant) mt.f[7] = bump.value;
         else mt.bump_tex = bump.tex;

@@ -11,9 +11,10 @@
 namespace pbrtamd {
 
 static const char kMagic[8] = {'P', 'B', 'R', 'T', 'P', 'A', 'C', 'K'};
-static const uint32_t kVersion = 11;   // 6: + merl tables; 7: + metadata ids; 8: + Renderer; 9: + lens diffraction;
+static const uint32_t kVersion = 12;   // 6: + merl tables; 7: + metadata ids; 8: + Renderer; 9: + lens diffraction;
                                        // 10: + pinhole array / microlens / eye IOR; 11: image maps as MIPMap
-                                       // pyramids (texture records + texel pool; 5-10 still load)
+                                       // pyramids (texture records + texel pool); 12: material normal maps
+                                       // (normal_tex, a former pad word: -1 for older packs); 5-11 still load
 
 // the texture record of packs before v11: one MIPMap texel inline (the one-texel maps they held)
 struct TexV10 {
@@ -178,6 +179,8 @@ bool LoadPack(const std::string &path, HostScene *s, std::string *err) {
     s->eyeIor.clear();
     if (ok && ver >= 10) ok = RArr(f, s->eyeIor);
     if (ok && ver >= 11) ok = RArr(f, s->texels);
+    if (ok && ver < 12)
+        for (auto &m : s->materials) m.normal_tex = -1;
     gzclose(f);
     if (!ok && err) *err = "bad or truncated scene pack " + path;
     return ok;

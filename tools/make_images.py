@@ -50,6 +50,13 @@ def main():
     pfm(os.path.join(out, "rgb5x3.pfm"), prgb, -1.0)                   # PF, little-endian
     y, x = np.mgrid[0:2, 0:8]
     pfm(os.path.join(out, "grey8x2.pfm"), (0.05 * x + 0.3 * y)[..., None].astype(np.float32), 2.0)   # Pf, big-endian, x2
+    # a tangent-space normal map (RGB = (n + 1) / 2): a bumpy grid of tilted normals, one texel (1/2, 1/2, 1)
+    y, x = np.mgrid[0:8, 0:8]
+    nx, ny = 0.45 * np.sin(x * 1.3 + y * 0.4), 0.45 * np.cos(y * 1.1 - x * 0.7)
+    nx[3, 5], ny[3, 5] = 0.0, 0.0
+    nz = np.sqrt(np.maximum(0.0, 1.0 - nx * nx - ny * ny))
+    nrm = np.stack([(nx + 1) * 127.5, (ny + 1) * 127.5, (nz + 1) * 127.5], -1).round().clip(0, 255)
+    tga(os.path.join(out, "normal8x8.tga"), nrm)
 
 
 if __name__ == "__main__":
