@@ -290,6 +290,9 @@ typedef struct pbrtgpu_flat_scene {
     pbrtgpu_lens lens;
     int32_t n_texel_floats;       /* the MIPMap pyramids of the IMAGE textures (pbrtgpu_texture) */
     const float *texels;
+    const pbrtgpu_instance *camera_motion;   /* an animated perspective camera's CameraToWorld
+                                   * (AnimatedTransform, camera.cpp:84-103; start_m / end_m camera->world,
+                                   * T / R / S their Decompose), or NULL: camera.cam2world_m */
 } pbrtgpu_flat_scene;
 
 /* SurfaceIntegrator of a flattened scene: "path" (integrators/path.cpp:44-115),

@@ -2106,8 +2106,17 @@ static Ray camera_ray(const Ctx *c, float imageX, float imageY, float lensU, flo
         r.o = v3(lu, lv, 0.f);
         r.d = vnorm(vsub(Pfocus, r.o));
     }
-    r.time = lerpf(timeU, cam->shutter_open, cam->shutter_close);
+    /* Sample::time = Lerp(u, open, close) (LDPixelSample, montecarlo.cpp:229), lerped again by the camera
+     * (perspective.cpp:67, 102; realisticDiffraction.cpp:1157) */
+    r.time = lerpf(lerpf(timeU, cam->shutter_open, cam->shutter_close), cam->shutter_open, cam->shutter_close);
+    /* CameraToWorld at the ray's time: AnimatedTransform's start / end transform or
+     * Interpolate (transform.cpp:356-381, 427-455) for an animated camera */
+    float cwb[16];
     const float *cw = cam->cam2world_m;
+    if (c->s->camera_motion) {
+        inst_interp(c->s->camera_motion, r.time, cwb, NULL);
+        cw = cwb;
+    }
     Ray o = r;
     {
         V p = r.o;
@@ -2395,7 +2404,9 @@ static float lens_ray(const Ctx *c, float imageX, float imageY, float lensU, flo
         }
     }
     r.o = sp;
-    r.time = lerpf(timeU, cam->shutter_open, cam->shutter_close);
+    /* Sample::time = Lerp(u, open, close) (LDPixelSample, montecarlo.cpp:229), lerped again by the camera
+     * (perspective.cpp:67, 102; realisticDiffraction.cpp:1157) */
+    r.time = lerpf(lerpf(timeU, cam->shutter_open, cam->shutter_close), cam->shutter_open, cam->shutter_close);
     out->o = xpoint(cam->cam2world_m, r.o);
     out->d = vnorm(xvec(cam->cam2world_m, r.d));
     out->mint = r.mint; out->maxt = r.maxt; out->time = r.time;

@@ -334,6 +334,7 @@ struct DevScene {
     const pbrtgpu_texture *tex;       // texture nodes (image maps, scale, constants)
     const float *ewa;                 // [128] MIPMap::weightLut
     const float *texels;              // the image maps' MIPMap pyramids (pbrtgpu_texture::texel_off)
+    const pbrtgpu_instance *camMotion;   // an animated camera's CameraToWorld, or null (cam.cam2world_m)
     const float *basis;               // [14][nbp] FromRGB basis spectra, band-quad padded
     int nbp;                          // padded band count (multiple of 4)
     int nInf;                         // infinite lights among lights[]
@@ -2281,7 +2282,10 @@ PGD_INLINE Ray camera_local(const pbrtgpu_camera &cam, float imageX, float image
         r.o = v3(lu, lv, 0.f);
         r.d = vnorm(vsub(Pfocus, r.o));
     }
-    r.time = lerpf(timeU, cam.shutter_open, cam.shutter_close);
+    // the sampler's Sample::time is already Lerp(u, shutterOpen, shutterClose) (LDPixelSample,
+    // montecarlo.cpp:229) and the camera lerps it again (perspective.cpp:67, 102;
+    // realisticDiffraction.cpp:1157): the identity only for the default shutter [0, 1]
+    r.time = lerpf(lerpf(timeU, cam.shutter_open, cam.shutter_close), cam.shutter_open, cam.shutter_close);
     *PcOut = Pc;
     return r;
 }
@@ -2296,11 +2300,19 @@ PGD_INLINE V cam_point(const float *cw, V p) {   // Transform::operator()(Point)
 }
 // the camera ray's offset rays (perspective.cpp:98-104) in world space, after
 // RayDifferential::ScaleDifferentials(1 / sqrtf(spp)) (samplerrenderer.cpp:91)
+// CameraToWorld at the ray's time: the static matrix, or AnimatedTransform's start / end
+// transform or Interpolate(time) (transform.cpp:356-381, 427-455) of an animated camera
+PGD_INLINE const float *cam_xform(const pbrtgpu_camera &cam, const pbrtgpu_instance *cm, float time, float *buf) {
+    if (!cm) return cam.cam2world_m;
+    inst_interp(*cm, time, buf, nullptr);
+    return buf;
+}
 PGD_INLINE RayDiff camera_diff(const pbrtgpu_camera &cam, int spp, float imageX, float imageY, float lensU, float lensV,
-                               float timeU) {
+                               float timeU, const pbrtgpu_instance *cm = nullptr) {
     V Pc;
     Ray r = camera_local(cam, imageX, imageY, lensU, lensV, timeU, &Pc);
-    const float *cw = cam.cam2world_m;
+    float cwb[16];
+    const float *cw = cam_xform(cam, cm, r.time, cwb);
     V o = cam_point(cw, r.o), d = xvec(cw, r.d);
     V rxd = xvec(cw, vnorm(vadd(Pc, v3(cam.dx_camera[0], cam.dx_camera[1], cam.dx_camera[2]))));
     V ryd = xvec(cw, vnorm(vadd(Pc, v3(cam.dy_camera[0], cam.dy_camera[1], cam.dy_camera[2]))));
@@ -2313,10 +2325,12 @@ PGD_INLINE RayDiff camera_diff(const pbrtgpu_camera &cam, int spp, float imageX,
     return rd;
 }
 // camera sample -> world ray (perspective.cpp:73-106)
-PGD_INLINE Ray camera_ray(const pbrtgpu_camera &cam, float imageX, float imageY, float lensU, float lensV, float timeU) {
+PGD_INLINE Ray camera_ray(const pbrtgpu_camera &cam, float imageX, float imageY, float lensU, float lensV, float timeU,
+                          const pbrtgpu_instance *cm = nullptr) {
     V Pc;
     Ray r = camera_local(cam, imageX, imageY, lensU, lensV, timeU, &Pc);
-    const float *cw = cam.cam2world_m;
+    float cwb[16];
+    const float *cw = cam_xform(cam, cm, r.time, cwb);
     Ray o = r;
     o.o = cam_point(cw, r.o);
     o.d = xvec(cw, r.d);
@@ -2616,7 +2630,10 @@ PGD_INLINE float lens_ray(const DevScene &S, float imageX, float imageY, float l
         if (S.lensDiffraction && !lens_diffract(st, ip, cx, cy, ap, wl, &r.d, !micro)) return 0.f;
     }
     r.o = sp;
-    r.time = lerpf(timeU, cam.shutter_open, cam.shutter_close);
+    // the sampler's Sample::time is already Lerp(u, shutterOpen, shutterClose) (LDPixelSample,
+    // montecarlo.cpp:229) and the camera lerps it again (perspective.cpp:67, 102;
+    // realisticDiffraction.cpp:1157): the identity only for the default shutter [0, 1]
+    r.time = lerpf(lerpf(timeU, cam.shutter_open, cam.shutter_close), cam.shutter_open, cam.shutter_close);
     const float *cw = cam.cam2world_m;
     out->o = cam_point(cw, r.o);
     out->d = vnorm(xvec(cw, r.d));
@@ -2670,7 +2687,7 @@ PGD_INLINE RayDiff path_camera_diff(const DevScene &S, int item, uint32_t hp, ui
                             diff_key(hp, path_rng_index(S, (uint32_t)item, smp)), &r, &rd);
         return rd;
     }
-    return camera_diff(S.cam, S.spp, imageX, imageY, lensU, lensV, timeU);
+    return camera_diff(S.cam, S.spp, imageX, imageY, lensU, lensV, timeU, S.camMotion);
 }
 
 }  // namespace pgd

@@ -495,6 +495,11 @@ static int scene_build(const pbrtgpu_flat_scene *s, int topNodes, DevScene &S, i
     SB_PUT(s->ewa_lut, (size_t)128, &S.ewa);
     S.texels = nullptr;
     if (s->n_texel_floats > 0) SB_PUT(s->texels, (size_t)s->n_texel_floats, &S.texels);
+    S.camMotion = nullptr;
+    if (s->camera_motion) {
+        if (s->camera_type != PBRTGPU_CAMERA_PERSPECTIVE) SB_FAIL(PBRTGPU_E_UNSUPPORTED, "animated lens camera");
+        SB_PUT(s->camera_motion, (size_t)1, &S.camMotion);
+    }
     SB_PUT(pt.data(), pt.size(), &S.primTri);
     SB_PUT(s->tris, (size_t)s->n_tris, &S.tris);
     SB_PUT(s->meshes, (size_t)s->n_meshes, &S.meshes);

@@ -646,7 +646,7 @@ PGD_INLINE void path_start(const DevScene &S, const PathSoA &P, const ItemSrc &s
             r.maxt = 0.f;
         }
     }
-    else r = camera_ray(S.cam, imageX, imageY, lens[0], lens[1], timeU);
+    else r = camera_ray(S.cam, imageX, imageY, lens[0], lens[1], timeU, S.camMotion);
     ray_store(P, RAY_C, slot, r);
     // AnimatedTransform::Interpolate (transform.cpp:356-381) of every instance at the path's
     // time, once per path: all of the path's rays carry this time

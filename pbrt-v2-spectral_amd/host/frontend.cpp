@@ -1926,7 +1926,26 @@ private:
             throw std::runtime_error("camera '" + cameraName + "' is not supported by this build");
         Xform c2w[2];
         for (int i = 0; i < 2; ++i) LookupCache(cameraToWorld.t[i], &c2w[i], nullptr);
-        if (c2w[0] != c2w[1]) throw std::runtime_error("animated cameras are not supported yet");
+        // an animated CameraToWorld (AnimatedTransform(cam2world[0], transformStartTime,
+        // cam2world[1], transformEndTime), api.cpp MakeCamera): its start / end matrices and
+        // Decompose for the per-ray Interpolate (camera.cpp:84-103)
+        out->cameraMotion.clear();
+        if (c2w[0] != c2w[1]) {
+            if (cameraName != "perspective") throw std::runtime_error("animated lens cameras are not supported yet");
+            const AnimXform A(c2w[0], tStart, c2w[1], tEnd);
+            pbrtgpu_instance cm{};
+            cm.root = -1; cm.single_prim = -1;
+            cm.animated = A.animated ? 1 : 0;
+            cm.start_time = A.startTime; cm.end_time = A.endTime;
+            memcpy(cm.start_m, A.start.m.m, 64); memcpy(cm.start_minv, A.start.mInv.m, 64);
+            memcpy(cm.end_m, A.end.m.m, 64); memcpy(cm.end_minv, A.end.mInv.m, 64);
+            for (int k = 0; k < 2; ++k) {
+                cm.T[k][0] = A.T[k].x; cm.T[k][1] = A.T[k].y; cm.T[k][2] = A.T[k].z; cm.T[k][3] = 0.f;
+                cm.R[k][0] = A.R[k].v.x; cm.R[k][1] = A.R[k].v.y; cm.R[k][2] = A.R[k].v.z; cm.R[k][3] = A.R[k].w;
+                memcpy(cm.S[k], A.S[k].m, 64);
+            }
+            out->cameraMotion.push_back(cm);
+        }
         CameraParams &cp = out->camParams;
         cp.shutterOpen = cameraParams.FindOneFloat("shutteropen", 0.f);
         cp.shutterClose = cameraParams.FindOneFloat("shutterclose", 1.f);
@@ -2207,6 +2226,7 @@ void HostScene::Flat(pbrtgpu_flat_scene *f) const {
     f->lens = lens;
     f->n_texel_floats = (int32_t)texels.size();
     f->texels = texels.empty() ? nullptr : texels.data();
+    f->camera_motion = cameraMotion.empty() ? nullptr : cameraMotion.data();
     f->lens.n_elements = (int)lensEl.size() / 4;
     f->lens.elements = lensEl.empty() ? nullptr : lensEl.data();
     f->lens.eye_ior = lens.ior_eye && (int)eyeIor.size() == 4 * nBands ? eyeIor.data() : nullptr;

@@ -11,10 +11,11 @@
 namespace pbrtamd {
 
 static const char kMagic[8] = {'P', 'B', 'R', 'T', 'P', 'A', 'C', 'K'};
-static const uint32_t kVersion = 12;   // 6: + merl tables; 7: + metadata ids; 8: + Renderer; 9: + lens diffraction;
+static const uint32_t kVersion = 13;   // 6: + merl tables; 7: + metadata ids; 8: + Renderer; 9: + lens diffraction;
                                        // 10: + pinhole array / microlens / eye IOR; 11: image maps as MIPMap
                                        // pyramids (texture records + texel pool); 12: material normal maps
-                                       // (normal_tex, a former pad word: -1 for older packs); 5-11 still load
+                                       // (normal_tex, a former pad word: -1 for older packs); 13: an animated
+                                       // camera's CameraToWorld; 5-12 still load
 
 // the texture record of packs before v11: one MIPMap texel inline (the one-texel maps they held)
 struct TexV10 {
@@ -98,6 +99,8 @@ bool SavePack(const HostScene &s, const std::string &path, std::string *err) {
     ok = ok && WArr(f, s.eyeIor);
     // v11: the texel pool of the MIPMap pyramids
     ok = ok && WArr(f, s.texels);
+    // v13: the animated camera
+    ok = ok && WArr(f, s.cameraMotion);
     ok = (gzclose(f) == Z_OK) && ok;
     if (!ok && err) *err = "write error on " + path;
     return ok;
@@ -181,6 +184,8 @@ bool LoadPack(const std::string &path, HostScene *s, std::string *err) {
     if (ok && ver >= 11) ok = RArr(f, s->texels);
     if (ok && ver < 12)
         for (auto &m : s->materials) m.normal_tex = -1;
+    s->cameraMotion.clear();
+    if (ok && ver >= 13) ok = RArr(f, s->cameraMotion) && s->cameraMotion.size() <= 1;
     gzclose(f);
     if (!ok && err) *err = "bad or truncated scene pack " + path;
     return ok;

@@ -62,6 +62,7 @@ struct HostScene {
     std::vector<pbrtgpu_kdnode> kdnodes;      // measured BRDF kd-trees
     std::vector<pbrtgpu_texture> textures;
     std::vector<float> texels;                // MIPMap pyramids of the IMAGE textures (pbrtgpu_texture)
+    std::vector<pbrtgpu_instance> cameraMotion;   // 0 or 1: an animated camera's CameraToWorld
     std::vector<float> ewaLut;                // [128] MIPMap::weightLut
     std::vector<float> rgbBasis;              // [14][nBands] FromRGB basis spectra
     std::vector<float> merl;                  // RegularHalfangleBRDF RGB tables (pbrtgpu_flat_scene::merl)

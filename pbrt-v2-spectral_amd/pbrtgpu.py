@@ -72,7 +72,7 @@ class FlatScene(ctypes.Structure):
                 ("n_merl_floats", I32), ("merl", P), ("integrator", I32), ("dl_strategy", I32),
                 ("meta_strategy", I32), ("prim_meta", P), ("renderer", I32), ("wave_bands", I32),
                 ("spectral_sampling", I32), ("camera_type", I32), ("lens", Lens),
-                ("n_texel_floats", I32), ("texels", P)]
+                ("n_texel_floats", I32), ("texels", P), ("camera_motion", P)]
 
 
 PBRTHOST_ABI_VERSION = 2   # include/pbrthost.h

@@ -103,7 +103,8 @@ def _golden_scene(pg, cfg, name="killeroo"):
     from conftest import PACKS
     w, h, spp, seed, md = [int(v) for v in cfg]
     pack = {"anim": "anim-killeroos-moving.pack", "bunny": "bunny.pack", "metal": "metal.pack",
-            "coverage": "coverage.pack", "imagemap": "imagemap.pack"}.get(name.split("_")[0],
+            "coverage": "coverage.pack", "imagemap": "imagemap.pack",
+            "animcam": "animcam.pack"}.get(name.split("_")[0],
                                                                                               "killeroo-simple.pack")
     if "_b30_" in name:
         pack = pack.replace(".pack", "-b30.pack")
@@ -116,7 +117,7 @@ def _golden_scene(pg, cfg, name="killeroo"):
                                   "bunny_keys_c3_1920x1080s1024", "metal_keys_c4_400x400s4096",
                                   "anim_keys_c5_600x600s512", "killeroo_b30_paths_48x40s4",
                                   "coverage_b30_paths_48x36s4", "imagemap_paths_64x48s4",
-                                  "imagemap_paths_96x72s2_seed5"])
+                                  "imagemap_paths_96x72s2_seed5", "animcam_paths_64x48s4"])
 def test_paths_vs_reference_golden(pg, name):
     """GPU against the reference harness's own per-path radiance (fixed seeds); the *_keys_*
     fixtures are the configs at their real resolution and sample count."""
@@ -138,7 +139,8 @@ def test_paths_vs_reference_golden(pg, name):
 
 @pytest.mark.parametrize("name", ["killeroo_film_96x72s16", "anim_film_40x40s8", "bunny_film_48x27s8",
                                   "metal_film_40x40s8", "coverage_film_64x48s8", "killeroo_b30_film_40x32s8",
-                                  "coverage_b30_film_40x30s4", "imagemap_film_64x48s8"])
+                                  "coverage_b30_film_40x30s4", "imagemap_film_64x48s8",
+                                  "animcam_film_64x48s4"])
 def test_film_vs_reference_golden(pg, name):
     """Whole-film render against the reference's film (raw sums, incl. neighbour-pixel
     samples): image L-inf relative error < 1e-4 (BASELINE.json north star)."""

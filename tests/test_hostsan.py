@@ -78,6 +78,7 @@ CASES = [
     (LENS_D, dict(xres=32, yres=24, spp=2, maxdepth=5, integrator="directlighting", strategy="all")),
     ("imagemap.pack", dict(xres=48, yres=36, spp=4, maxdepth=3)),
     ("imagemap.pack", dict(xres=40, yres=30, spp=2, maxdepth=3, integrator="directlighting", strategy="all")),
+    ("animcam.pack", dict(xres=40, yres=30, spp=4, maxdepth=6)),
 ]
 
 
@@ -85,7 +86,7 @@ CASES = [
                                                "path_bunny", "path_metal60", "metadata", "path_coverage_b30",
                                                "lens_diffraction", "lens_diffraction_spectral", "lens_pinholes",
                                                "lens_microlens_spectral", "eye", "eye_spectral", "lens_diffraction_dl",
-                                               "imagemap", "imagemap_dl"])
+                                               "imagemap", "imagemap_dl", "animcam"])
 def test_replay_matches_oracle(pg, tmp_path, pack, a):
     exe = _build("shade_host")
     scene = pg.Scene.load(os.path.join(PACKS, pack), **a)

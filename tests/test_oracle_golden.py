@@ -18,7 +18,8 @@ from conftest import GOLDEN, PACKS
 def _scene(pg, cfg, name="killeroo"):
     w, h, spp, seed, md = [int(v) for v in cfg]
     pack = {"anim": "anim-killeroos-moving.pack", "bunny": "bunny.pack", "metal": "metal.pack",
-            "coverage": "coverage.pack", "imagemap": "imagemap.pack"}.get(name.split("_")[0],
+            "coverage": "coverage.pack", "imagemap": "imagemap.pack",
+            "animcam": "animcam.pack"}.get(name.split("_")[0],
                                                                                               "killeroo-simple.pack")
     # *_b30_*: the upstream 30-band, 400-700 nm build (b30 harness, spectrum.h.original:36-38)
     if "_b30_" in name:
@@ -34,7 +35,7 @@ def exact_rate(name):
 
 PATHS = ["killeroo_paths_64x64s4", "killeroo_paths_48x48s8_seed7_md7", "anim_paths_48x48s4", "bunny_paths_64x36s4",
          "metal_paths_48x48s4", "coverage_paths_64x48s8", "killeroo_b30_paths_48x40s4", "coverage_b30_paths_48x36s4",
-         "imagemap_paths_64x48s4", "imagemap_paths_96x72s2_seed5"]
+         "imagemap_paths_64x48s4", "imagemap_paths_96x72s2_seed5", "animcam_paths_64x48s4"]
 # the configs at their real size and sample count (BASELINE.json configs 2-5; harness --keys):
 # every sample of a few pixels plus random keys of the whole sample extent
 KEYS = ["killeroo_keys_c2_700x700s256", "bunny_keys_c3_1920x1080s1024", "metal_keys_c4_400x400s4096",
@@ -69,7 +70,8 @@ def test_paths_restated_libm_bit_exact_vs_reference(pg, name):
 
 @pytest.mark.parametrize("name", ["killeroo_film_96x72s16", "anim_film_40x40s8", "bunny_film_48x27s8",
                                   "metal_film_40x40s8", "coverage_film_64x48s8", "killeroo_b30_film_40x32s8",
-                                  "coverage_b30_film_40x30s4", "imagemap_film_64x48s8"])
+                                  "coverage_b30_film_40x30s4", "imagemap_film_64x48s8",
+                                  "animcam_film_64x48s4"])
 def test_film_bit_exact_vs_reference(pg, ora_libm, name):
     g = np.load(os.path.join(GOLDEN, name + ".npz"))
     scene = _scene(pg, g["config"], name)

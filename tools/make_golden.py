@@ -49,13 +49,16 @@ Fixtures (numpy .npz, inputs + expected outputs only):
   *_b30_*, fromrgb_30.npz         the upstream 30-band build (b30 harness, 400-700 nm)
   imagemap_*                      tests/scenes/imagemap.pbrt: TGA / PFM image maps decoded by the
                                   reference's imageio.cpp into MIPMap pyramids (mipmap.h): EWA
-                                  over several levels, trilinear, noFiltering, repeat / clamp / black
+                                  over several levels, trilinear, noFiltering, repeat / clamp / black,
+                                  normal maps (image, scaled, constant)
+  animcam_*                       tests/scenes/animcam.pbrt: an animated camera (AnimatedTransform
+                                  CameraToWorld interpolated per ray, camera.cpp:84-103)
   <scene>_window_<cfg>_*.npz      film crops at the configs' REAL size and sample count: every
                                   sample of a one-pixel-larger window (--window), so each cropped
                                   pixel holds all of its contributions (incl. exact-boundary samples
                                   of its neighbours, spectralImage.cpp:77-152); C2 at the sphere
                                   light's edge and at a killeroo silhouette, C3-C5 at an edge each
-Usage: python tools/make_golden.py [--only keys|dat|merl|dl|meta|spec|rgb|b30|window|imagemap]
+Usage: python tools/make_golden.py [--only keys|dat|merl|dl|meta|spec|rgb|b30|window|imagemap|animcam]
        (after `make -C oracle ref`, `ref60`, `ref30` and `refrgb`)
 """
 import os
@@ -300,6 +303,13 @@ def imagemap_fixtures(tmp):
     paths_fixture("imagemap_paths_96x72s2_seed5", (96, 72), 2, 5, 3, 2, tmp, scene=sc)
 
 
+def animcam_fixtures(tmp):
+    """tests/scenes/animcam.pbrt: an animated CameraToWorld (coverage.pbrt's world)"""
+    sc = os.path.join(ROOT, "tests", "scenes", "animcam.pbrt")
+    paths_fixture("animcam_paths_64x48s4", (64, 48), 4, 0, 6, 2, tmp, scene=sc)
+    film_fixture("animcam_film_64x48s4", (64, 48), 4, 0, 6, tmp, scene=sc)
+
+
 def main():
     if not os.path.exists(HARNESS):
         sys.exit("build the reference harness first: make -C oracle ref")
@@ -328,6 +338,8 @@ def main():
                 b30_fixtures(tmp)
             elif only == "imagemap":
                 imagemap_fixtures(tmp)
+            elif only == "animcam":
+                animcam_fixtures(tmp)
             elif only == "window":
                 sel = sys.argv[3:]
                 for cfg in WINDOW_CONFIGS:
@@ -364,6 +376,7 @@ def main():
                 window_fixture(*cfg, tmp)
         merl_fixtures(tmp)
         imagemap_fixtures(tmp)
+        animcam_fixtures(tmp)
         dl_fixtures(tmp)
         meta_fixtures(tmp)
         spec_fixtures(tmp)

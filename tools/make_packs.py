@@ -27,6 +27,8 @@ PACKS = [
     ("coverage-b30", os.path.join(ROOT, "tests", "scenes", "coverage.pbrt"), 30, 64, 48, 8),
     # decoded TGA / PFM image maps in MIPMap pyramids (tests/scenes/textures, tools/make_images.py)
     ("imagemap", os.path.join(ROOT, "tests", "scenes", "imagemap.pbrt"), 32, 64, 48, 4),
+    # an animated camera (coverage.pbrt's world)
+    ("animcam", os.path.join(ROOT, "tests", "scenes", "animcam.pbrt"), 32, 64, 48, 4),
 ]
 
 
@@ -39,7 +41,7 @@ def main():
             continue
         # the configs render with "path" (SURVEY App. B); load a pack with integrator="directlighting"
         # to render it with the DirectLightingIntegrator the scene files name
-        s = pg.Scene.load(os.path.join(REF, fn), xres=xr, yres=yr, spp=spp, maxdepth=-1 if name.startswith(("coverage", "imagemap")) else 5,
+        s = pg.Scene.load(os.path.join(REF, fn), xres=xr, yres=yr, spp=spp, maxdepth=-1 if name.startswith(("coverage", "imagemap", "animcam")) else 5,
                           bands=bands, integrator="path")
         path = os.path.join(out, name + ".pack")
         s.save_pack(path)

@@ -1,7 +1,7 @@
 #!/bin/bash
-# r04i: material normal maps (pack v12) -- GPU suite incl.
+# r04j: normal maps, animated camera (pack v13) -- GPU suite incl.
 # the imagemap goldens, then the C2 / C4 bench lines
-OUT=$PWD/gpurun_out/r04i
+OUT=$PWD/gpurun_out/r04j
 mkdir -p $OUT
 timeout -k 10 700 python3 -u -m pytest tests -m gpu -q --timeout 150 --timeout-method thread -rf > $OUT/pytest_gpu.log 2>&1
 rc=$?
