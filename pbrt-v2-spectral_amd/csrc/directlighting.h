@@ -78,7 +78,8 @@ PGD_INLINE int dl_sample(const DevScene &S, uint32_t hp, uint32_t s, int k, floa
     return i;
 }
 
-// the top vertex rebuilt from its frame: intersection, differentials, BSDF
+// the top vertex rebuilt from its frame: intersection, differentials, BSDF (col: the column of
+// the textured-spectrum scratch PathSoA::K it uses -- the slot, or k_dl_nee's list row)
 struct DLVertex {
     Ray ray;
     RayDiff rd;
@@ -88,7 +89,7 @@ struct DLVertex {
     float diff[4];
 };
 template <int NB, int FEAT>
-PGD_INLINE void dl_vertex(const DevScene &S, const PathSoA &P, int slot, int d, DLVertex &v) {
+PGD_INLINE void dl_vertex(const DevScene &S, const PathSoA &P, int slot, int d, DLVertex &v, int col) {
     const size_t c = P.cap;
     const float *fr = P.fRay + (size_t)d * 9 * c + slot;
     v.ray.o = dl_vec_load(fr, c);
@@ -115,7 +116,7 @@ PGD_INLINE void dl_vertex(const DevScene &S, const PathSoA &P, int slot, int d, 
         v.rd.ryd = dl_vec_load(fd + 9 * c, c);
     }
     compute_differentials(v.is.dg, v.rd, v.diff, &v.dpdx, &v.dpdy);
-    get_bsdf<FEAT>(S, v.is, v.diff, P.K + slot, c, v.bs, &v.p, &v.n, v.dn);
+    get_bsdf<FEAT>(S, v.is, v.diff, P.K + col, c, v.bs, &v.p, &v.n, v.dn);
     v.wo = vneg(v.ray.d);
 }
 
@@ -176,8 +177,10 @@ enum {
 // the light-sample batches of a slot marked PF_DLNEE, run by k_dl_nee right after k_shade in
 // the same pass: the vertex, then batches [k, kEnd) until one queues a ray (PF_PEND: the next
 // k_shade adds it) or the last one is added (PF_DLSPEC: k_dl_spec takes the slot next).
+// row: the slot's entry in the light-sample list (PathSoA::dlList): the batch's A / B column,
+// the K / M scratch column and (without instances) the ray slots row + j * cap
 template <int NB, int FEAT>
-PGD_INLINE void dl_light_batches(const DevScene &S, const PathSoA &P, int slot, Pushes &out) {
+PGD_INLINE void dl_light_batches(const DevScene &S, const PathSoA &P, int slot, int row, Pushes &out) {
     constexpr int NQ = Bands<NB>::NQ;
     const size_t c = P.cap;
     uint32_t fl = P.flags[slot] & ~PF_DLNEE;
@@ -186,13 +189,14 @@ PGD_INLINE void dl_light_batches(const DevScene &S, const PathSoA &P, int slot, 
     const int K = all ? S.dlK : 1;
     const uint32_t hp = P.hp[slot], s = P.smp[slot];
     int k = (int)P.dlk[slot];
+    const int rb = P.nInst ? slot : row;   // ray slots: the trace of an instanced scene finds the slot from them
     BSDF bs;
     V vp, vn, vwo;
     float vEps, vTime;
     {   // the vertex (its record is filled through out-of-line calls, so it lives in scratch
         // memory); the light samples read register copies of the fields they use
         DLVertex vx;
-        dl_vertex<NB, FEAT>(S, P, slot, d, vx);
+        dl_vertex<NB, FEAT>(S, P, slot, d, vx, row);
         bs = vx.bs; vp = vx.p; vn = vx.n; vwo = vx.wo; vEps = vx.is.rayEps; vTime = vx.ray.time;
     }
     for (;;) {
@@ -208,8 +212,8 @@ PGD_INLINE void dl_light_batches(const DevScene &S, const PathSoA &P, int slot, 
             FVal F;
             uint32_t f2 = 0u;
             Pushes o2 = {false, false, false, 0u, 0u};
-            estimate_direct<NB, FEAT>(S, P, slot, slot + jb * (int)c, Col<float4>{P.A, (uint32_t)(jb * NQ * c + slot)},
-                                      Col<float4>{P.B, (uint32_t)(jb * NQ * c + slot)}, ln, bs, pm, vp, vn, vwo,
+            estimate_direct<NB, FEAT>(S, P, row, rb + jb * (int)c, Col<float4>{P.A, (uint32_t)(jb * NQ * c + row)},
+                                      Col<float4>{P.B, (uint32_t)(jb * NQ * c + row)}, ln, bs, pm, vp, vn, vwo,
                                       vEps, vTime, ul, ub, F, f2, o2, nullptr, nullptr);
             if (f2 & PF_PA) mA |= 1u << jb;
             if (f2 & PF_PB) mB |= 1u << jb;
@@ -220,6 +224,7 @@ PGD_INLINE void dl_light_batches(const DevScene &S, const PathSoA &P, int slot, 
             out.mMask = mB;
             fl |= PF_PEND | (all ? 0u : (uint32_t)lnOne << PF_LIGHT_SHIFT);
             P.dlMask[slot] = mA | (mB << 16);
+            P.dlRow[slot] = (uint32_t)row;
             break;
         }
         // nothing queued: every ED of the batch is 0, added now
@@ -303,7 +308,7 @@ PGD_INLINE Pushes dl_spec_step(const DevScene &S, const PathSoA &P, int slot, fl
             ++br;
             if (!SPAWN || !canSpec) continue;
             DLVertex vx;
-            dl_vertex<NB, FEAT>(S, P, slot, d, vx);
+            dl_vertex<NB, FEAT>(S, P, slot, d, vx, slot);
             const int flags = BSDF_SPECULAR | (refl ? BSDF_REFLECTION : BSDF_TRANSMISSION);
             FVal F;
             V wi;
@@ -424,11 +429,12 @@ PGD_INLINE Pushes shade_slot_dl(const DevScene &S, const PathSoA &P, int slot, f
         // ---- the answered batch of light samples [k, kEnd): ED = (0 [+ A]) [+ B] each
         // (EstimateDirect), added in sample order
         const uint32_t msk = P.dlMask[slot];
+        const int row = (int)P.dlRow[slot], rb = P.nInst ? slot : row;   // the batch's row (dl_light_batches)
         const int kEnd = min(k + P.dlBatch, K);
         const int lnOne = (int)(fl >> PF_LIGHT_SHIFT);
         fl &= ~(PF_PEND | PF_PA | PF_PB | (PF_LIGHT_MASK << PF_LIGHT_SHIFT));
         for (int kk = k; kk < kEnd; ++kk) {
-            const int jb = kk - k, rs = slot + jb * (int)c;
+            const int jb = kk - k, rs = rb + jb * (int)c;
             int ln = lnOne;
             if (all) { int j, ns; dl_cursor(S, kk, &ln, &j, &ns); }
             const bool useA = ((msk >> jb) & 1u) && !P.occ[rs];
@@ -441,8 +447,8 @@ PGD_INLINE Pushes shade_slot_dl(const DevScene &S, const PathSoA &P, int slot, f
                     useB = vdot(isect_nn(S, mr, mp, P.hitT[P.rcap + rs], inst_rec(P, slot)), vneg(mr.d)) > 0.f;
                 }
             }
-            dl_add<NB>(S, P, slot, d, kk, K, all, useA, useB, P.A + (size_t)jb * NQ * c + slot,
-                       P.B + (size_t)jb * NQ * c + slot);
+            dl_add<NB>(S, P, slot, d, kk, K, all, useA, useB, P.A + (size_t)jb * NQ * c + row,
+                       P.B + (size_t)jb * NQ * c + row);
         }
         k = kEnd;
         spec = k >= K;
@@ -505,6 +511,7 @@ PGD_INLINE Pushes shade_slot_dl(const DevScene &S, const PathSoA &P, int slot, f
     P.dlk[slot] = (uint32_t)k;
     if (!spec) {
         P.flags[slot] = fl | PF_DLNEE;
+        out.t = true;   // k_shade lists the slot for k_dl_nee
         return out;
     }
     // the top frame's branches: completed here if it cannot branch, else in k_dl_spec

@@ -1261,6 +1261,7 @@ static int ensure_slots(Lane *c, int cap, int NB, int nInst, int nFrames, int ba
     const size_t F = (size_t)nFrames;
     size_t oFL = take(C * F * NBP * 4), oFF = take(C * F * NBP * 4), oFRay = take(C * F * 36), oFDiff = take(C * F * 48),
            oFS = take(C * F * 8), oFHit = take(C * F * 8), oFBr = take(C * F * 4), oDlk = take(nFrames ? C * 4 : 0),
+           oDlList = take(nFrames ? C * 4 : 0), oDlRow = take(nFrames ? C * 4 : 0),
            oMtExt = take(mtExt ? C * 624 * 4 : 0);
     HIPCHK(c->slots.ensure(off));
     char *base = (char *)c->slots.p;
@@ -1294,6 +1295,8 @@ static int ensure_slots(Lane *c, int cap, int NB, int nInst, int nFrames, int ba
     P.fHit = nFrames ? (int *)(base + oFHit) : nullptr;
     P.fBr = nFrames ? (uint32_t *)(base + oFBr) : nullptr;
     P.dlk = nFrames ? (uint32_t *)(base + oDlk) : nullptr;
+    P.dlList = nFrames ? (uint32_t *)(base + oDlList) : nullptr;
+    P.dlRow = nFrames ? (uint32_t *)(base + oDlRow) : nullptr;
     P.mtExt = mtExt ? (uint32_t *)(base + oMtExt) : nullptr;
     c->slotMtExt = mtExt;
     c->slotFrames = nFrames;
@@ -1517,6 +1520,7 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
                 const int nq = q ^ 1;
                 HIPCHK(hipMemsetAsync(P.cnt + CNT_QC(nq), 0, 4, L.s));
                 HIPCHK(hipMemsetAsync(P.cnt + CNT_QS(nq), 0, 4, L.s));
+                if (dl) HIPCHK(hipMemsetAsync(P.cnt + CNT_DLN, 0, 4, L.s));   // this pass's light-sample list
                 HIPCHK(hipEventRecord(e[0], L.s));
                 if (serial) {   // closest-hit queries first, alone on the device
                     if (instPT) {

@@ -109,6 +109,15 @@ __global__ __launch_bounds__(kShadeBlock) PGD_SHADE_ATTR void k_shade(DevScene S
         const unsigned long long m = __ballot(zeroed);
         if ((threadIdx.x & 63) == 0) atomicAdd(&P.cnt[CNT_ZEROED], (uint32_t)__popcll(m));
     }
+    if (MODE == MODE_DL) {   // the slots marked for k_dl_nee join its list, in lane order
+        const unsigned long long bN = __ballot(pu.t);
+        if (bN) {
+            uint32_t base = 0u;
+            if ((threadIdx.x & 63) == __ffsll((long long)bN) - 1) base = atomicAdd(&P.cnt[CNT_DLN], (uint32_t)__popcll(bN));
+            base = __shfl(base, __ffsll((long long)bN) - 1);
+            if (pu.t) P.dlList[base + (uint32_t)__popcll(bN & ((1ull << (threadIdx.x & 63)) - 1ull))] = (uint32_t)slot;
+        }
+    }
     // Regeneration and the queue pushes of the block in one step -- one pair of barriers and at
     // most three atomics per block: free slots take the next camera samples; the closest-hit
     // queue gets the block's continuation / child rays, then the regenerated camera rays, then
@@ -213,13 +222,17 @@ static hipError_t launch(int grid, hipStream_t stream, const DevScene &S, const 
 #ifndef PGD_SPEC_ATTR
 #define PGD_SPEC_ATTR __attribute__((amdgpu_waves_per_eu(SHADE_NB > 32 ? 1 : 2, SHADE_NB > 32 ? 1 : 2)))
 #endif
+// k_dl_nee: thread i takes entry i of the pass's light-sample list (PathSoA::dlList, CNT_DLN
+// entries); blocks past its end return at once
 template <int NB, int FEAT>
 __global__ __launch_bounds__(kShadeBlock) PGD_NEE_ATTR void k_dl_nee(DevScene S, PathSoA P, int qout) {
+    const uint32_t n = P.cnt[CNT_DLN], i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (blockIdx.x * blockDim.x >= n) return;   // (block-uniform, before any barrier)
     if (FEAT & FEAT_MEAS) kd_lds_fill(S);   // measured-BRDF lookups read the LDS copy (as in k_shade)
-    int slot = blockIdx.x * blockDim.x + threadIdx.x;
-    if (P.listMode) slot = (uint32_t)slot < P.cnt[CNT_LIVE] ? (int)P.live[slot] : P.cap;   // the drain (k_shade)
+    const int slot = i < n ? (int)P.dlList[i] : P.cap;
+    const int rb = P.nInst ? slot : (int)i;   // the ray slots' base (dl_light_batches)
     Pushes pu = {false, false, false, 0u, 0u};
-    if (slot < P.cap && P.item[slot] >= 0 && (P.flags[slot] & PF_DLNEE)) dl_light_batches<NB, FEAT>(S, P, slot, pu);
+    if (slot < P.cap && P.item[slot] >= 0 && (P.flags[slot] & PF_DLNEE)) dl_light_batches<NB, FEAT>(S, P, slot, (int)i, pu);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     __shared__ uint32_t qsh[12];   // per wave: M, S totals -> offsets; bases
     const uint32_t nm = (uint32_t)__popc(pu.mMask), ns = (uint32_t)__popc(pu.sMask);
@@ -236,8 +249,8 @@ __global__ __launch_bounds__(kShadeBlock) PGD_NEE_ATTR void k_dl_nee(DevScene S,
     __syncthreads();
     uint32_t *qC = P.qC + (size_t)qout * 2 * P.rcap, *qS = P.qS + (size_t)qout * P.rcap;
     uint32_t km = qsh[8] + qsh[2 * wave] + im - nm, ks = qsh[9] + qsh[2 * wave + 1] + is - ns;
-    for (uint32_t m = pu.mMask; m; m &= m - 1u) qC[km++] = ((uint32_t)(slot + (__ffs(m) - 1) * P.cap) << 1) | 1u;
-    for (uint32_t m = pu.sMask; m; m &= m - 1u) qS[ks++] = (uint32_t)(slot + (__ffs(m) - 1) * P.cap);
+    for (uint32_t m = pu.mMask; m; m &= m - 1u) qC[km++] = ((uint32_t)(rb + (__ffs(m) - 1) * P.cap) << 1) | 1u;
+    for (uint32_t m = pu.sMask; m; m &= m - 1u) qS[ks++] = (uint32_t)(rb + (__ffs(m) - 1) * P.cap);
 }
 template <int NB, int FEAT>
 __global__ __launch_bounds__(kShadeBlock) PGD_SPEC_ATTR void k_dl_spec(DevScene S, PathSoA P, int qout,

@@ -71,8 +71,9 @@ enum { RAY_C = 0, RAY_M = 1, RAY_S = 2 };
 #define CNT_QS(q) (64 + 32 * (q))     // shadow queue size
 #define CNT_QT(q) (224 + 32 * (q))    // MT-window list size (qT): k_mt_init of set q clears set q ^ 1
 // CNT_ERR: nonzero when a path drew past MT output 227 without its full-state row (mt_store), which
-// the host turns into PBRTGPU_E_STATE instead of a silently wrong radiance
-enum { CNT_NEXT = 128, CNT_ZEROED = 160, CNT_WORK = 192, CNT_LIVE = 288, CNT_ERR = 320, CNT_WORDS = 352 };
+// the host turns into PBRTGPU_E_STATE instead of a silently wrong radiance; CNT_DLN: entries of
+// the DirectLighting light-sample list (PathSoA::dlList) of this pass
+enum { CNT_NEXT = 128, CNT_ZEROED = 160, CNT_WORK = 192, CNT_LIVE = 288, CNT_ERR = 320, CNT_DLN = 352, CNT_WORDS = 384 };
 enum { W_RAYS = 0, W_SHADOW = 1, W_NODES_C = 2, W_NODES_S = 3, W_TRIS_C = 4, W_TRIS_S = 5, W_QUADS_C = 6, W_QUADS_S = 7,
        W_HITS = 8, W_RAYS_M = 9, W_HITS_M = 10, W_COUNT = 12 };
 
@@ -133,6 +134,14 @@ struct PathSoA {
     uint32_t *dlk;      // [cap]: light-sample cursor of the top vertex (first sample of its batch)
     uint32_t *dlMask;   // [cap]: the batch's queued shadow rays (bits 0-15) and MIS rays (16-31)
     int dlBatch;        // light samples issued per pass (<= 16); A, B hold [dlBatch][NQ][cap]
+    // the light-sample list: k_shade appends the slots it marks PF_DLNEE (in wave order, count at
+    // CNT_DLN), k_dl_nee's thread i takes entry i, so its waves hold marked slots only.  Entry i is
+    // the slot's batch row: its A / B terms sit in column i of [dlBatch][NQ][cap], its shadow / MIS
+    // rays at ray slots i + j * cap (without instances), and dlRow[slot] = i tells the next
+    // k_shade where to find them -- the rows of one k_shade wave's slots are contiguous, so
+    // writers and readers touch whole lines instead of every other lane's
+    uint32_t *dlList;   // [cap]
+    uint32_t *dlRow;    // [cap]
 };
 // the slot a ray slot belongs to
 PGD_INLINE int slot_of_ray(const PathSoA &P, int rs) { return rs < P.cap ? rs : rs % P.cap; }
@@ -744,6 +753,7 @@ PGD_INLINE bool path_output(const DevScene &S, const float4 (&L)[Bands<NB>::NQ],
 // ray requests produced by one shade step (DirectLighting batches: the MIS / shadow rays of
 // batch samples j at ray slots slot + j * cap, bit j of mMask / sMask)
 // t (path integrator): the slot's MT window goes to k_mt_init's list (mt_window_init)
+// (DirectLighting k_shade: t = the slot was marked PF_DLNEE, it joins the light-sample list)
 struct Pushes { bool c, m, s; uint32_t mMask, sMask; int sIdx, mIdx; bool t; };   // the shadow / MIS ray's ray slot (path)
 
 // Additions to L a vertex makes before its direct light is known, in order: emitted
@@ -768,7 +778,8 @@ template <int NB, int FEAT>
 // stay ONE call site per k_shade pass (shade_vertex): the first active lane overwrites the wave's
 // mask, and the next pass's readers rank themselves in it (PF_PA / PF_PB are set in the same
 // pass).  A second call site, or a persistent k_shade reusing a wave for other slots, would read
-// another lane's entry.  (DirectLighting passes null masks: its batches are indexed per slot.)
+// another lane's entry.  (DirectLighting passes null masks: its batches are indexed by the slot's
+// light-sample list row, passed as `slot` -- here only the column of the M / K scratch and A / B.)
 PGD_INLINE void estimate_direct(const DevScene &S, const PathSoA &P, int slot, int rs, Col<float4> A, Col<float4> B,
                                 int lightNum, const BSDF &bs, PowMemo &pm, V p, V n, V wo, float rayEps, float time,
                                 const float ul[3], const float ub[3], FVal &F, uint32_t &fl, Pushes &out,

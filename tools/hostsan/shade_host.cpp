@@ -82,6 +82,7 @@ static void unpoison_flat(const pbrtgpu_flat_scene *s) {
     u(s->light_shapes, sizeof(*s->light_shapes) * (size_t)s->n_light_shapes);
     u(s->spectra, 4 * (size_t)s->n_spectra_floats);
     u(s->instances, sizeof(*s->instances) * (size_t)std::max(0, s->n_instances));
+    u(s->camera_motion, sizeof(*s->camera_motion));
     if (s->n_instances > 0) u(s->prim_instance, 4 * (size_t)s->n_prims);
     u(s->kdnodes, sizeof(*s->kdnodes) * (size_t)std::max(0, s->n_kdnodes));
     u(s->textures, sizeof(*s->textures) * (size_t)std::max(0, s->n_textures));
@@ -122,6 +123,7 @@ static PathSoA make_soa(int cap, int NB, int nInst, int nFrames, int batch, bool
     P.nFrames = nFrames;
     if (nFrames) {
         P.dlMask = arr<uint32_t>(C);
+        P.dlList = arr<uint32_t>(C); P.dlRow = arr<uint32_t>(C);
         P.fL = arr<float4>(F * NQ * C); P.fF = arr<float4>(F * NQ * C);
         P.fRay = arr<float>(F * 9 * C); P.fDiff = arr<float>(F * 12 * C); P.fS = arr<float>(F * 2 * C);
         P.fHit = arr<int>(F * 2 * C); P.fBr = arr<uint32_t>(F * C); P.dlk = arr<uint32_t>(C);
@@ -146,11 +148,13 @@ static int run(const DevScene &S, PathSoA &P, const ItemSrc &src, int nSlots, fl
     const int64_t pathPasses = MODE == MODE_DL ? (P.nFrames >= 40 ? ((int64_t)1 << 60) : (((int64_t)1 << P.nFrames) - 1) * (S.dlK + 1) + 2)
                                                : S.maxDepth + 3;
     const int64_t maxPasses = 2 * ((src.nItems + nSlots - 1) / nSlots + 1) * pathPasses + 8;
-    auto push = [&](int q, const Pushes &pu, int slot) {
+    // rb: the base of a DirectLighting batch's ray slots (k_dl_nee: its list row without instances)
+    auto push = [&](int q, const Pushes &pu, int slot, int rb = -1) {
         if (pu.c) Q[q].c.push_back((uint32_t)slot << 1);
         if (MODE == MODE_DL) {
-            for (uint32_t m = pu.mMask; m; m &= m - 1u) Q[q].c.push_back(((uint32_t)(slot + (__builtin_ctz(m)) * cap) << 1) | 1u);
-            for (uint32_t m = pu.sMask; m; m &= m - 1u) Q[q].s.push_back((uint32_t)(slot + (__builtin_ctz(m)) * cap));
+            if (rb < 0) rb = slot;
+            for (uint32_t m = pu.mMask; m; m &= m - 1u) Q[q].c.push_back(((uint32_t)(rb + (__builtin_ctz(m)) * cap) << 1) | 1u);
+            for (uint32_t m = pu.sMask; m; m &= m - 1u) Q[q].s.push_back((uint32_t)(rb + (__builtin_ctz(m)) * cap));
         } else {
             if (pu.m) Q[q].c.push_back(((uint32_t)(MODE == MODE_PATH ? pu.mIdx : slot) << 1) | 1u);
             if (pu.s) Q[q].s.push_back((uint32_t)(MODE == MODE_PATH ? pu.sIdx : slot));
@@ -165,6 +169,7 @@ static int run(const DevScene &S, PathSoA &P, const ItemSrc &src, int nSlots, fl
     auto shade = [&](int qout) {
         Q[qout].c.clear();
         Q[qout].s.clear();
+        P.cnt[CNT_DLN] = 0;
         for (int i = 0; i < nSlots; ++i) {
             const int slot = 64 * i;
             threadIdx.x = (unsigned)(slot & 63);
@@ -183,18 +188,19 @@ static int run(const DevScene &S, PathSoA &P, const ItemSrc &src, int nSlots, fl
                 if (done) { P.item[slot] = -1; freeSlot = true; ++finished; note_draws(slot); }
             }
             push(qout, pu, slot);
+            if (MODE == MODE_DL && pu.t) P.dlList[P.cnt[CNT_DLN]++] = (uint32_t)slot;   // the light-sample list
             if (freeSlot && next < src.nItems) {
                 path_start<NB>(S, P, src, slot, next++);
                 Q[qout].c.push_back((uint32_t)slot << 1);
             }
         }
         if (MODE == MODE_DL) {
-            for (int i = 0; i < nSlots; ++i) {   // k_dl_nee
-                const int slot = 64 * i;
-                threadIdx.x = (unsigned)(slot & 63);
+            for (uint32_t i = 0; i < P.cnt[CNT_DLN]; ++i) {   // k_dl_nee: entry i of the list, row i
+                const int slot = (int)P.dlList[i];
+                threadIdx.x = (unsigned)(i & 63);
                 Pushes pu = {false, false, false, 0u, 0u};
-                if (P.item[slot] >= 0 && (P.flags[slot] & PF_DLNEE)) dl_light_batches<NB, FEAT>(S, P, slot, pu);
-                push(qout, pu, slot);
+                if (P.item[slot] >= 0 && (P.flags[slot] & PF_DLNEE)) dl_light_batches<NB, FEAT>(S, P, slot, (int)i, pu);
+                push(qout, pu, slot, P.nInst ? slot : (int)i);
             }
             for (int i = 0; i < nSlots; ++i) {   // k_dl_spec
                 const int slot = 64 * i;
