@@ -79,6 +79,9 @@ CASES = [
     ("imagemap.pack", dict(xres=48, yres=36, spp=4, maxdepth=3)),
     ("imagemap.pack", dict(xres=40, yres=30, spp=2, maxdepth=3, integrator="directlighting", strategy="all")),
     ("animcam.pack", dict(xres=40, yres=30, spp=4, maxdepth=6)),
+    # DirectLighting over instances (ray slots stay per slot, terms per list row) and at 60 bands
+    ("anim-killeroos-moving.pack", dict(xres=24, yres=24, spp=4, maxdepth=5, integrator="directlighting", strategy="all")),
+    ("metal.pack", dict(xres=24, yres=24, spp=4, maxdepth=5, integrator="directlighting", strategy="all")),
 ]
 
 
@@ -86,7 +89,7 @@ CASES = [
                                                "path_bunny", "path_metal60", "metadata", "path_coverage_b30",
                                                "lens_diffraction", "lens_diffraction_spectral", "lens_pinholes",
                                                "lens_microlens_spectral", "eye", "eye_spectral", "lens_diffraction_dl",
-                                               "imagemap", "imagemap_dl", "animcam"])
+                                               "imagemap", "imagemap_dl", "animcam", "dl_anim_inst", "dl_metal60"])
 def test_replay_matches_oracle(pg, tmp_path, pack, a):
     exe = _build("shade_host")
     scene = pg.Scene.load(os.path.join(PACKS, pack), **a)
