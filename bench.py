@@ -130,16 +130,31 @@ def cpu_info():
     return model, ncpu, aff
 
 
+def cgroup_cpus():
+    """CPUs this process's cgroup may use (cgroup v2 cpu.max quota / period), or None"""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, p = f.read().split()[:2]
+        return None if q == "max" else float(q) / float(p)
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_baseline(scene, target_s):
     """CPU restatement (oracle/liboracle_libm.so, TEST INFRASTRUCTURE: the build with glibc's float
     transcendentals, whose per-core rate profiles/cpu_calibration.json measured against the
     reference harness itself on one box) on the host: all spp of
     pseudo-randomly spread pixels of the same frame, sized to ~target_s seconds on every core
     this process may use (the affinity mask, capped by OMP_NUM_THREADS where the box sets a
-    CPU share), then ~target_s / 3 on one core."""
+    CPU share and by the cgroup's cpu.max quota: 16 CPUs of the 256-CPU host on the GPU box,
+    profiles/r05/r05a/cpu_share.txt), then ~target_s / 3 on one core.  The whole host is reported
+    as the one-core rate times its CPU count, marked as an extrapolation."""
     model, ncpu, aff = cpu_info()
     share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    quota = cgroup_cpus()
     threads = max(1, min(aff, share) if share > 0 else aff)
+    if quota is not None:   # more threads than the cgroup's CPU quota run no faster
+        threads = max(1, min(threads, int(quota)))
     o = pg.oracle(libm_float=True)
     spp = scene.spp
     pps = scene.paths_per_sample()   # SpectralRenderer singleDirection: a sample is nWaveBands paths
@@ -161,6 +176,11 @@ def cpu_baseline(scene, target_s):
     per_core = n1 / dt1 / 1e6
     return {"value": round(n / dt / 1e6, 4), "unit": "Mpaths/s", "cores": threads, "kind": "port",
             "one_core": round(per_core, 4), "host_cpus": ncpu, "affinity_cpus": aff, "cpu_model": model,
+            "cgroup_cpus": quota,
+            "all_host_cores_extrapolated": {
+                "value": round(per_core * ncpu, 2), "cores": ncpu,
+                "how": "one_core x host_cpus (linear, an upper bound): this job's cgroup quota (cgroup_cpus) caps "
+                       "what it can run on the host, so the whole host is not measurable from here"},
             "sample": "%d paths = all %d samples of %d pseudo-randomly spread pixels of the same frame, %.1f s on "
                       "%d threads; 1-core leg %d paths in %.1f s" % (n, spp, n // spp // pps, dt, threads, n1, dt1),
             "calibration": "this build (liboracle_libm.so) vs the reference harness per core, same box: "

@@ -30,6 +30,23 @@
  *
  * The table values below are the glibc sources' hexadecimal constants; tools/libmf_check.c
  * verifies each one against the data of the system libm.
+ *
+ * ATTRIBUTION AND LICENSE.  This file is a derivative of the GNU C Library, version 2.35, and is
+ * distributed under the GNU Lesser General Public License, version 2.1 or (at your option) any
+ * later version (https://www.gnu.org/licenses/old-licenses/lgpl-2.1.html), as those sources are:
+ *   - sinf, cosf, sincosf, expf, logf, powf and their data tables (sysdeps/ieee754/flt-32,
+ *     sincosf.h, e_exp2f_data.c, e_logf_data.c, e_powf_log2_data.c, math_config.h):
+ *     Copyright (C) 2017-2022 Free Software Foundation, Inc.; contributed by ARM Ltd
+ *     (Szabolcs Nagy, Wilco Dijkstra).
+ *   - acosf, atanf, atan2f, tanf (e_acosf.c, s_atanf.c, e_atan2f.c, s_tanf.c, k_tanf.c): from
+ *     fdlibm, Copyright (C) 1993 by Sun Microsystems, Inc.  All rights reserved.  Developed at
+ *     SunPro, a Sun Microsystems, Inc. business.  Permission to use, copy, modify, and distribute
+ *     this software is freely granted, provided that this notice is preserved.  Float versions by
+ *     Ian Lance Taylor, Cygnus Support.
+ * This library is distributed in the hope that it will be useful, but WITHOUT ANY WARRANTY;
+ * without even the implied warranty of MERCHANTABILITY or FITNESS FOR A PARTICULAR PURPOSE.  See
+ * the GNU Lesser General Public License for more details.  The rest of this repository is not
+ * derived from glibc; the LGPL terms apply to this file and the object code compiled from it.
  */
 #ifndef PBRT_LIBMF_H
 #define PBRT_LIBMF_H

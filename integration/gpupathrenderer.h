@@ -1,7 +1,7 @@
 // integration/gpupathrenderer.h -- the reference-side binding of the MI355X core: a
 // Renderer (core/renderer.h:35-46) that renders a WorldBlock's frame on the GPUs of one node
-// through the C ABIs include/pbrthost.h and include/pbrtgpu.h, and writes the film with the
-// spectral film's .dat layout (film/spectralImage.cpp:267-378).
+// through the C ABIs include/pbrthost.h and include/pbrtgpu.h, and hands the rendered film to
+// the camera's own Film, whose WriteImage writes it (film/spectralImage.cpp:267-378: the .dat).
 //
 // A maintainer adds this file and gpupathrenderer.cpp to the reference tree (e.g.
 // src/renderers/), one branch to RenderOptions::MakeRenderer (core/api.cpp:1333-1420) and
@@ -27,9 +27,13 @@ public:
     //   "integer slices" (tile slices per GPU), "string scenefile" (overrides SceneFile()),
     //   "integer nWaveBands" / "string samplingMethod" (the SpectralRenderer's, api.cpp:1378-1379).
     //   "bool gpusetup" (refine loopsubdiv shapes on the GPU, pbrtgpu_loop_subdivide).
+    //   "integer pixelsamples" / "integer maxdepth": override the scene file's Sampler /
+    //   SurfaceIntegrator values (the harness's --spp / --maxdepth; default: the scene's).
+    // The resolution is the camera film's (Film::xResolution / yResolution).
     GpuPathRenderer(Camera *camera, const ParamSet &params);
     ~GpuPathRenderer();
-    // Renderer::Render: one frame over all GPUs, .dat written; on failure Error() and no file
+    // Renderer::Render: one frame over all GPUs, added to camera->film (one AddSample per
+    // pixel, exact) and written by its WriteImage; on failure Error() and no file
     void Render(const Scene *scene);
     // per-ray queries stay on the CPU path: the core renders whole frames only
     Spectrum Li(const Scene *scene, const RayDifferential &ray, const Sample *sample, RNG &rng,
@@ -52,6 +56,7 @@ private:
     int ngpu, slices, status;
     bool gpuSetup;   // "bool gpusetup": refine loopsubdiv shapes on the GPU (pbrtgpu_loop_subdivide)
     int waveBands, spectralSampling;   // "nWaveBands" (> 0: SpectralRenderer), "samplingMethod"
+    int spp, maxDepth;                 // "pixelsamples", "maxdepth" overrides (-1: the scene's)
     uint32_t seed;
 };
 

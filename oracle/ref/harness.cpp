@@ -356,6 +356,7 @@ static bool specSampler = false;
 static Scene *gScene = NULL;
 static Camera *gCamera = NULL;
 static HarnessFilm *gFilm = NULL;
+static Film *gCameraFilm = NULL;   // --gpupath with --refdat: the camera's film is the reference's own
 static Filter *gFilter = NULL;
 static SurfaceIntegrator *gSurf = NULL;
 static VolumeIntegrator *gVol = NULL;
@@ -534,7 +535,7 @@ void pbrtWorldEnd() {
     tcache.Lookup(cameraToWorld[1], &c2w[1], NULL);
     AnimatedTransform ac2w(c2w[0], tStart, c2w[1], tEnd);
     if (cameraName != "perspective") { fprintf(stderr, "harness: camera %s unsupported\n", cameraName.c_str()); exit(2); }
-    gCamera = CreatePerspectiveCamera(cameraParams, ac2w, gFilm);
+    gCamera = CreatePerspectiveCamera(cameraParams, ac2w, gCameraFilm ? gCameraFilm : (Film *)gFilm);
     if (ovMaxDepth >= 0) { int v = ovMaxDepth; surfParams.AddInt("maxdepth", &v, 1); }
     // the configs override the scene's integrator to "path" (SURVEY App. B), the harness's
     // default; --surf directlighting creates the DirectLightingIntegrator from the scene's
@@ -656,6 +657,9 @@ int main(int argc, char **argv) {
 #else
     if (specOut) { fprintf(stderr, "harness: --spectra needs the SampledSpectrum build\n"); return 1; }
 #endif
+#ifdef HARNESS_GPUPATH
+    if (gpupath && refFilm) gCameraFilm = refFilm;
+#endif
     if (string(scene) == "-") return 0;
     if (!ParseFile(scene)) { fprintf(stderr, "harness: cannot parse %s\n", scene); return 1; }
     if (!gScene) { fprintf(stderr, "harness: no WorldEnd\n"); return 1; }
@@ -663,8 +667,16 @@ int main(int argc, char **argv) {
     if (gpupath) {
         // Renderer "gpupath" as the binding's MakeRenderer branch creates it (INTEGRATION.md
         // §1): the renderer owns the camera; Render() reports failures through Error()
+        // With --refdat the camera's film is the reference's SpectralImageNoCameraFilm (created
+        // before the scene, refFilm above): the renderer hands its frame to it and its own
+        // WriteImage writes the .dat.  --spp / --maxdepth / --seed go to the renderer as its
+        // parameters (the film's --res it reads from the film).
         GpuPathRenderer::SetSceneFile(scene);
-        GpuPathRenderer *r = CreateGpuPathRenderer(gCamera, ParamSet());
+        ParamSet rp;
+        rp.AddInt("seed", &seed, 1);
+        if (spp > 0) rp.AddInt("pixelsamples", &spp, 1);
+        if (ovMaxDepth >= 0) { int md = ovMaxDepth; rp.AddInt("maxdepth", &md, 1); }
+        GpuPathRenderer *r = CreateGpuPathRenderer(gCamera, rp);
         r->Render(gScene);
         fprintf(stderr, "harness: gpupath status %d\n", r->LastStatus());
         int st = r->LastStatus();

@@ -25,7 +25,8 @@
     (defined(PGD_EXPERIMENT_FASTMATH) || defined(PGD_EXPERIMENT_NO_MIS) || defined(PGD_EXPERIMENT_NO_NEE) ||  \
      defined(PGD_EXP_KD_FIXED) || defined(PGD_EXP_MEAS_CHEAP) || defined(PGD_EXP_MT_CHEAP) ||              \
      defined(PGD_EXP_NOBETA) || defined(PGD_EXP_NOSPEC) || defined(PGD_EXP_NO_AB) ||                        \
-     defined(PGD_EXP_NO_MT_LIST) || defined(PGD_EXP_NO_OUT) || defined(PGD_EXP_NO_ABLOOP))
+     defined(PGD_EXP_NO_MT_LIST) || defined(PGD_EXP_NO_OUT) || defined(PGD_EXP_NO_ABLOOP) ||                  \
+     defined(PGD_EXP_NB_HALF))
 #error "PGD_EXP* / PGD_EXPERIMENT_* switches change the radiance: experiment builds only (tools/build_exp.sh)"
 #endif
 

@@ -173,6 +173,21 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_shadow(DevScene S, PathSo
 // rays).  One loop trip is one traversal step: an interior node (both children tested) and
 // then, if the lane stands on a leaf, that leaf's primitives.  Per ray the nodes visited,
 // primitives tested and their order are bvh_walk's.
+// The persistent trace waves own contiguous ranges of the queue, in wave order.  Blocks are dealt
+// round-robin over the 8 XCDs (blocks b, b + 8, ... share one, MI355X_MICROARCH.md "Workgroup
+// dispatch"), so with the plain order every XCD traces rays from every stretch of the queue and
+// its 4 MiB L2 holds the BVH nodes and triangles of the whole image region the pass covers.  With
+// xcdMap the blocks of one XCD take one contiguous eighth of the queue: queue order follows slot
+// order, and slots follow the pixel order of the items they took, so an XCD's rays come from
+// neighbouring pixels (and their paths) and share the part of the scene they see.  Speed only:
+// any block-to-XCD placement gives the same answers.
+PGD_INLINE uint32_t trace_wave(int xcdMap) {
+    uint32_t b = blockIdx.x;
+    const uint32_t nb = gridDim.x;
+    if (xcdMap && (nb & 7u) == 0u) b = (b & 7u) * (nb >> 3) + (b >> 3);
+    return (b * blockDim.x + threadIdx.x) >> 6;
+}
+
 template <bool ANY, bool STATS>
 __global__ __launch_bounds__(kTraceBlock) PGD_TRACE_ATTR void k_trace_pt(DevScene S, PathSoA P, int q, int refill, int ring, uint2 *__restrict__ spill) {
     // traversal stack: the top kStackLDS entries of each lane in LDS (a ring, column per
@@ -191,7 +206,7 @@ __global__ __launch_bounds__(kTraceBlock) PGD_TRACE_ATTR void k_trace_pt(DevScen
     const uint32_t n = ANY ? P.cnt[CNT_QS(q)] : P.cnt[CNT_QC(q)];
     const uint32_t *Q = ANY ? P.qS + (size_t)q * P.rcap : P.qC + (size_t)q * 2 * P.rcap;
     const uint32_t lane = threadIdx.x & 63;
-    const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = (gridDim.x * blockDim.x) >> 6;
+    const uint32_t wave = trace_wave(P.xcdMap), nw = (gridDim.x * blockDim.x) >> 6;
     uint32_t next = (uint32_t)((uint64_t)n * wave / nw);
     const uint32_t end = (uint32_t)((uint64_t)n * (wave + 1) / nw);
     bool active = false;
@@ -349,7 +364,7 @@ __global__ __launch_bounds__(kTraceBlock) PGD_TRACE_ATTR void k_trace_s4(DevScen
     const uint32_t n = P.cnt[CNT_QS(q)];
     const uint32_t *Q = P.qS + (size_t)q * P.rcap;
     const uint32_t lane = threadIdx.x & 63;
-    const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = (gridDim.x * blockDim.x) >> 6;
+    const uint32_t wave = trace_wave(P.xcdMap), nw = (gridDim.x * blockDim.x) >> 6;
     uint32_t next = (uint32_t)((uint64_t)n * wave / nw);
     const uint32_t end = (uint32_t)((uint64_t)n * (wave + 1) / nw);
     bool active = false;
@@ -468,7 +483,7 @@ __global__ __launch_bounds__(kTraceBlock) PGD_TRACE_ATTR void k_trace_c4(DevScen
     const uint32_t n = P.cnt[CNT_QC(q)];
     const uint32_t *Q = P.qC + (size_t)q * 2 * P.rcap;
     const uint32_t lane = threadIdx.x & 63;
-    const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = (gridDim.x * blockDim.x) >> 6;
+    const uint32_t wave = trace_wave(P.xcdMap), nw = (gridDim.x * blockDim.x) >> 6;
     uint32_t next = (uint32_t)((uint64_t)n * wave / nw);
     const uint32_t end = (uint32_t)((uint64_t)n * (wave + 1) / nw);
     bool active = false;
@@ -617,7 +632,7 @@ __global__ __launch_bounds__(kTraceBlock) PGD_TRACE_INST_ATTR void k_trace_inst(
     const uint32_t n = ANY ? P.cnt[CNT_QS(q)] : P.cnt[CNT_QC(q)];
     const uint32_t *Q = ANY ? P.qS + (size_t)q * P.rcap : P.qC + (size_t)q * 2 * P.rcap;
     const uint32_t lane = threadIdx.x & 63;
-    const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = (gridDim.x * blockDim.x) >> 6;
+    const uint32_t wave = trace_wave(P.xcdMap), nw = (gridDim.x * blockDim.x) >> 6;
     uint32_t next = (uint32_t)((uint64_t)n * wave / nw);
     const uint32_t end = (uint32_t)((uint64_t)n * (wave + 1) / nw);
     bool active = false;
@@ -1205,6 +1220,10 @@ static bool shadow4_on() {
     const char *e = getenv("PBRTGPU_SHADOW4");
     return !e || atoi(e) != 0;
 }
+static int xcd_map_on() {
+    const char *e = getenv("PBRTGPU_XCD_MAP");
+    return (!e || atoi(e) != 0) ? 1 : 0;
+}
 static bool drain_list_on() {
     const char *e = getenv("PBRTGPU_DRAIN_LIST");
     return !e || atoi(e) != 0;
@@ -1283,6 +1302,7 @@ static int ensure_slots(Lane *c, int cap, int NB, int nInst, int nFrames, int ba
     P.qT = (uint32_t *)(base + oQT);
     P.live = (uint32_t *)(base + oLive);
     P.listMode = 0;
+    P.xcdMap = 0;
     P.cnt = (uint32_t *)(base + oCnt);
     P.nInst = nInst;
     P.instM = nInst ? (float4 *)(base + oInst) : nullptr;
@@ -1408,6 +1428,7 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
         r.drain = false;
         r.liveGrid = r.grid;
         L.P.listMode = 0;
+        L.P.xcdMap = xcd_map_on();
         // drain bound of this run: a path lives at most pathPasses passes, so every slot
         // takes a new item at least once per pathPasses passes while items remain; twice
         // that, plus the overshoot of one enqueued batch, means the wavefront is stuck

@@ -350,6 +350,9 @@ template hipError_t launch_shade_meta<SHADE_NB, SHADE_FEAT>(int, hipStream_t, co
 template <int NB, int FEAT>
 hipError_t launch_shade(int grid, hipStream_t stream, const DevScene &S, const PathSoA &P, const ItemSrc &src, int qout,
                         float *Lout) {
+#ifdef PGD_EXP_NB_HALF   // timing experiment only: a 32-band scene shaded by the 16-band kernel (wrong radiance)
+    if constexpr (NB == 32) return launch<16, FEAT, MODE_PATH>(grid, stream, S, P, src, qout, Lout);
+#endif
     return launch<NB, FEAT, MODE_PATH>(grid, stream, S, P, src, qout, Lout);
 }
 template hipError_t launch_shade<SHADE_NB, SHADE_FEAT>(int, hipStream_t, const DevScene &, const PathSoA &,

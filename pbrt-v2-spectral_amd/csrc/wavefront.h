@@ -117,6 +117,7 @@ struct PathSoA {
     // region's mask to all ones, so every reader (which ranks itself in the stored mask) finds it
     // there, whatever mode the writing pass ran in.
     int listMode;
+    int xcdMap;         // the trace kernels' XCD-contiguous queue ranges (pbrtgpu.hip trace_wave)
     uint32_t *live;     // [cap]
     uint32_t *cnt;     // counters (CNT_*), work counters as u64 from word CNT_WORK
     float4 *instM;      // [cap][nInst][8]: the path's instance transforms (inst_load), or null

@@ -990,7 +990,15 @@ private:
                 if (a.text == "All") activeBits = 3; else if (a.text == "EndTime") activeBits = 2; else if (a.text == "StartTime") activeBits = 1;
                 else throw std::runtime_error("bad ActiveTransform " + a.text);
             } else if (d == "TransformTimes") { tStart = Num(); tEnd = Num(); }
-            else if (d == "PixelFilter") { Str(); Params(); }   // api.cpp:857-860 keeps the name only
+            else if (d == "PixelFilter") {
+                // api.cpp:857-860 keeps the name and parameters, MakeFilter (api.cpp:673-690) creates
+                // the filter; the core renders the box filter at its default width (box.cpp:36-41),
+                // the packaged scenes' only filter: anything else is refused, not approximated
+                const std::string fname = Str();
+                const ParamSet fp = Params();
+                if (fname != "box" || fp.FindOneFloat("xwidth", .5f) != .5f || fp.FindOneFloat("ywidth", .5f) != .5f)
+                    throw std::runtime_error("PixelFilter \"" + fname + "\": only the box filter of width .5 is supported");
+            }
             else if (d == "Film") { Str(); filmParams = Params(); }
             else if (d == "Sampler") { Str(); samplerParams = Params(); }
             else if (d == "Accelerator") { Str(); accelParams = Params(); }
@@ -2154,7 +2162,7 @@ void ComputeCamera(const CameraParams &cp, int xres, int yres, pbrtgpu_camera *o
     C.px_count = std::max(1, Ceil2Int(xres * cp.crop[1]) - C.px_start);
     C.py_start = Ceil2Int(yres * cp.crop[2]);
     C.py_count = std::max(1, Ceil2Int(yres * cp.crop[3]) - C.py_start);
-    const float fw = 0.5f;   // BoxFilter default width (box.cpp:36-41); PixelFilter params are ignored (api.cpp:857-860)
+    const float fw = 0.5f;   // BoxFilter default width (box.cpp:36-41); other filters are refused at PixelFilter
     C.sx_start = Floor2Int(C.px_start + 0.5f - fw);
     C.sx_end = Floor2Int(C.px_start + 0.5f + C.px_count + fw);
     C.sy_start = Floor2Int(C.py_start + 0.5f - fw);

@@ -1,6 +1,7 @@
 import os
 import sys
 
+import numpy as np
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -50,3 +51,24 @@ def merl_dir(tmp_path_factory):
 def merl_scene(pg, merl_dir, cfg):
     w, h, spp, seed, md = [int(v) for v in cfg]
     return pg.Scene.load(os.path.join(merl_dir, "merl.pbrt"), xres=w, yres=h, spp=spp, maxdepth=md, seed=seed)
+
+
+def bits_equal(a, b):
+    """elementwise: the float32 bits are equal, or both values are NaN"""
+    a = np.ascontiguousarray(a, dtype=np.float32)
+    b = np.ascontiguousarray(b, dtype=np.float32)
+    assert a.shape == b.shape, (a.shape, b.shape)
+    return (a.view(np.int32) == b.view(np.int32)) | (np.isnan(a) & np.isnan(b))
+
+
+def assert_bit_exact(got, ref, what=""):
+    """every float32 of `got` has the bits of `ref` (NaN as NaN); on failure the message names
+    the elements that differ and their largest relative error"""
+    same = bits_equal(got, ref)
+    if not same.all():
+        g64, r64 = np.asarray(got, np.float64), np.asarray(ref, np.float64)
+        d = np.abs(g64 - r64)[~same]
+        den = np.maximum(np.abs(r64)[~same], 1e-30)
+        first = np.argwhere(~same)[:4].tolist()
+        raise AssertionError("%s: %d of %d values differ (first %s), max rel %.3e"
+                             % (what, int((~same).sum()), same.size, first, float(np.nanmax(d / den))))

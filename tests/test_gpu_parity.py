@@ -1,17 +1,19 @@
-"""GPU parity: the HIP path (libpbrtgpu.so, through the C ABI) against the CPU oracle.
+"""GPU parity: the HIP path (libpbrtgpu.so, through the C ABI) against the CPU oracle and the
+reference harness's own fixtures.
 
-The oracle here is oracle/liboracle.so (transcendentals double-rounded, the definition the
-kernels implement), which is itself pinned bit-exactly to the reference harness by
-tests/test_oracle_golden.py.  Integer/byte work (sampler, MT19937, BVH hit indices, spill
-bookkeeping) must match exactly; radiance must match bit for bit except for paths where a
-double-rounded transcendental lands within one double ulp of a float rounding boundary
-(probability ~1e-8 per call), which we bound at 1e-4 of paths with max relative error 1e-3.
+The oracle here is oracle/liboracle.so, whose float transcendentals are glibc 2.35's routines
+restated (include/pbrt_libmf.h, checked over all 2^32 inputs against the system libm), the same
+header the kernels compile; it is pinned bit-exactly to the reference harness by
+tests/test_oracle_golden.py.  Every assertion here is bit equality of the float32 results (NaN as
+NaN, conftest.assert_bit_exact): per-path radiance, films, hit records, occlusion answers.  The
+lens camera's results are pinned to the oracle only (its reference TU needs GSL, absent here:
+parity unpinned vs the reference).
 """
 import os
 
 import numpy as np
 
-from test_oracle_golden import exact_rate
+from conftest import assert_bit_exact
 import pytest
 
 pytestmark = pytest.mark.gpu
@@ -42,10 +44,7 @@ def test_paths_match_oracle(pg, killeroo64, dev):
     keys = _keys(killeroo64)
     Lg = dev.trace_paths(keys)
     Lo = pg.oracle().trace_paths(killeroo64, keys)
-    exact = np.all(Lg.view(np.int32) == Lo.view(np.int32), axis=1)
-    rel = np.abs(Lg - Lo).max(axis=1) / np.maximum(np.abs(Lo).max(axis=1), 1e-30)
-    assert exact.mean() >= 1 - 1e-4, "bit-exact paths %d/%d" % (exact.sum(), len(exact))
-    assert rel.max() < 1e-3
+    assert_bit_exact(Lg, Lo, "paths vs oracle")
 
 
 def test_film_matches_oracle(pg, killeroo64, dev):
@@ -53,10 +52,7 @@ def test_film_matches_oracle(pg, killeroo64, dev):
     film = dev.film()
     ref, ost = pg.oracle().render(killeroo64)
     assert st[pg.STAT_PATHS] == killeroo64.width * killeroo64.height * killeroo64.spp
-    exact = np.all(film.view(np.int32) == ref.view(np.int32), axis=2)
-    assert exact.mean() >= 0.999, "bit-exact pixels %d/%d" % (exact.sum(), exact.size)
-    den = np.maximum(np.abs(ref).max(axis=2), 1e-3)
-    assert (np.abs(film - ref).max(axis=2) / den).max() < 1e-3
+    assert_bit_exact(film, ref, "film vs oracle")
 
 
 def test_intersect_matches_oracle(pg, killeroo64, dev):
@@ -127,14 +123,7 @@ def test_paths_vs_reference_golden(pg, name):
     with pg.Device(0) as d:
         d.upload(scene)
         L = d.trace_paths(g["keys"])
-    ref = g["L"]
-    same = np.all(L.view(np.int32) == ref.view(np.int32), axis=1)
-    rel = np.abs(L - ref).max(axis=1) / np.maximum(np.abs(ref).max(axis=1), 1e-30)
-    # a path with many transcendental calls (measured BRDF: 2 atan2 + ~10 exp per lookup)
-    # meets a last-ulp difference more often; the bounds that matter are the two below
-    assert same.mean() >= exact_rate(name)
-    assert (rel > 1e-4).mean() <= 5e-4
-    assert np.abs(L.sum(0) - ref.sum(0)).max() / np.abs(ref.sum(0)).max() < 1e-5
+    assert_bit_exact(L, g["L"], name)
 
 
 @pytest.mark.parametrize("name", ["killeroo_film_96x72s16", "anim_film_40x40s8", "bunny_film_48x27s8",
@@ -143,7 +132,7 @@ def test_paths_vs_reference_golden(pg, name):
                                   "animcam_film_64x48s4"])
 def test_film_vs_reference_golden(pg, name):
     """Whole-film render against the reference's film (raw sums, incl. neighbour-pixel
-    samples): image L-inf relative error < 1e-4 (BASELINE.json north star)."""
+    samples): bit for bit."""
     from conftest import GOLDEN
     g = np.load(os.path.join(GOLDEN, name + ".npz"))
     scene = _golden_scene(pg, g["config"], name)
@@ -154,13 +143,7 @@ def test_film_vs_reference_golden(pg, name):
     ref = g["film"]
     if name.startswith("killeroo_film"):
         assert st[pg.STAT_SPILLS] > 0
-    assert np.abs(film - ref).max() / np.abs(ref).max() < 1e-4
-    # a fraction 1 - r of paths differs from glibc-float transcendentals in the last ulp
-    # (DESIGN.md §3.2), so an spp-sample pixel is bit-exact with probability ~r^spp
-    # (killeroo: r ~0.993, spp 16 -> 0.89; metal: r ~0.925, spp 8 -> 0.54)
-    spp = int(g["config"][2])
-    r = {"metal": 0.925, "coverage": 0.955}.get(name.split("_")[0], 0.993)
-    assert np.all(film.view(np.int32) == ref.view(np.int32), axis=2).mean() >= r ** spp - 0.05
+    assert_bit_exact(film, ref, name)
 
 
 def test_tile_shards_compose_to_full_frame(pg, killeroo64, dev):
@@ -209,9 +192,9 @@ def test_motion_blur_instances_match_oracle(pg, monkeypatch, walk):
         hg, og = d.intersect(rays)
     o = pg.oracle()
     Lo = o.trace_paths(scene, keys)
-    assert np.all(Lg.view(np.int32) == Lo.view(np.int32), axis=1).mean() >= 1 - 1e-4
+    assert_bit_exact(Lg, Lo, "paths vs oracle")
     ref, _ = o.render(scene)
-    assert np.all(film.view(np.int32) == ref.view(np.int32), axis=2).mean() >= 0.999
+    assert_bit_exact(film, ref, "film vs oracle")
     ho, oo = o.intersect(scene, rays)
     assert np.array_equal(hg[:, 3].view(np.int32), ho[:, 3].view(np.int32))
     assert np.array_equal(og, oo)
@@ -234,9 +217,9 @@ def test_measured_brdf_matches_oracle(pg, monkeypatch, kd_lds):
         film = d.film()
     o = pg.oracle()
     Lo = o.trace_paths(scene, keys)
-    assert np.all(Lg.view(np.int32) == Lo.view(np.int32), axis=1).mean() >= 1 - 1e-4
+    assert_bit_exact(Lg, Lo, "paths vs oracle")
     ref, _ = o.render(scene)
-    assert np.all(film.view(np.int32) == ref.view(np.int32), axis=2).mean() >= 0.999
+    assert_bit_exact(film, ref, "film vs oracle")
 
 
 def test_metal_textures_environment_match_oracle(pg):
@@ -253,9 +236,9 @@ def test_metal_textures_environment_match_oracle(pg):
         film = d.film()
     o = pg.oracle()
     Lo = o.trace_paths(scene, keys)
-    assert np.all(Lg.view(np.int32) == Lo.view(np.int32), axis=1).mean() >= 1 - 1e-4
+    assert_bit_exact(Lg, Lo, "paths vs oracle")
     ref, _ = o.render(scene)
-    assert np.all(film.view(np.int32) == ref.view(np.int32), axis=2).mean() >= 0.999
+    assert_bit_exact(film, ref, "film vs oracle")
 
 
 def test_shade_variants_agree(pg, killeroo64, monkeypatch):
@@ -286,9 +269,9 @@ def test_coverage_scene_matches_oracle(pg):
         film = d.film()
     o = pg.oracle()
     Lo = o.trace_paths(scene, keys)
-    assert np.all(Lg.view(np.int32) == Lo.view(np.int32), axis=1).mean() >= 1 - 1e-4
+    assert_bit_exact(Lg, Lo, "paths vs oracle")
     ref, _ = o.render(scene)
-    assert np.all(film.view(np.int32) == ref.view(np.int32), axis=2).mean() >= 0.999
+    assert_bit_exact(film, ref, "film vs oracle")
 
 
 @pytest.mark.parametrize("ring,refill", [("1", "1"), ("2", "64"), ("4", "7")])
@@ -312,8 +295,8 @@ def test_traversal_stack_spill_and_ray_replacement(pg, killeroo64, dev, monkeypa
         assert w[k] == w0[k], k
 
 
-@pytest.mark.parametrize("name,exact", [("bunny", True), ("coverage", False)])
-def test_mis_rays_that_can_reach_the_light_are_traced(pg, name, exact):
+@pytest.mark.parametrize("name", ["bunny", "coverage"])
+def test_mis_rays_that_can_reach_the_light_are_traced(pg, name):
     """k_shade skips only MIS rays that miss every shape of the sampled area light
     (wavefront.h mis_may_reach).  In scenes whose BSDF samples do reach the light some MIS
     rays are still traced, and per-path radiance stays identical to the oracle, which traces
@@ -328,13 +311,12 @@ def test_mis_rays_that_can_reach_the_light_are_traced(pg, name, exact):
         Lg = d.trace_paths(keys)
     assert w["mis_rays"] > 0
     Lo = pg.oracle().trace_paths(scene, keys)
-    same = np.all(Lg.view(np.int32) == Lo.view(np.int32), axis=1).mean()
-    assert same == 1.0 if exact else same >= 1 - 1e-4
+    assert_bit_exact(Lg, Lo, name)
 
 
 def test_regular_halfangle_brdf_vs_reference_golden(pg, merl_dir):
     """GPU RegularHalfangleBRDF against the reference harness's per-path radiance and film
-    (tests/scenes/merl.pbrt with the synthetic MERL table), same bounds as the other goldens."""
+    (tests/scenes/merl.pbrt with the synthetic MERL table), bit for bit."""
     from conftest import GOLDEN, merl_scene
     g = np.load(os.path.join(GOLDEN, "merl_paths_64x48s8.npz"))
     scene = merl_scene(pg, merl_dir, g["config"])
@@ -344,14 +326,9 @@ def test_regular_halfangle_brdf_vs_reference_golden(pg, merl_dir):
         L = d.trace_paths(g["keys"])
         d.render()
         film = d.film()
-    ref = g["L"]
-    same = np.all(L.view(np.int32) == ref.view(np.int32), axis=1)
-    rel = np.abs(L - ref).max(axis=1) / np.maximum(np.abs(ref).max(axis=1), 1e-30)
-    assert same.mean() >= 0.97
-    assert (rel > 1e-4).mean() <= 5e-4
-    assert np.abs(film - gf["film"]).max() / np.abs(gf["film"]).max() < 1e-4
-    Lo = pg.oracle().trace_paths(scene, g["keys"])
-    assert np.all(L.view(np.int32) == Lo.view(np.int32), axis=1).mean() >= 1 - 1e-4
+    assert_bit_exact(L, g["L"], "merl paths vs reference")
+    assert_bit_exact(film, gf["film"], "merl film vs reference")
+    assert_bit_exact(L, pg.oracle().trace_paths(scene, g["keys"]), "merl paths vs oracle")
 
 
 DL = ["killeroo_dl_%s_48x40s4", "bunny_dl_%s_48x27s4", "anim_dl_%s_40x40s4", "coverage_dl_%s_64x48s4",
@@ -373,16 +350,9 @@ def test_direct_lighting_vs_reference_golden(pg, base):
         L = d.trace_paths(g["keys"])
         d.render()
         film = d.film()
-    ref = g["L"]
-    same = np.all(L.view(np.int32) == ref.view(np.int32), axis=1)
-    rel = np.abs(L - ref).max(axis=1) / np.maximum(np.abs(ref).max(axis=1), 1e-30)
-    # last-ulp transcendental differences: coverage.pbrt samples three lights
-    # per vertex ("all"), so more of its paths meet one (path integrator there: 0.955)
-    assert same.mean() >= (0.90 if base.startswith("coverage") else 0.97), "bit-exact paths %d/%d" % (same.sum(), len(same))
-    assert (rel > 1e-4).mean() <= 5e-4
-    assert np.abs(film - gf["film"]).max() / np.abs(gf["film"]).max() < 1e-4
-    Lo = pg.oracle().trace_paths(scene, g["keys"])
-    assert np.all(L.view(np.int32) == Lo.view(np.int32), axis=1).mean() >= 1 - 1e-4
+    assert_bit_exact(L, g["L"], base % "paths")
+    assert_bit_exact(film, gf["film"], base % "film")
+    assert_bit_exact(L, pg.oracle().trace_paths(scene, g["keys"]), base + " vs oracle")
 
 
 @pytest.mark.parametrize("strategy,md", [("all", 6), ("one", 3)])
@@ -406,9 +376,7 @@ def test_direct_lighting_recursion_and_regeneration(pg, monkeypatch, strategy, m
         films = d.film()
     assert np.array_equal(L.view(np.int32), Ls.view(np.int32))
     assert np.array_equal(film.view(np.int32), films.view(np.int32))
-    Lo = pg.oracle().trace_paths(scene, keys)
-    assert np.all(L.view(np.int32) == Lo.view(np.int32), axis=1).mean() >= 1 - 1e-4
-    assert np.abs(L - Lo).max() / np.abs(Lo).max() < 1e-4
+    assert_bit_exact(L, pg.oracle().trace_paths(scene, keys), "paths vs oracle")
 
 
 def test_rng_sequence_matches_reference(pg):
@@ -434,8 +402,7 @@ def test_deep_paths_past_the_first_rng_block(pg, integ, md, strategy):
     with pg.Device(0) as d:
         d.upload(scene)
         L = d.trace_paths(keys)
-    Lo = pg.oracle().trace_paths(scene, keys)
-    assert np.all(L.view(np.int32) == Lo.view(np.int32), axis=1).mean() >= 1 - 1e-4
+    assert_bit_exact(L, pg.oracle().trace_paths(scene, keys), "paths vs oracle")
 
 
 @pytest.mark.parametrize("integ,strategy,md", [("directlighting", "all", 6), ("directlighting", "one", 4),
@@ -461,8 +428,7 @@ def test_independent_of_unwritten_state_and_slot_layout(pg, monkeypatch, integ, 
                 runs.append(d.trace_paths(keys))
     for r in runs[1:]:
         assert np.array_equal(r.view(np.int32), runs[0].view(np.int32))
-    Lo = pg.oracle().trace_paths(scene, keys)
-    assert np.all(runs[0].view(np.int32) == Lo.view(np.int32), axis=1).mean() >= 1 - 1e-4
+    assert_bit_exact(runs[0], pg.oracle().trace_paths(scene, keys), "paths vs oracle")
 
 
 @pytest.mark.parametrize("integ,strategy,md", [("directlighting", "all", 6), ("path", None, 5), ("path", None, 24)])
@@ -489,8 +455,7 @@ def test_drain_list_mode_is_exact(pg, monkeypatch, integ, strategy, md):
     for k, (film, paths) in out.items():
         assert np.array_equal(film.view(np.int32), ref[0].view(np.int32)), k
         assert np.array_equal(paths.view(np.int32), ref[1].view(np.int32)), k
-    Lo = pg.oracle().trace_paths(scene, keys)
-    assert np.all(ref[1].view(np.int32) == Lo.view(np.int32), axis=1).mean() >= 1 - 1e-4
+    assert_bit_exact(ref[1], pg.oracle().trace_paths(scene, keys), "paths vs oracle")
 
 
 META = ["metadata_material_%s_48x36s4", "metadata_mesh_%s_48x36s4", "metadata_depth_%s_48x36s4",
@@ -500,11 +465,8 @@ META = ["metadata_material_%s_48x36s4", "metadata_mesh_%s_48x36s4", "metadata_de
 @pytest.mark.parametrize("base", META)
 def test_metadata_vs_reference_golden(pg, base):
     """MetadataIntegrator on the GPU (metadata.h: one pass per camera sample) against the
-    reference harness and the oracle.  Hits (ids, depth = one sqrt of the hit distance) are bit
-    for bit; camera rays that miss into metadata.pbrt's environment light carry its Le, whose
-    direction mapping meets the last-ulp transcendental differences of DESIGN.md §3.2 (57 of
-    7,252 paths), so those are checked against the double-rounded oracle bit for bit and against
-    the reference to 1e-6."""
+    reference harness and the oracle, bit for bit: hits (ids, depth = one sqrt of the hit
+    distance) and camera rays that miss into metadata.pbrt's environment light (its Le)."""
     from conftest import GOLDEN
     from test_oracle_golden import meta_scene
     g = np.load(os.path.join(GOLDEN, base % "paths" + ".npz"))
@@ -515,17 +477,12 @@ def test_metadata_vs_reference_golden(pg, base):
         L = d.trace_paths(g["keys"])
         d.render()
         film = d.film()
-    ref = g["L"]
-    same = np.all(L.view(np.int32) == ref.view(np.int32), axis=1)
-    assert same.mean() >= 0.99
-    assert np.abs(L - ref).max() / np.abs(ref).max() < 1e-6
-    hit = np.all(ref == ref[:, :1], axis=1)    # flat spectra: ids and depths (misses: Le(env))
-    assert same[hit].all()
+    assert_bit_exact(L, g["L"], base % "paths")
+    assert_bit_exact(film, gf["film"], base % "film")
     o = pg.oracle()
-    assert np.array_equal(L.view(np.int32), o.trace_paths(scene, g["keys"]).view(np.int32))
-    assert np.abs(film - gf["film"]).max() / np.abs(gf["film"]).max() < 1e-6
+    assert_bit_exact(L, o.trace_paths(scene, g["keys"]), "paths vs oracle")
     of, _ = o.render(scene)
-    assert np.array_equal(film.view(np.int32), of.view(np.int32))
+    assert_bit_exact(film, of, "film vs oracle")
 
 
 SPEC = ["killeroo_spec32_%s_40x32s4", "coverage_spec3_%s_48x36s4", "coverage_specsampler8_%s_48x36s8",
@@ -548,19 +505,9 @@ def test_spectral_renderer_vs_reference_golden(pg, base):
         L = d.trace_paths(g["keys"])
         d.render()
         film = d.film()
-    ref = g["L"]
-    same = np.all(L.view(np.int32) == ref.view(np.int32), axis=1)
-    rel = np.abs(L - ref).max(axis=1) / np.maximum(np.abs(ref).max(axis=1), 1e-30)
-    # a singleDirection sample is nWaveBands paths: one last-ulp transcendental difference
-    #  in any of them shows in its row (measured: 0.970 - 1.0 bit-exact,
-    # tools/exact_rates.py; the oracle 1.0)
-    assert same.mean() >= 0.95, "bit-exact samples %d/%d" % (same.sum(), len(same))
-    assert (rel > 1e-4).mean() <= 5e-4
-    assert np.abs(film - gf["film"]).max() / np.abs(gf["film"]).max() < 1e-4
-    o = pg.oracle()
-    Lo = o.trace_paths(scene, g["keys"])
-    assert np.all(L.view(np.int32) == Lo.view(np.int32), axis=1).mean() >= 1 - 1e-4
-    assert np.abs(L - Lo).max() / np.abs(Lo).max() < 1e-4
+    assert_bit_exact(L, g["L"], base % "paths")
+    assert_bit_exact(film, gf["film"], base % "film")
+    assert_bit_exact(L, pg.oracle().trace_paths(scene, g["keys"]), base + " vs oracle")
 
 
 def test_spectral_renderer_lanes_batches_and_rejects(pg, monkeypatch):
@@ -584,8 +531,7 @@ def test_spectral_renderer_lanes_batches_and_rejects(pg, monkeypatch):
         films = d.film()
         assert np.array_equal(L.view(np.int32), Ls.view(np.int32))
         assert np.array_equal(film.view(np.int32), films.view(np.int32))
-        Lo = pg.oracle().trace_paths(scene, keys)
-        assert np.all(L.view(np.int32) == Lo.view(np.int32), axis=1).mean() >= 1 - 1e-3
+        assert_bit_exact(L, pg.oracle().trace_paths(scene, keys), "paths vs oracle")
         m = pg.Scene.load(os.path.join(PACKS, "metal.pack"), xres=8, yres=8, spp=1, renderer="spectral")
         assert m.flat.n_bands == 60 and m.flat.wave_bands == 32
         with pytest.raises(RuntimeError, match="past the spectrum"):
@@ -628,11 +574,9 @@ def test_realistic_diffraction_camera_vs_oracle(pg, monkeypatch, scene_file, kw)
     zero = ~np.any(Lo != 0, axis=1)
     assert 0.3 < zero.mean() < 0.8                       # blocked camera rays (and the GPU agrees)
     assert np.array_equal(zero, ~np.any(L != 0, axis=1))
-    same = np.all(L.view(np.int32) == Lo.view(np.int32), axis=1)
-    assert same.mean() >= 1 - 1e-3, "samples differing %d / %d" % ((~same).sum(), len(same))
-    assert np.abs(L - Lo).max() / np.abs(Lo).max() < 1e-4
+    assert_bit_exact(L, Lo, "paths vs oracle")
     of, _ = o.render(scene)
-    assert np.abs(film - of).max() / np.abs(of).max() < 1e-4
+    assert_bit_exact(film, of, "film vs oracle")
 
 
 @pytest.mark.parametrize("scene_file,kw", [
@@ -663,9 +607,9 @@ def test_light_field_and_eye_cameras_vs_oracle(pg, scene_file, kw):
     o = pg.oracle()
     Lo = o.trace_paths(scene, keys)
     assert np.any(Lo != 0)
-    assert np.array_equal(L.view(np.int32), Lo.view(np.int32))
+    assert_bit_exact(L, Lo, "paths vs oracle")
     of, _ = o.render(scene)
-    assert np.array_equal(film.view(np.int32), of.view(np.int32))
+    assert_bit_exact(film, of, "film vs oracle")
 
 
 @pytest.mark.parametrize("name", ["killeroo_rgb_paths_48x40s4", "killeroo_rgb_keys_c1_400x400s64"])
@@ -687,15 +631,10 @@ def test_rgb_build_vs_reference_golden(pg, name):
             d.upload(fs)
             d.render()
             film = d.film()
-    ref = g["L"]
-    same = np.all(L.view(np.int32) == ref.view(np.int32), axis=1)
-    rel = np.abs(L - ref).max(axis=1) / np.maximum(np.abs(ref).max(axis=1), 1e-30)
-    assert same.mean() >= 0.97, "bit-exact paths %d / %d" % (same.sum(), len(same))
-    assert (rel > 1e-4).mean() <= 5e-4
-    Lo = pg.oracle().trace_paths(scene, g["keys"])
-    assert np.all(L.view(np.int32) == Lo.view(np.int32), axis=1).mean() >= 1 - 1e-4
+    assert_bit_exact(L, g["L"], name)
+    assert_bit_exact(L, pg.oracle().trace_paths(scene, g["keys"]), name + " vs oracle")
     if film is not None:
-        assert np.abs(film - gf["film"]).max() / np.abs(gf["film"]).max() < 1e-4
+        assert_bit_exact(film, gf["film"], "killeroo_rgb_film_40x32s8")
 
 
 def test_integrator_scene_checks(pg):

@@ -7,7 +7,7 @@ import os
 import numpy as np
 import pytest
 
-from conftest import PACKS, REF_SCENES
+from conftest import PACKS, REF_SCENES, ROOT
 
 PACK = os.path.join(PACKS, "killeroo-simple.pack")
 
@@ -368,3 +368,24 @@ def test_rgb_build_front_end(pg):
     with pytest.raises(RuntimeError, match="RGB build"):
         pg.Scene.load(os.path.join(here, "coverage.pbrt"), bands=3)
     assert s.flat.n_lights == 1
+
+
+def test_gpupath_dat_fixture_vs_oracle(pg, tmp_path):
+    """tests/golden/coverage_gpupath_dat_40x32s4.npz -- the .dat the reference's own spectral film
+    wrote for tests/scenes/coverage.pbrt (the scene's path integrator, 40x32, 4 spp) -- against
+    pbrthost_write_dat of the oracle's film of the same render: payload bit for bit.  This pins the
+    fixture that tests/test_binding_gpu.py holds Renderer "gpupath" to on the GPU."""
+    from conftest import GOLDEN
+    g = np.load(os.path.join(GOLDEN, "coverage_gpupath_dat_40x32s4.npz"))
+    ref = g["dat"].tobytes()
+    W, H, spp = [int(v) for v in g["config"][:3]]
+    s = pg.Scene.load(os.path.join(ROOT, "scenes", "coverage.pack"), xres=W, yres=H, spp=spp, seed=0)
+    film, _ = pg.oracle(libm_float=True).render(s)
+    fn = str(tmp_path / "c.dat")
+    s.write_dat(fn, film)
+    mine = open(fn, "rb").read()
+    r1 = ref.index(b"\n") + 1
+    m1 = mine.index(b"\n") + 1
+    m2 = mine.index(b"\n", m1) + 1
+    assert ref[:r1] == mine[:m1] == b"%d %d %d\n" % (W, H, s.bands)
+    assert ref[r1:] == mine[m2:]

@@ -130,7 +130,7 @@ def test_gpu_bvh_paths(pg):
         d.upload(bvh)
         L1 = d.trace_paths(keys)
     Lo = pg.oracle().trace_paths(bvh, keys)
-    exact_o = np.all(L1.view(np.int32) == Lo.view(np.int32), axis=1)
-    assert exact_o.mean() >= 1 - 1e-4, "GPU vs oracle over the GPU BVH: %d/%d" % (exact_o.sum(), len(keys))
+    from conftest import assert_bit_exact
+    assert_bit_exact(L1, Lo, "GPU vs oracle over the GPU BVH")
     exact_r = np.all(L1.view(np.int32) == L0.view(np.int32), axis=1)
     assert exact_r.mean() >= 0.999, "GPU BVH vs reference BVH: %d/%d" % (exact_r.sum(), len(keys))

@@ -53,12 +53,15 @@ Fixtures (numpy .npz, inputs + expected outputs only):
                                   normal maps (image, scaled, constant)
   animcam_*                       tests/scenes/animcam.pbrt: an animated camera (AnimatedTransform
                                   CameraToWorld interpolated per ray, camera.cpp:84-103)
+  coverage_gpupath_dat_40x32s4.npz   the .dat the reference's own spectral film writes for
+                                  tests/scenes/coverage.pbrt (--refdat, the scene's integrator): the
+                                  end-to-end check of Renderer "gpupath" (tests/test_binding_gpu.py)
   <scene>_window_<cfg>_*.npz      film crops at the configs' REAL size and sample count: every
                                   sample of a one-pixel-larger window (--window), so each cropped
                                   pixel holds all of its contributions (incl. exact-boundary samples
                                   of its neighbours, spectralImage.cpp:77-152); C2 at the sphere
                                   light's edge and at a killeroo silhouette, C3-C5 at an edge each
-Usage: python tools/make_golden.py [--only keys|dat|merl|dl|meta|spec|rgb|b30|window|imagemap|animcam]
+Usage: python tools/make_golden.py [--only keys|dat|merl|dl|meta|spec|rgb|b30|window|imagemap|animcam|gpupath]
        (after `make -C oracle ref`, `ref60`, `ref30` and `refrgb`)
 """
 import os
@@ -310,6 +313,20 @@ def animcam_fixtures(tmp):
     film_fixture("animcam_film_64x48s4", (64, 48), 4, 0, 6, tmp, scene=sc)
 
 
+def gpupath_fixture(tmp):
+    """The .dat the reference's own spectral film (SpectralImageNoCameraFilm, --refdat) writes for
+    tests/scenes/coverage.pbrt rendered by the harness on the CPU (the scene's own integrator):
+    tests/test_binding_gpu.py renders the same film through Renderer "gpupath" on the GPU, which
+    hands its frame to that film class and lets its WriteImage write the file."""
+    cov = os.path.join(ROOT, "tests", "scenes", "coverage.pbrt")
+    fn = os.path.join(tmp, "gp.dat")
+    subprocess.run([HARNESS, cov, "--res", "40", "32", "--spp", "4", "--seed", "0", "--surf", "scene", "--refdat", fn],
+                   check=True, cwd=tmp)
+    np.savez_compressed(os.path.join(OUT, "coverage_gpupath_dat_40x32s4.npz"),
+                        dat=np.frombuffer(open(fn, "rb").read(), np.uint8), config=np.array([40, 32, 4, 0, -1], np.int32))
+    print("coverage_gpupath_dat_40x32s4")
+
+
 def main():
     if not os.path.exists(HARNESS):
         sys.exit("build the reference harness first: make -C oracle ref")
@@ -340,6 +357,8 @@ def main():
                 imagemap_fixtures(tmp)
             elif only == "animcam":
                 animcam_fixtures(tmp)
+            elif only == "gpupath":
+                gpupath_fixture(tmp)
             elif only == "window":
                 sel = sys.argv[3:]
                 for cfg in WINDOW_CONFIGS:
@@ -377,6 +396,7 @@ def main():
         merl_fixtures(tmp)
         imagemap_fixtures(tmp)
         animcam_fixtures(tmp)
+        gpupath_fixture(tmp)
         dl_fixtures(tmp)
         meta_fixtures(tmp)
         spec_fixtures(tmp)
