@@ -64,6 +64,7 @@ CONFIGS = {
 
 
 NODE4_BYTES = 128              # a node of the shadow queries' 4-wide BVH copy (4 child boxes + refs)
+NODE4Q_BYTES = 64              # a node of its quantized copy (k_trace_s4q: 8-bit child boxes + refs)
 
 
 def wide4_active(scene, kind):
@@ -73,7 +74,12 @@ def wide4_active(scene, kind):
     return scene.flat.n_instances == 0 and os.environ.get(var, "1") != "0"
 
 
-def trace_bytes(work, kernel, wide4=False):
+def shadow4q_active(scene):
+    """the shadow queries run on the quantized 4-wide copy (k_trace_s4q) with PBRTGPU_SHADOW4Q=1"""
+    return wide4_active(scene, "shadow") and os.environ.get("PBRTGPU_SHADOW4Q", "0") != "0"
+
+
+def trace_bytes(work, kernel, wide4=False, quant=False):
     """algorithmic bytes of a traversal kernel = every BVH node it visits
     (32 B; a 4-wide node 128 B, after the root box test of 32 B per ray), every primitive
     it tests (48 B pre-gathered triangle, 176 B quadric record), plus the ray it reads, the answer
@@ -83,8 +89,8 @@ def trace_bytes(work, kernel, wide4=False):
                  else NODE_BYTES * work["nodes_closest"])
         return (nodes + TRI_BYTES * work["tris_closest"]
                 + QUAD_BYTES * work["quads_closest"] + (RAY_BYTES + HIT_BYTES + QENTRY_BYTES) * work["rays"])
-    nodes = (NODE_BYTES * work["shadow_rays"] + NODE4_BYTES * (work["nodes_shadow"] - work["shadow_rays"]) if wide4
-             else NODE_BYTES * work["nodes_shadow"])
+    nodes = (NODE_BYTES * work["shadow_rays"] + (NODE4Q_BYTES if quant else NODE4_BYTES) * (work["nodes_shadow"] - work["shadow_rays"])
+             if wide4 else NODE_BYTES * work["nodes_shadow"])
     return (nodes + TRI_BYTES * work["tris_shadow"] + QUAD_BYTES * work["quads_shadow"]
             + (RAY_BYTES + 4 + QENTRY_BYTES) * work["shadow_rays"])
 
@@ -245,7 +251,7 @@ def exclusive_roofline(dev, scene, tiles, tile, frame_paths, cfg, pps=1):
     dev.render(tiles=tiles, tile=tile, count_work=True)
     work = dev.timing()["work"]
     byts = {"k_trace_closest": trace_bytes(work, "k_trace_closest", wide4_active(scene, "closest")),
-            "k_trace_shadow": trace_bytes(work, "k_trace_shadow", wide4_active(scene, "shadow")),
+            "k_trace_shadow": trace_bytes(work, "k_trace_shadow", wide4_active(scene, "shadow"), shadow4q_active(scene)),
             "k_shade": shade_bytes(work, frame_paths, scene.bands),
             "k_accum": accum_bytes(frame_paths / pps, scene.bands)}   # one row per camera sample
     traffic = {}

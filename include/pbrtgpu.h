@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define PBRTGPU_ABI_VERSION 12
+#define PBRTGPU_ABI_VERSION 14
 #define PBRTGPU_MAX_BANDS 64
 
 #define PBRTGPU_E_INVALID   (-1)
@@ -121,10 +121,16 @@ typedef struct pbrtgpu_texture {
 } pbrtgpu_texture;
 
 /* Material parameters.  A spectrum slot is either the constant spec[i] or, when
- * tex[i] >= 0, a spectrum texture evaluated per hit (at most one textured slot).  The bump
- * displacement is the constant f[7] or, when bump_tex >= 0, a float texture (Material::Bump,
- * material.cpp:39-81, is applied either way: bumpmap defaults to constant 0).
- * black_mask bit i: constant spec[i] IsBlack() (plastic/substrate/mirror skip such BxDFs). */
+ * tex[i] >= 0, a spectrum texture evaluated per hit (at most two textured slots per material,
+ * the most any reference material has: plastic / substrate Kd, Ks; glass Kr, Kt; metal eta, k).
+ * The float parameters f[0], f[1] (matte sigma; plastic / metal roughness; substrate u / v
+ * roughness; glass index) are the constants or, when ftex[j] >= 0, float textures evaluated per
+ * hit (matte clamps sigma to [0, 90] as matte.cpp:54 does).  The bump displacement is the
+ * constant f[7] or, when bump_tex >= 0, a float texture (Material::Bump, material.cpp:39-81, is
+ * applied either way: bumpmap defaults to constant 0).
+ * black_mask bit i: constant spec[i] IsBlack() (plastic/substrate/mirror skip such BxDFs);
+ * bit 4 + i: textured slot i is used as evaluated, without the .Clamp() of the other materials
+ * (metal eta and k, metal.cpp:64-65). */
 typedef struct pbrtgpu_material {
     int32_t type;
     int32_t spec[4];      /* offsets (in floats) into spectra[] */
@@ -135,7 +141,7 @@ typedef struct pbrtgpu_material {
     int32_t black_mask;
     int32_t normal_tex;   /* "normalmap" spectrum texture (Material::NormalMap, material.cpp:82-126, used
                            * where its value is not black), or -1 (the constant-0 default) */
-    int32_t pad[2];
+    int32_t ftex[2];      /* float texture of f[0], f[1], or -1 (ABI 13; packs before v14 hold -1) */
 } pbrtgpu_material;
 
 enum { PBRTGPU_LIGHT_AREA = 0, PBRTGPU_LIGHT_POINT = 1, PBRTGPU_LIGHT_INFINITE = 2 };
@@ -150,15 +156,20 @@ typedef struct pbrtgpu_light {
     int32_t is_black;      /* emitted spectrum IsBlack() */
     int32_t n_samples;     /* Light::nSamples = max(1, "nsamples") (light.h:45); DirectLighting's
                             * strategy "all" takes RoundUpPow2 of it (LDSampler::RoundSize) */
-    int32_t pad[2];
+    int32_t map_tex;       /* infinite, decoded environment image: its radiance MIPMap (an IMAGE
+                            * texture of textures[], RGB, MIPMap defaults), or -1: the one texel below */
+    int32_t dist_off;      /* infinite with map_tex: its Distribution2D in texels[] (infinite.cpp:93-109,
+                            * montecarlo.h:134-160, montecarlo.cpp:350-362): marginal {funcInt,
+                            * func[nv], cdf[nv + 1]}, then per row v {funcInt, func[nu], cdf[nu + 1]} */
     float l2w_m[16];
     float l2w_minv[16];
-    /* infinite (InfiniteAreaLight, lights/infinite.cpp): the radiance MIPMap's single texel
-     * (RGB, after L.ToRGBSpectrum()) with its wrap mode; Distribution2D of the one-texel
-     * image: map_pdf = SampleContinuous's pdf, dist_pdf = Distribution2D::Pdf */
+    /* infinite (InfiniteAreaLight, lights/infinite.cpp) without map_tex: the radiance MIPMap's
+     * single texel (RGB, after L.ToRGBSpectrum()) with its wrap mode; Distribution2D of the
+     * one-texel image: map_pdf = SampleContinuous's pdf, dist_pdf = Distribution2D::Pdf.  With
+     * map_tex: dist_nu x dist_nv, the image's own resolution (before the MIPMap's resampling). */
     float texel[3];
     float map_pdf, dist_pdf;
-    int32_t wrap, pad2[2];
+    int32_t wrap, dist_nu, dist_nv;
 } pbrtgpu_light;
 
 typedef struct pbrtgpu_light_shape {

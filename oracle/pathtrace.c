@@ -742,7 +742,8 @@ typedef struct {
     V nn, ng, sn, tn;
     int n;
     BxDF bx[4];
-    float texbuf[MAXB];   /* a textured reflectance evaluated at this hit */
+    float texbuf[2][MAXB];   /* the material's textured spectra evaluated at this hit (slots 0, 1) */
+    float eta;               /* BSDF::eta: the glass material's index, 1 otherwise (glass.cpp:47-48) */
 } BSDF;
 static inline int matches(const BxDF *b, int flags) { return (b->type & flags) == b->type; }
 static inline V to_local(const BSDF *b, V v) { return v3(vdot(v, b->sn), vdot(v, b->tn), vdot(v, b->nn)); }
@@ -1156,10 +1157,12 @@ static inline float LOGF(float x) { return libmf_logf(x); }
 /* Log2 (pbrt.h:243-246) */
 static inline float log2_(float x) { float invLog2 = 1.f / LOGF(2.f); return LOGF(x) * invLog2; }
 
-/* SampledSpectrum::FromRGB (spectrum.cpp:93-178), basis tables from the flattened scene */
+/* SampledSpectrum::FromRGB (spectrum.cpp:93-178), basis tables from the flattened scene; the RGB
+ * build's RGBSpectrum::FromRGB is the triple itself */
 static void add_scaled(float *r, int nb, float a, const float *B) { for (int i = 0; i < nb; ++i) r[i] += B[i] * a; }
 static void from_rgb(const Ctx *c, const float rgb[3], int illum, float *r) {
     int nb = c->nb;
+    if (nb == 3) { r[0] = rgb[0]; r[1] = rgb[1]; r[2] = rgb[2]; return; }   /* RGBSpectrum::FromRGB (spectrum.h:463-470) */
     const float *base = c->s->rgb_basis + (size_t)(illum ? 7 : 0) * nb;
     const float *W = base, *Cy = base + nb, *Mg = base + 2 * nb, *Ye = base + 3 * nb, *Rd = base + 4 * nb,
                 *Gr = base + 5 * nb, *Bl = base + 6 * nb;
@@ -1491,26 +1494,40 @@ static void get_bsdf(const Ctx *c, const Isect *is, const float diff[4], BSDF *b
     bs->tn = vcross(bs->nn, bs->sn);
     bs->n = 0;
     *dgsOut = b;
-    /* material spectra: constants, or the one textured slot evaluated here (.Clamp()) */
-    const float *K[4];
-    int black[4];
-    for (int k = 0; k < 4; ++k) {
+    /* material spectra (slots 0, 1): constants, or textures evaluated here -- .Clamp()ed, except
+       metal's eta and k (metal.cpp:64-65: Evaluate(dgs) as is; black_mask bit 4 + k) */
+    const float *K[2];
+    int black[2];
+    for (int k = 0; k < 2; ++k) {
         if (mt->tex[k] >= 0) {
-            tex_spec(c, mt->tex[k], &q, bs->texbuf);
-            for (int i = 0; i < c->nb; ++i) bs->texbuf[i] = clampf(bs->texbuf[i], 0.f, INFINITY);
-            K[k] = bs->texbuf;
-            black[k] = spec_black(c, bs->texbuf);
+            tex_spec(c, mt->tex[k], &q, bs->texbuf[k]);
+            if (!((mt->black_mask >> (4 + k)) & 1))
+                for (int i = 0; i < c->nb; ++i) bs->texbuf[k][i] = clampf(bs->texbuf[k][i], 0.f, INFINITY);
+            K[k] = bs->texbuf[k];
+            black[k] = spec_black(c, bs->texbuf[k]);
         } else {
             K[k] = mt->spec[k] >= 0 ? SPEC(c, mt->spec[k]) : NULL;
             black[k] = (mt->black_mask >> k) & 1;
         }
     }
+    /* float parameters f[0], f[1]: constants or float textures at the shading geometry (matte's
+       sigma clamped to [0, 90], matte.cpp:54; plastic / metal roughness, substrate u / v roughness,
+       glass index: Evaluate(dgs) as is) */
+    float fp[2];
+    for (int j = 0; j < 2; ++j) {
+        fp[j] = mt->f[j];
+        if (mt->ftex[j] >= 0) {
+            fp[j] = tex_float(c, mt->ftex[j], &q);
+            if (mt->type == PBRTGPU_MAT_MATTE) fp[j] = clampf(fp[j], 0.f, 90.f);
+        }
+    }
+    bs->eta = mt->type == PBRTGPU_MAT_GLASS ? fp[0] : 1.f;
     switch (mt->type) {
         case PBRTGPU_MAT_MATTE: {
             BxDF *x = &bs->bx[bs->n++];
             x->R = K[0];
             x->type = BSDF_REFLECTION | BSDF_DIFFUSE;
-            float sig = mt->f[0];
+            float sig = fp[0];
             if (sig == 0.) x->kind = BX_LAMBERT;
             else {
                 x->kind = BX_OREN;
@@ -1526,7 +1543,7 @@ static void get_bsdf(const Ctx *c, const Isect *is, const float diff[4], BSDF *b
             x->kind = BX_LAMBERT; x->type = BSDF_REFLECTION | BSDF_DIFFUSE; x->R = K[0];
             x = &bs->bx[bs->n++];
             x->kind = BX_MICRO_BLINN_DIEL; x->type = BSDF_REFLECTION | BSDF_GLOSSY; x->R = K[1];
-            float e = 1.f / mt->f[0];
+            float e = 1.f / fp[0];
             if (e > 10000.f || isnan(e)) e = 10000.f;   /* Blinn ctor */
             x->a = e; x->eta_i = 1.5f; x->eta_t = 1.f;
             break;
@@ -1535,7 +1552,7 @@ static void get_bsdf(const Ctx *c, const Isect *is, const float diff[4], BSDF *b
             BxDF *x = &bs->bx[bs->n++];
             x->kind = BX_MICRO_BLINN_COND; x->type = BSDF_REFLECTION | BSDF_GLOSSY;
             x->eta = K[0]; x->k = K[1];
-            float e = 1.f / mt->f[0];
+            float e = 1.f / fp[0];
             if (e > 10000.f || isnan(e)) e = 10000.f;
             x->a = e;
             break;
@@ -1550,11 +1567,11 @@ static void get_bsdf(const Ctx *c, const Isect *is, const float diff[4], BSDF *b
         case PBRTGPU_MAT_GLASS: {   /* glass.cpp:34-57 */
             if (!black[0]) {
                 BxDF *x = &bs->bx[bs->n++];
-                x->kind = BX_SPEC_REFL_DIEL; x->type = BSDF_REFLECTION | BSDF_SPECULAR; x->R = K[0]; x->eta_t = mt->f[0];
+                x->kind = BX_SPEC_REFL_DIEL; x->type = BSDF_REFLECTION | BSDF_SPECULAR; x->R = K[0]; x->eta_t = fp[0];
             }
             if (!black[1]) {
                 BxDF *x = &bs->bx[bs->n++];
-                x->kind = BX_SPEC_TRANS; x->type = BSDF_TRANSMISSION | BSDF_SPECULAR; x->R = K[1]; x->eta_t = mt->f[0];
+                x->kind = BX_SPEC_TRANS; x->type = BSDF_TRANSMISSION | BSDF_SPECULAR; x->R = K[1]; x->eta_t = fp[0];
             }
             break;
         }
@@ -1575,7 +1592,7 @@ static void get_bsdf(const Ctx *c, const Isect *is, const float diff[4], BSDF *b
             BxDF *x = &bs->bx[bs->n++];
             x->kind = BX_FRESNEL_BLEND_ANISO; x->type = BSDF_REFLECTION | BSDF_GLOSSY;
             x->R = K[0]; x->R2 = K[1];
-            float ex = 1.f / mt->f[0], ey = 1.f / mt->f[1];
+            float ex = 1.f / fp[0], ey = 1.f / fp[1];
             if (ex > 10000.f || isnan(ex)) ex = 10000.f;
             if (ey > 10000.f || isnan(ey)) ey = 10000.f;
             x->a = ex; x->b = ey;
@@ -1673,13 +1690,50 @@ static int sample_discrete(const pbrtgpu_light_shape *ls, int n, float u) {
     return off < 0 ? 0 : off;
 }
 typedef struct { V o, d; float mint, maxt; } Seg;
-/* InfiniteAreaLight (lights/infinite.cpp) with its one-texel radiance map */
+/* InfiniteAreaLight (lights/infinite.cpp): a one-texel radiance map, or a decoded image's MIPMap
+   (map_tex) with its Distribution2D (in the texel pool from dist_off) */
 static inline float spherical_theta(V v) { return ACOSF(clampf(v.z, -1.f, 1.f)); }   /* geometry.h:642-650 */
 static inline float spherical_phi(V v) { float p = ATAN2F(v.y, v.x); return (p < 0.f) ? p + 2.f * PI_F : p; }
 static void inf_radiance(const Ctx *c, const pbrtgpu_light *L, float s, float t, float *out) {
     float rgb[3];
-    mip_triangle(L->texel, 3, L->wrap, s, t, rgb);   /* MIPMap::Lookup(s, t), width 0 */
+    if (L->map_tex >= 0) mip_lookup_w(c, &c->s->textures[L->map_tex], 3, s, t, 0.f, rgb);   /* MIPMap::Lookup(s, t) */
+    else mip_triangle(L->texel, 3, L->wrap, s, t, rgb);   /* MIPMap::Lookup(s, t), width 0 */
     from_rgb(c, rgb, 1, out);                          /* Spectrum(rgb, SPECTRUM_ILLUMINANT) */
+}
+/* Distribution1D::SampleContinuous (montecarlo.h:68-84) of {funcInt, func[n], cdf[n + 1]} */
+static float dist1d_sample(const float *D, int n, float u, float *pdf, int *off) {
+    const float *cdf = D + 1 + n;
+    int lo = 0, count = n + 1;   /* std::upper_bound(cdf, cdf + n + 1, u) */
+    while (count > 0) {
+        int step = count / 2, it = lo + step;
+        if (!(u < cdf[it])) { lo = it + 1; count -= step + 1; }
+        else count = step;
+    }
+    int offset = lo - 1 > 0 ? lo - 1 : 0;
+    *off = offset;
+    float du = (u - cdf[offset]) / (cdf[offset + 1] - cdf[offset]);
+    *pdf = D[1 + offset] / D[0];
+    return (offset + du) / n;
+}
+/* Distribution2D::SampleContinuous / Pdf (montecarlo.h:137-152) */
+static void dist2d_sample(const Ctx *c, const pbrtgpu_light *L, float u0, float u1, float uv[2], float *pdf) {
+    const int nu = L->dist_nu, nv = L->dist_nv;
+    const float *M = c->s->texels + L->dist_off;
+    float pdfs[2];
+    int v, o;
+    uv[1] = dist1d_sample(M, nv, u1, &pdfs[1], &v);
+    uv[0] = dist1d_sample(M + (2 + 2 * nv) + (size_t)v * (2 + 2 * nu), nu, u0, &pdfs[0], &o);
+    *pdf = pdfs[0] * pdfs[1];
+}
+static float dist2d_pdf(const Ctx *c, const pbrtgpu_light *L, float u, float v) {
+    const int nu = L->dist_nu, nv = L->dist_nv;
+    const float *M = c->s->texels + L->dist_off;
+    int iu = (int)(u * nu), iv = (int)(v * nv);   /* Clamp(Float2Int(.), 0, count - 1) */
+    iu = iu < 0 ? 0 : (iu > nu - 1 ? nu - 1 : iu);
+    iv = iv < 0 ? 0 : (iv > nv - 1 ? nv - 1 : iv);
+    const float *R = M + (2 + 2 * nv) + (size_t)iv * (2 + 2 * nu);
+    if (R[0] * M[0] == 0.f) return 0.f;
+    return (R[1 + iu] * M[1 + iv]) / (R[0] * M[0]);
 }
 /* InfiniteAreaLight::Le (infinite.cpp:84-89) */
 static void inf_Le(const Ctx *c, const pbrtgpu_light *L, V d, float *out) {
@@ -1687,12 +1741,13 @@ static void inf_Le(const Ctx *c, const pbrtgpu_light *L, V d, float *out) {
     inf_radiance(c, L, spherical_phi(wh) * INV_TWOPI_F, spherical_theta(wh) * INV_PI_F, out);
 }
 /* InfiniteAreaLight::Pdf (infinite.cpp:188-197); Distribution2D::Pdf of one texel is dist_pdf */
-static float inf_pdf(const pbrtgpu_light *L, V w) {
+static float inf_pdf(const Ctx *c, const pbrtgpu_light *L, V w) {
     V wi = xvec(L->l2w_minv, w);
     float theta = spherical_theta(wi);
     float sintheta = SINF(theta);
     if (sintheta == 0.f) return 0.f;
-    return L->dist_pdf / (2.f * PI_F * PI_F * sintheta);
+    float dp = L->map_tex >= 0 ? dist2d_pdf(c, L, spherical_phi(wi) * INV_TWOPI_F, theta * INV_PI_F) : L->dist_pdf;
+    return dp / (2.f * PI_F * PI_F * sintheta);
 }
 /* Light::Sample_L (diffuse.cpp:61-74, point.cpp:42-49, infinite.cpp:155-185); returns Li into Li[] */
 static void light_sample_L(const Ctx *c, const pbrtgpu_light *L, V p, float pEps, const float u[3], float time,
@@ -1701,8 +1756,13 @@ static void light_sample_L(const Ctx *c, const pbrtgpu_light *L, V p, float pEps
     const float *Ls = SPEC(c, L->spec);
     (void)time;
     if (L->type == PBRTGPU_LIGHT_INFINITE) {
-        /* Distribution2D::SampleContinuous of one texel returns (u0, u1) with pdf map_pdf */
+        /* Distribution2D::SampleContinuous; of one texel it returns (u0, u1) with pdf map_pdf */
         float uv0 = u[0], uv1 = u[1], mapPdf = L->map_pdf;
+        if (L->map_tex >= 0) {
+            float uv[2];
+            dist2d_sample(c, L, u[0], u[1], uv, &mapPdf);
+            uv0 = uv[0]; uv1 = uv[1];
+        }
         if (mapPdf == 0.f) { *pdf = 0.f; for (int i = 0; i < nb; ++i) Li[i] = 0.f; return; }
         float theta = uv1 * PI_F, phi = uv0 * 2.f * PI_F;
         float costheta = COSF(theta), sintheta = SINF(theta);
@@ -1755,7 +1815,7 @@ static void light_sample_L(const Ctx *c, const pbrtgpu_light *L, V p, float pEps
 }
 static float light_pdf(const Ctx *c, const pbrtgpu_light *L, V p, V wi) {
     if (L->type == PBRTGPU_LIGHT_POINT) return 0.;
-    if (L->type == PBRTGPU_LIGHT_INFINITE) return inf_pdf(L, wi);
+    if (L->type == PBRTGPU_LIGHT_INFINITE) return inf_pdf(c, L, wi);
     const pbrtgpu_light_shape *shs = c->s->light_shapes + L->shape_offset;
     float pp = 0.f;
     for (int i = 0; i < L->n_shapes; ++i) pp += shs[i].area * shape_pdf(c, shs[i].shape_type, shs[i].shape_index, p, wi);
@@ -2008,8 +2068,7 @@ static void dl_radiance(const Ctx *c, Ray ray, const RayDiff *rd, int depth, Pat
         }
     }
     if (depth + 1 < c->s->max_depth) {
-        const pbrtgpu_material *mt = &c->s->materials[c->s->prims[is.prim].material];
-        float bsdfEta = mt->type == PBRTGPU_MAT_GLASS ? mt->f[0] : 1.f;   /* BSDF::eta (glass.cpp:48) */
+        float bsdfEta = bs.eta;   /* BSDF::eta (glass.cpp:47-48) */
         for (int pass = 0; pass < 2; ++pass) {   /* SpecularReflect, then SpecularTransmit */
             float u0 = rng_float(&ps->rng), u1 = rng_float(&ps->rng), uc = rng_float(&ps->rng);   /* BSDFSample(rng) */
             int flags = BSDF_SPECULAR | (pass ? BSDF_TRANSMISSION : BSDF_REFLECTION), st;
@@ -2407,8 +2466,16 @@ static float lens_ray(const Ctx *c, float imageX, float imageY, float lensU, flo
     /* Sample::time = Lerp(u, open, close) (LDPixelSample, montecarlo.cpp:229), lerped again by the camera
      * (perspective.cpp:67, 102; realisticDiffraction.cpp:1157) */
     r.time = lerpf(lerpf(timeU, cam->shutter_open, cam->shutter_close), cam->shutter_open, cam->shutter_close);
-    out->o = xpoint(cam->cam2world_m, r.o);
-    out->d = vnorm(xvec(cam->cam2world_m, r.d));
+    /* CameraToWorld(*ray, ray) at the ray's time (realisticDiffraction.cpp:1158): the static
+     * matrix, or the animated camera's start / end transform or Interpolate */
+    float cwb[16];
+    const float *cw = cam->cam2world_m;
+    if (c->s->camera_motion) {
+        inst_interp(c->s->camera_motion, r.time, cwb, NULL);
+        cw = cwb;
+    }
+    out->o = xpoint(cw, r.o);
+    out->d = vnorm(xvec(cw, r.d));
     out->mint = r.mint; out->maxt = r.maxt; out->time = r.time;
     return 1.f;
 }

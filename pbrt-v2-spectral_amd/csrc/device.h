@@ -314,6 +314,8 @@ struct DevScene {
     int nTop;                         // wide nodes [0, nTop): the BVH's top levels, breadth-first (LDS in k_trace_pt)
     const float4 *w4nodes;            // 4-wide copy for the shadow queries (wide4_bvh): 8 x float4 per node
     int w4N, w4Stack;                 // its nodes (0: none) and the any-hit stack bound (3 per level + 1)
+    const uint4 *w4q;                 // its quantized copy (scene_build.h quant_w4): 4 x uint4 per node, or null
+    const int *leafOf;                // per first primitive of a leaf: the binary leaf node (quant_w4)
     const pbrtgpu_prim *prims;
     const DevTri *primTri;            // per prim (triangles only meaningful)
     const pbrtgpu_triangle *tris;
@@ -1075,6 +1077,87 @@ PGD_INLINE bool bvh_intersectP4(const DevScene &S, Stack &st, const Ray &ray0) {
     }
     return false;
 }
+// ---- the quantized 4-wide copy (scene_build.h quant_w4) for the shadow queries
+// the stack entries of a quantized walk carry a "certain" bit: every box on the path to them passed
+// its inner (contained) test, so the reference's exact walk reaches them too
+enum : uint32_t { WQ_CERT = 0x40000000u };
+// slot k's boxes of a quantized node: outer (containing the exact box) and inner (contained in it;
+// empty -- lo > hi -- where the quantization has no step inside)
+PGD_INLINE void wq_boxes(const uint4 &q0, const uint4 &q1, const uint4 &q2, const uint4 &q3, int k, float4 *olo,
+                         float4 *ohi, float4 *ilo, float4 *ihi) {
+    const uint32_t pk[6] = {q1.x, q1.y, q1.z, q1.w, q2.x, q2.y};
+    const float o[3] = {__uint_as_float(q0.x), __uint_as_float(q0.y), __uint_as_float(q0.z)};
+    float lo[3], hi[3], li[3], hj[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const float sc = __uint_as_float(((q0.w >> (8 * a)) & 0xffu) << 23);   // 2^e
+        const int bl = 6 * k + a, bh = 6 * k + 3 + a;
+        const uint32_t ql = (pk[bl >> 2] >> (8 * (bl & 3))) & 0xffu, qh = (pk[bh >> 2] >> (8 * (bh & 3))) & 0xffu;
+        const uint32_t el = (q3.z >> bl) & 1u, eh = (q3.z >> bh) & 1u;
+        lo[a] = o[a] + (float)ql * sc;
+        hi[a] = o[a] + (float)qh * sc;
+        li[a] = el ? lo[a] : o[a] + (float)(ql + 1u) * sc;
+        hj[a] = eh ? hi[a] : o[a] + (float)(qh - 1u) * sc;   // qh >= 1 wherever it is not exact (qh = 0 is exact)
+    }
+    *olo = make_float4(lo[0], lo[1], lo[2], 0.f);
+    *ohi = make_float4(hi[0], hi[1], hi[2], 0.f);
+    *ilo = make_float4(li[0], li[1], li[2], 0.f);
+    *ihi = make_float4(hj[0], hj[1], hj[2], 0.f);
+}
+// BBox::IntersectP of the exact boxes of binary leaf `leaf`'s ancestors and itself, from the root
+// (the nodes the reference's IntersectP tests on its way to the leaf: bvh.cpp:435-481), found by
+// descending the depth-first node order (the right child of node i is nodes[i].offset, every node
+// of i's left subtree below it)
+PGD_INLINE bool leaf_reached(const DevScene &S, const Ray &ray, V invDir, const int neg[3], int leaf) {
+    int i = 0;
+    for (;;) {
+        const float4 n0 = (*sa(S.nodes, (uint32_t)(2 * i))), n1 = (*sa(S.nodes, (uint32_t)(2 * i + 1)));
+        if (!bbox_hit(n0, n1, ray, invDir, neg)) return false;
+        if (i == leaf) return true;
+        if (__float_as_uint(n1.w) & 0xffu) return false;   // another leaf: not an ancestor (corrupt leafOf)
+        const int right = (int)__float_as_uint(n1.z);
+        i = leaf >= right ? right : i + 1;
+    }
+}
+// The shadow query on the quantized copy as one plain walk (host replay and tests; the GPU runs
+// k_trace_s4q): outer boxes to descend, inner boxes to keep the "certain" bit, an uncertain leaf's
+// hit confirmed by leaf_reached.  Same answer as bvh_intersectP (quant_w4).
+PGD_INLINE bool bvh_intersectP4q(const DevScene &S, Stack &st, const Ray &ray0) {
+    Ray ray = ray0;
+    const V invDir = v3(1.f / ray.d.x, 1.f / ray.d.y, 1.f / ray.d.z);
+    const int neg[3] = {invDir.x < 0, invDir.y < 0, invDir.z < 0};
+    if (!bbox_hit((*sa(S.nodes, 0u)), (*sa(S.nodes, 1u)), ray, invDir, neg)) return false;
+    int todo = 0, prim = -1;
+    float thit = INFINITY;
+    st.set(todo++, 0u | WQ_CERT);   // the root box passed its exact test
+    while (todo > 0) {
+        const uint32_t e = st.get(--todo), ref = e & ~WQ_CERT;
+        const bool cert = (e & WQ_CERT) != 0;
+        if (ref & WREF_LEAF) {
+            const uint32_t np = (ref >> WREF_NP_SHIFT) & 0x3fu, off = ref & WREF_OFF_MASK;
+            for (uint32_t i = 0; i < np; ++i)
+                if (prim_test<true, false>(S, st, todo, (int)(off + i), ray, &prim, &thit)) {
+                    if (cert || leaf_reached(S, ray, invDir, neg, (*sa(S.leafOf, off)))) return true;
+                    break;   // the reference never tests this leaf
+                }
+            continue;
+        }
+        const uint4 *q = sa(S.w4q, (uint32_t)(4 * (size_t)ref));
+        const uint4 q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3];
+        const uint32_t refs[4] = {q2.z, q2.w, q3.x, q3.y};
+        for (int k = 0; k < 4; ++k) {
+            if (refs[k] == 0xffffffffu) continue;
+            float4 olo, ohi, ilo, ihi;
+            wq_boxes(q0, q1, q2, q3, k, &olo, &ohi, &ilo, &ihi);
+            float t = 0.f, ti = 0.f;
+            if (slab_enter(olo, ohi, ray, invDir, neg, &t) && t < ray.maxt) {
+                const bool c = cert && slab_enter(ilo, ihi, ray, invDir, neg, &ti) && ti < ray.maxt;
+                st.set(todo++, refs[k] | (c ? WQ_CERT : 0u));
+            }
+        }
+    }
+    return false;
+}
 // im: the path's instance transforms (PathSoA::instM, per instance 8 float4: world->primitive
 // m rows, then its inverse), or null in scenes without instances
 struct Isect { DG dg; float rayEps; int prim; int inst; float time; const float4 *im; };
@@ -1145,7 +1228,9 @@ enum { BX_LAMBERT, BX_OREN, BX_MICRO_BLINN_DIEL, BX_SPEC_REFL_NOOP, BX_FRESNEL_B
        BX_MEASURED_HALF };                                        // RegularHalfangleBRDF: R = first texel
 // R, R2: offsets into DevScene::spectra, or -1 for the per-slot textured spectrum (K bands)
 struct BxDF { int kind, type; int R, R2; float a, b; };
-struct BSDF { V nn, ng, sn, tn; int n; BxDF bx[2]; };
+// eta: BSDF::eta, the glass material's index (glass.cpp:47-48), 1 otherwise (DirectLighting's
+// SpecularTransmit differentials read it, integrator.cpp:219-247)
+struct BSDF { V nn, ng, sn, tn; int n; BxDF bx[2]; float eta; };
 PGD_INLINE bool matches(const BxDF &b, int flags) { return (b.type & flags) == b.type; }
 PGD_INLINE V to_local(const BSDF &b, V v) { return v3(vdot(v, b.sn), vdot(v, b.tn), vdot(v, b.nn)); }
 PGD_INLINE V to_world(const BSDF &b, V v) {
@@ -1586,12 +1671,15 @@ PGD_INLINE void bsdf_sample_specular(const BSDF &bs, V woW, V *wiW, float uc, fl
 // ------------------------------------------------------------------ RGB spectra and textures
 // SampledSpectrum::FromRGB (spectrum.cpp:93-178) for band quad q: the branch picks three basis
 // spectra and weights; every band is r = ((0 + B0*a0) + B1*a1) + B2*a2, then *0.94 / *0.86445
-// and Clamp(0, inf), exactly the reference's per-band operation sequence
+// and Clamp(0, inf), exactly the reference's per-band operation sequence.  The RGB build
+// (S.nb == 3) is RGBSpectrum::FromRGB (rgb.h): the triple itself, no basis, scale or clamp (k0 < 0)
 struct RGBPick { int k0, k1, k2; float a0, a1, a2; };
-PGD_INLINE RGBPick rgb_pick(const float rgb[3]) {
+PGD_INLINE RGBPick rgb_pick(const DevScene &S, const float rgb[3]) {
     enum { W = 0, Cy, Mg, Ye, Rd, Gr, Bl };
     RGBPick p;
-    if (rgb[0] <= rgb[1] && rgb[0] <= rgb[2]) {
+    if (S.nb == 3) {
+        p.k0 = p.k1 = p.k2 = -1; p.a0 = rgb[0]; p.a1 = rgb[1]; p.a2 = rgb[2];
+    } else if (rgb[0] <= rgb[1] && rgb[0] <= rgb[2]) {
         p.k0 = W; p.a0 = rgb[0];
         if (rgb[1] <= rgb[2]) { p.k1 = Cy; p.a1 = rgb[1] - rgb[0]; p.k2 = Bl; p.a2 = rgb[2] - rgb[1]; }
         else { p.k1 = Cy; p.a1 = rgb[2] - rgb[0]; p.k2 = Gr; p.a2 = rgb[1] - rgb[2]; }
@@ -1607,6 +1695,7 @@ PGD_INLINE RGBPick rgb_pick(const float rgb[3]) {
     return p;
 }
 PGD_INLINE float4 from_rgb4(const DevScene &S, const RGBPick &p, bool illum, int q) {
+    if (p.k0 < 0) return make_float4(p.a0, p.a1, p.a2, 0.f);
     const float *b = sa(S.basis, (uint32_t)((illum ? 7 : 0) * S.nbp + 4 * q));
     const float4 x = *reinterpret_cast<const float4 *>(b + p.k0 * S.nbp);
     const float4 y = *reinterpret_cast<const float4 *>(b + p.k1 * S.nbp);
@@ -1822,7 +1911,7 @@ PGD_HEAVY SpecTex tex_spec_prepare(const DevScene &S, int id, const TexPt &q) {
     }
     float rgb[3];
     tex_image<3>(S, (*sa(S.tex, (uint32_t)(img))), q, rgb);
-    r.pick = rgb_pick(rgb);
+    r.pick = rgb_pick(S, rgb);
     return r;
 }
 PGD_INLINE float4 tex_spec4(const DevScene &S, const SpecTex &t, int q) {
@@ -1911,8 +2000,9 @@ PGD_HEAVY void compute_differentials(const DG &dg, const RayDiff &rd, float out[
 
 // Intersection::GetBSDF -> GetShadingGeometry -> Material::GetBSDF (+ Bump, material.cpp:39-81)
 // diff: dudx, dvdx, dudy, dvdy of the hit (zero without ray differentials); the material's
-// textured spectrum, if any, is written clamped into the slot's K bands (kb[q * c]) and its
-// BxDF refers to it with offset -1
+// textured spectra (at most two) are evaluated in slot order into the slot's K band buffers j = 0,
+// 1 (kb[(j * NQ + q) * c], clamped unless the material uses them raw) and its BxDFs refer to
+// buffer j with offset -1 - j * NQ (spec4)
 // dnOut (optional): dndu, dndv of the shading geometry (SpecularReflect / SpecularTransmit ray
 // differentials, integrator.cpp:190-192)
 template <int FEAT>
@@ -1976,41 +2066,58 @@ PGD_HEAVY void get_bsdf(const DevScene &S, const Isect &is, const float diff[4],
     *pOut = dgs.p;
     *nOut = nn;
     if (dnOut) { dnOut[0] = dgs.dndu; dnOut[1] = dgs.dndv; }
-    // material spectra: constant offsets, or the textured slot materialised in K
-    int off[4];
+    // material spectra: constant offsets, or the textured slots materialised in K (every material's
+    // spectrum parameters are slots 0 and 1)
+    int off[2];
     bool black0 = (mt.black_mask & 1) != 0, black1 = (mt.black_mask & 2) != 0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) off[k] = mt.spec[k];
-    int ts = -1;
+    off[0] = mt.spec[0];
+    off[1] = mt.spec[1];
+    float fp0 = mt.f[0], fp1 = mt.f[1];
     if (FEAT & FEAT_TEX) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-            if (mt.tex[k] >= 0) ts = k;
-    }
-    if ((FEAT & FEAT_TEX) && ts >= 0) {
-        SpecTex st = tex_spec_prepare(S, mt.tex[ts], tq);
-        bool black = true;
         const int nq = S.nbp / 4;
-        for (int q = 0; q < nq; ++q) {
-            float4 v = tex_spec4(S, st, q);   // FromRGB clamps; .Clamp() again is the identity
-            v = make_float4(clampf(v.x, 0.f, INFINITY), clampf(v.y, 0.f, INFINITY), clampf(v.z, 0.f, INFINITY),
-                            clampf(v.w, 0.f, INFINITY));
-            kb[q * c] = v;
-            black = black && v.x == 0.f && (4 * q + 1 >= S.nb || v.y == 0.f) && (4 * q + 2 >= S.nb || v.z == 0.f) &&
-                    (4 * q + 3 >= S.nb || v.w == 0.f);
+        int j = 0;   // K buffer of the next textured slot
+        // one copy of the lookup code for both slots (unrolled, the inlined texture lookups
+        // doubled and k_shade's register peak with them)
+#pragma unroll 1
+        for (int k = 0; k < 2; ++k) {
+            const int tid = k == 0 ? mt.tex[0] : mt.tex[1];
+            if (tid < 0) continue;
+            SpecTex st = tex_spec_prepare(S, tid, tq);
+            const bool raw = (mt.black_mask >> (4 + k)) & 1;   // metal eta / k: Evaluate(dgs), no .Clamp()
+            bool black = true;
+            float4 *kj = kb + (size_t)j * nq * c;
+            for (int q = 0; q < nq; ++q) {
+                float4 v = tex_spec4(S, st, q);
+                if (!raw)
+                    v = make_float4(clampf(v.x, 0.f, INFINITY), clampf(v.y, 0.f, INFINITY), clampf(v.z, 0.f, INFINITY),
+                                    clampf(v.w, 0.f, INFINITY));
+                kj[q * c] = v;
+                black = black && v.x == 0.f && (4 * q + 1 >= S.nb || v.y == 0.f) && (4 * q + 2 >= S.nb || v.z == 0.f) &&
+                        (4 * q + 3 >= S.nb || v.w == 0.f);
+            }
+            if (k == 0) { off[0] = -1 - j * nq; black0 = black; }
+            else { off[1] = -1 - j * nq; black1 = black; }
+            ++j;
         }
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-            if (k == ts) off[k] = -1;   // static indices only (no scratch)
-        if (ts == 0) black0 = black;
-        if (ts == 1) black1 = black;
+        // float parameters f[0], f[1]: the constants, or float textures at the shading geometry
+        // (matte's sigma clamped to [0, 90], matte.cpp:54; the constant was clamped on the host)
+#pragma unroll 1
+        for (int k = 0; k < 2; ++k) {
+            const int tid = k == 0 ? mt.ftex[0] : mt.ftex[1];
+            if (tid < 0) continue;
+            float v = tex_float(S, tid, tq);
+            if (mt.type == PBRTGPU_MAT_MATTE) v = clampf(v, 0.f, 90.f);
+            if (k == 0) fp0 = v; else fp1 = v;
+        }
     }
+    const float f0 = fp0;
+    bs.eta = mt.type == PBRTGPU_MAT_GLASS ? f0 : 1.f;
     switch (mt.type) {
         case PBRTGPU_MAT_MATTE: {
             BxDF &x = bs.bx[bs.n++];
             x.R = off[0]; x.R2 = x.R;
             x.type = BSDF_REFLECTION | BSDF_DIFFUSE;
-            float sig = mt.f[0];
+            float sig = f0;
             if (sig == 0.) { x.kind = BX_LAMBERT; x.a = x.b = 0.f; }
             else {
                 x.kind = BX_OREN;
@@ -2027,7 +2134,7 @@ PGD_HEAVY void get_bsdf(const DevScene &S, const Isect &is, const float diff[4],
             x0.a = x0.b = 0.f;
             BxDF &x1 = bs.bx[bs.n++];
             x1.kind = BX_MICRO_BLINN_DIEL; x1.type = BSDF_REFLECTION | BSDF_GLOSSY; x1.R = off[1]; x1.R2 = x1.R;
-            float e = 1.f / mt.f[0];
+            float e = 1.f / f0;
             if (e > 10000.f || isnan(e)) e = 10000.f;
             x1.a = e; x1.b = 0.f;
             break;
@@ -2036,7 +2143,7 @@ PGD_HEAVY void get_bsdf(const DevScene &S, const Isect &is, const float diff[4],
             BxDF &x = bs.bx[bs.n++];
             x.kind = BX_MICRO_BLINN_COND; x.type = BSDF_REFLECTION | BSDF_GLOSSY;
             x.R = off[0]; x.R2 = off[1];
-            float e = 1.f / mt.f[0];
+            float e = 1.f / f0;
             if (e > 10000.f || isnan(e)) e = 10000.f;
             x.a = e; x.b = 0.f;
             break;
@@ -2053,12 +2160,12 @@ PGD_HEAVY void get_bsdf(const DevScene &S, const Isect &is, const float diff[4],
             if (!black0) {
                 BxDF &x = bs.bx[bs.n++];
                 x.kind = BX_SPEC_REFL_DIEL; x.type = BSDF_REFLECTION | BSDF_SPECULAR; x.R = off[0]; x.R2 = x.R;
-                x.a = mt.f[0]; x.b = 0.f;
+                x.a = f0; x.b = 0.f;
             }
             if (!black1) {
                 BxDF &x = bs.bx[bs.n++];
                 x.kind = BX_SPEC_TRANS; x.type = BSDF_TRANSMISSION | BSDF_SPECULAR; x.R = off[1]; x.R2 = x.R;
-                x.a = mt.f[0]; x.b = 0.f;
+                x.a = f0; x.b = 0.f;
             }
             break;
         }
@@ -2081,7 +2188,7 @@ PGD_HEAVY void get_bsdf(const DevScene &S, const Isect &is, const float diff[4],
             BxDF &x = bs.bx[bs.n++];
             x.kind = BX_FRESNEL_BLEND_ANISO; x.type = BSDF_REFLECTION | BSDF_GLOSSY;
             x.R = off[0]; x.R2 = off[1];
-            float ex = 1.f / mt.f[0], ey = 1.f / mt.f[1];
+            float ex = 1.f / f0, ey = 1.f / fp1;
             if (ex > 10000.f || isnan(ex)) ex = 10000.f;
             if (ey > 10000.f || isnan(ey)) ey = 10000.f;
             x.a = ex; x.b = ey;
@@ -2175,21 +2282,60 @@ struct Seg { V o, d; float mint, maxt; };
 // point light's 1/d^2), FromRGB(illuminant) of an environment-map lookup, or black
 enum { EM_BLACK = 0, EM_POOL = 1, EM_RGB = 2 };
 struct Emit { int mode; int off; float div; bool point; RGBPick pick; };
-// InfiniteAreaLight (lights/infinite.cpp) with its one-texel radiance map
+// InfiniteAreaLight (lights/infinite.cpp): its radiance map is one texel (an unreadable or
+// non-TGA / PFM mapname, or none) or a decoded image's MIPMap (map_tex) with its Distribution2D
 PGD_INLINE float spherical_theta(V v) { return ACOSF(clampf(v.z, -1.f, 1.f)); }   // geometry.h:642-650
 PGD_INLINE float spherical_phi(V v) { float p = ATAN2F(v.y, v.x); return (p < 0.f) ? p + 2.f * kPi : p; }
-PGD_INLINE Emit inf_radiance(const pbrtgpu_light &L, float s, float t) {
+PGD_INLINE Emit inf_radiance(const DevScene &S, const pbrtgpu_light &L, float s, float t) {
     float rgb[3];
-    mip_triangle<3>(L.texel, L.wrap, s, t, rgb);   // MIPMap::Lookup(s, t), width 0
+    if (L.map_tex >= 0) mip_lookup_w<3>(S, (*sa(S.tex, (uint32_t)L.map_tex)), s, t, 0.f, rgb);   // MIPMap::Lookup(s, t)
+    else mip_triangle<3>(L.texel, L.wrap, s, t, rgb);   // the one texel: MIPMap::Lookup(s, t), width 0
     Emit e;
     e.mode = EM_RGB; e.off = -1; e.div = 1.f; e.point = false;
-    e.pick = rgb_pick(rgb);
+    e.pick = rgb_pick(S, rgb);
     return e;
 }
 // InfiniteAreaLight::Le (infinite.cpp:84-89)
-PGD_HEAVY Emit inf_Le(const pbrtgpu_light &L, V d) {
+PGD_HEAVY Emit inf_Le(const DevScene &S, const pbrtgpu_light &L, V d) {
     V wh = vnorm(xvec(L.l2w_minv, d));
-    return inf_radiance(L, spherical_phi(wh) * kInvTwoPi, spherical_theta(wh) * kInvPi);
+    return inf_radiance(S, L, spherical_phi(wh) * kInvTwoPi, spherical_theta(wh) * kInvPi);
+}
+// Distribution1D::SampleContinuous (montecarlo.h:68-84) of a record {funcInt, func[n], cdf[n + 1]}:
+// std::upper_bound over the cdf (the first entry > u), the offset along its segment, the pdf
+PGD_INLINE float dist1d_sample(const float *D, int n, float u, float *pdf, int *off) {
+    const float *cdf = D + 1 + n;
+    int lo = 0, len = n + 1;   // upper_bound: first i in [0, n + 1) with cdf[i] > u
+    while (len > 0) {
+        const int half = len >> 1;
+        if (!(u < cdf[lo + half])) { lo += half + 1; len -= half + 1; }
+        else len = half;
+    }
+    const int offset = lo - 1 > 0 ? lo - 1 : 0;
+    *off = offset;
+    const float du = (u - cdf[offset]) / (cdf[offset + 1] - cdf[offset]);
+    *pdf = D[1 + offset] / D[0];
+    return (offset + du) / n;
+}
+// Distribution2D::SampleContinuous (montecarlo.h:137-143) of a decoded environment map
+PGD_INLINE void dist2d_sample(const DevScene &S, const pbrtgpu_light &L, float u0, float u1, float uv[2], float *pdf) {
+    const int nu = L.dist_nu, nv = L.dist_nv;
+    const float *M = sa(S.texels, (uint32_t)L.dist_off);
+    float pdfs[2];
+    int v;
+    uv[1] = dist1d_sample(M, nv, u1, &pdfs[1], &v);
+    const float *R = M + (2 + 2 * nv) + (size_t)v * (2 + 2 * nu);
+    int o;
+    uv[0] = dist1d_sample(R, nu, u0, &pdfs[0], &o);
+    *pdf = pdfs[0] * pdfs[1];
+}
+// Distribution2D::Pdf (montecarlo.h:144-152)
+PGD_INLINE float dist2d_pdf(const DevScene &S, const pbrtgpu_light &L, float u, float v) {
+    const int nu = L.dist_nu, nv = L.dist_nv;
+    const float *M = sa(S.texels, (uint32_t)L.dist_off);
+    const int iu = clampi((int)(u * nu), 0, nu - 1), iv = clampi((int)(v * nv), 0, nv - 1);   // Float2Int
+    const float *R = M + (2 + 2 * nv) + (size_t)iv * (2 + 2 * nu);
+    if (R[0] * M[0] == 0.f) return 0.f;
+    return (R[1 + iu] * M[1 + iv]) / (R[0] * M[0]);
 }
 // Light::Sample_L (diffuse.cpp:61-74, point.cpp:42-49, infinite.cpp:155-185)
 template <int FEAT>
@@ -2197,8 +2343,13 @@ PGD_HEAVY void light_sample_L(const DevScene &S, const pbrtgpu_light &L, V p, fl
                               float *pdf, Seg *vis, Emit *em) {
     em->mode = EM_BLACK; em->off = L.spec; em->div = 1.f; em->point = false;
     if ((FEAT & FEAT_INF) && L.type == PBRTGPU_LIGHT_INFINITE) {
-        // Distribution2D::SampleContinuous of one texel returns (u0, u1) with pdf map_pdf
+        // Distribution2D::SampleContinuous: of one texel it returns (u0, u1) with pdf map_pdf
         float uv0 = u[0], uv1 = u[1], mapPdf = L.map_pdf;
+        if (L.map_tex >= 0) {
+            float uv[2];
+            dist2d_sample(S, L, u[0], u[1], uv, &mapPdf);
+            uv0 = uv[0]; uv1 = uv[1];
+        }
         if (mapPdf == 0.f) { *pdf = 0.f; return; }
         float theta = uv1 * kPi, phi = uv0 * 2.f * kPi;
         const float2 st = SINCOSF(theta), sp = SINCOSF(phi);
@@ -2208,7 +2359,7 @@ PGD_HEAVY void light_sample_L(const DevScene &S, const pbrtgpu_light &L, V p, fl
         *pdf = mapPdf / (2.f * kPi * kPi * sintheta);
         if (sintheta == 0.f) *pdf = 0.f;
         vis->o = p; vis->d = *wi; vis->mint = pEps; vis->maxt = INFINITY;   // VisibilityTester::SetRay
-        *em = inf_radiance(L, uv0, uv1);
+        *em = inf_radiance(S, L, uv0, uv1);
         return;
     }
     if (L.type == PBRTGPU_LIGHT_POINT) {
@@ -2247,11 +2398,14 @@ PGD_HEAVY void light_sample_L(const DevScene &S, const pbrtgpu_light &L, V p, fl
 template <int FEAT>
 PGD_HEAVY float light_pdf(const DevScene &S, const pbrtgpu_light &L, V p, V wi) {
     if (L.type == PBRTGPU_LIGHT_POINT) return 0.;
-    if ((FEAT & FEAT_INF) && L.type == PBRTGPU_LIGHT_INFINITE) {   // infinite.cpp:188-197; Distribution2D::Pdf of one texel
+    if ((FEAT & FEAT_INF) && L.type == PBRTGPU_LIGHT_INFINITE) {   // infinite.cpp:188-197
         V w = xvec(L.l2w_minv, wi);
-        float sintheta = SINF(spherical_theta(w));
+        const float theta = spherical_theta(w);
+        float sintheta = SINF(theta);
         if (sintheta == 0.f) return 0.f;
-        return L.dist_pdf / (2.f * kPi * kPi * sintheta);
+        // Distribution2D::Pdf(phi / 2pi, theta / pi); of one texel the constant dist_pdf
+        const float dp = L.map_tex >= 0 ? dist2d_pdf(S, L, spherical_phi(w) * kInvTwoPi, theta * kInvPi) : L.dist_pdf;
+        return dp / (2.f * kPi * kPi * sintheta);
     }
     const pbrtgpu_light_shape *shs = sa(S.lightShapes, (uint32_t)(L.shape_offset));
     float pp = 0.f;
@@ -2635,7 +2789,8 @@ PGD_INLINE float lens_ray(const DevScene &S, float imageX, float imageY, float l
     // montecarlo.cpp:229) and the camera lerps it again (perspective.cpp:67, 102;
     // realisticDiffraction.cpp:1157): the identity only for the default shutter [0, 1]
     r.time = lerpf(lerpf(timeU, cam.shutter_open, cam.shutter_close), cam.shutter_open, cam.shutter_close);
-    const float *cw = cam.cam2world_m;
+    float cwb[16];   // CameraToWorld(*ray, ray) at the ray's time (realisticDiffraction.cpp:1158)
+    const float *cw = cam_xform(cam, S.camMotion, r.time, cwb);
     out->o = cam_point(cw, r.o);
     out->d = vnorm(xvec(cw, r.d));
     out->mint = r.mint;

@@ -350,9 +350,9 @@ PGD_INLINE Pushes dl_spec_step(const DevScene &S, const PathSoA &P, int slot, fl
                 rxd = vadd(vsub(wi, dwodx), vmul(vadd(vmul(dndx, won), vmul(n, dDNdx)), 2.f));
                 ryd = vadd(vsub(wi, dwody), vmul(vadd(vmul(dndy, won), vmul(n, dDNdy)), 2.f));
             } else {
-                // BSDF::eta: the glass material's index, 1 otherwise (glass.cpp:48)
-                const pbrtgpu_material &mt = (*sa(S.mats, (uint32_t)((*sa(S.prims, (uint32_t)(vx.is.prim))).material)));
-                float eta = mt.type == PBRTGPU_MAT_GLASS ? mt.f[0] : 1.f;
+                // BSDF::eta: the glass material's index (a constant or its texture at the hit), 1
+                // otherwise (glass.cpp:47-48)
+                float eta = vx.bs.eta;
                 const V w = vneg(wo);
                 if (vdot(wo, n) < 0) eta = 1.f / eta;
                 const float mu = eta * vdot(w, n) - vdot(wi, n);
@@ -465,7 +465,7 @@ PGD_INLINE Pushes shade_slot_dl(const DevScene &S, const PathSoA &P, int slot, f
             if ((FEAT & FEAT_INF) && S.nInf > 0)
                 for (int l = 0; l < nLights; ++l)
                     if ((*sa(S.lights, (uint32_t)(l))).type == PBRTGPU_LIGHT_INFINITE) {
-                        const Emit e = inf_Le((*sa(S.lights, (uint32_t)(l))), ray.d);
+                        const Emit e = inf_Le(S, (*sa(S.lights, (uint32_t)(l))), ray.d);
 #pragma unroll
                         for (int q = 0; q < NQ; ++q) {
                             const float4 v = emit4<FEAT>(S, e, q);

@@ -22,7 +22,7 @@ PGD_INLINE Pushes shade_slot_meta(const DevScene &S, const PathSoA &P, int slot,
         if ((FEAT & FEAT_INF) && S.nInf > 0)
             for (int l = 0; l < S.nLights; ++l)
                 if ((*sa(S.lights, (uint32_t)(l))).type == PBRTGPU_LIGHT_INFINITE) {
-                    const Emit e = inf_Le((*sa(S.lights, (uint32_t)(l))), ray.d);
+                    const Emit e = inf_Le(S, (*sa(S.lights, (uint32_t)(l))), ray.d);
 #pragma unroll
                     for (int q = 0; q < NQ; ++q) {
                         const float4 v = emit4<FEAT>(S, e, q);

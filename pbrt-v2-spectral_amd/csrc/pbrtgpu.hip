@@ -180,7 +180,10 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_shadow(DevScene S, PathSo
 // xcdMap the blocks of one XCD take one contiguous eighth of the queue: queue order follows slot
 // order, and slots follow the pixel order of the items they took, so an XCD's rays come from
 // neighbouring pixels (and their paths) and share the part of the scene they see.  Speed only:
-// any block-to-XCD placement gives the same answers.
+// any block-to-XCD placement gives the same answers.  Measured (r05b, C2, two interleaved rounds):
+// L2 hits and misses of both trace kernels unchanged to 0.2 %, closest 76 -> 82 ms and shadow
+// 40 -> 46 ms per frame (the blocks that share a CU get neighbouring ranges of correlated cost),
+// 492 -> 471 Mpaths/s; so it is off unless PBRTGPU_XCD_MAP=1.
 PGD_INLINE uint32_t trace_wave(int xcdMap) {
     uint32_t b = blockIdx.x;
     const uint32_t nb = gridDim.x;
@@ -438,6 +441,130 @@ __global__ __launch_bounds__(kTraceBlock) PGD_TRACE_ATTR void k_trace_s4(DevScen
                     if (prim_test<true, false>(S, st, todo, (int)(off + i), ray, &prim, &thit)) {
                         occluded = true;
                         break;
+                    }
+                ref = NONE;
+            }
+            bool done = occluded;
+            if (!occluded && ref == NONE) {
+                if (todo > 0) {
+                    --todo;
+                    if (todo < bottom) {
+                        ref = gsp[todo].x;
+                        bottom = todo;
+                    } else ref = sref[(todo & (ring - 1)) * kTraceBlock + threadIdx.x];
+                } else done = true;
+            }
+            if (done) {
+                active = false;
+                P.occ[slot] = occluded ? 1u : 0u;
+            }
+        }
+    }
+    if (STATS) {
+        unsigned long long *w = reinterpret_cast<unsigned long long *>(P.cnt + CNT_WORK);
+        atomicAdd(&w[W_SHADOW], (unsigned long long)st.cShadow);
+        atomicAdd(&w[W_NODES_S], (unsigned long long)st.cNodes);
+        atomicAdd(&w[W_TRIS_S], (unsigned long long)st.cTris);
+        atomicAdd(&w[W_QUADS_S], (unsigned long long)st.cQuads);
+    }
+}
+
+// Shadow queries of one pass on the QUANTIZED 4-wide copy (scene_build.h quant_w4: 64 B per node,
+// 8-bit child boxes relative to the node's origin): k_trace_s4's persistent ray-replacement walk,
+// descending on the children's outer (containing) boxes; a stack entry keeps a "certain" bit while
+// every box on its path passed its inner (contained) test too, which implies the exact box passes.
+// A primitive hit in a certain leaf occludes; a hit in an uncertain leaf occludes only if the
+// leaf's binary ancestors' exact boxes all pass (leaf_reached) -- then the reference's IntersectP,
+// whose answer depends only on the leaves its exact box tests reach (maxt is fixed), reaches it.
+template <bool STATS>
+__global__ __launch_bounds__(kTraceBlock) PGD_TRACE_ATTR void k_trace_s4q(DevScene S, PathSoA P, int q, int refill, int ring, uint2 *__restrict__ spill) {
+    __shared__ uint32_t sref[kStackLDS * kTraceBlock];
+    uint2 *gsp = spill + (size_t)(blockIdx.x * blockDim.x + threadIdx.x) * S.w4Stack;
+    int bottom = 0;
+    Stack st;
+    const uint32_t n = P.cnt[CNT_QS(q)];
+    const uint32_t *Q = P.qS + (size_t)q * P.rcap;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wave = trace_wave(P.xcdMap), nw = (gridDim.x * blockDim.x) >> 6;
+    uint32_t next = (uint32_t)((uint64_t)n * wave / nw);
+    const uint32_t end = (uint32_t)((uint64_t)n * (wave + 1) / nw);
+    bool active = false;
+    int slot = 0, todo = 0, prim = -1;
+    uint32_t ref = 0;   // a stack entry: ref | WQ_CERT
+    float thit = INFINITY;
+    Ray ray;
+    V invDir = v3(0.f, 0.f, 0.f);
+    int neg[3] = {0, 0, 0};
+    const uint32_t NONE = 0xffffffffu;
+    auto push = [&](uint32_t r) {
+        if (todo - bottom == ring) {   // ring full: oldest entry to HBM
+            gsp[bottom] = make_uint2(sref[(bottom & (ring - 1)) * kTraceBlock + threadIdx.x], 0u);
+            ++bottom;
+        }
+        sref[(todo & (ring - 1)) * kTraceBlock + threadIdx.x] = r;
+        ++todo;
+    };
+    for (;;) {
+        const unsigned long long idle = __ballot(!active);
+        const uint32_t nIdle = (uint32_t)__popcll(idle);
+        if (next < end && (nIdle >= (uint32_t)refill || nIdle == 64u)) {
+            if (!active) {
+                const uint32_t i = next + (uint32_t)__popcll(idle & ((1ull << lane) - 1ull));
+                if (i < end) {
+                    slot = (int)Q[i];
+                    ray = ray_load(P, RAY_S, slot);
+                    invDir = v3(1.f / ray.d.x, 1.f / ray.d.y, 1.f / ray.d.z);
+                    neg[0] = invDir.x < 0; neg[1] = invDir.y < 0; neg[2] = invDir.z < 0;
+                    prim = -1;
+                    thit = INFINITY;
+                    todo = 0;
+                    bottom = 0;
+                    st.cShadow++;
+                    st.cNodes++;
+                    if (bbox_hit((*sa(S.nodes, (uint32_t)(0))), (*sa(S.nodes, (uint32_t)(1))), ray, invDir, neg)) {
+                        ref = 0u | WQ_CERT;   // the quantized root (the root's grandchildren); its box passed exactly
+                        active = true;
+                    } else P.occ[slot] = 0u;
+                }
+            }
+            next = min(end, next + nIdle);
+        }
+        if (!__ballot(active)) {
+            if (next >= end) break;
+            continue;
+        }
+        if (active) {
+            bool occluded = false;
+            const bool cert = (ref & WQ_CERT) != 0u;
+            const uint32_t r0 = ref & ~WQ_CERT;
+            if (!(r0 & WREF_LEAF)) {
+                const uint4 *w = sa(S.w4q, (uint32_t)(4 * (size_t)r0));
+                const uint4 q0 = w[0], q1 = w[1], q2 = w[2], q3 = w[3];
+                const uint32_t refs[4] = {q2.z, q2.w, q3.x, q3.y};
+                st.cNodes++;
+                uint32_t nxt = NONE;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    float4 olo, ohi, ilo, ihi;
+                    wq_boxes(q0, q1, q2, q3, k, &olo, &ohi, &ilo, &ihi);
+                    float t = 0.f, ti = 0.f;
+                    if (refs[k] != NONE && slab_enter(olo, ohi, ray, invDir, neg, &t) && t < ray.maxt) {
+                        const bool c = cert && slab_enter(ilo, ihi, ray, invDir, neg, &ti) && ti < ray.maxt;
+                        const uint32_t e = refs[k] | (c ? WQ_CERT : 0u);
+                        if (nxt == NONE) nxt = e;
+                        else push(e);
+                    }
+                }
+                ref = nxt;
+            }
+            if (ref != NONE && (ref & WREF_LEAF)) {
+                const bool lc = (ref & WQ_CERT) != 0u;
+                const uint32_t lr = ref & ~WQ_CERT;
+                const uint32_t np = (lr >> WREF_NP_SHIFT) & 0x3fu, off = lr & WREF_OFF_MASK;
+                for (uint32_t i = 0; i < np; ++i)
+                    if (prim_test<true, false>(S, st, todo, (int)(off + i), ray, &prim, &thit)) {
+                        occluded = lc || leaf_reached(S, ray, invDir, neg, (*sa(S.leafOf, off)));
+                        break;   // a hit in a leaf the reference never tests: the walk goes on
                     }
                 ref = NONE;
             }
@@ -1005,7 +1132,15 @@ __global__ __launch_bounds__(kTraceBlock) void k_intersect(DevScene S, const flo
     float t = INFINITY;
     if (!bvh_intersect(S, st, r, &prim, &t)) { prim = -1; t = INFINITY; }
     hits[4 * k] = t; hits[4 * k + 1] = 0.f; hits[4 * k + 2] = 0.f; hits[4 * k + 3] = __int_as_float(prim);
-    occ[k] = bvh_intersectP(S, st, r2) ? 1 : 0;
+    const int o = bvh_intersectP(S, st, r2) ? 1 : 0;
+    // the shadow walks of the renders answer the same: the 4-wide copy's (k_trace_s4) and its
+    // quantized copy's (k_trace_s4q); a disagreement is reported as -1, which no oracle answer is
+    bool same = true;
+    if (S.w4N > 0) {
+        same = same && (bvh_intersectP4(S, st, r2) ? 1 : 0) == o;
+        if (S.w4q) same = same && (bvh_intersectP4q(S, st, r2) ? 1 : 0) == o;
+    }
+    occ[k] = same ? o : -1;
 }
 
 // pbrtgpu_mt_sequence: one lane draws the RNG's first n outputs with the shading code's MT
@@ -1137,6 +1272,7 @@ struct pbrtgpu_ctx {
     int ptBlocksPerCU = 0;    // occupancy of k_trace_pt closest (computed on first use)
     int ptBlocksPerCUS = 0;   // occupancy of k_trace_pt shadow
     int s4BlocksPerCU = 0;    // occupancy of k_trace_s4 (shadow queries on the 4-wide BVH)
+    int s4qBlocksPerCU = 0;   // occupancy of k_trace_s4q (shadow queries on its quantized copy)
     int c4BlocksPerCU = 0;    // occupancy of k_trace_c4 (closest-hit queries on the 4-wide BVH)
     int instBlocksPerCU = 0, instBlocksPerCUS = 0;   // occupancy of k_trace_inst closest / shadow
     int ring = kStackLDS;     // LDS ring entries in use (PBRTGPU_STACK_LDS: tests force HBM spills)
@@ -1216,13 +1352,27 @@ static bool closest4_on() {
     const char *e = getenv("PBRTGPU_CLOSEST4");
     return !e || atoi(e) != 0;
 }
+// PBRTGPU_SHADOW4Q=1: the shadow queries on the quantized copy of the 4-wide tree instead of the
+// exact one.  Exact either way; opt-in because it measured slower (r05d: C2 shadow 49.5 vs 40.4
+// ms/frame, DirectLighting 236 vs 189; L2 misses -6 %): the walk is latency-bound, not byte-bound
+static bool shadow4q_on() {
+    const char *e = getenv("PBRTGPU_SHADOW4Q");
+    return e && atoi(e) != 0;
+}
 static bool shadow4_on() {
     const char *e = getenv("PBRTGPU_SHADOW4");
     return !e || atoi(e) != 0;
 }
+// PBRTGPU_TAIL=<rays>: the drain's remaining paths run to their end in one k_tail launch once the
+// queued rays of a lane (closest + shadow) are at most this many (path integrator, no instances,
+// after three list-mode passes); 0: off
+static uint32_t tail_rays() {
+    const char *e = getenv("PBRTGPU_TAIL");
+    return e ? (uint32_t)strtoul(e, nullptr, 0) : 131072u;
+}
 static int xcd_map_on() {
     const char *e = getenv("PBRTGPU_XCD_MAP");
-    return (!e || atoi(e) != 0) ? 1 : 0;
+    return (e && atoi(e) != 0) ? 1 : 0;
 }
 static bool drain_list_on() {
     const char *e = getenv("PBRTGPU_DRAIN_LIST");
@@ -1272,7 +1422,7 @@ static int ensure_slots(Lane *c, int cap, int NB, int nInst, int nFrames, int ba
     auto take = [&](size_t bytes) { size_t o = off; off += (bytes + 255) & ~(size_t)255; return o; };
     size_t oItem = take(C * 4), oHp = take(C * 4), oSmp = take(C * 4), oBounce = take(C * 4), oFlags = take(C * 4),
            oMt = take(C * 20), oBeta = take(C * 3 * NBP * 4), oL = take(C * NBP * 4), oA = take(C * AB * NBP * 4),
-           oB = take(C * AB * NBP * 4), oM = take(C * NBP * 4), oK = take(C * NBP * 4), oPix = take(C * 4),
+           oB = take(C * AB * NBP * 4), oM = take(C * NBP * 4), oK = take(C * 2 * NBP * 4) /* [2][NQ][cap]: two textured spectra */, oPix = take(C * 4),
            oRay = take(R * 27 * 4), oHitP = take(R * 8), oHitT = take(R * 8), oOcc = take(R * 4), oQC = take(R * 16),
            oQS = take(R * 8), oQT = take(C * 8), oLive = take(C * 4), oCnt = take(CNT_WORDS * 4), oInst = take(C * (size_t)nInst * 128),
            oMask = take(nFrames ? C * 4 : 0), oAMask = take(2 * ((C + 63) / 64) * 8),
@@ -1350,10 +1500,12 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
         HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&b1, k_trace_pt<true, false>, kTraceBlock, 0));
         HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&b2, k_trace_inst<false, false>, kTraceBlock, 0));
         HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&b3, k_trace_inst<true, false>, kTraceBlock, 0));
-        int b4 = 0, b5 = 0;
+        int b4 = 0, b5 = 0, b6 = 0;
         HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&b4, k_trace_s4<false>, kTraceBlock, 0));
         HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&b5, k_trace_c4<false>, kTraceBlock, 0));
+        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&b6, k_trace_s4q<false>, kTraceBlock, 0));
         c->s4BlocksPerCU = std::max(1, b4);
+        c->s4qBlocksPerCU = std::max(1, b6);
         c->c4BlocksPerCU = std::max(1, b5);
         c->ptBlocksPerCU = std::max(1, b0);
         c->ptBlocksPerCUS = std::max(1, b1);
@@ -1368,7 +1520,9 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
     const uint32_t ptGrid = (uint32_t)(c->numCUs * (instPT ? c->instBlocksPerCU : c4 ? c->c4BlocksPerCU : c->ptBlocksPerCU));
     // shadow queries on the 4-wide BVH copy (scenes without instances; PBRTGPU_SHADOW4=0: the binary walk)
     const bool s4 = !inst && c->S.w4N > 0 && shadow4_on();
-    const uint32_t ptGridS = (uint32_t)(c->numCUs * (instPT ? c->instBlocksPerCUS : s4 ? c->s4BlocksPerCU : c->ptBlocksPerCUS));
+    const bool s4q = s4 && c->S.w4q && shadow4q_on();   // ... on its quantized copy (quant_w4)
+    const uint32_t ptGridS = (uint32_t)(c->numCUs * (instPT ? c->instBlocksPerCUS
+                                                     : s4q ? c->s4qBlocksPerCU : s4 ? c->s4BlocksPerCU : c->ptBlocksPerCUS));
     const size_t spillLane = (size_t)std::max(ptGrid, ptGridS) * kTraceBlock *
                              (size_t)std::max(c->stackDepth, (s4 || c4) ? c->S.w4Stack : 0);   // uint2 per kernel
     // scenes without measured BRDFs, textures and environment lights run the variant with
@@ -1402,7 +1556,12 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
     // drain: the run's items are all taken; its k_shade passes take the live slots' list
     // (PathSoA::listMode) on a grid of liveGrid blocks (live slots <= the queued rays at the last
     // read-back, as every live slot ends a pass with a ray queued)
-    struct Run { Lane *L; ItemSrc src; int cap, grid, q, batch, passes, maxPasses; bool done, drain; int liveGrid; };
+    struct Run { Lane *L; ItemSrc src; int cap, grid, q, batch, passes, maxPasses; bool done, drain; int liveGrid, listPasses; };
+    // the drain's tail kernel (k_tail): path integrator, scenes without instances (the 4-wide walks),
+    // not in work-counting runs (it counts no traversal work)
+    const uint32_t tailMax = (!dl && c->S.integrator == PBRTGPU_INTEGRATOR_PATH && !inst && c->S.w4N > 0 && !countWork)
+                                 ? tail_rays() : 0u;
+    auto kTail = c->feat ? launch_tail<NB, FEAT_ALL> : launch_tail<NB, 0>;
     Run R[kLanes];
     const bool serial = serial_mode();
     const int nl = (src.nItems >= 8192u && !serial) ? kLanes : 1;
@@ -1427,6 +1586,7 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
         r.done = false;
         r.drain = false;
         r.liveGrid = r.grid;
+        r.listPasses = 0;
         L.P.listMode = 0;
         L.P.xcdMap = xcd_map_on();
         // drain bound of this run: a path lives at most pathPasses passes, so every slot
@@ -1504,8 +1664,10 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
                 fprintf(stderr, "pass_log lane %d after pass %d: closest queue %u shadow queue %u items taken %u of %u\n", l,
                         r.passes - 1, L.hostCnt[CNT_QC(r.q)], L.hostCnt[CNT_QS(r.q)], L.hostCnt[CNT_NEXT], r.src.nItems);
             int q = r.q;
-            if (L.hostCnt[CNT_ERR])
+            if (L.hostCnt[CNT_ERR] & 1u)
                 return fail(PBRTGPU_E_STATE, "a path drew past 227 MT19937 outputs without its state row");
+            if (L.hostCnt[CNT_ERR] & 2u)
+                return fail(PBRTGPU_E_STATE, "drain: a pass's live list exceeded its shade grid");
             // every live slot ends a pass with a ray queued, so the drain's list fits the grid sized
             // from the last queue sizes; a longer list would leave slots unshaded (their beta / A / B
             // buffers then rotate under them): refuse instead
@@ -1526,6 +1688,28 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
                 r.drain = true;
                 const uint64_t bound = std::min<uint64_t>((uint64_t)r.cap, (uint64_t)L.hostCnt[CNT_QC(q)] + L.hostCnt[CNT_QS(q)]);
                 r.liveGrid = (int)std::max<uint64_t>(1, (bound + kShadeBlock - 1) / kShadeBlock);
+            }
+            if (r.drain && r.listPasses >= 3 && tailMax &&
+                (uint64_t)L.hostCnt[CNT_QC(q)] + L.hostCnt[CNT_QS(q)] <= tailMax) {
+                // the tail: the live list, then k_tail runs those paths to their end; the next queue
+                // set stays empty, so the next read-back finds the lane drained (its time is the
+                // batch-0 event pair, a shade launch)
+                const int nq = q ^ 1;
+                HIPCHK(hipMemsetAsync(P.cnt + CNT_QC(nq), 0, 4, L.s));
+                HIPCHK(hipMemsetAsync(P.cnt + CNT_QS(nq), 0, 4, L.s));
+                HIPCHK(hipEventRecord(L.ev[0], L.s));
+                HIPCHK(drain_list(L, true, r.cap));
+                const uint64_t bound = std::min<uint64_t>((uint64_t)r.cap, (uint64_t)L.hostCnt[CNT_QC(q)] + L.hostCnt[CNT_QS(q)]);
+                HIPCHK(kTail((int)std::max<uint64_t>(1, (bound + kTailBlock - 1) / kTailBlock), L.s, c->S, L.P, q, Lout,
+                             (int)std::min<int64_t>(pathPasses, INT32_MAX)));
+                HIPCHK(hipEventRecord(L.ev[1], L.s));
+                r.batch = 0;
+                r.q = nq;
+                T.passes++;
+                r.passes++;
+                HIPCHK(hipMemcpyAsync(L.hostCnt, P.cnt, CNT_WORDS * 4, hipMemcpyDeviceToHost, L.s));
+                HIPCHK(hipEventRecord(L.done, L.s));
+                continue;
             }
             uint2 *spillC = (uint2 *)L.spill.p, *spillS = spillC + spillLane;
             // serial mode: the shadow queries follow the closest-hit queries on the main stream
@@ -1563,7 +1747,9 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
                     } else if (inst) {
                         if (countWork) hipLaunchKernelGGL((k_trace_shadow<true, true>), dim3(traceGrid), dim3(kTraceBlock), ldsS, L.s, c->S, P, q);
                         else hipLaunchKernelGGL((k_trace_shadow<false, true>), dim3(traceGrid), dim3(kTraceBlock), ldsS, L.s, c->S, P, q);
-                    } else if (s4 && countWork) hipLaunchKernelGGL((k_trace_s4<true>), dim3(ptGridS), dim3(kTraceBlock), 0, L.s, c->S, P, q, c->refill, c->ring, spillS);
+                    } else if (s4q && countWork) hipLaunchKernelGGL((k_trace_s4q<true>), dim3(ptGridS), dim3(kTraceBlock), 0, L.s, c->S, P, q, c->refill, c->ring, spillS);
+                    else if (s4q) hipLaunchKernelGGL((k_trace_s4q<false>), dim3(ptGridS), dim3(kTraceBlock), 0, L.s, c->S, P, q, c->refill, c->ring, spillS);
+                    else if (s4 && countWork) hipLaunchKernelGGL((k_trace_s4<true>), dim3(ptGridS), dim3(kTraceBlock), 0, L.s, c->S, P, q, c->refill, c->ring, spillS);
                     else if (s4) hipLaunchKernelGGL((k_trace_s4<false>), dim3(ptGridS), dim3(kTraceBlock), 0, L.s, c->S, P, q, c->refill, c->ring, spillS);
                     else if (countWork) hipLaunchKernelGGL((k_trace_pt<true, true>), dim3(ptGridS), dim3(kTraceBlock), 0, L.s, c->S, P, q, c->refill, c->ring, spillS);
                     else hipLaunchKernelGGL((k_trace_pt<true, false>), dim3(ptGridS), dim3(kTraceBlock), 0, L.s, c->S, P, q, c->refill, c->ring, spillS);
@@ -1585,6 +1771,7 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
                     HIPCHK(hipEventRecord(e[5], L.s));
                     T.passes++;
                     r.passes++;
+                    r.listPasses += r.drain ? 1 : 0;
                     q = nq;
                     continue;
                 }
@@ -1611,7 +1798,9 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
                     else if (countWork) hipLaunchKernelGGL((k_trace_pt<false, true>), dim3(ptGrid), dim3(kTraceBlock), 0, L.s, c->S, P, q, c->refill, c->ring, spillC);
                     else hipLaunchKernelGGL((k_trace_pt<false, false>), dim3(ptGrid), dim3(kTraceBlock), 0, L.s, c->S, P, q, c->refill, c->ring, spillC);
                     HIPCHK(hipGetLastError());
-                    if (s4 && countWork) hipLaunchKernelGGL((k_trace_s4<true>), dim3(ptGridS), dim3(kTraceBlock), 0, s2, c->S, P, q, c->refill, c->ring, spillS);
+                    if (s4q && countWork) hipLaunchKernelGGL((k_trace_s4q<true>), dim3(ptGridS), dim3(kTraceBlock), 0, s2, c->S, P, q, c->refill, c->ring, spillS);
+                    else if (s4q) hipLaunchKernelGGL((k_trace_s4q<false>), dim3(ptGridS), dim3(kTraceBlock), 0, s2, c->S, P, q, c->refill, c->ring, spillS);
+                    else if (s4 && countWork) hipLaunchKernelGGL((k_trace_s4<true>), dim3(ptGridS), dim3(kTraceBlock), 0, s2, c->S, P, q, c->refill, c->ring, spillS);
                     else if (s4) hipLaunchKernelGGL((k_trace_s4<false>), dim3(ptGridS), dim3(kTraceBlock), 0, s2, c->S, P, q, c->refill, c->ring, spillS);
                     else if (countWork) hipLaunchKernelGGL((k_trace_pt<true, true>), dim3(ptGridS), dim3(kTraceBlock), 0, s2, c->S, P, q, c->refill, c->ring, spillS);
                     else hipLaunchKernelGGL((k_trace_pt<true, false>), dim3(ptGridS), dim3(kTraceBlock), 0, s2, c->S, P, q, c->refill, c->ring, spillS);
@@ -1636,6 +1825,7 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
                 HIPCHK(hipEventRecord(e[5], L.s));
                 T.passes++;
                 r.passes++;
+                r.listPasses += r.drain ? 1 : 0;
                 q = nq;
             }
             r.q = q;
@@ -2263,7 +2453,7 @@ int pbrtgpu_intersect(pbrtgpu_ctx *c, const float *rays, int32_t n, float *hits,
     HIPCHK(c->scratch[1].ensure((size_t)n * 16));
     HIPCHK(c->scratch[2].ensure((size_t)n * 4));
     HIPCHK(hipMemcpyAsync(c->scratch[0].p, rays, (size_t)n * 32, hipMemcpyHostToDevice, c->stream));
-    size_t lds = 2 * (size_t)c->stackDepth * kTraceBlock * 4;
+    size_t lds = 2 * (size_t)std::max(c->stackDepth, c->S.w4Stack + 1) * kTraceBlock * 4;
     hipLaunchKernelGGL(k_intersect, dim3((n + kTraceBlock - 1) / kTraceBlock), dim3(kTraceBlock), lds, c->stream, c->S,
                        (const float *)c->scratch[0].p, n, (float *)c->scratch[1].p, (int *)c->scratch[2].p);
     HIPCHK(hipGetLastError());

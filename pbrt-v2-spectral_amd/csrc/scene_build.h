@@ -159,6 +159,98 @@ static inline int wide4_bvh(const pbrtgpu_flat_scene *s, const std::vector<uint3
     return 0;
 }
 
+// Quantized copy of the 4-wide BVH for the shadow queries (k_trace_s4q): 64 B per node instead of
+// 128, so the tree a shadow walk reads is half as large in L2 / MALL.  Per node (4 x uint4):
+//   q0 = {origin.xyz (float bits), biased exponents ex | ey << 8 | ez << 16}
+//   q1, q2.xy = per slot k the bytes qlo.x qlo.y qlo.z qhi.x qhi.y qhi.z at byte 6k
+//   q2.zw, q3.xy = the slots' refs (as the 4-wide node's; ~0u empty)
+//   q3.z = per slot 6 "exact" bits (bit 6k + c: bound c of slot k dequantizes to the box exactly)
+// A bound dequantizes as origin + float(q) * 2^e in float arithmetic (the device repeats the same
+// two operations): the lower bound takes the largest q whose value is <= the box's, the upper the
+// smallest whose value is >= (the outer box, containing the exact one); the inner box takes q + 1 /
+// q - 1 where the bound is not exact (contained in the exact box).  A slab test is monotonic in
+// the box (see wide4_bvh), so: exact pass => outer pass, and inner pass => exact pass.  The walk
+// (k_trace_s4q) descends on outer passes, marking a path "certain" while every box on it passes
+// its inner test; a primitive hit in a certain leaf is a hit the reference's walk reaches.  A hit
+// in an uncertain leaf is confirmed by re-testing the leaf's binary ancestors' exact boxes from the
+// root (leaf_reached) -- IntersectP's answer depends only on which leaves its exact box tests
+// reach, and maxt does not change during a shadow query.  leafOf[first primitive] = the binary
+// leaf node.  Returns 0 without building when a leaf holds more than 63 primitives or the tree
+// has 2^29 nodes or more (the walk keeps a "certain" bit at bit 30 of its stack entries).
+static inline int quant_w4(const pbrtgpu_flat_scene *s, const std::vector<float4> &w4, std::vector<uint4> *wq,
+                           std::vector<int32_t> *leafOf, std::string *err) {
+    wq->clear();
+    leafOf->clear();
+    const size_t nw = w4.size() / 8;
+    if (nw == 0 || nw >= (1u << 29)) return 0;
+    for (int i = 0; i < s->n_nodes; ++i)
+        if ((s->nodes[i].meta & 0xff) > 63) return 0;
+    leafOf->assign((size_t)std::max(1, s->n_prims), -1);
+    for (int i = 0; i < s->n_nodes; ++i) {
+        const pbrtgpu_bvh_node &b = s->nodes[i];
+        if ((b.meta & 0xff) && b.offset < (uint32_t)s->n_prims) (*leafOf)[b.offset] = i;
+    }
+    wq->assign(nw * 4, make_uint4(0u, 0u, 0u, 0u));
+    auto fbits = [](float f) { uint32_t u; memcpy(&u, &f, 4); return u; };
+    for (size_t n = 0; n < nw; ++n) {
+        const float4 *w = &w4[n * 8];
+        uint32_t refs[4];
+        float lo[4][3], hi[4][3];
+        int used = 0;
+        for (int k = 0; k < 4; ++k) {
+            uint32_t r;
+            memcpy(&r, &w[2 * k].w, 4);
+            refs[k] = r;
+            lo[k][0] = w[2 * k].x; lo[k][1] = w[2 * k].y; lo[k][2] = w[2 * k].z;
+            hi[k][0] = w[2 * k + 1].x; hi[k][1] = w[2 * k + 1].y; hi[k][2] = w[2 * k + 1].z;
+            if (r != 0xffffffffu) ++used;
+        }
+        if (!used) SB_FAIL(PBRTGPU_E_INVALID, "4-wide node without children");
+        uint8_t qb[24] = {0};
+        uint32_t exactBits = 0, expBits = 0;
+        float org[3];
+        for (int a = 0; a < 3; ++a) {
+            float o = INFINITY, top = -INFINITY;
+            for (int k = 0; k < 4; ++k)
+                if (refs[k] != 0xffffffffu) { o = std::min(o, lo[k][a]); top = std::max(top, hi[k][a]); }
+            if (!(o <= top) || !std::isfinite(o) || !std::isfinite(top)) SB_FAIL(PBRTGPU_E_INVALID, "BVH box");
+            org[a] = o;
+            // the smallest exponent whose 255 steps reach the top bound from the origin
+            int e = -126;
+            const float span = top - o;
+            if (span > 0.f) e = std::max(-126, (int)std::ceil(std::log2((double)span / 250.0)));
+            auto deq = [&](int q, int ee) {
+                const float sc = std::ldexp(1.f, ee);
+                const float v = (float)q * sc;   // exact: q < 256, sc a power of two
+                return o + v;                    // rounded as the device rounds it
+            };
+            while (e < 127 && deq(255, e) < top) ++e;
+            if (e >= 127) SB_FAIL(PBRTGPU_E_UNSUPPORTED, "BVH box too large to quantize");
+            expBits |= (uint32_t)(e + 127) << (8 * a);
+            for (int k = 0; k < 4; ++k) {
+                if (refs[k] == 0xffffffffu) continue;
+                int ql = 0;   // the largest q with deq(q) <= lo
+                while (ql < 255 && deq(ql + 1, e) <= lo[k][a]) ++ql;
+                int qh = 255;   // the smallest q with deq(q) >= hi
+                while (qh > 0 && deq(qh - 1, e) >= hi[k][a]) --qh;
+                if (!(deq(ql, e) <= lo[k][a]) || !(deq(qh, e) >= hi[k][a])) SB_FAIL(PBRTGPU_E_INVALID, "BVH quantization");
+                qb[6 * k + a] = (uint8_t)ql;
+                qb[6 * k + 3 + a] = (uint8_t)qh;
+                if (deq(ql, e) == lo[k][a]) exactBits |= 1u << (6 * k + a);
+                if (deq(qh, e) == hi[k][a]) exactBits |= 1u << (6 * k + 3 + a);
+            }
+        }
+        uint32_t pk[6];
+        memcpy(pk, qb, 24);
+        uint4 *q = &(*wq)[n * 4];
+        q[0] = make_uint4(fbits(org[0]), fbits(org[1]), fbits(org[2]), expBits);
+        q[1] = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+        q[2] = make_uint4(pk[4], pk[5], refs[0], refs[1]);
+        q[3] = make_uint4(refs[2], refs[3], exactBits, 0u);
+    }
+    return 0;
+}
+
 // SpectralRendererTask::Run's wave bands (spectralrenderer.cpp:99-100, 124, 180-188) in the
 // reference's own int / float arithmetic (sampledLambdaStart / sampledLambdaEnd are ints:
 // 395 / 715 in the 32- and 60-band builds, spectrum.h:41-42; 400 / 700 in the upstream 30-band
@@ -199,15 +291,8 @@ static inline int scene_check(const pbrtgpu_flat_scene *s, std::string *err) {
     if (s->abi_version != PBRTGPU_ABI_VERSION) SB_FAIL(PBRTGPU_E_INVALID, "ABI version mismatch");
     if (!(s->n_bands == 32 || s->n_bands == 60 || s->n_bands == 30 || s->n_bands == 3))
         SB_FAIL(PBRTGPU_E_UNSUPPORTED, "n_bands must be 30, 32, 60 or 3 (RGB)");
-    // the RGB build (C1): image textures, the environment light and MERL tables convert RGB with
-    // SampledSpectrum::FromRGB's basis on the device; the host front end refuses them there
-    if (s->n_bands == 3 && (s->n_textures > 0 || s->n_merl_floats > 0))
-        for (int i = 0; i < s->n_textures; ++i)
-            if (s->textures[i].type == PBRTGPU_TEX_IMAGE) SB_FAIL(PBRTGPU_E_UNSUPPORTED, "RGB build: image textures");
-    if (s->n_bands == 3 && s->n_merl_floats > 0) SB_FAIL(PBRTGPU_E_UNSUPPORTED, "RGB build: MERL BRDFs");
-    if (s->n_bands == 3)
-        for (int i = 0; i < s->n_lights; ++i)
-            if (s->lights[i].type == PBRTGPU_LIGHT_INFINITE) SB_FAIL(PBRTGPU_E_UNSUPPORTED, "RGB build: infinite lights");
+    // the RGB build (C1): image textures, the environment light and MERL tables take their RGB
+    // as the spectrum (RGBSpectrum::FromRGB, device.h rgb_pick); the SpectralRenderer does not exist
     if (s->n_bands == 3 && s->renderer == PBRTGPU_RENDERER_SPECTRAL)
         SB_FAIL(PBRTGPU_E_UNSUPPORTED, "RGB build: the SpectralRenderer needs SampledSpectrum");
     if (s->spp <= 0 || (s->spp & (s->spp - 1))) SB_FAIL(PBRTGPU_E_INVALID, "spp must be a power of two");
@@ -297,17 +382,18 @@ static inline int scene_check(const pbrtgpu_flat_scene *s, std::string *err) {
         const pbrtgpu_material &m = s->materials[i];
         if (m.type < PBRTGPU_MAT_MATTE || m.type > PBRTGPU_MAT_MEASURED_HALFANGLE)
             SB_FAIL(PBRTGPU_E_UNSUPPORTED, "material type not yet supported on the GPU");
-        int nt = 0;
+        // textured spectra in slots 0 and 1 only (device.h get_bsdf's two K buffers), textured float
+        // parameters f[0], f[1]; the measured materials have none
         for (int k = 0; k < 4; ++k)
-            if (m.tex[k] >= 0) {
-                ++nt;
-                if (!texOk(m.tex[k], 1, true) || m.type == PBRTGPU_MAT_METAL || m.type == PBRTGPU_MAT_MEASURED ||
-                    m.type == PBRTGPU_MAT_MEASURED_HALFANGLE)
-                    SB_FAIL(PBRTGPU_E_UNSUPPORTED, "material spectrum texture");
-            }
-        if (nt > 1) SB_FAIL(PBRTGPU_E_UNSUPPORTED, "more than one textured spectrum per material");
+            if (m.tex[k] >= 0 && (k > 1 || !texOk(m.tex[k], 1, true) || m.type == PBRTGPU_MAT_MEASURED ||
+                                  m.type == PBRTGPU_MAT_MEASURED_HALFANGLE))
+                SB_FAIL(PBRTGPU_E_UNSUPPORTED, "material spectrum texture");
+        for (int j = 0; j < 2; ++j)
+            if (m.ftex[j] >= 0 && (!texOk(m.ftex[j], 0, false) || m.type == PBRTGPU_MAT_MEASURED ||
+                                   m.type == PBRTGPU_MAT_MEASURED_HALFANGLE || m.type == PBRTGPU_MAT_MIRROR))
+                SB_FAIL(PBRTGPU_E_INVALID, "material float texture");
         if (m.bump_tex >= 0 && !texOk(m.bump_tex, 0, false)) SB_FAIL(PBRTGPU_E_INVALID, "bump texture");
-        if (m.normal_tex >= 0 && (!texOk(m.normal_tex, 1, false) || s->n_bands == 3)) SB_FAIL(PBRTGPU_E_INVALID, "normal map texture");
+        if (m.normal_tex >= 0 && !texOk(m.normal_tex, 1, false)) SB_FAIL(PBRTGPU_E_INVALID, "normal map texture");
         if (m.type == PBRTGPU_MAT_MEASURED_HALFANGLE && m.aux >= 0 &&
             (!s->merl || s->n_merl_floats < 0 || (int64_t)m.aux * 3 + 3 * 90 * 90 * 180 > (int64_t)s->n_merl_floats))
             SB_FAIL(PBRTGPU_E_INVALID, "RegularHalfangle table out of range");
@@ -429,11 +515,20 @@ static int scene_build(const pbrtgpu_flat_scene *s, int topNodes, DevScene &S, i
         S.w4nodes = nullptr;
         S.w4N = 0;
         S.w4Stack = 0;
+        S.w4q = nullptr;
+        S.leafOf = nullptr;
         if (s->n_instances == 0) {
             if (int e = wide4_bvh(s, ref, &w4, &S.w4Stack, err)) return e;
             if (!w4.empty()) {
                 SB_PUT(w4.data(), w4.size(), &S.w4nodes);
                 S.w4N = (int)(w4.size() / 8);
+                std::vector<uint4> wq;
+                std::vector<int32_t> leafOf;
+                if (int e = quant_w4(s, w4, &wq, &leafOf, err)) return e;
+                if (!wq.empty()) {
+                    SB_PUT(wq.data(), wq.size(), &S.w4q);
+                    SB_PUT(leafOf.data(), leafOf.size(), &S.leafOf);
+                }
             }
         }
     }
@@ -496,10 +591,7 @@ static int scene_build(const pbrtgpu_flat_scene *s, int topNodes, DevScene &S, i
     S.texels = nullptr;
     if (s->n_texel_floats > 0) SB_PUT(s->texels, (size_t)s->n_texel_floats, &S.texels);
     S.camMotion = nullptr;
-    if (s->camera_motion) {
-        if (s->camera_type != PBRTGPU_CAMERA_PERSPECTIVE) SB_FAIL(PBRTGPU_E_UNSUPPORTED, "animated lens camera");
-        SB_PUT(s->camera_motion, (size_t)1, &S.camMotion);
-    }
+    if (s->camera_motion) SB_PUT(s->camera_motion, (size_t)1, &S.camMotion);
     SB_PUT(pt.data(), pt.size(), &S.primTri);
     SB_PUT(s->tris, (size_t)s->n_tris, &S.tris);
     SB_PUT(s->meshes, (size_t)s->n_meshes, &S.meshes);
@@ -564,7 +656,8 @@ static int scene_build(const pbrtgpu_flat_scene *s, int topNodes, DevScene &S, i
     for (int i = 0; i < s->n_materials; ++i) {
         const pbrtgpu_material &m = s->materials[i];
         if (m.type == PBRTGPU_MAT_MEASURED || m.type == PBRTGPU_MAT_MEASURED_HALFANGLE) *feat |= FEAT_MEAS;
-        if (m.bump_tex >= 0 || m.normal_tex >= 0 || m.tex[0] >= 0 || m.tex[1] >= 0 || m.tex[2] >= 0 || m.tex[3] >= 0)
+        if (m.bump_tex >= 0 || m.normal_tex >= 0 || m.tex[0] >= 0 || m.tex[1] >= 0 || m.tex[2] >= 0 || m.tex[3] >= 0 ||
+            m.ftex[0] >= 0 || m.ftex[1] >= 0)
             *feat |= FEAT_TEX;
     }
     return 0;

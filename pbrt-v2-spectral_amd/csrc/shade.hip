@@ -85,6 +85,9 @@ __global__ __launch_bounds__(kShadeBlock) PGD_SHADE_ATTR void k_shade(DevScene S
     bool inRange = slot < P.cap;
     if (LIST) {   // the drain: thread i takes the i-th live slot
         const uint32_t i = (uint32_t)slot;
+        // every pass of a read-back batch checks its own list against its grid (the host sees
+        // only the last pass's count): a longer list would leave slots unshaded
+        if (i == 0 && P.cnt[CNT_LIVE] > gridDim.x * blockDim.x) atomicOr(&P.cnt[CNT_ERR], 2u);
         inRange = i < P.cnt[CNT_LIVE];
         slot = inRange ? (int)P.live[i] : 0;
     }
@@ -357,6 +360,79 @@ hipError_t launch_shade(int grid, hipStream_t stream, const DevScene &S, const P
 }
 template hipError_t launch_shade<SHADE_NB, SHADE_FEAT>(int, hipStream_t, const DevScene &, const PathSoA &,
                                                        const ItemSrc &, int, float *);
+#endif
+
+#if !SHADE_DL
+// The drain's tail (path integrator, scenes without instances).  Once a lane's items are all taken
+// and the drain's list passes have left few live paths, each pass still costs its launches and a
+// host read-back for a few thousand rays, and the last passes of a small render (one GPU's tile
+// slice at 8 GPUs) are mostly that.  k_tail runs every live slot's path to its end in one launch,
+// one thread per slot of the live list (k_live_list): the slot's pending queries of the last
+// shading step -- continuation ray, MIS ray, shadow ray -- answered by the per-thread walks of the
+// 4-wide BVH copy (bvh_intersect4 / bvh_intersectP4: the primitives and order k_trace_c4 / k_trace_s4
+// test, replayed against the oracle on the host), then shade_slot as the next list-mode pass would
+// run it, then the MT window where k_mt_init would compute it; until the path is done.
+// Exact: a slot's pass-to-pass state is its own in list mode (every writer stores at the identity
+// entry and sets its region's writer masks to all ones, wavefront.h PathSoA::listMode); the host
+// starts k_tail only after three list-mode passes, so every entry a slot still reads (beta up to
+// two passes back, A / B one) was written that way; each thread then advances its own pass index
+// and queue set as the host would per pass.  Nothing is queued: the queues of the next set are
+// left empty, and the lane reads as drained.
+template <int NB, int FEAT>
+__global__ __launch_bounds__(kTailBlock) void k_tail(DevScene S, PathSoA P0, int q0, float *__restrict__ Lout, int maxSteps) {
+    PathSoA P = P0;
+    P.listMode = 1;
+    if (FEAT & FEAT_MEAS) kd_lds_fill(S);   // the measured-BRDF kd-trees, once per block (before any return)
+    // the traversal stack after the kd-trees in the dynamic LDS: refs, then entry distances
+    const int depth = (S.stackDepth > S.w4Stack ? S.stackDepth : S.w4Stack) + 1;
+    uint32_t *stk = reinterpret_cast<uint32_t *>(pgd_kd_lds + (((FEAT & FEAT_MEAS) && S.kdInLds) ? 2 * S.nKd : 0));
+    Stack st;
+    st.base = stk + threadIdx.x;
+    st.tbase = reinterpret_cast<float *>(stk + (size_t)depth * blockDim.x) + threadIdx.x;
+    st.stride = blockDim.x;
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P.cnt[CNT_LIVE]) return;
+    const int slot = (int)P.live[i];
+    const uint32_t rc = (uint32_t)P.rcap;
+    int qout = q0;
+    for (int step = 0; step < maxSteps && P.item[slot] >= 0; ++step) {
+        const uint32_t fl = P.flags[slot];
+        if (fl & PF_CONT) {   // the continuation ray (list mode: every record at the slot)
+            Ray r = ray_load(P, RAY_C, slot);
+            int prim = -1;
+            float t = INFINITY;
+            if (!bvh_intersect4(S, st, r, &prim, &t)) prim = -1;
+            P.hitPrim[slot] = prim;
+            P.hitT[slot] = prim >= 0 ? t : INFINITY;
+        }
+        if (fl & PF_PB) {   // the MIS ray
+            Ray r = ray_load(P, RAY_M, slot);
+            int prim = -1;
+            float t = INFINITY;
+            if (!bvh_intersect4(S, st, r, &prim, &t)) prim = -1;
+            P.hitPrim[rc + (uint32_t)slot] = prim;
+            P.hitT[rc + (uint32_t)slot] = prim >= 0 ? t : INFINITY;
+        }
+        if (fl & PF_PA) P.occ[slot] = bvh_intersectP4(S, st, ray_load(P, RAY_S, slot)) ? 1u : 0u;
+        P.pass = (P.pass + 1) % 3;   // the next pass: beta buffers rotate, A / B take the other queue set
+        qout ^= 1;
+        bool done = false, zeroed = false;
+        const Pushes pu = shade_slot<NB, FEAT>(S, P, slot, Lout, &done, &zeroed, qout);
+        if (zeroed) atomicAdd(&P.cnt[CNT_ZEROED], 1u);
+        if (done) P.item[slot] = -1;
+        else if (pu.t) mt_window_init(P, (uint32_t)slot);   // vertex 3 draws first (k_mt_init's list)
+    }
+}
+template <int NB, int FEAT>
+hipError_t launch_tail(int grid, hipStream_t stream, const DevScene &S, const PathSoA &P, int q, float *Lout,
+                       int maxSteps) {
+    const size_t kd = ((FEAT & FEAT_MEAS) && S.kdInLds) ? (size_t)S.nKd * 32 : 0;
+    const int depth = (S.stackDepth > S.w4Stack ? S.stackDepth : S.w4Stack) + 1;
+    const size_t lds = kd + (size_t)depth * kTailBlock * 8;
+    hipLaunchKernelGGL((k_tail<NB, FEAT>), dim3(grid), dim3(kTailBlock), lds, stream, S, P, q, Lout, maxSteps);
+    return hipGetLastError();
+}
+template hipError_t launch_tail<SHADE_NB, SHADE_FEAT>(int, hipStream_t, const DevScene &, const PathSoA &, int, float *, int);
 #endif
 
 }  // namespace pgd

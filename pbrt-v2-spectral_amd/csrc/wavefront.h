@@ -70,7 +70,8 @@ enum { RAY_C = 0, RAY_M = 1, RAY_S = 2 };
 #define CNT_QC(q) (32 * (q))          // closest-hit queue size, queue set q = 0, 1
 #define CNT_QS(q) (64 + 32 * (q))     // shadow queue size
 #define CNT_QT(q) (224 + 32 * (q))    // MT-window list size (qT): k_mt_init of set q clears set q ^ 1
-// CNT_ERR: nonzero when a path drew past MT output 227 without its full-state row (mt_store), which
+// CNT_ERR: bit 0 when a path drew past MT output 227 without its full-state row (mt_store), bit 1
+// when a drain pass's live list was longer than its grid (k_shade LIST: slots left unshaded), which
 // the host turns into PBRTGPU_E_STATE instead of a silently wrong radiance; CNT_DLN: entries of
 // the DirectLighting light-sample list (PathSoA::dlList) of this pass
 enum { CNT_NEXT = 128, CNT_ZEROED = 160, CNT_WORK = 192, CNT_LIVE = 288, CNT_ERR = 320, CNT_DLN = 352, CNT_WORDS = 384 };
@@ -99,7 +100,7 @@ struct PathSoA {
                                  // a beta in the pass with index pass % 3 (beta = wave region + rank)
     int pass;                    // index of this k_shade pass within the run (host counter)
     float4 *M;          // [NQ][cap]: measured-BRDF spectrum of the BSDF value being consumed
-    float4 *K;          // [NQ][cap]: the material's textured spectrum at the current vertex
+    float4 *K;          // [2][NQ][cap]: the material's textured spectra at the current vertex (device.h get_bsdf)
     // ray records are indexed by ray slot rs: the slot itself, or (DirectLighting, a batch of
     // light samples per pass) slot + j * cap for the batch's sample j; rcap = cap x batch
     int rcap;
@@ -324,9 +325,10 @@ PGD_INLINE float term_val(const FTerm &t, float r, float r2) {
         default: return 0.f;
     }
 }
-// band quad q of a spectrum reference: pool offset, or -1 = the slot's K bands
+// band quad q of a spectrum reference: pool offset, or -1 - j * NQ = the slot's K band buffer j
+// (device.h get_bsdf)
 PGD_INLINE float4 spec4(const float *sp, int off, int q, const float4 *kb, size_t c) {
-    return off >= 0 ? ld4(sp, off + 4 * q) : kb[q * c];
+    return off >= 0 ? ld4(sp, off + 4 * q) : kb[(size_t)(-1 - off + q) * c];
 }
 // one term's share of four bands (quad q), added to v
 template <int FEAT>
@@ -573,7 +575,7 @@ PGD_INLINE void term_prepare(const DevScene &S, FTerm &t, float4 *mb, size_t c) 
         // Spectrum::FromRGB(&brdf[3 * index]) (reflection.cpp:299), reflectance
         const float *rgb = sa(S.merl, (uint32_t)(3 * ((size_t)t.R + (size_t)t.R2)));
         const float v[3] = {rgb[0], rgb[1], rgb[2]};
-        const RGBPick pk = rgb_pick(v);
+        const RGBPick pk = rgb_pick(S, v);
 #pragma unroll
         for (int q = 0; q < Bands<NB>::NQ; ++q) mb[q * c] = from_rgb4(S, pk, false, q);
         t.kind = T_BUF;
@@ -888,7 +890,7 @@ PGD_UNROLL_BANDS
             }
             Emit eb;
             if ((FEAT & FEAT_INF) && Lt.type == PBRTGPU_LIGHT_INFINITE) {
-                if (go) eb = inf_Le(Lt, wi);
+                if (go) eb = inf_Le(S, Lt, wi);
             } else {
                 eb.mode = Lt.is_black ? EM_BLACK : EM_POOL; eb.off = Lt.spec; eb.div = 1.f; eb.point = false;
             }
@@ -970,7 +972,8 @@ PGD_INLINE Pushes shade_vertex(const DevScene &S, const PathSoA &P, int slot, in
     float diff[4] = {0.f, 0.f, 0.f, 0.f};
     if ((FEAT & FEAT_TEX) && vb == 0) {
         const pbrtgpu_material &mt = (*sa(S.mats, (uint32_t)((*sa(S.prims, (uint32_t)(is.prim))).material)));
-        if (mt.bump_tex >= 0 || mt.normal_tex >= 0 || mt.tex[0] >= 0 || mt.tex[1] >= 0 || mt.tex[2] >= 0 || mt.tex[3] >= 0) {
+        if (mt.bump_tex >= 0 || mt.normal_tex >= 0 || mt.tex[0] >= 0 || mt.tex[1] >= 0 || mt.tex[2] >= 0 || mt.tex[3] >= 0 ||
+            mt.ftex[0] >= 0 || mt.ftex[1] >= 0) {
             const uint32_t pxy = P.pix[slot];
             float u[2], lens[2];
             s2d(hp, 0, s, spp, u);
@@ -1242,7 +1245,7 @@ PGD_INLINE Pushes shade_slot(const DevScene &S, const PathSoA &P, int slot, floa
             const Ray ray = ray_load(P, RAY_C, slot);
             for (int l = 0; l < S.nLights; ++l)
                 if ((*sa(S.lights, (uint32_t)(l))).type == PBRTGPU_LIGHT_INFINITE) {
-                    const Emit e = inf_Le((*sa(S.lights, (uint32_t)(l))), ray.d);
+                    const Emit e = inf_Le(S, (*sa(S.lights, (uint32_t)(l))), ray.d);
 #pragma unroll
                     for (int q = 0; q < NQ; ++q) {
                         float4 v = emit4<FEAT>(S, e, q);
@@ -1257,7 +1260,7 @@ PGD_INLINE Pushes shade_slot(const DevScene &S, const PathSoA &P, int slot, floa
         for (int l = 0; l < S.nLights; ++l) {
             Emit e;
             e.mode = EM_BLACK;
-            if ((FEAT & FEAT_INF) && (*sa(S.lights, (uint32_t)(l))).type == PBRTGPU_LIGHT_INFINITE) e = inf_Le((*sa(S.lights, (uint32_t)(l))), d);
+            if ((FEAT & FEAT_INF) && (*sa(S.lights, (uint32_t)(l))).type == PBRTGPU_LIGHT_INFINITE) e = inf_Le(S, (*sa(S.lights, (uint32_t)(l))), d);
 #pragma unroll
             for (int q = 0; q < NQ; ++q) {
                 float4 bt = beta_q(beta_rd<NB>(P, vb, 1, slot, wm.b1), q, c), v = emit4<FEAT>(S, e, q);
@@ -1284,6 +1287,7 @@ static const int kShadeBlock = PGD_SHADE_BLOCK;
 // slot & ~63, rank = lanes below that wrote) needs whole 64-lane waves with slot = block * blockDim
 // + lane, every pass
 static_assert(kShadeBlock % 64 == 0, "k_shade blocks must be whole waves");
+static const int kTailBlock = 64;   // k_tail (shade.hip): one wave per block, its traversal stack in LDS
 // k_shade<NB, FEAT> launch (defined in shade.hip, one translation unit per variant)
 template <int NB, int FEAT>
 hipError_t launch_shade(int grid, hipStream_t stream, const DevScene &S, const PathSoA &P, const ItemSrc &src, int qout,
@@ -1303,6 +1307,10 @@ hipError_t launch_dl_spec(int grid, hipStream_t stream, const DevScene &S, const
 // k_regen alone (instantiated once per band count, in the FEAT_ALL DirectLighting object)
 template <int NB>
 hipError_t launch_regen(int grid, hipStream_t stream, const DevScene &S, const PathSoA &P, const ItemSrc &src, int qout);
+// k_tail: the drain's last live paths run to their end in one launch (path integrator, no instances)
+template <int NB, int FEAT>
+hipError_t launch_tail(int grid, hipStream_t stream, const DevScene &S, const PathSoA &P, int q, float *Lout,
+                       int maxSteps);
 // k_shade with the MetadataIntegrator step
 template <int NB, int FEAT>
 hipError_t launch_shade_meta(int grid, hipStream_t stream, const DevScene &S, const PathSoA &P, const ItemSrc &src,

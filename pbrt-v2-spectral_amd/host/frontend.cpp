@@ -219,6 +219,7 @@ struct MaterialObj {
 };
 struct LightObj {
     pbrtgpu_light l{};
+    LightObj() { l.map_tex = -1; l.dist_off = -1; l.dist_nu = l.dist_nv = 1; }   // no decoded environment map
     Spec L;
     std::vector<Isect> shapeSet;      // area light ShapeSet (light.cpp:114-135)
 };
@@ -1082,7 +1083,6 @@ private:
     // in a MIPMap pyramid (BuildMipmap) in out->texels; an unreadable .tga / .pfm gives the
     // one-valued MIPMap(1, 1, powf(scale, gamma)) with the MIPMap defaults
     int MakeImageTexture(const ParamSet &p, bool spectral) {
-        if (spec.rgb()) throw std::runtime_error("image textures are not supported in the RGB build");
         pbrtgpu_texture t = TexNode(PBRTGPU_TEX_IMAGE, spectral);
         std::string mapping = GetString(p, p, "mapping", "uv");
         if (mapping != "uv") throw std::runtime_error("texture mapping '" + mapping + "' is not supported yet");
@@ -1095,6 +1095,14 @@ private:
         float scale = GetFloat(p, p, "scale", 1.f), gamma = GetFloat(p, p, "gamma", 1.f);
         std::string fn = GetString(p, p, "filename", "");
         if (!fn.empty()) fn = Resolve(fn);
+        const TexInfoKey key{fn, trilerp, maxAniso, wm, scale, gamma};
+        auto hit = mipCache[spectral ? 1 : 0].find(key);
+        if (hit != mipCache[spectral ? 1 : 0].end()) {   // the cached MIPMap: its pyramid and flags
+            const pbrtgpu_texture &c = hit->second;
+            t.texel_off = c.texel_off; t.width = c.width; t.height = c.height; t.levels = c.levels;
+            t.trilinear = c.trilinear; t.nofilter = c.nofilter; t.max_aniso = c.max_aniso; t.wrap = c.wrap;
+            return AddTexture(t);
+        }
         const int nc = spectral ? 3 : 1;
         std::vector<float> rgb, img;
         int w = 0, h = 0;
@@ -1120,6 +1128,7 @@ private:
         if ((size_t)out->texels.size() + (size_t)w * h * nc * 2 > (size_t)INT32_MAX)
             throw std::runtime_error("image map " + fn + ": texel pool exceeds 2^31 floats");
         BuildMipmap(w, h, std::move(img), nc, t.wrap, out->texels, &t.width, &t.height, &t.levels);
+        mipCache[spectral ? 1 : 0][key] = t;
         return AddTexture(t);
     }
     // operand of a ScaleTexture: a CONST or IMAGE node
@@ -1200,33 +1209,32 @@ private:
         }
         SpecTex t; t.value = GetSpec(g, m, n, d); return t;
     }
-    Spec ConstSpecTex(const ParamSet &g, const ParamSet &m, const std::string &n, const Spec &d) {
-        SpecTex t = GetSpecTex(g, m, n, d);
-        if (!t.constant) throw std::runtime_error("non-constant spectrum texture for '" + n + "' is not supported yet");
-        return t.value;
-    }
-    float ConstFloatTex(const ParamSet &g, const ParamSet &m, const std::string &n, float d) {
-        FloatTex t = GetFloatTex(g, m, n, d);
-        if (!t.constant) throw std::runtime_error("non-constant float texture for '" + n + "' is not supported yet");
-        return t.value;
-    }
-    // spectrum parameter k of a material: a constant (clamped where the material clamps) or
-    // one textured slot evaluated per hit on the device
+    // spectrum parameter k of a material: a constant (clamped where the material clamps) or a
+    // textured slot evaluated per hit on the device (`.Clamp()`ed there unless clamp is false:
+    // black_mask bit 4 + k); a material has at most two spectrum parameters
     void SpecSlot(MaterialObj &mo, int k, const ParamSet &g, const ParamSet &m, const std::string &n, const Spec &d,
                   bool clamp) {
         SpecTex t = GetSpecTex(g, m, n, d);
-        if ((int)mo.spectra.size() != k) throw std::runtime_error("internal: material slot order");
+        if ((int)mo.spectra.size() != k || k > 1) throw std::runtime_error("internal: material slot order");
         if (t.constant) { mo.spectra.push_back(clamp ? SpecClamp(t.value) : t.value); return; }
-        for (int j = 0; j < 4; ++j)
-            if (mo.m.tex[j] >= 0) throw std::runtime_error("more than one textured spectrum parameter per material is not supported yet");
-        if (!clamp) throw std::runtime_error("textured '" + n + "' is not supported yet");
         mo.m.tex[k] = t.tex;
+        if (!clamp) mo.m.black_mask |= 1 << (4 + k);
         mo.spectra.push_back(spec.Const(0.f));   // placeholder; the device evaluates tex[k]
+    }
+    // float parameter j (f[0], f[1]) of a material: a constant, or a float texture evaluated per hit
+    // on the device (ftex[j]); matte's sigma is clamped to [0, 90] on either side (matte.cpp:54)
+    void FloatSlot(MaterialObj &mo, int j, const ParamSet &g, const ParamSet &m, const std::string &n, float d,
+                   bool clampSigma = false) {
+        FloatTex t = GetFloatTex(g, m, n, d);
+        if (t.constant) { mo.m.f[j] = clampSigma ? Clamp(t.value, 0.f, 90.f) : t.value; return; }
+        mo.m.ftex[j] = t.tex;
+        mo.m.f[j] = 0.f;   // unused: the device evaluates ftex[j]
     }
     std::shared_ptr<MaterialObj> MakeMaterial(const std::string &name, const ParamSet &g, const ParamSet &m) {
         auto mo = std::make_shared<MaterialObj>();
         pbrtgpu_material &mt = mo->m;
         for (int k = 0; k < 4; ++k) mt.tex[k] = -1;
+        mt.ftex[0] = mt.ftex[1] = -1;
         mt.bump_tex = -1;
         mt.normal_tex = -1;
         // every material: normalmap (Material::NormalMap where its value is not black; the default
@@ -1234,7 +1242,6 @@ private:
         SpecTex nmap = GetSpecTex(g, m, "normalmap", spec.Const(0.f));
         if (nmap.constant) {
             if (!SpecIsBlack(nmap.value)) {   // EvaluateMemory of a constant is RGB 0 (constant.h:45-47)
-                if (spec.rgb()) throw std::runtime_error("normal maps are not supported in the RGB build");
                 pbrtgpu_texture c = TexNode(PBRTGPU_TEX_CONST, true);
                 c.spec = EmitSpectrum(nmap.value);
                 mt.normal_tex = AddTexture(c);
@@ -1246,12 +1253,12 @@ private:
         if (name == "matte") {   // matte.cpp:34-72
             mt.type = PBRTGPU_MAT_MATTE;
             SpecSlot(*mo, 0, g, m, "Kd", spec.Const(0.5f), true);
-            mt.f[0] = Clamp(ConstFloatTex(g, m, "sigma", 0.f), 0.f, 90.f);
+            FloatSlot(*mo, 0, g, m, "sigma", 0.f, true);
         } else if (name == "plastic") {   // plastic.cpp:34-74
             mt.type = PBRTGPU_MAT_PLASTIC;
             SpecSlot(*mo, 0, g, m, "Kd", spec.Const(0.25f), true);
             SpecSlot(*mo, 1, g, m, "Ks", spec.Const(0.25f), true);
-            mt.f[0] = ConstFloatTex(g, m, "roughness", .1f);
+            FloatSlot(*mo, 0, g, m, "roughness", .1f);
         } else if (name == "mirror") {   // mirror.cpp
             mt.type = PBRTGPU_MAT_MIRROR;
             SpecSlot(*mo, 0, g, m, "Kr", spec.Const(0.9f), true);
@@ -1259,18 +1266,18 @@ private:
             mt.type = PBRTGPU_MAT_SUBSTRATE;
             SpecSlot(*mo, 0, g, m, "Kd", spec.Const(.5f), true);
             SpecSlot(*mo, 1, g, m, "Ks", spec.Const(.5f), true);
-            mt.f[0] = ConstFloatTex(g, m, "uroughness", .1f);
-            mt.f[1] = ConstFloatTex(g, m, "vroughness", .1f);
+            FloatSlot(*mo, 0, g, m, "uroughness", .1f);
+            FloatSlot(*mo, 1, g, m, "vroughness", .1f);
         } else if (name == "glass") {   // glass.cpp:34-68
             mt.type = PBRTGPU_MAT_GLASS;
             SpecSlot(*mo, 0, g, m, "Kr", spec.Const(1.f), true);
             SpecSlot(*mo, 1, g, m, "Kt", spec.Const(1.f), true);
-            mt.f[0] = ConstFloatTex(g, m, "index", 1.5f);
+            FloatSlot(*mo, 0, g, m, "index", 1.5f);
         } else if (name == "metal") {   // metal.cpp:44-62, 99-110 (eta, k unclamped)
             mt.type = PBRTGPU_MAT_METAL;
             SpecSlot(*mo, 0, g, m, "eta", CopperSpectrum(false), false);
             SpecSlot(*mo, 1, g, m, "k", CopperSpectrum(true), false);
-            mt.f[0] = ConstFloatTex(g, m, "roughness", .01f);
+            FloatSlot(*mo, 0, g, m, "roughness", .01f);
         } else if (name == "measured") {   // measured.cpp:66-130, 182-206 (.brdf: IrregIsotropicBRDF)
             mt.type = PBRTGPU_MAT_MEASURED;
             std::string fn = Resolve(GetString(g, m, "filename", ""));
@@ -1319,6 +1326,26 @@ private:
         return spec.FromSampled(wl, kAbsorption ? kk : eta, 56);
     }
     std::map<std::string, std::shared_ptr<MeasuredData> > measuredCache;
+    // ImageTexture::GetTexture's MIPMap cache (imagemap.cpp:47-80, imagemap.h:39-55), one per
+    // ImageTexture instantiation (float, spectrum): keyed by TexInfo -- filename, doTrilinear,
+    // maxAniso, wrap, scale, gamma, NOT noFiltering -- so a later texture with the same key takes
+    // the first one's MIPMap, its pyramid and its filtering flags; the value is that texture record
+    struct TexInfoKey {
+        std::string filename;
+        bool trilinear;
+        float maxAniso;
+        int wrap;
+        float scale, gamma;
+        bool operator<(const TexInfoKey &o) const {   // TexInfo::operator< (its field order)
+            if (filename != o.filename) return filename < o.filename;
+            if (trilinear != o.trilinear) return trilinear < o.trilinear;
+            if (maxAniso != o.maxAniso) return maxAniso < o.maxAniso;
+            if (scale != o.scale) return scale < o.scale;
+            if (gamma != o.gamma) return gamma < o.gamma;
+            return wrap < o.wrap;
+        }
+    };
+    std::map<TexInfoKey, pbrtgpu_texture> mipCache[2];
     std::map<std::string, int> merlCache;   // loadedRegularHalfangle (measured.cpp:99)
     // ReadFloatFile (floatfile.cpp:30-74)
     static std::vector<float> ReadFloatFile(const std::string &fn) {
@@ -1361,7 +1388,6 @@ private:
     // stored as float.  Returns the first texel in out->merl, or -1 when the reference's loader
     // fails (Error(); the material then has no BxDF).
     int LoadMerl(const std::string &fn) {
-        if (spec.rgb()) throw std::runtime_error("measured (MERL) BRDFs are not supported in the RGB build");
         const uint32_t nThetaH = 90, nThetaD = 90, nPhiD = 180;
         FILE *f = fopen(fn.c_str(), "rb");
         if (!f) { out->warnings.push_back("Unable to open BRDF data file " + fn); return -1; }
@@ -1490,7 +1516,6 @@ private:
             lo->l.pos[0] = lp.x; lo->l.pos[1] = lp.y; lo->l.pos[2] = lp.z;
             memcpy(lo->l.l2w_m, l2w.m.m, 64); memcpy(lo->l.l2w_minv, l2w.mInv.m, 64);
         } else if (name == "infinite" || name == "exinfinite") {   // infinite.cpp:41-80, 232-245
-            if (spec.rgb()) throw std::runtime_error("infinite lights are not supported in the RGB build");
             Spec L = p.FindOneSpectrum("L", spec.Const(1.0f));
             Spec sc = p.FindOneSpectrum("scale", spec.Const(1.0f));
             std::string texmap = p.FindOneString("mapname", "");
@@ -1499,17 +1524,23 @@ private:
             float rgb[3];
             spec.ToRGB(lo->L, rgb);   // L.ToRGBSpectrum()
             float texel[3] = {rgb[0], rgb[1], rgb[2]};
+            lo->l.map_tex = -1;
+            lo->l.dist_off = -1;
+            lo->l.dist_nu = lo->l.dist_nv = 1;
+            lo->l.wrap = PBRTGPU_WRAP_REPEAT;
             if (texmap != "") {   // ReadImage (imageio.cpp:45-66): NULL keeps the one texel L
                 std::vector<float> img;
                 int w = 0, h = 0;
                 if (ReadImageFile(Resolve(texmap), img, &w, &h)) {
-                    if (w != 1 || h != 1) throw std::runtime_error("environment image maps are not supported yet: " + texmap);
-                    for (int k = 0; k < 3; ++k) texel[k] = img[k] * rgb[k];   // texels[i] *= L.ToRGBSpectrum()
+                    for (size_t i = 0; i < (size_t)w * h; ++i)   // texels[i] *= L.ToRGBSpectrum()
+                        for (int k = 0; k < 3; ++k) img[3 * i + k] *= rgb[k];
+                    if (w == 1 && h == 1) for (int k = 0; k < 3; ++k) texel[k] = img[k];
+                    else EnvMap(lo->l, w, h, std::move(img));
                 }
             }
             for (int k = 0; k < 3; ++k) lo->l.texel[k] = texel[k];
-            lo->l.wrap = PBRTGPU_WRAP_REPEAT;
-            // Distribution2D of img[0] = Lookup(0, 0, 1).y() * sinTheta (one texel: Texel(0, 0, 0))
+            // Distribution2D of img[0] = Lookup(0, 0, 1).y() * sinTheta (one texel: Texel(0, 0, 0));
+            // unused with a decoded map (EnvMap's distribution)
             const float kPiF = 3.14159265358979323846f;
             float img = 0.212671f * texel[0] + 0.715160f * texel[1] + 0.072169f * texel[2];
             img *= sinf(kPiF * float(0 + .5f) / float(1));
@@ -1525,6 +1556,103 @@ private:
         // Light::nSamples (light.h:45): point lights take none, infinite "nsamples" (infinite.cpp:181)
         lo->l.n_samples = std::max(1, name == "point" ? 1 : p.FindOneInt("nsamples", 1));
         lights.push_back(lo);
+    }
+    // InfiniteAreaLight's constructor for a decoded environment image (infinite.cpp:60-109): the
+    // radiance MIPMap<RGBSpectrum>(width, height, texels) with the MIPMap defaults (no trilinear,
+    // max anisotropy 8, repeat; BuildMipmap resamples a non-power-of-two image and clamps it), then
+    // the scalar image img[u + v w] = radianceMap->Lookup(u / w, v / h, 1 / max(w, h)).y() *
+    // sinf(M_PI * (v + .5) / h) and its Distribution2D, stored after the pyramid in the texel pool
+    void EnvMap(pbrtgpu_light &l, int w, int h, std::vector<float> img) {
+        pbrtgpu_texture t = TexNode(PBRTGPU_TEX_IMAGE, true);
+        t.trilinear = 0; t.nofilter = 0; t.max_aniso = 8.f; t.wrap = PBRTGPU_WRAP_REPEAT;
+        t.texel_off = (int)out->texels.size();
+        if ((size_t)out->texels.size() + (size_t)w * h * 3 * 2 + (size_t)(w + 2) * (h + 2) * 2 > (size_t)INT32_MAX)
+            throw std::runtime_error("environment map: texel pool exceeds 2^31 floats");
+        BuildMipmap(w, h, std::move(img), 3, t.wrap, out->texels, &t.width, &t.height, &t.levels);
+        l.map_tex = AddTexture(t);
+        l.dist_nu = w;
+        l.dist_nv = h;
+        const float kPiF = 3.14159265358979323846f;   // pbrt.h:179: M_PI is a float literal here
+        const float filter = 1.f / std::max(w, h);
+        std::vector<float> f((size_t)w * h);
+        for (int v = 0; v < h; ++v) {
+            const float vp = (float)v / (float)h;
+            const float sinTheta = sinf(kPiF * float(v + .5f) / float(h));
+            for (int u = 0; u < w; ++u) {
+                const float up = (float)u / (float)w;
+                float c[3];
+                MipLookupW(t, up, vp, filter, c);
+                f[u + (size_t)v * w] = 0.212671f * c[0] + 0.715160f * c[1] + 0.072169f * c[2];   // RGBSpectrum::y()
+                f[u + (size_t)v * w] *= sinTheta;
+            }
+        }
+        // Distribution2D (montecarlo.cpp:350-362): a Distribution1D per row, then the marginal of
+        // their integrals; Distribution1D (montecarlo.h:45-66) in the reference's float order
+        auto dist1d = [](const float *fn, int n, std::vector<float> &o) {   // {funcInt, func[n], cdf[n + 1]}
+            std::vector<float> cdf(n + 1);
+            cdf[0] = 0.;
+            for (int i = 1; i < n + 1; ++i) cdf[i] = cdf[i - 1] + fn[i - 1] / n;
+            const float funcInt = cdf[n];
+            if (funcInt == 0.f) for (int i = 1; i < n + 1; ++i) cdf[i] = float(i) / float(n);
+            else for (int i = 1; i < n + 1; ++i) cdf[i] /= funcInt;
+            o.push_back(funcInt);
+            o.insert(o.end(), fn, fn + n);
+            o.insert(o.end(), cdf.begin(), cdf.end());
+            return funcInt;
+        };
+        std::vector<float> rows, marg((size_t)h);
+        for (int v = 0; v < h; ++v) marg[v] = dist1d(&f[(size_t)v * w], w, rows);
+        l.dist_off = (int)out->texels.size();
+        dist1d(marg.data(), h, out->texels);
+        out->texels.insert(out->texels.end(), rows.begin(), rows.end());
+    }
+    // MIPMap::Lookup(s, t, width) (mipmap.h:226-259) of an IMAGE texture's pyramid in the texel pool:
+    // the level from the width, triangle filters (mipmap.h:263-274) at one or two levels, Texel's
+    // wrap (mipmap.h:197-222); as the device's mip_lookup_w
+    void MipLookupW(const pbrtgpu_texture &t, float s, float tt, float width, float res[3]) const {
+        const int nc = 3;
+        auto level = [&](int lv, const float **T, int *w, int *h) {
+            size_t off = (size_t)t.texel_off;
+            int ww = t.width, hh = t.height;
+            for (int i = 0; i < lv; ++i) { off += (size_t)ww * hh * nc; ww = ww > 1 ? ww >> 1 : 1; hh = hh > 1 ? hh >> 1 : 1; }
+            *T = out->texels.data() + off; *w = ww; *h = hh;
+        };
+        auto texel = [&](const float *T, int w, int h, int s0, int t0, float *o) {
+            if (t.wrap == PBRTGPU_WRAP_REPEAT) {
+                auto mod = [](int a, int b) { int n = int(a / b); a -= n * b; if (a < 0) a += b; return a; };
+                s0 = mod(s0, w); t0 = mod(t0, h);
+            } else if (t.wrap == PBRTGPU_WRAP_CLAMP) { s0 = std::min(std::max(s0, 0), w - 1); t0 = std::min(std::max(t0, 0), h - 1); }
+            else if (s0 < 0 || s0 >= w || t0 < 0 || t0 >= h) { o[0] = o[1] = o[2] = 0.f; return; }
+            for (int k = 0; k < nc; ++k) o[k] = T[((size_t)t0 * w + s0) * nc + k];
+        };
+        auto tri = [&](int lv, float s, float tv, float *o) {
+            lv = std::min(std::max(lv, 0), t.levels - 1);
+            const float *T; int w, h;
+            level(lv, &T, &w, &h);
+            s = s * (float)w - 0.5f;
+            tv = tv * (float)h - 0.5f;
+            const int s0 = Floor2Int(s), t0 = Floor2Int(tv);
+            const float ds = s - s0, dt = tv - t0;
+            const float w00 = (1.f - ds) * (1.f - dt), w01 = (1.f - ds) * dt, w10 = ds * (1.f - dt), w11 = ds * dt;
+            float a[3], b[3], c[3], d[3];
+            texel(T, w, h, s0, t0, a); texel(T, w, h, s0, t0 + 1, b); texel(T, w, h, s0 + 1, t0, c); texel(T, w, h, s0 + 1, t0 + 1, d);
+            for (int k = 0; k < nc; ++k) o[k] = ((w00 * a[k] + w01 * b[k]) + w10 * c[k]) + w11 * d[k];
+        };
+        const float invLog2 = 1.f / logf(2.f);
+        const float lvl = (float)(t.levels - 1) + logf(std::max(width, 1e-8f)) * invLog2;   // Log2 (pbrt.h:243-246)
+        if (lvl < 0) tri(0, s, tt, res);
+        else if (lvl >= (float)(t.levels - 1)) {
+            const float *T; int w, h;
+            level(t.levels - 1, &T, &w, &h);
+            texel(T, w, h, 0, 0, res);
+        } else {
+            const int il = Floor2Int(lvl);
+            const float delta = lvl - il;
+            float a[3], b[3];
+            tri(il, s, tt, a);
+            tri(il + 1, s, tt, b);
+            for (int k = 0; k < nc; ++k) res[k] = (1.f - delta) * a[k] + delta * b[k];
+        }
     }
     // ShapeSet (light.cpp:114-135): refine with a LIFO todo list
     void ShapeSetOf(const std::shared_ptr<ShapeObj> &s, std::vector<Isect> *set) {
@@ -1843,7 +1971,7 @@ private:
         if (m->flatIndex >= 0) return m->flatIndex;
         pbrtgpu_material fm = m->m;
         for (int k = 0; k < 4; ++k) fm.spec[k] = k < (int)m->spectra.size() ? EmitSpectrum(m->spectra[k]) : -1;
-        fm.black_mask = 0;
+        fm.black_mask &= ~0xf;   // bits 4-7 (unclamped textured slots) stay
         for (int k = 0; k < (int)m->spectra.size() && k < 4; ++k)
             if (fm.tex[k] < 0 && SpecIsBlack(m->spectra[k])) fm.black_mask |= 1 << k;
         if (m->measured) fm.aux = EmitMeasured(m->measured.get(), &fm.aux2);
@@ -1939,7 +2067,6 @@ private:
         // Decompose for the per-ray Interpolate (camera.cpp:84-103)
         out->cameraMotion.clear();
         if (c2w[0] != c2w[1]) {
-            if (cameraName != "perspective") throw std::runtime_error("animated lens cameras are not supported yet");
             const AnimXform A(c2w[0], tStart, c2w[1], tEnd);
             pbrtgpu_instance cm{};
             cm.root = -1; cm.single_prim = -1;

@@ -11,11 +11,13 @@
 namespace pbrtamd {
 
 static const char kMagic[8] = {'P', 'B', 'R', 'T', 'P', 'A', 'C', 'K'};
-static const uint32_t kVersion = 13;   // 6: + merl tables; 7: + metadata ids; 8: + Renderer; 9: + lens diffraction;
+static const uint32_t kVersion = 15;   // 6: + merl tables; 7: + metadata ids; 8: + Renderer; 9: + lens diffraction;
                                        // 10: + pinhole array / microlens / eye IOR; 11: image maps as MIPMap
                                        // pyramids (texture records + texel pool); 12: material normal maps
                                        // (normal_tex, a former pad word: -1 for older packs); 13: an animated
-                                       // camera's CameraToWorld; 5-12 still load
+                                       // camera's CameraToWorld; 14: textured float parameters (ftex, the
+                                       // former pad words: -1 for older packs); 15: decoded environment maps
+                                       // (light map_tex / dist_off, former pad words: -1); 5-14 still load
 
 // the texture record of packs before v11: one MIPMap texel inline (the one-texel maps they held)
 struct TexV10 {
@@ -184,6 +186,10 @@ bool LoadPack(const std::string &path, HostScene *s, std::string *err) {
     if (ok && ver >= 11) ok = RArr(f, s->texels);
     if (ok && ver < 12)
         for (auto &m : s->materials) m.normal_tex = -1;
+    if (ok && ver < 14)
+        for (auto &m : s->materials) m.ftex[0] = m.ftex[1] = -1;
+    if (ok && ver < 15)
+        for (auto &l : s->lights) { l.map_tex = -1; l.dist_off = -1; l.dist_nu = l.dist_nv = 1; }
     s->cameraMotion.clear();
     if (ok && ver >= 13) ok = RArr(f, s->cameraMotion) && s->cameraMotion.size() <= 1;
     gzclose(f);

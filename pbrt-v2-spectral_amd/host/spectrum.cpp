@@ -65,9 +65,19 @@ Spec SpectrumCtx::FromXYZ(const float xyz[3], bool illum) const {
     return FromRGB(rgb, illum);
 }
 
+// spectrum.cpp:199-212
+static float InterpolateSpectrumSamples(const float *lambda, const float *vals, int n, float l) {
+    if (l <= lambda[0]) return vals[0];
+    if (l >= lambda[n - 1]) return vals[n - 1];
+    for (int i = 0; i < n - 1; ++i)
+        if (l >= lambda[i] && l <= lambda[i + 1]) return Lerp((l - lambda[i]) / (lambda[i + 1] - lambda[i]), vals[i], vals[i + 1]);
+    throw std::runtime_error("InterpolateSpectrumSamples: unsorted wavelengths");
+}
+
+// SampledSpectrum::FromSampled (spectrum.h:276-295): band averages; the RGB build's
+// RGBSpectrum::FromSampled (spectrum.h:493-516): XYZ by the 1 nm matching functions over the
+// interpolated samples, each divided by sum(CIE_Y), then FromXYZ (XYZToRGB, no clamp)
 Spec SpectrumCtx::FromSampled(const float *lambda, const float *v, int n) const {
-    if (rgb()) throw std::runtime_error("sampled spectra (SPD files, default metal, measured BRDFs, blackbody) are not "
-                                        "supported in the RGB build");
     bool sorted = true;
     for (int i = 0; i < n - 1; ++i) if (lambda[i] > lambda[i + 1]) { sorted = false; break; }
     if (!sorted) {
@@ -77,6 +87,18 @@ Spec SpectrumCtx::FromSampled(const float *lambda, const float *v, int n) const 
         std::vector<float> sl(n), svv(n);
         for (int i = 0; i < n; ++i) { sl[i] = sv[i].first; svv[i] = sv[i].second; }
         return FromSampled(sl.data(), svv.data(), n);
+    }
+    if (rgb()) {
+        float xyz[3] = {0.f, 0.f, 0.f}, yint = 0.f;
+        for (int i = 0; i < kCIE_nsamples; ++i) {
+            yint += kCIE_Y[i];
+            const float val = InterpolateSpectrumSamples(lambda, v, n, (float)(kCIE_lambda_first + i));
+            xyz[0] += val * kCIE_X[i];
+            xyz[1] += val * kCIE_Y[i];
+            xyz[2] += val * kCIE_Z[i];
+        }
+        for (int k = 0; k < 3; ++k) xyz[k] /= yint;
+        return FromXYZ(xyz, false);
     }
     Spec r(nb, 0.f);
     for (int i = 0; i < nb; ++i) {

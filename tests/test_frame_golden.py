@@ -44,7 +44,7 @@ def _load(pg, name):
 
 
 def test_frame_fixtures_present():
-    assert "killeroo_frame_c2_700x700s256" in AVAILABLE
+    assert "killeroo_frame_c2_700x700s256" in AVAILABLE and "anim_frame_c5_600x600s512" in AVAILABLE
 
 
 @pytest.mark.parametrize("name", AVAILABLE)

@@ -100,7 +100,7 @@ def _golden_scene(pg, cfg, name="killeroo"):
     w, h, spp, seed, md = [int(v) for v in cfg]
     pack = {"anim": "anim-killeroos-moving.pack", "bunny": "bunny.pack", "metal": "metal.pack",
             "coverage": "coverage.pack", "imagemap": "imagemap.pack",
-            "animcam": "animcam.pack"}.get(name.split("_")[0],
+            "animcam": "animcam.pack", "textured": "textured.pack", "envmap": "envmap.pack"}.get(name.split("_")[0],
                                                                                               "killeroo-simple.pack")
     if "_b30_" in name:
         pack = pack.replace(".pack", "-b30.pack")
@@ -113,7 +113,7 @@ def _golden_scene(pg, cfg, name="killeroo"):
                                   "bunny_keys_c3_1920x1080s1024", "metal_keys_c4_400x400s4096",
                                   "anim_keys_c5_600x600s512", "killeroo_b30_paths_48x40s4",
                                   "coverage_b30_paths_48x36s4", "imagemap_paths_64x48s4",
-                                  "imagemap_paths_96x72s2_seed5", "animcam_paths_64x48s4"])
+                                  "imagemap_paths_96x72s2_seed5", "animcam_paths_64x48s4", "textured_paths_64x48s4", "envmap_paths_64x48s4"])
 def test_paths_vs_reference_golden(pg, name):
     """GPU against the reference harness's own per-path radiance (fixed seeds); the *_keys_*
     fixtures are the configs at their real resolution and sample count."""
@@ -129,7 +129,7 @@ def test_paths_vs_reference_golden(pg, name):
 @pytest.mark.parametrize("name", ["killeroo_film_96x72s16", "anim_film_40x40s8", "bunny_film_48x27s8",
                                   "metal_film_40x40s8", "coverage_film_64x48s8", "killeroo_b30_film_40x32s8",
                                   "coverage_b30_film_40x30s4", "imagemap_film_64x48s8",
-                                  "animcam_film_64x48s4"])
+                                  "animcam_film_64x48s4", "textured_film_64x48s8", "envmap_film_64x48s8"])
 def test_film_vs_reference_golden(pg, name):
     """Whole-film render against the reference's film (raw sums, incl. neighbour-pixel
     samples): bit for bit."""
@@ -331,7 +331,7 @@ def test_regular_halfangle_brdf_vs_reference_golden(pg, merl_dir):
     assert_bit_exact(L, pg.oracle().trace_paths(scene, g["keys"]), "merl paths vs oracle")
 
 
-DL = ["killeroo_dl_%s_48x40s4", "bunny_dl_%s_48x27s4", "anim_dl_%s_40x40s4", "coverage_dl_%s_64x48s4",
+DL = ["textured_dl_%s_48x36s4", "envmap_dl_%s_48x36s4", "killeroo_dl_%s_48x40s4", "bunny_dl_%s_48x27s4", "anim_dl_%s_40x40s4", "coverage_dl_%s_64x48s4",
       "coverage_dlone_%s_64x48s4"]
 
 
@@ -437,7 +437,8 @@ def test_drain_list_mode_is_exact(pg, monkeypatch, integ, strategy, md):
     DirectLighting kernels take the live slots of k_live_list; the per-wave compaction becomes the
     identity) against the same runs with it off (PBRTGPU_DRAIN_LIST=0): films and per-path
     radiance bit for bit, with slot pools small enough that most passes run in list mode (193
-    slots: many drains of a few waves) and one large pool."""
+    slots: many drains of a few waves) and one large pool; and the drain's tail kernel (k_tail:
+    the last paths run to their end in one launch) off and switched on as early as allowed."""
     from conftest import PACKS
     kw = dict(integrator=integ, strategy=strategy) if strategy else {}
     scene = pg.Scene.load(os.path.join(PACKS, "coverage.pack"), xres=40, yres=30, spp=4, maxdepth=md, **kw)
@@ -451,11 +452,39 @@ def test_drain_list_mode_is_exact(pg, monkeypatch, integ, strategy, md):
                 monkeypatch.setenv("PBRTGPU_DRAIN_LIST", on)
                 d.render()
                 out[(slots, on)] = (d.film(), d.trace_paths(keys))
+        # the drain's tail kernel (k_tail, path integrator): off, and on from the first eligible pass
+        for tail in ("0", "100000000"):
+            monkeypatch.setenv("PBRTGPU_DRAIN_LIST", "1")
+            monkeypatch.setenv("PBRTGPU_SLOTS", "4096")
+            monkeypatch.setenv("PBRTGPU_TAIL", tail)
+            d.render()
+            out[("tail", tail)] = (d.film(), d.trace_paths(keys))
+        monkeypatch.delenv("PBRTGPU_TAIL")
     ref = out[("4096", "0")]
     for k, (film, paths) in out.items():
         assert np.array_equal(film.view(np.int32), ref[0].view(np.int32)), k
         assert np.array_equal(paths.view(np.int32), ref[1].view(np.int32)), k
     assert_bit_exact(ref[1], pg.oracle().trace_paths(scene, keys), "paths vs oracle")
+
+
+@pytest.mark.parametrize("name", ["killeroo_keys_c2_700x700s256", "killeroo_film_96x72s16", "killeroo_dl_paths_48x40s4",
+                                  "killeroo_dl_film_48x40s4", "coverage_paths_64x48s8"])
+def test_quantized_shadow_walk_vs_reference_golden(pg, monkeypatch, name):
+    """The opt-in quantized 4-wide shadow walk (PBRTGPU_SHADOW4Q=1, k_trace_s4q: 64-byte nodes with
+    conservative outer / inner boxes, a leaf's hit kept only when its exact ancestors pass) against
+    the reference harness: per path and film, bit for bit, path integrator and DirectLighting."""
+    from conftest import GOLDEN
+    from test_oracle_golden import dl_scene
+    monkeypatch.setenv("PBRTGPU_SHADOW4Q", "1")
+    g = np.load(os.path.join(GOLDEN, name + ".npz"))
+    scene = dl_scene(pg, g, name) if "_dl_" in name else _golden_scene(pg, g["config"], name)
+    with pg.Device(0) as d:
+        d.upload(scene)
+        if "film" in name:
+            d.render()
+            assert_bit_exact(d.film(), g["film"], name)
+        else:
+            assert_bit_exact(d.trace_paths(g["keys"]), g["L"], name)
 
 
 META = ["metadata_material_%s_48x36s4", "metadata_mesh_%s_48x36s4", "metadata_depth_%s_48x36s4",
@@ -547,7 +576,9 @@ def test_spectral_renderer_lanes_batches_and_rejects(pg, monkeypatch):
     ("lens.pbrt", dict(renderer="spectral", wave_bands=10, sampling="sampler")),
     ("lens_diffraction.pbrt", dict()),
     ("lens_diffraction.pbrt", dict(renderer="spectral", wave_bands=8, sampling="single")),
-    ("lens_diffraction.pbrt", dict(renderer="spectral", wave_bands=10, sampling="sampler", integrator="directlighting"))])
+    ("lens_diffraction.pbrt", dict(renderer="spectral", wave_bands=10, sampling="sampler", integrator="directlighting")),
+    ("lens_animated.pbrt", dict()),
+    ("lens_animated.pbrt", dict(renderer="spectral", wave_bands=8, sampling="single", integrator="directlighting"))])
 def test_realistic_diffraction_camera_vs_oracle(pg, monkeypatch, scene_file, kw):
     """RealisticDiffractionCamera (tests/scenes/lens.pbrt: a double-Gauss lens, chromatic
     aberration on, so every SpectralRenderer band refracts with its own n) on the GPU against
@@ -635,6 +666,29 @@ def test_rgb_build_vs_reference_golden(pg, name):
     assert_bit_exact(L, pg.oracle().trace_paths(scene, g["keys"]), name + " vs oracle")
     if film is not None:
         assert_bit_exact(film, gf["film"], "killeroo_rgb_film_40x32s8")
+
+
+@pytest.mark.parametrize("name", ["imagemap_rgb_paths_64x48s4", "textured_rgb_paths_64x48s4", "envmap_rgb_paths_64x48s4",
+                                  "coverage_rgb_paths_64x48s4", "merl_rgb_paths_64x48s4", "envmap_rgb_dl_paths_48x36s4",
+                                  "coverage_rgb_dl_paths_48x36s4"])
+def test_rgb_build_features_vs_reference_golden(pg, name, request):
+    """The RGB build's image textures, normal maps, textured parameters, environment map, SPD
+    spectra and MERL tables (NB = 3 kernels, FromRGB the identity) against the brgb harness per
+    path and film, bit for bit."""
+    from conftest import GOLDEN
+    from test_oracle_golden import rgbfeat_scene
+    g = np.load(os.path.join(GOLDEN, name + ".npz"))
+    gf = np.load(os.path.join(GOLDEN, name.replace("_paths_", "_film_") + ".npz"))
+    scene = rgbfeat_scene(pg, g, name, request)
+    fs = rgbfeat_scene(pg, gf, name, request)
+    with pg.Device(0) as d:
+        d.upload(scene)
+        L = d.trace_paths(g["keys"])
+        d.upload(fs)
+        d.render()
+        film = d.film()
+    assert_bit_exact(L, g["L"], name)
+    assert_bit_exact(film, gf["film"], name.replace("_paths_", "_film_"))
 
 
 def test_integrator_scene_checks(pg):

@@ -258,6 +258,25 @@ def test_realistic_diffraction_camera(pg, tmp_path):
     assert line2 == "%g %g %g" % (50.0, f.lens.fstop, fov)
 
 
+def test_animated_lens_camera(pg):
+    """An animated CameraToWorld under the RealisticDiffractionCamera (tests/scenes/
+    lens_animated.pbrt): the flat scene carries the camera's AnimatedTransform and its shutter;
+    the oracle's rays take the transform at each ray's time (realisticDiffraction.cpp:1157-1158),
+    so the radiance differs from the same camera held at its start transform.  PARITY UNPINNED vs
+    the reference (the camera's TU needs GSL); the GPU = oracle in tests/test_gpu_parity.py."""
+    here = os.path.join(os.path.dirname(os.path.abspath(__file__)), "scenes")
+    s = pg.Scene.load(os.path.join(here, "lens_animated.pbrt"), xres=24, yres=18, spp=2, maxdepth=4)
+    f = s.flat
+    assert f.camera_type == 1 and f.camera_motion
+    assert (f.camera.shutter_open, f.camera.shutter_close) == (np.float32(0.1), np.float32(0.9))
+    keys = np.array([(x, y, k) for y in range(0, 18, 3) for x in range(0, 24, 3) for k in range(2)], np.int32)
+    o = pg.oracle()
+    La = o.trace_paths(s, keys)
+    s.flat.camera_motion = None   # the start transform's matrix is cam2world_m
+    Ls = o.trace_paths(s, keys)
+    assert np.any(La != 0) and not np.array_equal(La, Ls)
+
+
 def _pinhole_array(W, H, xres, yres, film_diag, film_dist, last_ap):
     """RealisticDiffractionCamera's pinholeArray (realisticDiffraction.cpp:248-304) restated in
     numpy float32 / double arithmetic"""
@@ -358,15 +377,16 @@ def test_eye_ior_tables_from_reference_curves(pg):
 
 def test_rgb_build_front_end(pg):
     """bands=3 is the reference's RGB build: 'color' parameters stay RGB triples (no basis, no
-    clamp), y() uses RGBSpectrum's YWeight with yint 1; what converts spectra on the device
-    (image textures, the environment light) or needs sampled spectra is refused."""
+    clamp), y() uses RGBSpectrum's YWeight with yint 1; sampled spectra (SPD files, the copper
+    default, blackbody) go through RGBSpectrum::FromSampled, so the coverage scene loads with its
+    image textures, environment light and metals (pinned by the *_rgb_* goldens)."""
     s = pg.Scene.load(os.path.join(PACKS, "killeroo-simple-rgb.pack"))
     assert s.bands == 3 and s.flat.y_int == 1.0
     y = np.ctypeslib.as_array(ctypes.cast(s.flat.band_Y, ctypes.POINTER(ctypes.c_float)), (3,))
     assert y.tolist() == [np.float32(0.212671), np.float32(0.715160), np.float32(0.072169)]
     here = os.path.join(os.path.dirname(os.path.abspath(__file__)), "scenes")
-    with pytest.raises(RuntimeError, match="RGB build"):
-        pg.Scene.load(os.path.join(here, "coverage.pbrt"), bands=3)
+    c = pg.Scene.load(os.path.join(here, "coverage.pbrt"), bands=3)
+    assert c.bands == 3 and c.flat.n_textures > 0 and c.flat.n_lights >= 3
     assert s.flat.n_lights == 1
 
 

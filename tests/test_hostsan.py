@@ -28,6 +28,7 @@ LENS_D = os.path.join(ROOT, "tests", "scenes", "lens_diffraction.pbrt")
 LF_P = os.path.join(ROOT, "tests", "scenes", "lens_pinholes.pbrt")
 LF_M = os.path.join(ROOT, "tests", "scenes", "lens_microlens.pbrt")
 EYE = os.path.join(ROOT, "tests", "scenes", "eye.pbrt")
+SCN = os.path.join(ROOT, "tests", "scenes", "")
 
 
 def _build(target):
@@ -79,9 +80,19 @@ CASES = [
     ("imagemap.pack", dict(xres=48, yres=36, spp=4, maxdepth=3)),
     ("imagemap.pack", dict(xres=40, yres=30, spp=2, maxdepth=3, integrator="directlighting", strategy="all")),
     ("animcam.pack", dict(xres=40, yres=30, spp=4, maxdepth=6)),
+    ("textured.pack", dict(xres=40, yres=30, spp=4, maxdepth=5)),
+    ("textured.pack", dict(xres=32, yres=24, spp=2, maxdepth=5, integrator="directlighting", strategy="all")),
+    ("envmap.pack", dict(xres=40, yres=30, spp=4, maxdepth=5)),
+    ("envmap.pack", dict(xres=32, yres=24, spp=2, maxdepth=5, integrator="directlighting", strategy="all")),
     # DirectLighting over instances (ray slots stay per slot, terms per list row) and at 60 bands
     ("anim-killeroos-moving.pack", dict(xres=24, yres=24, spp=4, maxdepth=5, integrator="directlighting", strategy="all")),
     ("metal.pack", dict(xres=24, yres=24, spp=4, maxdepth=5, integrator="directlighting", strategy="all")),
+    # the RGB build (NB = 3): image textures and normal maps, the environment map, SPD spectra
+    (SCN + "imagemap.pbrt", dict(xres=40, yres=30, spp=2, maxdepth=3, bands=3)),
+    (SCN + "envmap.pbrt", dict(xres=32, yres=24, spp=2, maxdepth=5, bands=3, integrator="directlighting", strategy="all")),
+    (SCN + "coverage.pbrt", dict(xres=32, yres=24, spp=2, maxdepth=6, bands=3)),
+    # an animated CameraToWorld under the lens camera
+    (SCN + "lens_animated.pbrt", dict(xres=32, yres=24, spp=2, maxdepth=5)),
 ]
 
 
@@ -89,7 +100,9 @@ CASES = [
                                                "path_bunny", "path_metal60", "metadata", "path_coverage_b30",
                                                "lens_diffraction", "lens_diffraction_spectral", "lens_pinholes",
                                                "lens_microlens_spectral", "eye", "eye_spectral", "lens_diffraction_dl",
-                                               "imagemap", "imagemap_dl", "animcam", "dl_anim_inst", "dl_metal60"])
+                                               "imagemap", "imagemap_dl", "animcam", "textured", "textured_dl", "envmap", "envmap_dl",
+                                               "dl_anim_inst",
+                                               "dl_metal60", "rgb_imagemap", "rgb_envmap_dl", "rgb_coverage", "lens_animated"])
 def test_replay_matches_oracle(pg, tmp_path, pack, a):
     exe = _build("shade_host")
     scene = pg.Scene.load(os.path.join(PACKS, pack), **a)

@@ -35,6 +35,8 @@ struct int2 { int x, y; };
 struct int3 { int x, y, z; };
 struct int4 { int x, y, z, w; };
 struct uint2 { unsigned x, y; };
+struct uint4 { unsigned x, y, z, w; };
+inline uint4 make_uint4(unsigned x, unsigned y, unsigned z, unsigned w) { return uint4{x, y, z, w}; }
 inline float2 make_float2(float x, float y) { return float2{x, y}; }
 inline float4 make_float4(float x, float y, float z, float w) { return float4{x, y, z, w}; }
 inline int2 make_int2(int x, int y) { return int2{x, y}; }

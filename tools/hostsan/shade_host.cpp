@@ -110,7 +110,7 @@ static PathSoA make_soa(int cap, int NB, int nInst, int nFrames, int batch, bool
     P.flags = arr<uint32_t>(C); P.mt = arr<uint32_t>(5 * C); P.pix = arr<uint32_t>(C);
     P.beta = arr<float4>(3 * NQ * C); P.L = arr<float4>(NQ * C);
     P.A = arr<float4>(AB * NQ * C); P.B = arr<float4>(AB * NQ * C);
-    P.M = arr<float4>(NQ * C); P.K = arr<float4>(NQ * C);
+    P.M = arr<float4>(NQ * C); P.K = arr<float4>(2 * NQ * C);
     P.aMask = arr<unsigned long long>(2 * W); P.bMask = arr<unsigned long long>(3 * W);
     P.mMask = arr<unsigned long long>(2 * W);
     P.ray = arr<float>(3 * 9 * R); P.hitPrim = arr<int>(2 * R); P.hitT = arr<float>(2 * R); P.occ = arr<uint32_t>(R);
@@ -243,11 +243,12 @@ static int run(const DevScene &S, PathSoA &P, const ItemSrc &src, int nSlots, fl
         }
         // shadow queries: on the 4-wide copy where the GPU uses it (k_trace_s4; PBRTGPU_SHADOW4=0:
         // the binary walk), so the replay checks its boxes and leaves against the oracle too
-        const char *s4e = getenv("PBRTGPU_SHADOW4");
+        const char *s4e = getenv("PBRTGPU_SHADOW4"), *s4qe = getenv("PBRTGPU_SHADOW4Q");
         const bool s4 = S.nInsts == 0 && S.w4N > 0 && !(s4e && atoi(s4e) == 0);
+        const bool s4q = s4 && S.w4q && !(s4qe && atoi(s4qe) == 0);   // k_trace_s4q's quantized copy
         for (uint32_t rs : Q[q].s) {
             const Ray r = ray_load(P, RAY_S, (int)rs);
-            P.occ[rs] = (s4 ? bvh_intersectP4(S, st, r)
+            P.occ[rs] = (s4q ? bvh_intersectP4q(S, st, r) : s4 ? bvh_intersectP4(S, st, r)
                             : S.nInsts > 0 ? bvh_intersectP<true>(S, st, r) : bvh_intersectP<false>(S, st, r)) ? 1u : 0u;
         }
     };

@@ -59,7 +59,7 @@ def render_frame(scene, W, H, spp, bands, jobs, tmp):
         y0, y1 = int(strips[j]), int(strips[j + 1])
         fn = os.path.join(tmp, "strip%d.f32" % j)
         args = [exe, os.path.join(SCENES, scene), "--res", str(W), str(H), "--spp", str(spp), "--seed", "0",
-                "--maxdepth", "5", "--window", "-1", str(W + 1), str(y0 - 1), str(y1 + 1), "--raw", fn]
+                "--maxdepth", "5", "--window", "0", str(W), str(y0 - 1), str(y1 + 1), "--raw", fn]   # x0 < 0 = no window
         procs.append((y0, y1, fn, subprocess.Popen(args, cwd=SCENES, stdout=subprocess.DEVNULL)))
     film = None
     for y0, y1, fn, p in procs:

@@ -53,6 +53,15 @@ Fixtures (numpy .npz, inputs + expected outputs only):
                                   normal maps (image, scaled, constant)
   animcam_*                       tests/scenes/animcam.pbrt: an animated camera (AnimatedTransform
                                   CameraToWorld interpolated per ray, camera.cpp:84-103)
+  textured_*                      tests/scenes/textured.pbrt: every material parameter as a texture
+                                  (two textured spectra per material, textured roughness / sigma /
+                                  index, metal eta / k unclamped), path and DirectLighting
+  envmap_*                        tests/scenes/envmap.pbrt: an image-based infinite light (decoded PFM
+                                  lat-long map: radiance MIPMap, Distribution2D sampling and pdf)
+  <scene>_rgb_*                   the RGB build (brgb harness, Spectrum = RGBSpectrum) on imagemap,
+                                  textured, envmap, coverage and merl: image textures and normal
+                                  maps, RGBSpectrum::FromSampled (SPD metals, sampled operands), the
+                                  environment map, MERL tables; DirectLighting on envmap / coverage
   coverage_gpupath_dat_40x32s4.npz   the .dat the reference's own spectral film writes for
                                   tests/scenes/coverage.pbrt (--refdat, the scene's integrator): the
                                   end-to-end check of Renderer "gpupath" (tests/test_binding_gpu.py)
@@ -61,7 +70,7 @@ Fixtures (numpy .npz, inputs + expected outputs only):
                                   pixel holds all of its contributions (incl. exact-boundary samples
                                   of its neighbours, spectralImage.cpp:77-152); C2 at the sphere
                                   light's edge and at a killeroo silhouette, C3-C5 at an edge each
-Usage: python tools/make_golden.py [--only keys|dat|merl|dl|meta|spec|rgb|b30|window|imagemap|animcam|gpupath]
+Usage: python tools/make_golden.py [--only keys|dat|merl|dl|meta|spec|rgb|rgbfeat|b30|window|imagemap|animcam|gpupath|textured|envmap]
        (after `make -C oracle ref`, `ref60`, `ref30` and `refrgb`)
 """
 import os
@@ -138,6 +147,27 @@ def rgb_fixtures(tmp):
     paths_fixture("killeroo_rgb_paths_48x40s4", (48, 40), 4, 0, 5, 1, tmp, bands=3)
     film_fixture("killeroo_rgb_film_40x32s8", (40, 32), 8, 0, 5, tmp, bands=3)
     keys_fixture("killeroo_rgb_keys_c1_400x400s64", "killeroo-simple.pbrt", 400, 400, 64, 3, 1, tmp)
+
+
+def rgbfeat_fixtures(tmp):
+    """The RGB build (Spectrum = RGBSpectrum) on the feature scenes: decoded image textures and
+    normal / bump maps, textured material parameters (sampled-spectrum operands through
+    RGBSpectrum::FromSampled), the image-based environment light, the coverage scene (SPD metals,
+    every light type), a RegularHalfangle MERL table; path integrator and DirectLighting"""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import make_merl
+    sd = os.path.join(ROOT, "tests", "scenes")
+    make_merl.write(os.path.join(sd, "synthetic.merl"))   # git-ignored, regenerated here
+    for stem, scene, md in (("imagemap", "imagemap.pbrt", 3), ("textured", "textured.pbrt", 5),
+                            ("envmap", "envmap.pbrt", 5), ("coverage", "coverage.pbrt", 6), ("merl", "merl.pbrt", 5)):
+        sc = os.path.join(sd, scene)
+        paths_fixture("%s_rgb_paths_64x48s4" % stem, (64, 48), 4, 0, md, 1, tmp, scene=sc, bands=3)
+        film_fixture("%s_rgb_film_64x48s4" % stem, (64, 48), 4, 0, md, tmp, scene=sc, bands=3)
+    for stem, scene in (("envmap", "envmap.pbrt"), ("coverage", "coverage.pbrt")):
+        sc = os.path.join(sd, scene)
+        ex = ("--surf", "directlighting", "--dl-strategy", "all")
+        paths_fixture("%s_rgb_dl_paths_48x36s4" % stem, (48, 36), 4, 0, 5, 1, tmp, scene=sc, bands=3, extra=ex)
+        film_fixture("%s_rgb_dl_film_48x36s4" % stem, (48, 36), 4, 0, 5, tmp, scene=sc, bands=3, extra=ex)
 
 
 def spectra_fixture(bands, tmp):
@@ -306,6 +336,30 @@ def imagemap_fixtures(tmp):
     paths_fixture("imagemap_paths_96x72s2_seed5", (96, 72), 2, 5, 3, 2, tmp, scene=sc)
 
 
+def textured_fixtures(tmp):
+    """tests/scenes/textured.pbrt: every material parameter as a texture -- two textured spectra
+    per material, textured roughness / sigma / u-v roughness / index, metal's unclamped eta and k"""
+    sc = os.path.join(ROOT, "tests", "scenes", "textured.pbrt")
+    paths_fixture("textured_paths_64x48s4", (64, 48), 4, 0, 5, 1, tmp, scene=sc)
+    film_fixture("textured_film_64x48s8", (64, 48), 8, 0, 5, tmp, scene=sc)
+    paths_fixture("textured_dl_paths_48x36s4", (48, 36), 4, 0, 5, 1, tmp, scene=sc,
+                  extra=("--surf", "directlighting", "--dl-strategy", "all"))
+    film_fixture("textured_dl_film_48x36s4", (48, 36), 4, 0, 5, tmp, scene=sc,
+                 extra=("--surf", "directlighting", "--dl-strategy", "all"))
+
+
+def envmap_fixtures(tmp):
+    """tests/scenes/envmap.pbrt: an image-based InfiniteAreaLight (a decoded PFM lat-long map: its
+    radiance MIPMap and Distribution2D), path integrator and DirectLighting"""
+    sc = os.path.join(ROOT, "tests", "scenes", "envmap.pbrt")
+    paths_fixture("envmap_paths_64x48s4", (64, 48), 4, 0, 5, 1, tmp, scene=sc)
+    film_fixture("envmap_film_64x48s8", (64, 48), 8, 0, 5, tmp, scene=sc)
+    paths_fixture("envmap_dl_paths_48x36s4", (48, 36), 4, 0, 5, 1, tmp, scene=sc,
+                  extra=("--surf", "directlighting", "--dl-strategy", "all"))
+    film_fixture("envmap_dl_film_48x36s4", (48, 36), 4, 0, 5, tmp, scene=sc,
+                 extra=("--surf", "directlighting", "--dl-strategy", "all"))
+
+
 def animcam_fixtures(tmp):
     """tests/scenes/animcam.pbrt: an animated CameraToWorld (coverage.pbrt's world)"""
     sc = os.path.join(ROOT, "tests", "scenes", "animcam.pbrt")
@@ -351,6 +405,8 @@ def main():
                 spec_fixtures(tmp)
             elif only == "rgb":
                 rgb_fixtures(tmp)
+            elif only == "rgbfeat":
+                rgbfeat_fixtures(tmp)
             elif only == "b30":
                 b30_fixtures(tmp)
             elif only == "imagemap":
@@ -359,6 +415,10 @@ def main():
                 animcam_fixtures(tmp)
             elif only == "gpupath":
                 gpupath_fixture(tmp)
+            elif only == "textured":
+                textured_fixtures(tmp)
+            elif only == "envmap":
+                envmap_fixtures(tmp)
             elif only == "window":
                 sel = sys.argv[3:]
                 for cfg in WINDOW_CONFIGS:
@@ -397,6 +457,8 @@ def main():
         imagemap_fixtures(tmp)
         animcam_fixtures(tmp)
         gpupath_fixture(tmp)
+        textured_fixtures(tmp)
+        envmap_fixtures(tmp)
         dl_fixtures(tmp)
         meta_fixtures(tmp)
         spec_fixtures(tmp)

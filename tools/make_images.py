@@ -57,6 +57,18 @@ def main():
     nz = np.sqrt(np.maximum(0.0, 1.0 - nx * nx - ny * ny))
     nrm = np.stack([(nx + 1) * 127.5, (ny + 1) * 127.5, (nz + 1) * 127.5], -1).round().clip(0, 255)
     tga(os.path.join(out, "normal8x8.tga"), nrm)
+    # tests/scenes/textured.pbrt: a glass index map (Pf, values 1.25 - 1.75) and a roughness map
+    y, x = np.mgrid[0:4, 0:6]
+    pfm(os.path.join(out, "index6x4.pfm"), (1.25 + 0.08 * x + 0.05 * y)[..., None].astype(np.float32), -1.0)
+    y, x = np.mgrid[0:3, 0:7]
+    pfm(os.path.join(out, "rough7x3.pfm"), (0.01 + 0.04 * ((x * 3 + y * 5) % 7))[..., None].astype(np.float32), 1.0)
+    # an environment map (lat-long PF RGB, 16 x 8): a bright warm patch over a blue-grey sky (the
+    # InfiniteAreaLight's radiance MIPMap and Distribution2D, infinite.cpp:60-114)
+    y, x = np.mgrid[0:8, 0:16]
+    sky = np.stack([0.2 + 0.02 * x, 0.25 + 0.03 * y, 0.45 + 0.01 * (x + y)], -1)
+    sky[1:3, 4:7] = [6.0, 5.0, 3.5]
+    sky[6, 12] = [0.0, 0.0, 0.0]
+    pfm(os.path.join(out, "env16x8.pfm"), sky.astype(np.float32), -1.0)
 
 
 if __name__ == "__main__":

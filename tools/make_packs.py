@@ -29,6 +29,10 @@ PACKS = [
     ("imagemap", os.path.join(ROOT, "tests", "scenes", "imagemap.pbrt"), 32, 64, 48, 4),
     # an animated camera (coverage.pbrt's world)
     ("animcam", os.path.join(ROOT, "tests", "scenes", "animcam.pbrt"), 32, 64, 48, 4),
+    # every material parameter as a texture (two textured spectra, textured floats, raw metal eta / k)
+    ("textured", os.path.join(ROOT, "tests", "scenes", "textured.pbrt"), 32, 64, 48, 4),
+    # an image-based infinite light (decoded lat-long PFM: radiance MIPMap + Distribution2D)
+    ("envmap", os.path.join(ROOT, "tests", "scenes", "envmap.pbrt"), 32, 64, 48, 4),
 ]
 
 
@@ -41,7 +45,7 @@ def main():
             continue
         # the configs render with "path" (SURVEY App. B); load a pack with integrator="directlighting"
         # to render it with the DirectLightingIntegrator the scene files name
-        s = pg.Scene.load(os.path.join(REF, fn), xres=xr, yres=yr, spp=spp, maxdepth=-1 if name.startswith(("coverage", "imagemap", "animcam")) else 5,
+        s = pg.Scene.load(os.path.join(REF, fn), xres=xr, yres=yr, spp=spp, maxdepth=-1 if name.startswith(("coverage", "imagemap", "animcam", "textured", "envmap")) else 5,
                           bands=bands, integrator="path")
         path = os.path.join(out, name + ".pack")
         s.save_pack(path)

@@ -21,7 +21,7 @@ import sys
 NAMES = {"k_trace_closest": ("k_trace_pt<false, false>", "k_trace_closest<false, true>", "k_trace_inst<false, false>",
                              "k_trace_c4<false>"),
          "k_trace_shadow": ("k_trace_pt<true, false>", "k_trace_shadow<false, true>", "k_trace_inst<true, false>",
-                            "k_trace_s4<false>"),
+                            "k_trace_s4<false>", "k_trace_s4q<false>"),
          "k_shade": ("k_shade<", "k_dl_nee<", "k_dl_spec<", "k_regen<"),
          "k_accum": ("k_accum<",)}
 
