@@ -431,113 +431,131 @@ PGD_INLINE int kd_next(const float4 &a, const float4 &b, int cur, int prev, bool
 // The radius the reference's retry loop ends at, without its retries: the loop walks at
 // maxDist2 = .001f * 2^k for k = 0, 1, ... and stops at the first k with more than 2 samples
 // strictly inside, or at k = 11 (maxDist2 = 2.048 > 1.5).  That k is the first with
-// d3 < .001f * 2^k, d3 the third-smallest sample distance^2, which one 3-nearest walk finds
-// (pruning far children at the current third-best: a sample beyond a split plane is at least
-// the plane's float distance^2 away, the float subtraction and sums being monotonic).  The
-// samples found are then accumulated by the reference's own walk at that radius, so the sum and
-// its order are the reference's.  C3's points needed ~3-4 walks of growing radius each.
-// The 3-nearest walk visits a node's own sample when it first arrives there (pre-order), before
-// its children: the bound d3 tightens on the way down and prunes far children early (the
-// reference's own walk, below, must visit children first; this one only finds d3, which does
-// not depend on the order).
-template <class NodePtr>
-PGD_INLINE float kd_final_radius(NodePtr nodes, float p0, float p1, float p2) {
-    const float capD2 = .001f * 1024.f;   // k = 10; beyond it the loop ends at k = 11 regardless
-    float d1 = capD2, d2 = capD2, d3 = capD2;
-    int cur = 0, prev = -1;
+// d3 < .001f * 2^k, d3 the third-smallest sample distance^2 (C3's points needed ~3-4 walks of
+// growing radius each in the reference).
+PGD_INLINE float kd_radius_of(float d3) {
+    float m = .001f;
+    for (int k = 0; k < 11 && !(d3 < m); ++k) m *= 2.f;
+    return m;
+}
+// One walk finds d3 and the samples the reference's final walk accumulates, in its order:
+//   * A node's own sample is compared on arrival (pre-order): d1 <= d2 <= d3 keep the three
+//     smallest distances (capped at .001f * 1024, beyond which the radius is 2.048 regardless),
+//     and the pruning bound is kd_radius_of(d3) -- never below the final radius, which it becomes
+//     once d3 is final.  A pruned far child holds only samples at least its split plane's float
+//     distance^2 away (the float subtraction and the sums of squares are monotonic), so pruning
+//     at any bound >= the final radius loses none of them.
+//   * The walk's order is the reference's (children first, near child before far child, then the
+//     node; near / far fixed by the split), so its post-order visits of the nodes the final walk
+//     visits come in the final walk's order; it visits more nodes early, while the bound is
+//     looser, and every node it leaves within the bound of that moment is a candidate.  The
+//     candidates are kept in the slot's M bands (4 NQ indices, the lookup's own output), then
+//     re-tested against the final radius and accumulated in that order -- the reference's sum.
+//   * More candidates than fit: the final walk is run as such at the final radius.
+// Against a radius walk followed by the final walk, about half the node visits (C3: each visit a
+// dependent LDS read, and a wave waits for its slowest lane).
+template <int NB, class NodePtr>
+PGD_INLINE void kd_accumulate(NodePtr nodes, const float *__restrict__ spectra, int node, float p0, float p1, float p2,
+                              float maxD2, float4 *acc, float &sumWeights) {
+    constexpr int NQ = Bands<NB>::NQ;
+    const float4 a = kd_node(nodes, 2 * node), b = kd_node(nodes, 2 * node + 1);
+    const V d = vsub(v3(a.x, a.y, a.z), v3(p0, p1, p2));
+    const float dist2 = vlen2(d);
+    if (dist2 < maxD2) {
+        const float weight = libmf_expf(-100.f * dist2);   // glibc expf, inline
+        const float4 *sv = reinterpret_cast<const float4 *>(spectra + __float_as_int(b.x));
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            const float4 sq = sv[q];
+            acc[q].x += weight * sq.x; acc[q].y += weight * sq.y;
+            acc[q].z += weight * sq.z; acc[q].w += weight * sq.w;
+        }
+        sumWeights += weight;
+    }
+}
+template <int NB, class NodePtr>
+PGD_INLINE void kd_lookup(NodePtr nodes, const float *__restrict__ spectra, float p0, float p1, float p2,
+                          float4 *__restrict__ mb, size_t c) {
+    constexpr int NQ = Bands<NB>::NQ;
+    float4 acc[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) acc[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+    float sumWeights = 0.f;
+#ifdef PGD_KD_RETRY   // the reference's retry loop (timing comparison)
+    float maxD2 = .001f;
+    for (;;) {
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) acc[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+        sumWeights = 0.f;
+        int nFound = 0, cur = 0, prev = -1;
+        bool down = true;
+        for (;;) {
+            const float4 a = kd_node(nodes, 2 * cur), b = kd_node(nodes, 2 * cur + 1);
+            const int nxt = kd_next(a, b, cur, prev, down, p0, p1, p2, maxD2);
+            if (nxt >= 0) { prev = cur; cur = nxt; down = true; continue; }
+            if (vlen2(vsub(v3(a.x, a.y, a.z), v3(p0, p1, p2))) < maxD2) ++nFound;
+            kd_accumulate<NB>(nodes, spectra, cur, p0, p1, p2, maxD2, acc, sumWeights);
+            if (cur == 0) break;
+            prev = cur; cur = __float_as_int(b.z); down = false;
+        }
+        if (nFound > 2 || maxD2 > 1.5f) break;
+        maxD2 *= 2.f;
+    }
+#else
+    constexpr int CAP = 4 * NQ;
+    float *cand = reinterpret_cast<float *>(mb);   // candidate j: component j & 3 of mb[(j >> 2) * c]
+    const float capD2 = .001f * 1024.f;
+    float d1 = capD2, d2 = capD2, d3 = capD2, bound = kd_radius_of(capD2);
+    int n = 0, cur = 0, prev = -1;
     bool down = true;
     for (;;) {
         const float4 a = kd_node(nodes, 2 * cur), b = kd_node(nodes, 2 * cur + 1);
-        if (down) {
-            const V d = vsub(v3(a.x, a.y, a.z), v3(p0, p1, p2));
-            const float dist2 = vlen2(d);
-            if (dist2 < d3) {   // keep d1 <= d2 <= d3 the three smallest
-                d3 = fminf(fmaxf(dist2, d2), d3);
-                d2 = fminf(fmaxf(dist2, d1), d2);
-                d1 = fminf(dist2, d1);
-            }
+        const V d = vsub(v3(a.x, a.y, a.z), v3(p0, p1, p2));
+        const float dist2 = vlen2(d);
+        if (down && dist2 < d3) {   // keep d1 <= d2 <= d3 the three smallest
+            d3 = fminf(fmaxf(dist2, d2), d3);
+            d2 = fminf(fmaxf(dist2, d1), d2);
+            d1 = fminf(dist2, d1);
+            bound = kd_radius_of(d3);
         }
-        const int nxt = kd_next(a, b, cur, prev, down, p0, p1, p2, d3);
+        const int nxt = kd_next(a, b, cur, prev, down, p0, p1, p2, bound);
         if (nxt >= 0) {
             prev = cur;
             cur = nxt;
             down = true;
             continue;
         }
+        if (dist2 < bound) {   // post-order: a candidate of the final walk
+            if (n < CAP) cand[(size_t)(n >> 2) * 4 * c + (n & 3)] = __int_as_float(cur);
+            ++n;
+        }
         if (cur == 0) break;
         prev = cur;
         cur = __float_as_int(b.z);
         down = false;
     }
-    float maxD2 = .001f;
-    for (int k = 0; k < 11 && !(d3 < maxD2); ++k) maxD2 *= 2.f;
-    return maxD2;
-}
-template <int NB, class NodePtr>
-PGD_INLINE void kd_lookup(NodePtr nodes, const float *__restrict__ spectra, float p0, float p1, float p2,
-                          float4 *__restrict__ mb, size_t c) {
-    constexpr int NQ = Bands<NB>::NQ;
-#ifdef PGD_KD_RETRY   // the reference's retry loop (timing comparison)
-    float maxD2 = .001f;
-    for (;;) {
-#elif defined(PGD_EXP_KD_FIXED)   // timing experiment only: no radius walk (wrong radiance)
-    const float maxD2 = PGD_EXP_KD_FIXED;
-    {
-#else
-    const float maxD2 = kd_final_radius(nodes, p0, p1, p2);
-    {
-#endif
-        float4 acc[NQ];
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) acc[q] = make_float4(0.f, 0.f, 0.f, 0.f);
-        float sumWeights = 0.f;
-        int nFound = 0;
-        int cur = 0, prev = -1;
-        bool down = true;
+    const float maxD2 = bound;
+    if (n <= CAP) {
+        for (int j = 0; j < n; ++j)
+            kd_accumulate<NB>(nodes, spectra, __float_as_int(cand[(size_t)(j >> 2) * 4 * c + (j & 3)]), p0, p1, p2, maxD2,
+                              acc, sumWeights);
+    } else {   // the final walk itself
+        cur = 0; prev = -1; down = true;
         for (;;) {
             const float4 a = kd_node(nodes, 2 * cur), b = kd_node(nodes, 2 * cur + 1);
             const int nxt = kd_next(a, b, cur, prev, down, p0, p1, p2, maxD2);
-            if (nxt >= 0) {
-                prev = cur;
-                cur = nxt;
-                down = true;
-                continue;
-            }
-            // the node itself, after its children
-            const V d = vsub(v3(a.x, a.y, a.z), v3(p0, p1, p2));
-            const float dist2 = vlen2(d);
-            if (dist2 < maxD2) {
-                const float weight = libmf_expf(-100.f * dist2);   // glibc expf, inline
-                const float4 *sv = reinterpret_cast<const float4 *>(spectra + __float_as_int(b.x));
-#pragma unroll
-                for (int q = 0; q < NQ; ++q) {
-                    const float4 sq = sv[q];
-                    acc[q].x += weight * sq.x; acc[q].y += weight * sq.y;
-                    acc[q].z += weight * sq.z; acc[q].w += weight * sq.w;
-                }
-                sumWeights += weight;
-                ++nFound;
-            }
+            if (nxt >= 0) { prev = cur; cur = nxt; down = true; continue; }
+            kd_accumulate<NB>(nodes, spectra, cur, p0, p1, p2, maxD2, acc, sumWeights);
             if (cur == 0) break;
-            prev = cur;
-            cur = __float_as_int(b.z);
-            down = false;
+            prev = cur; cur = __float_as_int(b.z); down = false;
         }
-#ifdef PGD_KD_RETRY
-        if (!(nFound > 2 || maxD2 > 1.5f)) {
-            maxD2 *= 2.f;
-            continue;
-        }
+    }
 #endif
 #pragma unroll
-        for (int q = 0; q < NQ; ++q) {
-            const float4 v = acc[q];
-            mb[q * c] = make_float4(clampf(v.x, 0.f, INFINITY) / sumWeights, clampf(v.y, 0.f, INFINITY) / sumWeights,
-                                    clampf(v.z, 0.f, INFINITY) / sumWeights, clampf(v.w, 0.f, INFINITY) / sumWeights);
-        }
-#ifdef PGD_KD_RETRY
-        return;
-#endif
+    for (int q = 0; q < NQ; ++q) {
+        const float4 v = acc[q];
+        mb[q * c] = make_float4(clampf(v.x, 0.f, INFINITY) / sumWeights, clampf(v.y, 0.f, INFINITY) / sumWeights,
+                                clampf(v.z, 0.f, INFINITY) / sumWeights, clampf(v.w, 0.f, INFINITY) / sumWeights);
     }
 }
 template <int NB>

@@ -59,7 +59,10 @@ def render_frame(scene, W, H, spp, bands, jobs, tmp):
         y0, y1 = int(strips[j]), int(strips[j + 1])
         fn = os.path.join(tmp, "strip%d.f32" % j)
         args = [exe, os.path.join(SCENES, scene), "--res", str(W), str(H), "--spp", str(spp), "--seed", "0",
-                "--maxdepth", "5", "--window", "0", str(W), str(y0 - 1), str(y1 + 1), "--raw", fn]   # x0 < 0 = no window
+                "--maxdepth", "5", "--window", "0", str(W + 1), str(y0 - 1), str(y1 + 1), "--raw", fn]
+        # sample pixels [0, W + 1) x [y0 - 1, y1 + 1) (end-exclusive; x0 < 0 would mean no window): the
+        # sample extent ends at W + 1 (film.cpp GetSampleExtent), and samples at exactly x = W land on
+        # film pixel W - 1
         procs.append((y0, y1, fn, subprocess.Popen(args, cwd=SCENES, stdout=subprocess.DEVNULL)))
     film = None
     for y0, y1, fn, p in procs:
