@@ -58,6 +58,8 @@ CONFIGS = {
     "c2": ("killeroo-simple.pack", "killeroo-simple SampledSpectrum %d bands, path maxdepth %d, %dspp, %dx%d"),
     "c3": ("bunny.pack", "bunny (mystique measured BRDF) SampledSpectrum %d bands, path maxdepth %d, %dspp, %dx%d"),
     "c4": ("metal.pack", "metal (Au conductor, env light) SampledSpectrum %d bands, path maxdepth %d, %dspp, %dx%d"),
+    # not a BASELINE config: C2's scene in the 60-band build (the plain 60-band kernels, e.g. DirectLighting)
+    "c2_b60": ("killeroo-simple-b60.pack", "killeroo-simple SampledSpectrum %d bands, path maxdepth %d, %dspp, %dx%d"),
     "c5": ("anim-killeroos-moving.pack",
            "anim-killeroos-moving (motion-blur BVHs) SampledSpectrum %d bands, path maxdepth %d, %dspp, %dx%d"),
 }

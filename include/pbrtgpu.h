@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define PBRTGPU_ABI_VERSION 14
+#define PBRTGPU_ABI_VERSION 15
 #define PBRTGPU_MAX_BANDS 64
 
 #define PBRTGPU_E_INVALID   (-1)
@@ -144,15 +144,19 @@ typedef struct pbrtgpu_material {
     int32_t ftex[2];      /* float texture of f[0], f[1], or -1 (ABI 13; packs before v14 hold -1) */
 } pbrtgpu_material;
 
-enum { PBRTGPU_LIGHT_AREA = 0, PBRTGPU_LIGHT_POINT = 1, PBRTGPU_LIGHT_INFINITE = 2 };
+/* area (DiffuseAreaLight), point (PointLight), infinite (InfiniteAreaLight), spot (SpotLight,
+ * lights/spot.cpp), distant (DistantLight, lights/distant.cpp) */
+enum { PBRTGPU_LIGHT_AREA = 0, PBRTGPU_LIGHT_POINT = 1, PBRTGPU_LIGHT_INFINITE = 2, PBRTGPU_LIGHT_SPOT = 3,
+       PBRTGPU_LIGHT_DISTANT = 4 };
 
 typedef struct pbrtgpu_light {
     int32_t type;
-    int32_t spec;          /* Lemit (area) / intensity (point) / L (infinite), offset into spectra[] */
+    int32_t spec;          /* Lemit (area) / intensity (point, spot) / L (infinite, distant), offset into spectra[] */
     int32_t shape_offset;  /* area: first entry in light_shapes[] (ShapeSet, light.cpp:114-135) */
     int32_t n_shapes;
     float sum_area;        /* ShapeSet::sumArea */
-    float pos[3];          /* point light position LightToWorld(0,0,0) */
+    float pos[3];          /* point / spot: the position LightToWorld(0,0,0); distant: lightDir =
+                            * Normalize(LightToWorld(from - to)) */
     int32_t is_black;      /* emitted spectrum IsBlack() */
     int32_t n_samples;     /* Light::nSamples = max(1, "nsamples") (light.h:45); DirectLighting's
                             * strategy "all" takes RoundUpPow2 of it (LDSampler::RoundSize) */
@@ -167,7 +171,8 @@ typedef struct pbrtgpu_light {
      * single texel (RGB, after L.ToRGBSpectrum()) with its wrap mode; Distribution2D of the
      * one-texel image: map_pdf = SampleContinuous's pdf, dist_pdf = Distribution2D::Pdf.  With
      * map_tex: dist_nu x dist_nv, the image's own resolution (before the MIPMap's resampling). */
-    float texel[3];
+    float texel[3];        /* spot: texel[0] = cosTotalWidth, texel[1] = cosFalloffStart (spot.cpp:35-36);
+                            * l2w_m / l2w_minv its LightToWorld / WorldToLight */
     float map_pdf, dist_pdf;
     int32_t wrap, dist_nu, dist_nv;
 } pbrtgpu_light;

@@ -1749,7 +1749,8 @@ static float inf_pdf(const Ctx *c, const pbrtgpu_light *L, V w) {
     float dp = L->map_tex >= 0 ? dist2d_pdf(c, L, spherical_phi(wi) * INV_TWOPI_F, theta * INV_PI_F) : L->dist_pdf;
     return dp / (2.f * PI_F * PI_F * sintheta);
 }
-/* Light::Sample_L (diffuse.cpp:61-74, point.cpp:42-49, infinite.cpp:155-185); returns Li into Li[] */
+/* Light::Sample_L (diffuse.cpp:61-74, point.cpp:42-49, spot.cpp:41-48, distant.cpp:39-46,
+ * infinite.cpp:155-185); returns Li into Li[] */
 static void light_sample_L(const Ctx *c, const pbrtgpu_light *L, V p, float pEps, const float u[3], float time,
                            V *wi, float *pdf, Seg *vis, float *Li) {
     int nb = c->nb;
@@ -1784,6 +1785,32 @@ static void light_sample_L(const Ctx *c, const pbrtgpu_light *L, V p, float pEps
         for (int i = 0; i < nb; ++i) Li[i] = Ls[i] / d2;
         return;
     }
+    if (L->type == PBRTGPU_LIGHT_SPOT) {   /* spot.cpp:41-48: Intensity * Falloff(-wi) / DistanceSquared */
+        V lp = v3(L->pos[0], L->pos[1], L->pos[2]);
+        *wi = vnorm(vsub(lp, p));
+        *pdf = 1.f;
+        float dist = vlen(vsub(p, lp));
+        vis->o = p; vis->d = vdiv(vsub(lp, p), dist); vis->mint = pEps; vis->maxt = dist * (1.f - 0.f);
+        /* Falloff (spot.cpp:51-60): wl = Normalize(WorldToLight(w)) */
+        V wl = vnorm(xvec(L->l2w_minv, vneg(*wi)));
+        float fo;
+        if (wl.z < L->texel[0]) fo = 0.f;
+        else if (wl.z > L->texel[1]) fo = 1.f;
+        else {
+            float delta = (wl.z - L->texel[0]) / (L->texel[1] - L->texel[0]);
+            fo = delta * delta * delta * delta;
+        }
+        float d2 = vlen2(vsub(lp, p));
+        for (int i = 0; i < nb; ++i) Li[i] = (Ls[i] * fo) / d2;
+        return;
+    }
+    if (L->type == PBRTGPU_LIGHT_DISTANT) {   /* distant.cpp:39-46: L, toward lightDir */
+        *wi = v3(L->pos[0], L->pos[1], L->pos[2]);
+        *pdf = 1.f;
+        vis->o = p; vis->d = *wi; vis->mint = pEps; vis->maxt = INFINITY;   /* VisibilityTester::SetRay */
+        for (int i = 0; i < nb; ++i) Li[i] = Ls[i];
+        return;
+    }
     /* area: ShapeSet::Sample(p, ls, &ns) (light.cpp:137-151) */
     const pbrtgpu_light_shape *shs = c->s->light_shapes + L->shape_offset;
     int sn = sample_discrete(shs, L->n_shapes, u[2]);
@@ -1814,14 +1841,16 @@ static void light_sample_L(const Ctx *c, const pbrtgpu_light *L, V p, float pEps
     else for (int i = 0; i < nb; ++i) Li[i] = 0.f;
 }
 static float light_pdf(const Ctx *c, const pbrtgpu_light *L, V p, V wi) {
-    if (L->type == PBRTGPU_LIGHT_POINT) return 0.;
+    if (L->type == PBRTGPU_LIGHT_POINT || L->type == PBRTGPU_LIGHT_SPOT || L->type == PBRTGPU_LIGHT_DISTANT) return 0.;
     if (L->type == PBRTGPU_LIGHT_INFINITE) return inf_pdf(c, L, wi);
     const pbrtgpu_light_shape *shs = c->s->light_shapes + L->shape_offset;
     float pp = 0.f;
     for (int i = 0; i < L->n_shapes; ++i) pp += shs[i].area * shape_pdf(c, shs[i].shape_type, shs[i].shape_index, p, wi);
     return pp / L->sum_area;
 }
-static inline int light_is_delta(const pbrtgpu_light *L) { return L->type == PBRTGPU_LIGHT_POINT; }
+static inline int light_is_delta(const pbrtgpu_light *L) {   /* Light::IsDeltaLight: point, spot, distant */
+    return L->type == PBRTGPU_LIGHT_POINT || L->type == PBRTGPU_LIGHT_SPOT || L->type == PBRTGPU_LIGHT_DISTANT;
+}
 /* AreaLight::L via Intersection::Le (intersection.cpp:53-57, diffuse.h:43-45) */
 static void isect_Le(const Ctx *c, const Isect *is, V w, float *out) {
     int al = c->s->prims[is->prim].area_light;

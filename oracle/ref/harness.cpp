@@ -67,6 +67,8 @@
 #include "lights/diffuse.h"
 #include "lights/point.h"
 #include "lights/infinite.h"
+#include "lights/spot.h"
+#include "lights/distant.h"
 #include "materials/matte.h"
 #include "materials/plastic.h"
 #include "materials/metal.h"
@@ -453,6 +455,8 @@ void pbrtLightSource(const string &n, const ParamSet &p) {
     Light *lt = NULL;
     if (n == "point") lt = CreatePointLight(curT[0], p);
     else if (n == "infinite" || n == "exinfinite") lt = CreateInfiniteLight(curT[0], p);
+    else if (n == "spot") lt = CreateSpotLight(curT[0], p);
+    else if (n == "distant") lt = CreateDistantLight(curT[0], p);
     else { fprintf(stderr, "harness: light %s unsupported\n", n.c_str()); exit(2); }
     lights.push_back(lt);
 }

@@ -2281,7 +2281,9 @@ struct Seg { V o, d; float mint, maxt; };
 // The radiance a light sample or a missed ray brings: a pool spectrum (divided by `div` for a
 // point light's 1/d^2), FromRGB(illuminant) of an environment-map lookup, or black
 enum { EM_BLACK = 0, EM_POOL = 1, EM_RGB = 2 };
-struct Emit { int mode; int off; float div; bool point; RGBPick pick; };
+// point (a delta light: PointLight, SpotLight, DistantLight): the pool spectrum times mul (the
+// spot's Falloff) divided by div (the squared distance; 1 for the distant light)
+struct Emit { int mode; int off; float div; bool point; RGBPick pick; float mul = 1.f; };
 // InfiniteAreaLight (lights/infinite.cpp): its radiance map is one texel (an unreadable or
 // non-TGA / PFM mapname, or none) or a decoded image's MIPMap (map_tex) with its Distribution2D
 PGD_INLINE float spherical_theta(V v) { return ACOSF(clampf(v.z, -1.f, 1.f)); }   // geometry.h:642-650
@@ -2337,7 +2339,17 @@ PGD_INLINE float dist2d_pdf(const DevScene &S, const pbrtgpu_light &L, float u, 
     if (R[0] * M[0] == 0.f) return 0.f;
     return (R[1 + iu] * M[1 + iv]) / (R[0] * M[0]);
 }
-// Light::Sample_L (diffuse.cpp:61-74, point.cpp:42-49, infinite.cpp:155-185)
+// SpotLight::Falloff (spot.cpp:51-60): 0 outside the cone, 1 inside the falloff start, a quartic between
+PGD_INLINE float spot_falloff(const pbrtgpu_light &L, V w) {
+    const V wl = vnorm(xvec(L.l2w_minv, w));   // Normalize(WorldToLight(w))
+    const float costheta = wl.z, cosTotal = L.texel[0], cosFalloff = L.texel[1];
+    if (costheta < cosTotal) return 0.f;
+    if (costheta > cosFalloff) return 1.f;
+    const float delta = (costheta - cosTotal) / (cosFalloff - cosTotal);
+    return delta * delta * delta * delta;
+}
+// Light::Sample_L (diffuse.cpp:61-74, point.cpp:42-49, spot.cpp:41-48, distant.cpp:39-46,
+// infinite.cpp:155-185)
 template <int FEAT>
 PGD_HEAVY void light_sample_L(const DevScene &S, const pbrtgpu_light &L, V p, float pEps, const float u[3], V *wi,
                               float *pdf, Seg *vis, Emit *em) {
@@ -2362,7 +2374,7 @@ PGD_HEAVY void light_sample_L(const DevScene &S, const pbrtgpu_light &L, V p, fl
         *em = inf_radiance(S, L, uv0, uv1);
         return;
     }
-    if (L.type == PBRTGPU_LIGHT_POINT) {
+    if (L.type == PBRTGPU_LIGHT_POINT || ((FEAT & FEAT_INF) && L.type == PBRTGPU_LIGHT_SPOT)) {
         V lp = v3(L.pos[0], L.pos[1], L.pos[2]);
         *wi = vnorm(vsub(lp, p));
         *pdf = 1.f;
@@ -2370,6 +2382,14 @@ PGD_HEAVY void light_sample_L(const DevScene &S, const pbrtgpu_light &L, V p, fl
         vis->o = p; vis->d = vdiv(vsub(lp, p), dist); vis->mint = pEps; vis->maxt = dist * (1.f - 0.f);
         em->mode = EM_POOL; em->point = true;
         em->div = vlen2(vsub(lp, p));   // Intensity / DistanceSquared
+        if ((FEAT & FEAT_INF) && L.type == PBRTGPU_LIGHT_SPOT) em->mul = spot_falloff(L, vneg(*wi));   // spot.cpp:41-48
+        return;
+    }
+    if ((FEAT & FEAT_INF) && L.type == PBRTGPU_LIGHT_DISTANT) {   // distant.cpp:39-46: L toward lightDir
+        *wi = v3(L.pos[0], L.pos[1], L.pos[2]);
+        *pdf = 1.f;
+        vis->o = p; vis->d = *wi; vis->mint = pEps; vis->maxt = INFINITY;   // VisibilityTester::SetRay
+        em->mode = EM_POOL; em->point = true;
         return;
     }
     const pbrtgpu_light_shape *shs = sa(S.lightShapes, (uint32_t)(L.shape_offset));
@@ -2398,6 +2418,7 @@ PGD_HEAVY void light_sample_L(const DevScene &S, const pbrtgpu_light &L, V p, fl
 template <int FEAT>
 PGD_HEAVY float light_pdf(const DevScene &S, const pbrtgpu_light &L, V p, V wi) {
     if (L.type == PBRTGPU_LIGHT_POINT) return 0.;
+    if ((FEAT & FEAT_INF) && (L.type == PBRTGPU_LIGHT_SPOT || L.type == PBRTGPU_LIGHT_DISTANT)) return 0.;
     if ((FEAT & FEAT_INF) && L.type == PBRTGPU_LIGHT_INFINITE) {   // infinite.cpp:188-197
         V w = xvec(L.l2w_minv, wi);
         const float theta = spherical_theta(w);

@@ -344,7 +344,7 @@ static inline int scene_check(const pbrtgpu_flat_scene *s, std::string *err) {
     if (s->integrator == PBRTGPU_INTEGRATOR_DIRECT && s->dl_strategy != PBRTGPU_DL_ALL && s->dl_strategy != PBRTGPU_DL_ONE)
         SB_FAIL(PBRTGPU_E_INVALID, "unknown DirectLighting strategy");
     for (int i = 0; i < s->n_lights; ++i)
-        if (s->lights[i].type < PBRTGPU_LIGHT_AREA || s->lights[i].type > PBRTGPU_LIGHT_INFINITE)
+        if (s->lights[i].type < PBRTGPU_LIGHT_AREA || s->lights[i].type > PBRTGPU_LIGHT_DISTANT)
             SB_FAIL(PBRTGPU_E_INVALID, "bad light type");
     if (!s->rgb_basis || !s->ewa_lut) SB_FAIL(PBRTGPU_E_INVALID, "rgb_basis / ewa_lut missing");
     // texture graph: SCALE nodes combine CONST / IMAGE leaves; a material's spectrum slot is an
@@ -572,9 +572,11 @@ static int scene_build(const pbrtgpu_flat_scene *s, int topNodes, DevScene &S, i
             if (!remap(m.spec[k], &m.spec[k])) SB_FAIL(PBRTGPU_E_INVALID, "material spectrum offset");
     std::vector<pbrtgpu_light> lts(s->lights, s->lights + s->n_lights);
     S.nInf = 0;
+    int nSpotDistant = 0;
     for (auto &l : lts) {
         if (!remap(l.spec, &l.spec)) SB_FAIL(PBRTGPU_E_INVALID, "light spectrum offset");
         if (l.type == PBRTGPU_LIGHT_INFINITE) ++S.nInf;
+        if (l.type == PBRTGPU_LIGHT_SPOT || l.type == PBRTGPU_LIGHT_DISTANT) ++nSpotDistant;
     }
     std::vector<pbrtgpu_texture> texs(s->textures, s->textures + std::max(0, s->n_textures));
     for (auto &t : texs)
@@ -652,7 +654,9 @@ static int scene_build(const pbrtgpu_flat_scene *s, int topNodes, DevScene &S, i
         S.nKd = (int)kd.size();
         S.kdInLds = (S.nKd > 0 && S.nKd <= kKdLdsNodes) ? 1 : 0;
     }
-    *feat = S.nInf > 0 ? FEAT_INF : 0;
+    // FEAT_INF: the light types beyond area and point (infinite, spot, distant) -- the kernels of
+    // scenes with area and point lights only (C2, C3) carry none of their code
+    *feat = (S.nInf > 0 || nSpotDistant > 0) ? FEAT_INF : 0;
     for (int i = 0; i < s->n_materials; ++i) {
         const pbrtgpu_material &m = s->materials[i];
         if (m.type == PBRTGPU_MAT_MEASURED || m.type == PBRTGPU_MAT_MEASURED_HALFANGLE) *feat |= FEAT_MEAS;

@@ -369,7 +369,10 @@ PGD_INLINE float4 emit4(const DevScene &S, const Emit &e, int q) {
     if ((FEAT & FEAT_INF) && e.mode == EM_RGB) return from_rgb4(S, e.pick, true, q);
     if (e.mode == EM_BLACK) return make_float4(0.f, 0.f, 0.f, 0.f);
     float4 v = ld4(S.spectra, e.off + 4 * q);
-    if (e.point) v = make_float4(v.x / e.div, v.y / e.div, v.z / e.div, v.w / e.div);
+    if (e.point) {
+        if (FEAT & FEAT_INF) v = make_float4(v.x * e.mul, v.y * e.mul, v.z * e.mul, v.w * e.mul);   // spot Falloff
+        v = make_float4(v.x / e.div, v.y / e.div, v.z / e.div, v.w / e.div);
+    }
     return v;
 }
 template <int NB, int FEAT>

@@ -1515,6 +1515,38 @@ private:
             V3 lp = l2w.Point(V3(0, 0, 0));
             lo->l.pos[0] = lp.x; lo->l.pos[1] = lp.y; lo->l.pos[2] = lp.z;
             memcpy(lo->l.l2w_m, l2w.m.m, 64); memcpy(lo->l.l2w_minv, l2w.mInv.m, 64);
+        } else if (name == "spot") {   // spot.cpp:32-38, 70-92
+            Spec I = p.FindOneSpectrum("I", spec.Const(1.0f));
+            Spec sc = p.FindOneSpectrum("scale", spec.Const(1.0f));
+            const float coneangle = p.FindOneFloat("coneangle", 30.f);
+            const float conedelta = p.FindOneFloat("conedeltaangle", 5.f);
+            const V3 from = p.FindOnePoint("from", V3(0, 0, 0)), to = p.FindOnePoint("to", V3(0, 0, 1));
+            const V3 dir = Normalize(to - from);
+            V3 du, dv;
+            CoordinateSystem(dir, &du, &dv);
+            M4 d2z;
+            const float rows[4][4] = {{du.x, du.y, du.z, 0.f}, {dv.x, dv.y, dv.z, 0.f}, {dir.x, dir.y, dir.z, 0.f}, {0.f, 0.f, 0.f, 1.f}};
+            for (int i = 0; i < 4; ++i)
+                for (int j = 0; j < 4; ++j) d2z.m[i][j] = rows[i][j];
+            const Xform dirToZ(d2z);
+            const Xform l2w = curT.t[0] * Translate(V3(from.x, from.y, from.z)) * Inverse(dirToZ);
+            lo->l.type = PBRTGPU_LIGHT_SPOT;
+            lo->L = SpecMul(I, sc);
+            const V3 lp = l2w.Point(V3(0, 0, 0));
+            lo->l.pos[0] = lp.x; lo->l.pos[1] = lp.y; lo->l.pos[2] = lp.z;
+            lo->l.texel[0] = cosf(Radians(coneangle));               // cosTotalWidth
+            lo->l.texel[1] = cosf(Radians(coneangle - conedelta));   // cosFalloffStart
+            memcpy(lo->l.l2w_m, l2w.m.m, 64); memcpy(lo->l.l2w_minv, l2w.mInv.m, 64);
+        } else if (name == "distant") {   // distant.cpp:31-36, 56-64
+            Spec L = p.FindOneSpectrum("L", spec.Const(1.0f));
+            Spec sc = p.FindOneSpectrum("scale", spec.Const(1.0f));
+            const V3 from = p.FindOnePoint("from", V3(0, 0, 0)), to = p.FindOnePoint("to", V3(0, 0, 1));
+            const Xform &l2w = curT.t[0];
+            lo->l.type = PBRTGPU_LIGHT_DISTANT;
+            lo->L = SpecMul(L, sc);
+            const V3 d = Normalize(l2w.Vector(from - to));   // lightDir
+            lo->l.pos[0] = d.x; lo->l.pos[1] = d.y; lo->l.pos[2] = d.z;
+            memcpy(lo->l.l2w_m, l2w.m.m, 64); memcpy(lo->l.l2w_minv, l2w.mInv.m, 64);
         } else if (name == "infinite" || name == "exinfinite") {   // infinite.cpp:41-80, 232-245
             Spec L = p.FindOneSpectrum("L", spec.Const(1.0f));
             Spec sc = p.FindOneSpectrum("scale", spec.Const(1.0f));

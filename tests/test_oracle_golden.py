@@ -19,7 +19,7 @@ def _scene(pg, cfg, name="killeroo"):
     w, h, spp, seed, md = [int(v) for v in cfg]
     pack = {"anim": "anim-killeroos-moving.pack", "bunny": "bunny.pack", "metal": "metal.pack",
             "coverage": "coverage.pack", "imagemap": "imagemap.pack",
-            "animcam": "animcam.pack", "textured": "textured.pack", "envmap": "envmap.pack"}.get(name.split("_")[0],
+            "animcam": "animcam.pack", "textured": "textured.pack", "envmap": "envmap.pack", "lights": "lights.pack"}.get(name.split("_")[0],
                                                                                               "killeroo-simple.pack")
     # *_b30_*: the upstream 30-band, 400-700 nm build (b30 harness, spectrum.h.original:36-38)
     if "_b30_" in name:
@@ -35,7 +35,8 @@ def exact_rate(name):
 
 PATHS = ["killeroo_paths_64x64s4", "killeroo_paths_48x48s8_seed7_md7", "anim_paths_48x48s4", "bunny_paths_64x36s4",
          "metal_paths_48x48s4", "coverage_paths_64x48s8", "killeroo_b30_paths_48x40s4", "coverage_b30_paths_48x36s4",
-         "imagemap_paths_64x48s4", "imagemap_paths_96x72s2_seed5", "animcam_paths_64x48s4", "textured_paths_64x48s4", "envmap_paths_64x48s4"]
+         "imagemap_paths_64x48s4", "imagemap_paths_96x72s2_seed5", "animcam_paths_64x48s4", "textured_paths_64x48s4", "envmap_paths_64x48s4",
+         "lights_paths_64x48s4"]
 # the configs at their real size and sample count (BASELINE.json configs 2-5; harness --keys):
 # every sample of a few pixels plus random keys of the whole sample extent
 KEYS = ["killeroo_keys_c2_700x700s256", "bunny_keys_c3_1920x1080s1024", "metal_keys_c4_400x400s4096",
@@ -71,7 +72,8 @@ def test_paths_restated_libm_bit_exact_vs_reference(pg, name):
 @pytest.mark.parametrize("name", ["killeroo_film_96x72s16", "anim_film_40x40s8", "bunny_film_48x27s8",
                                   "metal_film_40x40s8", "coverage_film_64x48s8", "killeroo_b30_film_40x32s8",
                                   "coverage_b30_film_40x30s4", "imagemap_film_64x48s8",
-                                  "animcam_film_64x48s4", "textured_film_64x48s8", "envmap_film_64x48s8"])
+                                  "animcam_film_64x48s4", "textured_film_64x48s8", "envmap_film_64x48s8",
+                                  "lights_film_64x48s8"])
 def test_film_bit_exact_vs_reference(pg, ora_libm, name):
     g = np.load(os.path.join(GOLDEN, name + ".npz"))
     scene = _scene(pg, g["config"], name)
@@ -125,7 +127,7 @@ def test_regular_halfangle_brdf_bit_exact_vs_reference(pg, ora_libm, merl_dir, n
         assert np.array_equal(film.view(np.int32), g["film"].view(np.int32))
 
 
-DL = ["textured_dl_%s_48x36s4", "envmap_dl_%s_48x36s4", "killeroo_dl_%s_48x40s4", "bunny_dl_%s_48x27s4", "anim_dl_%s_40x40s4", "coverage_dl_%s_64x48s4",
+DL = ["lights_dl_%s_48x36s4", "textured_dl_%s_48x36s4", "envmap_dl_%s_48x36s4", "killeroo_dl_%s_48x40s4", "bunny_dl_%s_48x27s4", "anim_dl_%s_40x40s4", "coverage_dl_%s_64x48s4",
       "coverage_dlone_%s_64x48s4"]
 
 
@@ -134,7 +136,7 @@ def dl_scene(pg, g, name):
     files name (packs record "path", the configs' override)."""
     w, h, spp, seed, md = [int(v) for v in g["config"]]
     pack = {"anim": "anim-killeroos-moving.pack", "bunny": "bunny.pack", "coverage": "coverage.pack",
-            "textured": "textured.pack", "envmap": "envmap.pack"}.get(
+            "textured": "textured.pack", "envmap": "envmap.pack", "lights": "lights.pack"}.get(
         name.split("_")[0], "killeroo-simple.pack")
     return pg.Scene.load(os.path.join(PACKS, pack), xres=w, yres=h, spp=spp, maxdepth=md, seed=seed,
                          integrator="directlighting", strategy="one" if "_dlone_" in name else "all")
@@ -264,8 +266,8 @@ def test_rgb_build_bit_exact_vs_reference(pg, ora_libm, name):
 # the RGB build on the feature scenes (tools/make_golden.py --only rgbfeat): image textures and
 # normal maps, textured parameters with sampled-spectrum operands (RGBSpectrum::FromSampled), the
 # image-based environment light, the coverage scene (SPD metals, every light type), MERL tables
-RGBFEAT = ["%s_rgb_paths_64x48s4" % s for s in ("imagemap", "textured", "envmap", "coverage", "merl")] + \
-          ["%s_rgb_film_64x48s4" % s for s in ("imagemap", "textured", "envmap", "coverage", "merl")] + \
+RGBFEAT = ["%s_rgb_paths_64x48s4" % s for s in ("imagemap", "textured", "envmap", "coverage", "merl", "lights")] + \
+          ["%s_rgb_film_64x48s4" % s for s in ("imagemap", "textured", "envmap", "coverage", "merl", "lights")] + \
           ["envmap_rgb_dl_paths_48x36s4", "envmap_rgb_dl_film_48x36s4", "coverage_rgb_dl_paths_48x36s4",
            "coverage_rgb_dl_film_48x36s4"]
 

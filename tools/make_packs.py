@@ -25,6 +25,8 @@ PACKS = [
     # the upstream 30-band, 400-700 nm sampling (spectrum.h.original:36-38; BASELINE's "30 bands")
     ("killeroo-simple-b30", "killeroo-simple.pbrt", 30, 700, 700, 256),
     ("coverage-b30", os.path.join(ROOT, "tests", "scenes", "coverage.pbrt"), 30, 64, 48, 8),
+    # C2's scene in the 60-band build (C4's band count): the 60-band kernels of the plain variants
+    ("killeroo-simple-b60", "killeroo-simple.pbrt", 60, 700, 700, 256),
     # decoded TGA / PFM image maps in MIPMap pyramids (tests/scenes/textures, tools/make_images.py)
     ("imagemap", os.path.join(ROOT, "tests", "scenes", "imagemap.pbrt"), 32, 64, 48, 4),
     # an animated camera (coverage.pbrt's world)
@@ -33,6 +35,8 @@ PACKS = [
     ("textured", os.path.join(ROOT, "tests", "scenes", "textured.pbrt"), 32, 64, 48, 4),
     # an image-based infinite light (decoded lat-long PFM: radiance MIPMap + Distribution2D)
     ("envmap", os.path.join(ROOT, "tests", "scenes", "envmap.pbrt"), 32, 64, 48, 4),
+    # spot and distant lights beside an area light
+    ("lights", os.path.join(ROOT, "tests", "scenes", "lights.pbrt"), 32, 64, 48, 4),
 ]
 
 
@@ -45,7 +49,7 @@ def main():
             continue
         # the configs render with "path" (SURVEY App. B); load a pack with integrator="directlighting"
         # to render it with the DirectLightingIntegrator the scene files name
-        s = pg.Scene.load(os.path.join(REF, fn), xres=xr, yres=yr, spp=spp, maxdepth=-1 if name.startswith(("coverage", "imagemap", "animcam", "textured", "envmap")) else 5,
+        s = pg.Scene.load(os.path.join(REF, fn), xres=xr, yres=yr, spp=spp, maxdepth=-1 if name.startswith(("coverage", "imagemap", "animcam", "textured", "envmap", "lights")) else 5,
                           bands=bands, integrator="path")
         path = os.path.join(out, name + ".pack")
         s.save_pack(path)
