@@ -222,8 +222,11 @@ typedef struct pbrtgpu_camera {
     int32_t xres, yres;
     int32_t px_start, px_count, py_start, py_count;   /* film pixel window */
     int32_t sx_start, sx_end, sy_start, sy_end;       /* sample extent (incl. border) */
-    float dx_camera[3], dy_camera[3];                 /* PerspectiveCamera dxCamera / dyCamera */
-    int32_t pad[2];
+    float dx_camera[3], dy_camera[3];                 /* dxCamera / dyCamera (perspective.cpp:45-48,
+                                                       * orthographic.cpp:39-40) */
+    int32_t ortho;        /* 1: OrthoCamera (cameras/orthographic.cpp): rays from Pcamera along +z,
+                           * differentials from origins one pixel over */
+    int32_t pad;
 } pbrtgpu_camera;
 
 /* RealisticDiffractionCamera (cameras/realisticDiffraction.cpp:32-94 parameters, 99-193
@@ -302,7 +305,7 @@ typedef struct pbrtgpu_flat_scene {
     int32_t renderer;             /* PBRTGPU_RENDERER_*: the scene's Renderer */
     int32_t wave_bands;           /* SpectralRenderer "nWaveBands" (api.cpp:1378, default 32) */
     int32_t spectral_sampling;    /* SpectralRenderer "samplingMethod": PBRTGPU_SPECTRAL_* */
-    int32_t camera_type;          /* PBRTGPU_CAMERA_*: "perspective" (camera) or "realisticDiffraction" (lens) */
+    int32_t camera_type;          /* PBRTGPU_CAMERA_*: "perspective" / "orthographic" (camera) or "realisticDiffraction" (lens) */
     pbrtgpu_lens lens;
     int32_t n_texel_floats;       /* the MIPMap pyramids of the IMAGE textures (pbrtgpu_texture) */
     const float *texels;
@@ -329,7 +332,7 @@ enum { PBRTGPU_META_MESH = 0, PBRTGPU_META_MATERIAL = 1, PBRTGPU_META_DEPTH = 2 
  * per sample, path b drawing from RNG(path_seed(hp, s nWaveBands + b))); samplerDirection
  * traces band s % nWaveBands of sample s only.  A sample's unassigned indices are 0. */
 enum { PBRTGPU_RENDERER_SAMPLER = 0, PBRTGPU_RENDERER_SPECTRAL = 1 };
-enum { PBRTGPU_CAMERA_PERSPECTIVE = 0, PBRTGPU_CAMERA_REALISTIC = 1 };
+enum { PBRTGPU_CAMERA_PERSPECTIVE = 0, PBRTGPU_CAMERA_REALISTIC = 1, PBRTGPU_CAMERA_ORTHOGRAPHIC = 2 };
 enum { PBRTGPU_SPECTRAL_SINGLE = 0, PBRTGPU_SPECTRAL_SAMPLER = 1 };
 
 /* ---- render description ----------------------------------------------------------- */

@@ -2170,7 +2170,7 @@ static void meta_radiance(const Ctx *c, Ray ray, float *Lout) {
     for (int i = 0; i < nb; ++i) Lout[i] = (1.f * L[i]) + 0.f;
 }
 
-/* camera sample -> world ray (perspective.cpp:73-106, transform.h:253-262) */
+/* camera sample -> world ray (perspective.cpp:73-106, orthographic.cpp:42-102, transform.h:253-262) */
 static Ray camera_ray(const Ctx *c, float imageX, float imageY, float lensU, float lensV, float timeU, RayDiff *rd) {
     const pbrtgpu_camera *cam = &c->s->camera;
     const float *m = cam->raster_to_camera;
@@ -2182,8 +2182,13 @@ static Ray camera_ray(const Ctx *c, float imageX, float imageY, float lensU, flo
     float w = m[12] * x + m[13] * y + m[14] * z + m[15];
     if (w != 1.) Pc = vdiv(Pc, w);
     Ray r;
-    r.o = v3(0, 0, 0);
-    r.d = vnorm(v3(Pc.x, Pc.y, Pc.z));
+    if (cam->ortho) {   /* orthographic.cpp:42-65: from Pcamera along +z */
+        r.o = Pc;
+        r.d = v3(0.f, 0.f, 1.f);
+    } else {
+        r.o = v3(0, 0, 0);
+        r.d = vnorm(v3(Pc.x, Pc.y, Pc.z));
+    }
     r.mint = 0.f; r.maxt = INFINITY;
     if (cam->lens_radius > 0.) {
         float lu, lv;
@@ -2219,11 +2224,16 @@ static Ray camera_ray(const Ctx *c, float imageX, float imageY, float lensU, flo
     if (rd) {   /* rx/ry rays in camera space, CameraToWorld, ScaleDifferentials(1/sqrt(spp)) */
         const float *dx = cam->dx_camera, *dy = cam->dy_camera;
         V rxd = vnorm(vadd(Pc, v3(dx[0], dx[1], dx[2]))), ryd = vnorm(vadd(Pc, v3(dy[0], dy[1], dy[2])));
-        V ow = o.o;   /* rxOrigin = ryOrigin = ray->o, transformed like o */
+        V owx = o.o, owy = o.o;   /* rxOrigin = ryOrigin = ray->o, transformed like o */
+        if (cam->ortho) {   /* orthographic.cpp:95-98: o + dxCamera / dyCamera, direction d */
+            owx = xpoint(cw, vadd(r.o, v3(dx[0], dx[1], dx[2])));
+            owy = xpoint(cw, vadd(r.o, v3(dy[0], dy[1], dy[2])));
+            rxd = ryd = r.d;
+        }
         rxd = xvec(cw, rxd); ryd = xvec(cw, ryd);
         float sc = 1.f / sqrtf((float)c->s->spp);
-        rd->rxo = vadd(o.o, vmul(vsub(ow, o.o), sc));
-        rd->ryo = vadd(o.o, vmul(vsub(ow, o.o), sc));
+        rd->rxo = vadd(o.o, vmul(vsub(owx, o.o), sc));
+        rd->ryo = vadd(o.o, vmul(vsub(owy, o.o), sc));
         rd->rxd = vadd(o.d, vmul(vsub(rxd, o.d), sc));
         rd->ryd = vadd(o.d, vmul(vsub(ryd, o.d), sc));
         rd->has = 1;

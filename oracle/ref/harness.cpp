@@ -52,6 +52,7 @@
 #include "reflection.h"
 #include "accelerators/bvh.h"
 #include "cameras/perspective.h"
+#include "cameras/orthographic.h"
 #include "filters/box.h"
 #ifndef HARNESS_RGB
 #include "film/spectralImageNoCamera.h"
@@ -538,8 +539,10 @@ void pbrtWorldEnd() {
     tcache.Lookup(cameraToWorld[0], &c2w[0], NULL);
     tcache.Lookup(cameraToWorld[1], &c2w[1], NULL);
     AnimatedTransform ac2w(c2w[0], tStart, c2w[1], tEnd);
-    if (cameraName != "perspective") { fprintf(stderr, "harness: camera %s unsupported\n", cameraName.c_str()); exit(2); }
-    gCamera = CreatePerspectiveCamera(cameraParams, ac2w, gCameraFilm ? gCameraFilm : (Film *)gFilm);
+    if (cameraName == "orthographic")
+        gCamera = CreateOrthographicCamera(cameraParams, ac2w, gCameraFilm ? gCameraFilm : (Film *)gFilm);
+    else if (cameraName != "perspective") { fprintf(stderr, "harness: camera %s unsupported\n", cameraName.c_str()); exit(2); }
+    else gCamera = CreatePerspectiveCamera(cameraParams, ac2w, gCameraFilm ? gCameraFilm : (Film *)gFilm);
     if (ovMaxDepth >= 0) { int v = ovMaxDepth; surfParams.AddInt("maxdepth", &v, 1); }
     // the configs override the scene's integrator to "path" (SURVEY App. B), the harness's
     // default; --surf directlighting creates the DirectLightingIntegrator from the scene's

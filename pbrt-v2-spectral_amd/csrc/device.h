@@ -2434,7 +2434,8 @@ PGD_HEAVY float light_pdf(const DevScene &S, const pbrtgpu_light &L, V p, V wi) 
     return pp / L.sum_area;
 }
 
-// camera sample -> camera-space ray before CameraToWorld, and Pcamera (perspective.cpp:73-97)
+// camera sample -> camera-space ray before CameraToWorld, and Pcamera (perspective.cpp:73-97;
+// orthographic.cpp:42-65: the ray starts at Pcamera along +z)
 PGD_INLINE Ray camera_local(const pbrtgpu_camera &cam, float imageX, float imageY, float lensU, float lensV,
                             float timeU, V *PcOut) {
     const float *m = cam.raster_to_camera;
@@ -2446,8 +2447,13 @@ PGD_INLINE Ray camera_local(const pbrtgpu_camera &cam, float imageX, float image
     float w = m[12] * x + m[13] * y + m[14] * z + m[15];
     if (w != 1.) Pc = vdiv(Pc, w);
     Ray r;
-    r.o = v3(0, 0, 0);
-    r.d = vnorm(v3(Pc.x, Pc.y, Pc.z));
+    if (cam.ortho) {
+        r.o = Pc;
+        r.d = v3(0.f, 0.f, 1.f);
+    } else {
+        r.o = v3(0, 0, 0);
+        r.d = vnorm(v3(Pc.x, Pc.y, Pc.z));
+    }
     r.mint = 0.f; r.maxt = INFINITY;
     if (cam.lens_radius > 0.) {
         float lu, lv;
@@ -2490,10 +2496,18 @@ PGD_INLINE RayDiff camera_diff(const pbrtgpu_camera &cam, int spp, float imageX,
     float cwb[16];
     const float *cw = cam_xform(cam, cm, r.time, cwb);
     V o = cam_point(cw, r.o), d = xvec(cw, r.d);
-    V rxd = xvec(cw, vnorm(vadd(Pc, v3(cam.dx_camera[0], cam.dx_camera[1], cam.dx_camera[2]))));
-    V ryd = xvec(cw, vnorm(vadd(Pc, v3(cam.dy_camera[0], cam.dy_camera[1], cam.dy_camera[2]))));
+    const V dx = v3(cam.dx_camera[0], cam.dx_camera[1], cam.dx_camera[2]), dy = v3(cam.dy_camera[0], cam.dy_camera[1], cam.dy_camera[2]);
     float sc = 1.f / sqrtf((float)spp);
     RayDiff rd;
+    if (cam.ortho) {   // orthographic.cpp:95-98: origins one pixel over, the ray's own direction
+        rd.rxo = vadd(o, vmul(vsub(cam_point(cw, vadd(r.o, dx)), o), sc));
+        rd.ryo = vadd(o, vmul(vsub(cam_point(cw, vadd(r.o, dy)), o), sc));
+        rd.rxd = vadd(d, vmul(vsub(d, d), sc));
+        rd.ryd = rd.rxd;
+        return rd;
+    }
+    V rxd = xvec(cw, vnorm(vadd(Pc, dx)));
+    V ryd = xvec(cw, vnorm(vadd(Pc, dy)));
     rd.rxo = vadd(o, vmul(vsub(o, o), sc));
     rd.ryo = rd.rxo;
     rd.rxd = vadd(d, vmul(vsub(rxd, d), sc));

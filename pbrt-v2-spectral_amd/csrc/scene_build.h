@@ -317,8 +317,11 @@ static inline int scene_check(const pbrtgpu_flat_scene *s, std::string *err) {
         if (s->wave_bands < 1 || s->wave_bands > 1024) SB_FAIL(PBRTGPU_E_INVALID, "nWaveBands must be 1..1024");
         if (int e = spectral_table(s->n_bands, s->wave_bands, &specTab, &specWl, err)) return e;
     }
-    if (s->camera_type != PBRTGPU_CAMERA_PERSPECTIVE && s->camera_type != PBRTGPU_CAMERA_REALISTIC)
+    if (s->camera_type != PBRTGPU_CAMERA_PERSPECTIVE && s->camera_type != PBRTGPU_CAMERA_REALISTIC &&
+        s->camera_type != PBRTGPU_CAMERA_ORTHOGRAPHIC)
         SB_FAIL(PBRTGPU_E_INVALID, "unknown camera type");
+    if ((s->camera.ortho != 0) != (s->camera_type == PBRTGPU_CAMERA_ORTHOGRAPHIC))
+        SB_FAIL(PBRTGPU_E_INVALID, "camera.ortho does not match camera_type");
     if (s->camera_type == PBRTGPU_CAMERA_REALISTIC) {
         const pbrtgpu_lens &L = s->lens;
         if (L.n_elements < 1 || L.n_elements > 4096 || !L.elements) SB_FAIL(PBRTGPU_E_INVALID, "lens camera without elements");

@@ -44,7 +44,7 @@ int pbrthost_load(const char *path, const pbrthost_overrides *ov, pbrthost_scene
     if (ov && p.size() > 5 && p.substr(p.size() - 5) == ".pack") {
         if (ov->xres > 0 || ov->yres > 0) {
             int xr = ov->xres > 0 ? ov->xres : s->camParams.xres, yr = ov->yres > 0 ? ov->yres : s->camParams.yres;
-            ComputeCamera(s->camParams, xr, yr, &s->camera);
+            ComputeCamera(s->camParams, xr, yr, &s->camera, s->cameraType);
         }
         if (ov->bands > 0 && ov->bands != s->nBands) { delete s; SetErr(err, errlen, "scene pack was built for a different band count"); return -1; }
         if (ov->spp > 0) { uint32_t v = ov->spp; v--; v |= v >> 1; v |= v >> 2; v |= v >> 4; v |= v >> 8; v |= v >> 16; s->spp = v + 1; }

@@ -2089,8 +2089,9 @@ private:
             crop[0] = Clamp(pmin(cr->f[0], cr->f[1]), 0., 1.); crop[1] = Clamp(pmax(cr->f[0], cr->f[1]), 0., 1.);
             crop[2] = Clamp(pmin(cr->f[2], cr->f[3]), 0., 1.); crop[3] = Clamp(pmax(cr->f[2], cr->f[3]), 0., 1.);
         }
-        // ---- camera (perspective.cpp:110-147) -- parameters kept resolution independent
-        if (cameraName != "perspective" && cameraName != "realisticDiffraction")
+        // ---- camera (perspective.cpp:110-147, orthographic.cpp:105-140) -- parameters kept
+        // resolution independent
+        if (cameraName != "perspective" && cameraName != "orthographic" && cameraName != "realisticDiffraction")
             throw std::runtime_error("camera '" + cameraName + "' is not supported by this build");
         Xform c2w[2];
         for (int i = 0; i < 2; ++i) LookupCache(cameraToWorld.t[i], &c2w[i], nullptr);
@@ -2117,7 +2118,7 @@ private:
         cp.shutterOpen = cameraParams.FindOneFloat("shutteropen", 0.f);
         cp.shutterClose = cameraParams.FindOneFloat("shutterclose", 1.f);
         if (cp.shutterClose < cp.shutterOpen) std::swap(cp.shutterOpen, cp.shutterClose);
-        out->cameraType = PBRTGPU_CAMERA_PERSPECTIVE;
+        out->cameraType = cameraName == "orthographic" ? PBRTGPU_CAMERA_ORTHOGRAPHIC : PBRTGPU_CAMERA_PERSPECTIVE;
         if (cameraName == "realisticDiffraction") RealisticCamera(&cp);
         cp.lensRadius = cameraParams.FindOneFloat("lensradius", 0.f);
         cp.focalDistance = cameraParams.FindOneFloat("focaldistance", 1e30f);
@@ -2133,7 +2134,7 @@ private:
         for (int k = 0; k < 4; ++k) cp.crop[k] = crop[k];
         memcpy(cp.cam2world, c2w[0].m.m, 64);
         cp.xres = xres; cp.yres = yres;
-        ComputeCamera(cp, xres, yres, &out->camera);
+        ComputeCamera(cp, xres, yres, &out->camera, out->cameraType);
         // ---- integrator / sampler
         out->maxDepth = ov.maxdepth >= 0 ? ov.maxdepth : surfParams.FindOneInt("maxdepth", 5);
         // SurfaceIntegrator (api.cpp:551-583): "path" or "directlighting" (strategy "all" / "one",
@@ -2313,7 +2314,7 @@ private:
 
 // film extent (spectralImage.cpp:40-50, 176-185) and projective camera matrices
 // (camera.cpp:84-103, perspective.cpp:33-40) for a film resolution
-void ComputeCamera(const CameraParams &cp, int xres, int yres, pbrtgpu_camera *outc) {
+void ComputeCamera(const CameraParams &cp, int xres, int yres, pbrtgpu_camera *outc, int cameraType) {
     pbrtgpu_camera &C = *outc;
     memset(&C, 0, sizeof(C));
     C.xres = xres; C.yres = yres;
@@ -2331,17 +2332,28 @@ void ComputeCamera(const CameraParams &cp, int xres, int yres, pbrtgpu_camera *o
     if (frame > 1.f) { screen[0] = -frame; screen[1] = frame; screen[2] = -1.f; screen[3] = 1.f; }
     else { screen[0] = -1.f; screen[1] = 1.f; screen[2] = -1.f / frame; screen[3] = 1.f / frame; }
     if (cp.hasScreenWindow) for (int k = 0; k < 4; ++k) screen[k] = cp.screenWindow[k];
-    Xform camToScreen = Perspective(cp.fov, 1e-2f, 1000.f);
+    const bool ortho = cameraType == PBRTGPU_CAMERA_ORTHOGRAPHIC;
+    // CameraToScreen: Perspective(fov, 1e-2f, 1000.f) or Orthographic(0., 1.) (transform.cpp:292-295)
+    Xform camToScreen = ortho ? Scale(1.f, 1.f, 1.f / (1.f - 0.f)) * Translate(V3(0.f, 0.f, -0.f))
+                              : Perspective(cp.fov, 1e-2f, 1000.f);
     Xform screenToRaster = Scale(float(xres), float(yres), 1.f) *
                            Scale(1.f / (screen[1] - screen[0]), 1.f / (screen[2] - screen[3]), 1.f) *
                            Translate(V3(-screen[0], -screen[3], 0.f));
     Xform rasterToScreen = Inverse(screenToRaster);
     Xform rasterToCamera = Inverse(camToScreen) * rasterToScreen;
     memcpy(C.raster_to_camera, rasterToCamera.m.m, 64);
-    // dxCamera / dyCamera (perspective.cpp:45-48)
-    V3 r0 = rasterToCamera.Point(V3(0, 0, 0)), rx = rasterToCamera.Point(V3(1, 0, 0)), ry = rasterToCamera.Point(V3(0, 1, 0));
-    C.dx_camera[0] = rx.x - r0.x; C.dx_camera[1] = rx.y - r0.y; C.dx_camera[2] = rx.z - r0.z;
-    C.dy_camera[0] = ry.x - r0.x; C.dy_camera[1] = ry.y - r0.y; C.dy_camera[2] = ry.z - r0.z;
+    // dxCamera / dyCamera: differences of raster points one pixel apart (perspective.cpp:45-48), or
+    // the raster unit vectors themselves (orthographic.cpp:39-40)
+    if (ortho) {
+        const V3 dx = rasterToCamera.Vector(V3(1, 0, 0)), dy = rasterToCamera.Vector(V3(0, 1, 0));
+        C.dx_camera[0] = dx.x; C.dx_camera[1] = dx.y; C.dx_camera[2] = dx.z;
+        C.dy_camera[0] = dy.x; C.dy_camera[1] = dy.y; C.dy_camera[2] = dy.z;
+        C.ortho = 1;
+    } else {
+        V3 r0 = rasterToCamera.Point(V3(0, 0, 0)), rx = rasterToCamera.Point(V3(1, 0, 0)), ry = rasterToCamera.Point(V3(0, 1, 0));
+        C.dx_camera[0] = rx.x - r0.x; C.dx_camera[1] = rx.y - r0.y; C.dx_camera[2] = rx.z - r0.z;
+        C.dy_camera[0] = ry.x - r0.x; C.dy_camera[1] = ry.y - r0.y; C.dy_camera[2] = ry.z - r0.z;
+    }
     memcpy(C.cam2world_m, cp.cam2world, 64);
     C.lens_radius = cp.lensRadius; C.focal_distance = cp.focalDistance;
     C.shutter_open = cp.shutterOpen; C.shutter_close = cp.shutterClose;

@@ -35,7 +35,7 @@ struct CameraParams {
     float cam2world[16];
     int xres = 640, yres = 480;     // film resolution the scene was built with
 };
-void ComputeCamera(const CameraParams &cp, int xres, int yres, pbrtgpu_camera *out);
+void ComputeCamera(const CameraParams &cp, int xres, int yres, pbrtgpu_camera *out, int cameraType);
 
 // Host-owned storage behind a pbrtgpu_flat_scene.
 struct HostScene {

@@ -39,7 +39,8 @@ class Camera(ctypes.Structure):
                 ("py_start", ctypes.c_int32), ("py_count", ctypes.c_int32),
                 ("sx_start", ctypes.c_int32), ("sx_end", ctypes.c_int32),
                 ("sy_start", ctypes.c_int32), ("sy_end", ctypes.c_int32),
-                ("dx_camera", ctypes.c_float * 3), ("dy_camera", ctypes.c_float * 3), ("pad", ctypes.c_int32 * 2)]
+                ("dx_camera", ctypes.c_float * 3), ("dy_camera", ctypes.c_float * 3), ("ortho", ctypes.c_int32),
+                ("pad", ctypes.c_int32)]
 
 
 P = ctypes.c_void_p

@@ -58,6 +58,8 @@ Fixtures (numpy .npz, inputs + expected outputs only):
                                   index, metal eta / k unclamped), path and DirectLighting
   envmap_*                        tests/scenes/envmap.pbrt: an image-based infinite light (decoded PFM
                                   lat-long map: radiance MIPMap, Distribution2D sampling and pdf)
+  ortho_*                         tests/scenes/ortho.pbrt: the orthographic camera (screen window,
+                                  thin lens, shutter, ray differentials), path and DirectLighting
   lights_*                        tests/scenes/lights.pbrt: spot lights (falloff band, transformed
                                   frames) and a distant light beside an area light (path, DL, RGB)
   <scene>_rgb_*                   the RGB build (brgb harness, Spectrum = RGBSpectrum) on imagemap,
@@ -72,7 +74,7 @@ Fixtures (numpy .npz, inputs + expected outputs only):
                                   pixel holds all of its contributions (incl. exact-boundary samples
                                   of its neighbours, spectralImage.cpp:77-152); C2 at the sphere
                                   light's edge and at a killeroo silhouette, C3-C5 at an edge each
-Usage: python tools/make_golden.py [--only keys|dat|merl|dl|meta|spec|rgb|rgbfeat|lights|b30|window|imagemap|animcam|gpupath|textured|envmap]
+Usage: python tools/make_golden.py [--only keys|dat|merl|dl|meta|spec|rgb|rgbfeat|lights|ortho|b30|window|imagemap|animcam|gpupath|textured|envmap]
        (after `make -C oracle ref`, `ref60`, `ref30` and `refrgb`)
 """
 import os
@@ -364,6 +366,17 @@ def lights_fixtures(tmp):
         film_fixture("lights_rgb_film_64x48s4", (64, 48), 4, 0, 5, tmp, scene=sc, bands=3)
 
 
+def ortho_fixtures(tmp):
+    """tests/scenes/ortho.pbrt: the orthographic camera (screen window, thin lens, shutter) over a
+    textured, bump-mapped floor (its ray differentials); path and DirectLighting"""
+    sc = os.path.join(ROOT, "tests", "scenes", "ortho.pbrt")
+    paths_fixture("ortho_paths_64x48s4", (64, 48), 4, 0, 5, 1, tmp, scene=sc)
+    film_fixture("ortho_film_64x48s4", (64, 48), 4, 0, 5, tmp, scene=sc)
+    ex = ("--surf", "directlighting", "--dl-strategy", "all")
+    paths_fixture("ortho_dl_paths_48x36s4", (48, 36), 4, 0, 5, 1, tmp, scene=sc, extra=ex)
+    film_fixture("ortho_dl_film_48x36s4", (48, 36), 4, 0, 5, tmp, scene=sc, extra=ex)
+
+
 def envmap_fixtures(tmp):
     """tests/scenes/envmap.pbrt: an image-based InfiniteAreaLight (a decoded PFM lat-long map: its
     radiance MIPMap and Distribution2D), path integrator and DirectLighting"""
@@ -421,6 +434,8 @@ def main():
                 spec_fixtures(tmp)
             elif only == "rgb":
                 rgb_fixtures(tmp)
+            elif only == "ortho":
+                ortho_fixtures(tmp)
             elif only == "lights":
                 lights_fixtures(tmp)
             elif only == "rgbfeat":
