@@ -78,6 +78,7 @@
 #include "materials/mirror.h"
 #include "materials/glass.h"
 #include "shapes/sphere.h"
+#include "shapes/heightfield.h"
 // output channels of a radiance: the spectrum's bands, or RGB in the C1 build (HARNESS_RGB:
 // Spectrum = RGBSpectrum, pbrt.h:144)
 #ifdef HARNESS_RGB
@@ -468,6 +469,7 @@ static Reference<Shape> MakeShp(const string &n, const Transform *o2w, const Tra
     if (n == "disk") return CreateDiskShape(o2w, w2o, ro, p);
     if (n == "trianglemesh") return CreateTriangleMeshShape(o2w, w2o, ro, p, &gs.floatTextures);
     if (n == "loopsubdiv") return CreateLoopSubdivShape(o2w, w2o, ro, p);
+    if (n == "heightfield") return CreateHeightfieldShape(o2w, w2o, ro, p);
     fprintf(stderr, "harness: shape %s unsupported\n", n.c_str()); exit(2);
 }
 static Reference<Material> CreateMaterialFromState(const ParamSet &params) {

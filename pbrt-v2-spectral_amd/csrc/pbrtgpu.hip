@@ -102,6 +102,9 @@ static const int kTopNodes = PGD_TOP_NODES;   // k_trace_pt: traversal-stack ent
 #ifndef PGD_TRACE_ATTR   // occupancy experiments (tools/build_exp.sh)
 #define PGD_TRACE_ATTR
 #endif
+#ifndef PGD_TRACE_S4_ATTR   // k_trace_s4 alone (experiments; r05g forced every trace kernel to 6 / 8 waves)
+#define PGD_TRACE_S4_ATTR PGD_TRACE_ATTR
+#endif
 #ifndef PGD_TRACE_INST_ATTR   // the two-level kernel: the instance transform's peak would give 148 VGPRs (3 waves)
 #define PGD_TRACE_INST_ATTR __attribute__((amdgpu_waves_per_eu(4, 8)))
 #endif
@@ -359,7 +362,7 @@ __global__ __launch_bounds__(kTraceBlock) PGD_TRACE_ATTR void k_trace_pt(DevScen
 // (wide4_bvh), and any-hit does not depend on the order they are tested in.  Half as many
 // dependent node loads per ray as the binary walk.
 template <bool STATS>
-__global__ __launch_bounds__(kTraceBlock) PGD_TRACE_ATTR void k_trace_s4(DevScene S, PathSoA P, int q, int refill, int ring, uint2 *__restrict__ spill) {
+__global__ __launch_bounds__(kTraceBlock) PGD_TRACE_S4_ATTR void k_trace_s4(DevScene S, PathSoA P, int q, int refill, int ring, uint2 *__restrict__ spill) {
     __shared__ uint32_t sref[kStackLDS * kTraceBlock];
     uint2 *gsp = spill + (size_t)(blockIdx.x * blockDim.x + threadIdx.x) * S.w4Stack;
     int bottom = 0;

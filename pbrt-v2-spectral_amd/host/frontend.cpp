@@ -236,7 +236,7 @@ struct SDVertex { V3 P; int startFace = -1; int child = -1; bool regular = false
 struct SDFace { int v[3] = {-1, -1, -1}; int f[3] = {-1, -1, -1}; int children[4] = {-1, -1, -1, -1}; };
 
 struct ShapeObj {
-    enum { MESH, QUADRIC, LOOP } kind;
+    enum { MESH, QUADRIC, LOOP, HFIELD } kind;   // HFIELD: a Heightfield, its TriangleMesh in mesh
     std::shared_ptr<TriMesh> mesh;
     std::shared_ptr<Quadric> quad;
     // loop subdivision control mesh
@@ -1725,6 +1725,31 @@ private:
             m->uv = uv;
             s->kind = ShapeObj::MESH; s->mesh = m;
             allMeshes.push_back(m);
+        } else if (name == "heightfield") {   // heightfield.cpp:55-113: Refine -> one TriangleMesh
+            const int nu = p.FindOneInt("nu", -1), nv = p.FindOneInt("nv", -1);
+            const Param *Pz = p.Find(P_FLOAT, "Pz");
+            if (nu < 2 || nv < 2 || !Pz || (int64_t)Pz->f.size() != (int64_t)nu * nv)
+                throw std::runtime_error("heightfield: \"nu\" x \"nv\" \"Pz\" values required");
+            auto m = std::make_shared<TriMesh>();
+            m->o2w = o2w; m->ro = ro; m->swaps = o2w.SwapsHandedness();
+            m->nverts = nu * nv;
+            m->ntris = 2 * (nu - 1) * (nv - 1);
+            m->p.resize(m->nverts);
+            m->uv.resize(2 * (size_t)m->nverts);
+            for (int y = 0, pos = 0; y < nv; ++y)
+                for (int x = 0; x < nu; ++x, ++pos) {
+                    const float px = (float)x / (float)(nu - 1), py = (float)y / (float)(nv - 1);
+                    m->uv[2 * pos] = px; m->uv[2 * pos + 1] = py;
+                    m->p[pos] = o2w.Point(V3(px, py, Pz->f[pos]));
+                }
+            m->vi.reserve(3 * (size_t)m->ntris);
+            for (int y = 0; y < nv - 1; ++y)
+                for (int x = 0; x < nu - 1; ++x) {
+                    const int v00 = x + y * nu, v10 = (x + 1) + y * nu, v11 = (x + 1) + (y + 1) * nu, v01 = x + (y + 1) * nu;
+                    m->vi.insert(m->vi.end(), {v00, v10, v11, v00, v11, v01});
+                }
+            s->kind = ShapeObj::HFIELD; s->mesh = m;
+            allMeshes.push_back(m);
         } else if (name == "loopsubdiv") {   // loopsubdiv.cpp:489-502
             int nlevels = p.FindOneInt("nlevels", 3);
             const Param *vi = p.Find(P_INT, "indices"), *P = p.Find(P_POINT, "P");
@@ -1791,7 +1816,7 @@ private:
             if (shape->kind != ShapeObj::QUADRIC) {
                 std::vector<Isect> r;
                 RefineShape(shape, &r);
-                nextPrimId += (uint32_t)r.size() + (shape->kind == ShapeObj::LOOP ? 1u : 0u);
+                nextPrimId += (uint32_t)r.size() + (shape->kind == ShapeObj::LOOP || shape->kind == ShapeObj::HFIELD ? 1u : 0u);
                 if (r.empty()) return;   // api.cpp:1099: no TransformedPrimitive (and no id) then
                 if (r.size() > 1) nextPrimId++;
             }
@@ -2188,7 +2213,7 @@ private:
             RefineShape(shape, &r);
             uint32_t base = fixedId;
             if (!fixedId) {
-                if (shape->kind == ShapeObj::LOOP) nextPrimId++;
+                if (shape->kind == ShapeObj::LOOP || shape->kind == ShapeObj::HFIELD) nextPrimId++;   // the refined mesh's own
                 base = nextPrimId;
                 nextPrimId += (uint32_t)r.size();
             }

@@ -101,7 +101,7 @@ def _golden_scene(pg, cfg, name="killeroo"):
     pack = {"anim": "anim-killeroos-moving.pack", "bunny": "bunny.pack", "metal": "metal.pack",
             "coverage": "coverage.pack", "imagemap": "imagemap.pack",
             "animcam": "animcam.pack", "textured": "textured.pack", "envmap": "envmap.pack", "lights": "lights.pack",
-            "ortho": "ortho.pack"}.get(name.split("_")[0],
+            "ortho": "ortho.pack", "heightfield": "heightfield.pack"}.get(name.split("_")[0],
                                                                                               "killeroo-simple.pack")
     if "_b30_" in name:
         pack = pack.replace(".pack", "-b30.pack")
@@ -115,7 +115,7 @@ def _golden_scene(pg, cfg, name="killeroo"):
                                   "anim_keys_c5_600x600s512", "killeroo_b30_paths_48x40s4",
                                   "coverage_b30_paths_48x36s4", "imagemap_paths_64x48s4",
                                   "imagemap_paths_96x72s2_seed5", "animcam_paths_64x48s4", "textured_paths_64x48s4", "envmap_paths_64x48s4",
-                                  "lights_paths_64x48s4", "ortho_paths_64x48s4"])
+                                  "lights_paths_64x48s4", "ortho_paths_64x48s4", "heightfield_paths_64x48s4"])
 def test_paths_vs_reference_golden(pg, name):
     """GPU against the reference harness's own per-path radiance (fixed seeds); the *_keys_*
     fixtures are the configs at their real resolution and sample count."""
@@ -132,7 +132,7 @@ def test_paths_vs_reference_golden(pg, name):
                                   "metal_film_40x40s8", "coverage_film_64x48s8", "killeroo_b30_film_40x32s8",
                                   "coverage_b30_film_40x30s4", "imagemap_film_64x48s8",
                                   "animcam_film_64x48s4", "textured_film_64x48s8", "envmap_film_64x48s8",
-                                  "lights_film_64x48s8", "ortho_film_64x48s4"])
+                                  "lights_film_64x48s8", "ortho_film_64x48s4", "heightfield_film_64x48s4"])
 def test_film_vs_reference_golden(pg, name):
     """Whole-film render against the reference's film (raw sums, incl. neighbour-pixel
     samples): bit for bit."""
@@ -491,7 +491,8 @@ def test_quantized_shadow_walk_vs_reference_golden(pg, monkeypatch, name):
 
 
 META = ["metadata_material_%s_48x36s4", "metadata_mesh_%s_48x36s4", "metadata_depth_%s_48x36s4",
-        "killeroo_meta_mesh_%s_40x32s2", "anim_meta_mesh_%s_40x32s2", "bunny_meta_depth_%s_40x32s2"]
+        "killeroo_meta_mesh_%s_40x32s2", "anim_meta_mesh_%s_40x32s2", "bunny_meta_depth_%s_40x32s2",
+        "heightfield_meta_mesh_%s_48x36s2"]
 
 
 @pytest.mark.parametrize("base", META)

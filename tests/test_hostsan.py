@@ -94,6 +94,8 @@ CASES = [
     # spot and distant lights (FEAT_INF kernels) beside an area light
     ("lights.pack", dict(xres=40, yres=30, spp=4, maxdepth=5)),
     ("lights.pack", dict(xres=32, yres=24, spp=2, maxdepth=5, integrator="directlighting", strategy="all")),
+    # heightfield shapes (refined on the host; one as an area light)
+    ("heightfield.pack", dict(xres=40, yres=30, spp=4, maxdepth=5)),
     # the orthographic camera (thin lens, ray differentials from shifted origins)
     ("ortho.pack", dict(xres=40, yres=30, spp=4, maxdepth=5)),
     # an animated CameraToWorld under the lens camera
@@ -107,7 +109,7 @@ CASES = [
                                                "lens_microlens_spectral", "eye", "eye_spectral", "lens_diffraction_dl",
                                                "imagemap", "imagemap_dl", "animcam", "textured", "textured_dl", "envmap", "envmap_dl",
                                                "dl_anim_inst",
-                                               "dl_metal60", "rgb_imagemap", "rgb_envmap_dl", "rgb_coverage", "lights", "lights_dl", "ortho", "lens_animated"])
+                                               "dl_metal60", "rgb_imagemap", "rgb_envmap_dl", "rgb_coverage", "lights", "lights_dl", "heightfield", "ortho", "lens_animated"])
 def test_replay_matches_oracle(pg, tmp_path, pack, a):
     exe = _build("shade_host")
     scene = pg.Scene.load(os.path.join(PACKS, pack), **a)

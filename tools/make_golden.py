@@ -58,6 +58,8 @@ Fixtures (numpy .npz, inputs + expected outputs only):
                                   index, metal eta / k unclamped), path and DirectLighting
   envmap_*                        tests/scenes/envmap.pbrt: an image-based infinite light (decoded PFM
                                   lat-long map: radiance MIPMap, Distribution2D sampling and pdf)
+  heightfield_*                   tests/scenes/heightfield.pbrt: heightfield shapes (terrain, area
+                                  light), path and metadata (mesh ids)
   ortho_*                         tests/scenes/ortho.pbrt: the orthographic camera (screen window,
                                   thin lens, shutter, ray differentials), path and DirectLighting
   lights_*                        tests/scenes/lights.pbrt: spot lights (falloff band, transformed
@@ -74,7 +76,7 @@ Fixtures (numpy .npz, inputs + expected outputs only):
                                   pixel holds all of its contributions (incl. exact-boundary samples
                                   of its neighbours, spectralImage.cpp:77-152); C2 at the sphere
                                   light's edge and at a killeroo silhouette, C3-C5 at an edge each
-Usage: python tools/make_golden.py [--only keys|dat|merl|dl|meta|spec|rgb|rgbfeat|lights|ortho|b30|window|imagemap|animcam|gpupath|textured|envmap]
+Usage: python tools/make_golden.py [--only keys|dat|merl|dl|meta|spec|rgb|rgbfeat|lights|ortho|heightfield|b30|window|imagemap|animcam|gpupath|textured|envmap]
        (after `make -C oracle ref`, `ref60`, `ref30` and `refrgb`)
 """
 import os
@@ -377,6 +379,17 @@ def ortho_fixtures(tmp):
     film_fixture("ortho_dl_film_48x36s4", (48, 36), 4, 0, 5, tmp, scene=sc, extra=ex)
 
 
+def heightfield_fixtures(tmp):
+    """tests/scenes/heightfield.pbrt: heightfield shapes (terrain, area light) refined as the
+    reference does; path integrator and the metadata integrator's mesh ids"""
+    sc = os.path.join(ROOT, "tests", "scenes", "heightfield.pbrt")
+    paths_fixture("heightfield_paths_64x48s4", (64, 48), 4, 0, 5, 1, tmp, scene=sc)
+    film_fixture("heightfield_film_64x48s4", (64, 48), 4, 0, 5, tmp, scene=sc)
+    ex = ("--surf", "metadata", "--meta-strategy", "mesh")
+    paths_fixture("heightfield_meta_mesh_paths_48x36s2", (48, 36), 2, 0, 5, 1, tmp, scene=sc, extra=ex)
+    film_fixture("heightfield_meta_mesh_film_48x36s2", (48, 36), 2, 0, 5, tmp, scene=sc, extra=ex)
+
+
 def envmap_fixtures(tmp):
     """tests/scenes/envmap.pbrt: an image-based InfiniteAreaLight (a decoded PFM lat-long map: its
     radiance MIPMap and Distribution2D), path integrator and DirectLighting"""
@@ -434,6 +447,8 @@ def main():
                 spec_fixtures(tmp)
             elif only == "rgb":
                 rgb_fixtures(tmp)
+            elif only == "heightfield":
+                heightfield_fixtures(tmp)
             elif only == "ortho":
                 ortho_fixtures(tmp)
             elif only == "lights":
