@@ -46,7 +46,8 @@ typedef struct pbrtgpu_bvh_node {
     uint32_t meta;
 } pbrtgpu_bvh_node;
 
-enum { PBRTGPU_SHAPE_TRIANGLE = 0, PBRTGPU_SHAPE_SPHERE = 1, PBRTGPU_SHAPE_DISK = 2, PBRTGPU_SHAPE_INSTANCE = 3 };
+enum { PBRTGPU_SHAPE_TRIANGLE = 0, PBRTGPU_SHAPE_SPHERE = 1, PBRTGPU_SHAPE_DISK = 2, PBRTGPU_SHAPE_INSTANCE = 3,
+       PBRTGPU_SHAPE_CYLINDER = 4 };
 
 /* one GeometricPrimitive, in BVH (orderedPrims) order */
 typedef struct pbrtgpu_prim {
@@ -70,9 +71,10 @@ typedef struct pbrtgpu_mesh {
     int32_t vert_offset, nverts, pad0, pad1;
 } pbrtgpu_mesh;
 
-/* Sphere (sphere.cpp) / Disk (disk.cpp); WorldToObject = (o2w_minv, o2w_m) */
+/* Sphere (sphere.cpp) / Disk (disk.cpp) / Cylinder (cylinder.cpp: radius, zmin, zmax, phi_max);
+ * WorldToObject = (o2w_minv, o2w_m) */
 typedef struct pbrtgpu_quadric {
-    int32_t type;         /* PBRTGPU_SHAPE_SPHERE or _DISK */
+    int32_t type;         /* PBRTGPU_SHAPE_SPHERE, _DISK or _CYLINDER */
     int32_t reverse_orientation, swaps_handedness, pad0;
     float o2w_m[16];
     float o2w_minv[16];
@@ -87,10 +89,12 @@ enum {
     PBRTGPU_MAT_MIRROR = 4,     /* spec[0]=Kr */
     PBRTGPU_MAT_GLASS = 5,      /* spec[0]=Kr, spec[1]=Kt; f[0]=index */
     PBRTGPU_MAT_MEASURED = 6,   /* IrregIsotropicBRDF: aux = first kd-tree node, aux2 = node count */
-    PBRTGPU_MAT_MEASURED_HALFANGLE = 7   /* RegularHalfangleBRDF (.merl): aux = first texel of its
+    PBRTGPU_MAT_MEASURED_HALFANGLE = 7,  /* RegularHalfangleBRDF (.merl): aux = first texel of its
                                           * 90 x 90 x 180 RGB table in merl[] (3 floats per texel),
                                           * -1 when the file could not be read (no BxDF, as the
                                           * reference's MeasuredMaterial then adds none) */
+    PBRTGPU_MAT_ANISOWARD = 8   /* the fork's anisotropic Ward material (materials/anisoward.cpp,
+                                 * AnisoWardBrdf.cpp): spec[0]=Kd, spec[1]=Ks; f[0]=alphaU, f[1]=alphaV */
 };
 
 /* Texture<float> / Texture<Spectrum> (texture.h, textures/{constant,scale,imagemap}.cpp).

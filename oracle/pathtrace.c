@@ -476,6 +476,45 @@ static int disk_intersect(const pbrtgpu_quadric *q, const Ray *r, float *tHit, f
     *rayEps = 5e-4f * *tHit;
     return 1;
 }
+/* Cylinder::Intersect (cylinder.cpp:48-111); dg may be NULL (IntersectP, :113-176) */
+static int cylinder_intersect(const pbrtgpu_quadric *q, const Ray *r, float *tHit, float *rayEps, DG *dg) {
+    Ray ray = to_object(q, r);
+    float A = ray.d.x * ray.d.x + ray.d.y * ray.d.y;
+    float B = 2 * (ray.d.x * ray.o.x + ray.d.y * ray.o.y);
+    float C = ray.o.x * ray.o.x + ray.o.y * ray.o.y - q->radius * q->radius;
+    float t0, t1;
+    if (!quadratic(A, B, C, &t0, &t1)) return 0;
+    if (t0 > ray.maxt || t1 < ray.mint) return 0;
+    float thit = t0;
+    if (t0 < ray.mint) { thit = t1; if (thit > ray.maxt) return 0; }
+    V phit = rayat(&ray, thit);
+    float phi = ATAN2F(phit.y, phit.x);
+    if (phi < 0.) phi += 2.f * PI_F;
+    if (phit.z < q->zmin || phit.z > q->zmax || phi > q->phi_max) {
+        if (thit == t1) return 0;
+        thit = t1;
+        if (t1 > ray.maxt) return 0;
+        phit = rayat(&ray, thit);
+        phi = ATAN2F(phit.y, phit.x);
+        if (phi < 0.) phi += 2.f * PI_F;
+        if (phit.z < q->zmin || phit.z > q->zmax || phi > q->phi_max) return 0;
+    }
+    if (!dg) { if (tHit) *tHit = thit; return 1; }
+    float u = phi / q->phi_max, v = (phit.z - q->zmin) / (q->zmax - q->zmin);
+    V dpdu = v3(-q->phi_max * phit.y, q->phi_max * phit.x, 0), dpdv = v3(0, 0, q->zmax - q->zmin);
+    V d2Pduu = vmul(v3(phit.x, phit.y, 0), -q->phi_max * q->phi_max), d2Pduv = v3(0, 0, 0), d2Pdvv = v3(0, 0, 0);
+    float E = vdot(dpdu, dpdu), F = vdot(dpdu, dpdv), G = vdot(dpdv, dpdv);
+    V N = vnorm(vcross(dpdu, dpdv));
+    float e = vdot(N, d2Pduu), f = vdot(N, d2Pduv), g = vdot(N, d2Pdvv);
+    float invEGF2 = 1.f / (E * G - F * F);
+    V dndu = vadd(vmul(dpdu, (f * F - e * G) * invEGF2), vmul(dpdv, (e * F - f * E) * invEGF2));
+    V dndv = vadd(vmul(dpdu, (g * F - f * G) * invEGF2), vmul(dpdv, (f * F - g * E) * invEGF2));
+    dg_init(dg, xpoint(q->o2w_m, phit), xvec(q->o2w_m, dpdu), xvec(q->o2w_m, dpdv), xnormal(q->o2w_minv, dndu),
+            xnormal(q->o2w_minv, dndv), u, v, q->reverse_orientation ^ q->swaps_handedness);
+    *tHit = thit;
+    *rayEps = 5e-4f * *tHit;
+    return 1;
+}
 static float shape_area(const Ctx *c, int type, int idx) {
     if (type == PBRTGPU_SHAPE_TRIANGLE) {
         const pbrtgpu_triangle *t = &c->s->tris[idx];
@@ -484,11 +523,13 @@ static float shape_area(const Ctx *c, int type, int idx) {
     }
     const pbrtgpu_quadric *q = &c->s->quadrics[idx];
     if (type == PBRTGPU_SHAPE_SPHERE) return q->phi_max * q->radius * (q->zmax - q->zmin);
+    if (type == PBRTGPU_SHAPE_CYLINDER) return (q->zmax - q->zmin) * q->phi_max * q->radius;   /* cylinder.cpp:180-182 */
     return q->phi_max * 0.5f * (q->radius * q->radius - q->inner_radius * q->inner_radius);
 }
 static int shape_intersect(const Ctx *c, int type, int idx, const Ray *r, float *tHit, float *eps, DG *dg) {
     if (type == PBRTGPU_SHAPE_TRIANGLE) return tri_intersect(c, idx, r, tHit, eps, dg);
     if (type == PBRTGPU_SHAPE_SPHERE) return sphere_intersect(&c->s->quadrics[idx], r, tHit, eps, dg);
+    if (type == PBRTGPU_SHAPE_CYLINDER) return cylinder_intersect(&c->s->quadrics[idx], r, tHit, eps, dg);
     return disk_intersect(&c->s->quadrics[idx], r, tHit, eps, dg);
 }
 
@@ -726,7 +767,8 @@ enum { BSDF_REFLECTION = 1, BSDF_TRANSMISSION = 2, BSDF_DIFFUSE = 4, BSDF_GLOSSY
        BSDF_ALL = 31 };
 enum { BX_LAMBERT, BX_OREN, BX_MICRO_BLINN_DIEL, BX_SPEC_REFL_NOOP, BX_FRESNEL_BLEND_ANISO, BX_MEASURED_IRREG,
        BX_MICRO_BLINN_COND, BX_SPEC_REFL_DIEL, BX_SPEC_TRANS,    /* eta_t = index of refraction for these two */
-       BX_MEASURED_HALF };                                        /* RegularHalfangleBRDF: merl = its table */
+       BX_MEASURED_HALF,                                          /* RegularHalfangleBRDF: merl = its table */
+       BX_ANISOWARD };                                            /* AnisoWardBrdf: R = Rs, a = Ax, b = Ay */
 typedef struct {
     int kind, type;
     const float *R;      /* reflectance spectrum */
@@ -1000,6 +1042,19 @@ static void bx_f_add(const Ctx *c, const BxDF *b, V wo, V wi, float *out) {
         case BX_SPEC_TRANS:
             for (int i = 0; i < nb; ++i) out[i] += 0.f;
             break;
+        case BX_ANISOWARD: {   /* AnisoWardBrdf::f (AnisoWardBrdf.cpp:10-23) */
+            V wh = vadd(wi, wo);
+            if (wh.z == 0.0f) { for (int i = 0; i < nb; ++i) out[i] += 0.f; break; }
+            float cosi_coso = wi.z * wo.z;
+            if (cosi_coso <= 0.0f) { for (int i = 0; i < nb; ++i) out[i] += 0.f; break; }
+            float invAx2 = 1.0f / (b->a * b->a), invAy2 = 1.0f / (b->b * b->b);
+            float fourPiAxAy = (4.0f * PI_F * b->a * b->b);
+            float expTerm = EXPF(-1.0f * (wh.x * wh.x * invAx2 + wh.y * wh.y * invAy2) / (wh.z * wh.z));
+            cosi_coso = sqrtf(cosi_coso);
+            float den = cosi_coso * fourPiAxAy;
+            for (int i = 0; i < nb; ++i) out[i] += (b->R[i] * expTerm) / den;
+            break;
+        }
         case BX_FRESNEL_BLEND_ANISO: {   /* FresnelBlend::f (reflection.cpp:224-236) */
             float cd = (28.f / (23.f * PI_F));
             float ta = (1.f - POWF(1.f - .5f * abscos(wi), 5)), tb = (1.f - POWF(1.f - .5f * abscos(wo), 5));
@@ -1588,6 +1643,14 @@ static void get_bsdf(const Ctx *c, const Isect *is, const float diff[4], BSDF *b
             x->merl = c->s->merl + 3 * (size_t)mt->aux;
             break;
         }
+        case PBRTGPU_MAT_ANISOWARD: {   /* anisoward.cpp:35-60: Lambertian(Kd) + AnisoWardBrdf(Ks, alphaU, alphaV) */
+            BxDF *x = &bs->bx[bs->n++];
+            x->kind = BX_LAMBERT; x->type = BSDF_REFLECTION | BSDF_DIFFUSE; x->R = K[0];
+            x = &bs->bx[bs->n++];
+            x->kind = BX_ANISOWARD; x->type = BSDF_REFLECTION | BSDF_GLOSSY; x->R = K[1];
+            x->a = fp[0]; x->b = fp[1];
+            break;
+        }
         case PBRTGPU_MAT_SUBSTRATE: {   /* substrate.cpp:34-56 */
             BxDF *x = &bs->bx[bs->n++];
             x->kind = BX_FRESNEL_BLEND_ANISO; x->type = BSDF_REFLECTION | BSDF_GLOSSY;
@@ -1655,6 +1718,14 @@ static float shape_pdf(const Ctx *c, int type, int idx, V p, V wi) {
 /* Shape::Sample(p, u1, u2) for triangle / disk = Sample(u1, u2) */
 static V shape_sample_p(const Ctx *c, int type, int idx, V p, float u1, float u2, V *ns) {
     if (type == PBRTGPU_SHAPE_SPHERE) return sphere_sample_p(&c->s->quadrics[idx], p, u1, u2, ns);
+    if (type == PBRTGPU_SHAPE_CYLINDER) {   /* cylinder.cpp:195-203 */
+        const pbrtgpu_quadric *q = &c->s->quadrics[idx];
+        float z = lerpf(u1, q->zmin, q->zmax), t = u2 * q->phi_max;
+        V pp = v3(q->radius * COSF(t), q->radius * SINF(t), z);
+        *ns = vnorm(xnormal(q->o2w_minv, v3(pp.x, pp.y, 0.f)));
+        if (q->reverse_orientation) *ns = vmul(*ns, -1.f);
+        return xpoint(q->o2w_m, pp);
+    }
     if (type == PBRTGPU_SHAPE_DISK) {   /* disk.cpp:140-150 */
         const pbrtgpu_quadric *q = &c->s->quadrics[idx];
         V pp;

@@ -72,6 +72,7 @@
 #include "lights/distant.h"
 #include "materials/matte.h"
 #include "materials/plastic.h"
+#include "materials/anisoward.h"
 #include "materials/metal.h"
 #include "materials/substrate.h"
 #include "materials/measured.h"
@@ -79,6 +80,7 @@
 #include "materials/glass.h"
 #include "shapes/sphere.h"
 #include "shapes/heightfield.h"
+#include "shapes/cylinder.h"
 // output channels of a radiance: the spectrum's bands, or RGB in the C1 build (HARNESS_RGB:
 // Spectrum = RGBSpectrum, pbrt.h:144)
 #ifdef HARNESS_RGB
@@ -441,6 +443,7 @@ static Reference<Material> MakeMat(const string &n, const Transform &x, const Te
     if (n == "plastic") return CreatePlasticMaterial(x, mp);
     if (n == "metal") return CreateMetalMaterial(x, mp);
     if (n == "substrate") return CreateSubstrateMaterial(x, mp);
+    if (n == "anisoward") return CreateAnisoWardMaterial(x, mp);
     if (n == "measured") return CreateMeasuredMaterial(x, mp);
     if (n == "mirror") return CreateMirrorMaterial(x, mp);
     if (n == "glass") return CreateGlassMaterial(x, mp);
@@ -470,6 +473,7 @@ static Reference<Shape> MakeShp(const string &n, const Transform *o2w, const Tra
     if (n == "trianglemesh") return CreateTriangleMeshShape(o2w, w2o, ro, p, &gs.floatTextures);
     if (n == "loopsubdiv") return CreateLoopSubdivShape(o2w, w2o, ro, p);
     if (n == "heightfield") return CreateHeightfieldShape(o2w, w2o, ro, p);
+    if (n == "cylinder") return CreateCylinderShape(o2w, w2o, ro, p);
     fprintf(stderr, "harness: shape %s unsupported\n", n.c_str()); exit(2);
 }
 static Reference<Material> CreateMaterialFromState(const ParamSet &params) {

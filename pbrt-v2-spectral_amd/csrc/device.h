@@ -643,6 +643,53 @@ PGD_INLINE bool disk_intersect(const pbrtgpu_quadric &q, const Ray &r, float *tH
     *rayEps = 5e-4f * *tHit;
     return true;
 }
+// Cylinder::Intersect / IntersectP (cylinder.cpp:48-176); nnOnly as for the sphere
+PGD_INLINE bool cylinder_intersect(const pbrtgpu_quadric &q, const Ray &r, float *tHit, float *rayEps, DG *dg,
+                                   bool nnOnly = false) {
+    Ray ray = to_object(q, r);
+    float A = ray.d.x * ray.d.x + ray.d.y * ray.d.y;
+    float B = 2 * (ray.d.x * ray.o.x + ray.d.y * ray.o.y);
+    float C = ray.o.x * ray.o.x + ray.o.y * ray.o.y - q.radius * q.radius;
+    float t0, t1;
+    if (!quadratic(A, B, C, &t0, &t1)) return false;
+    if (t0 > ray.maxt || t1 < ray.mint) return false;
+    float thit = t0;
+    if (t0 < ray.mint) { thit = t1; if (thit > ray.maxt) return false; }
+    V phit = rayat(ray, thit);
+    float phi = ATAN2F(phit.y, phit.x);
+    if (phi < 0.) phi += 2.f * kPi;
+    if (phit.z < q.zmin || phit.z > q.zmax || phi > q.phi_max) {
+        if (thit == t1) return false;
+        thit = t1;
+        if (t1 > ray.maxt) return false;
+        phit = rayat(ray, thit);
+        phi = ATAN2F(phit.y, phit.x);
+        if (phi < 0.) phi += 2.f * kPi;
+        if (phit.z < q.zmin || phit.z > q.zmax || phi > q.phi_max) return false;
+    }
+    if (!dg) { *tHit = thit; return true; }
+    const V dpdu = v3(-q.phi_max * phit.y, q.phi_max * phit.x, 0), dpdv = v3(0, 0, q.zmax - q.zmin);
+    if (nnOnly) {
+        dg->nn = vnorm(vcross(xvec(q.o2w_m, dpdu), xvec(q.o2w_m, dpdv)));
+        if (q.reverse_orientation ^ q.swaps_handedness) dg->nn = vmul(dg->nn, -1.f);
+        *tHit = thit;
+        *rayEps = 5e-4f * *tHit;
+        return true;
+    }
+    const float u = phi / q.phi_max, v = (phit.z - q.zmin) / (q.zmax - q.zmin);
+    const V d2Pduu = vmul(v3(phit.x, phit.y, 0), -q.phi_max * q.phi_max), d2Pduv = v3(0, 0, 0), d2Pdvv = v3(0, 0, 0);
+    const float E = vdot(dpdu, dpdu), F = vdot(dpdu, dpdv), G = vdot(dpdv, dpdv);
+    const V N = vnorm(vcross(dpdu, dpdv));
+    const float e = vdot(N, d2Pduu), f = vdot(N, d2Pduv), g = vdot(N, d2Pdvv);
+    const float invEGF2 = 1.f / (E * G - F * F);
+    const V dndu = vadd(vmul(dpdu, (f * F - e * G) * invEGF2), vmul(dpdv, (e * F - f * E) * invEGF2));
+    const V dndv = vadd(vmul(dpdu, (g * F - f * G) * invEGF2), vmul(dpdv, (f * F - g * E) * invEGF2));
+    dg_init(*dg, xpoint(q.o2w_m, phit), xvec(q.o2w_m, dpdu), xvec(q.o2w_m, dpdv), xnormal(q.o2w_minv, dndu),
+            xnormal(q.o2w_minv, dndv), u, v, q.reverse_orientation ^ q.swaps_handedness);
+    *tHit = thit;
+    *rayEps = 5e-4f * *tHit;
+    return true;
+}
 PGD_INLINE float shape_area(const DevScene &S, int type, int idx) {
     if (type == PBRTGPU_SHAPE_TRIANGLE) {
         const pbrtgpu_triangle t = (*sa(S.tris, (uint32_t)(idx)));
@@ -651,12 +698,14 @@ PGD_INLINE float shape_area(const DevScene &S, int type, int idx) {
     }
     const pbrtgpu_quadric &q = (*sa(S.quads, (uint32_t)(idx)));
     if (type == PBRTGPU_SHAPE_SPHERE) return q.phi_max * q.radius * (q.zmax - q.zmin);
+    if (type == PBRTGPU_SHAPE_CYLINDER) return (q.zmax - q.zmin) * q.phi_max * q.radius;   // cylinder.cpp:180-182
     return q.phi_max * 0.5f * (q.radius * q.radius - q.inner_radius * q.inner_radius);
 }
 PGD_HEAVY bool shape_intersect(const DevScene &S, int type, int idx, const Ray &r, float *tHit, float *eps, DG *dg,
                                bool nnOnly = false) {
     if (type == PBRTGPU_SHAPE_TRIANGLE) return tri_intersect(S, idx, r, tHit, eps, dg);
     if (type == PBRTGPU_SHAPE_SPHERE) return sphere_intersect((*sa(S.quads, (uint32_t)(idx))), r, tHit, eps, dg, nnOnly);
+    if (type == PBRTGPU_SHAPE_CYLINDER) return cylinder_intersect((*sa(S.quads, (uint32_t)(idx))), r, tHit, eps, dg, nnOnly);
     return disk_intersect((*sa(S.quads, (uint32_t)(idx))), r, tHit, eps, dg, nnOnly);
 }
 
@@ -719,13 +768,48 @@ struct Stack {
 #ifndef PGD_QUAD_ATTR   // quadric hit test out of line (traversal register budget); experiments may inline it
 #define PGD_QUAD_ATTR __attribute__((noinline))
 #endif
+// hit-only Sphere / Cylinder::IntersectP in one body (sphere.cpp:153-202, cylinder.cpp:113-176): the
+// cylinder drops the z terms of A, B, C, the sphere's phit.x nudge and the sphere's "clipped at all"
+// guards of its z tests; the operations and their order are each shape's own.  One body keeps the
+// traversal kernels' registers where the sphere test alone put them (a separate cylinder test cost
+// k_trace_c4 94 -> 103 VGPRs inlined, and scratch out of line)
+PGD_INLINE bool sphere_cyl_hit(const pbrtgpu_quadric &q, const Ray &r, bool cyl, float *tHit) {
+    Ray ray = to_object(q, r);
+    const float dz2 = ray.d.z * ray.d.z, dozz = ray.d.z * ray.o.z, oz2 = ray.o.z * ray.o.z;
+    const float A = cyl ? ray.d.x * ray.d.x + ray.d.y * ray.d.y : ray.d.x * ray.d.x + ray.d.y * ray.d.y + dz2;
+    const float B = 2 * (cyl ? ray.d.x * ray.o.x + ray.d.y * ray.o.y : ray.d.x * ray.o.x + ray.d.y * ray.o.y + dozz);
+    const float C = (cyl ? ray.o.x * ray.o.x + ray.o.y * ray.o.y : ray.o.x * ray.o.x + ray.o.y * ray.o.y + oz2) -
+                    q.radius * q.radius;
+    float t0, t1;
+    if (!quadratic(A, B, C, &t0, &t1)) return false;
+    if (t0 > ray.maxt || t1 < ray.mint) return false;
+    float thit = t0;
+    if (t0 < ray.mint) { thit = t1; if (thit > ray.maxt) return false; }
+    // phi <= 2.f * kPi always (atan2 in [-pi, pi], + 2pi in float): with phi_max >= that bound
+    // the phi test cannot fail and the atan2 is skipped
+    const bool needPhi = !(q.phi_max >= 2.f * kPi);
+    const bool zLo = cyl || q.zmin > -q.radius, zHi = cyl || q.zmax < q.radius;
+    for (int k = 0; k < 2; ++k) {
+        V phit = rayat(ray, thit);
+        if (!cyl && phit.x == 0.f && phit.y == 0.f) phit.x = 1e-5f * q.radius;
+        float phi = 0.f;
+        if (needPhi) {
+            phi = ATAN2F(phit.y, phit.x);
+            if (phi < 0.) phi += 2.f * kPi;
+        }
+        if (!((zLo && phit.z < q.zmin) || (zHi && phit.z > q.zmax) || phi > q.phi_max)) { *tHit = thit; return true; }
+        if (k == 1 || thit == t1 || t1 > ray.maxt) return false;
+        thit = t1;
+    }
+    return false;
+}
 PGD_INLINE float quadric_hit_inl(const pbrtgpu_quadric *quads, int type, int idx, float ox, float oy, float oz, float dx,
                                  float dy, float dz, float mint, float maxt, float time) {
     Ray ray;
     ray.o = v3(ox, oy, oz); ray.d = v3(dx, dy, dz); ray.mint = mint; ray.maxt = maxt; ray.time = time;
     float t, e;
-    const bool hit = type == PBRTGPU_SHAPE_SPHERE ? sphere_intersect(quads[idx], ray, &t, &e, nullptr)
-                                                  : disk_intersect(quads[idx], ray, &t, &e, nullptr);
+    const bool hit = type == PBRTGPU_SHAPE_DISK ? disk_intersect(quads[idx], ray, &t, &e, nullptr)
+                                                : sphere_cyl_hit(quads[idx], ray, type == PBRTGPU_SHAPE_CYLINDER, &t);
     return hit ? t : -INFINITY;   // a hit has t >= mint >= 0 (or NaN)
 }
 __device__ PGD_QUAD_ATTR float quadric_hit(const pbrtgpu_quadric *quads, int type, int idx, float ox, float oy, float oz,
@@ -1225,7 +1309,8 @@ PGD_HEAVY void isect_fill(const DevScene &S, const Ray &ray, int prim, float t, 
 enum { BSDF_REFLECTION = 1, BSDF_TRANSMISSION = 2, BSDF_DIFFUSE = 4, BSDF_GLOSSY = 8, BSDF_SPECULAR = 16, BSDF_ALL = 31 };
 enum { BX_LAMBERT, BX_OREN, BX_MICRO_BLINN_DIEL, BX_SPEC_REFL_NOOP, BX_FRESNEL_BLEND_ANISO, BX_MEASURED_IRREG,
        BX_MICRO_BLINN_COND, BX_SPEC_REFL_DIEL, BX_SPEC_TRANS,    // a = index of refraction for these two
-       BX_MEASURED_HALF };                                        // RegularHalfangleBRDF: R = first texel
+       BX_MEASURED_HALF,                                          // RegularHalfangleBRDF: R = first texel
+       BX_ANISOWARD };                                            // AnisoWardBrdf: R = Rs, a = Ax, b = Ay
 // R, R2: offsets into DevScene::spectra, or -1 for the per-slot textured spectrum (K bands)
 struct BxDF { int kind, type; int R, R2; float a, b; };
 // eta: BSDF::eta, the glass material's index (glass.cpp:47-48), 1 otherwise (DirectLighting's
@@ -1476,6 +1561,20 @@ PGD_INLINE FTerm bx_term(PowMemo &pm, const BxDF &b, V wo, V wi) {
         case BX_MEASURED_HALF: {
             const int idx = halfangle_index(wo, wi);
             if (idx >= 0) { t.kind = T_MERL; t.R2 = idx; }
+            break;
+        }
+        case BX_ANISOWARD: {   // AnisoWardBrdf::f (AnisoWardBrdf.cpp:10-23): Rs * expTerm / (sqrt(cos cos) 4 pi Ax Ay)
+            const V wh = vadd(wi, wo);
+            if (wh.z == 0.f) break;
+            float cc = wi.z * wo.z;
+            if (cc <= 0.f) break;
+            const float invAx2 = 1.0f / (b.a * b.a), invAy2 = 1.0f / (b.b * b.b);
+            const float fourPiAxAy = (4.0f * kPi * b.a * b.b);
+            const float expTerm = libmf_expf(-1.0f * (wh.x * wh.x * invAx2 + wh.y * wh.y * invAy2) / (wh.z * wh.z));
+            cc = sqrtf(cc);
+            // ((Rs * expTerm) * 1 * 1) / den: T_BLINN's band operation with unit G and F
+            t.kind = T_BLINN;
+            t.s0 = expTerm; t.s1 = 1.f; t.s2 = 1.f; t.s3 = cc * fourPiAxAy;
             break;
         }
         default: break;   // SpecularReflection::f == 0
@@ -2184,6 +2283,15 @@ PGD_HEAVY void get_bsdf(const DevScene &S, const Isect &is, const float diff[4],
             x.a = x.b = 0.f;
             break;
         }
+        case PBRTGPU_MAT_ANISOWARD: {   // anisoward.cpp:35-60: Lambertian(Kd) + AnisoWardBrdf(Ks, alphaU, alphaV)
+            BxDF &x0 = bs.bx[bs.n++];
+            x0.kind = BX_LAMBERT; x0.type = BSDF_REFLECTION | BSDF_DIFFUSE; x0.R = off[0]; x0.R2 = x0.R;
+            x0.a = x0.b = 0.f;
+            BxDF &x1 = bs.bx[bs.n++];
+            x1.kind = BX_ANISOWARD; x1.type = BSDF_REFLECTION | BSDF_GLOSSY; x1.R = off[1]; x1.R2 = x1.R;
+            x1.a = f0; x1.b = fp1;   // sampled and weighed by BxDF's cosine defaults (reflection.cpp:303-315)
+            break;
+        }
         case PBRTGPU_MAT_SUBSTRATE: {
             BxDF &x = bs.bx[bs.n++];
             x.kind = BX_FRESNEL_BLEND_ANISO; x.type = BSDF_REFLECTION | BSDF_GLOSSY;
@@ -2247,6 +2355,14 @@ PGD_INLINE float shape_pdf(const DevScene &S, int type, int idx, V p, V wi) {
 }
 PGD_INLINE V shape_sample_p(const DevScene &S, int type, int idx, V p, float u1, float u2, V *ns) {
     if (type == PBRTGPU_SHAPE_SPHERE) return sphere_sample_p((*sa(S.quads, (uint32_t)(idx))), p, u1, u2, ns);
+    if (type == PBRTGPU_SHAPE_CYLINDER) {   // Cylinder::Sample (cylinder.cpp:195-203)
+        const pbrtgpu_quadric &q = (*sa(S.quads, (uint32_t)(idx)));
+        const float z = lerpf(u1, q.zmin, q.zmax), t = u2 * q.phi_max;
+        const V pp = v3(q.radius * COSF(t), q.radius * SINF(t), z);
+        *ns = vnorm(xnormal(q.o2w_minv, v3(pp.x, pp.y, 0.f)));
+        if (q.reverse_orientation) *ns = vmul(*ns, -1.f);
+        return xpoint(q.o2w_m, pp);
+    }
     if (type == PBRTGPU_SHAPE_DISK) {
         const pbrtgpu_quadric &q = (*sa(S.quads, (uint32_t)(idx)));
         V pp;

@@ -383,7 +383,7 @@ static inline int scene_check(const pbrtgpu_flat_scene *s, std::string *err) {
     }
     for (int i = 0; i < s->n_materials; ++i) {
         const pbrtgpu_material &m = s->materials[i];
-        if (m.type < PBRTGPU_MAT_MATTE || m.type > PBRTGPU_MAT_MEASURED_HALFANGLE)
+        if (m.type < PBRTGPU_MAT_MATTE || m.type > PBRTGPU_MAT_ANISOWARD)
             SB_FAIL(PBRTGPU_E_UNSUPPORTED, "material type not yet supported on the GPU");
         // textured spectra in slots 0 and 1 only (device.h get_bsdf's two K buffers), textured float
         // parameters f[0], f[1]; the measured materials have none

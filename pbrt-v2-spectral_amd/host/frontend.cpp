@@ -171,12 +171,13 @@ struct Quadric {
     pbrtgpu_quadric q{};
     Xform o2w;
     BBox ObjectBound() const {
-        if (q.type == PBRTGPU_SHAPE_SPHERE)
+        if (q.type == PBRTGPU_SHAPE_SPHERE || q.type == PBRTGPU_SHAPE_CYLINDER)   // cylinder.cpp:40-44
             return BBox(V3(-q.radius, -q.radius, q.zmin), V3(q.radius, q.radius, q.zmax));
         return BBox(V3(-q.radius, -q.radius, q.height), V3(q.radius, q.radius, q.height));
     }
     float Area() const {
         if (q.type == PBRTGPU_SHAPE_SPHERE) return q.phi_max * q.radius * (q.zmax - q.zmin);
+        if (q.type == PBRTGPU_SHAPE_CYLINDER) return (q.zmax - q.zmin) * q.phi_max * q.radius;   // cylinder.cpp:180-182
         return q.phi_max * 0.5f * (q.radius * q.radius - q.inner_radius * q.inner_radius);
     }
     int flatIndex = -1;
@@ -1262,6 +1263,12 @@ private:
         } else if (name == "mirror") {   // mirror.cpp
             mt.type = PBRTGPU_MAT_MIRROR;
             SpecSlot(*mo, 0, g, m, "Kr", spec.Const(0.9f), true);
+        } else if (name == "anisoward") {   // anisoward.cpp:62-74 (the fork's anisotropic Ward material)
+            mt.type = PBRTGPU_MAT_ANISOWARD;
+            SpecSlot(*mo, 0, g, m, "Kd", spec.Const(0.25f), true);
+            SpecSlot(*mo, 1, g, m, "Ks", spec.Const(0.25f), true);
+            FloatSlot(*mo, 0, g, m, "alphaU", .1f);
+            FloatSlot(*mo, 1, g, m, "alphaV", .1f);
         } else if (name == "substrate") {   // substrate.cpp
             mt.type = PBRTGPU_MAT_SUBSTRATE;
             SpecSlot(*mo, 0, g, m, "Kd", spec.Const(.5f), true);
@@ -1758,7 +1765,7 @@ private:
             for (size_t i = 0; i < pts.size(); ++i) pts[i] = V3(P->f[3 * i], P->f[3 * i + 1], P->f[3 * i + 2]);
             s->kind = ShapeObj::LOOP; s->o2w = o2w; s->ro = ro; s->nLevels = nlevels;
             LoopInit(*s, (int)vi->i.size() / 3, (int)pts.size(), vi->i.data(), pts.data());
-        } else if (name == "sphere" || name == "disk") {
+        } else if (name == "sphere" || name == "disk" || name == "cylinder") {
             auto q = std::make_shared<Quadric>();
             q->o2w = o2w;
             pbrtgpu_quadric &Q = q->q;
@@ -1775,6 +1782,13 @@ private:
                 Q.theta_min = acosf(Clamp(Q.zmin / radius, -1.f, 1.f));
                 Q.theta_max = acosf(Clamp(Q.zmax / radius, -1.f, 1.f));
                 Q.phi_max = Radians(Clamp(pm, 0.0f, 360.0f));
+            } else if (name == "cylinder") {   // cylinder.cpp:30-37, 184-192
+                const float radius = p.FindOneFloat("radius", 1), z0 = p.FindOneFloat("zmin", -1), z1 = p.FindOneFloat("zmax", 1);
+                Q.type = PBRTGPU_SHAPE_CYLINDER;
+                Q.radius = radius;
+                Q.zmin = pmin(z0, z1);
+                Q.zmax = pmax(z0, z1);
+                Q.phi_max = Radians(Clamp(p.FindOneFloat("phimax", 360), 0.0f, 360.0f));
             } else {   // disk.cpp:32-38, 125-131
                 Q.type = PBRTGPU_SHAPE_DISK;
                 Q.height = p.FindOneFloat("height", 0.);

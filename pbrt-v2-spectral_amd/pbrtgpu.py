@@ -22,7 +22,7 @@ ROOT = os.path.dirname(HERE)
 LIBDIR = os.path.join(HERE, "lib")
 
 MAX_BANDS = 64
-SHAPE_TRIANGLE, SHAPE_SPHERE, SHAPE_DISK = 0, 1, 2
+SHAPE_TRIANGLE, SHAPE_SPHERE, SHAPE_DISK, SHAPE_CYLINDER = 0, 1, 2, 4
 
 
 class BVHNode(ctypes.Structure):
@@ -348,8 +348,8 @@ def _arr(ptr, ctype, n):
 
 def prim_bounds(scene):
     """[n_prims][6] float32 world bounds of the scene's primitives (bmin, bmax): a triangle's
-    three world-space vertices (Triangle::WorldBound, trianglemesh.cpp:97-103); a sphere's or
-    disk's object bound (sphere.cpp:42-46, disk.cpp:41-45) through ObjectToWorld's eight corners
+    three world-space vertices (Triangle::WorldBound, trianglemesh.cpp:97-103); a sphere's, disk's
+    or cylinder's object bound (sphere.cpp:42-46, disk.cpp:41-45, cylinder.cpp:40-44) through ObjectToWorld's eight corners
     (transform.cpp:144-156), evaluated in double and rounded outward to float.  The input of
     the GPU BVH build (pbrtgpu_build_bvh)."""
     f = scene.flat
@@ -372,7 +372,7 @@ def prim_bounds(scene):
         for i in quads:
             r = q[prims[i, 1]]
             rad, zmin, zmax, h = float(r[36]), float(r[37]), float(r[38]), float(r[42])
-            if qt[prims[i, 1]] == SHAPE_SPHERE:
+            if qt[prims[i, 1]] in (SHAPE_SPHERE, SHAPE_CYLINDER):   # cylinder.cpp:40-44
                 lo, hi = (-rad, -rad, zmin), (rad, rad, zmax)
             else:
                 lo, hi = (-rad, -rad, h), (rad, rad, h)

@@ -101,7 +101,8 @@ def _golden_scene(pg, cfg, name="killeroo"):
     pack = {"anim": "anim-killeroos-moving.pack", "bunny": "bunny.pack", "metal": "metal.pack",
             "coverage": "coverage.pack", "imagemap": "imagemap.pack",
             "animcam": "animcam.pack", "textured": "textured.pack", "envmap": "envmap.pack", "lights": "lights.pack",
-            "ortho": "ortho.pack", "heightfield": "heightfield.pack"}.get(name.split("_")[0],
+            "ortho": "ortho.pack", "heightfield": "heightfield.pack",
+            "cylinder": "cylinder.pack", "anisoward": "anisoward.pack"}.get(name.split("_")[0],
                                                                                               "killeroo-simple.pack")
     if "_b30_" in name:
         pack = pack.replace(".pack", "-b30.pack")
@@ -115,7 +116,8 @@ def _golden_scene(pg, cfg, name="killeroo"):
                                   "anim_keys_c5_600x600s512", "killeroo_b30_paths_48x40s4",
                                   "coverage_b30_paths_48x36s4", "imagemap_paths_64x48s4",
                                   "imagemap_paths_96x72s2_seed5", "animcam_paths_64x48s4", "textured_paths_64x48s4", "envmap_paths_64x48s4",
-                                  "lights_paths_64x48s4", "ortho_paths_64x48s4", "heightfield_paths_64x48s4"])
+                                  "lights_paths_64x48s4", "ortho_paths_64x48s4", "heightfield_paths_64x48s4",
+         "cylinder_paths_64x48s4", "anisoward_paths_64x48s4"])
 def test_paths_vs_reference_golden(pg, name):
     """GPU against the reference harness's own per-path radiance (fixed seeds); the *_keys_*
     fixtures are the configs at their real resolution and sample count."""
@@ -132,7 +134,8 @@ def test_paths_vs_reference_golden(pg, name):
                                   "metal_film_40x40s8", "coverage_film_64x48s8", "killeroo_b30_film_40x32s8",
                                   "coverage_b30_film_40x30s4", "imagemap_film_64x48s8",
                                   "animcam_film_64x48s4", "textured_film_64x48s8", "envmap_film_64x48s8",
-                                  "lights_film_64x48s8", "ortho_film_64x48s4", "heightfield_film_64x48s4"])
+                                  "lights_film_64x48s8", "ortho_film_64x48s4", "heightfield_film_64x48s4",
+                                  "cylinder_film_64x48s4", "anisoward_film_64x48s4"])
 def test_film_vs_reference_golden(pg, name):
     """Whole-film render against the reference's film (raw sums, incl. neighbour-pixel
     samples): bit for bit."""
@@ -334,7 +337,7 @@ def test_regular_halfangle_brdf_vs_reference_golden(pg, merl_dir):
     assert_bit_exact(L, pg.oracle().trace_paths(scene, g["keys"]), "merl paths vs oracle")
 
 
-DL = ["ortho_dl_%s_48x36s4", "lights_dl_%s_48x36s4", "textured_dl_%s_48x36s4", "envmap_dl_%s_48x36s4", "killeroo_dl_%s_48x40s4", "bunny_dl_%s_48x27s4", "anim_dl_%s_40x40s4", "coverage_dl_%s_64x48s4",
+DL = ["anisoward_dl_%s_48x36s4", "cylinder_dl_%s_48x36s4", "ortho_dl_%s_48x36s4", "lights_dl_%s_48x36s4", "textured_dl_%s_48x36s4", "envmap_dl_%s_48x36s4", "killeroo_dl_%s_48x40s4", "bunny_dl_%s_48x27s4", "anim_dl_%s_40x40s4", "coverage_dl_%s_64x48s4",
       "coverage_dlone_%s_64x48s4"]
 
 

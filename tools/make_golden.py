@@ -58,6 +58,10 @@ Fixtures (numpy .npz, inputs + expected outputs only):
                                   index, metal eta / k unclamped), path and DirectLighting
   envmap_*                        tests/scenes/envmap.pbrt: an image-based infinite light (decoded PFM
                                   lat-long map: radiance MIPMap, Distribution2D sampling and pdf)
+  anisoward_*                     tests/scenes/anisoward.pbrt: the fork's anisotropic Ward material
+                                  (anisoward.cpp, AnisoWardBrdf.cpp), path and DirectLighting
+  cylinder_*                      tests/scenes/cylinder.pbrt: cylinders (phimax, inside / outside hits,
+                                  textured, reversed, area light), path and DirectLighting
   heightfield_*                   tests/scenes/heightfield.pbrt: heightfield shapes (terrain, area
                                   light), path and metadata (mesh ids)
   ortho_*                         tests/scenes/ortho.pbrt: the orthographic camera (screen window,
@@ -76,7 +80,7 @@ Fixtures (numpy .npz, inputs + expected outputs only):
                                   pixel holds all of its contributions (incl. exact-boundary samples
                                   of its neighbours, spectralImage.cpp:77-152); C2 at the sphere
                                   light's edge and at a killeroo silhouette, C3-C5 at an edge each
-Usage: python tools/make_golden.py [--only keys|dat|merl|dl|meta|spec|rgb|rgbfeat|lights|ortho|heightfield|b30|window|imagemap|animcam|gpupath|textured|envmap]
+Usage: python tools/make_golden.py [--only keys|dat|merl|dl|meta|spec|rgb|rgbfeat|lights|ortho|heightfield|cylinder|anisoward|b30|window|imagemap|animcam|gpupath|textured|envmap]
        (after `make -C oracle ref`, `ref60`, `ref30` and `refrgb`)
 """
 import os
@@ -390,6 +394,28 @@ def heightfield_fixtures(tmp):
     film_fixture("heightfield_meta_mesh_film_48x36s2", (48, 36), 2, 0, 5, tmp, scene=sc, extra=ex)
 
 
+def cylinder_fixtures(tmp):
+    """tests/scenes/cylinder.pbrt: cylinders (phimax cut, both roots, textured, reversed, an area
+    light); path and DirectLighting"""
+    sc = os.path.join(ROOT, "tests", "scenes", "cylinder.pbrt")
+    paths_fixture("cylinder_paths_64x48s4", (64, 48), 4, 0, 5, 1, tmp, scene=sc)
+    film_fixture("cylinder_film_64x48s4", (64, 48), 4, 0, 5, tmp, scene=sc)
+    ex = ("--surf", "directlighting", "--dl-strategy", "all")
+    paths_fixture("cylinder_dl_paths_48x36s4", (48, 36), 4, 0, 5, 1, tmp, scene=sc, extra=ex)
+    film_fixture("cylinder_dl_film_48x36s4", (48, 36), 4, 0, 5, tmp, scene=sc, extra=ex)
+
+
+def anisoward_fixtures(tmp):
+    """tests/scenes/anisoward.pbrt: the fork's anisotropic Ward material (constant, anisotropic,
+    textured parameters); path and DirectLighting, and the RGB build"""
+    sc = os.path.join(ROOT, "tests", "scenes", "anisoward.pbrt")
+    paths_fixture("anisoward_paths_64x48s4", (64, 48), 4, 0, 5, 1, tmp, scene=sc)
+    film_fixture("anisoward_film_64x48s4", (64, 48), 4, 0, 5, tmp, scene=sc)
+    ex = ("--surf", "directlighting", "--dl-strategy", "all")
+    paths_fixture("anisoward_dl_paths_48x36s4", (48, 36), 4, 0, 5, 1, tmp, scene=sc, extra=ex)
+    film_fixture("anisoward_dl_film_48x36s4", (48, 36), 4, 0, 5, tmp, scene=sc, extra=ex)
+
+
 def envmap_fixtures(tmp):
     """tests/scenes/envmap.pbrt: an image-based InfiniteAreaLight (a decoded PFM lat-long map: its
     radiance MIPMap and Distribution2D), path integrator and DirectLighting"""
@@ -447,6 +473,10 @@ def main():
                 spec_fixtures(tmp)
             elif only == "rgb":
                 rgb_fixtures(tmp)
+            elif only == "anisoward":
+                anisoward_fixtures(tmp)
+            elif only == "cylinder":
+                cylinder_fixtures(tmp)
             elif only == "heightfield":
                 heightfield_fixtures(tmp)
             elif only == "ortho":
