@@ -93,8 +93,11 @@ enum {
                                           * 90 x 90 x 180 RGB table in merl[] (3 floats per texel),
                                           * -1 when the file could not be read (no BxDF, as the
                                           * reference's MeasuredMaterial then adds none) */
-    PBRTGPU_MAT_ANISOWARD = 8   /* the fork's anisotropic Ward material (materials/anisoward.cpp,
+    PBRTGPU_MAT_ANISOWARD = 8,  /* the fork's anisotropic Ward material (materials/anisoward.cpp,
                                  * AnisoWardBrdf.cpp): spec[0]=Kd, spec[1]=Ks; f[0]=alphaU, f[1]=alphaV */
+    PBRTGPU_MAT_SHINYMETAL = 9  /* shinymetal.cpp: spec[0] = FresnelApproxEta(Ks.Clamp()), spec[1] =
+                                 * FresnelApproxEta(Kr.Clamp()) (constant Ks / Kr), spec[2] = k = 0;
+                                 * f[0]=roughness */
 };
 
 /* Texture<float> / Texture<Spectrum> (texture.h, textures/{constant,scale,imagemap}.cpp).

@@ -768,7 +768,8 @@ enum { BSDF_REFLECTION = 1, BSDF_TRANSMISSION = 2, BSDF_DIFFUSE = 4, BSDF_GLOSSY
 enum { BX_LAMBERT, BX_OREN, BX_MICRO_BLINN_DIEL, BX_SPEC_REFL_NOOP, BX_FRESNEL_BLEND_ANISO, BX_MEASURED_IRREG,
        BX_MICRO_BLINN_COND, BX_SPEC_REFL_DIEL, BX_SPEC_TRANS,    /* eta_t = index of refraction for these two */
        BX_MEASURED_HALF,                                          /* RegularHalfangleBRDF: merl = its table */
-       BX_ANISOWARD };                                            /* AnisoWardBrdf: R = Rs, a = Ax, b = Ay */
+       BX_ANISOWARD,                                              /* AnisoWardBrdf: R = Rs, a = Ax, b = Ay */
+       BX_SPEC_REFL_COND };                                       /* SpecularReflection(1, FresnelConductor(eta, 0)) */
 typedef struct {
     int kind, type;
     const float *R;      /* reflectance spectrum */
@@ -1039,6 +1040,7 @@ static void bx_f_add(const Ctx *c, const BxDF *b, V wo, V wi, float *out) {
         }
         case BX_SPEC_REFL_NOOP:
         case BX_SPEC_REFL_DIEL:
+        case BX_SPEC_REFL_COND:
         case BX_SPEC_TRANS:
             for (int i = 0; i < nb; ++i) out[i] += 0.f;
             break;
@@ -1082,6 +1084,7 @@ static float bx_pdf(const BxDF *b, V wo, V wi) {
             return blinn_pdf(b->a, wo, wi);
         case BX_SPEC_REFL_NOOP:
         case BX_SPEC_REFL_DIEL:
+        case BX_SPEC_REFL_COND:
         case BX_SPEC_TRANS: return 0.;
         case BX_FRESNEL_BLEND_ANISO:
             if (!samehemi(wo, wi)) return 0.f;
@@ -1112,6 +1115,13 @@ static void bx_sample_f(const Ctx *c, const BxDF *b, V wo, V *wi, float u1, floa
             *pdf = 1.f;
             float F = fr_dielectric(costh(wo), 1.f, b->eta_t), d = abscos(*wi);
             for (int i = 0; i < nb; ++i) fout[i] = (F * b->R[i]) / d;
+            return;
+        }
+        case BX_SPEC_REFL_COND: {   /* SpecularReflection::Sample_f, FresnelConductor(eta, 0) (reflection.cpp:102-104) */
+            *wi = v3(-wo.x, -wo.y, wo.z);
+            *pdf = 1.f;
+            float ci = fabsf(costh(wo)), d = abscos(*wi);
+            for (int i = 0; i < nb; ++i) fout[i] = (fr_cond(ci, b->eta[i], 0.f) * 1.f) / d;
             return;
         }
         case BX_SPEC_TRANS: {   /* SpecularTransmission::Sample_f (reflection.cpp:139-162) */
@@ -1610,6 +1620,18 @@ static void get_bsdf(const Ctx *c, const Isect *is, const float diff[4], BSDF *b
             float e = 1.f / fp[0];
             if (e > 10000.f || isnan(e)) e = 10000.f;
             x->a = e;
+            break;
+        }
+        case PBRTGPU_MAT_SHINYMETAL: {   /* shinymetal.cpp:45-68 */
+            BxDF *x = &bs->bx[bs->n++];
+            x->kind = BX_MICRO_BLINN_COND; x->type = BSDF_REFLECTION | BSDF_GLOSSY;
+            x->eta = K[0]; x->k = SPEC(c, mt->spec[2]);
+            float e = 1.f / fp[0];
+            if (e > 10000.f || isnan(e)) e = 10000.f;
+            x->a = e;
+            x = &bs->bx[bs->n++];
+            x->kind = BX_SPEC_REFL_COND; x->type = BSDF_REFLECTION | BSDF_SPECULAR;
+            x->eta = SPEC(c, mt->spec[1]);
             break;
         }
         case PBRTGPU_MAT_MIRROR: {

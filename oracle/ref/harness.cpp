@@ -73,6 +73,7 @@
 #include "materials/matte.h"
 #include "materials/plastic.h"
 #include "materials/anisoward.h"
+#include "materials/shinymetal.h"
 #include "materials/metal.h"
 #include "materials/substrate.h"
 #include "materials/measured.h"
@@ -81,6 +82,7 @@
 #include "shapes/sphere.h"
 #include "shapes/heightfield.h"
 #include "shapes/cylinder.h"
+#include "shapes/nurbs.h"
 // output channels of a radiance: the spectrum's bands, or RGB in the C1 build (HARNESS_RGB:
 // Spectrum = RGBSpectrum, pbrt.h:144)
 #ifdef HARNESS_RGB
@@ -444,6 +446,7 @@ static Reference<Material> MakeMat(const string &n, const Transform &x, const Te
     if (n == "metal") return CreateMetalMaterial(x, mp);
     if (n == "substrate") return CreateSubstrateMaterial(x, mp);
     if (n == "anisoward") return CreateAnisoWardMaterial(x, mp);
+    if (n == "shinymetal") return CreateShinyMetalMaterial(x, mp);
     if (n == "measured") return CreateMeasuredMaterial(x, mp);
     if (n == "mirror") return CreateMirrorMaterial(x, mp);
     if (n == "glass") return CreateGlassMaterial(x, mp);
@@ -474,6 +477,7 @@ static Reference<Shape> MakeShp(const string &n, const Transform *o2w, const Tra
     if (n == "loopsubdiv") return CreateLoopSubdivShape(o2w, w2o, ro, p);
     if (n == "heightfield") return CreateHeightfieldShape(o2w, w2o, ro, p);
     if (n == "cylinder") return CreateCylinderShape(o2w, w2o, ro, p);
+    if (n == "nurbs") return CreateNURBSShape(o2w, w2o, ro, p);
     fprintf(stderr, "harness: shape %s unsupported\n", n.c_str()); exit(2);
 }
 static Reference<Material> CreateMaterialFromState(const ParamSet &params) {

@@ -1310,7 +1310,8 @@ enum { BSDF_REFLECTION = 1, BSDF_TRANSMISSION = 2, BSDF_DIFFUSE = 4, BSDF_GLOSSY
 enum { BX_LAMBERT, BX_OREN, BX_MICRO_BLINN_DIEL, BX_SPEC_REFL_NOOP, BX_FRESNEL_BLEND_ANISO, BX_MEASURED_IRREG,
        BX_MICRO_BLINN_COND, BX_SPEC_REFL_DIEL, BX_SPEC_TRANS,    // a = index of refraction for these two
        BX_MEASURED_HALF,                                          // RegularHalfangleBRDF: R = first texel
-       BX_ANISOWARD };                                            // AnisoWardBrdf: R = Rs, a = Ax, b = Ay
+       BX_ANISOWARD,                                              // AnisoWardBrdf: R = Rs, a = Ax, b = Ay
+       BX_SPEC_REFL_COND };                                       // SpecularReflection(1, FresnelConductor(R, 0))
 // R, R2: offsets into DevScene::spectra, or -1 for the per-slot textured spectrum (K bands)
 struct BxDF { int kind, type; int R, R2; float a, b; };
 // eta: BSDF::eta, the glass material's index (glass.cpp:47-48), 1 otherwise (DirectLighting's
@@ -1440,8 +1441,9 @@ PGD_INLINE void aniso_sample(float ex, float ey, V wo, V *wi, float u1, float u2
 // bands (fval_prepare, like T_MEAS)
 enum { T_ZERO = 0, T_LAMB, T_OREN, T_BLINN, T_FB, T_MEAS, T_BUF, T_BLINNC, T_MERL };
 struct FTerm { int kind; int R, R2; float s0, s1, s2, s3; };
-enum { FV_SUM = 0, FV_SPEC = 1 };
+enum { FV_SUM = 0, FV_SPEC = 1, FV_SPEC_COND = 2 };
 // FV_SPEC: a specular BxDF's sampled value (fs * R_i) / d (reflection.cpp:130-162)
+// FV_SPEC_COND: SpecularReflection(1, FresnelConductor(eta = R, k = 0)): (FrCond(fs, eta_i, 0) * 1) / d
 // The two terms are named members, not an array: any access through a runtime index (or an
 // address the compiler selects between them) keeps the whole FVal in scratch memory, and the
 // band loops then reload its terms from there (r03: 3 x 64 scratch loads in k_shade's band loops)
@@ -1587,6 +1589,7 @@ PGD_INLINE float bx_pdf(PowMemo &pm, const BxDF &b, V wo, V wi) {
         case BX_MICRO_BLINN_COND: if (!samehemi(wo, wi)) return 0.f; return blinn_pdf(pm, b.a, wo, wi);
         case BX_SPEC_REFL_NOOP:
         case BX_SPEC_REFL_DIEL:
+        case BX_SPEC_REFL_COND:
         case BX_SPEC_TRANS: return 0.;
         case BX_FRESNEL_BLEND_ANISO:
             if (!samehemi(wo, wi)) return 0.f;
@@ -1603,6 +1606,12 @@ PGD_INLINE void bx_sample_specular(const BxDF &b, V wo, V *wi, float *pdf, FVal 
             *pdf = 1.f;
             F.mode = FV_SPEC; F.R = b.R; F.d = abscos(*wi);
             F.fs = b.kind == BX_SPEC_REFL_NOOP ? 1.f : fr_dielectric(wo.z, 1.f, b.a);
+            return;
+        case BX_SPEC_REFL_COND:    // ... with FresnelConductor(eta, 0): Evaluate(CosTheta(wo)) * 1 / |cos|
+            *wi = v3(-wo.x, -wo.y, wo.z);
+            *pdf = 1.f;
+            F.mode = FV_SPEC_COND; F.R = b.R; F.d = abscos(*wi);
+            F.fs = fabsf(wo.z);    // FresnelConductor::Evaluate takes |cosi| (reflection.cpp:102-104)
             return;
         case BX_SPEC_TRANS: {      // SpecularTransmission(T, 1, ior): (Spectrum(1) - F) * T / |cos|
             const bool entering = wo.z > 0.;
@@ -1636,6 +1645,7 @@ PGD_INLINE void bx_sample_f(PowMemo &pm, const BxDF &b, V wo, V *wi, float u1, f
             return;
         case BX_SPEC_REFL_NOOP:
         case BX_SPEC_REFL_DIEL:
+        case BX_SPEC_REFL_COND:
         case BX_SPEC_TRANS:
             bx_sample_specular(b, wo, wi, pdf, F);
             return;
@@ -2290,6 +2300,18 @@ PGD_HEAVY void get_bsdf(const DevScene &S, const Isect &is, const float diff[4],
             BxDF &x1 = bs.bx[bs.n++];
             x1.kind = BX_ANISOWARD; x1.type = BSDF_REFLECTION | BSDF_GLOSSY; x1.R = off[1]; x1.R2 = x1.R;
             x1.a = f0; x1.b = fp1;   // sampled and weighed by BxDF's cosine defaults (reflection.cpp:303-315)
+            break;
+        }
+        case PBRTGPU_MAT_SHINYMETAL: {   // shinymetal.cpp:45-68: Microfacet(1, FresnelConductor(etaKs, 0), Blinn(1/rough))
+            BxDF &x0 = bs.bx[bs.n++];     // + SpecularReflection(1, FresnelConductor(etaKr, 0))
+            x0.kind = BX_MICRO_BLINN_COND; x0.type = BSDF_REFLECTION | BSDF_GLOSSY;
+            x0.R = off[0]; x0.R2 = mt.spec[2];
+            float e = 1.f / f0;
+            if (e > 10000.f || isnan(e)) e = 10000.f;
+            x0.a = e; x0.b = 0.f;
+            BxDF &x1 = bs.bx[bs.n++];
+            x1.kind = BX_SPEC_REFL_COND; x1.type = BSDF_REFLECTION | BSDF_SPECULAR; x1.R = mt.spec[1]; x1.R2 = x1.R;
+            x1.a = x1.b = 0.f;
             break;
         }
         case PBRTGPU_MAT_SUBSTRATE: {

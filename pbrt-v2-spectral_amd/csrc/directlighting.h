@@ -287,12 +287,12 @@ PGD_INLINE Pushes dl_spec_step(const DevScene &S, const PathSoA &P, int slot, fl
         // ---- the specular branches of frame d
         uint32_t br = P.fBr[(size_t)d * c + slot];
         bool spawned = false;
-        // only mirror and glass have specular BxDFs: elsewhere the two BSDFSample(rng) draws
+        // only mirror, glass and shinymetal have specular BxDFs: elsewhere the two BSDFSample(rng) draws
         // still happen (the reference constructs them) but no child can be sampled, and the
         // vertex need not be rebuilt
         const int vprim = P.fHit[(size_t)2 * d * c + slot];
         const int vtype = (*sa(S.mats, (uint32_t)((*sa(S.prims, (uint32_t)(vprim))).material))).type;
-        const bool canSpec = vtype == PBRTGPU_MAT_MIRROR || vtype == PBRTGPU_MAT_GLASS;
+        const bool canSpec = vtype == PBRTGPU_MAT_MIRROR || vtype == PBRTGPU_MAT_GLASS || vtype == PBRTGPU_MAT_SHINYMETAL;
         if (!SPAWN && canSpec && d + 1 < S.maxDepth && br < 2u) {
             fl |= PF_DLSPEC;
             break;

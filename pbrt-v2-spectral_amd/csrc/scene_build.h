@@ -383,7 +383,7 @@ static inline int scene_check(const pbrtgpu_flat_scene *s, std::string *err) {
     }
     for (int i = 0; i < s->n_materials; ++i) {
         const pbrtgpu_material &m = s->materials[i];
-        if (m.type < PBRTGPU_MAT_MATTE || m.type > PBRTGPU_MAT_ANISOWARD)
+        if (m.type < PBRTGPU_MAT_MATTE || m.type > PBRTGPU_MAT_SHINYMETAL)
             SB_FAIL(PBRTGPU_E_UNSUPPORTED, "material type not yet supported on the GPU");
         // textured spectra in slots 0 and 1 only (device.h get_bsdf's two K buffers), textured float
         // parameters f[0], f[1]; the measured materials have none
@@ -663,6 +663,7 @@ static int scene_build(const pbrtgpu_flat_scene *s, int topNodes, DevScene &S, i
     for (int i = 0; i < s->n_materials; ++i) {
         const pbrtgpu_material &m = s->materials[i];
         if (m.type == PBRTGPU_MAT_MEASURED || m.type == PBRTGPU_MAT_MEASURED_HALFANGLE) *feat |= FEAT_MEAS;
+        if (m.type == PBRTGPU_MAT_SHINYMETAL) *feat |= FEAT_TEX;   // its conductor SpecularReflection (fval4)
         if (m.bump_tex >= 0 || m.normal_tex >= 0 || m.tex[0] >= 0 || m.tex[1] >= 0 || m.tex[2] >= 0 || m.tex[3] >= 0 ||
             m.ftex[0] >= 0 || m.ftex[1] >= 0)
             *feat |= FEAT_TEX;

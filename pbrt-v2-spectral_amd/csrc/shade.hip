@@ -218,15 +218,17 @@ static hipError_t launch(int grid, hipStream_t stream, const DevScene &S, const 
 //              same pass (as k_shade's regeneration does for the others), so a slot is not left
 //              idle for a pass -- without it a C2 frame took 76 passes instead of 52.
 // 2 waves/SIMD for <= 32 bands (k_dl_nee: 47 VGPRs spilled, k_dl_spec: 148) and for the 60-band
-// FEAT 0 kernels since the light-sample list (k_dl_nee 90, k_dl_spec 146 spilled, 768 / 912 B of
-// scratch per lane); the 60-band all-features kernels stay at 1 wave/SIMD to keep within
-// tools/kernel_budget.py (at 2 waves k_dl_nee spills 225 VGPRs, 1,300 B of scratch)
-#define PGD_DL_WAVES ((SHADE_NB > 32 && SHADE_FEAT != 0) ? 1 : 2)
+// FEAT 0 k_dl_nee since the light-sample list (90 spilled, 768 B of scratch per lane); the 60-band
+// k_dl_spec and the all-features k_dl_nee stay at 1 wave/SIMD to keep within tools/kernel_budget.py
+// (at 2 waves k_dl_nee<60, 7> spills 225 VGPRs, 1,300 B; k_dl_spec<60, 0> 160, 1,056 B once
+// shinymetal's conductor mirror lobe joined the specular sampler)
+#define PGD_NEE_WAVES ((SHADE_NB > 32 && SHADE_FEAT != 0) ? 1 : 2)
+#define PGD_SPEC_WAVES (SHADE_NB > 32 ? 1 : 2)
 #ifndef PGD_NEE_ATTR
-#define PGD_NEE_ATTR __attribute__((amdgpu_waves_per_eu(PGD_DL_WAVES, PGD_DL_WAVES)))
+#define PGD_NEE_ATTR __attribute__((amdgpu_waves_per_eu(PGD_NEE_WAVES, PGD_NEE_WAVES)))
 #endif
 #ifndef PGD_SPEC_ATTR
-#define PGD_SPEC_ATTR __attribute__((amdgpu_waves_per_eu(PGD_DL_WAVES, PGD_DL_WAVES)))
+#define PGD_SPEC_ATTR __attribute__((amdgpu_waves_per_eu(PGD_SPEC_WAVES, PGD_SPEC_WAVES)))
 #endif
 // k_dl_nee: thread i takes entry i of the pass's light-sample list (PathSoA::dlList, CNT_DLN
 // entries); blocks past its end return at once

@@ -183,6 +183,57 @@ struct Quadric {
     int flatIndex = -1;
 };
 struct LoopSubdivShape;
+// NURBS evaluation (nurbs.cpp:33-141), in the reference's float operations and order: the
+// de Boor triangle over one knot span of homogeneous control points, the derivative from the last
+// step.  Control point k of a call is cp[k * stride - bias] (the reference offsets the pointer).
+struct NurbsH3 { float x = 0.f, y = 0.f, z = 0.f, w = 0.f; };
+static int NurbsKnotOffset(const float *knot, int order, float t) {
+    int k = order - 1;
+    while (t > knot[k + 1]) ++k;
+    return k;
+}
+static NurbsH3 NurbsEvaluate(int order, const float *knot, const NurbsH3 *cp, int bias, int cpStride, float t, V3 *deriv) {
+    const int ko = NurbsKnotOffset(knot, order, t);
+    knot += ko;
+    const int cpOffset = ko - order + 1;
+    std::vector<NurbsH3> w(order);
+    for (int i = 0; i < order; ++i) w[i] = cp[(cpOffset + i) * cpStride - bias];
+    for (int i = 0; i < order - 2; ++i)
+        for (int j = 0; j < order - 1 - i; ++j) {
+            const float alpha = (knot[1 + j] - t) / (knot[1 + j] - knot[j + 2 - order + i]);
+            w[j].x = w[j].x * alpha + w[j + 1].x * (1 - alpha);
+            w[j].y = w[j].y * alpha + w[j + 1].y * (1 - alpha);
+            w[j].z = w[j].z * alpha + w[j + 1].z * (1 - alpha);
+            w[j].w = w[j].w * alpha + w[j + 1].w * (1 - alpha);
+        }
+    const float alpha = (knot[1] - t) / (knot[1] - knot[0]);
+    NurbsH3 val;
+    val.x = w[0].x * alpha + w[1].x * (1 - alpha);
+    val.y = w[0].y * alpha + w[1].y * (1 - alpha);
+    val.z = w[0].z * alpha + w[1].z * (1 - alpha);
+    val.w = w[0].w * alpha + w[1].w * (1 - alpha);
+    if (deriv) {
+        const float factor = (order - 1) / (knot[1] - knot[0]);
+        const float dx = (w[1].x - w[0].x) * factor, dy = (w[1].y - w[0].y) * factor, dz = (w[1].z - w[0].z) * factor,
+                    dw = (w[1].w - w[0].w) * factor;
+        deriv->x = dx / val.w - (val.x * dw / (val.w * val.w));
+        deriv->y = dy / val.w - (val.y * dw / (val.w * val.w));
+        deriv->z = dz / val.w - (val.z * dw / (val.w * val.w));
+    }
+    return val;
+}
+static V3 NurbsEvaluateSurface(int uOrder, const float *uKnot, int ucp, float u, int vOrder, const float *vKnot, int vcp,
+                               float v, const NurbsH3 *cp, V3 *dPdu, V3 *dPdv) {
+    std::vector<NurbsH3> iso(std::max(uOrder, vOrder));
+    const int uFirstCp = NurbsKnotOffset(uKnot, uOrder, u) - uOrder + 1;
+    for (int i = 0; i < uOrder; ++i) iso[i] = NurbsEvaluate(vOrder, vKnot, cp + uFirstCp + i, 0, ucp, v, nullptr);
+    const int vFirstCp = NurbsKnotOffset(vKnot, vOrder, v) - vOrder + 1;
+    const NurbsH3 P = NurbsEvaluate(uOrder, uKnot, iso.data(), uFirstCp, 1, u, dPdu);
+    for (int i = 0; i < vOrder; ++i) iso[i] = NurbsEvaluate(uOrder, uKnot, cp + (size_t)(vFirstCp + i) * ucp, 0, 1, u, nullptr);
+    (void)NurbsEvaluate(vOrder, vKnot, iso.data(), vFirstCp, 1, v, dPdv);
+    (void)vcp;
+    return V3(P.x / P.w, P.y / P.w, P.z / P.w);
+}
 // an intersectable shape after refinement
 struct Isect {
     int kind;             // PBRTGPU_SHAPE_*
@@ -237,7 +288,7 @@ struct SDVertex { V3 P; int startFace = -1; int child = -1; bool regular = false
 struct SDFace { int v[3] = {-1, -1, -1}; int f[3] = {-1, -1, -1}; int children[4] = {-1, -1, -1, -1}; };
 
 struct ShapeObj {
-    enum { MESH, QUADRIC, LOOP, HFIELD } kind;   // HFIELD: a Heightfield, its TriangleMesh in mesh
+    enum { MESH, QUADRIC, LOOP, HFIELD } kind;   // HFIELD: a Heightfield or NURBS, its refined TriangleMesh in mesh
     std::shared_ptr<TriMesh> mesh;
     std::shared_ptr<Quadric> quad;
     // loop subdivision control mesh
@@ -1263,6 +1314,22 @@ private:
         } else if (name == "mirror") {   // mirror.cpp
             mt.type = PBRTGPU_MAT_MIRROR;
             SpecSlot(*mo, 0, g, m, "Kr", spec.Const(0.9f), true);
+        } else if (name == "shinymetal") {   // shinymetal.cpp:31-38 FresnelApproxEta, 45-84
+            mt.type = PBRTGPU_MAT_SHINYMETAL;
+            SpecTex kr = GetSpecTex(g, m, "Kr", spec.Const(1.f)), ks = GetSpecTex(g, m, "Ks", spec.Const(1.f));
+            if (!kr.constant || !ks.constant) throw std::runtime_error("shinymetal: textured Kr / Ks are not supported yet");
+            auto approxEta = [](const Spec &fr) {   // (1 + Sqrt(r)) / (1 - Sqrt(r)), r = Fr.Clamp(0, .999)
+                Spec e(fr.size());
+                for (size_t i = 0; i < fr.size(); ++i) {
+                    const float r = Clamp(fr[i], 0.f, .999f);
+                    e[i] = (1.f + sqrtf(r)) / (1.f - sqrtf(r));
+                }
+                return e;
+            };
+            mo->spectra.push_back(approxEta(SpecClamp(ks.value)));   // Ks->Evaluate(dgs).Clamp()
+            mo->spectra.push_back(approxEta(SpecClamp(kr.value)));   // Kr->Evaluate(dgs).Clamp()
+            mo->spectra.push_back(spec.Const(0.f));                  // k = 0.
+            FloatSlot(*mo, 0, g, m, "roughness", .1f);
         } else if (name == "anisoward") {   // anisoward.cpp:62-74 (the fork's anisotropic Ward material)
             mt.type = PBRTGPU_MAT_ANISOWARD;
             SpecSlot(*mo, 0, g, m, "Kd", spec.Const(0.25f), true);
@@ -1756,6 +1823,49 @@ private:
                     m->vi.insert(m->vi.end(), {v00, v10, v11, v00, v11, v01});
                 }
             s->kind = ShapeObj::HFIELD; s->mesh = m;
+            allMeshes.push_back(m);
+        } else if (name == "nurbs") {   // nurbs.cpp:221-298 Refine (30 x 30 dicing), 300-349 parameters
+            const int nu = p.FindOneInt("nu", -1), uorder = p.FindOneInt("uorder", -1);
+            const int nv = p.FindOneInt("nv", -1), vorder = p.FindOneInt("vorder", -1);
+            const Param *uk = p.Find(P_FLOAT, "uknots"), *vk = p.Find(P_FLOAT, "vknots");
+            if (nu < 1 || uorder < 2 || nv < 1 || vorder < 2 || !uk || !vk || (int)uk->f.size() != nu + uorder ||
+                (int)vk->f.size() != nv + vorder)
+                throw std::runtime_error("nurbs: nu / uorder / uknots and nv / vorder / vknots required");
+            const float u0 = p.FindOneFloat("u0", uk->f[uorder - 1]), u1 = p.FindOneFloat("u1", uk->f[nu]);
+            const float v0 = p.FindOneFloat("v0", vk->f[vorder - 1]), v1 = p.FindOneFloat("v1", vk->f[nv]);
+            std::vector<NurbsH3> Pw((size_t)nu * nv);
+            if (const Param *P = p.Find(P_POINT, "P")) {
+                if ((int)P->f.size() / 3 != nu * nv) { out->warnings.push_back("NURBS shape: control point count"); return nullptr; }
+                for (int i = 0; i < nu * nv; ++i) { Pw[i].x = P->f[3 * i]; Pw[i].y = P->f[3 * i + 1]; Pw[i].z = P->f[3 * i + 2]; Pw[i].w = 1.; }
+            } else if (const Param *Q = p.Find(P_FLOAT, "Pw")) {
+                if (Q->f.size() % 4 || (int)Q->f.size() / 4 != nu * nv) { out->warnings.push_back("NURBS shape: \"Pw\" count"); return nullptr; }
+                for (int i = 0; i < nu * nv; ++i) { Pw[i].x = Q->f[4 * i]; Pw[i].y = Q->f[4 * i + 1]; Pw[i].z = Q->f[4 * i + 2]; Pw[i].w = Q->f[4 * i + 3]; }
+            } else { out->warnings.push_back("Must provide control points via \"P\" or \"Pw\" parameter to NURBS shape."); return nullptr; }
+            const int dice = 30;
+            float ueval[dice], veval[dice];
+            for (int i = 0; i < dice; ++i) ueval[i] = Lerp((float)i / (float)(dice - 1), u0, u1);
+            for (int i = 0; i < dice; ++i) veval[i] = Lerp((float)i / (float)(dice - 1), v0, v1);
+            auto m = std::make_shared<TriMesh>();
+            m->o2w = o2w; m->ro = ro; m->swaps = o2w.SwapsHandedness();
+            m->nverts = dice * dice; m->ntris = 2 * (dice - 1) * (dice - 1);
+            m->p.resize(m->nverts); m->n.resize(m->nverts); m->uv.resize(2 * (size_t)m->nverts);
+            for (int v = 0; v < dice; ++v)
+                for (int u = 0; u < dice; ++u) {
+                    const int k = v * dice + u;
+                    m->uv[2 * k] = ueval[u]; m->uv[2 * k + 1] = veval[v];
+                    V3 dPdu, dPdv;
+                    const V3 pt = NurbsEvaluateSurface(uorder, uk->f.data(), nu, ueval[u], vorder, vk->f.data(), nv, veval[v],
+                                                       Pw.data(), &dPdu, &dPdv);
+                    m->p[k] = o2w.Point(pt);
+                    m->n[k] = Normalize(Cross(dPdu, dPdv));
+                }
+            m->vi.reserve(3 * (size_t)m->ntris);
+            for (int v = 0; v < dice - 1; ++v)
+                for (int u = 0; u < dice - 1; ++u) {
+                    const int a = v * dice + u, b = v * dice + u + 1, c2 = (v + 1) * dice + u + 1, d = (v + 1) * dice + u;
+                    m->vi.insert(m->vi.end(), {a, b, c2, a, c2, d});
+                }
+            s->kind = ShapeObj::HFIELD; s->mesh = m;   // refined into one TriangleMesh, as a heightfield
             allMeshes.push_back(m);
         } else if (name == "loopsubdiv") {   // loopsubdiv.cpp:489-502
             int nlevels = p.FindOneInt("nlevels", 3);

@@ -58,6 +58,10 @@ Fixtures (numpy .npz, inputs + expected outputs only):
                                   index, metal eta / k unclamped), path and DirectLighting
   envmap_*                        tests/scenes/envmap.pbrt: an image-based infinite light (decoded PFM
                                   lat-long map: radiance MIPMap, Distribution2D sampling and pdf)
+  nurbs_*                         tests/scenes/nurbs.pbrt: NURBS patches refined into meshes, path and
+                                  metadata mesh ids
+  shinymetal_*                    tests/scenes/shinymetal.pbrt: shinymetal (conductor microfacet and
+                                  mirror lobes), path and DirectLighting
   anisoward_*                     tests/scenes/anisoward.pbrt: the fork's anisotropic Ward material
                                   (anisoward.cpp, AnisoWardBrdf.cpp), path and DirectLighting
   cylinder_*                      tests/scenes/cylinder.pbrt: cylinders (phimax, inside / outside hits,
@@ -80,7 +84,7 @@ Fixtures (numpy .npz, inputs + expected outputs only):
                                   pixel holds all of its contributions (incl. exact-boundary samples
                                   of its neighbours, spectralImage.cpp:77-152); C2 at the sphere
                                   light's edge and at a killeroo silhouette, C3-C5 at an edge each
-Usage: python tools/make_golden.py [--only keys|dat|merl|dl|meta|spec|rgb|rgbfeat|lights|ortho|heightfield|cylinder|anisoward|b30|window|imagemap|animcam|gpupath|textured|envmap]
+Usage: python tools/make_golden.py [--only keys|dat|merl|dl|meta|spec|rgb|rgbfeat|lights|ortho|heightfield|cylinder|anisoward|shinymetal|nurbs|b30|window|imagemap|animcam|gpupath|textured|envmap]
        (after `make -C oracle ref`, `ref60`, `ref30` and `refrgb`)
 """
 import os
@@ -416,6 +420,28 @@ def anisoward_fixtures(tmp):
     film_fixture("anisoward_dl_film_48x36s4", (48, 36), 4, 0, 5, tmp, scene=sc, extra=ex)
 
 
+def shinymetal_fixtures(tmp):
+    """tests/scenes/shinymetal.pbrt: shinymetal's conductor microfacet and mirror lobes (FresnelApproxEta
+    of constant Ks / Kr); path and DirectLighting (its specular recursion)"""
+    sc = os.path.join(ROOT, "tests", "scenes", "shinymetal.pbrt")
+    paths_fixture("shinymetal_paths_64x48s4", (64, 48), 4, 0, 5, 1, tmp, scene=sc)
+    film_fixture("shinymetal_film_64x48s4", (64, 48), 4, 0, 5, tmp, scene=sc)
+    ex = ("--surf", "directlighting", "--dl-strategy", "all")
+    paths_fixture("shinymetal_dl_paths_48x36s4", (48, 36), 4, 0, 5, 1, tmp, scene=sc, extra=ex)
+    film_fixture("shinymetal_dl_film_48x36s4", (48, 36), 4, 0, 5, tmp, scene=sc, extra=ex)
+
+
+def nurbs_fixtures(tmp):
+    """tests/scenes/nurbs.pbrt: NURBS patches (P and rational Pw, interior knots, a u range) refined as
+    the reference refines them; path integrator and metadata mesh ids"""
+    sc = os.path.join(ROOT, "tests", "scenes", "nurbs.pbrt")
+    paths_fixture("nurbs_paths_64x48s4", (64, 48), 4, 0, 5, 1, tmp, scene=sc)
+    film_fixture("nurbs_film_64x48s4", (64, 48), 4, 0, 5, tmp, scene=sc)
+    ex = ("--surf", "metadata", "--meta-strategy", "mesh")
+    paths_fixture("nurbs_meta_mesh_paths_48x36s2", (48, 36), 2, 0, 5, 1, tmp, scene=sc, extra=ex)
+    film_fixture("nurbs_meta_mesh_film_48x36s2", (48, 36), 2, 0, 5, tmp, scene=sc, extra=ex)
+
+
 def envmap_fixtures(tmp):
     """tests/scenes/envmap.pbrt: an image-based InfiniteAreaLight (a decoded PFM lat-long map: its
     radiance MIPMap and Distribution2D), path integrator and DirectLighting"""
@@ -473,6 +499,10 @@ def main():
                 spec_fixtures(tmp)
             elif only == "rgb":
                 rgb_fixtures(tmp)
+            elif only == "nurbs":
+                nurbs_fixtures(tmp)
+            elif only == "shinymetal":
+                shinymetal_fixtures(tmp)
             elif only == "anisoward":
                 anisoward_fixtures(tmp)
             elif only == "cylinder":
