@@ -123,10 +123,17 @@ def main():
         tr = {"configs": {}}
     ent = {"source": "%s: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (separate) of bench.py --config %s --steps 1 "
                      "--warmup 0 --serial; FETCH_SIZE x2 (gfx950 correction, MI355X_MICROARCH.md) + WRITE_SIZE" % (tag, cfg)}
+    # per launch of the family's first kernel: bench.py times a DirectLighting shade step (k_shade,
+    # k_dl_nee, k_dl_spec, k_regen) as one k_shade launch, so its bytes are the step's
+    lead = {}
+    for (k, c), v in pm.items():
+        t = timing_name(k)
+        if t and c == "FETCH_SIZE" and k.startswith(NAMES[t][0]):
+            lead[t] = lead.get(t, 0) + len(v)
     for t, cs in per.items():
         if "FETCH_SIZE" in cs and "WRITE_SIZE" in cs:
-            fb, n = cs["FETCH_SIZE"][0] * 1024.0, cs["FETCH_SIZE"][1]
-            wb, nw = cs["WRITE_SIZE"][0] * 1024.0, cs["WRITE_SIZE"][1]
+            fb, n = cs["FETCH_SIZE"][0] * 1024.0, lead.get(t) or cs["FETCH_SIZE"][1]
+            wb, nw = cs["WRITE_SIZE"][0] * 1024.0, lead.get(t) or cs["WRITE_SIZE"][1]
             ent[t] = {"launches": n, "fetch_bytes_raw_per_launch": fb / n, "write_bytes_per_launch": wb / nw,
                       "hbm_bytes_per_launch": 2.0 * fb / n + wb / nw}
     tr["configs"][cfg] = ent
