@@ -35,6 +35,7 @@ using namespace pgd;
 // weak: an experiment build may compile only some shade variants with PGD_SECTIONS
 extern "C" {
 __attribute__((weak)) int pgd_sections_read_32_0(unsigned long long *, int);
+__attribute__((weak)) int pgd_sections_read_32_1(unsigned long long *, int);
 __attribute__((weak)) int pgd_sections_read_32_7(unsigned long long *, int);
 __attribute__((weak)) int pgd_sections_read_60_0(unsigned long long *, int);
 __attribute__((weak)) int pgd_sections_read_60_7(unsigned long long *, int);
@@ -44,7 +45,7 @@ __attribute__((weak)) int pgd_sections_read_30_7(unsigned long long *, int);
 static int pgd_sections_read(unsigned long long *out, int reset) {
     for (int k = 0; k < SEC_N; ++k) out[k] = 0;
     int e = 0;
-    for (auto f : {pgd_sections_read_32_0, pgd_sections_read_32_7, pgd_sections_read_60_0, pgd_sections_read_60_7,
+    for (auto f : {pgd_sections_read_32_0, pgd_sections_read_32_1, pgd_sections_read_32_7, pgd_sections_read_60_0, pgd_sections_read_60_7,
                    pgd_sections_read_30_0, pgd_sections_read_30_7})
         if (f) e |= f(out, reset);
     return e;
@@ -1487,6 +1488,22 @@ static int ensure_slots(Lane *c, int cap, int NB, int nInst, int nFrames, int ba
 // their queue sizes on the device, and passes after the queues have drained are empty
 // launches.  The shadow queries run on the lane's second stream beside the closest-hit
 // queries (their tails overlap); shade waits for both.
+// The path integrator's shading variant for a scene's features: FEAT 0, FEAT_ALL, and for 32
+// bands a measured-BRDF-only build (C3: FEAT_MEAS without the texture / environment-light code,
+// 4 spilled VGPRs instead of 37 in k_shade)
+template <int NB>
+static auto path_shade_variant(int feat) -> decltype(&launch_shade<NB, 0>) {
+    if constexpr (NB == 32)
+        if (feat == FEAT_MEAS) return launch_shade<32, FEAT_MEAS>;
+    return feat ? launch_shade<NB, FEAT_ALL> : launch_shade<NB, 0>;
+}
+template <int NB>
+static auto path_tail_variant(int feat) -> decltype(&launch_tail<NB, 0>) {
+    if constexpr (NB == 32)
+        if (feat == FEAT_MEAS) return launch_tail<32, FEAT_MEAS>;
+    return feat ? launch_tail<NB, FEAT_ALL> : launch_tail<NB, 0>;
+}
+
 template <int NB>
 static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool countWork, Timing &T,
                          unsigned int *zeroedOut) {
@@ -1535,7 +1552,7 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
     auto kShade = dl ? (c->feat ? launch_shade_dl<NB, FEAT_ALL> : launch_shade_dl<NB, 0>)
                   : c->S.integrator == PBRTGPU_INTEGRATOR_METADATA
                       ? (c->feat ? launch_shade_meta<NB, FEAT_ALL> : launch_shade_meta<NB, 0>)
-                  : c->feat ? launch_shade<NB, FEAT_ALL> : launch_shade<NB, 0>;
+                  : path_shade_variant<NB>(c->feat);
     const int nFrames = dl ? std::max(1, c->S.maxDepth) : 0;
     // the path integrator's k_shade lists the slots about to make their first MT draws (k_mt_init)
     const bool mtList = c->S.integrator != PBRTGPU_INTEGRATOR_DIRECT && c->S.integrator != PBRTGPU_INTEGRATOR_METADATA;
@@ -1564,7 +1581,7 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
     // not in work-counting runs (it counts no traversal work)
     const uint32_t tailMax = (!dl && c->S.integrator == PBRTGPU_INTEGRATOR_PATH && !inst && c->S.w4N > 0 && !countWork)
                                  ? tail_rays() : 0u;
-    auto kTail = c->feat ? launch_tail<NB, FEAT_ALL> : launch_tail<NB, 0>;
+    auto kTail = path_tail_variant<NB>(c->feat);
     Run R[kLanes];
     const bool serial = serial_mode();
     const int nl = (src.nItems >= 8192u && !serial) ? kLanes : 1;

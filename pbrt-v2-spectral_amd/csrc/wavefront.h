@@ -346,10 +346,27 @@ PGD_INLINE void term4(const float *sp, const FTerm &t, int q, const float4 *mb, 
         r = ld4(sp, t.R + 4 * q);
         r2 = (t.kind == T_FB || t.kind == T_BLINNC) ? ld4(sp, t.R2 + 4 * q) : r;
     }
-    v.x += term_val(t, r.x, r2.x);
-    v.y += term_val(t, r.y, r2.y);
-    v.z += term_val(t, r.z, r2.z);
-    v.w += term_val(t, r.w, r2.w);
+    // the kind is chosen once for the quad: a switch per band (term_val) had compiled to a branch
+    // tree per band -- ~20 exec-mask instructions per band and term in every band loop
+    float4 f;
+    switch (t.kind) {
+        case T_LAMB: f = make_float4(r.x * kInvPi, r.y * kInvPi, r.z * kInvPi, r.w * kInvPi); break;
+        case T_OREN:
+            f = make_float4((r.x * kInvPi) * t.s0, (r.y * kInvPi) * t.s0, (r.z * kInvPi) * t.s0, (r.w * kInvPi) * t.s0);
+            break;
+        case T_BLINN:
+            f = make_float4((((r.x * t.s0) * t.s1) * t.s2) / t.s3, (((r.y * t.s0) * t.s1) * t.s2) / t.s3,
+                            (((r.z * t.s0) * t.s1) * t.s2) / t.s3, (((r.w * t.s0) * t.s1) * t.s2) / t.s3);
+            break;
+        default:
+            f = make_float4(term_val(t, r.x, r2.x), term_val(t, r.y, r2.y), term_val(t, r.z, r2.z),
+                            term_val(t, r.w, r2.w));
+            break;
+    }
+    v.x += f.x;
+    v.y += f.y;
+    v.z += f.z;
+    v.w += f.w;
 }
 // BSDF value of four bands (quad q): mb = measured scratch, kb = texture scratch of the slot
 template <int FEAT>
@@ -441,10 +458,15 @@ PGD_INLINE int kd_next(const float4 &a, const float4 &b, int cur, int prev, bool
 // strictly inside, or at k = 11 (maxDist2 = 2.048 > 1.5).  That k is the first with
 // d3 < .001f * 2^k, d3 the third-smallest sample distance^2 (C3's points needed ~3-4 walks of
 // growing radius each in the reference).
+// Closed form of  m = .001f; for (k = 0; k < 11 && !(d3 < m); ++k) m *= 2.f;  -- the doublings
+// are exact, so m = .001f * 2^k at the first k with d3 < m, found from d3's exponent and whether
+// its mantissa is below .001f's (1.024); checked against the loop over every non-negative float
+// (tests/test_hostsan.py).  No loop: its trip count diverged across a wave.
 PGD_INLINE float kd_radius_of(float d3) {
-    float m = .001f;
-    for (int k = 0; k < 11 && !(d3 < m); ++k) m *= 2.f;
-    return m;
+    const uint32_t b = __float_as_uint(d3);
+    int k = (int)(b >> 23) - 116 - ((b & 0x7fffffu) < 0x03126fu ? 1 : 0);
+    k = min(max(k, 0), 11);
+    return __uint_as_float(0x3a83126fu + ((uint32_t)k << 23));
 }
 // One walk finds d3 and the samples the reference's final walk accumulates, in its order:
 //   * A node's own sample is compared on arrival (pre-order): d1 <= d2 <= d3 keep the three

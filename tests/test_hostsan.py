@@ -149,6 +149,14 @@ def test_replay_config_golden_keys(pg, tmp_path, name, pack):
     assert np.all(L.view(np.int32) == g["L"].view(np.int32), axis=1).mean() >= exact_rate(name)
 
 
+def test_kd_radius_closed_form():
+    """wavefront.h kd_radius_of (no loop) equals the reference retry loop's final radius
+    (IrregIsotropicBRDF::f, measured.cpp) over every non-negative float"""
+    exe = _build("shade_host")
+    r = subprocess.run([exe, "--kd-radius-check"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "mismatches 0" in r.stdout, r.stdout + r.stderr
+
+
 def test_device_rng_matches_oracle(pg, tmp_path):
     """device.h's MT19937 (5-word window, then the full state rebuilt at output 227 and twisted
     every 624) against the oracle's, over 4 generations."""

@@ -293,6 +293,19 @@ int main(int argc, char **argv) {
                         "--out FILE\n", argv[0]);
         return 2;
     }
+    if (!strcmp(argv[1], "--kd-radius-check")) {   // kd_radius_of (the device source) against the
+        // reference retry loop's radius (measured.cpp, IrregIsotropicBRDF::f) over every non-negative float
+        uint64_t bad = 0;
+        for (uint64_t i = 0; i < 0x80000000ull; ++i) {
+            const float d3 = __uint_as_float((uint32_t)i);
+            float m = .001f;
+            for (int k = 0; k < 11 && !(d3 < m); ++k) m *= 2.f;
+            const float r = kd_radius_of(d3);
+            if (__float_as_uint(r) != __float_as_uint(m)) ++bad;
+        }
+        printf("mismatches %llu\n", (unsigned long long)bad);
+        return bad ? 1 : 0;
+    }
     pbrthost_overrides ov = {PBRTHOST_ABI_VERSION, -1, -1, -1, -1, 0, PBRTHOST_KEEP_SEED, -1, -1, -1, -1, -1, -1};
     int nSlots = 256, mtKat = 0;
     const char *out = nullptr, *keyFile = nullptr, *strategy = nullptr;
