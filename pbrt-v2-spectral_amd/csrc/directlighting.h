@@ -88,7 +88,10 @@ struct DLVertex {
     V p, n, wo, dpdx, dpdy, dn[2];
     float diff[4];
 };
-template <int NB, int FEAT>
+// DIFF: the ray differentials at the vertex (the specular branches' child rays need them); the
+// light samples read them only through textured BSDF parameters (FEAT_TEX), so k_dl_nee's FEAT 0
+// build skips the camera re-derivation and the differential solve
+template <int NB, int FEAT, bool DIFF = true>
 PGD_INLINE void dl_vertex(const DevScene &S, const PathSoA &P, int slot, int d, DLVertex &v, int col) {
     const size_t c = P.cap;
     const float *fr = P.fRay + (size_t)d * 9 * c + slot;
@@ -98,6 +101,12 @@ PGD_INLINE void dl_vertex(const DevScene &S, const PathSoA &P, int slot, int d, 
     const int prim = P.fHit[(size_t)2 * d * c + slot];
     const float t = __int_as_float(P.fHit[(size_t)(2 * d + 1) * c + slot]);
     isect_fill(S, v.ray, prim, t, v.is, inst_rec(P, slot));
+    if (!DIFF) {
+        v.diff[0] = v.diff[1] = v.diff[2] = v.diff[3] = 0.f;
+        get_bsdf<FEAT>(S, v.is, v.diff, P.K + col, c, v.bs, &v.p, &v.n, v.dn);
+        v.wo = vneg(v.ray.d);
+        return;
+    }
     if (d == 0 && S.camType != PBRTGPU_CAMERA_REALISTIC) {
         // the perspective camera's differentials are re-derived from its sample; the lens camera's
         // were stored in frame 0 by path_start (their lens trace stays out of these kernels)
@@ -196,7 +205,7 @@ PGD_INLINE void dl_light_batches(const DevScene &S, const PathSoA &P, int slot, 
     {   // the vertex (its record is filled through out-of-line calls, so it lives in scratch
         // memory); the light samples read register copies of the fields they use
         DLVertex vx;
-        dl_vertex<NB, FEAT>(S, P, slot, d, vx, row);
+        dl_vertex<NB, FEAT, (FEAT & FEAT_TEX) != 0>(S, P, slot, d, vx, row);
         bs = vx.bs; vp = vx.p; vn = vx.n; vwo = vx.wo; vEps = vx.is.rayEps; vTime = vx.ray.time;
     }
     for (;;) {

@@ -38,6 +38,7 @@ __attribute__((weak)) int pgd_sections_read_32_0(unsigned long long *, int);
 __attribute__((weak)) int pgd_sections_read_32_1(unsigned long long *, int);
 __attribute__((weak)) int pgd_sections_read_32_7(unsigned long long *, int);
 __attribute__((weak)) int pgd_sections_read_60_0(unsigned long long *, int);
+__attribute__((weak)) int pgd_sections_read_60_6(unsigned long long *, int);
 __attribute__((weak)) int pgd_sections_read_60_7(unsigned long long *, int);
 __attribute__((weak)) int pgd_sections_read_30_0(unsigned long long *, int);
 __attribute__((weak)) int pgd_sections_read_30_7(unsigned long long *, int);
@@ -45,7 +46,7 @@ __attribute__((weak)) int pgd_sections_read_30_7(unsigned long long *, int);
 static int pgd_sections_read(unsigned long long *out, int reset) {
     for (int k = 0; k < SEC_N; ++k) out[k] = 0;
     int e = 0;
-    for (auto f : {pgd_sections_read_32_0, pgd_sections_read_32_1, pgd_sections_read_32_7, pgd_sections_read_60_0, pgd_sections_read_60_7,
+    for (auto f : {pgd_sections_read_32_0, pgd_sections_read_32_1, pgd_sections_read_32_7, pgd_sections_read_60_0, pgd_sections_read_60_6, pgd_sections_read_60_7,
                    pgd_sections_read_30_0, pgd_sections_read_30_7})
         if (f) e |= f(out, reset);
     return e;
@@ -1488,19 +1489,24 @@ static int ensure_slots(Lane *c, int cap, int NB, int nInst, int nFrames, int ba
 // their queue sizes on the device, and passes after the queues have drained are empty
 // launches.  The shadow queries run on the lane's second stream beside the closest-hit
 // queries (their tails overlap); shade waits for both.
-// The path integrator's shading variant for a scene's features: FEAT 0, FEAT_ALL, and for 32
-// bands a measured-BRDF-only build (C3: FEAT_MEAS without the texture / environment-light code,
-// 4 spilled VGPRs instead of 37 in k_shade)
+// The path integrator's shading variant for a scene's features: FEAT 0, FEAT_ALL, and two
+// partial builds -- 32 bands with measured BRDFs only (C3: FEAT_MEAS without the texture /
+// environment-light code, 4 spilled VGPRs instead of 37 in k_shade) and 60 bands with textures and
+// environment lights but no measured BRDFs (C4: FEAT_TEX | FEAT_INF, no kd-tree walk)
 template <int NB>
 static auto path_shade_variant(int feat) -> decltype(&launch_shade<NB, 0>) {
     if constexpr (NB == 32)
         if (feat == FEAT_MEAS) return launch_shade<32, FEAT_MEAS>;
+    if constexpr (NB == 60)
+        if (feat == (FEAT_TEX | FEAT_INF) && !getenv("PGD_NO60_6")) return launch_shade<60, FEAT_TEX | FEAT_INF>;
     return feat ? launch_shade<NB, FEAT_ALL> : launch_shade<NB, 0>;
 }
 template <int NB>
 static auto path_tail_variant(int feat) -> decltype(&launch_tail<NB, 0>) {
     if constexpr (NB == 32)
         if (feat == FEAT_MEAS) return launch_tail<32, FEAT_MEAS>;
+    if constexpr (NB == 60)
+        if (feat == (FEAT_TEX | FEAT_INF) && !getenv("PGD_NO60_6")) return launch_tail<60, FEAT_TEX | FEAT_INF>;
     return feat ? launch_tail<NB, FEAT_ALL> : launch_tail<NB, 0>;
 }
 
