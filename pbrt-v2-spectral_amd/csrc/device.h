@@ -881,6 +881,24 @@ PGD_INLINE void m4_inverse(const float *m, float *out) {
             }
     for (int i = 0; i < 16; ++i) out[i] = minv[i];
 }
+// m4_inverse of the scale factor S of an AnimatedTransform's decomposition.  Gauss-Jordan over
+// dynamic pivot indices compiles to select chains over all 16 entries per access; when S is
+// diagonal (every off-diagonal entry +0) with positive normal-range entries -- an animation
+// without scaling has S = I -- every pivot is a diagonal entry (the first candidate of each step
+// is one, an off-diagonal +0 never beats it, so no row is swapped), each row is scaled by its own
+// 1/d, and the eliminations subtract +0 products: the result is diag(1/d) with +0 elsewhere, the
+// general routine's bits (checked against it by the host replay, tests/test_hostsan.py)
+PGD_INLINE void m4_inverse_scale(const float *S, float *out) {
+    bool diag = true;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        if (i % 5 == 0) diag = diag && S[i] >= 0x1p-100f && S[i] <= 0x1p100f;
+        else diag = diag && __float_as_uint(S[i]) == 0u;
+    }
+    if (!diag) { m4_inverse(S, out); return; }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) out[i] = (i % 5 == 0) ? 1.f / S[i] : 0.f;
+}
 struct Quat { float x, y, z, w; };
 PGD_INLINE float qdot(Quat a, Quat b) { return (a.x * b.x + a.y * b.y + a.z * b.z) + a.w * b.w; }
 PGD_INLINE Quat qmk(float x, float y, float z, float w) { Quat q; q.x = x; q.y = y; q.z = z; q.w = w; return q; }
@@ -939,7 +957,7 @@ PGD_INLINE void inst_interp(const pbrtgpu_instance &I, float time, float *m, flo
     if (minv) {
         float Ti[16], Si[16], RiTi[16];
         m4_identity(Ti); Ti[3] = -tr[0]; Ti[7] = -tr[1]; Ti[11] = -tr[2];
-        m4_inverse(Sm, Si);
+        m4_inverse_scale(Sm, Si);
         m4_mul(M, Ti, RiTi);
         m4_mul(Si, RiTi, minv);
     }

@@ -157,6 +157,14 @@ def test_kd_radius_closed_form():
     assert r.returncode == 0 and "mismatches 0" in r.stdout, r.stdout + r.stderr
 
 
+def test_scale_inverse_fast_path():
+    """device.h m4_inverse_scale (a diagonal AnimatedTransform scale factor inverted directly)
+    gives the general Gauss-Jordan m4_inverse's bits (transform.cpp:68-130) on 2 M matrices"""
+    exe = _build("shade_host")
+    r = subprocess.run([exe, "--m4inv-check"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "mismatches 0 " in r.stdout, r.stdout + r.stderr
+
+
 def test_device_rng_matches_oracle(pg, tmp_path):
     """device.h's MT19937 (5-word window, then the full state rebuilt at output 227 and twisted
     every 624) against the oracle's, over 4 generations."""

@@ -293,6 +293,35 @@ int main(int argc, char **argv) {
                         "--out FILE\n", argv[0]);
         return 2;
     }
+    if (!strcmp(argv[1], "--m4inv-check")) {   // m4_inverse_scale (its diagonal fast path) against
+        // the general Gauss-Jordan m4_inverse (transform.cpp:68-130): random diagonal scale factors,
+        // identities, ties, and general / degenerate matrices (those take the general routine)
+        uint64_t bad = 0, fast = 0;
+        uint32_t x = 12345u;
+        auto rnd = [&]() { x ^= x << 13; x ^= x >> 17; x ^= x << 5; return x; };
+        auto chk = [&](const float *m) {
+            float a[16], b[16];
+            m4_inverse(m, a);
+            m4_inverse_scale(m, b);
+            bool d = true;
+            for (int i = 0; i < 16; ++i) d = d && (i % 5 == 0 ? (m[i] >= 0x1p-100f && m[i] <= 0x1p100f) : __float_as_uint(m[i]) == 0u);
+            fast += d;
+            if (memcmp(a, b, sizeof(a))) ++bad;
+        };
+        const float pool[] = {1.f, 2.f, .5f, 3.f, 1e-3f, 7.25f, 1e30f, 0x1p-100f, 0x1p100f, 1.0000001f, 0.9999999f};
+        for (int it = 0; it < 2000000; ++it) {
+            float m[16];
+            for (int i = 0; i < 16; ++i) m[i] = 0.f;
+            for (int i = 0; i < 4; ++i)
+                m[5 * i] = (rnd() & 3) ? __uint_as_float(0x3c000000u + rnd() % 0x0a000000u) : pool[rnd() % 11];
+            if ((it & 7) == 0) m[5 * (rnd() & 3)] = m[5 * (rnd() & 3)];   // ties
+            if ((it & 15) == 1) m[rnd() & 15] = -m[rnd() & 15];           // negative / -0 entries
+            if ((it & 31) == 2) m[1 + 5 * (rnd() % 3)] = __uint_as_float(rnd() & 0x3fffffffu);   // off-diagonal
+            chk(m);
+        }
+        printf("mismatches %llu fast %llu\n", (unsigned long long)bad, (unsigned long long)fast);
+        return bad || fast < 1000000 ? 1 : 0;
+    }
     if (!strcmp(argv[1], "--kd-radius-check")) {   // kd_radius_of (the device source) against the
         // reference retry loop's radius (measured.cpp, IrregIsotropicBRDF::f) over every non-negative float
         uint64_t bad = 0;
