@@ -8,7 +8,7 @@ cd $R/pbrt-v2-spectral_amd
 T=lib/exp/$NAME.obj; mkdir -p $T
 H="/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -DPGD_EXPERIMENT_BUILD -I../include -Ihost -Icsrc"
 pids=()
-for v in 32_0 32_7 60_0 60_7 30_0 30_7 3_0 3_7; do
+for v in 32_0 32_1 32_7 60_0 60_6 60_7 30_0 30_7 3_0 3_7; do
   $H "$@" -DSHADE_NB=${v%_*} -DSHADE_FEAT=${v#*_} -c csrc/shade.hip -o $T/s$v.o & pids+=($!)
   $H "$@" -DSHADE_NB=${v%_*} -DSHADE_FEAT=${v#*_} -DSHADE_DL=1 -c csrc/shade.hip -o $T/d$v.o & pids+=($!)
 done

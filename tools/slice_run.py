@@ -38,10 +38,13 @@ def main():
     for r in range(a.reps + 1):   # call 0 sizes the slot pools
         t = time.perf_counter()
         st = dev.render(tiles=tiles, tile=tile)
+        t1 = time.perf_counter()
         dev.gather(film, tiles=tiles, tile=tile)
         dt = time.perf_counter() - t
+        gms = (time.perf_counter() - t1) * 1e3
         tm = dev.timing()
         print(json.dumps({"config": a.config, "slice": a.slice, "call": r, "ms": round(dt * 1e3, 2),
+                          "render_ms": round(dt * 1e3 - gms, 2), "gather_ms": round(gms, 2),
                           "paths": int(st[pg.STAT_PATHS]), "passes": tm["passes"],
                           "Mpaths_s": round(st[pg.STAT_PATHS] / dt / 1e6, 2),
                           "kernel_ms": {k: round(tm[k]["ms"], 2) for k in pg.Timing.KERNELS},
