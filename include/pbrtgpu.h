@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define PBRTGPU_ABI_VERSION 15
+#define PBRTGPU_ABI_VERSION 16
 #define PBRTGPU_MAX_BANDS 64
 
 #define PBRTGPU_E_INVALID   (-1)
@@ -123,9 +123,13 @@ typedef struct pbrtgpu_texture {
     int32_t width, height; /* IMAGE: level-0 resolution (powers of two) */
     int32_t levels;        /* IMAGE: nLevels = 1 + Log2Int(max(width, height)) */
     float value;           /* CONST float */
-    float su, sv, du, dv;  /* UVMapping2D */
+    float su, sv, du, dv;  /* UVMapping2D; PlanarMapping2D: du, dv are its ds, dt */
     float max_aniso;
+    int32_t mapping;       /* IMAGE: PBRTGPU_MAP_* (the "mapping" parameter, imagemap.cpp:104-125) */
+    float map[16];         /* SPHERICAL / CYLINDRICAL: WorldToTexture.m = Inverse(tex2world), row-major;
+                              PLANAR: vs.xyz, vt.xyz (the "v1", "v2" parameters) */
 } pbrtgpu_texture;
+enum { PBRTGPU_MAP_UV = 0, PBRTGPU_MAP_SPHERICAL = 1, PBRTGPU_MAP_CYLINDRICAL = 2, PBRTGPU_MAP_PLANAR = 3 };
 
 /* Material parameters.  A spectrum slot is either the constant spec[i] or, when
  * tex[i] >= 0, a spectrum texture evaluated per hit (at most two textured slots per material,

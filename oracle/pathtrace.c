@@ -1391,12 +1391,56 @@ static void mip_lookup(const Ctx *c, const pbrtgpu_texture *tx, int nc, float s,
     mip_ewa(c, tx, nc, ilod + 1, s, t, ds0, dt0, ds1, dt1, e1);
     for (int k = 0; k < nc; ++k) out[k] = (1.f - d) * e0[k] + d * e1[k];
 }
-/* texture-space position and screen-space derivatives of the hit (dgs.u, v, dudx, ...) */
-typedef struct { float u, v, dudx, dvdx, dudy, dvdy; } TexPt;
-/* ImageTexture::Evaluate with UVMapping2D::Map (texture.cpp:80-90) */
+/* texture-space position and screen-space derivatives of the hit (dgs.u, v, dudx, ...), and its
+ * world-space point with the ray-differential offsets dpdx, dpdy (the non-uv mappings) */
+typedef struct { float u, v, dudx, dvdx, dudy, dvdy; V p, dpdx, dpdy; } TexPt;
+/* SphericalMapping2D::sphere (texture.cpp:104-110), CylindricalMapping2D::cylinder (texture.h);
+ * M_PI is a float in pbrt (pbrt.h:176-179) */
+static void map_dir(const pbrtgpu_texture *tx, V p, float *s, float *t) {
+    V vec = vnorm(xpoint(tx->map, p));
+    if (tx->mapping == PBRTGPU_MAP_SPHERICAL) {
+        float theta = ACOSF(clampf(vec.z, -1.f, 1.f));
+        float pp = ATAN2F(vec.y, vec.x);
+        float phi = (pp < 0.f) ? pp + 2.f * PI_F : pp;
+        *s = theta * INV_PI_F;
+        *t = phi * INV_TWOPI_F;
+    } else {
+        *s = (PI_F + ATAN2F(vec.y, vec.x)) / (2.f * PI_F);
+        *t = vec.z;
+    }
+}
+/* TextureMapping2D::Map: UVMapping2D (texture.cpp:80-90), SphericalMapping2D (:93-110, delta
+ * .1f), CylindricalMapping2D (:113-131, delta .01f), PlanarMapping2D (:134-144) */
+static void tex_map(const pbrtgpu_texture *tx, const TexPt *q, float *s, float *t, float *dsdx, float *dtdx,
+                    float *dsdy, float *dtdy) {
+    if (tx->mapping == PBRTGPU_MAP_UV) {
+        *s = tx->su * q->u + tx->du; *t = tx->sv * q->v + tx->dv;
+        *dsdx = tx->su * q->dudx; *dtdx = tx->sv * q->dvdx; *dsdy = tx->su * q->dudy; *dtdy = tx->sv * q->dvdy;
+    } else if (tx->mapping == PBRTGPU_MAP_PLANAR) {
+        V vs = v3(tx->map[0], tx->map[1], tx->map[2]), vt = v3(tx->map[3], tx->map[4], tx->map[5]);
+        V vec = vsub(q->p, v3(0.f, 0.f, 0.f));
+        *s = tx->du + vdot(vec, vs); *t = tx->dv + vdot(vec, vt);
+        *dsdx = vdot(q->dpdx, vs); *dtdx = vdot(q->dpdx, vt); *dsdy = vdot(q->dpdy, vs); *dtdy = vdot(q->dpdy, vt);
+    } else {
+        const float delta = tx->mapping == PBRTGPU_MAP_SPHERICAL ? .1f : .01f;
+        float sx, tx_, sy, ty;
+        map_dir(tx, q->p, s, t);
+        map_dir(tx, vadd(q->p, vmul(q->dpdx, delta)), &sx, &tx_);
+        *dsdx = (sx - *s) / delta;
+        *dtdx = (tx_ - *t) / delta;
+        if (*dtdx > .5) *dtdx = 1.f - *dtdx;
+        else if (*dtdx < -.5f) *dtdx = -(*dtdx + 1);
+        map_dir(tx, vadd(q->p, vmul(q->dpdy, delta)), &sy, &ty);
+        *dsdy = (sy - *s) / delta;
+        *dtdy = (ty - *t) / delta;
+        if (*dtdy > .5) *dtdy = 1.f - *dtdy;
+        else if (*dtdy < -.5f) *dtdy = -(*dtdy + 1);
+    }
+}
+/* ImageTexture::Evaluate (imagemap.cpp:84-101) */
 static void tex_image(const Ctx *c, const pbrtgpu_texture *tx, int nc, const TexPt *q, float *out) {
-    float s = tx->su * q->u + tx->du, t = tx->sv * q->v + tx->dv;
-    float dsdx = tx->su * q->dudx, dtdx = tx->sv * q->dvdx, dsdy = tx->su * q->dudy, dtdy = tx->sv * q->dvdy;
+    float s, t, dsdx, dtdx, dsdy, dtdy;
+    tex_map(tx, q, &s, &t, &dsdx, &dtdx, &dsdy, &dtdy);
     mip_lookup(c, tx, nc, s, t, dsdx, dtdx, dsdy, dtdy, out);
 }
 static float tex_float(const Ctx *c, int id, const TexPt *q) {
@@ -1449,8 +1493,9 @@ static void compute_differentials2(const DG *dg, const RayDiff *rd, float out[4]
     if (!solve2x2(A, Bx, &out[0], &out[1])) out[0] = out[1] = 0.f;
     if (!solve2x2(A, By, &out[2], &out[3])) out[2] = out[3] = 0.f;
 }
-static void compute_differentials(const DG *dg, const RayDiff *rd, float out[4]) {
-    out[0] = out[1] = out[2] = out[3] = 0.f;
+/* out = dudx, dvdx, dudy, dvdy, dpdx.xyz, dpdy.xyz (zero where the reference leaves them zero) */
+static void compute_differentials(const DG *dg, const RayDiff *rd, float out[10]) {
+    for (int i = 0; i < 10; ++i) out[i] = 0.f;
     if (!rd || !rd->has) return;
     float d = -vdot(dg->nn, dg->p);
     float tx = -(vdot(dg->nn, rd->rxo) + d) / vdot(dg->nn, rd->rxd);
@@ -1459,6 +1504,8 @@ static void compute_differentials(const DG *dg, const RayDiff *rd, float out[4])
     float ty = -(vdot(dg->nn, rd->ryo) + d) / vdot(dg->nn, rd->ryd);
     if (isnan(ty)) return;
     V py = vadd(rd->ryo, vmul(rd->ryd, ty));
+    V dpx = vsub(px, dg->p), dpy = vsub(py, dg->p);
+    out[4] = dpx.x; out[5] = dpx.y; out[6] = dpx.z; out[7] = dpy.x; out[8] = dpy.y; out[9] = dpy.z;
     int a0, a1;
     if (fabsf(dg->nn.x) > fabsf(dg->nn.y) && fabsf(dg->nn.x) > fabsf(dg->nn.z)) { a0 = 1; a1 = 2; }
     else if (fabsf(dg->nn.y) > fabsf(dg->nn.z)) { a0 = 0; a1 = 2; }
@@ -1508,7 +1555,7 @@ static int normal_map(const Ctx *c, int id, const TexPt *q, V nn, V *nOut) {
 }
 
 /* Intersection::GetBSDF -> GetShadingGeometry -> Material::GetBSDF (with Bump or NormalMap) */
-static void get_bsdf(const Ctx *c, const Isect *is, const float diff[4], BSDF *bs, DG *dgsOut) {
+static void get_bsdf(const Ctx *c, const Isect *is, const float diff[10], BSDF *bs, DG *dgsOut) {
     const pbrtgpu_prim *pr = &c->s->prims[is->prim];
     const pbrtgpu_material *mt = &c->s->materials[pr->material];
     DG dgs;
@@ -1522,7 +1569,8 @@ static void get_bsdf(const Ctx *c, const Isect *is, const float diff[4], BSDF *b
         const pbrtgpu_quadric *q = &c->s->quadrics[pr->shape_index];
         ro = q->reverse_orientation; swaps = q->swaps_handedness;
     }
-    const TexPt q = {dgs.u, dgs.v, diff[0], diff[1], diff[2], diff[3]};
+    const TexPt q = {dgs.u, dgs.v, diff[0], diff[1], diff[2], diff[3], dgs.p, {diff[4], diff[5], diff[6]},
+                     {diff[7], diff[8], diff[9]}};
     DG b = dgs;
     V nmapN;
     const int nmap = mt->normal_tex >= 0 && normal_map(c, mt->normal_tex, &q, dgs.nn, &nmapN);
@@ -1539,11 +1587,11 @@ static void get_bsdf(const Ctx *c, const Isect *is, const float diff[4], BSDF *b
         /* Material::Bump with a displacement texture: u- and v-shifted evaluations */
         float du = .5f * (fabsf(q.dudx) + fabsf(q.dudy));
         if (du == 0.f) du = .01f;
-        TexPt qu = q; qu.u = dgs.u + du;
+        TexPt qu = q; qu.u = dgs.u + du; qu.p = vadd(dgs.p, vmul(dgs.dpdu, du));   /* dgEval.p (material.cpp:49) */
         float uDisplace = tex_float(c, mt->bump_tex, &qu);
         float dv = .5f * (fabsf(q.dvdx) + fabsf(q.dvdy));
         if (dv == 0.f) dv = .01f;
-        TexPt qv = q; qv.v = dgs.v + dv;
+        TexPt qv = q; qv.v = dgs.v + dv; qv.p = vadd(dgs.p, vmul(dgs.dpdv, dv));
         float vDisplace = tex_float(c, mt->bump_tex, &qv);
         float displace = tex_float(c, mt->bump_tex, &q);
         b.dpdu = vadd(vadd(dgs.dpdu, vmul(dgs.nn, (uDisplace - displace) / du)), vmul(dgs.dndu, displace));
@@ -2041,7 +2089,7 @@ static void radiance(const Ctx *c, Ray ray, const RayDiff *rd, PathSampler *ps, 
         }
         BSDF bs;
         DG dgs;
-        float diff[4];   /* only the camera ray carries differentials (path.cpp:107) */
+        float diff[10];   /* only the camera ray carries differentials (path.cpp:107) */
         compute_differentials(&is.dg, bounces == 0 ? rd : NULL, diff);
         get_bsdf(c, &is, diff, &bs, &dgs);
         V p = dgs.p, n = dgs.nn;
@@ -2156,9 +2204,10 @@ static void dl_radiance(const Ctx *c, Ray ray, const RayDiff *rd, int depth, Pat
         return;
     }
     isect_fill(c, &ray, &h, &is);
-    float diff[4];
+    float diff[10];
     V dpdx, dpdy;
     compute_differentials2(&is.dg, rd, diff, &dpdx, &dpdy);
+    diff[4] = dpdx.x; diff[5] = dpdx.y; diff[6] = dpdx.z; diff[7] = dpdy.x; diff[8] = dpdy.y; diff[9] = dpdy.z;
     BSDF bs;
     DG dgs;
     get_bsdf(c, &is, diff, &bs, &dgs);

@@ -2000,13 +2000,55 @@ PGD_INLINE void mip_lookup(const DevScene &S, const pbrtgpu_texture &tx, float s
 #pragma unroll
     for (int k = 0; k < NC; ++k) out[k] = (1.f - d) * e0[k] + d * e1[k];
 }
-// hit position in texture space with its screen-space derivatives
-struct TexPt { float u, v, dudx, dvdx, dudy, dvdy; };
-// ImageTexture::Evaluate + UVMapping2D::Map (texture.cpp:80-90)
+// hit position in texture space with its screen-space derivatives, and the world-space point with
+// its ray-differential offsets (dpdx, dpdy) for the non-uv mappings
+struct TexPt { float u, v, dudx, dvdx, dudy, dvdy; V p, dpdx, dpdy; };
+// SphericalMapping2D::sphere / CylindricalMapping2D::cylinder (texture.cpp:104-110, texture.h):
+// the direction of the point in texture space (pbrt.h:176-179 makes M_PI a float)
+PGD_INLINE void map_dir(const pbrtgpu_texture &tx, V p, float *s, float *t) {
+    const V vec = vnorm(xpoint(tx.map, p));
+    if (tx.mapping == PBRTGPU_MAP_SPHERICAL) {
+        const float theta = ACOSF(clampf(vec.z, -1.f, 1.f));
+        const float pp = ATAN2F(vec.y, vec.x);
+        const float phi = (pp < 0.f) ? pp + 2.f * kPi : pp;
+        *s = theta * kInvPi;
+        *t = phi * kInvTwoPi;
+    } else {
+        *s = (kPi + ATAN2F(vec.y, vec.x)) / (2.f * kPi);
+        *t = vec.z;
+    }
+}
+// TextureMapping2D::Map (texture.cpp:80-150): (s, t) and their screen-space derivatives
+PGD_INLINE void tex_map(const pbrtgpu_texture &tx, const TexPt &q, float *s, float *t, float *dsdx, float *dtdx,
+                        float *dsdy, float *dtdy) {
+    if (tx.mapping == PBRTGPU_MAP_UV) {   // UVMapping2D
+        *s = tx.su * q.u + tx.du; *t = tx.sv * q.v + tx.dv;
+        *dsdx = tx.su * q.dudx; *dtdx = tx.sv * q.dvdx; *dsdy = tx.su * q.dudy; *dtdy = tx.sv * q.dvdy;
+    } else if (tx.mapping == PBRTGPU_MAP_PLANAR) {   // PlanarMapping2D
+        const V vs = v3(tx.map[0], tx.map[1], tx.map[2]), vt = v3(tx.map[3], tx.map[4], tx.map[5]);
+        *s = tx.du + vdot(q.p, vs); *t = tx.dv + vdot(q.p, vt);
+        *dsdx = vdot(q.dpdx, vs); *dtdx = vdot(q.dpdx, vt); *dsdy = vdot(q.dpdy, vs); *dtdy = vdot(q.dpdy, vt);
+    } else {   // spherical (delta .1) / cylindrical (delta .01): forward differences
+        const float delta = tx.mapping == PBRTGPU_MAP_SPHERICAL ? .1f : .01f;
+        float sx, tx_, sy, ty;
+        map_dir(tx, q.p, s, t);
+        map_dir(tx, vadd(q.p, vmul(q.dpdx, delta)), &sx, &tx_);
+        *dsdx = (sx - *s) / delta;
+        *dtdx = (tx_ - *t) / delta;
+        if (*dtdx > .5f) *dtdx = 1.f - *dtdx;
+        else if (*dtdx < -.5f) *dtdx = -(*dtdx + 1.f);
+        map_dir(tx, vadd(q.p, vmul(q.dpdy, delta)), &sy, &ty);
+        *dsdy = (sy - *s) / delta;
+        *dtdy = (ty - *t) / delta;
+        if (*dtdy > .5f) *dtdy = 1.f - *dtdy;
+        else if (*dtdy < -.5f) *dtdy = -(*dtdy + 1.f);
+    }
+}
+// ImageTexture::Evaluate (imagemap.cpp:84-101): the mapping, then the MIPMap lookup
 template <int NC>
 PGD_INLINE void tex_image(const DevScene &S, const pbrtgpu_texture &tx, const TexPt &q, float *out) {
-    float s = tx.su * q.u + tx.du, t = tx.sv * q.v + tx.dv;
-    float dsdx = tx.su * q.dudx, dtdx = tx.sv * q.dvdx, dsdy = tx.su * q.dudy, dtdy = tx.sv * q.dvdy;
+    float s, t, dsdx, dtdx, dsdy, dtdy;
+    tex_map(tx, q, &s, &t, &dsdx, &dtdx, &dsdy, &dtdy);
     mip_lookup<NC>(S, tx, s, t, dsdx, dtdx, dsdy, dtdy, out);
 }
 PGD_INLINE float tex_leaf_float(const DevScene &S, int id, const TexPt &q) {
@@ -2133,7 +2175,7 @@ PGD_HEAVY void compute_differentials(const DG &dg, const RayDiff &rd, float out[
 // dnOut (optional): dndu, dndv of the shading geometry (SpecularReflect / SpecularTransmit ray
 // differentials, integrator.cpp:190-192)
 template <int FEAT>
-PGD_HEAVY void get_bsdf(const DevScene &S, const Isect &is, const float diff[4], float4 *kb, size_t c, BSDF &bs,
+PGD_HEAVY void get_bsdf(const DevScene &S, const Isect &is, const float diff[10], float4 *kb, size_t c, BSDF &bs,
                         V *pOut, V *nOut, V *dnOut = nullptr) {
     const pbrtgpu_prim pr = (*sa(S.prims, (uint32_t)(is.prim)));
     const pbrtgpu_material &mt = (*sa(S.mats, (uint32_t)(pr.material)));
@@ -2158,6 +2200,7 @@ PGD_HEAVY void get_bsdf(const DevScene &S, const Isect &is, const float diff[4],
     }
     TexPt tq;
     tq.u = dgs.u; tq.v = dgs.v; tq.dudx = diff[0]; tq.dvdx = diff[1]; tq.dudy = diff[2]; tq.dvdy = diff[3];
+    tq.p = dgs.p; tq.dpdx = v3(diff[4], diff[5], diff[6]); tq.dpdy = v3(diff[7], diff[8], diff[9]);
     V bdpdu, bdpdv;
     V nmapN;
     const bool nmap = (FEAT & FEAT_TEX) && mt.normal_tex >= 0 && normal_map(S, mt.normal_tex, tq, dgs.nn, &nmapN);
@@ -2172,11 +2215,11 @@ PGD_HEAVY void get_bsdf(const DevScene &S, const Isect &is, const float diff[4],
     } else {
         float du = .5f * (fabsf(tq.dudx) + fabsf(tq.dudy));
         if (du == 0.f) du = .01f;
-        TexPt qu = tq; qu.u = dgs.u + du;
+        TexPt qu = tq; qu.u = dgs.u + du; qu.p = vadd(dgs.p, vmul(dgs.dpdu, du));   // dgEval (material.cpp:49-51)
         float uDisplace = tex_float(S, mt.bump_tex, qu);
         float dv = .5f * (fabsf(tq.dvdx) + fabsf(tq.dvdy));
         if (dv == 0.f) dv = .01f;
-        TexPt qv = tq; qv.v = dgs.v + dv;
+        TexPt qv = tq; qv.v = dgs.v + dv; qv.p = vadd(dgs.p, vmul(dgs.dpdv, dv));
         float vDisplace = tex_float(S, mt.bump_tex, qv);
         float displace = tex_float(S, mt.bump_tex, tq);
         bdpdu = vadd(vadd(dgs.dpdu, vmul(dgs.nn, (uDisplace - displace) / du)), vmul(dgs.dndu, displace));

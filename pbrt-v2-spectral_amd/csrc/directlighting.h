@@ -86,7 +86,7 @@ struct DLVertex {
     Isect is;
     BSDF bs;
     V p, n, wo, dpdx, dpdy, dn[2];
-    float diff[4];
+    float diff[10];   // du/dv (x, y), dpdx, dpdy (get_bsdf's texture point)
 };
 // DIFF: the ray differentials at the vertex (the specular branches' child rays need them); the
 // light samples read them only through textured BSDF parameters (FEAT_TEX), so k_dl_nee's FEAT 0
@@ -102,7 +102,7 @@ PGD_INLINE void dl_vertex(const DevScene &S, const PathSoA &P, int slot, int d, 
     const float t = __int_as_float(P.fHit[(size_t)(2 * d + 1) * c + slot]);
     isect_fill(S, v.ray, prim, t, v.is, inst_rec(P, slot));
     if (!DIFF) {
-        v.diff[0] = v.diff[1] = v.diff[2] = v.diff[3] = 0.f;
+        for (int i = 0; i < 10; ++i) v.diff[i] = 0.f;
         get_bsdf<FEAT>(S, v.is, v.diff, P.K + col, c, v.bs, &v.p, &v.n, v.dn);
         v.wo = vneg(v.ray.d);
         return;
@@ -125,6 +125,8 @@ PGD_INLINE void dl_vertex(const DevScene &S, const PathSoA &P, int slot, int d, 
         v.rd.ryd = dl_vec_load(fd + 9 * c, c);
     }
     compute_differentials(v.is.dg, v.rd, v.diff, &v.dpdx, &v.dpdy);
+    v.diff[4] = v.dpdx.x; v.diff[5] = v.dpdx.y; v.diff[6] = v.dpdx.z;
+    v.diff[7] = v.dpdy.x; v.diff[8] = v.dpdy.y; v.diff[9] = v.dpdy.z;
     get_bsdf<FEAT>(S, v.is, v.diff, P.K + col, c, v.bs, &v.p, &v.n, v.dn);
     v.wo = vneg(v.ray.d);
 }

@@ -1017,7 +1017,7 @@ PGD_INLINE Pushes shade_vertex(const DevScene &S, const PathSoA &P, int slot, in
     const uint32_t hp = *sa(P.hp, us), s = *sa(P.smp, us), spp = (uint32_t)S.spp;
     // only the camera ray carries differentials (path.cpp:107 drops them); they matter only
     // to textured materials
-    float diff[4] = {0.f, 0.f, 0.f, 0.f};
+    float diff[10] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};   // du/dv (x, y), dpdx, dpdy
     if ((FEAT & FEAT_TEX) && vb == 0) {
         const pbrtgpu_material &mt = (*sa(S.mats, (uint32_t)((*sa(S.prims, (uint32_t)(is.prim))).material)));
         if (mt.bump_tex >= 0 || mt.normal_tex >= 0 || mt.tex[0] >= 0 || mt.tex[1] >= 0 || mt.tex[2] >= 0 || mt.tex[3] >= 0 ||
@@ -1029,7 +1029,9 @@ PGD_INLINE Pushes shade_vertex(const DevScene &S, const PathSoA &P, int slot, in
             const float timeU = s1d(hp, 2, s, spp);
             RayDiff rd = path_camera_diff(S, P.item[slot], hp, s, (int)(pxy & 0xffffu) + u[0], (int)(pxy >> 16) + u[1],
                                           lens[0], lens[1], timeU);
-            compute_differentials(is.dg, rd, diff);
+            V dpdx, dpdy;
+            compute_differentials(is.dg, rd, diff, &dpdx, &dpdy);
+            diff[4] = dpdx.x; diff[5] = dpdx.y; diff[6] = dpdx.z; diff[7] = dpdy.x; diff[8] = dpdy.y; diff[9] = dpdy.z;
         }
     }
     float4 *kb = P.K + slot;

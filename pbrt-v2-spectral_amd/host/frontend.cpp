@@ -63,6 +63,7 @@ struct ParamSet {
     std::string FindTexture(const std::string &n) const { const Param *p = Find(P_TEXTURE, n); return (p && p->s.size()) ? p->s[0] : ""; }
     Spec FindOneSpectrum(const std::string &n, const Spec &d) const { const Param *p = Find(P_SPECTRUM, n); return (p && p->spec.size()) ? p->spec[0] : d; }
     V3 FindOnePoint(const std::string &n, const V3 &d) const { const Param *p = Find(P_POINT, n); return (p && p->f.size() >= 3) ? V3(p->f[0], p->f[1], p->f[2]) : d; }
+    V3 FindOneVector(const std::string &n, const V3 &d) const { const Param *p = Find(P_VECTOR, n); return (p && p->f.size() >= 3) ? V3(p->f[0], p->f[1], p->f[2]) : d; }
 };
 
 // texture values known at scene-build time (constant textures; 1x1 fallback images)
@@ -1136,10 +1137,23 @@ private:
     // one-valued MIPMap(1, 1, powf(scale, gamma)) with the MIPMap defaults
     int MakeImageTexture(const ParamSet &p, bool spectral) {
         pbrtgpu_texture t = TexNode(PBRTGPU_TEX_IMAGE, spectral);
-        std::string mapping = GetString(p, p, "mapping", "uv");
-        if (mapping != "uv") throw std::runtime_error("texture mapping '" + mapping + "' is not supported yet");
-        t.su = GetFloat(p, p, "uscale", 1.f); t.sv = GetFloat(p, p, "vscale", 1.f);
-        t.du = GetFloat(p, p, "udelta", 0.f); t.dv = GetFloat(p, p, "vdelta", 0.f);
+        // the 2D mapping (imagemap.cpp:107-125): uv (its scales / offsets), spherical and cylindrical
+        // (WorldToTexture = Inverse(tex2world), the CTM at the Texture directive), planar (v1, v2 and
+        // the udelta / vdelta offsets); an unknown name is the reference's Error + default UVMapping2D
+        const std::string mapping = GetString(p, p, "mapping", "uv");
+        if (mapping == "uv") {
+            t.su = GetFloat(p, p, "uscale", 1.f); t.sv = GetFloat(p, p, "vscale", 1.f);
+            t.du = GetFloat(p, p, "udelta", 0.f); t.dv = GetFloat(p, p, "vdelta", 0.f);
+        } else if (mapping == "spherical" || mapping == "cylindrical") {
+            t.mapping = mapping == "spherical" ? PBRTGPU_MAP_SPHERICAL : PBRTGPU_MAP_CYLINDRICAL;
+            const Xform w2t = Inverse(curT.t[0]);
+            for (int i = 0; i < 16; ++i) t.map[i] = w2t.m.m[i / 4][i % 4];
+        } else if (mapping == "planar") {
+            t.mapping = PBRTGPU_MAP_PLANAR;
+            const V3 vs = p.FindOneVector("v1", V3(1, 0, 0)), vt = p.FindOneVector("v2", V3(0, 1, 0));
+            t.map[0] = vs.x; t.map[1] = vs.y; t.map[2] = vs.z; t.map[3] = vt.x; t.map[4] = vt.y; t.map[5] = vt.z;
+            t.du = GetFloat(p, p, "udelta", 0.f); t.dv = GetFloat(p, p, "vdelta", 0.f);
+        } else fprintf(stderr, "pbrthost: 2D texture mapping \"%s\" unknown (UVMapping2D)\n", mapping.c_str());
         float maxAniso = GetFloat(p, p, "maxanisotropy", 8.f);
         bool trilerp = p.FindOneBool("trilinear", false), noFilt = p.FindOneBool("noFiltering", false);
         std::string wrap = GetString(p, p, "wrap", "repeat");

@@ -100,7 +100,7 @@ class RenderDesc(ctypes.Structure):
 STAT_PATHS, STAT_KERNEL_MS, STAT_ACCUM_MS, STAT_ZEROED, STAT_SPILLS, STAT_PASSES = 0, 1, 2, 3, 4, 5
 F_ACCUMULATE, F_COUNT_WORK = 1, 2
 KEEP_SEED = 0xFFFFFFFF
-ABI_VERSION = 15
+ABI_VERSION = 16
 
 
 class Timing(ctypes.Structure):

@@ -60,6 +60,9 @@ Fixtures (numpy .npz, inputs + expected outputs only):
                                   lat-long map: radiance MIPMap, Distribution2D sampling and pdf)
   nurbs_*                         tests/scenes/nurbs.pbrt: NURBS patches refined into meshes, path and
                                   metadata mesh ids
+  mappings_*                      tests/scenes/mappings.pbrt: spherical, cylindrical and planar 2D
+                                  texture mappings (image textures and bump maps), path and
+                                  DirectLighting
   shinymetal_*                    tests/scenes/shinymetal.pbrt: shinymetal (conductor microfacet and
                                   mirror lobes), path and DirectLighting
   anisoward_*                     tests/scenes/anisoward.pbrt: the fork's anisotropic Ward material
@@ -84,7 +87,7 @@ Fixtures (numpy .npz, inputs + expected outputs only):
                                   pixel holds all of its contributions (incl. exact-boundary samples
                                   of its neighbours, spectralImage.cpp:77-152); C2 at the sphere
                                   light's edge and at a killeroo silhouette, C3-C5 at an edge each
-Usage: python tools/make_golden.py [--only keys|dat|merl|dl|meta|spec|rgb|rgbfeat|lights|ortho|heightfield|cylinder|anisoward|shinymetal|nurbs|b30|window|imagemap|animcam|gpupath|textured|envmap]
+Usage: python tools/make_golden.py [--only keys|dat|merl|dl|meta|spec|rgb|rgbfeat|mappings|lights|ortho|heightfield|cylinder|anisoward|shinymetal|nurbs|b30|window|imagemap|animcam|gpupath|textured|envmap]
        (after `make -C oracle ref`, `ref60`, `ref30` and `refrgb`)
 """
 import os
@@ -420,6 +423,17 @@ def anisoward_fixtures(tmp):
     film_fixture("anisoward_dl_film_48x36s4", (48, 36), 4, 0, 5, tmp, scene=sc, extra=ex)
 
 
+def mappings_fixtures(tmp):
+    """tests/scenes/mappings.pbrt: the spherical / cylindrical / planar 2D texture mappings
+    (texture.cpp:93-144) on image textures and bump maps; path and DirectLighting"""
+    sc = os.path.join(ROOT, "tests", "scenes", "mappings.pbrt")
+    paths_fixture("mappings_paths_64x48s4", (64, 48), 4, 0, 5, 1, tmp, scene=sc)
+    film_fixture("mappings_film_64x48s4", (64, 48), 4, 0, 5, tmp, scene=sc)
+    ex = ("--surf", "directlighting", "--dl-strategy", "all")
+    paths_fixture("mappings_dl_paths_48x36s4", (48, 36), 4, 0, 5, 1, tmp, scene=sc, extra=ex)
+    film_fixture("mappings_dl_film_48x36s4", (48, 36), 4, 0, 5, tmp, scene=sc, extra=ex)
+
+
 def shinymetal_fixtures(tmp):
     """tests/scenes/shinymetal.pbrt: shinymetal's conductor microfacet and mirror lobes (FresnelApproxEta
     of constant Ks / Kr); path and DirectLighting (its specular recursion)"""
@@ -501,6 +515,8 @@ def main():
                 rgb_fixtures(tmp)
             elif only == "nurbs":
                 nurbs_fixtures(tmp)
+            elif only == "mappings":
+                mappings_fixtures(tmp)
             elif only == "shinymetal":
                 shinymetal_fixtures(tmp)
             elif only == "anisoward":

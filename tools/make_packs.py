@@ -47,6 +47,8 @@ PACKS = [
     ("anisoward", os.path.join(ROOT, "tests", "scenes", "anisoward.pbrt"), 32, 64, 48, 4),
     # shinymetal
     ("shinymetal", os.path.join(ROOT, "tests", "scenes", "shinymetal.pbrt"), 32, 64, 48, 4),
+    # spherical / cylindrical / planar texture mappings
+    ("mappings", os.path.join(ROOT, "tests", "scenes", "mappings.pbrt"), 32, 64, 48, 4),
     # NURBS surfaces
     ("nurbs", os.path.join(ROOT, "tests", "scenes", "nurbs.pbrt"), 32, 64, 48, 4),
 ]
@@ -61,7 +63,7 @@ def main():
             continue
         # the configs render with "path" (SURVEY App. B); load a pack with integrator="directlighting"
         # to render it with the DirectLightingIntegrator the scene files name
-        s = pg.Scene.load(os.path.join(REF, fn), xres=xr, yres=yr, spp=spp, maxdepth=-1 if name.startswith(("coverage", "imagemap", "animcam", "textured", "envmap", "lights", "ortho", "heightfield", "cylinder", "anisoward", "shinymetal", "nurbs")) else 5,
+        s = pg.Scene.load(os.path.join(REF, fn), xres=xr, yres=yr, spp=spp, maxdepth=-1 if name.startswith(("coverage", "imagemap", "animcam", "textured", "envmap", "lights", "ortho", "heightfield", "cylinder", "anisoward", "shinymetal", "nurbs", "mappings")) else 5,
                           bands=bands, integrator="path")
         path = os.path.join(out, name + ".pack")
         s.save_pack(path)
