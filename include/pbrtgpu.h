@@ -109,7 +109,7 @@ enum {
  * 3 floats (RGB) per texel for spectrum textures, 1 for float textures).  Lookups follow
  * MIPMap::Lookup (EWA, mipmap.h:278-375, or width-based / noFiltering, :232-259) with the
  * ImageWrap mode, texture coordinates from UVMapping2D (texture.cpp:80-90). */
-enum { PBRTGPU_TEX_CONST = 0, PBRTGPU_TEX_IMAGE = 1, PBRTGPU_TEX_SCALE = 2 };
+enum { PBRTGPU_TEX_CONST = 0, PBRTGPU_TEX_IMAGE = 1, PBRTGPU_TEX_SCALE = 2, PBRTGPU_TEX_CHECKER = 3 };
 enum { PBRTGPU_WRAP_REPEAT = 0, PBRTGPU_WRAP_BLACK = 1, PBRTGPU_WRAP_CLAMP = 2 };
 typedef struct pbrtgpu_texture {
     int32_t type;          /* PBRTGPU_TEX_* */
@@ -128,7 +128,10 @@ typedef struct pbrtgpu_texture {
     int32_t mapping;       /* IMAGE: PBRTGPU_MAP_* (the "mapping" parameter, imagemap.cpp:104-125) */
     float map[16];         /* SPHERICAL / CYLINDRICAL: WorldToTexture.m = Inverse(tex2world), row-major;
                               PLANAR: vs.xyz, vt.xyz (the "v1", "v2" parameters) */
+    int32_t aamode;        /* CHECKER (Checkerboard2DTexture over tex1, tex2: CONST / IMAGE leaves, the
+                              mapping above): 0 closedform box filter, 1 none (point sampled) */
 } pbrtgpu_texture;
+/* IMAGE and CHECKER nodes */
 enum { PBRTGPU_MAP_UV = 0, PBRTGPU_MAP_SPHERICAL = 1, PBRTGPU_MAP_CYLINDRICAL = 2, PBRTGPU_MAP_PLANAR = 3 };
 
 /* Material parameters.  A spectrum slot is either the constant spec[i] or, when

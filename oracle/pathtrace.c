@@ -1443,11 +1443,35 @@ static void tex_image(const Ctx *c, const pbrtgpu_texture *tx, int nc, const Tex
     tex_map(tx, q, &s, &t, &dsdx, &dtdx, &dsdy, &dtdy);
     mip_lookup(c, tx, nc, s, t, dsdx, dtdx, dsdy, dtdy, out);
 }
+/* Checkerboard2DTexture::Evaluate (checkerboard.h:84-125) without its operands: 0 = tex1, 1 = tex2,
+ * 2 = (1 - area2) * tex1 + area2 * tex2 */
+static float bumpint(float x) { int f = (int)floorf(x / 2); return (float)f + 2.f * fmaxf_((x / 2) - (float)f - .5f, 0.f); }
+static int checker_pick(const pbrtgpu_texture *tx, const TexPt *q, float *area2) {
+    float s, t, dsdx, dtdx, dsdy, dtdy;
+    tex_map(tx, q, &s, &t, &dsdx, &dtdx, &dsdy, &dtdy);
+    int point = (((int)floorf(s) + (int)floorf(t)) % 2 == 0) ? 0 : 1;
+    if (tx->aamode == 1) return point;
+    float ds = fmaxf_(fabsf(dsdx), fabsf(dsdy)), dt = fmaxf_(fabsf(dtdx), fabsf(dtdy));
+    float s0 = s - ds, s1 = s + ds, t0 = t - dt, t1 = t + dt;
+    if ((int)floorf(s0) == (int)floorf(s1) && (int)floorf(t0) == (int)floorf(t1)) return point;
+    float sint = (bumpint(s1) - bumpint(s0)) / (2.f * ds);
+    float tint = (bumpint(t1) - bumpint(t0)) / (2.f * dt);
+    float a = sint + tint - 2.f * sint * tint;
+    if (ds > 1.f || dt > 1.f) a = .5f;
+    *area2 = a;
+    return 2;
+}
 static float tex_float(const Ctx *c, int id, const TexPt *q) {
     const pbrtgpu_texture *tx = &c->s->textures[id];
     switch (tx->type) {
         case PBRTGPU_TEX_CONST: return tx->value;
         case PBRTGPU_TEX_IMAGE: { float v; tex_image(c, tx, 1, q, &v); return v; }
+        case PBRTGPU_TEX_CHECKER: {
+            float a2 = 0.f;
+            int k = checker_pick(tx, q, &a2);
+            if (k < 2) return tex_float(c, k == 0 ? tx->tex1 : tx->tex2, q);
+            return (1.f - a2) * tex_float(c, tx->tex1, q) + a2 * tex_float(c, tx->tex2, q);
+        }
         default: return tex_float(c, tx->tex1, q) * tex_float(c, tx->tex2, q);   /* ScaleTexture */
     }
 }
@@ -1457,6 +1481,16 @@ static void tex_spec(const Ctx *c, int id, const TexPt *q, float *out) {
     switch (tx->type) {
         case PBRTGPU_TEX_CONST: memcpy(out, SPEC(c, tx->spec), sizeof(float) * nb); return;
         case PBRTGPU_TEX_IMAGE: { float rgb[3]; tex_image(c, tx, 3, q, rgb); from_rgb(c, rgb, 0, out); return; }
+        case PBRTGPU_TEX_CHECKER: {
+            float a2 = 0.f;
+            int k = checker_pick(tx, q, &a2);
+            if (k < 2) { tex_spec(c, k == 0 ? tx->tex1 : tx->tex2, q, out); return; }
+            float a[MAXB], b[MAXB];
+            tex_spec(c, tx->tex1, q, a);
+            tex_spec(c, tx->tex2, q, b);
+            for (int i = 0; i < nb; ++i) out[i] = (a[i] * (1.f - a2)) + (b[i] * a2);   /* s * a, then the sum */
+            return;
+        }
         default: {
             float a[MAXB], b[MAXB];
             tex_spec(c, tx->tex1, q, a);

@@ -97,6 +97,7 @@ static inline void spec_out(const Spectrum &L, float *c) { L.GetOrigC(c); }
 #include "shapes/loopsubdiv.h"
 #include "textures/constant.h"
 #include "textures/imagemap.h"
+#include "textures/checkerboard.h"
 #include "textures/scale.h"
 
 #include <map>
@@ -427,12 +428,14 @@ static Reference<Texture<float> > MakeFloatTex(const string &n, const Transform 
     if (n == "constant") return CreateConstantFloatTexture(x, tp);
     if (n == "scale") return CreateScaleFloatTexture(x, tp);
     if (n == "imagemap") return CreateImageFloatTexture(x, tp);
+    if (n == "checkerboard") return CreateCheckerboardFloatTexture(x, tp);
     fprintf(stderr, "harness: float texture %s unsupported\n", n.c_str()); exit(2);
 }
 static Reference<Texture<Spectrum> > MakeSpecTex(const string &n, const Transform &x, const TextureParams &tp) {
     if (n == "constant") return CreateConstantSpectrumTexture(x, tp);
     if (n == "scale") return CreateScaleSpectrumTexture(x, tp);
     if (n == "imagemap") return CreateImageSpectrumTexture(x, tp);
+    if (n == "checkerboard") return CreateCheckerboardSpectrumTexture(x, tp);
     fprintf(stderr, "harness: spectrum texture %s unsupported\n", n.c_str()); exit(2);
 }
 void pbrtTexture(const string &name, const string &type, const string &texname, const ParamSet &params) {

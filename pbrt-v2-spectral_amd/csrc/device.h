@@ -2058,20 +2058,73 @@ PGD_INLINE float tex_leaf_float(const DevScene &S, int id, const TexPt &q) {
     tex_image<1>(S, tx, q, &v);
     return v;
 }
-// Texture<float>: CONST, IMAGE, or ScaleTexture of two leaves (front end guarantees the depth)
+// Checkerboard2DTexture::Evaluate (checkerboard.h:84-125) without its operands: 0 = tex1 alone,
+// 1 = tex2 alone, 2 = (1 - area2) * tex1 + area2 * tex2 (*area2 set)
+PGD_INLINE int checker_pick(const pbrtgpu_texture &tx, const TexPt &q, float *area2) {
+    float s, t, dsdx, dtdx, dsdy, dtdy;
+    tex_map(tx, q, &s, &t, &dsdx, &dtdx, &dsdy, &dtdy);
+    const int point = ((int)floorf(s) + (int)floorf(t)) % 2 == 0 ? 0 : 1;   // Floor2Int
+    if (tx.aamode == 1) return point;
+    const float ds = pmax(fabsf(dsdx), fabsf(dsdy)), dt = pmax(fabsf(dtdx), fabsf(dtdy));   // std::max
+    const float s0 = s - ds, s1 = s + ds, t0 = t - dt, t1 = t + dt;
+    if ((int)floorf(s0) == (int)floorf(s1) && (int)floorf(t0) == (int)floorf(t1)) return point;
+    // BUMPINT(x) = Floor2Int(x / 2) + 2 * max(x / 2 - Floor2Int(x / 2) - .5, 0)
+    auto bumpint = [](float x) {
+        const int f = (int)floorf(x / 2);
+        return (float)f + 2.f * pmax((x / 2) - (float)f - .5f, 0.f);
+    };
+    const float sint = (bumpint(s1) - bumpint(s0)) / (2.f * ds);
+    const float tint = (bumpint(t1) - bumpint(t0)) / (2.f * dt);
+    float a = sint + tint - 2.f * sint * tint;
+    if (ds > 1.f || dt > 1.f) a = .5f;
+    *area2 = a;
+    return 2;
+}
+// Texture<float>: CONST, IMAGE, ScaleTexture or Checkerboard2DTexture of two leaves (the front end
+// guarantees the depth)
 PGD_HEAVY float tex_float(const DevScene &S, int id, const TexPt &q) {
     const pbrtgpu_texture &tx = (*sa(S.tex, (uint32_t)(id)));
+    if (tx.type == PBRTGPU_TEX_CHECKER) {
+        float a2 = 0.f;
+        const int k = checker_pick(tx, q, &a2);
+        if (k < 2) return tex_leaf_float(S, k == 0 ? tx.tex1 : tx.tex2, q);
+        return (1.f - a2) * tex_leaf_float(S, tx.tex1, q) + a2 * tex_leaf_float(S, tx.tex2, q);
+    }
     if (tx.type != PBRTGPU_TEX_SCALE) return tex_leaf_float(S, id, q);
     return tex_leaf_float(S, tx.tex1, q) * tex_leaf_float(S, tx.tex2, q);
 }
 // Texture<Spectrum> in device form: FromRGB(image lookup) [times a constant spectrum, in the
 // ScaleTexture operand order]; SpecTex carries the per-hit part, spec4 evaluates a band quad
-struct SpecTex { RGBPick pick; int constOff; bool constFirst; };
+// A Checkerboard2DTexture becomes one of its leaves (CONST: constOnly) or a blend of both: the
+// second leaf in pick2 / constOff2 and the weights w1 = 1 - area2, w2 = area2 (blend)
+struct SpecTex { RGBPick pick; int constOff; bool constFirst, constOnly, blend; RGBPick pick2; int constOff2; float w1, w2; };
+// one leaf of a checkerboard (CONST or IMAGE) into pick / constOff (constant: constOff >= 0)
+PGD_INLINE void spec_leaf(const DevScene &S, int id, const TexPt &q, RGBPick *pick, int *constOff) {
+    const pbrtgpu_texture &lf = (*sa(S.tex, (uint32_t)(id)));
+    if (lf.type == PBRTGPU_TEX_CONST) { *constOff = lf.spec; pick->k0 = pick->k1 = pick->k2 = -1; pick->a0 = pick->a1 = pick->a2 = 0.f; return; }
+    float rgb[3];
+    tex_image<3>(S, lf, q, rgb);
+    *pick = rgb_pick(S, rgb);
+    *constOff = -1;
+}
 PGD_HEAVY SpecTex tex_spec_prepare(const DevScene &S, int id, const TexPt &q) {
     SpecTex r;
-    r.constOff = -1; r.constFirst = false;
+    r.constOff = -1; r.constFirst = false; r.constOnly = false; r.blend = false; r.constOff2 = -1; r.w1 = r.w2 = 0.f;
     int img = id;
     const pbrtgpu_texture &tx = (*sa(S.tex, (uint32_t)(id)));
+    if (tx.type == PBRTGPU_TEX_CHECKER) {
+        float a2 = 0.f;
+        const int k = checker_pick(tx, q, &a2);
+        spec_leaf(S, k == 1 ? tx.tex2 : tx.tex1, q, &r.pick, &r.constOff);
+        r.constOnly = r.constOff >= 0;
+        if (k == 2) {
+            r.blend = true;
+            spec_leaf(S, tx.tex2, q, &r.pick2, &r.constOff2);
+            r.w1 = 1.f - a2;
+            r.w2 = a2;
+        }
+        return r;
+    }
     if (tx.type == PBRTGPU_TEX_SCALE) {
         const bool firstConst = (*sa(S.tex, (uint32_t)(tx.tex1))).type == PBRTGPU_TEX_CONST;
         img = firstConst ? tx.tex2 : tx.tex1;
@@ -2084,6 +2137,16 @@ PGD_HEAVY SpecTex tex_spec_prepare(const DevScene &S, int id, const TexPt &q) {
     return r;
 }
 PGD_INLINE float4 tex_spec4(const DevScene &S, const SpecTex &t, int q) {
+    if (t.constOnly || t.blend) {   // a checkerboard: leaf 1 [blended with leaf 2]
+        const float4 a = t.constOnly ? *reinterpret_cast<const float4 *>(sa(S.spectra, (uint32_t)(t.constOff + 4 * q)))
+                                     : from_rgb4(S, t.pick, false, q);
+        if (!t.blend) return a;
+        const float4 b = t.constOff2 >= 0 ? *reinterpret_cast<const float4 *>(sa(S.spectra, (uint32_t)(t.constOff2 + 4 * q)))
+                                          : from_rgb4(S, t.pick2, false, q);
+        // (1 - area2) * tex1 + area2 * tex2: CoefficientSpectrum's s * a, then the sum
+        return make_float4((a.x * t.w1) + (b.x * t.w2), (a.y * t.w1) + (b.y * t.w2), (a.z * t.w1) + (b.z * t.w2),
+                           (a.w * t.w1) + (b.w * t.w2));
+    }
     float4 a = from_rgb4(S, t.pick, false, q);
     if (t.constOff < 0) return a;
     float4 b = *reinterpret_cast<const float4 *>(sa(S.spectra, (uint32_t)(t.constOff + 4 * q)));

@@ -1131,15 +1131,11 @@ private:
         *w = *h = 1;
         return true;
     }
-    // ImageTexture (imagemap.cpp:47-73 GetTexture, :97-160 Create*): the image after convertIn --
-    // Pow(scale * rgb, gamma) per channel, or powf(scale * rgb.y(), gamma) for a float texture --
-    // in a MIPMap pyramid (BuildMipmap) in out->texels; an unreadable .tga / .pfm gives the
-    // one-valued MIPMap(1, 1, powf(scale, gamma)) with the MIPMap defaults
-    int MakeImageTexture(const ParamSet &p, bool spectral) {
-        pbrtgpu_texture t = TexNode(PBRTGPU_TEX_IMAGE, spectral);
-        // the 2D mapping (imagemap.cpp:107-125): uv (its scales / offsets), spherical and cylindrical
-        // (WorldToTexture = Inverse(tex2world), the CTM at the Texture directive), planar (v1, v2 and
-        // the udelta / vdelta offsets); an unknown name is the reference's Error + default UVMapping2D
+    // the 2D mapping of an image or checkerboard texture (imagemap.cpp:107-125, checkerboard.cpp:
+    // 36-55): uv (its scales / offsets), spherical and cylindrical (WorldToTexture = Inverse(tex2world),
+    // the CTM at the Texture directive), planar (v1, v2 and the udelta / vdelta offsets); an unknown
+    // name is the reference's Error + default UVMapping2D
+    void ParseMapping(const ParamSet &p, pbrtgpu_texture &t) {
         const std::string mapping = GetString(p, p, "mapping", "uv");
         if (mapping == "uv") {
             t.su = GetFloat(p, p, "uscale", 1.f); t.sv = GetFloat(p, p, "vscale", 1.f);
@@ -1154,6 +1150,14 @@ private:
             t.map[0] = vs.x; t.map[1] = vs.y; t.map[2] = vs.z; t.map[3] = vt.x; t.map[4] = vt.y; t.map[5] = vt.z;
             t.du = GetFloat(p, p, "udelta", 0.f); t.dv = GetFloat(p, p, "vdelta", 0.f);
         } else fprintf(stderr, "pbrthost: 2D texture mapping \"%s\" unknown (UVMapping2D)\n", mapping.c_str());
+    }
+    // ImageTexture (imagemap.cpp:47-73 GetTexture, :97-160 Create*): the image after convertIn --
+    // Pow(scale * rgb, gamma) per channel, or powf(scale * rgb.y(), gamma) for a float texture --
+    // in a MIPMap pyramid (BuildMipmap) in out->texels; an unreadable .tga / .pfm gives the
+    // one-valued MIPMap(1, 1, powf(scale, gamma)) with the MIPMap defaults
+    int MakeImageTexture(const ParamSet &p, bool spectral) {
+        pbrtgpu_texture t = TexNode(PBRTGPU_TEX_IMAGE, spectral);
+        ParseMapping(p, t);
         float maxAniso = GetFloat(p, p, "maxanisotropy", 8.f);
         bool trilerp = p.FindOneBool("trilinear", false), noFilt = p.FindOneBool("noFiltering", false);
         std::string wrap = GetString(p, p, "wrap", "repeat");
@@ -1197,6 +1201,38 @@ private:
         mipCache[spectral ? 1 : 0][key] = t;
         return AddTexture(t);
     }
+    // a Checkerboard2DTexture node: the 2D mapping and the antialiasing mode ("closedform", "none";
+    // anything else is the reference's warning + closedform); dimension 3 (Checkerboard3DTexture)
+    // is not built
+    pbrtgpu_texture CheckerNode(const ParamSet &p, bool spectral) {
+        if (p.FindOneInt("dimension", 2) != 2) throw std::runtime_error("3D checkerboard textures are not supported yet");
+        pbrtgpu_texture n = TexNode(PBRTGPU_TEX_CHECKER, spectral);
+        ParseMapping(p, n);
+        const std::string aa = GetString(p, p, "aamode", "closedform");
+        if (aa != "none" && aa != "closedform")
+            fprintf(stderr, "pbrthost: antialiasing mode \"%s\" not understood by Checkerboard2DTexture; using \"closedform\"\n", aa.c_str());
+        n.aamode = aa == "none" ? 1 : 0;
+        return n;
+    }
+    // operands of a checkerboard: constants become CONST nodes, textures must be image maps
+    int CheckerLeaf(const FloatTex &f) {
+        if (f.constant) {
+            pbrtgpu_texture t = TexNode(PBRTGPU_TEX_CONST, false);
+            t.value = f.value;
+            return AddTexture(t);
+        }
+        if (out->textures[f.tex].type != PBRTGPU_TEX_IMAGE) throw std::runtime_error("checkerboard operands other than constants and image maps are not supported yet");
+        return f.tex;
+    }
+    int CheckerLeaf(const SpecTex &f) {
+        if (f.constant) {
+            pbrtgpu_texture t = TexNode(PBRTGPU_TEX_CONST, true);
+            t.spec = EmitSpectrum(f.value);
+            return AddTexture(t);
+        }
+        if (out->textures[f.tex].type != PBRTGPU_TEX_IMAGE) throw std::runtime_error("checkerboard operands other than constants and image maps are not supported yet");
+        return f.tex;
+    }
     // operand of a ScaleTexture: a CONST or IMAGE node
     int FloatLeaf(const FloatTex &f) {
         if (!f.constant) {
@@ -1221,6 +1257,12 @@ private:
                     t.constant = false; t.tex = AddTexture(n);
                 }
             } else if (cls == "imagemap") { t.constant = false; t.tex = MakeImageTexture(p, false); }
+            else if (cls == "checkerboard") {   // Checkerboard2DTexture<float> (checkerboard.cpp:29-67)
+                pbrtgpu_texture n = CheckerNode(p, false);
+                n.tex1 = CheckerLeaf(GetFloatTex(p, p, "tex1", 1.f));
+                n.tex2 = CheckerLeaf(GetFloatTex(p, p, "tex2", 0.f));
+                t.constant = false; t.tex = AddTexture(n);
+            }
             else throw std::runtime_error("float texture '" + cls + "' is not supported yet");
             gs.floatTextures[name] = t;
         } else if (type == "color" || type == "spectrum") {
@@ -1242,6 +1284,12 @@ private:
                     t.constant = false; t.tex = AddTexture(n);
                 }
             } else if (cls == "imagemap") { t.constant = false; t.tex = MakeImageTexture(p, true); }
+            else if (cls == "checkerboard") {   // Checkerboard2DTexture<Spectrum> (checkerboard.cpp:71-110)
+                pbrtgpu_texture n = CheckerNode(p, true);
+                n.tex1 = CheckerLeaf(GetSpecTex(p, p, "tex1", spec.Const(1.f)));
+                n.tex2 = CheckerLeaf(GetSpecTex(p, p, "tex2", spec.Const(0.f)));
+                t.constant = false; t.tex = AddTexture(n);
+            }
             else throw std::runtime_error("spectrum texture '" + cls + "' is not supported yet");
             gs.spectrumTextures[name] = t;
         }

@@ -102,7 +102,7 @@ def _golden_scene(pg, cfg, name="killeroo"):
             "coverage": "coverage.pack", "imagemap": "imagemap.pack",
             "animcam": "animcam.pack", "textured": "textured.pack", "envmap": "envmap.pack", "lights": "lights.pack",
             "ortho": "ortho.pack", "heightfield": "heightfield.pack",
-            "cylinder": "cylinder.pack", "anisoward": "anisoward.pack", "mappings": "mappings.pack",
+            "cylinder": "cylinder.pack", "anisoward": "anisoward.pack", "mappings": "mappings.pack", "checker": "checker.pack",
             "shinymetal": "shinymetal.pack", "nurbs": "nurbs.pack"}.get(name.split("_")[0],
                                                                                               "killeroo-simple.pack")
     if "_b30_" in name:
@@ -118,7 +118,7 @@ def _golden_scene(pg, cfg, name="killeroo"):
                                   "coverage_b30_paths_48x36s4", "imagemap_paths_64x48s4",
                                   "imagemap_paths_96x72s2_seed5", "animcam_paths_64x48s4", "textured_paths_64x48s4", "envmap_paths_64x48s4",
                                   "lights_paths_64x48s4", "ortho_paths_64x48s4", "heightfield_paths_64x48s4",
-         "cylinder_paths_64x48s4", "anisoward_paths_64x48s4", "mappings_paths_64x48s4",
+         "cylinder_paths_64x48s4", "anisoward_paths_64x48s4", "mappings_paths_64x48s4", "checker_paths_64x48s4",
          "shinymetal_paths_64x48s4", "nurbs_paths_64x48s4"])
 def test_paths_vs_reference_golden(pg, name):
     """GPU against the reference harness's own per-path radiance (fixed seeds); the *_keys_*
@@ -137,7 +137,7 @@ def test_paths_vs_reference_golden(pg, name):
                                   "coverage_b30_film_40x30s4", "imagemap_film_64x48s8",
                                   "animcam_film_64x48s4", "textured_film_64x48s8", "envmap_film_64x48s8",
                                   "lights_film_64x48s8", "ortho_film_64x48s4", "heightfield_film_64x48s4",
-                                  "cylinder_film_64x48s4", "anisoward_film_64x48s4", "mappings_film_64x48s4",
+                                  "cylinder_film_64x48s4", "anisoward_film_64x48s4", "mappings_film_64x48s4", "checker_film_64x48s4",
                                   "shinymetal_film_64x48s4", "nurbs_film_64x48s4"])
 def test_film_vs_reference_golden(pg, name):
     """Whole-film render against the reference's film (raw sums, incl. neighbour-pixel
@@ -340,7 +340,7 @@ def test_regular_halfangle_brdf_vs_reference_golden(pg, merl_dir):
     assert_bit_exact(L, pg.oracle().trace_paths(scene, g["keys"]), "merl paths vs oracle")
 
 
-DL = ["mappings_dl_%s_48x36s4", "shinymetal_dl_%s_48x36s4", "anisoward_dl_%s_48x36s4", "cylinder_dl_%s_48x36s4", "ortho_dl_%s_48x36s4", "lights_dl_%s_48x36s4", "textured_dl_%s_48x36s4", "envmap_dl_%s_48x36s4", "killeroo_dl_%s_48x40s4", "bunny_dl_%s_48x27s4", "anim_dl_%s_40x40s4", "coverage_dl_%s_64x48s4",
+DL = ["checker_dl_%s_48x36s4", "mappings_dl_%s_48x36s4", "shinymetal_dl_%s_48x36s4", "anisoward_dl_%s_48x36s4", "cylinder_dl_%s_48x36s4", "ortho_dl_%s_48x36s4", "lights_dl_%s_48x36s4", "textured_dl_%s_48x36s4", "envmap_dl_%s_48x36s4", "killeroo_dl_%s_48x40s4", "bunny_dl_%s_48x27s4", "anim_dl_%s_40x40s4", "coverage_dl_%s_64x48s4",
       "coverage_dlone_%s_64x48s4"]
 
 

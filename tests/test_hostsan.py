@@ -105,6 +105,9 @@ CASES = [
     # spherical / cylindrical / planar texture mappings (image textures, bump maps)
     ("mappings.pack", dict(xres=40, yres=30, spp=4, maxdepth=3)),
     ("mappings.pack", dict(xres=32, yres=24, spp=2, maxdepth=3, integrator="directlighting", strategy="all")),
+    # Checkerboard2DTexture (closed form / point sampled, constant and image operands, mappings)
+    ("checker.pack", dict(xres=40, yres=30, spp=4, maxdepth=3)),
+    ("checker.pack", dict(xres=32, yres=24, spp=2, maxdepth=3, integrator="directlighting", strategy="all")),
     # NURBS patches (refined on the host into a mesh with normals)
     ("nurbs.pack", dict(xres=40, yres=30, spp=2, maxdepth=5)),
     # heightfield shapes (refined on the host; one as an area light)
@@ -122,7 +125,7 @@ CASES = [
                                                "lens_microlens_spectral", "eye", "eye_spectral", "lens_diffraction_dl",
                                                "imagemap", "imagemap_dl", "animcam", "textured", "textured_dl", "envmap", "envmap_dl",
                                                "dl_anim_inst",
-                                               "dl_metal60", "rgb_imagemap", "rgb_envmap_dl", "rgb_coverage", "lights", "lights_dl", "shinymetal", "shinymetal_dl", "anisoward", "cylinder", "cylinder_dl", "mappings", "mappings_dl", "nurbs", "heightfield", "ortho", "lens_animated"])
+                                               "dl_metal60", "rgb_imagemap", "rgb_envmap_dl", "rgb_coverage", "lights", "lights_dl", "shinymetal", "shinymetal_dl", "anisoward", "cylinder", "cylinder_dl", "mappings", "mappings_dl", "checker", "checker_dl", "nurbs", "heightfield", "ortho", "lens_animated"])
 def test_replay_matches_oracle(pg, tmp_path, pack, a):
     exe = _build("shade_host")
     scene = pg.Scene.load(os.path.join(PACKS, pack), **a)

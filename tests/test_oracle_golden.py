@@ -21,7 +21,7 @@ def _scene(pg, cfg, name="killeroo"):
             "coverage": "coverage.pack", "imagemap": "imagemap.pack",
             "animcam": "animcam.pack", "textured": "textured.pack", "envmap": "envmap.pack", "lights": "lights.pack",
             "ortho": "ortho.pack", "heightfield": "heightfield.pack",
-            "cylinder": "cylinder.pack", "anisoward": "anisoward.pack", "mappings": "mappings.pack",
+            "cylinder": "cylinder.pack", "anisoward": "anisoward.pack", "mappings": "mappings.pack", "checker": "checker.pack",
             "shinymetal": "shinymetal.pack", "nurbs": "nurbs.pack"}.get(name.split("_")[0],
                                                                                               "killeroo-simple.pack")
     # *_b30_*: the upstream 30-band, 400-700 nm build (b30 harness, spectrum.h.original:36-38)
@@ -40,7 +40,7 @@ PATHS = ["killeroo_paths_64x64s4", "killeroo_paths_48x48s8_seed7_md7", "anim_pat
          "metal_paths_48x48s4", "coverage_paths_64x48s8", "killeroo_b30_paths_48x40s4", "coverage_b30_paths_48x36s4",
          "imagemap_paths_64x48s4", "imagemap_paths_96x72s2_seed5", "animcam_paths_64x48s4", "textured_paths_64x48s4", "envmap_paths_64x48s4",
          "lights_paths_64x48s4", "ortho_paths_64x48s4", "heightfield_paths_64x48s4",
-         "cylinder_paths_64x48s4", "anisoward_paths_64x48s4", "mappings_paths_64x48s4",
+         "cylinder_paths_64x48s4", "anisoward_paths_64x48s4", "mappings_paths_64x48s4", "checker_paths_64x48s4",
          "shinymetal_paths_64x48s4", "nurbs_paths_64x48s4"]
 # the configs at their real size and sample count (BASELINE.json configs 2-5; harness --keys):
 # every sample of a few pixels plus random keys of the whole sample extent
@@ -79,7 +79,7 @@ def test_paths_restated_libm_bit_exact_vs_reference(pg, name):
                                   "coverage_b30_film_40x30s4", "imagemap_film_64x48s8",
                                   "animcam_film_64x48s4", "textured_film_64x48s8", "envmap_film_64x48s8",
                                   "lights_film_64x48s8", "ortho_film_64x48s4", "heightfield_film_64x48s4",
-                                  "cylinder_film_64x48s4", "anisoward_film_64x48s4", "mappings_film_64x48s4",
+                                  "cylinder_film_64x48s4", "anisoward_film_64x48s4", "mappings_film_64x48s4", "checker_film_64x48s4",
                                   "shinymetal_film_64x48s4", "nurbs_film_64x48s4"])
 def test_film_bit_exact_vs_reference(pg, ora_libm, name):
     g = np.load(os.path.join(GOLDEN, name + ".npz"))
@@ -134,7 +134,7 @@ def test_regular_halfangle_brdf_bit_exact_vs_reference(pg, ora_libm, merl_dir, n
         assert np.array_equal(film.view(np.int32), g["film"].view(np.int32))
 
 
-DL = ["mappings_dl_%s_48x36s4", "shinymetal_dl_%s_48x36s4", "anisoward_dl_%s_48x36s4", "cylinder_dl_%s_48x36s4", "ortho_dl_%s_48x36s4", "lights_dl_%s_48x36s4", "textured_dl_%s_48x36s4", "envmap_dl_%s_48x36s4", "killeroo_dl_%s_48x40s4", "bunny_dl_%s_48x27s4", "anim_dl_%s_40x40s4", "coverage_dl_%s_64x48s4",
+DL = ["checker_dl_%s_48x36s4", "mappings_dl_%s_48x36s4", "shinymetal_dl_%s_48x36s4", "anisoward_dl_%s_48x36s4", "cylinder_dl_%s_48x36s4", "ortho_dl_%s_48x36s4", "lights_dl_%s_48x36s4", "textured_dl_%s_48x36s4", "envmap_dl_%s_48x36s4", "killeroo_dl_%s_48x40s4", "bunny_dl_%s_48x27s4", "anim_dl_%s_40x40s4", "coverage_dl_%s_64x48s4",
       "coverage_dlone_%s_64x48s4"]
 
 
@@ -145,7 +145,7 @@ def dl_scene(pg, g, name):
     pack = {"anim": "anim-killeroos-moving.pack", "bunny": "bunny.pack", "coverage": "coverage.pack",
             "textured": "textured.pack", "envmap": "envmap.pack", "lights": "lights.pack",
             "ortho": "ortho.pack", "heightfield": "heightfield.pack",
-            "cylinder": "cylinder.pack", "anisoward": "anisoward.pack", "mappings": "mappings.pack",
+            "cylinder": "cylinder.pack", "anisoward": "anisoward.pack", "mappings": "mappings.pack", "checker": "checker.pack",
             "shinymetal": "shinymetal.pack", "nurbs": "nurbs.pack"}.get(
         name.split("_")[0], "killeroo-simple.pack")
     return pg.Scene.load(os.path.join(PACKS, pack), xres=w, yres=h, spp=spp, maxdepth=md, seed=seed,

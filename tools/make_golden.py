@@ -63,6 +63,10 @@ Fixtures (numpy .npz, inputs + expected outputs only):
   mappings_*                      tests/scenes/mappings.pbrt: spherical, cylindrical and planar 2D
                                   texture mappings (image textures and bump maps), path and
                                   DirectLighting
+  checker_*                       tests/scenes/checker.pbrt: Checkerboard2DTexture (closed-form box
+                                  filter and point sampled, constant / image operands, uv, planar and
+                                  spherical mappings, float checkerboards as bump and roughness),
+                                  path and DirectLighting
   shinymetal_*                    tests/scenes/shinymetal.pbrt: shinymetal (conductor microfacet and
                                   mirror lobes), path and DirectLighting
   anisoward_*                     tests/scenes/anisoward.pbrt: the fork's anisotropic Ward material
@@ -87,7 +91,7 @@ Fixtures (numpy .npz, inputs + expected outputs only):
                                   pixel holds all of its contributions (incl. exact-boundary samples
                                   of its neighbours, spectralImage.cpp:77-152); C2 at the sphere
                                   light's edge and at a killeroo silhouette, C3-C5 at an edge each
-Usage: python tools/make_golden.py [--only keys|dat|merl|dl|meta|spec|rgb|rgbfeat|mappings|lights|ortho|heightfield|cylinder|anisoward|shinymetal|nurbs|b30|window|imagemap|animcam|gpupath|textured|envmap]
+Usage: python tools/make_golden.py [--only keys|dat|merl|dl|meta|spec|rgb|rgbfeat|mappings|checker|lights|ortho|heightfield|cylinder|anisoward|shinymetal|nurbs|b30|window|imagemap|animcam|gpupath|textured|envmap]
        (after `make -C oracle ref`, `ref60`, `ref30` and `refrgb`)
 """
 import os
@@ -434,6 +438,17 @@ def mappings_fixtures(tmp):
     film_fixture("mappings_dl_film_48x36s4", (48, 36), 4, 0, 5, tmp, scene=sc, extra=ex)
 
 
+def checker_fixtures(tmp):
+    """tests/scenes/checker.pbrt: Checkerboard2DTexture (checkerboard.h:84-125) with its mappings and
+    operands; path and DirectLighting"""
+    sc = os.path.join(ROOT, "tests", "scenes", "checker.pbrt")
+    paths_fixture("checker_paths_64x48s4", (64, 48), 4, 0, 5, 1, tmp, scene=sc)
+    film_fixture("checker_film_64x48s4", (64, 48), 4, 0, 5, tmp, scene=sc)
+    ex = ("--surf", "directlighting", "--dl-strategy", "all")
+    paths_fixture("checker_dl_paths_48x36s4", (48, 36), 4, 0, 5, 1, tmp, scene=sc, extra=ex)
+    film_fixture("checker_dl_film_48x36s4", (48, 36), 4, 0, 5, tmp, scene=sc, extra=ex)
+
+
 def shinymetal_fixtures(tmp):
     """tests/scenes/shinymetal.pbrt: shinymetal's conductor microfacet and mirror lobes (FresnelApproxEta
     of constant Ks / Kr); path and DirectLighting (its specular recursion)"""
@@ -517,6 +532,8 @@ def main():
                 nurbs_fixtures(tmp)
             elif only == "mappings":
                 mappings_fixtures(tmp)
+            elif only == "checker":
+                checker_fixtures(tmp)
             elif only == "shinymetal":
                 shinymetal_fixtures(tmp)
             elif only == "anisoward":

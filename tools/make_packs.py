@@ -49,6 +49,8 @@ PACKS = [
     ("shinymetal", os.path.join(ROOT, "tests", "scenes", "shinymetal.pbrt"), 32, 64, 48, 4),
     # spherical / cylindrical / planar texture mappings
     ("mappings", os.path.join(ROOT, "tests", "scenes", "mappings.pbrt"), 32, 64, 48, 4),
+    # Checkerboard2DTexture
+    ("checker", os.path.join(ROOT, "tests", "scenes", "checker.pbrt"), 32, 64, 48, 4),
     # NURBS surfaces
     ("nurbs", os.path.join(ROOT, "tests", "scenes", "nurbs.pbrt"), 32, 64, 48, 4),
 ]
@@ -63,7 +65,7 @@ def main():
             continue
         # the configs render with "path" (SURVEY App. B); load a pack with integrator="directlighting"
         # to render it with the DirectLightingIntegrator the scene files name
-        s = pg.Scene.load(os.path.join(REF, fn), xres=xr, yres=yr, spp=spp, maxdepth=-1 if name.startswith(("coverage", "imagemap", "animcam", "textured", "envmap", "lights", "ortho", "heightfield", "cylinder", "anisoward", "shinymetal", "nurbs", "mappings")) else 5,
+        s = pg.Scene.load(os.path.join(REF, fn), xres=xr, yres=yr, spp=spp, maxdepth=-1 if name.startswith(("coverage", "imagemap", "animcam", "textured", "envmap", "lights", "ortho", "heightfield", "cylinder", "anisoward", "shinymetal", "nurbs", "mappings", "checker")) else 5,
                           bands=bands, integrator="path")
         path = os.path.join(out, name + ".pack")
         s.save_pack(path)
