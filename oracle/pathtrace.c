@@ -1443,6 +1443,14 @@ static void tex_image(const Ctx *c, const pbrtgpu_texture *tx, int nc, const Tex
     tex_map(tx, q, &s, &t, &dsdx, &dtdx, &dsdy, &dtdy);
     mip_lookup(c, tx, nc, s, t, dsdx, dtdx, dsdy, dtdy, out);
 }
+/* UVTexture::Evaluate / EvaluateMemory (uv.h:38-51): the RGB (s - Floor2Int(s), t - Floor2Int(t), 0) */
+static void uv_rgb(const pbrtgpu_texture *tx, const TexPt *q, float rgb[3]) {
+    float s, t, dsdx, dtdx, dsdy, dtdy;
+    tex_map(tx, q, &s, &t, &dsdx, &dtdx, &dsdy, &dtdy);
+    rgb[0] = s - (float)(int)floorf(s);
+    rgb[1] = t - (float)(int)floorf(t);
+    rgb[2] = 0.f;
+}
 /* Checkerboard2DTexture::Evaluate (checkerboard.h:84-125) without its operands: 0 = tex1, 1 = tex2,
  * 2 = (1 - area2) * tex1 + area2 * tex2 */
 static float bumpint(float x) { int f = (int)floorf(x / 2); return (float)f + 2.f * fmaxf_((x / 2) - (float)f - .5f, 0.f); }
@@ -1481,6 +1489,7 @@ static void tex_spec(const Ctx *c, int id, const TexPt *q, float *out) {
     switch (tx->type) {
         case PBRTGPU_TEX_CONST: memcpy(out, SPEC(c, tx->spec), sizeof(float) * nb); return;
         case PBRTGPU_TEX_IMAGE: { float rgb[3]; tex_image(c, tx, 3, q, rgb); from_rgb(c, rgb, 0, out); return; }
+        case PBRTGPU_TEX_UV: { float rgb[3]; uv_rgb(tx, q, rgb); from_rgb(c, rgb, 0, out); return; }
         case PBRTGPU_TEX_CHECKER: {
             float a2 = 0.f;
             int k = checker_pick(tx, q, &a2);
@@ -1556,6 +1565,7 @@ static void compute_differentials(const DG *dg, const RayDiff *rd, float out[10]
 static void tex_memory_leaf(const Ctx *c, int id, const TexPt *q, float rgb[3]) {
     const pbrtgpu_texture *tx = &c->s->textures[id];
     if (tx->type == PBRTGPU_TEX_IMAGE) tex_image(c, tx, 3, q, rgb);
+    else if (tx->type == PBRTGPU_TEX_UV) uv_rgb(tx, q, rgb);
     else rgb[0] = rgb[1] = rgb[2] = 0.f;
 }
 /* Material::NormalMap (material.cpp:82-126), taken by every material where the map's Evaluate is

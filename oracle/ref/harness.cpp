@@ -98,6 +98,7 @@ static inline void spec_out(const Spectrum &L, float *c) { L.GetOrigC(c); }
 #include "textures/constant.h"
 #include "textures/imagemap.h"
 #include "textures/checkerboard.h"
+#include "textures/uv.h"
 #include "textures/scale.h"
 
 #include <map>
@@ -436,6 +437,7 @@ static Reference<Texture<Spectrum> > MakeSpecTex(const string &n, const Transfor
     if (n == "scale") return CreateScaleSpectrumTexture(x, tp);
     if (n == "imagemap") return CreateImageSpectrumTexture(x, tp);
     if (n == "checkerboard") return CreateCheckerboardSpectrumTexture(x, tp);
+    if (n == "uv") return CreateUVSpectrumTexture(x, tp);
     fprintf(stderr, "harness: spectrum texture %s unsupported\n", n.c_str()); exit(2);
 }
 void pbrtTexture(const string &name, const string &type, const string &texname, const ParamSet &params) {

@@ -2051,6 +2051,17 @@ PGD_INLINE void tex_image(const DevScene &S, const pbrtgpu_texture &tx, const Te
     tex_map(tx, q, &s, &t, &dsdx, &dtdx, &dsdy, &dtdy);
     mip_lookup<NC>(S, tx, s, t, dsdx, dtdx, dsdy, dtdy, out);
 }
+// the RGB of a spectrum leaf before FromRGB: an image map's MIPMap lookup, or UVTexture's
+// (s - Floor2Int(s), t - Floor2Int(t), 0) (uv.h:38-44)
+PGD_INLINE void leaf_rgb(const DevScene &S, const pbrtgpu_texture &tx, const TexPt &q, float rgb[3]) {
+    if (tx.type == PBRTGPU_TEX_UV) {
+        float s, t, dsdx, dtdx, dsdy, dtdy;
+        tex_map(tx, q, &s, &t, &dsdx, &dtdx, &dsdy, &dtdy);
+        rgb[0] = s - (float)(int)floorf(s);
+        rgb[1] = t - (float)(int)floorf(t);
+        rgb[2] = 0.f;
+    } else tex_image<3>(S, tx, q, rgb);
+}
 PGD_INLINE float tex_leaf_float(const DevScene &S, int id, const TexPt &q) {
     const pbrtgpu_texture &tx = (*sa(S.tex, (uint32_t)(id)));
     if (tx.type == PBRTGPU_TEX_CONST) return tx.value;
@@ -2103,7 +2114,7 @@ PGD_INLINE void spec_leaf(const DevScene &S, int id, const TexPt &q, RGBPick *pi
     const pbrtgpu_texture &lf = (*sa(S.tex, (uint32_t)(id)));
     if (lf.type == PBRTGPU_TEX_CONST) { *constOff = lf.spec; pick->k0 = pick->k1 = pick->k2 = -1; pick->a0 = pick->a1 = pick->a2 = 0.f; return; }
     float rgb[3];
-    tex_image<3>(S, lf, q, rgb);
+    leaf_rgb(S, lf, q, rgb);
     *pick = rgb_pick(S, rgb);
     *constOff = -1;
 }
@@ -2132,7 +2143,7 @@ PGD_HEAVY SpecTex tex_spec_prepare(const DevScene &S, int id, const TexPt &q) {
         r.constFirst = firstConst;
     }
     float rgb[3];
-    tex_image<3>(S, (*sa(S.tex, (uint32_t)(img))), q, rgb);
+    leaf_rgb(S, (*sa(S.tex, (uint32_t)(img))), q, rgb);
     r.pick = rgb_pick(S, rgb);
     return r;
 }
@@ -2157,7 +2168,7 @@ PGD_INLINE float4 tex_spec4(const DevScene &S, const SpecTex &t, int q) {
 // MIPMap lookup, RGB 0 for a constant (constant.h:45-47), the product for a scale (scale.h:47-49)
 PGD_INLINE void tex_memory_leaf(const DevScene &S, int id, const TexPt &q, float rgb[3]) {
     const pbrtgpu_texture &tx = (*sa(S.tex, (uint32_t)(id)));
-    if (tx.type == PBRTGPU_TEX_IMAGE) tex_image<3>(S, tx, q, rgb);
+    if (tx.type == PBRTGPU_TEX_IMAGE || tx.type == PBRTGPU_TEX_UV) leaf_rgb(S, tx, q, rgb);   // uv.h:46-51
     else rgb[0] = rgb[1] = rgb[2] = 0.f;
 }
 // Material::NormalMap (material.cpp:82-126) where the map's spectrum (Evaluate, FromRGB of its

@@ -355,15 +355,19 @@ static inline int scene_check(const pbrtgpu_flat_scene *s, std::string *err) {
     auto texOk = [&](int id, int spectral, bool slot) -> bool {
         if (id < 0 || id >= s->n_textures || !s->textures) return false;
         const pbrtgpu_texture &t = s->textures[id];
-        if (t.spectral != spectral || t.type < PBRTGPU_TEX_CONST || t.type > PBRTGPU_TEX_CHECKER) return false;
+        if (t.spectral != spectral || t.type < PBRTGPU_TEX_CONST || t.type > PBRTGPU_TEX_UV) return false;
+        if (t.type == PBRTGPU_TEX_UV && !spectral) return false;   // UVTexture is Texture<Spectrum> only
         if (t.type == PBRTGPU_TEX_CHECKER) {   // two CONST / IMAGE leaves (device.h tex_spec_prepare)
             for (int o : {t.tex1, t.tex2}) {
                 if (o < 0 || o >= s->n_textures || s->textures[o].spectral != spectral) return false;
-                if (s->textures[o].type != PBRTGPU_TEX_CONST && s->textures[o].type != PBRTGPU_TEX_IMAGE) return false;
+                if (s->textures[o].type != PBRTGPU_TEX_CONST && s->textures[o].type != PBRTGPU_TEX_IMAGE &&
+                    s->textures[o].type != PBRTGPU_TEX_UV)
+                    return false;
             }
             if (t.aamode < 0 || t.aamode > 1) return false;
         }
-        if (t.type != PBRTGPU_TEX_IMAGE && t.type != PBRTGPU_TEX_CHECKER && t.mapping != PBRTGPU_MAP_UV) return false;
+        if (t.type != PBRTGPU_TEX_IMAGE && t.type != PBRTGPU_TEX_CHECKER && t.type != PBRTGPU_TEX_UV && t.mapping != PBRTGPU_MAP_UV)
+            return false;
         if (t.mapping < PBRTGPU_MAP_UV || t.mapping > PBRTGPU_MAP_PLANAR) return false;
         if (t.type == PBRTGPU_TEX_SCALE) {
             for (int o : {t.tex1, t.tex2}) {

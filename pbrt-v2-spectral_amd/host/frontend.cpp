@@ -1230,7 +1230,7 @@ private:
             t.spec = EmitSpectrum(f.value);
             return AddTexture(t);
         }
-        if (out->textures[f.tex].type != PBRTGPU_TEX_IMAGE) throw std::runtime_error("checkerboard operands other than constants and image maps are not supported yet");
+        if (out->textures[f.tex].type != PBRTGPU_TEX_IMAGE && out->textures[f.tex].type != PBRTGPU_TEX_UV) throw std::runtime_error("checkerboard operands other than constants and image maps are not supported yet");
         return f.tex;
     }
     // operand of a ScaleTexture: a CONST or IMAGE node
@@ -1275,7 +1275,8 @@ private:
                     // device form: one image leaf times one constant spectrum
                     if (!a.constant && !b.constant) throw std::runtime_error("scale of two non-constant spectrum textures is not supported yet");
                     const SpecTex &img = a.constant ? b : a, &cst = a.constant ? a : b;
-                    if (out->textures[img.tex].type != PBRTGPU_TEX_IMAGE) throw std::runtime_error("nested scale textures are not supported yet");
+                    if (out->textures[img.tex].type != PBRTGPU_TEX_IMAGE && out->textures[img.tex].type != PBRTGPU_TEX_UV)
+                        throw std::runtime_error("nested scale textures are not supported yet");
                     pbrtgpu_texture c = TexNode(PBRTGPU_TEX_CONST, true);
                     c.spec = EmitSpectrum(cst.value);
                     int ci = AddTexture(c);
@@ -1284,6 +1285,11 @@ private:
                     t.constant = false; t.tex = AddTexture(n);
                 }
             } else if (cls == "imagemap") { t.constant = false; t.tex = MakeImageTexture(p, true); }
+            else if (cls == "uv") {   // UVTexture (uv.cpp:37-62): its 2D mapping alone
+                pbrtgpu_texture n = TexNode(PBRTGPU_TEX_UV, true);
+                ParseMapping(p, n);
+                t.constant = false; t.tex = AddTexture(n);
+            }
             else if (cls == "checkerboard") {   // Checkerboard2DTexture<Spectrum> (checkerboard.cpp:71-110)
                 pbrtgpu_texture n = CheckerNode(p, true);
                 n.tex1 = CheckerLeaf(GetSpecTex(p, p, "tex1", spec.Const(1.f)));
