@@ -109,7 +109,8 @@ enum {
  * 3 floats (RGB) per texel for spectrum textures, 1 for float textures).  Lookups follow
  * MIPMap::Lookup (EWA, mipmap.h:278-375, or width-based / noFiltering, :232-259) with the
  * ImageWrap mode, texture coordinates from UVMapping2D (texture.cpp:80-90). */
-enum { PBRTGPU_TEX_CONST = 0, PBRTGPU_TEX_IMAGE = 1, PBRTGPU_TEX_SCALE = 2, PBRTGPU_TEX_CHECKER = 3, PBRTGPU_TEX_UV = 4 };
+enum { PBRTGPU_TEX_CONST = 0, PBRTGPU_TEX_IMAGE = 1, PBRTGPU_TEX_SCALE = 2, PBRTGPU_TEX_CHECKER = 3, PBRTGPU_TEX_UV = 4,
+       PBRTGPU_TEX_MIX = 5 };
 enum { PBRTGPU_WRAP_REPEAT = 0, PBRTGPU_WRAP_BLACK = 1, PBRTGPU_WRAP_CLAMP = 2 };
 typedef struct pbrtgpu_texture {
     int32_t type;          /* PBRTGPU_TEX_* */
@@ -130,6 +131,8 @@ typedef struct pbrtgpu_texture {
                               PLANAR: vs.xyz, vt.xyz (the "v1", "v2" parameters) */
     int32_t aamode;        /* CHECKER (Checkerboard2DTexture over tex1, tex2: CONST / IMAGE leaves, the
                               mapping above): 0 closedform box filter, 1 none (point sampled) */
+    int32_t amount;        /* MIX ((1 - amount) * tex1 + amount * tex2, mix.h:38-43): the amount, a float
+                              CONST / IMAGE texture */
 } pbrtgpu_texture;
 /* IMAGE and CHECKER nodes */
 enum { PBRTGPU_MAP_UV = 0, PBRTGPU_MAP_SPHERICAL = 1, PBRTGPU_MAP_CYLINDRICAL = 2, PBRTGPU_MAP_PLANAR = 3 };

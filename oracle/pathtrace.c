@@ -1480,6 +1480,10 @@ static float tex_float(const Ctx *c, int id, const TexPt *q) {
             if (k < 2) return tex_float(c, k == 0 ? tx->tex1 : tx->tex2, q);
             return (1.f - a2) * tex_float(c, tx->tex1, q) + a2 * tex_float(c, tx->tex2, q);
         }
+        case PBRTGPU_TEX_MIX: {   /* MixTexture::Evaluate (mix.h:38-43) */
+            float amt = tex_float(c, tx->amount, q);
+            return (1.f - amt) * tex_float(c, tx->tex1, q) + amt * tex_float(c, tx->tex2, q);
+        }
         default: return tex_float(c, tx->tex1, q) * tex_float(c, tx->tex2, q);   /* ScaleTexture */
     }
 }
@@ -1490,6 +1494,14 @@ static void tex_spec(const Ctx *c, int id, const TexPt *q, float *out) {
         case PBRTGPU_TEX_CONST: memcpy(out, SPEC(c, tx->spec), sizeof(float) * nb); return;
         case PBRTGPU_TEX_IMAGE: { float rgb[3]; tex_image(c, tx, 3, q, rgb); from_rgb(c, rgb, 0, out); return; }
         case PBRTGPU_TEX_UV: { float rgb[3]; uv_rgb(tx, q, rgb); from_rgb(c, rgb, 0, out); return; }
+        case PBRTGPU_TEX_MIX: {
+            float a[MAXB], b[MAXB];
+            tex_spec(c, tx->tex1, q, a);
+            tex_spec(c, tx->tex2, q, b);
+            float amt = tex_float(c, tx->amount, q);
+            for (int i = 0; i < nb; ++i) out[i] = (a[i] * (1.f - amt)) + (b[i] * amt);
+            return;
+        }
         case PBRTGPU_TEX_CHECKER: {
             float a2 = 0.f;
             int k = checker_pick(tx, q, &a2);

@@ -99,6 +99,7 @@ static inline void spec_out(const Spectrum &L, float *c) { L.GetOrigC(c); }
 #include "textures/imagemap.h"
 #include "textures/checkerboard.h"
 #include "textures/uv.h"
+#include "textures/mix.h"
 #include "textures/scale.h"
 
 #include <map>
@@ -430,6 +431,7 @@ static Reference<Texture<float> > MakeFloatTex(const string &n, const Transform 
     if (n == "scale") return CreateScaleFloatTexture(x, tp);
     if (n == "imagemap") return CreateImageFloatTexture(x, tp);
     if (n == "checkerboard") return CreateCheckerboardFloatTexture(x, tp);
+    if (n == "mix") return CreateMixFloatTexture(x, tp);
     fprintf(stderr, "harness: float texture %s unsupported\n", n.c_str()); exit(2);
 }
 static Reference<Texture<Spectrum> > MakeSpecTex(const string &n, const Transform &x, const TextureParams &tp) {
@@ -438,6 +440,7 @@ static Reference<Texture<Spectrum> > MakeSpecTex(const string &n, const Transfor
     if (n == "imagemap") return CreateImageSpectrumTexture(x, tp);
     if (n == "checkerboard") return CreateCheckerboardSpectrumTexture(x, tp);
     if (n == "uv") return CreateUVSpectrumTexture(x, tp);
+    if (n == "mix") return CreateMixSpectrumTexture(x, tp);
     fprintf(stderr, "harness: spectrum texture %s unsupported\n", n.c_str()); exit(2);
 }
 void pbrtTexture(const string &name, const string &type, const string &texname, const ParamSet &params) {

@@ -2091,18 +2091,32 @@ PGD_INLINE int checker_pick(const pbrtgpu_texture &tx, const TexPt &q, float *ar
     *area2 = a;
     return 2;
 }
-// Texture<float>: CONST, IMAGE, ScaleTexture or Checkerboard2DTexture of two leaves (the front end
-// guarantees the depth)
+// Texture<float>: CONST, IMAGE, ScaleTexture, Checkerboard2DTexture or MixTexture of leaves (the
+// front end guarantees the depth); the leaves are looked up in one loop (one copy of the MIPMap
+// lookup code per call site)
 PGD_HEAVY float tex_float(const DevScene &S, int id, const TexPt &q) {
     const pbrtgpu_texture &tx = (*sa(S.tex, (uint32_t)(id)));
+    int l0 = id, l1 = -1, l2 = -1;
+    float a2 = 0.f;
+    int kind = 0;   // 0 the leaf, 1 product, 2 checker blend, 3 mix
     if (tx.type == PBRTGPU_TEX_CHECKER) {
-        float a2 = 0.f;
         const int k = checker_pick(tx, q, &a2);
-        if (k < 2) return tex_leaf_float(S, k == 0 ? tx.tex1 : tx.tex2, q);
-        return (1.f - a2) * tex_leaf_float(S, tx.tex1, q) + a2 * tex_leaf_float(S, tx.tex2, q);
+        if (k < 2) l0 = k == 0 ? tx.tex1 : tx.tex2;
+        else { l0 = tx.tex1; l1 = tx.tex2; kind = 2; }
+    } else if (tx.type == PBRTGPU_TEX_MIX) { l0 = tx.amount; l1 = tx.tex1; l2 = tx.tex2; kind = 3; }
+    else if (tx.type == PBRTGPU_TEX_SCALE) { l0 = tx.tex1; l1 = tx.tex2; kind = 1; }
+    float v0 = 0.f, v1 = 0.f, v2 = 0.f;
+#pragma unroll 1
+    for (int l = 0; l < 3; ++l) {
+        const int lid = l == 0 ? l0 : (l == 1 ? l1 : l2);
+        if (lid < 0) break;
+        const float v = tex_leaf_float(S, lid, q);
+        if (l == 0) v0 = v; else if (l == 1) v1 = v; else v2 = v;
     }
-    if (tx.type != PBRTGPU_TEX_SCALE) return tex_leaf_float(S, id, q);
-    return tex_leaf_float(S, tx.tex1, q) * tex_leaf_float(S, tx.tex2, q);
+    if (kind == 1) return v0 * v1;                            // ScaleTexture: tex1 * tex2
+    if (kind == 2) return (1.f - a2) * v0 + a2 * v1;           // checkerboard.h:120-121
+    if (kind == 3) return (1.f - v0) * v1 + v0 * v2;           // mix.h:38-43 (v0 = amount)
+    return v0;
 }
 // Texture<Spectrum> in device form: FromRGB(image lookup) [times a constant spectrum, in the
 // ScaleTexture operand order]; SpecTex carries the per-hit part, spec4 evaluates a band quad
@@ -2121,30 +2135,37 @@ PGD_INLINE void spec_leaf(const DevScene &S, int id, const TexPt &q, RGBPick *pi
 PGD_HEAVY SpecTex tex_spec_prepare(const DevScene &S, int id, const TexPt &q) {
     SpecTex r;
     r.constOff = -1; r.constFirst = false; r.constOnly = false; r.blend = false; r.constOff2 = -1; r.w1 = r.w2 = 0.f;
-    int img = id;
     const pbrtgpu_texture &tx = (*sa(S.tex, (uint32_t)(id)));
-    if (tx.type == PBRTGPU_TEX_CHECKER) {
+    // the leaves to look up (one copy of the lookup code below): leaf[0], and leaf[1] for a blend
+    int leaf0 = id, leaf1 = -1;
+    const bool two = tx.type == PBRTGPU_TEX_MIX || tx.type == PBRTGPU_TEX_CHECKER;   // leaves are CONST / IMAGE / UV
+    if (tx.type == PBRTGPU_TEX_MIX) {   // MixTexture::Evaluate: always the blend (mix.h:38-43)
+        const float amt = tex_leaf_float(S, tx.amount, q);
+        leaf0 = tx.tex1; leaf1 = tx.tex2;
+        r.blend = true; r.w1 = 1.f - amt; r.w2 = amt;
+    } else if (tx.type == PBRTGPU_TEX_CHECKER) {
         float a2 = 0.f;
         const int k = checker_pick(tx, q, &a2);
-        spec_leaf(S, k == 1 ? tx.tex2 : tx.tex1, q, &r.pick, &r.constOff);
-        r.constOnly = r.constOff >= 0;
-        if (k == 2) {
-            r.blend = true;
-            spec_leaf(S, tx.tex2, q, &r.pick2, &r.constOff2);
-            r.w1 = 1.f - a2;
-            r.w2 = a2;
-        }
-        return r;
-    }
-    if (tx.type == PBRTGPU_TEX_SCALE) {
+        leaf0 = k == 1 ? tx.tex2 : tx.tex1;
+        if (k == 2) { leaf1 = tx.tex2; r.blend = true; r.w1 = 1.f - a2; r.w2 = a2; }
+    } else if (tx.type == PBRTGPU_TEX_SCALE) {   // one image / uv leaf times a constant spectrum
         const bool firstConst = (*sa(S.tex, (uint32_t)(tx.tex1))).type == PBRTGPU_TEX_CONST;
-        img = firstConst ? tx.tex2 : tx.tex1;
+        leaf0 = firstConst ? tx.tex2 : tx.tex1;
         r.constOff = (*sa(S.tex, (uint32_t)(firstConst ? tx.tex1 : tx.tex2))).spec;
         r.constFirst = firstConst;
     }
-    float rgb[3];
-    leaf_rgb(S, (*sa(S.tex, (uint32_t)(img))), q, rgb);
-    r.pick = rgb_pick(S, rgb);
+#pragma unroll 1
+    for (int l = 0; l < 2; ++l) {
+        const int lid = l == 0 ? leaf0 : leaf1;
+        if (lid < 0) break;
+        RGBPick p;
+        int co;
+        spec_leaf(S, lid, q, &p, &co);
+        if (l == 0) {
+            r.pick = p;
+            if (two) { r.constOff = co; r.constOnly = co >= 0; }
+        } else { r.pick2 = p; r.constOff2 = co; }
+    }
     return r;
 }
 PGD_INLINE float4 tex_spec4(const DevScene &S, const SpecTex &t, int q) {
@@ -2289,13 +2310,19 @@ PGD_HEAVY void get_bsdf(const DevScene &S, const Isect &is, const float diff[10]
     } else {
         float du = .5f * (fabsf(tq.dudx) + fabsf(tq.dudy));
         if (du == 0.f) du = .01f;
-        TexPt qu = tq; qu.u = dgs.u + du; qu.p = vadd(dgs.p, vmul(dgs.dpdu, du));   // dgEval (material.cpp:49-51)
-        float uDisplace = tex_float(S, mt.bump_tex, qu);
         float dv = .5f * (fabsf(tq.dvdx) + fabsf(tq.dvdy));
         if (dv == 0.f) dv = .01f;
-        TexPt qv = tq; qv.v = dgs.v + dv; qv.p = vadd(dgs.p, vmul(dgs.dpdv, dv));
-        float vDisplace = tex_float(S, mt.bump_tex, qv);
-        float displace = tex_float(S, mt.bump_tex, tq);
+        // the u-shifted, v-shifted and unshifted evaluations (dgEval, material.cpp:47-62), in one
+        // loop: one copy of the texture code
+        float uDisplace = 0.f, vDisplace = 0.f, displace = 0.f;
+#pragma unroll 1
+        for (int l = 0; l < 3; ++l) {
+            TexPt qe = tq;
+            if (l == 0) { qe.u = dgs.u + du; qe.p = vadd(dgs.p, vmul(dgs.dpdu, du)); }
+            else if (l == 1) { qe.v = dgs.v + dv; qe.p = vadd(dgs.p, vmul(dgs.dpdv, dv)); }
+            const float dsp = tex_float(S, mt.bump_tex, qe);
+            if (l == 0) uDisplace = dsp; else if (l == 1) vDisplace = dsp; else displace = dsp;
+        }
         bdpdu = vadd(vadd(dgs.dpdu, vmul(dgs.nn, (uDisplace - displace) / du)), vmul(dgs.dndu, displace));
         bdpdv = vadd(vadd(dgs.dpdv, vmul(dgs.nn, (vDisplace - displace) / dv)), vmul(dgs.dndv, displace));
     }

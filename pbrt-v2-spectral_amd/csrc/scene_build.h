@@ -355,7 +355,18 @@ static inline int scene_check(const pbrtgpu_flat_scene *s, std::string *err) {
     auto texOk = [&](int id, int spectral, bool slot) -> bool {
         if (id < 0 || id >= s->n_textures || !s->textures) return false;
         const pbrtgpu_texture &t = s->textures[id];
-        if (t.spectral != spectral || t.type < PBRTGPU_TEX_CONST || t.type > PBRTGPU_TEX_UV) return false;
+        if (t.spectral != spectral || t.type < PBRTGPU_TEX_CONST || t.type > PBRTGPU_TEX_MIX) return false;
+        if (t.type == PBRTGPU_TEX_MIX) {   // two CONST / IMAGE / UV leaves, a CONST / IMAGE float amount
+            for (int o : {t.tex1, t.tex2}) {
+                if (o < 0 || o >= s->n_textures || s->textures[o].spectral != spectral) return false;
+                const int ty = s->textures[o].type;
+                if (ty != PBRTGPU_TEX_CONST && ty != PBRTGPU_TEX_IMAGE && ty != PBRTGPU_TEX_UV) return false;
+            }
+            const int a = t.amount;
+            if (a < 0 || a >= s->n_textures || s->textures[a].spectral ||
+                (s->textures[a].type != PBRTGPU_TEX_CONST && s->textures[a].type != PBRTGPU_TEX_IMAGE))
+                return false;
+        }
         if (t.type == PBRTGPU_TEX_UV && !spectral) return false;   // UVTexture is Texture<Spectrum> only
         if (t.type == PBRTGPU_TEX_CHECKER) {   // two CONST / IMAGE leaves (device.h tex_spec_prepare)
             for (int o : {t.tex1, t.tex2}) {
@@ -372,7 +383,9 @@ static inline int scene_check(const pbrtgpu_flat_scene *s, std::string *err) {
         if (t.type == PBRTGPU_TEX_SCALE) {
             for (int o : {t.tex1, t.tex2}) {
                 if (o < 0 || o >= s->n_textures || s->textures[o].spectral != spectral) return false;
-                if (s->textures[o].type == PBRTGPU_TEX_SCALE || s->textures[o].type == PBRTGPU_TEX_CHECKER) return false;
+                if (s->textures[o].type == PBRTGPU_TEX_SCALE || s->textures[o].type == PBRTGPU_TEX_CHECKER ||
+                    s->textures[o].type == PBRTGPU_TEX_MIX)
+                    return false;
             }
             if (spectral && (s->textures[t.tex1].type == PBRTGPU_TEX_CONST) == (s->textures[t.tex2].type == PBRTGPU_TEX_CONST))
                 return false;
@@ -409,7 +422,8 @@ static inline int scene_check(const pbrtgpu_flat_scene *s, std::string *err) {
                                    m.type == PBRTGPU_MAT_MEASURED_HALFANGLE || m.type == PBRTGPU_MAT_MIRROR))
                 SB_FAIL(PBRTGPU_E_INVALID, "material float texture");
         if (m.bump_tex >= 0 && !texOk(m.bump_tex, 0, false)) SB_FAIL(PBRTGPU_E_INVALID, "bump texture");
-        if (m.normal_tex >= 0 && !texOk(m.normal_tex, 1, false)) SB_FAIL(PBRTGPU_E_INVALID, "normal map texture");
+        if (m.normal_tex >= 0 && (!texOk(m.normal_tex, 1, false) || s->textures[m.normal_tex].type == PBRTGPU_TEX_MIX))
+            SB_FAIL(PBRTGPU_E_INVALID, "normal map texture");
         if (m.type == PBRTGPU_MAT_MEASURED_HALFANGLE && m.aux >= 0 &&
             (!s->merl || s->n_merl_floats < 0 || (int64_t)m.aux * 3 + 3 * 90 * 90 * 180 > (int64_t)s->n_merl_floats))
             SB_FAIL(PBRTGPU_E_INVALID, "RegularHalfangle table out of range");

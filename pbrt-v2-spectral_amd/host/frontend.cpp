@@ -1214,7 +1214,8 @@ private:
         n.aamode = aa == "none" ? 1 : 0;
         return n;
     }
-    // operands of a checkerboard: constants become CONST nodes, textures must be image maps
+    // operands of a checkerboard or mix texture (and a mix's amount): constants become CONST nodes,
+    // textures must be image maps (or uv textures)
     int CheckerLeaf(const FloatTex &f) {
         if (f.constant) {
             pbrtgpu_texture t = TexNode(PBRTGPU_TEX_CONST, false);
@@ -1257,6 +1258,13 @@ private:
                     t.constant = false; t.tex = AddTexture(n);
                 }
             } else if (cls == "imagemap") { t.constant = false; t.tex = MakeImageTexture(p, false); }
+            else if (cls == "mix") {   // MixTexture<float> (mix.cpp:30-36)
+                pbrtgpu_texture n = TexNode(PBRTGPU_TEX_MIX, false);
+                n.tex1 = CheckerLeaf(GetFloatTex(p, p, "tex1", 0.f));
+                n.tex2 = CheckerLeaf(GetFloatTex(p, p, "tex2", 1.f));
+                n.amount = CheckerLeaf(GetFloatTex(p, p, "amount", .5f));
+                t.constant = false; t.tex = AddTexture(n);
+            }
             else if (cls == "checkerboard") {   // Checkerboard2DTexture<float> (checkerboard.cpp:29-67)
                 pbrtgpu_texture n = CheckerNode(p, false);
                 n.tex1 = CheckerLeaf(GetFloatTex(p, p, "tex1", 1.f));
@@ -1288,6 +1296,13 @@ private:
             else if (cls == "uv") {   // UVTexture (uv.cpp:37-62): its 2D mapping alone
                 pbrtgpu_texture n = TexNode(PBRTGPU_TEX_UV, true);
                 ParseMapping(p, n);
+                t.constant = false; t.tex = AddTexture(n);
+            }
+            else if (cls == "mix") {   // MixTexture<Spectrum> (mix.cpp:40-46)
+                pbrtgpu_texture n = TexNode(PBRTGPU_TEX_MIX, true);
+                n.tex1 = CheckerLeaf(GetSpecTex(p, p, "tex1", spec.Const(0.f)));
+                n.tex2 = CheckerLeaf(GetSpecTex(p, p, "tex2", spec.Const(1.f)));
+                n.amount = CheckerLeaf(GetFloatTex(p, p, "amount", .5f));
                 t.constant = false; t.tex = AddTexture(n);
             }
             else if (cls == "checkerboard") {   // Checkerboard2DTexture<Spectrum> (checkerboard.cpp:71-110)
