@@ -110,7 +110,8 @@ enum {
  * MIPMap::Lookup (EWA, mipmap.h:278-375, or width-based / noFiltering, :232-259) with the
  * ImageWrap mode, texture coordinates from UVMapping2D (texture.cpp:80-90). */
 enum { PBRTGPU_TEX_CONST = 0, PBRTGPU_TEX_IMAGE = 1, PBRTGPU_TEX_SCALE = 2, PBRTGPU_TEX_CHECKER = 3, PBRTGPU_TEX_UV = 4,
-       PBRTGPU_TEX_MIX = 5 };
+       PBRTGPU_TEX_MIX = 5, PBRTGPU_TEX_BILERP = 6 /* BilerpTexture: spectral v00, v01, v10, v11 at spec, spec + 1
+       spectrum, ...; float at texels[texel_off .. + 3] */ };
 enum { PBRTGPU_WRAP_REPEAT = 0, PBRTGPU_WRAP_BLACK = 1, PBRTGPU_WRAP_CLAMP = 2 };
 typedef struct pbrtgpu_texture {
     int32_t type;          /* PBRTGPU_TEX_* */

@@ -1480,6 +1480,12 @@ static float tex_float(const Ctx *c, int id, const TexPt *q) {
             if (k < 2) return tex_float(c, k == 0 ? tx->tex1 : tx->tex2, q);
             return (1.f - a2) * tex_float(c, tx->tex1, q) + a2 * tex_float(c, tx->tex2, q);
         }
+        case PBRTGPU_TEX_BILERP: {   /* BilerpTexture::Evaluate (bilerp.h:38-44) */
+            float s, t, dsdx, dtdx, dsdy, dtdy;
+            tex_map(tx, q, &s, &t, &dsdx, &dtdx, &dsdy, &dtdy);
+            const float *v = &c->s->texels[tx->texel_off];
+            return (1 - s) * (1 - t) * v[0] + (1 - s) * (t) * v[1] + (s) * (1 - t) * v[2] + (s) * (t) * v[3];
+        }
         case PBRTGPU_TEX_MIX: {   /* MixTexture::Evaluate (mix.h:38-43) */
             float amt = tex_float(c, tx->amount, q);
             return (1.f - amt) * tex_float(c, tx->tex1, q) + amt * tex_float(c, tx->tex2, q);
@@ -1494,6 +1500,15 @@ static void tex_spec(const Ctx *c, int id, const TexPt *q, float *out) {
         case PBRTGPU_TEX_CONST: memcpy(out, SPEC(c, tx->spec), sizeof(float) * nb); return;
         case PBRTGPU_TEX_IMAGE: { float rgb[3]; tex_image(c, tx, 3, q, rgb); from_rgb(c, rgb, 0, out); return; }
         case PBRTGPU_TEX_UV: { float rgb[3]; uv_rgb(tx, q, rgb); from_rgb(c, rgb, 0, out); return; }
+        case PBRTGPU_TEX_BILERP: {
+            float s, t, dsdx, dtdx, dsdy, dtdy;
+            tex_map(tx, q, &s, &t, &dsdx, &dtdx, &dsdy, &dtdy);
+            const float w00 = (1 - s) * (1 - t), w01 = (1 - s) * (t), w10 = (s) * (1 - t), w11 = (s) * (t);
+            const float *v00 = SPEC(c, tx->spec), *v01 = SPEC(c, tx->spec + nb), *v10 = SPEC(c, tx->spec + 2 * nb),
+                        *v11 = SPEC(c, tx->spec + 3 * nb);
+            for (int i = 0; i < nb; ++i) out[i] = ((v00[i] * w00 + v01[i] * w01) + v10[i] * w10) + v11[i] * w11;
+            return;
+        }
         case PBRTGPU_TEX_MIX: {
             float a[MAXB], b[MAXB];
             tex_spec(c, tx->tex1, q, a);

@@ -100,6 +100,7 @@ static inline void spec_out(const Spectrum &L, float *c) { L.GetOrigC(c); }
 #include "textures/checkerboard.h"
 #include "textures/uv.h"
 #include "textures/mix.h"
+#include "textures/bilerp.h"
 #include "textures/scale.h"
 
 #include <map>
@@ -432,6 +433,7 @@ static Reference<Texture<float> > MakeFloatTex(const string &n, const Transform 
     if (n == "imagemap") return CreateImageFloatTexture(x, tp);
     if (n == "checkerboard") return CreateCheckerboardFloatTexture(x, tp);
     if (n == "mix") return CreateMixFloatTexture(x, tp);
+    if (n == "bilerp") return CreateBilerpFloatTexture(x, tp);
     fprintf(stderr, "harness: float texture %s unsupported\n", n.c_str()); exit(2);
 }
 static Reference<Texture<Spectrum> > MakeSpecTex(const string &n, const Transform &x, const TextureParams &tp) {
@@ -441,6 +443,7 @@ static Reference<Texture<Spectrum> > MakeSpecTex(const string &n, const Transfor
     if (n == "checkerboard") return CreateCheckerboardSpectrumTexture(x, tp);
     if (n == "uv") return CreateUVSpectrumTexture(x, tp);
     if (n == "mix") return CreateMixSpectrumTexture(x, tp);
+    if (n == "bilerp") return CreateBilerpSpectrumTexture(x, tp);
     fprintf(stderr, "harness: spectrum texture %s unsupported\n", n.c_str()); exit(2);
 }
 void pbrtTexture(const string &name, const string &type, const string &texname, const ParamSet &params) {

@@ -2094,8 +2094,20 @@ PGD_INLINE int checker_pick(const pbrtgpu_texture &tx, const TexPt &q, float *ar
 // Texture<float>: CONST, IMAGE, ScaleTexture, Checkerboard2DTexture or MixTexture of leaves (the
 // front end guarantees the depth); the leaves are looked up in one loop (one copy of the MIPMap
 // lookup code per call site)
+// BilerpTexture's weights (bilerp.h:38-44): (1-s)(1-t), (1-s)t, s(1-t), st
+PGD_INLINE void bilerp_w(const pbrtgpu_texture &tx, const TexPt &q, float w[4]) {
+    float s, t, dsdx, dtdx, dsdy, dtdy;
+    tex_map(tx, q, &s, &t, &dsdx, &dtdx, &dsdy, &dtdy);
+    w[0] = (1.f - s) * (1.f - t); w[1] = (1.f - s) * t; w[2] = s * (1.f - t); w[3] = s * t;
+}
 PGD_HEAVY float tex_float(const DevScene &S, int id, const TexPt &q) {
     const pbrtgpu_texture &tx = (*sa(S.tex, (uint32_t)(id)));
+    if (tx.type == PBRTGPU_TEX_BILERP) {
+        float w[4];
+        bilerp_w(tx, q, w);
+        const float *v = sa(S.texels, (uint32_t)tx.texel_off);
+        return ((w[0] * v[0] + w[1] * v[1]) + w[2] * v[2]) + w[3] * v[3];
+    }
     int l0 = id, l1 = -1, l2 = -1;
     float a2 = 0.f;
     int kind = 0;   // 0 the leaf, 1 product, 2 checker blend, 3 mix
@@ -2122,7 +2134,8 @@ PGD_HEAVY float tex_float(const DevScene &S, int id, const TexPt &q) {
 // ScaleTexture operand order]; SpecTex carries the per-hit part, spec4 evaluates a band quad
 // A Checkerboard2DTexture becomes one of its leaves (CONST: constOnly) or a blend of both: the
 // second leaf in pick2 / constOff2 and the weights w1 = 1 - area2, w2 = area2 (blend)
-struct SpecTex { RGBPick pick; int constOff; bool constFirst, constOnly, blend; RGBPick pick2; int constOff2; float w1, w2; };
+// (a BilerpTexture: its four spectra from constOff at one spectrum's stride, weights in w1, w2, w3, w4)
+struct SpecTex { RGBPick pick; int constOff; bool constFirst, constOnly, blend, bilerp; RGBPick pick2; int constOff2; float w1, w2, w3, w4; };
 // one leaf of a checkerboard (CONST or IMAGE) into pick / constOff (constant: constOff >= 0)
 PGD_INLINE void spec_leaf(const DevScene &S, int id, const TexPt &q, RGBPick *pick, int *constOff) {
     const pbrtgpu_texture &lf = (*sa(S.tex, (uint32_t)(id)));
@@ -2134,8 +2147,15 @@ PGD_INLINE void spec_leaf(const DevScene &S, int id, const TexPt &q, RGBPick *pi
 }
 PGD_HEAVY SpecTex tex_spec_prepare(const DevScene &S, int id, const TexPt &q) {
     SpecTex r;
-    r.constOff = -1; r.constFirst = false; r.constOnly = false; r.blend = false; r.constOff2 = -1; r.w1 = r.w2 = 0.f;
+    r.constOff = -1; r.constFirst = false; r.constOnly = false; r.blend = false; r.bilerp = false; r.constOff2 = -1;
+    r.w1 = r.w2 = r.w3 = r.w4 = 0.f;
     const pbrtgpu_texture &tx = (*sa(S.tex, (uint32_t)(id)));
+    if (tx.type == PBRTGPU_TEX_BILERP) {
+        float w[4];
+        bilerp_w(tx, q, w);
+        r.bilerp = true; r.constOff = tx.spec; r.w1 = w[0]; r.w2 = w[1]; r.w3 = w[2]; r.w4 = w[3];
+        return r;
+    }
     // the leaves to look up (one copy of the lookup code below): leaf[0], and leaf[1] for a blend
     int leaf0 = id, leaf1 = -1;
     const bool two = tx.type == PBRTGPU_TEX_MIX || tx.type == PBRTGPU_TEX_CHECKER;   // leaves are CONST / IMAGE / UV
@@ -2169,6 +2189,17 @@ PGD_HEAVY SpecTex tex_spec_prepare(const DevScene &S, int id, const TexPt &q) {
     return r;
 }
 PGD_INLINE float4 tex_spec4(const DevScene &S, const SpecTex &t, int q) {
+    if (t.bilerp) {   // ((v00 w00 + v01 w01) + v10 w10) + v11 w11 per band (Spectrum * float: c * w)
+        const uint32_t st = (uint32_t)S.nbp;
+        const float4 a = *reinterpret_cast<const float4 *>(sa(S.spectra, (uint32_t)(t.constOff + 4 * q)));
+        const float4 b = *reinterpret_cast<const float4 *>(sa(S.spectra, (uint32_t)(t.constOff + st + 4 * q)));
+        const float4 c = *reinterpret_cast<const float4 *>(sa(S.spectra, (uint32_t)(t.constOff + 2 * st + 4 * q)));
+        const float4 d = *reinterpret_cast<const float4 *>(sa(S.spectra, (uint32_t)(t.constOff + 3 * st + 4 * q)));
+        return make_float4(((a.x * t.w1 + b.x * t.w2) + c.x * t.w3) + d.x * t.w4,
+                           ((a.y * t.w1 + b.y * t.w2) + c.y * t.w3) + d.y * t.w4,
+                           ((a.z * t.w1 + b.z * t.w2) + c.z * t.w3) + d.z * t.w4,
+                           ((a.w * t.w1 + b.w * t.w2) + c.w * t.w3) + d.w * t.w4);
+    }
     if (t.constOnly || t.blend) {   // a checkerboard: leaf 1 [blended with leaf 2]
         const float4 a = t.constOnly ? *reinterpret_cast<const float4 *>(sa(S.spectra, (uint32_t)(t.constOff + 4 * q)))
                                      : from_rgb4(S, t.pick, false, q);

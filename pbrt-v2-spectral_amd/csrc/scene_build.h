@@ -355,7 +355,12 @@ static inline int scene_check(const pbrtgpu_flat_scene *s, std::string *err) {
     auto texOk = [&](int id, int spectral, bool slot) -> bool {
         if (id < 0 || id >= s->n_textures || !s->textures) return false;
         const pbrtgpu_texture &t = s->textures[id];
-        if (t.spectral != spectral || t.type < PBRTGPU_TEX_CONST || t.type > PBRTGPU_TEX_MIX) return false;
+        if (t.spectral != spectral || t.type < PBRTGPU_TEX_CONST || t.type > PBRTGPU_TEX_BILERP) return false;
+        if (t.type == PBRTGPU_TEX_BILERP) {   // its four values: spectra in the pool / floats in texels[]
+            if (spectral ? (t.spec < 0 || (int64_t)t.spec + 4LL * s->n_bands > (int64_t)s->n_spectra_floats)
+                         : (t.texel_off < 0 || !s->texels || (int64_t)t.texel_off + 4 > (int64_t)s->n_texel_floats))
+                return false;
+        }
         if (t.type == PBRTGPU_TEX_MIX) {   // two CONST / IMAGE / UV leaves, a CONST / IMAGE float amount
             for (int o : {t.tex1, t.tex2}) {
                 if (o < 0 || o >= s->n_textures || s->textures[o].spectral != spectral) return false;
@@ -377,7 +382,8 @@ static inline int scene_check(const pbrtgpu_flat_scene *s, std::string *err) {
             }
             if (t.aamode < 0 || t.aamode > 1) return false;
         }
-        if (t.type != PBRTGPU_TEX_IMAGE && t.type != PBRTGPU_TEX_CHECKER && t.type != PBRTGPU_TEX_UV && t.mapping != PBRTGPU_MAP_UV)
+        if (t.type != PBRTGPU_TEX_IMAGE && t.type != PBRTGPU_TEX_CHECKER && t.type != PBRTGPU_TEX_UV &&
+            t.type != PBRTGPU_TEX_BILERP && t.mapping != PBRTGPU_MAP_UV)
             return false;
         if (t.mapping < PBRTGPU_MAP_UV || t.mapping > PBRTGPU_MAP_PLANAR) return false;
         if (t.type == PBRTGPU_TEX_SCALE) {
@@ -610,7 +616,7 @@ static int scene_build(const pbrtgpu_flat_scene *s, int topNodes, DevScene &S, i
     }
     std::vector<pbrtgpu_texture> texs(s->textures, s->textures + std::max(0, s->n_textures));
     for (auto &t : texs)
-        if (t.type == PBRTGPU_TEX_CONST && t.spectral && !remap(t.spec, &t.spec))
+        if ((t.type == PBRTGPU_TEX_CONST || t.type == PBRTGPU_TEX_BILERP) && t.spectral && !remap(t.spec, &t.spec))
             SB_FAIL(PBRTGPU_E_INVALID, "texture spectrum offset");
     // FromRGB basis, each of the 14 spectra padded to whole quads
     std::vector<float> basis((size_t)14 * nbp, 0.f);

@@ -1258,6 +1258,14 @@ private:
                     t.constant = false; t.tex = AddTexture(n);
                 }
             } else if (cls == "imagemap") { t.constant = false; t.tex = MakeImageTexture(p, false); }
+            else if (cls == "bilerp") {   // BilerpTexture<float> (bilerp.cpp:30-55): v00 .. v11 in texels[]
+                pbrtgpu_texture n = TexNode(PBRTGPU_TEX_BILERP, false);
+                ParseMapping(p, n);
+                n.texel_off = (int)out->texels.size();
+                for (const char *k : {"v00", "v01", "v10", "v11"})
+                    out->texels.push_back(GetFloat(p, p, k, (k[2] == '1') ? 1.f : 0.f));
+                t.constant = false; t.tex = AddTexture(n);
+            }
             else if (cls == "mix") {   // MixTexture<float> (mix.cpp:30-36)
                 pbrtgpu_texture n = TexNode(PBRTGPU_TEX_MIX, false);
                 n.tex1 = CheckerLeaf(GetFloatTex(p, p, "tex1", 0.f));
@@ -1296,6 +1304,16 @@ private:
             else if (cls == "uv") {   // UVTexture (uv.cpp:37-62): its 2D mapping alone
                 pbrtgpu_texture n = TexNode(PBRTGPU_TEX_UV, true);
                 ParseMapping(p, n);
+                t.constant = false; t.tex = AddTexture(n);
+            }
+            else if (cls == "bilerp") {   // BilerpTexture<Spectrum> (bilerp.cpp:59-84): four consecutive spectra
+                pbrtgpu_texture n = TexNode(PBRTGPU_TEX_BILERP, true);
+                ParseMapping(p, n);
+                n.spec = -1;
+                for (const char *k : {"v00", "v01", "v10", "v11"}) {
+                    const int o = EmitSpectrum(GetSpec(p, p, k, spec.Const((k[2] == '1') ? 1.f : 0.f)));
+                    if (n.spec < 0) n.spec = o;
+                }
                 t.constant = false; t.tex = AddTexture(n);
             }
             else if (cls == "mix") {   // MixTexture<Spectrum> (mix.cpp:40-46)
