@@ -111,7 +111,10 @@ enum {
  * ImageWrap mode, texture coordinates from UVMapping2D (texture.cpp:80-90). */
 enum { PBRTGPU_TEX_CONST = 0, PBRTGPU_TEX_IMAGE = 1, PBRTGPU_TEX_SCALE = 2, PBRTGPU_TEX_CHECKER = 3, PBRTGPU_TEX_UV = 4,
        PBRTGPU_TEX_MIX = 5, PBRTGPU_TEX_BILERP = 6 /* BilerpTexture: spectral v00, v01, v10, v11 at spec, spec + 1
-       spectrum, ...; float at texels[texel_off .. + 3] */ };
+       spectrum, ...; float at texels[texel_off .. + 3] */,
+       /* float noise textures over IdentityMapping3D(tex2world) (map[16] = tex2world.m): FBmTexture,
+          WrinkledTexture (octaves in levels, roughness / omega in value), WindyTexture */
+       PBRTGPU_TEX_FBM = 7, PBRTGPU_TEX_WRINKLED = 8, PBRTGPU_TEX_WINDY = 9 };
 enum { PBRTGPU_WRAP_REPEAT = 0, PBRTGPU_WRAP_BLACK = 1, PBRTGPU_WRAP_CLAMP = 2 };
 typedef struct pbrtgpu_texture {
     int32_t type;          /* PBRTGPU_TEX_* */

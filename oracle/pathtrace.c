@@ -1443,6 +1443,67 @@ static void tex_image(const Ctx *c, const pbrtgpu_texture *tx, int nc, const Tex
     tex_map(tx, q, &s, &t, &dsdx, &dtdx, &dsdy, &dtdy);
     mip_lookup(c, tx, nc, s, t, dsdx, dtdx, dsdy, dtdy, out);
 }
+/* Perlin noise (texture.cpp:163-250): NoisePerm, Grad, NoiseWeight, Noise, FBm, Turbulence */
+static const int kNoisePerm[512] = {
+#include "pbrt_noise_perm.inc"
+};
+static float noise_grad(int x, int y, int z, float dx, float dy, float dz) {
+    int h = kNoisePerm[kNoisePerm[kNoisePerm[x] + y] + z];
+    h &= 15;
+    float u = h < 8 || h == 12 || h == 13 ? dx : dy;
+    float v = h < 4 || h == 12 || h == 13 ? dy : dz;
+    return ((h & 1) ? -u : u) + ((h & 2) ? -v : v);
+}
+static float noise_weight(float t) { float t3 = t * t * t; float t4 = t3 * t; return 6.f * t4 * t - 15.f * t4 + 10.f * t3; }
+static float noise3(float x, float y, float z) {
+    int ix = (int)floorf(x), iy = (int)floorf(y), iz = (int)floorf(z);
+    float dx = x - ix, dy = y - iy, dz = z - iz;
+    ix &= 255; iy &= 255; iz &= 255;
+    float w000 = noise_grad(ix, iy, iz, dx, dy, dz);
+    float w100 = noise_grad(ix + 1, iy, iz, dx - 1, dy, dz);
+    float w010 = noise_grad(ix, iy + 1, iz, dx, dy - 1, dz);
+    float w110 = noise_grad(ix + 1, iy + 1, iz, dx - 1, dy - 1, dz);
+    float w001 = noise_grad(ix, iy, iz + 1, dx, dy, dz - 1);
+    float w101 = noise_grad(ix + 1, iy, iz + 1, dx - 1, dy, dz - 1);
+    float w011 = noise_grad(ix, iy + 1, iz + 1, dx, dy - 1, dz - 1);
+    float w111 = noise_grad(ix + 1, iy + 1, iz + 1, dx - 1, dy - 1, dz - 1);
+    float wx = noise_weight(dx), wy = noise_weight(dy), wz = noise_weight(dz);
+    float x00 = lerpf(wx, w000, w100), x10 = lerpf(wx, w010, w110);
+    float x01 = lerpf(wx, w001, w101), x11 = lerpf(wx, w011, w111);
+    float y0 = lerpf(wy, x00, x10), y1 = lerpf(wy, x01, x11);
+    return lerpf(wz, y0, y1);
+}
+static float smoothstep_(float a, float b, float value) {
+    float v = clampf((value - a) / (b - a), 0.f, 1.f);
+    return v * v * (-2.f * v + 3.f);
+}
+static float fbm_turb(V P, V dpdx, V dpdy, float omega, int maxOctaves, int turb) {
+    float s2 = fmaxf_(vdot(dpdx, dpdx), vdot(dpdy, dpdy));
+    float foctaves = fminf_((float)maxOctaves, 1.f - .5f * log2_(s2));
+    int octaves = (int)floorf(foctaves);
+    float sum = 0., lambda = 1., o = 1.;
+    for (int i = 0; i < octaves; ++i) {
+        float n = noise3(P.x * lambda, P.y * lambda, P.z * lambda);
+        sum += o * (turb ? fabsf(n) : n);
+        lambda *= 1.99f;
+        o *= omega;
+    }
+    float partialOctave = foctaves - octaves;
+    float n = noise3(P.x * lambda, P.y * lambda, P.z * lambda);
+    sum += o * smoothstep_(.3f, .7f, partialOctave) * (turb ? fabsf(n) : n);
+    if (turb) sum += (maxOctaves - foctaves) * 0.2f;
+    return sum;
+}
+/* FBmTexture / WrinkledTexture / WindyTexture (fbm.h, wrinkled.h, windy.h) over IdentityMapping3D */
+static float tex_noise(const pbrtgpu_texture *tx, const TexPt *q) {
+    V P = xpoint(tx->map, q->p), dpdx = xvec(tx->map, q->dpdx), dpdy = xvec(tx->map, q->dpdy);
+    if (tx->type == PBRTGPU_TEX_WINDY) {
+        float windStrength = fbm_turb(vmul(P, .1f), vmul(dpdx, .1f), vmul(dpdy, .1f), .5f, 3, 0);
+        float waveHeight = fbm_turb(P, dpdx, dpdy, .5f, 6, 0);
+        return fabsf(windStrength) * waveHeight;
+    }
+    return fbm_turb(P, dpdx, dpdy, tx->value, tx->levels, tx->type == PBRTGPU_TEX_WRINKLED);
+}
 /* UVTexture::Evaluate / EvaluateMemory (uv.h:38-51): the RGB (s - Floor2Int(s), t - Floor2Int(t), 0) */
 static void uv_rgb(const pbrtgpu_texture *tx, const TexPt *q, float rgb[3]) {
     float s, t, dsdx, dtdx, dsdy, dtdy;
@@ -1480,6 +1541,7 @@ static float tex_float(const Ctx *c, int id, const TexPt *q) {
             if (k < 2) return tex_float(c, k == 0 ? tx->tex1 : tx->tex2, q);
             return (1.f - a2) * tex_float(c, tx->tex1, q) + a2 * tex_float(c, tx->tex2, q);
         }
+        case PBRTGPU_TEX_FBM: case PBRTGPU_TEX_WRINKLED: case PBRTGPU_TEX_WINDY: return tex_noise(tx, q);
         case PBRTGPU_TEX_BILERP: {   /* BilerpTexture::Evaluate (bilerp.h:38-44) */
             float s, t, dsdx, dtdx, dsdy, dtdy;
             tex_map(tx, q, &s, &t, &dsdx, &dtdx, &dsdy, &dtdy);

@@ -101,6 +101,9 @@ static inline void spec_out(const Spectrum &L, float *c) { L.GetOrigC(c); }
 #include "textures/uv.h"
 #include "textures/mix.h"
 #include "textures/bilerp.h"
+#include "textures/fbm.h"
+#include "textures/wrinkled.h"
+#include "textures/windy.h"
 #include "textures/scale.h"
 
 #include <map>
@@ -434,6 +437,9 @@ static Reference<Texture<float> > MakeFloatTex(const string &n, const Transform 
     if (n == "checkerboard") return CreateCheckerboardFloatTexture(x, tp);
     if (n == "mix") return CreateMixFloatTexture(x, tp);
     if (n == "bilerp") return CreateBilerpFloatTexture(x, tp);
+    if (n == "fbm") return CreateFBmFloatTexture(x, tp);
+    if (n == "wrinkled") return CreateWrinkledFloatTexture(x, tp);
+    if (n == "windy") return CreateWindyFloatTexture(x, tp);
     fprintf(stderr, "harness: float texture %s unsupported\n", n.c_str()); exit(2);
 }
 static Reference<Texture<Spectrum> > MakeSpecTex(const string &n, const Transform &x, const TextureParams &tp) {

@@ -2062,9 +2062,11 @@ PGD_INLINE void leaf_rgb(const DevScene &S, const pbrtgpu_texture &tx, const Tex
         rgb[2] = 0.f;
     } else tex_image<3>(S, tx, q, rgb);
 }
+PGD_HEAVY float tex_noise_leaf(const pbrtgpu_texture &tx, const TexPt &q);
 PGD_INLINE float tex_leaf_float(const DevScene &S, int id, const TexPt &q) {
     const pbrtgpu_texture &tx = (*sa(S.tex, (uint32_t)(id)));
     if (tx.type == PBRTGPU_TEX_CONST) return tx.value;
+    if (tx.type >= PBRTGPU_TEX_FBM) return tex_noise_leaf(tx, q);
     float v;
     tex_image<1>(S, tx, q, &v);
     return v;
@@ -2094,6 +2096,67 @@ PGD_INLINE int checker_pick(const pbrtgpu_texture &tx, const TexPt &q, float *ar
 // Texture<float>: CONST, IMAGE, ScaleTexture, Checkerboard2DTexture or MixTexture of leaves (the
 // front end guarantees the depth); the leaves are looked up in one loop (one copy of the MIPMap
 // lookup code per call site)
+// Perlin noise (texture.cpp:163-250): NoisePerm, Grad, NoiseWeight, Noise, FBm, Turbulence
+__constant__ int pgd_noise_perm[512] = {
+#include "pbrt_noise_perm.inc"
+};
+PGD_INLINE float noise_grad(int x, int y, int z, float dx, float dy, float dz) {
+    int h = pgd_noise_perm[pgd_noise_perm[pgd_noise_perm[x] + y] + z];
+    h &= 15;
+    const float u = h < 8 || h == 12 || h == 13 ? dx : dy;
+    const float v = h < 4 || h == 12 || h == 13 ? dy : dz;
+    return ((h & 1) ? -u : u) + ((h & 2) ? -v : v);
+}
+PGD_INLINE float noise_weight(float t) {
+    const float t3 = t * t * t, t4 = t3 * t;
+    return 6.f * t4 * t - 15.f * t4 + 10.f * t3;
+}
+PGD_HEAVY float noise3(V P) {
+    int ix = (int)floorf(P.x), iy = (int)floorf(P.y), iz = (int)floorf(P.z);
+    const float dx = P.x - ix, dy = P.y - iy, dz = P.z - iz;
+    ix &= 255; iy &= 255; iz &= 255;
+    const float w000 = noise_grad(ix, iy, iz, dx, dy, dz), w100 = noise_grad(ix + 1, iy, iz, dx - 1, dy, dz);
+    const float w010 = noise_grad(ix, iy + 1, iz, dx, dy - 1, dz), w110 = noise_grad(ix + 1, iy + 1, iz, dx - 1, dy - 1, dz);
+    const float w001 = noise_grad(ix, iy, iz + 1, dx, dy, dz - 1), w101 = noise_grad(ix + 1, iy, iz + 1, dx - 1, dy, dz - 1);
+    const float w011 = noise_grad(ix, iy + 1, iz + 1, dx, dy - 1, dz - 1);
+    const float w111 = noise_grad(ix + 1, iy + 1, iz + 1, dx - 1, dy - 1, dz - 1);
+    const float wx = noise_weight(dx), wy = noise_weight(dy), wz = noise_weight(dz);
+    const float x00 = lerpf(wx, w000, w100), x10 = lerpf(wx, w010, w110), x01 = lerpf(wx, w001, w101),
+                x11 = lerpf(wx, w011, w111);
+    const float y0 = lerpf(wy, x00, x10), y1 = lerpf(wy, x01, x11);
+    return lerpf(wz, y0, y1);
+}
+// FBm (turb = false) / Turbulence (turb = true), texture.cpp:214-250
+PGD_HEAVY float fbm_turb(V P, V dpdx, V dpdy, float omega, int maxOctaves, bool turb) {
+    const float s2 = pmax(vlen2(dpdx), vlen2(dpdy));
+    const float foctaves = pmin((float)maxOctaves, 1.f - .5f * log2_(s2));
+    const int octaves = (int)floorf(foctaves);
+    float sum = 0.f, lambda = 1.f, o = 1.f;
+    for (int i = 0; i < octaves; ++i) {
+        const float n = noise3(vmul(P, lambda));
+        sum += o * (turb ? fabsf(n) : n);
+        lambda *= 1.99f;
+        o *= omega;
+    }
+    const float partialOctave = foctaves - octaves;
+    const float v = clampf((partialOctave - .3f) / (.7f - .3f), 0.f, 1.f);   // SmoothStep(.3, .7, x)
+    const float n = noise3(vmul(P, lambda));
+    sum += o * (v * v * (-2.f * v + 3.f)) * (turb ? fabsf(n) : n);
+    if (turb) sum += (maxOctaves - foctaves) * 0.2f;
+    return sum;
+}
+// FBmTexture / WrinkledTexture / WindyTexture::Evaluate (fbm.h, wrinkled.h, windy.h) with
+// IdentityMapping3D::Map (texture.cpp:155-160: tex2world applied to p, dpdx, dpdy)
+PGD_INLINE float tex_noise(const pbrtgpu_texture &tx, const TexPt &q) {
+    const V P = xpoint(tx.map, q.p), dpdx = xvec(tx.map, q.dpdx), dpdy = xvec(tx.map, q.dpdy);
+    if (tx.type == PBRTGPU_TEX_WINDY) {
+        const float windStrength = fbm_turb(vmul(P, .1f), vmul(dpdx, .1f), vmul(dpdy, .1f), .5f, 3, false);
+        const float waveHeight = fbm_turb(P, dpdx, dpdy, .5f, 6, false);
+        return fabsf(windStrength) * waveHeight;
+    }
+    return fbm_turb(P, dpdx, dpdy, tx.value, tx.levels, tx.type == PBRTGPU_TEX_WRINKLED);
+}
+PGD_HEAVY float tex_noise_leaf(const pbrtgpu_texture &tx, const TexPt &q) { return tex_noise(tx, q); }
 // BilerpTexture's weights (bilerp.h:38-44): (1-s)(1-t), (1-s)t, s(1-t), st
 PGD_INLINE void bilerp_w(const pbrtgpu_texture &tx, const TexPt &q, float w[4]) {
     float s, t, dsdx, dtdx, dsdy, dtdy;

@@ -221,9 +221,11 @@ static hipError_t launch(int grid, hipStream_t stream, const DevScene &S, const 
 // FEAT 0 k_dl_nee since the light-sample list (90 spilled, 768 B of scratch per lane); the 60-band
 // k_dl_spec and the all-features k_dl_nee stay at 1 wave/SIMD to keep within tools/kernel_budget.py
 // (at 2 waves k_dl_nee<60, 7> spills 225 VGPRs, 1,300 B; k_dl_spec<60, 0> 160, 1,056 B once
-// shinymetal's conductor mirror lobe joined the specular sampler)
+// shinymetal's conductor mirror lobe joined the specular sampler); the all-features k_dl_spec at
+// every band count runs at 1 wave since the noise textures (FBm / Turbulence inlined: 174 spilled at
+// 2 waves, 1,040 B) -- the FEAT 0 builds of the benchmark configs are unaffected
 #define PGD_NEE_WAVES ((SHADE_NB > 32 && SHADE_FEAT != 0) ? 1 : 2)
-#define PGD_SPEC_WAVES (SHADE_NB > 32 ? 1 : 2)
+#define PGD_SPEC_WAVES ((SHADE_NB > 32 || SHADE_FEAT != 0) ? 1 : 2)
 #ifndef PGD_NEE_ATTR
 #define PGD_NEE_ATTR __attribute__((amdgpu_waves_per_eu(PGD_NEE_WAVES, PGD_NEE_WAVES)))
 #endif

@@ -1258,6 +1258,17 @@ private:
                     t.constant = false; t.tex = AddTexture(n);
                 }
             } else if (cls == "imagemap") { t.constant = false; t.tex = MakeImageTexture(p, false); }
+            else if (cls == "fbm" || cls == "wrinkled" || cls == "windy") {
+                // FBmTexture / WrinkledTexture / WindyTexture<float> (fbm.cpp, wrinkled.cpp, windy.cpp):
+                // IdentityMapping3D(tex2world), octaves (8) and roughness (.5)
+                pbrtgpu_texture n = TexNode(cls == "fbm" ? PBRTGPU_TEX_FBM : cls == "wrinkled" ? PBRTGPU_TEX_WRINKLED
+                                                                                                : PBRTGPU_TEX_WINDY, false);
+                for (int i = 0; i < 16; ++i) n.map[i] = curT.t[0].m.m[i / 4][i % 4];
+                n.levels = p.FindOneInt("octaves", 8);
+                n.value = GetFloat(p, p, "roughness", .5f);
+                if (n.levels < 0 || n.levels > 64) throw std::runtime_error("noise texture octaves out of range");
+                t.constant = false; t.tex = AddTexture(n);
+            }
             else if (cls == "bilerp") {   // BilerpTexture<float> (bilerp.cpp:30-55): v00 .. v11 in texels[]
                 pbrtgpu_texture n = TexNode(PBRTGPU_TEX_BILERP, false);
                 ParseMapping(p, n);
