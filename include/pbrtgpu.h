@@ -114,7 +114,10 @@ enum { PBRTGPU_TEX_CONST = 0, PBRTGPU_TEX_IMAGE = 1, PBRTGPU_TEX_SCALE = 2, PBRT
        spectrum, ...; float at texels[texel_off .. + 3] */,
        /* float noise textures over IdentityMapping3D(tex2world) (map[16] = tex2world.m): FBmTexture,
           WrinkledTexture (octaves in levels, roughness / omega in value), WindyTexture */
-       PBRTGPU_TEX_FBM = 7, PBRTGPU_TEX_WRINKLED = 8, PBRTGPU_TEX_WINDY = 9 };
+       PBRTGPU_TEX_FBM = 7, PBRTGPU_TEX_WRINKLED = 8, PBRTGPU_TEX_WINDY = 9,
+       /* DotsTexture (dots.h): tex1 = its "inside" parameter, tex2 = "outside" (the constructor
+          stores them as outsideDot / insideDot), a 2D mapping; leaves as for CHECKER */
+       PBRTGPU_TEX_DOTS = 10 };
 enum { PBRTGPU_WRAP_REPEAT = 0, PBRTGPU_WRAP_BLACK = 1, PBRTGPU_WRAP_CLAMP = 2 };
 typedef struct pbrtgpu_texture {
     int32_t type;          /* PBRTGPU_TEX_* */

@@ -1494,6 +1494,21 @@ static float fbm_turb(V P, V dpdx, V dpdy, float omega, int maxOctaves, int turb
     if (turb) sum += (maxOctaves - foctaves) * 0.2f;
     return sum;
 }
+/* DotsTexture::Evaluate (dots.h:47-66): 1 = tex2 (insideDot, the "outside" parameter), 0 = tex1 */
+static int dots_pick(const pbrtgpu_texture *tx, const TexPt *q) {
+    float s, t, dsdx, dtdx, dsdy, dtdy;
+    tex_map(tx, q, &s, &t, &dsdx, &dtdx, &dsdy, &dtdy);
+    int sCell = (int)floorf(s + .5f), tCell = (int)floorf(t + .5f);
+    if (noise3(sCell + .5f, tCell + .5f, .5f) > 0) {
+        float radius = .35f;
+        float maxShift = 0.5f - radius;
+        float sCenter = sCell + maxShift * noise3(sCell + 1.5f, tCell + 2.8f, .5f);
+        float tCenter = tCell + maxShift * noise3(sCell + 4.5f, tCell + 9.8f, .5f);
+        float ds = s - sCenter, dt = t - tCenter;
+        if (ds * ds + dt * dt < radius * radius) return 1;
+    }
+    return 0;
+}
 /* FBmTexture / WrinkledTexture / WindyTexture (fbm.h, wrinkled.h, windy.h) over IdentityMapping3D */
 static float tex_noise(const pbrtgpu_texture *tx, const TexPt *q) {
     V P = xpoint(tx->map, q->p), dpdx = xvec(tx->map, q->dpdx), dpdy = xvec(tx->map, q->dpdy);
@@ -1542,6 +1557,7 @@ static float tex_float(const Ctx *c, int id, const TexPt *q) {
             return (1.f - a2) * tex_float(c, tx->tex1, q) + a2 * tex_float(c, tx->tex2, q);
         }
         case PBRTGPU_TEX_FBM: case PBRTGPU_TEX_WRINKLED: case PBRTGPU_TEX_WINDY: return tex_noise(tx, q);
+        case PBRTGPU_TEX_DOTS: return tex_float(c, dots_pick(tx, q) ? tx->tex2 : tx->tex1, q);
         case PBRTGPU_TEX_BILERP: {   /* BilerpTexture::Evaluate (bilerp.h:38-44) */
             float s, t, dsdx, dtdx, dsdy, dtdy;
             tex_map(tx, q, &s, &t, &dsdx, &dtdx, &dsdy, &dtdy);
@@ -1562,6 +1578,7 @@ static void tex_spec(const Ctx *c, int id, const TexPt *q, float *out) {
         case PBRTGPU_TEX_CONST: memcpy(out, SPEC(c, tx->spec), sizeof(float) * nb); return;
         case PBRTGPU_TEX_IMAGE: { float rgb[3]; tex_image(c, tx, 3, q, rgb); from_rgb(c, rgb, 0, out); return; }
         case PBRTGPU_TEX_UV: { float rgb[3]; uv_rgb(tx, q, rgb); from_rgb(c, rgb, 0, out); return; }
+        case PBRTGPU_TEX_DOTS: tex_spec(c, dots_pick(tx, q) ? tx->tex2 : tx->tex1, q, out); return;
         case PBRTGPU_TEX_BILERP: {
             float s, t, dsdx, dtdx, dsdy, dtdy;
             tex_map(tx, q, &s, &t, &dsdx, &dtdx, &dsdy, &dtdy);

@@ -104,6 +104,7 @@ static inline void spec_out(const Spectrum &L, float *c) { L.GetOrigC(c); }
 #include "textures/fbm.h"
 #include "textures/wrinkled.h"
 #include "textures/windy.h"
+#include "textures/dots.h"
 #include "textures/scale.h"
 
 #include <map>
@@ -440,6 +441,7 @@ static Reference<Texture<float> > MakeFloatTex(const string &n, const Transform 
     if (n == "fbm") return CreateFBmFloatTexture(x, tp);
     if (n == "wrinkled") return CreateWrinkledFloatTexture(x, tp);
     if (n == "windy") return CreateWindyFloatTexture(x, tp);
+    if (n == "dots") return CreateDotsFloatTexture(x, tp);
     fprintf(stderr, "harness: float texture %s unsupported\n", n.c_str()); exit(2);
 }
 static Reference<Texture<Spectrum> > MakeSpecTex(const string &n, const Transform &x, const TextureParams &tp) {
@@ -450,6 +452,7 @@ static Reference<Texture<Spectrum> > MakeSpecTex(const string &n, const Transfor
     if (n == "uv") return CreateUVSpectrumTexture(x, tp);
     if (n == "mix") return CreateMixSpectrumTexture(x, tp);
     if (n == "bilerp") return CreateBilerpSpectrumTexture(x, tp);
+    if (n == "dots") return CreateDotsSpectrumTexture(x, tp);
     fprintf(stderr, "harness: spectrum texture %s unsupported\n", n.c_str()); exit(2);
 }
 void pbrtTexture(const string &name, const string &type, const string &texname, const ParamSet &params) {

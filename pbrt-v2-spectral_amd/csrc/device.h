@@ -2066,10 +2066,26 @@ PGD_HEAVY float tex_noise_leaf(const pbrtgpu_texture &tx, const TexPt &q);
 PGD_INLINE float tex_leaf_float(const DevScene &S, int id, const TexPt &q) {
     const pbrtgpu_texture &tx = (*sa(S.tex, (uint32_t)(id)));
     if (tx.type == PBRTGPU_TEX_CONST) return tx.value;
-    if (tx.type >= PBRTGPU_TEX_FBM) return tex_noise_leaf(tx, q);
+    if (tx.type >= PBRTGPU_TEX_FBM && tx.type <= PBRTGPU_TEX_WINDY) return tex_noise_leaf(tx, q);
     float v;
     tex_image<1>(S, tx, q, &v);
     return v;
+}
+PGD_HEAVY float noise3(V P);
+// DotsTexture::Evaluate (dots.h:47-66) without its operands: 1 = tex2 (insideDot: the "outside"
+// parameter, as the reference's constructor stores them), 0 = tex1
+PGD_INLINE int dots_pick(const pbrtgpu_texture &tx, const TexPt &q) {
+    float s, t, dsdx, dtdx, dsdy, dtdy;
+    tex_map(tx, q, &s, &t, &dsdx, &dtdx, &dsdy, &dtdy);
+    const int sCell = (int)floorf(s + .5f), tCell = (int)floorf(t + .5f);
+    if (noise3(v3(sCell + .5f, tCell + .5f, .5f)) > 0) {
+        const float radius = .35f, maxShift = 0.5f - radius;
+        const float sCenter = sCell + maxShift * noise3(v3(sCell + 1.5f, tCell + 2.8f, .5f));
+        const float tCenter = tCell + maxShift * noise3(v3(sCell + 4.5f, tCell + 9.8f, .5f));
+        const float ds = s - sCenter, dt = t - tCenter;
+        if (ds * ds + dt * dt < radius * radius) return 1;
+    }
+    return 0;
 }
 // Checkerboard2DTexture::Evaluate (checkerboard.h:84-125) without its operands: 0 = tex1 alone,
 // 1 = tex2 alone, 2 = (1 - area2) * tex1 + area2 * tex2 (*area2 set)
@@ -2178,7 +2194,7 @@ PGD_HEAVY float tex_float(const DevScene &S, int id, const TexPt &q) {
         const int k = checker_pick(tx, q, &a2);
         if (k < 2) l0 = k == 0 ? tx.tex1 : tx.tex2;
         else { l0 = tx.tex1; l1 = tx.tex2; kind = 2; }
-    } else if (tx.type == PBRTGPU_TEX_MIX) { l0 = tx.amount; l1 = tx.tex1; l2 = tx.tex2; kind = 3; }
+    } else if (tx.type == PBRTGPU_TEX_DOTS) l0 = dots_pick(tx, q) ? tx.tex2 : tx.tex1; else if (tx.type == PBRTGPU_TEX_MIX) { l0 = tx.amount; l1 = tx.tex1; l2 = tx.tex2; kind = 3; }
     else if (tx.type == PBRTGPU_TEX_SCALE) { l0 = tx.tex1; l1 = tx.tex2; kind = 1; }
     float v0 = 0.f, v1 = 0.f, v2 = 0.f;
 #pragma unroll 1
@@ -2221,7 +2237,7 @@ PGD_HEAVY SpecTex tex_spec_prepare(const DevScene &S, int id, const TexPt &q) {
     }
     // the leaves to look up (one copy of the lookup code below): leaf[0], and leaf[1] for a blend
     int leaf0 = id, leaf1 = -1;
-    const bool two = tx.type == PBRTGPU_TEX_MIX || tx.type == PBRTGPU_TEX_CHECKER;   // leaves are CONST / IMAGE / UV
+    const bool two = tx.type == PBRTGPU_TEX_MIX || tx.type == PBRTGPU_TEX_CHECKER || tx.type == PBRTGPU_TEX_DOTS;   // leaves: CONST / IMAGE / UV
     if (tx.type == PBRTGPU_TEX_MIX) {   // MixTexture::Evaluate: always the blend (mix.h:38-43)
         const float amt = tex_leaf_float(S, tx.amount, q);
         leaf0 = tx.tex1; leaf1 = tx.tex2;
@@ -2231,6 +2247,8 @@ PGD_HEAVY SpecTex tex_spec_prepare(const DevScene &S, int id, const TexPt &q) {
         const int k = checker_pick(tx, q, &a2);
         leaf0 = k == 1 ? tx.tex2 : tx.tex1;
         if (k == 2) { leaf1 = tx.tex2; r.blend = true; r.w1 = 1.f - a2; r.w2 = a2; }
+    } else if (tx.type == PBRTGPU_TEX_DOTS) {
+        leaf0 = dots_pick(tx, q) ? tx.tex2 : tx.tex1;
     } else if (tx.type == PBRTGPU_TEX_SCALE) {   // one image / uv leaf times a constant spectrum
         const bool firstConst = (*sa(S.tex, (uint32_t)(tx.tex1))).type == PBRTGPU_TEX_CONST;
         leaf0 = firstConst ? tx.tex2 : tx.tex1;

@@ -355,8 +355,9 @@ static inline int scene_check(const pbrtgpu_flat_scene *s, std::string *err) {
     auto texOk = [&](int id, int spectral, bool slot) -> bool {
         if (id < 0 || id >= s->n_textures || !s->textures) return false;
         const pbrtgpu_texture &t = s->textures[id];
-        if (t.spectral != spectral || t.type < PBRTGPU_TEX_CONST || t.type > PBRTGPU_TEX_WINDY) return false;
-        if (t.type >= PBRTGPU_TEX_FBM && (spectral || t.levels < 0 || t.levels > 64)) return false;   // float noise
+        if (t.spectral != spectral || t.type < PBRTGPU_TEX_CONST || t.type > PBRTGPU_TEX_DOTS) return false;
+        if (t.type >= PBRTGPU_TEX_FBM && t.type <= PBRTGPU_TEX_WINDY && (spectral || t.levels < 0 || t.levels > 64))
+            return false;   // float noise
         if (t.type == PBRTGPU_TEX_BILERP) {   // its four values: spectra in the pool / floats in texels[]
             if (spectral ? (t.spec < 0 || (int64_t)t.spec + 4LL * s->n_bands > (int64_t)s->n_spectra_floats)
                          : (t.texel_off < 0 || !s->texels || (int64_t)t.texel_off + 4 > (int64_t)s->n_texel_floats))
@@ -374,7 +375,7 @@ static inline int scene_check(const pbrtgpu_flat_scene *s, std::string *err) {
                 return false;
         }
         if (t.type == PBRTGPU_TEX_UV && !spectral) return false;   // UVTexture is Texture<Spectrum> only
-        if (t.type == PBRTGPU_TEX_CHECKER) {   // two CONST / IMAGE leaves (device.h tex_spec_prepare)
+        if (t.type == PBRTGPU_TEX_CHECKER || t.type == PBRTGPU_TEX_DOTS) {   // two CONST / IMAGE / UV leaves
             for (int o : {t.tex1, t.tex2}) {
                 if (o < 0 || o >= s->n_textures || s->textures[o].spectral != spectral) return false;
                 if (s->textures[o].type != PBRTGPU_TEX_CONST && s->textures[o].type != PBRTGPU_TEX_IMAGE &&
@@ -384,14 +385,15 @@ static inline int scene_check(const pbrtgpu_flat_scene *s, std::string *err) {
             if (t.aamode < 0 || t.aamode > 1) return false;
         }
         if (t.type != PBRTGPU_TEX_IMAGE && t.type != PBRTGPU_TEX_CHECKER && t.type != PBRTGPU_TEX_UV &&
-            t.type != PBRTGPU_TEX_BILERP && t.mapping != PBRTGPU_MAP_UV)
+            t.type != PBRTGPU_TEX_BILERP && t.type != PBRTGPU_TEX_DOTS && t.mapping != PBRTGPU_MAP_UV)
             return false;
         if (t.mapping < PBRTGPU_MAP_UV || t.mapping > PBRTGPU_MAP_PLANAR) return false;
         if (t.type == PBRTGPU_TEX_SCALE) {
             for (int o : {t.tex1, t.tex2}) {
                 if (o < 0 || o >= s->n_textures || s->textures[o].spectral != spectral) return false;
                 if (s->textures[o].type == PBRTGPU_TEX_SCALE || s->textures[o].type == PBRTGPU_TEX_CHECKER ||
-                    s->textures[o].type == PBRTGPU_TEX_MIX)
+                    s->textures[o].type == PBRTGPU_TEX_MIX || s->textures[o].type == PBRTGPU_TEX_DOTS ||
+                    s->textures[o].type == PBRTGPU_TEX_BILERP)
                     return false;
             }
             if (spectral && (s->textures[t.tex1].type == PBRTGPU_TEX_CONST) == (s->textures[t.tex2].type == PBRTGPU_TEX_CONST))

@@ -1269,6 +1269,13 @@ private:
                 if (n.levels < 0 || n.levels > 64) throw std::runtime_error("noise texture octaves out of range");
                 t.constant = false; t.tex = AddTexture(n);
             }
+            else if (cls == "dots") {   // DotsTexture<float> (dots.cpp:30-55): tex1 = "inside", tex2 = "outside"
+                pbrtgpu_texture n = TexNode(PBRTGPU_TEX_DOTS, false);
+                ParseMapping(p, n);
+                n.tex1 = CheckerLeaf(GetFloatTex(p, p, "inside", 1.f));
+                n.tex2 = CheckerLeaf(GetFloatTex(p, p, "outside", 0.f));
+                t.constant = false; t.tex = AddTexture(n);
+            }
             else if (cls == "bilerp") {   // BilerpTexture<float> (bilerp.cpp:30-55): v00 .. v11 in texels[]
                 pbrtgpu_texture n = TexNode(PBRTGPU_TEX_BILERP, false);
                 ParseMapping(p, n);
@@ -1315,6 +1322,13 @@ private:
             else if (cls == "uv") {   // UVTexture (uv.cpp:37-62): its 2D mapping alone
                 pbrtgpu_texture n = TexNode(PBRTGPU_TEX_UV, true);
                 ParseMapping(p, n);
+                t.constant = false; t.tex = AddTexture(n);
+            }
+            else if (cls == "dots") {   // DotsTexture<Spectrum> (dots.cpp:59-84)
+                pbrtgpu_texture n = TexNode(PBRTGPU_TEX_DOTS, true);
+                ParseMapping(p, n);
+                n.tex1 = CheckerLeaf(GetSpecTex(p, p, "inside", spec.Const(1.f)));
+                n.tex2 = CheckerLeaf(GetSpecTex(p, p, "outside", spec.Const(0.f)));
                 t.constant = false; t.tex = AddTexture(n);
             }
             else if (cls == "bilerp") {   // BilerpTexture<Spectrum> (bilerp.cpp:59-84): four consecutive spectra
