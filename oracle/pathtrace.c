@@ -1579,6 +1579,11 @@ static void tex_spec(const Ctx *c, int id, const TexPt *q, float *out) {
         case PBRTGPU_TEX_IMAGE: { float rgb[3]; tex_image(c, tx, 3, q, rgb); from_rgb(c, rgb, 0, out); return; }
         case PBRTGPU_TEX_UV: { float rgb[3]; uv_rgb(tx, q, rgb); from_rgb(c, rgb, 0, out); return; }
         case PBRTGPU_TEX_DOTS: tex_spec(c, dots_pick(tx, q) ? tx->tex2 : tx->tex1, q, out); return;
+        case PBRTGPU_TEX_FBM: case PBRTGPU_TEX_WRINKLED: case PBRTGPU_TEX_WINDY: {   /* Spectrum(FBm(...)) */
+            float v = tex_noise(tx, q);
+            for (int i = 0; i < nb; ++i) out[i] = v;
+            return;
+        }
         case PBRTGPU_TEX_BILERP: {
             float s, t, dsdx, dtdx, dsdy, dtdy;
             tex_map(tx, q, &s, &t, &dsdx, &dtdx, &dsdy, &dtdy);

@@ -453,6 +453,9 @@ static Reference<Texture<Spectrum> > MakeSpecTex(const string &n, const Transfor
     if (n == "mix") return CreateMixSpectrumTexture(x, tp);
     if (n == "bilerp") return CreateBilerpSpectrumTexture(x, tp);
     if (n == "dots") return CreateDotsSpectrumTexture(x, tp);
+    if (n == "fbm") return CreateFBmSpectrumTexture(x, tp);
+    if (n == "wrinkled") return CreateWrinkledSpectrumTexture(x, tp);
+    if (n == "windy") return CreateWindySpectrumTexture(x, tp);
     fprintf(stderr, "harness: spectrum texture %s unsupported\n", n.c_str()); exit(2);
 }
 void pbrtTexture(const string &name, const string &type, const string &texname, const ParamSet &params) {

@@ -2214,7 +2214,8 @@ PGD_HEAVY float tex_float(const DevScene &S, int id, const TexPt &q) {
 // A Checkerboard2DTexture becomes one of its leaves (CONST: constOnly) or a blend of both: the
 // second leaf in pick2 / constOff2 and the weights w1 = 1 - area2, w2 = area2 (blend)
 // (a BilerpTexture: its four spectra from constOff at one spectrum's stride, weights in w1, w2, w3, w4)
-struct SpecTex { RGBPick pick; int constOff; bool constFirst, constOnly, blend, bilerp; RGBPick pick2; int constOff2; float w1, w2, w3, w4; };
+// (a spectrum noise texture, Spectrum(value) of its float: every band w1, uniform)
+struct SpecTex { RGBPick pick; int constOff; bool constFirst, constOnly, blend, bilerp, uniform; RGBPick pick2; int constOff2; float w1, w2, w3, w4; };
 // one leaf of a checkerboard (CONST or IMAGE) into pick / constOff (constant: constOff >= 0)
 PGD_INLINE void spec_leaf(const DevScene &S, int id, const TexPt &q, RGBPick *pick, int *constOff) {
     const pbrtgpu_texture &lf = (*sa(S.tex, (uint32_t)(id)));
@@ -2226,9 +2227,15 @@ PGD_INLINE void spec_leaf(const DevScene &S, int id, const TexPt &q, RGBPick *pi
 }
 PGD_HEAVY SpecTex tex_spec_prepare(const DevScene &S, int id, const TexPt &q) {
     SpecTex r;
-    r.constOff = -1; r.constFirst = false; r.constOnly = false; r.blend = false; r.bilerp = false; r.constOff2 = -1;
+    r.constOff = -1; r.constFirst = false; r.constOnly = false; r.blend = false; r.bilerp = false; r.uniform = false;
+    r.constOff2 = -1;
     r.w1 = r.w2 = r.w3 = r.w4 = 0.f;
     const pbrtgpu_texture &tx = (*sa(S.tex, (uint32_t)(id)));
+    if (tx.type >= PBRTGPU_TEX_FBM && tx.type <= PBRTGPU_TEX_WINDY) {   // T(FBm(...)) for T = Spectrum
+        r.uniform = true;
+        r.w1 = tex_noise_leaf(tx, q);
+        return r;
+    }
     if (tx.type == PBRTGPU_TEX_BILERP) {
         float w[4];
         bilerp_w(tx, q, w);
@@ -2270,6 +2277,7 @@ PGD_HEAVY SpecTex tex_spec_prepare(const DevScene &S, int id, const TexPt &q) {
     return r;
 }
 PGD_INLINE float4 tex_spec4(const DevScene &S, const SpecTex &t, int q) {
+    if (t.uniform) return make_float4(t.w1, t.w1, t.w1, t.w1);
     if (t.bilerp) {   // ((v00 w00 + v01 w01) + v10 w10) + v11 w11 per band (Spectrum * float: c * w)
         const uint32_t st = (uint32_t)S.nbp;
         const float4 a = *reinterpret_cast<const float4 *>(sa(S.spectra, (uint32_t)(t.constOff + 4 * q)));

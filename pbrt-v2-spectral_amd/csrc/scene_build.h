@@ -356,8 +356,8 @@ static inline int scene_check(const pbrtgpu_flat_scene *s, std::string *err) {
         if (id < 0 || id >= s->n_textures || !s->textures) return false;
         const pbrtgpu_texture &t = s->textures[id];
         if (t.spectral != spectral || t.type < PBRTGPU_TEX_CONST || t.type > PBRTGPU_TEX_DOTS) return false;
-        if (t.type >= PBRTGPU_TEX_FBM && t.type <= PBRTGPU_TEX_WINDY && (spectral || t.levels < 0 || t.levels > 64))
-            return false;   // float noise
+        if (t.type >= PBRTGPU_TEX_FBM && t.type <= PBRTGPU_TEX_WINDY && (t.levels < 0 || t.levels > 64))
+            return false;   // noise
         if (t.type == PBRTGPU_TEX_BILERP) {   // its four values: spectra in the pool / floats in texels[]
             if (spectral ? (t.spec < 0 || (int64_t)t.spec + 4LL * s->n_bands > (int64_t)s->n_spectra_floats)
                          : (t.texel_off < 0 || !s->texels || (int64_t)t.texel_off + 4 > (int64_t)s->n_texel_floats))

@@ -1324,6 +1324,15 @@ private:
                 ParseMapping(p, n);
                 t.constant = false; t.tex = AddTexture(n);
             }
+            else if (cls == "fbm" || cls == "wrinkled" || cls == "windy") {   // Texture<Spectrum>: Spectrum(value)
+                pbrtgpu_texture n = TexNode(cls == "fbm" ? PBRTGPU_TEX_FBM : cls == "wrinkled" ? PBRTGPU_TEX_WRINKLED
+                                                                                                : PBRTGPU_TEX_WINDY, true);
+                for (int i = 0; i < 16; ++i) n.map[i] = curT.t[0].m.m[i / 4][i % 4];
+                n.levels = p.FindOneInt("octaves", 8);
+                n.value = GetFloat(p, p, "roughness", .5f);
+                if (n.levels < 0 || n.levels > 64) throw std::runtime_error("noise texture octaves out of range");
+                t.constant = false; t.tex = AddTexture(n);
+            }
             else if (cls == "dots") {   // DotsTexture<Spectrum> (dots.cpp:59-84)
                 pbrtgpu_texture n = TexNode(PBRTGPU_TEX_DOTS, true);
                 ParseMapping(p, n);
