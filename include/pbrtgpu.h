@@ -117,7 +117,11 @@ enum { PBRTGPU_TEX_CONST = 0, PBRTGPU_TEX_IMAGE = 1, PBRTGPU_TEX_SCALE = 2, PBRT
        PBRTGPU_TEX_FBM = 7, PBRTGPU_TEX_WRINKLED = 8, PBRTGPU_TEX_WINDY = 9,
        /* DotsTexture (dots.h): tex1 = its "inside" parameter, tex2 = "outside" (the constructor
           stores them as outsideDot / insideDot), a 2D mapping; leaves as for CHECKER */
-       PBRTGPU_TEX_DOTS = 10 };
+       PBRTGPU_TEX_DOTS = 10,
+       /* MarbleTexture (marble.h, spectrum only): map = tex2world (IdentityMapping3D), levels =
+          octaves, value = roughness, su = scale, sv = variation; spec = the first of the nine
+          FromRGB spline colours, consecutive spectra */
+       PBRTGPU_TEX_MARBLE = 11 };
 enum { PBRTGPU_WRAP_REPEAT = 0, PBRTGPU_WRAP_BLACK = 1, PBRTGPU_WRAP_CLAMP = 2 };
 typedef struct pbrtgpu_texture {
     int32_t type;          /* PBRTGPU_TEX_* */

@@ -1517,6 +1517,12 @@ static float tex_noise(const pbrtgpu_texture *tx, const TexPt *q) {
         float waveHeight = fbm_turb(P, dpdx, dpdy, .5f, 6, 0);
         return fabsf(windStrength) * waveHeight;
     }
+    if (tx->type == PBRTGPU_TEX_MARBLE) {   /* MarbleTexture::Evaluate (marble.h:45-49): the spline's t */
+        float sc = tx->su;
+        V Ps = vmul(P, sc);
+        float marble = Ps.y + tx->sv * fbm_turb(Ps, vmul(dpdx, sc), vmul(dpdy, sc), tx->value, tx->levels, 0);
+        return .5f + .5f * SINF(marble);
+    }
     return fbm_turb(P, dpdx, dpdy, tx->value, tx->levels, tx->type == PBRTGPU_TEX_WRINKLED);
 }
 /* UVTexture::Evaluate / EvaluateMemory (uv.h:38-51): the RGB (s - Floor2Int(s), t - Floor2Int(t), 0) */
@@ -1582,6 +1588,21 @@ static void tex_spec(const Ctx *c, int id, const TexPt *q, float *out) {
         case PBRTGPU_TEX_FBM: case PBRTGPU_TEX_WRINKLED: case PBRTGPU_TEX_WINDY: {   /* Spectrum(FBm(...)) */
             float v = tex_noise(tx, q);
             for (int i = 0; i < nb; ++i) out[i] = v;
+            return;
+        }
+        case PBRTGPU_TEX_MARBLE: {   /* marble.h:50-66; first clamped to 0..5 (6 reads past the table) */
+            float t = tex_noise(tx, q) * 6.f;
+            float ff = floorf(t);
+            int first = ff >= 5.f ? 5 : (ff >= 0.f ? (int)ff : 0);
+            t = t - (float)first;
+            float u = 1.f - t;
+            const float *c0 = SPEC(c, tx->spec + first * nb), *c1 = c0 + nb, *c2 = c1 + nb, *c3 = c2 + nb;
+            for (int i = 0; i < nb; ++i) {
+                float s0 = c0[i] * u + c1[i] * t, s1 = c1[i] * u + c2[i] * t, s2 = c2[i] * u + c3[i] * t;
+                s0 = s0 * u + s1 * t;
+                s1 = s1 * u + s2 * t;
+                out[i] = (s0 * u + s1 * t) * 1.5f;
+            }
             return;
         }
         case PBRTGPU_TEX_BILERP: {

@@ -105,6 +105,7 @@ static inline void spec_out(const Spectrum &L, float *c) { L.GetOrigC(c); }
 #include "textures/wrinkled.h"
 #include "textures/windy.h"
 #include "textures/dots.h"
+#include "textures/marble.h"
 #include "textures/scale.h"
 
 #include <map>
@@ -453,6 +454,7 @@ static Reference<Texture<Spectrum> > MakeSpecTex(const string &n, const Transfor
     if (n == "mix") return CreateMixSpectrumTexture(x, tp);
     if (n == "bilerp") return CreateBilerpSpectrumTexture(x, tp);
     if (n == "dots") return CreateDotsSpectrumTexture(x, tp);
+    if (n == "marble") return CreateMarbleSpectrumTexture(x, tp);
     if (n == "fbm") return CreateFBmSpectrumTexture(x, tp);
     if (n == "wrinkled") return CreateWrinkledSpectrumTexture(x, tp);
     if (n == "windy") return CreateWindySpectrumTexture(x, tp);

@@ -2170,6 +2170,12 @@ PGD_INLINE float tex_noise(const pbrtgpu_texture &tx, const TexPt &q) {
         const float waveHeight = fbm_turb(P, dpdx, dpdy, .5f, 6, false);
         return fabsf(windStrength) * waveHeight;
     }
+    if (tx.type == PBRTGPU_TEX_MARBLE) {   // MarbleTexture::Evaluate (marble.h:45-49): its spline parameter t
+        const float sc = tx.su;
+        const V Ps = vmul(P, sc);
+        const float marble = Ps.y + tx.sv * fbm_turb(Ps, vmul(dpdx, sc), vmul(dpdy, sc), tx.value, tx.levels, false);
+        return .5f + .5f * SINF(marble);
+    }
     return fbm_turb(P, dpdx, dpdy, tx.value, tx.levels, tx.type == PBRTGPU_TEX_WRINKLED);
 }
 PGD_HEAVY float tex_noise_leaf(const pbrtgpu_texture &tx, const TexPt &q) { return tex_noise(tx, q); }
@@ -2215,7 +2221,8 @@ PGD_HEAVY float tex_float(const DevScene &S, int id, const TexPt &q) {
 // second leaf in pick2 / constOff2 and the weights w1 = 1 - area2, w2 = area2 (blend)
 // (a BilerpTexture: its four spectra from constOff at one spectrum's stride, weights in w1, w2, w3, w4)
 // (a spectrum noise texture, Spectrum(value) of its float: every band w1, uniform)
-struct SpecTex { RGBPick pick; int constOff; bool constFirst, constOnly, blend, bilerp, uniform; RGBPick pick2; int constOff2; float w1, w2, w3, w4; };
+// (a MarbleTexture: the spline's four colours from constOff at one spectrum's stride, t in w1)
+struct SpecTex { RGBPick pick; int constOff; bool constFirst, constOnly, blend, bilerp, uniform, marble; RGBPick pick2; int constOff2; float w1, w2, w3, w4; };
 // one leaf of a checkerboard (CONST or IMAGE) into pick / constOff (constant: constOff >= 0)
 PGD_INLINE void spec_leaf(const DevScene &S, int id, const TexPt &q, RGBPick *pick, int *constOff) {
     const pbrtgpu_texture &lf = (*sa(S.tex, (uint32_t)(id)));
@@ -2228,12 +2235,21 @@ PGD_INLINE void spec_leaf(const DevScene &S, int id, const TexPt &q, RGBPick *pi
 PGD_HEAVY SpecTex tex_spec_prepare(const DevScene &S, int id, const TexPt &q) {
     SpecTex r;
     r.constOff = -1; r.constFirst = false; r.constOnly = false; r.blend = false; r.bilerp = false; r.uniform = false;
-    r.constOff2 = -1;
+    r.marble = false; r.constOff2 = -1;
     r.w1 = r.w2 = r.w3 = r.w4 = 0.f;
     const pbrtgpu_texture &tx = (*sa(S.tex, (uint32_t)(id)));
     if (tx.type >= PBRTGPU_TEX_FBM && tx.type <= PBRTGPU_TEX_WINDY) {   // T(FBm(...)) for T = Spectrum
         r.uniform = true;
         r.w1 = tex_noise_leaf(tx, q);
+        return r;
+    }
+    if (tx.type == PBRTGPU_TEX_MARBLE) {   // marble.h:50-57: the segment (Floor2Int(t * NSEG)) and its t
+        const float t6 = tex_noise_leaf(tx, q) * 6.f;
+        // first is 0..6 in the reference; 6 (t == 1) reads one colour past its table -- 5 with t = 1
+        // gives the same colour (c[6] == c[8]) without that read; NaN takes segment 0
+        const float ff = floorf(t6);
+        const int first = ff >= 5.f ? 5 : (ff >= 0.f ? (int)ff : 0);
+        r.marble = true; r.constOff = tx.spec + first * S.nbp; r.w1 = t6 - (float)first;
         return r;
     }
     if (tx.type == PBRTGPU_TEX_BILERP) {
@@ -2278,6 +2294,24 @@ PGD_HEAVY SpecTex tex_spec_prepare(const DevScene &S, int id, const TexPt &q) {
 }
 PGD_INLINE float4 tex_spec4(const DevScene &S, const SpecTex &t, int q) {
     if (t.uniform) return make_float4(t.w1, t.w1, t.w1, t.w1);
+    if (t.marble) {   // de Casteljau over c0..c3 (marble.h:58-66), per band, then * 1.5
+        const uint32_t st = (uint32_t)S.nbp;
+        const float tt = t.w1, u = 1.f - tt;
+        float r[4];
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const float c0 = *sa(S.spectra, (uint32_t)(t.constOff + 4 * q + b));
+            const float c1 = *sa(S.spectra, (uint32_t)(t.constOff + st + 4 * q + b));
+            const float c2 = *sa(S.spectra, (uint32_t)(t.constOff + 2 * st + 4 * q + b));
+            const float c3 = *sa(S.spectra, (uint32_t)(t.constOff + 3 * st + 4 * q + b));
+            float s0 = c0 * u + c1 * tt, s1 = c1 * u + c2 * tt;
+            const float s2 = c2 * u + c3 * tt;
+            s0 = s0 * u + s1 * tt;
+            s1 = s1 * u + s2 * tt;
+            r[b] = (s0 * u + s1 * tt) * 1.5f;
+        }
+        return make_float4(r[0], r[1], r[2], r[3]);
+    }
     if (t.bilerp) {   // ((v00 w00 + v01 w01) + v10 w10) + v11 w11 per band (Spectrum * float: c * w)
         const uint32_t st = (uint32_t)S.nbp;
         const float4 a = *reinterpret_cast<const float4 *>(sa(S.spectra, (uint32_t)(t.constOff + 4 * q)));

@@ -355,7 +355,11 @@ static inline int scene_check(const pbrtgpu_flat_scene *s, std::string *err) {
     auto texOk = [&](int id, int spectral, bool slot) -> bool {
         if (id < 0 || id >= s->n_textures || !s->textures) return false;
         const pbrtgpu_texture &t = s->textures[id];
-        if (t.spectral != spectral || t.type < PBRTGPU_TEX_CONST || t.type > PBRTGPU_TEX_DOTS) return false;
+        if (t.spectral != spectral || t.type < PBRTGPU_TEX_CONST || t.type > PBRTGPU_TEX_MARBLE) return false;
+        if (t.type == PBRTGPU_TEX_MARBLE &&   // spectrum only; its nine spline colours in the pool
+            (!spectral || t.levels < 0 || t.levels > 64 || t.spec < 0 ||
+             (int64_t)t.spec + 9LL * s->n_bands > (int64_t)s->n_spectra_floats))
+            return false;
         if (t.type >= PBRTGPU_TEX_FBM && t.type <= PBRTGPU_TEX_WINDY && (t.levels < 0 || t.levels > 64))
             return false;   // noise
         if (t.type == PBRTGPU_TEX_BILERP) {   // its four values: spectra in the pool / floats in texels[]
@@ -393,7 +397,7 @@ static inline int scene_check(const pbrtgpu_flat_scene *s, std::string *err) {
                 if (o < 0 || o >= s->n_textures || s->textures[o].spectral != spectral) return false;
                 if (s->textures[o].type == PBRTGPU_TEX_SCALE || s->textures[o].type == PBRTGPU_TEX_CHECKER ||
                     s->textures[o].type == PBRTGPU_TEX_MIX || s->textures[o].type == PBRTGPU_TEX_DOTS ||
-                    s->textures[o].type == PBRTGPU_TEX_BILERP)
+                    s->textures[o].type == PBRTGPU_TEX_BILERP || s->textures[o].type == PBRTGPU_TEX_MARBLE)
                     return false;
             }
             if (spectral && (s->textures[t.tex1].type == PBRTGPU_TEX_CONST) == (s->textures[t.tex2].type == PBRTGPU_TEX_CONST))
@@ -619,7 +623,8 @@ static int scene_build(const pbrtgpu_flat_scene *s, int topNodes, DevScene &S, i
     }
     std::vector<pbrtgpu_texture> texs(s->textures, s->textures + std::max(0, s->n_textures));
     for (auto &t : texs)
-        if ((t.type == PBRTGPU_TEX_CONST || t.type == PBRTGPU_TEX_BILERP) && t.spectral && !remap(t.spec, &t.spec))
+        if ((t.type == PBRTGPU_TEX_CONST || t.type == PBRTGPU_TEX_BILERP || t.type == PBRTGPU_TEX_MARBLE) && t.spectral &&
+            !remap(t.spec, &t.spec))
             SB_FAIL(PBRTGPU_E_INVALID, "texture spectrum offset");
     // FromRGB basis, each of the 14 spectra padded to whole quads
     std::vector<float> basis((size_t)14 * nbp, 0.f);

@@ -1333,6 +1333,24 @@ private:
                 if (n.levels < 0 || n.levels > 64) throw std::runtime_error("noise texture octaves out of range");
                 t.constant = false; t.tex = AddTexture(n);
             }
+            else if (cls == "marble") {   // MarbleTexture (marble.cpp:37-46), its spline colours FromRGB'd here
+                static const float c[9][3] = {{.58f, .58f, .6f}, {.58f, .58f, .6f}, {.58f, .58f, .6f}, {.5f, .5f, .5f},
+                                              {.6f, .59f, .58f}, {.58f, .58f, .6f}, {.58f, .58f, .6f}, {.2f, .2f, .33f},
+                                              {.58f, .58f, .6f}};   // marble.h:51-53
+                pbrtgpu_texture n = TexNode(PBRTGPU_TEX_MARBLE, true);
+                for (int i = 0; i < 16; ++i) n.map[i] = curT.t[0].m.m[i / 4][i % 4];
+                n.levels = p.FindOneInt("octaves", 8);
+                n.value = GetFloat(p, p, "roughness", .5f);
+                n.su = GetFloat(p, p, "scale", 1.f);
+                n.sv = GetFloat(p, p, "variation", .2f);
+                if (n.levels < 0 || n.levels > 64) throw std::runtime_error("marble texture octaves out of range");
+                n.spec = -1;
+                for (int i = 0; i < 9; ++i) {
+                    const int o = EmitSpectrum(spec.FromRGB(c[i]));
+                    if (n.spec < 0) n.spec = o;
+                }
+                t.constant = false; t.tex = AddTexture(n);
+            }
             else if (cls == "dots") {   // DotsTexture<Spectrum> (dots.cpp:59-84)
                 pbrtgpu_texture n = TexNode(PBRTGPU_TEX_DOTS, true);
                 ParseMapping(p, n);
