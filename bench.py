@@ -313,6 +313,68 @@ def slice_efficiency(dev, scene, tile, full_ms, full_paths, reps=2):
     return out
 
 
+def setup_times(dev, scene, cfg, load_ms, upload_ms, gpu_bvh):
+    """scene setup, reported apart from the timed frames (api.cpp:1309-1330 parses
+    the scene and builds the accelerator before Render).  The pack load stands for the parse (the
+    pack is the front end's flattened scene, SAH BVH included: pbrthost_load of a .pbrt does the
+    parse, Loop subdivision and the bvh.cpp:145-194 build, which needs the reference's scene files
+    that stay in the build container); the GPU BVH build (lbvh.hip) over the same primitives and
+    the Loop subdivision of the killeroo control mesh (host front end and loopsubdiv.hip) are timed
+    here on this box, untimed by the frames."""
+    out = {"pack_load_ms": round(load_ms, 2), "upload_ms": round(upload_ms, 2),
+           "what": "pack load (the front end's flattened scene incl. its SAH BVH) + pbrtgpu_scene_upload; "
+                   "the GPU builds below are timed separately (not part of total_ms unless --bvh gpu)"}
+    total = load_ms + upload_ms
+    try:
+        if not gpu_bvh:
+            b = dev.build_bvh(scene)
+            out["gpu_bvh_build_ms"] = {"device": round(b.build_ms[0], 3), "call": round(b.build_ms[1], 3),
+                                       "prims": int(scene.flat.n_prims)}
+        else:
+            out["gpu_bvh_build_ms"] = {"device": round(scene.build_ms[0], 3), "call": round(scene.build_ms[1], 3)}
+            total += scene.build_ms[1]
+    except Exception as e:   # instanced scenes: the top level is the front end's
+        out["gpu_bvh_build_ms"] = "n/a (%s)" % str(e)[:80]
+    ctl = os.path.join(ROOT, "tests", "golden", "killeroo_control.npz")
+    if cfg in ("c1", "c2", "c2_b60", "c5") and os.path.exists(ctl):
+        g = np.load(ctl)
+        vi, P, lv = g["vi"], g["P"], int(g["levels"])
+        dev.loop_subdivide(vi, P, lv)   # first call: module load
+        t = time.perf_counter()
+        dev.loop_subdivide(vi, P, lv)
+        gms = (time.perf_counter() - t) * 1e3
+        t = time.perf_counter()
+        pg.loop_refine_host(vi, P, lv)
+        hms = (time.perf_counter() - t) * 1e3
+        out["loop_subdivision_ms"] = {"gpu_call": round(gms, 3), "host_one_core": round(hms, 2), "levels": lv,
+                                      "faces_in": int(len(vi))}
+    out["total_ms"] = round(total, 2)
+    return out
+
+
+def frame_hbm(roof, cfg, integrator, renderer, step_s, n_gpus):
+    """Whole-frame HBM GB/s (the metric's "+ HBM GB/s"): the PMC bytes of one frame of this workload
+    (FETCH_SIZE x2 + WRITE_SIZE per kernel launch x launches, profiles/hbm_traffic.json, taken by
+    tools/gpu_profile.sh on a serial-mode frame of the same tree) over this run's timed frame."""
+    tf = os.path.join(ROOT, "profiles", "hbm_traffic.json")
+    if not os.path.exists(tf) or n_gpus != 1:
+        return None
+    key = cfg + {"path": "", "directlighting": "_dl", "metadata": "_meta"}[integrator] + (
+        "" if renderer == "sampler" else "_spec")
+    with open(tf) as f:
+        tr = json.load(f).get("configs", {}).get(key)
+    if not tr:
+        return None
+    byts = sum(v["hbm_bytes_per_launch"] * v["launches"] for k, v in tr.items() if isinstance(v, dict))
+    out = {"bytes_per_frame": round(byts), "GBps": round(byts / step_s / 1e9, 1),
+           "frac_of_peak": round(byts / step_s / 1e9 / HBM_PEAK_GBS, 4), "source": tr.get("source")}
+    if roof is not None:
+        alg = sum(v["alg_bytes_per_launch"] * v["launches"] for v in roof["kernels"].values())
+        out["alg_bytes_per_frame"] = round(alg)
+        out["alg_GBps"] = round(alg / step_s / 1e9, 1)
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -360,6 +422,7 @@ def main():
         dist.init_process_group("gloo")          # host-side barrier / max only (no RCCL needed)
 
     pack, desc = CONFIGS[args.config]
+    t_load = time.perf_counter()
     scene = pg.Scene.load(args.scene or os.path.join(ROOT, "scenes", pack), xres=args.res, yres=args.res,
                           spp=args.spp, seed=rank if args.shard == "frames" else 0,
                           integrator=args.integrator, strategy=args.strategy,
@@ -367,6 +430,7 @@ def main():
                           sampling=args.sampling)
     if args.integrator != "path":
         desc = desc.replace("path maxdepth", "%s (%s) maxdepth" % (args.integrator, args.strategy or "scene"))
+    load_ms = (time.perf_counter() - t_load) * 1e3
     pps = scene.paths_per_sample()
     if args.renderer == "spectral":
         desc += ", SpectralRenderer nWaveBands %d %sDirection (%d paths per camera sample)" % (
@@ -382,8 +446,10 @@ def main():
         devs = [pg.Device(i) for i in range(args.gpus)]
         if args.bvh == "gpu":
             scene = devs[0].build_bvh(scene)
+        t_up = time.perf_counter()
         for d in devs:
             d.upload(scene)
+        upload_ms = (time.perf_counter() - t_up) * 1e3
         film = np.zeros(shape, np.float32)
         dev, tiles = devs[0], None
 
@@ -396,7 +462,9 @@ def main():
         dev = pg.Device(local % max(1, pg.gpu_lib().pbrtgpu_device_count()))
         if args.bvh == "gpu":
             scene = dev.build_bvh(scene)
+        t_up = time.perf_counter()
         dev.upload(scene)
+        upload_ms = (time.perf_counter() - t_up) * 1e3
         if world > 1 and args.shard == "tiles":
             tiles = pg.tile_slice(ntx * nty, rank, world)
             if one_node(world):
@@ -449,6 +517,10 @@ def main():
     if rank == 0 and n_gpus == 1 and not threads_mode and args.shard == "tiles" and not args.no_slices:
         slices = slice_efficiency(dev, scene, tile, elapsed / args.steps * 1e3, frame_paths)
 
+    setup = None
+    if rank == 0:
+        setup = setup_times(dev, scene, args.config, load_ms, upload_ms, args.bvh == "gpu")
+
     cpu = None
     if rank == 0 and n_gpus == 1 and not args.no_cpu:
         cpu = cpu_baseline(scene, args.cpu_seconds)
@@ -471,6 +543,13 @@ def main():
             "roofline": roof,
             "cpu_baseline": cpu,
         }
+        if setup is not None:
+            line["setup_ms"] = setup["total_ms"]
+            line["setup"] = setup
+        hbm = frame_hbm(roof, args.config, args.integrator, args.renderer, elapsed / args.steps, n_gpus)
+        if hbm is not None:
+            line["hbm_GBps"] = hbm["GBps"]
+            line["hbm"] = hbm
         if slices is not None:
             line["slice_efficiency"] = slices
         if per_rank is not None:

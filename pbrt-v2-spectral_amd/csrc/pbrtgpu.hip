@@ -1237,9 +1237,12 @@ struct Lane {
     bool slotMtExt = false;
     PathSoA P{};
     hipStream_t s = nullptr, s2 = nullptr;
-    hipEvent_t ev[2 + 6 * 8] = {};
-    uint32_t *hostCnt = nullptr;   // pinned mirror of the queue counters
-    hipEvent_t done = nullptr;     // recorded after each batch's counter read-back (polled)
+    // two batch slots (run_wavefront keeps up to two batches of passes in flight): per slot the
+    // passes' event pairs, the pinned mirror of the queue counters at the batch's end, and the
+    // event recorded after that read-back (polled)
+    hipEvent_t ev[2][2 + 6 * 8] = {};
+    uint32_t *hostCnt[2] = {};
+    hipEvent_t done[2] = {};
 };
 #ifndef PGD_LANES
 #define PGD_LANES 2
@@ -1582,7 +1585,20 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
     // drain: the run's items are all taken; its k_shade passes take the live slots' list
     // (PathSoA::listMode) on a grid of liveGrid blocks (live slots <= the queued rays at the last
     // read-back, as every live slot ends a pass with a ray queued)
-    struct Run { Lane *L; ItemSrc src; int cap, grid, q, batch, passes, maxPasses; bool done, drain; int liveGrid, listPasses; };
+    // One batch of passes between two counter read-backs, as enqueued.  A lane keeps up to two
+    // batches in flight (slots 0 / 1 of Lane::ev / hostCnt / done): while the GPU runs batch k+1,
+    // the host reads batch k's counters and enqueues batch k+2, so a read-back never leaves the
+    // lane's streams idle (round 5: 15 such gaps, 5.6 ms of a 41 ms 1/8-slice timeline).  The
+    // decisions batch k+2 takes from batch k's counters stay valid one batch late:
+    //   * the drain's list mode: once every item is taken (CNT_NEXT) no slot regenerates, so the
+    //     live slots only decrease and the queued rays of batch k bound them at k+2 (liveGrid);
+    //   * the tail (k_tail): queued rays at batch k bound those at k+2, and the three list-mode
+    //     passes before it are counted as enqueued;
+    //   * the end: queues empty at batch k stay empty, and batch k+1 is then empty passes.
+    // Every pass runs in the same stream order whatever the batching, so the radiance is unchanged.
+    struct Batch { int n; bool single, drain; int liveGrid, qEnd; };
+    struct Run { Lane *L; ItemSrc src; int cap, grid, q, passes, maxPasses; bool done, drain, ending, tailed; int liveGrid, listPasses;
+                 Batch b[2]; int head, inflight; };
     // the drain's tail kernel (k_tail): path integrator, scenes without instances (the 4-wide walks),
     // not in work-counting runs (it counts no traversal work)
     const uint32_t tailMax = (!dl && c->S.integrator == PBRTGPU_INTEGRATOR_PATH && !inst && c->S.w4N > 0 && !countWork)
@@ -1591,216 +1607,93 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
     Run R[kLanes];
     const bool serial = serial_mode();
     const int nl = (src.nItems >= 8192u && !serial) ? kLanes : 1;
-    HIPCHK(hipEventRecord(c->ev[0], c->stream));   // the other lanes start after the work queued so far
-    for (int l = 0; l < nl; ++l) {
-        Run &r = R[l];
-        Lane &L = c->lane[l];
-        r.L = &L;
-        r.src = src;
-        const uint32_t lo = (uint32_t)((uint64_t)src.nItems * l / nl), hi = (uint32_t)((uint64_t)src.nItems * (l + 1) / nl);
-        r.src.base = src.base + lo;
-        r.src.nItems = hi - lo;
-        r.cap = lane_slots(r.src.nItems, nl);
-        if (dl)   // the frame stacks and light-sample batches: at most 24 GiB per lane
-            r.cap = (int)std::max<size_t>(64, std::min<size_t>((size_t)r.cap, ((size_t)24 << 30) /
-                                                               (frame_bytes(NB) * nFrames + batch_bytes(NB) * batch)));
-        if (mtExt && !getenv("PBRTGPU_SLOTS")) r.cap = std::min(r.cap, 1 << 20);   // 2.5 KiB of MT state per slot
-        r.cap = std::min(r.cap, max_slots_32bit(NB, batch));
-        r.grid = (r.cap + kShadeBlock - 1) / kShadeBlock;
-        r.q = 0;
-        r.batch = 0;
-        r.done = false;
-        r.drain = false;
-        r.liveGrid = r.grid;
-        r.listPasses = 0;
-        L.P.listMode = 0;
-        L.P.xcdMap = xcd_map_on();
-        // drain bound of this run: a path lives at most pathPasses passes, so every slot
-        // takes a new item at least once per pathPasses passes while items remain; twice
-        // that, plus the overshoot of one enqueued batch, means the wavefront is stuck
-        r.passes = 0;
-        r.maxPasses = (int)std::min<int64_t>(INT32_MAX / 2, 2 * ((r.src.nItems + r.cap - 1) / r.cap + 1) * pathPasses) +
-                      2 * kPassBatch;
-        if (int e = ensure_slots(&L, r.cap, NB, c->S.nInsts, nFrames, batch, mtExt)) return e;
-        HIPCHK(L.spill.ensure(2 * spillLane * sizeof(uint2)));
-        if (l > 0) HIPCHK(hipStreamWaitEvent(L.s, c->ev[0], 0));
-        if (const int pb = poison_byte(); pb >= 0) {
-            HIPCHK(hipMemsetAsync(L.slots.p, pb, L.slots.n, L.s));
-            HIPCHK(hipMemsetAsync(L.spill.p, pb, L.spill.n, L.s));
+    // batch `bi` of run r after its passes: the counters to the host, the completion event
+    auto close_batch = [&](Run &r, int bi, const Batch &B) -> int {
+        Lane &L = *r.L;
+        HIPCHK(hipMemcpyAsync(L.hostCnt[bi], L.P.cnt, CNT_WORDS * 4, hipMemcpyDeviceToHost, L.s));
+        HIPCHK(hipEventRecord(L.done[bi], L.s));
+        r.b[bi] = B;
+        r.inflight++;
+        return 0;
+    };
+    // the next batch of run r from the counters `cnt` of its last completed batch (qc: that batch's
+    // final queue set): the drain / tail decisions above, then the passes
+    auto enqueue = [&](Run &r, const uint32_t *cnt, int qc) -> int {
+        Lane &L = *r.L;
+        const PathSoA &P = L.P;
+        const int bi = r.inflight ? (r.head ^ 1) : r.head;
+        const uint64_t queued = (uint64_t)cnt[CNT_QC(qc)] + cnt[CNT_QS(qc)];
+        if (drainList && cnt[CNT_NEXT] >= r.src.nItems) {
+            r.drain = true;
+            const uint64_t bound = std::min<uint64_t>((uint64_t)r.cap, queued);
+            r.liveGrid = (int)std::max<uint64_t>(1, (bound + kShadeBlock - 1) / kShadeBlock);
         }
-        HIPCHK(hipMemsetAsync(L.P.item, 0xff, (size_t)r.cap * 4, L.s));
-        HIPCHK(hipMemsetAsync(L.P.cnt, 0, CNT_WORDS * 4, L.s));
-        {   // the per-wave writer masks start empty: k_shade loads a wave's masks before it knows
-            // which of them its lanes will use (wave_masks), so none is read unwritten
-            const size_t W = (size_t)((r.cap + 63) / 64) * 8;
-            HIPCHK(hipMemsetAsync(L.P.aMask, 0, 2 * W, L.s));
-            HIPCHK(hipMemsetAsync(L.P.bMask, 0, 3 * W, L.s));
-            HIPCHK(hipMemsetAsync(L.P.mMask, 0, 2 * W, L.s));
+        int q = r.q;
+        hipEvent_t *ev = L.ev[bi];
+        if (r.drain && r.listPasses >= 3 && tailMax && queued <= tailMax) {
+            // the tail: the live list, then k_tail runs those paths to their end; the next queue
+            // set stays empty, so the lane reads as drained at this batch's read-back (its time is
+            // the batch's single event pair, a shade launch)
+            const int nq = q ^ 1;
+            HIPCHK(hipMemsetAsync(P.cnt + CNT_QC(nq), 0, 4, L.s));
+            HIPCHK(hipMemsetAsync(P.cnt + CNT_QS(nq), 0, 4, L.s));
+            HIPCHK(hipEventRecord(ev[0], L.s));
+            HIPCHK(drain_list(L, true, r.cap));
+            const uint64_t bound = std::min<uint64_t>((uint64_t)r.cap, queued);
+            HIPCHK(kTail((int)std::max<uint64_t>(1, (bound + kTailBlock - 1) / kTailBlock), L.s, c->S, L.P, q, Lout,
+                         (int)std::min<int64_t>(pathPasses, INT32_MAX)));
+            HIPCHK(hipEventRecord(ev[1], L.s));
+            r.q = nq;
+            r.tailed = true;
+            T.passes++;
+            r.passes++;
+            return close_batch(r, bi, Batch{0, true, true, r.liveGrid, nq});
         }
-        // pass 0: every slot is free -> regeneration fills them with camera rays (queue 0)
-        HIPCHK(hipEventRecord(L.ev[0], L.s));
-        L.P.pass = 0;   // k_shade pass index (mod 3) of this run: the beta buffers rotate with it
-        HIPCHK(kShade(r.grid, L.s, c->S, L.P, r.src, 0, Lout));
-        HIPCHK(hipEventRecord(L.ev[1], L.s));
-        HIPCHK(hipMemcpyAsync(L.hostCnt, L.P.cnt, CNT_WORDS * 4, hipMemcpyDeviceToHost, L.s));
-        HIPCHK(hipEventRecord(L.done, L.s));
-    }
-    int live = nl;
-    float m;
-    int rr = 0;   // round-robin start of the lane poll
-    while (live > 0) {
-        // the next lane whose batch has completed: the host never blocks on one lane while the
-        // other lane's queue has run dry (it would idle until that wait ended)
-        int l = -1;
-        int spins = 0;
-        for (;;) {
-            for (int k = 0; k < nl && l < 0; ++k) {
-                const int i = (rr + k) % nl;
-                if (R[i].done) continue;
-                const hipError_t qe = hipEventQuery(R[i].L->done);
-                if (qe == hipSuccess) l = i;
-                else if (qe != hipErrorNotReady) HIPCHK(qe);
-            }
-            if (l >= 0) break;
-            // a few empty polls, then short sleeps: a batch of passes takes milliseconds, and a host
-            // thread per device (render_multi) should not burn a core for the whole frame
-            if (++spins > 64) std::this_thread::sleep_for(std::chrono::microseconds(20));
-            else std::this_thread::yield();
-        }
-        rr = l + 1;
-        {
-            Run &r = R[l];
-            Lane &L = *r.L;
-            const PathSoA &P = L.P;
-            if (r.batch == 0) {
-                HIPCHK(hipEventElapsedTime(&m, L.ev[0], L.ev[1])); T.ms[K_SHADE] += m;
-                T.launches[K_SHADE]++;
-            }
-            for (int j = 0; j < r.batch; ++j) {
-                hipEvent_t *e = L.ev + 2 + 6 * j;
-                float mc, ms, mh;
-                HIPCHK(hipEventElapsedTime(&mc, e[0], e[1])); T.ms[K_CLOSEST] += mc;
-                HIPCHK(hipEventElapsedTime(&ms, e[2], e[3])); T.ms[K_SHADOW] += ms;
-                HIPCHK(hipEventElapsedTime(&mh, e[4], e[5])); T.ms[K_SHADE] += mh;
-                if (pass_log())   // diagnostics: per-pass device time of each lane
-                    fprintf(stderr, "pass_log lane %d pass %d closest %.3f shadow %.3f shade %.3f\n", l,
-                            r.passes - r.batch + j, mc, ms, mh);
-            }
-            if (pass_log() && r.batch)
-                fprintf(stderr, "pass_log lane %d after pass %d: closest queue %u shadow queue %u items taken %u of %u\n", l,
-                        r.passes - 1, L.hostCnt[CNT_QC(r.q)], L.hostCnt[CNT_QS(r.q)], L.hostCnt[CNT_NEXT], r.src.nItems);
-            int q = r.q;
-            if (L.hostCnt[CNT_ERR] & 1u)
-                return fail(PBRTGPU_E_STATE, "a path drew past 227 MT19937 outputs without its state row");
-            if (L.hostCnt[CNT_ERR] & 2u)
-                return fail(PBRTGPU_E_STATE, "drain: a pass's live list exceeded its shade grid");
-            // every live slot ends a pass with a ray queued, so the drain's list fits the grid sized
-            // from the last queue sizes; a longer list would leave slots unshaded (their beta / A / B
-            // buffers then rotate under them): refuse instead
-            if (r.drain && (uint64_t)L.hostCnt[CNT_LIVE] > (uint64_t)r.liveGrid * kShadeBlock)
-                return fail(PBRTGPU_E_STATE, "drain: more live slots than the shade grid covers");
-            if (L.hostCnt[CNT_QC(q)] == 0 && L.hostCnt[CNT_QS(q)] == 0) {
-                r.done = true;
-                --live;
-                uint64_t w[W_COUNT];
-                HIPCHK(hipMemcpy(w, P.cnt + CNT_WORK, sizeof(w), hipMemcpyDeviceToHost));
-                if (countWork)
-                    for (int i = 0; i < W_COUNT; ++i) T.work[i] += w[i];
-                if (zeroedOut) *zeroedOut += L.hostCnt[CNT_ZEROED];
-                continue;
-            }
-            if (r.passes > r.maxPasses) return fail(PBRTGPU_E_STATE, "wavefront did not drain");
-            if (drainList && L.hostCnt[CNT_NEXT] >= r.src.nItems) {
-                r.drain = true;
-                const uint64_t bound = std::min<uint64_t>((uint64_t)r.cap, (uint64_t)L.hostCnt[CNT_QC(q)] + L.hostCnt[CNT_QS(q)]);
-                r.liveGrid = (int)std::max<uint64_t>(1, (bound + kShadeBlock - 1) / kShadeBlock);
-            }
-            if (r.drain && r.listPasses >= 3 && tailMax &&
-                (uint64_t)L.hostCnt[CNT_QC(q)] + L.hostCnt[CNT_QS(q)] <= tailMax) {
-                // the tail: the live list, then k_tail runs those paths to their end; the next queue
-                // set stays empty, so the next read-back finds the lane drained (its time is the
-                // batch-0 event pair, a shade launch)
-                const int nq = q ^ 1;
-                HIPCHK(hipMemsetAsync(P.cnt + CNT_QC(nq), 0, 4, L.s));
-                HIPCHK(hipMemsetAsync(P.cnt + CNT_QS(nq), 0, 4, L.s));
-                HIPCHK(hipEventRecord(L.ev[0], L.s));
-                HIPCHK(drain_list(L, true, r.cap));
-                const uint64_t bound = std::min<uint64_t>((uint64_t)r.cap, (uint64_t)L.hostCnt[CNT_QC(q)] + L.hostCnt[CNT_QS(q)]);
-                HIPCHK(kTail((int)std::max<uint64_t>(1, (bound + kTailBlock - 1) / kTailBlock), L.s, c->S, L.P, q, Lout,
-                             (int)std::min<int64_t>(pathPasses, INT32_MAX)));
-                HIPCHK(hipEventRecord(L.ev[1], L.s));
-                r.batch = 0;
-                r.q = nq;
-                T.passes++;
-                r.passes++;
-                HIPCHK(hipMemcpyAsync(L.hostCnt, P.cnt, CNT_WORDS * 4, hipMemcpyDeviceToHost, L.s));
-                HIPCHK(hipEventRecord(L.done, L.s));
-                continue;
-            }
-            uint2 *spillC = (uint2 *)L.spill.p, *spillS = spillC + spillLane;
-            // serial mode: the shadow queries follow the closest-hit queries on the main stream
-            hipStream_t s2 = serial ? L.s : L.s2;
-            // passes per read-back: kPassBatch while the lane has items for more than one more
-            // pool, then fewer, so that the switch to the drain's list mode and the lane's end
-            // are seen within a few passes (2 in the drain, 4 before it)
-            r.batch = r.drain ? std::min(2, kPassBatch)
-                              : (uint64_t)L.hostCnt[CNT_NEXT] + (uint64_t)r.cap >= r.src.nItems ? std::min(4, kPassBatch)
-                                                                                              : kPassBatch;
-            for (int j = 0; j < r.batch; ++j) {
-                hipEvent_t *e = L.ev + 2 + 6 * j;
-                const int nq = q ^ 1;
-                HIPCHK(hipMemsetAsync(P.cnt + CNT_QC(nq), 0, 4, L.s));
-                HIPCHK(hipMemsetAsync(P.cnt + CNT_QS(nq), 0, 4, L.s));
-                if (dl) HIPCHK(hipMemsetAsync(P.cnt + CNT_DLN, 0, 4, L.s));   // this pass's light-sample list
-                HIPCHK(hipEventRecord(e[0], L.s));
-                if (serial) {   // closest-hit queries first, alone on the device
-                    if (instPT) {
-                        if (countWork) hipLaunchKernelGGL((k_trace_inst<false, true>), dim3(ptGrid), dim3(kTraceBlock), 0, L.s, c->S, P, q, c->refill, c->ring, spillC);
-                        else hipLaunchKernelGGL((k_trace_inst<false, false>), dim3(ptGrid), dim3(kTraceBlock), 0, L.s, c->S, P, q, c->refill, c->ring, spillC);
-                    } else if (inst) {
-                        if (countWork) hipLaunchKernelGGL((k_trace_closest<true, true>), dim3(traceGrid), dim3(kTraceBlock), lds, L.s, c->S, P, q);
-                        else hipLaunchKernelGGL((k_trace_closest<false, true>), dim3(traceGrid), dim3(kTraceBlock), lds, L.s, c->S, P, q);
-                    } else if (c4 && countWork) hipLaunchKernelGGL((k_trace_c4<true>), dim3(ptGrid), dim3(kTraceBlock), 0, L.s, c->S, P, q, c->refill, c->ring, spillC);
-                    else if (c4) hipLaunchKernelGGL((k_trace_c4<false>), dim3(ptGrid), dim3(kTraceBlock), 0, L.s, c->S, P, q, c->refill, c->ring, spillC);
-                    else if (countWork) hipLaunchKernelGGL((k_trace_pt<false, true>), dim3(ptGrid), dim3(kTraceBlock), 0, L.s, c->S, P, q, c->refill, c->ring, spillC);
-                    else hipLaunchKernelGGL((k_trace_pt<false, false>), dim3(ptGrid), dim3(kTraceBlock), 0, L.s, c->S, P, q, c->refill, c->ring, spillC);
-                    HIPCHK(hipGetLastError());
-                    HIPCHK(hipEventRecord(e[1], L.s));
-                    HIPCHK(hipEventRecord(e[2], L.s));
-                    if (instPT) {
-                        if (countWork) hipLaunchKernelGGL((k_trace_inst<true, true>), dim3(ptGridS), dim3(kTraceBlock), 0, L.s, c->S, P, q, c->refill, c->ring, spillS);
-                        else hipLaunchKernelGGL((k_trace_inst<true, false>), dim3(ptGridS), dim3(kTraceBlock), 0, L.s, c->S, P, q, c->refill, c->ring, spillS);
-                    } else if (inst) {
-                        if (countWork) hipLaunchKernelGGL((k_trace_shadow<true, true>), dim3(traceGrid), dim3(kTraceBlock), ldsS, L.s, c->S, P, q);
-                        else hipLaunchKernelGGL((k_trace_shadow<false, true>), dim3(traceGrid), dim3(kTraceBlock), ldsS, L.s, c->S, P, q);
-                    } else if (s4q && countWork) hipLaunchKernelGGL((k_trace_s4q<true>), dim3(ptGridS), dim3(kTraceBlock), 0, L.s, c->S, P, q, c->refill, c->ring, spillS);
-                    else if (s4q) hipLaunchKernelGGL((k_trace_s4q<false>), dim3(ptGridS), dim3(kTraceBlock), 0, L.s, c->S, P, q, c->refill, c->ring, spillS);
-                    else if (s4 && countWork) hipLaunchKernelGGL((k_trace_s4<true>), dim3(ptGridS), dim3(kTraceBlock), 0, L.s, c->S, P, q, c->refill, c->ring, spillS);
-                    else if (s4) hipLaunchKernelGGL((k_trace_s4<false>), dim3(ptGridS), dim3(kTraceBlock), 0, L.s, c->S, P, q, c->refill, c->ring, spillS);
-                    else if (countWork) hipLaunchKernelGGL((k_trace_pt<true, true>), dim3(ptGridS), dim3(kTraceBlock), 0, L.s, c->S, P, q, c->refill, c->ring, spillS);
-                    else hipLaunchKernelGGL((k_trace_pt<true, false>), dim3(ptGridS), dim3(kTraceBlock), 0, L.s, c->S, P, q, c->refill, c->ring, spillS);
-                    HIPCHK(hipGetLastError());
-                    T.launches[K_CLOSEST]++;
-                    T.launches[K_SHADOW]++;
-                    HIPCHK(hipEventRecord(e[3], L.s));
-                    HIPCHK(hipEventRecord(e[4], L.s));
-                    L.P.pass = (L.P.pass + 1) % 3;
-                    HIPCHK(drain_list(L, r.drain, r.cap));
-                    HIPCHK(kShade(r.drain ? r.liveGrid : r.grid, L.s, c->S, P, r.src, nq, Lout));
-                    if (dl) {
-                        const int g = r.drain ? r.liveGrid : r.grid;
-                        HIPCHK(kNee(g, L.s, c->S, L.P, nq));
-                        HIPCHK(kSpec(g, L.s, c->S, L.P, r.src, nq, Lout));
-                    }
-                    if (mtList) HIPCHK(launch_mt_init(L.s, P, nq));
-                    T.launches[K_SHADE]++;
-                    HIPCHK(hipEventRecord(e[5], L.s));
-                    T.passes++;
-                    r.passes++;
-                    r.listPasses += r.drain ? 1 : 0;
-                    q = nq;
-                    continue;
-                }
+        uint2 *spillC = (uint2 *)L.spill.p, *spillS = spillC + spillLane;
+        // serial mode: the shadow queries follow the closest-hit queries on the main stream
+        hipStream_t s2 = serial ? L.s : L.s2;
+        // passes per read-back: kPassBatch while the lane has items for more than one more
+        // pool, then fewer, so that the switch to the drain's list mode and the lane's end
+        // are seen within a few passes (2 in the drain, 4 before it)
+        const int n = r.drain ? std::min(2, kPassBatch)
+                              : (uint64_t)cnt[CNT_NEXT] + (uint64_t)r.cap >= r.src.nItems ? std::min(4, kPassBatch)
+                                                                                        : kPassBatch;
+        for (int j = 0; j < n; ++j) {
+            hipEvent_t *e = ev + 2 + 6 * j;
+            const int nq = q ^ 1;
+            HIPCHK(hipMemsetAsync(P.cnt + CNT_QC(nq), 0, 4, L.s));
+            HIPCHK(hipMemsetAsync(P.cnt + CNT_QS(nq), 0, 4, L.s));
+            if (dl) HIPCHK(hipMemsetAsync(P.cnt + CNT_DLN, 0, 4, L.s));   // this pass's light-sample list
+            HIPCHK(hipEventRecord(e[0], L.s));
+            if (serial) {   // closest-hit queries first, alone on the device
+                if (instPT) {
+                    if (countWork) hipLaunchKernelGGL((k_trace_inst<false, true>), dim3(ptGrid), dim3(kTraceBlock), 0, L.s, c->S, P, q, c->refill, c->ring, spillC);
+                    else hipLaunchKernelGGL((k_trace_inst<false, false>), dim3(ptGrid), dim3(kTraceBlock), 0, L.s, c->S, P, q, c->refill, c->ring, spillC);
+                } else if (inst) {
+                    if (countWork) hipLaunchKernelGGL((k_trace_closest<true, true>), dim3(traceGrid), dim3(kTraceBlock), lds, L.s, c->S, P, q);
+                    else hipLaunchKernelGGL((k_trace_closest<false, true>), dim3(traceGrid), dim3(kTraceBlock), lds, L.s, c->S, P, q);
+                } else if (c4 && countWork) hipLaunchKernelGGL((k_trace_c4<true>), dim3(ptGrid), dim3(kTraceBlock), 0, L.s, c->S, P, q, c->refill, c->ring, spillC);
+                else if (c4) hipLaunchKernelGGL((k_trace_c4<false>), dim3(ptGrid), dim3(kTraceBlock), 0, L.s, c->S, P, q, c->refill, c->ring, spillC);
+                else if (countWork) hipLaunchKernelGGL((k_trace_pt<false, true>), dim3(ptGrid), dim3(kTraceBlock), 0, L.s, c->S, P, q, c->refill, c->ring, spillC);
+                else hipLaunchKernelGGL((k_trace_pt<false, false>), dim3(ptGrid), dim3(kTraceBlock), 0, L.s, c->S, P, q, c->refill, c->ring, spillC);
+                HIPCHK(hipGetLastError());
+                HIPCHK(hipEventRecord(e[1], L.s));
+                HIPCHK(hipEventRecord(e[2], L.s));
+                if (instPT) {
+                    if (countWork) hipLaunchKernelGGL((k_trace_inst<true, true>), dim3(ptGridS), dim3(kTraceBlock), 0, L.s, c->S, P, q, c->refill, c->ring, spillS);
+                    else hipLaunchKernelGGL((k_trace_inst<true, false>), dim3(ptGridS), dim3(kTraceBlock), 0, L.s, c->S, P, q, c->refill, c->ring, spillS);
+                } else if (inst) {
+                    if (countWork) hipLaunchKernelGGL((k_trace_shadow<true, true>), dim3(traceGrid), dim3(kTraceBlock), ldsS, L.s, c->S, P, q);
+                    else hipLaunchKernelGGL((k_trace_shadow<false, true>), dim3(traceGrid), dim3(kTraceBlock), ldsS, L.s, c->S, P, q);
+                } else if (s4q && countWork) hipLaunchKernelGGL((k_trace_s4q<true>), dim3(ptGridS), dim3(kTraceBlock), 0, L.s, c->S, P, q, c->refill, c->ring, spillS);
+                else if (s4q) hipLaunchKernelGGL((k_trace_s4q<false>), dim3(ptGridS), dim3(kTraceBlock), 0, L.s, c->S, P, q, c->refill, c->ring, spillS);
+                else if (s4 && countWork) hipLaunchKernelGGL((k_trace_s4<true>), dim3(ptGridS), dim3(kTraceBlock), 0, L.s, c->S, P, q, c->refill, c->ring, spillS);
+                else if (s4) hipLaunchKernelGGL((k_trace_s4<false>), dim3(ptGridS), dim3(kTraceBlock), 0, L.s, c->S, P, q, c->refill, c->ring, spillS);
+                else if (countWork) hipLaunchKernelGGL((k_trace_pt<true, true>), dim3(ptGridS), dim3(kTraceBlock), 0, L.s, c->S, P, q, c->refill, c->ring, spillS);
+                else hipLaunchKernelGGL((k_trace_pt<true, false>), dim3(ptGridS), dim3(kTraceBlock), 0, L.s, c->S, P, q, c->refill, c->ring, spillS);
+                HIPCHK(hipGetLastError());
+                HIPCHK(hipEventRecord(e[3], L.s));
+            } else {
                 // shadow queries of queue set q on s2, after the counter resets
                 HIPCHK(hipStreamWaitEvent(s2, e[0], 0));
                 HIPCHK(hipEventRecord(e[2], s2));
@@ -1832,32 +1725,166 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
                     else hipLaunchKernelGGL((k_trace_pt<true, false>), dim3(ptGridS), dim3(kTraceBlock), 0, s2, c->S, P, q, c->refill, c->ring, spillS);
                 }
                 HIPCHK(hipGetLastError());
-                T.launches[K_CLOSEST]++;
-                T.launches[K_SHADOW]++;
                 HIPCHK(hipEventRecord(e[1], L.s));
                 HIPCHK(hipEventRecord(e[3], s2));
                 HIPCHK(hipStreamWaitEvent(L.s, e[3], 0));
-                HIPCHK(hipEventRecord(e[4], L.s));
-                L.P.pass = (L.P.pass + 1) % 3;
-                HIPCHK(drain_list(L, r.drain, r.cap));
-                HIPCHK(kShade(r.drain ? r.liveGrid : r.grid, L.s, c->S, P, r.src, nq, Lout));
-                if (dl) {
-                    const int g = r.drain ? r.liveGrid : r.grid;
-                    HIPCHK(kNee(g, L.s, c->S, L.P, nq));
-                    HIPCHK(kSpec(g, L.s, c->S, L.P, r.src, nq, Lout));
-                }
-                if (mtList) HIPCHK(launch_mt_init(L.s, P, nq));
-                T.launches[K_SHADE]++;
-                HIPCHK(hipEventRecord(e[5], L.s));
-                T.passes++;
-                r.passes++;
-                r.listPasses += r.drain ? 1 : 0;
-                q = nq;
             }
-            r.q = q;
-            HIPCHK(hipMemcpyAsync(L.hostCnt, P.cnt, CNT_WORDS * 4, hipMemcpyDeviceToHost, L.s));
-            HIPCHK(hipEventRecord(L.done, L.s));
+            T.launches[K_CLOSEST]++;
+            T.launches[K_SHADOW]++;
+            HIPCHK(hipEventRecord(e[4], L.s));
+            L.P.pass = (L.P.pass + 1) % 3;
+            HIPCHK(drain_list(L, r.drain, r.cap));
+            HIPCHK(kShade(r.drain ? r.liveGrid : r.grid, L.s, c->S, P, r.src, nq, Lout));
+            if (dl) {
+                const int g = r.drain ? r.liveGrid : r.grid;
+                HIPCHK(kNee(g, L.s, c->S, L.P, nq));
+                HIPCHK(kSpec(g, L.s, c->S, L.P, r.src, nq, Lout));
+            }
+            if (mtList) HIPCHK(launch_mt_init(L.s, P, nq));
+            T.launches[K_SHADE]++;
+            HIPCHK(hipEventRecord(e[5], L.s));
+            T.passes++;
+            r.passes++;
+            r.listPasses += r.drain ? 1 : 0;
+            q = nq;
         }
+        r.q = q;
+        return close_batch(r, bi, Batch{n, false, r.drain, r.liveGrid, q});
+    };
+    HIPCHK(hipEventRecord(c->ev[0], c->stream));   // the other lanes start after the work queued so far
+    for (int l = 0; l < nl; ++l) {
+        Run &r = R[l];
+        Lane &L = c->lane[l];
+        r.L = &L;
+        r.src = src;
+        const uint32_t lo = (uint32_t)((uint64_t)src.nItems * l / nl), hi = (uint32_t)((uint64_t)src.nItems * (l + 1) / nl);
+        r.src.base = src.base + lo;
+        r.src.nItems = hi - lo;
+        r.cap = lane_slots(r.src.nItems, nl);
+        if (dl)   // the frame stacks and light-sample batches: at most 24 GiB per lane
+            r.cap = (int)std::max<size_t>(64, std::min<size_t>((size_t)r.cap, ((size_t)24 << 30) /
+                                                               (frame_bytes(NB) * nFrames + batch_bytes(NB) * batch)));
+        if (mtExt && !getenv("PBRTGPU_SLOTS")) r.cap = std::min(r.cap, 1 << 20);   // 2.5 KiB of MT state per slot
+        r.cap = std::min(r.cap, max_slots_32bit(NB, batch));
+        r.grid = (r.cap + kShadeBlock - 1) / kShadeBlock;
+        r.q = 0;
+        r.done = false;
+        r.drain = false;
+        r.ending = false;
+        r.tailed = false;
+        r.liveGrid = r.grid;
+        r.listPasses = 0;
+        r.head = 0;
+        r.inflight = 0;
+        L.P.listMode = 0;
+        L.P.xcdMap = xcd_map_on();
+        // drain bound of this run: a path lives at most pathPasses passes, so every slot
+        // takes a new item at least once per pathPasses passes while items remain; twice
+        // that, plus the overshoot of the enqueued batches, means the wavefront is stuck
+        r.passes = 0;
+        r.maxPasses = (int)std::min<int64_t>(INT32_MAX / 2, 2 * ((r.src.nItems + r.cap - 1) / r.cap + 1) * pathPasses) +
+                      4 * kPassBatch;
+        if (int e = ensure_slots(&L, r.cap, NB, c->S.nInsts, nFrames, batch, mtExt)) return e;
+        HIPCHK(L.spill.ensure(2 * spillLane * sizeof(uint2)));
+        if (l > 0) HIPCHK(hipStreamWaitEvent(L.s, c->ev[0], 0));
+        if (const int pb = poison_byte(); pb >= 0) {
+            HIPCHK(hipMemsetAsync(L.slots.p, pb, L.slots.n, L.s));
+            HIPCHK(hipMemsetAsync(L.spill.p, pb, L.spill.n, L.s));
+        }
+        HIPCHK(hipMemsetAsync(L.P.item, 0xff, (size_t)r.cap * 4, L.s));
+        HIPCHK(hipMemsetAsync(L.P.cnt, 0, CNT_WORDS * 4, L.s));
+        {   // the per-wave writer masks start empty: k_shade loads a wave's masks before it knows
+            // which of them its lanes will use (wave_masks), so none is read unwritten
+            const size_t W = (size_t)((r.cap + 63) / 64) * 8;
+            HIPCHK(hipMemsetAsync(L.P.aMask, 0, 2 * W, L.s));
+            HIPCHK(hipMemsetAsync(L.P.bMask, 0, 3 * W, L.s));
+            HIPCHK(hipMemsetAsync(L.P.mMask, 0, 2 * W, L.s));
+        }
+        // pass 0: every slot is free -> regeneration fills them with camera rays (queue 0)
+        HIPCHK(hipEventRecord(L.ev[0][0], L.s));
+        L.P.pass = 0;   // k_shade pass index (mod 3) of this run: the beta buffers rotate with it
+        HIPCHK(kShade(r.grid, L.s, c->S, L.P, r.src, 0, Lout));
+        HIPCHK(hipEventRecord(L.ev[0][1], L.s));
+        if (int e = close_batch(r, 0, Batch{0, true, false, r.grid, 0})) return e;
+        // ... and the first batch of passes right behind it: after pass 0 the slots hold the first
+        // min(cap, items) items (every slot regenerated), each with its camera ray queued
+        uint32_t c0[CNT_WORDS] = {};
+        c0[CNT_NEXT] = (uint32_t)std::min<uint64_t>((uint64_t)r.cap, r.src.nItems);
+        c0[CNT_QC(0)] = (uint32_t)r.cap;
+        if (int e = enqueue(r, c0, 0)) return e;
+    }
+    int live = nl;
+    float m;
+    int rr = 0;   // round-robin start of the lane poll
+    while (live > 0) {
+        // the next lane whose oldest batch has completed: the host never blocks on one lane while
+        // the other lane's queue has run dry (it would idle until that wait ended)
+        int l = -1;
+        int spins = 0;
+        for (;;) {
+            for (int k = 0; k < nl && l < 0; ++k) {
+                const int i = (rr + k) % nl;
+                if (R[i].done) continue;
+                const hipError_t qe = hipEventQuery(R[i].L->done[R[i].head]);
+                if (qe == hipSuccess) l = i;
+                else if (qe != hipErrorNotReady) HIPCHK(qe);
+            }
+            if (l >= 0) break;
+            // a few empty polls, then short sleeps: a batch of passes takes milliseconds, and a host
+            // thread per device (render_multi) should not burn a core for the whole frame
+            if (++spins > 64) std::this_thread::sleep_for(std::chrono::microseconds(20));
+            else std::this_thread::yield();
+        }
+        rr = l + 1;
+        Run &r = R[l];
+        Lane &L = *r.L;
+        const int bi = r.head;
+        const Batch B = r.b[bi];
+        uint32_t cnt[CNT_WORDS];
+        memcpy(cnt, L.hostCnt[bi], sizeof(cnt));
+        r.head ^= 1;
+        r.inflight--;
+        if (B.single) {
+            HIPCHK(hipEventElapsedTime(&m, L.ev[bi][0], L.ev[bi][1])); T.ms[K_SHADE] += m;
+            T.launches[K_SHADE]++;
+        }
+        for (int j = 0; j < B.n; ++j) {
+            hipEvent_t *e = L.ev[bi] + 2 + 6 * j;
+            float mc, ms, mh;
+            HIPCHK(hipEventElapsedTime(&mc, e[0], e[1])); T.ms[K_CLOSEST] += mc;
+            HIPCHK(hipEventElapsedTime(&ms, e[2], e[3])); T.ms[K_SHADOW] += ms;
+            HIPCHK(hipEventElapsedTime(&mh, e[4], e[5])); T.ms[K_SHADE] += mh;
+            if (pass_log())   // diagnostics: per-pass device time of each lane
+                fprintf(stderr, "pass_log lane %d closest %.3f shadow %.3f shade %.3f\n", l, mc, ms, mh);
+        }
+        if (pass_log())
+            fprintf(stderr, "pass_log lane %d batch of %d%s: closest queue %u shadow queue %u items taken %u of %u%s\n", l,
+                    B.n, B.single ? " (single launch)" : "", cnt[CNT_QC(B.qEnd)], cnt[CNT_QS(B.qEnd)], cnt[CNT_NEXT],
+                    r.src.nItems, B.drain ? " (drain list)" : "");
+        if (cnt[CNT_ERR] & 1u) return fail(PBRTGPU_E_STATE, "a path drew past 227 MT19937 outputs without its state row");
+        if (cnt[CNT_ERR] & 2u) return fail(PBRTGPU_E_STATE, "drain: a pass's live list exceeded its shade grid");
+        if (cnt[CNT_ERR] & 4u) return fail(PBRTGPU_E_STATE, "tail: the live list exceeded the tail kernel's grid");
+        if (cnt[CNT_ERR] & 8u) return fail(PBRTGPU_E_STATE, "tail: a path was still live after the tail kernel's steps");
+        // every live slot ends a pass with a ray queued, so the drain's list fits the grid sized
+        // from the queue sizes of an earlier read-back; a longer list would leave slots unshaded
+        // (their beta / A / B buffers then rotate under them): refuse instead
+        if (B.drain && !B.single && (uint64_t)cnt[CNT_LIVE] > (uint64_t)B.liveGrid * kShadeBlock)
+            return fail(PBRTGPU_E_STATE, "drain: more live slots than the shade grid covers");
+        if (cnt[CNT_QC(B.qEnd)] == 0 && cnt[CNT_QS(B.qEnd)] == 0) r.ending = true;   // nothing queued: empty from here on
+        if (r.ending || r.tailed) {
+            if (r.inflight > 0) continue;   // the batch behind it (empty passes, or the tail) completes first
+            if (!r.ending) return fail(PBRTGPU_E_STATE, "tail: paths left after the tail kernel");
+            r.done = true;
+            --live;
+            uint64_t w[W_COUNT];
+            HIPCHK(hipMemcpy(w, L.P.cnt + CNT_WORK, sizeof(w), hipMemcpyDeviceToHost));
+            if (countWork)
+                for (int i = 0; i < W_COUNT; ++i) T.work[i] += w[i];
+            if (zeroedOut) *zeroedOut += cnt[CNT_ZEROED];
+            continue;
+        }
+        if (r.passes > r.maxPasses) return fail(PBRTGPU_E_STATE, "wavefront did not drain");
+        if (int e = enqueue(r, cnt, B.qEnd)) return e;
     }
     if (c->S.specMode == 1) {   // the rows' luminance guard once every band of them is in
         for (int l = 1; l < nl; ++l) {
@@ -1905,9 +1932,11 @@ int pbrtgpu_context_create(int device, pbrtgpu_ctx **out) {
         if (l == 0) L.s = c->stream;
         else ok = hipStreamCreateWithFlags(&L.s, hipStreamNonBlocking) == hipSuccess;
         ok = ok && hipStreamCreateWithFlags(&L.s2, hipStreamNonBlocking) == hipSuccess;
-        for (int i = 0; i < 2 + 6 * 8 && ok; ++i) ok = hipEventCreate(&L.ev[i]) == hipSuccess;
-        ok = ok && hipEventCreateWithFlags(&L.done, hipEventDisableTiming) == hipSuccess;
-        ok = ok && hipHostMalloc((void **)&L.hostCnt, CNT_WORDS * 4, hipHostMallocDefault) == hipSuccess;
+        for (int b = 0; b < 2; ++b) {
+            for (int i = 0; i < 2 + 6 * 8 && ok; ++i) ok = hipEventCreate(&L.ev[b][i]) == hipSuccess;
+            ok = ok && hipEventCreateWithFlags(&L.done[b], hipEventDisableTiming) == hipSuccess;
+            ok = ok && hipHostMalloc((void **)&L.hostCnt[b], CNT_WORDS * 4, hipHostMallocDefault) == hipSuccess;
+        }
     }
     if (!ok) {
         delete c;
@@ -1933,11 +1962,13 @@ int pbrtgpu_context_destroy(pbrtgpu_ctx *c) {
         if (L.s2) (void)hipStreamSynchronize(L.s2);
         L.slots.release();
         L.spill.release();
-        for (hipEvent_t e : L.ev) if (e) (void)hipEventDestroy(e);
-        if (L.done) (void)hipEventDestroy(L.done);
+        for (int b = 0; b < 2; ++b) {
+            for (hipEvent_t e : L.ev[b]) if (e) (void)hipEventDestroy(e);
+            if (L.done[b]) (void)hipEventDestroy(L.done[b]);
+            if (L.hostCnt[b]) (void)hipHostFree(L.hostCnt[b]);
+        }
         if (L.s2) (void)hipStreamDestroy(L.s2);
         if (L.s && L.s != c->stream) (void)hipStreamDestroy(L.s);
-        if (L.hostCnt) (void)hipHostFree(L.hostCnt);
     }
     (void)hipStreamDestroy(c->stream);
     delete c;

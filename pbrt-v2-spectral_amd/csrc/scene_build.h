@@ -352,6 +352,22 @@ static inline int scene_check(const pbrtgpu_flat_scene *s, std::string *err) {
     if (!s->rgb_basis || !s->ewa_lut) SB_FAIL(PBRTGPU_E_INVALID, "rgb_basis / ewa_lut missing");
     // texture graph: SCALE nodes combine CONST / IMAGE leaves; a material's spectrum slot is an
     // IMAGE or SCALE(IMAGE, CONST) spectrum texture, its bump a float texture
+    // a leaf of a combining node (SCALE, MIX, CHECKER, DOTS): exactly the kinds the device evaluates
+    // as leaves -- spectral: CONST / IMAGE / UV (spec_leaf -> leaf_rgb); float: CONST / IMAGE and the
+    // noise textures (tex_leaf_float) -- with a valid mapping and octave count.  Checked against
+    // this list rather than against refused kinds, so a node kind added later is refused as a leaf
+    // until the device evaluates it there.
+    auto leafOk = [&](int o, int spectral) -> bool {
+        if (o < 0 || o >= s->n_textures || !s->textures) return false;
+        const pbrtgpu_texture &l = s->textures[o];
+        if (l.spectral != spectral) return false;
+        const int ty = l.type;
+        const bool noise = ty >= PBRTGPU_TEX_FBM && ty <= PBRTGPU_TEX_WINDY;
+        const bool ok = ty == PBRTGPU_TEX_CONST || ty == PBRTGPU_TEX_IMAGE || (spectral ? ty == PBRTGPU_TEX_UV : noise);
+        if (!ok) return false;
+        if (noise && (l.levels < 0 || l.levels > 64)) return false;
+        return l.mapping >= PBRTGPU_MAP_UV && l.mapping <= PBRTGPU_MAP_PLANAR;
+    };
     auto texOk = [&](int id, int spectral, bool slot) -> bool {
         if (id < 0 || id >= s->n_textures || !s->textures) return false;
         const pbrtgpu_texture &t = s->textures[id];
@@ -368,11 +384,8 @@ static inline int scene_check(const pbrtgpu_flat_scene *s, std::string *err) {
                 return false;
         }
         if (t.type == PBRTGPU_TEX_MIX) {   // two CONST / IMAGE / UV leaves, a CONST / IMAGE float amount
-            for (int o : {t.tex1, t.tex2}) {
-                if (o < 0 || o >= s->n_textures || s->textures[o].spectral != spectral) return false;
-                const int ty = s->textures[o].type;
-                if (ty != PBRTGPU_TEX_CONST && ty != PBRTGPU_TEX_IMAGE && ty != PBRTGPU_TEX_UV) return false;
-            }
+            for (int o : {t.tex1, t.tex2})
+                if (!leafOk(o, spectral) || s->textures[o].type > PBRTGPU_TEX_UV) return false;
             const int a = t.amount;
             if (a < 0 || a >= s->n_textures || s->textures[a].spectral ||
                 (s->textures[a].type != PBRTGPU_TEX_CONST && s->textures[a].type != PBRTGPU_TEX_IMAGE))
@@ -380,12 +393,8 @@ static inline int scene_check(const pbrtgpu_flat_scene *s, std::string *err) {
         }
         if (t.type == PBRTGPU_TEX_UV && !spectral) return false;   // UVTexture is Texture<Spectrum> only
         if (t.type == PBRTGPU_TEX_CHECKER || t.type == PBRTGPU_TEX_DOTS) {   // two CONST / IMAGE / UV leaves
-            for (int o : {t.tex1, t.tex2}) {
-                if (o < 0 || o >= s->n_textures || s->textures[o].spectral != spectral) return false;
-                if (s->textures[o].type != PBRTGPU_TEX_CONST && s->textures[o].type != PBRTGPU_TEX_IMAGE &&
-                    s->textures[o].type != PBRTGPU_TEX_UV)
-                    return false;
-            }
+            for (int o : {t.tex1, t.tex2})
+                if (!leafOk(o, spectral) || s->textures[o].type > PBRTGPU_TEX_UV) return false;
             if (t.aamode < 0 || t.aamode > 1) return false;
         }
         if (t.type != PBRTGPU_TEX_IMAGE && t.type != PBRTGPU_TEX_CHECKER && t.type != PBRTGPU_TEX_UV &&
@@ -393,13 +402,8 @@ static inline int scene_check(const pbrtgpu_flat_scene *s, std::string *err) {
             return false;
         if (t.mapping < PBRTGPU_MAP_UV || t.mapping > PBRTGPU_MAP_PLANAR) return false;
         if (t.type == PBRTGPU_TEX_SCALE) {
-            for (int o : {t.tex1, t.tex2}) {
-                if (o < 0 || o >= s->n_textures || s->textures[o].spectral != spectral) return false;
-                if (s->textures[o].type == PBRTGPU_TEX_SCALE || s->textures[o].type == PBRTGPU_TEX_CHECKER ||
-                    s->textures[o].type == PBRTGPU_TEX_MIX || s->textures[o].type == PBRTGPU_TEX_DOTS ||
-                    s->textures[o].type == PBRTGPU_TEX_BILERP || s->textures[o].type == PBRTGPU_TEX_MARBLE)
-                    return false;
-            }
+            for (int o : {t.tex1, t.tex2})
+                if (!leafOk(o, spectral)) return false;
             if (spectral && (s->textures[t.tex1].type == PBRTGPU_TEX_CONST) == (s->textures[t.tex2].type == PBRTGPU_TEX_CONST))
                 return false;
         }

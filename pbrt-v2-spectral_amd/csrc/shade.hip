@@ -398,6 +398,8 @@ __global__ __launch_bounds__(kTailBlock) void k_tail(DevScene S, PathSoA P0, int
     st.tbase = reinterpret_cast<float *>(stk + (size_t)depth * blockDim.x) + threadIdx.x;
     st.stride = blockDim.x;
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    // a live list longer than the grid would leave paths unfinished (read as drained): CNT_ERR bit 2
+    if (i == 0 && P.cnt[CNT_LIVE] > gridDim.x * blockDim.x) atomicOr(&P.cnt[CNT_ERR], 4u);
     if (i >= P.cnt[CNT_LIVE]) return;
     const int slot = (int)P.live[i];
     const uint32_t rc = (uint32_t)P.rcap;
@@ -429,6 +431,9 @@ __global__ __launch_bounds__(kTailBlock) void k_tail(DevScene S, PathSoA P0, int
         if (done) P.item[slot] = -1;
         else if (pu.t) mt_window_init(P, (uint32_t)slot);   // vertex 3 draws first (k_mt_init's list)
     }
+    // still live after maxSteps (a path lives at most maxdepth + 3 passes): its radiance would be
+    // lost with nothing queued -- CNT_ERR bit 3, which the host turns into PBRTGPU_E_STATE
+    if (P.item[slot] >= 0) atomicOr(&P.cnt[CNT_ERR], 8u);
 }
 template <int NB, int FEAT>
 hipError_t launch_tail(int grid, hipStream_t stream, const DevScene &S, const PathSoA &P, int q, float *Lout,

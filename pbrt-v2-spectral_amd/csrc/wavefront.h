@@ -72,7 +72,8 @@ enum { RAY_C = 0, RAY_M = 1, RAY_S = 2 };
 #define CNT_QT(q) (224 + 32 * (q))    // MT-window list size (qT): k_mt_init of set q clears set q ^ 1
 // CNT_ERR: bit 0 when a path drew past MT output 227 without its full-state row (mt_store), bit 1
 // when a drain pass's live list was longer than its grid (k_shade LIST: slots left unshaded), which
-// the host turns into PBRTGPU_E_STATE instead of a silently wrong radiance; CNT_DLN: entries of
+// the host turns into PBRTGPU_E_STATE instead of a silently wrong radiance; k_tail (shade.hip): bit 2
+// when its live list was longer than its grid, bit 3 when a path was still live after its steps; CNT_DLN: entries of
 // the DirectLighting light-sample list (PathSoA::dlList) of this pass
 enum { CNT_NEXT = 128, CNT_ZEROED = 160, CNT_WORK = 192, CNT_LIVE = 288, CNT_ERR = 320, CNT_DLN = 352, CNT_WORDS = 384 };
 enum { W_RAYS = 0, W_SHADOW = 1, W_NODES_C = 2, W_NODES_S = 3, W_TRIS_C = 4, W_TRIS_S = 5, W_QUADS_C = 6, W_QUADS_S = 7,

@@ -1234,10 +1234,15 @@ private:
         if (out->textures[f.tex].type != PBRTGPU_TEX_IMAGE && out->textures[f.tex].type != PBRTGPU_TEX_UV) throw std::runtime_error("checkerboard operands other than constants and image maps are not supported yet");
         return f.tex;
     }
-    // operand of a ScaleTexture: a CONST or IMAGE node
+    // operand of a ScaleTexture<float>: a CONST, IMAGE or noise (fbm / wrinkled / windy) node -- the
+    // leaf kinds the device evaluates (device.h tex_leaf_float; scene_build.h leafOk)
     int FloatLeaf(const FloatTex &f) {
         if (!f.constant) {
-            if (out->textures[f.tex].type == PBRTGPU_TEX_SCALE) throw std::runtime_error("nested scale textures are not supported yet");
+            const int ty = out->textures[f.tex].type;
+            if (ty == PBRTGPU_TEX_SCALE) throw std::runtime_error("nested scale textures are not supported yet");
+            if (ty != PBRTGPU_TEX_IMAGE && !(ty >= PBRTGPU_TEX_FBM && ty <= PBRTGPU_TEX_WINDY))
+                throw std::runtime_error("scale texture operands other than constants, image maps and noise "
+                                         "textures are not supported yet");
             return f.tex;
         }
         pbrtgpu_texture t = TexNode(PBRTGPU_TEX_CONST, false);

@@ -6,18 +6,25 @@
 #include <cstdio>
 #include <algorithm>
 #include <cstring>
+#include <string>
 #include <zlib.h>
 
 namespace pbrtamd {
 
 static const char kMagic[8] = {'P', 'B', 'R', 'T', 'P', 'A', 'C', 'K'};
-static const uint32_t kVersion = 15;   // 6: + merl tables; 7: + metadata ids; 8: + Renderer; 9: + lens diffraction;
+static const uint32_t kVersion = 16;   // 6: + merl tables; 7: + metadata ids; 8: + Renderer; 9: + lens diffraction;
                                        // 10: + pinhole array / microlens / eye IOR; 11: image maps as MIPMap
                                        // pyramids (texture records + texel pool); 12: material normal maps
                                        // (normal_tex, a former pad word: -1 for older packs); 13: an animated
                                        // camera's CameraToWorld; 14: textured float parameters (ftex, the
                                        // former pad words: -1 for older packs); 15: decoded environment maps
-                                       // (light map_tex / dist_off, former pad words: -1); 5-14 still load
+                                       // (light map_tex / dist_off, former pad words: -1); 16: the texture
+                                       // record's size ahead of the texture array.  The record grew
+                                       // within v15 (amount, aamode, mapping + map[16]: ABI 16), so a
+                                       // v11-v15 pack holding textures has an unknown record layout and is
+                                       // refused (re-pack it); without textures v5-v15 still load
+
+static const uint32_t kTexRecord = (uint32_t)sizeof(pbrtgpu_texture);   // v16: written ahead of the textures
 
 // the texture record of packs before v11: one MIPMap texel inline (the one-texel maps they held)
 struct TexV10 {
@@ -83,7 +90,7 @@ bool SavePack(const HostScene &s, const std::string &path, std::string *err) {
     ok = ok && WArr(f, s.bandY) && WArr(f, s.nodes) && WArr(f, s.prims) && WArr(f, s.tris) && WArr(f, s.meshes) &&
          WArr(f, s.vertP) && WArr(f, s.vertN) && WArr(f, s.vertUV) && WArr(f, s.quadrics) && WArr(f, s.materials) &&
          WArr(f, s.lights) && WArr(f, s.lightShapes) && WArr(f, s.spectra) && WArr(f, s.instances) &&
-         WArr(f, s.primInstance) && WArr(f, s.kdnodes) && WArr(f, s.textures) && WArr(f, s.ewaLut) &&
+         WArr(f, s.primInstance) && WArr(f, s.kdnodes) && W(f, &kTexRecord, 4) && WArr(f, s.textures) && WArr(f, s.ewaLut) &&
          WArr(f, s.rgbBasis) && WArr(f, s.merl);
     int32_t integ[2] = {s.integrator, s.dlStrategy};
     ok = ok && W(f, integ, 8);
@@ -123,7 +130,25 @@ bool LoadPack(const std::string &path, HostScene *s, std::string *err) {
          RArr(f, s->lights) && RArr(f, s->lightShapes) && RArr(f, s->spectra) && RArr(f, s->instances) &&
          RArr(f, s->primInstance) && RArr(f, s->kdnodes);
     std::vector<TexV10> oldTex;
-    ok = ok && (ver >= 11 ? RArr(f, s->textures) : RArr(f, oldTex));
+    bool texLayout = true;
+    if (ok && ver >= 16) {
+        uint32_t rec = 0;
+        ok = R(f, &rec, 4);
+        texLayout = rec == kTexRecord;
+    } else if (ok && ver >= 11) {   // v11-v15: the record's layout is not recorded; only an empty array is safe
+        uint64_t n = 0;
+        ok = R(f, &n, 8);
+        texLayout = n == 0;
+        s->textures.clear();
+    }
+    if (ok && !texLayout) {
+        gzclose(f);
+        if (err)
+            *err = "scene pack " + path + " holds texture records of another layout (pack version " + std::to_string(ver) +
+                   "; this build reads v16 records of " + std::to_string(kTexRecord) + " bytes): re-pack the scene";
+        return false;
+    }
+    ok = ok && (ver >= 16 ? RArr(f, s->textures) : ver >= 11 ? true : RArr(f, oldTex));
     ok = ok && RArr(f, s->ewaLut) && RArr(f, s->rgbBasis);
     s->texels.clear();
     if (ok && ver < 11) {   // each one-texel map becomes a 1x1 pyramid in the texel pool

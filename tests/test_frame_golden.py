@@ -1,5 +1,5 @@
-"""Whole-frame parity at the configs' REAL resolution and sample count (BASELINE.json configs 2
-and 5, and 4 where generated; north star: image error vs the CPU reference).
+"""Whole-frame parity at the configs' REAL resolution and sample count (BASELINE.json configs 1-5:
+C1 in the reference's RGB build; north star: image error vs the CPU reference).
 
 The fixtures (tools/make_frame_golden.py) hold, for every 16x16 tile of the reference harness's
 film at full size and spp, a blake2b-64 hash of the tile's float32 bits, its float64 sum and its
@@ -24,20 +24,28 @@ from conftest import GOLDEN, PACKS, ROOT
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 from make_frame_golden import tile_digest  # noqa: E402
 
-FRAMES = ["killeroo_frame_c2_700x700s256", "anim_frame_c5_600x600s512", "metal_frame_c4_400x400s4096"]
+FRAMES = ["killeroo_frame_c2_700x700s256", "anim_frame_c5_600x600s512", "metal_frame_c4_400x400s4096",
+          "killeroo_rgb_frame_c1_400x400s64", "bunny_frame_c3_1920x1080s1024"]
+# the scene pack of a frame (its name's prefix before "_frame"): C1 is the reference's RGB build
 PACK = {"killeroo": "killeroo-simple.pack", "bunny": "bunny.pack", "metal": "metal.pack",
-        "anim": "anim-killeroos-moving.pack"}
+        "anim": "anim-killeroos-moving.pack", "killeroo_rgb": "killeroo-simple-rgb.pack"}
 # tiles (tx, ty) the CPU test renders with the oracle: a frame corner, a tile of the right /
-# bottom border (partial tiles: 700 = 43 * 16 + 12), and two interior tiles
+# bottom border (partial tiles: 700 = 43 * 16 + 12), and two interior tiles (C3: 1 M paths per
+# tile at 1024 spp, so two tiles)
 CPU_TILES = {"killeroo": [(0, 0), (43, 43), (5, 2), (7, 19)], "anim": [(0, 0), (37, 37), (8, 16)],
-             "metal": [(0, 0), (24, 24), (7, 8)]}
+             "metal": [(0, 0), (24, 24), (7, 8)], "killeroo_rgb": [(0, 0), (24, 24), (6, 9), (12, 13)],
+             "bunny": [(0, 0), (60, 34)]}
+
+
+def _key(name):
+    return name.split("_frame")[0]
 AVAILABLE = [n for n in FRAMES if os.path.exists(os.path.join(GOLDEN, n + ".npz"))]
 
 
 def _load(pg, name):
     g = np.load(os.path.join(GOLDEN, name + ".npz"))
     w, h, spp, seed, md, bands, tile = [int(v) for v in g["config"]]
-    scene = pg.Scene.load(os.path.join(PACKS, PACK[name.split("_")[0]]), xres=w, yres=h, spp=spp, maxdepth=md,
+    scene = pg.Scene.load(os.path.join(PACKS, PACK[_key(name)]), xres=w, yres=h, spp=spp, maxdepth=md,
                           seed=seed)
     assert scene.bands == bands and tile == 16
     return g, scene
@@ -62,7 +70,7 @@ def test_frame_tiles_oracle_bit_exact_vs_reference(pg, name):
     of a window one pixel larger): their hashes are the reference frame's."""
     g, scene = _load(pg, name)
     o = pg.oracle(libm_float=True)
-    for tx, ty in CPU_TILES[name.split("_")[0]]:
+    for tx, ty in CPU_TILES[_key(name)]:
         x0, y0 = 16 * tx, 16 * ty
         x1, y1 = min(x0 + 16, scene.width), min(y0 + 16, scene.height)
         film, _ = o.render(scene, window=(x0 - 1, x1 + 1, y0 - 1, y1 + 1), threads=min(16, os.cpu_count() or 8))

@@ -409,3 +409,22 @@ def test_gpupath_dat_fixture_vs_oracle(pg, tmp_path):
     m2 = mine.index(b"\n", m1) + 1
     assert ref[:r1] == mine[:m1] == b"%d %d %d\n" % (W, H, s.bands)
     assert ref[r1:] == mine[m2:]
+
+
+def test_pack_v15_layouts(pg):
+    """Pack v16 writes the texture record's size ahead of the texture array.  pbrtgpu_texture grew
+    within v15 (amount, aamode, mapping + map[16]), so a v15 pack's texture records have an
+    unknown layout: a v15 pack holding textures is refused with a re-pack message, a v15 pack
+    without textures loads to the same flattened scene as its v16 re-pack (fixtures: the round-5
+    v15 packs of checker.pbrt and lights.pbrt, written by this front end)."""
+    from conftest import GOLDEN
+    with pytest.raises(RuntimeError, match="re-pack"):
+        pg.Scene.load(os.path.join(GOLDEN, "pack_v15_checker.pack"))
+    old = pg.Scene.load(os.path.join(GOLDEN, "pack_v15_lights.pack"))
+    new = pg.Scene.load(os.path.join(PACKS, "lights.pack"))
+    a, b = flat_arrays(old), flat_arrays(new)
+    for k in a:
+        assert np.array_equal(a[k], b[k]), k
+    assert new.flat.n_textures == old.flat.n_textures == 0
+    chk = pg.Scene.load(os.path.join(PACKS, "checker.pack"))
+    assert chk.flat.n_textures > 0

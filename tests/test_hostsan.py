@@ -217,3 +217,30 @@ def test_replay_under_sanitizers(pg, tmp_path, variant):
         Lo = pg.oracle().trace_paths(scene, _keys(scene))
         L = _replay(exe, os.path.join(PACKS, pack), tmp_path, **a).reshape(Lo.shape)
         assert np.array_equal(L.view(np.int32), Lo.view(np.int32))
+
+
+def test_scene_check_refuses_leaf_kinds_the_device_cannot_evaluate(pg, tmp_path):
+    """scene_check (scene_build.h) admits as leaves of a combining texture (SCALE, MIX, CHECKER,
+    DOTS) only the kinds the device evaluates there: a spectral SCALE over a noise node (whose
+    `levels` is an octave count and whose width / height are 0) would reach tex_image<3> through
+    spec_leaf -> leaf_rgb and index texels[] modulo 0.  The front end never builds that graph; a
+    pack is untrusted input, so the check refuses it before any upload (the host replay runs the
+    same scene_check the GPU upload does)."""
+    import ctypes
+    exe = _build("shade_host")
+    s = pg.Scene.load(os.path.join(PACKS, "textured.pack"), xres=8, yres=6, spp=1)
+    f = s.flat
+    rec = np.frombuffer((ctypes.c_char * (f.n_textures * 148)).from_address(f.textures), dtype=np.int32).reshape(-1, 37)
+    scale = [i for i in range(f.n_textures) if rec[i, 0] == 2 and rec[i, 1] == 1]   # spectral SCALE nodes
+    assert scale
+    t1, t2 = rec[scale[0], 2], rec[scale[0], 3]
+    leaf = t1 if rec[t1, 0] != 0 else t2          # its image leaf (the other one is the CONST)
+    ok = str(tmp_path / "ok.pack")
+    s.save_pack(ok)
+    _replay(exe, ok, tmp_path)                     # as built: admitted and rendered
+    rec[leaf, 0] = 7                               # PBRTGPU_TEX_FBM, spectral: SCALE(FBM, CONST)
+    rec[leaf, 11] = 8                              # a valid octave count: only the leaf kind is wrong
+    bad = str(tmp_path / "bad.pack")
+    s.save_pack(bad)
+    r = subprocess.run([exe, bad, "--out", str(tmp_path / "L.f32")], capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0 and "scene:" in r.stderr and "texture" in r.stderr, r.stderr[-2000:]

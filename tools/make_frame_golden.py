@@ -12,7 +12,7 @@ in the reference's order.  The committed fixture is small:
 
 tests/test_frame_golden.py renders the same frame on the GPU and compares every tile's hash.
 
-Usage: python tools/make_frame_golden.py [c2|c4|c5|c3 ...] [--jobs 8]
+Usage: python tools/make_frame_golden.py [c1|c2|c4|c5|c3 ...] [--jobs 8]
 """
 import hashlib
 import os
@@ -25,11 +25,13 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "tools"))
-from make_golden import HARNESS, HARNESS60, SCENES, OUT  # noqa: E402
+from make_golden import HARNESS, HARNESS60, HARNESSRGB, SCENES, OUT  # noqa: E402
 
 TILE = 16
 # name, scene file, W, H, spp, bands
-FRAMES = {"c2": ("killeroo_frame_c2_700x700s256", "killeroo-simple.pbrt", 700, 700, 256, 32),
+# bands 3 = the reference's RGBSpectrum build (C1, BASELINE configs[0]; oracle/_ref/brgb)
+FRAMES = {"c1": ("killeroo_rgb_frame_c1_400x400s64", "killeroo-simple.pbrt", 400, 400, 64, 3),
+          "c2": ("killeroo_frame_c2_700x700s256", "killeroo-simple.pbrt", 700, 700, 256, 32),
           "c3": ("bunny_frame_c3_1920x1080s1024", "bunny.pbrt", 1920, 1080, 1024, 32),
           "c4": ("metal_frame_c4_400x400s4096", "metal.pbrt", 400, 400, 4096, 60),
           "c5": ("anim_frame_c5_600x600s512", "anim-killeroos-moving.pbrt", 600, 600, 512, 32)}
@@ -52,7 +54,7 @@ def tile_digest(film, tile=TILE):
 
 
 def render_frame(scene, W, H, spp, bands, jobs, tmp):
-    exe = HARNESS60 if bands == 60 else HARNESS
+    exe = {60: HARNESS60, 3: HARNESSRGB}.get(bands, HARNESS)
     strips = np.linspace(0, H, jobs + 1).astype(int)
     procs = []
     for j in range(jobs):
