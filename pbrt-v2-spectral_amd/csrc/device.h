@@ -318,6 +318,7 @@ struct DevScene {
     const int *leafOf;                // per first primitive of a leaf: the binary leaf node (quant_w4)
     const pbrtgpu_prim *prims;
     const DevTri *primTri;            // per prim (triangles only meaningful)
+    const float4 *primRec;            // per prim: its shading record, 8 float4 (PrimRec below)
     const pbrtgpu_triangle *tris;
     const pbrtgpu_mesh *meshes;
     const float *vertP, *vertN, *vertUV;
@@ -485,6 +486,94 @@ PGD_INLINE void tri_shading(const DevScene &S, int ti, const float *nmat, const 
     }
     dg_init(dgs, dg.p, ss, ts, xnormal(nmat, dndu), xnormal(nmat, dndv), dg.u, dg.v,
             m.reverse_orientation ^ m.swaps_handedness);
+}
+
+// Per-primitive shading record (scene_build.h, built at upload from the flattened scene): what
+// isect_fill and get_bsdf read of a hit, in one 128-byte line per primitive instead of the chain
+// prim -> triangle -> 3 vertices, 3 uvs, the mesh -> 3 normals (about 15 divergent cache-line
+// requests per lane over three dependent levels).  The values are the flattened scene's, so every
+// result is bit-identical:
+//   r[0..2]  {p_k.xyz, w}   the triangle's vertices; w = u0, v0, u1
+//   r[3..5]  {n_k.xyz, w}   its shading normals (mesh without normals: 0); w = v1, u2, v2
+//            (the uvs are the mesh's, or Triangle::GetUVs's defaults (0,0) (1,0) (1,1))
+//   r[6]     {shape_type, shape_index, material, area_light}   the pbrtgpu_prim
+//   r[7]     {flags, mesh, 0, 0}   flags: REC_NORMALS the mesh has normals, REC_FLIP reverse ^ swaps
+enum { REC_NORMALS = 2, REC_FLIP = 4 };
+PGD_INLINE const float4 *prim_rec(const DevScene &S, int prim) { return sa(S.primRec, (uint32_t)(8 * prim)); }
+PGD_INLINE int4 rec_prim(const float4 *rec) {
+    const float4 v = rec[6];
+    return make_int4(__float_as_int(v.x), __float_as_int(v.y), __float_as_int(v.z), __float_as_int(v.w));
+}
+// Triangle::Intersect (trianglemesh.cpp:119-199) of a known-hit triangle from its record:
+// tri_intersect's arithmetic, operand for operand
+PGD_INLINE bool tri_intersect_rec(const float4 *rec, const Ray &ray, float *tHit, float *rayEps, DG *dg) {
+    const float4 a = rec[0], b = rec[1], cc = rec[2];
+    V p1 = v3(a.x, a.y, a.z), p2 = v3(b.x, b.y, b.z), p3 = v3(cc.x, cc.y, cc.z);
+    V e1 = vsub(p2, p1), e2 = vsub(p3, p1);
+    V s1 = vcross(ray.d, e2);
+    float divisor = vdot(s1, e1);
+    if (divisor == 0.) return false;
+    float invDivisor = 1.f / divisor;
+    V d = vsub(ray.o, p1);
+    float b1 = vdot(d, s1) * invDivisor;
+    if (b1 < 0. || b1 > 1.) return false;
+    V s2 = vcross(d, e1);
+    float b2 = vdot(ray.d, s2) * invDivisor;
+    if (b2 < 0. || b1 + b2 > 1.) return false;
+    float tt = vdot(e2, s2) * invDivisor;
+    if (tt < ray.mint || tt > ray.maxt) return false;
+    if (!dg) { *tHit = tt; return true; }
+    const float4 n0 = rec[3], n1 = rec[4], n2 = rec[5];
+    const float uvs[3][2] = {{a.w, b.w}, {cc.w, n0.w}, {n1.w, n2.w}};
+    float du1 = uvs[0][0] - uvs[2][0], du2 = uvs[1][0] - uvs[2][0];
+    float dv1 = uvs[0][1] - uvs[2][1], dv2 = uvs[1][1] - uvs[2][1];
+    V dp1 = vsub(p1, p3), dp2 = vsub(p2, p3);
+    float determinant = du1 * dv2 - dv1 * du2;
+    V dpdu, dpdv;
+    if (determinant == 0.f) coordsys(vnorm(vcross(e2, e1)), &dpdu, &dpdv);
+    else {
+        float invdet = 1.f / determinant;
+        dpdu = vmul(vsub(vmul(dp1, dv2), vmul(dp2, dv1)), invdet);
+        dpdv = vmul(vadd(vmul(dp1, -du2), vmul(dp2, du1)), invdet);
+    }
+    float b0 = 1 - b1 - b2;
+    float tu = b0 * uvs[0][0] + b1 * uvs[1][0] + b2 * uvs[2][0];
+    float tv = b0 * uvs[0][1] + b1 * uvs[1][1] + b2 * uvs[2][1];
+    dg_init(*dg, rayat(ray, tt), dpdu, dpdv, v3(0, 0, 0), v3(0, 0, 0), tu, tv, (__float_as_int(rec[7].x) & REC_FLIP) != 0);
+    *tHit = tt;
+    *rayEps = 1e-3f * *tHit;
+    return true;
+}
+// Triangle::GetShadingGeometry (trianglemesh.cpp:285-360) from the record: tri_shading's arithmetic
+PGD_INLINE void tri_shading_rec(const float4 *rec, const float *nmat, const DG &dg, DG &dgs) {
+    const int flags = __float_as_int(rec[7].x);
+    if (!(flags & REC_NORMALS)) { dgs = dg; return; }
+    const float4 a = rec[0], b4 = rec[1], cc = rec[2], r3 = rec[3], r4 = rec[4], r5 = rec[5];
+    const float uv[3][2] = {{a.w, b4.w}, {cc.w, r3.w}, {r4.w, r5.w}};
+    float b[3];
+    float A[2][2] = {{uv[1][0] - uv[0][0], uv[2][0] - uv[0][0]}, {uv[1][1] - uv[0][1], uv[2][1] - uv[0][1]}};
+    float C[2] = {dg.u - uv[0][0], dg.v - uv[0][1]};
+    if (!solve2x2(A, C, &b[1], &b[2])) b[0] = b[1] = b[2] = 1.f / 3.f;
+    else b[0] = 1.f - b[1] - b[2];
+    V n0 = v3(r3.x, r3.y, r3.z), n1 = v3(r4.x, r4.y, r4.z), n2 = v3(r5.x, r5.y, r5.z);
+    V ni = vadd(vadd(vmul(n0, b[0]), vmul(n1, b[1])), vmul(n2, b[2]));
+    V ns = vnorm(xnormal(nmat, ni));
+    V ss = vnorm(dg.dpdu);
+    V ts = vcross(ss, ns);
+    if (vlen2(ts) > 0.f) { ts = vnorm(ts); ss = vcross(ts, ns); }
+    else coordsys(ns, &ss, &ts);
+    V dndu, dndv;
+    float du1 = uv[0][0] - uv[2][0], du2 = uv[1][0] - uv[2][0];
+    float dv1 = uv[0][1] - uv[2][1], dv2 = uv[1][1] - uv[2][1];
+    V dn1 = vsub(n0, n2), dn2 = vsub(n1, n2);
+    float determinant = du1 * dv2 - dv1 * du2;
+    if (determinant == 0.f) dndu = dndv = v3(0, 0, 0);
+    else {
+        float invdet = 1.f / determinant;
+        dndu = vmul(vsub(vmul(dn1, dv2), vmul(dn2, dv1)), invdet);
+        dndv = vmul(vadd(vmul(dn1, -du2), vmul(dn2, du1)), invdet);
+    }
+    dg_init(dgs, dg.p, ss, ts, xnormal(nmat, dndu), xnormal(nmat, dndv), dg.u, dg.v, (flags & REC_FLIP) != 0);
 }
 
 PGD_INLINE bool quadratic(float A, float B, float C, float *t0, float *t1) {
@@ -1262,7 +1351,8 @@ PGD_INLINE bool bvh_intersectP4q(const DevScene &S, Stack &st, const Ray &ray0) 
 }
 // im: the path's instance transforms (PathSoA::instM, per instance 8 float4: world->primitive
 // m rows, then its inverse), or null in scenes without instances
-struct Isect { DG dg; float rayEps; int prim; int inst; float time; const float4 *im; };
+// mat, al: the hit primitive's material and area light (its record, filled by isect_fill)
+struct Isect { DG dg; float rayEps; int prim; int inst; float time; const float4 *im; int mat, al; };
 // instance transforms of a path, computed once at path start (every ray of a path carries
 // the camera sample's time, so AnimatedTransform::Interpolate gives the same matrices for all
 // of them): m (and mInv) of instance i from the path's record
@@ -1295,7 +1385,8 @@ PGD_INLINE V isect_nn(const DevScene &S, const Ray &ray, int prim, float t, cons
 // full intersection record for a recorded closest hit; primitives of a transformed instance
 // are intersected in primitive space and moved to world space (primitive.cpp:94-110)
 PGD_HEAVY void isect_fill(const DevScene &S, const Ray &ray, int prim, float t, Isect &is, const float4 *im) {
-    const pbrtgpu_prim pr = (*sa(S.prims, (uint32_t)(prim)));
+    const float4 *rec = prim_rec(S, prim);
+    const int4 pr = rec_prim(rec);   // shape_type, shape_index, material, area_light
     Ray r = ray;
     r.maxt = t;
     float th;
@@ -1303,15 +1394,24 @@ PGD_HEAVY void isect_fill(const DevScene &S, const Ray &ray, int prim, float t, 
     is.inst = -1;
     is.time = ray.time;
     is.im = im;
+    is.mat = pr.z;
+    is.al = pr.w;
     const int inst = S.nInsts ? (*sa(S.primInst, (uint32_t)(prim))) : -1;
+#ifdef PGD_AB_NO_PRIMREC   // A/B timing build only: the triangle from the prim -> triangle -> vertex chain
+    const bool useRec = false;
+#else
+    const bool useRec = true;
+#endif
     if (inst < 0) {
-        shape_intersect(S, pr.shape_type, pr.shape_index, r, &th, &is.rayEps, &is.dg);
+        if (useRec && pr.x == PBRTGPU_SHAPE_TRIANGLE) tri_intersect_rec(rec, r, &th, &is.rayEps, &is.dg);
+        else shape_intersect(S, pr.x, pr.y, r, &th, &is.rayEps, &is.dg);
         return;
     }
     float m[16], minv[16];
     inst_load(im, inst, m, minv);
     Ray ro = xray(m, r);
-    shape_intersect(S, pr.shape_type, pr.shape_index, ro, &th, &is.rayEps, &is.dg);
+    if (useRec && pr.x == PBRTGPU_SHAPE_TRIANGLE) tri_intersect_rec(rec, ro, &th, &is.rayEps, &is.dg);
+    else shape_intersect(S, pr.x, pr.y, ro, &th, &is.rayEps, &is.dg);
     if (m4_is_identity(m)) return;
     is.inst = inst;
     DG &g = is.dg;   // PrimitiveToWorld = Inverse(w2p): points/vectors with mInv, normals with m
@@ -2426,25 +2526,30 @@ PGD_HEAVY void compute_differentials(const DG &dg, const RayDiff &rd, float out[
 template <int FEAT>
 PGD_HEAVY void get_bsdf(const DevScene &S, const Isect &is, const float diff[10], float4 *kb, size_t c, BSDF &bs,
                         V *pOut, V *nOut, V *dnOut = nullptr) {
-    const pbrtgpu_prim pr = (*sa(S.prims, (uint32_t)(is.prim)));
-    const pbrtgpu_material &mt = (*sa(S.mats, (uint32_t)(pr.material)));
+    const float4 *rec = prim_rec(S, is.prim);
+    const pbrtgpu_material &mt = (*sa(S.mats, (uint32_t)(is.mat)));
     DG dgs;
     int ro, swaps;
-    if (pr.shape_type == PBRTGPU_SHAPE_TRIANGLE) {
-        const pbrtgpu_mesh &m = (*sa(S.meshes, (uint32_t)((*sa(S.tris, (uint32_t)(pr.shape_index))).mesh)));
-        if (is.inst < 0) tri_shading(S, pr.shape_index, m.o2w_minv, is.dg, dgs);
-        else {
+    if (__float_as_int(rec[6].x) == PBRTGPU_SHAPE_TRIANGLE) {
+        if (is.inst < 0) {
+            const pbrtgpu_mesh &m = (*sa(S.meshes, (uint32_t)__float_as_int(rec[7].y)));
+#ifdef PGD_AB_NO_PRIMREC
+            tri_shading(S, __float_as_int(rec[6].y), m.o2w_minv, is.dg, dgs);
+#else
+            tri_shading_rec(rec, m.o2w_minv, is.dg, dgs);
+#endif
+        } else {
             // ObjectToWorld = Inverse(Identity * w2p): its mInv is Mul(Identity, w2p.m)
             float w[16], id[16], nm[16];
             inst_load(is.im, is.inst, w, nullptr);
             m4_identity(id);
             m4_mul(id, w, nm);
-            tri_shading(S, pr.shape_index, nm, is.dg, dgs);
+            tri_shading_rec(rec, nm, is.dg, dgs);
         }
-        ro = m.reverse_orientation; swaps = m.swaps_handedness;
+        ro = (__float_as_int(rec[7].x) & REC_FLIP) ? 1 : 0; swaps = 0;   // only reverse ^ swaps is used
     } else {
         dgs = is.dg;
-        const pbrtgpu_quadric &q = (*sa(S.quads, (uint32_t)(pr.shape_index)));
+        const pbrtgpu_quadric &q = (*sa(S.quads, (uint32_t)__float_as_int(rec[6].y)));
         ro = q.reverse_orientation; swaps = q.swaps_handedness;
     }
     TexPt tq;

@@ -504,7 +504,7 @@ PGD_INLINE Pushes shade_slot_dl(const DevScene &S, const PathSoA &P, int slot, f
             k = 0;
             Isect is0;   // the hit alone decides the emission
             isect_fill(S, ray, prim, P.hitT[slot], is0, inst_rec(P, slot));
-            const int al = (*sa(S.prims, (uint32_t)(is0.prim))).area_light;
+            const int al = is0.al;
             const int eo = (al >= 0 && vdot(is0.dg.nn, vneg(ray.d)) > 0.f) ? (*sa(S.lights, (uint32_t)(al))).spec : -1;   // AreaLight::L
             float4 *Lv = dl_L<NB>(P, d, slot);
 #pragma unroll

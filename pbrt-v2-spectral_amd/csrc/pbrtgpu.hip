@@ -1382,6 +1382,15 @@ static int xcd_map_on() {
     const char *e = getenv("PBRTGPU_XCD_MAP");
     return (e && atoi(e) != 0) ? 1 : 0;
 }
+// Batches of passes in flight per lane (run_wavefront): PBRTGPU_PIPE=0 one (every decision from the
+// last batch's counters, the host idle gap at each read-back), 2 two always (the decisions one batch
+// late), 1 (default) two while the lane has more than two slot pools of items left -- decisions that
+// far from the drain cannot change -- and one from there on
+static int pipe_mode() {
+    const char *e = getenv("PBRTGPU_PIPE");
+    const int v = e ? atoi(e) : 1;
+    return v < 0 ? 0 : (v > 2 ? 2 : v);
+}
 static bool drain_list_on() {
     const char *e = getenv("PBRTGPU_DRAIN_LIST");
     return !e || atoi(e) != 0;
@@ -1751,6 +1760,11 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
         r.q = q;
         return close_batch(r, bi, Batch{n, false, r.drain, r.liveGrid, q});
     };
+    // a second batch may be enqueued behind the one in flight (pipe_mode)
+    const int pipe = pipe_mode();
+    auto pipe_far = [&](const Run &r, const uint32_t *cnt) -> bool {
+        return pipe == 2 || (pipe == 1 && (uint64_t)cnt[CNT_NEXT] + 2ull * (uint64_t)r.cap < r.src.nItems);
+    };
     HIPCHK(hipEventRecord(c->ev[0], c->stream));   // the other lanes start after the work queued so far
     for (int l = 0; l < nl; ++l) {
         Run &r = R[l];
@@ -1806,12 +1820,14 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
         HIPCHK(kShade(r.grid, L.s, c->S, L.P, r.src, 0, Lout));
         HIPCHK(hipEventRecord(L.ev[0][1], L.s));
         if (int e = close_batch(r, 0, Batch{0, true, false, r.grid, 0})) return e;
-        // ... and the first batch of passes right behind it: after pass 0 the slots hold the first
-        // min(cap, items) items (every slot regenerated), each with its camera ray queued
+        // ... and the first batch of passes right behind it when the lane is far from its drain:
+        // after pass 0 the slots hold the first min(cap, items) items (every slot regenerated),
+        // each with its camera ray queued
         uint32_t c0[CNT_WORDS] = {};
         c0[CNT_NEXT] = (uint32_t)std::min<uint64_t>((uint64_t)r.cap, r.src.nItems);
         c0[CNT_QC(0)] = (uint32_t)r.cap;
-        if (int e = enqueue(r, c0, 0)) return e;
+        if (pipe_far(r, c0))
+            if (int e = enqueue(r, c0, 0)) return e;
     }
     int live = nl;
     float m;
@@ -1884,6 +1900,9 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
             continue;
         }
         if (r.passes > r.maxPasses) return fail(PBRTGPU_E_STATE, "wavefront did not drain");
+        // a batch still in flight behind this one: enqueue behind it only far from the drain;
+        // otherwise decide at its read-back, from its counters
+        if (r.inflight > 0 && !pipe_far(r, cnt)) continue;
         if (int e = enqueue(r, cnt, B.qEnd)) return e;
     }
     if (c->S.specMode == 1) {   // the rows' luminance guard once every band of them is in

@@ -591,6 +591,9 @@ static int scene_build(const pbrtgpu_flat_scene *s, int topNodes, DevScene &S, i
         if (p.shape_type == PBRTGPU_SHAPE_TRIANGLE) {
             if (p.shape_index < 0 || p.shape_index >= s->n_tris) SB_FAIL(PBRTGPU_E_INVALID, "bad triangle index");
             const pbrtgpu_triangle &tr = s->tris[p.shape_index];
+            if (tr.mesh < 0 || tr.mesh >= s->n_meshes) SB_FAIL(PBRTGPU_E_INVALID, "bad triangle mesh");
+            for (int k = 0; k < 3; ++k)
+                if (tr.v[k] < 0 || tr.v[k] >= s->n_verts) SB_FAIL(PBRTGPU_E_INVALID, "bad triangle vertex");
             const float *a = s->vert_p + 3 * tr.v[0], *b = s->vert_p + 3 * tr.v[1], *cc = s->vert_p + 3 * tr.v[2];
             t.a = make_float4(a[0], a[1], a[2], 0.f);
             t.b = make_float4(b[0], b[1], b[2], 0.f);
@@ -599,6 +602,34 @@ static int scene_build(const pbrtgpu_flat_scene *s, int topNodes, DevScene &S, i
             SB_FAIL(PBRTGPU_E_INVALID, "bad quadric index");
         pt[i] = t;
     }
+    // the per-primitive shading records (device.h PrimRec): the hit's geometry, uvs, normals,
+    // prim fields and mesh flags in one 128-byte line, values copied from the flattened scene
+    std::vector<float4> rec((size_t)8 * s->n_prims, make_float4(0.f, 0.f, 0.f, 0.f));
+    auto fi = [](int32_t v) { float f; memcpy(&f, &v, 4); return f; };
+    for (int i = 0; i < s->n_prims; ++i) {
+        const pbrtgpu_prim &p = s->prims[i];
+        float4 *r = &rec[(size_t)8 * i];
+        r[6] = make_float4(fi(p.shape_type), fi(p.shape_index), fi(p.material), fi(p.area_light));
+        if (p.shape_type != PBRTGPU_SHAPE_TRIANGLE) continue;
+        const pbrtgpu_triangle &tr = s->tris[p.shape_index];
+        const pbrtgpu_mesh &m = s->meshes[tr.mesh];
+        float uv[3][2] = {{0.f, 0.f}, {1.f, 0.f}, {1.f, 1.f}};   // Triangle::GetUVs without uvs
+        if (m.has_uvs) {
+            if (!s->vert_uv) SB_FAIL(PBRTGPU_E_INVALID, "mesh uvs missing");
+            for (int k = 0; k < 3; ++k) { uv[k][0] = s->vert_uv[2 * tr.v[k]]; uv[k][1] = s->vert_uv[2 * tr.v[k] + 1]; }
+        }
+        if (m.has_normals && !s->vert_n) SB_FAIL(PBRTGPU_E_INVALID, "mesh normals missing");
+        const float w[6] = {uv[0][0], uv[0][1], uv[1][0], uv[1][1], uv[2][0], uv[2][1]};
+        for (int k = 0; k < 3; ++k) {
+            const float *v = s->vert_p + 3 * tr.v[k];
+            r[k] = make_float4(v[0], v[1], v[2], w[k]);
+            const float *n = m.has_normals ? s->vert_n + 3 * tr.v[k] : nullptr;
+            r[3 + k] = make_float4(n ? n[0] : 0.f, n ? n[1] : 0.f, n ? n[2] : 0.f, w[3 + k]);
+        }
+        const int flags = (m.has_normals ? 2 : 0) | ((m.reverse_orientation ^ m.swaps_handedness) ? 4 : 0);
+        r[7] = make_float4(fi(flags), fi(tr.mesh), 0.f, 0.f);
+    }
+    SB_PUT(rec.data(), rec.size(), &S.primRec);
     // spectrum pool re-laid out with a stride of whole float4 quads (16-byte aligned band
     // quads for the shading loads); every offset in the flattened scene is a multiple of
     // n_bands (front end emits whole spectra)

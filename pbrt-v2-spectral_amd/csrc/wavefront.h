@@ -1010,7 +1010,7 @@ PGD_INLINE Pushes shade_vertex(const DevScene &S, const PathSoA &P, int slot, in
     la->emit = false;
     la->zero = false;
     if (vb == 0 || (fl & PF_SPEC)) {
-        int al = (*sa(S.prims, (uint32_t)(is.prim))).area_light;
+        const int al = is.al;
         la->emit = true;
         la->emitOff = (al >= 0 && vdot(is.dg.nn, vneg(ray.d)) > 0.f) ? (*sa(S.lights, (uint32_t)(al))).spec : -1;
     }
@@ -1020,7 +1020,7 @@ PGD_INLINE Pushes shade_vertex(const DevScene &S, const PathSoA &P, int slot, in
     // to textured materials
     float diff[10] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};   // du/dv (x, y), dpdx, dpdy
     if ((FEAT & FEAT_TEX) && vb == 0) {
-        const pbrtgpu_material &mt = (*sa(S.mats, (uint32_t)((*sa(S.prims, (uint32_t)(is.prim))).material)));
+        const pbrtgpu_material &mt = (*sa(S.mats, (uint32_t)(is.mat)));
         if (mt.bump_tex >= 0 || mt.normal_tex >= 0 || mt.tex[0] >= 0 || mt.tex[1] >= 0 || mt.tex[2] >= 0 || mt.tex[3] >= 0 ||
             mt.ftex[0] >= 0 || mt.ftex[1] >= 0) {
             const uint32_t pxy = P.pix[slot];
