@@ -1382,13 +1382,17 @@ static int xcd_map_on() {
     const char *e = getenv("PBRTGPU_XCD_MAP");
     return (e && atoi(e) != 0) ? 1 : 0;
 }
-// Batches of passes in flight per lane (run_wavefront): PBRTGPU_PIPE=0 one (every decision from the
-// last batch's counters, the host idle gap at each read-back), 2 two always (the decisions one batch
-// late), 1 (default) two while the lane has more than two slot pools of items left -- decisions that
-// far from the drain cannot change -- and one from there on
+// Batches of passes in flight per lane (run_wavefront): PBRTGPU_PIPE=0 (default) one -- every
+// decision from the last batch's counters, with the host's gap at each read-back; 2 two always (the
+// decisions one batch late); 1 two while the lane has more than two slot pools of items left --
+// decisions that far from the drain cannot change -- and one from there on.  Measured (r06c, one
+// box, two runs each): C2 504-506 Mpaths/s with one, 486-487 with 1, 483-488 with 2; one GPU's 1/8
+// slice 455-457 Mpaths/s either way with 0 and 1, 1/4 and 1/8 much worse with 2 (the drain's list
+// mode and tail a batch late).  The read-back gaps are not what bounds the frame: with two
+// batches queued, the two lanes' kernels fall into step and overlap less
 static int pipe_mode() {
     const char *e = getenv("PBRTGPU_PIPE");
-    const int v = e ? atoi(e) : 1;
+    const int v = e ? atoi(e) : 0;
     return v < 0 ? 0 : (v > 2 ? 2 : v);
 }
 static bool drain_list_on() {
