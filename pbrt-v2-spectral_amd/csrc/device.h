@@ -41,6 +41,12 @@ namespace pgd {
 #define PGD_HEAVY __device__ __forceinline__
 #endif
 #define PGD_HD __host__ __device__ __forceinline__
+// the global address space, spelled out where an out-of-line function receives a pointer (its
+// accesses would be generic: flat loads / stores, which also count on the LDS counter); the host
+// replay of tools/hostsan defines it empty
+#ifndef PGD_GLOBAL_AS
+#define PGD_GLOBAL_AS __attribute__((address_space(1)))
+#endif
 static constexpr float kPi = 3.14159265358979323846f;
 static constexpr float kInvPi = 0.31830988618379067154f;
 static constexpr float kInvTwoPi = 0.15915494309189533577f;
@@ -903,7 +909,17 @@ PGD_INLINE float quadric_hit_inl(const pbrtgpu_quadric *quads, int type, int idx
 }
 __device__ PGD_QUAD_ATTR float quadric_hit(const pbrtgpu_quadric *quads, int type, int idx, float ox, float oy, float oz,
                                            float dx, float dy, float dz, float mint, float maxt, float time) {
-    return quadric_hit_inl(quads, type, idx, ox, oy, oz, dx, dy, dz, mint, maxt, time);
+    // the record through global loads (not flat), as whole float4s
+    typedef float Q4 __attribute__((ext_vector_type(4)));
+    static_assert(sizeof(pbrtgpu_quadric) % 16 == 0, "quadric records are whole float4s");
+    constexpr int NW = (int)(sizeof(pbrtgpu_quadric) / 16);
+    const PGD_GLOBAL_AS Q4 *src = (const PGD_GLOBAL_AS Q4 *)(quads + idx);
+    Q4 w[NW];
+#pragma unroll
+    for (int k = 0; k < NW; ++k) w[k] = src[k];
+    pbrtgpu_quadric q;
+    memcpy(&q, w, sizeof(q));
+    return quadric_hit_inl(&q, type, 0, ox, oy, oz, dx, dy, dz, mint, maxt, time);
 }
 // INL: the persistent traversal kernels inline the hit-only test (fewer VGPRs than the call
 // there); the shading kernel calls it (inlined, it costs k_shade registers)

@@ -435,6 +435,13 @@ typedef float F4N __attribute__((ext_vector_type(4)));
 #define PGD_LDS_AS __attribute__((address_space(3)))
 #endif
 typedef PGD_LDS_AS const F4N LdsF4;   // an LDS float4 (ds_read_b128)
+// The global address space, spelled out in the out-of-line kd-tree lookup: its pointer arguments
+// (the spectrum pool, the slot's M bands) would otherwise be generic, and a generic (flat) access
+// counts on the LDS counter as well -- every ds_read of the walk then waited (s_waitcnt lgkmcnt)
+// for the candidate stores and spectrum loads still in flight
+typedef PGD_GLOBAL_AS const F4N GlbF4c;
+typedef PGD_GLOBAL_AS F4N GlbF4;
+typedef PGD_GLOBAL_AS float GlbF;
 PGD_INLINE float4 kd_node(const float4 *__restrict__ p, int i) { return p[i]; }
 PGD_INLINE float4 kd_node(LdsF4 *p, int i) { const F4N v = p[i]; return make_float4(v.x, v.y, v.z, v.w); }
 
@@ -494,10 +501,10 @@ PGD_INLINE void kd_accumulate(NodePtr nodes, const float *__restrict__ spectra, 
     const float dist2 = vlen2(d);
     if (dist2 < maxD2) {
         const float weight = libmf_expf(-100.f * dist2);   // glibc expf, inline
-        const float4 *sv = reinterpret_cast<const float4 *>(spectra + __float_as_int(b.x));
+        const GlbF4c *sv = (const GlbF4c *)(spectra + __float_as_int(b.x));
 #pragma unroll
         for (int q = 0; q < NQ; ++q) {
-            const float4 sq = sv[q];
+            const F4N sq = sv[q];
             acc[q].x += weight * sq.x; acc[q].y += weight * sq.y;
             acc[q].z += weight * sq.z; acc[q].w += weight * sq.w;
         }
@@ -534,7 +541,10 @@ PGD_INLINE void kd_lookup(NodePtr nodes, const float *__restrict__ spectra, floa
     }
 #else
     constexpr int CAP = 4 * NQ;
-    float *cand = reinterpret_cast<float *>(mb);   // candidate j: component j & 3 of mb[(j >> 2) * c]
+    // candidate j: component j & 3 of mb[(j >> 2) * c], a 32-bit offset (slot arrays < 4 GiB,
+    // ensure_slots) from the slot's global pointer
+    GlbF *cand = (GlbF *)mb;
+    const uint32_t c4 = 4u * (uint32_t)c;
     const float capD2 = .001f * 1024.f;
     float d1 = capD2, d2 = capD2, d3 = capD2, bound = kd_radius_of(capD2);
     int n = 0, cur = 0, prev = -1;
@@ -557,7 +567,7 @@ PGD_INLINE void kd_lookup(NodePtr nodes, const float *__restrict__ spectra, floa
             continue;
         }
         if (dist2 < bound) {   // post-order: a candidate of the final walk
-            if (n < CAP) cand[(size_t)(n >> 2) * 4 * c + (n & 3)] = __int_as_float(cur);
+            if (n < CAP) cand[(uint32_t)(n >> 2) * c4 + (uint32_t)(n & 3)] = __int_as_float(cur);
             ++n;
         }
         if (cur == 0) break;
@@ -568,8 +578,8 @@ PGD_INLINE void kd_lookup(NodePtr nodes, const float *__restrict__ spectra, floa
     const float maxD2 = bound;
     if (n <= CAP) {
         for (int j = 0; j < n; ++j)
-            kd_accumulate<NB>(nodes, spectra, __float_as_int(cand[(size_t)(j >> 2) * 4 * c + (j & 3)]), p0, p1, p2, maxD2,
-                              acc, sumWeights);
+            kd_accumulate<NB>(nodes, spectra, __float_as_int(cand[(uint32_t)(j >> 2) * c4 + (uint32_t)(j & 3)]), p0, p1, p2,
+                              maxD2, acc, sumWeights);
     } else {   // the final walk itself
         cur = 0; prev = -1; down = true;
         for (;;) {
@@ -582,11 +592,14 @@ PGD_INLINE void kd_lookup(NodePtr nodes, const float *__restrict__ spectra, floa
         }
     }
 #endif
+    GlbF4 *mo = (GlbF4 *)mb;
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
         const float4 v = acc[q];
-        mb[q * c] = make_float4(clampf(v.x, 0.f, INFINITY) / sumWeights, clampf(v.y, 0.f, INFINITY) / sumWeights,
-                                clampf(v.z, 0.f, INFINITY) / sumWeights, clampf(v.w, 0.f, INFINITY) / sumWeights);
+        F4N o;
+        o.x = clampf(v.x, 0.f, INFINITY) / sumWeights; o.y = clampf(v.y, 0.f, INFINITY) / sumWeights;
+        o.z = clampf(v.z, 0.f, INFINITY) / sumWeights; o.w = clampf(v.w, 0.f, INFINITY) / sumWeights;
+        mo[(uint32_t)q * (uint32_t)c] = o;
     }
 }
 template <int NB>

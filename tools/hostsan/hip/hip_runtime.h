@@ -24,6 +24,7 @@
 #define __forceinline__ inline
 #define __launch_bounds__(...)
 #define PGD_LDS_AS   // LDS address space qualifier of wavefront.h: ordinary memory here
+#define PGD_GLOBAL_AS   // global address space qualifier of wavefront.h (kd lookup): ordinary memory here
 
 typedef int hipError_t;
 typedef void *hipStream_t;
