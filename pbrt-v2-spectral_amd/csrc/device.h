@@ -845,6 +845,26 @@ PGD_INLINE bool slab_enter(float4 lo, float4 hi, const Ray &ray, V invDir, const
     *tEnter = tmin;
     return tmax > ray.mint;
 }
+// slab_enter as one straight-line sequence (every plane distance computed, the early exits folded
+// into the result): the same answer and, where it passes, the same entry distance.  In the 4-wide
+// walks the four child tests then run as value selects rather than divergent branches under exec
+// masks (the short-circuit && of four tests per node compiled to a branch each)
+PGD_INLINE bool slab_enter_bf(float4 lo, float4 hi, const Ray &ray, V invDir, const int neg[3], float *tEnter) {
+    float tmin = ((neg[0] ? hi.x : lo.x) - ray.o.x) * invDir.x;
+    float tmax = ((neg[0] ? lo.x : hi.x) - ray.o.x) * invDir.x;
+    const float tymin = ((neg[1] ? hi.y : lo.y) - ray.o.y) * invDir.y;
+    const float tymax = ((neg[1] ? lo.y : hi.y) - ray.o.y) * invDir.y;
+    const bool ok1 = !(tmin > tymax) & !(tymin > tmax);
+    tmin = (tymin > tmin) ? tymin : tmin;
+    tmax = (tymax < tmax) ? tymax : tmax;
+    const float tzmin = ((neg[2] ? hi.z : lo.z) - ray.o.z) * invDir.z;
+    const float tzmax = ((neg[2] ? lo.z : hi.z) - ray.o.z) * invDir.z;
+    const bool ok2 = !(tmin > tzmax) & !(tzmin > tmax);
+    tmin = (tzmin > tmin) ? tzmin : tmin;
+    tmax = (tzmax < tmax) ? tzmax : tmax;
+    *tEnter = tmin;
+    return ok1 & ok2 & (tmax > ray.mint);
+}
 // LDS stack: column per lane
 struct Stack {
     uint32_t *base;   // &lds[lane]: child refs

@@ -276,8 +276,8 @@ __global__ __launch_bounds__(kTraceBlock) PGD_TRACE_ATTR void k_trace_pt(DevScen
                 }
                 st.cNodes++;
                 float tl = 0.f, tr = 0.f;
-                const bool hl = slab_enter(l0, l1, ray, invDir, neg, &tl) && tl < ray.maxt;
-                const bool hr = slab_enter(r0, r1, ray, invDir, neg, &tr) && tr < ray.maxt;
+                const bool hl = slab_enter_bf(l0, l1, ray, invDir, neg, &tl) & (tl < ray.maxt);
+                const bool hr = slab_enter_bf(r0, r1, ray, invDir, neg, &tr) & (tr < ray.maxt);
                 const uint32_t refL = __float_as_uint(l0.w), refR = __float_as_uint(l1.w);
                 const bool swap = ((negMask >> __float_as_uint(r0.w)) & 1u) != 0;   // no indexed private array
                 const bool hn = swap ? hr : hl, hf = swap ? hl : hr;
@@ -429,11 +429,17 @@ __global__ __launch_bounds__(kTraceBlock) PGD_TRACE_S4_ATTR void k_trace_s4(DevS
                 for (int k = 0; k < 8; ++k) b[k] = w[k];
                 st.cNodes++;
                 uint32_t nxt = NONE;
+                bool h[4];   // the four tests first, straight-line (slab_enter_bf)
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    float t = 0.f;
+                    h[k] = (__float_as_uint(b[2 * k].w) != NONE) & slab_enter_bf(b[2 * k], b[2 * k + 1], ray, invDir, neg, &t) &
+                           (t < ray.maxt);
+                }
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
                     const uint32_t r = __float_as_uint(b[2 * k].w);
-                    float t = 0.f;
-                    if (r != NONE && slab_enter(b[2 * k], b[2 * k + 1], ray, invDir, neg, &t) && t < ray.maxt) {
+                    if (h[k]) {
                         if (nxt == NONE) nxt = r;
                         else push(r);
                     }
@@ -684,21 +690,34 @@ __global__ __launch_bounds__(kTraceBlock) PGD_TRACE_ATTR void k_trace_c4(DevScen
                 float e0 = 0.f, e1 = 0.f, e2 = 0.f, e3 = 0.f;
                 const uint32_t r0 = __float_as_uint(b0.w), r1 = __float_as_uint(b2.w), r2 = __float_as_uint(b4.w),
                                r3 = __float_as_uint(b6.w);
-                const bool h0 = r0 != NONE && slab_enter(b0, b1, ray, invDir, neg, &e0) && e0 < ray.maxt;
-                const bool h1 = r1 != NONE && slab_enter(b2, b3, ray, invDir, neg, &e1) && e1 < ray.maxt;
-                const bool h2 = r2 != NONE && slab_enter(b4, b5, ray, invDir, neg, &e2) && e2 < ray.maxt;
-                const bool h3 = r3 != NONE && slab_enter(b6, b7, ray, invDir, neg, &e3) && e3 < ray.maxt;
+                // the four tests and the selections by slot as straight-line value selects (slab_enter_bf):
+                // a hit flag per slot in a bit mask, refs and entry distances picked by index
+                const bool h0 = (r0 != NONE) & slab_enter_bf(b0, b1, ray, invDir, neg, &e0) & (e0 < ray.maxt);
+                const bool h1 = (r1 != NONE) & slab_enter_bf(b2, b3, ray, invDir, neg, &e1) & (e1 < ray.maxt);
+                const bool h2 = (r2 != NONE) & slab_enter_bf(b4, b5, ray, invDir, neg, &e2) & (e2 < ray.maxt);
+                const bool h3 = (r3 != NONE) & slab_enter_bf(b6, b7, ray, invDir, neg, &e3) & (e3 < ray.maxt);
+                const uint32_t hm = (uint32_t)h0 | ((uint32_t)h1 << 1) | ((uint32_t)h2 << 2) | ((uint32_t)h3 << 3);
                 const uint32_t ord = w4_order(__float_as_uint(b1.w), negMask);
-                auto pr = [&](uint32_t sl) { return sl == 0 ? r0 : sl == 1 ? r1 : sl == 2 ? r2 : r3; };
-                auto ph = [&](uint32_t sl) { return sl == 0 ? h0 : sl == 1 ? h1 : sl == 2 ? h2 : h3; };
-                auto pe = [&](uint32_t sl) { return sl == 0 ? e0 : sl == 1 ? e1 : sl == 2 ? e2 : e3; };
+                // slot sl's ref / entry distance by two bit selects (a compare chain compiled to branches)
+                auto pr = [&](uint32_t sl) {
+                    const uint32_t lo = (sl & 1u) ? r1 : r0, hi = (sl & 1u) ? r3 : r2;
+                    return (sl & 2u) ? hi : lo;
+                };
+                auto ph = [&](uint32_t sl) { return ((hm >> sl) & 1u) != 0u; };
+                auto pe = [&](uint32_t sl) {
+                    const float lo = (sl & 1u) ? e1 : e0, hi = (sl & 1u) ? e3 : e2;
+                    return (sl & 2u) ? hi : lo;
+                };
                 const uint32_t s0 = ord & 3u, s1 = (ord >> 2) & 3u, s2 = (ord >> 4) & 3u, s3 = (ord >> 6) & 3u;
                 const bool k0 = ph(s0), k1 = ph(s1), k2 = ph(s2), k3 = ph(s3);
                 const int first = k0 ? 0 : k1 ? 1 : k2 ? 2 : k3 ? 3 : 4;
-                if (k3 && first < 3) push(pr(s3), pe(s3));
-                if (k2 && first < 2) push(pr(s2), pe(s2));
-                if (k1 && first < 1) push(pr(s1), pe(s1));
-                ref = first == 0 ? pr(s0) : first == 1 ? pr(s1) : first == 2 ? pr(s2) : first == 3 ? pr(s3) : NONE;
+                const uint32_t q1 = pr(s1), q2 = pr(s2), q3 = pr(s3);
+                const float t1 = pe(s1), t2 = pe(s2), t3 = pe(s3);
+                if (k3 & (first < 3)) push(q3, t3);
+                if (k2 & (first < 2)) push(q2, t2);
+                if (k1 & (first < 1)) push(q1, t1);
+                const uint32_t f01 = first == 0 ? pr(s0) : q1, f23 = first == 2 ? q2 : (first == 3 ? q3 : NONE);
+                ref = first < 2 ? f01 : f23;
             }
             if (ref != NONE && (ref & WREF_LEAF)) {
                 const uint32_t np = (ref >> WREF_NP_SHIFT) & WREF_NP_MASK, off = ref & WREF_OFF_MASK;
@@ -834,8 +853,8 @@ __global__ __launch_bounds__(kTraceBlock) PGD_TRACE_INST_ATTR void k_trace_inst(
                     const float4 l0 = w[0], l1 = w[1], r0 = w[2], r1 = w[3];
                     st.cNodes++;
                     float tl = 0.f, tr = 0.f;
-                    const bool hl = slab_enter(l0, l1, ray, invDir, neg, &tl) && tl < ray.maxt;
-                    const bool hr = slab_enter(r0, r1, ray, invDir, neg, &tr) && tr < ray.maxt;
+                    const bool hl = slab_enter_bf(l0, l1, ray, invDir, neg, &tl) & (tl < ray.maxt);
+                    const bool hr = slab_enter_bf(r0, r1, ray, invDir, neg, &tr) & (tr < ray.maxt);
                     const uint32_t refL = __float_as_uint(l0.w), refR = __float_as_uint(l1.w);
                     const bool swap = ((negMask >> __float_as_uint(r0.w)) & 1u) != 0;
                     const bool hn = swap ? hr : hl, hf = swap ? hl : hr;
