@@ -113,10 +113,16 @@ PGD_INLINE float vdot(V a, V b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
 PGD_INLINE float vlen2(V a) { return a.x * a.x + a.y * a.y + a.z * a.z; }
 PGD_INLINE float vlen(V a) { return sqrtf(vlen2(a)); }
 PGD_INLINE V vnorm(V a) { return vdiv(a, vlen(a)); }
-// geometry.h:461-468: products exact in double, one rounding per component
+// geometry.h:461-468: products exact in double, one rounding per component.  A product of two floats
+// is exact in double (48 significant bits), so (p - q) rounded once equals fma(a, b, -q) rounded
+// once: one DMUL and one DFMA per component instead of two DMULs and a DADD, the same bits
 PGD_INLINE V vcross(V a, V b) {
     double ax = a.x, ay = a.y, az = a.z, bx = b.x, by = b.y, bz = b.z;
+#ifdef PGD_AB_VCROSS_DFMA
+    return v3((float)fma(ay, bz, -(az * by)), (float)fma(az, bx, -(ax * bz)), (float)fma(ax, by, -(ay * bx)));
+#else
     return v3((float)((ay * bz) - (az * by)), (float)((az * bx) - (ax * bz)), (float)((ax * by) - (ay * bx)));
+#endif
 }
 PGD_HD float pmin(float a, float b) { return (b < a) ? b : a; }
 PGD_HD float pmax(float a, float b) { return (a < b) ? b : a; }
@@ -307,7 +313,10 @@ PGD_INLINE float power_heuristic(float fPdf, float gPdf) {
 }
 
 // ------------------------------------------------------------------ device scene
-struct DevTri { float4 a, b, c; };   // p1.xyz,pad | p2.xyz,pad | p3.xyz,pad
+// p1.xyz, shape | p2.xyz, pad | p3.xyz, pad -- `shape` (bits of a.w) the primitive's shape type
+// (PBRTGPU_SHAPE_TRIANGLE = 0, the vertices meaningful), so a leaf's primitive test loads this one
+// record first and the pbrtgpu_prim only for the other shapes
+struct DevTri { float4 a, b, c; };
 struct DevScene {
     int nb, maxDepth, spp, stackDepth;
     uint32_t seed;
@@ -372,7 +381,19 @@ struct DevScene {
 
 // scene features a shade kernel is specialised for (k_shade<NB, FEAT>): a scene without
 // them runs a variant with that code compiled out
-enum { FEAT_MEAS = 1, FEAT_TEX = 2, FEAT_INF = 4, FEAT_ALL = 7 };
+enum { FEAT_MEAS = 1, FEAT_TEX = 2, FEAT_INF = 4, FEAT_ALL = 7, FEAT_BASIC = 8 };
+// FEAT_BASIC: a scene without textures or infinite / spot / distant lights whose materials are all
+// matte or plastic, or also measured with FEAT_MEAS (C2 and C5's killeroos: FEAT_BASIC; C3's bunny:
+// FEAT_MEAS | FEAT_BASIC).  Its shading objects (shade.hip built with SHADE_FEAT 8 or 9) compile
+// the Lambertian, Oren-Nayar, dielectric-Blinn (and measured) BxDFs only: the other kinds' sample,
+// pdf and band code is never reached there (pbrtgpu.hip path_shade_variant)
+#if defined(SHADE_FEAT) && (SHADE_FEAT & 8)
+#define PGD_BASIC_MATS 1
+#define PGD_BASIC_MEAS (SHADE_FEAT & 1)
+#else
+#define PGD_BASIC_MATS 0
+#define PGD_BASIC_MEAS 0
+#endif
 
 struct DG { V p, nn, dpdu, dpdv, dndu, dndv; float u, v; };
 PGD_INLINE void dg_init(DG &dg, V p, V dpdu, V dpdv, V dndu, V dndv, float u, float v, int flip) {
@@ -951,8 +972,9 @@ PGD_INLINE bool quadric_test(const DevScene &S, int type, int idx, const Ray &r,
     return th != -INFINITY;
 }
 PGD_INLINE bool prim_hit(const DevScene &S, Stack &st, int pi, const Ray &ray, float *t) {
+    const DevTri tr = (*sa(S.primTri, (uint32_t)(pi)));
+    if (__float_as_int(tr.a.w) == PBRTGPU_SHAPE_TRIANGLE) { st.cTris++; return tri_hit(tr, ray, t); }
     const pbrtgpu_prim pr = (*sa(S.prims, (uint32_t)(pi)));
-    if (pr.shape_type == PBRTGPU_SHAPE_TRIANGLE) { st.cTris++; return tri_hit((*sa(S.primTri, (uint32_t)(pi))), ray, t); }
     st.cQuads++;
     return quadric_test(S, pr.shape_type, pr.shape_index, ray, t);
 }
@@ -1109,12 +1131,27 @@ PGD_INLINE bool bvh_walk(const DevScene &S, Stack &st, int base, uint32_t root, 
 
 template <bool ANY, bool INST>
 PGD_INLINE bool prim_test(const DevScene &S, Stack &st, int base, int pi, Ray &ray, int *hitPrim, float *hitT) {
-    const pbrtgpu_prim pr = (*sa(S.prims, (uint32_t)(pi)));
+    // Any-hit walks read the shape type from the triangle record (DevTri a.w): one dependent load
+    // per triangle test.  The closest walk reads the primitive record first: holding the triangle
+    // record across the type test takes it past 96 VGPRs (4 waves/SIMD instead of 5)
     float t;
-    if (pr.shape_type == PBRTGPU_SHAPE_TRIANGLE) {
+    DevTri tr;
+    bool isTri;
+    if constexpr (ANY) {
+        tr = (*sa(S.primTri, (uint32_t)(pi)));
+        isTri = __float_as_int(tr.a.w) == PBRTGPU_SHAPE_TRIANGLE;
+    } else {
+        isTri = (*sa(S.prims, (uint32_t)(pi))).shape_type == PBRTGPU_SHAPE_TRIANGLE;
+        if (isTri) tr = (*sa(S.primTri, (uint32_t)(pi)));
+    }
+    if (isTri) {
         st.cTris++;
-        if (!tri_hit((*sa(S.primTri, (uint32_t)(pi))), ray, &t)) return false;
-    } else if (!INST || pr.shape_type != PBRTGPU_SHAPE_INSTANCE) {
+        if (!tri_hit(tr, ray, &t)) return false;
+        if (!ANY) { ray.maxt = t; *hitPrim = pi; *hitT = t; }
+        return true;
+    }
+    const pbrtgpu_prim pr = (*sa(S.prims, (uint32_t)(pi)));
+    if (!INST || pr.shape_type != PBRTGPU_SHAPE_INSTANCE) {
         st.cQuads++;
         if (!quadric_test<true>(S, pr.shape_type, pr.shape_index, ray, &t)) return false;
     } else {
@@ -1468,6 +1505,10 @@ enum { BX_LAMBERT, BX_OREN, BX_MICRO_BLINN_DIEL, BX_SPEC_REFL_NOOP, BX_FRESNEL_B
        BX_SPEC_REFL_COND };                                       // SpecularReflection(1, FresnelConductor(R, 0))
 // R, R2: offsets into DevScene::spectra, or -1 for the per-slot textured spectrum (K bands)
 struct BxDF { int kind, type; int R, R2; float a, b; };
+// the BxDF kinds a shading object compiles (FEAT_BASIC objects: the basic materials' kinds only)
+PGD_INLINE bool bx_kind_on(int k) {
+    return !PGD_BASIC_MATS || k <= BX_MICRO_BLINN_DIEL || (PGD_BASIC_MEAS && (k == BX_MEASURED_IRREG || k == BX_MEASURED_HALF));
+}
 // eta: BSDF::eta, the glass material's index (glass.cpp:47-48), 1 otherwise (DirectLighting's
 // SpecularTransmit differentials read it, integrator.cpp:219-247)
 struct BSDF { V nn, ng, sn, tn; int n; BxDF bx[2]; float eta; };
@@ -1663,7 +1704,7 @@ PGD_INLINE int halfangle_index(V WO, V WI) {
 PGD_INLINE FTerm bx_term(PowMemo &pm, const BxDF &b, V wo, V wi) {
     FTerm t;
     t.kind = T_ZERO; t.R = b.R; t.R2 = b.R2; t.s0 = t.s1 = t.s2 = t.s3 = 0.f;
-    switch (b.kind) {
+    switch (bx_kind_on(b.kind) ? b.kind : -1) {
         case BX_LAMBERT: t.kind = T_LAMB; break;
         case BX_OREN: {
             float sinthetai = sinth(wi), sinthetao = sinth(wo);
@@ -1738,7 +1779,7 @@ PGD_INLINE FTerm bx_term(PowMemo &pm, const BxDF &b, V wo, V wi) {
     return t;
 }
 PGD_INLINE float bx_pdf(PowMemo &pm, const BxDF &b, V wo, V wi) {
-    switch (b.kind) {
+    switch (bx_kind_on(b.kind) ? b.kind : -1) {
         case BX_MICRO_BLINN_DIEL:
         case BX_MICRO_BLINN_COND: if (!samehemi(wo, wi)) return 0.f; return blinn_pdf(pm, b.a, wo, wi);
         case BX_SPEC_REFL_NOOP:
@@ -1753,7 +1794,7 @@ PGD_INLINE float bx_pdf(PowMemo &pm, const BxDF &b, V wo, V wi) {
 }
 // the specular BxDFs' Sample_f (reflection.cpp SpecularReflection / SpecularTransmission::Sample_f)
 PGD_INLINE void bx_sample_specular(const BxDF &b, V wo, V *wi, float *pdf, FVal &F) {
-    switch (b.kind) {
+    switch (PGD_BASIC_MATS ? -1 : b.kind) {
         case BX_SPEC_REFL_NOOP:    // SpecularReflection with FresnelNoOp: Spectrum(1) * R / |cos|
         case BX_SPEC_REFL_DIEL:    // ... with FresnelDielectric(1, ior)
             *wi = v3(-wo.x, -wo.y, wo.z);
@@ -1790,7 +1831,7 @@ PGD_INLINE void bx_sample_specular(const BxDF &b, V wo, V *wi, float *pdf, FVal 
 // BxDF::Sample_f: direction + pdf; f as a one-term sum (or the specular spectrum)
 PGD_INLINE void bx_sample_f(PowMemo &pm, const BxDF &b, V wo, V *wi, float u1, float u2, float *pdf, FVal &F) {
     fval_zero(F);
-    switch (b.kind) {
+    switch (bx_kind_on(b.kind) ? b.kind : -1) {
         case BX_MICRO_BLINN_DIEL:
         case BX_MICRO_BLINN_COND:
             blinn_sample(b.a, wo, wi, u1, u2, pdf);
@@ -2678,6 +2719,8 @@ PGD_HEAVY void get_bsdf(const DevScene &S, const Isect &is, const float diff[10]
     }
     const float f0 = fp0;
     bs.eta = mt.type == PBRTGPU_MAT_GLASS ? f0 : 1.f;
+    // (the material switch itself is left whole in FEAT_BASIC objects: pruned, it moved k_shade's
+    // register allocation from 9 to 31 spilled VGPRs, r06q)
     switch (mt.type) {
         case PBRTGPU_MAT_MATTE: {
             BxDF &x = bs.bx[bs.n++];

@@ -35,7 +35,8 @@ using namespace pgd;
 // weak: an experiment build may compile only some shade variants with PGD_SECTIONS
 extern "C" {
 __attribute__((weak)) int pgd_sections_read_32_0(unsigned long long *, int);
-__attribute__((weak)) int pgd_sections_read_32_1(unsigned long long *, int);
+__attribute__((weak)) int pgd_sections_read_32_8(unsigned long long *, int);
+__attribute__((weak)) int pgd_sections_read_32_9(unsigned long long *, int);
 __attribute__((weak)) int pgd_sections_read_32_7(unsigned long long *, int);
 __attribute__((weak)) int pgd_sections_read_60_0(unsigned long long *, int);
 __attribute__((weak)) int pgd_sections_read_60_6(unsigned long long *, int);
@@ -46,7 +47,7 @@ __attribute__((weak)) int pgd_sections_read_30_7(unsigned long long *, int);
 static int pgd_sections_read(unsigned long long *out, int reset) {
     for (int k = 0; k < SEC_N; ++k) out[k] = 0;
     int e = 0;
-    for (auto f : {pgd_sections_read_32_0, pgd_sections_read_32_1, pgd_sections_read_32_7, pgd_sections_read_60_0, pgd_sections_read_60_6, pgd_sections_read_60_7,
+    for (auto f : {pgd_sections_read_32_0, pgd_sections_read_32_8, pgd_sections_read_32_9, pgd_sections_read_32_7, pgd_sections_read_60_0, pgd_sections_read_60_6, pgd_sections_read_60_7,
                    pgd_sections_read_30_0, pgd_sections_read_30_7})
         if (f) e |= f(out, reset);
     return e;
@@ -1524,25 +1525,31 @@ static int ensure_slots(Lane *c, int cap, int NB, int nInst, int nFrames, int ba
 // their queue sizes on the device, and passes after the queues have drained are empty
 // launches.  The shadow queries run on the lane's second stream beside the closest-hit
 // queries (their tails overlap); shade waits for both.
-// The path integrator's shading variant for a scene's features: FEAT 0, FEAT_ALL, and two
-// partial builds -- 32 bands with measured BRDFs only (C3: FEAT_MEAS without the texture /
-// environment-light code, 4 spilled VGPRs instead of 37 in k_shade) and 60 bands with textures and
-// environment lights but no measured BRDFs (C4: FEAT_TEX | FEAT_INF, no kd-tree walk)
+// The path integrator's shading variant for a scene's features: FEAT 0, FEAT_ALL, and three
+// partial builds -- 32 bands with matte / plastic materials only (C2, C5: FEAT_BASIC, device.h), 32
+// bands with those and measured BRDFs (C3: FEAT_MEAS | FEAT_BASIC, without the texture /
+// environment-light code and the other materials' BxDFs) and 60 bands with textures and environment
+// lights but no measured BRDFs (C4: FEAT_TEX | FEAT_INF, no kd-tree walk).  FEAT_BASIC is a
+// restriction, not a feature: other band counts and integrators take (feat & FEAT_ALL)
 template <int NB>
 static auto path_shade_variant(int feat) -> decltype(&launch_shade<NB, 0>) {
-    if constexpr (NB == 32)
-        if (feat == FEAT_MEAS) return launch_shade<32, FEAT_MEAS>;
+    if constexpr (NB == 32) {
+        if (feat == FEAT_BASIC) return launch_shade<32, FEAT_BASIC>;
+        if (feat == (FEAT_MEAS | FEAT_BASIC)) return launch_shade<32, FEAT_MEAS | FEAT_BASIC>;
+    }
     if constexpr (NB == 60)
         if (feat == (FEAT_TEX | FEAT_INF) && !getenv("PGD_NO60_6")) return launch_shade<60, FEAT_TEX | FEAT_INF>;
-    return feat ? launch_shade<NB, FEAT_ALL> : launch_shade<NB, 0>;
+    return (feat & FEAT_ALL) ? launch_shade<NB, FEAT_ALL> : launch_shade<NB, 0>;
 }
 template <int NB>
 static auto path_tail_variant(int feat) -> decltype(&launch_tail<NB, 0>) {
-    if constexpr (NB == 32)
-        if (feat == FEAT_MEAS) return launch_tail<32, FEAT_MEAS>;
+    if constexpr (NB == 32) {
+        if (feat == FEAT_BASIC) return launch_tail<32, FEAT_BASIC>;
+        if (feat == (FEAT_MEAS | FEAT_BASIC)) return launch_tail<32, FEAT_MEAS | FEAT_BASIC>;
+    }
     if constexpr (NB == 60)
         if (feat == (FEAT_TEX | FEAT_INF) && !getenv("PGD_NO60_6")) return launch_tail<60, FEAT_TEX | FEAT_INF>;
-    return feat ? launch_tail<NB, FEAT_ALL> : launch_tail<NB, 0>;
+    return (feat & FEAT_ALL) ? launch_tail<NB, FEAT_ALL> : launch_tail<NB, 0>;
 }
 
 template <int NB>
@@ -1590,9 +1597,9 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
     // that code compiled out (fewer registers, no kd-tree stack)
     // the DirectLighting integrator has its own step (all features compiled in)
     const bool dl = c->S.integrator == PBRTGPU_INTEGRATOR_DIRECT;
-    auto kShade = dl ? (c->feat ? launch_shade_dl<NB, FEAT_ALL> : launch_shade_dl<NB, 0>)
+    auto kShade = dl ? ((c->feat & FEAT_ALL) ? launch_shade_dl<NB, FEAT_ALL> : launch_shade_dl<NB, 0>)
                   : c->S.integrator == PBRTGPU_INTEGRATOR_METADATA
-                      ? (c->feat ? launch_shade_meta<NB, FEAT_ALL> : launch_shade_meta<NB, 0>)
+                      ? ((c->feat & FEAT_ALL) ? launch_shade_meta<NB, FEAT_ALL> : launch_shade_meta<NB, 0>)
                   : path_shade_variant<NB>(c->feat);
     const int nFrames = dl ? std::max(1, c->S.maxDepth) : 0;
     // the path integrator's k_shade lists the slots about to make their first MT draws (k_mt_init)
@@ -1600,8 +1607,8 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
     // the path and DirectLighting integrators' drain runs on the live slots' list
     // (PBRTGPU_DRAIN_LIST=0: off, A/B)
     const bool drainList = c->S.integrator != PBRTGPU_INTEGRATOR_METADATA && drain_list_on();
-    auto kNee = c->feat ? launch_dl_nee<NB, FEAT_ALL> : launch_dl_nee<NB, 0>;
-    auto kSpec = c->feat ? launch_dl_spec<NB, FEAT_ALL> : launch_dl_spec<NB, 0>;
+    auto kNee = (c->feat & FEAT_ALL) ? launch_dl_nee<NB, FEAT_ALL> : launch_dl_nee<NB, 0>;
+    auto kSpec = (c->feat & FEAT_ALL) ? launch_dl_spec<NB, FEAT_ALL> : launch_dl_spec<NB, 0>;
     // DirectLighting issues up to kDlBatch light samples of a vertex per pass
     const int batch = dl ? std::max(1, std::min(c->S.dlStrategy == PBRTGPU_DL_ONE ? 1 : c->S.dlK, kDlBatch)) : 1;
     // passes one path can take: the camera ray + maxdepth + 1 vertices + 1 finish (path); per

@@ -584,6 +584,8 @@ static int scene_build(const pbrtgpu_flat_scene *s, int topNodes, DevScene &S, i
     for (int i = 0; i < s->n_prims; ++i) {
         const pbrtgpu_prim &p = s->prims[i];
         DevTri t{};
+        int32_t ty = p.shape_type;   // a.w: the shape type (device.h DevTri)
+        memcpy(&t.a.w, &ty, 4);
         if (p.shape_type == PBRTGPU_SHAPE_INSTANCE) {
             pt[i] = t;
             continue;
@@ -595,7 +597,7 @@ static int scene_build(const pbrtgpu_flat_scene *s, int topNodes, DevScene &S, i
             for (int k = 0; k < 3; ++k)
                 if (tr.v[k] < 0 || tr.v[k] >= s->n_verts) SB_FAIL(PBRTGPU_E_INVALID, "bad triangle vertex");
             const float *a = s->vert_p + 3 * tr.v[0], *b = s->vert_p + 3 * tr.v[1], *cc = s->vert_p + 3 * tr.v[2];
-            t.a = make_float4(a[0], a[1], a[2], 0.f);
+            t.a = make_float4(a[0], a[1], a[2], 0.f);   // a.w = 0 = PBRTGPU_SHAPE_TRIANGLE
             t.b = make_float4(b[0], b[1], b[2], 0.f);
             t.c = make_float4(cc[0], cc[1], cc[2], 0.f);
         } else if (p.shape_index < 0 || p.shape_index >= s->n_quadrics)
@@ -744,6 +746,14 @@ static int scene_build(const pbrtgpu_flat_scene *s, int topNodes, DevScene &S, i
             m.ftex[0] >= 0 || m.ftex[1] >= 0)
             *feat |= FEAT_TEX;
     }
+    // FEAT_BASIC (device.h): matte / plastic (and measured) materials only
+    bool basic = (*feat & ~FEAT_MEAS) == 0;
+    for (int i = 0; i < s->n_materials; ++i) {
+        const int t = s->materials[i].type;
+        basic = basic && (t == PBRTGPU_MAT_MATTE || t == PBRTGPU_MAT_PLASTIC ||
+                          ((*feat & FEAT_MEAS) && (t == PBRTGPU_MAT_MEASURED || t == PBRTGPU_MAT_MEASURED_HALFANGLE)));
+    }
+    if (basic) *feat |= FEAT_BASIC;
     return 0;
 }
 

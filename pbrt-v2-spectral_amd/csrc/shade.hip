@@ -10,7 +10,7 @@
 #include "metadata.h"
 
 #if !defined(SHADE_NB) || !defined(SHADE_FEAT)
-#error "compile with -DSHADE_NB=<3|30|32|60> -DSHADE_FEAT=<0|1|7> [-DSHADE_DL=1]"
+#error "compile with -DSHADE_NB=<3|30|32|60> -DSHADE_FEAT=<0|6|7|8|9> [-DSHADE_DL=1]"
 #endif
 #ifndef SHADE_DL
 #define SHADE_DL 0

@@ -340,7 +340,10 @@ PGD_INLINE void term4(const float *sp, const FTerm &t, int q, const float4 *mb, 
         return;
     }
     float4 r, r2;
-    if (FEAT & FEAT_TEX) {
+    if (PGD_BASIC_MATS) {   // Lambertian, Oren-Nayar, dielectric Blinn: one spectrum
+        r = ld4(sp, t.R + 4 * q);
+        r2 = r;
+    } else if (FEAT & FEAT_TEX) {
         r = spec4(sp, t.R, q, kb, c);
         r2 = (t.kind == T_FB || t.kind == T_BLINNC) ? spec4(sp, t.R2, q, kb, c) : r;
     } else {
@@ -360,6 +363,7 @@ PGD_INLINE void term4(const float *sp, const FTerm &t, int q, const float4 *mb, 
                             (((r.z * t.s0) * t.s1) * t.s2) / t.s3, (((r.w * t.s0) * t.s1) * t.s2) / t.s3);
             break;
         default:
+            if (PGD_BASIC_MATS) { f = make_float4(0.f, 0.f, 0.f, 0.f); break; }
             f = make_float4(term_val(t, r.x, r2.x), term_val(t, r.y, r2.y), term_val(t, r.z, r2.z),
                             term_val(t, r.w, r2.w));
             break;
@@ -373,7 +377,7 @@ PGD_INLINE void term4(const float *sp, const FTerm &t, int q, const float4 *mb, 
 template <int FEAT>
 PGD_INLINE float4 fval4(const float *sp, const FVal &F, int q, const float4 *mb, const float4 *kb, size_t c) {
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (F.mode == FV_SPEC) {
+    if (!PGD_BASIC_MATS && F.mode == FV_SPEC) {
         float4 r = (FEAT & FEAT_TEX) ? spec4(sp, F.R, q, kb, c) : ld4(sp, F.R + 4 * q);
         return make_float4((F.fs * r.x) / F.d, (F.fs * r.y) / F.d, (F.fs * r.z) / F.d, (F.fs * r.w) / F.d);
     }

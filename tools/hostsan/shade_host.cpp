@@ -280,10 +280,10 @@ template <int NB>
 static int run_nb(const DevScene &S, PathSoA &P, const ItemSrc &src, int nSlots, int feat, float *Lout, std::string *err) {
     // the variant pbrtgpu.hip launches: FEAT_ALL when the scene uses a feature, else FEAT 0
     if (S.integrator == PBRTGPU_INTEGRATOR_DIRECT)
-        return feat ? run<NB, FEAT_ALL, 1>(S, P, src, nSlots, Lout, err) : run<NB, 0, 1>(S, P, src, nSlots, Lout, err);
+        return (feat & FEAT_ALL) ? run<NB, FEAT_ALL, 1>(S, P, src, nSlots, Lout, err) : run<NB, 0, 1>(S, P, src, nSlots, Lout, err);
     if (S.integrator == PBRTGPU_INTEGRATOR_METADATA)
-        return feat ? run<NB, FEAT_ALL, 2>(S, P, src, nSlots, Lout, err) : run<NB, 0, 2>(S, P, src, nSlots, Lout, err);
-    return feat ? run<NB, FEAT_ALL, 0>(S, P, src, nSlots, Lout, err) : run<NB, 0, 0>(S, P, src, nSlots, Lout, err);
+        return (feat & FEAT_ALL) ? run<NB, FEAT_ALL, 2>(S, P, src, nSlots, Lout, err) : run<NB, 0, 2>(S, P, src, nSlots, Lout, err);
+    return (feat & FEAT_ALL) ? run<NB, FEAT_ALL, 0>(S, P, src, nSlots, Lout, err) : run<NB, 0, 0>(S, P, src, nSlots, Lout, err);
 }
 
 int main(int argc, char **argv) {

@@ -1,0 +1,13 @@
+#!/bin/bash
+# r06o: shape type in DevTri a.w read first by the any-hit walks only (closest keeps 93 VGPRs),
+# vcross as before -- GPU suite, then A/B against the previous library
+OUT=$PWD/gpurun_out/r06o
+mkdir -p $OUT
+export TMPDIR=/tmp
+timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 || { tail -30 $OUT/pytest_gpu.log; exit 1; }
+tail -1 $OUT/pytest_gpu.log
+rm -f gpurun_out/frame_parity.jsonl
+timeout -k 10 500 bash tools/gpu_ab_rounds.sh r06o/ab_c2 2 "--config c2" prev || exit 1
+timeout -k 10 500 bash tools/gpu_ab_rounds.sh r06o/ab_dl 1 "--config c2 --integrator directlighting" prev || exit 1
+timeout -k 10 500 bash tools/gpu_ab_rounds.sh r06o/ab_c5 1 "--config c5" prev || exit 1
+echo done
