@@ -225,7 +225,7 @@ PGD_INLINE void dl_light_batches(const DevScene &S, const PathSoA &P, int slot, 
             Pushes o2 = {false, false, false, 0u, 0u};
             estimate_direct<NB, FEAT>(S, P, row, rb + jb * (int)c, Col<float4>{P.A, (uint32_t)(jb * NQ * c + row)},
                                       Col<float4>{P.B, (uint32_t)(jb * NQ * c + row)}, ln, bs, pm, vp, vn, vwo,
-                                      vEps, vTime, ul, ub, F, f2, o2, nullptr, nullptr);
+                                      vEps, vTime, ul, ub, F, f2, o2, nullptr, nullptr, RAY_M);
             if (f2 & PF_PA) mA |= 1u << jb;
             if (f2 & PF_PB) mB |= 1u << jb;
             lnOne = ln;

@@ -127,7 +127,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_closest(DevScene S, PathS
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const uint32_t e = Q[i];
         const int slot = (int)(e >> 1), kind = (int)(e & 1);
-        Ray r = ray_load(P, kind, slot);
+        Ray r = ray_load(P, rec_kind(S, q, kind), slot);
         int prim = -1;
         float t = INFINITY;
         if (!bvh_intersect<INST>(S, st, r, &prim, &t)) prim = -1;
@@ -237,7 +237,7 @@ __global__ __launch_bounds__(kTraceBlock) PGD_TRACE_ATTR void k_trace_pt(DevScen
                     const uint32_t e = Q[i];
                     slot = ANY ? (int)e : (int)(e >> 1);
                     kind = ANY ? RAY_S : (int)(e & 1);
-                    ray = ray_load(P, kind, slot);
+                    ray = ray_load(P, rec_kind(S, q, kind), slot);
                     invDir = v3(1.f / ray.d.x, 1.f / ray.d.y, 1.f / ray.d.z);
                     neg[0] = invDir.x < 0; neg[1] = invDir.y < 0; neg[2] = invDir.z < 0;
                     negMask = (uint32_t)neg[0] | ((uint32_t)neg[1] << 1) | ((uint32_t)neg[2] << 2);
@@ -656,7 +656,7 @@ __global__ __launch_bounds__(kTraceBlock) PGD_TRACE_ATTR void k_trace_c4(DevScen
                     const uint32_t e = Q[i];
                     slot = (int)(e >> 1);
                     kind = (int)(e & 1);
-                    ray = ray_load(P, kind, slot);
+                    ray = ray_load(P, rec_kind(S, q, kind), slot);
                     invDir = v3(1.f / ray.d.x, 1.f / ray.d.y, 1.f / ray.d.z);
                     neg[0] = invDir.x < 0; neg[1] = invDir.y < 0; neg[2] = invDir.z < 0;
                     negMask = (uint32_t)neg[0] | ((uint32_t)neg[1] << 1) | ((uint32_t)neg[2] << 2);
@@ -818,7 +818,7 @@ __global__ __launch_bounds__(kTraceBlock) PGD_TRACE_INST_ATTR void k_trace_inst(
                     const uint32_t e = Q[i];
                     slot = ANY ? (int)e : (int)(e >> 1);
                     kind = ANY ? RAY_S : (int)(e & 1);
-                    setRay(ray_load(P, kind, slot));
+                    setRay(ray_load(P, rec_kind(S, q, kind), slot));
                     prim = -1;
                     thit = INFINITY;
                     todo = 0;
@@ -922,7 +922,7 @@ __global__ __launch_bounds__(kTraceBlock) PGD_TRACE_INST_ATTR void k_trace_inst(
                     const uint32_t root = (uint32_t)I.root;
                     const int negI[3] = {(int)(negMask & 1u), (int)((negMask >> 1) & 1u), (int)(negMask >> 2)};
                     if (!bbox_hit((*sa(S.nodes, (uint32_t)(2 * root))), (*sa(S.nodes, (uint32_t)(2 * root + 1))), ray, invDir, negI)) {
-                        Ray wr = ray_load(P, kind, slot);   // back to the world ray
+                        Ray wr = ray_load(P, rec_kind(S, q, kind), slot);   // back to the world ray
                         wr.maxt = wmaxt;
                         setRay(wr);
                         continue;
@@ -946,7 +946,7 @@ __global__ __launch_bounds__(kTraceBlock) PGD_TRACE_INST_ATTR void k_trace_inst(
                         if (level == 0) { done = true; break; }
                         // instance walked: back to the world ray (maxt shrunk by its hits),
                         // resume the suspended leaf
-                        Ray wr = ray_load(P, kind, slot);
+                        Ray wr = ray_load(P, rec_kind(S, q, kind), slot);
                         wr.maxt = ANY ? wmaxt : ray.maxt;
                         setRay(wr);
                         level = 0;
@@ -1431,8 +1431,8 @@ static bool serial_mode() {
     const char *e = getenv("PBRTGPU_SERIAL");
     return e && atoi(e) != 0;
 }
-// PBRTGPU_POISON=<byte> (debugging / tests): every path-slot array and the traversal stack spill
-// area are filled with that byte before each wavefront run, so a read of state no pass wrote
+// PBRTGPU_POISON=<byte> (debugging / tests): every path-slot array, the traversal stack spill
+// area and a render's per-sample radiance buffer are filled with that byte before each wavefront run, so a read of state no pass wrote
 // gives a result that changes with the byte; -1 (unset): left as they are
 static int poison_byte() {
     const char *e = getenv("PBRTGPU_POISON");
@@ -1443,12 +1443,15 @@ static int poison_byte() {
 static size_t frame_bytes(int NB) { return (size_t)8 * ((NB + 3) / 4 * 4) + 104; }
 // DirectLighting bytes per slot and batched light sample: A, B terms and the ray records
 static size_t batch_bytes(int NB) { return (size_t)8 * ((NB + 3) / 4 * 4) + 27 * 4 + 8 + 8 + 4 + 24; }
+// ray record floats per ray slot: 9 per kind -- RAY_C, RAY_M, RAY_S, and RAY_M1 (the path
+// integrator's second MIS record set, wavefront.h mis_kind; DirectLighting, batch > 1, has none)
+static size_t ray_floats(int batch) { return batch == 1 ? 36 : 27; }
 // The shading step addresses the slot arrays through 32-bit byte offsets (wavefront.h sa / Col):
 // the largest of them -- A / B at max(2, batch) x padded bands, beta at 3 x, the ray records at
-// 27 floats per ray slot -- must stay below 4 GiB, which bounds a lane's slots
+// ray_floats per ray slot -- must stay below 4 GiB, which bounds a lane's slots
 static int max_slots_32bit(int NB, int batch) {
     const size_t NBP = (size_t)(NB + 3) / 4 * 4;
-    const size_t per = std::max({(size_t)std::max(2, batch) * NBP * 4, 3 * NBP * 4, (size_t)batch * 27 * 4});
+    const size_t per = std::max({(size_t)std::max(2, batch) * NBP * 4, 3 * NBP * 4, (size_t)batch * ray_floats(batch) * 4});
     return (int)std::min<size_t>(INT32_MAX / 2, (((size_t)1 << 32) - 1) / per);
 }
 // batch: ray slots per slot (light samples a DirectLighting pass issues; 1 for the other integrators)
@@ -1464,7 +1467,7 @@ static int ensure_slots(Lane *c, int cap, int NB, int nInst, int nFrames, int ba
     size_t oItem = take(C * 4), oHp = take(C * 4), oSmp = take(C * 4), oBounce = take(C * 4), oFlags = take(C * 4),
            oMt = take(C * 20), oBeta = take(C * 3 * NBP * 4), oL = take(C * NBP * 4), oA = take(C * AB * NBP * 4),
            oB = take(C * AB * NBP * 4), oM = take(C * NBP * 4), oK = take(C * 2 * NBP * 4) /* [2][NQ][cap]: two textured spectra */, oPix = take(C * 4),
-           oRay = take(R * 27 * 4), oHitP = take(R * 8), oHitT = take(R * 8), oOcc = take(R * 4), oQC = take(R * 16),
+           oRay = take(R * ray_floats(batch) * 4), oHitP = take(R * 8), oHitT = take(R * 8), oOcc = take(R * 4), oQC = take(R * 16),
            oQS = take(R * 8), oQT = take(C * 8), oLive = take(C * 4), oCnt = take(CNT_WORDS * 4), oInst = take(C * (size_t)nInst * 128),
            oMask = take(nFrames ? C * 4 : 0), oAMask = take(2 * ((C + 63) / 64) * 8),
            oBMask = take(3 * ((C + 63) / 64) * 8), oMMask = take(2 * ((C + 63) / 64) * 8);
@@ -2283,6 +2286,8 @@ static int render_impl(pbrtgpu_ctx *c, const pbrtgpu_render_desc *d, const int32
             src.nItems += (uint32_t)nSpill;
         }
         src.nItems *= (uint32_t)bi;   // keyBase stays in samples
+        if (const int pb = poison_byte(); pb >= 0)   // an item no path writes reads as the byte (not last batch's)
+            HIPCHK(hipMemsetAsync(c->Lbuf.p, pb, (size_t)src.nItems * NB * 4, c->stream));
         if (int e = run_wavefront<NB>(c, src, (float *)c->Lbuf.p, countWork, T, &zeroed)) return e;
         if (withSpills) {   // keep the spill radiance (later batches reuse Lbuf), add the pre lists
             HIPCHK(hipMemcpyAsync(c->spillL.p, (const float *)c->Lbuf.p + (size_t)src.keyBase * NB,

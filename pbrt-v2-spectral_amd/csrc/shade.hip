@@ -415,7 +415,7 @@ __global__ __launch_bounds__(kTailBlock) void k_tail(DevScene S, PathSoA P0, int
             P.hitT[slot] = prim >= 0 ? t : INFINITY;
         }
         if (fl & PF_PB) {   // the MIS ray
-            Ray r = ray_load(P, RAY_M, slot);
+            Ray r = ray_load(P, mis_kind(qout), slot);   // the set the last step wrote
             int prim = -1;
             float t = INFINITY;
             if (!bvh_intersect4(S, st, r, &prim, &t)) prim = -1;

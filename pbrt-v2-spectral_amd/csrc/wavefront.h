@@ -64,7 +64,19 @@ enum {
 #define PF_LIGHT_SHIFT 12
 #define PF_LIGHT_MASK 0xfffffu
 
-enum { RAY_C = 0, RAY_M = 1, RAY_S = 2 };
+enum { RAY_C = 0, RAY_M = 1, RAY_S = 2, RAY_M1 = 3 };
+// The path integrator's MIS ray records alternate between two sets by the queue set of the pass
+// that wrote them (RAY_M for set 0, RAY_M1 for set 1): a pass reads the records of the set the pass
+// before wrote, at their compacted entries, while it writes its own at its entries.  With one set,
+// the first pass of the drain's list mode (wavefront.h PathSoA::listMode: a 64-slot region's live
+// slots may be shaded by two waves) could overwrite a record at its new identity entry before the
+// slot that owned that compacted entry read it: an MIS term dropped, about 1 frame in 15 of C3
+// (DESIGN.md §4.3).  DirectLighting indexes its records by light-sample row: RAY_M alone.
+PGD_INLINE int mis_kind(int q) { return (q & 1) ? RAY_M1 : RAY_M; }
+// the ray record of a closest-hit queue entry of queue set q (kind RAY_C or RAY_M)
+PGD_INLINE int rec_kind(const DevScene &S, int q, int kind) {
+    return (kind == RAY_M && S.integrator == PBRTGPU_INTEGRATOR_PATH) ? mis_kind(q) : kind;
+}
 // counters (u32 words), each on its own 128-byte line so that the per-block atomics of
 // different queues do not serialise on one memory-side atomic unit; work = u64 at CNT_WORK
 #define CNT_QC(q) (32 * (q))          // closest-hit queue size, queue set q = 0, 1
@@ -105,7 +117,8 @@ struct PathSoA {
     // ray records are indexed by ray slot rs: the slot itself, or (DirectLighting, a batch of
     // light samples per pass) slot + j * cap for the batch's sample j; rcap = cap x batch
     int rcap;
-    float *ray;         // [3][9][rcap]: o.xyz, d.xyz, mint, maxt, time  for RAY_C, RAY_M, RAY_S
+    float *ray;         // [3 or 4][9][rcap]: o.xyz, d.xyz, mint, maxt, time  for RAY_C, RAY_M, RAY_S
+                        // (and RAY_M1: the path integrator's second MIS record set, mis_kind)
     int *hitPrim;       // [2][rcap]  (RAY_C, RAY_M)
     float *hitT;        // [2][rcap]
     uint32_t *occ;      // [rcap]
@@ -859,7 +872,7 @@ template <int NB, int FEAT>
 PGD_INLINE void estimate_direct(const DevScene &S, const PathSoA &P, int slot, int rs, Col<float4> A, Col<float4> B,
                                 int lightNum, const BSDF &bs, PowMemo &pm, V p, V n, V wo, float rayEps, float time,
                                 const float ul[3], const float ub[3], FVal &F, uint32_t &fl, Pushes &out,
-                                unsigned long long *aMask, unsigned long long *mMask) {
+                                unsigned long long *aMask, unsigned long long *mMask, int mKind) {
     constexpr int NQ = Bands<NB>::NQ;
     const uint32_t c = (uint32_t)P.cap;
     const float *sp = S.spectra;
@@ -1004,7 +1017,7 @@ PGD_UNROLL_BANDS
                     B[(uint32_t)q * c] = b;
                 }
                 if (!black) {
-                    ray_store(P, RAY_M, rsM, mr);
+                    ray_store(P, mKind, rsM, mr);
                     fl |= PF_PB;
                     out.m = true;
                     out.mIdx = rsM;
@@ -1097,7 +1110,7 @@ PGD_INLINE Pushes shade_vertex(const DevScene &S, const PathSoA &P, int slot, in
         if (lightNum > nLights - 1) lightNum = nLights - 1;
         estimate_direct<NB, FEAT>(S, P, slot, slot, A_reg<NB>(P, qout, slot), B_reg<NB>(P, qout, slot), lightNum, bs, pm,
                                   p, n, wo, is.rayEps, ray.time, ul, ub, F, fl, out, A_mask(P, qout, slot),
-                                  B_mask(P, qout, slot));
+                                  B_mask(P, qout, slot), mis_kind(qout));
         if (!(fl & (PF_PA | PF_PB))) {
             // nothing can add to Ld: finish now (L += beta * (nLights * 0), nLights * 0 == 0)
             la->zero = true;
@@ -1229,7 +1242,7 @@ PGD_INLINE Pushes shade_slot(const DevScene &S, const PathSoA &P, int slot, floa
             int mp = *sa(P.hitPrim, rc + (uint32_t)mi);
             if ((FEAT & FEAT_INF) && (*sa(S.lights, (uint32_t)(ln))).type == PBRTGPU_LIGHT_INFINITE) useB = mp < 0;   // Li = light->Le(ray)
             else if (mp >= 0 && (*sa(S.prims, (uint32_t)(mp))).area_light == ln) {
-                Ray mr = ray_load(P, RAY_M, mi);
+                Ray mr = ray_load(P, mis_kind(qout ^ 1), mi);   // written by the pass before
                 useB = vdot(isect_nn(S, mr, mp, *sa(P.hitT, rc + (uint32_t)mi), inst_rec(P, slot)), vneg(mr.d)) > 0.f;   // DiffuseAreaLight::L
             }
         }

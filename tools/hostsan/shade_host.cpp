@@ -113,7 +113,7 @@ static PathSoA make_soa(int cap, int NB, int nInst, int nFrames, int batch, bool
     P.M = arr<float4>(NQ * C); P.K = arr<float4>(2 * NQ * C);
     P.aMask = arr<unsigned long long>(2 * W); P.bMask = arr<unsigned long long>(3 * W);
     P.mMask = arr<unsigned long long>(2 * W);
-    P.ray = arr<float>(3 * 9 * R); P.hitPrim = arr<int>(2 * R); P.hitT = arr<float>(2 * R); P.occ = arr<uint32_t>(R);
+    P.ray = arr<float>(4 * 9 * R); P.hitPrim = arr<int>(2 * R); P.hitT = arr<float>(2 * R); P.occ = arr<uint32_t>(R);
     P.qC = arr<uint32_t>(2 * 2 * R); P.qS = arr<uint32_t>(2 * R);
     P.cnt = arr<uint32_t>(CNT_WORDS);
     memset(P.cnt, 0, CNT_WORDS * 4);
@@ -230,7 +230,7 @@ static int run(const DevScene &S, PathSoA &P, const ItemSrc &src, int nSlots, fl
         st.stride = 1;
         for (uint32_t e : Q[q].c) {
             const int rs = (int)(e >> 1), kind = (int)(e & 1u);
-            Ray r = ray_load(P, kind, rs);
+            Ray r = ray_load(P, rec_kind(S, q, kind), rs);
             int prim = -1;
             float t = INFINITY;
             const char *c4e = getenv("PBRTGPU_CLOSEST4");
