@@ -492,8 +492,10 @@ typedef struct pbrtgpu_timing {
     double ms[4];
     int32_t launches[4];
     int32_t passes;
-    int32_t shade_feat;   /* FEAT_* of the k_shade variant the call ran: 0 = lean (no measured BRDF,
-                             texture or environment light), 7 = full (csrc/scene_build.h) */
+    int32_t shade_feat;   /* the scene's FEAT_* bits, which select the k_shade variant (csrc/scene_build.h,
+                             pbrtgpu.hip path_shade_variant): 1 measured BRDFs, 2 textures, 4 infinite /
+                             spot / distant lights, | 8 when every material is matte / plastic (or
+                             measured): 0 and 8 = lean, 7 = full */
     uint64_t work[12];
 } pbrtgpu_timing;
 int pbrtgpu_last_timing(pbrtgpu_ctx *ctx, pbrtgpu_timing *out);

@@ -1544,6 +1544,14 @@ static auto path_shade_variant(int feat) -> decltype(&launch_shade<NB, 0>) {
         if (feat == (FEAT_TEX | FEAT_INF) && !getenv("PGD_NO60_6")) return launch_shade<60, FEAT_TEX | FEAT_INF>;
     return (feat & FEAT_ALL) ? launch_shade<NB, FEAT_ALL> : launch_shade<NB, 0>;
 }
+// the DirectLighting step's objects: FEAT_BASIC at 32 bands (C2's scene), else FEAT_ALL or FEAT 0
+// (PBRTGPU_DL_BASIC=0: the FEAT 0 objects on FEAT_BASIC scenes, A/B)
+template <int NB, class F>
+static F dl_variant(int feat, F all, F lean, F basic) {
+    static const bool on = !getenv("PBRTGPU_DL_BASIC") || atoi(getenv("PBRTGPU_DL_BASIC")) != 0;
+    if (NB == 32 && feat == FEAT_BASIC && on) return basic;
+    return (feat & FEAT_ALL) ? all : lean;
+}
 template <int NB>
 static auto path_tail_variant(int feat) -> decltype(&launch_tail<NB, 0>) {
     if constexpr (NB == 32) {
@@ -1600,7 +1608,7 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
     // that code compiled out (fewer registers, no kd-tree stack)
     // the DirectLighting integrator has its own step (all features compiled in)
     const bool dl = c->S.integrator == PBRTGPU_INTEGRATOR_DIRECT;
-    auto kShade = dl ? ((c->feat & FEAT_ALL) ? launch_shade_dl<NB, FEAT_ALL> : launch_shade_dl<NB, 0>)
+    auto kShade = dl ? dl_variant<NB>(c->feat, launch_shade_dl<NB, FEAT_ALL>, launch_shade_dl<NB, 0>, launch_shade_dl<32, FEAT_BASIC>)
                   : c->S.integrator == PBRTGPU_INTEGRATOR_METADATA
                       ? ((c->feat & FEAT_ALL) ? launch_shade_meta<NB, FEAT_ALL> : launch_shade_meta<NB, 0>)
                   : path_shade_variant<NB>(c->feat);
@@ -1610,8 +1618,8 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
     // the path and DirectLighting integrators' drain runs on the live slots' list
     // (PBRTGPU_DRAIN_LIST=0: off, A/B)
     const bool drainList = c->S.integrator != PBRTGPU_INTEGRATOR_METADATA && drain_list_on();
-    auto kNee = (c->feat & FEAT_ALL) ? launch_dl_nee<NB, FEAT_ALL> : launch_dl_nee<NB, 0>;
-    auto kSpec = (c->feat & FEAT_ALL) ? launch_dl_spec<NB, FEAT_ALL> : launch_dl_spec<NB, 0>;
+    auto kNee = dl_variant<NB>(c->feat, launch_dl_nee<NB, FEAT_ALL>, launch_dl_nee<NB, 0>, launch_dl_nee<32, FEAT_BASIC>);
+    auto kSpec = dl_variant<NB>(c->feat, launch_dl_spec<NB, FEAT_ALL>, launch_dl_spec<NB, 0>, launch_dl_spec<32, FEAT_BASIC>);
     // DirectLighting issues up to kDlBatch light samples of a vertex per pass
     const int batch = dl ? std::max(1, std::min(c->S.dlStrategy == PBRTGPU_DL_ONE ? 1 : c->S.dlK, kDlBatch)) : 1;
     // passes one path can take: the camera ray + maxdepth + 1 vertices + 1 finish (path); per

@@ -224,8 +224,8 @@ static hipError_t launch(int grid, hipStream_t stream, const DevScene &S, const 
 // shinymetal's conductor mirror lobe joined the specular sampler); the all-features k_dl_spec at
 // every band count runs at 1 wave since the noise textures (FBm / Turbulence inlined: 174 spilled at
 // 2 waves, 1,040 B) -- the FEAT 0 builds of the benchmark configs are unaffected
-#define PGD_NEE_WAVES ((SHADE_NB > 32 && SHADE_FEAT != 0) ? 1 : 2)
-#define PGD_SPEC_WAVES ((SHADE_NB > 32 || SHADE_FEAT != 0) ? 1 : 2)
+#define PGD_NEE_WAVES ((SHADE_NB > 32 && (SHADE_FEAT & 7) != 0) ? 1 : 2)   // (FEAT_BASIC: as FEAT 0)
+#define PGD_SPEC_WAVES ((SHADE_NB > 32 || (SHADE_FEAT & 7) != 0) ? 1 : 2)
 #ifndef PGD_NEE_ATTR
 #define PGD_NEE_ATTR __attribute__((amdgpu_waves_per_eu(PGD_NEE_WAVES, PGD_NEE_WAVES)))
 #endif
