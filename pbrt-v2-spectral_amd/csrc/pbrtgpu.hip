@@ -1529,7 +1529,7 @@ static int ensure_slots(Lane *c, int cap, int NB, int nInst, int nFrames, int ba
 // launches.  The shadow queries run on the lane's second stream beside the closest-hit
 // queries (their tails overlap); shade waits for both.
 // The path integrator's shading variant for a scene's features: FEAT 0, FEAT_ALL, and three
-// partial builds -- 32 bands with matte / plastic materials only (C2, C5: FEAT_BASIC, device.h), 32
+// partial builds -- 32 (and 3: C1) bands with matte / plastic materials only (C2, C5: FEAT_BASIC, device.h), 32
 // bands with those and measured BRDFs (C3: FEAT_MEAS | FEAT_BASIC, without the texture /
 // environment-light code and the other materials' BxDFs) and 60 bands with textures and environment
 // lights but no measured BRDFs (C4: FEAT_TEX | FEAT_INF, no kd-tree walk).  FEAT_BASIC is a
@@ -1540,6 +1540,8 @@ static auto path_shade_variant(int feat) -> decltype(&launch_shade<NB, 0>) {
         if (feat == FEAT_BASIC) return launch_shade<32, FEAT_BASIC>;
         if (feat == (FEAT_MEAS | FEAT_BASIC)) return launch_shade<32, FEAT_MEAS | FEAT_BASIC>;
     }
+    if constexpr (NB == 3)   // the RGB build (C1)
+        if (feat == FEAT_BASIC) return launch_shade<3, FEAT_BASIC>;
     if constexpr (NB == 60)
         if (feat == (FEAT_TEX | FEAT_INF) && !getenv("PGD_NO60_6")) return launch_shade<60, FEAT_TEX | FEAT_INF>;
     return (feat & FEAT_ALL) ? launch_shade<NB, FEAT_ALL> : launch_shade<NB, 0>;
@@ -1549,15 +1551,19 @@ static auto path_shade_variant(int feat) -> decltype(&launch_shade<NB, 0>) {
 template <int NB, class F>
 static F dl_variant(int feat, F all, F lean, F basic) {
     static const bool on = !getenv("PBRTGPU_DL_BASIC") || atoi(getenv("PBRTGPU_DL_BASIC")) != 0;
-    if (NB == 32 && feat == FEAT_BASIC && on) return basic;
+    if (basic && feat == FEAT_BASIC && on) return basic;
     return (feat & FEAT_ALL) ? all : lean;
 }
+// the FEAT_BASIC DirectLighting objects built (Makefile SHADEVARS): 32 and 60 bands
+template <int NB> static constexpr bool kDlBasic = NB == 32 || NB == 60;
 template <int NB>
 static auto path_tail_variant(int feat) -> decltype(&launch_tail<NB, 0>) {
     if constexpr (NB == 32) {
         if (feat == FEAT_BASIC) return launch_tail<32, FEAT_BASIC>;
         if (feat == (FEAT_MEAS | FEAT_BASIC)) return launch_tail<32, FEAT_MEAS | FEAT_BASIC>;
     }
+    if constexpr (NB == 3)
+        if (feat == FEAT_BASIC) return launch_tail<3, FEAT_BASIC>;
     if constexpr (NB == 60)
         if (feat == (FEAT_TEX | FEAT_INF) && !getenv("PGD_NO60_6")) return launch_tail<60, FEAT_TEX | FEAT_INF>;
     return (feat & FEAT_ALL) ? launch_tail<NB, FEAT_ALL> : launch_tail<NB, 0>;
@@ -1608,7 +1614,8 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
     // that code compiled out (fewer registers, no kd-tree stack)
     // the DirectLighting integrator has its own step (all features compiled in)
     const bool dl = c->S.integrator == PBRTGPU_INTEGRATOR_DIRECT;
-    auto kShade = dl ? dl_variant<NB>(c->feat, launch_shade_dl<NB, FEAT_ALL>, launch_shade_dl<NB, 0>, launch_shade_dl<32, FEAT_BASIC>)
+    auto kShade = dl ? dl_variant<NB>(c->feat, launch_shade_dl<NB, FEAT_ALL>, launch_shade_dl<NB, 0>,
+                                      kDlBasic<NB> ? launch_shade_dl<kDlBasic<NB> ? NB : 32, FEAT_BASIC> : nullptr)
                   : c->S.integrator == PBRTGPU_INTEGRATOR_METADATA
                       ? ((c->feat & FEAT_ALL) ? launch_shade_meta<NB, FEAT_ALL> : launch_shade_meta<NB, 0>)
                   : path_shade_variant<NB>(c->feat);
@@ -1618,8 +1625,10 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
     // the path and DirectLighting integrators' drain runs on the live slots' list
     // (PBRTGPU_DRAIN_LIST=0: off, A/B)
     const bool drainList = c->S.integrator != PBRTGPU_INTEGRATOR_METADATA && drain_list_on();
-    auto kNee = dl_variant<NB>(c->feat, launch_dl_nee<NB, FEAT_ALL>, launch_dl_nee<NB, 0>, launch_dl_nee<32, FEAT_BASIC>);
-    auto kSpec = dl_variant<NB>(c->feat, launch_dl_spec<NB, FEAT_ALL>, launch_dl_spec<NB, 0>, launch_dl_spec<32, FEAT_BASIC>);
+    auto kNee = dl_variant<NB>(c->feat, launch_dl_nee<NB, FEAT_ALL>, launch_dl_nee<NB, 0>,
+                               kDlBasic<NB> ? launch_dl_nee<kDlBasic<NB> ? NB : 32, FEAT_BASIC> : nullptr);
+    auto kSpec = dl_variant<NB>(c->feat, launch_dl_spec<NB, FEAT_ALL>, launch_dl_spec<NB, 0>,
+                                kDlBasic<NB> ? launch_dl_spec<kDlBasic<NB> ? NB : 32, FEAT_BASIC> : nullptr);
     // DirectLighting issues up to kDlBatch light samples of a vertex per pass
     const int batch = dl ? std::max(1, std::min(c->S.dlStrategy == PBRTGPU_DL_ONE ? 1 : c->S.dlK, kDlBatch)) : 1;
     // passes one path can take: the camera ray + maxdepth + 1 vertices + 1 finish (path); per

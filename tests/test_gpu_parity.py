@@ -265,6 +265,34 @@ def test_shade_variants_agree(pg, killeroo64, monkeypatch):
     assert np.array_equal(lean.view(np.int32), full.view(np.int32))
 
 
+@pytest.mark.parametrize("pack,integ", [("killeroo-simple-b60.pack", "directlighting"), ("killeroo-simple.pack", "directlighting"),
+                                        ("killeroo-simple-rgb.pack", "path"), ("killeroo-simple.pack", "path")])
+def test_basic_material_objects_match_oracle(pg, monkeypatch, pack, integ):
+    """Scenes whose materials are all matte / plastic run the FEAT_BASIC shading objects (the other
+    BxDF kinds compiled out: path integrator at 32 and 3 bands, DirectLighting at 32 and 60): per
+    path and film bit-exact against the oracle, and the film equal to the lean (FEAT 0) objects'."""
+    from conftest import PACKS
+    scene = pg.Scene.load(os.path.join(PACKS, pack), xres=40, yres=32, spp=2, maxdepth=5, integrator=integ)
+    keys = _keys(scene, stride=3)
+    with pg.Device(0) as d:
+        d.upload(scene)
+        L = d.trace_paths(keys)
+        d.render()
+        film = d.film()
+        assert d.timing()["shade_feat"] == 8   # FEAT_BASIC
+    o = pg.oracle()
+    assert np.any(L != 0)
+    assert_bit_exact(L, o.trace_paths(scene, keys), "paths vs oracle")
+    ref, _ = o.render(scene)
+    assert_bit_exact(film, ref, "film vs oracle")
+    monkeypatch.setenv("PBRTGPU_SHADE_FULL", "1")   # the all-features objects
+    with pg.Device(0) as d:
+        d.upload(scene)
+        d.render()
+        full = d.film()
+    assert np.array_equal(film.view(np.int32), full.view(np.int32))
+
+
 def test_coverage_scene_matches_oracle(pg):
     """tests/scenes/coverage.pbrt: glass, mirror, Oren-Nayar, copper with textured bump,
     textures, three light types -- GPU against the oracle path by path and film."""
