@@ -1398,6 +1398,14 @@ static uint32_t tail_rays() {
     const char *e = getenv("PBRTGPU_TAIL");
     return e ? (uint32_t)strtoul(e, nullptr, 0) : 131072u;
 }
+// passes per read-back in the drain (default 2) and within one slot pool of the lane's last item
+// (default 4): PBRTGPU_DRAIN_BATCH / PBRTGPU_NEAR_BATCH (A/B; at least 1)
+static int env_int(const char *name, int def) {
+    const char *e = getenv(name);
+    return e && *e ? std::max(1, atoi(e)) : def;
+}
+static int drain_batch() { static const int v = env_int("PBRTGPU_DRAIN_BATCH", 2); return v; }
+static int near_batch() { static const int v = env_int("PBRTGPU_NEAR_BATCH", 4); return v; }
 static int xcd_map_on() {
     const char *e = getenv("PBRTGPU_XCD_MAP");
     return (e && atoi(e) != 0) ? 1 : 0;
@@ -1714,8 +1722,8 @@ static int run_wavefront(pbrtgpu_ctx *c, const ItemSrc &src, float *Lout, bool c
         // passes per read-back: kPassBatch while the lane has items for more than one more
         // pool, then fewer, so that the switch to the drain's list mode and the lane's end
         // are seen within a few passes (2 in the drain, 4 before it)
-        const int n = r.drain ? std::min(2, kPassBatch)
-                              : (uint64_t)cnt[CNT_NEXT] + (uint64_t)r.cap >= r.src.nItems ? std::min(4, kPassBatch)
+        const int n = r.drain ? std::min(drain_batch(), kPassBatch)
+                              : (uint64_t)cnt[CNT_NEXT] + (uint64_t)r.cap >= r.src.nItems ? std::min(near_batch(), kPassBatch)
                                                                                         : kPassBatch;
         for (int j = 0; j < n; ++j) {
             hipEvent_t *e = ev + 2 + 6 * j;
