@@ -495,7 +495,8 @@ typedef struct pbrtgpu_timing {
     int32_t shade_feat;   /* the scene's FEAT_* bits, which select the k_shade variant (csrc/scene_build.h,
                              pbrtgpu.hip path_shade_variant): 1 measured BRDFs, 2 textures, 4 infinite /
                              spot / distant lights, | 8 when every material is matte / plastic (or
-                             measured): 0 and 8 = lean, 7 = full */
+                             measured), | 16 when otherwise matte / plastic / metal / substrate:
+                             0 and 8 = lean, 7 = full */
     uint64_t work[12];
 } pbrtgpu_timing;
 int pbrtgpu_last_timing(pbrtgpu_ctx *ctx, pbrtgpu_timing *out);

@@ -381,7 +381,7 @@ struct DevScene {
 
 // scene features a shade kernel is specialised for (k_shade<NB, FEAT>): a scene without
 // them runs a variant with that code compiled out
-enum { FEAT_MEAS = 1, FEAT_TEX = 2, FEAT_INF = 4, FEAT_ALL = 7, FEAT_BASIC = 8 };
+enum { FEAT_MEAS = 1, FEAT_TEX = 2, FEAT_INF = 4, FEAT_ALL = 7, FEAT_BASIC = 8, FEAT_NOSPEC = 16 };
 // FEAT_BASIC: a scene without textures or infinite / spot / distant lights whose materials are all
 // matte or plastic, or also measured with FEAT_MEAS (C2 and C5's killeroos: FEAT_BASIC; C3's bunny:
 // FEAT_MEAS | FEAT_BASIC).  Its shading objects (shade.hip built with SHADE_FEAT 8 or 9) compile
@@ -393,6 +393,13 @@ enum { FEAT_MEAS = 1, FEAT_TEX = 2, FEAT_INF = 4, FEAT_ALL = 7, FEAT_BASIC = 8 }
 #else
 #define PGD_BASIC_MATS 0
 #define PGD_BASIC_MEAS 0
+#endif
+// FEAT_NOSPEC: likewise for a scene without measured BRDFs whose materials are all matte, plastic,
+// metal or substrate (C4's): its objects (SHADE_FEAT | 16) compile no specular, measured or Ward kind
+#if defined(SHADE_FEAT) && (SHADE_FEAT & 16)
+#define PGD_NOSPEC_MATS 1
+#else
+#define PGD_NOSPEC_MATS 0
 #endif
 
 struct DG { V p, nn, dpdu, dpdv, dndu, dndv; float u, v; };
@@ -1507,6 +1514,7 @@ enum { BX_LAMBERT, BX_OREN, BX_MICRO_BLINN_DIEL, BX_SPEC_REFL_NOOP, BX_FRESNEL_B
 struct BxDF { int kind, type; int R, R2; float a, b; };
 // the BxDF kinds a shading object compiles (FEAT_BASIC objects: the basic materials' kinds only)
 PGD_INLINE bool bx_kind_on(int k) {
+    if (PGD_NOSPEC_MATS) return k <= BX_MICRO_BLINN_DIEL || k == BX_FRESNEL_BLEND_ANISO || k == BX_MICRO_BLINN_COND;
     return !PGD_BASIC_MATS || k <= BX_MICRO_BLINN_DIEL || (PGD_BASIC_MEAS && (k == BX_MEASURED_IRREG || k == BX_MEASURED_HALF));
 }
 // eta: BSDF::eta, the glass material's index (glass.cpp:47-48), 1 otherwise (DirectLighting's
@@ -1794,7 +1802,7 @@ PGD_INLINE float bx_pdf(PowMemo &pm, const BxDF &b, V wo, V wi) {
 }
 // the specular BxDFs' Sample_f (reflection.cpp SpecularReflection / SpecularTransmission::Sample_f)
 PGD_INLINE void bx_sample_specular(const BxDF &b, V wo, V *wi, float *pdf, FVal &F) {
-    switch (PGD_BASIC_MATS ? -1 : b.kind) {
+    switch ((PGD_BASIC_MATS || PGD_NOSPEC_MATS) ? -1 : b.kind) {
         case BX_SPEC_REFL_NOOP:    // SpecularReflection with FresnelNoOp: Spectrum(1) * R / |cos|
         case BX_SPEC_REFL_DIEL:    // ... with FresnelDielectric(1, ior)
             *wi = v3(-wo.x, -wo.y, wo.z);

@@ -1550,8 +1550,11 @@ static auto path_shade_variant(int feat) -> decltype(&launch_shade<NB, 0>) {
     }
     if constexpr (NB == 3)   // the RGB build (C1)
         if (feat == FEAT_BASIC) return launch_shade<3, FEAT_BASIC>;
-    if constexpr (NB == 60)
-        if (feat == (FEAT_TEX | FEAT_INF) && !getenv("PGD_NO60_6")) return launch_shade<60, FEAT_TEX | FEAT_INF>;
+    if constexpr (NB == 60) {
+        if (feat == (FEAT_TEX | FEAT_INF | FEAT_NOSPEC) && !getenv("PGD_NO60_6"))   // C4
+            return launch_shade<60, FEAT_TEX | FEAT_INF | FEAT_NOSPEC>;
+        if ((feat & FEAT_ALL) == (FEAT_TEX | FEAT_INF) && !getenv("PGD_NO60_6")) return launch_shade<60, FEAT_TEX | FEAT_INF>;
+    }
     return (feat & FEAT_ALL) ? launch_shade<NB, FEAT_ALL> : launch_shade<NB, 0>;
 }
 // the DirectLighting step's objects: FEAT_BASIC at 32 bands (C2's scene), else FEAT_ALL or FEAT 0
@@ -1572,8 +1575,11 @@ static auto path_tail_variant(int feat) -> decltype(&launch_tail<NB, 0>) {
     }
     if constexpr (NB == 3)
         if (feat == FEAT_BASIC) return launch_tail<3, FEAT_BASIC>;
-    if constexpr (NB == 60)
-        if (feat == (FEAT_TEX | FEAT_INF) && !getenv("PGD_NO60_6")) return launch_tail<60, FEAT_TEX | FEAT_INF>;
+    if constexpr (NB == 60) {
+        if (feat == (FEAT_TEX | FEAT_INF | FEAT_NOSPEC) && !getenv("PGD_NO60_6"))
+            return launch_tail<60, FEAT_TEX | FEAT_INF | FEAT_NOSPEC>;
+        if ((feat & FEAT_ALL) == (FEAT_TEX | FEAT_INF) && !getenv("PGD_NO60_6")) return launch_tail<60, FEAT_TEX | FEAT_INF>;
+    }
     return (feat & FEAT_ALL) ? launch_tail<NB, FEAT_ALL> : launch_tail<NB, 0>;
 }
 

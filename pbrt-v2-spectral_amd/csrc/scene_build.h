@@ -754,6 +754,14 @@ static int scene_build(const pbrtgpu_flat_scene *s, int topNodes, DevScene &S, i
                           ((*feat & FEAT_MEAS) && (t == PBRTGPU_MAT_MEASURED || t == PBRTGPU_MAT_MEASURED_HALFANGLE)));
     }
     if (basic) *feat |= FEAT_BASIC;
+    // FEAT_NOSPEC (device.h): otherwise matte / plastic / metal / substrate only, no measured BRDF
+    bool nospec = !basic && (*feat & FEAT_MEAS) == 0;
+    for (int i = 0; i < s->n_materials; ++i) {
+        const int t = s->materials[i].type;
+        nospec = nospec && (t == PBRTGPU_MAT_MATTE || t == PBRTGPU_MAT_PLASTIC || t == PBRTGPU_MAT_METAL ||
+                            t == PBRTGPU_MAT_SUBSTRATE);
+    }
+    if (nospec) *feat |= FEAT_NOSPEC;
     return 0;
 }
 

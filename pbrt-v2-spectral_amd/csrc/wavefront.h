@@ -390,11 +390,11 @@ PGD_INLINE void term4(const float *sp, const FTerm &t, int q, const float4 *mb, 
 template <int FEAT>
 PGD_INLINE float4 fval4(const float *sp, const FVal &F, int q, const float4 *mb, const float4 *kb, size_t c) {
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (!PGD_BASIC_MATS && F.mode == FV_SPEC) {
+    if (!PGD_BASIC_MATS && !PGD_NOSPEC_MATS && F.mode == FV_SPEC) {
         float4 r = (FEAT & FEAT_TEX) ? spec4(sp, F.R, q, kb, c) : ld4(sp, F.R + 4 * q);
         return make_float4((F.fs * r.x) / F.d, (F.fs * r.y) / F.d, (F.fs * r.z) / F.d, (F.fs * r.w) / F.d);
     }
-    if ((FEAT & FEAT_TEX) && F.mode == FV_SPEC_COND) {   // shinymetal's mirror lobe (scenes with one run FEAT_TEX)
+    if (!PGD_NOSPEC_MATS && (FEAT & FEAT_TEX) && F.mode == FV_SPEC_COND) {   // shinymetal's mirror lobe (scenes with one run FEAT_TEX)
         const float4 e = ld4(sp, F.R + 4 * q);
         return make_float4((fr_cond(F.fs, e.x, 0.f) * 1.f) / F.d, (fr_cond(F.fs, e.y, 0.f) * 1.f) / F.d,
                            (fr_cond(F.fs, e.z, 0.f) * 1.f) / F.d, (fr_cond(F.fs, e.w, 0.f) * 1.f) / F.d);
